@@ -1,0 +1,225 @@
+#!/usr/bin/env python3
+"""Benchmark of the depth -> points -> flying-pixel -> crop -> voxel-occupancy hot path.
+
+Workload (BASELINE.json configs[1], "C2"): one 640x480 16-bit synthetic depth stream per GPU,
+launch-file defaults (flying-pixel F=4, thr 0.3; crop = voxel bounds -10..30 x -20..20 x -1..1.5,
+cells 0.1/0.1/0.12 -> 400x400x21 = 3.36 M cells; voxelize with averaging; lifetime 10).
+A step = one full frame of GPUDepthmapFusionComponent::processDepthmaps on the GPU: fused
+convert+flying+crop+ordered compaction+voxel keys+occupancy marks, GPU voxelize (radix sort +
+ordered means), historic-grid update.  Frames are device-resident (a ring of distinct frames
+generated once and uploaded before timing).
+
+N > 1 (torchrun, one rank per GPU over RCCL): rank k owns camera k (weak scaling).  The shared
+voxel grid needs one real exchange per frame: the per-rank occupancy marks (1 bit per cell) are
+all-gathered and OR-merged before every rank's identical historic-grid update.
+
+Prints ONE JSON line (rank 0).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mpoints/s end-to-end depth→fused voxel grid @1/2/4/8 GPU; % HBM roofline"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--width", type=int, default=640)
+    ap.add_argument("--height", type=int, default=480)
+    ap.add_argument("--ring", type=int, default=8, help="distinct device-resident frames")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="do not bracket launches with HIP events (for rocprofv3 runs)")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    dist = None
+    rank, local_rank = 0, 0
+    if args.gpus > 1 or world > 1:
+        import torch
+        import torch.distributed as dist
+        rank = int(os.environ.get("RANK", "0"))
+        local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        world = dist.get_world_size()
+    import numpy as np
+    from ros_gpu_depthmap_fusion_amd import build_library, hiprt, synth
+    from ros_gpu_depthmap_fusion_amd.gdf import ComponentParams, GPUDepthmapFusion
+
+    build_library()
+    hiprt.set_device(local_rank)
+    W, H = args.width, args.height
+    P = W * H
+    cam = synth.make_camera(rank, W, H)
+    frames = [synth.depth_frame(cam, rank, f) for f in range(args.ring)]
+    dframes = [hiprt.DeviceArray.from_numpy(f) for f in frames]
+    params = ComponentParams()
+    eng = GPUDepthmapFusion(local_rank)
+
+    words = None
+    if dist is not None:
+        import torch
+        stream = torch.cuda.current_stream()
+        eng.set_stream(stream.cuda_stream)
+
+    def add(i):
+        eng.clear()
+        eng.addDepthmapDevice(dframes[i % args.ring].ptr, W, H, *cam.intrinsics(), cam.T_world,
+                              cam.T_crop)
+
+    # per-frame point counts (for the algorithmic byte model), one synchronous pass over the ring
+    npts, nvox = [], []
+    for i in range(args.ring):
+        add(i)
+        r = eng.processFrame(params, synchronous=True)
+        npts.append(r.num_points)
+        nvox.append(r.num_voxelized)
+    (gx, gy, gz), ncells = eng.grid_size()
+
+    if dist is not None:
+        words = (ncells + 31) // 32
+        local_bits = torch.zeros(words, dtype=torch.int32, device="cuda")
+        all_bits = torch.zeros(world * words, dtype=torch.int32, device="cuda")
+
+    def step(i):
+        add(i)
+        if dist is None:
+            eng.processFrame(params, synchronous=False)
+        else:
+            eng.processFrame(params, synchronous=False, defer_occupancy_grid=True)
+            eng.export_marks(local_bits.data_ptr(), words)
+            dist.all_gather_into_tensor(all_bits, local_bits)
+            eng.import_marks(all_bits.data_ptr(), words, world)
+            eng.voxelOccupancyGrid(params.occupancy_lifetime)
+
+    def barrier_sync():
+        eng.synchronize()
+        if dist is not None:
+            torch.cuda.synchronize()
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    for i in range(args.warmup):
+        step(i)
+    barrier_sync()
+    if not args.no_kernel_timing:
+        eng.set_profiling(True)
+    barrier_sync()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    barrier_sync()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ktimes = eng.kernel_times() if not args.no_kernel_timing else None
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * P * args.steps / elapsed / 1e6
+    # frames used in the timed region, for the byte model
+    idx = [(args.warmup + i) % args.ring for i in range(args.steps)]
+    n_avg = float(np.mean([npts[i] for i in idx]))
+    g_avg = float(np.mean([nvox[i] for i in idx]))
+    model_bytes = {
+        # algorithmic bytes per launch (DESIGN.md "Kernels and their rooflines")
+        "frame": 2.0 * P + 21.0 * n_avg,
+        "grid": 2.0 * ncells,
+        "voxelize": 76.0 * n_avg + 16.0 * g_avg,
+    }
+    survey_bytes = 2.0 * P + 24.0 * n_avg + 9.0 * ncells  # SURVEY.md §8(d) B_alg per frame
+
+    roofline = None
+    if ktimes:
+        slot = max(("frame", "grid", "voxelize"), key=lambda k: ktimes[k][0])
+        ms, n = ktimes[slot]
+        avg_s = ms / 1e3 / max(n, 1)
+        achieved = model_bytes[slot] / avg_s / 1e9
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc):
+            try:
+                rec = json.load(open(pmc)).get(slot)
+                if rec and rec.get("workload") == f"{W}x{H}":
+                    traffic = rec.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        roofline = {
+            "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+            "kernel": slot, "avg_launch_us": round(avg_s * 1e6, 3),
+            "bytes_per_launch": round(model_bytes[slot]),
+            "per_kernel_us": {k: round(v[0] * 1e3 / max(v[1], 1), 3) for k, v in ktimes.items()
+                              if v[1]},
+            "step_survey_bytes": round(survey_bytes),
+            "step_survey_GBps": round(survey_bytes * args.steps / elapsed / 1e9, 2),
+        }
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        from oracle import OracleFusion  # cpu_baseline leg only
+        threads = min(16, os.cpu_count() or 1)
+        orc = OracleFusion(threads=threads)
+        done, t_cpu = 0, 0.0
+        for i in range(2):  # warm-up
+            orc.clear()
+            orc.addDepthmap(frames[i % args.ring], *cam.intrinsics(), cam.T_world, cam.T_crop)
+            orc.processFrame(params)
+        tc0 = time.perf_counter()
+        while True:
+            orc.clear()
+            orc.addDepthmap(frames[done % args.ring], *cam.intrinsics(), cam.T_world, cam.T_crop)
+            orc.processFrame(params)
+            done += 1
+            t_cpu = time.perf_counter() - tc0
+            if t_cpu >= args.cpu_seconds or done >= 2000:
+                break
+        cpu = {"value": round(done * P / t_cpu / 1e6, 3), "unit": "Mpoints/s", "cores": threads,
+               "kind": "port",
+               "sample": f"{done} frames of the same {W}x{H} C2 workload through the C "
+                         f"restatement (oracle/gdf_oracle.c, OpenMP {threads} threads), "
+                         f"{t_cpu:.1f} s"}
+
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "Mpoints/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 5),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (ray-cast analytic scene, counter-hash noise/holes; "
+                    "device-resident ring of %d frames)" % args.ring,
+            "config": {"workload": "C2: %dx%d u16 depth stream per GPU, launch defaults "
+                                   "(F=4 thr 0.3, crop/voxel -10..30/-20..20/-1..1.5, "
+                                   "cells 0.1/0.1/0.12 -> %dx%dx%d, voxelize average, "
+                                   "lifetime 10)" % (W, H, gx, gy, gz),
+                       "cameras_per_gpu": 1, "points_per_frame_after_crop": round(n_avg),
+                       "voxels_per_frame": round(g_avg), "grid_cells": ncells,
+                       "parallelism": "camera-per-GPU x%d, occupancy-mark all-gather" % world
+                       if world > 1 else "single GPU"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,246 @@
+/*
+ * gdf.h — C-ABI of the MI355X-native depth-map fusion hot path.
+ *
+ * Drop-in boundary for the `GPUDepthmapFusion` engine of xaedes/ros_gpu_depthmap_fusion
+ * (include/gpu_depthmap_fusion/gpu_depthmap_fusion.h:159-526, src/gpu_depthmap_fusion.cpp).
+ * Every entry point below names the reference method it replaces (file:line, paths relative to
+ * the reference root).  The ROS component (src/gpu_depthmap_fusion_component.cpp) keeps calling the
+ * same method sequence through the C++ facade in include/gdf_fusion.hpp, which forwards here.
+ *
+ * Conventions
+ *   - plain pointers and sizes only; no C++/torch/OpenCV types cross this boundary;
+ *   - every function returns an int status (GDF_OK == 0, negative on error) and never throws;
+ *     the message of the last error on the calling thread is returned by gdf_last_error();
+ *   - 4x4 matrices are 16 floats, ROW-major, i.e. the memory of a cv::Matx44f
+ *     (the reference uploads them with transpose=false and multiplies `point * M` in GLSL, which
+ *     is M·p for the row-major matrix, include/gpu_depthmap_fusion/program_uniform.h:197-209);
+ *   - points are float4 {x, y, z, w} (16 bytes), the layout of the reference's vec4 buffers;
+ *   - an engine is bound to one HIP device and one HIP stream; frame calls must be serialised by
+ *     the caller (the reference holds m_mutexCallbackN, component.cpp:95);
+ *     gdf_add_point_sequence is internally locked and may be called from another thread
+ *     (the reference's m_mutexCallbackPointSequence, component.cpp:162,997).
+ */
+#ifndef GDF_H_
+#define GDF_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GDF_VERSION_MAJOR 0
+#define GDF_VERSION_MINOR 1
+
+#define GDF_MAX_CAMERAS 16
+
+enum gdf_status_code {
+    GDF_OK = 0,
+    GDF_ERR_ARG = -1,       /* invalid argument (null pointer, bad size, bad grid bounds)      */
+    GDF_ERR_STATE = -2,     /* call out of order, or rollbuffer bookkeeping would underflow    */
+    GDF_ERR_HIP = -3,       /* HIP runtime error                                               */
+    GDF_ERR_NOMEM = -4,     /* device or host allocation failed                                */
+    GDF_ERR_CAPACITY = -5,  /* a caller-provided output buffer is too small                    */
+    GDF_ERR_TIME = -6,      /* ROS time arithmetic out of range (ros::Time would throw)        */
+    GDF_ERR_DEVICE = -7     /* a kernel reported an internal error (bounded spin expired)      */
+};
+
+typedef struct gdf_engine gdf_engine;
+
+/* Rollbuffer bookkeeping, the public m_rollBuffer* members of the reference
+ * (gpu_depthmap_fusion.h:345-354). */
+typedef struct gdf_rollbuffer_state {
+    uint32_t num_points;                /* m_rollBufferNumPoints              */
+    uint32_t num_seqs;                  /* m_rollBufferNumSeqs                */
+    uint32_t selection_point_start;     /* m_rollBufferSelectionPointStart    */
+    uint32_t selection_point_count;     /* m_rollBufferSelectionPointCount    */
+    uint32_t selection_sequence_start;  /* m_rollBufferSelectionSequenceStart */
+    uint32_t selection_sequence_count;  /* m_rollBufferSelectionSequenceCount */
+    uint32_t earliest_time_sec;         /* m_rollBufferEarliestTimeSec        */
+    uint32_t earliest_time_nsec;        /* m_rollBufferEarliestTimeNSec       */
+    uint32_t last_time_sec;             /* m_rollBufferLastTimeSec            */
+    uint32_t last_time_nsec;            /* m_rollBufferLastTimeNSec           */
+} gdf_rollbuffer_state;
+
+/* Parameters of one depth-fusion frame: the GPUDepthmapFusionComponent parameters read in
+ * onInit (src/gpu_depthmap_fusion_component.cpp:1115-1187) plus the move-frame transforms
+ * looked up per frame (component.cpp:192-197). */
+typedef struct gdf_frame_params {
+    /* point-sequence (lidar) chain, component.cpp:158-211 */
+    float ps_filter_threshold;          /* point_sequence_flying_pixel_filter_threshold */
+    uint32_t ps_filter_size;            /* point_sequence_flying_pixel_filter_size      */
+    float ps_timespan;                  /* point_sequence_aggregation_timespan [s]      */
+    int32_t move_transform_available;   /* canTransform(world, move) && canTransform(crop, move) */
+    float T_world_move[16];
+    float T_crop_move[16];
+    /* depth chain, component.cpp:228-300 */
+    uint32_t flying_filter_size;        /* flyingpixels_filter_size        */
+    float flying_threshold;             /* flyingpixels_filter_threshold   */
+    int32_t flying_rot45;               /* flyingpixels_filter_enable_rot45 */
+    float crop_min[3];
+    float crop_max[3];
+    int32_t enable_voxel_filter;        /* enable_voxel_filter              */
+    float voxel_min[3];
+    float voxel_max[3];
+    float voxel_size[3];
+    int32_t voxel_average;              /* voxel_filter_enable_average       */
+    uint32_t occupancy_lifetime;        /* voxel_occupancy_lifetime          */
+    int32_t defer_occupancy_grid;       /* 1: stop after the voxel keys / occupancy marks / voxelize;
+                                           the caller merges marks across ranks and then calls
+                                           gdf_voxel_occupancy_grid (multi-GPU exchange step)  */
+    int32_t synchronous;                /* 1: wait for the frame and fill the host mirrors
+                                           (m_points / m_points_voxelized / m_occupancyGrid),
+                                           0: enqueue only (results stay on the device)      */
+} gdf_frame_params;
+
+/* What gdf_process_frame produced (counts are only valid when synchronous != 0). */
+typedef struct gdf_frame_result {
+    int32_t processed;                  /* 0 when there was nothing to do (no depth, no points) */
+    uint32_t num_depth_points;          /* m_depthmapsTotalElements            */
+    uint32_t num_points_total;          /* m_numPointsTotal (depth + selected) */
+    uint32_t num_points;                /* m_numItemsAfterMask                 */
+    uint32_t num_voxelized;             /* m_points_voxelized.size()           */
+    uint32_t latest_time_sec;           /* header stamp chosen by the component (overallLatestTime) */
+    uint32_t latest_time_nsec;
+} gdf_frame_result;
+
+/* ---- lifetime ------------------------------------------------------------------------- */
+/* GPUDepthmapFusion() + init(shaderPath) (gpu_depthmap_fusion.cpp:16-128): allocates the
+ * device arena on HIP device `device` and creates the engine's stream. */
+int gdf_create(int device, gdf_engine** out_engine);
+int gdf_destroy(gdf_engine* engine);
+const char* gdf_last_error(void);
+int gdf_version(int* major, int* minor);
+/* Use a caller-owned hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL restores
+ * the engine's own stream. */
+int gdf_set_stream(gdf_engine* engine, void* hip_stream);
+int gdf_synchronize(gdf_engine* engine);
+/* voxel_group_size parameter (component.cpp:1149); kept for interface parity, it only tuned
+ * the reference's CPU radix sort and does not change results. */
+int gdf_set_voxel_group_size(gdf_engine* engine, int group_size);
+
+/* ---- per-frame inputs ------------------------------------------------------------------ */
+/* GPUDepthmapFusion::clear() (gpu_depthmap_fusion.cpp:725-732). */
+int gdf_clear(gdf_engine* engine);
+/* addDepthmap (gpu_depthmap_fusion.cpp:798-816).  `depth` is a HOST pointer to width*height
+ * uint16 depth values; like the reference it is borrowed (not copied) until
+ * gdf_upload_depthmaps returns. */
+int gdf_add_depthmap(gdf_engine* engine, const uint16_t* depth, uint32_t width, uint32_t height,
+                     float depth_scale, float fx, float fy, float cx, float cy,
+                     const float T_world[16], const float T_crop[16]);
+/* Same, for a depth map already resident in device memory of this engine's GPU (no copy). */
+int gdf_add_depthmap_device(gdf_engine* engine, const uint16_t* depth_device, uint32_t width,
+                            uint32_t height, float depth_scale, float fx, float fy, float cx,
+                            float cy, const float T_world[16], const float T_crop[16]);
+/* addPointSequence (gpu_depthmap_fusion.cpp:747-796): copies x,y,z (float32 at byte offsets
+ * 0, 4, 8 of each point_step record, the PointCloud2 layout) with w = 1 into the collect
+ * buffer.  Thread-safe with respect to the frame calls. */
+int gdf_add_point_sequence(gdf_engine* engine, const void* records, uint32_t num_points,
+                           uint32_t point_step, uint32_t time_sec, uint32_t time_nsec,
+                           const float T_move[16]);
+/* numCollectedPointSequencePoints() (gpu_depthmap_fusion.h:356). */
+int gdf_num_collected_point_sequence_points(gdf_engine* engine, uint32_t* out_count);
+
+/* ---- point-sequence rollbuffer chain --------------------------------------------------- */
+int gdf_upload_point_sequences(gdf_engine* engine);                      /* :819-857   */
+int gdf_filter_new_point_sequences(gdf_engine* engine, float threshold,
+                                   uint32_t filter_size);                /* :928-976   */
+int gdf_insert_new_point_sequences(gdf_engine* engine);                  /* :979-1087  */
+int gdf_roll_rollbuffer(gdf_engine* engine, uint32_t min_sec,
+                        uint32_t min_nsec);                               /* :1098-1217 */
+int gdf_select_timespan(gdf_engine* engine, uint32_t min_sec, uint32_t min_nsec,
+                        uint32_t max_sec, uint32_t max_nsec);             /* :1358-1416 */
+int gdf_prepare_point_and_mask_buffers(gdf_engine* engine);              /* :1497-1508 */
+int gdf_insert_selected_point_sequence(gdf_engine* engine, const float T_world_move[16],
+                                       const float T_crop_move[16]);     /* :1509-1553 */
+int gdf_transform_point_sequence(gdf_engine* engine);                    /* :1555-1581 */
+int gdf_get_rollbuffer_state(gdf_engine* engine, gdf_rollbuffer_state* out);
+
+/* ---- depth chain ------------------------------------------------------------------------ */
+int gdf_upload_depthmaps(gdf_engine* engine);                            /* :1583-1593 */
+int gdf_convert_depthmaps(gdf_engine* engine);                           /* :1595-1628 */
+int gdf_filter_flying_pixels(gdf_engine* engine, uint32_t filter_size, float threshold,
+                             int enable_rot45);                          /* :1629-1648 */
+int gdf_crop_points(gdf_engine* engine, const float lower[3],
+                    const float upper[3]);                               /* :1649-1660 */
+/* applyPointMask (:1661-1678): ordered compaction (pixel order, cameras in add order, selected
+ * rollbuffer points after the depth points).  Writes the count when out_count != NULL (this
+ * waits for the device, like the reference's blocking count download). */
+int gdf_apply_point_mask(gdf_engine* engine, uint32_t* out_count);
+int gdf_compute_voxel_coords(gdf_engine* engine, const float lower[3], const float upper[3],
+                             const float cell_size[3]);                  /* :1680-1711 */
+/* voxelize (:1743-1756): stable radix sort of the voxel keys + per-voxel mean (average != 0)
+ * or voxel lower corner (average == 0), on the GPU. */
+int gdf_voxelize(gdf_engine* engine, int average_voxels);
+/* voxelOccupancyGrid (:1757-1823): decaying occupancy with `lifetime`. */
+int gdf_voxel_occupancy_grid(gdf_engine* engine, uint32_t lifetime);
+
+/* ---- results (device -> host) ----------------------------------------------------------- */
+int gdf_get_point_count(gdf_engine* engine, uint32_t* out_count);        /* m_numItemsAfterMask */
+/* downloadPoints (:2946-2951): compacted world points, float4[count]. */
+int gdf_download_points(gdf_engine* engine, float* out_xyzw, uint32_t capacity,
+                        uint32_t* out_count);
+/* downloadVoxelCoords (:1712-1718): voxel index per compacted point. */
+int gdf_download_voxel_coords(gdf_engine* engine, uint32_t* out, uint32_t capacity,
+                              uint32_t* out_count);
+/* m_points_voxelized after voxelize. */
+int gdf_download_voxelized_points(gdf_engine* engine, float* out_xyzw, uint32_t capacity,
+                                  uint32_t* out_count);
+/* downloadVoxelOccupancyGrid (:1824-1839): uint8 per cell, x fastest, then y, then z. */
+int gdf_download_occupancy_grid(gdf_engine* engine, uint8_t* out, uint64_t capacity);
+/* VoxelGridMeta (gpu_depthmap_fusion.h:507): grid size per axis and cell count. */
+int gdf_get_grid_size(gdf_engine* engine, uint32_t grid_size[3], uint64_t* num_cells);
+/* Device pointers of the results (valid until the next frame call), for zero-copy consumers. */
+int gdf_get_device_results(gdf_engine* engine, const float** points, const uint32_t** coords,
+                           const float** voxelized, const uint8_t** occupancy);
+
+/* ---- whole frame -------------------------------------------------------------------------- */
+/* The per-frame sequence of GPUDepthmapFusionComponent::processDepthmaps
+ * (component.cpp:92-300) from uploadPointSequences through downloadVoxelOccupancyGrid, for the
+ * depth maps added since gdf_clear.  Runs the fused kernels (one compaction launch for depth +
+ * rollbuffer points with voxel keys and occupancy marks, one grid launch, the GPU voxelize). */
+int gdf_process_frame(gdf_engine* engine, const gdf_frame_params* params,
+                      gdf_frame_result* out_result);
+
+/* ---- multi-GPU (one camera per rank) ------------------------------------------------------- */
+/* Per-frame occupancy marks of this rank as a bitmask of ceil(num_cells/32) uint32 words, and
+ * the merge of all ranks' masks (bitwise OR of `num_ranks` masks laid out back to back, as
+ * produced by an all-gather) back into this engine before gdf_voxel_occupancy_grid. */
+int gdf_export_occupancy_marks(gdf_engine* engine, uint32_t* device_bitmask, uint64_t words);
+int gdf_import_occupancy_marks(gdf_engine* engine, const uint32_t* device_bitmasks,
+                               uint64_t words, uint32_t num_ranks);
+
+/* ---- live kernel timing (HIP events on the engine stream) ------------------------------------ */
+enum gdf_kernel_slot {
+    GDF_KERNEL_FRAME = 0,      /* k_frame: fused convert/flying/crop/transform/compaction(+keys) */
+    GDF_KERNEL_GRID = 1,       /* k_grid_u8 / k_grid_u32: historic occupancy update              */
+    GDF_KERNEL_VOXELIZE = 2,   /* radix sort passes + group mean                                  */
+    GDF_KERNEL_PS_INSERT = 3,  /* point-sequence filter + rollbuffer insert                      */
+    GDF_KERNEL_SLOTS = 4
+};
+/* enable: record an event pair around every launch of each slot; reset clears the sums */
+int gdf_set_profiling(gdf_engine* engine, int enable);
+/* sum of event-measured milliseconds and number of launches per slot since the last reset
+ * (synchronises the engine stream) */
+int gdf_get_kernel_times(gdf_engine* engine, double* ms_sum, uint64_t* launches, int slots);
+
+/* ---- debug / parity hooks ------------------------------------------------------------------ */
+/* Keep per-point stage masks of the next compaction launch: bit0 = valid after convert
+ * (depth != 0 or rollbuffer mask != 0), bit1 = after the flying-pixel filter, bit2 = after crop. */
+int gdf_set_debug(gdf_engine* engine, int enable);
+int gdf_debug_stage_masks(gdf_engine* engine, uint8_t* out, uint32_t capacity,
+                          uint32_t* out_count);
+/* The rollbuffer in the reference's logical layout (the B buffers after a roll): points,
+ * mask (0/1) and sequence index per point; sequence headers (sec, nsec, start, numPoints). */
+int gdf_debug_rollbuffer(gdf_engine* engine, float* points_xyzw, uint32_t* mask,
+                         uint32_t* seq_idx, uint32_t capacity, uint32_t* header_sec_nsec_start_num,
+                         uint32_t header_capacity);
+/* The historic occupancy grid as uint32 per cell (m_bufHistoricVoxelOccupancyA). */
+int gdf_debug_historic_grid(gdf_engine* engine, uint32_t* out, uint64_t capacity);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GDF_H_ */

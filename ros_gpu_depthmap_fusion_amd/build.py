@@ -1,0 +1,42 @@
+"""Build libgdf.so (HIP, gfx950) in-tree with hipcc."""
+from __future__ import annotations
+
+import os
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB_PATH = os.path.join(PKG, "lib", "libgdf.so")
+SOURCES = ["gdf_kernels.hip", "gdf_engine.cpp"]
+HEADERS = ["gdf_device.hpp", "gdf_kernels.hpp"]
+
+# Float contract of SURVEY.md Appendix A: no FMA contraction, correctly rounded / and sqrt.
+HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+               "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
+               "-Wall", "-Wno-unused-result"]
+
+
+def _stale(out: str, deps) -> bool:
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_library(force: bool = False, verbose: bool = False) -> str:
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
+    deps.append(os.path.join(ROOT, "include", "gdf.h"))
+    if not force and not _stale(LIB_PATH, deps):
+        return LIB_PATH
+    os.makedirs(os.path.dirname(LIB_PATH), exist_ok=True)
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    cmd = [hipcc, *HIPCC_FLAGS, "-I" + os.path.join(ROOT, "include"), "-I" + CSRC,
+           "-o", LIB_PATH + ".tmp", *[os.path.join(CSRC, f) for f in SOURCES]]
+    if verbose:
+        print(" ".join(cmd))
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("hipcc failed:\n" + r.stdout + r.stderr)
+    os.replace(LIB_PATH + ".tmp", LIB_PATH)
+    return LIB_PATH

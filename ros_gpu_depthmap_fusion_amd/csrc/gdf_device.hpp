@@ -1,0 +1,130 @@
+// gdf_device.hpp — data layout and float semantics shared by the gfx950 kernels.
+//
+// Float contract: binary32, correctly rounded / and sqrt
+// (-fhip-fp32-correctly-rounded-divide-sqrt), no FMA contraction (-ffp-contract=off), explicit
+// summation order — the same order the reference GLSL writes and the oracle restates, so
+// masks, voxel keys and occupancy come out bit-identical.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gdf {
+
+constexpr int kMaxCams = 16;          // GDF_MAX_CAMERAS
+constexpr int kFrameThreads = 256;    // compaction block: 4 waves
+constexpr int kFramePerThread = 4;    // 4 consecutive items per thread (8-byte depth load)
+constexpr int kFrameTile = kFrameThreads * kFramePerThread;  // 1024 items per tile
+constexpr int kSortThreads = 256;
+constexpr int kSortPerThread = 16;
+constexpr int kSortTile = kSortThreads * kSortPerThread;     // 4096 keys per tile
+constexpr int kGroupThreads = 256;
+constexpr int kGroupPerThread = 8;
+constexpr int kGroupTile = kGroupThreads * kGroupPerThread;  // 2048 sorted keys per tile
+constexpr uint32_t kSpinLimit = 1u << 26;                   // bounded look-back spins
+
+// One depth camera of the frame (DepthmapConversion, gpu_depthmap_fusion.h:163-176).
+// `off` is the camera's first index in the concatenated point space (fusion.cpp:1605-1626).
+// A halo camera (emit == 0, multi-GPU sharding) sits at a negative offset: its pixels are only
+// read as flying-pixel neighbours, exactly where the reference's uint index arithmetic lands in
+// the previous camera of the concatenated buffer.
+struct CamDesc {
+    int64_t off;            // first index in the concatenated point space
+    const uint16_t* depth;  // device pointer to pixel 0 of this camera
+    uint32_t W, H, n;
+    uint32_t emit;          // 1: pixels are processed; 0: halo camera, only read as neighbours
+    float scale, fx, fy, cx, cy;
+    float Tw[16];           // row-major T_world
+    float Tc[16];           // row-major T_crop
+    uint32_t pad[3];
+};
+static_assert(sizeof(CamDesc) % 16 == 0, "CamDesc must stay 16-byte sized");
+
+// Arguments of the fused compaction launch (k_frame).
+struct FrameArgs {
+    const CamDesc* cams;
+    int32_t ncams;
+    uint32_t depth_total;       // ΣP of emitting cameras' index space (tiles cover [0, depth_total))
+    uint32_t depth_tiles;
+    uint32_t total_tiles;
+    // flying-pixel filter (sh/filter_flying_pixels.glsl)
+    int32_t do_flying;
+    uint32_t F;
+    float thr;
+    int32_t rot45;
+    // crop (sh/crop_points.glsl)
+    int32_t do_crop;
+    float lo[3], hi[3];
+    // selected rollbuffer points (insertSelected + transform_points_indirect)
+    uint32_t sel_count;
+    const float4* ring;
+    uint64_t ring_cap;
+    uint64_t ring_first;        // physical index of logical point sel_point_start
+    uint32_t nseg;
+    const uint32_t* seg_start;  // relative first point of each covered sequence (ascending)
+    const uint32_t* seg_tf;     // transform index of that sequence
+    const float* tfw;           // row-major T_world_move·T_move per selected sequence
+    const float* tfc;
+    // voxel keys + occupancy marks (compute_voxel_coords + voxel_grid_occupancy_of_points)
+    int32_t do_voxel;
+    int32_t occ_mode;           // 0 none, 1 mark bit 7 of the u8 grid, 2 set u8 flag array
+    float vlo[3], vcs[3], gmax[3];
+    uint32_t gs[3];
+    uint8_t* occ;
+    // outputs
+    float4* out_pts;
+    uint32_t* out_coords;
+    uint32_t* out_count;
+    uint8_t* dbg;               // optional per-item stage bits
+    // decoupled look-back
+    unsigned long long* status;
+    uint32_t* tile_ctr;
+    uint32_t* err;
+};
+
+// ---- canonical float helpers (mirror oracle/gdf_oracle.c) ----------------------------------
+__device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, float by, float bz) {
+    return (ax * bx + ay * by) + az * bz;
+}
+
+// out = M·p, ((m0·x + m1·y) + m2·z) + m3·w per row
+__device__ __forceinline__ float mrow(const float* m, float x, float y, float z, float w) {
+    return ((m[0] * x + m[1] * y) + m[2] * z) + m[3] * w;
+}
+
+// GLSL normalize(v) = v / length(v)
+__device__ __forceinline__ void normalize3(float& x, float& y, float& z) {
+    float l = sqrtf(dot3(x, y, z, x, y, z));
+    x = x / l;
+    y = y / l;
+    z = z / l;
+}
+
+// sh/convert_depthmap_to_points.glsl:64-81 (u = idx mod W, v = idx / W)
+__device__ __forceinline__ void cam_point(const CamDesc& c, uint32_t local, uint32_t d, float& x,
+                                          float& y, float& z) {
+    float u = (float)(local % c.W);
+    float v = (float)(local / c.W);
+    float zz = (float)d * c.scale;
+    float xn = (u - c.cx) / c.fx;
+    float yn = (v - c.cy) / c.fy;
+    x = xn * zz;
+    y = yn * zz;
+    z = zz;
+}
+
+// sh/compute_voxel_coords.glsl:44-53: clamp-then-floor per axis, x fastest
+__device__ __forceinline__ uint32_t voxel_key(float px, float py, float pz, const float* vlo,
+                                              const float* vcs, const float* gmax,
+                                              const uint32_t* gs) {
+    float fx = (px - vlo[0]) / vcs[0];
+    float fy = (py - vlo[1]) / vcs[1];
+    float fz = (pz - vlo[2]) / vcs[2];
+    fx = fminf(fmaxf(fx, 0.0f), gmax[0]);
+    fy = fminf(fmaxf(fy, 0.0f), gmax[1]);
+    fz = fminf(fmaxf(fz, 0.0f), gmax[2]);
+    uint32_t ux = (uint32_t)floorf(fx), uy = (uint32_t)floorf(fy), uz = (uint32_t)floorf(fz);
+    return ux + uy * gs[0] + uz * gs[0] * gs[1];
+}
+
+}  // namespace gdf

@@ -1,0 +1,1240 @@
+// gdf_engine.cpp — host runtime of the MI355X depth-fusion engine and the C-ABI of include/gdf.h.
+//
+// Replaces the reference's GL host layer (src/gpu_depthmap_fusion.cpp:29-1839 + the
+// StorageBuffer/ComputeProgram runtime in include/gpu_depthmap_fusion/*.h) with:
+//   - a grow-only device arena (DevBuf) instead of glBufferData-backed StorageBuffers;
+//   - one HIP stream per engine; stream order replaces every glMemoryBarrier;
+//   - a rollbuffer RING of points with the mask in w (O(new) insert, O(1) roll) instead of the
+//     reference's A/B double buffers that copy the whole window twice per frame
+//     (fusion.cpp:1005-1032, 1174-1207);
+//   - host mirrors of the sequence headers so roll/select need no device->host download
+//     (the reference downloads them, fusion.cpp:1102 and :1369);
+//   - deferred stage calls: convert/flying/crop/transform only record their parameters and
+//     run as ONE fused compaction launch (k_frame) when applyPointMask needs the result.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "gdf.h"
+#include "gdf_kernels.hpp"
+
+using namespace gdf;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct GdfError {
+    int code;
+    std::string msg;
+};
+
+[[noreturn]] void fail(int code, const std::string& msg) { throw GdfError{code, msg}; }
+
+#define HIPCHK(expr)                                                                       \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            fail(GDF_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));          \
+    } while (0)
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    // grow-only; contents are NOT preserved (like StorageBuffer::resize, storage_buffer.h:25-44)
+    bool ensure(size_t need) {
+        if (need <= bytes) return false;
+        size_t nb = std::max(need, bytes + bytes / 2);
+        nb = (nb + 255) & ~size_t(255);
+        void* q = nullptr;
+        if (p) {
+            HIPCHK(hipDeviceSynchronize());
+            HIPCHK(hipFree(p));
+            p = nullptr;
+            bytes = 0;
+        }
+        hipError_t e = hipMalloc(&q, nb);
+        if (e != hipSuccess) fail(GDF_ERR_NOMEM, "hipMalloc of " + std::to_string(nb) + " bytes failed");
+        p = q;
+        bytes = nb;
+        return true;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+struct Hdr {  // PointSequence, gpu_depthmap_fusion.h:178-204
+    uint32_t sec, nsec, start, num;
+    float T[16];
+};
+
+struct PsBuf {  // PointSequences, gpu_depthmap_fusion.h:206-217
+    uint32_t total = 0;
+    std::vector<Hdr> seqs;
+    std::vector<float> pts;
+    void clear() {
+        total = 0;
+        seqs.clear();
+        pts.clear();
+    }
+};
+
+struct Cam {
+    const uint16_t* host = nullptr;
+    const uint16_t* dev = nullptr;
+    uint32_t W, H, n;
+    float scale, fx, fy, cx, cy;
+    float Tw[16], Tc[16];
+};
+
+int compare_time(uint32_t sa, uint32_t na, uint32_t sb, uint32_t nb) {  // fusion.cpp:1089-1096
+    if (sa < sb) return -1;
+    if (sa > sb) return +1;
+    if (na < nb) return -1;
+    if (na > nb) return +1;
+    return 0;
+}
+
+// R = A·B row-major, ((a0·b0 + a1·b1) + a2·b2) + a3·b3 (rollbuffer_transfer_selected_transforms
+// .glsl:60-65 computes Move^T·World^T on the transposed storage = (T_world_move·T_move)^T)
+void mat_mul(const float* A, const float* B, float* R) {
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 4; ++c)
+            R[4 * r + c] = ((A[4 * r + 0] * B[0 * 4 + c] + A[4 * r + 1] * B[1 * 4 + c]) +
+                            A[4 * r + 2] * B[2 * 4 + c]) + A[4 * r + 3] * B[3 * 4 + c];
+}
+
+// ros::Time - ros::Duration(double) as in roscpp_core (DurationBase::fromSec,
+// normalizeSecNSecSigned/Unsigned); false where ROS would throw.
+bool ros_time_minus(uint32_t sec, uint32_t nsec, double seconds, uint32_t* os, uint32_t* ons) {
+    int64_t dsec64 = (int64_t)std::floor(seconds);
+    if (dsec64 < INT32_MIN || dsec64 > INT32_MAX) return false;
+    int32_t dsec = (int32_t)dsec64;
+    int32_t dnsec = (int32_t)std::round((seconds - (double)dsec) * 1e9);
+    int32_t rollover = (int32_t)((int64_t)dnsec / 1000000000LL);
+    dsec += rollover;
+    dnsec = (int32_t)((int64_t)dnsec % 1000000000LL);
+    int64_t ns = -(int64_t)dnsec, ss = -(int64_t)dsec;
+    int64_t np = ns % 1000000000LL, sp = ss + ns / 1000000000LL;
+    if (np < 0) { np += 1000000000LL; --sp; }
+    if (sp < INT32_MIN || sp > INT32_MAX) return false;
+    int64_t sec_sum = (int64_t)sec + sp, nsec_sum = (int64_t)nsec + np;
+    int64_t np2 = nsec_sum % 1000000000LL, sp2 = sec_sum + nsec_sum / 1000000000LL;
+    if (np2 < 0) { np2 += 1000000000LL; --sp2; }
+    if (sp2 < 0 || sp2 > 0xFFFFFFFFLL) return false;
+    *os = (uint32_t)sp2;
+    *ons = (uint32_t)np2;
+    return true;
+}
+
+enum MiscSlot { kCount = 0, kTileCtr = 1, kErr = 2, kVoxCount = 3, kSortCtrs = 4, kMiscWords = 16 };
+
+}  // namespace
+
+struct gdf_engine {
+    int device = 0;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+    std::mutex ps_mutex;
+    int voxel_group_size = 1024;
+
+    // point-sequence collect/upload double buffer (fusion.cpp:734-746)
+    PsBuf psA, psB;
+    PsBuf* collect = &psA;
+    PsBuf* upload = &psB;
+
+    // frame inputs
+    std::vector<Cam> cams;
+    uint32_t depth_total = 0;
+    std::vector<CamDesc> halo;      // halo cameras (multi-GPU), negative offsets
+    DevBuf d_depth, d_cams;
+    std::vector<CamDesc> h_cams;
+    bool depth_uploaded = false;
+
+    // new sequences on the device
+    DevBuf d_new;
+    uint32_t n_new = 0;
+    std::vector<Hdr> new_hdrs;
+    bool ps_filter_set = false;
+    float ps_thr = 0.f;
+    uint32_t ps_F = 0;
+
+    // rollbuffer ring + host header mirrors of the A (after insert) / B (after roll) buffers
+    DevBuf d_ring;
+    uint64_t ring_cap = 0, ring_head = 0;
+    std::vector<Hdr> hdrA, hdrB;
+    gdf_rollbuffer_state rb{};
+
+    // selected rollbuffer points
+    uint32_t n_total = 0;
+    bool prepared = false, sel_inserted = false;
+    DevBuf d_seg_start, d_seg_tf, d_tfw, d_tfc;
+    uint32_t nseg = 0;
+
+    // deferred depth plan
+    bool converted = false, flying_set = false, crop_set = false;
+    uint32_t F = 0;
+    float thr = 0.f;
+    int rot45 = 0;
+    float lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
+
+    // compaction outputs
+    DevBuf d_pts, d_coords, d_status, d_dbg;
+    DevBuf d_misc;
+    uint32_t* h_misc = nullptr;  // pinned
+    bool compacted = false, coords_valid = false, marks_set = false;
+    uint32_t dbg_count = 0;
+
+    // voxel grid
+    bool grid_set = false;
+    float vlo[3] = {0, 0, 0}, vhi[3] = {0, 0, 0}, vcs[3] = {0, 0, 0};
+    uint32_t gs[3] = {0, 0, 0};
+    uint64_t ncells = 0;
+    uint32_t key_bits = 0;
+    VoxelParams vp{};
+    DevBuf d_grid8, d_hist32, d_marks, d_out8;
+    int grid_mode = 0;  // 0: u8 grid with mark bit 7; 1: u32 history + u8 marks + u8 output
+    bool grid_alloc = false;
+    bool invoked_once = false;
+
+    // voxelize
+    DevBuf d_ka, d_kb, d_va, d_vb, d_shist, d_sstatus, d_gstatus, d_vox;
+    bool vox_valid = false;
+
+    bool debug = false;
+
+    // live timing: event pairs per launch, resolved on query
+    bool profiling = false;
+    struct EvPair { hipEvent_t a, b; int slot; };
+    std::vector<EvPair> ev_pending;
+    std::vector<hipEvent_t> ev_pool;
+    double prof_ms[GDF_KERNEL_SLOTS] = {0, 0, 0, 0};
+    uint64_t prof_n[GDF_KERNEL_SLOTS] = {0, 0, 0, 0};
+
+    hipStream_t s() const { return stream; }
+
+    hipEvent_t take_event() {
+        if (!ev_pool.empty()) {
+            hipEvent_t ev = ev_pool.back();
+            ev_pool.pop_back();
+            return ev;
+        }
+        hipEvent_t ev;
+        HIPCHK(hipEventCreate(&ev));
+        return ev;
+    }
+    // brackets one launch (or launch group) of `slot` with an event pair when profiling
+    template <class F>
+    void timed(int slot, F&& launch) {
+        if (!profiling) {
+            launch();
+            return;
+        }
+        EvPair p{take_event(), take_event(), slot};
+        HIPCHK(hipEventRecord(p.a, stream));
+        launch();
+        HIPCHK(hipEventRecord(p.b, stream));
+        ev_pending.push_back(p);
+        if (ev_pending.size() > 4096) resolve_events();
+    }
+    void resolve_events() {
+        for (EvPair& p : ev_pending) {
+            HIPCHK(hipEventSynchronize(p.b));
+            float ms = 0.f;
+            HIPCHK(hipEventElapsedTime(&ms, p.a, p.b));
+            prof_ms[p.slot] += ms;
+            prof_n[p.slot] += 1;
+            ev_pool.push_back(p.a);
+            ev_pool.push_back(p.b);
+        }
+        ev_pending.clear();
+    }
+
+    void sync() {
+        HIPCHK(hipStreamSynchronize(stream));
+        if (h_misc && h_misc[kErr]) {
+            const uint32_t e = h_misc[kErr];
+            h_misc[kErr] = 0;
+            HIPCHK(hipMemsetAsync(d_misc.as<uint32_t>() + kErr, 0, 4, stream));
+            fail(GDF_ERR_DEVICE, "device look-back spin limit expired (code " + std::to_string(e) + ")");
+        }
+    }
+    // read the small device counters into pinned memory (after the producing kernels)
+    void read_misc() {
+        HIPCHK(hipMemcpyAsync(h_misc, d_misc.p, kMiscWords * 4, hipMemcpyDeviceToHost, stream));
+        sync();
+    }
+};
+
+namespace {
+
+// ---- frame inputs ---------------------------------------------------------------------------------
+void engine_clear(gdf_engine* e) {  // fusion.cpp:725-732
+    e->rb.selection_point_count = 0;
+    e->rb.selection_sequence_count = 0;
+    e->depth_total = 0;
+    e->cams.clear();
+    e->depth_uploaded = false;
+    e->converted = e->flying_set = e->crop_set = false;
+    e->prepared = e->sel_inserted = false;
+}
+
+void add_depthmap(gdf_engine* e, const uint16_t* host, const uint16_t* dev, uint32_t W, uint32_t H,
+                  float scale, float fx, float fy, float cx, float cy, const float* Tw,
+                  const float* Tc) {
+    if ((!host && !dev) || !Tw || !Tc || W == 0 || H == 0) fail(GDF_ERR_ARG, "addDepthmap: bad argument");
+    if (e->cams.size() >= GDF_MAX_CAMERAS) fail(GDF_ERR_ARG, "addDepthmap: too many cameras");
+    if ((uint64_t)W * H >= (1ull << 24))
+        fail(GDF_ERR_ARG, "addDepthmap: W*H must stay below 2^24 (exact f32 pixel coordinates)");
+    if ((uint64_t)e->depth_total + (uint64_t)W * H >= (1ull << 31))
+        fail(GDF_ERR_ARG, "addDepthmap: total pixels exceed 2^31");
+    Cam c;
+    c.host = host;
+    c.dev = dev;
+    c.W = W; c.H = H; c.n = W * H;
+    c.scale = scale; c.fx = fx; c.fy = fy; c.cx = cx; c.cy = cy;
+    std::memcpy(c.Tw, Tw, 64);
+    std::memcpy(c.Tc, Tc, 64);
+    e->cams.push_back(c);
+    e->depth_total += c.n;
+    e->depth_uploaded = false;
+}
+
+void add_point_sequence(gdf_engine* e, const void* rec, uint32_t n, uint32_t step, uint32_t sec,
+                        uint32_t nsec, const float* Tm) {  // fusion.cpp:747-796
+    if ((n && (!rec || step < 12)) || !Tm) fail(GDF_ERR_ARG, "addPointSequence: bad argument");
+    std::lock_guard<std::mutex> lk(e->ps_mutex);
+    PsBuf* b = e->collect;
+    Hdr h;
+    h.sec = sec; h.nsec = nsec; h.start = b->total; h.num = n;
+    std::memcpy(h.T, Tm, 64);
+    b->pts.resize((size_t)(b->total + n) * 4);
+    const uint8_t* r = static_cast<const uint8_t*>(rec);
+    float* o = b->pts.data() + (size_t)h.start * 4;
+    for (uint32_t k = 0; k < n; ++k) {
+        std::memcpy(o + 4 * (size_t)k, r + (size_t)k * step, 12);
+        o[4 * (size_t)k + 3] = 1.0f;
+    }
+    b->total += n;
+    b->seqs.push_back(h);
+}
+
+// ---- point-sequence chain -----------------------------------------------------------------------
+void upload_point_sequences(gdf_engine* e) {  // fusion.cpp:819-857
+    std::lock_guard<std::mutex> lk(e->ps_mutex);
+    if (e->collect == &e->psA) { e->upload = &e->psA; e->collect = &e->psB; }
+    else { e->collect = &e->psA; e->upload = &e->psB; }
+    e->collect->clear();
+    e->n_new = e->upload->total;
+    e->new_hdrs = e->upload->seqs;
+    if (e->n_new) {
+        e->d_new.ensure((size_t)e->n_new * 16);
+        HIPCHK(hipMemcpyWithStream(e->d_new.p, e->upload->pts.data(), (size_t)e->n_new * 16,
+                                   hipMemcpyHostToDevice, e->s()));
+    }
+    e->ps_filter_set = false;
+}
+
+void ensure_ring(gdf_engine* e, uint64_t need) {
+    if (need <= e->ring_cap) return;
+    uint64_t cap = std::max<uint64_t>(need + need / 2, 1u << 20);
+    void* q = nullptr;
+    HIPCHK(hipStreamSynchronize(e->s()));
+    if (hipMalloc(&q, cap * 16) != hipSuccess) fail(GDF_ERR_NOMEM, "rollbuffer ring allocation failed");
+    const uint64_t R = e->rb.num_points;
+    if (R && e->d_ring.p) {  // linearise the live window into the new ring
+        const uint64_t first = e->ring_head % e->ring_cap;
+        const uint64_t a = std::min<uint64_t>(R, e->ring_cap - first);
+        HIPCHK(hipMemcpyAsync(q, e->d_ring.as<float4>() + first, a * 16, hipMemcpyDeviceToDevice, e->s()));
+        if (R > a)
+            HIPCHK(hipMemcpyAsync(static_cast<float4*>(q) + a, e->d_ring.p, (R - a) * 16,
+                                  hipMemcpyDeviceToDevice, e->s()));
+        HIPCHK(hipStreamSynchronize(e->s()));
+    }
+    if (e->d_ring.p) HIPCHK(hipFree(e->d_ring.p));
+    e->d_ring.p = q;
+    e->d_ring.bytes = cap * 16;
+    e->ring_cap = cap;
+    e->ring_head = 0;
+}
+
+void insert_new_point_sequences(gdf_engine* e) {  // fusion.cpp:979-1087
+    const uint32_t R = e->rb.num_points, S = e->rb.num_seqs;
+    if (e->hdrB.size() < S) fail(GDF_ERR_STATE, "insert: rollbuffer headers out of sync");
+    if ((uint64_t)R + e->n_new >= (1ull << 31)) fail(GDF_ERR_CAPACITY, "rollbuffer exceeds 2^31 points");
+    ensure_ring(e, (uint64_t)R + e->n_new);
+    if (e->n_new)
+        e->timed(GDF_KERNEL_PS_INSERT, [&] {
+            HIPCHK(launch_ps_filter_insert(e->d_new.as<float4>(), e->n_new, e->ps_filter_set ? 1 : 0,
+                                           e->ps_thr, e->ps_F, e->d_ring.as<float4>(), e->ring_cap,
+                                           (e->ring_head + R) % e->ring_cap, e->s()));
+        });
+    e->hdrA.assign(e->hdrB.begin(), e->hdrB.begin() + S);
+    e->hdrA.insert(e->hdrA.end(), e->new_hdrs.begin(), e->new_hdrs.end());
+    e->rb.num_points = R + e->n_new;
+    e->rb.num_seqs = S + (uint32_t)e->new_hdrs.size();
+    if (!e->new_hdrs.empty()) {
+        e->rb.last_time_sec = e->new_hdrs.back().sec;
+        e->rb.last_time_nsec = e->new_hdrs.back().nsec;
+    }
+}
+
+void roll_rollbuffer(gdf_engine* e, uint32_t min_sec, uint32_t min_nsec) {  // fusion.cpp:1098-1217
+    uint32_t d_seqs = 0, d_pts = 0;
+    const uint32_t nseq = (uint32_t)e->hdrA.size();
+    for (uint32_t i = 0; i < nseq; ++i) {
+        const Hdr& q = e->hdrA[i];
+        if (compare_time(q.sec, q.nsec, min_sec, min_nsec) < 0) {
+            d_pts += q.num;
+        } else {
+            d_seqs = i;
+            break;
+        }
+    }
+    if (nseq > d_seqs) {
+        e->rb.earliest_time_sec = e->hdrA[d_seqs].sec;
+        e->rb.earliest_time_nsec = e->hdrA[d_seqs].nsec;
+    } else {
+        e->rb.earliest_time_sec = e->rb.earliest_time_nsec = 0;
+        e->rb.last_time_sec = e->rb.last_time_nsec = 0;
+    }
+    if (d_pts > e->rb.num_points || d_seqs > e->rb.num_seqs)
+        fail(GDF_ERR_STATE, "roll: discarded points exceed the rollbuffer (reference uint underflow)");
+    if (e->ring_cap) e->ring_head = (e->ring_head + d_pts) % e->ring_cap;
+    e->hdrB.assign(e->hdrA.begin() + d_seqs, e->hdrA.end());
+    e->rb.num_points -= d_pts;
+    e->rb.num_seqs -= d_seqs;
+}
+
+void select_timespan(gdf_engine* e, uint32_t mins, uint32_t minn, uint32_t maxs,
+                     uint32_t maxn) {  // fusion.cpp:1358-1416
+    const uint32_t num_seqs = e->rb.num_seqs;
+    int64_t start = num_seqs, last = 0;
+    uint32_t pcount = 0, pstart = 0;
+    for (uint32_t i = 0; i < e->hdrB.size(); ++i) {
+        const Hdr& q = e->hdrB[i];
+        if (compare_time(mins, minn, q.sec, q.nsec) <= 0 && compare_time(q.sec, q.nsec, maxs, maxn) <= 0) {
+            if ((int64_t)i < start) start = i;
+            if ((int64_t)i > last) last = i;
+            pcount += q.num;
+        }
+    }
+    const int64_t count = last < start ? 0 : 1 + last - start;
+    for (int64_t i = 0; i < start && i < (int64_t)e->hdrB.size(); ++i) pstart += e->hdrB[i].num;
+    e->rb.selection_point_start = pstart;
+    e->rb.selection_point_count = pcount;
+    e->rb.selection_sequence_start = (uint32_t)start;
+    e->rb.selection_sequence_count = (uint32_t)count;
+}
+
+void prepare_buffers(gdf_engine* e) {  // fusion.cpp:1497-1508
+    const uint64_t n = (uint64_t)e->depth_total + e->rb.selection_point_count;
+    if (n >= (1ull << 31)) fail(GDF_ERR_CAPACITY, "more than 2^31 points in one frame");
+    e->n_total = (uint32_t)n;
+    e->d_pts.ensure((size_t)(n ? n : 1) * 16);
+    e->d_coords.ensure((size_t)(n ? n : 1) * 4);
+    e->prepared = true;
+}
+
+void insert_selected(gdf_engine* e, const float* Twm, const float* Tcm) {  // fusion.cpp:1509-1553
+    if (!Twm || !Tcm) fail(GDF_ERR_ARG, "insertSelectedPointSequence: null transform");
+    if (!e->prepared) fail(GDF_ERR_STATE, "insertSelectedPointSequence before preparePointAndMaskBuffers");
+    const uint32_t ps = e->rb.selection_point_start, cnt = e->rb.selection_point_count;
+    const uint32_t ss = e->rb.selection_sequence_start, sc = e->rb.selection_sequence_count;
+    if ((uint64_t)e->depth_total + cnt > e->n_total) fail(GDF_ERR_STATE, "selection exceeds prepared buffers");
+    if (cnt && (uint64_t)ps + cnt > e->rb.num_points) fail(GDF_ERR_STATE, "selection exceeds rollbuffer points");
+    if (sc && (uint64_t)ss + sc > e->hdrB.size()) fail(GDF_ERR_STATE, "selection exceeds rollbuffer sequences");
+    // transforms of the selected sequences (kernel 19 of SURVEY §2b, computed host-side)
+    std::vector<float> tfw((size_t)std::max<uint32_t>(sc, 1) * 16), tfc(tfw.size());
+    for (uint32_t j = 0; j < sc; ++j) {
+        mat_mul(Twm, e->hdrB[ss + j].T, tfw.data() + 16 * (size_t)j);
+        mat_mul(Tcm, e->hdrB[ss + j].T, tfc.data() + 16 * (size_t)j);
+    }
+    // transform index per point = seq_idx[p] - seq_idx[sel_point_start] (kernel 18): the points
+    // of sequence j get index j - s0, s0 = sequence containing point sel_point_start.
+    std::vector<uint32_t> seg_start, seg_tf;
+    if (cnt) {
+        uint64_t cum = 0;
+        int64_t s0 = -1;
+        for (uint32_t j = 0; j < e->hdrB.size(); ++j) {
+            const uint64_t a = cum, b = cum + e->hdrB[j].num;
+            cum = b;
+            if (b <= ps || a == b) continue;
+            if (a >= (uint64_t)ps + cnt) break;
+            if (s0 < 0) s0 = j;
+            const uint64_t rel = a > ps ? a - ps : 0;
+            const uint32_t t = (uint32_t)(j - s0);
+            if (t >= sc) fail(GDF_ERR_STATE, "transform index outside the selected sequences");
+            seg_start.push_back((uint32_t)rel);
+            seg_tf.push_back(t);
+        }
+        if (seg_start.empty()) fail(GDF_ERR_STATE, "selected points not covered by sequences");
+    }
+    e->nseg = (uint32_t)seg_start.size();
+    if (e->nseg) {
+        e->d_seg_start.ensure(e->nseg * 4);
+        e->d_seg_tf.ensure(e->nseg * 4);
+        HIPCHK(hipMemcpyWithStream(e->d_seg_start.p, seg_start.data(), e->nseg * 4, hipMemcpyHostToDevice, e->s()));
+        HIPCHK(hipMemcpyWithStream(e->d_seg_tf.p, seg_tf.data(), e->nseg * 4, hipMemcpyHostToDevice, e->s()));
+    }
+    e->d_tfw.ensure(tfw.size() * 4);
+    e->d_tfc.ensure(tfc.size() * 4);
+    HIPCHK(hipMemcpyWithStream(e->d_tfw.p, tfw.data(), tfw.size() * 4, hipMemcpyHostToDevice, e->s()));
+    HIPCHK(hipMemcpyWithStream(e->d_tfc.p, tfc.data(), tfc.size() * 4, hipMemcpyHostToDevice, e->s()));
+    e->sel_inserted = true;
+}
+
+// ---- depth chain ------------------------------------------------------------------------------------
+void upload_depthmaps(gdf_engine* e) {  // fusion.cpp:1583-1593
+    uint64_t host_px = 0;
+    for (const Cam& c : e->cams) if (!c.dev) host_px += c.n;
+    if (host_px) e->d_depth.ensure(host_px * 2);
+    e->h_cams.clear();
+    uint64_t off = 0, hoff = 0;
+    for (const Cam& c : e->cams) {
+        CamDesc d{};
+        d.off = (int64_t)off;
+        if (c.dev) {
+            d.depth = c.dev;
+        } else {
+            uint16_t* dst = e->d_depth.as<uint16_t>() + hoff;
+            HIPCHK(hipMemcpyWithStream(dst, c.host, (size_t)c.n * 2, hipMemcpyHostToDevice, e->s()));
+            d.depth = dst;
+            hoff += c.n;
+        }
+        d.W = c.W; d.H = c.H; d.n = c.n; d.emit = 1;
+        d.scale = c.scale; d.fx = c.fx; d.fy = c.fy; d.cx = c.cx; d.cy = c.cy;
+        std::memcpy(d.Tw, c.Tw, 64);
+        std::memcpy(d.Tc, c.Tc, 64);
+        e->h_cams.push_back(d);
+        off += c.n;
+    }
+    // halo cameras first (negative offsets), then the emitting cameras: sorted by offset
+    std::vector<CamDesc> all = e->halo;
+    all.insert(all.end(), e->h_cams.begin(), e->h_cams.end());
+    if (all.size() > (size_t)kMaxCams) fail(GDF_ERR_ARG, "too many cameras (incl. halo)");
+    e->h_cams = all;
+    if (!all.empty()) {
+        e->d_cams.ensure(all.size() * sizeof(CamDesc));
+        HIPCHK(hipMemcpyWithStream(e->d_cams.p, all.data(), all.size() * sizeof(CamDesc),
+                                   hipMemcpyHostToDevice, e->s()));
+    }
+    e->depth_uploaded = true;
+}
+
+void set_grid(gdf_engine* e, const float* lo, const float* hi, const float* cs) {
+    // shader grid size (fusion.cpp:1693-1698) and VoxelGridMeta (grid_meta.h:140-158) must agree
+    uint32_t g[3];
+    uint64_t cells = 1;
+    for (int a = 0; a < 3; ++a) {
+        const float f = (hi[a] - lo[a]) / cs[a];
+        if (!(f > 0.0f) || !(f < 4294967040.0f)) fail(GDF_ERR_ARG, "voxel grid: need lower < upper and cell_size > 0");
+        g[a] = (uint32_t)std::ceil(f);
+        cells *= g[a];
+    }
+    if (cells >= 0xFFFFFFFFull) fail(GDF_ERR_ARG, "voxel grid: more than 2^32-1 cells");
+    std::memcpy(e->vlo, lo, 12);
+    std::memcpy(e->vhi, hi, 12);
+    std::memcpy(e->vcs, cs, 12);
+    std::memcpy(e->gs, g, 12);
+    for (int a = 0; a < 3; ++a) {
+        e->vp.vlo[a] = lo[a];
+        e->vp.vcs[a] = cs[a];
+        e->vp.gmax[a] = (float)(g[a] - 1u);
+        e->vp.gs[a] = g[a];
+    }
+    e->key_bits = cells <= 1 ? 0u : 64u - (uint32_t)__builtin_clzll(cells - 1);
+    const bool changed = !e->grid_alloc || cells != e->ncells;
+    e->ncells = cells;
+    e->grid_set = true;
+    if (changed) {  // historic grid cleared on first use / resize (fusion.cpp:1759-1773)
+        const size_t padded = (size_t)((cells + 15) / 16) * 16;
+        e->d_grid8.ensure(padded);
+        HIPCHK(hipMemsetAsync(e->d_grid8.p, 0, padded, e->s()));
+        e->grid_mode = 0;
+        e->grid_alloc = true;
+        e->marks_set = false;
+    }
+}
+
+int occ_mode(const gdf_engine* e) { return e->grid_mode == 0 ? 1 : 2; }
+uint8_t* occ_ptr(const gdf_engine* e) {
+    return e->grid_mode == 0 ? e->d_grid8.as<uint8_t>() : e->d_marks.as<uint8_t>();
+}
+
+void ensure_misc(gdf_engine* e) {
+    if (!e->d_misc.p) {
+        e->d_misc.ensure(kMiscWords * 4);
+        HIPCHK(hipMemsetAsync(e->d_misc.p, 0, kMiscWords * 4, e->s()));
+    }
+}
+
+// The fused compaction launch: convert + flying + crop + selected-point transform + ordered
+// compaction (+ voxel keys and occupancy marks when fused_voxel).
+void run_frame(gdf_engine* e, bool fused_voxel) {
+    if (!e->prepared) prepare_buffers(e);
+    if (!e->depth_uploaded) upload_depthmaps(e);
+    ensure_misc(e);
+    FrameArgs a{};
+    a.cams = e->d_cams.as<CamDesc>();
+    a.ncams = (int32_t)e->h_cams.size();
+    a.depth_total = e->depth_total;
+    a.depth_tiles = (e->depth_total + kFrameTile - 1) / kFrameTile;
+    const uint32_t sel = e->sel_inserted ? e->rb.selection_point_count : 0u;
+    const uint32_t sel_tiles = (sel + kFrameTile - 1) / kFrameTile;
+    a.total_tiles = a.depth_tiles + sel_tiles;
+    a.do_flying = e->flying_set ? 1 : 0;
+    a.F = e->F;
+    a.thr = e->thr;
+    a.rot45 = e->rot45;
+    a.do_crop = e->crop_set ? 1 : 0;
+    std::memcpy(a.lo, e->lo, 12);
+    std::memcpy(a.hi, e->hi, 12);
+    a.sel_count = sel;
+    a.ring = e->d_ring.as<const float4>();
+    a.ring_cap = e->ring_cap ? e->ring_cap : 1;
+    a.ring_first = e->ring_cap ? (e->ring_head + e->rb.selection_point_start) % e->ring_cap : 0;
+    a.nseg = e->nseg;
+    a.seg_start = e->d_seg_start.as<uint32_t>();
+    a.seg_tf = e->d_seg_tf.as<uint32_t>();
+    a.tfw = e->d_tfw.as<float>();
+    a.tfc = e->d_tfc.as<float>();
+    a.do_voxel = fused_voxel ? 1 : 0;
+    if (fused_voxel) {
+        a.occ_mode = occ_mode(e);
+        a.occ = occ_ptr(e);
+        std::memcpy(a.vlo, e->vp.vlo, 12);
+        std::memcpy(a.vcs, e->vp.vcs, 12);
+        std::memcpy(a.gmax, e->vp.gmax, 12);
+        std::memcpy(a.gs, e->vp.gs, 12);
+    }
+    a.out_pts = e->d_pts.as<float4>();
+    a.out_coords = e->d_coords.as<uint32_t>();
+    a.out_count = e->d_misc.as<uint32_t>() + kCount;
+    if (e->debug) {
+        e->d_dbg.ensure((size_t)std::max<uint32_t>(e->n_total, 1));
+        a.dbg = e->d_dbg.as<uint8_t>();
+        e->dbg_count = e->n_total;
+    }
+    e->d_status.ensure((size_t)std::max<uint32_t>(a.total_tiles, 1) * 8);
+    a.status = e->d_status.as<unsigned long long>();
+    a.tile_ctr = e->d_misc.as<uint32_t>() + kTileCtr;
+    a.err = e->d_misc.as<uint32_t>() + kErr;
+    e->timed(GDF_KERNEL_FRAME, [&] { HIPCHK(launch_frame(a, e->s())); });
+    e->compacted = true;
+    e->coords_valid = fused_voxel;
+    e->marks_set = fused_voxel;
+    e->vox_valid = false;
+}
+
+void compute_voxel_coords(gdf_engine* e, const float* lo, const float* hi, const float* cs) {
+    if (!e->compacted) fail(GDF_ERR_STATE, "computeVoxelCoords before applyPointMask");
+    set_grid(e, lo, hi, cs);
+    HIPCHK(launch_coords(e->d_pts.as<float4>(), e->d_misc.as<uint32_t>() + kCount,
+                         std::max<uint32_t>(e->n_total, 1), e->d_coords.as<uint32_t>(), e->vp, e->s()));
+    e->coords_valid = true;
+    e->marks_set = false;
+}
+
+void voxelize(gdf_engine* e, int average) {  // fusion.cpp:1743-1756
+    if (!e->grid_set || !e->coords_valid) fail(GDF_ERR_STATE, "voxelize before computeVoxelCoords");
+    const uint32_t nmax = std::max<uint32_t>(e->n_total, 1);
+    if (nmax >= (1u << 30)) fail(GDF_ERR_CAPACITY, "voxelize supports < 2^30 points");
+    e->d_ka.ensure((size_t)nmax * 4);
+    e->d_kb.ensure((size_t)nmax * 4);
+    e->d_va.ensure((size_t)nmax * 4);
+    e->d_vb.ensure((size_t)nmax * 4);
+    e->d_shist.ensure(4 * 256 * 4 + 8 * 4);
+    e->d_sstatus.ensure(voxelize_status_words(nmax) * 4);
+    e->d_gstatus.ensure(voxelize_group_tiles(nmax) * 8);
+    e->d_vox.ensure((size_t)nmax * 16);
+    VoxelizeArgs v{};
+    v.keys = e->d_coords.as<uint32_t>();
+    v.pts = e->d_pts.as<float4>();
+    v.count = e->d_misc.as<uint32_t>() + kCount;
+    v.nmax = nmax;
+    v.key_bits = e->key_bits;
+    v.average = average;
+    v.vp = e->vp;
+    v.keys_a = e->d_ka.as<uint32_t>();
+    v.keys_b = e->d_kb.as<uint32_t>();
+    v.vals_a = e->d_va.as<uint32_t>();
+    v.vals_b = e->d_vb.as<uint32_t>();
+    v.hist = e->d_shist.as<uint32_t>();
+    v.ctrs = e->d_shist.as<uint32_t>() + 4 * 256;
+    v.status = e->d_sstatus.as<uint32_t>();
+    v.gstatus = e->d_gstatus.as<unsigned long long>();
+    v.err = e->d_misc.as<uint32_t>() + kErr;
+    v.out = e->d_vox.as<float4>();
+    v.out_count = e->d_misc.as<uint32_t>() + kVoxCount;
+    e->timed(GDF_KERNEL_VOXELIZE, [&] { HIPCHK(launch_voxelize(v, e->s())); });
+    e->vox_valid = true;
+}
+
+void occupancy_grid(gdf_engine* e, uint32_t lifetime) {  // fusion.cpp:1757-1823
+    if (!e->grid_set) fail(GDF_ERR_STATE, "voxelOccupancyGrid before computeVoxelCoords");
+    if (e->grid_mode == 0 && lifetime > 127) {
+        // widen the u8 grid (values <= 127, mark in bit 7) into the general u32 history
+        e->d_hist32.ensure((size_t)e->ncells * 4);
+        e->d_marks.ensure((size_t)e->ncells);
+        e->d_out8.ensure((size_t)((e->ncells + 15) / 16) * 16);
+        HIPCHK(launch_widen_grid(e->d_grid8.as<uint8_t>(), e->d_hist32.as<uint32_t>(),
+                                 e->d_marks.as<uint8_t>(), e->ncells, e->s()));
+        e->grid_mode = 1;
+    }
+    if (!e->marks_set) {
+        if (!e->coords_valid) fail(GDF_ERR_STATE, "voxelOccupancyGrid needs voxel coordinates");
+        HIPCHK(launch_scatter(e->d_coords.as<uint32_t>(), e->d_misc.as<uint32_t>() + kCount,
+                              std::max<uint32_t>(e->n_total, 1), occ_ptr(e), occ_mode(e), e->s()));
+    }
+    e->timed(GDF_KERNEL_GRID, [&] {
+        if (e->grid_mode == 0)
+            HIPCHK(launch_grid_u8(e->d_grid8.as<uint8_t>(), e->ncells, lifetime, e->s()));
+        else
+            HIPCHK(launch_grid_u32(e->d_hist32.as<uint32_t>(), e->d_marks.as<uint8_t>(),
+                                   e->d_out8.as<uint8_t>(), e->ncells, lifetime, e->s()));
+    });
+    e->marks_set = false;
+    e->invoked_once = true;
+}
+
+const uint8_t* grid_out_ptr(const gdf_engine* e) {
+    return e->grid_mode == 0 ? e->d_grid8.as<uint8_t>() : e->d_out8.as<uint8_t>();
+}
+
+template <class F>
+int guarded(gdf_engine* e, F&& f) {
+    try {
+        if (e) HIPCHK(hipSetDevice(e->device));
+        f();
+        return GDF_OK;
+    } catch (const GdfError& err) {
+        g_last_error = err.msg;
+        return err.code;
+    } catch (const std::bad_alloc&) {
+        g_last_error = "host allocation failed";
+        return GDF_ERR_NOMEM;
+    } catch (...) {
+        g_last_error = "unknown error";
+        return GDF_ERR_STATE;
+    }
+}
+
+#define ENGINE_OR_FAIL(e)                                                   \
+    do {                                                                    \
+        if (!(e)) {                                                         \
+            g_last_error = "null engine";                                   \
+            return GDF_ERR_ARG;                                             \
+        }                                                                   \
+    } while (0)
+
+}  // namespace
+
+// ==== C-ABI ============================================================================================
+extern "C" {
+
+const char* gdf_last_error(void) { return g_last_error.c_str(); }
+
+int gdf_version(int* major, int* minor) {
+    if (major) *major = GDF_VERSION_MAJOR;
+    if (minor) *minor = GDF_VERSION_MINOR;
+    return GDF_OK;
+}
+
+int gdf_create(int device, gdf_engine** out) {
+    if (!out) {
+        g_last_error = "null output";
+        return GDF_ERR_ARG;
+    }
+    *out = nullptr;
+    gdf_engine* e = new (std::nothrow) gdf_engine();
+    if (!e) return GDF_ERR_NOMEM;
+    e->device = device;
+    int rc = guarded(e, [&] {
+        HIPCHK(hipStreamCreateWithFlags(&e->own, hipStreamNonBlocking));
+        e->stream = e->own;
+        HIPCHK(hipHostMalloc((void**)&e->h_misc, kMiscWords * 4, hipHostMallocDefault));
+        std::memset(e->h_misc, 0, kMiscWords * 4);
+        ensure_misc(e);
+        HIPCHK(hipStreamSynchronize(e->stream));
+    });
+    if (rc != GDF_OK) {
+        delete e;
+        return rc;
+    }
+    *out = e;
+    return GDF_OK;
+}
+
+int gdf_destroy(gdf_engine* e) {
+    if (!e) return GDF_OK;
+    (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    for (auto& p : e->ev_pending) {
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
+    }
+    for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
+    if (e->h_misc) (void)hipHostFree(e->h_misc);
+    if (e->own) (void)hipStreamDestroy(e->own);
+    delete e;
+    return GDF_OK;
+}
+
+int gdf_set_stream(gdf_engine* e, void* stream) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        HIPCHK(hipStreamSynchronize(e->stream));
+        e->stream = stream ? static_cast<hipStream_t>(stream) : e->own;
+    });
+}
+
+int gdf_synchronize(gdf_engine* e) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] { e->sync(); });
+}
+
+int gdf_set_voxel_group_size(gdf_engine* e, int group_size) {
+    ENGINE_OR_FAIL(e);
+    if (group_size <= 0) {
+        g_last_error = "voxel group size must be positive";
+        return GDF_ERR_ARG;
+    }
+    e->voxel_group_size = group_size;
+    return GDF_OK;
+}
+
+int gdf_clear(gdf_engine* e) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] { engine_clear(e); });
+}
+
+int gdf_add_depthmap(gdf_engine* e, const uint16_t* depth, uint32_t W, uint32_t H, float scale,
+                     float fx, float fy, float cx, float cy, const float Tw[16], const float Tc[16]) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] { add_depthmap(e, depth, nullptr, W, H, scale, fx, fy, cx, cy, Tw, Tc); });
+}
+
+int gdf_add_depthmap_device(gdf_engine* e, const uint16_t* depth, uint32_t W, uint32_t H,
+                            float scale, float fx, float fy, float cx, float cy, const float Tw[16],
+                            const float Tc[16]) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] { add_depthmap(e, nullptr, depth, W, H, scale, fx, fy, cx, cy, Tw, Tc); });
+}
+
+int gdf_add_point_sequence(gdf_engine* e, const void* rec, uint32_t n, uint32_t step,
+                           uint32_t sec, uint32_t nsec, const float Tm[16]) {
+    ENGINE_OR_FAIL(e);
+    return guarded(nullptr, [&] { add_point_sequence(e, rec, n, step, sec, nsec, Tm); });
+}
+
+int gdf_num_collected_point_sequence_points(gdf_engine* e, uint32_t* out) {
+    ENGINE_OR_FAIL(e);
+    if (!out) return GDF_ERR_ARG;
+    std::lock_guard<std::mutex> lk(e->ps_mutex);
+    *out = e->collect->total;
+    return GDF_OK;
+}
+
+int gdf_upload_point_sequences(gdf_engine* e) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] { upload_point_sequences(e); });
+}
+
+int gdf_filter_new_point_sequences(gdf_engine* e, float threshold, uint32_t filter_size) {
+    ENGINE_OR_FAIL(e);
+    e->ps_filter_set = true;
+    e->ps_thr = threshold;
+    e->ps_F = filter_size;
+    return GDF_OK;
+}
+
+int gdf_insert_new_point_sequences(gdf_engine* e) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] { insert_new_point_sequences(e); });
+}
+
+int gdf_roll_rollbuffer(gdf_engine* e, uint32_t min_sec, uint32_t min_nsec) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] { roll_rollbuffer(e, min_sec, min_nsec); });
+}
+
+int gdf_select_timespan(gdf_engine* e, uint32_t mins, uint32_t minn, uint32_t maxs, uint32_t maxn) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] { select_timespan(e, mins, minn, maxs, maxn); });
+}
+
+int gdf_prepare_point_and_mask_buffers(gdf_engine* e) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] { prepare_buffers(e); });
+}
+
+int gdf_insert_selected_point_sequence(gdf_engine* e, const float Twm[16], const float Tcm[16]) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] { insert_selected(e, Twm, Tcm); });
+}
+
+int gdf_transform_point_sequence(gdf_engine* e) {
+    ENGINE_OR_FAIL(e);
+    if (!e->sel_inserted && e->rb.selection_point_count) {
+        g_last_error = "transformPointSequence before insertSelectedPointSequence";
+        return GDF_ERR_STATE;
+    }
+    return GDF_OK;  // fused into the compaction launch
+}
+
+int gdf_get_rollbuffer_state(gdf_engine* e, gdf_rollbuffer_state* out) {
+    ENGINE_OR_FAIL(e);
+    if (!out) return GDF_ERR_ARG;
+    *out = e->rb;
+    return GDF_OK;
+}
+
+int gdf_upload_depthmaps(gdf_engine* e) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] { upload_depthmaps(e); });
+}
+
+int gdf_convert_depthmaps(gdf_engine* e) {
+    ENGINE_OR_FAIL(e);
+    if (!e->depth_uploaded) {
+        g_last_error = "convertDepthmaps before uploadDepthmaps";
+        return GDF_ERR_STATE;
+    }
+    e->converted = true;
+    return GDF_OK;
+}
+
+int gdf_filter_flying_pixels(gdf_engine* e, uint32_t filter_size, float threshold, int rot45) {
+    ENGINE_OR_FAIL(e);
+    e->flying_set = true;
+    e->F = filter_size;
+    e->thr = threshold;
+    e->rot45 = rot45 ? 1 : 0;
+    return GDF_OK;
+}
+
+int gdf_crop_points(gdf_engine* e, const float lower[3], const float upper[3]) {
+    ENGINE_OR_FAIL(e);
+    if (!lower || !upper) return GDF_ERR_ARG;
+    e->crop_set = true;
+    std::memcpy(e->lo, lower, 12);
+    std::memcpy(e->hi, upper, 12);
+    return GDF_OK;
+}
+
+int gdf_apply_point_mask(gdf_engine* e, uint32_t* out_count) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        run_frame(e, false);
+        if (out_count) {
+            e->read_misc();
+            *out_count = e->h_misc[kCount];
+        }
+    });
+}
+
+int gdf_compute_voxel_coords(gdf_engine* e, const float lo[3], const float hi[3], const float cs[3]) {
+    ENGINE_OR_FAIL(e);
+    if (!lo || !hi || !cs) return GDF_ERR_ARG;
+    return guarded(e, [&] { compute_voxel_coords(e, lo, hi, cs); });
+}
+
+int gdf_voxelize(gdf_engine* e, int average) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] { voxelize(e, average); });
+}
+
+int gdf_voxel_occupancy_grid(gdf_engine* e, uint32_t lifetime) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] { occupancy_grid(e, lifetime); });
+}
+
+int gdf_get_point_count(gdf_engine* e, uint32_t* out) {
+    ENGINE_OR_FAIL(e);
+    if (!out) return GDF_ERR_ARG;
+    return guarded(e, [&] {
+        if (!e->compacted) fail(GDF_ERR_STATE, "no compaction has run");
+        e->read_misc();
+        *out = e->h_misc[kCount];
+    });
+}
+
+int gdf_download_points(gdf_engine* e, float* out, uint32_t cap, uint32_t* out_count) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        if (!e->compacted) fail(GDF_ERR_STATE, "downloadPoints before applyPointMask");
+        e->read_misc();
+        const uint32_t n = e->h_misc[kCount];
+        if (out_count) *out_count = n;
+        if (out) {
+            if (cap < n) fail(GDF_ERR_CAPACITY, "downloadPoints: buffer too small");
+            if (n) HIPCHK(hipMemcpy(out, e->d_pts.p, (size_t)n * 16, hipMemcpyDeviceToHost));
+        }
+    });
+}
+
+int gdf_download_voxel_coords(gdf_engine* e, uint32_t* out, uint32_t cap, uint32_t* out_count) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        if (!e->coords_valid) fail(GDF_ERR_STATE, "downloadVoxelCoords before computeVoxelCoords");
+        e->read_misc();
+        const uint32_t n = e->h_misc[kCount];
+        if (out_count) *out_count = n;
+        if (out) {
+            if (cap < n) fail(GDF_ERR_CAPACITY, "downloadVoxelCoords: buffer too small");
+            if (n) HIPCHK(hipMemcpy(out, e->d_coords.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+        }
+    });
+}
+
+int gdf_download_voxelized_points(gdf_engine* e, float* out, uint32_t cap, uint32_t* out_count) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        if (!e->vox_valid) fail(GDF_ERR_STATE, "no voxelize has run");
+        e->read_misc();
+        const uint32_t n = e->h_misc[kVoxCount];
+        if (out_count) *out_count = n;
+        if (out) {
+            if (cap < n) fail(GDF_ERR_CAPACITY, "voxelized points: buffer too small");
+            if (n) HIPCHK(hipMemcpy(out, e->d_vox.p, (size_t)n * 16, hipMemcpyDeviceToHost));
+        }
+    });
+}
+
+int gdf_download_occupancy_grid(gdf_engine* e, uint8_t* out, uint64_t cap) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        if (!e->grid_set || !e->invoked_once) fail(GDF_ERR_STATE, "no voxelOccupancyGrid has run");
+        if (!out || cap < e->ncells) fail(GDF_ERR_CAPACITY, "occupancy grid: buffer too small");
+        e->sync();
+        HIPCHK(hipMemcpy(out, grid_out_ptr(e), e->ncells, hipMemcpyDeviceToHost));
+        if (e->grid_mode == 0 && e->marks_set)  // pending marks of the next frame: hide bit 7
+            for (uint64_t c = 0; c < e->ncells; ++c) out[c] &= 0x7Fu;
+    });
+}
+
+int gdf_get_grid_size(gdf_engine* e, uint32_t g[3], uint64_t* ncells) {
+    ENGINE_OR_FAIL(e);
+    if (!e->grid_set) {
+        g_last_error = "no voxel grid set";
+        return GDF_ERR_STATE;
+    }
+    if (g) std::memcpy(g, e->gs, 12);
+    if (ncells) *ncells = e->ncells;
+    return GDF_OK;
+}
+
+int gdf_get_device_results(gdf_engine* e, const float** pts, const uint32_t** coords,
+                           const float** vox, const uint8_t** occ) {
+    ENGINE_OR_FAIL(e);
+    if (pts) *pts = e->d_pts.as<const float>();
+    if (coords) *coords = e->d_coords.as<const uint32_t>();
+    if (vox) *vox = e->d_vox.as<const float>();
+    if (occ) *occ = e->grid_set ? grid_out_ptr(e) : nullptr;
+    return GDF_OK;
+}
+
+int gdf_process_frame(gdf_engine* e, const gdf_frame_params* p, gdf_frame_result* r) {
+    ENGINE_OR_FAIL(e);
+    if (!p) return GDF_ERR_ARG;
+    return guarded(e, [&] {
+        gdf_frame_result res{};
+        uint32_t collected;
+        {
+            std::lock_guard<std::mutex> lk(e->ps_mutex);
+            collected = e->collect->total;
+        }
+        // component.cpp:150: if ((numAdded>0) || (numCollectedPointSequencePoints()>0))
+        if (!(e->cams.size() > 0 || collected > 0)) {
+            if (r) *r = res;
+            return;
+        }
+        res.processed = 1;
+        upload_point_sequences(e);
+        e->ps_filter_set = true;
+        e->ps_thr = p->ps_filter_threshold;
+        e->ps_F = p->ps_filter_size;
+        insert_new_point_sequences(e);
+        uint32_t lts = 0, ltn = 0, ets = 0, etn = 0;
+        if (e->rb.last_time_sec != 0 || e->rb.last_time_nsec != 0) {
+            lts = e->rb.last_time_sec;
+            ltn = e->rb.last_time_nsec;
+            if (!ros_time_minus(lts, ltn, (double)p->ps_timespan, &ets, &etn))
+                fail(GDF_ERR_TIME, "latest time - timespan is out of ROS time range");
+        }
+        roll_rollbuffer(e, ets, etn);
+        if (p->move_transform_available) {
+            select_timespan(e, ets, etn, lts, ltn);
+            prepare_buffers(e);
+            insert_selected(e, p->T_world_move, p->T_crop_move);
+        } else {
+            prepare_buffers(e);
+        }
+        res.latest_time_sec = lts;
+        res.latest_time_nsec = ltn;
+        upload_depthmaps(e);
+        e->converted = true;
+        e->flying_set = true;
+        e->F = p->flying_filter_size;
+        e->thr = p->flying_threshold;
+        e->rot45 = p->flying_rot45 ? 1 : 0;
+        e->crop_set = true;
+        std::memcpy(e->lo, p->crop_min, 12);
+        std::memcpy(e->hi, p->crop_max, 12);
+        if (p->enable_voxel_filter) {
+            set_grid(e, p->voxel_min, p->voxel_max, p->voxel_size);
+            if (e->grid_mode == 0 && p->occupancy_lifetime > 127) {
+                // switch representation before marks are written
+                e->d_hist32.ensure((size_t)e->ncells * 4);
+                e->d_marks.ensure((size_t)e->ncells);
+                e->d_out8.ensure((size_t)((e->ncells + 15) / 16) * 16);
+                HIPCHK(launch_widen_grid(e->d_grid8.as<uint8_t>(), e->d_hist32.as<uint32_t>(),
+                                         e->d_marks.as<uint8_t>(), e->ncells, e->s()));
+                e->grid_mode = 1;
+            }
+            run_frame(e, true);
+            voxelize(e, p->voxel_average);
+            if (!p->defer_occupancy_grid) occupancy_grid(e, p->occupancy_lifetime);
+        } else {
+            run_frame(e, false);
+        }
+        res.num_depth_points = e->depth_total;
+        res.num_points_total = e->n_total;
+        if (p->synchronous) {
+            e->read_misc();
+            res.num_points = e->h_misc[kCount];
+            res.num_voxelized = p->enable_voxel_filter ? e->h_misc[kVoxCount] : 0;
+        }
+        if (r) *r = res;
+    });
+}
+
+int gdf_export_occupancy_marks(gdf_engine* e, uint32_t* bits, uint64_t words) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        if (!e->grid_set || !bits) fail(GDF_ERR_STATE, "no voxel grid");
+        if (words < (e->ncells + 31) / 32) fail(GDF_ERR_CAPACITY, "mark bitmask too small");
+        HIPCHK(launch_export_marks(occ_ptr(e), occ_mode(e), e->ncells, bits, e->s()));
+    });
+}
+
+int gdf_import_occupancy_marks(gdf_engine* e, const uint32_t* bits, uint64_t words, uint32_t nranks) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        if (!e->grid_set || !bits) fail(GDF_ERR_STATE, "no voxel grid");
+        if (words < (e->ncells + 31) / 32) fail(GDF_ERR_CAPACITY, "mark bitmask too small");
+        HIPCHK(launch_import_marks(occ_ptr(e), occ_mode(e), e->ncells, bits, words, nranks, e->s()));
+        e->marks_set = true;
+    });
+}
+
+int gdf_set_profiling(gdf_engine* e, int enable) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        e->resolve_events();
+        e->profiling = enable != 0;
+        for (int i = 0; i < GDF_KERNEL_SLOTS; ++i) {
+            e->prof_ms[i] = 0.0;
+            e->prof_n[i] = 0;
+        }
+    });
+}
+
+int gdf_get_kernel_times(gdf_engine* e, double* ms, uint64_t* n, int slots) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        e->resolve_events();
+        for (int i = 0; i < slots && i < GDF_KERNEL_SLOTS; ++i) {
+            if (ms) ms[i] = e->prof_ms[i];
+            if (n) n[i] = e->prof_n[i];
+        }
+    });
+}
+
+int gdf_set_debug(gdf_engine* e, int enable) {
+    ENGINE_OR_FAIL(e);
+    e->debug = enable != 0;
+    return GDF_OK;
+}
+
+int gdf_debug_stage_masks(gdf_engine* e, uint8_t* out, uint32_t cap, uint32_t* out_count) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        if (!e->debug || !e->d_dbg.p) fail(GDF_ERR_STATE, "debug masks not enabled");
+        if (out_count) *out_count = e->dbg_count;
+        if (out) {
+            if (cap < e->dbg_count) fail(GDF_ERR_CAPACITY, "debug masks: buffer too small");
+            e->sync();
+            if (e->dbg_count) HIPCHK(hipMemcpy(out, e->d_dbg.p, e->dbg_count, hipMemcpyDeviceToHost));
+        }
+    });
+}
+
+int gdf_debug_rollbuffer(gdf_engine* e, float* pts, uint32_t* mask, uint32_t* seq_idx,
+                         uint32_t cap, uint32_t* hdr, uint32_t hdr_cap) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        const uint32_t R = e->rb.num_points;
+        if (cap < R || hdr_cap < e->hdrB.size()) fail(GDF_ERR_CAPACITY, "rollbuffer debug: buffer too small");
+        e->sync();
+        std::vector<float> tmp((size_t)R * 4);
+        if (R) {
+            const uint64_t first = e->ring_head % e->ring_cap;
+            const uint64_t a = std::min<uint64_t>(R, e->ring_cap - first);
+            HIPCHK(hipMemcpy(tmp.data(), e->d_ring.as<float4>() + first, a * 16, hipMemcpyDeviceToHost));
+            if (R > a) HIPCHK(hipMemcpy(tmp.data() + 4 * a, e->d_ring.p, (R - a) * 16, hipMemcpyDeviceToHost));
+        }
+        for (uint32_t i = 0; i < R; ++i) {
+            if (pts) {
+                pts[4 * (size_t)i + 0] = tmp[4 * (size_t)i + 0];
+                pts[4 * (size_t)i + 1] = tmp[4 * (size_t)i + 1];
+                pts[4 * (size_t)i + 2] = tmp[4 * (size_t)i + 2];
+                pts[4 * (size_t)i + 3] = 1.0f;
+            }
+            if (mask) mask[i] = tmp[4 * (size_t)i + 3] != 0.0f ? 1u : 0u;
+        }
+        if (seq_idx) {
+            uint64_t pos = 0;
+            for (uint32_t j = 0; j < e->hdrB.size() && pos < R; ++j)
+                for (uint32_t k = 0; k < e->hdrB[j].num && pos < R; ++k) seq_idx[pos++] = j;
+        }
+        if (hdr)
+            for (uint32_t j = 0; j < e->hdrB.size(); ++j) {
+                hdr[4 * j + 0] = e->hdrB[j].sec;
+                hdr[4 * j + 1] = e->hdrB[j].nsec;
+                hdr[4 * j + 2] = e->hdrB[j].start;
+                hdr[4 * j + 3] = e->hdrB[j].num;
+            }
+    });
+}
+
+int gdf_debug_historic_grid(gdf_engine* e, uint32_t* out, uint64_t cap) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        if (!e->grid_set) fail(GDF_ERR_STATE, "no voxel grid");
+        if (!out || cap < e->ncells) fail(GDF_ERR_CAPACITY, "historic grid: buffer too small");
+        e->sync();
+        if (e->grid_mode == 1) {
+            HIPCHK(hipMemcpy(out, e->d_hist32.p, e->ncells * 4, hipMemcpyDeviceToHost));
+        } else {
+            std::vector<uint8_t> g(e->ncells);
+            HIPCHK(hipMemcpy(g.data(), e->d_grid8.p, e->ncells, hipMemcpyDeviceToHost));
+            for (uint64_t c = 0; c < e->ncells; ++c) out[c] = g[c] & 0x7Fu;
+        }
+    });
+}
+
+}  // extern "C"

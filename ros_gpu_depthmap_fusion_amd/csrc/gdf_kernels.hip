@@ -1,0 +1,775 @@
+// gdf_kernels.hip — gfx950 (CDNA4, wave64) kernels of the depth-fusion hot path.
+//
+// Reference shaders restated here (paths relative to the reference root, shader/):
+//   k_frame            convert_depthmap_to_points.glsl:83-120, filter_flying_pixels.glsl:43-165,
+//                      transform_points_indirect.glsl:50-69, crop_points.glsl:38-67,
+//                      apply_point_mask.glsl:42-55 (ordered: decoupled look-back scan),
+//                      compute_voxel_coords.glsl:34-55, voxel_grid_occupancy_of_points.glsl:30-40
+//   k_ps_filter_insert filter_point_sequence.glsl:78-122 + transfer_data.glsl (rollbuffer insert)
+//   k_grid_*           zero_uints / decrement_uints.glsl:31-51 / max_with_uints_times_scalar.glsl:36-46
+//                      / uints_to_chars.glsl:31-50, fused into one pass over the cells
+//   k_sort_*, k_group  inc/voxelize.h:74-105 + radix_grouper.h + radix_sort.h (GPU version)
+#include "gdf_kernels.hpp"
+
+namespace gdf {
+
+// ---- small helpers ----------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long lanemask_lt() {
+    const int lane = threadIdx.x & 63;
+    return lane ? (~0ull >> (64 - lane)) : 0ull;
+}
+
+// Block (256 threads) exclusive scan of one value per thread.
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t& total,
+                                                         uint32_t* s_wave) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_wave[wid] = x;
+    __syncthreads();
+    uint32_t wbase = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        uint32_t t = s_wave[w];
+        wbase += (w < wid) ? t : 0u;
+        tot += t;
+    }
+    total = tot;
+    __syncthreads();
+    return wbase + x - v;
+}
+
+// Decoupled look-back over 8-byte {flag, value} granules (flag 1 = aggregate, 2 = inclusive).
+// Each granule is written by ONE agent-scope atomic store and polled with agent-scope atomic
+// loads (MI355X hand-off form "R2": the data is the flag, no fence needed).
+__device__ __forceinline__ uint32_t lookback64(unsigned long long* status, uint32_t tile,
+                                               uint32_t agg, uint32_t* err) {
+    if (tile == 0) {
+        __hip_atomic_store(&status[0], (2ull << 32) | agg, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        return 0;
+    }
+    __hip_atomic_store(&status[tile], (1ull << 32) | agg, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t excl = 0, spins = 0;
+    int64_t j = (int64_t)tile - 1;
+    while (j >= 0) {
+        unsigned long long s = __hip_atomic_load(&status[j], __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t flag = (uint32_t)(s >> 32);
+        if (flag == 0) {
+            if (++spins > kSpinLimit) {
+                atomicOr(err, 1u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        excl += (uint32_t)s;
+        if (flag == 2) break;
+        --j;
+    }
+    __hip_atomic_store(&status[tile], (2ull << 32) | (uint32_t)(excl + agg), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    return excl;
+}
+
+// ---- fused frame kernel ------------------------------------------------------------------------
+// Camera owning global index gi (cameras sorted by offset); -1 when gi is outside every camera
+// (the reference's out-of-bounds read, canonicalised as mask 0).
+__device__ __forceinline__ int find_cam(const CamDesc* cams, int ncams, int64_t gi) {
+    for (int j = ncams - 1; j >= 0; --j) {
+        if (gi >= cams[j].off) return (gi < cams[j].off + (int64_t)cams[j].n) ? j : -1;
+    }
+    return -1;
+}
+
+// mask + camera point of a neighbour read by check_at (filter_flying_pixels.glsl:63-80)
+__device__ __forceinline__ bool nb_point(const CamDesc* cams, int ncams, int k, int64_t gi,
+                                         float& x, float& y, float& z) {
+    int j = k;
+    if (gi < cams[k].off || gi >= cams[k].off + (int64_t)cams[k].n) j = find_cam(cams, ncams, gi);
+    if (j < 0) return false;
+    uint32_t local = (uint32_t)(gi - cams[j].off);
+    uint32_t d = cams[j].depth[local];
+    if (d == 0) return false;
+    cam_point(cams[j], local, d, x, y, z);
+    return true;
+}
+
+// check_at / check_at_rot45 (filter_flying_pixels.glsl:55-133) for ring i
+__device__ __forceinline__ bool flying_check(const CamDesc* cams, int ncams, int k, int64_t g,
+                                             uint32_t x, uint32_t y, uint32_t i, bool rot45,
+                                             float thr, float nx, float ny, float nz) {
+    const CamDesc& c = cams[k];
+    if (x + i > c.W - 1 || y + i > c.H - 1) return false;
+    const int64_t iw = (int64_t)i * c.W;
+    int64_t up, down, left, right;
+    if (!rot45) {
+        up = g - iw; down = g + iw; left = g - i; right = g + i;
+    } else {
+        up = g - iw - i; down = g + iw + i; left = g + iw - i; right = g - iw + i;
+    }
+    float ux, uy, uz, dx_, dy_, dz_, lx, ly, lz, rx, ry, rz;
+    if (!nb_point(cams, ncams, k, up, ux, uy, uz)) return false;
+    if (!nb_point(cams, ncams, k, down, dx_, dy_, dz_)) return false;
+    if (!nb_point(cams, ncams, k, left, lx, ly, lz)) return false;
+    if (!nb_point(cams, ncams, k, right, rx, ry, rz)) return false;
+    // dx = right - left, dy = down - up, normal = normalize(cross(dy, dx))
+    float ax = dx_ - ux, ay = dy_ - uy, az = dz_ - uz;  // dy
+    float bx = rx - lx, by = ry - ly, bz = rz - lz;      // dx
+    float cx = ay * bz - az * by;
+    float cy = az * bx - ax * bz;
+    float cz = ax * by - ay * bx;
+    normalize3(cx, cy, cz);
+    float cv = dot3(cx, cy, cz, nx, ny, nz);
+    return !(cv < thr);  // NaN passes
+}
+
+struct ItemOut {
+    float4 w;
+    uint32_t bits;  // bit0 convert, bit1 flying, bit2 crop
+};
+
+__device__ __forceinline__ ItemOut eval_depth(const FrameArgs& a, const CamDesc* cams, uint32_t g,
+                                              uint32_t d) {
+    ItemOut r;
+    r.bits = 0;
+    r.w = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (d == 0) return r;
+    r.bits = 1;
+    const int k = find_cam(cams, a.ncams, (int64_t)g);
+    const CamDesc& c = cams[k];
+    const uint32_t local = (uint32_t)((int64_t)g - c.off);
+    float px, py, pz;
+    cam_point(c, local, d, px, py, pz);
+    if (a.do_flying) {
+        if (sqrtf(dot3(px, py, pz, px, py, pz)) > 10.0f) return r;  // max_distance (:41,:143)
+        float nx = px, ny = py, nz = pz;
+        normalize3(nx, ny, nz);
+        nx = -nx; ny = -ny; nz = -nz;
+        const uint32_t x = local % c.W, y = local / c.W;
+        for (uint32_t i = 1; i <= a.F; ++i) {
+            if (!flying_check(cams, a.ncams, k, (int64_t)g, x, y, i, false, a.thr, nx, ny, nz))
+                return r;
+            if (a.rot45 &&
+                !flying_check(cams, a.ncams, k, (int64_t)g, x, y, i, true, a.thr, nx, ny, nz))
+                return r;
+        }
+    }
+    r.bits |= 2;
+    if (a.do_crop) {
+        float qx = mrow(c.Tc + 0, px, py, pz, 1.0f);
+        float qy = mrow(c.Tc + 4, px, py, pz, 1.0f);
+        float qz = mrow(c.Tc + 8, px, py, pz, 1.0f);
+        if (qx < a.lo[0] || qx > a.hi[0] || qy < a.lo[1] || qy > a.hi[1] || qz < a.lo[2] ||
+            qz > a.hi[2])
+            return r;
+    }
+    r.bits |= 4;
+    r.w.x = mrow(c.Tw + 0, px, py, pz, 1.0f);
+    r.w.y = mrow(c.Tw + 4, px, py, pz, 1.0f);
+    r.w.z = mrow(c.Tw + 8, px, py, pz, 1.0f);
+    r.w.w = mrow(c.Tw + 12, px, py, pz, 1.0f);
+    return r;
+}
+
+__device__ __forceinline__ ItemOut eval_sel(const FrameArgs& a, uint32_t i) {
+    ItemOut r;
+    r.bits = 0;
+    r.w = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 p = a.ring[(a.ring_first + i) % a.ring_cap];
+    if (p.w == 0.0f) return r;  // rollbuffer mask 0
+    r.bits = 3;
+    // transform index: last covered sequence starting at or before i
+    uint32_t lo = 0, hi = a.nseg;
+    while (hi - lo > 1) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (a.seg_start[mid] <= i) lo = mid; else hi = mid;
+    }
+    const uint32_t t = a.seg_tf[lo];
+    const float* Tw = a.tfw + 16 * (size_t)t;
+    const float* Tc = a.tfc + 16 * (size_t)t;
+    if (a.do_crop) {
+        float qx = mrow(Tc + 0, p.x, p.y, p.z, 1.0f);
+        float qy = mrow(Tc + 4, p.x, p.y, p.z, 1.0f);
+        float qz = mrow(Tc + 8, p.x, p.y, p.z, 1.0f);
+        if (qx < a.lo[0] || qx > a.hi[0] || qy < a.lo[1] || qy > a.hi[1] || qz < a.lo[2] ||
+            qz > a.hi[2])
+            return r;
+    }
+    r.bits |= 4;
+    r.w.x = mrow(Tw + 0, p.x, p.y, p.z, 1.0f);
+    r.w.y = mrow(Tw + 4, p.x, p.y, p.z, 1.0f);
+    r.w.z = mrow(Tw + 8, p.x, p.y, p.z, 1.0f);
+    r.w.w = mrow(Tw + 12, p.x, p.y, p.z, 1.0f);
+    return r;
+}
+
+__global__ __launch_bounds__(kFrameThreads) void k_frame(FrameArgs a) {
+    __shared__ CamDesc s_cams[kMaxCams];
+    __shared__ uint32_t s_wave[4];
+    __shared__ uint32_t s_tile, s_excl;
+    {
+        const uint32_t words = (uint32_t)a.ncams * (uint32_t)(sizeof(CamDesc) / 4);
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.cams);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(s_cams);
+        for (uint32_t w = threadIdx.x; w < words; w += kFrameThreads) dst[w] = src[w];
+    }
+    if (threadIdx.x == 0) s_tile = atomicAdd(a.tile_ctr, 1u);
+    __syncthreads();
+    const uint32_t tile = s_tile;
+
+    ItemOut it[kFramePerThread];
+    uint32_t item0;
+    if (tile < a.depth_tiles) {
+        item0 = tile * kFrameTile + threadIdx.x * kFramePerThread;
+#pragma unroll
+        for (int j = 0; j < kFramePerThread; ++j) {
+            const uint32_t g = item0 + j;
+            if (g < a.depth_total) {
+                const int k = find_cam(s_cams, a.ncams, (int64_t)g);
+                const uint32_t d = s_cams[k].depth[(uint32_t)((int64_t)g - s_cams[k].off)];
+                it[j] = eval_depth(a, s_cams, g, d);
+            } else {
+                it[j].bits = 0;
+            }
+        }
+    } else {
+        const uint32_t base = (tile - a.depth_tiles) * kFrameTile + threadIdx.x * kFramePerThread;
+        item0 = a.depth_total + base;
+#pragma unroll
+        for (int j = 0; j < kFramePerThread; ++j) {
+            const uint32_t i = base + j;
+            if (i < a.sel_count) it[j] = eval_sel(a, i);
+            else it[j].bits = 0;
+        }
+    }
+
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int j = 0; j < kFramePerThread; ++j) cnt += (it[j].bits & 4) ? 1u : 0u;
+    uint32_t total;
+    const uint32_t excl_thread = block_exclusive_scan(cnt, total, s_wave);
+    if (threadIdx.x == 0) {
+        uint32_t ex = lookback64(a.status, tile, total, a.err);
+        s_excl = ex;
+        if (tile == a.total_tiles - 1) *a.out_count = ex + total;
+    }
+    __syncthreads();
+    uint32_t pos = s_excl + excl_thread;
+#pragma unroll
+    for (int j = 0; j < kFramePerThread; ++j) {
+        if (a.dbg) {
+            const uint32_t idx = item0 + j;
+            if ((tile < a.depth_tiles && idx < a.depth_total) ||
+                (tile >= a.depth_tiles && idx - a.depth_total < a.sel_count))
+                a.dbg[idx] = (uint8_t)it[j].bits;
+        }
+        if (it[j].bits & 4) {
+            a.out_pts[pos] = it[j].w;
+            if (a.do_voxel) {
+                const uint32_t key = voxel_key(it[j].w.x, it[j].w.y, it[j].w.z, a.vlo, a.vcs,
+                                               a.gmax, a.gs);
+                a.out_coords[pos] = key;
+                if (a.occ_mode == 1) {
+                    const uint8_t h = a.occ[key];
+                    if (!(h & 0x80u)) a.occ[key] = (uint8_t)(h | 0x80u);
+                } else if (a.occ_mode == 2) {
+                    a.occ[key] = 1;
+                }
+            }
+            ++pos;
+        }
+    }
+}
+
+hipError_t launch_frame(const FrameArgs& a, hipStream_t s) {
+    if (a.total_tiles == 0) return hipMemsetAsync(a.out_count, 0, 4, s);
+    hipError_t e = hipMemsetAsync(a.status, 0, (size_t)a.total_tiles * 8, s);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(a.tile_ctr, 0, 4, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_frame, dim3(a.total_tiles), dim3(kFrameThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+// ---- point-sequence filter + rollbuffer insert --------------------------------------------------
+// filter_point_sequence.glsl:49-76 neighbour test
+__device__ __forceinline__ bool ps_ok(const float4* pts, float px, float py, float pz, float nx,
+                                      float ny, float nz, uint32_t other, float thr) {
+    const float4 q = pts[other];
+    float dx = q.x - px, dy = q.y - py, dz = q.z - pz;
+    normalize3(dx, dy, dz);
+    float c = fabsf(dot3(dx, dy, dz, nx, ny, nz));
+    return !(1.0f - c < thr);
+}
+
+__global__ __launch_bounds__(256) void k_ps_filter_insert(const float4* __restrict__ pts,
+                                                          uint32_t n, int do_filter, float thr,
+                                                          uint32_t F, float4* __restrict__ ring,
+                                                          uint64_t cap, uint64_t first) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n) return;
+    const float4 p = pts[g];
+    bool valid = true;
+    if (do_filter) {
+        if (sqrtf(dot3(p.x, p.y, p.z, p.x, p.y, p.z)) < 1e-3f) {
+            valid = false;
+        } else {
+            float nx = p.x, ny = p.y, nz = p.z;
+            normalize3(nx, ny, nz);
+            nx = -nx; ny = -ny; nz = -nz;
+            for (uint32_t i = 0; i < F && valid; ++i) {
+                const uint32_t j0 = g + i - 1u;
+                if (j0 < n && !ps_ok(pts, p.x, p.y, p.z, nx, ny, nz, j0, thr)) valid = false;
+                const uint32_t j1 = g + i + 1u;
+                if (valid && j1 < n && !ps_ok(pts, p.x, p.y, p.z, nx, ny, nz, j1, thr))
+                    valid = false;
+            }
+        }
+    }
+    ring[(first + g) % cap] = make_float4(p.x, p.y, p.z, valid ? 1.0f : 0.0f);
+}
+
+hipError_t launch_ps_filter_insert(const float4* new_pts, uint32_t n, int do_filter, float thr,
+                                   uint32_t F, float4* ring, uint64_t cap, uint64_t first,
+                                   hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_ps_filter_insert, dim3((n + 255) / 256), dim3(256), 0, s, new_pts, n,
+                       do_filter, thr, F, ring, cap, first);
+    return hipGetLastError();
+}
+
+// ---- historic occupancy grid ---------------------------------------------------------------------
+// new = mark ? max(sat_dec(h), L) : sat_dec(h); output byte = new & 0xFF (L <= 127 keeps bit 7 free)
+__device__ __forceinline__ uint32_t grid_byte(uint32_t h, uint32_t L) {
+    const uint32_t v = h & 0x7Fu;
+    const uint32_t dec = v ? v - 1u : 0u;
+    return (h & 0x80u) ? (dec > L ? dec : L) : dec;
+}
+
+__device__ __forceinline__ uint32_t grid_word(uint32_t w, uint32_t L) {
+    return grid_byte(w & 0xFFu, L) | (grid_byte((w >> 8) & 0xFFu, L) << 8) |
+           (grid_byte((w >> 16) & 0xFFu, L) << 16) | (grid_byte(w >> 24, L) << 24);
+}
+
+__global__ __launch_bounds__(256) void k_grid_u8(uint4* __restrict__ grid, uint64_t nvec,
+                                                 uint32_t L) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nvec;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint4 v = grid[i];
+        v.x = grid_word(v.x, L);
+        v.y = grid_word(v.y, L);
+        v.z = grid_word(v.z, L);
+        v.w = grid_word(v.w, L);
+        grid[i] = v;
+    }
+}
+
+static unsigned grid_blocks(uint64_t work, unsigned per_block) {
+    uint64_t b = (work + per_block - 1) / per_block;
+    if (b > 2048) b = 2048;
+    if (b == 0) b = 1;
+    return (unsigned)b;
+}
+
+hipError_t launch_grid_u8(uint8_t* grid, uint64_t ncells, uint32_t lifetime, hipStream_t s) {
+    const uint64_t nvec = (ncells + 15) / 16;  // grid allocation is padded to 16 bytes
+    hipLaunchKernelGGL(k_grid_u8, dim3(grid_blocks(nvec, 256)), dim3(256), 0, s,
+                       reinterpret_cast<uint4*>(grid), nvec, lifetime);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_grid_u32(uint32_t* __restrict__ hist,
+                                                  uint8_t* __restrict__ marks,
+                                                  uint8_t* __restrict__ out8, uint64_t ncells,
+                                                  uint32_t L) {
+    for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < ncells;
+         c += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t h = hist[c];
+        const uint32_t dec = h >= 1u ? h - 1u : 0u;
+        const uint32_t m = marks[c] ? L : 0u;
+        const uint32_t nv = dec > m ? dec : m;
+        hist[c] = nv;
+        out8[c] = (uint8_t)(nv & 0xFFu);
+        if (marks[c]) marks[c] = 0;
+    }
+}
+
+hipError_t launch_grid_u32(uint32_t* hist, uint8_t* marks, uint8_t* out8, uint64_t ncells,
+                           uint32_t lifetime, hipStream_t s) {
+    hipLaunchKernelGGL(k_grid_u32, dim3(grid_blocks(ncells, 256)), dim3(256), 0, s, hist, marks,
+                       out8, ncells, lifetime);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_widen(const uint8_t* __restrict__ g8,
+                                               uint32_t* __restrict__ hist,
+                                               uint8_t* __restrict__ marks, uint64_t ncells) {
+    for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < ncells;
+         c += (uint64_t)gridDim.x * blockDim.x) {
+        const uint8_t h = g8[c];
+        hist[c] = h & 0x7Fu;
+        marks[c] = (h & 0x80u) ? 1 : 0;
+    }
+}
+
+hipError_t launch_widen_grid(const uint8_t* grid8, uint32_t* hist, uint8_t* marks,
+                             uint64_t ncells, hipStream_t s) {
+    hipLaunchKernelGGL(k_widen, dim3(grid_blocks(ncells, 256)), dim3(256), 0, s, grid8, hist,
+                       marks, ncells);
+    return hipGetLastError();
+}
+
+// ---- standalone voxel keys / occupancy marks (stage-by-stage API) --------------------------------
+__global__ __launch_bounds__(256) void k_coords(const float4* __restrict__ pts,
+                                                const uint32_t* __restrict__ count,
+                                                uint32_t* __restrict__ coords, VoxelParams v) {
+    const uint32_t n = *count;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const float4 p = pts[i];
+        coords[i] = voxel_key(p.x, p.y, p.z, v.vlo, v.vcs, v.gmax, v.gs);
+    }
+}
+
+hipError_t launch_coords(const float4* pts, const uint32_t* count, uint32_t nmax,
+                         uint32_t* coords, const VoxelParams& v, hipStream_t s) {
+    hipLaunchKernelGGL(k_coords, dim3(grid_blocks(nmax, 256)), dim3(256), 0, s, pts, count,
+                       coords, v);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_scatter(const uint32_t* __restrict__ coords,
+                                                 const uint32_t* __restrict__ count,
+                                                 uint8_t* occ, int mode) {
+    const uint32_t n = *count;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint32_t key = coords[i];
+        if (mode == 1) {
+            const uint8_t h = occ[key];
+            if (!(h & 0x80u)) occ[key] = (uint8_t)(h | 0x80u);
+        } else {
+            occ[key] = 1;
+        }
+    }
+}
+
+hipError_t launch_scatter(const uint32_t* coords, const uint32_t* count, uint32_t nmax,
+                          uint8_t* occ, int mode, hipStream_t s) {
+    hipLaunchKernelGGL(k_scatter, dim3(grid_blocks(nmax, 256)), dim3(256), 0, s, coords, count,
+                       occ, mode);
+    return hipGetLastError();
+}
+
+// ---- GPU voxelize: onesweep LSD radix sort + ordered group mean ---------------------------------
+__global__ __launch_bounds__(256) void k_sort_hist(const uint32_t* __restrict__ keys,
+                                                   const uint32_t* __restrict__ count,
+                                                   uint32_t npasses, uint32_t* __restrict__ hist) {
+    __shared__ uint32_t s_h[4 * 256];
+    for (uint32_t i = threadIdx.x; i < 4 * 256; i += 256) s_h[i] = 0;
+    __syncthreads();
+    const uint32_t n = *count;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint32_t k = keys[i];
+        for (uint32_t p = 0; p < npasses; ++p) atomicAdd(&s_h[p * 256 + ((k >> (8 * p)) & 0xFFu)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < npasses * 256; i += 256)
+        if (s_h[i]) atomicAdd(&hist[i], s_h[i]);
+}
+
+// Stable scatter of one 8-bit digit.  Tile = 4096 keys: wave w owns keys [w*1024, w*1024+1024)
+// of the tile in slot-major order (slot j, lane l -> w*1024 + j*64 + l), so ranking the slots in
+// order with wave ballots keeps the sort stable.  Per-digit tile offsets come from a decoupled
+// look-back over 32-bit {2-bit flag, 30-bit count} granules.
+__global__ __launch_bounds__(kSortThreads) void k_sort_pass(
+    const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+    uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, const uint32_t* __restrict__ count,
+    const uint32_t* __restrict__ ghist, uint32_t* status, uint32_t* tile_ctr, uint32_t* err,
+    uint32_t shift, uint32_t dbits) {
+    __shared__ uint32_t s_cnt[4][256];
+    __shared__ uint32_t s_base[256];
+    __shared__ uint32_t s_excl[256];
+    __shared__ uint32_t s_tile;
+    const uint32_t n = *count;
+    const uint32_t ntiles = (n + kSortTile - 1) / kSortTile;
+    if (threadIdx.x == 0) s_tile = atomicAdd(tile_ctr, 1u);
+    for (uint32_t i = threadIdx.x; i < 4 * 256; i += kSortThreads) (&s_cnt[0][0])[i] = 0;
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    if (tile >= ntiles) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long ltm = lanemask_lt();
+
+    uint32_t key[kSortPerThread], val[kSortPerThread], rank[kSortPerThread];
+    const uint32_t wbase = tile * kSortTile + w * 1024;
+#pragma unroll
+    for (int j = 0; j < kSortPerThread; ++j) {
+        const uint32_t idx = wbase + j * 64 + lane;
+        const bool ok = idx < n;
+        key[j] = ok ? kin[idx] : 0xFFFFFFFFu;
+        val[j] = ok ? (vin ? vin[idx] : idx) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < kSortPerThread; ++j) {
+        const uint32_t idx = wbase + j * 64 + lane;
+        const bool ok = idx < n;
+        const uint32_t d = (key[j] >> shift) & 0xFFu;
+        unsigned long long m = __ballot(ok);
+        for (uint32_t b = 0; b < dbits; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const unsigned long long bb = __ballot(bit);
+            m &= bit ? bb : ~bb;
+        }
+        const uint32_t before = (uint32_t)__popcll(m & ltm);
+        uint32_t base = 0;
+        if (ok) base = s_cnt[w][d];
+        rank[j] = base + before;
+        __builtin_amdgcn_wave_barrier();
+        if (ok && before == 0) s_cnt[w][d] = base + (uint32_t)__popcll(m);
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    // per digit: tile total, per-wave offsets, global base, look-back
+    {
+        const uint32_t d = threadIdx.x;
+        uint32_t tot = 0;
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) {
+            const uint32_t c = s_cnt[ww][d];
+            s_cnt[ww][d] = tot;
+            tot += c;
+        }
+        // global exclusive base over digits
+        uint32_t gh = ghist[d];
+        s_base[d] = gh;
+        __syncthreads();
+        // simple 256-wide exclusive scan in LDS (Hillis-Steele on s_base)
+        for (uint32_t o = 1; o < 256; o <<= 1) {
+            uint32_t add = d >= o ? s_base[d - o] : 0u;
+            __syncthreads();
+            s_base[d] += add;
+            __syncthreads();
+        }
+        const uint32_t incl = s_base[d];
+        __syncthreads();
+        s_base[d] = incl - gh;
+        // look-back for this digit
+        uint32_t* st = status + (size_t)tile * 256 + d;
+        uint32_t excl = 0;
+        if (tile == 0) {
+            __hip_atomic_store(st, (2u << 30) | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(st, (1u << 30) | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int64_t j = (int64_t)tile - 1;
+            uint32_t spins = 0;
+            while (j >= 0) {
+                const uint32_t sv = __hip_atomic_load(status + (size_t)j * 256 + d, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t flag = sv >> 30;
+                if (flag == 0) {
+                    if (++spins > kSpinLimit) {
+                        atomicOr(err, 2u);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                excl += sv & 0x3FFFFFFFu;
+                if (flag == 2) break;
+                --j;
+            }
+            __hip_atomic_store(st, (2u << 30) | (excl + tot), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_excl[d] = excl;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kSortPerThread; ++j) {
+        const uint32_t idx = wbase + j * 64 + lane;
+        if (idx < n) {
+            const uint32_t d = (key[j] >> shift) & 0xFFu;
+            const uint32_t pos = s_base[d] + s_excl[d] + s_cnt[w][d] + rank[j];
+            kout[pos] = key[j];
+            vout[pos] = val[j];
+        }
+    }
+}
+
+// Group boundaries, group ids (look-back scan) and the per-voxel sequential mean in stable
+// order (averageGridCells, inc/voxelize.h:9-48) or the voxel lower corner (occupiedGridCells,
+// :50-71 with GridMeta::worldCoord, inc/grid_meta.h:45-100).
+__global__ __launch_bounds__(kGroupThreads) void k_group(
+    const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+    const uint32_t* __restrict__ count, const float4* __restrict__ pts, float4* __restrict__ out,
+    uint32_t* __restrict__ out_count, unsigned long long* status, uint32_t* tile_ctr,
+    uint32_t* err, int average, VoxelParams vp) {
+    __shared__ uint32_t s_wave[4];
+    __shared__ uint32_t s_tile, s_excl;
+    const uint32_t n = *count;
+    const uint32_t ntiles = (n + kGroupTile - 1) / kGroupTile;
+    if (threadIdx.x == 0) s_tile = atomicAdd(tile_ctr, 1u);
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    if (tile >= ntiles) {
+        if (tile == 0 && threadIdx.x == 0) *out_count = 0;  // n == 0
+        return;
+    }
+    const uint32_t i0 = tile * kGroupTile + threadIdx.x * kGroupPerThread;
+    uint32_t flags = 0, cnt = 0;
+#pragma unroll
+    for (int j = 0; j < kGroupPerThread; ++j) {
+        const uint32_t i = i0 + j;
+        if (i < n && (i == 0 || keys[i] != keys[i - 1])) {
+            flags |= 1u << j;
+            ++cnt;
+        }
+    }
+    uint32_t total;
+    const uint32_t excl_thread = block_exclusive_scan(cnt, total, s_wave);
+    if (threadIdx.x == 0) {
+        const uint32_t ex = lookback64(status, tile, total, err);
+        s_excl = ex;
+        if (tile == ntiles - 1) *out_count = ex + total;
+    }
+    __syncthreads();
+    uint32_t g = s_excl + excl_thread;
+#pragma unroll
+    for (int j = 0; j < kGroupPerThread; ++j) {
+        if (!(flags & (1u << j))) continue;
+        const uint32_t i = i0 + j;
+        const uint32_t key = keys[i];
+        float4 o;
+        if (average) {
+            float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
+            uint32_t c = 0;
+            for (uint32_t k = i; k < n && keys[k] == key; ++k) {
+                const float4 p = pts[vals[k]];
+                sx = sx + p.x;
+                sy = sy + p.y;
+                sz = sz + p.z;
+                sw = sw + p.w;
+                ++c;
+            }
+            const float fc = (float)c;
+            o = make_float4(sx / fc, sy / fc, sz / fc, sw);
+        } else {
+            uint32_t kk = key;
+            const uint32_t steps[3] = {1u, vp.gs[0], vp.gs[0] * vp.gs[1]};
+            uint32_t gc[3];
+#pragma unroll
+            for (int ax = 0; ax < 3; ++ax) {
+                gc[ax] = (kk / steps[ax]) % vp.gs[ax];
+                kk -= gc[ax] * steps[ax];
+            }
+            o = make_float4((float)gc[0] * vp.vcs[0] + vp.vlo[0], (float)gc[1] * vp.vcs[1] + vp.vlo[1],
+                            (float)gc[2] * vp.vcs[2] + vp.vlo[2], 0.0f);
+        }
+        out[g] = o;
+        ++g;
+    }
+}
+
+size_t voxelize_status_words(uint32_t nmax) {
+    return (size_t)((nmax + kSortTile - 1) / kSortTile + 1) * 256;
+}
+size_t voxelize_group_tiles(uint32_t nmax) {
+    return (size_t)((nmax + kGroupTile - 1) / kGroupTile + 1);
+}
+
+hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s) {
+    const uint32_t npasses = a.key_bits == 0 ? 1u : (a.key_bits + 7) / 8;
+    const size_t swords = voxelize_status_words(a.nmax);
+    const size_t gtiles = voxelize_group_tiles(a.nmax);
+    hipError_t e;
+    if ((e = hipMemsetAsync(a.hist, 0, 4 * 256 * 4, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(a.ctrs, 0, 8 * 4, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_sort_hist, dim3(grid_blocks(a.nmax, 256 * 8)), dim3(256), 0, s, a.keys,
+                       a.count, npasses, a.hist);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const uint32_t sort_tiles = (a.nmax + kSortTile - 1) / kSortTile;
+    const uint32_t* kin = a.keys;
+    const uint32_t* vin = nullptr;
+    uint32_t* kbuf[2] = {a.keys_a, a.keys_b};
+    uint32_t* vbuf[2] = {a.vals_a, a.vals_b};
+    for (uint32_t p = 0; p < npasses; ++p) {
+        const uint32_t remaining = a.key_bits > 8 * p ? a.key_bits - 8 * p : 0u;
+        const uint32_t dbits = remaining >= 8 ? 8u : (remaining ? remaining : 1u);
+        if ((e = hipMemsetAsync(a.status, 0, swords * 4, s)) != hipSuccess) return e;
+        if (sort_tiles) {
+            hipLaunchKernelGGL(k_sort_pass, dim3(sort_tiles), dim3(kSortThreads), 0, s, kin, vin,
+                               kbuf[p & 1], vbuf[p & 1], a.count, a.hist + 256 * p, a.status,
+                               a.ctrs + p, a.err, 8 * p, dbits);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
+        kin = kbuf[p & 1];
+        vin = vbuf[p & 1];
+    }
+    if ((e = hipMemsetAsync(a.gstatus, 0, gtiles * 8, s)) != hipSuccess) return e;
+    const uint32_t group_tiles = (a.nmax + kGroupTile - 1) / kGroupTile;
+    hipLaunchKernelGGL(k_group, dim3(group_tiles ? group_tiles : 1), dim3(kGroupThreads), 0, s,
+                       kin, vin, a.count, a.pts, a.out, a.out_count, a.gstatus, a.ctrs + 4, a.err,
+                       a.average, a.vp);
+    return hipGetLastError();
+}
+
+// ---- multi-GPU occupancy marks ------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_export_marks(const uint8_t* __restrict__ occ, int mode,
+                                                      uint64_t ncells, uint32_t* __restrict__ bits,
+                                                      uint64_t words) {
+    for (uint64_t wi = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; wi < words;
+         wi += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t b = 0;
+        for (int k = 0; k < 32; ++k) {
+            const uint64_t c = wi * 32 + k;
+            if (c < ncells) {
+                const uint8_t h = occ[c];
+                const bool m = mode == 1 ? (h & 0x80u) != 0 : h != 0;
+                b |= (m ? 1u : 0u) << k;
+            }
+        }
+        bits[wi] = b;
+    }
+}
+
+hipError_t launch_export_marks(const uint8_t* occ, int mode, uint64_t ncells, uint32_t* bits,
+                               hipStream_t s) {
+    const uint64_t words = (ncells + 31) / 32;
+    hipLaunchKernelGGL(k_export_marks, dim3(grid_blocks(words, 256)), dim3(256), 0, s, occ, mode,
+                       ncells, bits, words);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_import_marks(uint8_t* __restrict__ occ, int mode,
+                                                      uint64_t ncells,
+                                                      const uint32_t* __restrict__ bits,
+                                                      uint64_t words, uint32_t nranks) {
+    for (uint64_t wi = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; wi < words;
+         wi += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t b = 0;
+        for (uint32_t r = 0; r < nranks; ++r) b |= bits[(uint64_t)r * words + wi];
+        if (!b) continue;
+        for (int k = 0; k < 32; ++k) {
+            const uint64_t c = wi * 32 + k;
+            if (c < ncells && ((b >> k) & 1u)) {
+                if (mode == 1) occ[c] = (uint8_t)(occ[c] | 0x80u);
+                else occ[c] = 1;
+            }
+        }
+    }
+}
+
+hipError_t launch_import_marks(uint8_t* occ, int mode, uint64_t ncells, const uint32_t* bits,
+                               uint64_t words, uint32_t nranks, hipStream_t s) {
+    hipLaunchKernelGGL(k_import_marks, dim3(grid_blocks(words, 256)), dim3(256), 0, s, occ, mode,
+                       ncells, bits, words, nranks);
+    return hipGetLastError();
+}
+
+}  // namespace gdf

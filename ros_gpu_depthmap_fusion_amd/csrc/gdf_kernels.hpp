@@ -1,0 +1,67 @@
+// gdf_kernels.hpp — host-side launchers of the gfx950 kernels (gdf_kernels.hip).
+#pragma once
+
+#include "gdf_device.hpp"
+
+namespace gdf {
+
+struct VoxelParams {
+    float vlo[3], vcs[3], gmax[3];
+    uint32_t gs[3];
+};
+
+// fused depth + rollbuffer compaction (convert, flying, crop, transform_indirect, apply,
+// optional voxel keys + occupancy marks); memsets its look-back state itself
+hipError_t launch_frame(const FrameArgs& a, hipStream_t s);
+
+// filter_point_sequence + insert into the rollbuffer ring (w = mask)
+hipError_t launch_ps_filter_insert(const float4* new_pts, uint32_t n, int do_filter, float thr,
+                                   uint32_t F, float4* ring, uint64_t cap, uint64_t first,
+                                   hipStream_t s);
+
+// historic grid update: u8 grid with the mark in bit 7 (lifetime <= 127)
+hipError_t launch_grid_u8(uint8_t* grid, uint64_t ncells, uint32_t lifetime, hipStream_t s);
+// general u32 historic grid with a separate u8 mark array; writes the u8 output grid
+hipError_t launch_grid_u32(uint32_t* hist, uint8_t* marks, uint8_t* out8, uint64_t ncells,
+                           uint32_t lifetime, hipStream_t s);
+hipError_t launch_widen_grid(const uint8_t* grid8, uint32_t* hist, uint8_t* marks,
+                             uint64_t ncells, hipStream_t s);
+
+// standalone voxel keys over the compacted points (count read on the device)
+hipError_t launch_coords(const float4* pts, const uint32_t* count, uint32_t nmax,
+                         uint32_t* coords, const VoxelParams& v, hipStream_t s);
+// occupancy marks from voxel keys (mode 1: bit 7 of u8 grid, 2: u8 mark array)
+hipError_t launch_scatter(const uint32_t* coords, const uint32_t* count, uint32_t nmax,
+                          uint8_t* occ, int mode, hipStream_t s);
+
+// GPU voxelize: stable LSD radix sort of (key, index) + ordered per-voxel mean
+struct VoxelizeArgs {
+    const uint32_t* keys;       // voxel keys [N]
+    const float4* pts;          // compacted points [N]
+    const uint32_t* count;      // N on the device
+    uint32_t nmax;              // capacity bound for launch sizing
+    uint32_t key_bits;          // bit width of (num_cells - 1)
+    int average;
+    VoxelParams vp;
+    // workspace
+    uint32_t *keys_a, *keys_b, *vals_a, *vals_b;
+    uint32_t* hist;             // [4*256]
+    uint32_t* status;           // [ntiles_max*256]
+    unsigned long long* gstatus;  // [group tiles]
+    uint32_t* ctrs;             // [8]
+    uint32_t* err;
+    // outputs
+    float4* out;
+    uint32_t* out_count;
+};
+hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s);
+size_t voxelize_status_words(uint32_t nmax);
+size_t voxelize_group_tiles(uint32_t nmax);
+
+// multi-GPU occupancy marks
+hipError_t launch_export_marks(const uint8_t* occ, int mode, uint64_t ncells, uint32_t* bits,
+                               hipStream_t s);
+hipError_t launch_import_marks(uint8_t* occ, int mode, uint64_t ncells, const uint32_t* bits,
+                               uint64_t words, uint32_t nranks, hipStream_t s);
+
+}  // namespace gdf

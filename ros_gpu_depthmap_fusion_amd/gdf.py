@@ -1,0 +1,458 @@
+"""ctypes binding of the C-ABI in include/gdf.h, with a Python mirror of the reference engine.
+
+`GPUDepthmapFusion` exposes the method names of the reference class
+(include/gpu_depthmap_fusion/gpu_depthmap_fusion.h:219-309, src/gpu_depthmap_fusion.cpp) so the
+parity tests read like the reference's call sequence (GPUDepthmapFusionComponent::processDepthmaps,
+src/gpu_depthmap_fusion_component.cpp:92-300).  Errors raise `GDFError` carrying the C status and
+gdf_last_error().  There is no CPU fallback: if libgdf.so is missing or no GPU is present, the
+constructor raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass, field
+from typing import Optional, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libgdf.so")
+
+GDF_OK = 0
+STATUS_NAMES = {
+    -1: "GDF_ERR_ARG", -2: "GDF_ERR_STATE", -3: "GDF_ERR_HIP", -4: "GDF_ERR_NOMEM",
+    -5: "GDF_ERR_CAPACITY", -6: "GDF_ERR_TIME", -7: "GDF_ERR_DEVICE",
+}
+
+_f16 = C.c_float * 16
+_f3 = C.c_float * 3
+
+
+class RollbufferState(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in (
+        "num_points", "num_seqs", "selection_point_start", "selection_point_count",
+        "selection_sequence_start", "selection_sequence_count", "earliest_time_sec",
+        "earliest_time_nsec", "last_time_sec", "last_time_nsec")]
+
+    def as_tuple(self):
+        return tuple(getattr(self, n) for n, _ in self._fields_)
+
+
+class FrameParams(C.Structure):
+    _fields_ = [
+        ("ps_filter_threshold", C.c_float), ("ps_filter_size", C.c_uint32),
+        ("ps_timespan", C.c_float), ("move_transform_available", C.c_int32),
+        ("T_world_move", _f16), ("T_crop_move", _f16),
+        ("flying_filter_size", C.c_uint32), ("flying_threshold", C.c_float),
+        ("flying_rot45", C.c_int32), ("crop_min", _f3), ("crop_max", _f3),
+        ("enable_voxel_filter", C.c_int32), ("voxel_min", _f3), ("voxel_max", _f3),
+        ("voxel_size", _f3), ("voxel_average", C.c_int32), ("occupancy_lifetime", C.c_uint32),
+        ("defer_occupancy_grid", C.c_int32), ("synchronous", C.c_int32),
+    ]
+
+
+KERNEL_SLOTS = ("frame", "grid", "voxelize", "ps_insert")
+
+
+class FrameResult(C.Structure):
+    _fields_ = [("processed", C.c_int32), ("num_depth_points", C.c_uint32),
+                ("num_points_total", C.c_uint32), ("num_points", C.c_uint32),
+                ("num_voxelized", C.c_uint32), ("latest_time_sec", C.c_uint32),
+                ("latest_time_nsec", C.c_uint32)]
+
+
+class GDFError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"{STATUS_NAMES.get(status, status)}: {msg}")
+        self.status = status
+
+
+_lib = None
+
+# every symbol declared in include/gdf.h (checked by tests/test_abi.py)
+EXPORTED = [
+    "gdf_create", "gdf_destroy", "gdf_last_error", "gdf_version", "gdf_set_stream",
+    "gdf_synchronize", "gdf_set_voxel_group_size", "gdf_clear", "gdf_add_depthmap",
+    "gdf_add_depthmap_device", "gdf_add_point_sequence", "gdf_num_collected_point_sequence_points",
+    "gdf_upload_point_sequences", "gdf_filter_new_point_sequences", "gdf_insert_new_point_sequences",
+    "gdf_roll_rollbuffer", "gdf_select_timespan", "gdf_prepare_point_and_mask_buffers",
+    "gdf_insert_selected_point_sequence", "gdf_transform_point_sequence", "gdf_get_rollbuffer_state",
+    "gdf_upload_depthmaps", "gdf_convert_depthmaps", "gdf_filter_flying_pixels", "gdf_crop_points",
+    "gdf_apply_point_mask", "gdf_compute_voxel_coords", "gdf_voxelize", "gdf_voxel_occupancy_grid",
+    "gdf_get_point_count", "gdf_download_points", "gdf_download_voxel_coords",
+    "gdf_download_voxelized_points", "gdf_download_occupancy_grid", "gdf_get_grid_size",
+    "gdf_get_device_results", "gdf_process_frame", "gdf_export_occupancy_marks",
+    "gdf_import_occupancy_marks", "gdf_set_profiling", "gdf_get_kernel_times", "gdf_set_debug", "gdf_debug_stage_masks", "gdf_debug_rollbuffer",
+    "gdf_debug_historic_grid",
+]
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libgdf.so (raises if it was not built: there is no fallback path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise GDFError(-2, f"{path} not built (run __graft_entry__.build())")
+    lib = C.CDLL(path)
+    vp, u32, i32, f, u64 = C.c_void_p, C.c_uint32, C.c_int, C.c_float, C.c_uint64
+    P = C.POINTER
+    sig = {
+        "gdf_create": (i32, [i32, P(vp)]),
+        "gdf_destroy": (i32, [vp]),
+        "gdf_last_error": (C.c_char_p, []),
+        "gdf_version": (i32, [P(i32), P(i32)]),
+        "gdf_set_stream": (i32, [vp, vp]),
+        "gdf_synchronize": (i32, [vp]),
+        "gdf_set_voxel_group_size": (i32, [vp, i32]),
+        "gdf_clear": (i32, [vp]),
+        "gdf_add_depthmap": (i32, [vp, vp, u32, u32, f, f, f, f, f, vp, vp]),
+        "gdf_add_depthmap_device": (i32, [vp, vp, u32, u32, f, f, f, f, f, vp, vp]),
+        "gdf_add_point_sequence": (i32, [vp, vp, u32, u32, u32, u32, vp]),
+        "gdf_num_collected_point_sequence_points": (i32, [vp, P(u32)]),
+        "gdf_upload_point_sequences": (i32, [vp]),
+        "gdf_filter_new_point_sequences": (i32, [vp, f, u32]),
+        "gdf_insert_new_point_sequences": (i32, [vp]),
+        "gdf_roll_rollbuffer": (i32, [vp, u32, u32]),
+        "gdf_select_timespan": (i32, [vp, u32, u32, u32, u32]),
+        "gdf_prepare_point_and_mask_buffers": (i32, [vp]),
+        "gdf_insert_selected_point_sequence": (i32, [vp, vp, vp]),
+        "gdf_transform_point_sequence": (i32, [vp]),
+        "gdf_get_rollbuffer_state": (i32, [vp, P(RollbufferState)]),
+        "gdf_upload_depthmaps": (i32, [vp]),
+        "gdf_convert_depthmaps": (i32, [vp]),
+        "gdf_filter_flying_pixels": (i32, [vp, u32, f, i32]),
+        "gdf_crop_points": (i32, [vp, vp, vp]),
+        "gdf_apply_point_mask": (i32, [vp, P(u32)]),
+        "gdf_compute_voxel_coords": (i32, [vp, vp, vp, vp]),
+        "gdf_voxelize": (i32, [vp, i32]),
+        "gdf_voxel_occupancy_grid": (i32, [vp, u32]),
+        "gdf_get_point_count": (i32, [vp, P(u32)]),
+        "gdf_download_points": (i32, [vp, vp, u32, P(u32)]),
+        "gdf_download_voxel_coords": (i32, [vp, vp, u32, P(u32)]),
+        "gdf_download_voxelized_points": (i32, [vp, vp, u32, P(u32)]),
+        "gdf_download_occupancy_grid": (i32, [vp, vp, u64]),
+        "gdf_get_grid_size": (i32, [vp, vp, P(u64)]),
+        "gdf_get_device_results": (i32, [vp, P(vp), P(vp), P(vp), P(vp)]),
+        "gdf_process_frame": (i32, [vp, P(FrameParams), P(FrameResult)]),
+        "gdf_export_occupancy_marks": (i32, [vp, vp, u64]),
+        "gdf_import_occupancy_marks": (i32, [vp, vp, u64, u32]),
+        "gdf_set_profiling": (i32, [vp, i32]),
+        "gdf_get_kernel_times": (i32, [vp, vp, vp, i32]),
+        "gdf_set_debug": (i32, [vp, i32]),
+        "gdf_debug_stage_masks": (i32, [vp, vp, u32, P(u32)]),
+        "gdf_debug_rollbuffer": (i32, [vp, vp, vp, vp, u32, vp, u32]),
+        "gdf_debug_historic_grid": (i32, [vp, vp, u64]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def _mat(m) -> np.ndarray:
+    a = np.ascontiguousarray(np.asarray(m, dtype=np.float32).reshape(16))
+    return a
+
+
+def _vec3(v) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(v, dtype=np.float32).reshape(3))
+
+
+@dataclass
+class ComponentParams:
+    """GPUDepthmapFusionComponent parameters (component.cpp:1115-1187) with the launch-file
+    defaults (launch/gpu_depthmap_fusion.launch:20-195)."""
+    ps_filter_threshold: float = 0.05
+    ps_filter_size: int = 1
+    ps_timespan: float = 1.0
+    flying_filter_size: int = 4
+    flying_threshold: float = 0.3
+    flying_rot45: bool = False
+    crop_min: Sequence[float] = (-10.0, -20.0, -1.0)
+    crop_max: Sequence[float] = (30.0, 20.0, 1.5)
+    enable_voxel_filter: bool = True
+    voxel_min: Sequence[float] = (-10.0, -20.0, -1.0)
+    voxel_max: Sequence[float] = (30.0, 20.0, 1.5)
+    voxel_size: Sequence[float] = (0.1, 0.1, 0.12)
+    voxel_average: bool = True
+    occupancy_lifetime: int = 10
+
+    @staticmethod
+    def code_defaults() -> "ComponentParams":
+        """Defaults compiled into onInit when the launch file sets nothing."""
+        return ComponentParams(ps_filter_threshold=0.5, ps_filter_size=1, ps_timespan=0.1,
+                               flying_filter_size=1, flying_threshold=0.5, flying_rot45=True,
+                               crop_min=(-1, -1, -1), crop_max=(1, 1, 1), voxel_min=(-1, -1, -1),
+                               voxel_max=(1, 1, 1), voxel_size=(0.1, 0.1, 0.1),
+                               occupancy_lifetime=1)
+
+    def to_c(self, T_world_move=None, T_crop_move=None, synchronous=True,
+             defer_occupancy_grid=False) -> FrameParams:
+        p = FrameParams()
+        p.ps_filter_threshold = self.ps_filter_threshold
+        p.ps_filter_size = self.ps_filter_size
+        p.ps_timespan = self.ps_timespan
+        p.move_transform_available = 1 if T_world_move is not None else 0
+        eye = np.eye(4, dtype=np.float32).reshape(16)
+        p.T_world_move = _f16(*(eye if T_world_move is None else _mat(T_world_move)))
+        p.T_crop_move = _f16(*(eye if T_crop_move is None else _mat(T_crop_move)))
+        p.flying_filter_size = self.flying_filter_size
+        p.flying_threshold = self.flying_threshold
+        p.flying_rot45 = 1 if self.flying_rot45 else 0
+        p.crop_min = _f3(*self.crop_min)
+        p.crop_max = _f3(*self.crop_max)
+        p.enable_voxel_filter = 1 if self.enable_voxel_filter else 0
+        p.voxel_min = _f3(*self.voxel_min)
+        p.voxel_max = _f3(*self.voxel_max)
+        p.voxel_size = _f3(*self.voxel_size)
+        p.voxel_average = 1 if self.voxel_average else 0
+        p.occupancy_lifetime = self.occupancy_lifetime
+        p.defer_occupancy_grid = 1 if defer_occupancy_grid else 0
+        p.synchronous = 1 if synchronous else 0
+        return p
+
+
+class GPUDepthmapFusion:
+    """Python mirror of GPUDepthmapFusion (gpu_depthmap_fusion.h:159-526) over libgdf.so."""
+
+    def __init__(self, device: int = 0, lib_path: str = LIB_PATH):
+        self._lib = load_library(lib_path)
+        h = C.c_void_p()
+        self._check(self._lib.gdf_create(device, C.byref(h)))
+        self._h = h
+        self._keep = []  # host depth maps borrowed until uploadDepthmaps
+
+    # ---- plumbing ----
+    def _check(self, rc: int):
+        if rc != GDF_OK:
+            raise GDFError(rc, self._lib.gdf_last_error().decode())
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.gdf_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_stream(self, stream_ptr: int):
+        self._check(self._lib.gdf_set_stream(self._h, C.c_void_p(stream_ptr)))
+
+    def synchronize(self):
+        self._check(self._lib.gdf_synchronize(self._h))
+
+    def set_debug(self, on: bool = True):
+        self._check(self._lib.gdf_set_debug(self._h, 1 if on else 0))
+
+    # ---- inputs ----
+    def clear(self):
+        self._keep = []
+        self._check(self._lib.gdf_clear(self._h))
+
+    def addDepthmap(self, depth: np.ndarray, depthScale: float, fx: float, fy: float, cx: float,
+                    cy: float, transform_world, transform_crop):
+        d = np.ascontiguousarray(depth, dtype=np.uint16)
+        H, W = d.shape
+        tw, tc = _mat(transform_world), _mat(transform_crop)
+        self._keep.append((d, tw, tc))
+        self._check(self._lib.gdf_add_depthmap(self._h, _ptr(d), W, H, depthScale, fx, fy, cx, cy,
+                                               _ptr(tw), _ptr(tc)))
+
+    def addDepthmapDevice(self, dev_ptr: int, width: int, height: int, depthScale: float,
+                          fx: float, fy: float, cx: float, cy: float, transform_world,
+                          transform_crop):
+        tw, tc = _mat(transform_world), _mat(transform_crop)
+        self._check(self._lib.gdf_add_depthmap_device(self._h, C.c_void_p(dev_ptr), width, height,
+                                                      depthScale, fx, fy, cx, cy, _ptr(tw),
+                                                      _ptr(tc)))
+
+    def addPointSequence(self, xyz: np.ndarray, timestampSec: int, timestampNSec: int,
+                         transform_move):
+        """xyz: (n, k>=3) float32 records (PointCloud2 with x,y,z at offsets 0/4/8)."""
+        rec = np.ascontiguousarray(xyz, dtype=np.float32)
+        if rec.ndim != 2 or rec.shape[1] < 3:
+            raise ValueError("point records must be (n, >=3) float32")
+        tm = _mat(transform_move)
+        self._check(self._lib.gdf_add_point_sequence(self._h, _ptr(rec), rec.shape[0],
+                                                     rec.shape[1] * 4, timestampSec,
+                                                     timestampNSec, _ptr(tm)))
+
+    def numCollectedPointSequencePoints(self) -> int:
+        n = C.c_uint32()
+        self._check(self._lib.gdf_num_collected_point_sequence_points(self._h, C.byref(n)))
+        return n.value
+
+    # ---- point-sequence chain ----
+    def uploadPointSequences(self):
+        self._check(self._lib.gdf_upload_point_sequences(self._h))
+
+    def filterNewPointSequences(self, threshold: float, filter_size: int):
+        self._check(self._lib.gdf_filter_new_point_sequences(self._h, threshold, filter_size))
+
+    def insertNewPointSequencesInRollbuffer(self):
+        self._check(self._lib.gdf_insert_new_point_sequences(self._h))
+
+    def rollPointSequenceRollbufferCPU(self, minSec: int, minNSec: int):
+        self._check(self._lib.gdf_roll_rollbuffer(self._h, minSec, minNSec))
+
+    def selectPointSequenceTimespanCPU(self, minSec, minNSec, maxSec, maxNSec):
+        self._check(self._lib.gdf_select_timespan(self._h, minSec, minNSec, maxSec, maxNSec))
+
+    def preparePointAndMaskBuffers(self):
+        self._check(self._lib.gdf_prepare_point_and_mask_buffers(self._h))
+
+    def insertSelectedPointSequence(self, tf_world_move, tf_crop_move):
+        a, b = _mat(tf_world_move), _mat(tf_crop_move)
+        self._check(self._lib.gdf_insert_selected_point_sequence(self._h, _ptr(a), _ptr(b)))
+
+    def transformPointSequence(self):
+        self._check(self._lib.gdf_transform_point_sequence(self._h))
+
+    def rollbuffer_state(self) -> RollbufferState:
+        st = RollbufferState()
+        self._check(self._lib.gdf_get_rollbuffer_state(self._h, C.byref(st)))
+        return st
+
+    # ---- depth chain ----
+    def uploadDepthmaps(self):
+        self._check(self._lib.gdf_upload_depthmaps(self._h))
+        self._keep = []
+
+    def convertDepthmaps(self):
+        self._check(self._lib.gdf_convert_depthmaps(self._h))
+
+    def filterFlyingPixels(self, filter_size: int, threshold: float, enable_rot45: bool):
+        self._check(self._lib.gdf_filter_flying_pixels(self._h, filter_size, threshold,
+                                                       1 if enable_rot45 else 0))
+
+    def cropPoints(self, lower_bound, upper_bound):
+        lo, hi = _vec3(lower_bound), _vec3(upper_bound)
+        self._check(self._lib.gdf_crop_points(self._h, _ptr(lo), _ptr(hi)))
+
+    def applyPointMask(self) -> int:
+        n = C.c_uint32()
+        self._check(self._lib.gdf_apply_point_mask(self._h, C.byref(n)))
+        return n.value
+
+    def computeVoxelCoords(self, lower_bound, upper_bound, cell_size):
+        lo, hi, cs = _vec3(lower_bound), _vec3(upper_bound), _vec3(cell_size)
+        self._check(self._lib.gdf_compute_voxel_coords(self._h, _ptr(lo), _ptr(hi), _ptr(cs)))
+
+    def voxelize(self, average_voxels: bool):
+        self._check(self._lib.gdf_voxelize(self._h, 1 if average_voxels else 0))
+
+    def voxelOccupancyGrid(self, lifetime: int):
+        self._check(self._lib.gdf_voxel_occupancy_grid(self._h, lifetime))
+
+    # ---- results ----
+    def point_count(self) -> int:
+        n = C.c_uint32()
+        self._check(self._lib.gdf_get_point_count(self._h, C.byref(n)))
+        return n.value
+
+    def downloadPoints(self) -> np.ndarray:
+        n = self.point_count()
+        out = np.empty((max(n, 1), 4), np.float32)
+        cnt = C.c_uint32()
+        self._check(self._lib.gdf_download_points(self._h, _ptr(out), out.shape[0], C.byref(cnt)))
+        return out[:cnt.value]
+
+    def downloadVoxelCoords(self) -> np.ndarray:
+        n = self.point_count()
+        out = np.empty(max(n, 1), np.uint32)
+        cnt = C.c_uint32()
+        self._check(self._lib.gdf_download_voxel_coords(self._h, _ptr(out), out.shape[0],
+                                                        C.byref(cnt)))
+        return out[:cnt.value]
+
+    def downloadVoxelizedPoints(self) -> np.ndarray:
+        cnt = C.c_uint32()
+        self._check(self._lib.gdf_download_voxelized_points(self._h, None, 0, C.byref(cnt)))
+        out = np.empty((max(cnt.value, 1), 4), np.float32)
+        self._check(self._lib.gdf_download_voxelized_points(self._h, _ptr(out), out.shape[0],
+                                                            C.byref(cnt)))
+        return out[:cnt.value]
+
+    def grid_size(self):
+        g = np.zeros(3, np.uint32)
+        nc = C.c_uint64()
+        self._check(self._lib.gdf_get_grid_size(self._h, _ptr(g), C.byref(nc)))
+        return tuple(int(x) for x in g), nc.value
+
+    def downloadVoxelOccupancyGrid(self) -> np.ndarray:
+        _, nc = self.grid_size()
+        out = np.empty(max(nc, 1), np.uint8)
+        self._check(self._lib.gdf_download_occupancy_grid(self._h, _ptr(out), out.shape[0]))
+        return out[:nc]
+
+    def historic_grid(self) -> np.ndarray:
+        _, nc = self.grid_size()
+        out = np.empty(max(nc, 1), np.uint32)
+        self._check(self._lib.gdf_debug_historic_grid(self._h, _ptr(out), out.shape[0]))
+        return out[:nc]
+
+    def stage_masks(self) -> np.ndarray:
+        cnt = C.c_uint32()
+        self._check(self._lib.gdf_debug_stage_masks(self._h, None, 0, C.byref(cnt)))
+        out = np.empty(max(cnt.value, 1), np.uint8)
+        self._check(self._lib.gdf_debug_stage_masks(self._h, _ptr(out), out.shape[0],
+                                                    C.byref(cnt)))
+        return out[:cnt.value]
+
+    def rollbuffer_arrays(self):
+        st = self.rollbuffer_state()
+        R, S = st.num_points, st.num_seqs
+        pts = np.empty((max(R, 1), 4), np.float32)
+        mask = np.empty(max(R, 1), np.uint32)
+        seq = np.empty(max(R, 1), np.uint32)
+        hdr = np.empty((max(S, 1), 4), np.uint32)
+        self._check(self._lib.gdf_debug_rollbuffer(self._h, _ptr(pts), _ptr(mask), _ptr(seq),
+                                                   pts.shape[0], _ptr(hdr), hdr.shape[0]))
+        return pts[:R], mask[:R], seq[:R], hdr[:S]
+
+    def device_results(self):
+        p, c, v, o = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_void_p()
+        self._check(self._lib.gdf_get_device_results(self._h, C.byref(p), C.byref(c),
+                                                     C.byref(v), C.byref(o)))
+        return p.value, c.value, v.value, o.value
+
+    def export_marks(self, dev_ptr: int, words: int):
+        self._check(self._lib.gdf_export_occupancy_marks(self._h, C.c_void_p(dev_ptr), words))
+
+    def import_marks(self, dev_ptr: int, words: int, nranks: int):
+        self._check(self._lib.gdf_import_occupancy_marks(self._h, C.c_void_p(dev_ptr), words,
+                                                         nranks))
+
+    # ---- whole frame ----
+    def set_profiling(self, on: bool = True):
+        self._check(self._lib.gdf_set_profiling(self._h, 1 if on else 0))
+
+    def kernel_times(self):
+        """{slot: (ms_sum, launches)} of the event-timed launches since set_profiling."""
+        ms = np.zeros(4, np.float64)
+        n = np.zeros(4, np.uint64)
+        self._check(self._lib.gdf_get_kernel_times(self._h, _ptr(ms), _ptr(n), 4))
+        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(KERNEL_SLOTS)}
+
+    def processFrame(self, params: ComponentParams, T_world_move=None, T_crop_move=None,
+                     synchronous: bool = True, defer_occupancy_grid: bool = False) -> FrameResult:
+        p = params.to_c(T_world_move, T_crop_move, synchronous, defer_occupancy_grid)
+        r = FrameResult()
+        self._check(self._lib.gdf_process_frame(self._h, C.byref(p), C.byref(r)))
+        self._keep = []
+        return r

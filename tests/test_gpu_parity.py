@@ -1,0 +1,277 @@
+"""GPU parity tests: libgdf.so (HIP, gfx950) through the C-ABI vs the CPU oracle.
+
+Bar (SURVEY.md §8c / north_star): masks, voxel keys, occupancy grids, historic grid and
+rollbuffer indices bit-exact; world points and voxel means compared bit for bit as well (the
+kernels follow the oracle's op order; the stated tolerance 1e-5 is the fallback, not needed).
+"""
+import numpy as np
+import pytest
+
+from drive import bits, compare_results, stagewise_frame
+from oracle import OracleFusion, RefRadix  # noqa: F401
+from ros_gpu_depthmap_fusion_amd import synth
+from ros_gpu_depthmap_fusion_amd.gdf import ComponentParams, GDFError
+
+pytestmark = pytest.mark.gpu
+
+EYE = np.eye(4, dtype=np.float32)
+
+
+def cam_args(cam, depth):
+    return (depth, *cam.intrinsics(), cam.T_world, cam.T_crop)
+
+
+@pytest.fixture(scope="module")
+def Engine(gpu_engine_factory):
+    return gpu_engine_factory
+
+
+def run_fused(eng, cams_frames, params, **kw):
+    eng.clear()
+    for c in cams_frames:
+        eng.addDepthmap(*c)
+    return eng.processFrame(params, **kw)
+
+
+def test_fused_vga_launch_defaults_multi_frame(Engine):
+    """C2 workload (1 x VGA, launch defaults) over 4 frames: the historic grid evolves."""
+    p = ComponentParams()
+    gpu, orc = Engine(), OracleFusion(threads=8)
+    cam = synth.make_camera(0, 640, 480)
+    for f in range(4):
+        args = [cam_args(cam, synth.depth_frame(cam, 0, f))]
+        r = run_fused(gpu, args, p)
+        run_fused(orc, args, p)
+        assert r.processed == 1 and r.num_points == orc.point_count()
+        compare_results(gpu, orc, tag=f"frame {f}")
+
+
+def test_stagewise_code_defaults_and_stage_masks(Engine):
+    """Stage-by-stage API (the component's exact call order) with the code defaults
+    (F=1, thr 0.5, rot45 on, lifetime 1) on two cameras; per-pixel stage masks compared."""
+    p = ComponentParams.code_defaults()
+    p.crop_min, p.crop_max = (-3, -3, -1), (6, 3, 2.5)
+    p.voxel_min, p.voxel_max = (-3, -3, -1), (6, 3, 2.5)
+    gpu, orc = Engine(), OracleFusion(threads=4)
+    gpu.set_debug(True)
+    cams = synth.cameras(2, 200, 150)
+    for f in range(3):
+        args = [cam_args(c, synth.depth_frame(c, k, f)) for k, c in enumerate(cams)]
+        stagewise_frame(gpu, args, p)
+        stagewise_frame(orc, args, p)
+        sm = gpu.stage_masks()
+        st = orc.stage_arrays()
+        n = orc.num_points_total()
+        assert len(sm) == n
+        depth_valid = np.concatenate([a[0].reshape(-1) != 0 for a in args])
+        np.testing.assert_array_equal((sm & 1) != 0, depth_valid)
+        np.testing.assert_array_equal((sm & 2) != 0, st["maskB"] != 0)
+        np.testing.assert_array_equal((sm & 4) != 0, st["maskA"] != 0)
+        compare_results(gpu, orc, tag=f"frame {f}")
+
+
+def test_multicamera_cross_camera_border_semantics(Engine):
+    """Cameras concatenated in one point space: camera k>0's top rows read camera k-1's bottom
+    rows, left border wraps to the previous row (A.6)."""
+    p = ComponentParams()
+    p.flying_filter_size = 3
+    gpu, orc = Engine(), OracleFusion(threads=4)
+    gpu.set_debug(True)
+    cams = synth.cameras(3, 128, 96)
+    args = [cam_args(c, synth.depth_frame(c, k, 7)) for k, c in enumerate(cams)]
+    run_fused(gpu, args, p)
+    run_fused(orc, args, p)
+    np.testing.assert_array_equal((gpu.stage_masks() & 4) != 0, orc.stage_arrays()["maskA"] != 0)
+    compare_results(gpu, orc)
+
+
+def test_uniform_random_depth_stress(Engine):
+    p = ComponentParams()
+    p.flying_rot45 = True
+    gpu, orc = Engine(), OracleFusion(threads=8)
+    cam = synth.make_camera(1, 320, 240)
+    for f in range(2):
+        args = [cam_args(cam, synth.uniform_frame(cam, 1, f))]
+        run_fused(gpu, args, p)
+        run_fused(orc, args, p)
+        compare_results(gpu, orc, tag=f"frame {f}")
+
+
+@pytest.mark.parametrize("W,H", [(1, 1), (2, 3), (5, 1), (1, 7), (33, 31)])
+def test_tiny_and_ragged_images(Engine, W, H):
+    p = ComponentParams.code_defaults()
+    p.crop_min = p.voxel_min = (-5, -5, -5)
+    p.crop_max = p.voxel_max = (5, 5, 5)
+    gpu, orc = Engine(), OracleFusion()
+    rng = np.random.default_rng(W * 100 + H)
+    cam = synth.make_camera(0, W, H)
+    for f in range(2):
+        d = rng.integers(0, 4000, (H, W)).astype(np.uint16)
+        d[rng.random((H, W)) < 0.2] = 0
+        run_fused(gpu, [cam_args(cam, d)], p)
+        run_fused(orc, [cam_args(cam, d)], p)
+        compare_results(gpu, orc)
+
+
+def test_empty_and_all_zero_frames(Engine):
+    p = ComponentParams()
+    gpu, orc = Engine(), OracleFusion()
+    gpu.clear()
+    r = gpu.processFrame(p)
+    assert r.processed == 0
+    cam = synth.make_camera(0, 64, 48)
+    # a populated frame, then an all-zero frame: no points, the grid only decays
+    for d in (synth.depth_frame(cam, 0, 0), np.zeros((48, 64), np.uint16)):
+        run_fused(gpu, [cam_args(cam, d)], p)
+        run_fused(orc, [cam_args(cam, d)], p)
+        compare_results(gpu, orc)
+    assert gpu.point_count() == 0 and len(gpu.downloadVoxelizedPoints()) == 0
+    assert gpu.downloadVoxelOccupancyGrid().max() == p.occupancy_lifetime - 1
+
+
+def test_lifetime_above_127_uses_u32_history(Engine):
+    p = ComponentParams()
+    cam = synth.make_camera(0, 160, 120)
+    gpu, orc = Engine(), OracleFusion()
+    for f, life in enumerate([10, 300, 300, 5, 1000]):
+        p.occupancy_lifetime = life
+        args = [cam_args(cam, synth.depth_frame(cam, 0, f))]
+        run_fused(gpu, args, p)
+        run_fused(orc, args, p)
+        compare_results(gpu, orc, tag=f"frame {f} lifetime {life}")
+
+
+def test_voxelize_corners_mode(Engine):
+    p = ComponentParams()
+    p.voxel_average = False
+    cam = synth.make_camera(2, 160, 120)
+    gpu, orc = Engine(), OracleFusion()
+    args = [cam_args(cam, synth.depth_frame(cam, 2, 3))]
+    run_fused(gpu, args, p)
+    run_fused(orc, args, p)
+    compare_results(gpu, orc)
+
+
+def _add_sequences(engines, k0, nseq, cam, depth_fn, rng, empty_every=0, nan_frac=0.0):
+    for k in range(k0, k0 + nseq):
+        if empty_every and k % empty_every == 0:
+            pts = np.zeros((0, 3), np.float32)
+        else:
+            pts = synth.back_project(cam, depth_fn(k))
+            if nan_frac:
+                pts[rng.random(len(pts)) < nan_frac] = np.nan
+        s, ns = synth.sequence_time(k)
+        for e in engines:
+            e.addPointSequence(pts, s, ns, synth.move_transform(k))
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_rollbuffer_chain(Engine, fused):
+    """Point sequences (with empty sequences and NaN points) through filter / insert / roll /
+    select / transform over 8 frames, window of ~5 sequences (rollbuffer indices bit-exact)."""
+    p = ComponentParams()
+    p.ps_timespan = 4.0 / 30.0
+    p.ps_filter_size = 2
+    lidar = synth.make_camera(0, 96, 64)
+    cam = synth.make_camera(1, 120, 90)
+    gpu, orc = Engine(), OracleFusion(threads=4)
+    rng = np.random.default_rng(9)
+    Twm = synth.move_transform(3)
+    Tcm = EYE
+    k = 0
+    for f in range(8):
+        nseq = 1 + (f % 3)
+        _add_sequences([gpu, orc], k, nseq, lidar, lambda kk: synth.depth_frame(lidar, 5, kk), rng,
+                       empty_every=4, nan_frac=0.01)
+        k += nseq
+        args = [cam_args(cam, synth.depth_frame(cam, 1, f))] if f % 4 != 3 else []
+        if fused:
+            for e in (gpu, orc):
+                e.clear()
+                for a in args:
+                    e.addDepthmap(*a)
+                e.processFrame(p, T_world_move=Twm, T_crop_move=Tcm)
+        else:
+            stagewise_frame(gpu, args, p, Twm, Tcm)
+            stagewise_frame(orc, args, p, Twm, Tcm)
+        assert gpu.rollbuffer_state().as_tuple() == orc.rollbuffer_state(), f"frame {f}"
+        gp, gm, gs, gh = gpu.rollbuffer_arrays()
+        op, om, os_, oh = orc.rollbuffer_arrays()
+        np.testing.assert_array_equal(gm, om)
+        np.testing.assert_array_equal(gs, os_)
+        np.testing.assert_array_equal(gh, oh)
+        np.testing.assert_array_equal(bits(gp), bits(op))
+        compare_results(gpu, orc, tag=f"frame {f}")
+
+
+def test_voxelize_pinned_to_reference_radix_golden(Engine):
+    """Points placed at voxel centres (through the rollbuffer with identity transforms) so the
+    voxel keys ARE the golden keys of tests/golden/radix_ref.npz; the GPU voxel groups must come
+    out in the reference RadixGrouper's order with the reference's group sizes."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "radix_ref.npz"))
+    p = ComponentParams()
+    p.ps_filter_size = 0
+    p.ps_timespan = 1000.0
+    p.voxel_min = p.crop_min = (0.0, 0.0, 0.0)
+    p.voxel_max = p.crop_max = (2048.0, 2048.0, 1.0)
+    p.voxel_size = (1.0, 1.0, 1.0)
+    for name in ("voxelish", "dups", "ragged_tiles"):
+        keys = g[name + "_keys"] % np.uint32(2048 * 2048)
+        if name == "voxelish":
+            keys = g[name + "_keys"]
+            keys = keys[keys < 2048 * 2048]
+        x = (keys % 2048).astype(np.float32) + np.float32(0.5)
+        y = (keys // 2048).astype(np.float32) + np.float32(0.5)
+        pts = np.stack([x, y, np.full_like(x, 0.5)], -1)
+        gpu = Engine()
+        gpu.clear()
+        gpu.addPointSequence(pts, 5, 0, EYE)
+        gpu.processFrame(p, T_world_move=EYE, T_crop_move=EYE)
+        assert gpu.point_count() == len(keys)
+        np.testing.assert_array_equal(gpu.downloadVoxelCoords(), keys)
+        vox = gpu.downloadVoxelizedPoints()
+        # expected groups from the reference radix sort of exactly these keys
+        ref_idx = np.argsort(keys, kind="stable")
+        sk = keys[ref_idx]
+        starts = np.flatnonzero(np.r_[True, sk[1:] != sk[:-1]])
+        sizes = np.diff(np.r_[starts, len(sk)])
+        assert len(vox) == len(starts)
+        np.testing.assert_array_equal(vox[:, 0], x[ref_idx[starts]])  # all points of a voxel equal
+        np.testing.assert_array_equal(vox[:, 3], sizes.astype(np.float32))  # w = sum of w = count
+        if name != "voxelish":
+            full = g[name + "_keys"]
+            if np.array_equal(full, keys):
+                np.testing.assert_array_equal(ref_idx, g[name + "_sorted_idx"])
+
+
+def test_large_4k_frame_properties(Engine):
+    """Full-size 4K frame: oracle parity (8 threads) plus size-independent properties."""
+    p = ComponentParams()
+    gpu, orc = Engine(), OracleFusion(threads=8)
+    gpu.set_debug(True)
+    cam = synth.make_camera(3, 3840, 2160)
+    args = [cam_args(cam, synth.depth_frame(cam, 3, 0))]
+    run_fused(gpu, args, p)
+    run_fused(orc, args, p)
+    compare_results(gpu, orc)
+    sm = gpu.stage_masks()
+    assert gpu.point_count() == int(np.count_nonzero(sm & 4))
+    c = gpu.downloadVoxelCoords()
+    vox = gpu.downloadVoxelizedPoints()
+    assert len(vox) == len(np.unique(c))
+    grid = gpu.downloadVoxelOccupancyGrid()
+    assert np.count_nonzero(grid == p.occupancy_lifetime) == len(np.unique(c))
+
+
+def test_errors_fail_loudly(Engine):
+    gpu = Engine()
+    with pytest.raises(GDFError):
+        gpu.computeVoxelCoords((0, 0, 0), (1, 1, 1), (0.1, 0.1, 0.1))  # before applyPointMask
+    gpu.clear()
+    cam = synth.make_camera(0, 8, 8)
+    gpu.addDepthmap(synth.depth_frame(cam, 0, 0), *cam.intrinsics(), cam.T_world, cam.T_crop)
+    p = ComponentParams()
+    p.voxel_min, p.voxel_max = (1, 1, 1), (0, 0, 0)
+    with pytest.raises(GDFError):
+        gpu.processFrame(p)
