@@ -12,37 +12,41 @@
 namespace gdf {
 
 constexpr int kMaxCams = 16;          // GDF_MAX_CAMERAS
-constexpr int kFrameThreads = 256;    // compaction block: 4 waves
-constexpr int kFramePerThread = 4;    // 4 consecutive items per thread (8-byte depth load)
-constexpr int kFrameTile = kFrameThreads * kFramePerThread;  // 1024 items per tile
+constexpr int kFrameThreads = 256;    // compaction block: 4 waves, one item per thread
+constexpr int kFrameTile = kFrameThreads;
 constexpr int kSortThreads = 256;
-constexpr int kSortPerThread = 16;
-constexpr int kSortTile = kSortThreads * kSortPerThread;     // 4096 keys per tile
 constexpr int kGroupThreads = 256;
 constexpr int kGroupPerThread = 8;
 constexpr int kGroupTile = kGroupThreads * kGroupPerThread;  // 2048 sorted keys per tile
+constexpr int kSumChunk = 256;                               // points per wave gather chunk
 constexpr uint32_t kSpinLimit = 1u << 26;                   // bounded look-back spins
 
-// One depth camera of the frame (DepthmapConversion, gpu_depthmap_fusion.h:163-176).
-// `off` is the camera's first index in the concatenated point space (fusion.cpp:1605-1626).
+// Device-wide counters: monotonically increasing tile tickets (the host passes each launch's
+// base, so no per-launch memset) and the global digit histogram of the voxel keys.
+enum CounterSlot { kCtrFrame = 0, kCtrSort0 = 1, kCtrGroup = 5, kCtrSlots = 8 };
+
 // A halo camera (emit == 0, multi-GPU sharding) sits at a negative offset: its pixels are only
 // read as flying-pixel neighbours, exactly where the reference's uint index arithmetic lands in
 // the previous camera of the concatenated buffer.
+// xn[u] = (u - cx) / fx and yn[v] = (v - cy) / fy are the per-column / per-row factors of
+// sh/convert_depthmap_to_points.glsl:64-73 (the same f32 divisions, computed once per camera).
 struct CamDesc {
     int64_t off;            // first index in the concatenated point space
     const uint16_t* depth;  // device pointer to pixel 0 of this camera
+    const float* xn;        // [W]
+    const float* yn;        // [H]
     uint32_t W, H, n;
     uint32_t emit;          // 1: pixels are processed; 0: halo camera, only read as neighbours
-    float scale, fx, fy, cx, cy;
+    float scale;
     float Tw[16];           // row-major T_world
     float Tc[16];           // row-major T_crop
     uint32_t pad[3];
 };
 static_assert(sizeof(CamDesc) % 16 == 0, "CamDesc must stay 16-byte sized");
 
-// Arguments of the fused compaction launch (k_frame).
+// Arguments of the fused compaction launch (k_frame), passed by value (cameras included).
 struct FrameArgs {
-    const CamDesc* cams;
+    CamDesc cams[kMaxCams];
     int32_t ncams;
     uint32_t depth_total;       // ΣP of emitting cameras' index space (tiles cover [0, depth_total))
     uint32_t depth_tiles;
@@ -71,16 +75,21 @@ struct FrameArgs {
     float vlo[3], vcs[3], gmax[3];
     uint32_t gs[3];
     uint8_t* occ;
+    uint32_t* key_hist;         // optional [npasses*256] digit histogram of the keys
+    uint32_t npasses;
     // outputs
     float4* out_pts;
-    uint32_t* out_coords;
     uint32_t* out_count;
+    uint32_t* out_coords;
     uint8_t* dbg;               // optional per-item stage bits
-    // decoupled look-back
+    // decoupled look-back (epoch-tagged granules, no memset) + tile tickets
     unsigned long long* status;
-    uint32_t* tile_ctr;
+    unsigned long long* tile_ctr;
+    unsigned long long tile_base;
+    uint32_t epoch;
     uint32_t* err;
 };
+static_assert(sizeof(FrameArgs) <= 4096, "kernel arguments are limited to 4 KiB");
 
 // ---- canonical float helpers (mirror oracle/gdf_oracle.c) ----------------------------------
 __device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, float by, float bz) {
@@ -100,16 +109,15 @@ __device__ __forceinline__ void normalize3(float& x, float& y, float& z) {
     z = z / l;
 }
 
-// sh/convert_depthmap_to_points.glsl:64-81 (u = idx mod W, v = idx / W)
+// sh/convert_depthmap_to_points.glsl:64-81 (u = idx mod W, v = idx / W):
+// p = ((u-cx)/fx · z, (v-cy)/fy · z, z) with z = f32(d)·scale
 __device__ __forceinline__ void cam_point(const CamDesc& c, uint32_t local, uint32_t d, float& x,
                                           float& y, float& z) {
-    float u = (float)(local % c.W);
-    float v = (float)(local / c.W);
-    float zz = (float)d * c.scale;
-    float xn = (u - c.cx) / c.fx;
-    float yn = (v - c.cy) / c.fy;
-    x = xn * zz;
-    y = yn * zz;
+    const uint32_t v = local / c.W;
+    const uint32_t u = local - v * c.W;
+    const float zz = (float)d * c.scale;
+    x = c.xn[u] * zz;
+    y = c.yn[v] * zz;
     z = zz;
 }
 

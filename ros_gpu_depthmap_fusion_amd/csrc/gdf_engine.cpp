@@ -71,8 +71,21 @@ struct DevBuf {
         bytes = nb;
         return true;
     }
+    // grow-only and zero-filled on growth (look-back granules / counters must start at 0)
+    bool ensure_zero(size_t need, hipStream_t s) {
+        if (!ensure(need)) return false;
+        HIPCHK(hipMemsetAsync(p, 0, bytes, s));
+        return true;
+    }
     template <class T>
     T* as() const { return static_cast<T*>(p); }
+};
+
+struct CamTable {  // cached per-camera ray factors (xn per column, yn per row)
+    uint32_t W = 0, H = 0;
+    float fx = 0, fy = 0, cx = 0, cy = 0;
+    bool valid = false;
+    DevBuf xn, yn;
 };
 
 struct Hdr {  // PointSequence, gpu_depthmap_fusion.h:178-204
@@ -147,6 +160,8 @@ struct gdf_engine {
     int device = 0;
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
+    hipStream_t aux = nullptr;          // historic-grid update, overlapped with voxelize
+    hipEvent_t ev_marks = nullptr, ev_grid = nullptr;
     std::mutex ps_mutex;
     int voxel_group_size = 1024;
 
@@ -159,7 +174,8 @@ struct gdf_engine {
     std::vector<Cam> cams;
     uint32_t depth_total = 0;
     std::vector<CamDesc> halo;      // halo cameras (multi-GPU), negative offsets
-    DevBuf d_depth, d_cams;
+    DevBuf d_depth;
+    std::vector<CamTable> tables = std::vector<CamTable>(kMaxCams);
     std::vector<CamDesc> h_cams;
     bool depth_uploaded = false;
 
@@ -190,6 +206,13 @@ struct gdf_engine {
     int rot45 = 0;
     float lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
 
+    // tile tickets + epochs of the look-back launches (no per-launch memsets)
+    DevBuf d_ctrs;
+    unsigned long long ctr_base[kCtrSlots] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t epoch = 0;
+    DevBuf d_khist;                 // digit histogram of the voxel keys [4*256]
+    bool khist_pending = false;     // accumulated by a fused k_frame, not yet consumed
+
     // compaction outputs
     DevBuf d_pts, d_coords, d_status, d_dbg;
     DevBuf d_misc;
@@ -210,7 +233,7 @@ struct gdf_engine {
     bool invoked_once = false;
 
     // voxelize
-    DevBuf d_ka, d_kb, d_va, d_vb, d_shist, d_sstatus, d_gstatus, d_vox;
+    DevBuf d_ka, d_kb, d_va, d_vb, d_sstatus, d_gstatus, d_gstart, d_vox;
     bool vox_valid = false;
 
     bool debug = false;
@@ -237,15 +260,17 @@ struct gdf_engine {
     }
     // brackets one launch (or launch group) of `slot` with an event pair when profiling
     template <class F>
-    void timed(int slot, F&& launch) {
+    void timed(int slot, F&& launch) { timed_on(slot, stream, launch); }
+    template <class F>
+    void timed_on(int slot, hipStream_t st, F&& launch) {
         if (!profiling) {
             launch();
             return;
         }
         EvPair p{take_event(), take_event(), slot};
-        HIPCHK(hipEventRecord(p.a, stream));
+        HIPCHK(hipEventRecord(p.a, st));
         launch();
-        HIPCHK(hipEventRecord(p.b, stream));
+        HIPCHK(hipEventRecord(p.b, st));
         ev_pending.push_back(p);
         if (ev_pending.size() > 4096) resolve_events();
     }
@@ -497,13 +522,27 @@ void insert_selected(gdf_engine* e, const float* Twm, const float* Tcm) {  // fu
 }
 
 // ---- depth chain ------------------------------------------------------------------------------------
+void ensure_table(gdf_engine* e, size_t slot, const Cam& c) {
+    CamTable& t = e->tables[slot];
+    if (t.valid && t.W == c.W && t.H == c.H && t.fx == c.fx && t.fy == c.fy && t.cx == c.cx &&
+        t.cy == c.cy)
+        return;
+    t.xn.ensure((size_t)c.W * 4);
+    t.yn.ensure((size_t)c.H * 4);
+    HIPCHK(launch_tables(c.W, c.H, c.fx, c.fy, c.cx, c.cy, t.xn.as<float>(), t.yn.as<float>(), e->s()));
+    t.W = c.W; t.H = c.H; t.fx = c.fx; t.fy = c.fy; t.cx = c.cx; t.cy = c.cy;
+    t.valid = true;
+}
+
 void upload_depthmaps(gdf_engine* e) {  // fusion.cpp:1583-1593
     uint64_t host_px = 0;
     for (const Cam& c : e->cams) if (!c.dev) host_px += c.n;
     if (host_px) e->d_depth.ensure(host_px * 2);
+    if (e->cams.size() + e->halo.size() > (size_t)kMaxCams) fail(GDF_ERR_ARG, "too many cameras (incl. halo)");
     e->h_cams.clear();
     uint64_t off = 0, hoff = 0;
-    for (const Cam& c : e->cams) {
+    for (size_t k = 0; k < e->cams.size(); ++k) {
+        const Cam& c = e->cams[k];
         CamDesc d{};
         d.off = (int64_t)off;
         if (c.dev) {
@@ -514,8 +553,11 @@ void upload_depthmaps(gdf_engine* e) {  // fusion.cpp:1583-1593
             d.depth = dst;
             hoff += c.n;
         }
+        ensure_table(e, e->halo.size() + k, c);
+        d.xn = e->tables[e->halo.size() + k].xn.as<float>();
+        d.yn = e->tables[e->halo.size() + k].yn.as<float>();
         d.W = c.W; d.H = c.H; d.n = c.n; d.emit = 1;
-        d.scale = c.scale; d.fx = c.fx; d.fy = c.fy; d.cx = c.cx; d.cy = c.cy;
+        d.scale = c.scale;
         std::memcpy(d.Tw, c.Tw, 64);
         std::memcpy(d.Tc, c.Tc, 64);
         e->h_cams.push_back(d);
@@ -524,13 +566,7 @@ void upload_depthmaps(gdf_engine* e) {  // fusion.cpp:1583-1593
     // halo cameras first (negative offsets), then the emitting cameras: sorted by offset
     std::vector<CamDesc> all = e->halo;
     all.insert(all.end(), e->h_cams.begin(), e->h_cams.end());
-    if (all.size() > (size_t)kMaxCams) fail(GDF_ERR_ARG, "too many cameras (incl. halo)");
     e->h_cams = all;
-    if (!all.empty()) {
-        e->d_cams.ensure(all.size() * sizeof(CamDesc));
-        HIPCHK(hipMemcpyWithStream(e->d_cams.p, all.data(), all.size() * sizeof(CamDesc),
-                                   hipMemcpyHostToDevice, e->s()));
-    }
     e->depth_uploaded = true;
 }
 
@@ -579,6 +615,8 @@ void ensure_misc(gdf_engine* e) {
         e->d_misc.ensure(kMiscWords * 4);
         HIPCHK(hipMemsetAsync(e->d_misc.p, 0, kMiscWords * 4, e->s()));
     }
+    if (!e->d_ctrs.p) e->d_ctrs.ensure_zero(kCtrSlots * 8, e->s());
+    if (!e->d_khist.p) e->d_khist.ensure_zero(4 * 256 * 4, e->s());
 }
 
 // The fused compaction launch: convert + flying + crop + selected-point transform + ordered
@@ -588,7 +626,7 @@ void run_frame(gdf_engine* e, bool fused_voxel) {
     if (!e->depth_uploaded) upload_depthmaps(e);
     ensure_misc(e);
     FrameArgs a{};
-    a.cams = e->d_cams.as<CamDesc>();
+    for (size_t k = 0; k < e->h_cams.size(); ++k) a.cams[k] = e->h_cams[k];
     a.ncams = (int32_t)e->h_cams.size();
     a.depth_total = e->depth_total;
     a.depth_tiles = (e->depth_total + kFrameTile - 1) / kFrameTile;
@@ -619,6 +657,9 @@ void run_frame(gdf_engine* e, bool fused_voxel) {
         std::memcpy(a.vcs, e->vp.vcs, 12);
         std::memcpy(a.gmax, e->vp.gmax, 12);
         std::memcpy(a.gs, e->vp.gs, 12);
+        if (e->khist_pending) HIPCHK(hipMemsetAsync(e->d_khist.p, 0, 4 * 256 * 4, e->s()));
+        a.key_hist = e->d_khist.as<uint32_t>();
+        a.npasses = e->key_bits == 0 ? 1u : (e->key_bits + 7) / 8;
     }
     a.out_pts = e->d_pts.as<float4>();
     a.out_coords = e->d_coords.as<uint32_t>();
@@ -628,11 +669,15 @@ void run_frame(gdf_engine* e, bool fused_voxel) {
         a.dbg = e->d_dbg.as<uint8_t>();
         e->dbg_count = e->n_total;
     }
-    e->d_status.ensure((size_t)std::max<uint32_t>(a.total_tiles, 1) * 8);
+    e->d_status.ensure_zero((size_t)std::max<uint32_t>(a.total_tiles, 1) * 8, e->s());
     a.status = e->d_status.as<unsigned long long>();
-    a.tile_ctr = e->d_misc.as<uint32_t>() + kTileCtr;
+    a.tile_ctr = e->d_ctrs.as<unsigned long long>() + kCtrFrame;
+    a.tile_base = e->ctr_base[kCtrFrame];
+    a.epoch = ++e->epoch;
     a.err = e->d_misc.as<uint32_t>() + kErr;
     e->timed(GDF_KERNEL_FRAME, [&] { HIPCHK(launch_frame(a, e->s())); });
+    e->ctr_base[kCtrFrame] += a.total_tiles;
+    e->khist_pending = fused_voxel;
     e->compacted = true;
     e->coords_valid = fused_voxel;
     e->marks_set = fused_voxel;
@@ -651,14 +696,15 @@ void compute_voxel_coords(gdf_engine* e, const float* lo, const float* hi, const
 void voxelize(gdf_engine* e, int average) {  // fusion.cpp:1743-1756
     if (!e->grid_set || !e->coords_valid) fail(GDF_ERR_STATE, "voxelize before computeVoxelCoords");
     const uint32_t nmax = std::max<uint32_t>(e->n_total, 1);
-    if (nmax >= (1u << 30)) fail(GDF_ERR_CAPACITY, "voxelize supports < 2^30 points");
+    if (nmax >= (1u << 31)) fail(GDF_ERR_CAPACITY, "voxelize supports < 2^31 points");
+    ensure_misc(e);
     e->d_ka.ensure((size_t)nmax * 4);
     e->d_kb.ensure((size_t)nmax * 4);
     e->d_va.ensure((size_t)nmax * 4);
     e->d_vb.ensure((size_t)nmax * 4);
-    e->d_shist.ensure(4 * 256 * 4 + 8 * 4);
-    e->d_sstatus.ensure(voxelize_status_words(nmax) * 4);
-    e->d_gstatus.ensure(voxelize_group_tiles(nmax) * 8);
+    e->d_gstart.ensure((size_t)nmax * 4);
+    e->d_sstatus.ensure_zero(voxelize_status_words(nmax) * 8, e->s());
+    e->d_gstatus.ensure_zero(voxelize_group_tiles(nmax) * 8, e->s());
     e->d_vox.ensure((size_t)nmax * 16);
     VoxelizeArgs v{};
     v.keys = e->d_coords.as<uint32_t>();
@@ -667,23 +713,28 @@ void voxelize(gdf_engine* e, int average) {  // fusion.cpp:1743-1756
     v.nmax = nmax;
     v.key_bits = e->key_bits;
     v.average = average;
+    v.hist_ready = e->khist_pending ? 1 : 0;
     v.vp = e->vp;
     v.keys_a = e->d_ka.as<uint32_t>();
     v.keys_b = e->d_kb.as<uint32_t>();
     v.vals_a = e->d_va.as<uint32_t>();
     v.vals_b = e->d_vb.as<uint32_t>();
-    v.hist = e->d_shist.as<uint32_t>();
-    v.ctrs = e->d_shist.as<uint32_t>() + 4 * 256;
-    v.status = e->d_sstatus.as<uint32_t>();
+    v.hist = e->d_khist.as<uint32_t>();
+    v.status = e->d_sstatus.as<unsigned long long>();
     v.gstatus = e->d_gstatus.as<unsigned long long>();
+    v.gstart = e->d_gstart.as<uint32_t>();
+    v.ctrs = e->d_ctrs.as<unsigned long long>();
+    v.ctr_base = e->ctr_base;
+    v.epoch = &e->epoch;
     v.err = e->d_misc.as<uint32_t>() + kErr;
     v.out = e->d_vox.as<float4>();
     v.out_count = e->d_misc.as<uint32_t>() + kVoxCount;
     e->timed(GDF_KERNEL_VOXELIZE, [&] { HIPCHK(launch_voxelize(v, e->s())); });
+    e->khist_pending = false;
     e->vox_valid = true;
 }
 
-void occupancy_grid(gdf_engine* e, uint32_t lifetime) {  // fusion.cpp:1757-1823
+void occupancy_grid(gdf_engine* e, uint32_t lifetime, hipStream_t st) {  // fusion.cpp:1757-1823
     if (!e->grid_set) fail(GDF_ERR_STATE, "voxelOccupancyGrid before computeVoxelCoords");
     if (e->grid_mode == 0 && lifetime > 127) {
         // widen the u8 grid (values <= 127, mark in bit 7) into the general u32 history
@@ -691,20 +742,20 @@ void occupancy_grid(gdf_engine* e, uint32_t lifetime) {  // fusion.cpp:1757-1823
         e->d_marks.ensure((size_t)e->ncells);
         e->d_out8.ensure((size_t)((e->ncells + 15) / 16) * 16);
         HIPCHK(launch_widen_grid(e->d_grid8.as<uint8_t>(), e->d_hist32.as<uint32_t>(),
-                                 e->d_marks.as<uint8_t>(), e->ncells, e->s()));
+                                 e->d_marks.as<uint8_t>(), e->ncells, st));
         e->grid_mode = 1;
     }
     if (!e->marks_set) {
         if (!e->coords_valid) fail(GDF_ERR_STATE, "voxelOccupancyGrid needs voxel coordinates");
         HIPCHK(launch_scatter(e->d_coords.as<uint32_t>(), e->d_misc.as<uint32_t>() + kCount,
-                              std::max<uint32_t>(e->n_total, 1), occ_ptr(e), occ_mode(e), e->s()));
+                              std::max<uint32_t>(e->n_total, 1), occ_ptr(e), occ_mode(e), st));
     }
-    e->timed(GDF_KERNEL_GRID, [&] {
+    e->timed_on(GDF_KERNEL_GRID, st, [&] {
         if (e->grid_mode == 0)
-            HIPCHK(launch_grid_u8(e->d_grid8.as<uint8_t>(), e->ncells, lifetime, e->s()));
+            HIPCHK(launch_grid_u8(e->d_grid8.as<uint8_t>(), e->ncells, lifetime, st));
         else
             HIPCHK(launch_grid_u32(e->d_hist32.as<uint32_t>(), e->d_marks.as<uint8_t>(),
-                                   e->d_out8.as<uint8_t>(), e->ncells, lifetime, e->s()));
+                                   e->d_out8.as<uint8_t>(), e->ncells, lifetime, st));
     });
     e->marks_set = false;
     e->invoked_once = true;
@@ -764,6 +815,9 @@ int gdf_create(int device, gdf_engine** out) {
     e->device = device;
     int rc = guarded(e, [&] {
         HIPCHK(hipStreamCreateWithFlags(&e->own, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&e->ev_marks, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&e->ev_grid, hipEventDisableTiming));
         e->stream = e->own;
         HIPCHK(hipHostMalloc((void**)&e->h_misc, kMiscWords * 4, hipHostMallocDefault));
         std::memset(e->h_misc, 0, kMiscWords * 4);
@@ -788,6 +842,10 @@ int gdf_destroy(gdf_engine* e) {
     }
     for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
     if (e->h_misc) (void)hipHostFree(e->h_misc);
+    if (e->aux) (void)hipStreamSynchronize(e->aux);
+    if (e->ev_marks) (void)hipEventDestroy(e->ev_marks);
+    if (e->ev_grid) (void)hipEventDestroy(e->ev_grid);
+    if (e->aux) (void)hipStreamDestroy(e->aux);
     if (e->own) (void)hipStreamDestroy(e->own);
     delete e;
     return GDF_OK;
@@ -959,7 +1017,7 @@ int gdf_voxelize(gdf_engine* e, int average) {
 
 int gdf_voxel_occupancy_grid(gdf_engine* e, uint32_t lifetime) {
     ENGINE_OR_FAIL(e);
-    return guarded(e, [&] { occupancy_grid(e, lifetime); });
+    return guarded(e, [&] { occupancy_grid(e, lifetime, e->s()); });
 }
 
 int gdf_get_point_count(gdf_engine* e, uint32_t* out) {
@@ -1106,8 +1164,17 @@ int gdf_process_frame(gdf_engine* e, const gdf_frame_params* p, gdf_frame_result
                 e->grid_mode = 1;
             }
             run_frame(e, true);
-            voxelize(e, p->voxel_average);
-            if (!p->defer_occupancy_grid) occupancy_grid(e, p->occupancy_lifetime);
+            if (!p->defer_occupancy_grid) {
+                // the grid update only needs the marks: run it on the aux stream beside voxelize
+                HIPCHK(hipEventRecord(e->ev_marks, e->s()));
+                HIPCHK(hipStreamWaitEvent(e->aux, e->ev_marks, 0));
+                occupancy_grid(e, p->occupancy_lifetime, e->aux);
+                HIPCHK(hipEventRecord(e->ev_grid, e->aux));
+                voxelize(e, p->voxel_average);
+                HIPCHK(hipStreamWaitEvent(e->s(), e->ev_grid, 0));
+            } else {
+                voxelize(e, p->voxel_average);
+            }
         } else {
             run_frame(e, false);
         }

@@ -43,62 +43,103 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t& t
     return wbase + x - v;
 }
 
-// Decoupled look-back over 8-byte {flag, value} granules (flag 1 = aggregate, 2 = inclusive).
-// Each granule is written by ONE agent-scope atomic store and polled with agent-scope atomic
-// loads (MI355X hand-off form "R2": the data is the flag, no fence needed).
-__device__ __forceinline__ uint32_t lookback64(unsigned long long* status, uint32_t tile,
-                                               uint32_t agg, uint32_t* err) {
+// Decoupled look-back over 8-byte {flag, value} granules.  flag = 2*epoch (aggregate) or
+// 2*epoch+1 (inclusive prefix); epoch >= 1 grows with every launch, so granules left by earlier
+// launches read as "not ready" and the status arrays never need a memset.  Each granule is
+// written by ONE agent-scope atomic store and polled with agent-scope atomic loads (MI355X
+// hand-off form "R2": the data is the flag, no fence needed).
+// Wave-cooperative variant, called by all 64 lanes of ONE wave: each hop polls the 64 nearest
+// predecessors at once (one cross-XCD round trip per 64 tiles instead of per tile), stops at the
+// nearest inclusive prefix and sums the aggregates in front of it.
+__device__ __forceinline__ uint32_t lookback_wave(unsigned long long* status, uint32_t tile,
+                                                  uint32_t agg, uint32_t epoch, uint32_t* err) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long fagg = 2ull * epoch, fincl = 2ull * epoch + 1ull;
     if (tile == 0) {
-        __hip_atomic_store(&status[0], (2ull << 32) | agg, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0)
+            __hip_atomic_store(&status[0], (fincl << 32) | agg, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         return 0;
     }
-    __hip_atomic_store(&status[tile], (1ull << 32) | agg, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0)
+        __hip_atomic_store(&status[tile], (fagg << 32) | agg, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     uint32_t excl = 0, spins = 0;
-    int64_t j = (int64_t)tile - 1;
-    while (j >= 0) {
-        unsigned long long s = __hip_atomic_load(&status[j], __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-        uint32_t flag = (uint32_t)(s >> 32);
-        if (flag == 0) {
+    int64_t base = (int64_t)tile - 1;
+    while (true) {
+        const int64_t j = base - lane;
+        unsigned long long sv = fincl << 32;  // j < 0 reads as an inclusive prefix of 0
+        if (j >= 0)
+            sv = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long flag = sv >> 32;
+        const unsigned long long m_incl = __ballot(flag == fincl);
+        const unsigned long long m_wait = __ballot(flag < fagg);
+        const int first = m_incl ? __ffsll((long long)m_incl) - 1 : 63;
+        const unsigned long long need = first == 63 ? ~0ull : ((2ull << first) - 1ull);
+        if (m_wait & need) {
             if (++spins > kSpinLimit) {
-                atomicOr(err, 1u);
+                if (lane == 0) atomicOr(err, 1u);
                 break;
             }
             __builtin_amdgcn_s_sleep(1);
             continue;
         }
-        excl += (uint32_t)s;
-        if (flag == 2) break;
-        --j;
+        uint32_t v = (lane <= first) ? (uint32_t)sv : 0u;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        excl += v;
+        if (m_incl) break;
+        base -= 64;
     }
-    __hip_atomic_store(&status[tile], (2ull << 32) | (uint32_t)(excl + agg), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0)
+        __hip_atomic_store(&status[tile], (fincl << 32) | (uint32_t)(excl + agg), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     return excl;
 }
 
 // ---- fused frame kernel ------------------------------------------------------------------------
-// Camera owning global index gi (cameras sorted by offset); -1 when gi is outside every camera
-// (the reference's out-of-bounds read, canonicalised as mask 0).
+// Camera owning global index gi; -1 when gi is outside every camera (the reference's
+// out-of-bounds read, canonicalised as mask 0).  Branch-free over the (uniform) camera count so
+// that the neighbour loads of one ring issue back to back.
 __device__ __forceinline__ int find_cam(const CamDesc* cams, int ncams, int64_t gi) {
-    for (int j = ncams - 1; j >= 0; --j) {
-        if (gi >= cams[j].off) return (gi < cams[j].off + (int64_t)cams[j].n) ? j : -1;
-    }
-    return -1;
+    int j = -1;
+    for (int c = 0; c < ncams; ++c)
+        j = (gi >= cams[c].off && gi < cams[c].off + (int64_t)cams[c].n) ? c : j;
+    return j;
 }
 
-// mask + camera point of a neighbour read by check_at (filter_flying_pixels.glsl:63-80)
-__device__ __forceinline__ bool nb_point(const CamDesc* cams, int ncams, int k, int64_t gi,
-                                         float& x, float& y, float& z) {
-    int j = k;
-    if (gi < cams[k].off || gi >= cams[k].off + (int64_t)cams[k].n) j = find_cam(cams, ncams, gi);
-    if (j < 0) return false;
-    uint32_t local = (uint32_t)(gi - cams[j].off);
-    uint32_t d = cams[j].depth[local];
-    if (d == 0) return false;
-    cam_point(cams[j], local, d, x, y, z);
-    return true;
+struct Nb {
+    uint32_t d;
+    float xn, yn, scale;
+};
+
+// depth + ray factors of a neighbour read by check_at (filter_flying_pixels.glsl:63-80); the
+// three loads depend only on the index, so all neighbours of a ring are in flight together
+__device__ __forceinline__ Nb nb_load(const CamDesc* cams, int ncams, int k, int64_t gi) {
+    int j = (gi >= cams[k].off && gi < cams[k].off + (int64_t)cams[k].n) ? k
+                                                                          : find_cam(cams, ncams, gi);
+    Nb r;
+    r.d = 0;
+    r.xn = r.yn = 0.0f;
+    r.scale = 0.0f;
+    if (j >= 0) {
+        const CamDesc& c = cams[j];
+        const uint32_t local = (uint32_t)(gi - c.off);
+        const uint32_t v = local / c.W;
+        const uint32_t u = local - v * c.W;
+        r.d = c.depth[local];
+        r.xn = c.xn[u];
+        r.yn = c.yn[v];
+        r.scale = c.scale;
+    }
+    return r;
+}
+
+__device__ __forceinline__ void nb_point(const Nb& n, float& x, float& y, float& z) {
+    const float zz = (float)n.d * n.scale;
+    x = n.xn * zz;
+    y = n.yn * zz;
+    z = zz;
 }
 
 // check_at / check_at_rot45 (filter_flying_pixels.glsl:55-133) for ring i
@@ -114,11 +155,16 @@ __device__ __forceinline__ bool flying_check(const CamDesc* cams, int ncams, int
     } else {
         up = g - iw - i; down = g + iw + i; left = g + iw - i; right = g - iw + i;
     }
+    const Nb nu = nb_load(cams, ncams, k, up);
+    const Nb nd = nb_load(cams, ncams, k, down);
+    const Nb nl = nb_load(cams, ncams, k, left);
+    const Nb nr = nb_load(cams, ncams, k, right);
+    if (nu.d == 0 || nd.d == 0 || nl.d == 0 || nr.d == 0) return false;
     float ux, uy, uz, dx_, dy_, dz_, lx, ly, lz, rx, ry, rz;
-    if (!nb_point(cams, ncams, k, up, ux, uy, uz)) return false;
-    if (!nb_point(cams, ncams, k, down, dx_, dy_, dz_)) return false;
-    if (!nb_point(cams, ncams, k, left, lx, ly, lz)) return false;
-    if (!nb_point(cams, ncams, k, right, rx, ry, rz)) return false;
+    nb_point(nu, ux, uy, uz);
+    nb_point(nd, dx_, dy_, dz_);
+    nb_point(nl, lx, ly, lz);
+    nb_point(nr, rx, ry, rz);
     // dx = right - left, dy = down - up, normal = normalize(cross(dy, dx))
     float ax = dx_ - ux, ay = dy_ - uy, az = dz_ - uz;  // dy
     float bx = rx - lx, by = ry - ly, bz = rz - lz;      // dx
@@ -214,87 +260,94 @@ __global__ __launch_bounds__(kFrameThreads) void k_frame(FrameArgs a) {
     __shared__ CamDesc s_cams[kMaxCams];
     __shared__ uint32_t s_wave[4];
     __shared__ uint32_t s_tile, s_excl;
+    __shared__ uint32_t s_hist[4 * 256];
     {
         const uint32_t words = (uint32_t)a.ncams * (uint32_t)(sizeof(CamDesc) / 4);
         const uint32_t* src = reinterpret_cast<const uint32_t*>(a.cams);
         uint32_t* dst = reinterpret_cast<uint32_t*>(s_cams);
         for (uint32_t w = threadIdx.x; w < words; w += kFrameThreads) dst[w] = src[w];
     }
-    if (threadIdx.x == 0) s_tile = atomicAdd(a.tile_ctr, 1u);
+    if (a.key_hist)
+        for (uint32_t i = threadIdx.x; i < a.npasses * 256; i += kFrameThreads) s_hist[i] = 0;
+    if (threadIdx.x == 0) s_tile = (uint32_t)(atomicAdd(a.tile_ctr, 1ull) - a.tile_base);
     __syncthreads();
     const uint32_t tile = s_tile;
 
-    ItemOut it[kFramePerThread];
-    uint32_t item0;
+    ItemOut it;
+    it.bits = 0;
+    uint32_t item;
+    bool in_range;
     if (tile < a.depth_tiles) {
-        item0 = tile * kFrameTile + threadIdx.x * kFramePerThread;
-#pragma unroll
-        for (int j = 0; j < kFramePerThread; ++j) {
-            const uint32_t g = item0 + j;
-            if (g < a.depth_total) {
-                const int k = find_cam(s_cams, a.ncams, (int64_t)g);
-                const uint32_t d = s_cams[k].depth[(uint32_t)((int64_t)g - s_cams[k].off)];
-                it[j] = eval_depth(a, s_cams, g, d);
-            } else {
-                it[j].bits = 0;
-            }
+        item = tile * kFrameTile + threadIdx.x;
+        in_range = item < a.depth_total;
+        if (in_range) {
+            const int k = find_cam(s_cams, a.ncams, (int64_t)item);
+            const uint32_t d = s_cams[k].depth[(uint32_t)((int64_t)item - s_cams[k].off)];
+            it = eval_depth(a, s_cams, item, d);
         }
     } else {
-        const uint32_t base = (tile - a.depth_tiles) * kFrameTile + threadIdx.x * kFramePerThread;
-        item0 = a.depth_total + base;
-#pragma unroll
-        for (int j = 0; j < kFramePerThread; ++j) {
-            const uint32_t i = base + j;
-            if (i < a.sel_count) it[j] = eval_sel(a, i);
-            else it[j].bits = 0;
-        }
+        const uint32_t i = (tile - a.depth_tiles) * kFrameTile + threadIdx.x;
+        item = a.depth_total + i;
+        in_range = i < a.sel_count;
+        if (in_range) it = eval_sel(a, i);
     }
 
-    uint32_t cnt = 0;
-#pragma unroll
-    for (int j = 0; j < kFramePerThread; ++j) cnt += (it[j].bits & 4) ? 1u : 0u;
+    const uint32_t valid = (it.bits & 4) ? 1u : 0u;
     uint32_t total;
-    const uint32_t excl_thread = block_exclusive_scan(cnt, total, s_wave);
-    if (threadIdx.x == 0) {
-        uint32_t ex = lookback64(a.status, tile, total, a.err);
-        s_excl = ex;
-        if (tile == a.total_tiles - 1) *a.out_count = ex + total;
+    const uint32_t excl_thread = block_exclusive_scan(valid, total, s_wave);
+    if (threadIdx.x < 64) {
+        const uint32_t ex = lookback_wave(a.status, tile, total, a.epoch, a.err);
+        if (threadIdx.x == 0) {
+            s_excl = ex;
+            if (tile == a.total_tiles - 1) *a.out_count = ex + total;
+        }
     }
     __syncthreads();
-    uint32_t pos = s_excl + excl_thread;
-#pragma unroll
-    for (int j = 0; j < kFramePerThread; ++j) {
-        if (a.dbg) {
-            const uint32_t idx = item0 + j;
-            if ((tile < a.depth_tiles && idx < a.depth_total) ||
-                (tile >= a.depth_tiles && idx - a.depth_total < a.sel_count))
-                a.dbg[idx] = (uint8_t)it[j].bits;
-        }
-        if (it[j].bits & 4) {
-            a.out_pts[pos] = it[j].w;
-            if (a.do_voxel) {
-                const uint32_t key = voxel_key(it[j].w.x, it[j].w.y, it[j].w.z, a.vlo, a.vcs,
-                                               a.gmax, a.gs);
-                a.out_coords[pos] = key;
-                if (a.occ_mode == 1) {
-                    const uint8_t h = a.occ[key];
-                    if (!(h & 0x80u)) a.occ[key] = (uint8_t)(h | 0x80u);
-                } else if (a.occ_mode == 2) {
-                    a.occ[key] = 1;
-                }
+    if (a.dbg && in_range) a.dbg[item] = (uint8_t)it.bits;
+    if (valid) {
+        const uint32_t pos = s_excl + excl_thread;
+        a.out_pts[pos] = it.w;
+        if (a.do_voxel) {
+            const uint32_t key = voxel_key(it.w.x, it.w.y, it.w.z, a.vlo, a.vcs, a.gmax, a.gs);
+            a.out_coords[pos] = key;
+            if (a.occ_mode == 1) {
+                const uint8_t h = a.occ[key];
+                if (!(h & 0x80u)) a.occ[key] = (uint8_t)(h | 0x80u);
+            } else if (a.occ_mode == 2) {
+                a.occ[key] = 1;
             }
-            ++pos;
+            if (a.key_hist)
+                for (uint32_t p = 0; p < a.npasses; ++p)
+                    atomicAdd(&s_hist[p * 256 + ((key >> (8 * p)) & 0xFFu)], 1u);
         }
+    }
+    if (a.key_hist) {
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < a.npasses * 256; i += kFrameThreads)
+            if (s_hist[i]) atomicAdd(&a.key_hist[i], s_hist[i]);
     }
 }
 
 hipError_t launch_frame(const FrameArgs& a, hipStream_t s) {
     if (a.total_tiles == 0) return hipMemsetAsync(a.out_count, 0, 4, s);
-    hipError_t e = hipMemsetAsync(a.status, 0, (size_t)a.total_tiles * 8, s);
-    if (e != hipSuccess) return e;
-    e = hipMemsetAsync(a.tile_ctr, 0, 4, s);
-    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_frame, dim3(a.total_tiles), dim3(kFrameThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+// per-camera ray factors (sh/convert_depthmap_to_points.glsl:68-69), one f32 division each
+__global__ __launch_bounds__(256) void k_tables(uint32_t W, uint32_t H, float fx, float fy,
+                                                float cx, float cy, float* __restrict__ xn,
+                                                float* __restrict__ yn) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < W) xn[i] = ((float)i - cx) / fx;
+    if (i < H) yn[i] = ((float)i - cy) / fy;
+}
+
+hipError_t launch_tables(uint32_t W, uint32_t H, float fx, float fy, float cx, float cy, float* xn,
+                         float* yn, hipStream_t s) {
+    const uint32_t n = W > H ? W : H;
+    hipLaunchKernelGGL(k_tables, dim3((n + 255) / 256), dim3(256), 0, s, W, H, fx, fy, cx, cy, xn,
+                       yn);
     return hipGetLastError();
 }
 
@@ -483,22 +536,38 @@ __global__ __launch_bounds__(256) void k_sort_hist(const uint32_t* __restrict__ 
         if (s_h[i]) atomicAdd(&hist[i], s_h[i]);
 }
 
-// Stable scatter of one 8-bit digit.  Tile = 4096 keys: wave w owns keys [w*1024, w*1024+1024)
-// of the tile in slot-major order (slot j, lane l -> w*1024 + j*64 + l), so ranking the slots in
-// order with wave ballots keeps the sort stable.  Per-digit tile offsets come from a decoupled
-// look-back over 32-bit {2-bit flag, 30-bit count} granules.
+// Exclusive scan of the 256-entry global digit histogram (4 waves x 64 digits), thread d gets
+// the base of digit d.
+__device__ __forceinline__ uint32_t digit_base(const uint32_t* ghist, uint32_t* s_wave) {
+    const uint32_t d = threadIdx.x;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t v = ghist[d];
+    uint32_t total;
+    (void)lane;
+    (void)wid;
+    return block_exclusive_scan(v, total, s_wave);
+}
+
+// Stable scatter of one 8-bit digit.  Tile = 256 threads x PT keys: wave w owns keys
+// [w*64*PT, (w+1)*64*PT) of the tile in slot-major order (slot j, lane l -> w*64*PT + j*64 + l),
+// so ranking the slots in order with wave ballots keeps the sort stable.  Per-digit tile offsets
+// come from a decoupled look-back over epoch-tagged {flag, count} granules.
+template <int PT>
 __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
     uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, const uint32_t* __restrict__ count,
-    const uint32_t* __restrict__ ghist, uint32_t* status, uint32_t* tile_ctr, uint32_t* err,
+    const uint32_t* __restrict__ ghist, unsigned long long* status,
+    unsigned long long* tile_ctr, unsigned long long tile_base, uint32_t epoch, uint32_t* err,
     uint32_t shift, uint32_t dbits) {
+    constexpr int kTile = kSortThreads * PT;
     __shared__ uint32_t s_cnt[4][256];
     __shared__ uint32_t s_base[256];
     __shared__ uint32_t s_excl[256];
+    __shared__ uint32_t s_wave[4];
     __shared__ uint32_t s_tile;
     const uint32_t n = *count;
-    const uint32_t ntiles = (n + kSortTile - 1) / kSortTile;
-    if (threadIdx.x == 0) s_tile = atomicAdd(tile_ctr, 1u);
+    const uint32_t ntiles = (n + kTile - 1) / kTile;
+    if (threadIdx.x == 0) s_tile = (uint32_t)(atomicAdd(tile_ctr, 1ull) - tile_base);
     for (uint32_t i = threadIdx.x; i < 4 * 256; i += kSortThreads) (&s_cnt[0][0])[i] = 0;
     __syncthreads();
     const uint32_t tile = s_tile;
@@ -506,17 +575,17 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const unsigned long long ltm = lanemask_lt();
 
-    uint32_t key[kSortPerThread], val[kSortPerThread], rank[kSortPerThread];
-    const uint32_t wbase = tile * kSortTile + w * 1024;
+    uint32_t key[PT], val[PT], rank[PT];
+    const uint32_t wbase = tile * kTile + w * 64 * PT;
 #pragma unroll
-    for (int j = 0; j < kSortPerThread; ++j) {
+    for (int j = 0; j < PT; ++j) {
         const uint32_t idx = wbase + j * 64 + lane;
         const bool ok = idx < n;
         key[j] = ok ? kin[idx] : 0xFFFFFFFFu;
         val[j] = ok ? (vin ? vin[idx] : idx) : 0u;
     }
 #pragma unroll
-    for (int j = 0; j < kSortPerThread; ++j) {
+    for (int j = 0; j < PT; ++j) {
         const uint32_t idx = wbase + j * 64 + lane;
         const bool ok = idx < n;
         const uint32_t d = (key[j] >> shift) & 0xFFu;
@@ -535,88 +604,91 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
         __builtin_amdgcn_wave_barrier();
     }
     __syncthreads();
-    // per digit: tile total, per-wave offsets, global base, look-back
-    {
-        const uint32_t d = threadIdx.x;
-        uint32_t tot = 0;
+    const uint32_t d = threadIdx.x;
+    uint32_t tot = 0;
 #pragma unroll
-        for (int ww = 0; ww < 4; ++ww) {
-            const uint32_t c = s_cnt[ww][d];
-            s_cnt[ww][d] = tot;
-            tot += c;
-        }
-        // global exclusive base over digits
-        uint32_t gh = ghist[d];
-        s_base[d] = gh;
-        __syncthreads();
-        // simple 256-wide exclusive scan in LDS (Hillis-Steele on s_base)
-        for (uint32_t o = 1; o < 256; o <<= 1) {
-            uint32_t add = d >= o ? s_base[d - o] : 0u;
-            __syncthreads();
-            s_base[d] += add;
-            __syncthreads();
-        }
-        const uint32_t incl = s_base[d];
-        __syncthreads();
-        s_base[d] = incl - gh;
-        // look-back for this digit
-        uint32_t* st = status + (size_t)tile * 256 + d;
+    for (int ww = 0; ww < 4; ++ww) {
+        const uint32_t c = s_cnt[ww][d];
+        s_cnt[ww][d] = tot;
+        tot += c;
+    }
+    s_base[d] = digit_base(ghist, s_wave);
+    // look-back for digit d
+    {
+        const unsigned long long fagg = 2ull * epoch, fincl = fagg + 1ull;
+        unsigned long long* st = status + (size_t)tile * 256 + d;
         uint32_t excl = 0;
         if (tile == 0) {
-            __hip_atomic_store(st, (2u << 30) | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(st, (fincl << 32) | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
-            __hip_atomic_store(st, (1u << 30) | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(st, (fagg << 32) | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // windowed: 4 predecessors per round trip
             int64_t j = (int64_t)tile - 1;
             uint32_t spins = 0;
             while (j >= 0) {
-                const uint32_t sv = __hip_atomic_load(status + (size_t)j * 256 + d, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT);
-                const uint32_t flag = sv >> 30;
-                if (flag == 0) {
+                unsigned long long sv[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    sv[q] = (j - q >= 0)
+                                ? __hip_atomic_load(status + (size_t)(j - q) * 256 + d,
+                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                : (fincl << 32);
+                int q = 0;
+                bool done = false;
+                for (; q < 4; ++q) {
+                    const unsigned long long flag = sv[q] >> 32;
+                    if (flag < fagg) break;
+                    excl += (uint32_t)sv[q];
+                    if (flag == fincl) {
+                        done = true;
+                        break;
+                    }
+                }
+                if (done) break;
+                j -= q;
+                if (q < 4) {
                     if (++spins > kSpinLimit) {
                         atomicOr(err, 2u);
                         break;
                     }
                     __builtin_amdgcn_s_sleep(1);
-                    continue;
                 }
-                excl += sv & 0x3FFFFFFFu;
-                if (flag == 2) break;
-                --j;
             }
-            __hip_atomic_store(st, (2u << 30) | (excl + tot), __ATOMIC_RELAXED,
+            __hip_atomic_store(st, (fincl << 32) | (excl + tot), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
         s_excl[d] = excl;
     }
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < kSortPerThread; ++j) {
+    for (int j = 0; j < PT; ++j) {
         const uint32_t idx = wbase + j * 64 + lane;
         if (idx < n) {
-            const uint32_t d = (key[j] >> shift) & 0xFFu;
-            const uint32_t pos = s_base[d] + s_excl[d] + s_cnt[w][d] + rank[j];
+            const uint32_t dd = (key[j] >> shift) & 0xFFu;
+            const uint32_t pos = s_base[dd] + s_excl[dd] + s_cnt[w][dd] + rank[j];
             kout[pos] = key[j];
             vout[pos] = val[j];
         }
     }
 }
 
-// Group boundaries, group ids (look-back scan) and the per-voxel sequential mean in stable
-// order (averageGridCells, inc/voxelize.h:9-48) or the voxel lower corner (occupiedGridCells,
-// :50-71 with GridMeta::worldCoord, inc/grid_meta.h:45-100).
-__global__ __launch_bounds__(kGroupThreads) void k_group(
-    const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
-    const uint32_t* __restrict__ count, const float4* __restrict__ pts, float4* __restrict__ out,
-    uint32_t* __restrict__ out_count, unsigned long long* status, uint32_t* tile_ctr,
-    uint32_t* err, int average, VoxelParams vp) {
+// Group boundaries of the sorted keys and group ids (look-back scan): gstart[g] = first sorted
+// position of voxel group g (RadixGrouper::makeGroups, inc/radix_grouper.h:35-64).  Also clears
+// the digit histogram for the next voxelize (its last reader was the final sort pass).
+__global__ __launch_bounds__(kGroupThreads) void k_group_scan(
+    const uint32_t* __restrict__ keys, const uint32_t* __restrict__ count,
+    uint32_t* __restrict__ gstart, uint32_t* __restrict__ out_count, unsigned long long* status,
+    unsigned long long* tile_ctr, unsigned long long tile_base, uint32_t epoch, uint32_t* err,
+    uint32_t* hist) {
     __shared__ uint32_t s_wave[4];
     __shared__ uint32_t s_tile, s_excl;
     const uint32_t n = *count;
     const uint32_t ntiles = (n + kGroupTile - 1) / kGroupTile;
-    if (threadIdx.x == 0) s_tile = atomicAdd(tile_ctr, 1u);
+    if (threadIdx.x == 0) s_tile = (uint32_t)(atomicAdd(tile_ctr, 1ull) - tile_base);
     __syncthreads();
     const uint32_t tile = s_tile;
+    if (tile == 0)
+        for (uint32_t i = threadIdx.x; i < 4 * 256; i += kGroupThreads) hist[i] = 0;
     if (tile >= ntiles) {
         if (tile == 0 && threadIdx.x == 0) *out_count = 0;  // n == 0
         return;
@@ -633,51 +705,99 @@ __global__ __launch_bounds__(kGroupThreads) void k_group(
     }
     uint32_t total;
     const uint32_t excl_thread = block_exclusive_scan(cnt, total, s_wave);
-    if (threadIdx.x == 0) {
-        const uint32_t ex = lookback64(status, tile, total, err);
-        s_excl = ex;
-        if (tile == ntiles - 1) *out_count = ex + total;
+    if (threadIdx.x < 64) {
+        const uint32_t ex = lookback_wave(status, tile, total, epoch, err);
+        if (threadIdx.x == 0) {
+            s_excl = ex;
+            if (tile == ntiles - 1) *out_count = ex + total;
+        }
     }
     __syncthreads();
     uint32_t g = s_excl + excl_thread;
 #pragma unroll
-    for (int j = 0; j < kGroupPerThread; ++j) {
-        if (!(flags & (1u << j))) continue;
-        const uint32_t i = i0 + j;
-        const uint32_t key = keys[i];
-        float4 o;
-        if (average) {
-            float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
-            uint32_t c = 0;
-            for (uint32_t k = i; k < n && keys[k] == key; ++k) {
-                const float4 p = pts[vals[k]];
-                sx = sx + p.x;
-                sy = sy + p.y;
-                sz = sz + p.z;
-                sw = sw + p.w;
-                ++c;
-            }
-            const float fc = (float)c;
-            o = make_float4(sx / fc, sy / fc, sz / fc, sw);
-        } else {
-            uint32_t kk = key;
-            const uint32_t steps[3] = {1u, vp.gs[0], vp.gs[0] * vp.gs[1]};
-            uint32_t gc[3];
+    for (int j = 0; j < kGroupPerThread; ++j)
+        if (flags & (1u << j)) gstart[g++] = i0 + j;
+}
+
+// Per-voxel output.  average: the sequential f32 sum in stable (index) order, x/y/z divided by
+// the count, w the un-divided sum (averageGridCells, inc/voxelize.h:9-48).  One wave per group:
+// the wave gathers chunks of 256 points into LDS (next chunk prefetched into registers while
+// the current one is summed); lanes 0..3 each run one component's dependent add chain.
+// !average: the voxel's lower corner (occupiedGridCells + GridMeta::worldCoord).
+__global__ __launch_bounds__(kGroupThreads) void k_group_sum(
+    const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+    const uint32_t* __restrict__ count, const uint32_t* __restrict__ gstart,
+    const uint32_t* __restrict__ gcount, const float4* __restrict__ pts, float* __restrict__ out,
+    int average, VoxelParams vp) {
+    __shared__ float4 s_buf[4][kSumChunk];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t n = *count;
+    const uint32_t G = *gcount;
+    const uint32_t nwaves = gridDim.x * 4;
+    for (uint32_t g = blockIdx.x * 4 + wid; g < G; g += nwaves) {
+        const uint32_t s = gstart[g];
+        const uint32_t e = (g + 1 < G) ? gstart[g + 1] : n;
+        if (!average) {
+            if (lane < 3) {
+                const uint32_t key = keys[s];
+                const uint32_t steps[3] = {1u, vp.gs[0], vp.gs[0] * vp.gs[1]};
+                uint32_t kk = key, gc[3];
 #pragma unroll
-            for (int ax = 0; ax < 3; ++ax) {
-                gc[ax] = (kk / steps[ax]) % vp.gs[ax];
-                kk -= gc[ax] * steps[ax];
+                for (int ax = 0; ax < 3; ++ax) {
+                    gc[ax] = (kk / steps[ax]) % vp.gs[ax];
+                    kk -= gc[ax] * steps[ax];
+                }
+                out[4 * (size_t)g + lane] = (float)gc[lane] * vp.vcs[lane] + vp.vlo[lane];
+            } else if (lane == 3) {
+                out[4 * (size_t)g + 3] = 0.0f;
             }
-            o = make_float4((float)gc[0] * vp.vcs[0] + vp.vlo[0], (float)gc[1] * vp.vcs[1] + vp.vlo[1],
-                            (float)gc[2] * vp.vcs[2] + vp.vlo[2], 0.0f);
+            continue;
         }
-        out[g] = o;
-        ++g;
+        float acc = 0.0f;
+        float4 r[kSumChunk / 64];
+#pragma unroll
+        for (int q = 0; q < kSumChunk / 64; ++q) {
+            const uint32_t k = s + q * 64 + lane;
+            r[q] = k < e ? pts[vals[k]] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        for (uint32_t c = s; c < e; c += kSumChunk) {
+#pragma unroll
+            for (int q = 0; q < kSumChunk / 64; ++q) s_buf[wid][q * 64 + lane] = r[q];
+            const uint32_t cn = c + kSumChunk;
+#pragma unroll
+            for (int q = 0; q < kSumChunk / 64; ++q) {
+                const uint32_t k = cn + q * 64 + lane;
+                r[q] = k < e ? pts[vals[k]] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (lane < 4) {
+                const float* comp = reinterpret_cast<const float*>(&s_buf[wid][0]) + lane;
+                const uint32_t m = (e - c) < (uint32_t)kSumChunk ? (e - c) : (uint32_t)kSumChunk;
+                uint32_t j = 0;
+                for (; j + 16 <= m; j += 16) {
+                    float t[16];
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) t[q] = comp[4 * (j + q)];
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) acc = acc + t[q];
+                }
+                for (; j < m; ++j) acc = acc + comp[4 * j];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        if (lane < 4) {
+            const float fc = (float)(e - s);
+            out[4 * (size_t)g + lane] = lane < 3 ? acc / fc : acc;
+        }
     }
 }
 
 size_t voxelize_status_words(uint32_t nmax) {
-    return (size_t)((nmax + kSortTile - 1) / kSortTile + 1) * 256;
+    return (size_t)((nmax + kSortThreads * 4 - 1) / (kSortThreads * 4) + 1) * 256;
 }
 size_t voxelize_group_tiles(uint32_t nmax) {
     return (size_t)((nmax + kGroupTile - 1) / kGroupTile + 1);
@@ -685,15 +805,17 @@ size_t voxelize_group_tiles(uint32_t nmax) {
 
 hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s) {
     const uint32_t npasses = a.key_bits == 0 ? 1u : (a.key_bits + 7) / 8;
-    const size_t swords = voxelize_status_words(a.nmax);
-    const size_t gtiles = voxelize_group_tiles(a.nmax);
+    // small N: 1024 keys per sort tile (more blocks in flight); large N: 4096
+    const bool small = a.nmax <= (1u << 21);
+    const uint32_t tile = small ? kSortThreads * 4 : kSortThreads * 16;
+    const uint32_t sort_tiles = (a.nmax + tile - 1) / tile;
     hipError_t e;
-    if ((e = hipMemsetAsync(a.hist, 0, 4 * 256 * 4, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(a.ctrs, 0, 8 * 4, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_sort_hist, dim3(grid_blocks(a.nmax, 256 * 8)), dim3(256), 0, s, a.keys,
-                       a.count, npasses, a.hist);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    const uint32_t sort_tiles = (a.nmax + kSortTile - 1) / kSortTile;
+    if (!a.hist_ready) {
+        unsigned hb = grid_blocks(a.nmax, 256 * 16);
+        if (hb > 64) hb = 64;
+        hipLaunchKernelGGL(k_sort_hist, dim3(hb), dim3(256), 0, s, a.keys, a.count, npasses, a.hist);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     const uint32_t* kin = a.keys;
     const uint32_t* vin = nullptr;
     uint32_t* kbuf[2] = {a.keys_a, a.keys_b};
@@ -701,21 +823,38 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s) {
     for (uint32_t p = 0; p < npasses; ++p) {
         const uint32_t remaining = a.key_bits > 8 * p ? a.key_bits - 8 * p : 0u;
         const uint32_t dbits = remaining >= 8 ? 8u : (remaining ? remaining : 1u);
-        if ((e = hipMemsetAsync(a.status, 0, swords * 4, s)) != hipSuccess) return e;
+        const uint32_t ep = ++(*a.epoch);
         if (sort_tiles) {
-            hipLaunchKernelGGL(k_sort_pass, dim3(sort_tiles), dim3(kSortThreads), 0, s, kin, vin,
-                               kbuf[p & 1], vbuf[p & 1], a.count, a.hist + 256 * p, a.status,
-                               a.ctrs + p, a.err, 8 * p, dbits);
+            if (small)
+                hipLaunchKernelGGL(k_sort_pass<4>, dim3(sort_tiles), dim3(kSortThreads), 0, s, kin,
+                                   vin, kbuf[p & 1], vbuf[p & 1], a.count, a.hist + 256 * p,
+                                   a.status, a.ctrs + kCtrSort0 + p, a.ctr_base[kCtrSort0 + p],
+                                   ep, a.err, 8 * p, dbits);
+            else
+                hipLaunchKernelGGL(k_sort_pass<16>, dim3(sort_tiles), dim3(kSortThreads), 0, s, kin,
+                                   vin, kbuf[p & 1], vbuf[p & 1], a.count, a.hist + 256 * p,
+                                   a.status, a.ctrs + kCtrSort0 + p, a.ctr_base[kCtrSort0 + p],
+                                   ep, a.err, 8 * p, dbits);
             if ((e = hipGetLastError()) != hipSuccess) return e;
+            a.ctr_base[kCtrSort0 + p] += sort_tiles;
         }
         kin = kbuf[p & 1];
         vin = vbuf[p & 1];
     }
-    if ((e = hipMemsetAsync(a.gstatus, 0, gtiles * 8, s)) != hipSuccess) return e;
     const uint32_t group_tiles = (a.nmax + kGroupTile - 1) / kGroupTile;
-    hipLaunchKernelGGL(k_group, dim3(group_tiles ? group_tiles : 1), dim3(kGroupThreads), 0, s,
-                       kin, vin, a.count, a.pts, a.out, a.out_count, a.gstatus, a.ctrs + 4, a.err,
-                       a.average, a.vp);
+    const uint32_t gblocks = group_tiles ? group_tiles : 1;
+    const uint32_t ep = ++(*a.epoch);
+    hipLaunchKernelGGL(k_group_scan, dim3(gblocks), dim3(kGroupThreads), 0, s, kin, a.count,
+                       a.gstart, a.out_count, a.gstatus, a.ctrs + kCtrGroup, a.ctr_base[kCtrGroup],
+                       ep, a.err, a.hist);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    a.ctr_base[kCtrGroup] += gblocks;
+    uint32_t sblocks = (a.nmax + 255) / 256;
+    if (sblocks > 1024) sblocks = 1024;
+    if (sblocks == 0) sblocks = 1;
+    hipLaunchKernelGGL(k_group_sum, dim3(sblocks), dim3(kGroupThreads), 0, s, kin, vin, a.count,
+                       a.gstart, a.out_count, a.pts, reinterpret_cast<float*>(a.out), a.average,
+                       a.vp);
     return hipGetLastError();
 }
 

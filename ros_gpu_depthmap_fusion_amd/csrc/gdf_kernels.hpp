@@ -10,8 +10,12 @@ struct VoxelParams {
     uint32_t gs[3];
 };
 
+// per-camera ray factors xn[u] = (u - cx)/fx, yn[v] = (v - cy)/fy
+hipError_t launch_tables(uint32_t W, uint32_t H, float fx, float fy, float cx, float cy, float* xn,
+                         float* yn, hipStream_t s);
+
 // fused depth + rollbuffer compaction (convert, flying, crop, transform_indirect, apply,
-// optional voxel keys + occupancy marks); memsets its look-back state itself
+// optional voxel keys + occupancy marks); needs no memset (epoch-tagged look-back, tickets)
 hipError_t launch_frame(const FrameArgs& a, hipStream_t s);
 
 // filter_point_sequence + insert into the rollbuffer ring (w = mask)
@@ -42,13 +46,17 @@ struct VoxelizeArgs {
     uint32_t nmax;              // capacity bound for launch sizing
     uint32_t key_bits;          // bit width of (num_cells - 1)
     int average;
+    int hist_ready;             // the key histogram was already accumulated (fused k_frame)
     VoxelParams vp;
     // workspace
     uint32_t *keys_a, *keys_b, *vals_a, *vals_b;
-    uint32_t* hist;             // [4*256]
-    uint32_t* status;           // [ntiles_max*256]
-    unsigned long long* gstatus;  // [group tiles]
-    uint32_t* ctrs;             // [8]
+    uint32_t* hist;                 // [4*256] zero on entry, left zero on exit
+    unsigned long long* status;     // [sort tiles * 256] epoch granules
+    unsigned long long* gstatus;    // [group tiles] epoch granules
+    uint32_t* gstart;               // [nmax] first sorted position of each group
+    unsigned long long* ctrs;       // [kCtrSlots] tile tickets
+    unsigned long long* ctr_base;   // host copy of the ticket bases (updated)
+    uint32_t* epoch;                // host epoch counter (advanced per look-back launch)
     uint32_t* err;
     // outputs
     float4* out;

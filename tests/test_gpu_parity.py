@@ -226,7 +226,7 @@ def test_voxelize_pinned_to_reference_radix_golden(Engine):
         pts = np.stack([x, y, np.full_like(x, 0.5)], -1)
         gpu = Engine()
         gpu.clear()
-        gpu.addPointSequence(pts, 5, 0, EYE)
+        gpu.addPointSequence(pts, 5000, 0, EYE)
         gpu.processFrame(p, T_world_move=EYE, T_crop_move=EYE)
         assert gpu.point_count() == len(keys)
         np.testing.assert_array_equal(gpu.downloadVoxelCoords(), keys)
