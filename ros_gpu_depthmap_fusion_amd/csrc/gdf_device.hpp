@@ -12,8 +12,9 @@
 namespace gdf {
 
 constexpr int kMaxCams = 16;          // GDF_MAX_CAMERAS
-constexpr int kFrameThreads = 256;    // compaction block: 4 waves, one item per thread
-constexpr int kFrameTile = kFrameThreads;
+constexpr int kFrameThreads = 256;    // k_mask block: 4 waves, one item per thread
+constexpr int kFrameTile = kFrameThreads;  // items per count tile
+constexpr int kEmitThreads = 1024;    // k_emit block: 4 count tiles, fewer histogram flushes
 constexpr int kSortThreads = 256;
 constexpr int kGroupThreads = 256;
 constexpr int kGroupPerThread = 8;
@@ -82,11 +83,10 @@ struct FrameArgs {
     uint32_t* out_count;
     uint32_t* out_coords;
     uint8_t* dbg;               // optional per-item stage bits
-    // decoupled look-back (epoch-tagged granules, no memset) + tile tickets
-    unsigned long long* status;
-    unsigned long long* tile_ctr;
-    unsigned long long tile_base;
-    uint32_t epoch;
+    // reduce-then-scan compaction state
+    unsigned long long* valid_bits;  // [tiles * 16] one ballot per wave
+    uint32_t* tile_counts;           // [tiles]
+    uint32_t* tile_offsets;          // [tiles]
     uint32_t* err;
 };
 static_assert(sizeof(FrameArgs) <= 4096, "kernel arguments are limited to 4 KiB");

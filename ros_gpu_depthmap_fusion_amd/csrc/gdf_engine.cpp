@@ -214,7 +214,7 @@ struct gdf_engine {
     bool khist_pending = false;     // accumulated by a fused k_frame, not yet consumed
 
     // compaction outputs
-    DevBuf d_pts, d_coords, d_status, d_dbg;
+    DevBuf d_pts, d_coords, d_status, d_tcounts, d_toffsets, d_dbg;
     DevBuf d_misc;
     uint32_t* h_misc = nullptr;  // pinned
     bool compacted = false, coords_valid = false, marks_set = false;
@@ -233,7 +233,7 @@ struct gdf_engine {
     bool invoked_once = false;
 
     // voxelize
-    DevBuf d_ka, d_kb, d_va, d_vb, d_sstatus, d_gstatus, d_gstart, d_vox;
+    DevBuf d_ka, d_kb, d_va, d_vb, d_sstatus, d_sgstatus, d_gstatus, d_ggstatus, d_gstart, d_vox;
     bool vox_valid = false;
 
     bool debug = false;
@@ -669,14 +669,15 @@ void run_frame(gdf_engine* e, bool fused_voxel) {
         a.dbg = e->d_dbg.as<uint8_t>();
         e->dbg_count = e->n_total;
     }
-    e->d_status.ensure_zero((size_t)std::max<uint32_t>(a.total_tiles, 1) * 8, e->s());
-    a.status = e->d_status.as<unsigned long long>();
-    a.tile_ctr = e->d_ctrs.as<unsigned long long>() + kCtrFrame;
-    a.tile_base = e->ctr_base[kCtrFrame];
-    a.epoch = ++e->epoch;
+    const size_t tiles = std::max<uint32_t>(a.total_tiles, 1);
+    e->d_status.ensure(tiles * (kFrameTile / 64) * 8);
+    e->d_tcounts.ensure(tiles * 4);
+    e->d_toffsets.ensure(tiles * 4);
+    a.valid_bits = e->d_status.as<unsigned long long>();
+    a.tile_counts = e->d_tcounts.as<uint32_t>();
+    a.tile_offsets = e->d_toffsets.as<uint32_t>();
     a.err = e->d_misc.as<uint32_t>() + kErr;
     e->timed(GDF_KERNEL_FRAME, [&] { HIPCHK(launch_frame(a, e->s())); });
-    e->ctr_base[kCtrFrame] += a.total_tiles;
     e->khist_pending = fused_voxel;
     e->compacted = true;
     e->coords_valid = fused_voxel;
@@ -704,7 +705,9 @@ void voxelize(gdf_engine* e, int average) {  // fusion.cpp:1743-1756
     e->d_vb.ensure((size_t)nmax * 4);
     e->d_gstart.ensure((size_t)nmax * 4);
     e->d_sstatus.ensure_zero(voxelize_status_words(nmax) * 8, e->s());
+    e->d_sgstatus.ensure_zero((voxelize_status_words(nmax) / 16 + 256) * 8, e->s());
     e->d_gstatus.ensure_zero(voxelize_group_tiles(nmax) * 8, e->s());
+    e->d_ggstatus.ensure_zero((voxelize_group_tiles(nmax) / 64 + 2) * 8, e->s());
     e->d_vox.ensure((size_t)nmax * 16);
     VoxelizeArgs v{};
     v.keys = e->d_coords.as<uint32_t>();
@@ -721,7 +724,9 @@ void voxelize(gdf_engine* e, int average) {  // fusion.cpp:1743-1756
     v.vals_b = e->d_vb.as<uint32_t>();
     v.hist = e->d_khist.as<uint32_t>();
     v.status = e->d_sstatus.as<unsigned long long>();
+    v.sgstatus = e->d_sgstatus.as<unsigned long long>();
     v.gstatus = e->d_gstatus.as<unsigned long long>();
+    v.ggstatus = e->d_ggstatus.as<unsigned long long>();
     v.gstart = e->d_gstart.as<uint32_t>();
     v.ctrs = e->d_ctrs.as<unsigned long long>();
     v.ctr_base = e->ctr_base;

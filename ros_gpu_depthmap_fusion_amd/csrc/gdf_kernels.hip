@@ -1,9 +1,9 @@
 // gdf_kernels.hip — gfx950 (CDNA4, wave64) kernels of the depth-fusion hot path.
 //
 // Reference shaders restated here (paths relative to the reference root, shader/):
-//   k_frame            convert_depthmap_to_points.glsl:83-120, filter_flying_pixels.glsl:43-165,
+//   k_mask/k_emit      convert_depthmap_to_points.glsl:83-120, filter_flying_pixels.glsl:43-165,
 //                      transform_points_indirect.glsl:50-69, crop_points.glsl:38-67,
-//                      apply_point_mask.glsl:42-55 (ordered: decoupled look-back scan),
+//                      apply_point_mask.glsl:42-55 (ordered: reduce-then-scan, k_scan_counts),
 //                      compute_voxel_coords.glsl:34-55, voxel_grid_occupancy_of_points.glsl:30-40
 //   k_ps_filter_insert filter_point_sequence.glsl:78-122 + transfer_data.glsl (rollbuffer insert)
 //   k_grid_*           zero_uints / decrement_uints.glsl:31-51 / max_with_uints_times_scalar.glsl:36-46
@@ -97,6 +97,168 @@ __device__ __forceinline__ uint32_t lookback_wave(unsigned long long* status, ui
     return excl;
 }
 
+// Two-level decoupled look-back, wave-cooperative, one prefix channel.  Tiles are grouped by 64:
+// level 1 sums the aggregates of the tile's predecessors inside its group (one 64-wide poll);
+// the group's last tile then publishes the group aggregate BEFORE resolving its own group prefix,
+// so level 2 (one 64-wide poll over earlier groups, stopping at the nearest inclusive group)
+// never waits on a chain of group prefixes.  ~2 round trips per tile, whatever the tile count.
+// gstat granules: flag 2*epoch = group aggregate, 2*epoch+1 = group inclusive prefix.
+__device__ __forceinline__ uint32_t lookback2_wave(unsigned long long* tstat,
+                                                   unsigned long long* gstat, uint32_t tile,
+                                                   uint32_t ntiles, uint32_t agg, uint32_t epoch,
+                                                   uint32_t* err) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long fagg = 2ull * epoch, fincl = 2ull * epoch + 1ull;
+    const uint32_t G = tile >> 6, first = G << 6, pos = tile & 63u;
+    const uint32_t last = (first + 63u < ntiles - 1u) ? first + 63u : ntiles - 1u;
+    if (lane == 0)
+        __hip_atomic_store(&tstat[tile], (fagg << 32) | agg, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t spins = 0;
+    // level 1: aggregates of tiles [first, tile)
+    uint32_t in_excl = 0;
+    if (pos > 0) {
+        while (true) {
+            unsigned long long sv = fagg << 32;
+            if ((uint32_t)lane < pos)
+                sv = __hip_atomic_load(&tstat[first + lane], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            if (__ballot((sv >> 32) < fagg)) {
+                if (++spins > kSpinLimit) {
+                    if (lane == 0) atomicOr(err, 1u);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            uint32_t v = (uint32_t)lane < pos ? (uint32_t)sv : 0u;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+            in_excl = v;
+            break;
+        }
+    }
+    const uint32_t gtotal = in_excl + agg;
+    if (tile == last && lane == 0)
+        __hip_atomic_store(&gstat[G], (fagg << 32) | gtotal, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    // level 2: prefix of the groups before G
+    uint32_t gpre = 0;
+    int64_t base = (int64_t)G - 1;
+    while (base >= 0) {
+        const int64_t j = base - lane;
+        unsigned long long sv = fincl << 32;
+        if (j >= 0)
+            sv = __hip_atomic_load(&gstat[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long flag = sv >> 32;
+        const unsigned long long m_incl = __ballot(flag == fincl);
+        const unsigned long long m_wait = __ballot(flag < fagg);
+        const int firsti = m_incl ? __ffsll((long long)m_incl) - 1 : 63;
+        const unsigned long long need = firsti == 63 ? ~0ull : ((2ull << firsti) - 1ull);
+        if (m_wait & need) {
+            if (++spins > kSpinLimit) {
+                if (lane == 0) atomicOr(err, 1u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        uint32_t v = (lane <= firsti) ? (uint32_t)sv : 0u;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        gpre += v;
+        if (m_incl) break;
+        base -= 64;
+    }
+    if (tile == last && lane == 0)
+        __hip_atomic_store(&gstat[G], (fincl << 32) | (gpre + gtotal), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    return gpre + in_excl;
+}
+
+// The same two-level scheme with one channel per THREAD (the 256 digits of a radix pass):
+// groups of 16 tiles, 16 independent polls per round trip.
+constexpr int kSortGroup = 16;
+__device__ __forceinline__ uint32_t lookback2_chan(unsigned long long* tstat,
+                                                   unsigned long long* gstat, uint32_t tile,
+                                                   uint32_t ntiles, uint32_t chan, uint32_t agg,
+                                                   uint32_t epoch, uint32_t* err) {
+    const unsigned long long fagg = 2ull * epoch, fincl = 2ull * epoch + 1ull;
+    const uint32_t G = tile / kSortGroup, first = G * kSortGroup, pos = tile - first;
+    const uint32_t last = (first + kSortGroup - 1u < ntiles - 1u) ? first + kSortGroup - 1u
+                                                                   : ntiles - 1u;
+    __hip_atomic_store(&tstat[(size_t)tile * 256 + chan], (fagg << 32) | agg, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t spins = 0;
+    uint32_t in_excl = 0;
+    if (pos > 0) {
+        while (true) {
+            unsigned long long sv[kSortGroup];
+#pragma unroll
+            for (int q = 0; q < kSortGroup; ++q)
+                sv[q] = ((uint32_t)q < pos)
+                            ? __hip_atomic_load(&tstat[(size_t)(first + q) * 256 + chan],
+                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                            : (fagg << 32);
+            bool wait = false;
+            uint32_t v = 0;
+#pragma unroll
+            for (int q = 0; q < kSortGroup; ++q) {
+                wait |= (sv[q] >> 32) < fagg;
+                v += (uint32_t)q < pos ? (uint32_t)sv[q] : 0u;
+            }
+            if (wait) {
+                if (++spins > kSpinLimit) {
+                    atomicOr(err, 2u);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            in_excl = v;
+            break;
+        }
+    }
+    const uint32_t gtotal = in_excl + agg;
+    if (tile == last)
+        __hip_atomic_store(&gstat[(size_t)G * 256 + chan], (fagg << 32) | gtotal,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t gpre = 0;
+    int64_t j = (int64_t)G - 1;
+    while (j >= 0) {
+        unsigned long long sv[kSortGroup];
+#pragma unroll
+        for (int q = 0; q < kSortGroup; ++q)
+            sv[q] = (j - q >= 0) ? __hip_atomic_load(&gstat[(size_t)(j - q) * 256 + chan],
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                 : (fincl << 32);
+        int q = 0;
+        bool done = false;
+        for (; q < kSortGroup; ++q) {
+            const unsigned long long flag = sv[q] >> 32;
+            if (flag < fagg) break;
+            gpre += (uint32_t)sv[q];
+            if (flag == fincl) {
+                done = true;
+                break;
+            }
+        }
+        if (done) break;
+        j -= q;
+        if (q < kSortGroup) {
+            if (++spins > kSpinLimit) {
+                atomicOr(err, 2u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    if (tile == last)
+        __hip_atomic_store(&gstat[(size_t)G * 256 + chan], (fincl << 32) | (gpre + gtotal),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return gpre + in_excl;
+}
+
 // ---- fused frame kernel ------------------------------------------------------------------------
 // Camera owning global index gi; -1 when gi is outside every camera (the reference's
 // out-of-bounds read, canonicalised as mask 0).  Branch-free over the (uniform) camera count so
@@ -142,195 +304,299 @@ __device__ __forceinline__ void nb_point(const Nb& n, float& x, float& y, float&
     z = zz;
 }
 
-// check_at / check_at_rot45 (filter_flying_pixels.glsl:55-133) for ring i
-__device__ __forceinline__ bool flying_check(const CamDesc* cams, int ncams, int k, int64_t g,
-                                             uint32_t x, uint32_t y, uint32_t i, bool rot45,
-                                             float thr, float nx, float ny, float nz) {
-    const CamDesc& c = cams[k];
-    if (x + i > c.W - 1 || y + i > c.H - 1) return false;
-    const int64_t iw = (int64_t)i * c.W;
-    int64_t up, down, left, right;
+// Neighbour indices of ring i (filter_flying_pixels.glsl:63-73 / :100-109): up, down, left, right.
+__device__ __forceinline__ void ring_idx(int64_t g, int64_t iw, uint32_t i, bool rot45,
+                                         int64_t* q) {
     if (!rot45) {
-        up = g - iw; down = g + iw; left = g - i; right = g + i;
+        q[0] = g - iw; q[1] = g + iw; q[2] = g - i; q[3] = g + i;
     } else {
-        up = g - iw - i; down = g + iw + i; left = g + iw - i; right = g - iw + i;
+        q[0] = g - iw - i; q[1] = g + iw + i; q[2] = g + iw - i; q[3] = g - iw + i;
     }
-    const Nb nu = nb_load(cams, ncams, k, up);
-    const Nb nd = nb_load(cams, ncams, k, down);
-    const Nb nl = nb_load(cams, ncams, k, left);
-    const Nb nr = nb_load(cams, ncams, k, right);
-    if (nu.d == 0 || nd.d == 0 || nl.d == 0 || nr.d == 0) return false;
+}
+
+// The surface test of check_at / check_at_rot45 (filter_flying_pixels.glsl:74-96) on loaded
+// neighbours: invalid if any mask is 0 or dot(normalize(cross(dy, dx)), -normalize(p)) < thr.
+__device__ __forceinline__ bool ring_ok(const Nb* n, float thr, float nx, float ny, float nz) {
+    if (n[0].d == 0 || n[1].d == 0 || n[2].d == 0 || n[3].d == 0) return false;
     float ux, uy, uz, dx_, dy_, dz_, lx, ly, lz, rx, ry, rz;
-    nb_point(nu, ux, uy, uz);
-    nb_point(nd, dx_, dy_, dz_);
-    nb_point(nl, lx, ly, lz);
-    nb_point(nr, rx, ry, rz);
-    // dx = right - left, dy = down - up, normal = normalize(cross(dy, dx))
-    float ax = dx_ - ux, ay = dy_ - uy, az = dz_ - uz;  // dy
-    float bx = rx - lx, by = ry - ly, bz = rz - lz;      // dx
+    nb_point(n[0], ux, uy, uz);
+    nb_point(n[1], dx_, dy_, dz_);
+    nb_point(n[2], lx, ly, lz);
+    nb_point(n[3], rx, ry, rz);
+    float ax = dx_ - ux, ay = dy_ - uy, az = dz_ - uz;  // dy = down - up
+    float bx = rx - lx, by = ry - ly, bz = rz - lz;      // dx = right - left
     float cx = ay * bz - az * by;
     float cy = az * bx - ax * bz;
     float cz = ax * by - ay * bx;
     normalize3(cx, cy, cz);
-    float cv = dot3(cx, cy, cz, nx, ny, nz);
+    const float cv = dot3(cx, cy, cz, nx, ny, nz);
     return !(cv < thr);  // NaN passes
 }
 
-struct ItemOut {
-    float4 w;
-    uint32_t bits;  // bit0 convert, bit1 flying, bit2 crop
-};
-
-__device__ __forceinline__ ItemOut eval_depth(const FrameArgs& a, const CamDesc* cams, uint32_t g,
-                                              uint32_t d) {
-    ItemOut r;
-    r.bits = 0;
-    r.w = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (d == 0) return r;
-    r.bits = 1;
-    const int k = find_cam(cams, a.ncams, (int64_t)g);
+// Stage bits of depth item g (bit0 convert, bit1 flying, bit2 crop): convert_depthmap_to_points
+// (:83-120) -> filter_flying_pixels (:135-165) -> crop_points (:38-67).  Ring i+1's neighbour
+// loads are issued before ring i is evaluated, so the flying filter costs ~one memory trip.
+template <bool ROT45>
+__device__ __forceinline__ uint32_t depth_bits(const FrameArgs& a, const CamDesc* cams, int k,
+                                               uint32_t local, uint32_t d) {
+    if (d == 0) return 0;
     const CamDesc& c = cams[k];
-    const uint32_t local = (uint32_t)((int64_t)g - c.off);
     float px, py, pz;
     cam_point(c, local, d, px, py, pz);
     if (a.do_flying) {
-        if (sqrtf(dot3(px, py, pz, px, py, pz)) > 10.0f) return r;  // max_distance (:41,:143)
+        if (sqrtf(dot3(px, py, pz, px, py, pz)) > 10.0f) return 1;  // max_distance (:41,:143)
         float nx = px, ny = py, nz = pz;
         normalize3(nx, ny, nz);
         nx = -nx; ny = -ny; nz = -nz;
-        const uint32_t x = local % c.W, y = local / c.W;
-        for (uint32_t i = 1; i <= a.F; ++i) {
-            if (!flying_check(cams, a.ncams, k, (int64_t)g, x, y, i, false, a.thr, nx, ny, nz))
-                return r;
-            if (a.rot45 &&
-                !flying_check(cams, a.ncams, k, (int64_t)g, x, y, i, true, a.thr, nx, ny, nz))
-                return r;
+        const uint32_t y = local / c.W, x = local - y * c.W;
+        const int64_t g = c.off + local;
+        constexpr int nv = ROT45 ? 2 : 1;
+        Nb cur[4 * nv], nxt[4 * nv];
+        int64_t q[4];
+        // rings whose bounds test fails never load (x+i > W-1 || y+i > H-1 -> invalid)
+        const uint32_t F = a.F;
+        if (F >= 1 && (x + 1 > c.W - 1 || y + 1 > c.H - 1)) return 1;
+        if (F >= 1) {
+#pragma unroll
+            for (int v = 0; v < nv; ++v) {
+                ring_idx(g, (int64_t)c.W, 1u, v == 1, q);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) cur[4 * v + t] = nb_load(cams, a.ncams, k, q[t]);
+            }
+        }
+        for (uint32_t i = 1; i <= F; ++i) {
+            const bool more = i < F && !(x + i + 1 > c.W - 1 || y + i + 1 > c.H - 1);
+            if (more) {
+#pragma unroll
+                for (int v = 0; v < nv; ++v) {
+                    ring_idx(g, (int64_t)(i + 1) * c.W, i + 1, v == 1, q);
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) nxt[4 * v + t] = nb_load(cams, a.ncams, k, q[t]);
+                }
+            }
+            if (!ring_ok(cur, a.thr, nx, ny, nz)) return 1;
+            if (ROT45 && !ring_ok(cur + 4, a.thr, nx, ny, nz)) return 1;
+            if (i < F && !more) return 1;  // next ring fails its bounds test
+#pragma unroll
+            for (int t = 0; t < 4 * nv; ++t) cur[t] = nxt[t];
         }
     }
-    r.bits |= 2;
     if (a.do_crop) {
-        float qx = mrow(c.Tc + 0, px, py, pz, 1.0f);
-        float qy = mrow(c.Tc + 4, px, py, pz, 1.0f);
-        float qz = mrow(c.Tc + 8, px, py, pz, 1.0f);
+        const float qx = mrow(c.Tc + 0, px, py, pz, 1.0f);
+        const float qy = mrow(c.Tc + 4, px, py, pz, 1.0f);
+        const float qz = mrow(c.Tc + 8, px, py, pz, 1.0f);
         if (qx < a.lo[0] || qx > a.hi[0] || qy < a.lo[1] || qy > a.hi[1] || qz < a.lo[2] ||
             qz > a.hi[2])
-            return r;
+            return 3;
     }
-    r.bits |= 4;
-    r.w.x = mrow(c.Tw + 0, px, py, pz, 1.0f);
-    r.w.y = mrow(c.Tw + 4, px, py, pz, 1.0f);
-    r.w.z = mrow(c.Tw + 8, px, py, pz, 1.0f);
-    r.w.w = mrow(c.Tw + 12, px, py, pz, 1.0f);
-    return r;
+    return 7;
 }
 
-__device__ __forceinline__ ItemOut eval_sel(const FrameArgs& a, uint32_t i) {
-    ItemOut r;
-    r.bits = 0;
-    r.w = make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 p = a.ring[(a.ring_first + i) % a.ring_cap];
-    if (p.w == 0.0f) return r;  // rollbuffer mask 0
-    r.bits = 3;
-    // transform index: last covered sequence starting at or before i
+__device__ __forceinline__ float4 depth_world(const CamDesc& c, uint32_t local, uint32_t d) {
+    float px, py, pz;
+    cam_point(c, local, d, px, py, pz);
+    return make_float4(mrow(c.Tw + 0, px, py, pz, 1.0f), mrow(c.Tw + 4, px, py, pz, 1.0f),
+                       mrow(c.Tw + 8, px, py, pz, 1.0f), mrow(c.Tw + 12, px, py, pz, 1.0f));
+}
+
+// transform index of selected point i: last covered sequence starting at or before i
+__device__ __forceinline__ uint32_t sel_tf(const FrameArgs& a, uint32_t i) {
     uint32_t lo = 0, hi = a.nseg;
     while (hi - lo > 1) {
-        uint32_t mid = (lo + hi) >> 1;
+        const uint32_t mid = (lo + hi) >> 1;
         if (a.seg_start[mid] <= i) lo = mid; else hi = mid;
     }
-    const uint32_t t = a.seg_tf[lo];
-    const float* Tw = a.tfw + 16 * (size_t)t;
-    const float* Tc = a.tfc + 16 * (size_t)t;
-    if (a.do_crop) {
-        float qx = mrow(Tc + 0, p.x, p.y, p.z, 1.0f);
-        float qy = mrow(Tc + 4, p.x, p.y, p.z, 1.0f);
-        float qz = mrow(Tc + 8, p.x, p.y, p.z, 1.0f);
-        if (qx < a.lo[0] || qx > a.hi[0] || qy < a.lo[1] || qy > a.hi[1] || qz < a.lo[2] ||
-            qz > a.hi[2])
-            return r;
-    }
-    r.bits |= 4;
-    r.w.x = mrow(Tw + 0, p.x, p.y, p.z, 1.0f);
-    r.w.y = mrow(Tw + 4, p.x, p.y, p.z, 1.0f);
-    r.w.z = mrow(Tw + 8, p.x, p.y, p.z, 1.0f);
-    r.w.w = mrow(Tw + 12, p.x, p.y, p.z, 1.0f);
-    return r;
+    return a.seg_tf[lo];
 }
 
-__global__ __launch_bounds__(kFrameThreads) void k_frame(FrameArgs a) {
-    __shared__ CamDesc s_cams[kMaxCams];
-    __shared__ uint32_t s_wave[4];
-    __shared__ uint32_t s_tile, s_excl;
-    __shared__ uint32_t s_hist[4 * 256];
-    {
-        const uint32_t words = (uint32_t)a.ncams * (uint32_t)(sizeof(CamDesc) / 4);
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.cams);
-        uint32_t* dst = reinterpret_cast<uint32_t*>(s_cams);
-        for (uint32_t w = threadIdx.x; w < words; w += kFrameThreads) dst[w] = src[w];
+// selected rollbuffer point i: mask (transfer_data of the selected mask), transform_points
+// _indirect (:50-69) into the crop frame, crop_points
+__device__ __forceinline__ uint32_t sel_bits(const FrameArgs& a, uint32_t i, float4& p, uint32_t& t) {
+    p = a.ring[(a.ring_first + i) % a.ring_cap];
+    if (p.w == 0.0f) return 0;  // rollbuffer mask 0
+    t = sel_tf(a, i);
+    if (a.do_crop) {
+        const float* Tc = a.tfc + 16 * (size_t)t;
+        const float qx = mrow(Tc + 0, p.x, p.y, p.z, 1.0f);
+        const float qy = mrow(Tc + 4, p.x, p.y, p.z, 1.0f);
+        const float qz = mrow(Tc + 8, p.x, p.y, p.z, 1.0f);
+        if (qx < a.lo[0] || qx > a.hi[0] || qy < a.lo[1] || qy > a.hi[1] || qz < a.lo[2] ||
+            qz > a.hi[2])
+            return 3;
     }
-    if (a.key_hist)
-        for (uint32_t i = threadIdx.x; i < a.npasses * 256; i += kFrameThreads) s_hist[i] = 0;
-    if (threadIdx.x == 0) s_tile = (uint32_t)(atomicAdd(a.tile_ctr, 1ull) - a.tile_base);
-    __syncthreads();
-    const uint32_t tile = s_tile;
+    return 7;
+}
 
-    ItemOut it;
-    it.bits = 0;
-    uint32_t item;
+__device__ __forceinline__ void load_cams(const FrameArgs& a, CamDesc* s_cams) {
+    const uint32_t words = (uint32_t)a.ncams * (uint32_t)(sizeof(CamDesc) / 4);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.cams);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(s_cams);
+    for (uint32_t w = threadIdx.x; w < words; w += blockDim.x) dst[w] = src[w];
+}
+
+// Pass 1 of the ordered compaction (apply_point_mask.glsl:42-55 made stable): per item stage
+// bits, one 64-bit validity ballot per wave and the valid count per 1024-item tile.
+template <bool ROT45>
+__global__ __launch_bounds__(kFrameThreads) void k_mask(FrameArgs a) {
+    __shared__ CamDesc s_cams[kMaxCams];
+    __shared__ uint32_t s_cnt[kFrameThreads / 64];
+    load_cams(a, s_cams);
+    __syncthreads();
+    const uint32_t tile = blockIdx.x;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t bits = 0, item;
     bool in_range;
     if (tile < a.depth_tiles) {
         item = tile * kFrameTile + threadIdx.x;
         in_range = item < a.depth_total;
         if (in_range) {
             const int k = find_cam(s_cams, a.ncams, (int64_t)item);
-            const uint32_t d = s_cams[k].depth[(uint32_t)((int64_t)item - s_cams[k].off)];
-            it = eval_depth(a, s_cams, item, d);
+            const uint32_t local = (uint32_t)((int64_t)item - s_cams[k].off);
+            bits = depth_bits<ROT45>(a, s_cams, k, local, s_cams[k].depth[local]);
         }
     } else {
         const uint32_t i = (tile - a.depth_tiles) * kFrameTile + threadIdx.x;
         item = a.depth_total + i;
         in_range = i < a.sel_count;
-        if (in_range) it = eval_sel(a, i);
-    }
-
-    const uint32_t valid = (it.bits & 4) ? 1u : 0u;
-    uint32_t total;
-    const uint32_t excl_thread = block_exclusive_scan(valid, total, s_wave);
-    if (threadIdx.x < 64) {
-        const uint32_t ex = lookback_wave(a.status, tile, total, a.epoch, a.err);
-        if (threadIdx.x == 0) {
-            s_excl = ex;
-            if (tile == a.total_tiles - 1) *a.out_count = ex + total;
+        if (in_range) {
+            float4 p;
+            uint32_t t;
+            bits = sel_bits(a, i, p, t);
         }
     }
+    const unsigned long long m = __ballot((bits & 4) != 0);
+    if (lane == 0) {
+        a.valid_bits[(size_t)tile * (kFrameTile / 64) + wid] = m;
+        s_cnt[wid] = (uint32_t)__popcll(m);
+    }
+    if (a.dbg && in_range) a.dbg[item] = (uint8_t)bits;
     __syncthreads();
-    if (a.dbg && in_range) a.dbg[item] = (uint8_t)it.bits;
-    if (valid) {
-        const uint32_t pos = s_excl + excl_thread;
-        a.out_pts[pos] = it.w;
-        if (a.do_voxel) {
-            const uint32_t key = voxel_key(it.w.x, it.w.y, it.w.z, a.vlo, a.vcs, a.gmax, a.gs);
-            a.out_coords[pos] = key;
-            if (a.occ_mode == 1) {
-                const uint8_t h = a.occ[key];
-                if (!(h & 0x80u)) a.occ[key] = (uint8_t)(h | 0x80u);
-            } else if (a.occ_mode == 2) {
-                a.occ[key] = 1;
+    if (threadIdx.x == 0) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int w = 0; w < kFrameThreads / 64; ++w) c += s_cnt[w];
+        a.tile_counts[tile] = c;
+    }
+}
+
+// Exclusive scan of the tile counts by one workgroup (chunks of 4096 with a running carry);
+// writes the total (m_numItemsAfterMask) too.
+__global__ __launch_bounds__(1024) void k_scan_counts(const uint32_t* __restrict__ counts,
+                                                      uint32_t m, uint32_t* __restrict__ offsets,
+                                                      uint32_t* __restrict__ total) {
+    __shared__ uint32_t s_w[16];
+    __shared__ uint32_t s_carry;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_carry = 0;
+    __syncthreads();
+    for (uint32_t base = 0; base < m; base += 4096) {
+        uint32_t v[4], sum = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t i = base + threadIdx.x * 4 + q;
+            v[q] = i < m ? counts[i] : 0u;
+            sum += v[q];
+        }
+        uint32_t x = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) s_w[wid] = x;
+        __syncthreads();
+        uint32_t wb = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) {
+            const uint32_t t = s_w[w];
+            wb += (w < wid) ? t : 0u;
+            tot += t;
+        }
+        uint32_t run = s_carry + wb + x - sum;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t i = base + threadIdx.x * 4 + q;
+            if (i < m) offsets[i] = run;
+            run += v[q];
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) s_carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *total = s_carry;
+}
+
+// Pass 2: each valid item recomputes its world point (the same f32 ops as pass 1) and writes it
+// at tile offset + rank (ballot popcount): stable pixel order, cameras in add order, selected
+// rollbuffer points after the depth points (fusion.cpp:1525,1559).  Optionally the voxel key
+// (compute_voxel_coords), the occupancy mark (voxel_grid_occupancy_of_points, as a no-return
+// atomic OR of bit 7) and the digit histogram of the keys for the radix sort.
+__global__ __launch_bounds__(kEmitThreads) void k_emit(FrameArgs a) {
+    __shared__ CamDesc s_cams[kMaxCams];
+    __shared__ uint32_t s_hist[4 * 256];
+    load_cams(a, s_cams);
+    if (a.key_hist)
+        for (uint32_t i = threadIdx.x; i < a.npasses * 256; i += kEmitThreads) s_hist[i] = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const uint32_t gidx = blockIdx.x * kEmitThreads + threadIdx.x;  // item index in tile space
+    const uint32_t tile = gidx / kFrameTile;
+    if (tile < a.total_tiles) {
+        const uint32_t wt = (gidx % kFrameTile) >> 6;  // wave within the count tile
+        const unsigned long long* vb = a.valid_bits + (size_t)tile * (kFrameTile / 64);
+        const unsigned long long m = vb[wt];
+        uint32_t before = 0;
+        for (uint32_t w = 0; w < wt; ++w) before += (uint32_t)__popcll(vb[w]);
+        if ((m >> lane) & 1ull) {
+            const uint32_t pos = a.tile_offsets[tile] + before +
+                                 (uint32_t)__popcll(m & (lane ? (~0ull >> (64 - lane)) : 0ull));
+            float4 w;
+            if (tile < a.depth_tiles) {
+                const uint32_t item = gidx;
+                const int k = find_cam(s_cams, a.ncams, (int64_t)item);
+                const uint32_t local = (uint32_t)((int64_t)item - s_cams[k].off);
+                w = depth_world(s_cams[k], local, s_cams[k].depth[local]);
+            } else {
+                const uint32_t i = gidx - a.depth_tiles * kFrameTile;
+                const float4 p = a.ring[(a.ring_first + i) % a.ring_cap];
+                const float* Tw = a.tfw + 16 * (size_t)sel_tf(a, i);
+                w = make_float4(mrow(Tw + 0, p.x, p.y, p.z, 1.0f), mrow(Tw + 4, p.x, p.y, p.z, 1.0f),
+                                mrow(Tw + 8, p.x, p.y, p.z, 1.0f), mrow(Tw + 12, p.x, p.y, p.z, 1.0f));
             }
-            if (a.key_hist)
-                for (uint32_t p = 0; p < a.npasses; ++p)
-                    atomicAdd(&s_hist[p * 256 + ((key >> (8 * p)) & 0xFFu)], 1u);
+            a.out_pts[pos] = w;
+            if (a.do_voxel) {
+                const uint32_t key = voxel_key(w.x, w.y, w.z, a.vlo, a.vcs, a.gmax, a.gs);
+                a.out_coords[pos] = key;
+                if (a.occ_mode == 1)
+                    atomicOr(reinterpret_cast<uint32_t*>(a.occ + (key & ~3u)), 0x80u << (8 * (key & 3u)));
+                else if (a.occ_mode == 2)
+                    a.occ[key] = 1;
+                if (a.key_hist)
+                    for (uint32_t p = 0; p < a.npasses; ++p)
+                        atomicAdd(&s_hist[p * 256 + ((key >> (8 * p)) & 0xFFu)], 1u);
+            }
         }
     }
     if (a.key_hist) {
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < a.npasses * 256; i += kFrameThreads)
+        for (uint32_t i = threadIdx.x; i < a.npasses * 256; i += kEmitThreads)
             if (s_hist[i]) atomicAdd(&a.key_hist[i], s_hist[i]);
     }
 }
 
 hipError_t launch_frame(const FrameArgs& a, hipStream_t s) {
     if (a.total_tiles == 0) return hipMemsetAsync(a.out_count, 0, 4, s);
-    hipLaunchKernelGGL(k_frame, dim3(a.total_tiles), dim3(kFrameThreads), 0, s, a);
+    if (a.rot45)
+        hipLaunchKernelGGL(k_mask<true>, dim3(a.total_tiles), dim3(kFrameThreads), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_mask<false>, dim3(a.total_tiles), dim3(kFrameThreads), 0, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, a.tile_counts, a.total_tiles,
+                       a.tile_offsets, a.out_count);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const uint32_t eblocks = (a.total_tiles * kFrameTile + kEmitThreads - 1) / kEmitThreads;
+    hipLaunchKernelGGL(k_emit, dim3(eblocks), dim3(kEmitThreads), 0, s, a);
     return hipGetLastError();
 }
 
@@ -556,7 +822,7 @@ template <int PT>
 __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
     uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, const uint32_t* __restrict__ count,
-    const uint32_t* __restrict__ ghist, unsigned long long* status,
+    const uint32_t* __restrict__ ghist, unsigned long long* status, unsigned long long* gstatus,
     unsigned long long* tile_ctr, unsigned long long tile_base, uint32_t epoch, uint32_t* err,
     uint32_t shift, uint32_t dbits) {
     constexpr int kTile = kSortThreads * PT;
@@ -613,52 +879,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
         tot += c;
     }
     s_base[d] = digit_base(ghist, s_wave);
-    // look-back for digit d
-    {
-        const unsigned long long fagg = 2ull * epoch, fincl = fagg + 1ull;
-        unsigned long long* st = status + (size_t)tile * 256 + d;
-        uint32_t excl = 0;
-        if (tile == 0) {
-            __hip_atomic_store(st, (fincl << 32) | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            __hip_atomic_store(st, (fagg << 32) | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            // windowed: 4 predecessors per round trip
-            int64_t j = (int64_t)tile - 1;
-            uint32_t spins = 0;
-            while (j >= 0) {
-                unsigned long long sv[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    sv[q] = (j - q >= 0)
-                                ? __hip_atomic_load(status + (size_t)(j - q) * 256 + d,
-                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                : (fincl << 32);
-                int q = 0;
-                bool done = false;
-                for (; q < 4; ++q) {
-                    const unsigned long long flag = sv[q] >> 32;
-                    if (flag < fagg) break;
-                    excl += (uint32_t)sv[q];
-                    if (flag == fincl) {
-                        done = true;
-                        break;
-                    }
-                }
-                if (done) break;
-                j -= q;
-                if (q < 4) {
-                    if (++spins > kSpinLimit) {
-                        atomicOr(err, 2u);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-            }
-            __hip_atomic_store(st, (fincl << 32) | (excl + tot), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
-        s_excl[d] = excl;
-    }
+    s_excl[d] = lookback2_chan(status, gstatus, tile, ntiles, d, tot, epoch, err);
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < PT; ++j) {
@@ -678,8 +899,8 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
 __global__ __launch_bounds__(kGroupThreads) void k_group_scan(
     const uint32_t* __restrict__ keys, const uint32_t* __restrict__ count,
     uint32_t* __restrict__ gstart, uint32_t* __restrict__ out_count, unsigned long long* status,
-    unsigned long long* tile_ctr, unsigned long long tile_base, uint32_t epoch, uint32_t* err,
-    uint32_t* hist) {
+    unsigned long long* gstatus, unsigned long long* tile_ctr, unsigned long long tile_base,
+    uint32_t epoch, uint32_t* err, uint32_t* hist) {
     __shared__ uint32_t s_wave[4];
     __shared__ uint32_t s_tile, s_excl;
     const uint32_t n = *count;
@@ -706,7 +927,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_scan(
     uint32_t total;
     const uint32_t excl_thread = block_exclusive_scan(cnt, total, s_wave);
     if (threadIdx.x < 64) {
-        const uint32_t ex = lookback_wave(status, tile, total, epoch, err);
+        const uint32_t ex = lookback2_wave(status, gstatus, tile, ntiles, total, epoch, err);
         if (threadIdx.x == 0) {
             s_excl = ex;
             if (tile == ntiles - 1) *out_count = ex + total;
@@ -797,7 +1018,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_sum(
 }
 
 size_t voxelize_status_words(uint32_t nmax) {
-    return (size_t)((nmax + kSortThreads * 4 - 1) / (kSortThreads * 4) + 1) * 256;
+    return (size_t)((nmax + kSortThreads * 16 - 1) / (kSortThreads * 16) + 1) * 256;
 }
 size_t voxelize_group_tiles(uint32_t nmax) {
     return (size_t)((nmax + kGroupTile - 1) / kGroupTile + 1);
@@ -806,8 +1027,7 @@ size_t voxelize_group_tiles(uint32_t nmax) {
 hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s) {
     const uint32_t npasses = a.key_bits == 0 ? 1u : (a.key_bits + 7) / 8;
     // small N: 1024 keys per sort tile (more blocks in flight); large N: 4096
-    const bool small = a.nmax <= (1u << 21);
-    const uint32_t tile = small ? kSortThreads * 4 : kSortThreads * 16;
+    const uint32_t tile = kSortThreads * 16;
     const uint32_t sort_tiles = (a.nmax + tile - 1) / tile;
     hipError_t e;
     if (!a.hist_ready) {
@@ -825,16 +1045,10 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s) {
         const uint32_t dbits = remaining >= 8 ? 8u : (remaining ? remaining : 1u);
         const uint32_t ep = ++(*a.epoch);
         if (sort_tiles) {
-            if (small)
-                hipLaunchKernelGGL(k_sort_pass<4>, dim3(sort_tiles), dim3(kSortThreads), 0, s, kin,
-                                   vin, kbuf[p & 1], vbuf[p & 1], a.count, a.hist + 256 * p,
-                                   a.status, a.ctrs + kCtrSort0 + p, a.ctr_base[kCtrSort0 + p],
-                                   ep, a.err, 8 * p, dbits);
-            else
-                hipLaunchKernelGGL(k_sort_pass<16>, dim3(sort_tiles), dim3(kSortThreads), 0, s, kin,
-                                   vin, kbuf[p & 1], vbuf[p & 1], a.count, a.hist + 256 * p,
-                                   a.status, a.ctrs + kCtrSort0 + p, a.ctr_base[kCtrSort0 + p],
-                                   ep, a.err, 8 * p, dbits);
+            hipLaunchKernelGGL(k_sort_pass<16>, dim3(sort_tiles), dim3(kSortThreads), 0, s, kin,
+                               vin, kbuf[p & 1], vbuf[p & 1], a.count, a.hist + 256 * p,
+                               a.status, a.sgstatus, a.ctrs + kCtrSort0 + p,
+                               a.ctr_base[kCtrSort0 + p], ep, a.err, 8 * p, dbits);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             a.ctr_base[kCtrSort0 + p] += sort_tiles;
         }
@@ -845,8 +1059,8 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s) {
     const uint32_t gblocks = group_tiles ? group_tiles : 1;
     const uint32_t ep = ++(*a.epoch);
     hipLaunchKernelGGL(k_group_scan, dim3(gblocks), dim3(kGroupThreads), 0, s, kin, a.count,
-                       a.gstart, a.out_count, a.gstatus, a.ctrs + kCtrGroup, a.ctr_base[kCtrGroup],
-                       ep, a.err, a.hist);
+                       a.gstart, a.out_count, a.gstatus, a.ggstatus, a.ctrs + kCtrGroup,
+                       a.ctr_base[kCtrGroup], ep, a.err, a.hist);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     a.ctr_base[kCtrGroup] += gblocks;
     uint32_t sblocks = (a.nmax + 255) / 256;

@@ -52,7 +52,9 @@ struct VoxelizeArgs {
     uint32_t *keys_a, *keys_b, *vals_a, *vals_b;
     uint32_t* hist;                 // [4*256] zero on entry, left zero on exit
     unsigned long long* status;     // [sort tiles * 256] epoch granules
+    unsigned long long* sgstatus;   // [sort tile groups * 256]
     unsigned long long* gstatus;    // [group tiles] epoch granules
+    unsigned long long* ggstatus;   // [group tiles / 64 + 1]
     uint32_t* gstart;               // [nmax] first sorted position of each group
     unsigned long long* ctrs;       // [kCtrSlots] tile tickets
     unsigned long long* ctr_base;   // host copy of the ticket bases (updated)
