@@ -12,8 +12,13 @@
 namespace gdf {
 
 constexpr int kMaxCams = 16;          // GDF_MAX_CAMERAS
-constexpr int kFrameThreads = 256;    // k_mask block: 4 waves, one item per thread
-constexpr int kFrameTile = kFrameThreads;  // items per count tile
+constexpr int kFrameThreads = 256;    // k_mask block: 4 waves
+constexpr int kFrameTile = 256;       // items per count tile (ordered-compaction granularity)
+constexpr int kArgCams = 4;           // camera descriptors passed in the kernel arguments
+constexpr int kTileW = 64;            // k_mask 2-D pixel tile: 64 columns (one per lane) ...
+constexpr int kTileH = 4;             // ... x 4 rows (one per wave)
+constexpr int kHalo = 8;              // LDS halo: rings i <= min(F, 8) read neighbours from LDS
+constexpr uint32_t kFusedPrefixTiles = 4096;  // up to 1 Mi items: k_emit sums the tile counts
 constexpr int kEmitThreads = 1024;    // k_emit block: 4 count tiles, fewer histogram flushes
 constexpr int kSortThreads = 256;
 constexpr int kGroupThreads = 256;
@@ -36,22 +41,28 @@ struct CamDesc {
     const uint16_t* depth;  // device pointer to pixel 0 of this camera
     const float* xn;        // [W]
     const float* yn;        // [H]
+    uint64_t wmagic;        // ceil(2^40 / W): exact local / W for local < 2^24, W < 2^16
     uint32_t W, H, n;
     uint32_t emit;          // 1: pixels are processed; 0: halo camera, only read as neighbours
     float scale;
+    uint32_t tiles_x;       // ceil(W / kTileW)
+    uint32_t block0;        // first k_mask block of this camera (emitting cameras)
+    uint32_t nblocks;       // tiles_x * ceil(H / kTileH)
+    uint32_t pad[2];
     float Tw[16];           // row-major T_world
     float Tc[16];           // row-major T_crop
-    uint32_t pad[3];
 };
 static_assert(sizeof(CamDesc) % 16 == 0, "CamDesc must stay 16-byte sized");
 
-// Arguments of the fused compaction launch (k_frame), passed by value (cameras included).
+// Arguments of the compaction launches, passed by value.  Up to kArgCams camera descriptors
+// travel in the kernel arguments (kernel-argument bytes cost launch latency); more cameras are
+// read from a device copy.
 struct FrameArgs {
-    CamDesc cams[kMaxCams];
+    CamDesc cams[kArgCams];
+    const CamDesc* cams_dev;    // all descriptors when ncams > kArgCams
     int32_t ncams;
-    uint32_t depth_total;       // ΣP of emitting cameras' index space (tiles cover [0, depth_total))
-    uint32_t depth_tiles;
-    uint32_t total_tiles;
+    uint32_t depth_total;       // ΣP of emitting cameras' index space
+    uint32_t total_tiles;       // 256-item count tiles over depth + selected items
     // flying-pixel filter (sh/filter_flying_pixels.glsl)
     int32_t do_flying;
     uint32_t F;
@@ -82,11 +93,15 @@ struct FrameArgs {
     float4* out_pts;
     uint32_t* out_count;
     uint32_t* out_coords;
-    uint8_t* dbg;               // optional per-item stage bits
     // reduce-then-scan compaction state
-    unsigned long long* valid_bits;  // [tiles * 16] one ballot per wave
-    uint32_t* tile_counts;           // [tiles]
-    uint32_t* tile_offsets;          // [tiles]
+    uint32_t depth_blocks;           // 2-D k_mask blocks over the emitting cameras
+    uint32_t sel_tiles;              // 1-D k_mask blocks over the selected rollbuffer points
+    uint8_t* stage;                  // [n] stage bits per item (also the debug masks)
+    uint32_t* tile_counts;           // [tiles] valid items per count tile (zero on entry)
+    uint32_t* tile_offsets;          // [tiles] (k_scan_counts path)
+    int32_t fused_prefix;            // k_emit sums the preceding tile counts itself
+    uint32_t* zero_counts;           // fused path: the other count buffer, cleared for the next frame
+    uint32_t zero_tiles;
     uint32_t* err;
 };
 static_assert(sizeof(FrameArgs) <= 4096, "kernel arguments are limited to 4 KiB");
@@ -111,9 +126,13 @@ __device__ __forceinline__ void normalize3(float& x, float& y, float& z) {
 
 // sh/convert_depthmap_to_points.glsl:64-81 (u = idx mod W, v = idx / W):
 // p = ((u-cx)/fx · z, (v-cy)/fy · z, z) with z = f32(d)·scale
+__device__ __forceinline__ uint32_t div_w(const CamDesc& c, uint32_t local) {
+    return (uint32_t)(((unsigned long long)local * c.wmagic) >> 40);
+}
+
 __device__ __forceinline__ void cam_point(const CamDesc& c, uint32_t local, uint32_t d, float& x,
                                           float& y, float& z) {
-    const uint32_t v = local / c.W;
+    const uint32_t v = div_w(c, local);
     const uint32_t u = local - v * c.W;
     const float zz = (float)d * c.scale;
     x = c.xn[u] * zz;

@@ -177,6 +177,7 @@ struct gdf_engine {
     DevBuf d_depth;
     std::vector<CamTable> tables = std::vector<CamTable>(kMaxCams);
     std::vector<CamDesc> h_cams;
+    uint32_t mask_blocks = 0;       // 2-D k_mask blocks over the emitting cameras
     bool depth_uploaded = false;
 
     // new sequences on the device
@@ -214,7 +215,10 @@ struct gdf_engine {
     bool khist_pending = false;     // accumulated by a fused k_frame, not yet consumed
 
     // compaction outputs
-    DevBuf d_pts, d_coords, d_status, d_tcounts, d_toffsets, d_dbg;
+    DevBuf d_pts, d_coords, d_stage, d_tcounts, d_toffsets, d_camdesc;
+    uint32_t cnt_cap = 0;           // count tiles per half of d_tcounts
+    uint32_t cnt_dirty[2] = {0, 0};  // tiles possibly non-zero in each half
+    int cnt_parity = 0;
     DevBuf d_misc;
     uint32_t* h_misc = nullptr;  // pinned
     bool compacted = false, coords_valid = false, marks_set = false;
@@ -540,6 +544,7 @@ void upload_depthmaps(gdf_engine* e) {  // fusion.cpp:1583-1593
     if (host_px) e->d_depth.ensure(host_px * 2);
     if (e->cams.size() + e->halo.size() > (size_t)kMaxCams) fail(GDF_ERR_ARG, "too many cameras (incl. halo)");
     e->h_cams.clear();
+    e->mask_blocks = 0;
     uint64_t off = 0, hoff = 0;
     for (size_t k = 0; k < e->cams.size(); ++k) {
         const Cam& c = e->cams[k];
@@ -558,6 +563,11 @@ void upload_depthmaps(gdf_engine* e) {  // fusion.cpp:1583-1593
         d.yn = e->tables[e->halo.size() + k].yn.as<float>();
         d.W = c.W; d.H = c.H; d.n = c.n; d.emit = 1;
         d.scale = c.scale;
+        d.wmagic = ((1ull << 40) + c.W - 1) / c.W;
+        d.tiles_x = (c.W + kTileW - 1) / kTileW;
+        d.nblocks = d.tiles_x * ((c.H + kTileH - 1) / kTileH);
+        d.block0 = e->mask_blocks;
+        e->mask_blocks += d.nblocks;
         std::memcpy(d.Tw, c.Tw, 64);
         std::memcpy(d.Tc, c.Tc, 64);
         e->h_cams.push_back(d);
@@ -626,13 +636,20 @@ void run_frame(gdf_engine* e, bool fused_voxel) {
     if (!e->depth_uploaded) upload_depthmaps(e);
     ensure_misc(e);
     FrameArgs a{};
-    for (size_t k = 0; k < e->h_cams.size(); ++k) a.cams[k] = e->h_cams[k];
     a.ncams = (int32_t)e->h_cams.size();
+    if (a.ncams <= kArgCams) {
+        for (size_t k = 0; k < e->h_cams.size(); ++k) a.cams[k] = e->h_cams[k];
+    } else {  // pageable source: the copy is staged before hipMemcpyAsync returns
+        e->d_camdesc.ensure(e->h_cams.size() * sizeof(CamDesc));
+        HIPCHK(hipMemcpyAsync(e->d_camdesc.p, e->h_cams.data(), e->h_cams.size() * sizeof(CamDesc),
+                              hipMemcpyHostToDevice, e->s()));
+        a.cams_dev = e->d_camdesc.as<const CamDesc>();
+    }
     a.depth_total = e->depth_total;
-    a.depth_tiles = (e->depth_total + kFrameTile - 1) / kFrameTile;
     const uint32_t sel = e->sel_inserted ? e->rb.selection_point_count : 0u;
-    const uint32_t sel_tiles = (sel + kFrameTile - 1) / kFrameTile;
-    a.total_tiles = a.depth_tiles + sel_tiles;
+    a.depth_blocks = e->mask_blocks;
+    a.sel_tiles = (sel + kFrameThreads - 1) / kFrameThreads;
+    a.total_tiles = (e->depth_total + sel + kFrameTile - 1) / kFrameTile;  // count tiles
     a.do_flying = e->flying_set ? 1 : 0;
     a.F = e->F;
     a.thr = e->thr;
@@ -664,20 +681,35 @@ void run_frame(gdf_engine* e, bool fused_voxel) {
     a.out_pts = e->d_pts.as<float4>();
     a.out_coords = e->d_coords.as<uint32_t>();
     a.out_count = e->d_misc.as<uint32_t>() + kCount;
-    if (e->debug) {
-        e->d_dbg.ensure((size_t)std::max<uint32_t>(e->n_total, 1));
-        a.dbg = e->d_dbg.as<uint8_t>();
-        e->dbg_count = e->n_total;
+    // Two count buffers: a fused-prefix frame counts into half p while its k_emit clears what the
+    // previous frame left in the other half, which the next frame then uses (no memset per frame);
+    // the k_scan_counts path clears its own half.  Invariant: cnt_dirty[cnt_parity] == 0.
+    const uint32_t tiles = std::max<uint32_t>(a.total_tiles, 1);
+    e->d_stage.ensure((size_t)std::max<uint32_t>(e->n_total, 1));
+    if (tiles > e->cnt_cap) {
+        const uint32_t cap = std::max<uint32_t>(tiles, e->cnt_cap + e->cnt_cap / 2);
+        e->d_tcounts.ensure_zero((size_t)2 * cap * 4, e->s());
+        e->cnt_cap = cap;
+        e->cnt_dirty[0] = e->cnt_dirty[1] = 0;
     }
-    const size_t tiles = std::max<uint32_t>(a.total_tiles, 1);
-    e->d_status.ensure(tiles * (kFrameTile / 64) * 8);
-    e->d_tcounts.ensure(tiles * 4);
-    e->d_toffsets.ensure(tiles * 4);
-    a.valid_bits = e->d_status.as<unsigned long long>();
-    a.tile_counts = e->d_tcounts.as<uint32_t>();
+    e->d_toffsets.ensure((size_t)tiles * 4);
+    const int p = e->cnt_parity;
+    a.stage = e->d_stage.as<uint8_t>();
+    a.tile_counts = e->d_tcounts.as<uint32_t>() + (size_t)p * e->cnt_cap;
     a.tile_offsets = e->d_toffsets.as<uint32_t>();
+    a.fused_prefix = a.total_tiles <= kFusedPrefixTiles ? 1 : 0;
+    if (a.fused_prefix) {
+        a.zero_counts = e->d_tcounts.as<uint32_t>() + (size_t)(1 - p) * e->cnt_cap;
+        a.zero_tiles = e->cnt_dirty[1 - p];
+    }
+    e->dbg_count = e->n_total;
     a.err = e->d_misc.as<uint32_t>() + kErr;
     e->timed(GDF_KERNEL_FRAME, [&] { HIPCHK(launch_frame(a, e->s())); });
+    if (a.fused_prefix && a.total_tiles) {
+        e->cnt_dirty[p] = a.total_tiles;
+        e->cnt_dirty[1 - p] = 0;
+        e->cnt_parity = 1 - p;
+    }
     e->khist_pending = fused_voxel;
     e->compacted = true;
     e->coords_valid = fused_voxel;
@@ -1245,12 +1277,12 @@ int gdf_set_debug(gdf_engine* e, int enable) {
 int gdf_debug_stage_masks(gdf_engine* e, uint8_t* out, uint32_t cap, uint32_t* out_count) {
     ENGINE_OR_FAIL(e);
     return guarded(e, [&] {
-        if (!e->debug || !e->d_dbg.p) fail(GDF_ERR_STATE, "debug masks not enabled");
+        if (!e->d_stage.p || !e->compacted) fail(GDF_ERR_STATE, "no compaction has run");
         if (out_count) *out_count = e->dbg_count;
         if (out) {
             if (cap < e->dbg_count) fail(GDF_ERR_CAPACITY, "debug masks: buffer too small");
             e->sync();
-            if (e->dbg_count) HIPCHK(hipMemcpy(out, e->d_dbg.p, e->dbg_count, hipMemcpyDeviceToHost));
+            if (e->dbg_count) HIPCHK(hipMemcpy(out, e->d_stage.p, e->dbg_count, hipMemcpyDeviceToHost));
         }
     });
 }

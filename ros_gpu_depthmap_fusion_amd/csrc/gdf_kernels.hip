@@ -287,7 +287,7 @@ __device__ __forceinline__ Nb nb_load(const CamDesc* cams, int ncams, int k, int
     if (j >= 0) {
         const CamDesc& c = cams[j];
         const uint32_t local = (uint32_t)(gi - c.off);
-        const uint32_t v = local / c.W;
+        const uint32_t v = div_w(c, local);
         const uint32_t u = local - v * c.W;
         r.d = c.depth[local];
         r.xn = c.xn[u];
@@ -316,6 +316,23 @@ __device__ __forceinline__ void ring_idx(int64_t g, int64_t iw, uint32_t i, bool
 
 // The surface test of check_at / check_at_rot45 (filter_flying_pixels.glsl:74-96) on loaded
 // neighbours: invalid if any mask is 0 or dot(normalize(cross(dy, dx)), -normalize(p)) < thr.
+// The exact value cv = dot3(c / sqrt(dd), n) is decided first by the filter
+// cva = dot3(c, n) · rsq(dd): both lie within 8 ulp(1) (≈5e-7) of the real (c·n)/|c| for
+// |n| ≈ 1, so outside thr ± 1e-5 the comparison cannot differ; inside it (and for dd outside
+// the normal range, incl. the NaN of a zero cross product) the exact reference sequence runs.
+__device__ __forceinline__ bool surface_ok(float cx, float cy, float cz, float thr, float nx,
+                                           float ny, float nz) {
+    const float dd = dot3(cx, cy, cz, cx, cy, cz);
+    if (dd > 1e-30f && dd < 1e30f) {
+        const float cva = dot3(cx, cy, cz, nx, ny, nz) * __builtin_amdgcn_rsqf(dd);
+        if (cva < thr - 1e-5f) return false;
+        if (cva > thr + 1e-5f) return true;
+    }
+    const float l = sqrtf(dd);
+    const float cv = dot3(cx / l, cy / l, cz / l, nx, ny, nz);
+    return !(cv < thr);  // NaN passes
+}
+
 __device__ __forceinline__ bool ring_ok(const Nb* n, float thr, float nx, float ny, float nz) {
     if (n[0].d == 0 || n[1].d == 0 || n[2].d == 0 || n[3].d == 0) return false;
     float ux, uy, uz, dx_, dy_, dz_, lx, ly, lz, rx, ry, rz;
@@ -328,57 +345,71 @@ __device__ __forceinline__ bool ring_ok(const Nb* n, float thr, float nx, float 
     float cx = ay * bz - az * by;
     float cy = az * bx - ax * bz;
     float cz = ax * by - ay * bx;
-    normalize3(cx, cy, cz);
-    const float cv = dot3(cx, cy, cz, nx, ny, nz);
-    return !(cv < thr);  // NaN passes
+    return surface_ok(cx, cy, cz, thr, nx, ny, nz);
 }
 
-// Stage bits of depth item g (bit0 convert, bit1 flying, bit2 crop): convert_depthmap_to_points
-// (:83-120) -> filter_flying_pixels (:135-165) -> crop_points (:38-67).  Ring i+1's neighbour
-// loads are issued before ring i is evaluated, so the flying filter costs ~one memory trip.
+// Stage bits of a depth pixel (bit0 convert, bit1 flying, bit2 crop):
+// convert_depthmap_to_points (:83-120) -> filter_flying_pixels (:135-165) -> crop_points (:38-67).
+// Neighbours come from the block's LDS depth tile (2-D offsets) whenever the reference's linear
+// index arithmetic stays inside the camera without wrapping; the wrap cases (x < i: the left
+// neighbour is the previous row's end; y < i: the previous camera or out of bounds, A.6/A.7) and
+// rings beyond the LDS halo take the exact linear-index global path.
+struct Tile {
+    const uint16_t* d;  // s_depth [kTileH + 2h][lw]
+    const float* xn;    // s_xn [lw]
+    const float* yn;    // s_yn [kTileH + 2h]
+    int lw;             // row stride kTileW + 2h
+    uint32_t h;         // halo width min(F, kHalo)
+};
+
+__device__ __forceinline__ Nb lds_nb(const Tile& t, int lx, int ly, float scale) {
+    Nb r;
+    r.d = t.d[ly * t.lw + lx];
+    r.xn = t.xn[lx];
+    r.yn = t.yn[ly];
+    r.scale = scale;
+    return r;
+}
+
 template <bool ROT45>
 __device__ __forceinline__ uint32_t depth_bits(const FrameArgs& a, const CamDesc* cams, int k,
-                                               uint32_t local, uint32_t d) {
+                                               const Tile& t, uint32_t x, uint32_t y, int lx,
+                                               int ly, uint32_t d) {
     if (d == 0) return 0;
     const CamDesc& c = cams[k];
-    float px, py, pz;
-    cam_point(c, local, d, px, py, pz);
+    const float zz = (float)d * c.scale;
+    const float px = t.xn[lx] * zz, py = t.yn[ly] * zz, pz = zz;
     if (a.do_flying) {
         if (sqrtf(dot3(px, py, pz, px, py, pz)) > 10.0f) return 1;  // max_distance (:41,:143)
         float nx = px, ny = py, nz = pz;
         normalize3(nx, ny, nz);
         nx = -nx; ny = -ny; nz = -nz;
-        const uint32_t y = local / c.W, x = local - y * c.W;
-        const int64_t g = c.off + local;
-        constexpr int nv = ROT45 ? 2 : 1;
-        Nb cur[4 * nv], nxt[4 * nv];
-        int64_t q[4];
-        // rings whose bounds test fails never load (x+i > W-1 || y+i > H-1 -> invalid)
-        const uint32_t F = a.F;
-        if (F >= 1 && (x + 1 > c.W - 1 || y + 1 > c.H - 1)) return 1;
-        if (F >= 1) {
+        const int64_t g = c.off + (int64_t)y * c.W + x;
+        for (uint32_t i = 1; i <= a.F; ++i) {
+            if (x + i > c.W - 1 || y + i > c.H - 1) return 1;  // bounds (:60; x-i<0 never true)
+            const int64_t iw = (int64_t)i * c.W;
+            const bool lds = i <= t.h;
+            const bool xw = x < i, yw = y < i;  // wrap / cross-camera cases
+            const int ii = (int)i;
 #pragma unroll
-            for (int v = 0; v < nv; ++v) {
-                ring_idx(g, (int64_t)c.W, 1u, v == 1, q);
-#pragma unroll
-                for (int t = 0; t < 4; ++t) cur[4 * v + t] = nb_load(cams, a.ncams, k, q[t]);
-            }
-        }
-        for (uint32_t i = 1; i <= F; ++i) {
-            const bool more = i < F && !(x + i + 1 > c.W - 1 || y + i + 1 > c.H - 1);
-            if (more) {
-#pragma unroll
-                for (int v = 0; v < nv; ++v) {
-                    ring_idx(g, (int64_t)(i + 1) * c.W, i + 1, v == 1, q);
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) nxt[4 * v + t] = nb_load(cams, a.ncams, k, q[t]);
+            for (int v = 0; v < (ROT45 ? 2 : 1); ++v) {
+                Nb n[4];
+                if (v == 0) {  // up (x, y-i), down (x, y+i), left (x-i, y), right (x+i, y)
+                    n[0] = (lds && !yw) ? lds_nb(t, lx, ly - ii, c.scale) : nb_load(cams, a.ncams, k, g - iw);
+                    n[1] = lds ? lds_nb(t, lx, ly + ii, c.scale) : nb_load(cams, a.ncams, k, g + iw);
+                    n[2] = (lds && !xw) ? lds_nb(t, lx - ii, ly, c.scale) : nb_load(cams, a.ncams, k, g - ii);
+                    n[3] = lds ? lds_nb(t, lx + ii, ly, c.scale) : nb_load(cams, a.ncams, k, g + ii);
+                } else {  // up (x-i, y-i), down (x+i, y+i), left (x-i, y+i), right (x+i, y-i)
+                    n[0] = (lds && !xw && !yw) ? lds_nb(t, lx - ii, ly - ii, c.scale)
+                                               : nb_load(cams, a.ncams, k, g - iw - ii);
+                    n[1] = lds ? lds_nb(t, lx + ii, ly + ii, c.scale) : nb_load(cams, a.ncams, k, g + iw + ii);
+                    n[2] = (lds && !xw) ? lds_nb(t, lx - ii, ly + ii, c.scale)
+                                        : nb_load(cams, a.ncams, k, g + iw - ii);
+                    n[3] = (lds && !yw) ? lds_nb(t, lx + ii, ly - ii, c.scale)
+                                        : nb_load(cams, a.ncams, k, g - iw + ii);
                 }
+                if (!ring_ok(n, a.thr, nx, ny, nz)) return 1;
             }
-            if (!ring_ok(cur, a.thr, nx, ny, nz)) return 1;
-            if (ROT45 && !ring_ok(cur + 4, a.thr, nx, ny, nz)) return 1;
-            if (i < F && !more) return 1;  // next ring fails its bounds test
-#pragma unroll
-            for (int t = 0; t < 4 * nv; ++t) cur[t] = nxt[t];
         }
     }
     if (a.do_crop) {
@@ -429,60 +460,101 @@ __device__ __forceinline__ uint32_t sel_bits(const FrameArgs& a, uint32_t i, flo
 
 __device__ __forceinline__ void load_cams(const FrameArgs& a, CamDesc* s_cams) {
     const uint32_t words = (uint32_t)a.ncams * (uint32_t)(sizeof(CamDesc) / 4);
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.cams);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.ncams <= kArgCams ? a.cams : a.cams_dev);
     uint32_t* dst = reinterpret_cast<uint32_t*>(s_cams);
     for (uint32_t w = threadIdx.x; w < words; w += blockDim.x) dst[w] = src[w];
 }
 
-// Pass 1 of the ordered compaction (apply_point_mask.glsl:42-55 made stable): per item stage
-// bits, one 64-bit validity ballot per wave and the valid count per 1024-item tile.
+// valid-count of one wave's 64 consecutive items starting at item g0 into the count tiles
+// (a 64-item run straddles at most two 256-item tiles)
+__device__ __forceinline__ void add_counts(uint32_t* counts, unsigned long long m, uint32_t g0) {
+    if (!m) return;
+    const uint32_t t0 = g0 / kFrameTile;
+    const uint32_t cut = (t0 + 1) * kFrameTile - g0;  // lanes [0, cut) belong to t0
+    if (cut >= 64) {
+        atomicAdd(&counts[t0], (uint32_t)__popcll(m));
+    } else {
+        const unsigned long long lo = (1ull << cut) - 1ull;
+        const uint32_t a = (uint32_t)__popcll(m & lo), b = (uint32_t)__popcll(m & ~lo);
+        if (a) atomicAdd(&counts[t0], a);
+        if (b) atomicAdd(&counts[t0 + 1], b);
+    }
+}
+
+// Pass 1 of the ordered compaction (apply_point_mask.glsl:42-55 made stable).  Depth blocks: a
+// 64x16 pixel tile of one camera with an 8-pixel LDS halo (depth + ray factors), one column per
+// lane, 4 rows per wave; rollbuffer blocks: 256 selected points.  Writes the stage bits of every
+// item and adds the valid counts of every 256-item count tile.
 template <bool ROT45>
 __global__ __launch_bounds__(kFrameThreads) void k_mask(FrameArgs a) {
     __shared__ CamDesc s_cams[kMaxCams];
-    __shared__ uint32_t s_cnt[kFrameThreads / 64];
+    __shared__ uint16_t s_depth[(kTileH + 2 * kHalo) * (kTileW + 2 * kHalo)];
+    __shared__ float s_xn[kTileW + 2 * kHalo];
+    __shared__ float s_yn[kTileH + 2 * kHalo];
     load_cams(a, s_cams);
     __syncthreads();
-    const uint32_t tile = blockIdx.x;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint32_t bits = 0, item;
-    bool in_range;
-    if (tile < a.depth_tiles) {
-        item = tile * kFrameTile + threadIdx.x;
-        in_range = item < a.depth_total;
-        if (in_range) {
-            const int k = find_cam(s_cams, a.ncams, (int64_t)item);
-            const uint32_t local = (uint32_t)((int64_t)item - s_cams[k].off);
-            bits = depth_bits<ROT45>(a, s_cams, k, local, s_cams[k].depth[local]);
+    const uint32_t b = blockIdx.x;
+    if (b < a.depth_blocks) {
+        int k = 0;
+        for (int c = 0; c < a.ncams; ++c)
+            if (s_cams[c].emit && b >= s_cams[c].block0 && b < s_cams[c].block0 + s_cams[c].nblocks) k = c;
+        const CamDesc& c = s_cams[k];
+        const uint32_t t = b - c.block0;
+        const uint32_t ty = t / c.tiles_x, tx = t - ty * c.tiles_x;
+        const int c0 = (int)(tx * kTileW), r0 = (int)(ty * kTileH);
+        const int h = a.do_flying ? (int)min(a.F, (uint32_t)kHalo) : 0;
+        const int lw = kTileW + 2 * h, lh = kTileH + 2 * h;
+        // depth tile + halo (rows by wave, columns by lane; outside the camera -> 0, never read)
+        for (int row = wid; row < lh; row += kFrameThreads / 64) {
+            const int gy = r0 - h + row;
+            const bool rin = gy >= 0 && gy < (int)c.H;
+            for (int col = lane; col < lw; col += 64) {
+                const int gx = c0 - h + col;
+                s_depth[row * lw + col] = (rin && gx >= 0 && gx < (int)c.W)
+                                              ? c.depth[(uint32_t)gy * c.W + (uint32_t)gx] : (uint16_t)0;
+            }
+        }
+        if (threadIdx.x < (unsigned)lw) {
+            const int gx = c0 - h + (int)threadIdx.x;
+            s_xn[threadIdx.x] = (gx >= 0 && gx < (int)c.W) ? c.xn[gx] : 0.0f;
+        } else if (threadIdx.x - lw < (unsigned)lh) {
+            const int row = (int)threadIdx.x - lw;
+            const int gy = r0 - h + row;
+            s_yn[row] = (gy >= 0 && gy < (int)c.H) ? c.yn[gy] : 0.0f;
+        }
+        __syncthreads();
+        const Tile tl{s_depth, s_xn, s_yn, lw, (uint32_t)h};
+        const uint32_t x = (uint32_t)(c0 + lane);
+        const uint32_t y = (uint32_t)(r0 + wid);
+        if (y < c.H) {  // wave-uniform
+            const int lx = lane + h, ly = wid + h;
+            uint32_t bits = 0;
+            const bool in = x < c.W;
+            if (in) bits = depth_bits<ROT45>(a, s_cams, k, tl, x, y, lx, ly, tl.d[ly * lw + lx]);
+            const uint32_t item = (uint32_t)c.off + y * c.W + (uint32_t)c0;  // item of lane 0
+            if (in) a.stage[item + lane] = (uint8_t)bits;
+            const unsigned long long m = __ballot((bits & 4) != 0);
+            if (lane == 0) add_counts(a.tile_counts, m, item);
         }
     } else {
-        const uint32_t i = (tile - a.depth_tiles) * kFrameTile + threadIdx.x;
-        item = a.depth_total + i;
-        in_range = i < a.sel_count;
-        if (in_range) {
+        const uint32_t i = (b - a.depth_blocks) * kFrameThreads + threadIdx.x;
+        uint32_t bits = 0;
+        if (i < a.sel_count) {
             float4 p;
-            uint32_t t;
-            bits = sel_bits(a, i, p, t);
+            uint32_t tf;
+            bits = sel_bits(a, i, p, tf);
+            a.stage[a.depth_total + i] = (uint8_t)bits;
         }
-    }
-    const unsigned long long m = __ballot((bits & 4) != 0);
-    if (lane == 0) {
-        a.valid_bits[(size_t)tile * (kFrameTile / 64) + wid] = m;
-        s_cnt[wid] = (uint32_t)__popcll(m);
-    }
-    if (a.dbg && in_range) a.dbg[item] = (uint8_t)bits;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t c = 0;
-#pragma unroll
-        for (int w = 0; w < kFrameThreads / 64; ++w) c += s_cnt[w];
-        a.tile_counts[tile] = c;
+        const unsigned long long m = __ballot((bits & 4) != 0);
+        if (lane == 0) add_counts(a.tile_counts, m, a.depth_total + (i - (uint32_t)lane));
     }
 }
 
 // Exclusive scan of the tile counts by one workgroup (chunks of 4096 with a running carry);
-// writes the total (m_numItemsAfterMask) too.
-__global__ __launch_bounds__(1024) void k_scan_counts(const uint32_t* __restrict__ counts,
-                                                      uint32_t m, uint32_t* __restrict__ offsets,
+// writes the total (m_numItemsAfterMask) and re-zeroes the counts for the next frame.
+__global__ __launch_bounds__(1024) void k_scan_counts(uint32_t* __restrict__ counts, uint32_t m,
+                                                      uint32_t* __restrict__ offsets,
                                                       uint32_t* __restrict__ total) {
     __shared__ uint32_t s_w[16];
     __shared__ uint32_t s_carry;
@@ -495,6 +567,7 @@ __global__ __launch_bounds__(1024) void k_scan_counts(const uint32_t* __restrict
         for (int q = 0; q < 4; ++q) {
             const uint32_t i = base + threadIdx.x * 4 + q;
             v[q] = i < m ? counts[i] : 0u;
+            if (i < m) counts[i] = 0u;
             sum += v[q];
         }
         uint32_t x = sum;
@@ -526,54 +599,93 @@ __global__ __launch_bounds__(1024) void k_scan_counts(const uint32_t* __restrict
     if (threadIdx.x == 0) *total = s_carry;
 }
 
-// Pass 2: each valid item recomputes its world point (the same f32 ops as pass 1) and writes it
-// at tile offset + rank (ballot popcount): stable pixel order, cameras in add order, selected
-// rollbuffer points after the depth points (fusion.cpp:1525,1559).  Optionally the voxel key
-// (compute_voxel_coords), the occupancy mark (voxel_grid_occupancy_of_points, as a no-return
-// atomic OR of bit 7) and the digit histogram of the keys for the radix sort.
+// Pass 2: item-ordered emission.  Each valid item (stage bit 2) recomputes its world point with
+// the same f32 ops as pass 1 and writes it at tile offset + rank: stable pixel order, cameras in
+// add order, selected rollbuffer points after the depth points (fusion.cpp:1525,1559).
+// Optionally the voxel key (compute_voxel_coords), the occupancy mark (no-return atomic OR of
+// bit 7, issued once per run of equal keys in a wave) and the key digit histogram.
 __global__ __launch_bounds__(kEmitThreads) void k_emit(FrameArgs a) {
     __shared__ CamDesc s_cams[kMaxCams];
     __shared__ uint32_t s_hist[4 * 256];
+    __shared__ uint32_t s_wc[kEmitThreads / 64];
+    __shared__ uint32_t s_red[kEmitThreads / 64];
     load_cams(a, s_cams);
     if (a.key_hist)
         for (uint32_t i = threadIdx.x; i < a.npasses * 256; i += kEmitThreads) s_hist[i] = 0;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t n = a.depth_total + a.sel_count;
+    const uint32_t item = blockIdx.x * kEmitThreads + threadIdx.x;
+    const uint32_t bits = item < n ? a.stage[item] : 0u;
+    const bool valid = (bits & 4) != 0;
+    const unsigned long long m = __ballot(valid);
+    if (lane == 0) s_wc[wid] = (uint32_t)__popcll(m);
+    // block base: the preceding tiles' counts summed here (fused) or the scanned offset
+    const uint32_t t0 = blockIdx.x * (kEmitThreads / kFrameTile);
+    if (a.fused_prefix) {
+        uint32_t sum = 0;
+        for (uint32_t t = threadIdx.x; t < t0; t += kEmitThreads) sum += a.tile_counts[t];
+        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+        if (lane == 0) s_red[wid] = sum;
+        for (uint32_t t = blockIdx.x * kEmitThreads + threadIdx.x; t < a.zero_tiles;
+             t += gridDim.x * kEmitThreads)
+            a.zero_counts[t] = 0u;
+    }
     __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const uint32_t gidx = blockIdx.x * kEmitThreads + threadIdx.x;  // item index in tile space
-    const uint32_t tile = gidx / kFrameTile;
-    if (tile < a.total_tiles) {
-        const uint32_t wt = (gidx % kFrameTile) >> 6;  // wave within the count tile
-        const unsigned long long* vb = a.valid_bits + (size_t)tile * (kFrameTile / 64);
-        const unsigned long long m = vb[wt];
-        uint32_t before = 0;
-        for (uint32_t w = 0; w < wt; ++w) before += (uint32_t)__popcll(vb[w]);
-        if ((m >> lane) & 1ull) {
-            const uint32_t pos = a.tile_offsets[tile] + before +
-                                 (uint32_t)__popcll(m & (lane ? (~0ull >> (64 - lane)) : 0ull));
-            float4 w;
-            if (tile < a.depth_tiles) {
-                const uint32_t item = gidx;
-                const int k = find_cam(s_cams, a.ncams, (int64_t)item);
-                const uint32_t local = (uint32_t)((int64_t)item - s_cams[k].off);
-                w = depth_world(s_cams[k], local, s_cams[k].depth[local]);
-            } else {
-                const uint32_t i = gidx - a.depth_tiles * kFrameTile;
-                const float4 p = a.ring[(a.ring_first + i) % a.ring_cap];
-                const float* Tw = a.tfw + 16 * (size_t)sel_tf(a, i);
-                w = make_float4(mrow(Tw + 0, p.x, p.y, p.z, 1.0f), mrow(Tw + 4, p.x, p.y, p.z, 1.0f),
-                                mrow(Tw + 8, p.x, p.y, p.z, 1.0f), mrow(Tw + 12, p.x, p.y, p.z, 1.0f));
-            }
-            a.out_pts[pos] = w;
-            if (a.do_voxel) {
-                const uint32_t key = voxel_key(w.x, w.y, w.z, a.vlo, a.vcs, a.gmax, a.gs);
-                a.out_coords[pos] = key;
-                if (a.occ_mode == 1)
-                    atomicOr(reinterpret_cast<uint32_t*>(a.occ + (key & ~3u)), 0x80u << (8 * (key & 3u)));
-                else if (a.occ_mode == 2)
-                    a.occ[key] = 1;
-                if (a.key_hist)
-                    for (uint32_t p = 0; p < a.npasses; ++p)
-                        atomicAdd(&s_hist[p * 256 + ((key >> (8 * p)) & 0xFFu)], 1u);
+    uint32_t base = 0, blk = 0;
+    if (a.fused_prefix) {
+#pragma unroll
+        for (int w = 0; w < kEmitThreads / 64; ++w) base += s_red[w];
+    } else {
+        base = a.tile_offsets[t0];
+    }
+    uint32_t before = 0;
+#pragma unroll
+    for (int w = 0; w < kEmitThreads / 64; ++w) {
+        before += (w < wid) ? s_wc[w] : 0u;
+        blk += s_wc[w];
+    }
+    if (a.fused_prefix && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *a.out_count = base + blk;
+    const unsigned long long ltm = lane ? (~0ull >> (64 - lane)) : 0ull;
+    uint32_t key = 0xFFFFFFFFu;
+    if (valid) {
+        const uint32_t pos = base + before + (uint32_t)__popcll(m & ltm);
+        float4 w;
+        if (item < a.depth_total) {
+            const int k = find_cam(s_cams, a.ncams, (int64_t)item);
+            const uint32_t local = (uint32_t)((int64_t)item - s_cams[k].off);
+            w = depth_world(s_cams[k], local, s_cams[k].depth[local]);
+        } else {
+            const uint32_t i = item - a.depth_total;
+            const float4 p = a.ring[(a.ring_first + i) % a.ring_cap];
+            const float* Tw = a.tfw + 16 * (size_t)sel_tf(a, i);
+            w = make_float4(mrow(Tw + 0, p.x, p.y, p.z, 1.0f), mrow(Tw + 4, p.x, p.y, p.z, 1.0f),
+                            mrow(Tw + 8, p.x, p.y, p.z, 1.0f), mrow(Tw + 12, p.x, p.y, p.z, 1.0f));
+        }
+        a.out_pts[pos] = w;
+        if (a.do_voxel) {
+            key = voxel_key(w.x, w.y, w.z, a.vlo, a.vcs, a.gmax, a.gs);
+            a.out_coords[pos] = key;
+        }
+    }
+    if (a.do_voxel) {
+        // runs of equal keys among the wave's valid lanes: the first lane of a run marks / counts
+        const unsigned long long below = m & ltm;
+        const int prev = below ? 63 - __clzll((long long)below) : -1;
+        const uint32_t pkey = __shfl(key, prev < 0 ? 0 : prev, 64);
+        const bool leader = valid && (prev < 0 || pkey != key);
+        const unsigned long long lm = __ballot(leader);
+        if (leader) {
+            if (a.occ_mode == 1)
+                atomicOr(reinterpret_cast<uint32_t*>(a.occ + (key & ~3u)), 0x80u << (8 * (key & 3u)));
+            else if (a.occ_mode == 2)
+                a.occ[key] = 1;
+            if (a.key_hist) {
+                const unsigned long long after = lm & ~(ltm | (1ull << lane));
+                const unsigned long long upto = after ? ((1ull << (__ffsll((long long)after) - 1)) - 1ull)
+                                                      : ~0ull;
+                const uint32_t run = (uint32_t)__popcll(m & ~ltm & upto);
+                for (uint32_t p = 0; p < a.npasses; ++p)
+                    atomicAdd(&s_hist[p * 256 + ((key >> (8 * p)) & 0xFFu)], run);
             }
         }
     }
@@ -586,15 +698,21 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(FrameArgs a) {
 
 hipError_t launch_frame(const FrameArgs& a, hipStream_t s) {
     if (a.total_tiles == 0) return hipMemsetAsync(a.out_count, 0, 4, s);
-    if (a.rot45)
-        hipLaunchKernelGGL(k_mask<true>, dim3(a.total_tiles), dim3(kFrameThreads), 0, s, a);
-    else
-        hipLaunchKernelGGL(k_mask<false>, dim3(a.total_tiles), dim3(kFrameThreads), 0, s, a);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, a.tile_counts, a.total_tiles,
-                       a.tile_offsets, a.out_count);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const uint32_t mblocks = a.depth_blocks + a.sel_tiles;
+    if (mblocks) {
+        if (a.rot45)
+            hipLaunchKernelGGL(k_mask<true>, dim3(mblocks), dim3(kFrameThreads), 0, s, a);
+        else
+            hipLaunchKernelGGL(k_mask<false>, dim3(mblocks), dim3(kFrameThreads), 0, s, a);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    if (!a.fused_prefix) {
+        hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, a.tile_counts, a.total_tiles,
+                           a.tile_offsets, a.out_count);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     const uint32_t eblocks = (a.total_tiles * kFrameTile + kEmitThreads - 1) / kEmitThreads;
     hipLaunchKernelGGL(k_emit, dim3(eblocks), dim3(kEmitThreads), 0, s, a);
     return hipGetLastError();

@@ -85,6 +85,45 @@ def test_multicamera_cross_camera_border_semantics(Engine):
     compare_results(gpu, orc)
 
 
+def test_six_cameras_mixed_sizes_rings_beyond_lds_halo(Engine):
+    """More cameras than travel in the kernel arguments (descriptors read from the device),
+    ragged sizes (tiles cut at right/bottom borders) and F=9: rings 1..8 read the LDS depth tile,
+    ring 9 the linear-index global path; rot45 doubles every ring."""
+    p = ComponentParams()
+    p.flying_filter_size = 9
+    p.flying_rot45 = True
+    p.flying_threshold = 0.1
+    gpu, orc = Engine(), OracleFusion(threads=8)
+    gpu.set_debug(True)
+    sizes = [(64, 48), (100, 75), (33, 20), (128, 96), (50, 50), (80, 61)]
+    cams = [synth.make_camera(k, w, h) for k, (w, h) in enumerate(sizes)]
+    for f in range(2):
+        args = [cam_args(c, synth.depth_frame(c, k, f)) for k, c in enumerate(cams)]
+        run_fused(gpu, args, p)
+        run_fused(orc, args, p)
+        np.testing.assert_array_equal((gpu.stage_masks() & 4) != 0,
+                                      orc.stage_arrays()["maskA"] != 0)
+        compare_results(gpu, orc, tag=f"frame {f}")
+
+
+def test_alternating_frame_sizes_count_buffers(Engine):
+    """Frames alternating between > 1 Mi items (separate tile-count scan) and small frames
+    (k_emit sums the tile counts; the two count buffers are cleared frame to frame) in one
+    engine."""
+    p = ComponentParams()
+    gpu, orc = Engine(), OracleFusion(threads=8)
+    big = synth.make_camera(0, 1280, 960)
+    small = synth.make_camera(1, 160, 120)
+    mid = synth.make_camera(2, 640, 480)
+    seq = [big, small, small, big, mid, big, mid, mid, small]
+    for f, cam in enumerate(seq):
+        args = [cam_args(cam, synth.depth_frame(cam, f % 3, f))]
+        r = run_fused(gpu, args, p)
+        run_fused(orc, args, p)
+        assert r.num_points == orc.point_count(), f"frame {f}"
+        compare_results(gpu, orc, tag=f"frame {f}")
+
+
 def test_uniform_random_depth_stress(Engine):
     p = ComponentParams()
     p.flying_rot45 = True
