@@ -95,12 +95,15 @@ def main():
         local_bits = torch.zeros(words, dtype=torch.int32, device="cuda")
         all_bits = torch.zeros(world * words, dtype=torch.int32, device="cuda")
 
+    pc_plain = params.to_c(None, None, False, False)
+    pc_defer = params.to_c(None, None, False, True)
+
     def step(i):
         add(i)
         if dist is None:
-            eng.processFrame(params, synchronous=False)
+            eng.processFramePrepared(pc_plain)
         else:
-            eng.processFrame(params, synchronous=False, defer_occupancy_grid=True)
+            eng.processFramePrepared(pc_defer)
             eng.export_marks(local_bits.data_ptr(), words)
             dist.all_gather_into_tensor(all_bits, local_bits)
             eng.import_marks(all_bits.data_ptr(), words, world)
@@ -116,9 +119,6 @@ def main():
     for i in range(args.warmup):
         step(i)
     barrier_sync()
-    if not args.no_kernel_timing:
-        eng.set_profiling(True)
-    barrier_sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
@@ -129,7 +129,19 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    ktimes = eng.kernel_times() if not args.no_kernel_timing else None
+
+    # per-kernel durations: a separate pass over the same frames with an HIP event pair around
+    # every launch on the engine stream (kept out of the timed region: the extra event records
+    # cost host time)
+    ktimes = None
+    if not args.no_kernel_timing:
+        kt_steps = min(args.steps, 200)
+        eng.set_profiling(True)
+        for i in range(kt_steps):
+            step(args.warmup + i)
+        barrier_sync()
+        ktimes = eng.kernel_times()
+        eng.set_profiling(False)
 
     ms_per_step = elapsed / args.steps * 1e3
     value = world * P * args.steps / elapsed / 1e6
@@ -137,17 +149,28 @@ def main():
     idx = [(args.warmup + i) % args.ring for i in range(args.steps)]
     n_avg = float(np.mean([npts[i] for i in idx]))
     g_avg = float(np.mean([nvox[i] for i in idx]))
+    tiles = (P + 255) // 256
+    # algorithmic HBM bytes per launch of each kernel (DESIGN.md "Kernels and their rooflines"):
+    # the bytes the algorithm must move once, not the cache traffic of an implementation
     model_bytes = {
-        # algorithmic bytes per launch (DESIGN.md "Kernels and their rooflines")
-        "frame": 2.0 * P + 21.0 * n_avg,
+        "mask": 3.0 * P,                           # u16 depth in, u8 stage bits out
+        "scan": 8.0 * tiles,
+        "emit": 1.0 * P + 22.0 * n_avg,            # stage in, depth of kept px, xyzw + key out
+        # 3 radix passes (key only in, key+index out; then key+index both ways) + the grid
+        # update carried by the first pass, averaged per launch
+        "sort": (12.0 * n_avg + 16.0 * n_avg * 2 + 2.0 * ncells) / 3.0,
+        "group_scan": 4.0 * n_avg + 4.0 * g_avg,
+        "group_sum": 20.0 * n_avg + 20.0 * g_avg,  # indices + gathered points in, means out
         "grid": 2.0 * ncells,
-        "voxelize": 76.0 * n_avg + 16.0 * g_avg,
     }
     survey_bytes = 2.0 * P + 24.0 * n_avg + 9.0 * ncells  # SURVEY.md §8(d) B_alg per frame
 
     roofline = None
     if ktimes:
-        slot = max(("frame", "grid", "voxelize"), key=lambda k: ktimes[k][0])
+        singles = [k for k in ("mask", "scan", "emit", "sort", "group_scan", "group_sum", "grid")
+                   if ktimes[k][1]]
+        per_step = {k: ktimes[k][0] / kt_steps for k in singles}  # ms per step
+        slot = max(singles, key=lambda k: per_step[k])
         ms, n = ktimes[slot]
         avg_s = ms / 1e3 / max(n, 1)
         achieved = model_bytes[slot] / avg_s / 1e9
@@ -162,11 +185,11 @@ def main():
                 traffic = None
         roofline = {
             "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic,
             "kernel": slot, "avg_launch_us": round(avg_s * 1e6, 3),
+            "launches_per_step": round(n / kt_steps, 3),
             "bytes_per_launch": round(model_bytes[slot]),
-            "per_kernel_us": {k: round(v[0] * 1e3 / max(v[1], 1), 3) for k, v in ktimes.items()
-                              if v[1]},
+            "per_kernel_us": {k: round(ktimes[k][0] * 1e3 / ktimes[k][1], 3) for k in singles},
             "step_survey_bytes": round(survey_bytes),
             "step_survey_GBps": round(survey_bytes * args.steps / elapsed / 1e9, 2),
         }

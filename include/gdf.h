@@ -217,7 +217,14 @@ enum gdf_kernel_slot {
     GDF_KERNEL_GRID = 1,       /* k_grid_u8 / k_grid_u32: historic occupancy update              */
     GDF_KERNEL_VOXELIZE = 2,   /* radix sort passes + group mean                                  */
     GDF_KERNEL_PS_INSERT = 3,  /* point-sequence filter + rollbuffer insert                      */
-    GDF_KERNEL_SLOTS = 4
+    /* single kernels inside the groups above (one launch each) */
+    GDF_KERNEL_MASK = 4,       /* k_mask: convert + flying-pixel + crop stage bits, tile counts   */
+    GDF_KERNEL_SCAN = 5,       /* k_scan_counts (frames over 1 Mi items only)                     */
+    GDF_KERNEL_EMIT = 6,       /* k_emit: ordered compaction + voxel keys + marks + digit hist    */
+    GDF_KERNEL_SORT = 7,       /* k_sort_pass: one radix pass (the first also updates the grid)   */
+    GDF_KERNEL_GROUP_SCAN = 8, /* k_group_scan: voxel group boundaries                            */
+    GDF_KERNEL_GROUP_SUM = 9,  /* k_group_sum: ordered per-voxel means                            */
+    GDF_KERNEL_SLOTS = 10
 };
 /* enable: record an event pair around every launch of each slot; reset clears the sums */
 int gdf_set_profiling(gdf_engine* engine, int enable);

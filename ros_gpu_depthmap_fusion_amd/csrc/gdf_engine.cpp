@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -160,8 +161,6 @@ struct gdf_engine {
     int device = 0;
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
-    hipStream_t aux = nullptr;          // historic-grid update, overlapped with voxelize
-    hipEvent_t ev_marks = nullptr, ev_grid = nullptr;
     std::mutex ps_mutex;
     int voxel_group_size = 1024;
 
@@ -209,8 +208,8 @@ struct gdf_engine {
 
     // tile tickets + epochs of the look-back launches (no per-launch memsets)
     DevBuf d_ctrs;
-    unsigned long long ctr_base[kCtrSlots] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t epoch = 0;
+    int sort_pt = 4;
     DevBuf d_khist;                 // digit histogram of the voxel keys [4*256]
     bool khist_pending = false;     // accumulated by a fused k_frame, not yet consumed
 
@@ -247,8 +246,8 @@ struct gdf_engine {
     struct EvPair { hipEvent_t a, b; int slot; };
     std::vector<EvPair> ev_pending;
     std::vector<hipEvent_t> ev_pool;
-    double prof_ms[GDF_KERNEL_SLOTS] = {0, 0, 0, 0};
-    uint64_t prof_n[GDF_KERNEL_SLOTS] = {0, 0, 0, 0};
+    double prof_ms[GDF_KERNEL_SLOTS] = {};
+    uint64_t prof_n[GDF_KERNEL_SLOTS] = {};
 
     hipStream_t s() const { return stream; }
 
@@ -278,6 +277,25 @@ struct gdf_engine {
         ev_pending.push_back(p);
         if (ev_pending.size() > 4096) resolve_events();
     }
+    // per-kernel event pairs inside launch_frame / launch_voxelize
+    struct Hook : LaunchHook {
+        gdf_engine* e;
+        std::vector<hipEvent_t> open;
+        explicit Hook(gdf_engine* e_) : e(e_) {}
+        void begin(int) override {
+            hipEvent_t a = e->take_event();
+            HIPCHK(hipEventRecord(a, e->stream));
+            open.push_back(a);
+        }
+        void end(int slot) override {
+            hipEvent_t b = e->take_event();
+            HIPCHK(hipEventRecord(b, e->stream));
+            e->ev_pending.push_back(EvPair{open.back(), b, slot});
+            open.pop_back();
+        }
+    };
+    Hook hook{this};
+    LaunchHook* hook_ptr() { return profiling ? &hook : nullptr; }
     void resolve_events() {
         for (EvPair& p : ev_pending) {
             HIPCHK(hipEventSynchronize(p.b));
@@ -704,7 +722,7 @@ void run_frame(gdf_engine* e, bool fused_voxel) {
     }
     e->dbg_count = e->n_total;
     a.err = e->d_misc.as<uint32_t>() + kErr;
-    e->timed(GDF_KERNEL_FRAME, [&] { HIPCHK(launch_frame(a, e->s())); });
+    e->timed(GDF_KERNEL_FRAME, [&] { HIPCHK(launch_frame(a, e->s(), e->hook_ptr())); });
     if (a.fused_prefix && a.total_tiles) {
         e->cnt_dirty[p] = a.total_tiles;
         e->cnt_dirty[1 - p] = 0;
@@ -726,7 +744,7 @@ void compute_voxel_coords(gdf_engine* e, const float* lo, const float* hi, const
     e->marks_set = false;
 }
 
-void voxelize(gdf_engine* e, int average) {  // fusion.cpp:1743-1756
+void voxelize(gdf_engine* e, int average, int fused_grid_lifetime = -1) {  // fusion.cpp:1743-1756
     if (!e->grid_set || !e->coords_valid) fail(GDF_ERR_STATE, "voxelize before computeVoxelCoords");
     const uint32_t nmax = std::max<uint32_t>(e->n_total, 1);
     if (nmax >= (1u << 31)) fail(GDF_ERR_CAPACITY, "voxelize supports < 2^31 points");
@@ -761,12 +779,21 @@ void voxelize(gdf_engine* e, int average) {  // fusion.cpp:1743-1756
     v.ggstatus = e->d_ggstatus.as<unsigned long long>();
     v.gstart = e->d_gstart.as<uint32_t>();
     v.ctrs = e->d_ctrs.as<unsigned long long>();
-    v.ctr_base = e->ctr_base;
     v.epoch = &e->epoch;
+    v.sort_pt = e->sort_pt;
     v.err = e->d_misc.as<uint32_t>() + kErr;
     v.out = e->d_vox.as<float4>();
     v.out_count = e->d_misc.as<uint32_t>() + kVoxCount;
-    e->timed(GDF_KERNEL_VOXELIZE, [&] { HIPCHK(launch_voxelize(v, e->s())); });
+    if (fused_grid_lifetime >= 0) {  // processFrame: the grid update rides on the first sort pass
+        v.grid8 = e->d_grid8.as<uint8_t>();
+        v.ncells = e->ncells;
+        v.lifetime = (uint32_t)fused_grid_lifetime;
+    }
+    e->timed(GDF_KERNEL_VOXELIZE, [&] { HIPCHK(launch_voxelize(v, e->s(), e->hook_ptr())); });
+    if (fused_grid_lifetime >= 0) {
+        e->marks_set = false;
+        e->invoked_once = true;
+    }
     e->khist_pending = false;
     e->vox_valid = true;
 }
@@ -852,10 +879,8 @@ int gdf_create(int device, gdf_engine** out) {
     e->device = device;
     int rc = guarded(e, [&] {
         HIPCHK(hipStreamCreateWithFlags(&e->own, hipStreamNonBlocking));
-        HIPCHK(hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking));
-        HIPCHK(hipEventCreateWithFlags(&e->ev_marks, hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&e->ev_grid, hipEventDisableTiming));
         e->stream = e->own;
+        if (const char* v = std::getenv("GDF_SORT_PT")) e->sort_pt = std::atoi(v);  // tuning knob
         HIPCHK(hipHostMalloc((void**)&e->h_misc, kMiscWords * 4, hipHostMallocDefault));
         std::memset(e->h_misc, 0, kMiscWords * 4);
         ensure_misc(e);
@@ -879,10 +904,6 @@ int gdf_destroy(gdf_engine* e) {
     }
     for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
     if (e->h_misc) (void)hipHostFree(e->h_misc);
-    if (e->aux) (void)hipStreamSynchronize(e->aux);
-    if (e->ev_marks) (void)hipEventDestroy(e->ev_marks);
-    if (e->ev_grid) (void)hipEventDestroy(e->ev_grid);
-    if (e->aux) (void)hipStreamDestroy(e->aux);
     if (e->own) (void)hipStreamDestroy(e->own);
     delete e;
     return GDF_OK;
@@ -1201,16 +1222,11 @@ int gdf_process_frame(gdf_engine* e, const gdf_frame_params* p, gdf_frame_result
                 e->grid_mode = 1;
             }
             run_frame(e, true);
-            if (!p->defer_occupancy_grid) {
-                // the grid update only needs the marks: run it on the aux stream beside voxelize
-                HIPCHK(hipEventRecord(e->ev_marks, e->s()));
-                HIPCHK(hipStreamWaitEvent(e->aux, e->ev_marks, 0));
-                occupancy_grid(e, p->occupancy_lifetime, e->aux);
-                HIPCHK(hipEventRecord(e->ev_grid, e->aux));
-                voxelize(e, p->voxel_average);
-                HIPCHK(hipStreamWaitEvent(e->s(), e->ev_grid, 0));
+            if (!p->defer_occupancy_grid && e->grid_mode == 0) {
+                voxelize(e, p->voxel_average, (int)p->occupancy_lifetime);
             } else {
                 voxelize(e, p->voxel_average);
+                if (!p->defer_occupancy_grid) occupancy_grid(e, p->occupancy_lifetime, e->s());
             }
         } else {
             run_frame(e, false);

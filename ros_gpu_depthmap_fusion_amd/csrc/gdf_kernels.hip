@@ -19,6 +19,15 @@ __device__ __forceinline__ unsigned long long lanemask_lt() {
     return lane ? (~0ull >> (64 - lane)) : 0ull;
 }
 
+// Tile ticket in block-arrival order (a block only ever waits on lower tickets, which are already
+// running).  Exactly ntiles blocks take one; the taker of the last resets the counter, so the
+// next launch on the stream starts from 0 again without a memset.
+__device__ __forceinline__ uint32_t take_ticket(uint32_t* ctr, uint32_t ntiles) {
+    const uint32_t t = atomicAdd(ctr, 1u);
+    if (t == ntiles - 1u) atomicExch(ctr, 0u);
+    return t;
+}
+
 // Block (256 threads) exclusive scan of one value per thread.
 __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t& total,
                                                          uint32_t* s_wave) {
@@ -696,10 +705,22 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(FrameArgs a) {
     }
 }
 
-hipError_t launch_frame(const FrameArgs& a, hipStream_t s) {
+struct HookScope {  // begin/end of one profiled launch
+    LaunchHook* h;
+    int slot;
+    HookScope(LaunchHook* h_, int s_) : h(h_), slot(s_) {
+        if (h) h->begin(slot);
+    }
+    ~HookScope() {
+        if (h) h->end(slot);
+    }
+};
+
+hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
     if (a.total_tiles == 0) return hipMemsetAsync(a.out_count, 0, 4, s);
     const uint32_t mblocks = a.depth_blocks + a.sel_tiles;
     if (mblocks) {
+        HookScope hs(hook, GDF_KERNEL_MASK);
         if (a.rot45)
             hipLaunchKernelGGL(k_mask<true>, dim3(mblocks), dim3(kFrameThreads), 0, s, a);
         else
@@ -708,11 +729,13 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s) {
         if (e != hipSuccess) return e;
     }
     if (!a.fused_prefix) {
+        HookScope hs(hook, GDF_KERNEL_SCAN);
         hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, a.tile_counts, a.total_tiles,
                            a.tile_offsets, a.out_count);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
+    HookScope hs(hook, GDF_KERNEL_EMIT);
     const uint32_t eblocks = (a.total_tiles * kFrameTile + kEmitThreads - 1) / kEmitThreads;
     hipLaunchKernelGGL(k_emit, dim3(eblocks), dim3(kEmitThreads), 0, s, a);
     return hipGetLastError();
@@ -795,10 +818,11 @@ __device__ __forceinline__ uint32_t grid_word(uint32_t w, uint32_t L) {
            (grid_byte((w >> 16) & 0xFFu, L) << 16) | (grid_byte(w >> 24, L) << 24);
 }
 
-__global__ __launch_bounds__(256) void k_grid_u8(uint4* __restrict__ grid, uint64_t nvec,
-                                                 uint32_t L) {
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nvec;
-         i += (uint64_t)gridDim.x * blockDim.x) {
+// blocks [0, nblocks) of a launch update the u8 grid, 16 cells per thread and step
+__device__ __forceinline__ void grid_u8_part(uint4* __restrict__ grid, uint64_t nvec, uint32_t L,
+                                             uint32_t block, uint32_t nblocks) {
+    for (uint64_t i = block * (uint64_t)blockDim.x + threadIdx.x; i < nvec;
+         i += (uint64_t)nblocks * blockDim.x) {
         uint4 v = grid[i];
         v.x = grid_word(v.x, L);
         v.y = grid_word(v.y, L);
@@ -806,6 +830,11 @@ __global__ __launch_bounds__(256) void k_grid_u8(uint4* __restrict__ grid, uint6
         v.w = grid_word(v.w, L);
         grid[i] = v;
     }
+}
+
+__global__ __launch_bounds__(256) void k_grid_u8(uint4* __restrict__ grid, uint64_t nvec,
+                                                 uint32_t L) {
+    grid_u8_part(grid, nvec, L, blockIdx.x, gridDim.x);
 }
 
 static unsigned grid_blocks(uint64_t work, unsigned per_block) {
@@ -941,9 +970,13 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
     uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, const uint32_t* __restrict__ count,
     const uint32_t* __restrict__ ghist, unsigned long long* status, unsigned long long* gstatus,
-    unsigned long long* tile_ctr, unsigned long long tile_base, uint32_t epoch, uint32_t* err,
-    uint32_t shift, uint32_t dbits) {
+    uint32_t* tile_ctr, uint32_t epoch, uint32_t* err, uint32_t shift, uint32_t dbits,
+    uint32_t grid_block0, uint4* grid, uint64_t grid_nvec, uint32_t lifetime) {
     constexpr int kTile = kSortThreads * PT;
+    if (blockIdx.x >= grid_block0) {  // fused historic-grid update (first pass only)
+        grid_u8_part(grid, grid_nvec, lifetime, blockIdx.x - grid_block0, gridDim.x - grid_block0);
+        return;
+    }
     __shared__ uint32_t s_cnt[4][256];
     __shared__ uint32_t s_base[256];
     __shared__ uint32_t s_excl[256];
@@ -951,11 +984,11 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
     __shared__ uint32_t s_tile;
     const uint32_t n = *count;
     const uint32_t ntiles = (n + kTile - 1) / kTile;
-    if (threadIdx.x == 0) s_tile = (uint32_t)(atomicAdd(tile_ctr, 1ull) - tile_base);
+    if (blockIdx.x >= ntiles) return;  // launched for the capacity; takes no ticket
+    if (threadIdx.x == 0) s_tile = take_ticket(tile_ctr, ntiles);
     for (uint32_t i = threadIdx.x; i < 4 * 256; i += kSortThreads) (&s_cnt[0][0])[i] = 0;
     __syncthreads();
     const uint32_t tile = s_tile;
-    if (tile >= ntiles) return;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const unsigned long long ltm = lanemask_lt();
 
@@ -1017,21 +1050,21 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
 __global__ __launch_bounds__(kGroupThreads) void k_group_scan(
     const uint32_t* __restrict__ keys, const uint32_t* __restrict__ count,
     uint32_t* __restrict__ gstart, uint32_t* __restrict__ out_count, unsigned long long* status,
-    unsigned long long* gstatus, unsigned long long* tile_ctr, unsigned long long tile_base,
-    uint32_t epoch, uint32_t* err, uint32_t* hist) {
+    unsigned long long* gstatus, uint32_t* tile_ctr, uint32_t epoch, uint32_t* err,
+    uint32_t* hist) {
     __shared__ uint32_t s_wave[4];
     __shared__ uint32_t s_tile, s_excl;
     const uint32_t n = *count;
     const uint32_t ntiles = (n + kGroupTile - 1) / kGroupTile;
-    if (threadIdx.x == 0) s_tile = (uint32_t)(atomicAdd(tile_ctr, 1ull) - tile_base);
-    __syncthreads();
-    const uint32_t tile = s_tile;
-    if (tile == 0)
+    if (blockIdx.x == 0)
         for (uint32_t i = threadIdx.x; i < 4 * 256; i += kGroupThreads) hist[i] = 0;
-    if (tile >= ntiles) {
-        if (tile == 0 && threadIdx.x == 0) *out_count = 0;  // n == 0
+    if (blockIdx.x >= ntiles) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) *out_count = 0;  // n == 0
         return;
     }
+    if (threadIdx.x == 0) s_tile = take_ticket(tile_ctr, ntiles);
+    __syncthreads();
+    const uint32_t tile = s_tile;
     const uint32_t i0 = tile * kGroupTile + threadIdx.x * kGroupPerThread;
     uint32_t flags = 0, cnt = 0;
 #pragma unroll
@@ -1136,16 +1169,30 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_sum(
 }
 
 size_t voxelize_status_words(uint32_t nmax) {
-    return (size_t)((nmax + kSortThreads * 16 - 1) / (kSortThreads * 16) + 1) * 256;
+    return (size_t)((nmax + kSortThreads * 4 - 1) / (kSortThreads * 4) + 1) * 256;
 }
 size_t voxelize_group_tiles(uint32_t nmax) {
     return (size_t)((nmax + kGroupTile - 1) / kGroupTile + 1);
 }
 
-hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s) {
+template <int PT>
+static void launch_sort_pass(uint32_t tiles, hipStream_t s, const uint32_t* kin, const uint32_t* vin,
+                             uint32_t* kout, uint32_t* vout, const VoxelizeArgs& a, uint32_t p,
+                             uint32_t ep, uint32_t dbits) {
+    // the first pass also carries the historic-grid update in extra blocks
+    const bool g = p == 0 && a.grid8 != nullptr;
+    const uint64_t nvec = g ? (a.ncells + 15) / 16 : 0;
+    const uint32_t gb = g ? grid_blocks(nvec, 256 * 4) : 0;
+    hipLaunchKernelGGL(k_sort_pass<PT>, dim3(tiles + gb), dim3(kSortThreads), 0, s, kin, vin, kout,
+                       vout, a.count, a.hist + 256 * p, a.status, a.sgstatus,
+                       reinterpret_cast<uint32_t*>(a.ctrs + kCtrSort0 + p), ep, a.err, 8 * p, dbits,
+                       tiles, reinterpret_cast<uint4*>(a.grid8), nvec, a.lifetime);
+}
+
+hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hook) {
     const uint32_t npasses = a.key_bits == 0 ? 1u : (a.key_bits + 7) / 8;
-    // small N: 1024 keys per sort tile (more blocks in flight); large N: 4096
-    const uint32_t tile = kSortThreads * 16;
+    const int pt = a.sort_pt == 4 || a.sort_pt == 8 ? a.sort_pt : 16;
+    const uint32_t tile = kSortThreads * pt;
     const uint32_t sort_tiles = (a.nmax + tile - 1) / tile;
     hipError_t e;
     if (!a.hist_ready) {
@@ -1163,12 +1210,14 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s) {
         const uint32_t dbits = remaining >= 8 ? 8u : (remaining ? remaining : 1u);
         const uint32_t ep = ++(*a.epoch);
         if (sort_tiles) {
-            hipLaunchKernelGGL(k_sort_pass<16>, dim3(sort_tiles), dim3(kSortThreads), 0, s, kin,
-                               vin, kbuf[p & 1], vbuf[p & 1], a.count, a.hist + 256 * p,
-                               a.status, a.sgstatus, a.ctrs + kCtrSort0 + p,
-                               a.ctr_base[kCtrSort0 + p], ep, a.err, 8 * p, dbits);
+            HookScope hs(hook, GDF_KERNEL_SORT);
+            if (pt == 4)
+                launch_sort_pass<4>(sort_tiles, s, kin, vin, kbuf[p & 1], vbuf[p & 1], a, p, ep, dbits);
+            else if (pt == 8)
+                launch_sort_pass<8>(sort_tiles, s, kin, vin, kbuf[p & 1], vbuf[p & 1], a, p, ep, dbits);
+            else
+                launch_sort_pass<16>(sort_tiles, s, kin, vin, kbuf[p & 1], vbuf[p & 1], a, p, ep, dbits);
             if ((e = hipGetLastError()) != hipSuccess) return e;
-            a.ctr_base[kCtrSort0 + p] += sort_tiles;
         }
         kin = kbuf[p & 1];
         vin = vbuf[p & 1];
@@ -1176,11 +1225,14 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s) {
     const uint32_t group_tiles = (a.nmax + kGroupTile - 1) / kGroupTile;
     const uint32_t gblocks = group_tiles ? group_tiles : 1;
     const uint32_t ep = ++(*a.epoch);
+    {
+    HookScope hs(hook, GDF_KERNEL_GROUP_SCAN);
     hipLaunchKernelGGL(k_group_scan, dim3(gblocks), dim3(kGroupThreads), 0, s, kin, a.count,
-                       a.gstart, a.out_count, a.gstatus, a.ggstatus, a.ctrs + kCtrGroup,
-                       a.ctr_base[kCtrGroup], ep, a.err, a.hist);
+                       a.gstart, a.out_count, a.gstatus, a.ggstatus,
+                       reinterpret_cast<uint32_t*>(a.ctrs + kCtrGroup), ep, a.err, a.hist);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    a.ctr_base[kCtrGroup] += gblocks;
+    }
+    HookScope hs(hook, GDF_KERNEL_GROUP_SUM);
     uint32_t sblocks = (a.nmax + 255) / 256;
     if (sblocks > 1024) sblocks = 1024;
     if (sblocks == 0) sblocks = 1;

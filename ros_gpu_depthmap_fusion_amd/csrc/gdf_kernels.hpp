@@ -1,9 +1,17 @@
 // gdf_kernels.hpp — host-side launchers of the gfx950 kernels (gdf_kernels.hip).
 #pragma once
 
+#include "gdf.h"
 #include "gdf_device.hpp"
 
 namespace gdf {
+
+// Optional per-launch callbacks (the engine records HIP event pairs when profiling).
+struct LaunchHook {
+    virtual void begin(int slot) = 0;
+    virtual void end(int slot) = 0;
+    virtual ~LaunchHook() = default;
+};
 
 struct VoxelParams {
     float vlo[3], vcs[3], gmax[3];
@@ -16,7 +24,7 @@ hipError_t launch_tables(uint32_t W, uint32_t H, float fx, float fy, float cx, f
 
 // fused depth + rollbuffer compaction (convert, flying, crop, transform_indirect, apply,
 // optional voxel keys + occupancy marks); needs no memset (epoch-tagged look-back, tickets)
-hipError_t launch_frame(const FrameArgs& a, hipStream_t s);
+hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook = nullptr);
 
 // filter_point_sequence + insert into the rollbuffer ring (w = mask)
 hipError_t launch_ps_filter_insert(const float4* new_pts, uint32_t n, int do_filter, float thr,
@@ -56,15 +64,20 @@ struct VoxelizeArgs {
     unsigned long long* gstatus;    // [group tiles] epoch granules
     unsigned long long* ggstatus;   // [group tiles / 64 + 1]
     uint32_t* gstart;               // [nmax] first sorted position of each group
-    unsigned long long* ctrs;       // [kCtrSlots] tile tickets
-    unsigned long long* ctr_base;   // host copy of the ticket bases (updated)
+    unsigned long long* ctrs;       // [kCtrSlots] self-resetting tile tickets (low 32 bits)
     uint32_t* epoch;                // host epoch counter (advanced per look-back launch)
+    int sort_pt;                    // keys per thread of a sort tile (4, 8 or 16)
+    // optional fused historic-grid update (u8 grid, lifetime <= 127), run by extra blocks of the
+    // first sort pass: it only needs the occupancy marks, which the compaction already wrote
+    uint8_t* grid8;
+    uint64_t ncells;
+    uint32_t lifetime;
     uint32_t* err;
     // outputs
     float4* out;
     uint32_t* out_count;
 };
-hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s);
+hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hook = nullptr);
 size_t voxelize_status_words(uint32_t nmax);
 size_t voxelize_group_tiles(uint32_t nmax);
 

@@ -52,7 +52,9 @@ class FrameParams(C.Structure):
     ]
 
 
-KERNEL_SLOTS = ("frame", "grid", "voxelize", "ps_insert")
+# gdf_kernel_slot order (include/gdf.h): launch groups, then single kernels
+KERNEL_SLOTS = ("frame", "grid", "voxelize", "ps_insert", "mask", "scan", "emit", "sort",
+                "group_scan", "group_sum")
 
 
 class FrameResult(C.Structure):
@@ -444,14 +446,20 @@ class GPUDepthmapFusion:
 
     def kernel_times(self):
         """{slot: (ms_sum, launches)} of the event-timed launches since set_profiling."""
-        ms = np.zeros(4, np.float64)
-        n = np.zeros(4, np.uint64)
-        self._check(self._lib.gdf_get_kernel_times(self._h, _ptr(ms), _ptr(n), 4))
+        k = len(KERNEL_SLOTS)
+        ms = np.zeros(k, np.float64)
+        n = np.zeros(k, np.uint64)
+        self._check(self._lib.gdf_get_kernel_times(self._h, _ptr(ms), _ptr(n), k))
         return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(KERNEL_SLOTS)}
 
     def processFrame(self, params: ComponentParams, T_world_move=None, T_crop_move=None,
                      synchronous: bool = True, defer_occupancy_grid: bool = False) -> FrameResult:
         p = params.to_c(T_world_move, T_crop_move, synchronous, defer_occupancy_grid)
+        return self.processFramePrepared(p)
+
+    def processFramePrepared(self, p: FrameParams) -> FrameResult:
+        """processFrame with parameters already converted by ComponentParams.to_c (a stream of
+        frames with fixed parameters converts them once)."""
         r = FrameResult()
         self._check(self._lib.gdf_process_frame(self._h, C.byref(p), C.byref(r)))
         self._keep = []
