@@ -12,14 +12,11 @@
 namespace gdf {
 
 constexpr int kMaxCams = 16;          // GDF_MAX_CAMERAS
-constexpr int kFrameThreads = 256;    // k_mask block: 4 waves
-constexpr int kFrameTile = 256;       // items per count tile (ordered-compaction granularity)
+constexpr int kFrameThreads = 256;    // k_mask / k_emit block: 4 waves, 4 items per thread
 constexpr int kArgCams = 4;           // camera descriptors passed in the kernel arguments
-constexpr int kTileW = 64;            // k_mask 2-D pixel tile: 64 columns (one per lane) ...
-constexpr int kTileH = 4;             // ... x 4 rows (one per wave)
-constexpr int kHalo = 8;              // LDS halo: rings i <= min(F, 8) read neighbours from LDS
-constexpr uint32_t kFusedPrefixTiles = 4096;  // up to 1 Mi items: k_emit sums the tile counts
-constexpr int kEmitThreads = 1024;    // k_emit block: 4 count tiles, fewer histogram flushes
+constexpr int kHalo = 8;              // band rows/columns staged around a segment: min(F, 8)
+constexpr uint32_t kSegItems = 1024;  // items per compaction segment (max)
+constexpr uint32_t kFusedPrefixSegs = 4096;  // up to this many segments k_emit sums the counts
 constexpr int kSortThreads = 256;
 constexpr int kGroupThreads = 256;
 constexpr int kGroupPerThread = 8;
@@ -45,10 +42,11 @@ struct CamDesc {
     uint32_t W, H, n;
     uint32_t emit;          // 1: pixels are processed; 0: halo camera, only read as neighbours
     float scale;
-    uint32_t tiles_x;       // ceil(W / kTileW)
-    uint32_t block0;        // first k_mask block of this camera (emitting cameras)
-    uint32_t nblocks;       // tiles_x * ceil(H / kTileH)
-    uint32_t pad[2];
+    uint32_t nchunk;        // segments per row: ceil(W / 1024)
+    uint32_t seg0;          // first segment of this camera (emitting cameras)
+    uint32_t nseg;          // H * nchunk
+    uint32_t segw;          // pixels per segment (a multiple of 64, <= 1024)
+    uint32_t pad;
     float Tw[16];           // row-major T_world
     float Tc[16];           // row-major T_crop
 };
@@ -62,7 +60,8 @@ struct FrameArgs {
     const CamDesc* cams_dev;    // all descriptors when ncams > kArgCams
     int32_t ncams;
     uint32_t depth_total;       // ΣP of emitting cameras' index space
-    uint32_t total_tiles;       // 256-item count tiles over depth + selected items
+    uint32_t depth_segs;        // segments over the depth pixels
+    uint32_t total_segs;        // + ceil(sel_count / kSegItems) rollbuffer segments
     // flying-pixel filter (sh/filter_flying_pixels.glsl)
     int32_t do_flying;
     uint32_t F;
@@ -94,14 +93,14 @@ struct FrameArgs {
     uint32_t* out_count;
     uint32_t* out_coords;
     // reduce-then-scan compaction state
-    uint32_t depth_blocks;           // 2-D k_mask blocks over the emitting cameras
-    uint32_t sel_tiles;              // 1-D k_mask blocks over the selected rollbuffer points
-    uint8_t* stage;                  // [n] stage bits per item (also the debug masks)
-    uint32_t* tile_counts;           // [tiles] valid items per count tile (zero on entry)
-    uint32_t* tile_offsets;          // [tiles] (k_scan_counts path)
-    int32_t fused_prefix;            // k_emit sums the preceding tile counts itself
-    uint32_t* zero_counts;           // fused path: the other count buffer, cleared for the next frame
-    uint32_t zero_tiles;
+    unsigned long long* vbits;  // [total_segs * 16] validity bitmask
+    uint32_t* seg_counts;       // [total_segs] valid items per segment
+    uint32_t* seg_offsets;      // [total_segs] (k_scan_counts path)
+    int32_t fused_prefix;       // k_emit sums the preceding segment counts itself
+    uint32_t band_rowb;         // bytes per staged band row (16-B chunks)
+    uint32_t band_lds;          // dynamic LDS of k_mask: band rows + column ray factors
+    uint32_t seg_threads;       // block size of k_mask / k_emit (>= every segment, 64-multiple)
+    uint8_t* dbg;               // optional per-item stage bits
     uint32_t* err;
 };
 static_assert(sizeof(FrameArgs) <= 4096, "kernel arguments are limited to 4 KiB");
@@ -112,7 +111,8 @@ __device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, fl
 }
 
 // out = M·p, ((m0·x + m1·y) + m2·z) + m3·w per row
-__device__ __forceinline__ float mrow(const float* m, float x, float y, float z, float w) {
+template <class P>  // const float* or a global-address-space pointer
+__device__ __forceinline__ float mrow(P m, float x, float y, float z, float w) {
     return ((m[0] * x + m[1] * y) + m[2] * z) + m[3] * w;
 }
 

@@ -176,7 +176,8 @@ struct gdf_engine {
     DevBuf d_depth;
     std::vector<CamTable> tables = std::vector<CamTable>(kMaxCams);
     std::vector<CamDesc> h_cams;
-    uint32_t mask_blocks = 0;       // 2-D k_mask blocks over the emitting cameras
+    uint32_t mask_blocks = 0;       // compaction segments over the emitting cameras
+    uint32_t max_segw = 0;          // widest segment (sizes k_mask's LDS band)
     bool depth_uploaded = false;
 
     // new sequences on the device
@@ -214,10 +215,7 @@ struct gdf_engine {
     bool khist_pending = false;     // accumulated by a fused k_frame, not yet consumed
 
     // compaction outputs
-    DevBuf d_pts, d_coords, d_stage, d_tcounts, d_toffsets, d_camdesc;
-    uint32_t cnt_cap = 0;           // count tiles per half of d_tcounts
-    uint32_t cnt_dirty[2] = {0, 0};  // tiles possibly non-zero in each half
-    int cnt_parity = 0;
+    DevBuf d_pts, d_coords, d_stage, d_vbits, d_tcounts, d_toffsets, d_camdesc;
     DevBuf d_misc;
     uint32_t* h_misc = nullptr;  // pinned
     bool compacted = false, coords_valid = false, marks_set = false;
@@ -563,6 +561,7 @@ void upload_depthmaps(gdf_engine* e) {  // fusion.cpp:1583-1593
     if (e->cams.size() + e->halo.size() > (size_t)kMaxCams) fail(GDF_ERR_ARG, "too many cameras (incl. halo)");
     e->h_cams.clear();
     e->mask_blocks = 0;
+    e->max_segw = 0;
     uint64_t off = 0, hoff = 0;
     for (size_t k = 0; k < e->cams.size(); ++k) {
         const Cam& c = e->cams[k];
@@ -582,10 +581,13 @@ void upload_depthmaps(gdf_engine* e) {  // fusion.cpp:1583-1593
         d.W = c.W; d.H = c.H; d.n = c.n; d.emit = 1;
         d.scale = c.scale;
         d.wmagic = ((1ull << 40) + c.W - 1) / c.W;
-        d.tiles_x = (c.W + kTileW - 1) / kTileW;
-        d.nblocks = d.tiles_x * ((c.H + kTileH - 1) / kTileH);
-        d.block0 = e->mask_blocks;
-        e->mask_blocks += d.nblocks;
+        // compaction segments: rows split into nchunk pieces of segw (a multiple of 64) pixels
+        d.nchunk = (c.W + kSegItems - 1) / kSegItems;
+        d.segw = ((c.W + d.nchunk - 1) / d.nchunk + 63) / 64 * 64;
+        d.nseg = c.H * d.nchunk;
+        d.seg0 = e->mask_blocks;
+        e->mask_blocks += d.nseg;
+        e->max_segw = std::max(e->max_segw, d.segw);
         std::memcpy(d.Tw, c.Tw, 64);
         std::memcpy(d.Tc, c.Tc, 64);
         e->h_cams.push_back(d);
@@ -665,9 +667,10 @@ void run_frame(gdf_engine* e, bool fused_voxel) {
     }
     a.depth_total = e->depth_total;
     const uint32_t sel = e->sel_inserted ? e->rb.selection_point_count : 0u;
-    a.depth_blocks = e->mask_blocks;
-    a.sel_tiles = (sel + kFrameThreads - 1) / kFrameThreads;
-    a.total_tiles = (e->depth_total + sel + kFrameTile - 1) / kFrameTile;  // count tiles
+    a.depth_segs = e->mask_blocks;
+    // one item per thread: blocks as wide as the widest segment (rollbuffer segments use the same)
+    a.seg_threads = e->max_segw ? std::max<uint32_t>(64, e->max_segw) : kSegItems;
+    a.total_segs = a.depth_segs + (sel + a.seg_threads - 1) / a.seg_threads;
     a.do_flying = e->flying_set ? 1 : 0;
     a.F = e->F;
     a.thr = e->thr;
@@ -699,35 +702,29 @@ void run_frame(gdf_engine* e, bool fused_voxel) {
     a.out_pts = e->d_pts.as<float4>();
     a.out_coords = e->d_coords.as<uint32_t>();
     a.out_count = e->d_misc.as<uint32_t>() + kCount;
-    // Two count buffers: a fused-prefix frame counts into half p while its k_emit clears what the
-    // previous frame left in the other half, which the next frame then uses (no memset per frame);
-    // the k_scan_counts path clears its own half.  Invariant: cnt_dirty[cnt_parity] == 0.
-    const uint32_t tiles = std::max<uint32_t>(a.total_tiles, 1);
-    e->d_stage.ensure((size_t)std::max<uint32_t>(e->n_total, 1));
-    if (tiles > e->cnt_cap) {
-        const uint32_t cap = std::max<uint32_t>(tiles, e->cnt_cap + e->cnt_cap / 2);
-        e->d_tcounts.ensure_zero((size_t)2 * cap * 4, e->s());
-        e->cnt_cap = cap;
-        e->cnt_dirty[0] = e->cnt_dirty[1] = 0;
+    const uint32_t segs = std::max<uint32_t>(a.total_segs, 1);
+    e->d_vbits.ensure((size_t)segs * 16 * 8);
+    e->d_tcounts.ensure((size_t)segs * 4);
+    e->d_toffsets.ensure((size_t)segs * 4);
+    a.vbits = e->d_vbits.as<unsigned long long>();
+    a.seg_counts = e->d_tcounts.as<uint32_t>();
+    a.seg_offsets = e->d_toffsets.as<uint32_t>();
+    a.fused_prefix = a.total_segs <= kFusedPrefixSegs ? 1 : 0;
+    // k_mask's LDS band: 2h+1 rows of 16-B chunks covering segw + 2h columns (+1 chunk of
+    // alignment), then the columns' ray factors
+    {
+        const uint32_t h = a.do_flying ? std::min<uint32_t>(a.F, kHalo) : 0u;
+        const uint32_t cols = e->max_segw + 2 * h;
+        a.band_rowb = ((cols * 2 + 15) / 16 + 1) * 16;
+        a.band_lds = (2 * h + 1) * a.band_rowb + (a.seg_threads * 2) * 4;
     }
-    e->d_toffsets.ensure((size_t)tiles * 4);
-    const int p = e->cnt_parity;
-    a.stage = e->d_stage.as<uint8_t>();
-    a.tile_counts = e->d_tcounts.as<uint32_t>() + (size_t)p * e->cnt_cap;
-    a.tile_offsets = e->d_toffsets.as<uint32_t>();
-    a.fused_prefix = a.total_tiles <= kFusedPrefixTiles ? 1 : 0;
-    if (a.fused_prefix) {
-        a.zero_counts = e->d_tcounts.as<uint32_t>() + (size_t)(1 - p) * e->cnt_cap;
-        a.zero_tiles = e->cnt_dirty[1 - p];
+    if (e->debug) {
+        e->d_stage.ensure((size_t)std::max<uint32_t>(e->n_total, 1));
+        a.dbg = e->d_stage.as<uint8_t>();
     }
     e->dbg_count = e->n_total;
     a.err = e->d_misc.as<uint32_t>() + kErr;
     e->timed(GDF_KERNEL_FRAME, [&] { HIPCHK(launch_frame(a, e->s(), e->hook_ptr())); });
-    if (a.fused_prefix && a.total_tiles) {
-        e->cnt_dirty[p] = a.total_tiles;
-        e->cnt_dirty[1 - p] = 0;
-        e->cnt_parity = 1 - p;
-    }
     e->khist_pending = fused_voxel;
     e->compacted = true;
     e->coords_valid = fused_voxel;
@@ -1293,7 +1290,8 @@ int gdf_set_debug(gdf_engine* e, int enable) {
 int gdf_debug_stage_masks(gdf_engine* e, uint8_t* out, uint32_t cap, uint32_t* out_count) {
     ENGINE_OR_FAIL(e);
     return guarded(e, [&] {
-        if (!e->d_stage.p || !e->compacted) fail(GDF_ERR_STATE, "no compaction has run");
+        if (!e->debug || !e->d_stage.p || !e->compacted)
+            fail(GDF_ERR_STATE, "stage masks need gdf_set_debug(1) before the compaction");
         if (out_count) *out_count = e->dbg_count;
         if (out) {
             if (cap < e->dbg_count) fail(GDF_ERR_CAPACITY, "debug masks: buffer too small");

@@ -13,6 +13,28 @@
 
 namespace gdf {
 
+// Pointers that arrive inside structs (kernel-argument structs, LDS camera copies) are generic to
+// the compiler, which then emits flat_* instructions: those count against BOTH vmcnt and lgkmcnt,
+// so every LDS wait also waits for in-flight global loads (no latency hiding).  G() re-types a
+// pointer as global (address space 1) so the frame kernels issue global_* instructions.
+template <class T>
+using gptr = __attribute__((address_space(1))) T*;
+template <class T>
+__device__ __forceinline__ gptr<T> G(T* p) {
+    return (gptr<T>)p;
+}
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 gld4(const float4* p, uint64_t i) {
+    const f4v v = ((gptr<const f4v>)p)[i];
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void gst4(float4* p, uint64_t i, const float4& w) {
+    f4v v;
+    v.x = w.x; v.y = w.y; v.z = w.z; v.w = w.w;
+    ((gptr<f4v>)p)[i] = v;
+}
+
 // ---- small helpers ----------------------------------------------------------------------------
 __device__ __forceinline__ unsigned long long lanemask_lt() {
     const int lane = threadIdx.x & 63;
@@ -298,9 +320,9 @@ __device__ __forceinline__ Nb nb_load(const CamDesc* cams, int ncams, int k, int
         const uint32_t local = (uint32_t)(gi - c.off);
         const uint32_t v = div_w(c, local);
         const uint32_t u = local - v * c.W;
-        r.d = c.depth[local];
-        r.xn = c.xn[u];
-        r.yn = c.yn[v];
+        r.d = G(c.depth)[local];
+        r.xn = G(c.xn)[u];
+        r.yn = G(c.yn)[v];
         r.scale = c.scale;
     }
     return r;
@@ -313,130 +335,181 @@ __device__ __forceinline__ void nb_point(const Nb& n, float& x, float& y, float&
     z = zz;
 }
 
-// Neighbour indices of ring i (filter_flying_pixels.glsl:63-73 / :100-109): up, down, left, right.
-__device__ __forceinline__ void ring_idx(int64_t g, int64_t iw, uint32_t i, bool rot45,
-                                         int64_t* q) {
-    if (!rot45) {
-        q[0] = g - iw; q[1] = g + iw; q[2] = g - i; q[3] = g + i;
-    } else {
-        q[0] = g - iw - i; q[1] = g + iw + i; q[2] = g + iw - i; q[3] = g - iw + i;
-    }
+// ---- depth stage bits: convert_depthmap_to_points (:83-120) -> filter_flying_pixels (:135-165)
+// -> crop_points (:38-67); bit0 convert, bit1 flying, bit2 crop.
+//
+// Work unit of the compaction: a SEGMENT = up to 1024 consecutive pixels of one camera row (rows
+// wider than 1024 are split evenly into 64-multiples), or 1024 consecutive selected rollbuffer
+// points.  Segments are numbered in item order, so the ordered compaction only needs one valid
+// count per segment (a plain store, no atomics) and a 16-word validity bitmask.
+//
+// k_mask stages the segment's depth band - rows y-h..y+h, columns x0-h..x0+len+h, h = min(F, 8) -
+// in LDS with 16-byte loads, plus the column ray factors.  Every neighbour the reference reaches
+// without wrapping its linear index is read from the band; the wrap cases (x < i: the previous
+// row's end; y < i: the previous camera or out of bounds) and rings beyond the
+// halo read global memory with the reference's linear index arithmetic.
+struct SegGeo {
+    int k;            // camera
+    uint32_t y, x0, len;
+    uint32_t item0;   // first item (global point index)
+};
+
+__device__ __forceinline__ SegGeo seg_geo(const CamDesc* cams, int ncams, uint32_t s) {
+    SegGeo g{0, 0, 0, 0, 0};
+    for (int c = 0; c < ncams; ++c)
+        if (cams[c].emit && s >= cams[c].seg0 && s < cams[c].seg0 + cams[c].nseg) g.k = c;
+    const CamDesc& c = cams[g.k];
+    const uint32_t i = s - c.seg0;
+    g.y = i / c.nchunk;
+    const uint32_t j = i - g.y * c.nchunk;
+    g.x0 = j * c.segw;
+    g.len = min(c.segw, c.W - g.x0);
+    g.item0 = (uint32_t)c.off + g.y * c.W + g.x0;
+    return g;
 }
 
-// The surface test of check_at / check_at_rot45 (filter_flying_pixels.glsl:74-96) on loaded
-// neighbours: invalid if any mask is 0 or dot(normalize(cross(dy, dx)), -normalize(p)) < thr.
-// The exact value cv = dot3(c / sqrt(dd), n) is decided first by the filter
-// cva = dot3(c, n) · rsq(dd): both lie within 8 ulp(1) (≈5e-7) of the real (c·n)/|c| for
-// |n| ≈ 1, so outside thr ± 1e-5 the comparison cannot differ; inside it (and for dd outside
-// the normal range, incl. the NaN of a zero cross product) the exact reference sequence runs.
-__device__ __forceinline__ bool surface_ok(float cx, float cy, float cz, float thr, float nx,
-                                           float ny, float nz) {
-    const float dd = dot3(cx, cy, cz, cx, cy, cz);
-    if (dd > 1e-30f && dd < 1e30f) {
-        const float cva = dot3(cx, cy, cz, nx, ny, nz) * __builtin_amdgcn_rsqf(dd);
-        if (cva < thr - 1e-5f) return false;
-        if (cva > thr + 1e-5f) return true;
-    }
-    const float l = sqrtf(dd);
-    const float cv = dot3(cx / l, cy / l, cz / l, nx, ny, nz);
+struct Band {
+    const uint8_t* b;   // LDS band (bytes)
+    const float* xn;    // LDS xn of columns ca..cb-1 (index x - ca)
+    const int* rowoff;  // LDS byte offset of column 0 of band row r (may be negative)
+    uint32_t ca;        // first staged column
+    int h;
+};
+
+__device__ __forceinline__ uint32_t band_d(const Band& t, int r, uint32_t x) {
+    return *reinterpret_cast<const uint16_t*>(t.b + t.rowoff[r] + 2 * (int)x);
+}
+
+struct P3 {
+    float x, y, z;
+    bool v;  // depth != 0
+};
+
+// neighbour (x, band row r) from LDS: the reference's f32 ops x = xn·z, y = yn·z, z = d·scale
+__device__ __forceinline__ P3 band_pt(const Band& t, int r, uint32_t x, float yn, float scale) {
+    const uint32_t d = band_d(t, r, x);
+    const float zz = (float)d * scale;
+    P3 p;
+    p.x = t.xn[x - t.ca] * zz;
+    p.y = yn * zz;
+    p.z = zz;
+    p.v = d != 0u;
+    return p;
+}
+
+__device__ __forceinline__ P3 glb_pt(const CamDesc* cams, int ncams, int k, int64_t gi) {
+    const Nb n = nb_load(cams, ncams, k, gi);
+    P3 p;
+    nb_point(n, p.x, p.y, p.z);
+    p.v = n.d != 0u;
+    return p;
+}
+
+// sqrtf(pp) > 10.0f (max_distance, filter_flying_pixels.glsl:41,143) <=> pp > 100.00001f: the
+// correctly rounded sqrt is monotonic and 0x42C80001 is the largest float whose root rounds to
+// at most 10 (tests/test_oracle_kat.py::test_max_distance_square_threshold checks both sides).
+__device__ __forceinline__ bool beyond_max_distance(float pp) {
+    return pp > __uint_as_float(0x42C80001u);
+}
+
+// check_at / check_at_rot45 (filter_flying_pixels.glsl:74-96) on four neighbour points: invalid
+// if any neighbour has depth 0 or dot(normalize(cross(down - up, right - left)), n) < thr with
+// n = -normalize(p).  The exact value cv is decided first by the filter
+// cva = dot3(c, na) · rsq(c·c) with na = -p · rsq(p·p): both stay within ~20 ulp(1) of the real
+// value for |n| ≈ 1, so outside thr ± 1e-5 the comparison cannot differ; only lanes inside it (or
+// with c·c outside the normal range, incl. the NaN of a zero cross product) run the reference
+// sequence, behind a wave-uniform branch.  `live` lanes are those whose result still matters.
+// the reference sequence: n = -normalize(p), c / sqrt(c·c), dot, compare.  Out of line so the
+// compiler cannot hoist the exact normal of p (3 divisions + sqrt) into every pixel's prologue.
+__device__ __noinline__ bool surface_exact(float cx, float cy, float cz, float dd, float thr,
+                                           float px, float py, float pz) {
+    float nx = px, ny = py, nz_ = pz;
+    normalize3(nx, ny, nz_);
+    const float len = sqrtf(dd);
+    const float cv = dot3(cx / len, cy / len, cz / len, -nx, -ny, -nz_);
     return !(cv < thr);  // NaN passes
 }
 
-__device__ __forceinline__ bool ring_ok(const Nb* n, float thr, float nx, float ny, float nz) {
-    if (n[0].d == 0 || n[1].d == 0 || n[2].d == 0 || n[3].d == 0) return false;
-    float ux, uy, uz, dx_, dy_, dz_, lx, ly, lz, rx, ry, rz;
-    nb_point(n[0], ux, uy, uz);
-    nb_point(n[1], dx_, dy_, dz_);
-    nb_point(n[2], lx, ly, lz);
-    nb_point(n[3], rx, ry, rz);
-    float ax = dx_ - ux, ay = dy_ - uy, az = dz_ - uz;  // dy = down - up
-    float bx = rx - lx, by = ry - ly, bz = rz - lz;      // dx = right - left
-    float cx = ay * bz - az * by;
-    float cy = az * bx - ax * bz;
-    float cz = ax * by - ay * bx;
-    return surface_ok(cx, cy, cz, thr, nx, ny, nz);
+__device__ __forceinline__ bool ring_pass(const P3& u, const P3& d, const P3& l, const P3& r,
+                                          float thr, float nax, float nay, float naz, float px,
+                                          float py, float pz, bool live) {
+    const bool nz = u.v & d.v & l.v & r.v;
+    const float ax = d.x - u.x, ay = d.y - u.y, az = d.z - u.z;  // dy = down - up
+    const float bx = r.x - l.x, by = r.y - l.y, bz = r.z - l.z;  // dx = right - left
+    const float cx = ay * bz - az * by;
+    const float cy = az * bx - ax * bz;
+    const float cz = ax * by - ay * bx;
+    const float dd = dot3(cx, cy, cz, cx, cy, cz);
+    const float cva = dot3(cx, cy, cz, nax, nay, naz) * __builtin_amdgcn_rsqf(dd);
+    const bool normal = (dd > 1e-30f) & (dd < 1e30f);
+    const bool hi = cva > thr + 1e-5f, lo = cva < thr - 1e-5f;
+    bool pass = normal & hi;
+    const bool undecided = live & nz & !(normal & (hi | lo));
+    if (__ballot(undecided)) {  // rare, wave-uniform
+        if (undecided) pass = surface_exact(cx, cy, cz, dd, thr, px, py, pz);
+    }
+    return nz & pass;
 }
 
-// Stage bits of a depth pixel (bit0 convert, bit1 flying, bit2 crop):
-// convert_depthmap_to_points (:83-120) -> filter_flying_pixels (:135-165) -> crop_points (:38-67).
-// Neighbours come from the block's LDS depth tile (2-D offsets) whenever the reference's linear
-// index arithmetic stays inside the camera without wrapping; the wrap cases (x < i: the left
-// neighbour is the previous row's end; y < i: the previous camera or out of bounds, A.6/A.7) and
-// rings beyond the LDS halo take the exact linear-index global path.
-struct Tile {
-    const uint16_t* d;  // s_depth [kTileH + 2h][lw]
-    const float* xn;    // s_xn [lw]
-    const float* yn;    // s_yn [kTileH + 2h]
-    int lw;             // row stride kTileW + 2h
-    uint32_t h;         // halo width min(F, kHalo)
-};
-
-__device__ __forceinline__ Nb lds_nb(const Tile& t, int lx, int ly, float scale) {
-    Nb r;
-    r.d = t.d[ly * t.lw + lx];
-    r.xn = t.xn[lx];
-    r.yn = t.yn[ly];
-    r.scale = scale;
-    return r;
-}
-
-template <bool ROT45>
+// Stage bits of pixel (x, y) of camera k (band row h = the pixel's row).  Rings are evaluated
+// without per-lane early exit (the reference's first-failure return only decides the same AND);
+// the wave leaves the ring loop once none of its lanes is still valid.
+template <bool ROT45, bool INTERIOR>
 __device__ __forceinline__ uint32_t depth_bits(const FrameArgs& a, const CamDesc* cams, int k,
-                                               const Tile& t, uint32_t x, uint32_t y, int lx,
-                                               int ly, uint32_t d) {
-    if (d == 0) return 0;
+                                               const Band& t, const float* s_yn, uint32_t x,
+                                               uint32_t y, bool in) {
     const CamDesc& c = cams[k];
-    const float zz = (float)d * c.scale;
-    const float px = t.xn[lx] * zz, py = t.yn[ly] * zz, pz = zz;
+    const int h = t.h;
+    const float scale = c.scale;
+    const P3 p = in ? band_pt(t, h, x, s_yn[h], scale) : P3{0.f, 0.f, 0.f, false};
+    const bool conv = in & p.v;
+    bool fly = conv;
     if (a.do_flying) {
-        if (sqrtf(dot3(px, py, pz, px, py, pz)) > 10.0f) return 1;  // max_distance (:41,:143)
-        float nx = px, ny = py, nz = pz;
-        normalize3(nx, ny, nz);
-        nx = -nx; ny = -ny; nz = -nz;
+        const float pp = dot3(p.x, p.y, p.z, p.x, p.y, p.z);
+        fly = fly & !beyond_max_distance(pp);
+        const float rr = __builtin_amdgcn_rsqf(pp);
+        const float nax = -(p.x * rr), nay = -(p.y * rr), naz = -(p.z * rr);
         const int64_t g = c.off + (int64_t)y * c.W + x;
         for (uint32_t i = 1; i <= a.F; ++i) {
-            if (x + i > c.W - 1 || y + i > c.H - 1) return 1;  // bounds (:60; x-i<0 never true)
-            const int64_t iw = (int64_t)i * c.W;
-            const bool lds = i <= t.h;
-            const bool xw = x < i, yw = y < i;  // wrap / cross-camera cases
+            if (!__ballot(fly)) break;  // wave-uniform exit
+            fly = fly & (x + i <= c.W - 1) & (y + i <= c.H - 1);  // bounds (:60)
             const int ii = (int)i;
-#pragma unroll
-            for (int v = 0; v < (ROT45 ? 2 : 1); ++v) {
-                Nb n[4];
-                if (v == 0) {  // up (x, y-i), down (x, y+i), left (x-i, y), right (x+i, y)
-                    n[0] = (lds && !yw) ? lds_nb(t, lx, ly - ii, c.scale) : nb_load(cams, a.ncams, k, g - iw);
-                    n[1] = lds ? lds_nb(t, lx, ly + ii, c.scale) : nb_load(cams, a.ncams, k, g + iw);
-                    n[2] = (lds && !xw) ? lds_nb(t, lx - ii, ly, c.scale) : nb_load(cams, a.ncams, k, g - ii);
-                    n[3] = lds ? lds_nb(t, lx + ii, ly, c.scale) : nb_load(cams, a.ncams, k, g + ii);
-                } else {  // up (x-i, y-i), down (x+i, y+i), left (x-i, y+i), right (x+i, y-i)
-                    n[0] = (lds && !xw && !yw) ? lds_nb(t, lx - ii, ly - ii, c.scale)
-                                               : nb_load(cams, a.ncams, k, g - iw - ii);
-                    n[1] = lds ? lds_nb(t, lx + ii, ly + ii, c.scale) : nb_load(cams, a.ncams, k, g + iw + ii);
-                    n[2] = (lds && !xw) ? lds_nb(t, lx - ii, ly + ii, c.scale)
-                                        : nb_load(cams, a.ncams, k, g + iw - ii);
-                    n[3] = (lds && !yw) ? lds_nb(t, lx + ii, ly - ii, c.scale)
-                                        : nb_load(cams, a.ncams, k, g - iw + ii);
-                }
-                if (!ring_ok(n, a.thr, nx, ny, nz)) return 1;
+            const int64_t gw = (int64_t)i * c.W;
+            // INTERIOR (wave-uniform: every lane has x >= F, y >= F, F <= h): all in the band
+            const bool L = INTERIOR || ii <= h;  // ring inside the band (uniform)
+            const bool yw = !INTERIOR && y < i;  // up neighbours leave the camera (uniform)
+            const bool xw = !INTERIOR && x < i;  // left neighbours wrap to the previous row
+            const uint32_t xs = x, xl = xw ? x : x - i, xr = x + i;
+            P3 n0, n1, n2, n3;
+            // up (x, y-i), down (x, y+i), left (x-i, y), right (x+i, y)
+            n0 = (L && !yw) ? band_pt(t, h - ii, xs, s_yn[h - ii], scale)
+                            : glb_pt(cams, a.ncams, k, g - gw);
+            n1 = L ? band_pt(t, h + ii, xs, s_yn[h + ii], scale) : glb_pt(cams, a.ncams, k, g + gw);
+            n2 = (L && !xw) ? band_pt(t, h, xl, s_yn[h], scale) : glb_pt(cams, a.ncams, k, g - ii);
+            n3 = L ? band_pt(t, h, xr, s_yn[h], scale) : glb_pt(cams, a.ncams, k, g + ii);
+            fly = fly & ring_pass(n0, n1, n2, n3, a.thr, nax, nay, naz, p.x, p.y, p.z, fly);
+            if (ROT45) {  // up (x-i, y-i), down (x+i, y+i), left (x-i, y+i), right (x+i, y-i)
+                n0 = (L && !xw && !yw) ? band_pt(t, h - ii, xl, s_yn[h - ii], scale)
+                                       : glb_pt(cams, a.ncams, k, g - gw - ii);
+                n1 = L ? band_pt(t, h + ii, xr, s_yn[h + ii], scale)
+                       : glb_pt(cams, a.ncams, k, g + gw + ii);
+                n2 = (L && !xw) ? band_pt(t, h + ii, xl, s_yn[h + ii], scale)
+                                : glb_pt(cams, a.ncams, k, g + gw - ii);
+                n3 = (L && !yw) ? band_pt(t, h - ii, xr, s_yn[h - ii], scale)
+                                : glb_pt(cams, a.ncams, k, g - gw + ii);
+                fly = fly & ring_pass(n0, n1, n2, n3, a.thr, nax, nay, naz, p.x, p.y, p.z, fly);
             }
         }
     }
+    bool crop = true;
     if (a.do_crop) {
-        const float qx = mrow(c.Tc + 0, px, py, pz, 1.0f);
-        const float qy = mrow(c.Tc + 4, px, py, pz, 1.0f);
-        const float qz = mrow(c.Tc + 8, px, py, pz, 1.0f);
-        if (qx < a.lo[0] || qx > a.hi[0] || qy < a.lo[1] || qy > a.hi[1] || qz < a.lo[2] ||
-            qz > a.hi[2])
-            return 3;
+        const float qx = mrow(c.Tc + 0, p.x, p.y, p.z, 1.0f);
+        const float qy = mrow(c.Tc + 4, p.x, p.y, p.z, 1.0f);
+        const float qz = mrow(c.Tc + 8, p.x, p.y, p.z, 1.0f);
+        crop = !((qx < a.lo[0]) | (qx > a.hi[0]) | (qy < a.lo[1]) | (qy > a.hi[1]) |
+                 (qz < a.lo[2]) | (qz > a.hi[2]));
     }
-    return 7;
-}
-
-__device__ __forceinline__ float4 depth_world(const CamDesc& c, uint32_t local, uint32_t d) {
-    float px, py, pz;
-    cam_point(c, local, d, px, py, pz);
-    return make_float4(mrow(c.Tw + 0, px, py, pz, 1.0f), mrow(c.Tw + 4, px, py, pz, 1.0f),
-                       mrow(c.Tw + 8, px, py, pz, 1.0f), mrow(c.Tw + 12, px, py, pz, 1.0f));
+    return (uint32_t)conv | ((uint32_t)fly << 1) | ((uint32_t)(fly & crop) << 2);
 }
 
 // transform index of selected point i: last covered sequence starting at or before i
@@ -444,19 +517,18 @@ __device__ __forceinline__ uint32_t sel_tf(const FrameArgs& a, uint32_t i) {
     uint32_t lo = 0, hi = a.nseg;
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
-        if (a.seg_start[mid] <= i) lo = mid; else hi = mid;
+        if (G(a.seg_start)[mid] <= i) lo = mid; else hi = mid;
     }
-    return a.seg_tf[lo];
+    return G(a.seg_tf)[lo];
 }
 
 // selected rollbuffer point i: mask (transfer_data of the selected mask), transform_points
 // _indirect (:50-69) into the crop frame, crop_points
-__device__ __forceinline__ uint32_t sel_bits(const FrameArgs& a, uint32_t i, float4& p, uint32_t& t) {
-    p = a.ring[(a.ring_first + i) % a.ring_cap];
+__device__ __forceinline__ uint32_t sel_bits(const FrameArgs& a, uint32_t i) {
+    const float4 p = gld4(a.ring, (a.ring_first + i) % a.ring_cap);
     if (p.w == 0.0f) return 0;  // rollbuffer mask 0
-    t = sel_tf(a, i);
     if (a.do_crop) {
-        const float* Tc = a.tfc + 16 * (size_t)t;
+        const gptr<const float> Tc = G(a.tfc + 16 * (size_t)sel_tf(a, i));
         const float qx = mrow(Tc + 0, p.x, p.y, p.z, 1.0f);
         const float qy = mrow(Tc + 4, p.x, p.y, p.z, 1.0f);
         const float qz = mrow(Tc + 8, p.x, p.y, p.z, 1.0f);
@@ -467,103 +539,134 @@ __device__ __forceinline__ uint32_t sel_bits(const FrameArgs& a, uint32_t i, flo
     return 7;
 }
 
+// Camera descriptors: kernel arguments for up to kArgCams cameras, else the device copy.
+__device__ __forceinline__ const CamDesc* cam_table(const FrameArgs& a) {
+    return a.ncams <= kArgCams ? a.cams : a.cams_dev;
+}
+
+// block-wide copy of the camera descriptors into LDS
 __device__ __forceinline__ void load_cams(const FrameArgs& a, CamDesc* s_cams) {
     const uint32_t words = (uint32_t)a.ncams * (uint32_t)(sizeof(CamDesc) / 4);
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.ncams <= kArgCams ? a.cams : a.cams_dev);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(cam_table(a));
     uint32_t* dst = reinterpret_cast<uint32_t*>(s_cams);
-    for (uint32_t w = threadIdx.x; w < words; w += blockDim.x) dst[w] = src[w];
+    for (uint32_t w = threadIdx.x; w < words; w += blockDim.x) dst[w] = G(src)[w];
 }
 
-// valid-count of one wave's 64 consecutive items starting at item g0 into the count tiles
-// (a 64-item run straddles at most two 256-item tiles)
-__device__ __forceinline__ void add_counts(uint32_t* counts, unsigned long long m, uint32_t g0) {
-    if (!m) return;
-    const uint32_t t0 = g0 / kFrameTile;
-    const uint32_t cut = (t0 + 1) * kFrameTile - g0;  // lanes [0, cut) belong to t0
-    if (cut >= 64) {
-        atomicAdd(&counts[t0], (uint32_t)__popcll(m));
-    } else {
-        const unsigned long long lo = (1ull << cut) - 1ull;
-        const uint32_t a = (uint32_t)__popcll(m & lo), b = (uint32_t)__popcll(m & ~lo);
-        if (a) atomicAdd(&counts[t0], a);
-        if (b) atomicAdd(&counts[t0 + 1], b);
-    }
-}
-
-// Pass 1 of the ordered compaction (apply_point_mask.glsl:42-55 made stable).  Depth blocks: a
-// 64x16 pixel tile of one camera with an 8-pixel LDS halo (depth + ray factors), one column per
-// lane, 4 rows per wave; rollbuffer blocks: 256 selected points.  Writes the stage bits of every
-// item and adds the valid counts of every 256-item count tile.
+// Pass 1 of the ordered compaction (apply_point_mask.glsl:42-55 made stable): one block per
+// segment, one item per thread (blockDim = a.seg_threads >= every segment's length).  The ballot
+// of wave w's valid bits is word w of the segment's 16-word bitmask.
 template <bool ROT45>
-__global__ __launch_bounds__(kFrameThreads) void k_mask(FrameArgs a) {
+__global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
     __shared__ CamDesc s_cams[kMaxCams];
-    __shared__ uint16_t s_depth[(kTileH + 2 * kHalo) * (kTileW + 2 * kHalo)];
-    __shared__ float s_xn[kTileW + 2 * kHalo];
-    __shared__ float s_yn[kTileH + 2 * kHalo];
+    __shared__ float s_yn[2 * kHalo + 1];
+    __shared__ int s_rowoff[2 * kHalo + 1];
+    __shared__ uint32_t s_cnt[16];
+    extern __shared__ uint4 s_dyn[];  // band rows (a.band_rowb bytes each), then xn
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int nwaves = blockDim.x >> 6;
+    const uint32_t s = blockIdx.x;
     load_cams(a, s_cams);
     __syncthreads();
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint32_t b = blockIdx.x;
-    if (b < a.depth_blocks) {
-        int k = 0;
-        for (int c = 0; c < a.ncams; ++c)
-            if (s_cams[c].emit && b >= s_cams[c].block0 && b < s_cams[c].block0 + s_cams[c].nblocks) k = c;
-        const CamDesc& c = s_cams[k];
-        const uint32_t t = b - c.block0;
-        const uint32_t ty = t / c.tiles_x, tx = t - ty * c.tiles_x;
-        const int c0 = (int)(tx * kTileW), r0 = (int)(ty * kTileH);
+    uint32_t bits = 0;
+    const uint32_t i = threadIdx.x;
+    if (s < a.depth_segs) {
+        const SegGeo sg = seg_geo(s_cams, a.ncams, s);
+        const CamDesc& c = s_cams[sg.k];
         const int h = a.do_flying ? (int)min(a.F, (uint32_t)kHalo) : 0;
-        const int lw = kTileW + 2 * h, lh = kTileH + 2 * h;
-        // depth tile + halo (rows by wave, columns by lane; outside the camera -> 0, never read)
-        for (int row = wid; row < lh; row += kFrameThreads / 64) {
-            const int gy = r0 - h + row;
-            const bool rin = gy >= 0 && gy < (int)c.H;
-            for (int col = lane; col < lw; col += 64) {
-                const int gx = c0 - h + col;
-                s_depth[row * lw + col] = (rin && gx >= 0 && gx < (int)c.W)
-                                              ? c.depth[(uint32_t)gy * c.W + (uint32_t)gx] : (uint16_t)0;
+        const uint32_t ca = sg.x0 >= (uint32_t)h ? sg.x0 - h : 0u;
+        const uint32_t cb = min(c.W, sg.x0 + sg.len + h);
+        const uint32_t nrows = 2 * h + 1;
+        uint8_t* band = reinterpret_cast<uint8_t*>(s_dyn);
+        float* s_xn = reinterpret_cast<float*>(band + (size_t)nrows * a.band_rowb);
+        // stage the band: 16-byte chunks, the row's first chunk aligned down (same 16-B line as
+        // a needed byte, so never outside the allocation's pages); all loads before any store
+        typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+        const uintptr_t dbase = reinterpret_cast<uintptr_t>(c.depth);
+        const uint32_t nch = a.band_rowb / 16;
+        const uint32_t r = (uint32_t)wid;  // one band row per wave (nrows <= 17 <= waves or looped)
+        u4v v[3];
+        float xv0 = 0.0f, xv1 = 0.0f;
+        uint32_t n16 = 0;
+        uintptr_t a16 = 0, first = 0;
+        const int gy = (int)sg.y - h + (int)r;
+        const bool rok = r < nrows && gy >= 0 && gy < (int)c.H;
+        if (rok) {
+            first = dbase + 2 * ((uintptr_t)gy * c.W + ca);
+            const uintptr_t last = dbase + 2 * ((uintptr_t)gy * c.W + cb);  // exclusive
+            a16 = first & ~(uintptr_t)15;
+            n16 = min((uint32_t)((last - a16 + 15) / 16), nch);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const uint32_t ch = (uint32_t)lane + 64u * q;
+                if (ch < n16) v[q] = *(gptr<const u4v>)(a16 + 16 * (uintptr_t)ch);
             }
         }
-        if (threadIdx.x < (unsigned)lw) {
-            const int gx = c0 - h + (int)threadIdx.x;
-            s_xn[threadIdx.x] = (gx >= 0 && gx < (int)c.W) ? c.xn[gx] : 0.0f;
-        } else if (threadIdx.x - lw < (unsigned)lh) {
-            const int row = (int)threadIdx.x - lw;
-            const int gy = r0 - h + row;
-            s_yn[row] = (gy >= 0 && gy < (int)c.H) ? c.yn[gy] : 0.0f;
+        if (ca + i < cb) xv0 = G(c.xn)[ca + i];
+        if (ca + i + blockDim.x < cb) xv1 = G(c.xn)[ca + i + blockDim.x];
+        if (i < nrows) {
+            const int gyi = (int)sg.y - h + (int)i;
+            s_yn[i] = (gyi >= 0 && gyi < (int)c.H) ? G(c.yn)[gyi] : 0.0f;
         }
+        if (rok) {
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const uint32_t ch = (uint32_t)lane + 64u * q;
+                if (ch < n16) *reinterpret_cast<u4v*>(band + r * a.band_rowb + 16 * ch) = v[q];
+            }
+        }
+        if (lane == 0 && r < nrows)  // rows outside the camera: any in-bounds offset (never live)
+            s_rowoff[r] = (int)(r * a.band_rowb) - 2 * (int)ca + (rok ? (int)(first - a16) : 0);
+        // bands taller than the block's waves (few waves, big F): remaining rows, plain loop
+        for (uint32_t rr = (uint32_t)nwaves + r; rr < nrows; rr += (uint32_t)nwaves) {
+            const int gy2 = (int)sg.y - h + (int)rr;
+            const bool ok2 = gy2 >= 0 && gy2 < (int)c.H;
+            uintptr_t f2 = 0, b2 = 0;
+            if (ok2) {
+                f2 = dbase + 2 * ((uintptr_t)gy2 * c.W + ca);
+                b2 = f2 & ~(uintptr_t)15;
+                const uint32_t m16 = min((uint32_t)((dbase + 2 * ((uintptr_t)gy2 * c.W + cb) - b2 + 15) / 16), nch);
+                for (uint32_t ch = (uint32_t)lane; ch < m16; ch += 64)
+                    *reinterpret_cast<u4v*>(band + rr * a.band_rowb + 16 * ch) =
+                        *(gptr<const u4v>)(b2 + 16 * (uintptr_t)ch);
+            }
+            if (lane == 0) s_rowoff[rr] = (int)(rr * a.band_rowb) - 2 * (int)ca + (ok2 ? (int)(f2 - b2) : 0);
+        }
+        if (ca + i < cb) s_xn[i] = xv0;
+        if (ca + i + blockDim.x < cb) s_xn[i + blockDim.x] = xv1;
         __syncthreads();
-        const Tile tl{s_depth, s_xn, s_yn, lw, (uint32_t)h};
-        const uint32_t x = (uint32_t)(c0 + lane);
-        const uint32_t y = (uint32_t)(r0 + wid);
-        if (y < c.H) {  // wave-uniform
-            const int lx = lane + h, ly = wid + h;
-            uint32_t bits = 0;
-            const bool in = x < c.W;
-            if (in) bits = depth_bits<ROT45>(a, s_cams, k, tl, x, y, lx, ly, tl.d[ly * lw + lx]);
-            const uint32_t item = (uint32_t)c.off + y * c.W + (uint32_t)c0;  // item of lane 0
-            if (in) a.stage[item + lane] = (uint8_t)bits;
-            const unsigned long long m = __ballot((bits & 4) != 0);
-            if (lane == 0) add_counts(a.tile_counts, m, item);
+        const Band t{band, s_xn, s_rowoff, ca, h};
+        if (64u * (uint32_t)wid < sg.len) {  // wave-uniform
+            const uint32_t xw0 = sg.x0 + 64u * wid;  // x of the wave's lane 0
+            if (!a.do_flying || (xw0 >= a.F && sg.y >= a.F && a.F <= (uint32_t)h))
+                bits = depth_bits<ROT45, true>(a, s_cams, sg.k, t, s_yn, sg.x0 + i, sg.y, i < sg.len);
+            else
+                bits = depth_bits<ROT45, false>(a, s_cams, sg.k, t, s_yn, sg.x0 + i, sg.y, i < sg.len);
+            if (a.dbg && i < sg.len) G(a.dbg)[sg.item0 + i] = (uint8_t)bits;
         }
     } else {
-        const uint32_t i = (b - a.depth_blocks) * kFrameThreads + threadIdx.x;
-        uint32_t bits = 0;
-        if (i < a.sel_count) {
-            float4 p;
-            uint32_t tf;
-            bits = sel_bits(a, i, p, tf);
-            a.stage[a.depth_total + i] = (uint8_t)bits;
+        const uint32_t si = (s - a.depth_segs) * blockDim.x + i;
+        if (si < a.sel_count) {
+            bits = sel_bits(a, si);
+            if (a.dbg) G(a.dbg)[a.depth_total + si] = (uint8_t)bits;
         }
-        const unsigned long long m = __ballot((bits & 4) != 0);
-        if (lane == 0) add_counts(a.tile_counts, m, a.depth_total + (i - (uint32_t)lane));
+    }
+    const unsigned long long m = __ballot((bits & 4u) != 0u);
+    if (lane == 0) {
+        G(a.vbits)[(size_t)s * 16 + wid] = m;
+        s_cnt[wid] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < nwaves; ++w) t += s_cnt[w];
+        G(a.seg_counts)[s] = t;
     }
 }
 
-// Exclusive scan of the tile counts by one workgroup (chunks of 4096 with a running carry);
-// writes the total (m_numItemsAfterMask) and re-zeroes the counts for the next frame.
-__global__ __launch_bounds__(1024) void k_scan_counts(uint32_t* __restrict__ counts, uint32_t m,
-                                                      uint32_t* __restrict__ offsets,
+// Exclusive scan of the segment counts by one workgroup (chunks of 4096 with a running carry);
+// writes the total (m_numItemsAfterMask).  Used when there are more than kFusedPrefixSegs.
+__global__ __launch_bounds__(1024) void k_scan_counts(const uint32_t* __restrict__ counts,
+                                                      uint32_t m, uint32_t* __restrict__ offsets,
                                                       uint32_t* __restrict__ total) {
     __shared__ uint32_t s_w[16];
     __shared__ uint32_t s_carry;
@@ -576,7 +679,6 @@ __global__ __launch_bounds__(1024) void k_scan_counts(uint32_t* __restrict__ cou
         for (int q = 0; q < 4; ++q) {
             const uint32_t i = base + threadIdx.x * 4 + q;
             v[q] = i < m ? counts[i] : 0u;
-            if (i < m) counts[i] = 0u;
             sum += v[q];
         }
         uint32_t x = sum;
@@ -608,100 +710,126 @@ __global__ __launch_bounds__(1024) void k_scan_counts(uint32_t* __restrict__ cou
     if (threadIdx.x == 0) *total = s_carry;
 }
 
-// Pass 2: item-ordered emission.  Each valid item (stage bit 2) recomputes its world point with
-// the same f32 ops as pass 1 and writes it at tile offset + rank: stable pixel order, cameras in
-// add order, selected rollbuffer points after the depth points (fusion.cpp:1525,1559).
-// Optionally the voxel key (compute_voxel_coords), the occupancy mark (no-return atomic OR of
-// bit 7, issued once per run of equal keys in a wave) and the key digit histogram.
-__global__ __launch_bounds__(kEmitThreads) void k_emit(FrameArgs a) {
-    __shared__ CamDesc s_cams[kMaxCams];
+// Pass 2: item-ordered emission, one block per segment.  Each valid item recomputes its world
+// point with the same f32 ops as pass 1 and writes it at segment offset + rank: stable pixel
+// order, cameras in add order, selected rollbuffer points after the depth points
+// (fusion.cpp:1525,1559).  Optionally the voxel key (compute_voxel_coords), the occupancy mark
+// (no-return atomic OR of bit 7, issued once per run of equal keys in a wave) and the key digit
+// histogram.  The segment offset is the sum of the preceding counts (<= kFusedPrefixSegs
+// segments) or k_scan_counts' result.
+__global__ __launch_bounds__(1024) void k_emit(FrameArgs a) {
     __shared__ uint32_t s_hist[4 * 256];
-    __shared__ uint32_t s_wc[kEmitThreads / 64];
-    __shared__ uint32_t s_red[kEmitThreads / 64];
-    load_cams(a, s_cams);
-    if (a.key_hist)
-        for (uint32_t i = threadIdx.x; i < a.npasses * 256; i += kEmitThreads) s_hist[i] = 0;
+    __shared__ uint32_t s_red[16];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint32_t n = a.depth_total + a.sel_count;
-    const uint32_t item = blockIdx.x * kEmitThreads + threadIdx.x;
-    const uint32_t bits = item < n ? a.stage[item] : 0u;
-    const bool valid = (bits & 4) != 0;
-    const unsigned long long m = __ballot(valid);
-    if (lane == 0) s_wc[wid] = (uint32_t)__popcll(m);
-    // block base: the preceding tiles' counts summed here (fused) or the scanned offset
-    const uint32_t t0 = blockIdx.x * (kEmitThreads / kFrameTile);
+    const int nwaves = blockDim.x >> 6;
+    const uint32_t s = blockIdx.x;
+    const gptr<const CamDesc> cams = G(cam_table(a));
+    if (a.key_hist)
+        for (uint32_t i = threadIdx.x; i < a.npasses * 256; i += blockDim.x) s_hist[i] = 0;
     if (a.fused_prefix) {
         uint32_t sum = 0;
-        for (uint32_t t = threadIdx.x; t < t0; t += kEmitThreads) sum += a.tile_counts[t];
+        for (uint32_t t = threadIdx.x; t < s; t += blockDim.x) sum += G(a.seg_counts)[t];
         for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
         if (lane == 0) s_red[wid] = sum;
-        for (uint32_t t = blockIdx.x * kEmitThreads + threadIdx.x; t < a.zero_tiles;
-             t += gridDim.x * kEmitThreads)
-            a.zero_counts[t] = 0u;
+    }
+    // the segment's geometry and the thread's item source, loaded before the barrier
+    const bool depth = s < a.depth_segs;
+    const uint32_t i = threadIdx.x;
+    int k = 0;
+    uint32_t y = 0, x0 = 0, len = 0, item0 = 0;
+    if (depth) {
+        for (int c = 0; c < a.ncams; ++c)
+            if (cams[c].emit && s >= cams[c].seg0 && s < cams[c].seg0 + cams[c].nseg) k = c;
+        const uint32_t j = s - cams[k].seg0;
+        y = j / cams[k].nchunk;
+        x0 = (j - y * cams[k].nchunk) * cams[k].segw;
+        len = min(cams[k].segw, cams[k].W - x0);
+        item0 = (uint32_t)cams[k].off + y * cams[k].W + x0;
+    } else {
+        item0 = a.depth_total + (s - a.depth_segs) * blockDim.x;
+        len = min((uint32_t)blockDim.x, a.depth_total + a.sel_count - item0);
+    }
+    const unsigned long long m = G(a.vbits)[(size_t)s * 16 + wid];
+    const bool valid = i < len && ((m >> lane) & 1ull);
+    uint32_t dval = 0;
+    float4 sp = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (valid) {
+        if (depth)
+            dval = G(cams[k].depth)[y * cams[k].W + x0 + i];
+        else
+            sp = gld4(a.ring, (a.ring_first + (item0 - a.depth_total + i)) % a.ring_cap);
     }
     __syncthreads();
-    uint32_t base = 0, blk = 0;
+    uint32_t base = 0;
     if (a.fused_prefix) {
-#pragma unroll
-        for (int w = 0; w < kEmitThreads / 64; ++w) base += s_red[w];
+        for (int w = 0; w < nwaves; ++w) base += s_red[w];
     } else {
-        base = a.tile_offsets[t0];
+        base = G(a.seg_offsets)[s];
     }
-    uint32_t before = 0;
-#pragma unroll
-    for (int w = 0; w < kEmitThreads / 64; ++w) {
-        before += (w < wid) ? s_wc[w] : 0u;
-        blk += s_wc[w];
+    // prefix of the valid counts of the waves before this one (uniform word loads)
+    uint32_t wpre = 0, tot = 0;
+    for (int w = 0; w < nwaves; ++w) {
+        const uint32_t pc = (uint32_t)__popcll(G(a.vbits)[(size_t)s * 16 + w]);
+        wpre += (w < wid) ? pc : 0u;
+        tot += pc;
     }
-    if (a.fused_prefix && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *a.out_count = base + blk;
+    if (a.fused_prefix && s == gridDim.x - 1 && threadIdx.x == 0) *G(a.out_count) = base + tot;
     const unsigned long long ltm = lane ? (~0ull >> (64 - lane)) : 0ull;
     uint32_t key = 0xFFFFFFFFu;
     if (valid) {
-        const uint32_t pos = base + before + (uint32_t)__popcll(m & ltm);
+        const uint32_t pos = base + wpre + (uint32_t)__popcll(m & ltm);
         float4 w;
-        if (item < a.depth_total) {
-            const int k = find_cam(s_cams, a.ncams, (int64_t)item);
-            const uint32_t local = (uint32_t)((int64_t)item - s_cams[k].off);
-            w = depth_world(s_cams[k], local, s_cams[k].depth[local]);
+        if (depth) {
+            const uint32_t x = x0 + i;
+            const float zz = (float)dval * cams[k].scale;
+            const float px = G(cams[k].xn)[x] * zz, py = G(cams[k].yn)[y] * zz, pz = zz;
+            w = make_float4(mrow(cams[k].Tw + 0, px, py, pz, 1.0f),
+                            mrow(cams[k].Tw + 4, px, py, pz, 1.0f),
+                            mrow(cams[k].Tw + 8, px, py, pz, 1.0f),
+                            mrow(cams[k].Tw + 12, px, py, pz, 1.0f));
         } else {
-            const uint32_t i = item - a.depth_total;
-            const float4 p = a.ring[(a.ring_first + i) % a.ring_cap];
-            const float* Tw = a.tfw + 16 * (size_t)sel_tf(a, i);
-            w = make_float4(mrow(Tw + 0, p.x, p.y, p.z, 1.0f), mrow(Tw + 4, p.x, p.y, p.z, 1.0f),
-                            mrow(Tw + 8, p.x, p.y, p.z, 1.0f), mrow(Tw + 12, p.x, p.y, p.z, 1.0f));
+            const uint32_t si = item0 - a.depth_total + i;
+            const gptr<const float> Tw = G(a.tfw + 16 * (size_t)sel_tf(a, si));
+            w = make_float4(mrow(Tw + 0, sp.x, sp.y, sp.z, 1.0f), mrow(Tw + 4, sp.x, sp.y, sp.z, 1.0f),
+                            mrow(Tw + 8, sp.x, sp.y, sp.z, 1.0f), mrow(Tw + 12, sp.x, sp.y, sp.z, 1.0f));
         }
-        a.out_pts[pos] = w;
+        gst4(a.out_pts, pos, w);
         if (a.do_voxel) {
             key = voxel_key(w.x, w.y, w.z, a.vlo, a.vcs, a.gmax, a.gs);
-            a.out_coords[pos] = key;
+            G(a.out_coords)[pos] = key;
         }
     }
     if (a.do_voxel) {
         // runs of equal keys among the wave's valid lanes: the first lane of a run marks / counts
-        const unsigned long long below = m & ltm;
+        const unsigned long long vm = __ballot(valid);
+        const unsigned long long below = vm & ltm;
         const int prev = below ? 63 - __clzll((long long)below) : -1;
         const uint32_t pkey = __shfl(key, prev < 0 ? 0 : prev, 64);
         const bool leader = valid && (prev < 0 || pkey != key);
         const unsigned long long lm = __ballot(leader);
         if (leader) {
             if (a.occ_mode == 1)
-                atomicOr(reinterpret_cast<uint32_t*>(a.occ + (key & ~3u)), 0x80u << (8 * (key & 3u)));
+                __hip_atomic_fetch_or(G(reinterpret_cast<uint32_t*>(a.occ + (key & ~3u))),
+                                      0x80u << (8 * (key & 3u)), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
             else if (a.occ_mode == 2)
-                a.occ[key] = 1;
+                G(a.occ)[key] = 1;
             if (a.key_hist) {
                 const unsigned long long after = lm & ~(ltm | (1ull << lane));
-                const unsigned long long upto = after ? ((1ull << (__ffsll((long long)after) - 1)) - 1ull)
-                                                      : ~0ull;
-                const uint32_t run = (uint32_t)__popcll(m & ~ltm & upto);
+                const unsigned long long upto =
+                    after ? ((1ull << (__ffsll((long long)after) - 1)) - 1ull) : ~0ull;
+                const uint32_t rl = (uint32_t)__popcll(vm & ~ltm & upto);
                 for (uint32_t p = 0; p < a.npasses; ++p)
-                    atomicAdd(&s_hist[p * 256 + ((key >> (8 * p)) & 0xFFu)], run);
+                    atomicAdd(&s_hist[p * 256 + ((key >> (8 * p)) & 0xFFu)], rl);
             }
         }
     }
     if (a.key_hist) {
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < a.npasses * 256; i += kEmitThreads)
-            if (s_hist[i]) atomicAdd(&a.key_hist[i], s_hist[i]);
+        for (uint32_t j = threadIdx.x; j < a.npasses * 256; j += blockDim.x)
+            if (s_hist[j])
+                __hip_atomic_fetch_add(G(a.key_hist + j), s_hist[j], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -717,27 +845,26 @@ struct HookScope {  // begin/end of one profiled launch
 };
 
 hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
-    if (a.total_tiles == 0) return hipMemsetAsync(a.out_count, 0, 4, s);
-    const uint32_t mblocks = a.depth_blocks + a.sel_tiles;
-    if (mblocks) {
+    if (a.total_segs == 0) return hipMemsetAsync(a.out_count, 0, 4, s);
+    {
         HookScope hs(hook, GDF_KERNEL_MASK);
+        const size_t lds = (size_t)a.band_lds;
         if (a.rot45)
-            hipLaunchKernelGGL(k_mask<true>, dim3(mblocks), dim3(kFrameThreads), 0, s, a);
+            hipLaunchKernelGGL(k_mask<true>, dim3(a.total_segs), dim3(a.seg_threads), lds, s, a);
         else
-            hipLaunchKernelGGL(k_mask<false>, dim3(mblocks), dim3(kFrameThreads), 0, s, a);
+            hipLaunchKernelGGL(k_mask<false>, dim3(a.total_segs), dim3(a.seg_threads), lds, s, a);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
     if (!a.fused_prefix) {
         HookScope hs(hook, GDF_KERNEL_SCAN);
-        hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, a.tile_counts, a.total_tiles,
-                           a.tile_offsets, a.out_count);
+        hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, a.seg_counts, a.total_segs,
+                           a.seg_offsets, a.out_count);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
     HookScope hs(hook, GDF_KERNEL_EMIT);
-    const uint32_t eblocks = (a.total_tiles * kFrameTile + kEmitThreads - 1) / kEmitThreads;
-    hipLaunchKernelGGL(k_emit, dim3(eblocks), dim3(kEmitThreads), 0, s, a);
+    hipLaunchKernelGGL(k_emit, dim3(a.total_segs), dim3(a.seg_threads), 0, s, a);
     return hipGetLastError();
 }
 

@@ -268,3 +268,14 @@ def test_stable_sort_matches_numpy():
         exp = np.argsort(k, kind="stable")
         np.testing.assert_array_equal(idx, exp)
         np.testing.assert_array_equal(sk, k[exp])
+
+
+def test_max_distance_square_threshold():
+    """The kernels test max_distance as p·p > 100.00001f (0x42C80001) instead of
+    sqrtf(p·p) > 10.0f: identical for every float around the threshold and far from it."""
+    thr = np.uint32(0x42C80001).view(np.float32)
+    v = np.arange(0x42C70000, 0x42C90000, dtype=np.uint32).view(np.float32)
+    np.testing.assert_array_equal(np.sqrt(v) > np.float32(10.0), v > thr)
+    rng = np.random.default_rng(5)
+    w = (rng.random(1 << 20) * 400).astype(np.float32)
+    np.testing.assert_array_equal(np.sqrt(w) > np.float32(10.0), w > thr)

@@ -12,6 +12,20 @@ __global__ void k_empty() {}
 __global__ void k_store(int* p) { if (threadIdx.x == 0 && blockIdx.x == 0) p[0] = 1; }
 __global__ void k_big(Big b) { if (threadIdx.x == 0 && blockIdx.x == 0) b.out[0] = (int)b.v[895]; }
 __global__ void k_ldst(const int* a, int* p) { if (threadIdx.x == 0) p[blockIdx.x] = a[blockIdx.x] + 1; }
+// every block reads 1 KiB of the by-value argument with vector loads (like a per-block LDS copy)
+__global__ void k_bigvec(Big b) {
+    __shared__ float s[256];
+    s[threadIdx.x] = b.v[threadIdx.x * 3];
+    __syncthreads();
+    if (threadIdx.x == 0) b.out[blockIdx.x] = (int)s[(blockIdx.x * 7) & 255];
+}
+// the same 1 KiB read from a device buffer
+__global__ void k_devvec(const float* v, int* out) {
+    __shared__ float s[256];
+    s[threadIdx.x] = v[threadIdx.x * 3];
+    __syncthreads();
+    if (threadIdx.x == 0) out[blockIdx.x] = (int)s[(blockIdx.x * 7) & 255];
+}
 
 template <class F>
 float time_chain(hipStream_t s, int n, F f) {
@@ -37,6 +51,11 @@ int main() {
     printf("empty 1024x256  %.2f us/launch\n", time_chain(s, n, [&] { hipLaunchKernelGGL(k_empty, dim3(1024), dim3(256), 0, s); }));
     printf("store 1x64      %.2f us/launch\n", time_chain(s, n, [&] { hipLaunchKernelGGL(k_store, dim3(1), dim3(64), 0, s, p); }));
     printf("big-arg 1x64    %.2f us/launch\n", time_chain(s, n, [&] { hipLaunchKernelGGL(k_big, dim3(1), dim3(64), 0, s, big); }));
+    float* dv; CK(hipMalloc(&dv, 4096)); CK(hipMemset(dv, 0, 4096));
+    printf("bigvec 1200x256 %.2f us/launch\n", time_chain(s, n, [&] { hipLaunchKernelGGL(k_bigvec, dim3(1200), dim3(256), 0, s, big); }));
+    printf("devvec 1200x256 %.2f us/launch\n", time_chain(s, n, [&] { hipLaunchKernelGGL(k_devvec, dim3(1200), dim3(256), 0, s, dv, p); }));
+    printf("bigvec 32kx256  %.2f us/launch\n", time_chain(s, 200, [&] { hipLaunchKernelGGL(k_bigvec, dim3(32768), dim3(256), 0, s, big); }));
+    printf("devvec 32kx256  %.2f us/launch\n", time_chain(s, 200, [&] { hipLaunchKernelGGL(k_devvec, dim3(32768), dim3(256), 0, s, dv, p); }));
     printf("ld+st 300x256   %.2f us/launch\n", time_chain(s, n, [&] { hipLaunchKernelGGL(k_ldst, dim3(300), dim3(256), 0, s, p, q); }));
     // single-launch latency: record/sync around one launch
     std::vector<float> lat;
