@@ -224,7 +224,8 @@ enum gdf_kernel_slot {
     GDF_KERNEL_SORT = 7,       /* k_sort_pass: one radix pass (the first also updates the grid)   */
     GDF_KERNEL_GROUP_SCAN = 8, /* k_group_scan: voxel group boundaries                            */
     GDF_KERNEL_GROUP_SUM = 9,  /* k_group_sum: ordered per-voxel means                            */
-    GDF_KERNEL_SLOTS = 10
+    GDF_KERNEL_EVENT_FLOOR = 10, /* an event pair around no launch: the timing method's own cost    */
+    GDF_KERNEL_SLOTS = 11
 };
 /* enable: record an event pair around every launch of each slot; reset clears the sums */
 int gdf_set_profiling(gdf_engine* engine, int enable);

@@ -724,6 +724,7 @@ void run_frame(gdf_engine* e, bool fused_voxel) {
     }
     e->dbg_count = e->n_total;
     a.err = e->d_misc.as<uint32_t>() + kErr;
+    if (e->profiling) e->timed(GDF_KERNEL_EVENT_FLOOR, [] {});  // calibrates the event overhead
     e->timed(GDF_KERNEL_FRAME, [&] { HIPCHK(launch_frame(a, e->s(), e->hook_ptr())); });
     e->khist_pending = fused_voxel;
     e->compacted = true;

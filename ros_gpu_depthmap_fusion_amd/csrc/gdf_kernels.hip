@@ -564,7 +564,10 @@ __global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
     extern __shared__ uint4 s_dyn[];  // band rows (a.band_rowb bytes each), then xn
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int nwaves = blockDim.x >> 6;
-    const uint32_t s = blockIdx.x;
+    // XCD-aware: blocks are dealt round-robin over the 8 XCDs (speed only, never correctness),
+    // so give each XCD a contiguous run of segments - neighbouring rows' bands then share its L2
+    const uint32_t n = gridDim.x, q8 = n / 8, r8 = n % 8, xcd = blockIdx.x % 8;
+    const uint32_t s = xcd * q8 + min(xcd, r8) + blockIdx.x / 8;
     load_cams(a, s_cams);
     __syncthreads();
     uint32_t bits = 0;
