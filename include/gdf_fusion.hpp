@@ -1,0 +1,244 @@
+// gdf_fusion.hpp — header-only C++ facade with the interface of the reference engine class
+// `GPUDepthmapFusion` (include/gpu_depthmap_fusion/gpu_depthmap_fusion.h:159-526 of
+// xaedes/ros_gpu_depthmap_fusion), forwarding to the C-ABI in gdf.h.
+//
+// The ROS component (src/gpu_depthmap_fusion_component.cpp) calls the engine through exactly
+// these method names and reads the same public members; INTEGRATION.md shows the swap.
+// No OpenCV / glm / ROS headers are needed here: the overloads taking cv::Mat_<uint16_t>,
+// cv::Matx44f, glm::vec3 and sensor_msgs::PointCloud2 are templates that only touch the members
+// those types have (`data`/`cols`/`rows`, `val[16]`, `x`/`y`/`z`, `data`/`width`/`height`/
+// `point_step`).  Errors of the C-ABI are thrown as std::runtime_error.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "gdf.h"
+
+namespace gdf {
+
+struct vec4 {  // memory layout of glm::vec4 / the reference's vec4 buffers
+    float x, y, z, w;
+};
+
+// the component calls m_measureTime.beginFrame()/endFrame() around addDepthmap
+// (component.cpp:105,155); per-kernel timing lives in gdf_set_profiling / gdf_get_kernel_times
+struct MeasureTime {
+    void beginFrame() {}
+    void endFrame() {}
+    void print(const char*) const {}
+};
+
+class GPUDepthmapFusion {
+public:
+    explicit GPUDepthmapFusion(int device = 0) { check(gdf_create(device, &h_)); }
+    ~GPUDepthmapFusion() { gdf_destroy(h_); }
+    GPUDepthmapFusion(const GPUDepthmapFusion&) = delete;
+    GPUDepthmapFusion& operator=(const GPUDepthmapFusion&) = delete;
+
+    // gpu_depthmap_fusion.cpp:16-128 loads and compiles the GLSL programs here; the HIP kernels
+    // are part of libgdf.so, so there is nothing to load.
+    void init(const std::string& /*shaderPath*/) {}
+
+    void clear() { check(gdf_clear(h_)); }  // :725-732
+
+    // addDepthmap (:798-816); the depth image is borrowed until uploadDepthmaps, as in the
+    // reference (the component keeps the cv_bridge image alive for the frame)
+    template <class DepthMat, class Matx44>
+    void addDepthmap(const DepthMat& depthmap, float depthScale, float fx, float fy, float cx,
+                     float cy, const Matx44& transform_world, const Matx44& transform_crop) {
+        addDepthmap(reinterpret_cast<const uint16_t*>(depthmap.data), (uint32_t)depthmap.cols,
+                    (uint32_t)depthmap.rows, depthScale, fx, fy, cx, cy, transform_world.val,
+                    transform_crop.val);
+    }
+    void addDepthmap(const uint16_t* depth, uint32_t width, uint32_t height, float depthScale,
+                     float fx, float fy, float cx, float cy, const float T_world[16],
+                     const float T_crop[16]) {
+        check(gdf_add_depthmap(h_, depth, width, height, depthScale, fx, fy, cx, cy, T_world,
+                               T_crop));
+    }
+    void addDepthmapDevice(const uint16_t* depth_device, uint32_t width, uint32_t height,
+                           float depthScale, float fx, float fy, float cx, float cy,
+                           const float T_world[16], const float T_crop[16]) {
+        check(gdf_add_depthmap_device(h_, depth_device, width, height, depthScale, fx, fy, cx,
+                                      cy, T_world, T_crop));
+    }
+
+    // addPointSequence (:747-796): x, y, z float32 at byte offsets 0/4/8 of each record
+    template <class PointCloud2, class Matx44>
+    void addPointSequence(const PointCloud2& pointcloud, uint32_t timestampSec,
+                          uint32_t timestampNSec, const Matx44& transform_move) {
+        check(gdf_add_point_sequence(h_, pointcloud.data.data(),
+                                     (uint32_t)(pointcloud.width * pointcloud.height),
+                                     (uint32_t)pointcloud.point_step, timestampSec,
+                                     timestampNSec, transform_move.val));
+    }
+    uint32_t numCollectedPointSequencePoints() {
+        uint32_t n = 0;
+        check(gdf_num_collected_point_sequence_points(h_, &n));
+        return n;
+    }
+
+    // ---- point-sequence rollbuffer chain (:819-1581) ----
+    void uploadPointSequences() { check(gdf_upload_point_sequences(h_)); }
+    void filterNewPointSequences(float threshold, uint32_t filter_size) {
+        check(gdf_filter_new_point_sequences(h_, threshold, filter_size));
+    }
+    void insertNewPointSequencesInRollbuffer() {
+        check(gdf_insert_new_point_sequences(h_));
+        syncRollbuffer();
+    }
+    void rollPointSequenceRollbufferCPU(uint32_t minSec, uint32_t minNSec) {
+        check(gdf_roll_rollbuffer(h_, minSec, minNSec));
+        syncRollbuffer();
+    }
+    // the reference's GPU variant (:1218-1356) is dead code with the same intended result
+    void rollPointSequenceRollbuffer(uint32_t minSec, uint32_t minNSec) {
+        rollPointSequenceRollbufferCPU(minSec, minNSec);
+    }
+    void selectPointSequenceTimespanCPU(uint32_t minSec, uint32_t minNSec, uint32_t maxSec,
+                                        uint32_t maxNSec) {
+        check(gdf_select_timespan(h_, minSec, minNSec, maxSec, maxNSec));
+        syncRollbuffer();
+    }
+    void selectPointSequenceTimespan(uint32_t minSec, uint32_t minNSec, uint32_t maxSec,
+                                     uint32_t maxNSec) {
+        selectPointSequenceTimespanCPU(minSec, minNSec, maxSec, maxNSec);
+    }
+    void preparePointAndMaskBuffers() { check(gdf_prepare_point_and_mask_buffers(h_)); }
+    template <class Matx44>
+    void insertSelectedPointSequence(const Matx44& tf_world_move, const Matx44& tf_crop_move) {
+        check(gdf_insert_selected_point_sequence(h_, tf_world_move.val, tf_crop_move.val));
+    }
+    void transformPointSequence() { check(gdf_transform_point_sequence(h_)); }
+
+    // ---- depth chain (:1583-1839) ----
+    void uploadDepthmaps() { check(gdf_upload_depthmaps(h_)); }
+    void convertDepthmaps() { check(gdf_convert_depthmaps(h_)); }
+    void filterFlyingPixels(uint32_t filter_size, float threshold, bool enable_rot45) {
+        check(gdf_filter_flying_pixels(h_, filter_size, threshold, enable_rot45 ? 1 : 0));
+    }
+    template <class Vec3>
+    void cropPoints(const Vec3& lower_bound, const Vec3& upper_bound) {
+        const float lo[3] = {lower_bound.x, lower_bound.y, lower_bound.z};
+        const float hi[3] = {upper_bound.x, upper_bound.y, upper_bound.z};
+        check(gdf_crop_points(h_, lo, hi));
+    }
+    void applyPointMask() {
+        uint32_t n = 0;
+        check(gdf_apply_point_mask(h_, &n));
+        m_numPoints = (int)n;
+    }
+    template <class Vec3>
+    void computeVoxelCoords(const Vec3& lower_bound, const Vec3& upper_bound,
+                            const Vec3& cell_size) {
+        const float lo[3] = {lower_bound.x, lower_bound.y, lower_bound.z};
+        const float hi[3] = {upper_bound.x, upper_bound.y, upper_bound.z};
+        const float cs[3] = {cell_size.x, cell_size.y, cell_size.z};
+        check(gdf_compute_voxel_coords(h_, lo, hi, cs));
+        for (int i = 0; i < 3; ++i) {  // GridMeta (grid_meta.h:140-158): sorted bounds
+            lo_[i] = lo[i] < hi[i] ? lo[i] : hi[i];
+            cs_[i] = cs[i];
+        }
+    }
+    void downloadVoxelCoords() {
+        uint32_t n = count();
+        m_voxelCoords.resize(n);
+        check(gdf_download_voxel_coords(h_, m_voxelCoords.data(), n, &n));
+        m_voxelCoords.resize(n);
+    }
+    // voxelize (:1743-1756): on the GPU; m_points_voxelized is filled like the reference's
+    void voxelize(bool average_voxels) {
+        check(gdf_voxelize(h_, average_voxels ? 1 : 0));
+        uint32_t n = count();
+        m_points_voxelized.resize(n);
+        check(gdf_download_voxelized_points(h_, reinterpret_cast<float*>(m_points_voxelized.data()),
+                                            n, &n));
+        m_points_voxelized.resize(n);
+    }
+    void voxelOccupancyGrid(uint32_t lifetime) { check(gdf_voxel_occupancy_grid(h_, lifetime)); }
+    void downloadVoxelOccupancyGrid() {
+        uint32_t gs[3];
+        uint64_t cells = 0;
+        check(gdf_get_grid_size(h_, gs, &cells));
+        m_occupancyGrid.resize(cells);
+        check(gdf_download_occupancy_grid(h_, m_occupancyGrid.data(), cells));
+        for (int i = 0; i < 3; ++i) gridSize_[i] = gs[i];
+    }
+    // m_occupancyLayers[z] of the reference is a (gy x gx) uint8 view of layer z
+    const uint8_t* occupancyLayer(uint32_t z) const {
+        return m_occupancyGrid.data() + (size_t)z * gridSize_[0] * gridSize_[1];
+    }
+    void downloadPoints() {
+        uint32_t n = count();
+        m_points.resize(n);
+        check(gdf_download_points(h_, reinterpret_cast<float*>(m_points.data()), n, &n));
+        m_points.resize(n);
+    }
+    // GridMeta::worldCoord: lower corner of voxel (x, y, z)
+    vec4 voxelCoordToWorldCoord(float x, float y, float z) const {
+        return vec4{x * cs_[0] + lo_[0], y * cs_[1] + lo_[1], z * cs_[2] + lo_[2], 1.0f};
+    }
+
+    // the component's whole per-frame sequence as one call (gdf_process_frame)
+    gdf_frame_result processFrame(const gdf_frame_params& params) {
+        gdf_frame_result r{};
+        check(gdf_process_frame(h_, &params, &r));
+        if (params.synchronous) m_numPoints = (int)r.num_points;
+        syncRollbuffer();
+        return r;
+    }
+
+    gdf_rollbuffer_state rollbufferState() {
+        gdf_rollbuffer_state s{};
+        check(gdf_get_rollbuffer_state(h_, &s));
+        return s;
+    }
+    gdf_engine* handle() const { return h_; }
+
+    // public members the component reads (gpu_depthmap_fusion.h:318-362)
+    int m_voxelGroupSize = 8;
+    std::vector<uint8_t> m_occupancyGrid;
+    std::vector<vec4> m_points;
+    std::vector<vec4> m_points_voxelized;
+    std::vector<uint32_t> m_voxelCoords;
+    int m_numPoints = 0;
+    MeasureTime m_measureTime;
+    // m_rollBuffer* (gpu_depthmap_fusion.h:345-354), refreshed after every rollbuffer call
+    uint32_t m_rollBufferNumPoints = 0, m_rollBufferNumSeqs = 0;
+    uint32_t m_rollBufferSelectionPointStart = 0, m_rollBufferSelectionPointCount = 0;
+    uint32_t m_rollBufferSelectionSequenceStart = 0, m_rollBufferSelectionSequenceCount = 0;
+    uint32_t m_rollBufferEarliestTimeSec = 0, m_rollBufferEarliestTimeNSec = 0;
+    uint32_t m_rollBufferLastTimeSec = 0, m_rollBufferLastTimeNSec = 0;
+
+private:
+    void syncRollbuffer() {
+        const gdf_rollbuffer_state r = rollbufferState();
+        m_rollBufferNumPoints = r.num_points;
+        m_rollBufferNumSeqs = r.num_seqs;
+        m_rollBufferSelectionPointStart = r.selection_point_start;
+        m_rollBufferSelectionPointCount = r.selection_point_count;
+        m_rollBufferSelectionSequenceStart = r.selection_sequence_start;
+        m_rollBufferSelectionSequenceCount = r.selection_sequence_count;
+        m_rollBufferEarliestTimeSec = r.earliest_time_sec;
+        m_rollBufferEarliestTimeNSec = r.earliest_time_nsec;
+        m_rollBufferLastTimeSec = r.last_time_sec;
+        m_rollBufferLastTimeNSec = r.last_time_nsec;
+    }
+    static void check(int rc) {
+        if (rc != GDF_OK) throw std::runtime_error(std::string("gdf: ") + gdf_last_error());
+    }
+    uint32_t count() {
+        uint32_t n = 0;
+        check(gdf_get_point_count(h_, &n));
+        return n;
+    }
+    gdf_engine* h_ = nullptr;
+    float lo_[3] = {0, 0, 0}, cs_[3] = {1, 1, 1};
+    uint32_t gridSize_[3] = {0, 0, 0};
+};
+
+}  // namespace gdf
