@@ -70,7 +70,6 @@ def main():
     params = ComponentParams()
     eng = GPUDepthmapFusion(local_rank)
 
-    words = None
     if dist is not None:
         import torch
         stream = torch.cuda.current_stream()
@@ -91,9 +90,8 @@ def main():
     (gx, gy, gz), ncells = eng.grid_size()
 
     if dist is not None:
-        words = (ncells + 31) // 32
-        local_bits = torch.zeros(words, dtype=torch.int32, device="cuda")
-        all_bits = torch.zeros(world * words, dtype=torch.int32, device="cuda")
+        from ros_gpu_depthmap_fusion_amd.multi import DeviceMarkExchange
+        marks = DeviceMarkExchange(eng, ncells, world)
 
     pc_plain = params.to_c(None, None, False, False)
     pc_defer = params.to_c(None, None, False, True)
@@ -104,9 +102,7 @@ def main():
             eng.processFramePrepared(pc_plain)
         else:
             eng.processFramePrepared(pc_defer)
-            eng.export_marks(local_bits.data_ptr(), words)
-            dist.all_gather_into_tensor(all_bits, local_bits)
-            eng.import_marks(all_bits.data_ptr(), words, world)
+            marks.exchange()  # occupancy union over RCCL (multi.py)
             eng.voxelOccupancyGrid(params.occupancy_lifetime)
 
     def barrier_sync():
@@ -159,15 +155,15 @@ def main():
         # 3 radix passes (key only in, key+index out; then key+index both ways) + the grid
         # update carried by the first pass, averaged per launch
         "sort": (12.0 * n_avg + 16.0 * n_avg * 2 + 2.0 * ncells) / 3.0,
-        "group_scan": 4.0 * n_avg + 4.0 * g_avg,
-        "group_sum": 20.0 * n_avg + 20.0 * g_avg,  # indices + gathered points in, means out
+        # sorted keys + indices + gathered points in, means out
+        "group": 24.0 * n_avg + 16.0 * g_avg,
         "grid": 2.0 * ncells,
     }
     survey_bytes = 2.0 * P + 24.0 * n_avg + 9.0 * ncells  # SURVEY.md §8(d) B_alg per frame
 
     roofline = None
     if ktimes:
-        singles = [k for k in ("mask", "scan", "emit", "sort", "group_scan", "group_sum", "grid")
+        singles = [k for k in ("mask", "scan", "emit", "sort", "group", "grid")
                    if ktimes[k][1]]
         per_step = {k: ktimes[k][0] / kt_steps for k in singles}  # ms per step
         slot = max(singles, key=lambda k: per_step[k])

@@ -222,8 +222,8 @@ enum gdf_kernel_slot {
     GDF_KERNEL_SCAN = 5,       /* k_scan_counts (frames over 1 Mi items only)                     */
     GDF_KERNEL_EMIT = 6,       /* k_emit: ordered compaction + voxel keys + marks + digit hist    */
     GDF_KERNEL_SORT = 7,       /* k_sort_pass: one radix pass (the first also updates the grid)   */
-    GDF_KERNEL_GROUP_SCAN = 8, /* k_group_scan: voxel group boundaries                            */
-    GDF_KERNEL_GROUP_SUM = 9,  /* k_group_sum: ordered per-voxel means                            */
+    GDF_KERNEL_GROUP = 8,      /* k_group: voxel groups of the sorted keys + ordered per-voxel means */
+    GDF_KERNEL_RESERVED9 = 9,
     GDF_KERNEL_EVENT_FLOOR = 10, /* an event pair around no launch: the timing method's own cost    */
     GDF_KERNEL_SLOTS = 11
 };

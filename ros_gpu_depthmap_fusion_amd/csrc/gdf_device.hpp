@@ -19,8 +19,6 @@ constexpr uint32_t kSegItems = 1024;  // items per compaction segment (max)
 constexpr uint32_t kFusedPrefixSegs = 4096;  // up to this many segments k_emit sums the counts
 constexpr int kSortThreads = 256;
 constexpr int kGroupThreads = 256;
-constexpr int kGroupPerThread = 8;
-constexpr int kGroupTile = kGroupThreads * kGroupPerThread;  // 2048 sorted keys per tile
 constexpr int kSumChunk = 256;                               // points per wave gather chunk
 constexpr uint32_t kSpinLimit = 1u << 26;                   // bounded look-back spins
 
@@ -82,10 +80,9 @@ struct FrameArgs {
     const float* tfc;
     // voxel keys + occupancy marks (compute_voxel_coords + voxel_grid_occupancy_of_points)
     int32_t do_voxel;
-    int32_t occ_mode;           // 0 none, 1 mark bit 7 of the u8 grid, 2 set u8 flag array
     float vlo[3], vcs[3], gmax[3];
     uint32_t gs[3];
-    uint8_t* occ;
+    uint32_t* marks;            // occupancy mark bitmask (cell c -> bit c % 32 of word c / 32)
     uint32_t* key_hist;         // optional [npasses*256] digit histogram of the keys
     uint32_t npasses;
     // outputs

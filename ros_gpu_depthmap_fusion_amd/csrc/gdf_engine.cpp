@@ -228,13 +228,13 @@ struct gdf_engine {
     uint64_t ncells = 0;
     uint32_t key_bits = 0;
     VoxelParams vp{};
-    DevBuf d_grid8, d_hist32, d_marks, d_out8;
-    int grid_mode = 0;  // 0: u8 grid with mark bit 7; 1: u32 history + u8 marks + u8 output
+    DevBuf d_grid8, d_hist32, d_markbits, d_out8;
+    int grid_mode = 0;  // 0: u8 grid = history (lifetime <= 255); 1: u32 history + u8 output
     bool grid_alloc = false;
     bool invoked_once = false;
 
     // voxelize
-    DevBuf d_ka, d_kb, d_va, d_vb, d_sstatus, d_sgstatus, d_gstatus, d_ggstatus, d_gstart, d_vox;
+    DevBuf d_ka, d_kb, d_va, d_vb, d_sstatus, d_sgstatus, d_gstatus, d_ggstatus, d_vox;
     bool vox_valid = false;
 
     bool debug = false;
@@ -626,18 +626,28 @@ void set_grid(gdf_engine* e, const float* lo, const float* hi, const float* cs) 
     e->ncells = cells;
     e->grid_set = true;
     if (changed) {  // historic grid cleared on first use / resize (fusion.cpp:1759-1773)
-        const size_t padded = (size_t)((cells + 15) / 16) * 16;
+        const size_t padded = (size_t)((cells + 31) / 32) * 32;
         e->d_grid8.ensure(padded);
         HIPCHK(hipMemsetAsync(e->d_grid8.p, 0, padded, e->s()));
+        e->d_markbits.ensure(padded / 8);
+        HIPCHK(hipMemsetAsync(e->d_markbits.p, 0, padded / 8, e->s()));
         e->grid_mode = 0;
         e->grid_alloc = true;
         e->marks_set = false;
     }
 }
 
-int occ_mode(const gdf_engine* e) { return e->grid_mode == 0 ? 1 : 2; }
-uint8_t* occ_ptr(const gdf_engine* e) {
-    return e->grid_mode == 0 ? e->d_grid8.as<uint8_t>() : e->d_marks.as<uint8_t>();
+// the frame's occupancy marks: 1 bit per cell, consumed (and cleared) by the grid update
+uint32_t* marks_ptr(const gdf_engine* e) { return e->d_markbits.as<uint32_t>(); }
+uint64_t mark_words(const gdf_engine* e) { return (e->ncells + 31) / 32; }
+
+// switch to the general u32 history once a lifetime no longer fits the u8 grid
+void widen_if_needed(gdf_engine* e, uint32_t lifetime, hipStream_t st) {
+    if (e->grid_mode != 0 || lifetime <= 255) return;
+    e->d_hist32.ensure((size_t)e->ncells * 4);
+    e->d_out8.ensure((size_t)((e->ncells + 31) / 32) * 32);
+    HIPCHK(launch_widen_grid(e->d_grid8.as<uint8_t>(), e->d_hist32.as<uint32_t>(), e->ncells, st));
+    e->grid_mode = 1;
 }
 
 void ensure_misc(gdf_engine* e) {
@@ -689,8 +699,7 @@ void run_frame(gdf_engine* e, bool fused_voxel) {
     a.tfc = e->d_tfc.as<float>();
     a.do_voxel = fused_voxel ? 1 : 0;
     if (fused_voxel) {
-        a.occ_mode = occ_mode(e);
-        a.occ = occ_ptr(e);
+        a.marks = marks_ptr(e);
         std::memcpy(a.vlo, e->vp.vlo, 12);
         std::memcpy(a.vcs, e->vp.vcs, 12);
         std::memcpy(a.gmax, e->vp.gmax, 12);
@@ -751,7 +760,6 @@ void voxelize(gdf_engine* e, int average, int fused_grid_lifetime = -1) {  // fu
     e->d_kb.ensure((size_t)nmax * 4);
     e->d_va.ensure((size_t)nmax * 4);
     e->d_vb.ensure((size_t)nmax * 4);
-    e->d_gstart.ensure((size_t)nmax * 4);
     e->d_sstatus.ensure_zero(voxelize_status_words(nmax) * 8, e->s());
     e->d_sgstatus.ensure_zero((voxelize_status_words(nmax) / 16 + 256) * 8, e->s());
     e->d_gstatus.ensure_zero(voxelize_group_tiles(nmax) * 8, e->s());
@@ -775,7 +783,6 @@ void voxelize(gdf_engine* e, int average, int fused_grid_lifetime = -1) {  // fu
     v.sgstatus = e->d_sgstatus.as<unsigned long long>();
     v.gstatus = e->d_gstatus.as<unsigned long long>();
     v.ggstatus = e->d_ggstatus.as<unsigned long long>();
-    v.gstart = e->d_gstart.as<uint32_t>();
     v.ctrs = e->d_ctrs.as<unsigned long long>();
     v.epoch = &e->epoch;
     v.sort_pt = e->sort_pt;
@@ -784,6 +791,7 @@ void voxelize(gdf_engine* e, int average, int fused_grid_lifetime = -1) {  // fu
     v.out_count = e->d_misc.as<uint32_t>() + kVoxCount;
     if (fused_grid_lifetime >= 0) {  // processFrame: the grid update rides on the first sort pass
         v.grid8 = e->d_grid8.as<uint8_t>();
+        v.marks = marks_ptr(e);
         v.ncells = e->ncells;
         v.lifetime = (uint32_t)fused_grid_lifetime;
     }
@@ -798,25 +806,17 @@ void voxelize(gdf_engine* e, int average, int fused_grid_lifetime = -1) {  // fu
 
 void occupancy_grid(gdf_engine* e, uint32_t lifetime, hipStream_t st) {  // fusion.cpp:1757-1823
     if (!e->grid_set) fail(GDF_ERR_STATE, "voxelOccupancyGrid before computeVoxelCoords");
-    if (e->grid_mode == 0 && lifetime > 127) {
-        // widen the u8 grid (values <= 127, mark in bit 7) into the general u32 history
-        e->d_hist32.ensure((size_t)e->ncells * 4);
-        e->d_marks.ensure((size_t)e->ncells);
-        e->d_out8.ensure((size_t)((e->ncells + 15) / 16) * 16);
-        HIPCHK(launch_widen_grid(e->d_grid8.as<uint8_t>(), e->d_hist32.as<uint32_t>(),
-                                 e->d_marks.as<uint8_t>(), e->ncells, st));
-        e->grid_mode = 1;
-    }
+    widen_if_needed(e, lifetime, st);
     if (!e->marks_set) {
         if (!e->coords_valid) fail(GDF_ERR_STATE, "voxelOccupancyGrid needs voxel coordinates");
         HIPCHK(launch_scatter(e->d_coords.as<uint32_t>(), e->d_misc.as<uint32_t>() + kCount,
-                              std::max<uint32_t>(e->n_total, 1), occ_ptr(e), occ_mode(e), st));
+                              std::max<uint32_t>(e->n_total, 1), marks_ptr(e), st));
     }
     e->timed_on(GDF_KERNEL_GRID, st, [&] {
         if (e->grid_mode == 0)
-            HIPCHK(launch_grid_u8(e->d_grid8.as<uint8_t>(), e->ncells, lifetime, st));
+            HIPCHK(launch_grid_u8(e->d_grid8.as<uint8_t>(), marks_ptr(e), e->ncells, lifetime, st));
         else
-            HIPCHK(launch_grid_u32(e->d_hist32.as<uint32_t>(), e->d_marks.as<uint8_t>(),
+            HIPCHK(launch_grid_u32(e->d_hist32.as<uint32_t>(), marks_ptr(e),
                                    e->d_out8.as<uint8_t>(), e->ncells, lifetime, st));
     });
     e->marks_set = false;
@@ -1135,8 +1135,6 @@ int gdf_download_occupancy_grid(gdf_engine* e, uint8_t* out, uint64_t cap) {
         if (!out || cap < e->ncells) fail(GDF_ERR_CAPACITY, "occupancy grid: buffer too small");
         e->sync();
         HIPCHK(hipMemcpy(out, grid_out_ptr(e), e->ncells, hipMemcpyDeviceToHost));
-        if (e->grid_mode == 0 && e->marks_set)  // pending marks of the next frame: hide bit 7
-            for (uint64_t c = 0; c < e->ncells; ++c) out[c] &= 0x7Fu;
     });
 }
 
@@ -1210,15 +1208,7 @@ int gdf_process_frame(gdf_engine* e, const gdf_frame_params* p, gdf_frame_result
         std::memcpy(e->hi, p->crop_max, 12);
         if (p->enable_voxel_filter) {
             set_grid(e, p->voxel_min, p->voxel_max, p->voxel_size);
-            if (e->grid_mode == 0 && p->occupancy_lifetime > 127) {
-                // switch representation before marks are written
-                e->d_hist32.ensure((size_t)e->ncells * 4);
-                e->d_marks.ensure((size_t)e->ncells);
-                e->d_out8.ensure((size_t)((e->ncells + 15) / 16) * 16);
-                HIPCHK(launch_widen_grid(e->d_grid8.as<uint8_t>(), e->d_hist32.as<uint32_t>(),
-                                         e->d_marks.as<uint8_t>(), e->ncells, e->s()));
-                e->grid_mode = 1;
-            }
+            widen_if_needed(e, p->occupancy_lifetime, e->s());  // before marks are consumed
             run_frame(e, true);
             if (!p->defer_occupancy_grid && e->grid_mode == 0) {
                 voxelize(e, p->voxel_average, (int)p->occupancy_lifetime);
@@ -1245,7 +1235,7 @@ int gdf_export_occupancy_marks(gdf_engine* e, uint32_t* bits, uint64_t words) {
     return guarded(e, [&] {
         if (!e->grid_set || !bits) fail(GDF_ERR_STATE, "no voxel grid");
         if (words < (e->ncells + 31) / 32) fail(GDF_ERR_CAPACITY, "mark bitmask too small");
-        HIPCHK(launch_export_marks(occ_ptr(e), occ_mode(e), e->ncells, bits, e->s()));
+        HIPCHK(launch_export_marks(marks_ptr(e), mark_words(e), bits, e->s()));
     });
 }
 
@@ -1254,7 +1244,7 @@ int gdf_import_occupancy_marks(gdf_engine* e, const uint32_t* bits, uint64_t wor
     return guarded(e, [&] {
         if (!e->grid_set || !bits) fail(GDF_ERR_STATE, "no voxel grid");
         if (words < (e->ncells + 31) / 32) fail(GDF_ERR_CAPACITY, "mark bitmask too small");
-        HIPCHK(launch_import_marks(occ_ptr(e), occ_mode(e), e->ncells, bits, words, nranks, e->s()));
+        HIPCHK(launch_import_marks(marks_ptr(e), mark_words(e), bits, nranks, e->s()));
         e->marks_set = true;
     });
 }
@@ -1351,7 +1341,7 @@ int gdf_debug_historic_grid(gdf_engine* e, uint32_t* out, uint64_t cap) {
         } else {
             std::vector<uint8_t> g(e->ncells);
             HIPCHK(hipMemcpy(g.data(), e->d_grid8.p, e->ncells, hipMemcpyDeviceToHost));
-            for (uint64_t c = 0; c < e->ncells; ++c) out[c] = g[c] & 0x7Fu;
+            for (uint64_t c = 0; c < e->ncells; ++c) out[c] = g[c];
         }
     });
 }

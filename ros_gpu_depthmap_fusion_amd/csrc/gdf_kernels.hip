@@ -811,12 +811,9 @@ __global__ __launch_bounds__(1024) void k_emit(FrameArgs a) {
         const bool leader = valid && (prev < 0 || pkey != key);
         const unsigned long long lm = __ballot(leader);
         if (leader) {
-            if (a.occ_mode == 1)
-                __hip_atomic_fetch_or(G(reinterpret_cast<uint32_t*>(a.occ + (key & ~3u))),
-                                      0x80u << (8 * (key & 3u)), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT);
-            else if (a.occ_mode == 2)
-                G(a.occ)[key] = 1;
+            if (a.marks)
+                __hip_atomic_fetch_or(G(a.marks + (key >> 5)), 1u << (key & 31u),
+                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (a.key_hist) {
                 const unsigned long long after = lm & ~(ltm | (1ull << lane));
                 const unsigned long long upto =
@@ -936,35 +933,49 @@ hipError_t launch_ps_filter_insert(const float4* new_pts, uint32_t n, int do_fil
 }
 
 // ---- historic occupancy grid ---------------------------------------------------------------------
-// new = mark ? max(sat_dec(h), L) : sat_dec(h); output byte = new & 0xFF (L <= 127 keeps bit 7 free)
-__device__ __forceinline__ uint32_t grid_byte(uint32_t h, uint32_t L) {
-    const uint32_t v = h & 0x7Fu;
-    const uint32_t dec = v ? v - 1u : 0u;
-    return (h & 0x80u) ? (dec > L ? dec : L) : dec;
+// Occupancy marks of a frame are a bitmask (cell c -> bit c % 32 of word c / 32), set by k_emit /
+// k_scatter and consumed - read and cleared - by the grid update.  hist' = max(sat_dec(hist),
+// mark·L) (decrement_uints.glsl:31-51 + max_with_uints_times_scalar.glsl:36-46); the output byte is
+// hist & 0xFF (uints_to_chars.glsl:31-50).  With L <= 255 the u8 grid IS the history.
+__device__ __forceinline__ uint32_t grid_byte(uint32_t h, uint32_t m, uint32_t L) {
+    const uint32_t dec = h ? h - 1u : 0u;
+    return m ? (dec > L ? dec : L) : dec;
 }
 
-__device__ __forceinline__ uint32_t grid_word(uint32_t w, uint32_t L) {
-    return grid_byte(w & 0xFFu, L) | (grid_byte((w >> 8) & 0xFFu, L) << 8) |
-           (grid_byte((w >> 16) & 0xFFu, L) << 16) | (grid_byte(w >> 24, L) << 24);
+// 4 cells of a u32 word of the u8 grid, marks in bits 0..3 of mb
+__device__ __forceinline__ uint32_t grid_word(uint32_t w, uint32_t mb, uint32_t L) {
+    return grid_byte(w & 0xFFu, mb & 1u, L) | (grid_byte((w >> 8) & 0xFFu, (mb >> 1) & 1u, L) << 8) |
+           (grid_byte((w >> 16) & 0xFFu, (mb >> 2) & 1u, L) << 16) |
+           (grid_byte(w >> 24, (mb >> 3) & 1u, L) << 24);
 }
 
-// blocks [0, nblocks) of a launch update the u8 grid, 16 cells per thread and step
-__device__ __forceinline__ void grid_u8_part(uint4* __restrict__ grid, uint64_t nvec, uint32_t L,
-                                             uint32_t block, uint32_t nblocks) {
-    for (uint64_t i = block * (uint64_t)blockDim.x + threadIdx.x; i < nvec;
+// blocks [0, nblocks) of a launch update the u8 grid: 32 cells (two 16-byte vectors and one mark
+// word) per thread and step; the grid allocation is padded to 32 bytes
+__device__ __forceinline__ void grid_u8_part(uint4* __restrict__ grid, uint32_t* __restrict__ marks,
+                                             uint64_t nwords, uint32_t L, uint32_t block,
+                                             uint32_t nblocks) {
+    for (uint64_t i = block * (uint64_t)blockDim.x + threadIdx.x; i < nwords;
          i += (uint64_t)nblocks * blockDim.x) {
-        uint4 v = grid[i];
-        v.x = grid_word(v.x, L);
-        v.y = grid_word(v.y, L);
-        v.z = grid_word(v.z, L);
-        v.w = grid_word(v.w, L);
-        grid[i] = v;
+        uint4 v0 = grid[2 * i], v1 = grid[2 * i + 1];
+        const uint32_t m = marks[i];
+        v0.x = grid_word(v0.x, m, L);
+        v0.y = grid_word(v0.y, m >> 4, L);
+        v0.z = grid_word(v0.z, m >> 8, L);
+        v0.w = grid_word(v0.w, m >> 12, L);
+        v1.x = grid_word(v1.x, m >> 16, L);
+        v1.y = grid_word(v1.y, m >> 20, L);
+        v1.z = grid_word(v1.z, m >> 24, L);
+        v1.w = grid_word(v1.w, m >> 28, L);
+        grid[2 * i] = v0;
+        grid[2 * i + 1] = v1;
+        if (m) marks[i] = 0u;
     }
 }
 
-__global__ __launch_bounds__(256) void k_grid_u8(uint4* __restrict__ grid, uint64_t nvec,
+__global__ __launch_bounds__(256) void k_grid_u8(uint4* __restrict__ grid,
+                                                 uint32_t* __restrict__ marks, uint64_t nwords,
                                                  uint32_t L) {
-    grid_u8_part(grid, nvec, L, blockIdx.x, gridDim.x);
+    grid_u8_part(grid, marks, nwords, L, blockIdx.x, gridDim.x);
 }
 
 static unsigned grid_blocks(uint64_t work, unsigned per_block) {
@@ -974,51 +985,56 @@ static unsigned grid_blocks(uint64_t work, unsigned per_block) {
     return (unsigned)b;
 }
 
-hipError_t launch_grid_u8(uint8_t* grid, uint64_t ncells, uint32_t lifetime, hipStream_t s) {
-    const uint64_t nvec = (ncells + 15) / 16;  // grid allocation is padded to 16 bytes
-    hipLaunchKernelGGL(k_grid_u8, dim3(grid_blocks(nvec, 256)), dim3(256), 0, s,
-                       reinterpret_cast<uint4*>(grid), nvec, lifetime);
+hipError_t launch_grid_u8(uint8_t* grid, uint32_t* marks, uint64_t ncells, uint32_t lifetime,
+                          hipStream_t s) {
+    const uint64_t nwords = (ncells + 31) / 32;
+    hipLaunchKernelGGL(k_grid_u8, dim3(grid_blocks(nwords, 256)), dim3(256), 0, s,
+                       reinterpret_cast<uint4*>(grid), marks, nwords, lifetime);
     return hipGetLastError();
 }
 
+// general u32 history (lifetime > 255) with a separate u8 output grid; 32 cells per thread
 __global__ __launch_bounds__(256) void k_grid_u32(uint32_t* __restrict__ hist,
-                                                  uint8_t* __restrict__ marks,
+                                                  uint32_t* __restrict__ marks,
                                                   uint8_t* __restrict__ out8, uint64_t ncells,
                                                   uint32_t L) {
-    for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < ncells;
-         c += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t h = hist[c];
-        const uint32_t dec = h >= 1u ? h - 1u : 0u;
-        const uint32_t m = marks[c] ? L : 0u;
-        const uint32_t nv = dec > m ? dec : m;
-        hist[c] = nv;
-        out8[c] = (uint8_t)(nv & 0xFFu);
-        if (marks[c]) marks[c] = 0;
+    const uint64_t nwords = (ncells + 31) / 32;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nwords;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t m = marks[i];
+        for (uint32_t b = 0; b < 32; ++b) {
+            const uint64_t c = 32 * i + b;
+            if (c >= ncells) break;
+            const uint32_t h = hist[c];
+            const uint32_t dec = h >= 1u ? h - 1u : 0u;
+            const uint32_t mv = ((m >> b) & 1u) ? L : 0u;
+            const uint32_t nv = dec > mv ? dec : mv;
+            hist[c] = nv;
+            out8[c] = (uint8_t)(nv & 0xFFu);
+        }
+        if (m) marks[i] = 0u;
     }
 }
 
-hipError_t launch_grid_u32(uint32_t* hist, uint8_t* marks, uint8_t* out8, uint64_t ncells,
+hipError_t launch_grid_u32(uint32_t* hist, uint32_t* marks, uint8_t* out8, uint64_t ncells,
                            uint32_t lifetime, hipStream_t s) {
-    hipLaunchKernelGGL(k_grid_u32, dim3(grid_blocks(ncells, 256)), dim3(256), 0, s, hist, marks,
-                       out8, ncells, lifetime);
+    hipLaunchKernelGGL(k_grid_u32, dim3(grid_blocks((ncells + 31) / 32, 256)), dim3(256), 0, s,
+                       hist, marks, out8, ncells, lifetime);
     return hipGetLastError();
 }
 
+// u8 history -> u32 history (switch to lifetime > 255)
 __global__ __launch_bounds__(256) void k_widen(const uint8_t* __restrict__ g8,
-                                               uint32_t* __restrict__ hist,
-                                               uint8_t* __restrict__ marks, uint64_t ncells) {
+                                               uint32_t* __restrict__ hist, uint64_t ncells) {
     for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < ncells;
-         c += (uint64_t)gridDim.x * blockDim.x) {
-        const uint8_t h = g8[c];
-        hist[c] = h & 0x7Fu;
-        marks[c] = (h & 0x80u) ? 1 : 0;
-    }
+         c += (uint64_t)gridDim.x * blockDim.x)
+        hist[c] = g8[c];
 }
 
-hipError_t launch_widen_grid(const uint8_t* grid8, uint32_t* hist, uint8_t* marks,
-                             uint64_t ncells, hipStream_t s) {
+hipError_t launch_widen_grid(const uint8_t* grid8, uint32_t* hist, uint64_t ncells,
+                             hipStream_t s) {
     hipLaunchKernelGGL(k_widen, dim3(grid_blocks(ncells, 256)), dim3(256), 0, s, grid8, hist,
-                       marks, ncells);
+                       ncells);
     return hipGetLastError();
 }
 
@@ -1042,23 +1058,18 @@ hipError_t launch_coords(const float4* pts, const uint32_t* count, uint32_t nmax
 
 __global__ __launch_bounds__(256) void k_scatter(const uint32_t* __restrict__ coords,
                                                  const uint32_t* __restrict__ count,
-                                                 uint8_t* occ, int mode) {
+                                                 uint32_t* __restrict__ marks) {
     const uint32_t n = *count;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t key = coords[i];
-        if (mode == 1) {
-            const uint8_t h = occ[key];
-            if (!(h & 0x80u)) occ[key] = (uint8_t)(h | 0x80u);
-        } else {
-            occ[key] = 1;
-        }
+        const uint32_t k = coords[i];
+        atomicOr(&marks[k >> 5], 1u << (k & 31u));
     }
 }
 
 hipError_t launch_scatter(const uint32_t* coords, const uint32_t* count, uint32_t nmax,
-                          uint8_t* occ, int mode, hipStream_t s) {
+                          uint32_t* marks, hipStream_t s) {
     hipLaunchKernelGGL(k_scatter, dim3(grid_blocks(nmax, 256)), dim3(256), 0, s, coords, count,
-                       occ, mode);
+                       marks);
     return hipGetLastError();
 }
 
@@ -1101,10 +1112,11 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
     uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, const uint32_t* __restrict__ count,
     const uint32_t* __restrict__ ghist, unsigned long long* status, unsigned long long* gstatus,
     uint32_t* tile_ctr, uint32_t epoch, uint32_t* err, uint32_t shift, uint32_t dbits,
-    uint32_t grid_block0, uint4* grid, uint64_t grid_nvec, uint32_t lifetime) {
+    uint32_t grid_block0, uint4* grid, uint32_t* marks, uint64_t grid_nwords, uint32_t lifetime) {
     constexpr int kTile = kSortThreads * PT;
     if (blockIdx.x >= grid_block0) {  // fused historic-grid update (first pass only)
-        grid_u8_part(grid, grid_nvec, lifetime, blockIdx.x - grid_block0, gridDim.x - grid_block0);
+        grid_u8_part(grid, marks, grid_nwords, lifetime, blockIdx.x - grid_block0,
+                     gridDim.x - grid_block0);
         return;
     }
     __shared__ uint32_t s_cnt[4][256];
@@ -1174,88 +1186,170 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
     }
 }
 
-// Group boundaries of the sorted keys and group ids (look-back scan): gstart[g] = first sorted
-// position of voxel group g (RadixGrouper::makeGroups, inc/radix_grouper.h:35-64).  Also clears
-// the digit histogram for the next voxelize (its last reader was the final sort pass).
-__global__ __launch_bounds__(kGroupThreads) void k_group_scan(
-    const uint32_t* __restrict__ keys, const uint32_t* __restrict__ count,
-    uint32_t* __restrict__ gstart, uint32_t* __restrict__ out_count, unsigned long long* status,
-    unsigned long long* gstatus, uint32_t* tile_ctr, uint32_t epoch, uint32_t* err,
-    uint32_t* hist) {
+// Voxel groups of the sorted keys and their outputs in ONE kernel (RadixGrouper::makeGroups,
+// inc/radix_grouper.h:35-64, + averageGridCells / occupiedGridCells, inc/voxelize.h:9-71).
+// Tile = 256 sorted keys: group starts (key != previous key), their ids by a block scan plus a
+// decoupled look-back over tiles, then the outputs of the groups that START in this tile.
+// average: the sequential f32 sum in stable (index) order, x/y/z divided by the count, w the
+// un-divided sum.  The points of the tile's groups (up to kStagePts) are gathered into LDS by the
+// whole block, then each group is summed by its owning thread; groups reaching past the staged
+// range are summed by a wave (chunks staged through LDS, lanes 0..3 each run one component's
+// dependent add chain).  !average: the voxel's lower corner (GridMeta::worldCoord).
+// Block 0 also clears the digit histogram for the next voxelize (its last reader was the final
+// sort pass).
+constexpr int kStagePts = 1024;  // points of a tile's groups staged in LDS (16 KiB)
+constexpr int kSmallGroup = 16;  // groups summed by one thread; longer ones by a wave
+
+__device__ __forceinline__ void group_corner(uint32_t key, const VoxelParams& vp, float* o) {
+    const uint32_t gx = key % vp.gs[0];
+    const uint32_t gy = (key / vp.gs[0]) % vp.gs[1];
+    const uint32_t gz = key / (vp.gs[0] * vp.gs[1]);
+    o[0] = (float)gx * vp.vcs[0] + vp.vlo[0];
+    o[1] = (float)gy * vp.vcs[1] + vp.vlo[1];
+    o[2] = (float)gz * vp.vcs[2] + vp.vlo[2];
+    o[3] = 0.0f;
+}
+
+__global__ __launch_bounds__(kGroupThreads) void k_group(
+    const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+    const uint32_t* __restrict__ count, const float4* __restrict__ pts, float* __restrict__ out,
+    uint32_t* __restrict__ out_count, unsigned long long* status, unsigned long long* gstatus,
+    uint32_t* tile_ctr, uint32_t epoch, uint32_t* err, uint32_t* hist, int average,
+    VoxelParams vp) {
     __shared__ uint32_t s_wave[4];
-    __shared__ uint32_t s_tile, s_excl;
+    __shared__ uint32_t s_tile, s_excl, s_nbig;
+    __shared__ uint32_t s_start[kGroupThreads + 1];
+    __shared__ uint32_t s_big[kGroupThreads];
+    __shared__ float4 s_buf[4][kSumChunk];
+    __shared__ float4 s_pts[kStagePts];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t n = *count;
-    const uint32_t ntiles = (n + kGroupTile - 1) / kGroupTile;
+    const uint32_t ntiles = (n + kGroupThreads - 1) / kGroupThreads;
     if (blockIdx.x == 0)
         for (uint32_t i = threadIdx.x; i < 4 * 256; i += kGroupThreads) hist[i] = 0;
     if (blockIdx.x >= ntiles) {
         if (blockIdx.x == 0 && threadIdx.x == 0) *out_count = 0;  // n == 0
         return;
     }
-    if (threadIdx.x == 0) s_tile = take_ticket(tile_ctr, ntiles);
+    if (threadIdx.x == 0) {
+        s_tile = take_ticket(tile_ctr, ntiles);
+        s_nbig = 0;
+    }
     __syncthreads();
     const uint32_t tile = s_tile;
-    const uint32_t i0 = tile * kGroupTile + threadIdx.x * kGroupPerThread;
-    uint32_t flags = 0, cnt = 0;
+    const uint32_t i = tile * kGroupThreads + threadIdx.x;
+    const uint32_t tend = min(n, (tile + 1) * kGroupThreads);
+    const uint32_t key = i < n ? keys[i] : 0u;
+    const uint32_t prev = (i < n && i > 0) ? keys[i - 1] : ~key;
+    const bool start = i < n && (i == 0 || key != prev);
+    uint32_t total;
+    const uint32_t local = block_exclusive_scan(start ? 1u : 0u, total, s_wave);
+    if (start) s_start[local] = i;
+    __syncthreads();
+    // Overlapped: every lane issues the staging gather of the points from the tile's first group
+    // start on (kStagePts positions; extra positions are harmless), wave 0 resolves the group-id
+    // prefix (look-back) and wave 1 finds where the tile's last group ends.
+    // (a tile without a group start - inside a group that began earlier - still publishes its
+    // zero count for the look-back)
+    const uint32_t S0 = total ? s_start[0] : n;
+    const uint32_t staged = min(n - S0, (uint32_t)kStagePts);
+    float4 sp[kStagePts / kGroupThreads];
+    if (average) {
 #pragma unroll
-    for (int j = 0; j < kGroupPerThread; ++j) {
-        const uint32_t i = i0 + j;
-        if (i < n && (i == 0 || keys[i] != keys[i - 1])) {
-            flags |= 1u << j;
-            ++cnt;
+        for (int q = 0; q < kStagePts / kGroupThreads; ++q) {
+            const uint32_t j = threadIdx.x + kGroupThreads * q;
+            if (j < staged) sp[q] = pts[vals[S0 + j]];
         }
     }
-    uint32_t total;
-    const uint32_t excl_thread = block_exclusive_scan(cnt, total, s_wave);
-    if (threadIdx.x < 64) {
+    if (wid == 0) {
         const uint32_t ex = lookback2_wave(status, gstatus, tile, ntiles, total, epoch, err);
-        if (threadIdx.x == 0) {
+        if (lane == 0) {
             s_excl = ex;
             if (tile == ntiles - 1) *out_count = ex + total;
         }
+    } else if (wid == 1 && total) {
+        uint32_t e = n;
+        const uint32_t lastkey = keys[tend - 1];
+        for (uint32_t b = tend; b < n; b += 64) {
+            const uint32_t j = b + lane;
+            const unsigned long long ch = __ballot(j < n && keys[j] != lastkey);
+            if (ch) {
+                e = b + (uint32_t)(__ffsll((long long)ch) - 1);
+                break;
+            }
+        }
+        if (lane == 0) s_start[total] = e;
+    }
+    if (average) {
+#pragma unroll
+        for (int q = 0; q < kStagePts / kGroupThreads; ++q) {
+            const uint32_t j = threadIdx.x + kGroupThreads * q;
+            if (j < staged) s_pts[j] = sp[q];
+        }
     }
     __syncthreads();
-    uint32_t g = s_excl + excl_thread;
-#pragma unroll
-    for (int j = 0; j < kGroupPerThread; ++j)
-        if (flags & (1u << j)) gstart[g++] = i0 + j;
-}
-
-// Per-voxel output.  average: the sequential f32 sum in stable (index) order, x/y/z divided by
-// the count, w the un-divided sum (averageGridCells, inc/voxelize.h:9-48).  One wave per group:
-// the wave gathers chunks of 256 points into LDS (next chunk prefetched into registers while
-// the current one is summed); lanes 0..3 each run one component's dependent add chain.
-// !average: the voxel's lower corner (occupiedGridCells + GridMeta::worldCoord).
-__global__ __launch_bounds__(kGroupThreads) void k_group_sum(
-    const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
-    const uint32_t* __restrict__ count, const uint32_t* __restrict__ gstart,
-    const uint32_t* __restrict__ gcount, const float4* __restrict__ pts, float* __restrict__ out,
-    int average, VoxelParams vp) {
-    __shared__ float4 s_buf[4][kSumChunk];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint32_t n = *count;
-    const uint32_t G = *gcount;
-    const uint32_t nwaves = gridDim.x * 4;
-    for (uint32_t g = blockIdx.x * 4 + wid; g < G; g += nwaves) {
-        const uint32_t s = gstart[g];
-        const uint32_t e = (g + 1 < G) ? gstart[g + 1] : n;
+    if (total == 0) return;  // block-uniform
+    // one group per thread: staged groups summed here in index order, the rest queued for waves
+    if (threadIdx.x < total) {
+        const uint32_t g = s_excl + threadIdx.x;
+        const uint32_t s = s_start[threadIdx.x], e = s_start[threadIdx.x + 1];
+        float* o = out + 4 * (size_t)g;
         if (!average) {
-            if (lane < 3) {
-                const uint32_t key = keys[s];
-                const uint32_t steps[3] = {1u, vp.gs[0], vp.gs[0] * vp.gs[1]};
-                uint32_t kk = key, gc[3];
+            float c[4];
+            group_corner(keys[s], vp, c);
+            *reinterpret_cast<float4*>(o) = make_float4(c[0], c[1], c[2], c[3]);
+        } else if (e - S0 <= staged && e - s <= (uint32_t)kSmallGroup) {
+            float ax = 0.f, ay = 0.f, az = 0.f, aw = 0.f;
+            uint32_t k = s - S0;
+            for (; k + 4 <= e - S0; k += 4) {
+                float4 p[4];
 #pragma unroll
-                for (int ax = 0; ax < 3; ++ax) {
-                    gc[ax] = (kk / steps[ax]) % vp.gs[ax];
-                    kk -= gc[ax] * steps[ax];
+                for (int q = 0; q < 4; ++q) p[q] = s_pts[k + q];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    ax = ax + p[q].x;
+                    ay = ay + p[q].y;
+                    az = az + p[q].z;
+                    aw = aw + p[q].w;
                 }
-                out[4 * (size_t)g + lane] = (float)gc[lane] * vp.vcs[lane] + vp.vlo[lane];
-            } else if (lane == 3) {
-                out[4 * (size_t)g + 3] = 0.0f;
+            }
+            for (; k < e - S0; ++k) {
+                const float4 p = s_pts[k];
+                ax = ax + p.x;
+                ay = ay + p.y;
+                az = az + p.z;
+                aw = aw + p.w;
+            }
+            const float fc = (float)(e - s);
+            *reinterpret_cast<float4*>(o) = make_float4(ax / fc, ay / fc, az / fc, aw);
+        } else {
+            s_big[atomicAdd(&s_nbig, 1u)] = threadIdx.x;
+        }
+    }
+    __syncthreads();
+    const uint32_t nbig = s_nbig;
+    for (uint32_t b = wid; b < nbig; b += kGroupThreads / 64) {
+        const uint32_t li = s_big[b];
+        const uint32_t g = s_excl + li;
+        const uint32_t s = s_start[li], e = s_start[li + 1];
+        float acc = 0.0f;
+        if (e - S0 <= staged) {  // staged: lanes 0..3 run the component chains from LDS
+            if (lane < 4) {
+                const float* comp = reinterpret_cast<const float*>(s_pts) + lane;
+                uint32_t j = s - S0;
+                for (; j + 16 <= e - S0; j += 16) {
+                    float t[16];
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) t[q] = comp[4 * (j + q)];
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) acc = acc + t[q];
+                }
+                for (; j < e - S0; ++j) acc = acc + comp[4 * j];
+                const float fc = (float)(e - s);
+                out[4 * (size_t)g + lane] = lane < 3 ? acc / fc : acc;
             }
             continue;
         }
-        float acc = 0.0f;
         float4 r[kSumChunk / 64];
 #pragma unroll
         for (int q = 0; q < kSumChunk / 64; ++q) {
@@ -1302,7 +1396,7 @@ size_t voxelize_status_words(uint32_t nmax) {
     return (size_t)((nmax + kSortThreads * 4 - 1) / (kSortThreads * 4) + 1) * 256;
 }
 size_t voxelize_group_tiles(uint32_t nmax) {
-    return (size_t)((nmax + kGroupTile - 1) / kGroupTile + 1);
+    return (size_t)((nmax + kGroupThreads - 1) / kGroupThreads + 1);
 }
 
 template <int PT>
@@ -1311,12 +1405,12 @@ static void launch_sort_pass(uint32_t tiles, hipStream_t s, const uint32_t* kin,
                              uint32_t ep, uint32_t dbits) {
     // the first pass also carries the historic-grid update in extra blocks
     const bool g = p == 0 && a.grid8 != nullptr;
-    const uint64_t nvec = g ? (a.ncells + 15) / 16 : 0;
-    const uint32_t gb = g ? grid_blocks(nvec, 256 * 4) : 0;
+    const uint64_t nwords = g ? (a.ncells + 31) / 32 : 0;
+    const uint32_t gb = g ? grid_blocks(nwords, 256 * 2) : 0;
     hipLaunchKernelGGL(k_sort_pass<PT>, dim3(tiles + gb), dim3(kSortThreads), 0, s, kin, vin, kout,
                        vout, a.count, a.hist + 256 * p, a.status, a.sgstatus,
                        reinterpret_cast<uint32_t*>(a.ctrs + kCtrSort0 + p), ep, a.err, 8 * p, dbits,
-                       tiles, reinterpret_cast<uint4*>(a.grid8), nvec, a.lifetime);
+                       tiles, reinterpret_cast<uint4*>(a.grid8), a.marks, nwords, a.lifetime);
 }
 
 hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hook) {
@@ -1352,76 +1446,39 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
         kin = kbuf[p & 1];
         vin = vbuf[p & 1];
     }
-    const uint32_t group_tiles = (a.nmax + kGroupTile - 1) / kGroupTile;
-    const uint32_t gblocks = group_tiles ? group_tiles : 1;
+    const uint32_t group_tiles = (a.nmax + kGroupThreads - 1) / kGroupThreads;
     const uint32_t ep = ++(*a.epoch);
-    {
-    HookScope hs(hook, GDF_KERNEL_GROUP_SCAN);
-    hipLaunchKernelGGL(k_group_scan, dim3(gblocks), dim3(kGroupThreads), 0, s, kin, a.count,
-                       a.gstart, a.out_count, a.gstatus, a.ggstatus,
-                       reinterpret_cast<uint32_t*>(a.ctrs + kCtrGroup), ep, a.err, a.hist);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
-    HookScope hs(hook, GDF_KERNEL_GROUP_SUM);
-    uint32_t sblocks = (a.nmax + 255) / 256;
-    if (sblocks > 1024) sblocks = 1024;
-    if (sblocks == 0) sblocks = 1;
-    hipLaunchKernelGGL(k_group_sum, dim3(sblocks), dim3(kGroupThreads), 0, s, kin, vin, a.count,
-                       a.gstart, a.out_count, a.pts, reinterpret_cast<float*>(a.out), a.average,
-                       a.vp);
+    HookScope hs(hook, GDF_KERNEL_GROUP);
+    hipLaunchKernelGGL(k_group, dim3(group_tiles ? group_tiles : 1), dim3(kGroupThreads), 0, s, kin,
+                       vin, a.count, a.pts, reinterpret_cast<float*>(a.out), a.out_count,
+                       a.gstatus, a.ggstatus, reinterpret_cast<uint32_t*>(a.ctrs + kCtrGroup), ep,
+                       a.err, a.hist, a.average, a.vp);
     return hipGetLastError();
 }
 
-// ---- multi-GPU occupancy marks ------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_export_marks(const uint8_t* __restrict__ occ, int mode,
-                                                      uint64_t ncells, uint32_t* __restrict__ bits,
-                                                      uint64_t words) {
-    for (uint64_t wi = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; wi < words;
-         wi += (uint64_t)gridDim.x * blockDim.x) {
-        uint32_t b = 0;
-        for (int k = 0; k < 32; ++k) {
-            const uint64_t c = wi * 32 + k;
-            if (c < ncells) {
-                const uint8_t h = occ[c];
-                const bool m = mode == 1 ? (h & 0x80u) != 0 : h != 0;
-                b |= (m ? 1u : 0u) << k;
-            }
-        }
-        bits[wi] = b;
-    }
-}
-
-hipError_t launch_export_marks(const uint8_t* occ, int mode, uint64_t ncells, uint32_t* bits,
-                               hipStream_t s) {
-    const uint64_t words = (ncells + 31) / 32;
-    hipLaunchKernelGGL(k_export_marks, dim3(grid_blocks(words, 256)), dim3(256), 0, s, occ, mode,
-                       ncells, bits, words);
-    return hipGetLastError();
-}
-
-__global__ __launch_bounds__(256) void k_import_marks(uint8_t* __restrict__ occ, int mode,
-                                                      uint64_t ncells,
+// ---- multi-GPU occupancy marks -------------------------------------------------------------------
+// The engine's marks already are the exchange format (1 bit per cell): export is a copy, import
+// ORs the all-gathered masks of every rank into them.
+__global__ __launch_bounds__(256) void k_import_marks(uint32_t* __restrict__ marks,
                                                       const uint32_t* __restrict__ bits,
                                                       uint64_t words, uint32_t nranks) {
-    for (uint64_t wi = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; wi < words;
-         wi += (uint64_t)gridDim.x * blockDim.x) {
-        uint32_t b = 0;
-        for (uint32_t r = 0; r < nranks; ++r) b |= bits[(uint64_t)r * words + wi];
-        if (!b) continue;
-        for (int k = 0; k < 32; ++k) {
-            const uint64_t c = wi * 32 + k;
-            if (c < ncells && ((b >> k) & 1u)) {
-                if (mode == 1) occ[c] = (uint8_t)(occ[c] | 0x80u);
-                else occ[c] = 1;
-            }
-        }
+    for (uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; w < words;
+         w += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t v = marks[w];
+        for (uint32_t r = 0; r < nranks; ++r) v |= bits[(uint64_t)r * words + w];
+        marks[w] = v;
     }
 }
 
-hipError_t launch_import_marks(uint8_t* occ, int mode, uint64_t ncells, const uint32_t* bits,
-                               uint64_t words, uint32_t nranks, hipStream_t s) {
-    hipLaunchKernelGGL(k_import_marks, dim3(grid_blocks(words, 256)), dim3(256), 0, s, occ, mode,
-                       ncells, bits, words, nranks);
+hipError_t launch_export_marks(const uint32_t* marks, uint64_t words, uint32_t* bits,
+                               hipStream_t s) {
+    return hipMemcpyAsync(bits, marks, words * 4, hipMemcpyDeviceToDevice, s);
+}
+
+hipError_t launch_import_marks(uint32_t* marks, uint64_t words, const uint32_t* bits,
+                               uint32_t nranks, hipStream_t s) {
+    hipLaunchKernelGGL(k_import_marks, dim3(grid_blocks(words, 256)), dim3(256), 0, s, marks, bits,
+                       words, nranks);
     return hipGetLastError();
 }
 

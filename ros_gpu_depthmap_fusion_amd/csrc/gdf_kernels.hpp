@@ -31,20 +31,20 @@ hipError_t launch_ps_filter_insert(const float4* new_pts, uint32_t n, int do_fil
                                    uint32_t F, float4* ring, uint64_t cap, uint64_t first,
                                    hipStream_t s);
 
-// historic grid update: u8 grid with the mark in bit 7 (lifetime <= 127)
-hipError_t launch_grid_u8(uint8_t* grid, uint64_t ncells, uint32_t lifetime, hipStream_t s);
-// general u32 historic grid with a separate u8 mark array; writes the u8 output grid
-hipError_t launch_grid_u32(uint32_t* hist, uint8_t* marks, uint8_t* out8, uint64_t ncells,
+// historic grid update from the frame's mark bitmask (cleared on the way): u8 grid = history for
+// lifetime <= 255; the general u32 history with a separate u8 output grid beyond
+hipError_t launch_grid_u8(uint8_t* grid, uint32_t* marks, uint64_t ncells, uint32_t lifetime,
+                          hipStream_t s);
+hipError_t launch_grid_u32(uint32_t* hist, uint32_t* marks, uint8_t* out8, uint64_t ncells,
                            uint32_t lifetime, hipStream_t s);
-hipError_t launch_widen_grid(const uint8_t* grid8, uint32_t* hist, uint8_t* marks,
-                             uint64_t ncells, hipStream_t s);
+hipError_t launch_widen_grid(const uint8_t* grid8, uint32_t* hist, uint64_t ncells, hipStream_t s);
 
 // standalone voxel keys over the compacted points (count read on the device)
 hipError_t launch_coords(const float4* pts, const uint32_t* count, uint32_t nmax,
                          uint32_t* coords, const VoxelParams& v, hipStream_t s);
-// occupancy marks from voxel keys (mode 1: bit 7 of u8 grid, 2: u8 mark array)
+// occupancy marks (bitmask) from voxel keys
 hipError_t launch_scatter(const uint32_t* coords, const uint32_t* count, uint32_t nmax,
-                          uint8_t* occ, int mode, hipStream_t s);
+                          uint32_t* marks, hipStream_t s);
 
 // GPU voxelize: stable LSD radix sort of (key, index) + ordered per-voxel mean
 struct VoxelizeArgs {
@@ -63,13 +63,13 @@ struct VoxelizeArgs {
     unsigned long long* sgstatus;   // [sort tile groups * 256]
     unsigned long long* gstatus;    // [group tiles] epoch granules
     unsigned long long* ggstatus;   // [group tiles / 64 + 1]
-    uint32_t* gstart;               // [nmax] first sorted position of each group
     unsigned long long* ctrs;       // [kCtrSlots] self-resetting tile tickets (low 32 bits)
     uint32_t* epoch;                // host epoch counter (advanced per look-back launch)
     int sort_pt;                    // keys per thread of a sort tile (4, 8 or 16)
-    // optional fused historic-grid update (u8 grid, lifetime <= 127), run by extra blocks of the
+    // optional fused historic-grid update (u8 grid, lifetime <= 255), run by extra blocks of the
     // first sort pass: it only needs the occupancy marks, which the compaction already wrote
     uint8_t* grid8;
+    uint32_t* marks;
     uint64_t ncells;
     uint32_t lifetime;
     uint32_t* err;
@@ -81,10 +81,9 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
 size_t voxelize_status_words(uint32_t nmax);
 size_t voxelize_group_tiles(uint32_t nmax);
 
-// multi-GPU occupancy marks
-hipError_t launch_export_marks(const uint8_t* occ, int mode, uint64_t ncells, uint32_t* bits,
-                               hipStream_t s);
-hipError_t launch_import_marks(uint8_t* occ, int mode, uint64_t ncells, const uint32_t* bits,
-                               uint64_t words, uint32_t nranks, hipStream_t s);
+// multi-GPU occupancy marks: export = copy of the mark bitmask, import = OR of nranks masks
+hipError_t launch_export_marks(const uint32_t* marks, uint64_t words, uint32_t* bits, hipStream_t s);
+hipError_t launch_import_marks(uint32_t* marks, uint64_t words, const uint32_t* bits,
+                               uint32_t nranks, hipStream_t s);
 
 }  // namespace gdf

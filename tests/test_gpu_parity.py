@@ -168,11 +168,13 @@ def test_empty_and_all_zero_frames(Engine):
     assert gpu.downloadVoxelOccupancyGrid().max() == p.occupancy_lifetime - 1
 
 
-def test_lifetime_above_127_uses_u32_history(Engine):
+def test_lifetime_u8_range_then_u32_history(Engine):
+    """Lifetimes up to 255 keep the u8 grid as the history; 256+ switches to the u32 history
+    (output byte = hist & 0xFF, uints_to_chars.glsl) and stays there."""
     p = ComponentParams()
     cam = synth.make_camera(0, 160, 120)
     gpu, orc = Engine(), OracleFusion()
-    for f, life in enumerate([10, 300, 300, 5, 1000]):
+    for f, life in enumerate([10, 200, 255, 255, 256, 300, 5, 1000]):
         p.occupancy_lifetime = life
         args = [cam_args(cam, synth.depth_frame(cam, 0, f))]
         run_fused(gpu, args, p)
@@ -314,3 +316,44 @@ def test_errors_fail_loudly(Engine):
     p.voxel_min, p.voxel_max = (1, 1, 1), (0, 0, 0)
     with pytest.raises(GDFError):
         gpu.processFrame(p)
+
+
+def test_multi_gpu_mark_export_import(Engine):
+    """The multi-GPU exchange kernels on one device: two engines (one camera each) defer their
+    grid, export marks (k_export_marks bit layout = multi.pack_marks), import the concatenated
+    masks of both (k_import_marks ORs them) and update; both grids must equal the oracle
+    history of the union of the two cameras' marks, frame after frame."""
+    from ros_gpu_depthmap_fusion_amd import hiprt, multi
+    p = ComponentParams()
+    p.occupancy_lifetime = 4
+    cams = [synth.make_camera(k, 160, 120) for k in range(2)]
+    gpus = [Engine() for _ in cams]
+    orcs = [OracleFusion(threads=4) for _ in cams]
+    hist = None
+    for f in range(3):
+        words = []
+        union = None
+        for k, (c, g, o) in enumerate(zip(cams, gpus, orcs)):
+            args = [cam_args(c, synth.depth_frame(c, k, f))]
+            run_fused(g, args, p, defer_occupancy_grid=True)
+            run_fused(o, args, p)
+            (_, _, _), ncells = g.grid_size()
+            nw = multi.words_for(ncells)
+            buf = hiprt.DeviceArray(nw * 4)
+            g.export_marks(buf.ptr, nw)
+            g.synchronize()
+            w = buf.to_numpy(np.uint32, nw)
+            m = np.zeros(ncells, bool)
+            m[o.downloadVoxelCoords()] = True
+            np.testing.assert_array_equal(w, multi.pack_marks(m), err_msg=f"export cam {k}")
+            words.append(w)
+            union = m if union is None else union | m
+        both = hiprt.DeviceArray.from_numpy(np.concatenate(words))
+        hist = np.zeros(union.size, np.uint32) if hist is None else hist
+        hist = multi.historic_update(hist, union, p.occupancy_lifetime)
+        for k, g in enumerate(gpus):
+            g.import_marks(both.ptr, len(words[0]), 2)
+            g.voxelOccupancyGrid(p.occupancy_lifetime)
+            np.testing.assert_array_equal(g.downloadVoxelOccupancyGrid().reshape(-1),
+                                          (hist & 0xFF).astype(np.uint8),
+                                          err_msg=f"frame {f} rank {k}")

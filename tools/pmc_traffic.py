@@ -15,8 +15,8 @@ import collections
 import csv
 import json
 
-SLOT = {"k_mask": "mask", "k_emit": "emit", "k_sort_pass": "sort", "k_group_scan": "group_scan",
-        "k_group_sum": "group_sum", "k_scan_counts": "scan", "k_grid_u8": "grid",
+SLOT = {"k_mask": "mask", "k_emit": "emit", "k_sort_pass": "sort", "k_group": "group",
+        "k_scan_counts": "scan", "k_grid_u8": "grid",
         "k_grid_u32": "grid"}
 
 
