@@ -36,6 +36,9 @@ def parse():
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--ring", type=int, default=8, help="distinct device-resident frames")
+    ap.add_argument("--pipeline", type=int, default=2,
+                    help="frames in flight on one GPU (engine slots, gdf_set_pipeline_depth); "
+                         "N > 1 runs on torch's stream with depth 1")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-kernel-timing", action="store_true",
@@ -89,9 +92,13 @@ def main():
         nvox.append(r.num_voxelized)
     (gx, gy, gz), ncells = eng.grid_size()
 
+    depth = 1
     if dist is not None:
         from ros_gpu_depthmap_fusion_amd.multi import DeviceMarkExchange
         marks = DeviceMarkExchange(eng, ncells, world)
+    else:
+        depth = max(1, min(4, args.pipeline))
+        eng.set_pipeline_depth(depth)
 
     pc_plain = params.to_c(None, None, False, False)
     pc_defer = params.to_c(None, None, False, True)
@@ -132,6 +139,8 @@ def main():
     ktimes = None
     if not args.no_kernel_timing:
         kt_steps = min(args.steps, 200)
+        if dist is None:
+            eng.set_pipeline_depth(1)  # one frame in flight: launch durations without overlap
         eng.set_profiling(True)
         for i in range(kt_steps):
             step(args.warmup + i)
@@ -237,6 +246,7 @@ def main():
                                    "lifetime 10)" % (W, H, gx, gy, gz),
                        "cameras_per_gpu": 1, "points_per_frame_after_crop": round(n_avg),
                        "voxels_per_frame": round(g_avg), "grid_cells": ncells,
+                       "frames_in_flight": depth,
                        "parallelism": "camera-per-GPU x%d, occupancy-mark all-gather" % world
                        if world > 1 else "single GPU"},
             "roofline": roofline,

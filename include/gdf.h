@@ -116,6 +116,13 @@ int gdf_version(int* major, int* minor);
  * the engine's own stream. */
 int gdf_set_stream(gdf_engine* engine, void* hip_stream);
 int gdf_synchronize(gdf_engine* engine);
+/* Frame pipelining (1..4, default 1): gdf_clear starts a frame on the next of `depth` slots,
+ * each with its own stream and per-frame buffers, so a frame's compaction overlaps the previous
+ * frame's sort / grouping.  Shared state stays ordered: grid updates run in frame order, frames
+ * that touch the rollbuffer or rebuild camera tables wait for the previous frame.  Results of a
+ * frame are read (downloads, gdf_get_device_results) before the next gdf_clear.  Call between
+ * frames; not available with gdf_set_stream. */
+int gdf_set_pipeline_depth(gdf_engine* engine, int depth);
 /* voxel_group_size parameter (component.cpp:1149); kept for interface parity, it only tuned
  * the reference's CPU radix sort and does not change results. */
 int gdf_set_voxel_group_size(gdf_engine* engine, int group_size);

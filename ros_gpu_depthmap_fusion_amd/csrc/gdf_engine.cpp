@@ -157,10 +157,45 @@ enum MiscSlot { kCount = 0, kTileCtr = 1, kErr = 2, kVoxCount = 3, kSortCtrs = 4
 
 }  // namespace
 
+
+constexpr int kMaxPipe = 4;
+
+// Everything one frame writes.  Frames rotate over npipe slots (gdf_clear starts a frame), so a
+// new frame's compaction runs while the previous frame's sort / grouping still execute; shared
+// state (rollbuffer ring, camera tables, the occupancy grid) is ordered by events.
+struct Slot {
+    hipStream_t own = nullptr;
+    hipEvent_t ev_done = nullptr;   // recorded when the next frame starts on another slot
+    hipEvent_t ev_grid = nullptr;   // recorded after this frame's grid update
+    bool done_recorded = false, grid_recorded = false;
+    DevBuf d_depth;                 // host depth maps uploaded for this frame
+    DevBuf d_camdesc;
+    DevBuf d_ctrs;                  // tile tickets of the look-back launches
+    DevBuf d_khist;                 // digit histogram of the voxel keys [4*256]
+    bool khist_pending = false;     // accumulated by the fused compaction, not yet consumed
+    DevBuf d_pts, d_coords, d_stage, d_vbits, d_tcounts, d_toffsets;
+    DevBuf d_misc;
+    uint32_t* h_misc = nullptr;     // pinned
+    bool compacted = false, coords_valid = false, marks_set = false;
+    uint32_t dbg_count = 0;
+    DevBuf d_ka, d_kb, d_va, d_vb, d_sstatus, d_sgstatus, d_gstatus, d_ggstatus, d_vox;
+    bool vox_valid = false;
+    DevBuf d_markbits;              // this frame's occupancy marks (1 bit per cell)
+    uint32_t marks_gen = ~0u;
+    uint32_t n_total = 0;
+};
+
 struct gdf_engine {
     int device = 0;
-    hipStream_t own = nullptr;
-    hipStream_t stream = nullptr;
+    // frame slots: per-frame buffers on their own streams (pipeline depth 1..kMaxPipe)
+    Slot slots[kMaxPipe];
+    int cur = 0;
+    int npipe = 1;
+    hipStream_t user_stream = nullptr;  // gdf_set_stream: single slot on the caller's stream
+    bool serialized = false;            // this frame already waits for the previous one
+    Slot& sl() { return slots[cur]; }
+    const Slot& sl() const { return slots[cur]; }
+    Slot& prev_slot() { return slots[(cur + npipe - 1) % npipe]; }
     std::mutex ps_mutex;
     int voxel_group_size = 1024;
 
@@ -173,7 +208,6 @@ struct gdf_engine {
     std::vector<Cam> cams;
     uint32_t depth_total = 0;
     std::vector<CamDesc> halo;      // halo cameras (multi-GPU), negative offsets
-    DevBuf d_depth;
     std::vector<CamTable> tables = std::vector<CamTable>(kMaxCams);
     std::vector<CamDesc> h_cams;
     uint32_t mask_blocks = 0;       // compaction segments over the emitting cameras
@@ -195,7 +229,6 @@ struct gdf_engine {
     gdf_rollbuffer_state rb{};
 
     // selected rollbuffer points
-    uint32_t n_total = 0;
     bool prepared = false, sel_inserted = false;
     DevBuf d_seg_start, d_seg_tf, d_tfw, d_tfc;
     uint32_t nseg = 0;
@@ -208,18 +241,10 @@ struct gdf_engine {
     float lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
 
     // tile tickets + epochs of the look-back launches (no per-launch memsets)
-    DevBuf d_ctrs;
     uint32_t epoch = 0;
     int sort_pt = 4;
-    DevBuf d_khist;                 // digit histogram of the voxel keys [4*256]
-    bool khist_pending = false;     // accumulated by a fused k_frame, not yet consumed
 
     // compaction outputs
-    DevBuf d_pts, d_coords, d_stage, d_vbits, d_tcounts, d_toffsets, d_camdesc;
-    DevBuf d_misc;
-    uint32_t* h_misc = nullptr;  // pinned
-    bool compacted = false, coords_valid = false, marks_set = false;
-    uint32_t dbg_count = 0;
 
     // voxel grid
     bool grid_set = false;
@@ -228,14 +253,13 @@ struct gdf_engine {
     uint64_t ncells = 0;
     uint32_t key_bits = 0;
     VoxelParams vp{};
-    DevBuf d_grid8, d_hist32, d_markbits, d_out8;
+    DevBuf d_grid8, d_hist32, d_out8;
+    uint32_t grid_gen = 0;          // bumped when the grid is (re)allocated: slots re-zero marks
     int grid_mode = 0;  // 0: u8 grid = history (lifetime <= 255); 1: u32 history + u8 output
     bool grid_alloc = false;
     bool invoked_once = false;
 
     // voxelize
-    DevBuf d_ka, d_kb, d_va, d_vb, d_sstatus, d_sgstatus, d_gstatus, d_ggstatus, d_vox;
-    bool vox_valid = false;
 
     bool debug = false;
 
@@ -247,7 +271,7 @@ struct gdf_engine {
     double prof_ms[GDF_KERNEL_SLOTS] = {};
     uint64_t prof_n[GDF_KERNEL_SLOTS] = {};
 
-    hipStream_t s() const { return stream; }
+    hipStream_t s() const { return user_stream ? user_stream : sl().own; }
 
     hipEvent_t take_event() {
         if (!ev_pool.empty()) {
@@ -261,7 +285,7 @@ struct gdf_engine {
     }
     // brackets one launch (or launch group) of `slot` with an event pair when profiling
     template <class F>
-    void timed(int slot, F&& launch) { timed_on(slot, stream, launch); }
+    void timed(int slot, F&& launch) { timed_on(slot, s(), launch); }
     template <class F>
     void timed_on(int slot, hipStream_t st, F&& launch) {
         if (!profiling) {
@@ -282,12 +306,12 @@ struct gdf_engine {
         explicit Hook(gdf_engine* e_) : e(e_) {}
         void begin(int) override {
             hipEvent_t a = e->take_event();
-            HIPCHK(hipEventRecord(a, e->stream));
+            HIPCHK(hipEventRecord(a, e->s()));
             open.push_back(a);
         }
         void end(int slot) override {
             hipEvent_t b = e->take_event();
-            HIPCHK(hipEventRecord(b, e->stream));
+            HIPCHK(hipEventRecord(b, e->s()));
             e->ev_pending.push_back(EvPair{open.back(), b, slot});
             open.pop_back();
         }
@@ -308,25 +332,71 @@ struct gdf_engine {
     }
 
     void sync() {
-        HIPCHK(hipStreamSynchronize(stream));
-        if (h_misc && h_misc[kErr]) {
-            const uint32_t e = h_misc[kErr];
-            h_misc[kErr] = 0;
-            HIPCHK(hipMemsetAsync(d_misc.as<uint32_t>() + kErr, 0, 4, stream));
-            fail(GDF_ERR_DEVICE, "device look-back spin limit expired (code " + std::to_string(e) + ")");
+        Slot& c = sl();
+        HIPCHK(hipStreamSynchronize(s()));
+        if (c.h_misc && c.h_misc[kErr]) {
+            const uint32_t code = c.h_misc[kErr];
+            c.h_misc[kErr] = 0;
+            HIPCHK(hipMemsetAsync(c.d_misc.as<uint32_t>() + kErr, 0, 4, s()));
+            fail(GDF_ERR_DEVICE, "device look-back spin limit expired (code " + std::to_string(code) + ")");
         }
     }
     // read the small device counters into pinned memory (after the producing kernels)
     void read_misc() {
-        HIPCHK(hipMemcpyAsync(h_misc, d_misc.p, kMiscWords * 4, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipMemcpyAsync(sl().h_misc, sl().d_misc.p, kMiscWords * 4, hipMemcpyDeviceToHost, s()));
         sync();
+    }
+    // once per frame, before touching state shared with the previous frame (rollbuffer ring,
+    // camera tables, grid allocation): the current slot's stream waits for the previous frame
+    void serialize() {
+        if (npipe <= 1 || serialized) return;
+        Slot& p = prev_slot();
+        if (p.done_recorded) HIPCHK(hipStreamWaitEvent(s(), p.ev_done, 0));
+        serialized = true;
+    }
+    // the previous frame's grid update precedes this frame's (the history is a chain)
+    void order_grid() {
+        if (npipe <= 1) return;
+        Slot& p = prev_slot();
+        if (p.grid_recorded) HIPCHK(hipStreamWaitEvent(s(), p.ev_grid, 0));
+    }
+    void grid_updated() {
+        if (npipe <= 1) return;
+        HIPCHK(hipEventRecord(sl().ev_grid, s()));
+        sl().grid_recorded = true;
     }
 };
 
 namespace {
 
+void create_slot(Slot& sl) {
+    if (sl.own) return;
+    HIPCHK(hipStreamCreateWithFlags(&sl.own, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&sl.ev_done, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&sl.ev_grid, hipEventDisableTiming));
+    HIPCHK(hipHostMalloc((void**)&sl.h_misc, kMiscWords * 4, hipHostMallocDefault));
+    std::memset(sl.h_misc, 0, kMiscWords * 4);
+}
+
+void sync_all(gdf_engine* e) {
+    if (e->user_stream) HIPCHK(hipStreamSynchronize(e->user_stream));
+    for (Slot& sl : e->slots)
+        if (sl.own) HIPCHK(hipStreamSynchronize(sl.own));
+}
+
+// frame boundary (gdf_clear): the next frame goes to the next slot
+void next_slot(gdf_engine* e) {
+    if (e->npipe <= 1) return;
+    Slot& c = e->sl();
+    HIPCHK(hipEventRecord(c.ev_done, e->s()));
+    c.done_recorded = true;
+    e->cur = (e->cur + 1) % e->npipe;
+    e->serialized = false;
+}
+
 // ---- frame inputs ---------------------------------------------------------------------------------
 void engine_clear(gdf_engine* e) {  // fusion.cpp:725-732
+    next_slot(e);
     e->rb.selection_point_count = 0;
     e->rb.selection_sequence_count = 0;
     e->depth_total = 0;
@@ -385,6 +455,7 @@ void upload_point_sequences(gdf_engine* e) {  // fusion.cpp:819-857
     e->n_new = e->upload->total;
     e->new_hdrs = e->upload->seqs;
     if (e->n_new) {
+        e->serialize();  // d_new / the ring are shared with the previous frame
         e->d_new.ensure((size_t)e->n_new * 16);
         HIPCHK(hipMemcpyWithStream(e->d_new.p, e->upload->pts.data(), (size_t)e->n_new * 16,
                                    hipMemcpyHostToDevice, e->s()));
@@ -416,6 +487,7 @@ void ensure_ring(gdf_engine* e, uint64_t need) {
 }
 
 void insert_new_point_sequences(gdf_engine* e) {  // fusion.cpp:979-1087
+    if (e->n_new) e->serialize();  // ring writes; without new points only host headers change
     const uint32_t R = e->rb.num_points, S = e->rb.num_seqs;
     if (e->hdrB.size() < S) fail(GDF_ERR_STATE, "insert: rollbuffer headers out of sync");
     if ((uint64_t)R + e->n_new >= (1ull << 31)) fail(GDF_ERR_CAPACITY, "rollbuffer exceeds 2^31 points");
@@ -437,6 +509,8 @@ void insert_new_point_sequences(gdf_engine* e) {  // fusion.cpp:979-1087
 }
 
 void roll_rollbuffer(gdf_engine* e, uint32_t min_sec, uint32_t min_nsec) {  // fusion.cpp:1098-1217
+    // host-side only (headers and the ring head); ring slots it frees are rewritten by a later
+    // insert, which serializes on the previous frame
     uint32_t d_seqs = 0, d_pts = 0;
     const uint32_t nseq = (uint32_t)e->hdrA.size();
     for (uint32_t i = 0; i < nseq; ++i) {
@@ -487,9 +561,9 @@ void select_timespan(gdf_engine* e, uint32_t mins, uint32_t minn, uint32_t maxs,
 void prepare_buffers(gdf_engine* e) {  // fusion.cpp:1497-1508
     const uint64_t n = (uint64_t)e->depth_total + e->rb.selection_point_count;
     if (n >= (1ull << 31)) fail(GDF_ERR_CAPACITY, "more than 2^31 points in one frame");
-    e->n_total = (uint32_t)n;
-    e->d_pts.ensure((size_t)(n ? n : 1) * 16);
-    e->d_coords.ensure((size_t)(n ? n : 1) * 4);
+    e->sl().n_total = (uint32_t)n;
+    e->sl().d_pts.ensure((size_t)(n ? n : 1) * 16);
+    e->sl().d_coords.ensure((size_t)(n ? n : 1) * 4);
     e->prepared = true;
 }
 
@@ -498,9 +572,15 @@ void insert_selected(gdf_engine* e, const float* Twm, const float* Tcm) {  // fu
     if (!e->prepared) fail(GDF_ERR_STATE, "insertSelectedPointSequence before preparePointAndMaskBuffers");
     const uint32_t ps = e->rb.selection_point_start, cnt = e->rb.selection_point_count;
     const uint32_t ss = e->rb.selection_sequence_start, sc = e->rb.selection_sequence_count;
-    if ((uint64_t)e->depth_total + cnt > e->n_total) fail(GDF_ERR_STATE, "selection exceeds prepared buffers");
+    if ((uint64_t)e->depth_total + cnt > e->sl().n_total) fail(GDF_ERR_STATE, "selection exceeds prepared buffers");
     if (cnt && (uint64_t)ps + cnt > e->rb.num_points) fail(GDF_ERR_STATE, "selection exceeds rollbuffer points");
     if (sc && (uint64_t)ss + sc > e->hdrB.size()) fail(GDF_ERR_STATE, "selection exceeds rollbuffer sequences");
+    if (cnt == 0) {  // nothing selected: the frame kernels read no selection table
+        e->nseg = 0;
+        e->sel_inserted = true;
+        return;
+    }
+    e->serialize();  // the selection tables are shared with the previous frame
     // transforms of the selected sequences (kernel 19 of SURVEY §2b, computed host-side)
     std::vector<float> tfw((size_t)std::max<uint32_t>(sc, 1) * 16), tfc(tfw.size());
     for (uint32_t j = 0; j < sc; ++j) {
@@ -547,6 +627,7 @@ void ensure_table(gdf_engine* e, size_t slot, const Cam& c) {
     if (t.valid && t.W == c.W && t.H == c.H && t.fx == c.fx && t.fy == c.fy && t.cx == c.cx &&
         t.cy == c.cy)
         return;
+    e->serialize();  // the previous frame may still read the old table
     t.xn.ensure((size_t)c.W * 4);
     t.yn.ensure((size_t)c.H * 4);
     HIPCHK(launch_tables(c.W, c.H, c.fx, c.fy, c.cx, c.cy, t.xn.as<float>(), t.yn.as<float>(), e->s()));
@@ -557,7 +638,7 @@ void ensure_table(gdf_engine* e, size_t slot, const Cam& c) {
 void upload_depthmaps(gdf_engine* e) {  // fusion.cpp:1583-1593
     uint64_t host_px = 0;
     for (const Cam& c : e->cams) if (!c.dev) host_px += c.n;
-    if (host_px) e->d_depth.ensure(host_px * 2);
+    if (host_px) e->sl().d_depth.ensure(host_px * 2);
     if (e->cams.size() + e->halo.size() > (size_t)kMaxCams) fail(GDF_ERR_ARG, "too many cameras (incl. halo)");
     e->h_cams.clear();
     e->mask_blocks = 0;
@@ -570,7 +651,7 @@ void upload_depthmaps(gdf_engine* e) {  // fusion.cpp:1583-1593
         if (c.dev) {
             d.depth = c.dev;
         } else {
-            uint16_t* dst = e->d_depth.as<uint16_t>() + hoff;
+            uint16_t* dst = e->sl().d_depth.as<uint16_t>() + hoff;
             HIPCHK(hipMemcpyWithStream(dst, c.host, (size_t)c.n * 2, hipMemcpyHostToDevice, e->s()));
             d.depth = dst;
             hoff += c.n;
@@ -600,6 +681,16 @@ void upload_depthmaps(gdf_engine* e) {  // fusion.cpp:1583-1593
     e->depth_uploaded = true;
 }
 
+// the slot's mark bitmask exists and is zero for the current grid
+void ensure_marks(gdf_engine* e) {
+    Slot& sl = e->sl();
+    if (sl.marks_gen == e->grid_gen) return;
+    const size_t bytes = (size_t)((e->ncells + 31) / 32) * 4;
+    sl.d_markbits.ensure(bytes);
+    HIPCHK(hipMemsetAsync(sl.d_markbits.p, 0, bytes, e->s()));
+    sl.marks_gen = e->grid_gen;
+}
+
 void set_grid(gdf_engine* e, const float* lo, const float* hi, const float* cs) {
     // shader grid size (fusion.cpp:1693-1698) and VoxelGridMeta (grid_meta.h:140-158) must agree
     uint32_t g[3];
@@ -626,24 +717,27 @@ void set_grid(gdf_engine* e, const float* lo, const float* hi, const float* cs) 
     e->ncells = cells;
     e->grid_set = true;
     if (changed) {  // historic grid cleared on first use / resize (fusion.cpp:1759-1773)
+        e->serialize();
+        e->order_grid();
         const size_t padded = (size_t)((cells + 31) / 32) * 32;
         e->d_grid8.ensure(padded);
         HIPCHK(hipMemsetAsync(e->d_grid8.p, 0, padded, e->s()));
-        e->d_markbits.ensure(padded / 8);
-        HIPCHK(hipMemsetAsync(e->d_markbits.p, 0, padded / 8, e->s()));
         e->grid_mode = 0;
         e->grid_alloc = true;
-        e->marks_set = false;
+        e->grid_gen++;
+        e->sl().marks_set = false;
     }
+    ensure_marks(e);
 }
 
 // the frame's occupancy marks: 1 bit per cell, consumed (and cleared) by the grid update
-uint32_t* marks_ptr(const gdf_engine* e) { return e->d_markbits.as<uint32_t>(); }
+uint32_t* marks_ptr(const gdf_engine* e) { return e->sl().d_markbits.as<uint32_t>(); }
 uint64_t mark_words(const gdf_engine* e) { return (e->ncells + 31) / 32; }
 
 // switch to the general u32 history once a lifetime no longer fits the u8 grid
 void widen_if_needed(gdf_engine* e, uint32_t lifetime, hipStream_t st) {
     if (e->grid_mode != 0 || lifetime <= 255) return;
+    e->order_grid();
     e->d_hist32.ensure((size_t)e->ncells * 4);
     e->d_out8.ensure((size_t)((e->ncells + 31) / 32) * 32);
     HIPCHK(launch_widen_grid(e->d_grid8.as<uint8_t>(), e->d_hist32.as<uint32_t>(), e->ncells, st));
@@ -651,12 +745,12 @@ void widen_if_needed(gdf_engine* e, uint32_t lifetime, hipStream_t st) {
 }
 
 void ensure_misc(gdf_engine* e) {
-    if (!e->d_misc.p) {
-        e->d_misc.ensure(kMiscWords * 4);
-        HIPCHK(hipMemsetAsync(e->d_misc.p, 0, kMiscWords * 4, e->s()));
+    if (!e->sl().d_misc.p) {
+        e->sl().d_misc.ensure(kMiscWords * 4);
+        HIPCHK(hipMemsetAsync(e->sl().d_misc.p, 0, kMiscWords * 4, e->s()));
     }
-    if (!e->d_ctrs.p) e->d_ctrs.ensure_zero(kCtrSlots * 8, e->s());
-    if (!e->d_khist.p) e->d_khist.ensure_zero(4 * 256 * 4, e->s());
+    if (!e->sl().d_ctrs.p) e->sl().d_ctrs.ensure_zero(kCtrSlots * 8, e->s());
+    if (!e->sl().d_khist.p) e->sl().d_khist.ensure_zero(4 * 256 * 4, e->s());
 }
 
 // The fused compaction launch: convert + flying + crop + selected-point transform + ordered
@@ -670,10 +764,10 @@ void run_frame(gdf_engine* e, bool fused_voxel) {
     if (a.ncams <= kArgCams) {
         for (size_t k = 0; k < e->h_cams.size(); ++k) a.cams[k] = e->h_cams[k];
     } else {  // pageable source: the copy is staged before hipMemcpyAsync returns
-        e->d_camdesc.ensure(e->h_cams.size() * sizeof(CamDesc));
-        HIPCHK(hipMemcpyAsync(e->d_camdesc.p, e->h_cams.data(), e->h_cams.size() * sizeof(CamDesc),
+        e->sl().d_camdesc.ensure(e->h_cams.size() * sizeof(CamDesc));
+        HIPCHK(hipMemcpyAsync(e->sl().d_camdesc.p, e->h_cams.data(), e->h_cams.size() * sizeof(CamDesc),
                               hipMemcpyHostToDevice, e->s()));
-        a.cams_dev = e->d_camdesc.as<const CamDesc>();
+        a.cams_dev = e->sl().d_camdesc.as<const CamDesc>();
     }
     a.depth_total = e->depth_total;
     const uint32_t sel = e->sel_inserted ? e->rb.selection_point_count : 0u;
@@ -704,20 +798,20 @@ void run_frame(gdf_engine* e, bool fused_voxel) {
         std::memcpy(a.vcs, e->vp.vcs, 12);
         std::memcpy(a.gmax, e->vp.gmax, 12);
         std::memcpy(a.gs, e->vp.gs, 12);
-        if (e->khist_pending) HIPCHK(hipMemsetAsync(e->d_khist.p, 0, 4 * 256 * 4, e->s()));
-        a.key_hist = e->d_khist.as<uint32_t>();
+        if (e->sl().khist_pending) HIPCHK(hipMemsetAsync(e->sl().d_khist.p, 0, 4 * 256 * 4, e->s()));
+        a.key_hist = e->sl().d_khist.as<uint32_t>();
         a.npasses = e->key_bits == 0 ? 1u : (e->key_bits + 7) / 8;
     }
-    a.out_pts = e->d_pts.as<float4>();
-    a.out_coords = e->d_coords.as<uint32_t>();
-    a.out_count = e->d_misc.as<uint32_t>() + kCount;
+    a.out_pts = e->sl().d_pts.as<float4>();
+    a.out_coords = e->sl().d_coords.as<uint32_t>();
+    a.out_count = e->sl().d_misc.as<uint32_t>() + kCount;
     const uint32_t segs = std::max<uint32_t>(a.total_segs, 1);
-    e->d_vbits.ensure((size_t)segs * 16 * 8);
-    e->d_tcounts.ensure((size_t)segs * 4);
-    e->d_toffsets.ensure((size_t)segs * 4);
-    a.vbits = e->d_vbits.as<unsigned long long>();
-    a.seg_counts = e->d_tcounts.as<uint32_t>();
-    a.seg_offsets = e->d_toffsets.as<uint32_t>();
+    e->sl().d_vbits.ensure((size_t)segs * 16 * 8);
+    e->sl().d_tcounts.ensure((size_t)segs * 4);
+    e->sl().d_toffsets.ensure((size_t)segs * 4);
+    a.vbits = e->sl().d_vbits.as<unsigned long long>();
+    a.seg_counts = e->sl().d_tcounts.as<uint32_t>();
+    a.seg_offsets = e->sl().d_toffsets.as<uint32_t>();
     a.fused_prefix = a.total_segs <= kFusedPrefixSegs ? 1 : 0;
     // k_mask's LDS band: 2h+1 rows of 16-B chunks covering segw + 2h columns (+1 chunk of
     // alignment), then the columns' ray factors
@@ -728,90 +822,94 @@ void run_frame(gdf_engine* e, bool fused_voxel) {
         a.band_lds = (2 * h + 1) * a.band_rowb + (a.seg_threads * 2) * 4;
     }
     if (e->debug) {
-        e->d_stage.ensure((size_t)std::max<uint32_t>(e->n_total, 1));
-        a.dbg = e->d_stage.as<uint8_t>();
+        e->sl().d_stage.ensure((size_t)std::max<uint32_t>(e->sl().n_total, 1));
+        a.dbg = e->sl().d_stage.as<uint8_t>();
     }
-    e->dbg_count = e->n_total;
-    a.err = e->d_misc.as<uint32_t>() + kErr;
+    e->sl().dbg_count = e->sl().n_total;
+    a.err = e->sl().d_misc.as<uint32_t>() + kErr;
     if (e->profiling) e->timed(GDF_KERNEL_EVENT_FLOOR, [] {});  // calibrates the event overhead
     e->timed(GDF_KERNEL_FRAME, [&] { HIPCHK(launch_frame(a, e->s(), e->hook_ptr())); });
-    e->khist_pending = fused_voxel;
-    e->compacted = true;
-    e->coords_valid = fused_voxel;
-    e->marks_set = fused_voxel;
-    e->vox_valid = false;
+    e->sl().khist_pending = fused_voxel;
+    e->sl().compacted = true;
+    e->sl().coords_valid = fused_voxel;
+    e->sl().marks_set = fused_voxel;
+    e->sl().vox_valid = false;
 }
 
 void compute_voxel_coords(gdf_engine* e, const float* lo, const float* hi, const float* cs) {
-    if (!e->compacted) fail(GDF_ERR_STATE, "computeVoxelCoords before applyPointMask");
+    if (!e->sl().compacted) fail(GDF_ERR_STATE, "computeVoxelCoords before applyPointMask");
     set_grid(e, lo, hi, cs);
-    HIPCHK(launch_coords(e->d_pts.as<float4>(), e->d_misc.as<uint32_t>() + kCount,
-                         std::max<uint32_t>(e->n_total, 1), e->d_coords.as<uint32_t>(), e->vp, e->s()));
-    e->coords_valid = true;
-    e->marks_set = false;
+    HIPCHK(launch_coords(e->sl().d_pts.as<float4>(), e->sl().d_misc.as<uint32_t>() + kCount,
+                         std::max<uint32_t>(e->sl().n_total, 1), e->sl().d_coords.as<uint32_t>(), e->vp, e->s()));
+    e->sl().coords_valid = true;
+    e->sl().marks_set = false;
 }
 
 void voxelize(gdf_engine* e, int average, int fused_grid_lifetime = -1) {  // fusion.cpp:1743-1756
-    if (!e->grid_set || !e->coords_valid) fail(GDF_ERR_STATE, "voxelize before computeVoxelCoords");
-    const uint32_t nmax = std::max<uint32_t>(e->n_total, 1);
+    if (!e->grid_set || !e->sl().coords_valid) fail(GDF_ERR_STATE, "voxelize before computeVoxelCoords");
+    const uint32_t nmax = std::max<uint32_t>(e->sl().n_total, 1);
     if (nmax >= (1u << 31)) fail(GDF_ERR_CAPACITY, "voxelize supports < 2^31 points");
     ensure_misc(e);
-    e->d_ka.ensure((size_t)nmax * 4);
-    e->d_kb.ensure((size_t)nmax * 4);
-    e->d_va.ensure((size_t)nmax * 4);
-    e->d_vb.ensure((size_t)nmax * 4);
-    e->d_sstatus.ensure_zero(voxelize_status_words(nmax) * 8, e->s());
-    e->d_sgstatus.ensure_zero((voxelize_status_words(nmax) / 16 + 256) * 8, e->s());
-    e->d_gstatus.ensure_zero(voxelize_group_tiles(nmax) * 8, e->s());
-    e->d_ggstatus.ensure_zero((voxelize_group_tiles(nmax) / 64 + 2) * 8, e->s());
-    e->d_vox.ensure((size_t)nmax * 16);
+    e->sl().d_ka.ensure((size_t)nmax * 4);
+    e->sl().d_kb.ensure((size_t)nmax * 4);
+    e->sl().d_va.ensure((size_t)nmax * 4);
+    e->sl().d_vb.ensure((size_t)nmax * 4);
+    e->sl().d_sstatus.ensure_zero(voxelize_status_words(nmax) * 8, e->s());
+    e->sl().d_sgstatus.ensure_zero((voxelize_status_words(nmax) / 16 + 256) * 8, e->s());
+    e->sl().d_gstatus.ensure_zero(voxelize_group_tiles(nmax) * 8, e->s());
+    e->sl().d_ggstatus.ensure_zero((voxelize_group_tiles(nmax) / 64 + 2) * 8, e->s());
+    e->sl().d_vox.ensure((size_t)nmax * 16);
     VoxelizeArgs v{};
-    v.keys = e->d_coords.as<uint32_t>();
-    v.pts = e->d_pts.as<float4>();
-    v.count = e->d_misc.as<uint32_t>() + kCount;
+    v.keys = e->sl().d_coords.as<uint32_t>();
+    v.pts = e->sl().d_pts.as<float4>();
+    v.count = e->sl().d_misc.as<uint32_t>() + kCount;
     v.nmax = nmax;
     v.key_bits = e->key_bits;
     v.average = average;
-    v.hist_ready = e->khist_pending ? 1 : 0;
+    v.hist_ready = e->sl().khist_pending ? 1 : 0;
     v.vp = e->vp;
-    v.keys_a = e->d_ka.as<uint32_t>();
-    v.keys_b = e->d_kb.as<uint32_t>();
-    v.vals_a = e->d_va.as<uint32_t>();
-    v.vals_b = e->d_vb.as<uint32_t>();
-    v.hist = e->d_khist.as<uint32_t>();
-    v.status = e->d_sstatus.as<unsigned long long>();
-    v.sgstatus = e->d_sgstatus.as<unsigned long long>();
-    v.gstatus = e->d_gstatus.as<unsigned long long>();
-    v.ggstatus = e->d_ggstatus.as<unsigned long long>();
-    v.ctrs = e->d_ctrs.as<unsigned long long>();
+    v.keys_a = e->sl().d_ka.as<uint32_t>();
+    v.keys_b = e->sl().d_kb.as<uint32_t>();
+    v.vals_a = e->sl().d_va.as<uint32_t>();
+    v.vals_b = e->sl().d_vb.as<uint32_t>();
+    v.hist = e->sl().d_khist.as<uint32_t>();
+    v.status = e->sl().d_sstatus.as<unsigned long long>();
+    v.sgstatus = e->sl().d_sgstatus.as<unsigned long long>();
+    v.gstatus = e->sl().d_gstatus.as<unsigned long long>();
+    v.ggstatus = e->sl().d_ggstatus.as<unsigned long long>();
+    v.ctrs = e->sl().d_ctrs.as<unsigned long long>();
     v.epoch = &e->epoch;
     v.sort_pt = e->sort_pt;
-    v.err = e->d_misc.as<uint32_t>() + kErr;
-    v.out = e->d_vox.as<float4>();
-    v.out_count = e->d_misc.as<uint32_t>() + kVoxCount;
+    v.err = e->sl().d_misc.as<uint32_t>() + kErr;
+    v.out = e->sl().d_vox.as<float4>();
+    v.out_count = e->sl().d_misc.as<uint32_t>() + kVoxCount;
     if (fused_grid_lifetime >= 0) {  // processFrame: the grid update rides on the first sort pass
         v.grid8 = e->d_grid8.as<uint8_t>();
         v.marks = marks_ptr(e);
         v.ncells = e->ncells;
         v.lifetime = (uint32_t)fused_grid_lifetime;
+        v.cb_ctx = e;
+        v.before_grid = [](void* c) { static_cast<gdf_engine*>(c)->order_grid(); };
+        v.after_grid = [](void* c) { static_cast<gdf_engine*>(c)->grid_updated(); };
     }
     e->timed(GDF_KERNEL_VOXELIZE, [&] { HIPCHK(launch_voxelize(v, e->s(), e->hook_ptr())); });
     if (fused_grid_lifetime >= 0) {
-        e->marks_set = false;
+        e->sl().marks_set = false;
         e->invoked_once = true;
     }
-    e->khist_pending = false;
-    e->vox_valid = true;
+    e->sl().khist_pending = false;
+    e->sl().vox_valid = true;
 }
 
 void occupancy_grid(gdf_engine* e, uint32_t lifetime, hipStream_t st) {  // fusion.cpp:1757-1823
     if (!e->grid_set) fail(GDF_ERR_STATE, "voxelOccupancyGrid before computeVoxelCoords");
     widen_if_needed(e, lifetime, st);
-    if (!e->marks_set) {
-        if (!e->coords_valid) fail(GDF_ERR_STATE, "voxelOccupancyGrid needs voxel coordinates");
-        HIPCHK(launch_scatter(e->d_coords.as<uint32_t>(), e->d_misc.as<uint32_t>() + kCount,
-                              std::max<uint32_t>(e->n_total, 1), marks_ptr(e), st));
+    if (!e->sl().marks_set) {
+        if (!e->sl().coords_valid) fail(GDF_ERR_STATE, "voxelOccupancyGrid needs voxel coordinates");
+        HIPCHK(launch_scatter(e->sl().d_coords.as<uint32_t>(), e->sl().d_misc.as<uint32_t>() + kCount,
+                              std::max<uint32_t>(e->sl().n_total, 1), marks_ptr(e), st));
     }
+    e->order_grid();
     e->timed_on(GDF_KERNEL_GRID, st, [&] {
         if (e->grid_mode == 0)
             HIPCHK(launch_grid_u8(e->d_grid8.as<uint8_t>(), marks_ptr(e), e->ncells, lifetime, st));
@@ -819,7 +917,8 @@ void occupancy_grid(gdf_engine* e, uint32_t lifetime, hipStream_t st) {  // fusi
             HIPCHK(launch_grid_u32(e->d_hist32.as<uint32_t>(), marks_ptr(e),
                                    e->d_out8.as<uint8_t>(), e->ncells, lifetime, st));
     });
-    e->marks_set = false;
+    e->grid_updated();
+    e->sl().marks_set = false;
     e->invoked_once = true;
 }
 
@@ -876,13 +975,10 @@ int gdf_create(int device, gdf_engine** out) {
     if (!e) return GDF_ERR_NOMEM;
     e->device = device;
     int rc = guarded(e, [&] {
-        HIPCHK(hipStreamCreateWithFlags(&e->own, hipStreamNonBlocking));
-        e->stream = e->own;
+        create_slot(e->slots[0]);
         if (const char* v = std::getenv("GDF_SORT_PT")) e->sort_pt = std::atoi(v);  // tuning knob
-        HIPCHK(hipHostMalloc((void**)&e->h_misc, kMiscWords * 4, hipHostMallocDefault));
-        std::memset(e->h_misc, 0, kMiscWords * 4);
         ensure_misc(e);
-        HIPCHK(hipStreamSynchronize(e->stream));
+        HIPCHK(hipStreamSynchronize(e->s()));
     });
     if (rc != GDF_OK) {
         delete e;
@@ -895,14 +991,20 @@ int gdf_create(int device, gdf_engine** out) {
 int gdf_destroy(gdf_engine* e) {
     if (!e) return GDF_OK;
     (void)hipSetDevice(e->device);
-    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->user_stream) (void)hipStreamSynchronize(e->user_stream);
+    for (Slot& sl : e->slots)
+        if (sl.own) (void)hipStreamSynchronize(sl.own);
     for (auto& p : e->ev_pending) {
         (void)hipEventDestroy(p.a);
         (void)hipEventDestroy(p.b);
     }
     for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
-    if (e->h_misc) (void)hipHostFree(e->h_misc);
-    if (e->own) (void)hipStreamDestroy(e->own);
+    for (Slot& sl : e->slots) {
+        if (sl.h_misc) (void)hipHostFree(sl.h_misc);
+        if (sl.ev_done) (void)hipEventDestroy(sl.ev_done);
+        if (sl.ev_grid) (void)hipEventDestroy(sl.ev_grid);
+        if (sl.own) (void)hipStreamDestroy(sl.own);
+    }
     delete e;
     return GDF_OK;
 }
@@ -910,14 +1012,40 @@ int gdf_destroy(gdf_engine* e) {
 int gdf_set_stream(gdf_engine* e, void* stream) {
     ENGINE_OR_FAIL(e);
     return guarded(e, [&] {
-        HIPCHK(hipStreamSynchronize(e->stream));
-        e->stream = stream ? static_cast<hipStream_t>(stream) : e->own;
+        sync_all(e);
+        e->user_stream = static_cast<hipStream_t>(stream);
+        if (stream) {  // the caller orders frames on its own stream: one slot
+            e->npipe = 1;
+            e->cur = 0;
+        }
     });
 }
 
 int gdf_synchronize(gdf_engine* e) {
     ENGINE_OR_FAIL(e);
-    return guarded(e, [&] { e->sync(); });
+    return guarded(e, [&] {
+        sync_all(e);
+        e->sync();
+    });
+}
+
+int gdf_set_pipeline_depth(gdf_engine* e, int depth) {
+    ENGINE_OR_FAIL(e);
+    if (depth < 1 || depth > kMaxPipe) {
+        g_last_error = "pipeline depth must be 1.." + std::to_string(kMaxPipe);
+        return GDF_ERR_ARG;
+    }
+    return guarded(e, [&] {
+        if (e->user_stream && depth > 1) fail(GDF_ERR_STATE, "pipelining needs the engine's own streams");
+        sync_all(e);
+        for (int i = 0; i < depth; ++i) create_slot(e->slots[i]);
+        // a configuration call between frames: the next frame starts on slot 0 (a shallower
+        // pipeline does not keep the results of the frame that was current)
+        if (e->cur >= depth) e->cur = 0;
+        for (Slot& sl : e->slots) sl.done_recorded = sl.grid_recorded = false;
+        e->npipe = depth;
+        e->serialized = false;
+    });
 }
 
 int gdf_set_voxel_group_size(gdf_engine* e, int group_size) {
@@ -1055,7 +1183,7 @@ int gdf_apply_point_mask(gdf_engine* e, uint32_t* out_count) {
         run_frame(e, false);
         if (out_count) {
             e->read_misc();
-            *out_count = e->h_misc[kCount];
+            *out_count = e->sl().h_misc[kCount];
         }
     });
 }
@@ -1080,22 +1208,22 @@ int gdf_get_point_count(gdf_engine* e, uint32_t* out) {
     ENGINE_OR_FAIL(e);
     if (!out) return GDF_ERR_ARG;
     return guarded(e, [&] {
-        if (!e->compacted) fail(GDF_ERR_STATE, "no compaction has run");
+        if (!e->sl().compacted) fail(GDF_ERR_STATE, "no compaction has run");
         e->read_misc();
-        *out = e->h_misc[kCount];
+        *out = e->sl().h_misc[kCount];
     });
 }
 
 int gdf_download_points(gdf_engine* e, float* out, uint32_t cap, uint32_t* out_count) {
     ENGINE_OR_FAIL(e);
     return guarded(e, [&] {
-        if (!e->compacted) fail(GDF_ERR_STATE, "downloadPoints before applyPointMask");
+        if (!e->sl().compacted) fail(GDF_ERR_STATE, "downloadPoints before applyPointMask");
         e->read_misc();
-        const uint32_t n = e->h_misc[kCount];
+        const uint32_t n = e->sl().h_misc[kCount];
         if (out_count) *out_count = n;
         if (out) {
             if (cap < n) fail(GDF_ERR_CAPACITY, "downloadPoints: buffer too small");
-            if (n) HIPCHK(hipMemcpy(out, e->d_pts.p, (size_t)n * 16, hipMemcpyDeviceToHost));
+            if (n) HIPCHK(hipMemcpy(out, e->sl().d_pts.p, (size_t)n * 16, hipMemcpyDeviceToHost));
         }
     });
 }
@@ -1103,13 +1231,13 @@ int gdf_download_points(gdf_engine* e, float* out, uint32_t cap, uint32_t* out_c
 int gdf_download_voxel_coords(gdf_engine* e, uint32_t* out, uint32_t cap, uint32_t* out_count) {
     ENGINE_OR_FAIL(e);
     return guarded(e, [&] {
-        if (!e->coords_valid) fail(GDF_ERR_STATE, "downloadVoxelCoords before computeVoxelCoords");
+        if (!e->sl().coords_valid) fail(GDF_ERR_STATE, "downloadVoxelCoords before computeVoxelCoords");
         e->read_misc();
-        const uint32_t n = e->h_misc[kCount];
+        const uint32_t n = e->sl().h_misc[kCount];
         if (out_count) *out_count = n;
         if (out) {
             if (cap < n) fail(GDF_ERR_CAPACITY, "downloadVoxelCoords: buffer too small");
-            if (n) HIPCHK(hipMemcpy(out, e->d_coords.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+            if (n) HIPCHK(hipMemcpy(out, e->sl().d_coords.p, (size_t)n * 4, hipMemcpyDeviceToHost));
         }
     });
 }
@@ -1117,13 +1245,13 @@ int gdf_download_voxel_coords(gdf_engine* e, uint32_t* out, uint32_t cap, uint32
 int gdf_download_voxelized_points(gdf_engine* e, float* out, uint32_t cap, uint32_t* out_count) {
     ENGINE_OR_FAIL(e);
     return guarded(e, [&] {
-        if (!e->vox_valid) fail(GDF_ERR_STATE, "no voxelize has run");
+        if (!e->sl().vox_valid) fail(GDF_ERR_STATE, "no voxelize has run");
         e->read_misc();
-        const uint32_t n = e->h_misc[kVoxCount];
+        const uint32_t n = e->sl().h_misc[kVoxCount];
         if (out_count) *out_count = n;
         if (out) {
             if (cap < n) fail(GDF_ERR_CAPACITY, "voxelized points: buffer too small");
-            if (n) HIPCHK(hipMemcpy(out, e->d_vox.p, (size_t)n * 16, hipMemcpyDeviceToHost));
+            if (n) HIPCHK(hipMemcpy(out, e->sl().d_vox.p, (size_t)n * 16, hipMemcpyDeviceToHost));
         }
     });
 }
@@ -1152,9 +1280,9 @@ int gdf_get_grid_size(gdf_engine* e, uint32_t g[3], uint64_t* ncells) {
 int gdf_get_device_results(gdf_engine* e, const float** pts, const uint32_t** coords,
                            const float** vox, const uint8_t** occ) {
     ENGINE_OR_FAIL(e);
-    if (pts) *pts = e->d_pts.as<const float>();
-    if (coords) *coords = e->d_coords.as<const uint32_t>();
-    if (vox) *vox = e->d_vox.as<const float>();
+    if (pts) *pts = e->sl().d_pts.as<const float>();
+    if (coords) *coords = e->sl().d_coords.as<const uint32_t>();
+    if (vox) *vox = e->sl().d_vox.as<const float>();
     if (occ) *occ = e->grid_set ? grid_out_ptr(e) : nullptr;
     return GDF_OK;
 }
@@ -1220,11 +1348,11 @@ int gdf_process_frame(gdf_engine* e, const gdf_frame_params* p, gdf_frame_result
             run_frame(e, false);
         }
         res.num_depth_points = e->depth_total;
-        res.num_points_total = e->n_total;
+        res.num_points_total = e->sl().n_total;
         if (p->synchronous) {
             e->read_misc();
-            res.num_points = e->h_misc[kCount];
-            res.num_voxelized = p->enable_voxel_filter ? e->h_misc[kVoxCount] : 0;
+            res.num_points = e->sl().h_misc[kCount];
+            res.num_voxelized = p->enable_voxel_filter ? e->sl().h_misc[kVoxCount] : 0;
         }
         if (r) *r = res;
     });
@@ -1245,7 +1373,7 @@ int gdf_import_occupancy_marks(gdf_engine* e, const uint32_t* bits, uint64_t wor
         if (!e->grid_set || !bits) fail(GDF_ERR_STATE, "no voxel grid");
         if (words < (e->ncells + 31) / 32) fail(GDF_ERR_CAPACITY, "mark bitmask too small");
         HIPCHK(launch_import_marks(marks_ptr(e), mark_words(e), bits, nranks, e->s()));
-        e->marks_set = true;
+        e->sl().marks_set = true;
     });
 }
 
@@ -1281,13 +1409,13 @@ int gdf_set_debug(gdf_engine* e, int enable) {
 int gdf_debug_stage_masks(gdf_engine* e, uint8_t* out, uint32_t cap, uint32_t* out_count) {
     ENGINE_OR_FAIL(e);
     return guarded(e, [&] {
-        if (!e->debug || !e->d_stage.p || !e->compacted)
+        if (!e->debug || !e->sl().d_stage.p || !e->sl().compacted)
             fail(GDF_ERR_STATE, "stage masks need gdf_set_debug(1) before the compaction");
-        if (out_count) *out_count = e->dbg_count;
+        if (out_count) *out_count = e->sl().dbg_count;
         if (out) {
-            if (cap < e->dbg_count) fail(GDF_ERR_CAPACITY, "debug masks: buffer too small");
+            if (cap < e->sl().dbg_count) fail(GDF_ERR_CAPACITY, "debug masks: buffer too small");
             e->sync();
-            if (e->dbg_count) HIPCHK(hipMemcpy(out, e->d_stage.p, e->dbg_count, hipMemcpyDeviceToHost));
+            if (e->sl().dbg_count) HIPCHK(hipMemcpy(out, e->sl().d_stage.p, e->sl().dbg_count, hipMemcpyDeviceToHost));
         }
     });
 }

@@ -1435,6 +1435,7 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
         const uint32_t ep = ++(*a.epoch);
         if (sort_tiles) {
             HookScope hs(hook, GDF_KERNEL_SORT);
+            if (p == 0 && a.grid8 && a.before_grid) a.before_grid(a.cb_ctx);
             if (pt == 4)
                 launch_sort_pass<4>(sort_tiles, s, kin, vin, kbuf[p & 1], vbuf[p & 1], a, p, ep, dbits);
             else if (pt == 8)
@@ -1442,6 +1443,7 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
             else
                 launch_sort_pass<16>(sort_tiles, s, kin, vin, kbuf[p & 1], vbuf[p & 1], a, p, ep, dbits);
             if ((e = hipGetLastError()) != hipSuccess) return e;
+            if (p == 0 && a.grid8 && a.after_grid) a.after_grid(a.cb_ctx);
         }
         kin = kbuf[p & 1];
         vin = vbuf[p & 1];

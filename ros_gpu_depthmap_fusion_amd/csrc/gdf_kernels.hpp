@@ -70,6 +70,10 @@ struct VoxelizeArgs {
     // first sort pass: it only needs the occupancy marks, which the compaction already wrote
     uint8_t* grid8;
     uint32_t* marks;
+    // ordering of the fused grid update with the previous frame's (frame pipelining)
+    void (*before_grid)(void*);
+    void (*after_grid)(void*);
+    void* cb_ctx;
     uint64_t ncells;
     uint32_t lifetime;
     uint32_t* err;

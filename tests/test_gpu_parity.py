@@ -206,16 +206,18 @@ def _add_sequences(engines, k0, nseq, cam, depth_fn, rng, empty_every=0, nan_fra
             e.addPointSequence(pts, s, ns, synth.move_transform(k))
 
 
-@pytest.mark.parametrize("fused", [True, False])
-def test_rollbuffer_chain(Engine, fused):
+@pytest.mark.parametrize("fused,depth", [(True, 1), (False, 1), (True, 3), (False, 2)])
+def test_rollbuffer_chain(Engine, fused, depth):
     """Point sequences (with empty sequences and NaN points) through filter / insert / roll /
-    select / transform over 8 frames, window of ~5 sequences (rollbuffer indices bit-exact)."""
+    select / transform over 8 frames, window of ~5 sequences (rollbuffer indices bit-exact);
+    depth > 1: frame pipelining, where the rollbuffer frames wait for their predecessor."""
     p = ComponentParams()
     p.ps_timespan = 4.0 / 30.0
     p.ps_filter_size = 2
     lidar = synth.make_camera(0, 96, 64)
     cam = synth.make_camera(1, 120, 90)
     gpu, orc = Engine(), OracleFusion(threads=4)
+    gpu.set_pipeline_depth(depth)
     rng = np.random.default_rng(9)
     Twm = synth.move_transform(3)
     Tcm = EYE
@@ -357,3 +359,39 @@ def test_multi_gpu_mark_export_import(Engine):
             np.testing.assert_array_equal(g.downloadVoxelOccupancyGrid().reshape(-1),
                                           (hist & 0xFF).astype(np.uint8),
                                           err_msg=f"frame {f} rank {k}")
+
+
+def _gpu_outputs(e):
+    return (e.downloadPoints(), e.downloadVoxelizedPoints(), e.downloadVoxelOccupancyGrid())
+
+
+def test_pipelined_frames_match_sequential(Engine):
+    """Frame pipelining (3 slots): synchronous frames give the sequential engine's outputs frame
+    by frame; then 40 asynchronous frames of two cameras, including a change of the flying
+    filter and of the lifetime (u8 -> u32 history), end in the same grid and last-frame outputs."""
+    p = ComponentParams()
+    cams = synth.cameras(2, 160, 120)
+    seq, pipe = Engine(), Engine()
+    pipe.set_pipeline_depth(3)
+    for f in range(6):
+        args = [cam_args(c, synth.depth_frame(c, k, f)) for k, c in enumerate(cams)]
+        for e in (seq, pipe):
+            run_fused(e, args, p)
+        for a, b in zip(_gpu_outputs(seq), _gpu_outputs(pipe)):
+            np.testing.assert_array_equal(bits(a) if a.dtype == np.float32 else a,
+                                          bits(b) if b.dtype == np.float32 else b,
+                                          err_msg=f"frame {f}")
+    for f in range(6, 46):
+        if f == 20:
+            p.flying_filter_size = 2
+        if f == 30:
+            p.occupancy_lifetime = 300
+        args = [cam_args(c, synth.depth_frame(c, k, f % 9)) for k, c in enumerate(cams)]
+        for e in (seq, pipe):
+            run_fused(e, args, p, synchronous=False)
+    seq.synchronize()
+    pipe.synchronize()
+    for a, b in zip(_gpu_outputs(seq), _gpu_outputs(pipe)):
+        np.testing.assert_array_equal(bits(a) if a.dtype == np.float32 else a,
+                                      bits(b) if b.dtype == np.float32 else b)
+    np.testing.assert_array_equal(seq.historic_grid(), pipe.historic_grid())

@@ -21,7 +21,9 @@ def main():
     dframes = [hiprt.DeviceArray.from_numpy(synth.depth_frame(cam, 0, f)) for f in range(4)]
     eng = GPUDepthmapFusion(0)
     params = ComponentParams()
-    prof = len(sys.argv) > 1 and sys.argv[1] == "prof"
+    prof = "prof" in sys.argv[1:]
+    depth = int(next((a[6:] for a in sys.argv[1:] if a.startswith("depth=")), "1"))
+    eng.set_pipeline_depth(depth)
     t = {"to_c": 0.0, "clear_add": 0.0, "process": 0.0}
     n = 0
     for i in range(2000):
@@ -46,7 +48,7 @@ def main():
         t["process"] += t3 - t2
         n += 1
     eng.synchronize()
-    print(json.dumps({k: round(v / n * 1e6, 2) for k, v in t.items()} | {"profiling": prof}))
+    print(json.dumps({k: round(v / n * 1e6, 2) for k, v in t.items()} | {"profiling": prof, "depth": depth}))
 
 
 if __name__ == "__main__":
