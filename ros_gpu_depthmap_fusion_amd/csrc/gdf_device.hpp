@@ -24,7 +24,16 @@ constexpr uint32_t kSpinLimit = 1u << 26;                   // bounded look-back
 
 // Device-wide counters: monotonically increasing tile tickets (the host passes each launch's
 // base, so no per-launch memset) and the global digit histogram of the voxel keys.
-enum CounterSlot { kCtrFrame = 0, kCtrSort0 = 1, kCtrGroup = 5, kCtrSlots = 8 };
+// per-stream device counters (u64 words, low 32 bits used): tile tickets, look-back epoch
+enum CounterSlot { kCtrFrame = 0, kCtrSort0 = 1, kCtrGroup = 5, kCtrEpoch = 6, kCtrSlots = 8 };
+
+// engine-order of historic-grid updates across streams (grid_seq_enter / grid_seq_leave)
+struct GridSeq {
+    uint32_t* ctl;         // [0] updates completed, [1] blocks finished of the running one
+    const uint32_t* fptr;  // the update's sequence number on the device (or nullptr: use f)
+    uint32_t f;
+    uint32_t* err;
+};
 
 // A halo camera (emit == 0, multi-GPU sharding) sits at a negative offset: its pixels are only
 // read as flying-pixel neighbours, exactly where the reference's uint index arithmetic lands in
@@ -99,6 +108,8 @@ struct FrameArgs {
     uint32_t seg_threads;       // block size of k_mask / k_emit (>= every segment, 64-multiple)
     uint8_t* dbg;               // optional per-item stage bits
     uint32_t* err;
+    uint32_t* grid_seq_out;     // optional: k_mask stores grid_seq here (the fused grid update's
+    uint32_t grid_seq;          // sequence number, read by the first sort pass of the frame)
 };
 static_assert(sizeof(FrameArgs) <= 4096, "kernel arguments are limited to 4 KiB");
 

@@ -153,7 +153,7 @@ bool ros_time_minus(uint32_t sec, uint32_t nsec, double seconds, uint32_t* os, u
     return true;
 }
 
-enum MiscSlot { kCount = 0, kTileCtr = 1, kErr = 2, kVoxCount = 3, kSortCtrs = 4, kMiscWords = 16 };
+enum MiscSlot { kCount = 0, kTileCtr = 1, kErr = 2, kVoxCount = 3, kGridTicket = 4, kMiscWords = 16 };
 
 }  // namespace
 
@@ -161,13 +161,13 @@ enum MiscSlot { kCount = 0, kTileCtr = 1, kErr = 2, kVoxCount = 3, kSortCtrs = 4
 constexpr int kMaxPipe = 4;
 
 // Everything one frame writes.  Frames rotate over npipe slots (gdf_clear starts a frame), so a
-// new frame's compaction runs while the previous frame's sort / grouping still execute; shared
-// state (rollbuffer ring, camera tables, the occupancy grid) is ordered by events.
+// new frame's compaction runs while the previous frame's sort / grouping still execute.  The
+// occupancy grid is ordered on the device (GridSeq: updates apply in ticket order whatever stream
+// they run on); other shared state (rollbuffer ring, selection and camera tables) is rewritten
+// only after the host has drained the other slots (serialize) - a cross-stream event wait costs
+// ~20 us of GPU time per frame on this device (tools/graph_probe.hip).
 struct Slot {
     hipStream_t own = nullptr;
-    hipEvent_t ev_done = nullptr;   // recorded when the next frame starts on another slot
-    hipEvent_t ev_grid = nullptr;   // recorded after this frame's grid update
-    bool done_recorded = false, grid_recorded = false;
     DevBuf d_depth;                 // host depth maps uploaded for this frame
     DevBuf d_camdesc;
     DevBuf d_ctrs;                  // tile tickets of the look-back launches
@@ -240,8 +240,6 @@ struct gdf_engine {
     int rot45 = 0;
     float lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
 
-    // tile tickets + epochs of the look-back launches (no per-launch memsets)
-    uint32_t epoch = 0;
     int sort_pt = 4;
 
     // compaction outputs
@@ -254,6 +252,8 @@ struct gdf_engine {
     uint32_t key_bits = 0;
     VoxelParams vp{};
     DevBuf d_grid8, d_hist32, d_out8;
+    DevBuf d_gridctl;               // GridSeq counters [0] updates done, [1] blocks finished
+    uint32_t grid_ticket = 0;       // sequence number of the next grid update
     uint32_t grid_gen = 0;          // bumped when the grid is (re)allocated: slots re-zero marks
     int grid_mode = 0;  // 0: u8 grid = history (lifetime <= 255); 1: u32 history + u8 output
     bool grid_alloc = false;
@@ -346,24 +346,23 @@ struct gdf_engine {
         HIPCHK(hipMemcpyAsync(sl().h_misc, sl().d_misc.p, kMiscWords * 4, hipMemcpyDeviceToHost, s()));
         sync();
     }
-    // once per frame, before touching state shared with the previous frame (rollbuffer ring,
-    // camera tables, grid allocation): the current slot's stream waits for the previous frame
+    // once per frame, before rewriting state the frames in flight may still read (rollbuffer
+    // ring, selection / camera tables, grid allocation): drain the other slots on the host
     void serialize() {
         if (npipe <= 1 || serialized) return;
-        Slot& p = prev_slot();
-        if (p.done_recorded) HIPCHK(hipStreamWaitEvent(s(), p.ev_done, 0));
+        for (int i = 0; i < npipe; ++i)
+            if (i != cur && slots[i].own) HIPCHK(hipStreamSynchronize(slots[i].own));
         serialized = true;
     }
-    // the previous frame's grid update precedes this frame's (the history is a chain)
-    void order_grid() {
-        if (npipe <= 1) return;
-        Slot& p = prev_slot();
-        if (p.grid_recorded) HIPCHK(hipStreamWaitEvent(s(), p.ev_grid, 0));
-    }
-    void grid_updated() {
-        if (npipe <= 1) return;
-        HIPCHK(hipEventRecord(sl().ev_grid, s()));
-        sl().grid_recorded = true;
+    // the ordering of one historic-grid update: ticket f (or the ticket the frame's k_mask stored)
+    // (one stream: stream order suffices, no device ordering)
+    GridSeq grid_seq(uint32_t f, const uint32_t* fptr = nullptr) {
+        GridSeq q{};
+        q.ctl = npipe > 1 ? d_gridctl.as<uint32_t>() : nullptr;
+        q.fptr = fptr;
+        q.f = f;
+        q.err = sl().d_misc.as<uint32_t>() + kErr;
+        return q;
     }
 };
 
@@ -372,8 +371,6 @@ namespace {
 void create_slot(Slot& sl) {
     if (sl.own) return;
     HIPCHK(hipStreamCreateWithFlags(&sl.own, hipStreamNonBlocking));
-    HIPCHK(hipEventCreateWithFlags(&sl.ev_done, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&sl.ev_grid, hipEventDisableTiming));
     HIPCHK(hipHostMalloc((void**)&sl.h_misc, kMiscWords * 4, hipHostMallocDefault));
     std::memset(sl.h_misc, 0, kMiscWords * 4);
 }
@@ -387,9 +384,6 @@ void sync_all(gdf_engine* e) {
 // frame boundary (gdf_clear): the next frame goes to the next slot
 void next_slot(gdf_engine* e) {
     if (e->npipe <= 1) return;
-    Slot& c = e->sl();
-    HIPCHK(hipEventRecord(c.ev_done, e->s()));
-    c.done_recorded = true;
     e->cur = (e->cur + 1) % e->npipe;
     e->serialized = false;
 }
@@ -717,11 +711,14 @@ void set_grid(gdf_engine* e, const float* lo, const float* hi, const float* cs) 
     e->ncells = cells;
     e->grid_set = true;
     if (changed) {  // historic grid cleared on first use / resize (fusion.cpp:1759-1773)
-        e->serialize();
-        e->order_grid();
+        sync_all(e);  // no grid update in flight on any stream
         const size_t padded = (size_t)((cells + 31) / 32) * 32;
         e->d_grid8.ensure(padded);
         HIPCHK(hipMemsetAsync(e->d_grid8.p, 0, padded, e->s()));
+        e->d_gridctl.ensure(64);
+        HIPCHK(hipMemsetAsync(e->d_gridctl.p, 0, 64, e->s()));
+        e->grid_ticket = 0;
+        HIPCHK(hipStreamSynchronize(e->s()));  // the other streams see the cleared counters
         e->grid_mode = 0;
         e->grid_alloc = true;
         e->grid_gen++;
@@ -734,13 +731,16 @@ void set_grid(gdf_engine* e, const float* lo, const float* hi, const float* cs) 
 uint32_t* marks_ptr(const gdf_engine* e) { return e->sl().d_markbits.as<uint32_t>(); }
 uint64_t mark_words(const gdf_engine* e) { return (e->ncells + 31) / 32; }
 
+void ensure_misc(gdf_engine* e);
+
 // switch to the general u32 history once a lifetime no longer fits the u8 grid
 void widen_if_needed(gdf_engine* e, uint32_t lifetime, hipStream_t st) {
     if (e->grid_mode != 0 || lifetime <= 255) return;
-    e->order_grid();
+    ensure_misc(e);
     e->d_hist32.ensure((size_t)e->ncells * 4);
     e->d_out8.ensure((size_t)((e->ncells + 31) / 32) * 32);
-    HIPCHK(launch_widen_grid(e->d_grid8.as<uint8_t>(), e->d_hist32.as<uint32_t>(), e->ncells, st));
+    HIPCHK(launch_widen_grid(e->d_grid8.as<uint8_t>(), e->d_hist32.as<uint32_t>(), e->ncells,
+                             e->grid_seq(e->grid_ticket++), st));
     e->grid_mode = 1;
 }
 
@@ -793,6 +793,9 @@ void run_frame(gdf_engine* e, bool fused_voxel) {
     a.tfc = e->d_tfc.as<float>();
     a.do_voxel = fused_voxel ? 1 : 0;
     if (fused_voxel) {
+        // the sequence number a fused grid update of this frame will take (voxelize)
+        a.grid_seq_out = e->sl().d_misc.as<uint32_t>() + kGridTicket;
+        a.grid_seq = e->grid_ticket;
         a.marks = marks_ptr(e);
         std::memcpy(a.vlo, e->vp.vlo, 12);
         std::memcpy(a.vcs, e->vp.vcs, 12);
@@ -878,7 +881,6 @@ void voxelize(gdf_engine* e, int average, int fused_grid_lifetime = -1) {  // fu
     v.gstatus = e->sl().d_gstatus.as<unsigned long long>();
     v.ggstatus = e->sl().d_ggstatus.as<unsigned long long>();
     v.ctrs = e->sl().d_ctrs.as<unsigned long long>();
-    v.epoch = &e->epoch;
     v.sort_pt = e->sort_pt;
     v.err = e->sl().d_misc.as<uint32_t>() + kErr;
     v.out = e->sl().d_vox.as<float4>();
@@ -888,9 +890,9 @@ void voxelize(gdf_engine* e, int average, int fused_grid_lifetime = -1) {  // fu
         v.marks = marks_ptr(e);
         v.ncells = e->ncells;
         v.lifetime = (uint32_t)fused_grid_lifetime;
-        v.cb_ctx = e;
-        v.before_grid = [](void* c) { static_cast<gdf_engine*>(c)->order_grid(); };
-        v.after_grid = [](void* c) { static_cast<gdf_engine*>(c)->grid_updated(); };
+        // the ticket was stored by this frame's k_mask (run_frame: grid_seq = grid_ticket)
+        v.gseq = e->grid_seq(0, e->sl().d_misc.as<uint32_t>() + kGridTicket);
+        e->grid_ticket++;
     }
     e->timed(GDF_KERNEL_VOXELIZE, [&] { HIPCHK(launch_voxelize(v, e->s(), e->hook_ptr())); });
     if (fused_grid_lifetime >= 0) {
@@ -909,15 +911,15 @@ void occupancy_grid(gdf_engine* e, uint32_t lifetime, hipStream_t st) {  // fusi
         HIPCHK(launch_scatter(e->sl().d_coords.as<uint32_t>(), e->sl().d_misc.as<uint32_t>() + kCount,
                               std::max<uint32_t>(e->sl().n_total, 1), marks_ptr(e), st));
     }
-    e->order_grid();
+    ensure_misc(e);
+    const GridSeq q = e->grid_seq(e->grid_ticket++);
     e->timed_on(GDF_KERNEL_GRID, st, [&] {
         if (e->grid_mode == 0)
-            HIPCHK(launch_grid_u8(e->d_grid8.as<uint8_t>(), marks_ptr(e), e->ncells, lifetime, st));
+            HIPCHK(launch_grid_u8(e->d_grid8.as<uint8_t>(), marks_ptr(e), e->ncells, lifetime, q, st));
         else
             HIPCHK(launch_grid_u32(e->d_hist32.as<uint32_t>(), marks_ptr(e),
-                                   e->d_out8.as<uint8_t>(), e->ncells, lifetime, st));
+                                   e->d_out8.as<uint8_t>(), e->ncells, lifetime, q, st));
     });
-    e->grid_updated();
     e->sl().marks_set = false;
     e->invoked_once = true;
 }
@@ -1001,8 +1003,6 @@ int gdf_destroy(gdf_engine* e) {
     for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
     for (Slot& sl : e->slots) {
         if (sl.h_misc) (void)hipHostFree(sl.h_misc);
-        if (sl.ev_done) (void)hipEventDestroy(sl.ev_done);
-        if (sl.ev_grid) (void)hipEventDestroy(sl.ev_grid);
         if (sl.own) (void)hipStreamDestroy(sl.own);
     }
     delete e;
@@ -1042,7 +1042,10 @@ int gdf_set_pipeline_depth(gdf_engine* e, int depth) {
         // a configuration call between frames: the next frame starts on slot 0 (a shallower
         // pipeline does not keep the results of the frame that was current)
         if (e->cur >= depth) e->cur = 0;
-        for (Slot& sl : e->slots) sl.done_recorded = sl.grid_recorded = false;
+        if (e->grid_alloc) {  // restart the grid-update sequence (nothing in flight)
+            HIPCHK(hipMemset(e->d_gridctl.p, 0, 64));
+            e->grid_ticket = 0;
+        }
         e->npipe = depth;
         e->serialized = false;
     });
@@ -1261,6 +1264,7 @@ int gdf_download_occupancy_grid(gdf_engine* e, uint8_t* out, uint64_t cap) {
     return guarded(e, [&] {
         if (!e->grid_set || !e->invoked_once) fail(GDF_ERR_STATE, "no voxelOccupancyGrid has run");
         if (!out || cap < e->ncells) fail(GDF_ERR_CAPACITY, "occupancy grid: buffer too small");
+        sync_all(e);  // grid updates may still run on another slot's stream
         e->sync();
         HIPCHK(hipMemcpy(out, grid_out_ptr(e), e->ncells, hipMemcpyDeviceToHost));
     });
@@ -1463,6 +1467,7 @@ int gdf_debug_historic_grid(gdf_engine* e, uint32_t* out, uint64_t cap) {
     return guarded(e, [&] {
         if (!e->grid_set) fail(GDF_ERR_STATE, "no voxel grid");
         if (!out || cap < e->ncells) fail(GDF_ERR_CAPACITY, "historic grid: buffer too small");
+        sync_all(e);
         e->sync();
         if (e->grid_mode == 1) {
             HIPCHK(hipMemcpy(out, e->d_hist32.p, e->ncells * 4, hipMemcpyDeviceToHost));

@@ -50,6 +50,26 @@ __device__ __forceinline__ uint32_t take_ticket(uint32_t* ctr, uint32_t ntiles) 
     return t;
 }
 
+// Ticket + look-back epoch of a launch, both device-resident (a captured frame replays with
+// unchanged kernel arguments).  Every ticket taker reads the stream's epoch word E before its
+// ticket; the taker of the last ticket - after every other block has read E - advances it, so
+// each launch that publishes granules uses a fresh epoch E + 1 >= 1 and the next launch on the
+// stream sees E + 1.  (A launch with no tiles takes no ticket, publishes nothing and leaves E.)
+__device__ __forceinline__ uint32_t take_ticket_epoch(uint32_t* ctr, uint32_t ntiles,
+                                                      uint32_t* epoch_word, uint32_t& epoch) {
+    const uint32_t e = __hip_atomic_load(epoch_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the read has returned before the ticket is taken (a wait, not an acquire fence: that would
+    // invalidate the XCD's L2 for every tile)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t t = atomicAdd(ctr, 1u);
+    if (t == ntiles - 1u) {
+        atomicExch(ctr, 0u);
+        __hip_atomic_store(epoch_word, e + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    epoch = e + 1u;
+    return t;
+}
+
 // Block (256 threads) exclusive scan of one value per thread.
 __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t& total,
                                                          uint32_t* s_wave) {
@@ -79,55 +99,6 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t& t
 // launches read as "not ready" and the status arrays never need a memset.  Each granule is
 // written by ONE agent-scope atomic store and polled with agent-scope atomic loads (MI355X
 // hand-off form "R2": the data is the flag, no fence needed).
-// Wave-cooperative variant, called by all 64 lanes of ONE wave: each hop polls the 64 nearest
-// predecessors at once (one cross-XCD round trip per 64 tiles instead of per tile), stops at the
-// nearest inclusive prefix and sums the aggregates in front of it.
-__device__ __forceinline__ uint32_t lookback_wave(unsigned long long* status, uint32_t tile,
-                                                  uint32_t agg, uint32_t epoch, uint32_t* err) {
-    const int lane = threadIdx.x & 63;
-    const unsigned long long fagg = 2ull * epoch, fincl = 2ull * epoch + 1ull;
-    if (tile == 0) {
-        if (lane == 0)
-            __hip_atomic_store(&status[0], (fincl << 32) | agg, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        return 0;
-    }
-    if (lane == 0)
-        __hip_atomic_store(&status[tile], (fagg << 32) | agg, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    uint32_t excl = 0, spins = 0;
-    int64_t base = (int64_t)tile - 1;
-    while (true) {
-        const int64_t j = base - lane;
-        unsigned long long sv = fincl << 32;  // j < 0 reads as an inclusive prefix of 0
-        if (j >= 0)
-            sv = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long flag = sv >> 32;
-        const unsigned long long m_incl = __ballot(flag == fincl);
-        const unsigned long long m_wait = __ballot(flag < fagg);
-        const int first = m_incl ? __ffsll((long long)m_incl) - 1 : 63;
-        const unsigned long long need = first == 63 ? ~0ull : ((2ull << first) - 1ull);
-        if (m_wait & need) {
-            if (++spins > kSpinLimit) {
-                if (lane == 0) atomicOr(err, 1u);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            continue;
-        }
-        uint32_t v = (lane <= first) ? (uint32_t)sv : 0u;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-        excl += v;
-        if (m_incl) break;
-        base -= 64;
-    }
-    if (lane == 0)
-        __hip_atomic_store(&status[tile], (fincl << 32) | (uint32_t)(excl + agg), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    return excl;
-}
-
 // Two-level decoupled look-back, wave-cooperative, one prefix channel.  Tiles are grouped by 64:
 // level 1 sums the aggregates of the tile's predecessors inside its group (one 64-wide poll);
 // the group's last tile then publishes the group aggregate BEFORE resolving its own group prefix,
@@ -569,6 +540,7 @@ __global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
     const uint32_t n = gridDim.x, q8 = n / 8, r8 = n % 8, xcd = blockIdx.x % 8;
     const uint32_t s = xcd * q8 + min(xcd, r8) + blockIdx.x / 8;
     load_cams(a, s_cams);
+    if (a.grid_seq_out && blockIdx.x == 0 && threadIdx.x == 0) *a.grid_seq_out = a.grid_seq;
     __syncthreads();
     uint32_t bits = 0;
     const uint32_t i = threadIdx.x;
@@ -937,6 +909,46 @@ hipError_t launch_ps_filter_insert(const float4* new_pts, uint32_t n, int do_fil
 // k_scatter and consumed - read and cleared - by the grid update.  hist' = max(sat_dec(hist),
 // mark·L) (decrement_uints.glsl:31-51 + max_with_uints_times_scalar.glsl:36-46); the output byte is
 // hist & 0xFF (uints_to_chars.glsl:31-50).  With L <= 255 the u8 grid IS the history.
+// Grid updates are applied in engine order even when consecutive frames run on different
+// streams (frame pipelining): update f waits until ctl[0] == f (updates completed), and the last
+// of its blocks to finish publishes ctl[0] = f + 1.  f comes from the host (the kernel argument,
+// or a per-slot word the frame's k_mask stored).  ctl == nullptr: no ordering (one stream).
+__device__ __forceinline__ uint32_t grid_seq_enter(const GridSeq& q) {
+    __shared__ uint32_t s_f;
+    if (!q.ctl) return 0;
+    if (threadIdx.x == 0) {
+        const uint32_t f = q.fptr ? __hip_atomic_load(q.fptr, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT) : q.f;
+        uint32_t spins = 0;
+        while ((int32_t)(__hip_atomic_load(&q.ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
+                         f) < 0) {
+            if (++spins > kSpinLimit) {
+                atomicOr(q.err, 4u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(8);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the previous update's grid
+        s_f = f;
+    }
+    __syncthreads();
+    return s_f;
+}
+
+__device__ __forceinline__ void grid_seq_leave(const GridSeq& q, uint32_t f, uint32_t nblocks) {
+    if (!q.ctl) return;
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's grid stores have reached L2
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // L2 write-back: visible to all XCDs
+        const uint32_t c = atomicAdd(&q.ctl[1], 1u);
+        if (c == nblocks - 1u) {
+            atomicExch(&q.ctl[1], 0u);
+            __hip_atomic_store(&q.ctl[0], f + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 __device__ __forceinline__ uint32_t grid_byte(uint32_t h, uint32_t m, uint32_t L) {
     const uint32_t dec = h ? h - 1u : 0u;
     return m ? (dec > L ? dec : L) : dec;
@@ -974,8 +986,10 @@ __device__ __forceinline__ void grid_u8_part(uint4* __restrict__ grid, uint32_t*
 
 __global__ __launch_bounds__(256) void k_grid_u8(uint4* __restrict__ grid,
                                                  uint32_t* __restrict__ marks, uint64_t nwords,
-                                                 uint32_t L) {
+                                                 uint32_t L, GridSeq q) {
+    const uint32_t f = grid_seq_enter(q);
     grid_u8_part(grid, marks, nwords, L, blockIdx.x, gridDim.x);
+    grid_seq_leave(q, f, gridDim.x);
 }
 
 static unsigned grid_blocks(uint64_t work, unsigned per_block) {
@@ -986,10 +1000,10 @@ static unsigned grid_blocks(uint64_t work, unsigned per_block) {
 }
 
 hipError_t launch_grid_u8(uint8_t* grid, uint32_t* marks, uint64_t ncells, uint32_t lifetime,
-                          hipStream_t s) {
+                          const GridSeq& q, hipStream_t s) {
     const uint64_t nwords = (ncells + 31) / 32;
     hipLaunchKernelGGL(k_grid_u8, dim3(grid_blocks(nwords, 256)), dim3(256), 0, s,
-                       reinterpret_cast<uint4*>(grid), marks, nwords, lifetime);
+                       reinterpret_cast<uint4*>(grid), marks, nwords, lifetime, q);
     return hipGetLastError();
 }
 
@@ -997,7 +1011,8 @@ hipError_t launch_grid_u8(uint8_t* grid, uint32_t* marks, uint64_t ncells, uint3
 __global__ __launch_bounds__(256) void k_grid_u32(uint32_t* __restrict__ hist,
                                                   uint32_t* __restrict__ marks,
                                                   uint8_t* __restrict__ out8, uint64_t ncells,
-                                                  uint32_t L) {
+                                                  uint32_t L, GridSeq q) {
+    const uint32_t f = grid_seq_enter(q);
     const uint64_t nwords = (ncells + 31) / 32;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nwords;
          i += (uint64_t)gridDim.x * blockDim.x) {
@@ -1014,27 +1029,31 @@ __global__ __launch_bounds__(256) void k_grid_u32(uint32_t* __restrict__ hist,
         }
         if (m) marks[i] = 0u;
     }
+    grid_seq_leave(q, f, gridDim.x);
 }
 
 hipError_t launch_grid_u32(uint32_t* hist, uint32_t* marks, uint8_t* out8, uint64_t ncells,
-                           uint32_t lifetime, hipStream_t s) {
+                           uint32_t lifetime, const GridSeq& q, hipStream_t s) {
     hipLaunchKernelGGL(k_grid_u32, dim3(grid_blocks((ncells + 31) / 32, 256)), dim3(256), 0, s,
-                       hist, marks, out8, ncells, lifetime);
+                       hist, marks, out8, ncells, lifetime, q);
     return hipGetLastError();
 }
 
 // u8 history -> u32 history (switch to lifetime > 255)
 __global__ __launch_bounds__(256) void k_widen(const uint8_t* __restrict__ g8,
-                                               uint32_t* __restrict__ hist, uint64_t ncells) {
+                                               uint32_t* __restrict__ hist, uint64_t ncells,
+                                               GridSeq q) {
+    const uint32_t f = grid_seq_enter(q);
     for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < ncells;
          c += (uint64_t)gridDim.x * blockDim.x)
         hist[c] = g8[c];
+    grid_seq_leave(q, f, gridDim.x);
 }
 
 hipError_t launch_widen_grid(const uint8_t* grid8, uint32_t* hist, uint64_t ncells,
-                             hipStream_t s) {
+                             const GridSeq& q, hipStream_t s) {
     hipLaunchKernelGGL(k_widen, dim3(grid_blocks(ncells, 256)), dim3(256), 0, s, grid8, hist,
-                       ncells);
+                       ncells, q);
     return hipGetLastError();
 }
 
@@ -1111,26 +1130,33 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
     uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, const uint32_t* __restrict__ count,
     const uint32_t* __restrict__ ghist, unsigned long long* status, unsigned long long* gstatus,
-    uint32_t* tile_ctr, uint32_t epoch, uint32_t* err, uint32_t shift, uint32_t dbits,
-    uint32_t grid_block0, uint4* grid, uint32_t* marks, uint64_t grid_nwords, uint32_t lifetime) {
+    uint32_t* tile_ctr, uint32_t* epoch_word, uint32_t* err, uint32_t shift, uint32_t dbits,
+    uint32_t grid_block0, uint4* grid, uint32_t* marks, uint64_t grid_nwords, uint32_t lifetime,
+    GridSeq q) {
     constexpr int kTile = kSortThreads * PT;
     if (blockIdx.x >= grid_block0) {  // fused historic-grid update (first pass only)
+        const uint32_t f = grid_seq_enter(q);
         grid_u8_part(grid, marks, grid_nwords, lifetime, blockIdx.x - grid_block0,
                      gridDim.x - grid_block0);
+        grid_seq_leave(q, f, gridDim.x - grid_block0);
         return;
     }
     __shared__ uint32_t s_cnt[4][256];
     __shared__ uint32_t s_base[256];
     __shared__ uint32_t s_excl[256];
     __shared__ uint32_t s_wave[4];
-    __shared__ uint32_t s_tile;
+    __shared__ uint32_t s_tile, s_epoch;
     const uint32_t n = *count;
     const uint32_t ntiles = (n + kTile - 1) / kTile;
     if (blockIdx.x >= ntiles) return;  // launched for the capacity; takes no ticket
-    if (threadIdx.x == 0) s_tile = take_ticket(tile_ctr, ntiles);
+    if (threadIdx.x == 0) {
+        uint32_t ep;
+        s_tile = take_ticket_epoch(tile_ctr, ntiles, epoch_word, ep);
+        s_epoch = ep;
+    }
     for (uint32_t i = threadIdx.x; i < 4 * 256; i += kSortThreads) (&s_cnt[0][0])[i] = 0;
     __syncthreads();
-    const uint32_t tile = s_tile;
+    const uint32_t tile = s_tile, epoch = s_epoch;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const unsigned long long ltm = lanemask_lt();
 
@@ -1214,10 +1240,10 @@ __global__ __launch_bounds__(kGroupThreads) void k_group(
     const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
     const uint32_t* __restrict__ count, const float4* __restrict__ pts, float* __restrict__ out,
     uint32_t* __restrict__ out_count, unsigned long long* status, unsigned long long* gstatus,
-    uint32_t* tile_ctr, uint32_t epoch, uint32_t* err, uint32_t* hist, int average,
+    uint32_t* tile_ctr, uint32_t* epoch_word, uint32_t* err, uint32_t* hist, int average,
     VoxelParams vp) {
     __shared__ uint32_t s_wave[4];
-    __shared__ uint32_t s_tile, s_excl, s_nbig;
+    __shared__ uint32_t s_tile, s_epoch, s_excl, s_nbig;
     __shared__ uint32_t s_start[kGroupThreads + 1];
     __shared__ uint32_t s_big[kGroupThreads];
     __shared__ float4 s_buf[4][kSumChunk];
@@ -1232,11 +1258,13 @@ __global__ __launch_bounds__(kGroupThreads) void k_group(
         return;
     }
     if (threadIdx.x == 0) {
-        s_tile = take_ticket(tile_ctr, ntiles);
+        uint32_t ep;
+        s_tile = take_ticket_epoch(tile_ctr, ntiles, epoch_word, ep);
+        s_epoch = ep;
         s_nbig = 0;
     }
     __syncthreads();
-    const uint32_t tile = s_tile;
+    const uint32_t tile = s_tile, epoch = s_epoch;
     const uint32_t i = tile * kGroupThreads + threadIdx.x;
     const uint32_t tend = min(n, (tile + 1) * kGroupThreads);
     const uint32_t key = i < n ? keys[i] : 0u;
@@ -1402,15 +1430,16 @@ size_t voxelize_group_tiles(uint32_t nmax) {
 template <int PT>
 static void launch_sort_pass(uint32_t tiles, hipStream_t s, const uint32_t* kin, const uint32_t* vin,
                              uint32_t* kout, uint32_t* vout, const VoxelizeArgs& a, uint32_t p,
-                             uint32_t ep, uint32_t dbits) {
+                             uint32_t dbits) {
     // the first pass also carries the historic-grid update in extra blocks
     const bool g = p == 0 && a.grid8 != nullptr;
     const uint64_t nwords = g ? (a.ncells + 31) / 32 : 0;
     const uint32_t gb = g ? grid_blocks(nwords, 256 * 2) : 0;
     hipLaunchKernelGGL(k_sort_pass<PT>, dim3(tiles + gb), dim3(kSortThreads), 0, s, kin, vin, kout,
                        vout, a.count, a.hist + 256 * p, a.status, a.sgstatus,
-                       reinterpret_cast<uint32_t*>(a.ctrs + kCtrSort0 + p), ep, a.err, 8 * p, dbits,
-                       tiles, reinterpret_cast<uint4*>(a.grid8), a.marks, nwords, a.lifetime);
+                       reinterpret_cast<uint32_t*>(a.ctrs + kCtrSort0 + p),
+                       reinterpret_cast<uint32_t*>(a.ctrs + kCtrEpoch), a.err, 8 * p, dbits, tiles,
+                       reinterpret_cast<uint4*>(a.grid8), a.marks, nwords, a.lifetime, a.gseq);
 }
 
 hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hook) {
@@ -1432,29 +1461,26 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
     for (uint32_t p = 0; p < npasses; ++p) {
         const uint32_t remaining = a.key_bits > 8 * p ? a.key_bits - 8 * p : 0u;
         const uint32_t dbits = remaining >= 8 ? 8u : (remaining ? remaining : 1u);
-        const uint32_t ep = ++(*a.epoch);
         if (sort_tiles) {
             HookScope hs(hook, GDF_KERNEL_SORT);
-            if (p == 0 && a.grid8 && a.before_grid) a.before_grid(a.cb_ctx);
             if (pt == 4)
-                launch_sort_pass<4>(sort_tiles, s, kin, vin, kbuf[p & 1], vbuf[p & 1], a, p, ep, dbits);
+                launch_sort_pass<4>(sort_tiles, s, kin, vin, kbuf[p & 1], vbuf[p & 1], a, p, dbits);
             else if (pt == 8)
-                launch_sort_pass<8>(sort_tiles, s, kin, vin, kbuf[p & 1], vbuf[p & 1], a, p, ep, dbits);
+                launch_sort_pass<8>(sort_tiles, s, kin, vin, kbuf[p & 1], vbuf[p & 1], a, p, dbits);
             else
-                launch_sort_pass<16>(sort_tiles, s, kin, vin, kbuf[p & 1], vbuf[p & 1], a, p, ep, dbits);
+                launch_sort_pass<16>(sort_tiles, s, kin, vin, kbuf[p & 1], vbuf[p & 1], a, p, dbits);
             if ((e = hipGetLastError()) != hipSuccess) return e;
-            if (p == 0 && a.grid8 && a.after_grid) a.after_grid(a.cb_ctx);
         }
         kin = kbuf[p & 1];
         vin = vbuf[p & 1];
     }
     const uint32_t group_tiles = (a.nmax + kGroupThreads - 1) / kGroupThreads;
-    const uint32_t ep = ++(*a.epoch);
     HookScope hs(hook, GDF_KERNEL_GROUP);
     hipLaunchKernelGGL(k_group, dim3(group_tiles ? group_tiles : 1), dim3(kGroupThreads), 0, s, kin,
                        vin, a.count, a.pts, reinterpret_cast<float*>(a.out), a.out_count,
-                       a.gstatus, a.ggstatus, reinterpret_cast<uint32_t*>(a.ctrs + kCtrGroup), ep,
-                       a.err, a.hist, a.average, a.vp);
+                       a.gstatus, a.ggstatus, reinterpret_cast<uint32_t*>(a.ctrs + kCtrGroup),
+                       reinterpret_cast<uint32_t*>(a.ctrs + kCtrEpoch), a.err, a.hist, a.average,
+                       a.vp);
     return hipGetLastError();
 }
 

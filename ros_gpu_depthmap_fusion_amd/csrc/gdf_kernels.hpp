@@ -33,11 +33,13 @@ hipError_t launch_ps_filter_insert(const float4* new_pts, uint32_t n, int do_fil
 
 // historic grid update from the frame's mark bitmask (cleared on the way): u8 grid = history for
 // lifetime <= 255; the general u32 history with a separate u8 output grid beyond
+// (q: engine order of grid updates across streams, see GridSeq)
 hipError_t launch_grid_u8(uint8_t* grid, uint32_t* marks, uint64_t ncells, uint32_t lifetime,
-                          hipStream_t s);
+                          const GridSeq& q, hipStream_t s);
 hipError_t launch_grid_u32(uint32_t* hist, uint32_t* marks, uint8_t* out8, uint64_t ncells,
-                           uint32_t lifetime, hipStream_t s);
-hipError_t launch_widen_grid(const uint8_t* grid8, uint32_t* hist, uint64_t ncells, hipStream_t s);
+                           uint32_t lifetime, const GridSeq& q, hipStream_t s);
+hipError_t launch_widen_grid(const uint8_t* grid8, uint32_t* hist, uint64_t ncells,
+                             const GridSeq& q, hipStream_t s);
 
 // standalone voxel keys over the compacted points (count read on the device)
 hipError_t launch_coords(const float4* pts, const uint32_t* count, uint32_t nmax,
@@ -64,16 +66,12 @@ struct VoxelizeArgs {
     unsigned long long* gstatus;    // [group tiles] epoch granules
     unsigned long long* ggstatus;   // [group tiles / 64 + 1]
     unsigned long long* ctrs;       // [kCtrSlots] self-resetting tile tickets (low 32 bits)
-    uint32_t* epoch;                // host epoch counter (advanced per look-back launch)
     int sort_pt;                    // keys per thread of a sort tile (4, 8 or 16)
     // optional fused historic-grid update (u8 grid, lifetime <= 255), run by extra blocks of the
     // first sort pass: it only needs the occupancy marks, which the compaction already wrote
     uint8_t* grid8;
     uint32_t* marks;
-    // ordering of the fused grid update with the previous frame's (frame pipelining)
-    void (*before_grid)(void*);
-    void (*after_grid)(void*);
-    void* cb_ctx;
+    GridSeq gseq;                   // engine order of the fused grid update (frame pipelining)
     uint64_t ncells;
     uint32_t lifetime;
     uint32_t* err;
