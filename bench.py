@@ -36,6 +36,9 @@ def parse():
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--ring", type=int, default=8, help="distinct device-resident frames")
+    ap.add_argument("--cameras", type=int, default=1,
+                    help="cameras per GPU (one frame = one depth map of each; camera ids "
+                         "rank*cameras + k)")
     ap.add_argument("--pipeline", type=int, default=3,
                     help="frames in flight on one GPU (engine slots, gdf_set_pipeline_depth); "
                          "N > 1 runs on torch's stream with depth 1")
@@ -66,10 +69,12 @@ def main():
     build_library()
     hiprt.set_device(local_rank)
     W, H = args.width, args.height
-    P = W * H
-    cam = synth.make_camera(rank, W, H)
-    frames = [synth.depth_frame(cam, rank, f) for f in range(args.ring)]
-    dframes = [hiprt.DeviceArray.from_numpy(f) for f in frames]
+    K = args.cameras
+    P = W * H * K
+    cams = [synth.make_camera(rank * K + k, W, H) for k in range(K)]
+    frames = [[synth.depth_frame(c, rank * K + k, f) for f in range(args.ring)]
+              for k, c in enumerate(cams)]
+    dframes = [[hiprt.DeviceArray.from_numpy(f) for f in fr] for fr in frames]
     params = ComponentParams()
     eng = GPUDepthmapFusion(local_rank)
 
@@ -80,8 +85,9 @@ def main():
 
     def add(i):
         eng.clear()
-        eng.addDepthmapDevice(dframes[i % args.ring].ptr, W, H, *cam.intrinsics(), cam.T_world,
-                              cam.T_crop)
+        for k, c in enumerate(cams):
+            eng.addDepthmapDevice(dframes[k][i % args.ring].ptr, W, H, *c.intrinsics(), c.T_world,
+                                  c.T_crop)
 
     # per-frame point counts (for the algorithmic byte model), one synchronous pass over the ring
     npts, nvox = [], []
@@ -103,12 +109,17 @@ def main():
     pc_plain = params.to_c(None, None, False, False)
     pc_defer = params.to_c(None, None, False, True)
 
-    def step(i):
-        add(i)
+    # the component's per-frame loop runs in C++ (gdf_run_depth_stream: clear + addDepthmapDevice
+    # + gdf_process_frame per frame), as the ROS component would drive the engine
+    scam = [eng.make_stream_camera([d.ptr for d in dframes[k]], W, H, *c.intrinsics(),
+                                   c.T_world, c.T_crop) for k, c in enumerate(cams)]
+
+    def run(first, count):
         if dist is None:
-            eng.processFramePrepared(pc_plain)
-        else:
-            eng.processFramePrepared(pc_defer)
+            eng.run_depth_stream(scam, pc_plain, first, count)
+            return
+        for i in range(first, first + count):
+            eng.run_depth_stream(scam, pc_defer, i, 1)
             marks.exchange()  # occupancy union over RCCL (multi.py)
             eng.voxelOccupancyGrid(params.occupancy_lifetime)
 
@@ -119,12 +130,10 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
 
-    for i in range(args.warmup):
-        step(i)
+    run(0, args.warmup)
     barrier_sync()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i)
+    run(args.warmup, args.steps)
     barrier_sync()
     t1 = time.perf_counter()
     elapsed = t1 - t0
@@ -142,8 +151,7 @@ def main():
         if dist is None:
             eng.set_pipeline_depth(1)  # one frame in flight: launch durations without overlap
         eng.set_profiling(True)
-        for i in range(kt_steps):
-            step(args.warmup + i)
+        run(args.warmup, kt_steps)
         barrier_sync()
         ktimes = eng.kernel_times()
         eng.set_profiling(False)
@@ -216,12 +224,15 @@ def main():
         done, t_cpu = 0, 0.0
         for i in range(2):  # warm-up
             orc.clear()
-            orc.addDepthmap(frames[i % args.ring], *cam.intrinsics(), cam.T_world, cam.T_crop)
+            for k, c in enumerate(cams):
+                orc.addDepthmap(frames[k][i % args.ring], *c.intrinsics(), c.T_world, c.T_crop)
             orc.processFrame(params)
         tc0 = time.perf_counter()
         while True:
             orc.clear()
-            orc.addDepthmap(frames[done % args.ring], *cam.intrinsics(), cam.T_world, cam.T_crop)
+            for k, c in enumerate(cams):
+                orc.addDepthmap(frames[k][done % args.ring], *c.intrinsics(), c.T_world,
+                                c.T_crop)
             orc.processFrame(params)
             done += 1
             t_cpu = time.perf_counter() - tc0
@@ -244,7 +255,7 @@ def main():
                                    "(F=4 thr 0.3, crop/voxel -10..30/-20..20/-1..1.5, "
                                    "cells 0.1/0.1/0.12 -> %dx%dx%d, voxelize average, "
                                    "lifetime 10)" % (W, H, gx, gy, gz),
-                       "cameras_per_gpu": 1, "points_per_frame_after_crop": round(n_avg),
+                       "cameras_per_gpu": K, "points_per_frame_after_crop": round(n_avg),
                        "voxels_per_frame": round(g_avg), "grid_cells": ncells,
                        "frames_in_flight": depth,
                        "parallelism": "camera-per-GPU x%d, occupancy-mark all-gather" % world

@@ -18,6 +18,11 @@ constexpr int kHalo = 8;              // band rows/columns staged around a segme
 constexpr uint32_t kSegItems = 1024;  // items per compaction segment (max)
 constexpr uint32_t kFusedPrefixSegs = 4096;  // up to this many segments k_emit sums the counts
 constexpr int kSortThreads = 256;
+// the voxel-key digit histogram is accumulated into kHistReps replicas of [4 passes][256 digits]
+// (block b adds into replica b % kHistReps): same-address atomics from hundreds of blocks
+// serialise at the memory-side atomic unit; the sort pass sums the replicas of its digit
+constexpr int kHistReps = 16;
+constexpr int kHistWords = kHistReps * 4 * 256;
 constexpr int kGroupThreads = 256;
 constexpr int kSumChunk = 256;                               // points per wave gather chunk
 constexpr uint32_t kSpinLimit = 1u << 26;                   // bounded look-back spins

@@ -750,7 +750,7 @@ void ensure_misc(gdf_engine* e) {
         HIPCHK(hipMemsetAsync(e->sl().d_misc.p, 0, kMiscWords * 4, e->s()));
     }
     if (!e->sl().d_ctrs.p) e->sl().d_ctrs.ensure_zero(kCtrSlots * 8, e->s());
-    if (!e->sl().d_khist.p) e->sl().d_khist.ensure_zero(4 * 256 * 4, e->s());
+    if (!e->sl().d_khist.p) e->sl().d_khist.ensure_zero(kHistWords * 4, e->s());
 }
 
 // The fused compaction launch: convert + flying + crop + selected-point transform + ordered
@@ -801,7 +801,7 @@ void run_frame(gdf_engine* e, bool fused_voxel) {
         std::memcpy(a.vcs, e->vp.vcs, 12);
         std::memcpy(a.gmax, e->vp.gmax, 12);
         std::memcpy(a.gs, e->vp.gs, 12);
-        if (e->sl().khist_pending) HIPCHK(hipMemsetAsync(e->sl().d_khist.p, 0, 4 * 256 * 4, e->s()));
+        if (e->sl().khist_pending) HIPCHK(hipMemsetAsync(e->sl().d_khist.p, 0, kHistWords * 4, e->s()));
         a.key_hist = e->sl().d_khist.as<uint32_t>();
         a.npasses = e->key_bits == 0 ? 1u : (e->key_bits + 7) / 8;
     }

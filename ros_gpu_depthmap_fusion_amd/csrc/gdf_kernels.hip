@@ -798,9 +798,10 @@ __global__ __launch_bounds__(1024) void k_emit(FrameArgs a) {
     }
     if (a.key_hist) {
         __syncthreads();
+        const gptr<uint32_t> rep = G(a.key_hist + (blockIdx.x % kHistReps) * 1024u);
         for (uint32_t j = threadIdx.x; j < a.npasses * 256; j += blockDim.x)
             if (s_hist[j])
-                __hip_atomic_fetch_add(G(a.key_hist + j), s_hist[j], __ATOMIC_RELAXED,
+                __hip_atomic_fetch_add(rep + j, s_hist[j], __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
     }
 }
@@ -1105,16 +1106,19 @@ __global__ __launch_bounds__(256) void k_sort_hist(const uint32_t* __restrict__ 
         for (uint32_t p = 0; p < npasses; ++p) atomicAdd(&s_h[p * 256 + ((k >> (8 * p)) & 0xFFu)], 1u);
     }
     __syncthreads();
+    uint32_t* rep = hist + (blockIdx.x % kHistReps) * 1024u;
     for (uint32_t i = threadIdx.x; i < npasses * 256; i += 256)
-        if (s_h[i]) atomicAdd(&hist[i], s_h[i]);
+        if (s_h[i]) atomicAdd(&rep[i], s_h[i]);
 }
 
-// Exclusive scan of the 256-entry global digit histogram (4 waves x 64 digits), thread d gets
-// the base of digit d.
+// Exclusive scan of the 256-entry global digit histogram (4 waves x 64 digits; the sum of the
+// kHistReps replicas), thread d gets the base of digit d.
 __device__ __forceinline__ uint32_t digit_base(const uint32_t* ghist, uint32_t* s_wave) {
     const uint32_t d = threadIdx.x;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint32_t v = ghist[d];
+    uint32_t v = 0;
+#pragma unroll
+    for (int r = 0; r < kHistReps; ++r) v += ghist[r * 1024 + d];
     uint32_t total;
     (void)lane;
     (void)wid;
@@ -1252,7 +1256,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_group(
     const uint32_t n = *count;
     const uint32_t ntiles = (n + kGroupThreads - 1) / kGroupThreads;
     if (blockIdx.x == 0)
-        for (uint32_t i = threadIdx.x; i < 4 * 256; i += kGroupThreads) hist[i] = 0;
+        for (uint32_t i = threadIdx.x; i < kHistWords; i += kGroupThreads) hist[i] = 0;
     if (blockIdx.x >= ntiles) {
         if (blockIdx.x == 0 && threadIdx.x == 0) *out_count = 0;  // n == 0
         return;

@@ -60,7 +60,7 @@ struct VoxelizeArgs {
     VoxelParams vp;
     // workspace
     uint32_t *keys_a, *keys_b, *vals_a, *vals_b;
-    uint32_t* hist;                 // [4*256] zero on entry, left zero on exit
+    uint32_t* hist;                 // [kHistReps][4*256] zero on entry, left zero on exit
     unsigned long long* status;     // [sort tiles * 256] epoch granules
     unsigned long long* sgstatus;   // [sort tile groups * 256]
     unsigned long long* gstatus;    // [group tiles] epoch granules

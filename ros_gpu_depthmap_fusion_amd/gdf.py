@@ -57,6 +57,15 @@ KERNEL_SLOTS = ("frame", "grid", "voxelize", "ps_insert", "mask", "scan", "emit"
                 "group", "reserved9", "event_floor")
 
 
+class StreamCamera(C.Structure):
+    """gdf_stream_camera (include/gdf_driver.h)."""
+    _fields_ = [
+        ("frames", C.POINTER(C.c_void_p)), ("ring", C.c_uint32), ("width", C.c_uint32),
+        ("height", C.c_uint32), ("depth_scale", C.c_float), ("fx", C.c_float), ("fy", C.c_float),
+        ("cx", C.c_float), ("cy", C.c_float), ("T_world", _f16), ("T_crop", _f16),
+    ]
+
+
 class FrameResult(C.Structure):
     _fields_ = [("processed", C.c_int32), ("num_depth_points", C.c_uint32),
                 ("num_points_total", C.c_uint32), ("num_points", C.c_uint32),
@@ -87,6 +96,8 @@ EXPORTED = [
     "gdf_get_device_results", "gdf_process_frame", "gdf_export_occupancy_marks",
     "gdf_import_occupancy_marks", "gdf_set_profiling", "gdf_get_kernel_times", "gdf_set_debug", "gdf_debug_stage_masks", "gdf_debug_rollbuffer",
     "gdf_debug_historic_grid",
+    # include/gdf_driver.h: the component's depth loop in C++ over the C-ABI
+    "gdf_run_depth_stream",
 ]
 
 
@@ -147,6 +158,7 @@ def load_library(path: str = LIB_PATH):
         "gdf_debug_stage_masks": (i32, [vp, vp, u32, P(u32)]),
         "gdf_debug_rollbuffer": (i32, [vp, vp, vp, vp, u32, vp, u32]),
         "gdf_debug_historic_grid": (i32, [vp, vp, u64]),
+        "gdf_run_depth_stream": (i32, [vp, P(StreamCamera), u32, P(FrameParams), u64, u64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -461,6 +473,28 @@ class GPUDepthmapFusion:
                      synchronous: bool = True, defer_occupancy_grid: bool = False) -> FrameResult:
         p = params.to_c(T_world_move, T_crop_move, synchronous, defer_occupancy_grid)
         return self.processFramePrepared(p)
+
+    def make_stream_camera(self, dev_ptrs: Sequence[int], width: int, height: int,
+                           depthScale: float, fx: float, fy: float, cx: float, cy: float,
+                           T_world, T_crop) -> StreamCamera:
+        """A camera of gdf_run_depth_stream: a ring of device depth maps + its geometry."""
+        c = StreamCamera()
+        arr = (C.c_void_p * len(dev_ptrs))(*dev_ptrs)
+        c.frames = C.cast(arr, C.POINTER(C.c_void_p))
+        c._frames_keepalive = arr
+        c.ring, c.width, c.height = len(dev_ptrs), width, height
+        c.depth_scale, c.fx, c.fy, c.cx, c.cy = depthScale, fx, fy, cx, cy
+        c.T_world[:] = _mat(T_world).ravel().tolist()
+        c.T_crop[:] = _mat(T_crop).ravel().tolist()
+        return c
+
+    def run_depth_stream(self, cameras: Sequence[StreamCamera], p: FrameParams, first: int,
+                         count: int):
+        """Frames first..first+count-1 through the C++ component loop (gdf_run_depth_stream):
+        clear + addDepthmapDevice per camera + processFrame, without Python per frame."""
+        arr = (StreamCamera * len(cameras))(*cameras)
+        self._check(self._lib.gdf_run_depth_stream(self._h, arr, len(cameras), C.byref(p),
+                                                   first, count))
 
     def processFramePrepared(self, p: FrameParams) -> FrameResult:
         """processFrame with parameters already converted by ComponentParams.to_c (a stream of

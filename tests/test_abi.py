@@ -1,4 +1,4 @@
-"""The C-ABI library builds, loads without a GPU, and exports every symbol of include/gdf.h."""
+"""The C-ABI library builds, loads without a GPU, and exports every symbol of include/*.h."""
 import os
 import re
 import subprocess
@@ -7,8 +7,13 @@ from conftest import ROOT
 
 
 def header_symbols():
-    txt = open(os.path.join(ROOT, "include", "gdf.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(gdf_\w+)\s*\(", txt, re.M)))
+    """Every function declared by the C headers in include/ (gdf.h, gdf_driver.h)."""
+    syms = set()
+    for h in sorted(os.listdir(os.path.join(ROOT, "include"))):
+        if h.endswith(".h"):
+            txt = open(os.path.join(ROOT, "include", h)).read()
+            syms |= set(re.findall(r"^\s*(?:int|const char\*)\s+(gdf_\w+)\s*\(", txt, re.M))
+    return sorted(syms)
 
 
 def test_library_exports_every_header_symbol():

@@ -395,3 +395,26 @@ def test_pipelined_frames_match_sequential(Engine):
         np.testing.assert_array_equal(bits(a) if a.dtype == np.float32 else a,
                                       bits(b) if b.dtype == np.float32 else b)
     np.testing.assert_array_equal(seq.historic_grid(), pipe.historic_grid())
+
+
+def test_cpp_stream_loop_matches_oracle(Engine):
+    """gdf_run_depth_stream (the component loop in C++, include/gdf_driver.h) over a ring of
+    device depth maps of two cameras, pipelined 3 deep, ends in the oracle's grid and last-frame
+    outputs; the ring index wraps."""
+    from ros_gpu_depthmap_fusion_amd import hiprt
+    p = ComponentParams()
+    cams = synth.cameras(2, 160, 120)
+    ring = 5
+    host = [[synth.depth_frame(c, k, f) for f in range(ring)] for k, c in enumerate(cams)]
+    dev = [[hiprt.DeviceArray.from_numpy(d) for d in h] for h in host]
+    gpu, orc = Engine(), OracleFusion(threads=4)
+    gpu.set_pipeline_depth(3)
+    scams = [gpu.make_stream_camera([d.ptr for d in dev[k]], c.width, c.height, *c.intrinsics(),
+                                    c.T_world, c.T_crop) for k, c in enumerate(cams)]
+    nframes = 13
+    gpu.run_depth_stream(scams, p.to_c(None, None, False, False), 0, nframes)
+    gpu.synchronize()
+    for f in range(nframes):
+        run_fused(orc, [cam_args(c, host[k][f % ring]) for k, c in enumerate(cams)], p)
+    compare_results(gpu, orc, tag="stream")
+    np.testing.assert_array_equal(gpu.historic_grid(), orc.historic_grid())
