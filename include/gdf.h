@@ -123,6 +123,12 @@ int gdf_synchronize(gdf_engine* engine);
  * frame are read (downloads, gdf_get_device_results) before the next gdf_clear.  Call between
  * frames; not available with gdf_set_stream. */
 int gdf_set_pipeline_depth(gdf_engine* engine, int depth);
+/* Steady-state frames of gdf_process_frame as HIP graphs (default on; env GDF_NO_GRAPHS turns
+ * the default off): when a slot's frame repeats the launch arguments of its previous frame (all
+ * but the depth pointers and the grid ticket) the frame's launches are captured once and then
+ * replayed - one graph launch per frame instead of six kernel launches.  Results are identical;
+ * not used while profiling, with stage-mask debugging, gdf_set_stream or more than 4 cameras. */
+int gdf_set_graphs(gdf_engine* engine, int enable);
 /* voxel_group_size parameter (component.cpp:1149); kept for interface parity, it only tuned
  * the reference's CPU radix sort and does not change results. */
 int gdf_set_voxel_group_size(gdf_engine* engine, int group_size);

@@ -183,6 +183,29 @@ struct Slot {
     DevBuf d_markbits;              // this frame's occupancy marks (1 bit per cell)
     uint32_t marks_gen = ~0u;
     uint32_t n_total = 0;
+    // steady-state frame as a HIP graph (the fused frame + voxelize launches of this slot): one
+    // graph launch and two kernel-node argument updates (depth pointers, grid ticket) per frame
+    // instead of six direct launches.  Replayed while the frame's launch arguments - minus those
+    // two fields - stay what they were at capture; captured once they repeat on two frames.
+    struct Graph {
+        hipGraph_t g = nullptr;
+        hipGraphExec_t x = nullptr;
+        hipGraphNode_t n_mask = nullptr, n_emit = nullptr;
+        hipKernelNodeParams p_mask{}, p_emit{};
+        FrameArgs key_a;
+        VoxelizeArgs key_v;
+        bool valid = false;
+        FrameArgs cand_a;
+        VoxelizeArgs cand_v;
+        bool cand = false;
+        void reset() {
+            if (x) (void)hipGraphExecDestroy(x);
+            if (g) (void)hipGraphDestroy(g);
+            x = nullptr;
+            g = nullptr;
+            valid = cand = false;
+        }
+    } graph;
 };
 
 struct gdf_engine {
@@ -241,6 +264,7 @@ struct gdf_engine {
     float lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
 
     int sort_pt = 4;
+    bool use_graphs = !getenv("GDF_NO_GRAPHS");  // gdf_set_graphs
 
     // compaction outputs
 
@@ -753,13 +777,14 @@ void ensure_misc(gdf_engine* e) {
     if (!e->sl().d_khist.p) e->sl().d_khist.ensure_zero(kHistWords * 4, e->s());
 }
 
-// The fused compaction launch: convert + flying + crop + selected-point transform + ordered
-// compaction (+ voxel keys and occupancy marks when fused_voxel).
-void run_frame(gdf_engine* e, bool fused_voxel) {
+// Arguments of the fused compaction launch: convert + flying + crop + selected-point transform +
+// ordered compaction (+ voxel keys and occupancy marks when fused_voxel).
+FrameArgs frame_args(gdf_engine* e, bool fused_voxel) {
     if (!e->prepared) prepare_buffers(e);
     if (!e->depth_uploaded) upload_depthmaps(e);
     ensure_misc(e);
-    FrameArgs a{};
+    FrameArgs a;
+    std::memset(&a, 0, sizeof(a));  // padding too: graph keys compare the bytes
     a.ncams = (int32_t)e->h_cams.size();
     if (a.ncams <= kArgCams) {
         for (size_t k = 0; k < e->h_cams.size(); ++k) a.cams[k] = e->h_cams[k];
@@ -830,13 +855,22 @@ void run_frame(gdf_engine* e, bool fused_voxel) {
     }
     e->sl().dbg_count = e->sl().n_total;
     a.err = e->sl().d_misc.as<uint32_t>() + kErr;
-    if (e->profiling) e->timed(GDF_KERNEL_EVENT_FLOOR, [] {});  // calibrates the event overhead
-    e->timed(GDF_KERNEL_FRAME, [&] { HIPCHK(launch_frame(a, e->s(), e->hook_ptr())); });
+    return a;
+}
+
+void frame_launched(gdf_engine* e, bool fused_voxel) {
     e->sl().khist_pending = fused_voxel;
     e->sl().compacted = true;
     e->sl().coords_valid = fused_voxel;
     e->sl().marks_set = fused_voxel;
     e->sl().vox_valid = false;
+}
+
+void run_frame(gdf_engine* e, bool fused_voxel) {
+    const FrameArgs a = frame_args(e, fused_voxel);
+    if (e->profiling) e->timed(GDF_KERNEL_EVENT_FLOOR, [] {});  // calibrates the event overhead
+    e->timed(GDF_KERNEL_FRAME, [&] { HIPCHK(launch_frame(a, e->s(), e->hook_ptr())); });
+    frame_launched(e, fused_voxel);
 }
 
 void compute_voxel_coords(gdf_engine* e, const float* lo, const float* hi, const float* cs) {
@@ -848,7 +882,7 @@ void compute_voxel_coords(gdf_engine* e, const float* lo, const float* hi, const
     e->sl().marks_set = false;
 }
 
-void voxelize(gdf_engine* e, int average, int fused_grid_lifetime = -1) {  // fusion.cpp:1743-1756
+VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime) {  // fusion.cpp:1743-1756
     if (!e->grid_set || !e->sl().coords_valid) fail(GDF_ERR_STATE, "voxelize before computeVoxelCoords");
     const uint32_t nmax = std::max<uint32_t>(e->sl().n_total, 1);
     if (nmax >= (1u << 31)) fail(GDF_ERR_CAPACITY, "voxelize supports < 2^31 points");
@@ -862,7 +896,8 @@ void voxelize(gdf_engine* e, int average, int fused_grid_lifetime = -1) {  // fu
     e->sl().d_gstatus.ensure_zero(voxelize_group_tiles(nmax) * 8, e->s());
     e->sl().d_ggstatus.ensure_zero((voxelize_group_tiles(nmax) / 64 + 2) * 8, e->s());
     e->sl().d_vox.ensure((size_t)nmax * 16);
-    VoxelizeArgs v{};
+    VoxelizeArgs v;
+    std::memset(&v, 0, sizeof(v));
     v.keys = e->sl().d_coords.as<uint32_t>();
     v.pts = e->sl().d_pts.as<float4>();
     v.count = e->sl().d_misc.as<uint32_t>() + kCount;
@@ -894,13 +929,99 @@ void voxelize(gdf_engine* e, int average, int fused_grid_lifetime = -1) {  // fu
         v.gseq = e->grid_seq(0, e->sl().d_misc.as<uint32_t>() + kGridTicket);
         e->grid_ticket++;
     }
-    e->timed(GDF_KERNEL_VOXELIZE, [&] { HIPCHK(launch_voxelize(v, e->s(), e->hook_ptr())); });
+    return v;
+}
+
+void voxelize_launched(gdf_engine* e, int fused_grid_lifetime) {
     if (fused_grid_lifetime >= 0) {
         e->sl().marks_set = false;
         e->invoked_once = true;
     }
     e->sl().khist_pending = false;
     e->sl().vox_valid = true;
+}
+
+void voxelize(gdf_engine* e, int average, int fused_grid_lifetime = -1) {
+    const VoxelizeArgs v = voxelize_args(e, average, fused_grid_lifetime);
+    e->timed(GDF_KERNEL_VOXELIZE, [&] { HIPCHK(launch_voxelize(v, e->s(), e->hook_ptr())); });
+    voxelize_launched(e, fused_grid_lifetime);
+}
+
+// graph key: the launch arguments without the per-frame fields (depth pointers, grid ticket)
+void graph_key(const FrameArgs& a, FrameArgs& k) {
+    k = a;
+    for (int c = 0; c < kArgCams; ++c) k.cams[c].depth = nullptr;
+    k.grid_seq = 0;
+}
+
+bool same_key(const FrameArgs& a, const VoxelizeArgs& v, const FrameArgs& ka, const VoxelizeArgs& kv) {
+    FrameArgs k;
+    graph_key(a, k);
+    return std::memcmp(&k, &ka, sizeof(k)) == 0 && std::memcmp(&v, &kv, sizeof(v)) == 0;
+}
+
+// processFrame's fused frame (compaction + voxelize + grid update) on the slot's stream:
+// direct launches, or the slot's captured graph when the launch arguments repeat
+void run_fused_frame(gdf_engine* e, int average, uint32_t lifetime) {
+    const FrameArgs a = frame_args(e, true);
+    frame_launched(e, true);  // (the launches below follow; voxelize_args checks this state)
+    const VoxelizeArgs v = voxelize_args(e, average, (int)lifetime);
+    Slot::Graph& G = e->sl().graph;
+    const bool eligible = e->use_graphs && !e->profiling && !e->debug && a.ncams <= kArgCams &&
+                          !e->user_stream;
+    hipStream_t st = e->s();
+    if (eligible && G.valid && same_key(a, v, G.key_a, G.key_v)) {
+        void* args[] = {const_cast<FrameArgs*>(&a)};
+        hipKernelNodeParams pm = G.p_mask, pe = G.p_emit;
+        pm.kernelParams = args;
+        pe.kernelParams = args;
+        HIPCHK(hipGraphExecKernelNodeSetParams(G.x, G.n_mask, &pm));
+        HIPCHK(hipGraphExecKernelNodeSetParams(G.x, G.n_emit, &pe));
+        HIPCHK(hipGraphLaunch(G.x, st));
+    } else if (eligible && G.cand && same_key(a, v, G.cand_a, G.cand_v)) {
+        // the arguments repeated: capture this frame's launches and replay from now on
+        if (G.x) HIPCHK(hipStreamSynchronize(st));  // no launch of the old graph in flight
+        G.reset();
+        HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+        hipError_t e1 = launch_frame(a, st, nullptr);
+        hipError_t e2 = e1 == hipSuccess ? launch_voxelize(v, st, nullptr) : e1;
+        hipGraph_t g = nullptr;
+        hipError_t e3 = hipStreamEndCapture(st, &g);
+        HIPCHK(e2);
+        HIPCHK(e3);
+        G.g = g;
+        HIPCHK(hipGraphInstantiate(&G.x, G.g, nullptr, nullptr, 0));
+        size_t nn = 0;
+        HIPCHK(hipGraphGetNodes(G.g, nullptr, &nn));
+        std::vector<hipGraphNode_t> nodes(nn);
+        HIPCHK(hipGraphGetNodes(G.g, nodes.data(), &nn));
+        const void* fm = frame_kernel(0, a.rot45);
+        const void* fe = frame_kernel(1, a.rot45);
+        for (hipGraphNode_t n : nodes) {
+            hipGraphNodeType t;
+            HIPCHK(hipGraphNodeGetType(n, &t));
+            if (t != hipGraphNodeTypeKernel) continue;
+            hipKernelNodeParams kp{};
+            HIPCHK(hipGraphKernelNodeGetParams(n, &kp));
+            if (kp.func == fm) { G.n_mask = n; G.p_mask = kp; }
+            if (kp.func == fe) { G.n_emit = n; G.p_emit = kp; }
+        }
+        if (!G.n_mask || !G.n_emit) fail(GDF_ERR_HIP, "frame graph: compaction kernels not found");
+        graph_key(a, G.key_a);
+        G.key_v = v;
+        G.valid = true;
+        HIPCHK(hipGraphLaunch(G.x, st));
+    } else {
+        if (eligible) {
+            graph_key(a, G.cand_a);
+            G.cand_v = v;
+            G.cand = true;
+        }
+        if (e->profiling) e->timed(GDF_KERNEL_EVENT_FLOOR, [] {});
+        e->timed(GDF_KERNEL_FRAME, [&] { HIPCHK(launch_frame(a, st, e->hook_ptr())); });
+        e->timed(GDF_KERNEL_VOXELIZE, [&] { HIPCHK(launch_voxelize(v, st, e->hook_ptr())); });
+    }
+    voxelize_launched(e, (int)lifetime);
 }
 
 void occupancy_grid(gdf_engine* e, uint32_t lifetime, hipStream_t st) {  // fusion.cpp:1757-1823
@@ -1002,6 +1123,7 @@ int gdf_destroy(gdf_engine* e) {
     }
     for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
     for (Slot& sl : e->slots) {
+        sl.graph.reset();
         if (sl.h_misc) (void)hipHostFree(sl.h_misc);
         if (sl.own) (void)hipStreamDestroy(sl.own);
     }
@@ -1048,6 +1170,17 @@ int gdf_set_pipeline_depth(gdf_engine* e, int depth) {
         }
         e->npipe = depth;
         e->serialized = false;
+    });
+}
+
+int gdf_set_graphs(gdf_engine* e, int enable) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        e->use_graphs = enable != 0;
+        if (!e->use_graphs) {
+            sync_all(e);
+            for (Slot& sl : e->slots) sl.graph.reset();
+        }
     });
 }
 
@@ -1341,10 +1474,10 @@ int gdf_process_frame(gdf_engine* e, const gdf_frame_params* p, gdf_frame_result
         if (p->enable_voxel_filter) {
             set_grid(e, p->voxel_min, p->voxel_max, p->voxel_size);
             widen_if_needed(e, p->occupancy_lifetime, e->s());  // before marks are consumed
-            run_frame(e, true);
             if (!p->defer_occupancy_grid && e->grid_mode == 0) {
-                voxelize(e, p->voxel_average, (int)p->occupancy_lifetime);
+                run_fused_frame(e, p->voxel_average, p->occupancy_lifetime);
             } else {
+                run_frame(e, true);
                 voxelize(e, p->voxel_average);
                 if (!p->defer_occupancy_grid) occupancy_grid(e, p->occupancy_lifetime, e->s());
             }

@@ -841,6 +841,12 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
     return hipGetLastError();
 }
 
+const void* frame_kernel(int which, int rot45) {
+    if (which == 1) return reinterpret_cast<const void*>(&k_emit);
+    return rot45 ? reinterpret_cast<const void*>(&k_mask<true>)
+                 : reinterpret_cast<const void*>(&k_mask<false>);
+}
+
 // per-camera ray factors (sh/convert_depthmap_to_points.glsl:68-69), one f32 division each
 __global__ __launch_bounds__(256) void k_tables(uint32_t W, uint32_t H, float fx, float fy,
                                                 float cx, float cy, float* __restrict__ xn,

@@ -25,11 +25,16 @@ hipError_t launch_tables(uint32_t W, uint32_t H, float fx, float fy, float cx, f
 // fused depth + rollbuffer compaction (convert, flying, crop, transform_indirect, apply,
 // optional voxel keys + occupancy marks); needs no memset (epoch-tagged look-back, tickets)
 hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook = nullptr);
+// the compaction kernels (0: k_mask, 1: k_emit) as launched for `rot45` (graph node lookup)
+const void* frame_kernel(int which, int rot45);
 
 // filter_point_sequence + insert into the rollbuffer ring (w = mask)
 hipError_t launch_ps_filter_insert(const float4* new_pts, uint32_t n, int do_filter, float thr,
                                    uint32_t F, float4* ring, uint64_t cap, uint64_t first,
                                    hipStream_t s);
+// device-resident PointCloud2 records (x, y, z at byte offsets 0/4/8, step % 4 == 0) -> float4 w=1
+hipError_t launch_gather_records(const void* rec, uint32_t n, uint32_t step, float4* out,
+                                 hipStream_t s);
 
 // historic grid update from the frame's mark bitmask (cleared on the way): u8 grid = history for
 // lifetime <= 255; the general u32 history with a separate u8 output grid beyond

@@ -84,7 +84,7 @@ _lib = None
 # every symbol declared in include/gdf.h (checked by tests/test_abi.py)
 EXPORTED = [
     "gdf_create", "gdf_destroy", "gdf_last_error", "gdf_version", "gdf_set_stream",
-    "gdf_synchronize", "gdf_set_pipeline_depth", "gdf_set_voxel_group_size", "gdf_clear", "gdf_add_depthmap",
+    "gdf_synchronize", "gdf_set_pipeline_depth", "gdf_set_graphs", "gdf_set_voxel_group_size", "gdf_clear", "gdf_add_depthmap",
     "gdf_add_depthmap_device", "gdf_add_point_sequence", "gdf_num_collected_point_sequence_points",
     "gdf_upload_point_sequences", "gdf_filter_new_point_sequences", "gdf_insert_new_point_sequences",
     "gdf_roll_rollbuffer", "gdf_select_timespan", "gdf_prepare_point_and_mask_buffers",
@@ -119,6 +119,7 @@ def load_library(path: str = LIB_PATH):
         "gdf_set_stream": (i32, [vp, vp]),
         "gdf_synchronize": (i32, [vp]),
         "gdf_set_pipeline_depth": (i32, [vp, i32]),
+        "gdf_set_graphs": (i32, [vp, i32]),
         "gdf_set_voxel_group_size": (i32, [vp, i32]),
         "gdf_clear": (i32, [vp]),
         "gdf_add_depthmap": (i32, [vp, vp, u32, u32, f, f, f, f, f, vp, vp]),
@@ -271,6 +272,10 @@ class GPUDepthmapFusion:
     def set_pipeline_depth(self, depth: int):
         """Frames in flight (1..4): clear() starts the next frame on the next slot."""
         self._check(self._lib.gdf_set_pipeline_depth(self._h, depth))
+
+    def set_graphs(self, on: bool = True):
+        """Replay steady-state frames from HIP graphs (default on)."""
+        self._check(self._lib.gdf_set_graphs(self._h, 1 if on else 0))
 
     def synchronize(self):
         self._check(self._lib.gdf_synchronize(self._h))

@@ -418,3 +418,53 @@ def test_cpp_stream_loop_matches_oracle(Engine):
         run_fused(orc, [cam_args(c, host[k][f % ring]) for k, c in enumerate(cams)], p)
     compare_results(gpu, orc, tag="stream")
     np.testing.assert_array_equal(gpu.historic_grid(), orc.historic_grid())
+
+
+def test_graph_replay_matches_direct_launches(Engine):
+    """Steady-state frames replayed from HIP graphs (kernel-node updates of the depth pointers
+    and the grid ticket) give the direct launches' outputs frame by frame: device depth maps of
+    two cameras from a ring (a new pointer every frame), 3 slots; then an asynchronous stretch
+    with a parameter change (recapture) ends in the same grid, checked against the oracle too."""
+    from ros_gpu_depthmap_fusion_amd import hiprt
+    p = ComponentParams()
+    cams = synth.cameras(2, 160, 120)
+    ring = 7
+    host = [[synth.depth_frame(c, k, f) for f in range(ring)] for k, c in enumerate(cams)]
+    dev = [[hiprt.DeviceArray.from_numpy(d) for d in h] for h in host]
+    direct, graph = Engine(), Engine()
+    direct.set_graphs(False)
+    graph.set_graphs(True)
+    for e in (direct, graph):
+        e.set_pipeline_depth(3)
+
+    def frame(e, f, **kw):
+        e.clear()
+        for k, c in enumerate(cams):
+            e.addDepthmapDevice(dev[k][f % ring].ptr, c.width, c.height, *c.intrinsics(),
+                                c.T_world, c.T_crop)
+        return e.processFrame(p, **kw)
+
+    for f in range(12):
+        for e in (direct, graph):
+            frame(e, f, synchronous=True)
+        for a, b in zip(_gpu_outputs(direct), _gpu_outputs(graph)):
+            np.testing.assert_array_equal(bits(a) if a.dtype == np.float32 else a,
+                                          bits(b) if b.dtype == np.float32 else b,
+                                          err_msg=f"frame {f}")
+    orc = OracleFusion(threads=4)
+    for f in range(12):
+        run_fused(orc, [cam_args(c, host[k][f % ring]) for k, c in enumerate(cams)], p)
+    for f in range(12, 40):
+        if f == 25:
+            p.flying_threshold = 0.4
+            p.voxel_average = False
+        for e in (direct, graph):
+            frame(e, f, synchronous=False)
+        run_fused(orc, [cam_args(c, host[k][f % ring]) for k, c in enumerate(cams)], p)
+    direct.synchronize()
+    graph.synchronize()
+    for a, b in zip(_gpu_outputs(direct), _gpu_outputs(graph)):
+        np.testing.assert_array_equal(bits(a) if a.dtype == np.float32 else a,
+                                      bits(b) if b.dtype == np.float32 else b)
+    np.testing.assert_array_equal(graph.historic_grid(), orc.historic_grid())
+    compare_results(graph, orc, tag="graph")
