@@ -152,6 +152,13 @@ int gdf_add_depthmap_device(gdf_engine* engine, const uint16_t* depth_device, ui
 int gdf_add_point_sequence(gdf_engine* engine, const void* records, uint32_t num_points,
                            uint32_t point_step, uint32_t time_sec, uint32_t time_nsec,
                            const float T_move[16]);
+/* Same, for PointCloud2 records already resident in device memory of this engine's GPU
+ * (point_step a multiple of 4, records 4-byte aligned): borrowed like gdf_add_depthmap's pointer,
+ * valid until the next gdf_upload_point_sequences / gdf_process_frame, which gathers x,y,z on the
+ * device (no host copy, no PCIe). */
+int gdf_add_point_sequence_device(gdf_engine* engine, const void* records_device,
+                                  uint32_t num_points, uint32_t point_step, uint32_t time_sec,
+                                  uint32_t time_nsec, const float T_move[16]);
 /* numCollectedPointSequencePoints() (gpu_depthmap_fusion.h:356). */
 int gdf_num_collected_point_sequence_points(gdf_engine* engine, uint32_t* out_count);
 

@@ -94,14 +94,35 @@ struct Hdr {  // PointSequence, gpu_depthmap_fusion.h:178-204
     float T[16];
 };
 
+// Where the points of collected sequences come from: a run of `n` points at collect offset `dst`,
+// either host xyzw at pts[4*hsrc] (copied at add time) or borrowed device records (`dev`, `step`).
+struct PsRun {
+    uint32_t dst = 0, n = 0, step = 0;
+    const void* dev = nullptr;
+    size_t hsrc = 0;
+};
+
 struct PsBuf {  // PointSequences, gpu_depthmap_fusion.h:206-217
     uint32_t total = 0;
+    size_t host_total = 0;
     std::vector<Hdr> seqs;
     std::vector<float> pts;
+    std::vector<PsRun> runs;
     void clear() {
         total = 0;
+        host_total = 0;
         seqs.clear();
         pts.clear();
+        runs.clear();
+    }
+    void add_run(const PsRun& r) {
+        if (!r.n) return;
+        if (!r.dev && !runs.empty() && !runs.back().dev && runs.back().dst + runs.back().n == r.dst &&
+            runs.back().hsrc + runs.back().n == r.hsrc) {
+            runs.back().n += r.n;  // contiguous host points: one copy
+            return;
+        }
+        runs.push_back(r);
     }
 };
 
@@ -263,7 +284,7 @@ struct gdf_engine {
     int rot45 = 0;
     float lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
 
-    int sort_pt = 4;
+    int sort_pt = 0;  // radix keys per thread (4, 8, 16); 0: chosen by frame capacity
     bool use_graphs = !getenv("GDF_NO_GRAPHS");  // gdf_set_graphs
 
     // compaction outputs
@@ -450,18 +471,47 @@ void add_point_sequence(gdf_engine* e, const void* rec, uint32_t n, uint32_t ste
     if ((n && (!rec || step < 12)) || !Tm) fail(GDF_ERR_ARG, "addPointSequence: bad argument");
     std::lock_guard<std::mutex> lk(e->ps_mutex);
     PsBuf* b = e->collect;
+    if ((uint64_t)b->total + n > 0xFFFFFFFFull) fail(GDF_ERR_CAPACITY, "addPointSequence: too many points");
     Hdr h;
     h.sec = sec; h.nsec = nsec; h.start = b->total; h.num = n;
     std::memcpy(h.T, Tm, 64);
-    b->pts.resize((size_t)(b->total + n) * 4);
+    PsRun run;
+    run.dst = b->total;
+    run.n = n;
+    run.hsrc = b->host_total;
+    b->pts.resize((b->host_total + n) * 4);
     const uint8_t* r = static_cast<const uint8_t*>(rec);
-    float* o = b->pts.data() + (size_t)h.start * 4;
+    float* o = b->pts.data() + b->host_total * 4;
     for (uint32_t k = 0; k < n; ++k) {
         std::memcpy(o + 4 * (size_t)k, r + (size_t)k * step, 12);
         o[4 * (size_t)k + 3] = 1.0f;
     }
+    b->host_total += n;
     b->total += n;
     b->seqs.push_back(h);
+    b->add_run(run);
+}
+
+// addPointSequence with the PointCloud2 records in device memory of the engine's GPU: borrowed
+// (like addDepthmap's pointer) until the next uploadPointSequences, gathered on the device there.
+void add_point_sequence_device(gdf_engine* e, const void* rec, uint32_t n, uint32_t step,
+                               uint32_t sec, uint32_t nsec, const float* Tm) {
+    if ((n && (!rec || step < 12 || step % 4 || reinterpret_cast<uintptr_t>(rec) % 4)) || !Tm)
+        fail(GDF_ERR_ARG, "addPointSequenceDevice: bad argument (records need 4-byte alignment)");
+    std::lock_guard<std::mutex> lk(e->ps_mutex);
+    PsBuf* b = e->collect;
+    if ((uint64_t)b->total + n > 0xFFFFFFFFull) fail(GDF_ERR_CAPACITY, "addPointSequence: too many points");
+    Hdr h;
+    h.sec = sec; h.nsec = nsec; h.start = b->total; h.num = n;
+    std::memcpy(h.T, Tm, 64);
+    PsRun run;
+    run.dst = b->total;
+    run.n = n;
+    run.step = step;
+    run.dev = rec;
+    b->total += n;
+    b->seqs.push_back(h);
+    b->add_run(run);
 }
 
 // ---- point-sequence chain -----------------------------------------------------------------------
@@ -475,8 +525,14 @@ void upload_point_sequences(gdf_engine* e) {  // fusion.cpp:819-857
     if (e->n_new) {
         e->serialize();  // d_new / the ring are shared with the previous frame
         e->d_new.ensure((size_t)e->n_new * 16);
-        HIPCHK(hipMemcpyWithStream(e->d_new.p, e->upload->pts.data(), (size_t)e->n_new * 16,
-                                   hipMemcpyHostToDevice, e->s()));
+        float4* dst = e->d_new.as<float4>();
+        for (const PsRun& r : e->upload->runs) {
+            if (r.dev)
+                HIPCHK(launch_gather_records(r.dev, r.n, r.step, dst + r.dst, e->s()));
+            else
+                HIPCHK(hipMemcpyWithStream(dst + r.dst, e->upload->pts.data() + 4 * r.hsrc,
+                                           (size_t)r.n * 16, hipMemcpyHostToDevice, e->s()));
+        }
     }
     e->ps_filter_set = false;
 }
@@ -916,7 +972,9 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime) 
     v.gstatus = e->sl().d_gstatus.as<unsigned long long>();
     v.ggstatus = e->sl().d_ggstatus.as<unsigned long long>();
     v.ctrs = e->sl().d_ctrs.as<unsigned long long>();
-    v.sort_pt = e->sort_pt;
+    // keys per thread of a radix tile: small frames want many tiles (latency), big ones few
+    // (each tile publishes 256 look-back words: 2 KiB per 1 Ki keys at PT=4)
+    v.sort_pt = e->sort_pt ? e->sort_pt : nmax <= (1u << 20) ? 4 : nmax <= (1u << 24) ? 8 : 16;
     v.err = e->sl().d_misc.as<uint32_t>() + kErr;
     v.out = e->sl().d_vox.as<float4>();
     v.out_count = e->sl().d_misc.as<uint32_t>() + kVoxCount;
@@ -1216,6 +1274,12 @@ int gdf_add_point_sequence(gdf_engine* e, const void* rec, uint32_t n, uint32_t 
                            uint32_t sec, uint32_t nsec, const float Tm[16]) {
     ENGINE_OR_FAIL(e);
     return guarded(nullptr, [&] { add_point_sequence(e, rec, n, step, sec, nsec, Tm); });
+}
+
+int gdf_add_point_sequence_device(gdf_engine* e, const void* rec, uint32_t n, uint32_t step,
+                                  uint32_t sec, uint32_t nsec, const float Tm[16]) {
+    ENGINE_OR_FAIL(e);
+    return guarded(nullptr, [&] { add_point_sequence_device(e, rec, n, step, sec, nsec, Tm); });
 }
 
 int gdf_num_collected_point_sequence_points(gdf_engine* e, uint32_t* out) {

@@ -911,6 +911,34 @@ hipError_t launch_ps_filter_insert(const float4* new_pts, uint32_t n, int do_fil
     return hipGetLastError();
 }
 
+// addPointSequence for device-resident PointCloud2 records (fusion.cpp:777-780: x, y, z floats at
+// byte offsets 0/4/8 of each point_step record, w = 1).  step is a multiple of 4; the common
+// step 16 (16-byte aligned records) reads one 16-byte vector per point.
+__global__ __launch_bounds__(256) void k_gather_records(const uint8_t* __restrict__ rec,
+                                                        uint32_t n, uint32_t step, int vec16,
+                                                        float4* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float4 p;
+    if (vec16) {
+        p = reinterpret_cast<const float4*>(rec)[i];
+    } else {
+        const float* r = reinterpret_cast<const float*>(rec + (size_t)i * step);
+        p = make_float4(r[0], r[1], r[2], 0.0f);
+    }
+    p.w = 1.0f;
+    out[i] = p;
+}
+
+hipError_t launch_gather_records(const void* rec, uint32_t n, uint32_t step, float4* out,
+                                 hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const int vec16 = step == 16 && (reinterpret_cast<uintptr_t>(rec) & 15u) == 0;
+    hipLaunchKernelGGL(k_gather_records, dim3((n + 255) / 256), dim3(256), 0, s,
+                       static_cast<const uint8_t*>(rec), n, step, vec16, out);
+    return hipGetLastError();
+}
+
 // ---- historic occupancy grid ---------------------------------------------------------------------
 // Occupancy marks of a frame are a bitmask (cell c -> bit c % 32 of word c / 32), set by k_emit /
 // k_scatter and consumed - read and cleared - by the grid update.  hist' = max(sat_dec(hist),

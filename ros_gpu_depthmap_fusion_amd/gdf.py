@@ -85,7 +85,8 @@ _lib = None
 EXPORTED = [
     "gdf_create", "gdf_destroy", "gdf_last_error", "gdf_version", "gdf_set_stream",
     "gdf_synchronize", "gdf_set_pipeline_depth", "gdf_set_graphs", "gdf_set_voxel_group_size", "gdf_clear", "gdf_add_depthmap",
-    "gdf_add_depthmap_device", "gdf_add_point_sequence", "gdf_num_collected_point_sequence_points",
+    "gdf_add_depthmap_device", "gdf_add_point_sequence", "gdf_add_point_sequence_device",
+    "gdf_num_collected_point_sequence_points",
     "gdf_upload_point_sequences", "gdf_filter_new_point_sequences", "gdf_insert_new_point_sequences",
     "gdf_roll_rollbuffer", "gdf_select_timespan", "gdf_prepare_point_and_mask_buffers",
     "gdf_insert_selected_point_sequence", "gdf_transform_point_sequence", "gdf_get_rollbuffer_state",
@@ -125,6 +126,7 @@ def load_library(path: str = LIB_PATH):
         "gdf_add_depthmap": (i32, [vp, vp, u32, u32, f, f, f, f, f, vp, vp]),
         "gdf_add_depthmap_device": (i32, [vp, vp, u32, u32, f, f, f, f, f, vp, vp]),
         "gdf_add_point_sequence": (i32, [vp, vp, u32, u32, u32, u32, vp]),
+        "gdf_add_point_sequence_device": (i32, [vp, vp, u32, u32, u32, u32, vp]),
         "gdf_num_collected_point_sequence_points": (i32, [vp, P(u32)]),
         "gdf_upload_point_sequences": (i32, [vp]),
         "gdf_filter_new_point_sequences": (i32, [vp, f, u32]),
@@ -315,6 +317,15 @@ class GPUDepthmapFusion:
         self._check(self._lib.gdf_add_point_sequence(self._h, _ptr(rec), rec.shape[0],
                                                      rec.shape[1] * 4, timestampSec,
                                                      timestampNSec, _ptr(tm)))
+
+    def addPointSequenceDevice(self, dev_ptr: int, num_points: int, point_step: int,
+                               timestampSec: int, timestampNSec: int, transform_move):
+        """Records already in device memory (x,y,z f32 at byte offsets 0/4/8 of each
+        point_step record); borrowed until the next uploadPointSequences / processFrame."""
+        tm = _mat(transform_move)
+        self._check(self._lib.gdf_add_point_sequence_device(
+            self._h, C.c_void_p(dev_ptr), num_points, point_step, timestampSec, timestampNSec,
+            _ptr(tm)))
 
     def numCollectedPointSequencePoints(self) -> int:
         n = C.c_uint32()

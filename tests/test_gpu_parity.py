@@ -468,3 +468,88 @@ def test_graph_replay_matches_direct_launches(Engine):
                                       bits(b) if b.dtype == np.float32 else b)
     np.testing.assert_array_equal(graph.historic_grid(), orc.historic_grid())
     compare_results(graph, orc, tag="graph")
+
+
+@pytest.mark.parametrize("step", [16, 20, 12])
+def test_device_point_sequences_match_host(Engine, step):
+    """addPointSequenceDevice (PointCloud2 records in device memory, gathered on the GPU) gives
+    the host path's rollbuffer and frame outputs, mixed with host sequences in one frame and
+    with records of other point_step (extra fields after x,y,z); oracle checked too."""
+    from ros_gpu_depthmap_fusion_amd import hiprt
+    p = ComponentParams()
+    p.ps_timespan = 3.0 / 30.0
+    lidar = synth.make_camera(0, 64, 48)
+    cam = synth.make_camera(1, 96, 72)
+    host, dev, orc = Engine(), Engine(), OracleFusion(threads=4)
+    keep = []
+    rng = np.random.default_rng(step)
+    k = 0
+    for f in range(5):
+        for j in range(2):
+            pts = synth.back_project(lidar, synth.depth_frame(lidar, 5, k))
+            if f == 2 and j == 0:
+                pts = pts[:0]  # an empty sequence
+            s, ns = synth.sequence_time(k)
+            T = synth.move_transform(k)
+            host.addPointSequence(pts, s, ns, T)
+            orc.addPointSequence(pts, s, ns, T)
+            if j == 1 and f % 2:  # a host sequence inside a device-fed frame
+                dev.addPointSequence(pts, s, ns, T)
+            else:
+                rec = np.zeros((len(pts), step // 4), np.float32)
+                rec[:, :3] = pts
+                if step > 12:
+                    rec[:, 3:] = rng.random((len(pts), step // 4 - 3))
+                d = hiprt.DeviceArray.from_numpy(rec) if len(pts) else None
+                keep.append(d)
+                dev.addPointSequenceDevice(d.ptr if d else 0, len(pts), step, s, ns, T)
+            k += 1
+        args = [cam_args(cam, synth.depth_frame(cam, 1, f))]
+        for e in (host, dev, orc):
+            e.clear()
+            for a in args:
+                e.addDepthmap(*a)
+            e.processFrame(p, T_world_move=cam.T_world, T_crop_move=cam.T_crop)
+        assert dev.rollbuffer_state().as_tuple() == orc.rollbuffer_state(), f"frame {f}"
+        for a, b in zip(_gpu_outputs(host), _gpu_outputs(dev)):
+            np.testing.assert_array_equal(bits(a) if a.dtype == np.float32 else a,
+                                          bits(b) if b.dtype == np.float32 else b,
+                                          err_msg=f"frame {f}")
+        gp, gm, gs, gh = dev.rollbuffer_arrays()
+        op, om, os_, oh = orc.rollbuffer_arrays()
+        np.testing.assert_array_equal(gm, om)
+        np.testing.assert_array_equal(bits(gp), bits(op))
+        compare_results(dev, orc, tag=f"frame {f}")
+    with pytest.raises(GDFError):  # misaligned records
+        dev.addPointSequenceDevice(keep[1].ptr + 2, 4, 16, 0, 0, EYE)
+
+
+def test_large_rollbuffer_window_properties(Engine):
+    """A C3-like window at reduced size (48 sequences of 320x240 device records = 3.7 M selected
+    points per frame; radix tiles at 16 keys per thread): the compaction count equals the
+    stage-mask count, one voxel mean per distinct key, and the grid holds exactly the frame's
+    voxels at full lifetime."""
+    from ros_gpu_depthmap_fusion_amd import hiprt
+    p = ComponentParams()
+    p.ps_timespan = 47.5 / 30.0
+    lidar = synth.make_camera(0, 320, 240)
+    n = 320 * 240
+    seqs = [hiprt.DeviceArray.from_numpy(np.concatenate(
+        [synth.back_project(lidar, synth.depth_frame(lidar, 0, f)),
+         np.ones((n, 1), np.float32)], 1)) for f in range(4)]
+    gpu = Engine()
+    gpu.set_debug(True)
+    for k in range(56):
+        s, ns = synth.sequence_time(k)
+        gpu.addPointSequenceDevice(seqs[k % 4].ptr, n, 16, s, ns, synth.move_transform(k))
+        gpu.clear()
+        r = gpu.processFrame(p, T_world_move=lidar.T_world, T_crop_move=lidar.T_crop,
+                             synchronous=k == 55)
+    st = gpu.rollbuffer_state()
+    assert st.selection_sequence_count == 48 and r.num_points_total == 48 * n
+    sm = gpu.stage_masks()
+    assert gpu.point_count() == int(np.count_nonzero(sm & 4)) > 1_000_000
+    c = gpu.downloadVoxelCoords()
+    assert len(gpu.downloadVoxelizedPoints()) == len(np.unique(c))
+    grid = gpu.downloadVoxelOccupancyGrid().reshape(-1)
+    assert np.array_equal(np.flatnonzero(grid == p.occupancy_lifetime), np.unique(c))

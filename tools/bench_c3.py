@@ -1,0 +1,154 @@
+#!/usr/bin/env python3
+"""C3 workload (BASELINE.json configs[2]): 1280x720 depth, 1 MI355X, rollbuffer timespan select +
+radix compaction over a 256-frame window.
+
+Per frame (GPUDepthmapFusionComponent::processDepthmaps, component.cpp:92-300): one new point
+sequence (a back-projected 720p frame, 921 600 points, device-resident PointCloud2 records fed
+through gdf_add_point_sequence_device) is filtered and inserted into the rollbuffer, the window
+is rolled to the last `window` sequences (timespan (window - 0.5)/30 s at 30 fps stamps), all of
+them are selected, transformed (T_world_move / T_crop_move = the lidar's camera transforms, so the
+points land in the crop box like the depth camera's) and fused with the 720p depth frame:
+compaction, voxel keys, occupancy marks, GPU voxelize (radix sort over every surviving point),
+historic grid.  SURVEY.md §8(d) byte model + C3 additions.
+
+    python tools/bench_c3.py [--window 256] [--steps 20] [--json out.json]
+
+Prints one JSON line.  Not the driver's bench (that is bench.py, configs[1]); this reports the
+C3 configuration with the same fields (value, roofline of the dominant kernel).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--width", type=int, default=1280)
+    ap.add_argument("--height", type=int, default=720)
+    ap.add_argument("--window", type=int, default=256)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--ring", type=int, default=4, help="distinct device-resident sequences/frames")
+    ap.add_argument("--profile-steps", type=int, default=5)
+    ap.add_argument("--json", default=None)
+    args = ap.parse_args()
+
+    import numpy as np
+    from ros_gpu_depthmap_fusion_amd import build_library, hiprt, synth
+    from ros_gpu_depthmap_fusion_amd.gdf import ComponentParams, GPUDepthmapFusion
+
+    build_library()
+    W, H = args.width, args.height
+    P = W * H
+    cam = synth.make_camera(0, W, H)        # depth camera
+    lidar = synth.make_camera(1, W, H)      # the point-sequence source (another view)
+    t0 = time.perf_counter()
+    depth = [hiprt.DeviceArray.from_numpy(synth.depth_frame(cam, 0, f)) for f in range(args.ring)]
+    seqs = []
+    for f in range(args.ring):
+        xyz = synth.back_project(lidar, synth.depth_frame(lidar, 1, f))
+        rec = np.concatenate([xyz, np.ones((len(xyz), 1), np.float32)], 1)  # step 16
+        seqs.append(hiprt.DeviceArray.from_numpy(np.ascontiguousarray(rec)))
+    gen_s = time.perf_counter() - t0
+
+    p = ComponentParams()
+    p.ps_timespan = (args.window - 0.5) / 30.0
+    eng = GPUDepthmapFusion(0)
+    pc_async = p.to_c(lidar.T_world, lidar.T_crop, False, False)
+    pc_sync = p.to_c(lidar.T_world, lidar.T_crop, True, False)
+    k = 0
+
+    def frame(pc):
+        nonlocal k
+        s, ns = synth.sequence_time(k)
+        eng.addPointSequenceDevice(seqs[k % args.ring].ptr, P, 16, s, ns, synth.move_transform(k))
+        eng.clear()
+        eng.addDepthmapDevice(depth[k % args.ring].ptr, W, H, *cam.intrinsics(), cam.T_world,
+                              cam.T_crop)
+        r = eng.processFramePrepared(pc)
+        k += 1
+        return r
+
+    # fill the window (untimed), then one synchronous frame for the counts
+    t0 = time.perf_counter()
+    for i in range(args.window + 1):
+        frame(pc_async)
+        if i % 32 == 0:
+            eng.synchronize()
+            print(f"# fill {i}/{args.window} {time.perf_counter() - t0:.1f}s", file=sys.stderr,
+                  flush=True)
+    eng.synchronize()
+    r = frame(pc_sync)
+    st = eng.rollbuffer_state()
+    S, N, G = st.selection_point_count, r.num_points, r.num_voxelized
+    (gx, gy, gz), ncells = eng.grid_size()
+
+    eng.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        frame(pc_async)
+    eng.synchronize()
+    elapsed = time.perf_counter() - t0
+
+    eng.set_profiling(True)
+    for _ in range(args.profile_steps):
+        frame(pc_async)
+    eng.synchronize()
+    kt = eng.kernel_times()
+    eng.set_profiling(False)
+
+    ms = elapsed / args.steps * 1e3
+    items = P + S
+    seg = 1024
+    # algorithmic HBM bytes per launch (SURVEY §8(d) + C3 terms)
+    model = {
+        "mask": 2.0 * P + 16.0 * S + 8.0 * (items / seg) * 17,  # depth, selected ring points,
+                                                                 # vbits + count per segment
+        "emit": 2.0 * P + 16.0 * S + 20.0 * N,                  # sources again, point + key out
+        "sort": (12.0 * N + 16.0 * N * 2 + 2.0 * ncells) / 3.0,
+        "group": 24.0 * N + 16.0 * G,
+        "ps_insert": 32.0 * P,                                   # new sequence in, ring out
+        "scan": 8.0 * (items / seg),
+    }
+    per = {}
+    for name in ("mask", "scan", "emit", "sort", "group", "ps_insert"):
+        tot, n = kt[name]
+        if n:
+            per[name] = {"avg_us": round(tot * 1e3 / n, 2), "launches_per_frame":
+                         round(n / args.profile_steps, 2),
+                         "GBps": round(model[name] / (tot / 1e3 / n) / 1e9, 1)}
+    dom = max(per, key=lambda q: per[q]["avg_us"] * per[q]["launches_per_frame"])
+    achieved = per[dom]["GBps"]
+    out = {
+        "metric": "Mpoints/s depth pixels (C3: 720p + 256-sequence rollbuffer window)",
+        "value": round(P / (elapsed / args.steps) / 1e6, 3),
+        "unit": "Mpoints/s", "n_gpus": 1, "steps": args.steps, "ms_per_step": round(ms, 4),
+        "points_per_frame_total": items,
+        "total_points_Mps": round(items / (elapsed / args.steps) / 1e6, 1),
+        "dtype": "f32", "data": "synthetic (ray-cast scene; %d device-resident frames and "
+                                "sequences reused round-robin)" % args.ring,
+        "config": {"workload": "C3: %dx%d depth + rollbuffer window of %d sequences of %d "
+                               "points (timespan select, transform, crop, compaction, voxelize, "
+                               "grid %dx%dx%d)" % (W, H, args.window, P, gx, gy, gz),
+                   "selected_points": S, "points_after_crop": N, "voxels": G,
+                   "grid_cells": ncells},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                     "per_kernel": per},
+        "setup_s": round(gen_s, 1),
+    }
+    line = json.dumps(out)
+    print(line)
+    if args.json:
+        with open(args.json, "w") as f:
+            f.write(line + "\n")
+
+
+if __name__ == "__main__":
+    main()
