@@ -17,6 +17,7 @@ constexpr int kArgCams = 4;           // camera descriptors passed in the kernel
 constexpr int kHalo = 8;              // band rows/columns staged around a segment: min(F, 8)
 constexpr uint32_t kSegItems = 1024;  // items per compaction segment (max)
 constexpr uint32_t kFusedPrefixSegs = 4096;  // up to this many segments k_emit sums the counts
+constexpr uint32_t kSelSegs = 8;      // rollbuffer segments per k_mask / k_emit block
 constexpr int kSortThreads = 256;
 // the voxel-key digit histogram is accumulated into kHistReps replicas of [4 passes][256 digits]
 // (block b adds into replica b % kHistReps): same-address atomics from hundreds of blocks

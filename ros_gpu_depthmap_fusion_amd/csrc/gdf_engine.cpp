@@ -211,8 +211,8 @@ struct Slot {
     struct Graph {
         hipGraph_t g = nullptr;
         hipGraphExec_t x = nullptr;
-        hipGraphNode_t n_mask = nullptr, n_emit = nullptr;
-        hipKernelNodeParams p_mask{}, p_emit{};
+        // the compaction kernel nodes (k_mask, k_emit, k_emit_sel): they take the FrameArgs
+        std::vector<std::pair<hipGraphNode_t, hipKernelNodeParams>> frame_nodes;
         FrameArgs key_a;
         VoxelizeArgs key_v;
         bool valid = false;
@@ -225,6 +225,7 @@ struct Slot {
             x = nullptr;
             g = nullptr;
             valid = cand = false;
+            frame_nodes.clear();
         }
     } graph;
 };
@@ -883,7 +884,10 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel) {
         std::memcpy(a.gmax, e->vp.gmax, 12);
         std::memcpy(a.gs, e->vp.gs, 12);
         if (e->sl().khist_pending) HIPCHK(hipMemsetAsync(e->sl().d_khist.p, 0, kHistWords * 4, e->s()));
-        a.key_hist = e->sl().d_khist.as<uint32_t>();
+        // digit histogram of the keys from the compaction blocks (frees the sort of a separate
+        // pass) - but not over a large rollbuffer window, where tens of thousands of blocks would
+        // each flush their histogram with device-scope atomics; k_sort_hist counts those keys
+        a.key_hist = a.total_segs <= kFusedPrefixSegs ? e->sl().d_khist.as<uint32_t>() : nullptr;
         a.npasses = e->key_bits == 0 ? 1u : (e->key_bits + 7) / 8;
     }
     a.out_pts = e->sl().d_pts.as<float4>();
@@ -892,7 +896,7 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel) {
     const uint32_t segs = std::max<uint32_t>(a.total_segs, 1);
     e->sl().d_vbits.ensure((size_t)segs * 16 * 8);
     e->sl().d_tcounts.ensure((size_t)segs * 4);
-    e->sl().d_toffsets.ensure((size_t)segs * 4);
+    e->sl().d_toffsets.ensure(seg_offsets_words(segs) * 4);
     a.vbits = e->sl().d_vbits.as<unsigned long long>();
     a.seg_counts = e->sl().d_tcounts.as<uint32_t>();
     a.seg_offsets = e->sl().d_toffsets.as<uint32_t>();
@@ -914,8 +918,8 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel) {
     return a;
 }
 
-void frame_launched(gdf_engine* e, bool fused_voxel) {
-    e->sl().khist_pending = fused_voxel;
+void frame_launched(gdf_engine* e, bool fused_voxel, bool key_hist) {
+    e->sl().khist_pending = fused_voxel && key_hist;
     e->sl().compacted = true;
     e->sl().coords_valid = fused_voxel;
     e->sl().marks_set = fused_voxel;
@@ -926,7 +930,7 @@ void run_frame(gdf_engine* e, bool fused_voxel) {
     const FrameArgs a = frame_args(e, fused_voxel);
     if (e->profiling) e->timed(GDF_KERNEL_EVENT_FLOOR, [] {});  // calibrates the event overhead
     e->timed(GDF_KERNEL_FRAME, [&] { HIPCHK(launch_frame(a, e->s(), e->hook_ptr())); });
-    frame_launched(e, fused_voxel);
+    frame_launched(e, fused_voxel, a.key_hist != nullptr);
 }
 
 void compute_voxel_coords(gdf_engine* e, const float* lo, const float* hi, const float* cs) {
@@ -1022,7 +1026,7 @@ bool same_key(const FrameArgs& a, const VoxelizeArgs& v, const FrameArgs& ka, co
 // direct launches, or the slot's captured graph when the launch arguments repeat
 void run_fused_frame(gdf_engine* e, int average, uint32_t lifetime) {
     const FrameArgs a = frame_args(e, true);
-    frame_launched(e, true);  // (the launches below follow; voxelize_args checks this state)
+    frame_launched(e, true, a.key_hist != nullptr);  // (the launches below follow)
     const VoxelizeArgs v = voxelize_args(e, average, (int)lifetime);
     Slot::Graph& G = e->sl().graph;
     const bool eligible = e->use_graphs && !e->profiling && !e->debug && a.ncams <= kArgCams &&
@@ -1030,11 +1034,11 @@ void run_fused_frame(gdf_engine* e, int average, uint32_t lifetime) {
     hipStream_t st = e->s();
     if (eligible && G.valid && same_key(a, v, G.key_a, G.key_v)) {
         void* args[] = {const_cast<FrameArgs*>(&a)};
-        hipKernelNodeParams pm = G.p_mask, pe = G.p_emit;
-        pm.kernelParams = args;
-        pe.kernelParams = args;
-        HIPCHK(hipGraphExecKernelNodeSetParams(G.x, G.n_mask, &pm));
-        HIPCHK(hipGraphExecKernelNodeSetParams(G.x, G.n_emit, &pe));
+        for (auto& np : G.frame_nodes) {
+            hipKernelNodeParams kp = np.second;
+            kp.kernelParams = args;
+            HIPCHK(hipGraphExecKernelNodeSetParams(G.x, np.first, &kp));
+        }
         HIPCHK(hipGraphLaunch(G.x, st));
     } else if (eligible && G.cand && same_key(a, v, G.cand_a, G.cand_v)) {
         // the arguments repeated: capture this frame's launches and replay from now on
@@ -1053,18 +1057,18 @@ void run_fused_frame(gdf_engine* e, int average, uint32_t lifetime) {
         HIPCHK(hipGraphGetNodes(G.g, nullptr, &nn));
         std::vector<hipGraphNode_t> nodes(nn);
         HIPCHK(hipGraphGetNodes(G.g, nodes.data(), &nn));
-        const void* fm = frame_kernel(0, a.rot45);
-        const void* fe = frame_kernel(1, a.rot45);
+        const void* fk[3] = {frame_kernel(0, a.rot45), frame_kernel(1, a.rot45), frame_kernel(2, a.rot45)};
+        G.frame_nodes.clear();
         for (hipGraphNode_t n : nodes) {
             hipGraphNodeType t;
             HIPCHK(hipGraphNodeGetType(n, &t));
             if (t != hipGraphNodeTypeKernel) continue;
             hipKernelNodeParams kp{};
             HIPCHK(hipGraphKernelNodeGetParams(n, &kp));
-            if (kp.func == fm) { G.n_mask = n; G.p_mask = kp; }
-            if (kp.func == fe) { G.n_emit = n; G.p_emit = kp; }
+            if (kp.func == fk[0] || kp.func == fk[1] || kp.func == fk[2])
+                G.frame_nodes.emplace_back(n, kp);
         }
-        if (!G.n_mask || !G.n_emit) fail(GDF_ERR_HIP, "frame graph: compaction kernels not found");
+        if (G.frame_nodes.empty()) fail(GDF_ERR_HIP, "frame graph: compaction kernels not found");
         graph_key(a, G.key_a);
         G.key_v = v;
         G.valid = true;

@@ -11,6 +11,8 @@
 //   k_sort_*, k_group  inc/voxelize.h:74-105 + radix_grouper.h + radix_sort.h (GPU version)
 #include "gdf_kernels.hpp"
 
+#include <algorithm>
+
 namespace gdf {
 
 // Pointers that arrive inside structs (kernel-argument structs, LDS camera copies) are generic to
@@ -67,6 +69,43 @@ __device__ __forceinline__ uint32_t take_ticket_epoch(uint32_t* ctr, uint32_t nt
         __hip_atomic_store(epoch_word, e + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     epoch = e + 1u;
+    return t;
+}
+
+// Persistent launches: of a launch's `grid` ticket-capable blocks, nblk = min(grid, ntiles)
+// take part (the others leave at once: a capacity-sized launch is mostly empty for small frames).
+// With ntiles <= grid every participant draws exactly one ticket (ntiles draws); otherwise each
+// draws until it gets one >= ntiles (ntiles + nblk draws).  The drawer of the last ticket resets
+// the counter and publishes the next epoch; every participant reads the epoch (read_epoch)
+// before its first draw, so before that last one.  The grid is capped by kPersistBlocks: a
+// capacity-sized grid of 10^5..10^6 mostly idle workgroups (a large rollbuffer window whose
+// points mostly leave the crop box) costs more dispatch time than the work.
+__device__ __forceinline__ uint32_t read_epoch(uint32_t* epoch_word) {
+    const uint32_t e = __hip_atomic_load(epoch_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return e + 1u;
+}
+
+struct Tickets {
+    uint32_t nblk, draws;
+    bool oneshot;
+};
+
+__device__ __forceinline__ Tickets tickets(uint32_t ntiles, uint32_t grid) {
+    Tickets t;
+    t.oneshot = ntiles <= grid;
+    t.nblk = t.oneshot ? ntiles : grid;
+    t.draws = t.oneshot ? ntiles : ntiles + grid;
+    return t;
+}
+
+__device__ __forceinline__ uint32_t next_ticket(uint32_t* ctr, const Tickets& tk,
+                                                uint32_t* epoch_word, uint32_t epoch) {
+    const uint32_t t = atomicAdd(ctr, 1u);
+    if (t == tk.draws - 1u) {
+        atomicExch(ctr, 0u);
+        __hip_atomic_store(epoch_word, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     return t;
 }
 
@@ -493,13 +532,55 @@ __device__ __forceinline__ uint32_t sel_tf(const FrameArgs& a, uint32_t i) {
     return G(a.seg_tf)[lo];
 }
 
+// The selected points of one segment (consecutive, block-uniform): the transform of its first
+// point and where the next sequence starts (sequences hold ~10^5..10^6 points, so a segment
+// almost never crosses one), and the ring position of its first point - one binary search and
+// one 64-bit modulo per segment instead of per point.
+struct SelSeg {
+    uint32_t si0;    // first selected-point index of the segment
+    uint32_t tf0;    // its transform index
+    uint32_t next;   // first index of the following sequence (UINT_MAX: none)
+    uint64_t r0;     // ring slot of si0
+};
+
+__device__ __forceinline__ SelSeg sel_seg(const FrameArgs& a, uint32_t si0) {
+    // last sequence starting at or before si0: 64-ary search by the wave (seg_start ascending,
+    // seg_start[0] == 0), one round trip per factor 64 of sequences
+    const int lane = threadIdx.x & 63;
+    uint32_t lo = 0, hi = a.nseg;
+    while (hi - lo > 1) {
+        const uint32_t step = (hi - lo + 63u) / 64u;
+        const uint32_t j = lo + (uint32_t)lane * step;
+        const unsigned long long le = __ballot(j < hi && G(a.seg_start)[j] <= si0);
+        const uint32_t L = 63u - (uint32_t)__clzll((long long)le);  // bit 0 is always set
+        lo = lo + L * step;
+        hi = min(hi, lo + step);
+    }
+    SelSeg g;
+    g.si0 = si0;
+    g.tf0 = G(a.seg_tf)[lo];
+    g.next = lo + 1 < a.nseg ? G(a.seg_start)[lo + 1] : 0xFFFFFFFFu;
+    g.r0 = (a.ring_first + si0) % a.ring_cap;
+    return g;
+}
+
+__device__ __forceinline__ float4 sel_point(const FrameArgs& a, const SelSeg& g, uint32_t i) {
+    uint64_t r = g.r0 + (i - g.si0);
+    if (r >= a.ring_cap) r -= a.ring_cap;
+    return gld4(a.ring, r);
+}
+
+__device__ __forceinline__ uint32_t sel_tf_in(const FrameArgs& a, const SelSeg& g, uint32_t i) {
+    return i < g.next ? g.tf0 : sel_tf(a, i);
+}
+
 // selected rollbuffer point i: mask (transfer_data of the selected mask), transform_points
 // _indirect (:50-69) into the crop frame, crop_points
-__device__ __forceinline__ uint32_t sel_bits(const FrameArgs& a, uint32_t i) {
-    const float4 p = gld4(a.ring, (a.ring_first + i) % a.ring_cap);
+__device__ __forceinline__ uint32_t sel_bits(const FrameArgs& a, const SelSeg& g, uint32_t i,
+                                             const float4& p) {
     if (p.w == 0.0f) return 0;  // rollbuffer mask 0
     if (a.do_crop) {
-        const gptr<const float> Tc = G(a.tfc + 16 * (size_t)sel_tf(a, i));
+        const gptr<const float> Tc = G(a.tfc + 16 * (size_t)sel_tf_in(a, g, i));
         const float qx = mrow(Tc + 0, p.x, p.y, p.z, 1.0f);
         const float qy = mrow(Tc + 4, p.x, p.y, p.z, 1.0f);
         const float qz = mrow(Tc + 8, p.x, p.y, p.z, 1.0f);
@@ -508,6 +589,43 @@ __device__ __forceinline__ uint32_t sel_bits(const FrameArgs& a, uint32_t i) {
             return 3;
     }
     return 7;
+}
+
+// k_mask for rollbuffer segments: one block covers kSelSegs consecutive segments of blockDim
+// selected points (all ring loads in flight together, one transform lookup per block); per
+// segment the validity words and the count, as for a depth segment.
+__device__ __forceinline__ void sel_mask_block(const FrameArgs& a, uint32_t sb, uint32_t* s_scnt) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int nwaves = blockDim.x >> 6;
+    const uint32_t B = blockDim.x, i = threadIdx.x;
+    const uint32_t seg0 = a.depth_segs + sb * kSelSegs;
+    const uint32_t nh = min(kSelSegs, a.total_segs - seg0);
+    const uint32_t si0 = sb * kSelSegs * B;
+    const SelSeg g = sel_seg(a, si0);
+    float4 p[kSelSegs];
+#pragma unroll
+    for (uint32_t j = 0; j < kSelSegs; ++j) {
+        const uint32_t si = si0 + j * B + i;
+        p[j] = (j < nh && si < a.sel_count) ? sel_point(a, g, si) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kSelSegs; ++j) {
+        const uint32_t si = si0 + j * B + i;
+        const bool in = j < nh && si < a.sel_count;
+        const uint32_t bits = in ? sel_bits(a, g, si, p[j]) : 0u;
+        if (a.dbg && in) G(a.dbg)[a.depth_total + si] = (uint8_t)bits;
+        const unsigned long long m = __ballot((bits & 4u) != 0u);
+        if (j < nh && lane == 0) {
+            G(a.vbits)[(size_t)(seg0 + j) * 16 + wid] = m;
+            s_scnt[j * 16 + wid] = (uint32_t)__popcll(m);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < nh) {
+        uint32_t t = 0;
+        for (int w = 0; w < nwaves; ++w) t += s_scnt[threadIdx.x * 16 + w];
+        G(a.seg_counts)[seg0 + threadIdx.x] = t;
+    }
 }
 
 // Camera descriptors: kernel arguments for up to kArgCams cameras, else the device copy.
@@ -531,7 +649,7 @@ __global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
     __shared__ CamDesc s_cams[kMaxCams];
     __shared__ float s_yn[2 * kHalo + 1];
     __shared__ int s_rowoff[2 * kHalo + 1];
-    __shared__ uint32_t s_cnt[16];
+    __shared__ uint32_t s_cnt[kSelSegs * 16];
     extern __shared__ uint4 s_dyn[];  // band rows (a.band_rowb bytes each), then xn
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int nwaves = blockDim.x >> 6;
@@ -539,12 +657,16 @@ __global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
     // so give each XCD a contiguous run of segments - neighbouring rows' bands then share its L2
     const uint32_t n = gridDim.x, q8 = n / 8, r8 = n % 8, xcd = blockIdx.x % 8;
     const uint32_t s = xcd * q8 + min(xcd, r8) + blockIdx.x / 8;
-    load_cams(a, s_cams);
     if (a.grid_seq_out && blockIdx.x == 0 && threadIdx.x == 0) *a.grid_seq_out = a.grid_seq;
+    if (s >= a.depth_segs) {  // block-uniform: rollbuffer segments
+        sel_mask_block(a, s - a.depth_segs, s_cnt);
+        return;
+    }
+    load_cams(a, s_cams);
     __syncthreads();
     uint32_t bits = 0;
     const uint32_t i = threadIdx.x;
-    if (s < a.depth_segs) {
+    {
         const SegGeo sg = seg_geo(s_cams, a.ncams, s);
         const CamDesc& c = s_cams[sg.k];
         const int h = a.do_flying ? (int)min(a.F, (uint32_t)kHalo) : 0;
@@ -618,12 +740,6 @@ __global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
                 bits = depth_bits<ROT45, false>(a, s_cams, sg.k, t, s_yn, sg.x0 + i, sg.y, i < sg.len);
             if (a.dbg && i < sg.len) G(a.dbg)[sg.item0 + i] = (uint8_t)bits;
         }
-    } else {
-        const uint32_t si = (s - a.depth_segs) * blockDim.x + i;
-        if (si < a.sel_count) {
-            bits = sel_bits(a, si);
-            if (a.dbg) G(a.dbg)[a.depth_total + si] = (uint8_t)bits;
-        }
     }
     const unsigned long long m = __ballot((bits & 4u) != 0u);
     if (lane == 0) {
@@ -640,15 +756,49 @@ __global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
 
 // Exclusive scan of the segment counts by one workgroup (chunks of 4096 with a running carry);
 // writes the total (m_numItemsAfterMask).  Used when there are more than kFusedPrefixSegs.
+// Reduce-then-scan over chunks of 4096 counts: k_scan_reduce sums chunk b into partial[b];
+// k_scan_counts block b starts from the sum of the partials before it and scans its chunk.
+__device__ __forceinline__ uint32_t block_sum_1024(uint32_t v, uint32_t* s_w) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) s_w[wid] = v;
+    __syncthreads();
+    uint32_t t = 0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) t += s_w[w];
+    return t;
+}
+
+__global__ __launch_bounds__(1024) void k_scan_reduce(const uint32_t* __restrict__ counts,
+                                                      uint32_t m, uint32_t* __restrict__ partial) {
+    __shared__ uint32_t s_w[16];
+    uint32_t v = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t i = blockIdx.x * 4096u + threadIdx.x * 4 + q;
+        v += i < m ? counts[i] : 0u;
+    }
+    const uint32_t t = block_sum_1024(v, s_w);
+    if (threadIdx.x == 0) partial[blockIdx.x] = t;
+}
+
 __global__ __launch_bounds__(1024) void k_scan_counts(const uint32_t* __restrict__ counts,
                                                       uint32_t m, uint32_t* __restrict__ offsets,
-                                                      uint32_t* __restrict__ total) {
+                                                      uint32_t* __restrict__ total,
+                                                      const uint32_t* __restrict__ partial) {
     __shared__ uint32_t s_w[16];
     __shared__ uint32_t s_carry;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    if (threadIdx.x == 0) s_carry = 0;
-    __syncthreads();
-    for (uint32_t base = 0; base < m; base += 4096) {
+    {
+        uint32_t v = 0;
+        for (uint32_t b = threadIdx.x; b < blockIdx.x; b += 1024) v += partial[b];
+        const uint32_t c = block_sum_1024(v, s_w);
+        if (threadIdx.x == 0) s_carry = c;
+        __syncthreads();
+    }
+    for (uint32_t base = blockIdx.x * 4096u; base < min(m, blockIdx.x * 4096u + 4096u);
+         base += 4096) {
         uint32_t v[4], sum = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -682,7 +832,7 @@ __global__ __launch_bounds__(1024) void k_scan_counts(const uint32_t* __restrict
         if (threadIdx.x == 0) s_carry += tot;
         __syncthreads();
     }
-    if (threadIdx.x == 0) *total = s_carry;
+    if (threadIdx.x == 0 && blockIdx.x == gridDim.x - 1) *total = s_carry;
 }
 
 // Pass 2: item-ordered emission, one block per segment.  Each valid item recomputes its world
@@ -692,48 +842,183 @@ __global__ __launch_bounds__(1024) void k_scan_counts(const uint32_t* __restrict
 // (no-return atomic OR of bit 7, issued once per run of equal keys in a wave) and the key digit
 // histogram.  The segment offset is the sum of the preceding counts (<= kFusedPrefixSegs
 // segments) or k_scan_counts' result.
+// occupancy mark + digit histogram of the wave's kept items (voxel_grid_occupancy_of_points):
+// runs of equal keys among the valid lanes - the first lane of a run marks / counts
+constexpr int kMarkCacheBits = 9;
+
+__device__ __forceinline__ void mark_and_count(const FrameArgs& a, bool valid, uint32_t key,
+                                               uint32_t* s_hist, uint32_t* s_mark) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long ltm = lanemask_lt();
+    const unsigned long long vm = __ballot(valid);
+    const unsigned long long below = vm & ltm;
+    const int prev = below ? 63 - __clzll((long long)below) : -1;
+    const uint32_t pkey = __shfl(key, prev < 0 ? 0 : prev, 64);
+    const bool leader = valid && (prev < 0 || pkey != key);
+    const unsigned long long lm = __ballot(leader);
+    if (leader) {
+        // a key this block already marked needs no second device-scope atomic: s_mark is a
+        // direct-mapped cache of marked keys (a lane only skips a key some lane wrote AFTER
+        // issuing its atomic; collisions just mark again)
+        uint32_t& slot = s_mark[(key * 0x9E3779B1u) >> (32 - kMarkCacheBits)];
+        if (a.marks && slot != key) {
+            slot = key;
+            __hip_atomic_fetch_or(G(a.marks + (key >> 5)), 1u << (key & 31u), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (a.key_hist) {
+            const unsigned long long after = lm & ~(ltm | (1ull << lane));
+            const unsigned long long upto =
+                after ? ((1ull << (__ffsll((long long)after) - 1)) - 1ull) : ~0ull;
+            const uint32_t rl = (uint32_t)__popcll(vm & ~ltm & upto);
+            for (uint32_t p = 0; p < a.npasses; ++p)
+                atomicAdd(&s_hist[p * 256 + ((key >> (8 * p)) & 0xFFu)], rl);
+        }
+    }
+}
+
+__device__ __forceinline__ void flush_hist(const FrameArgs& a, uint32_t* s_hist) {
+    if (!a.key_hist) return;
+    __syncthreads();
+    const gptr<uint32_t> rep = G(a.key_hist + (blockIdx.x % kHistReps) * 1024u);
+    for (uint32_t j = threadIdx.x; j < a.npasses * 256; j += blockDim.x)
+        if (s_hist[j])
+            __hip_atomic_fetch_add(rep + j, s_hist[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// sum of the counts of segments [0, s) by the block (fused-prefix form), into s_red per wave
+__device__ __forceinline__ void prefix_partials(const FrameArgs& a, uint32_t s, uint32_t* s_red) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t sum = 0;
+    for (uint32_t t = threadIdx.x; t < s; t += blockDim.x) sum += G(a.seg_counts)[t];
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    if (lane == 0) s_red[wid] = sum;
+}
+
+// prefix of the valid counts of the waves before this one in segment s (uniform word loads)
+__device__ __forceinline__ uint32_t wave_prefix(const FrameArgs& a, uint32_t s, uint32_t& tot) {
+    const int wid = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+    uint32_t wpre = 0;
+    tot = 0;
+    for (int w = 0; w < nwaves; ++w) {
+        const uint32_t pc = (uint32_t)__popcll(G(a.vbits)[(size_t)s * 16 + w]);
+        wpre += (w < wid) ? pc : 0u;
+        tot += pc;
+    }
+    return wpre;
+}
+
+// k_emit for rollbuffer segments (kSelSegs per block, as k_mask): blocks without kept items leave
+// after one load; otherwise every load of the block's segments is issued together (validity words,
+// ring points, the block's transform), then the points are transformed to the world frame
+// (transform_points_indirect with the world matrix) and written in order after the depth points.
+__device__ __forceinline__ void sel_emit_block(const FrameArgs& a, uint32_t sb, uint32_t* s_hist,
+                                               uint32_t* s_red, uint32_t* s_scnt,
+                                               uint32_t* s_mark) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int nwaves = blockDim.x >> 6;
+    const uint32_t B = blockDim.x, i = threadIdx.x;
+    const uint32_t seg0 = a.depth_segs + sb * kSelSegs;
+    const uint32_t nh = min(kSelSegs, a.total_segs - seg0);
+    const bool last = blockIdx.x == gridDim.x - 1;
+    const uint32_t c = i < nh ? G(a.seg_counts)[seg0 + i] : 0u;
+    if (!__syncthreads_or(c != 0u) && !(a.fused_prefix && last)) return;
+    uint32_t* s_wcnt = s_scnt + kSelSegs;  // [kSelSegs][16] valid items per wave
+    if (i < kSelSegs) s_scnt[i] = c;
+    for (uint32_t j = i; j < (1u << kMarkCacheBits); j += B) s_mark[j] = 0xFFFFFFFFu;
+    if (a.key_hist)
+        for (uint32_t j = i; j < a.npasses * 256; j += B) s_hist[j] = 0;
+    if (a.fused_prefix) prefix_partials(a, seg0, s_red);
+    const uint32_t si0 = sb * kSelSegs * B;
+    const SelSeg g = sel_seg(a, si0);
+    unsigned long long m[kSelSegs];
+#pragma unroll
+    for (uint32_t j = 0; j < kSelSegs; ++j)
+        m[j] = j < nh ? G(a.vbits)[(size_t)(seg0 + j) * 16 + wid] : 0ull;
+    const gptr<const float> T0 = G(a.tfw + 16 * (size_t)g.tf0);
+    float tw[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) tw[q] = T0[q];
+    float4 sp[kSelSegs];
+#pragma unroll
+    for (uint32_t j = 0; j < kSelSegs; ++j) {
+        const uint32_t si = si0 + j * B + i;
+        sp[j] = ((m[j] >> lane) & 1ull) && si < a.sel_count ? sel_point(a, g, si)
+                                                              : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (lane == 0) s_wcnt[j * 16 + wid] = (uint32_t)__popcll(m[j]);
+    }
+    __syncthreads();
+    uint32_t run = 0;
+    if (a.fused_prefix) {
+        for (int w = 0; w < nwaves; ++w) run += s_red[w];
+    } else {
+        run = G(a.seg_offsets)[seg0];
+    }
+    const unsigned long long ltm = lanemask_lt();
+#pragma unroll
+    for (uint32_t j = 0; j < kSelSegs; ++j) {
+        const uint32_t si = si0 + j * B + i;
+        const bool valid = ((m[j] >> lane) & 1ull) && si < a.sel_count;
+        uint32_t wpre = 0;
+        for (int w = 0; w < wid; ++w) wpre += s_wcnt[j * 16 + w];
+        uint32_t key = 0xFFFFFFFFu;
+        if (valid) {
+            const uint32_t pos = run + wpre + (uint32_t)__popcll(m[j] & ltm);
+            const float x = sp[j].x, y = sp[j].y, z = sp[j].z;
+            float4 w;
+            if (si < g.next) {
+                w = make_float4(mrow(tw + 0, x, y, z, 1.0f), mrow(tw + 4, x, y, z, 1.0f),
+                                mrow(tw + 8, x, y, z, 1.0f), mrow(tw + 12, x, y, z, 1.0f));
+            } else {  // a later sequence inside this block (rare)
+                const gptr<const float> Tw = G(a.tfw + 16 * (size_t)sel_tf(a, si));
+                w = make_float4(mrow(Tw + 0, x, y, z, 1.0f), mrow(Tw + 4, x, y, z, 1.0f),
+                                mrow(Tw + 8, x, y, z, 1.0f), mrow(Tw + 12, x, y, z, 1.0f));
+            }
+            gst4(a.out_pts, pos, w);
+            if (a.do_voxel) {
+                key = voxel_key(w.x, w.y, w.z, a.vlo, a.vcs, a.gmax, a.gs);
+                G(a.out_coords)[pos] = key;
+            }
+        }
+        if (a.do_voxel && j < nh && s_scnt[j]) mark_and_count(a, valid, key, s_hist, s_mark);
+        run += s_scnt[j];
+    }
+    if (a.fused_prefix && last && threadIdx.x == 0) *G(a.out_count) = run;
+    flush_hist(a, s_hist);
+}
+
+// Pass 2: item-ordered emission, one block per depth segment.  Each valid item recomputes its
+// world point with the same f32 ops as pass 1 and writes it at segment offset + rank: stable pixel
+// order, cameras in add order, selected rollbuffer points after the depth points
+// (fusion.cpp:1525,1559).  Optionally the voxel key (compute_voxel_coords), the occupancy mark
+// (no-return atomic OR, issued once per run of equal keys in a wave) and the key digit
+// histogram.  The segment offset is the sum of the preceding counts (<= kFusedPrefixSegs
+// segments) or k_scan_counts' result.
 __global__ __launch_bounds__(1024) void k_emit(FrameArgs a) {
     __shared__ uint32_t s_hist[4 * 256];
     __shared__ uint32_t s_red[16];
+    __shared__ uint32_t s_mark[1u << kMarkCacheBits];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int nwaves = blockDim.x >> 6;
     const uint32_t s = blockIdx.x;
+    for (uint32_t j = threadIdx.x; j < (1u << kMarkCacheBits); j += blockDim.x) s_mark[j] = 0xFFFFFFFFu;
     const gptr<const CamDesc> cams = G(cam_table(a));
     if (a.key_hist)
         for (uint32_t i = threadIdx.x; i < a.npasses * 256; i += blockDim.x) s_hist[i] = 0;
-    if (a.fused_prefix) {
-        uint32_t sum = 0;
-        for (uint32_t t = threadIdx.x; t < s; t += blockDim.x) sum += G(a.seg_counts)[t];
-        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
-        if (lane == 0) s_red[wid] = sum;
-    }
+    if (a.fused_prefix) prefix_partials(a, s, s_red);
     // the segment's geometry and the thread's item source, loaded before the barrier
-    const bool depth = s < a.depth_segs;
     const uint32_t i = threadIdx.x;
     int k = 0;
-    uint32_t y = 0, x0 = 0, len = 0, item0 = 0;
-    if (depth) {
-        for (int c = 0; c < a.ncams; ++c)
-            if (cams[c].emit && s >= cams[c].seg0 && s < cams[c].seg0 + cams[c].nseg) k = c;
-        const uint32_t j = s - cams[k].seg0;
-        y = j / cams[k].nchunk;
-        x0 = (j - y * cams[k].nchunk) * cams[k].segw;
-        len = min(cams[k].segw, cams[k].W - x0);
-        item0 = (uint32_t)cams[k].off + y * cams[k].W + x0;
-    } else {
-        item0 = a.depth_total + (s - a.depth_segs) * blockDim.x;
-        len = min((uint32_t)blockDim.x, a.depth_total + a.sel_count - item0);
-    }
+    for (int c = 0; c < a.ncams; ++c)
+        if (cams[c].emit && s >= cams[c].seg0 && s < cams[c].seg0 + cams[c].nseg) k = c;
+    const uint32_t j = s - cams[k].seg0;
+    const uint32_t y = j / cams[k].nchunk;
+    const uint32_t x0 = (j - y * cams[k].nchunk) * cams[k].segw;
+    const uint32_t len = min(cams[k].segw, cams[k].W - x0);
     const unsigned long long m = G(a.vbits)[(size_t)s * 16 + wid];
     const bool valid = i < len && ((m >> lane) & 1ull);
     uint32_t dval = 0;
-    float4 sp = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (valid) {
-        if (depth)
-            dval = G(cams[k].depth)[y * cams[k].W + x0 + i];
-        else
-            sp = gld4(a.ring, (a.ring_first + (item0 - a.depth_total + i)) % a.ring_cap);
-    }
+    if (valid) dval = G(cams[k].depth)[y * cams[k].W + x0 + i];
     __syncthreads();
     uint32_t base = 0;
     if (a.fused_prefix) {
@@ -741,69 +1026,38 @@ __global__ __launch_bounds__(1024) void k_emit(FrameArgs a) {
     } else {
         base = G(a.seg_offsets)[s];
     }
-    // prefix of the valid counts of the waves before this one (uniform word loads)
-    uint32_t wpre = 0, tot = 0;
-    for (int w = 0; w < nwaves; ++w) {
-        const uint32_t pc = (uint32_t)__popcll(G(a.vbits)[(size_t)s * 16 + w]);
-        wpre += (w < wid) ? pc : 0u;
-        tot += pc;
-    }
+    uint32_t tot;
+    const uint32_t wpre = wave_prefix(a, s, tot);
     if (a.fused_prefix && s == gridDim.x - 1 && threadIdx.x == 0) *G(a.out_count) = base + tot;
-    const unsigned long long ltm = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const unsigned long long ltm = lanemask_lt();
     uint32_t key = 0xFFFFFFFFu;
     if (valid) {
         const uint32_t pos = base + wpre + (uint32_t)__popcll(m & ltm);
-        float4 w;
-        if (depth) {
-            const uint32_t x = x0 + i;
-            const float zz = (float)dval * cams[k].scale;
-            const float px = G(cams[k].xn)[x] * zz, py = G(cams[k].yn)[y] * zz, pz = zz;
-            w = make_float4(mrow(cams[k].Tw + 0, px, py, pz, 1.0f),
-                            mrow(cams[k].Tw + 4, px, py, pz, 1.0f),
-                            mrow(cams[k].Tw + 8, px, py, pz, 1.0f),
-                            mrow(cams[k].Tw + 12, px, py, pz, 1.0f));
-        } else {
-            const uint32_t si = item0 - a.depth_total + i;
-            const gptr<const float> Tw = G(a.tfw + 16 * (size_t)sel_tf(a, si));
-            w = make_float4(mrow(Tw + 0, sp.x, sp.y, sp.z, 1.0f), mrow(Tw + 4, sp.x, sp.y, sp.z, 1.0f),
-                            mrow(Tw + 8, sp.x, sp.y, sp.z, 1.0f), mrow(Tw + 12, sp.x, sp.y, sp.z, 1.0f));
-        }
+        const uint32_t x = x0 + i;
+        const float zz = (float)dval * cams[k].scale;
+        const float px = G(cams[k].xn)[x] * zz, py = G(cams[k].yn)[y] * zz, pz = zz;
+        const float4 w = make_float4(mrow(cams[k].Tw + 0, px, py, pz, 1.0f),
+                                     mrow(cams[k].Tw + 4, px, py, pz, 1.0f),
+                                     mrow(cams[k].Tw + 8, px, py, pz, 1.0f),
+                                     mrow(cams[k].Tw + 12, px, py, pz, 1.0f));
         gst4(a.out_pts, pos, w);
         if (a.do_voxel) {
             key = voxel_key(w.x, w.y, w.z, a.vlo, a.vcs, a.gmax, a.gs);
             G(a.out_coords)[pos] = key;
         }
     }
-    if (a.do_voxel) {
-        // runs of equal keys among the wave's valid lanes: the first lane of a run marks / counts
-        const unsigned long long vm = __ballot(valid);
-        const unsigned long long below = vm & ltm;
-        const int prev = below ? 63 - __clzll((long long)below) : -1;
-        const uint32_t pkey = __shfl(key, prev < 0 ? 0 : prev, 64);
-        const bool leader = valid && (prev < 0 || pkey != key);
-        const unsigned long long lm = __ballot(leader);
-        if (leader) {
-            if (a.marks)
-                __hip_atomic_fetch_or(G(a.marks + (key >> 5)), 1u << (key & 31u),
-                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (a.key_hist) {
-                const unsigned long long after = lm & ~(ltm | (1ull << lane));
-                const unsigned long long upto =
-                    after ? ((1ull << (__ffsll((long long)after) - 1)) - 1ull) : ~0ull;
-                const uint32_t rl = (uint32_t)__popcll(vm & ~ltm & upto);
-                for (uint32_t p = 0; p < a.npasses; ++p)
-                    atomicAdd(&s_hist[p * 256 + ((key >> (8 * p)) & 0xFFu)], rl);
-            }
-        }
-    }
-    if (a.key_hist) {
-        __syncthreads();
-        const gptr<uint32_t> rep = G(a.key_hist + (blockIdx.x % kHistReps) * 1024u);
-        for (uint32_t j = threadIdx.x; j < a.npasses * 256; j += blockDim.x)
-            if (s_hist[j])
-                __hip_atomic_fetch_add(rep + j, s_hist[j], __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (a.do_voxel) mark_and_count(a, valid, key, s_hist, s_mark);
+    flush_hist(a, s_hist);
+}
+
+// Pass 2 over the rollbuffer segments (its own kernel: the batched loads of sel_emit_block need
+// registers the depth emission does not, and would halve its occupancy).
+__global__ __launch_bounds__(1024) void k_emit_sel(FrameArgs a) {
+    __shared__ uint32_t s_hist[4 * 256];
+    __shared__ uint32_t s_red[16];
+    __shared__ uint32_t s_scnt[kSelSegs * 17];
+    __shared__ uint32_t s_mark[1u << kMarkCacheBits];
+    sel_emit_block(a, blockIdx.x, s_hist, s_red, s_scnt, s_mark);
 }
 
 struct HookScope {  // begin/end of one profiled launch
@@ -819,30 +1073,45 @@ struct HookScope {  // begin/end of one profiled launch
 
 hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
     if (a.total_segs == 0) return hipMemsetAsync(a.out_count, 0, 4, s);
+    // one block per depth segment, one per kSelSegs rollbuffer segments
+    const uint32_t blocks = a.depth_segs + (a.total_segs - a.depth_segs + kSelSegs - 1) / kSelSegs;
     {
         HookScope hs(hook, GDF_KERNEL_MASK);
         const size_t lds = (size_t)a.band_lds;
         if (a.rot45)
-            hipLaunchKernelGGL(k_mask<true>, dim3(a.total_segs), dim3(a.seg_threads), lds, s, a);
+            hipLaunchKernelGGL(k_mask<true>, dim3(blocks), dim3(a.seg_threads), lds, s, a);
         else
-            hipLaunchKernelGGL(k_mask<false>, dim3(a.total_segs), dim3(a.seg_threads), lds, s, a);
+            hipLaunchKernelGGL(k_mask<false>, dim3(blocks), dim3(a.seg_threads), lds, s, a);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
     if (!a.fused_prefix) {
         HookScope hs(hook, GDF_KERNEL_SCAN);
-        hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, a.seg_counts, a.total_segs,
-                           a.seg_offsets, a.out_count);
+        const uint32_t chunks = (a.total_segs + 4095u) / 4096u;
+        uint32_t* partial = a.seg_offsets + scan_partials_offset(a.total_segs);
+        hipLaunchKernelGGL(k_scan_reduce, dim3(chunks), dim3(1024), 0, s, a.seg_counts,
+                           a.total_segs, partial);
         hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_scan_counts, dim3(chunks), dim3(1024), 0, s, a.seg_counts,
+                           a.total_segs, a.seg_offsets, a.out_count, partial);
+        e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
     HookScope hs(hook, GDF_KERNEL_EMIT);
-    hipLaunchKernelGGL(k_emit, dim3(a.total_segs), dim3(a.seg_threads), 0, s, a);
+    if (a.depth_segs) {
+        hipLaunchKernelGGL(k_emit, dim3(a.depth_segs), dim3(a.seg_threads), 0, s, a);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    if (blocks > a.depth_segs)  // the rollbuffer blocks' total (fused prefix) is written last
+        hipLaunchKernelGGL(k_emit_sel, dim3(blocks - a.depth_segs), dim3(a.seg_threads), 0, s, a);
     return hipGetLastError();
 }
 
 const void* frame_kernel(int which, int rot45) {
     if (which == 1) return reinterpret_cast<const void*>(&k_emit);
+    if (which == 2) return reinterpret_cast<const void*>(&k_emit_sel);
     return rot45 ? reinterpret_cast<const void*>(&k_mask<true>)
                  : reinterpret_cast<const void*>(&k_mask<false>);
 }
@@ -1186,67 +1455,71 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
     __shared__ uint32_t s_tile, s_epoch;
     const uint32_t n = *count;
     const uint32_t ntiles = (n + kTile - 1) / kTile;
-    if (blockIdx.x >= ntiles) return;  // launched for the capacity; takes no ticket
-    if (threadIdx.x == 0) {
-        uint32_t ep;
-        s_tile = take_ticket_epoch(tile_ctr, ntiles, epoch_word, ep);
-        s_epoch = ep;
-    }
-    for (uint32_t i = threadIdx.x; i < 4 * 256; i += kSortThreads) (&s_cnt[0][0])[i] = 0;
-    __syncthreads();
-    const uint32_t tile = s_tile, epoch = s_epoch;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const unsigned long long ltm = lanemask_lt();
+    const Tickets tk = tickets(ntiles, grid_block0);
+    if (blockIdx.x >= tk.nblk) return;
+    if (threadIdx.x == 0) s_epoch = read_epoch(epoch_word);
+    // the digit bases do not depend on the tile
+    s_base[threadIdx.x] = digit_base(ghist, s_wave);
+    for (bool first = true;; first = false) {  // persistent: tiles in ticket order
+        if (!first && tk.oneshot) return;
+        if (threadIdx.x == 0) s_tile = next_ticket(tile_ctr, tk, epoch_word, s_epoch);
+        for (uint32_t i = threadIdx.x; i < 4 * 256; i += kSortThreads) (&s_cnt[0][0])[i] = 0;
+        __syncthreads();
+        const uint32_t tile = s_tile, epoch = s_epoch;
+        if (tile >= ntiles) return;  // block-uniform
 
-    uint32_t key[PT], val[PT], rank[PT];
-    const uint32_t wbase = tile * kTile + w * 64 * PT;
+        uint32_t key[PT], val[PT], rank[PT];
+        const uint32_t wbase = tile * kTile + w * 64 * PT;
 #pragma unroll
-    for (int j = 0; j < PT; ++j) {
-        const uint32_t idx = wbase + j * 64 + lane;
-        const bool ok = idx < n;
-        key[j] = ok ? kin[idx] : 0xFFFFFFFFu;
-        val[j] = ok ? (vin ? vin[idx] : idx) : 0u;
-    }
-#pragma unroll
-    for (int j = 0; j < PT; ++j) {
-        const uint32_t idx = wbase + j * 64 + lane;
-        const bool ok = idx < n;
-        const uint32_t d = (key[j] >> shift) & 0xFFu;
-        unsigned long long m = __ballot(ok);
-        for (uint32_t b = 0; b < dbits; ++b) {
-            const bool bit = (d >> b) & 1u;
-            const unsigned long long bb = __ballot(bit);
-            m &= bit ? bb : ~bb;
+        for (int j = 0; j < PT; ++j) {
+            const uint32_t idx = wbase + j * 64 + lane;
+            const bool ok = idx < n;
+            key[j] = ok ? kin[idx] : 0xFFFFFFFFu;
+            val[j] = ok ? (vin ? vin[idx] : idx) : 0u;
         }
-        const uint32_t before = (uint32_t)__popcll(m & ltm);
-        uint32_t base = 0;
-        if (ok) base = s_cnt[w][d];
-        rank[j] = base + before;
-        __builtin_amdgcn_wave_barrier();
-        if (ok && before == 0) s_cnt[w][d] = base + (uint32_t)__popcll(m);
-        __builtin_amdgcn_wave_barrier();
-    }
-    __syncthreads();
-    const uint32_t d = threadIdx.x;
-    uint32_t tot = 0;
 #pragma unroll
-    for (int ww = 0; ww < 4; ++ww) {
-        const uint32_t c = s_cnt[ww][d];
-        s_cnt[ww][d] = tot;
-        tot += c;
-    }
-    s_base[d] = digit_base(ghist, s_wave);
-    s_excl[d] = lookback2_chan(status, gstatus, tile, ntiles, d, tot, epoch, err);
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < PT; ++j) {
-        const uint32_t idx = wbase + j * 64 + lane;
-        if (idx < n) {
-            const uint32_t dd = (key[j] >> shift) & 0xFFu;
-            const uint32_t pos = s_base[dd] + s_excl[dd] + s_cnt[w][dd] + rank[j];
-            kout[pos] = key[j];
-            vout[pos] = val[j];
+        for (int j = 0; j < PT; ++j) {
+            const uint32_t idx = wbase + j * 64 + lane;
+            const bool ok = idx < n;
+            const uint32_t d = (key[j] >> shift) & 0xFFu;
+            unsigned long long m = __ballot(ok);
+            for (uint32_t b = 0; b < dbits; ++b) {
+                const bool bit = (d >> b) & 1u;
+                const unsigned long long bb = __ballot(bit);
+                m &= bit ? bb : ~bb;
+            }
+            const uint32_t before = (uint32_t)__popcll(m & ltm);
+            uint32_t base = 0;
+            if (ok) base = s_cnt[w][d];
+            rank[j] = base + before;
+            __builtin_amdgcn_wave_barrier();
+            if (ok && before == 0) s_cnt[w][d] = base + (uint32_t)__popcll(m);
+            __builtin_amdgcn_wave_barrier();
         }
+        __syncthreads();
+        const uint32_t d = threadIdx.x;
+        uint32_t tot = 0;
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) {
+            const uint32_t c = s_cnt[ww][d];
+            s_cnt[ww][d] = tot;
+            tot += c;
+        }
+        s_excl[d] = lookback2_chan(status, gstatus, tile, ntiles, d, tot, epoch, err);
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < PT; ++j) {
+            const uint32_t idx = wbase + j * 64 + lane;
+            if (idx < n) {
+                const uint32_t dd = (key[j] >> shift) & 0xFFu;
+                const uint32_t pos = s_base[dd] + s_excl[dd] + s_cnt[w][dd] + rank[j];
+                kout[pos] = key[j];
+                vout[pos] = val[j];
+            }
+        }
+        __syncthreads();  // LDS reused by the next tile
     }
 }
 
@@ -1262,6 +1535,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
 // Block 0 also clears the digit histogram for the next voxelize (its last reader was the final
 // sort pass).
 constexpr int kStagePts = 1024;  // points of a tile's groups staged in LDS (16 KiB)
+constexpr uint32_t kPersistBlocks = 2048;  // blocks of a persistent sort / group launch
 constexpr int kSmallGroup = 16;  // groups summed by one thread; longer ones by a wave
 
 __device__ __forceinline__ void group_corner(uint32_t key, const VoxelParams& vp, float* o) {
@@ -1289,20 +1563,22 @@ __global__ __launch_bounds__(kGroupThreads) void k_group(
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t n = *count;
     const uint32_t ntiles = (n + kGroupThreads - 1) / kGroupThreads;
-    if (blockIdx.x == 0)
+    if (blockIdx.x == 0) {
         for (uint32_t i = threadIdx.x; i < kHistWords; i += kGroupThreads) hist[i] = 0;
-    if (blockIdx.x >= ntiles) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) *out_count = 0;  // n == 0
-        return;
+        if (ntiles == 0 && threadIdx.x == 0) *out_count = 0;  // n == 0
     }
+    const Tickets tk = tickets(ntiles, gridDim.x);
+    if (blockIdx.x >= tk.nblk) return;
+    if (threadIdx.x == 0) s_epoch = read_epoch(epoch_word);
+    for (bool first = true;; first = false) {  // persistent: tiles in ticket order
+    if (!first && tk.oneshot) return;
     if (threadIdx.x == 0) {
-        uint32_t ep;
-        s_tile = take_ticket_epoch(tile_ctr, ntiles, epoch_word, ep);
-        s_epoch = ep;
+        s_tile = next_ticket(tile_ctr, tk, epoch_word, s_epoch);
         s_nbig = 0;
     }
     __syncthreads();
     const uint32_t tile = s_tile, epoch = s_epoch;
+    if (tile >= ntiles) return;  // block-uniform
     const uint32_t i = tile * kGroupThreads + threadIdx.x;
     const uint32_t tend = min(n, (tile + 1) * kGroupThreads);
     const uint32_t key = i < n ? keys[i] : 0u;
@@ -1334,17 +1610,27 @@ __global__ __launch_bounds__(kGroupThreads) void k_group(
             if (tile == ntiles - 1) *out_count = ex + total;
         }
     } else if (wid == 1 && total) {
-        uint32_t e = n;
+        // end of the tile's last group = first index >= tend whose (sorted) key exceeds the
+        // tile's last key: the next 64 keys, then a 64-ary search of the rest (groups of
+        // thousands of points: a few round trips instead of one per 64 keys)
         const uint32_t lastkey = keys[tend - 1];
-        for (uint32_t b = tend; b < n; b += 64) {
-            const uint32_t j = b + lane;
-            const unsigned long long ch = __ballot(j < n && keys[j] != lastkey);
+        uint32_t lo = tend, hi = n;  // keys[tend, lo) <= lastkey; hi = n or keys[hi] > lastkey
+        while (lo < hi) {
+            const uint32_t len = hi - lo;
+            const uint32_t step = len <= 64u || lo == tend ? 1u : (len + 63u) / 64u;
+            const uint32_t j = lo + (uint32_t)lane * step;
+            const unsigned long long ch = __ballot(j < hi && keys[j] > lastkey);
             if (ch) {
-                e = b + (uint32_t)(__ffsll((long long)ch) - 1);
-                break;
+                const uint32_t f = (uint32_t)(__ffsll((long long)ch) - 1);
+                hi = lo + f * step;
+                if (step == 1u) break;
+                lo = f ? lo + (f - 1u) * step + 1u : lo;
+            } else {
+                const uint32_t lastp = lo + min(63u, (len - 1u) / step) * step;  // last probe
+                lo = lastp + 1u;
             }
         }
-        if (lane == 0) s_start[total] = e;
+        if (lane == 0) s_start[total] = hi;
     }
     if (average) {
 #pragma unroll
@@ -1354,7 +1640,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_group(
         }
     }
     __syncthreads();
-    if (total == 0) return;  // block-uniform
+    if (total == 0) continue;  // block-uniform (nothing of this tile is read after the barrier)
     // one group per thread: staged groups summed here in index order, the rest queued for waves
     if (threadIdx.x < total) {
         const uint32_t g = s_excl + threadIdx.x;
@@ -1456,6 +1742,8 @@ __global__ __launch_bounds__(kGroupThreads) void k_group(
             out[4 * (size_t)g + lane] = lane < 3 ? acc / fc : acc;
         }
     }
+    __syncthreads();  // LDS reused by the next tile
+    }
 }
 
 size_t voxelize_status_words(uint32_t nmax) {
@@ -1484,7 +1772,8 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
     const uint32_t npasses = a.key_bits == 0 ? 1u : (a.key_bits + 7) / 8;
     const int pt = a.sort_pt == 4 || a.sort_pt == 8 ? a.sort_pt : 16;
     const uint32_t tile = kSortThreads * pt;
-    const uint32_t sort_tiles = (a.nmax + tile - 1) / tile;
+    // persistent blocks (ticket loop): at most kPersistBlocks, fewer when the capacity is small
+    const uint32_t sort_tiles = std::min<uint32_t>((a.nmax + tile - 1) / tile, kPersistBlocks);
     hipError_t e;
     if (!a.hist_ready) {
         unsigned hb = grid_blocks(a.nmax, 256 * 16);
@@ -1512,7 +1801,8 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
         kin = kbuf[p & 1];
         vin = vbuf[p & 1];
     }
-    const uint32_t group_tiles = (a.nmax + kGroupThreads - 1) / kGroupThreads;
+    const uint32_t group_tiles =
+        std::min<uint32_t>((a.nmax + kGroupThreads - 1) / kGroupThreads, kPersistBlocks);
     HookScope hs(hook, GDF_KERNEL_GROUP);
     hipLaunchKernelGGL(k_group, dim3(group_tiles ? group_tiles : 1), dim3(kGroupThreads), 0, s, kin,
                        vin, a.count, a.pts, reinterpret_cast<float*>(a.out), a.out_count,

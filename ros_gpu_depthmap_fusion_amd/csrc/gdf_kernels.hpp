@@ -25,6 +25,12 @@ hipError_t launch_tables(uint32_t W, uint32_t H, float fx, float fy, float cx, f
 // fused depth + rollbuffer compaction (convert, flying, crop, transform_indirect, apply,
 // optional voxel keys + occupancy marks); needs no memset (epoch-tagged look-back, tickets)
 hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook = nullptr);
+// the seg_offsets buffer also holds the chunk partials of the multi-block count scan:
+// [scan_partials_offset(segs), + ceil(segs / 4096)) words
+inline uint32_t scan_partials_offset(uint32_t segs) { return (segs + 63u) & ~63u; }
+inline size_t seg_offsets_words(uint32_t segs) {
+    return scan_partials_offset(segs) + (segs + 4095u) / 4096u + 1u;
+}
 // the compaction kernels (0: k_mask, 1: k_emit) as launched for `rot45` (graph node lookup)
 const void* frame_kernel(int which, int rot45);
 

@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--ring", type=int, default=4, help="distinct device-resident sequences/frames")
     ap.add_argument("--profile-steps", type=int, default=5)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--corners", action="store_true",
+                    help="voxelize without averaging (voxel corners; diagnostics)")
     args = ap.parse_args()
 
     import numpy as np
@@ -59,6 +61,7 @@ def main():
 
     p = ComponentParams()
     p.ps_timespan = (args.window - 0.5) / 30.0
+    p.voxel_average = not args.corners
     eng = GPUDepthmapFusion(0)
     pc_async = p.to_c(lidar.T_world, lidar.T_crop, False, False)
     pc_sync = p.to_c(lidar.T_world, lidar.T_crop, True, False)
@@ -88,6 +91,10 @@ def main():
     st = eng.rollbuffer_state()
     S, N, G = st.selection_point_count, r.num_points, r.num_voxelized
     (gx, gy, gz), ncells = eng.grid_size()
+    _, gsz = np.unique(eng.downloadVoxelCoords(), return_counts=True)  # points per voxel
+    group_sizes = {"max": int(gsz.max()), "p50": int(np.percentile(gsz, 50)),
+                   "p99": int(np.percentile(gsz, 99)),
+                   "points_in_groups_over_4096": int(gsz[gsz > 4096].sum())}
 
     eng.synchronize()
     t0 = time.perf_counter()
@@ -137,6 +144,7 @@ def main():
                                "points (timespan select, transform, crop, compaction, voxelize, "
                                "grid %dx%dx%d)" % (W, H, args.window, P, gx, gy, gz),
                    "selected_points": S, "points_after_crop": N, "voxels": G,
+                   "points_per_voxel": group_sizes,
                    "grid_cells": ncells},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
