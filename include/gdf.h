@@ -243,7 +243,7 @@ enum gdf_kernel_slot {
     GDF_KERNEL_EMIT = 6,       /* k_emit: ordered compaction + voxel keys + marks + digit hist    */
     GDF_KERNEL_SORT = 7,       /* k_sort_pass: one radix pass (the first also updates the grid)   */
     GDF_KERNEL_GROUP = 8,      /* k_group: voxel groups of the sorted keys + ordered per-voxel means */
-    GDF_KERNEL_RESERVED9 = 9,
+    GDF_KERNEL_SEL = 9,        /* k_sel + k_sel_place: single-pass rollbuffer compaction      */
     GDF_KERNEL_EVENT_FLOOR = 10, /* an event pair around no launch: the timing method's own cost    */
     GDF_KERNEL_SLOTS = 11
 };

@@ -17,7 +17,8 @@ constexpr int kArgCams = 4;           // camera descriptors passed in the kernel
 constexpr int kHalo = 8;              // band rows/columns staged around a segment: min(F, 8)
 constexpr uint32_t kSegItems = 1024;  // items per compaction segment (max)
 constexpr uint32_t kFusedPrefixSegs = 4096;  // up to this many segments k_emit sums the counts
-constexpr uint32_t kSelSegs = 8;      // rollbuffer segments per k_mask / k_emit block
+constexpr uint32_t kSelSegs = 8;      // rollbuffer points per k_sel thread
+constexpr uint32_t kSelThreads = 512; // k_sel block: a tile is kSelSegs * kSelThreads points
 constexpr int kSortThreads = 256;
 // the voxel-key digit histogram is accumulated into kHistReps replicas of [4 passes][256 digits]
 // (block b adds into replica b % kHistReps): same-address atomics from hundreds of blocks
@@ -31,7 +32,7 @@ constexpr uint32_t kSpinLimit = 1u << 26;                   // bounded look-back
 // Device-wide counters: monotonically increasing tile tickets (the host passes each launch's
 // base, so no per-launch memset) and the global digit histogram of the voxel keys.
 // per-stream device counters (u64 words, low 32 bits used): tile tickets, look-back epoch
-enum CounterSlot { kCtrFrame = 0, kCtrSort0 = 1, kCtrGroup = 5, kCtrEpoch = 6, kCtrSlots = 8 };
+enum CounterSlot { kCtrSel = 0, kCtrSort0 = 1, kCtrGroup = 5, kCtrEpoch = 6, kCtrSlots = 8 };
 
 // engine-order of historic-grid updates across streams (grid_seq_enter / grid_seq_leave)
 struct GridSeq {
@@ -74,7 +75,7 @@ struct FrameArgs {
     int32_t ncams;
     uint32_t depth_total;       // ΣP of emitting cameras' index space
     uint32_t depth_segs;        // segments over the depth pixels
-    uint32_t total_segs;        // + ceil(sel_count / kSegItems) rollbuffer segments
+    uint32_t total_segs;        // segments of the two-pass (depth) compaction: depth_segs
     // flying-pixel filter (sh/filter_flying_pixels.glsl)
     int32_t do_flying;
     uint32_t F;
@@ -93,6 +94,15 @@ struct FrameArgs {
     const uint32_t* seg_tf;     // transform index of that sequence
     const float* tfw;           // row-major T_world_move·T_move per selected sequence
     const float* tfc;
+    // rollbuffer compaction (k_sel): tiles of kSelSegs * kSelThreads points, survivors staged at
+    // tile-local ranks, then placed by tile offsets (k_sel_place) behind the depth points
+    uint32_t sel_tiles;
+    uint32_t* sel_counts;       // [sel_tiles] survivors per tile
+    uint32_t* sel_offsets;      // [seg_offsets_words(sel_tiles)] exclusive scan (+ scan partials)
+    float4* sel_pts;            // staged survivors: tile t's at [t * tile, + count) ...
+    uint32_t* sel_keys;         // ... and their voxel keys
+    uint32_t* sel_total;        // survivors of the selection
+    uint32_t* final_count;      // depth + rollbuffer survivors (out_count then holds the depth part)
     // voxel keys + occupancy marks (compute_voxel_coords + voxel_grid_occupancy_of_points)
     int32_t do_voxel;
     float vlo[3], vcs[3], gmax[3];

@@ -174,7 +174,10 @@ bool ros_time_minus(uint32_t sec, uint32_t nsec, double seconds, uint32_t* os, u
     return true;
 }
 
-enum MiscSlot { kCount = 0, kTileCtr = 1, kErr = 2, kVoxCount = 3, kGridTicket = 4, kMiscWords = 16 };
+enum MiscSlot {
+    kCount = 0, kTileCtr = 1, kErr = 2, kVoxCount = 3, kGridTicket = 4, kDepthCount = 5,
+    kSelTotal = 6, kMiscWords = 16
+};
 
 }  // namespace
 
@@ -195,6 +198,7 @@ struct Slot {
     DevBuf d_khist;                 // digit histogram of the voxel keys [4*256]
     bool khist_pending = false;     // accumulated by the fused compaction, not yet consumed
     DevBuf d_pts, d_coords, d_stage, d_vbits, d_tcounts, d_toffsets;
+    DevBuf d_selpts, d_selkeys, d_selcnt, d_seloff;  // rollbuffer compaction (k_sel)
     DevBuf d_misc;
     uint32_t* h_misc = nullptr;     // pinned
     bool compacted = false, coords_valid = false, marks_set = false;
@@ -854,9 +858,22 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel) {
     a.depth_total = e->depth_total;
     const uint32_t sel = e->sel_inserted ? e->rb.selection_point_count : 0u;
     a.depth_segs = e->mask_blocks;
-    // one item per thread: blocks as wide as the widest segment (rollbuffer segments use the same)
+    // one item per thread: blocks as wide as the widest segment
     a.seg_threads = e->max_segw ? std::max<uint32_t>(64, e->max_segw) : kSegItems;
-    a.total_segs = a.depth_segs + (sel + a.seg_threads - 1) / a.seg_threads;
+    a.total_segs = a.depth_segs;
+    a.sel_tiles = (uint32_t)(((uint64_t)sel + kSelSegs * kSelThreads - 1) / (kSelSegs * kSelThreads));
+    if (a.sel_tiles) {  // rollbuffer compaction (k_sel) + placement behind the depth points
+        Slot& q = e->sl();
+        q.d_selpts.ensure((size_t)a.sel_tiles * kSelSegs * kSelThreads * 16);
+        q.d_selkeys.ensure((size_t)a.sel_tiles * kSelSegs * kSelThreads * 4);
+        q.d_selcnt.ensure((size_t)a.sel_tiles * 4);
+        q.d_seloff.ensure(seg_offsets_words(a.sel_tiles) * 4);
+        a.sel_counts = q.d_selcnt.as<uint32_t>();
+        a.sel_offsets = q.d_seloff.as<uint32_t>();
+        a.sel_pts = q.d_selpts.as<float4>();
+        a.sel_keys = q.d_selkeys.as<uint32_t>();
+        a.sel_total = q.d_misc.as<uint32_t>() + kSelTotal;
+    }
     a.do_flying = e->flying_set ? 1 : 0;
     a.F = e->F;
     a.thr = e->thr;
@@ -878,7 +895,7 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel) {
         // the sequence number a fused grid update of this frame will take (voxelize)
         a.grid_seq_out = e->sl().d_misc.as<uint32_t>() + kGridTicket;
         a.grid_seq = e->grid_ticket;
-        a.marks = marks_ptr(e);
+        a.marks = getenv("GDF_EXP_NOMARKS") ? nullptr : marks_ptr(e);  // (timing experiment only)
         std::memcpy(a.vlo, e->vp.vlo, 12);
         std::memcpy(a.vcs, e->vp.vcs, 12);
         std::memcpy(a.gmax, e->vp.gmax, 12);
@@ -887,12 +904,16 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel) {
         // digit histogram of the keys from the compaction blocks (frees the sort of a separate
         // pass) - but not over a large rollbuffer window, where tens of thousands of blocks would
         // each flush their histogram with device-scope atomics; k_sort_hist counts those keys
-        a.key_hist = a.total_segs <= kFusedPrefixSegs ? e->sl().d_khist.as<uint32_t>() : nullptr;
+        a.key_hist = a.total_segs <= kFusedPrefixSegs && !a.sel_tiles ? e->sl().d_khist.as<uint32_t>()
+                                                                      : nullptr;
         a.npasses = e->key_bits == 0 ? 1u : (e->key_bits + 7) / 8;
     }
     a.out_pts = e->sl().d_pts.as<float4>();
     a.out_coords = e->sl().d_coords.as<uint32_t>();
-    a.out_count = e->sl().d_misc.as<uint32_t>() + kCount;
+    // with rollbuffer points the depth compaction counts into kDepthCount and k_sel_place writes
+    // the frame's total
+    a.out_count = e->sl().d_misc.as<uint32_t>() + (a.sel_tiles ? kDepthCount : kCount);
+    a.final_count = e->sl().d_misc.as<uint32_t>() + kCount;
     const uint32_t segs = std::max<uint32_t>(a.total_segs, 1);
     e->sl().d_vbits.ensure((size_t)segs * 16 * 8);
     e->sl().d_tcounts.ensure((size_t)segs * 4);
@@ -1029,8 +1050,9 @@ void run_fused_frame(gdf_engine* e, int average, uint32_t lifetime) {
     frame_launched(e, true, a.key_hist != nullptr);  // (the launches below follow)
     const VoxelizeArgs v = voxelize_args(e, average, (int)lifetime);
     Slot::Graph& G = e->sl().graph;
+    // (a frame without compaction kernels stores its grid ticket with a memset: not replayable)
     const bool eligible = e->use_graphs && !e->profiling && !e->debug && a.ncams <= kArgCams &&
-                          !e->user_stream;
+                          !e->user_stream && (a.total_segs || a.sel_tiles);
     hipStream_t st = e->s();
     if (eligible && G.valid && same_key(a, v, G.key_a, G.key_v)) {
         void* args[] = {const_cast<FrameArgs*>(&a)};
@@ -1057,7 +1079,8 @@ void run_fused_frame(gdf_engine* e, int average, uint32_t lifetime) {
         HIPCHK(hipGraphGetNodes(G.g, nullptr, &nn));
         std::vector<hipGraphNode_t> nodes(nn);
         HIPCHK(hipGraphGetNodes(G.g, nodes.data(), &nn));
-        const void* fk[3] = {frame_kernel(0, a.rot45), frame_kernel(1, a.rot45), frame_kernel(2, a.rot45)};
+        const void* fk[4] = {frame_kernel(0, a.rot45), frame_kernel(1, a.rot45), frame_kernel(2, a.rot45),
+                             frame_kernel(3, a.rot45)};  // (the count scans take no FrameArgs)
         G.frame_nodes.clear();
         for (hipGraphNode_t n : nodes) {
             hipGraphNodeType t;
@@ -1065,7 +1088,7 @@ void run_fused_frame(gdf_engine* e, int average, uint32_t lifetime) {
             if (t != hipGraphNodeTypeKernel) continue;
             hipKernelNodeParams kp{};
             HIPCHK(hipGraphKernelNodeGetParams(n, &kp));
-            if (kp.func == fk[0] || kp.func == fk[1] || kp.func == fk[2])
+            if (kp.func == fk[0] || kp.func == fk[1] || kp.func == fk[2] || kp.func == fk[3])
                 G.frame_nodes.emplace_back(n, kp);
         }
         if (G.frame_nodes.empty()) fail(GDF_ERR_HIP, "frame graph: compaction kernels not found");

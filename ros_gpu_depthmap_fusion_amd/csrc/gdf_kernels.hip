@@ -556,10 +556,12 @@ __device__ __forceinline__ SelSeg sel_seg(const FrameArgs& a, uint32_t si0) {
         lo = lo + L * step;
         hi = min(hi, lo + step);
     }
+    // block-uniform values: keep them (and what is loaded through them) in scalar registers
+    lo = __builtin_amdgcn_readfirstlane(lo);
     SelSeg g;
     g.si0 = si0;
-    g.tf0 = G(a.seg_tf)[lo];
-    g.next = lo + 1 < a.nseg ? G(a.seg_start)[lo + 1] : 0xFFFFFFFFu;
+    g.tf0 = __builtin_amdgcn_readfirstlane(G(a.seg_tf)[lo]);
+    g.next = __builtin_amdgcn_readfirstlane(lo + 1 < a.nseg ? G(a.seg_start)[lo + 1] : 0xFFFFFFFFu);
     g.r0 = (a.ring_first + si0) % a.ring_cap;
     return g;
 }
@@ -591,43 +593,6 @@ __device__ __forceinline__ uint32_t sel_bits(const FrameArgs& a, const SelSeg& g
     return 7;
 }
 
-// k_mask for rollbuffer segments: one block covers kSelSegs consecutive segments of blockDim
-// selected points (all ring loads in flight together, one transform lookup per block); per
-// segment the validity words and the count, as for a depth segment.
-__device__ __forceinline__ void sel_mask_block(const FrameArgs& a, uint32_t sb, uint32_t* s_scnt) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int nwaves = blockDim.x >> 6;
-    const uint32_t B = blockDim.x, i = threadIdx.x;
-    const uint32_t seg0 = a.depth_segs + sb * kSelSegs;
-    const uint32_t nh = min(kSelSegs, a.total_segs - seg0);
-    const uint32_t si0 = sb * kSelSegs * B;
-    const SelSeg g = sel_seg(a, si0);
-    float4 p[kSelSegs];
-#pragma unroll
-    for (uint32_t j = 0; j < kSelSegs; ++j) {
-        const uint32_t si = si0 + j * B + i;
-        p[j] = (j < nh && si < a.sel_count) ? sel_point(a, g, si) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#pragma unroll
-    for (uint32_t j = 0; j < kSelSegs; ++j) {
-        const uint32_t si = si0 + j * B + i;
-        const bool in = j < nh && si < a.sel_count;
-        const uint32_t bits = in ? sel_bits(a, g, si, p[j]) : 0u;
-        if (a.dbg && in) G(a.dbg)[a.depth_total + si] = (uint8_t)bits;
-        const unsigned long long m = __ballot((bits & 4u) != 0u);
-        if (j < nh && lane == 0) {
-            G(a.vbits)[(size_t)(seg0 + j) * 16 + wid] = m;
-            s_scnt[j * 16 + wid] = (uint32_t)__popcll(m);
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < nh) {
-        uint32_t t = 0;
-        for (int w = 0; w < nwaves; ++w) t += s_scnt[threadIdx.x * 16 + w];
-        G(a.seg_counts)[seg0 + threadIdx.x] = t;
-    }
-}
-
 // Camera descriptors: kernel arguments for up to kArgCams cameras, else the device copy.
 __device__ __forceinline__ const CamDesc* cam_table(const FrameArgs& a) {
     return a.ncams <= kArgCams ? a.cams : a.cams_dev;
@@ -649,7 +614,7 @@ __global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
     __shared__ CamDesc s_cams[kMaxCams];
     __shared__ float s_yn[2 * kHalo + 1];
     __shared__ int s_rowoff[2 * kHalo + 1];
-    __shared__ uint32_t s_cnt[kSelSegs * 16];
+    __shared__ uint32_t s_cnt[16];
     extern __shared__ uint4 s_dyn[];  // band rows (a.band_rowb bytes each), then xn
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int nwaves = blockDim.x >> 6;
@@ -658,10 +623,6 @@ __global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
     const uint32_t n = gridDim.x, q8 = n / 8, r8 = n % 8, xcd = blockIdx.x % 8;
     const uint32_t s = xcd * q8 + min(xcd, r8) + blockIdx.x / 8;
     if (a.grid_seq_out && blockIdx.x == 0 && threadIdx.x == 0) *a.grid_seq_out = a.grid_seq;
-    if (s >= a.depth_segs) {  // block-uniform: rollbuffer segments
-        sel_mask_block(a, s - a.depth_segs, s_cnt);
-        return;
-    }
     load_cams(a, s_cams);
     __syncthreads();
     uint32_t bits = 0;
@@ -908,85 +869,6 @@ __device__ __forceinline__ uint32_t wave_prefix(const FrameArgs& a, uint32_t s, 
     return wpre;
 }
 
-// k_emit for rollbuffer segments (kSelSegs per block, as k_mask): blocks without kept items leave
-// after one load; otherwise every load of the block's segments is issued together (validity words,
-// ring points, the block's transform), then the points are transformed to the world frame
-// (transform_points_indirect with the world matrix) and written in order after the depth points.
-__device__ __forceinline__ void sel_emit_block(const FrameArgs& a, uint32_t sb, uint32_t* s_hist,
-                                               uint32_t* s_red, uint32_t* s_scnt,
-                                               uint32_t* s_mark) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int nwaves = blockDim.x >> 6;
-    const uint32_t B = blockDim.x, i = threadIdx.x;
-    const uint32_t seg0 = a.depth_segs + sb * kSelSegs;
-    const uint32_t nh = min(kSelSegs, a.total_segs - seg0);
-    const bool last = blockIdx.x == gridDim.x - 1;
-    const uint32_t c = i < nh ? G(a.seg_counts)[seg0 + i] : 0u;
-    if (!__syncthreads_or(c != 0u) && !(a.fused_prefix && last)) return;
-    uint32_t* s_wcnt = s_scnt + kSelSegs;  // [kSelSegs][16] valid items per wave
-    if (i < kSelSegs) s_scnt[i] = c;
-    for (uint32_t j = i; j < (1u << kMarkCacheBits); j += B) s_mark[j] = 0xFFFFFFFFu;
-    if (a.key_hist)
-        for (uint32_t j = i; j < a.npasses * 256; j += B) s_hist[j] = 0;
-    if (a.fused_prefix) prefix_partials(a, seg0, s_red);
-    const uint32_t si0 = sb * kSelSegs * B;
-    const SelSeg g = sel_seg(a, si0);
-    unsigned long long m[kSelSegs];
-#pragma unroll
-    for (uint32_t j = 0; j < kSelSegs; ++j)
-        m[j] = j < nh ? G(a.vbits)[(size_t)(seg0 + j) * 16 + wid] : 0ull;
-    const gptr<const float> T0 = G(a.tfw + 16 * (size_t)g.tf0);
-    float tw[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) tw[q] = T0[q];
-    float4 sp[kSelSegs];
-#pragma unroll
-    for (uint32_t j = 0; j < kSelSegs; ++j) {
-        const uint32_t si = si0 + j * B + i;
-        sp[j] = ((m[j] >> lane) & 1ull) && si < a.sel_count ? sel_point(a, g, si)
-                                                              : make_float4(0.f, 0.f, 0.f, 0.f);
-        if (lane == 0) s_wcnt[j * 16 + wid] = (uint32_t)__popcll(m[j]);
-    }
-    __syncthreads();
-    uint32_t run = 0;
-    if (a.fused_prefix) {
-        for (int w = 0; w < nwaves; ++w) run += s_red[w];
-    } else {
-        run = G(a.seg_offsets)[seg0];
-    }
-    const unsigned long long ltm = lanemask_lt();
-#pragma unroll
-    for (uint32_t j = 0; j < kSelSegs; ++j) {
-        const uint32_t si = si0 + j * B + i;
-        const bool valid = ((m[j] >> lane) & 1ull) && si < a.sel_count;
-        uint32_t wpre = 0;
-        for (int w = 0; w < wid; ++w) wpre += s_wcnt[j * 16 + w];
-        uint32_t key = 0xFFFFFFFFu;
-        if (valid) {
-            const uint32_t pos = run + wpre + (uint32_t)__popcll(m[j] & ltm);
-            const float x = sp[j].x, y = sp[j].y, z = sp[j].z;
-            float4 w;
-            if (si < g.next) {
-                w = make_float4(mrow(tw + 0, x, y, z, 1.0f), mrow(tw + 4, x, y, z, 1.0f),
-                                mrow(tw + 8, x, y, z, 1.0f), mrow(tw + 12, x, y, z, 1.0f));
-            } else {  // a later sequence inside this block (rare)
-                const gptr<const float> Tw = G(a.tfw + 16 * (size_t)sel_tf(a, si));
-                w = make_float4(mrow(Tw + 0, x, y, z, 1.0f), mrow(Tw + 4, x, y, z, 1.0f),
-                                mrow(Tw + 8, x, y, z, 1.0f), mrow(Tw + 12, x, y, z, 1.0f));
-            }
-            gst4(a.out_pts, pos, w);
-            if (a.do_voxel) {
-                key = voxel_key(w.x, w.y, w.z, a.vlo, a.vcs, a.gmax, a.gs);
-                G(a.out_coords)[pos] = key;
-            }
-        }
-        if (a.do_voxel && j < nh && s_scnt[j]) mark_and_count(a, valid, key, s_hist, s_mark);
-        run += s_scnt[j];
-    }
-    if (a.fused_prefix && last && threadIdx.x == 0) *G(a.out_count) = run;
-    flush_hist(a, s_hist);
-}
-
 // Pass 2: item-ordered emission, one block per depth segment.  Each valid item recomputes its
 // world point with the same f32 ops as pass 1 and writes it at segment offset + rank: stable pixel
 // order, cameras in add order, selected rollbuffer points after the depth points
@@ -1050,14 +932,104 @@ __global__ __launch_bounds__(1024) void k_emit(FrameArgs a) {
     flush_hist(a, s_hist);
 }
 
-// Pass 2 over the rollbuffer segments (its own kernel: the batched loads of sel_emit_block need
-// registers the depth emission does not, and would halve its occupancy).
-__global__ __launch_bounds__(1024) void k_emit_sel(FrameArgs a) {
-    __shared__ uint32_t s_hist[4 * 256];
-    __shared__ uint32_t s_red[16];
-    __shared__ uint32_t s_scnt[kSelSegs * 17];
+// Selected rollbuffer points (insertSelectedPointSequence + transformPointSequence + crop +
+// applyPointMask + computeVoxelCoords + occupancy marks for the rollbuffer part).  The window is
+// large (10^8 points) and mostly cropped away: each block owns a tile of kSelSegs x blockDim
+// consecutive selected points, reads them once, and writes its survivors (world point + voxel
+// key) at tile-local ranks of a staging area plus the tile's survivor count - no tickets, no
+// look-back, no second read of the window.  After the scan of the tile counts, k_sel_place moves
+// each tile's survivors behind the depth points (whose count is known only after the depth
+// compaction), in selection order.  Stage bits go to the debug buffer as before.
+__global__ __launch_bounds__(kSelThreads) void k_sel(FrameArgs a) {
+    __shared__ uint32_t s_wc[kSelSegs * 16];  // kept items per (segment j, wave w), j-major
     __shared__ uint32_t s_mark[1u << kMarkCacheBits];
-    sel_emit_block(a, blockIdx.x, s_hist, s_red, s_scnt, s_mark);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int nwaves = blockDim.x >> 6;
+    const uint32_t B = blockDim.x, i = threadIdx.x;
+    const uint32_t tile = blockIdx.x;
+    if (a.grid_seq_out && tile == 0 && i == 0) *a.grid_seq_out = a.grid_seq;  // (as k_mask)
+    const uint32_t si0 = tile * kSelSegs * B;
+    const SelSeg g = sel_seg(a, si0);
+    float4 p[kSelSegs];
+#pragma unroll
+    for (uint32_t j = 0; j < kSelSegs; ++j) {
+        const uint32_t si = si0 + j * B + i;
+        p[j] = si < a.sel_count ? sel_point(a, g, si) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    for (uint32_t j = i; j < (1u << kMarkCacheBits); j += B) s_mark[j] = 0xFFFFFFFFu;
+    uint32_t keep = 0;  // bit j: item j of this thread survives the crop
+#pragma unroll
+    for (uint32_t j = 0; j < kSelSegs; ++j) {
+        const uint32_t si = si0 + j * B + i;
+        const bool in = si < a.sel_count;
+        const uint32_t bits = in ? sel_bits(a, g, si, p[j]) : 0u;
+        if (a.dbg && in) G(a.dbg)[a.depth_total + si] = (uint8_t)bits;
+        keep |= ((bits >> 2) & 1u) << j;
+        const unsigned long long m = __ballot((bits & 4u) != 0u);
+        if (lane == 0) s_wc[j * nwaves + wid] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    // exclusive scan of the (segment, wave) counts in item order by wave 0 (<= 128 entries)
+    const uint32_t ne = kSelSegs * (uint32_t)nwaves;
+    if (wid == 0) {
+        const uint32_t e0 = (uint32_t)lane, e1 = (uint32_t)lane + 64u;
+        const uint32_t v0 = e0 < ne ? s_wc[e0] : 0u, v1 = e1 < ne ? s_wc[e1] : 0u;
+        uint32_t x0 = v0, x1 = v1;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y0 = __shfl_up(x0, o, 64), y1 = __shfl_up(x1, o, 64);
+            if (lane >= o) { x0 += y0; x1 += y1; }
+        }
+        const uint32_t tot0 = __shfl(x0, 63, 64), tot1 = __shfl(x1, 63, 64);
+        if (e0 < ne) s_wc[e0] = x0 - v0;
+        if (e1 < ne) s_wc[e1] = tot0 + x1 - v1;
+        if (lane == 0) G(a.sel_counts)[tile] = tot0 + tot1;
+    }
+    __syncthreads();
+    const uint64_t base = (uint64_t)tile * kSelSegs * B;  // the tile's staging slots
+    const unsigned long long ltm = lanemask_lt();
+    const gptr<const float> T0 = G(a.tfw + 16 * (size_t)g.tf0);
+#pragma unroll
+    for (uint32_t j = 0; j < kSelSegs; ++j) {
+        const bool valid = (keep >> j) & 1u;
+        const unsigned long long m = __ballot(valid);
+        if (!m) continue;  // wave-uniform
+        uint32_t key = 0xFFFFFFFFu;
+        if (valid) {
+            const uint32_t si = si0 + j * B + i;
+            const uint64_t pos = base + s_wc[j * nwaves + wid] + (uint32_t)__popcll(m & ltm);
+            const float x = p[j].x, y = p[j].y, z = p[j].z;
+            const gptr<const float> Tw =
+                si < g.next ? T0 : G(a.tfw + 16 * (size_t)sel_tf(a, si));  // (rare: next sequence)
+            const float4 w = make_float4(mrow(Tw + 0, x, y, z, 1.0f), mrow(Tw + 4, x, y, z, 1.0f),
+                                         mrow(Tw + 8, x, y, z, 1.0f), mrow(Tw + 12, x, y, z, 1.0f));
+            gst4(a.sel_pts, pos, w);
+            if (a.do_voxel) {
+                key = voxel_key(w.x, w.y, w.z, a.vlo, a.vcs, a.gmax, a.gs);
+                G(a.sel_keys)[pos] = key;
+            }
+        }
+        if (a.do_voxel) mark_and_count(a, valid, key, nullptr, s_mark);
+    }
+}
+
+// Each tile's staged survivors behind the depth survivors, at the tile's scanned offset
+// (m_points order: depth points first, fusion.cpp:1525,1559), and the frame's total count.
+// A persistent grid walks the tiles; empty tiles cost one load.
+__global__ __launch_bounds__(256) void k_sel_place(FrameArgs a) {
+    const uint32_t d = *G(a.out_count);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *G(a.final_count) = d + *G(a.sel_total);
+    const uint32_t tile_items = kSelSegs * kSelThreads;
+    for (uint32_t t = blockIdx.x; t < a.sel_tiles; t += gridDim.x) {
+        const uint32_t c = G(a.sel_counts)[t];
+        if (!c) continue;
+        const uint32_t o = d + G(a.sel_offsets)[t];
+        const uint64_t src = (uint64_t)t * tile_items;
+        for (uint32_t r = threadIdx.x; r < c; r += blockDim.x) {
+            gst4(a.out_pts, (uint64_t)o + r, gld4(a.sel_pts, src + r));
+            if (a.do_voxel) G(a.out_coords)[o + r] = G(a.sel_keys)[src + r];
+        }
+    }
 }
 
 struct HookScope {  // begin/end of one profiled launch
@@ -1072,46 +1044,60 @@ struct HookScope {  // begin/end of one profiled launch
 };
 
 hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
-    if (a.total_segs == 0) return hipMemsetAsync(a.out_count, 0, 4, s);
-    // one block per depth segment, one per kSelSegs rollbuffer segments
-    const uint32_t blocks = a.depth_segs + (a.total_segs - a.depth_segs + kSelSegs - 1) / kSelSegs;
-    {
-        HookScope hs(hook, GDF_KERNEL_MASK);
-        const size_t lds = (size_t)a.band_lds;
-        if (a.rot45)
-            hipLaunchKernelGGL(k_mask<true>, dim3(blocks), dim3(a.seg_threads), lds, s, a);
-        else
-            hipLaunchKernelGGL(k_mask<false>, dim3(blocks), dim3(a.seg_threads), lds, s, a);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
+    hipError_t e;
+    if (a.total_segs == 0) {  // no depth survivors to count
+        if ((e = hipMemsetAsync(a.out_count, 0, 4, s)) != hipSuccess) return e;
+        if (a.grid_seq_out && !a.sel_tiles &&  // no kernel of this frame stores the ticket
+            (e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(a.grid_seq_out),
+                                   (int)a.grid_seq, 1, s)) != hipSuccess)
+            return e;
+    } else {
+        {
+            HookScope hs(hook, GDF_KERNEL_MASK);
+            const size_t lds = (size_t)a.band_lds;
+            if (a.rot45)
+                hipLaunchKernelGGL(k_mask<true>, dim3(a.total_segs), dim3(a.seg_threads), lds, s, a);
+            else
+                hipLaunchKernelGGL(k_mask<false>, dim3(a.total_segs), dim3(a.seg_threads), lds, s, a);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
+        if (!a.fused_prefix) {
+            HookScope hs(hook, GDF_KERNEL_SCAN);
+            const uint32_t chunks = (a.total_segs + 4095u) / 4096u;
+            uint32_t* partial = a.seg_offsets + scan_partials_offset(a.total_segs);
+            hipLaunchKernelGGL(k_scan_reduce, dim3(chunks), dim3(1024), 0, s, a.seg_counts,
+                               a.total_segs, partial);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            hipLaunchKernelGGL(k_scan_counts, dim3(chunks), dim3(1024), 0, s, a.seg_counts,
+                               a.total_segs, a.seg_offsets, a.out_count, partial);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
+        HookScope hs(hook, GDF_KERNEL_EMIT);
+        hipLaunchKernelGGL(k_emit, dim3(a.total_segs), dim3(a.seg_threads), 0, s, a);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    if (!a.fused_prefix) {
-        HookScope hs(hook, GDF_KERNEL_SCAN);
-        const uint32_t chunks = (a.total_segs + 4095u) / 4096u;
-        uint32_t* partial = a.seg_offsets + scan_partials_offset(a.total_segs);
-        hipLaunchKernelGGL(k_scan_reduce, dim3(chunks), dim3(1024), 0, s, a.seg_counts,
-                           a.total_segs, partial);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_scan_counts, dim3(chunks), dim3(1024), 0, s, a.seg_counts,
-                           a.total_segs, a.seg_offsets, a.out_count, partial);
-        e = hipGetLastError();
-        if (e != hipSuccess) return e;
+    if (a.sel_tiles) {  // rollbuffer points: survivors per tile, tile offsets, placement
+        HookScope hs(hook, GDF_KERNEL_SEL);
+        hipLaunchKernelGGL(k_sel, dim3(a.sel_tiles), dim3(kSelThreads), 0, s, a);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        const uint32_t chunks = (a.sel_tiles + 4095u) / 4096u;
+        uint32_t* partial = a.sel_offsets + scan_partials_offset(a.sel_tiles);
+        hipLaunchKernelGGL(k_scan_reduce, dim3(chunks), dim3(1024), 0, s, a.sel_counts,
+                           a.sel_tiles, partial);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_scan_counts, dim3(chunks), dim3(1024), 0, s, a.sel_counts,
+                           a.sel_tiles, a.sel_offsets, a.sel_total, partial);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_sel_place, dim3(std::min<uint32_t>(a.sel_tiles, 4096u)), dim3(256), 0,
+                           s, a);
     }
-    HookScope hs(hook, GDF_KERNEL_EMIT);
-    if (a.depth_segs) {
-        hipLaunchKernelGGL(k_emit, dim3(a.depth_segs), dim3(a.seg_threads), 0, s, a);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
-    if (blocks > a.depth_segs)  // the rollbuffer blocks' total (fused prefix) is written last
-        hipLaunchKernelGGL(k_emit_sel, dim3(blocks - a.depth_segs), dim3(a.seg_threads), 0, s, a);
     return hipGetLastError();
 }
 
 const void* frame_kernel(int which, int rot45) {
     if (which == 1) return reinterpret_cast<const void*>(&k_emit);
-    if (which == 2) return reinterpret_cast<const void*>(&k_emit_sel);
+    if (which == 2) return reinterpret_cast<const void*>(&k_sel);
+    if (which == 3) return reinterpret_cast<const void*>(&k_sel_place);
     return rot45 ? reinterpret_cast<const void*>(&k_mask<true>)
                  : reinterpret_cast<const void*>(&k_mask<false>);
 }
@@ -1397,16 +1383,44 @@ hipError_t launch_scatter(const uint32_t* coords, const uint32_t* count, uint32_
 }
 
 // ---- GPU voxelize: onesweep LSD radix sort + ordered group mean ---------------------------------
+// Digit histograms of all passes in one read of the keys (when the compaction did not build
+// them: large frames).  Keys of neighbouring points repeat, so each wave adds run lengths: the
+// first lane of a run of equal digits adds the run (few LDS atomics on hot bins); each thread
+// keeps 4 chunk loads in flight.
 __global__ __launch_bounds__(256) void k_sort_hist(const uint32_t* __restrict__ keys,
                                                    const uint32_t* __restrict__ count,
                                                    uint32_t npasses, uint32_t* __restrict__ hist) {
     __shared__ uint32_t s_h[4 * 256];
     for (uint32_t i = threadIdx.x; i < 4 * 256; i += 256) s_h[i] = 0;
     __syncthreads();
+    const int lane = threadIdx.x & 63;
     const uint32_t n = *count;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t k = keys[i];
-        for (uint32_t p = 0; p < npasses; ++p) atomicAdd(&s_h[p * 256 + ((k >> (8 * p)) & 0xFFu)], 1u);
+    const uint32_t stride = gridDim.x * 256u;
+    for (uint32_t base = blockIdx.x * 256u; base < n; base += 4u * stride) {  // block-uniform
+        uint32_t k[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t i = base + q * stride + threadIdx.x;
+            k[q] = i < n ? keys[i] : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t i = base + q * stride + threadIdx.x;
+            const unsigned long long vm = __ballot(i < n);  // valid lanes: a prefix of the wave
+            if (!vm) break;
+            const uint32_t nv = (uint32_t)__popcll(vm);
+            for (uint32_t p = 0; p < npasses; ++p) {
+                const uint32_t d = (k[q] >> (8 * p)) & 0xFFu;
+                const uint32_t pd = __shfl_up(d, 1, 64);
+                const bool leader = (uint32_t)lane < nv && (lane == 0 || pd != d);
+                const unsigned long long lm = __ballot(leader);
+                if (leader) {
+                    const unsigned long long after = lane == 63 ? 0ull : lm & (~0ull << (lane + 1));
+                    const uint32_t end = after ? (uint32_t)(__ffsll((long long)after) - 1) : nv;
+                    atomicAdd(&s_h[p * 256 + d], end - (uint32_t)lane);
+                }
+            }
+        }
     }
     __syncthreads();
     uint32_t* rep = hist + (blockIdx.x % kHistReps) * 1024u;
@@ -1776,8 +1790,8 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
     const uint32_t sort_tiles = std::min<uint32_t>((a.nmax + tile - 1) / tile, kPersistBlocks);
     hipError_t e;
     if (!a.hist_ready) {
-        unsigned hb = grid_blocks(a.nmax, 256 * 16);
-        if (hb > 64) hb = 64;
+        unsigned hb = grid_blocks(a.nmax, 256 * 4);
+        if (hb > 512) hb = 512;
         hipLaunchKernelGGL(k_sort_hist, dim3(hb), dim3(256), 0, s, a.keys, a.count, npasses, a.hist);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }

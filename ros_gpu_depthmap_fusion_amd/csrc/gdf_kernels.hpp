@@ -31,7 +31,8 @@ inline uint32_t scan_partials_offset(uint32_t segs) { return (segs + 63u) & ~63u
 inline size_t seg_offsets_words(uint32_t segs) {
     return scan_partials_offset(segs) + (segs + 4095u) / 4096u + 1u;
 }
-// the compaction kernels (0: k_mask, 1: k_emit) as launched for `rot45` (graph node lookup)
+// the compaction kernels (0: k_mask, 1: k_emit, 2: k_sel, 3: k_sel_place) as launched for
+// `rot45` (graph node lookup)
 const void* frame_kernel(int which, int rot45);
 
 // filter_point_sequence + insert into the rollbuffer ring (w = mask)

@@ -54,7 +54,7 @@ class FrameParams(C.Structure):
 
 # gdf_kernel_slot order (include/gdf.h): launch groups, then single kernels
 KERNEL_SLOTS = ("frame", "grid", "voxelize", "ps_insert", "mask", "scan", "emit", "sort",
-                "group", "reserved9", "event_floor")
+                "group", "sel", "event_floor")
 
 
 class StreamCamera(C.Structure):

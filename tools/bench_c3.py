@@ -90,7 +90,15 @@ def main():
     r = frame(pc_sync)
     st = eng.rollbuffer_state()
     S, N, G = st.selection_point_count, r.num_points, r.num_voxelized
+    # survivors of the depth part alone (a frame with the depth map only, no selection)
     (gx, gy, gz), ncells = eng.grid_size()
+    probe = GPUDepthmapFusion(0)
+    probe.clear()
+    probe.addDepthmapDevice(depth[(k - 1) % args.ring].ptr, W, H, *cam.intrinsics(), cam.T_world,
+                            cam.T_crop)
+    N_depth = probe.processFrame(p).num_points
+    probe.close()
+    N_sel = N - N_depth
     _, gsz = np.unique(eng.downloadVoxelCoords(), return_counts=True)  # points per voxel
     group_sizes = {"max": int(gsz.max()), "p50": int(np.percentile(gsz, 50)),
                    "p99": int(np.percentile(gsz, 99)),
@@ -115,16 +123,17 @@ def main():
     seg = 1024
     # algorithmic HBM bytes per launch (SURVEY §8(d) + C3 terms)
     model = {
-        "mask": 2.0 * P + 16.0 * S + 8.0 * (items / seg) * 17,  # depth, selected ring points,
-                                                                 # vbits + count per segment
-        "emit": 2.0 * P + 16.0 * S + 20.0 * N,                  # sources again, point + key out
+        "mask": 3.0 * P,                                         # depth in, stage bits out
+        "emit": 1.0 * P + 22.0 * N_depth,                        # depth survivors: point + key
+        # selected ring points in once, survivors staged (point + key) and placed (read + write)
+        "sel": 16.0 * S + 20.0 * N_sel * 3,
         "sort": (12.0 * N + 16.0 * N * 2 + 2.0 * ncells) / 3.0,
         "group": 24.0 * N + 16.0 * G,
         "ps_insert": 32.0 * P,                                   # new sequence in, ring out
         "scan": 8.0 * (items / seg),
     }
     per = {}
-    for name in ("mask", "scan", "emit", "sort", "group", "ps_insert"):
+    for name in ("mask", "scan", "emit", "sel", "sort", "group", "ps_insert"):
         tot, n = kt[name]
         if n:
             per[name] = {"avg_us": round(tot * 1e3 / n, 2), "launches_per_frame":
@@ -144,6 +153,7 @@ def main():
                                "points (timespan select, transform, crop, compaction, voxelize, "
                                "grid %dx%dx%d)" % (W, H, args.window, P, gx, gy, gz),
                    "selected_points": S, "points_after_crop": N, "voxels": G,
+                   "depth_points_after_crop": N_depth,
                    "points_per_voxel": group_sizes,
                    "grid_cells": ncells},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBPS,
