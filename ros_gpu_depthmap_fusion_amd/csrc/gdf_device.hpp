@@ -17,8 +17,8 @@ constexpr int kArgCams = 4;           // camera descriptors passed in the kernel
 constexpr int kHalo = 8;              // band rows/columns staged around a segment: min(F, 8)
 constexpr uint32_t kSegItems = 1024;  // items per compaction segment (max)
 constexpr uint32_t kFusedPrefixSegs = 4096;  // up to this many segments k_emit sums the counts
-constexpr uint32_t kSelSegs = 8;      // rollbuffer points per k_sel thread
-constexpr uint32_t kSelThreads = 512; // k_sel block: a tile is kSelSegs * kSelThreads points
+constexpr uint32_t kSelSegs = 8;      // rollbuffer points per k_sel thread (default; 4, 8, 16)
+constexpr uint32_t kSelThreads = 512; // k_sel block (default): a tile is segs * threads points
 constexpr int kSortThreads = 256;
 // the voxel-key digit histogram is accumulated into kHistReps replicas of [4 passes][256 digits]
 // (block b adds into replica b % kHistReps): same-address atomics from hundreds of blocks
@@ -97,6 +97,8 @@ struct FrameArgs {
     // rollbuffer compaction (k_sel): tiles of kSelSegs * kSelThreads points, survivors staged at
     // tile-local ranks, then placed by tile offsets (k_sel_place) behind the depth points
     uint32_t sel_tiles;
+    uint32_t sel_tile;          // points per tile = sel_segs * k_sel block size
+    uint32_t sel_segs;
     uint32_t* sel_counts;       // [sel_tiles] survivors per tile
     uint32_t* sel_offsets;      // [seg_offsets_words(sel_tiles)] exclusive scan (+ scan partials)
     float4* sel_pts;            // staged survivors: tile t's at [t * tile, + count) ...

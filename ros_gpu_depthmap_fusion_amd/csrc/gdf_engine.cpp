@@ -202,6 +202,7 @@ struct Slot {
     DevBuf d_misc;
     uint32_t* h_misc = nullptr;     // pinned
     bool compacted = false, coords_valid = false, marks_set = false;
+    bool group_marks = false;       // this frame's marks are set by the voxel groups (k_group)
     uint32_t dbg_count = 0;
     DevBuf d_ka, d_kb, d_va, d_vb, d_sstatus, d_sgstatus, d_gstatus, d_ggstatus, d_vox;
     bool vox_valid = false;
@@ -290,6 +291,7 @@ struct gdf_engine {
     float lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
 
     int sort_pt = 0;  // radix keys per thread (4, 8, 16); 0: chosen by frame capacity
+    uint32_t sel_segs = kSelSegs, sel_threads = kSelThreads;  // k_sel tile shape
     bool use_graphs = !getenv("GDF_NO_GRAPHS");  // gdf_set_graphs
 
     // compaction outputs
@@ -861,11 +863,13 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel) {
     // one item per thread: blocks as wide as the widest segment
     a.seg_threads = e->max_segw ? std::max<uint32_t>(64, e->max_segw) : kSegItems;
     a.total_segs = a.depth_segs;
-    a.sel_tiles = (uint32_t)(((uint64_t)sel + kSelSegs * kSelThreads - 1) / (kSelSegs * kSelThreads));
+    a.sel_segs = e->sel_segs;
+    a.sel_tile = e->sel_segs * e->sel_threads;
+    a.sel_tiles = (uint32_t)(((uint64_t)sel + a.sel_tile - 1) / a.sel_tile);
     if (a.sel_tiles) {  // rollbuffer compaction (k_sel) + placement behind the depth points
         Slot& q = e->sl();
-        q.d_selpts.ensure((size_t)a.sel_tiles * kSelSegs * kSelThreads * 16);
-        q.d_selkeys.ensure((size_t)a.sel_tiles * kSelSegs * kSelThreads * 4);
+        q.d_selpts.ensure((size_t)a.sel_tiles * a.sel_tile * 16);
+        q.d_selkeys.ensure((size_t)a.sel_tiles * a.sel_tile * 4);
         q.d_selcnt.ensure((size_t)a.sel_tiles * 4);
         q.d_seloff.ensure(seg_offsets_words(a.sel_tiles) * 4);
         a.sel_counts = q.d_selcnt.as<uint32_t>();
@@ -891,11 +895,18 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel) {
     a.tfw = e->d_tfw.as<float>();
     a.tfc = e->d_tfc.as<float>();
     a.do_voxel = fused_voxel ? 1 : 0;
+    e->sl().group_marks = fused_voxel && a.sel_tiles;
     if (fused_voxel) {
-        // the sequence number a fused grid update of this frame will take (voxelize)
-        a.grid_seq_out = e->sl().d_misc.as<uint32_t>() + kGridTicket;
-        a.grid_seq = e->grid_ticket;
-        a.marks = getenv("GDF_EXP_NOMARKS") ? nullptr : marks_ptr(e);  // (timing experiment only)
+        // With rollbuffer points (10^7 survivors of a window that re-observes the same voxels) the
+        // occupancy marks come from the voxel groups after the sort - one per voxel - instead of
+        // device-scope atomics per run of survivors; the grid update is then its own launch.
+        // Otherwise: marks from the compaction, and the sequence number the grid update fused
+        // into the first radix pass will take.
+        if (!e->sl().group_marks) {
+            a.grid_seq_out = e->sl().d_misc.as<uint32_t>() + kGridTicket;
+            a.grid_seq = e->grid_ticket;
+            a.marks = marks_ptr(e);
+        }
         std::memcpy(a.vlo, e->vp.vlo, 12);
         std::memcpy(a.vcs, e->vp.vcs, 12);
         std::memcpy(a.gmax, e->vp.gmax, 12);
@@ -1003,7 +1014,8 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime) 
     v.err = e->sl().d_misc.as<uint32_t>() + kErr;
     v.out = e->sl().d_vox.as<float4>();
     v.out_count = e->sl().d_misc.as<uint32_t>() + kVoxCount;
-    if (fused_grid_lifetime >= 0) {  // processFrame: the grid update rides on the first sort pass
+    if (e->sl().group_marks) v.group_marks = marks_ptr(e);
+    if (fused_grid_lifetime >= 0 && !e->sl().group_marks) {  // processFrame: the grid update rides on the first sort pass
         v.grid8 = e->d_grid8.as<uint8_t>();
         v.marks = marks_ptr(e);
         v.ncells = e->ncells;
@@ -1016,7 +1028,9 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime) 
 }
 
 void voxelize_launched(gdf_engine* e, int fused_grid_lifetime) {
-    if (fused_grid_lifetime >= 0) {
+    if (e->sl().group_marks) {
+        e->sl().marks_set = true;  // set by k_group; the grid update follows separately
+    } else if (fused_grid_lifetime >= 0) {
         e->sl().marks_set = false;
         e->invoked_once = true;
     }
@@ -1029,6 +1043,8 @@ void voxelize(gdf_engine* e, int average, int fused_grid_lifetime = -1) {
     e->timed(GDF_KERNEL_VOXELIZE, [&] { HIPCHK(launch_voxelize(v, e->s(), e->hook_ptr())); });
     voxelize_launched(e, fused_grid_lifetime);
 }
+
+void occupancy_grid(gdf_engine* e, uint32_t lifetime, hipStream_t st);
 
 // graph key: the launch arguments without the per-frame fields (depth pointers, grid ticket)
 void graph_key(const FrameArgs& a, FrameArgs& k) {
@@ -1051,8 +1067,15 @@ void run_fused_frame(gdf_engine* e, int average, uint32_t lifetime) {
     const VoxelizeArgs v = voxelize_args(e, average, (int)lifetime);
     Slot::Graph& G = e->sl().graph;
     // (a frame without compaction kernels stores its grid ticket with a memset: not replayable)
+    if (e->sl().group_marks) {  // rollbuffer frame: marks from the voxel groups, then the grid
+        e->timed(GDF_KERNEL_FRAME, [&] { HIPCHK(launch_frame(a, e->s(), e->hook_ptr())); });
+        e->timed(GDF_KERNEL_VOXELIZE, [&] { HIPCHK(launch_voxelize(v, e->s(), e->hook_ptr())); });
+        voxelize_launched(e, -1);
+        occupancy_grid(e, lifetime, e->s());
+        return;
+    }
     const bool eligible = e->use_graphs && !e->profiling && !e->debug && a.ncams <= kArgCams &&
-                          !e->user_stream && (a.total_segs || a.sel_tiles);
+                          !e->user_stream && a.total_segs;
     hipStream_t st = e->s();
     if (eligible && G.valid && same_key(a, v, G.key_a, G.key_v)) {
         void* args[] = {const_cast<FrameArgs*>(&a)};
@@ -1079,8 +1102,9 @@ void run_fused_frame(gdf_engine* e, int average, uint32_t lifetime) {
         HIPCHK(hipGraphGetNodes(G.g, nullptr, &nn));
         std::vector<hipGraphNode_t> nodes(nn);
         HIPCHK(hipGraphGetNodes(G.g, nodes.data(), &nn));
-        const void* fk[4] = {frame_kernel(0, a.rot45), frame_kernel(1, a.rot45), frame_kernel(2, a.rot45),
-                             frame_kernel(3, a.rot45)};  // (the count scans take no FrameArgs)
+        const void* fk[6] = {frame_kernel(0, a.rot45), frame_kernel(1, a.rot45), frame_kernel(2, a.rot45),
+                             frame_kernel(3, a.rot45), frame_kernel(4, a.rot45),
+                             frame_kernel(5, a.rot45)};  // (the count scans take no FrameArgs)
         G.frame_nodes.clear();
         for (hipGraphNode_t n : nodes) {
             hipGraphNodeType t;
@@ -1088,7 +1112,7 @@ void run_fused_frame(gdf_engine* e, int average, uint32_t lifetime) {
             if (t != hipGraphNodeTypeKernel) continue;
             hipKernelNodeParams kp{};
             HIPCHK(hipGraphKernelNodeGetParams(n, &kp));
-            if (kp.func == fk[0] || kp.func == fk[1] || kp.func == fk[2] || kp.func == fk[3])
+            if (std::find(fk, fk + 6, kp.func) != fk + 6)
                 G.frame_nodes.emplace_back(n, kp);
         }
         if (G.frame_nodes.empty()) fail(GDF_ERR_HIP, "frame graph: compaction kernels not found");
@@ -1185,6 +1209,14 @@ int gdf_create(int device, gdf_engine** out) {
     int rc = guarded(e, [&] {
         create_slot(e->slots[0]);
         if (const char* v = std::getenv("GDF_SORT_PT")) e->sort_pt = std::atoi(v);  // tuning knob
+        if (const char* v = std::getenv("GDF_SEL_SHAPE")) {  // tuning knob: "segs,threads"
+            unsigned sg = 0, th = 0;
+            if (std::sscanf(v, "%u,%u", &sg, &th) == 2 && (sg == 4 || sg == 8 || sg == 16) &&
+                th >= 64 && th <= 1024 && th % 64 == 0 && sg * (th / 64) <= 256) {
+                e->sel_segs = sg;
+                e->sel_threads = th;
+            }
+        }
         ensure_misc(e);
         HIPCHK(hipStreamSynchronize(e->s()));
     });

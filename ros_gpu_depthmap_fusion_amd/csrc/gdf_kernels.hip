@@ -578,6 +578,20 @@ __device__ __forceinline__ uint32_t sel_tf_in(const FrameArgs& a, const SelSeg& 
 
 // selected rollbuffer point i: mask (transfer_data of the selected mask), transform_points
 // _indirect (:50-69) into the crop frame, crop_points
+__device__ __forceinline__ uint32_t sel_bits_m(const FrameArgs& a, const float4& p,
+                                               gptr<const float> Tc) {
+    if (p.w == 0.0f) return 0;  // rollbuffer mask 0
+    if (a.do_crop) {
+        const float qx = mrow(Tc + 0, p.x, p.y, p.z, 1.0f);
+        const float qy = mrow(Tc + 4, p.x, p.y, p.z, 1.0f);
+        const float qz = mrow(Tc + 8, p.x, p.y, p.z, 1.0f);
+        if (qx < a.lo[0] || qx > a.hi[0] || qy < a.lo[1] || qy > a.hi[1] || qz < a.lo[2] ||
+            qz > a.hi[2])
+            return 3;
+    }
+    return 7;
+}
+
 __device__ __forceinline__ uint32_t sel_bits(const FrameArgs& a, const SelSeg& g, uint32_t i,
                                              const float4& p) {
     if (p.w == 0.0f) return 0;  // rollbuffer mask 0
@@ -940,8 +954,11 @@ __global__ __launch_bounds__(1024) void k_emit(FrameArgs a) {
 // look-back, no second read of the window.  After the scan of the tile counts, k_sel_place moves
 // each tile's survivors behind the depth points (whose count is known only after the depth
 // compaction), in selection order.  Stage bits go to the debug buffer as before.
-__global__ __launch_bounds__(kSelThreads) void k_sel(FrameArgs a) {
+template <uint32_t kSegs>
+__global__ __launch_bounds__(1024) void k_sel(FrameArgs a) {
+    constexpr uint32_t kSelSegs = kSegs;
     __shared__ uint32_t s_wc[kSelSegs * 16];  // kept items per (segment j, wave w), j-major
+    static_assert(kSelSegs * 16 <= 256, "k_sel scan covers 256 entries");
     __shared__ uint32_t s_mark[1u << kMarkCacheBits];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int nwaves = blockDim.x >> 6;
@@ -949,41 +966,78 @@ __global__ __launch_bounds__(kSelThreads) void k_sel(FrameArgs a) {
     const uint32_t tile = blockIdx.x;
     if (a.grid_seq_out && tile == 0 && i == 0) *a.grid_seq_out = a.grid_seq;  // (as k_mask)
     const uint32_t si0 = tile * kSelSegs * B;
-    const SelSeg g = sel_seg(a, si0);
+    // the ring loads first (their slots need no search; 32-bit slot arithmetic: ring_cap < 2^32),
+    // branch-free (a point past the selection re-reads the tile's first slot and is dropped);
+    // the sequence search runs while they fly
     float4 p[kSelSegs];
+    {
+        const uint32_t cap = (uint32_t)a.ring_cap;
+        const uint32_t r0 = (uint32_t)((a.ring_first + si0) % a.ring_cap);
 #pragma unroll
-    for (uint32_t j = 0; j < kSelSegs; ++j) {
-        const uint32_t si = si0 + j * B + i;
-        p[j] = si < a.sel_count ? sel_point(a, g, si) : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (uint32_t j = 0; j < kSelSegs; ++j) {
+            const uint32_t si = si0 + j * B + i;
+            uint32_t q = r0 + j * B + i;
+            q = q >= cap ? q - cap : q;
+            p[j] = gld4(a.ring, si < a.sel_count ? q : r0);
+        }
     }
+    const SelSeg g = sel_seg(a, si0);
+    // the whole tile inside one sequence (all but ~1 in 10^2..10^3 tiles): its crop transform is
+    // block-uniform, read once into scalar registers, and the stage bits are computed without
+    // branches; a tile reaching into the next sequence takes the per-point lookup
+    const bool one_seq = si0 + kSelSegs * B <= g.next;
     for (uint32_t j = i; j < (1u << kMarkCacheBits); j += B) s_mark[j] = 0xFFFFFFFFu;
+    uint32_t bits[kSelSegs];
+    if (one_seq) {
+        const gptr<const float> Tc = G(a.tfc + 16 * (size_t)g.tf0);
+        float tc[12];
+#pragma unroll
+        for (int q = 0; q < 12; ++q) tc[q] = Tc[q];
+#pragma unroll
+        for (uint32_t j = 0; j < kSelSegs; ++j) {
+            const float x = p[j].x, y = p[j].y, z = p[j].z;
+            const float qx = mrow(tc + 0, x, y, z, 1.0f);
+            const float qy = mrow(tc + 4, x, y, z, 1.0f);
+            const float qz = mrow(tc + 8, x, y, z, 1.0f);
+            const bool out = a.do_crop && ((qx < a.lo[0]) | (qx > a.hi[0]) | (qy < a.lo[1]) |
+                                           (qy > a.hi[1]) | (qz < a.lo[2]) | (qz > a.hi[2]));
+            const bool live = (si0 + j * B + i < a.sel_count) & (p[j].w != 0.0f);
+            bits[j] = live ? (out ? 3u : 7u) : 0u;
+        }
+    } else {
+#pragma unroll
+        for (uint32_t j = 0; j < kSelSegs; ++j) {
+            const uint32_t si = si0 + j * B + i;
+            bits[j] = si < a.sel_count ? sel_bits(a, g, si, p[j]) : 0u;
+        }
+    }
     uint32_t keep = 0;  // bit j: item j of this thread survives the crop
 #pragma unroll
     for (uint32_t j = 0; j < kSelSegs; ++j) {
         const uint32_t si = si0 + j * B + i;
-        const bool in = si < a.sel_count;
-        const uint32_t bits = in ? sel_bits(a, g, si, p[j]) : 0u;
-        if (a.dbg && in) G(a.dbg)[a.depth_total + si] = (uint8_t)bits;
-        keep |= ((bits >> 2) & 1u) << j;
-        const unsigned long long m = __ballot((bits & 4u) != 0u);
+        if (a.dbg && si < a.sel_count) G(a.dbg)[a.depth_total + si] = (uint8_t)bits[j];
+        keep |= ((bits[j] >> 2) & 1u) << j;
+        const unsigned long long m = __ballot((bits[j] & 4u) != 0u);
         if (lane == 0) s_wc[j * nwaves + wid] = (uint32_t)__popcll(m);
     }
     __syncthreads();
-    // exclusive scan of the (segment, wave) counts in item order by wave 0 (<= 128 entries)
+    // exclusive scan of the (segment, wave) counts in item order by wave 0 (<= 256 entries)
     const uint32_t ne = kSelSegs * (uint32_t)nwaves;
     if (wid == 0) {
-        const uint32_t e0 = (uint32_t)lane, e1 = (uint32_t)lane + 64u;
-        const uint32_t v0 = e0 < ne ? s_wc[e0] : 0u, v1 = e1 < ne ? s_wc[e1] : 0u;
-        uint32_t x0 = v0, x1 = v1;
+        uint32_t carry = 0;
+        for (uint32_t e0 = 0; e0 < ne; e0 += 64) {  // uniform
+            const uint32_t e = e0 + (uint32_t)lane;
+            const uint32_t v = e < ne ? s_wc[e] : 0u;
+            uint32_t x = v;
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y0 = __shfl_up(x0, o, 64), y1 = __shfl_up(x1, o, 64);
-            if (lane >= o) { x0 += y0; x1 += y1; }
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(x, o, 64);
+                if (lane >= o) x += y;
+            }
+            if (e < ne) s_wc[e] = carry + x - v;
+            carry += __shfl(x, 63, 64);
         }
-        const uint32_t tot0 = __shfl(x0, 63, 64), tot1 = __shfl(x1, 63, 64);
-        if (e0 < ne) s_wc[e0] = x0 - v0;
-        if (e1 < ne) s_wc[e1] = tot0 + x1 - v1;
-        if (lane == 0) G(a.sel_counts)[tile] = tot0 + tot1;
+        if (lane == 0) G(a.sel_counts)[tile] = carry;
     }
     __syncthreads();
     const uint64_t base = (uint64_t)tile * kSelSegs * B;  // the tile's staging slots
@@ -999,17 +1053,22 @@ __global__ __launch_bounds__(kSelThreads) void k_sel(FrameArgs a) {
             const uint32_t si = si0 + j * B + i;
             const uint64_t pos = base + s_wc[j * nwaves + wid] + (uint32_t)__popcll(m & ltm);
             const float x = p[j].x, y = p[j].y, z = p[j].z;
-            const gptr<const float> Tw =
-                si < g.next ? T0 : G(a.tfw + 16 * (size_t)sel_tf(a, si));  // (rare: next sequence)
-            const float4 w = make_float4(mrow(Tw + 0, x, y, z, 1.0f), mrow(Tw + 4, x, y, z, 1.0f),
-                                         mrow(Tw + 8, x, y, z, 1.0f), mrow(Tw + 12, x, y, z, 1.0f));
+            float4 w;
+            if (one_seq) {
+                w = make_float4(mrow(T0 + 0, x, y, z, 1.0f), mrow(T0 + 4, x, y, z, 1.0f),
+                                mrow(T0 + 8, x, y, z, 1.0f), mrow(T0 + 12, x, y, z, 1.0f));
+            } else {  // (rare: a tile reaching into the next sequence)
+                const gptr<const float> Tw = si < g.next ? T0 : G(a.tfw + 16 * (size_t)sel_tf(a, si));
+                w = make_float4(mrow(Tw + 0, x, y, z, 1.0f), mrow(Tw + 4, x, y, z, 1.0f),
+                                mrow(Tw + 8, x, y, z, 1.0f), mrow(Tw + 12, x, y, z, 1.0f));
+            }
             gst4(a.sel_pts, pos, w);
             if (a.do_voxel) {
                 key = voxel_key(w.x, w.y, w.z, a.vlo, a.vcs, a.gmax, a.gs);
                 G(a.sel_keys)[pos] = key;
             }
         }
-        if (a.do_voxel) mark_and_count(a, valid, key, nullptr, s_mark);
+        if (a.do_voxel && a.marks) mark_and_count(a, valid, key, nullptr, s_mark);
     }
 }
 
@@ -1019,7 +1078,7 @@ __global__ __launch_bounds__(kSelThreads) void k_sel(FrameArgs a) {
 __global__ __launch_bounds__(256) void k_sel_place(FrameArgs a) {
     const uint32_t d = *G(a.out_count);
     if (blockIdx.x == 0 && threadIdx.x == 0) *G(a.final_count) = d + *G(a.sel_total);
-    const uint32_t tile_items = kSelSegs * kSelThreads;
+    const uint32_t tile_items = a.sel_tile;
     for (uint32_t t = blockIdx.x; t < a.sel_tiles; t += gridDim.x) {
         const uint32_t c = G(a.sel_counts)[t];
         if (!c) continue;
@@ -1078,7 +1137,13 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
     }
     if (a.sel_tiles) {  // rollbuffer points: survivors per tile, tile offsets, placement
         HookScope hs(hook, GDF_KERNEL_SEL);
-        hipLaunchKernelGGL(k_sel, dim3(a.sel_tiles), dim3(kSelThreads), 0, s, a);
+        const uint32_t thr = a.sel_tile / a.sel_segs;
+        if (a.sel_segs == 4)
+            hipLaunchKernelGGL(k_sel<4>, dim3(a.sel_tiles), dim3(thr), 0, s, a);
+        else if (a.sel_segs == 16)
+            hipLaunchKernelGGL(k_sel<16>, dim3(a.sel_tiles), dim3(thr), 0, s, a);
+        else
+            hipLaunchKernelGGL(k_sel<8>, dim3(a.sel_tiles), dim3(thr), 0, s, a);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         const uint32_t chunks = (a.sel_tiles + 4095u) / 4096u;
         uint32_t* partial = a.sel_offsets + scan_partials_offset(a.sel_tiles);
@@ -1096,7 +1161,9 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
 
 const void* frame_kernel(int which, int rot45) {
     if (which == 1) return reinterpret_cast<const void*>(&k_emit);
-    if (which == 2) return reinterpret_cast<const void*>(&k_sel);
+    if (which == 2) return reinterpret_cast<const void*>(&k_sel<8>);
+    if (which == 4) return reinterpret_cast<const void*>(&k_sel<4>);
+    if (which == 5) return reinterpret_cast<const void*>(&k_sel<16>);
     if (which == 3) return reinterpret_cast<const void*>(&k_sel_place);
     return rot45 ? reinterpret_cast<const void*>(&k_mask<true>)
                  : reinterpret_cast<const void*>(&k_mask<false>);
@@ -1567,7 +1634,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_group(
     const uint32_t* __restrict__ count, const float4* __restrict__ pts, float* __restrict__ out,
     uint32_t* __restrict__ out_count, unsigned long long* status, unsigned long long* gstatus,
     uint32_t* tile_ctr, uint32_t* epoch_word, uint32_t* err, uint32_t* hist, int average,
-    VoxelParams vp) {
+    VoxelParams vp, uint32_t* marks) {
     __shared__ uint32_t s_wave[4];
     __shared__ uint32_t s_tile, s_epoch, s_excl, s_nbig;
     __shared__ uint32_t s_start[kGroupThreads + 1];
@@ -1660,6 +1727,10 @@ __global__ __launch_bounds__(kGroupThreads) void k_group(
         const uint32_t g = s_excl + threadIdx.x;
         const uint32_t s = s_start[threadIdx.x], e = s_start[threadIdx.x + 1];
         float* o = out + 4 * (size_t)g;
+        if (marks) {  // voxel_grid_occupancy_of_points: one mark per occupied voxel
+            const uint32_t key = keys[s];
+            atomicOr(marks + (key >> 5), 1u << (key & 31u));
+        }
         if (!average) {
             float c[4];
             group_corner(keys[s], vp, c);
@@ -1822,7 +1893,7 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
                        vin, a.count, a.pts, reinterpret_cast<float*>(a.out), a.out_count,
                        a.gstatus, a.ggstatus, reinterpret_cast<uint32_t*>(a.ctrs + kCtrGroup),
                        reinterpret_cast<uint32_t*>(a.ctrs + kCtrEpoch), a.err, a.hist, a.average,
-                       a.vp);
+                       a.vp, a.group_marks);
     return hipGetLastError();
 }
 

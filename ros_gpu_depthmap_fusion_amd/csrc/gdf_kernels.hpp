@@ -31,7 +31,7 @@ inline uint32_t scan_partials_offset(uint32_t segs) { return (segs + 63u) & ~63u
 inline size_t seg_offsets_words(uint32_t segs) {
     return scan_partials_offset(segs) + (segs + 4095u) / 4096u + 1u;
 }
-// the compaction kernels (0: k_mask, 1: k_emit, 2: k_sel, 3: k_sel_place) as launched for
+// the compaction kernels (0: k_mask, 1: k_emit, 2/4/5: k_sel<8/4/16>, 3: k_sel_place) as launched for
 // `rot45` (graph node lookup)
 const void* frame_kernel(int which, int rot45);
 
@@ -83,6 +83,7 @@ struct VoxelizeArgs {
     // first sort pass: it only needs the occupancy marks, which the compaction already wrote
     uint8_t* grid8;
     uint32_t* marks;
+    uint32_t* group_marks;          // optional: k_group sets the occupancy mark of every voxel
     GridSeq gseq;                   // engine order of the fused grid update (frame pipelining)
     uint64_t ncells;
     uint32_t lifetime;
