@@ -205,6 +205,7 @@ struct Slot {
     bool group_marks = false;       // this frame's marks are set by the voxel groups (k_group)
     uint32_t dbg_count = 0;
     DevBuf d_ka, d_kb, d_va, d_vb, d_sstatus, d_sgstatus, d_gstatus, d_ggstatus, d_vox;
+    DevBuf d_gcnt, d_goff;          // group starts per tile + their scan (large frames)
     bool vox_valid = false;
     DevBuf d_markbits;              // this frame's occupancy marks (1 bit per cell)
     uint32_t marks_gen = ~0u;
@@ -988,6 +989,9 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime) 
     e->sl().d_gstatus.ensure_zero(voxelize_group_tiles(nmax) * 8, e->s());
     e->sl().d_ggstatus.ensure_zero((voxelize_group_tiles(nmax) / 64 + 2) * 8, e->s());
     e->sl().d_vox.ensure((size_t)nmax * 16);
+    const uint32_t gtiles = (uint32_t)voxelize_group_tiles(nmax);
+    e->sl().d_gcnt.ensure((size_t)gtiles * 4);
+    e->sl().d_goff.ensure(seg_offsets_words(gtiles) * 4);
     VoxelizeArgs v;
     std::memset(&v, 0, sizeof(v));
     v.keys = e->sl().d_coords.as<uint32_t>();
@@ -1010,6 +1014,8 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime) 
     v.ctrs = e->sl().d_ctrs.as<unsigned long long>();
     // keys per thread of a radix tile: small frames want many tiles (latency), big ones few
     // (each tile publishes 256 look-back words: 2 KiB per 1 Ki keys at PT=4)
+    v.group_counts = e->sl().d_gcnt.as<uint32_t>();
+    v.group_offsets = e->sl().d_goff.as<uint32_t>();
     v.sort_pt = e->sort_pt ? e->sort_pt : nmax <= (1u << 20) ? 4 : nmax <= (1u << 24) ? 8 : 16;
     v.err = e->sl().d_misc.as<uint32_t>() + kErr;
     v.out = e->sl().d_vox.as<float4>();

@@ -745,9 +745,17 @@ __device__ __forceinline__ uint32_t block_sum_1024(uint32_t v, uint32_t* s_w) {
     return t;
 }
 
+// (mdev: the number of counts is ceil(*mdev / per) <= m, read on the device)
+__device__ __forceinline__ uint32_t scan_len(uint32_t m, const uint32_t* mdev, uint32_t per) {
+    return mdev ? min(m, (*mdev + per - 1u) / per) : m;
+}
+
 __global__ __launch_bounds__(1024) void k_scan_reduce(const uint32_t* __restrict__ counts,
-                                                      uint32_t m, uint32_t* __restrict__ partial) {
+                                                      uint32_t m, uint32_t* __restrict__ partial,
+                                                      const uint32_t* mdev, uint32_t per) {
     __shared__ uint32_t s_w[16];
+    m = scan_len(m, mdev, per);
+    if (blockIdx.x * 4096u >= m && blockIdx.x) return;
     uint32_t v = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -761,9 +769,13 @@ __global__ __launch_bounds__(1024) void k_scan_reduce(const uint32_t* __restrict
 __global__ __launch_bounds__(1024) void k_scan_counts(const uint32_t* __restrict__ counts,
                                                       uint32_t m, uint32_t* __restrict__ offsets,
                                                       uint32_t* __restrict__ total,
-                                                      const uint32_t* __restrict__ partial) {
+                                                      const uint32_t* __restrict__ partial,
+                                                      const uint32_t* mdev, uint32_t per) {
     __shared__ uint32_t s_w[16];
     __shared__ uint32_t s_carry;
+    m = scan_len(m, mdev, per);
+    const uint32_t chunks = (m + 4095u) / 4096u;
+    if (blockIdx.x >= chunks && blockIdx.x) return;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     {
         uint32_t v = 0;
@@ -807,7 +819,7 @@ __global__ __launch_bounds__(1024) void k_scan_counts(const uint32_t* __restrict
         if (threadIdx.x == 0) s_carry += tot;
         __syncthreads();
     }
-    if (threadIdx.x == 0 && blockIdx.x == gridDim.x - 1) *total = s_carry;
+    if (threadIdx.x == 0 && blockIdx.x == (chunks ? chunks - 1u : 0u) && total) *total = s_carry;
 }
 
 // Pass 2: item-ordered emission, one block per segment.  Each valid item recomputes its world
@@ -1125,10 +1137,10 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
             const uint32_t chunks = (a.total_segs + 4095u) / 4096u;
             uint32_t* partial = a.seg_offsets + scan_partials_offset(a.total_segs);
             hipLaunchKernelGGL(k_scan_reduce, dim3(chunks), dim3(1024), 0, s, a.seg_counts,
-                               a.total_segs, partial);
+                               a.total_segs, partial, nullptr, 1u);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             hipLaunchKernelGGL(k_scan_counts, dim3(chunks), dim3(1024), 0, s, a.seg_counts,
-                               a.total_segs, a.seg_offsets, a.out_count, partial);
+                               a.total_segs, a.seg_offsets, a.out_count, partial, nullptr, 1u);
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
         HookScope hs(hook, GDF_KERNEL_EMIT);
@@ -1148,10 +1160,10 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
         const uint32_t chunks = (a.sel_tiles + 4095u) / 4096u;
         uint32_t* partial = a.sel_offsets + scan_partials_offset(a.sel_tiles);
         hipLaunchKernelGGL(k_scan_reduce, dim3(chunks), dim3(1024), 0, s, a.sel_counts,
-                           a.sel_tiles, partial);
+                           a.sel_tiles, partial, nullptr, 1u);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         hipLaunchKernelGGL(k_scan_counts, dim3(chunks), dim3(1024), 0, s, a.sel_counts,
-                           a.sel_tiles, a.sel_offsets, a.sel_total, partial);
+                           a.sel_tiles, a.sel_offsets, a.sel_total, partial, nullptr, 1u);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         hipLaunchKernelGGL(k_sel_place, dim3(std::min<uint32_t>(a.sel_tiles, 4096u)), dim3(256), 0,
                            s, a);
@@ -1617,7 +1629,29 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
 // sort pass).
 constexpr int kStagePts = 1024;  // points of a tile's groups staged in LDS (16 KiB)
 constexpr uint32_t kPersistBlocks = 2048;  // blocks of a persistent sort / group launch
+constexpr uint32_t kGroupScanTiles = 4096;  // above: group-id offsets by count + scan
 constexpr int kSmallGroup = 16;  // groups summed by one thread; longer ones by a wave
+
+// Group starts per tile of kGroupThreads sorted keys (large frames: the tiles' group-id offsets
+// then come from a scan of these counts instead of tickets and look-back in k_group).
+__global__ __launch_bounds__(256) void k_group_count(const uint32_t* __restrict__ keys,
+                                                     const uint32_t* __restrict__ count,
+                                                     uint32_t* __restrict__ counts) {
+    __shared__ uint32_t s_w[4];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t n = *count;
+    const uint32_t ntiles = (n + kGroupThreads - 1) / kGroupThreads;
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {  // block-uniform
+        const uint32_t i = t * kGroupThreads + threadIdx.x;
+        const uint32_t key = i < n ? keys[i] : 0u;
+        const uint32_t prev = (i < n && i > 0) ? keys[i - 1] : ~key;
+        const unsigned long long b = __ballot(i < n && (i == 0 || key != prev));
+        if (lane == 0) s_w[wid] = (uint32_t)__popcll(b);
+        __syncthreads();
+        if (threadIdx.x == 0) counts[t] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        __syncthreads();
+    }
+}
 
 __device__ __forceinline__ void group_corner(uint32_t key, const VoxelParams& vp, float* o) {
     const uint32_t gx = key % vp.gs[0];
@@ -1634,7 +1668,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_group(
     const uint32_t* __restrict__ count, const float4* __restrict__ pts, float* __restrict__ out,
     uint32_t* __restrict__ out_count, unsigned long long* status, unsigned long long* gstatus,
     uint32_t* tile_ctr, uint32_t* epoch_word, uint32_t* err, uint32_t* hist, int average,
-    VoxelParams vp, uint32_t* marks) {
+    VoxelParams vp, uint32_t* marks, const uint32_t* tile_base) {
     __shared__ uint32_t s_wave[4];
     __shared__ uint32_t s_tile, s_epoch, s_excl, s_nbig;
     __shared__ uint32_t s_start[kGroupThreads + 1];
@@ -1648,15 +1682,25 @@ __global__ __launch_bounds__(kGroupThreads) void k_group(
         for (uint32_t i = threadIdx.x; i < kHistWords; i += kGroupThreads) hist[i] = 0;
         if (ntiles == 0 && threadIdx.x == 0) *out_count = 0;  // n == 0
     }
+    // tile_base (large frames): the group-id offset of every tile is known (k_group_count + scan),
+    // so blocks walk the tiles by index with no ticket and no look-back; otherwise tickets +
+    // decoupled look-back in one launch
     const Tickets tk = tickets(ntiles, gridDim.x);
-    if (blockIdx.x >= tk.nblk) return;
-    if (threadIdx.x == 0) s_epoch = read_epoch(epoch_word);
-    for (bool first = true;; first = false) {  // persistent: tiles in ticket order
-    if (!first && tk.oneshot) return;
+    if (!tile_base && blockIdx.x >= tk.nblk) return;
+    if (!tile_base && threadIdx.x == 0) s_epoch = read_epoch(epoch_word);
+    uint32_t walk = blockIdx.x;
+    for (bool first = true;; first = false) {  // persistent
+    if (!first && !tile_base && tk.oneshot) return;
     if (threadIdx.x == 0) {
-        s_tile = next_ticket(tile_ctr, tk, epoch_word, s_epoch);
+        if (tile_base) {
+            s_tile = walk;
+            s_excl = walk < ntiles ? tile_base[walk] : 0u;
+        } else {
+            s_tile = next_ticket(tile_ctr, tk, epoch_word, s_epoch);
+        }
         s_nbig = 0;
     }
+    walk += gridDim.x;
     __syncthreads();
     const uint32_t tile = s_tile, epoch = s_epoch;
     if (tile >= ntiles) return;  // block-uniform
@@ -1685,7 +1729,8 @@ __global__ __launch_bounds__(kGroupThreads) void k_group(
         }
     }
     if (wid == 0) {
-        const uint32_t ex = lookback2_wave(status, gstatus, tile, ntiles, total, epoch, err);
+        const uint32_t ex = tile_base ? s_excl
+                                      : lookback2_wave(status, gstatus, tile, ntiles, total, epoch, err);
         if (lane == 0) {
             s_excl = ex;
             if (tile == ntiles - 1) *out_count = ex + total;
@@ -1886,14 +1931,32 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
         kin = kbuf[p & 1];
         vin = vbuf[p & 1];
     }
-    const uint32_t group_tiles =
-        std::min<uint32_t>((a.nmax + kGroupThreads - 1) / kGroupThreads, kPersistBlocks);
+    const uint32_t max_tiles = (a.nmax + kGroupThreads - 1) / kGroupThreads;
+    const uint32_t group_tiles = std::min<uint32_t>(max_tiles, kPersistBlocks);
     HookScope hs(hook, GDF_KERNEL_GROUP);
+    const uint32_t* tile_base = nullptr;
+    if (a.group_counts && max_tiles > kGroupScanTiles) {
+        // many tiles: their group-id offsets from a count + scan instead of one ticket each
+        // (a single ticket counter serves ~10^2 draws per microsecond)
+        hipLaunchKernelGGL(k_group_count, dim3(group_tiles), dim3(256), 0, s, kin, a.count,
+                           a.group_counts);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        const uint32_t chunks = (max_tiles + 4095u) / 4096u;
+        uint32_t* partial = a.group_offsets + scan_partials_offset(max_tiles);
+        hipLaunchKernelGGL(k_scan_reduce, dim3(chunks), dim3(1024), 0, s, a.group_counts,
+                           max_tiles, partial, a.count, (uint32_t)kGroupThreads);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_scan_counts, dim3(chunks), dim3(1024), 0, s, a.group_counts,
+                           max_tiles, a.group_offsets, (uint32_t*)nullptr, partial, a.count,
+                           (uint32_t)kGroupThreads);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        tile_base = a.group_offsets;
+    }
     hipLaunchKernelGGL(k_group, dim3(group_tiles ? group_tiles : 1), dim3(kGroupThreads), 0, s, kin,
                        vin, a.count, a.pts, reinterpret_cast<float*>(a.out), a.out_count,
                        a.gstatus, a.ggstatus, reinterpret_cast<uint32_t*>(a.ctrs + kCtrGroup),
                        reinterpret_cast<uint32_t*>(a.ctrs + kCtrEpoch), a.err, a.hist, a.average,
-                       a.vp, a.group_marks);
+                       a.vp, a.group_marks, tile_base);
     return hipGetLastError();
 }
 

@@ -84,6 +84,8 @@ struct VoxelizeArgs {
     uint8_t* grid8;
     uint32_t* marks;
     uint32_t* group_marks;          // optional: k_group sets the occupancy mark of every voxel
+    uint32_t* group_counts;         // [group tiles] group starts per tile (large frames)
+    uint32_t* group_offsets;        // [seg_offsets_words(group tiles)] their scan
     GridSeq gseq;                   // engine order of the fused grid update (frame pipelining)
     uint64_t ncells;
     uint32_t lifetime;
