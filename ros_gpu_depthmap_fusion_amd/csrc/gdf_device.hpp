@@ -26,7 +26,7 @@ constexpr int kSortThreads = 256;
 constexpr int kHistReps = 16;
 constexpr int kHistWords = kHistReps * 4 * 256;
 constexpr int kGroupThreads = 256;
-constexpr int kSumChunk = 256;                               // points per wave gather chunk
+constexpr int kSumChunk = 128;                               // points per wave gather chunk
 constexpr uint32_t kSpinLimit = 1u << 26;                   // bounded look-back spins
 
 // Device-wide counters: monotonically increasing tile tickets (the host passes each launch's

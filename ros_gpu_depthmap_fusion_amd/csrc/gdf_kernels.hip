@@ -1627,7 +1627,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
 // dependent add chain).  !average: the voxel's lower corner (GridMeta::worldCoord).
 // Block 0 also clears the digit histogram for the next voxelize (its last reader was the final
 // sort pass).
-constexpr int kStagePts = 1024;  // points of a tile's groups staged in LDS (16 KiB)
+constexpr int kStagePts = 512;   // points of a tile's groups staged in LDS (8 KiB)
 constexpr uint32_t kPersistBlocks = 2048;  // blocks of a persistent sort / group launch
 constexpr uint32_t kGroupScanTiles = 4096;  // above: group-id offsets by count + scan
 constexpr int kSmallGroup = 16;  // groups summed by one thread; longer ones by a wave
@@ -1663,7 +1663,7 @@ __device__ __forceinline__ void group_corner(uint32_t key, const VoxelParams& vp
     o[3] = 0.0f;
 }
 
-__global__ __launch_bounds__(kGroupThreads) void k_group(
+__global__ __launch_bounds__(kGroupThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_group(
     const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
     const uint32_t* __restrict__ count, const float4* __restrict__ pts, float* __restrict__ out,
     uint32_t* __restrict__ out_count, unsigned long long* status, unsigned long long* gstatus,
