@@ -16,8 +16,8 @@ import csv
 import json
 
 SLOT = {"k_mask": "mask", "k_emit": "emit", "k_sort_pass": "sort", "k_group": "group",
-        "k_scan_counts": "scan", "k_grid_u8": "grid",
-        "k_grid_u32": "grid"}
+        "k_scan_counts": "scan", "k_grid_u8": "grid", "k_grid_u32": "grid", "k_sel": "sel",
+        "k_sel_place": "sel_place", "k_sort_hist": "sort_hist", "k_group_count": "group_count"}
 
 
 def per_kernel(path, counter):
