@@ -76,6 +76,14 @@ public:
                                      (uint32_t)pointcloud.point_step, timestampSec,
                                      timestampNSec, transform_move.val));
     }
+    // the same for records already in device memory (e.g. a GPU lidar driver's buffer):
+    // borrowed until the next uploadPointSequences, gathered on the device
+    void addPointSequenceDevice(const void* records_device, uint32_t num_points,
+                                uint32_t point_step, uint32_t timestampSec, uint32_t timestampNSec,
+                                const float transform_move[16]) {
+        check(gdf_add_point_sequence_device(h_, records_device, num_points, point_step,
+                                            timestampSec, timestampNSec, transform_move));
+    }
     uint32_t numCollectedPointSequencePoints() {
         uint32_t n = 0;
         check(gdf_num_collected_point_sequence_points(h_, &n));
