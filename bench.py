@@ -11,7 +11,9 @@ generated once and uploaded before timing).
 
 N > 1 (torchrun, one rank per GPU over RCCL): rank k owns camera k (weak scaling).  The shared
 voxel grid needs one real exchange per frame: the per-rank occupancy marks (1 bit per cell) are
-all-gathered and OR-merged before every rank's identical historic-grid update.
+all-gathered and OR-merged before every rank's identical historic-grid update.  Frames stay
+pipelined on every rank; the marks of `--exchange-batch` frames travel in one all-gather and the
+grid updates then run in frame order (the grids after every frame equal the per-frame exchange's).
 
 Prints ONE JSON line (rank 0).
 """
@@ -42,6 +44,9 @@ def parse():
     ap.add_argument("--pipeline", type=int, default=3,
                     help="frames in flight on one GPU (engine slots, gdf_set_pipeline_depth); "
                          "N > 1 runs on torch's stream with depth 1")
+    ap.add_argument("--exchange-batch", type=int, default=8,
+                    help="N > 1: frames per occupancy-mark all-gather (multi.BatchedMarkExchange; "
+                         "1 = one collective per frame on torch's stream, no pipelining)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-kernel-timing", action="store_true",
@@ -78,7 +83,8 @@ def main():
     params = ComponentParams()
     eng = GPUDepthmapFusion(local_rank)
 
-    if dist is not None:
+    batched = dist is not None and args.exchange_batch > 1
+    if dist is not None and not batched:
         import torch
         stream = torch.cuda.current_stream()
         eng.set_stream(stream.cuda_stream)
@@ -99,12 +105,15 @@ def main():
     (gx, gy, gz), ncells = eng.grid_size()
 
     depth = 1
-    if dist is not None:
+    if dist is not None and not batched:
         from ros_gpu_depthmap_fusion_amd.multi import DeviceMarkExchange
         marks = DeviceMarkExchange(eng, ncells, world)
     else:
         depth = max(1, min(4, args.pipeline))
         eng.set_pipeline_depth(depth)
+        if batched:
+            from ros_gpu_depthmap_fusion_amd.multi import BatchedMarkExchange
+            marks = BatchedMarkExchange(eng, ncells, world, args.exchange_batch)
 
     pc_plain = params.to_c(None, None, False, False)
     pc_defer = params.to_c(None, None, False, True)
@@ -120,8 +129,15 @@ def main():
             return
         for i in range(first, first + count):
             eng.run_depth_stream(scam, pc_defer, i, 1)
-            marks.exchange()  # occupancy union over RCCL (multi.py)
-            eng.voxelOccupancyGrid(params.occupancy_lifetime)
+            if batched:  # occupancy union over RCCL, `exchange_batch` frames per all-gather
+                marks.take()
+                if marks.full():
+                    marks.flush(params.occupancy_lifetime)
+            else:  # one all-gather per frame (multi.py)
+                marks.exchange()
+                eng.voxelOccupancyGrid(params.occupancy_lifetime)
+        if batched:
+            marks.flush(params.occupancy_lifetime)
 
     def barrier_sync():
         eng.synchronize()
@@ -148,7 +164,7 @@ def main():
     ktimes = None
     if not args.no_kernel_timing:
         kt_steps = min(args.steps, 200)
-        if dist is None:
+        if dist is None or batched:
             eng.set_pipeline_depth(1)  # one frame in flight: launch durations without overlap
         eng.set_profiling(True)
         run(args.warmup, kt_steps)
@@ -258,8 +274,9 @@ def main():
                        "cameras_per_gpu": K, "points_per_frame_after_crop": round(n_avg),
                        "voxels_per_frame": round(g_avg), "grid_cells": ncells,
                        "frames_in_flight": depth,
-                       "parallelism": "camera-per-GPU x%d, occupancy-mark all-gather" % world
-                       if world > 1 else "single GPU"},
+                       "parallelism": ("camera-per-GPU x%d, occupancy-mark all-gather every %d "
+                                       "frame(s)" % (world, args.exchange_batch if batched else 1))
+                       if dist is not None else "single GPU"},
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

@@ -230,6 +230,24 @@ int gdf_process_frame(gdf_engine* engine, const gdf_frame_params* params,
 int gdf_export_occupancy_marks(gdf_engine* engine, uint32_t* device_bitmask, uint64_t words);
 int gdf_import_occupancy_marks(gdf_engine* engine, const uint32_t* device_bitmasks,
                                uint64_t words, uint32_t num_ranks);
+/* Batched exchange (several frames per collective, frames pipelined): gdf_take_occupancy_marks
+ * exports the marks of the frame just processed (defer_occupancy_grid = 1) AND clears them, so
+ * the engine can run the next frames; once the masks of a batch are all-gathered, each frame's
+ * union is imported in frame order - mask r of that frame at device_bitmasks + r *
+ * rank_stride_words - and followed by its gdf_voxel_occupancy_grid.  Same grids as the per-frame
+ * exchange. */
+int gdf_take_occupancy_marks(gdf_engine* engine, uint32_t* device_bitmask, uint64_t words);
+int gdf_import_occupancy_marks_strided(gdf_engine* engine, const uint32_t* device_bitmasks,
+                                       uint64_t words, uint32_t num_ranks,
+                                       uint64_t rank_stride_words);
+/* The grid updates of `num_frames` such frames in ONE pass (voxelOccupancyGrid applied frame
+ * after frame in registers): frame f's union is the OR over ranks r of the masks at
+ * device_bitmasks + r * rank_stride_words + f * frame_stride_words.  Equals num_frames
+ * import + gdf_voxel_occupancy_grid pairs; call after taking every frame's marks. */
+int gdf_voxel_occupancy_grid_batch(gdf_engine* engine, const uint32_t* device_bitmasks,
+                                   uint64_t words, uint32_t num_ranks, uint32_t num_frames,
+                                   uint64_t frame_stride_words, uint64_t rank_stride_words,
+                                   uint32_t lifetime);
 
 /* ---- live kernel timing (HIP events on the engine stream) ------------------------------------ */
 enum gdf_kernel_slot {

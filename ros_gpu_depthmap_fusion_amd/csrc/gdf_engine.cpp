@@ -1646,7 +1646,61 @@ int gdf_import_occupancy_marks(gdf_engine* e, const uint32_t* bits, uint64_t wor
     return guarded(e, [&] {
         if (!e->grid_set || !bits) fail(GDF_ERR_STATE, "no voxel grid");
         if (words < (e->ncells + 31) / 32) fail(GDF_ERR_CAPACITY, "mark bitmask too small");
-        HIPCHK(launch_import_marks(marks_ptr(e), mark_words(e), bits, nranks, e->s()));
+        HIPCHK(launch_import_marks(marks_ptr(e), mark_words(e), bits, nranks, mark_words(e), e->s()));
+        e->sl().marks_set = true;
+    });
+}
+
+int gdf_take_occupancy_marks(gdf_engine* e, uint32_t* bits, uint64_t words) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        if (!e->grid_set || !bits) fail(GDF_ERR_STATE, "no voxel grid");
+        if (words < (e->ncells + 31) / 32) fail(GDF_ERR_CAPACITY, "mark bitmask too small");
+        HIPCHK(launch_take_marks(marks_ptr(e), mark_words(e), bits, e->s()));
+        e->sl().marks_set = false;
+    });
+}
+
+int gdf_voxel_occupancy_grid_batch(gdf_engine* e, const uint32_t* bits, uint64_t words,
+                                   uint32_t nranks, uint32_t nframes, uint64_t frame_stride_words,
+                                   uint64_t rank_stride_words, uint32_t lifetime) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        if (!e->grid_set || (!bits && nframes)) fail(GDF_ERR_STATE, "no voxel grid");
+        if (words < (e->ncells + 31) / 32 || (nframes > 1 && frame_stride_words < words) ||
+            (nranks > 1 && rank_stride_words < frame_stride_words * (nframes ? nframes : 1)))
+            fail(GDF_ERR_CAPACITY, "mark bitmasks too small");
+        if (e->sl().marks_set) fail(GDF_ERR_STATE, "marks of a frame are pending (take them first)");
+        widen_if_needed(e, lifetime, e->s());
+        if (e->grid_mode == 0) {  // one pass for the batch
+            ensure_misc(e);
+            const GridSeq q = e->grid_seq(e->grid_ticket++);
+            e->timed_on(GDF_KERNEL_GRID, e->s(), [&] {
+                HIPCHK(launch_grid_u8_batch(e->d_grid8.as<uint8_t>(), bits, e->ncells, nranks,
+                                            nframes, frame_stride_words, rank_stride_words,
+                                            lifetime, q, e->s()));
+            });
+        } else {  // general history: frame by frame
+            for (uint32_t f = 0; f < nframes; ++f) {
+                HIPCHK(launch_import_marks(marks_ptr(e), mark_words(e), bits + f * frame_stride_words,
+                                           nranks, rank_stride_words, e->s()));
+                e->sl().marks_set = true;
+                occupancy_grid(e, lifetime, e->s());
+            }
+        }
+        e->invoked_once = true;
+    });
+}
+
+int gdf_import_occupancy_marks_strided(gdf_engine* e, const uint32_t* bits, uint64_t words,
+                                       uint32_t nranks, uint64_t rank_stride_words) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        if (!e->grid_set || !bits) fail(GDF_ERR_STATE, "no voxel grid");
+        if (words < (e->ncells + 31) / 32 || rank_stride_words < words)
+            fail(GDF_ERR_CAPACITY, "mark bitmask too small");
+        HIPCHK(launch_import_marks(marks_ptr(e), mark_words(e), bits, nranks, rank_stride_words,
+                                   e->s()));
         e->sl().marks_set = true;
     });
 }

@@ -1376,6 +1376,48 @@ hipError_t launch_grid_u8(uint8_t* grid, uint32_t* marks, uint64_t ncells, uint3
     return hipGetLastError();
 }
 
+// nframes consecutive grid updates in one pass (batched multi-GPU exchange): frame f's marks are
+// the OR over ranks of bits[r * rank_stride + f * frame_stride + word]; the updates are applied
+// in frame order in registers, so the grid equals nframes sequential k_grid_u8 updates
+__global__ __launch_bounds__(256) void k_grid_u8_batch(uint4* __restrict__ grid,
+                                                       const uint32_t* __restrict__ bits,
+                                                       uint64_t nwords, uint32_t nranks,
+                                                       uint32_t nframes, uint64_t frame_stride,
+                                                       uint64_t rank_stride, uint32_t L,
+                                                       GridSeq q) {
+    const uint32_t f0 = grid_seq_enter(q);
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nwords;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint4 v0 = grid[2 * i], v1 = grid[2 * i + 1];
+        for (uint32_t f = 0; f < nframes; ++f) {
+            uint32_t m = 0;
+            for (uint32_t r = 0; r < nranks; ++r) m |= bits[r * rank_stride + f * frame_stride + i];
+            v0.x = grid_word(v0.x, m, L);
+            v0.y = grid_word(v0.y, m >> 4, L);
+            v0.z = grid_word(v0.z, m >> 8, L);
+            v0.w = grid_word(v0.w, m >> 12, L);
+            v1.x = grid_word(v1.x, m >> 16, L);
+            v1.y = grid_word(v1.y, m >> 20, L);
+            v1.z = grid_word(v1.z, m >> 24, L);
+            v1.w = grid_word(v1.w, m >> 28, L);
+        }
+        grid[2 * i] = v0;
+        grid[2 * i + 1] = v1;
+    }
+    grid_seq_leave(q, f0, gridDim.x);
+}
+
+hipError_t launch_grid_u8_batch(uint8_t* grid, const uint32_t* bits, uint64_t ncells,
+                                uint32_t nranks, uint32_t nframes, uint64_t frame_stride,
+                                uint64_t rank_stride, uint32_t lifetime, const GridSeq& q,
+                                hipStream_t s) {
+    const uint64_t nwords = (ncells + 31) / 32;
+    hipLaunchKernelGGL(k_grid_u8_batch, dim3(grid_blocks(nwords, 256)), dim3(256), 0, s,
+                       reinterpret_cast<uint4*>(grid), bits, nwords, nranks, nframes,
+                       frame_stride, rank_stride, lifetime, q);
+    return hipGetLastError();
+}
+
 // general u32 history (lifetime > 255) with a separate u8 output grid; 32 cells per thread
 __global__ __launch_bounds__(256) void k_grid_u32(uint32_t* __restrict__ hist,
                                                   uint32_t* __restrict__ marks,
@@ -1965,12 +2007,25 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
 // ORs the all-gathered masks of every rank into them.
 __global__ __launch_bounds__(256) void k_import_marks(uint32_t* __restrict__ marks,
                                                       const uint32_t* __restrict__ bits,
-                                                      uint64_t words, uint32_t nranks) {
+                                                      uint64_t words, uint32_t nranks,
+                                                      uint64_t stride) {
     for (uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; w < words;
          w += (uint64_t)gridDim.x * blockDim.x) {
         uint32_t v = marks[w];
-        for (uint32_t r = 0; r < nranks; ++r) v |= bits[(uint64_t)r * words + w];
+        for (uint32_t r = 0; r < nranks; ++r) v |= bits[(uint64_t)r * stride + w];
         marks[w] = v;
+    }
+}
+
+// export that also clears: the frame's marks leave the engine (batched multi-GPU exchange; the
+// next frame of this slot starts from an empty mask, the union comes back through the import)
+__global__ __launch_bounds__(256) void k_take_marks(uint32_t* __restrict__ marks,
+                                                    uint32_t* __restrict__ bits, uint64_t words) {
+    for (uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; w < words;
+         w += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t v = marks[w];
+        bits[w] = v;
+        if (v) marks[w] = 0u;
     }
 }
 
@@ -1979,10 +2034,16 @@ hipError_t launch_export_marks(const uint32_t* marks, uint64_t words, uint32_t* 
     return hipMemcpyAsync(bits, marks, words * 4, hipMemcpyDeviceToDevice, s);
 }
 
+hipError_t launch_take_marks(uint32_t* marks, uint64_t words, uint32_t* bits, hipStream_t s) {
+    hipLaunchKernelGGL(k_take_marks, dim3(grid_blocks(words, 256)), dim3(256), 0, s, marks, bits,
+                       words);
+    return hipGetLastError();
+}
+
 hipError_t launch_import_marks(uint32_t* marks, uint64_t words, const uint32_t* bits,
-                               uint32_t nranks, hipStream_t s) {
+                               uint32_t nranks, uint64_t stride, hipStream_t s) {
     hipLaunchKernelGGL(k_import_marks, dim3(grid_blocks(words, 256)), dim3(256), 0, s, marks, bits,
-                       words, nranks);
+                       words, nranks, stride);
     return hipGetLastError();
 }
 

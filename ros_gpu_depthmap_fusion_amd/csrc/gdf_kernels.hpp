@@ -48,6 +48,10 @@ hipError_t launch_gather_records(const void* rec, uint32_t n, uint32_t step, flo
 // (q: engine order of grid updates across streams, see GridSeq)
 hipError_t launch_grid_u8(uint8_t* grid, uint32_t* marks, uint64_t ncells, uint32_t lifetime,
                           const GridSeq& q, hipStream_t s);
+hipError_t launch_grid_u8_batch(uint8_t* grid, const uint32_t* bits, uint64_t ncells,
+                                uint32_t nranks, uint32_t nframes, uint64_t frame_stride,
+                                uint64_t rank_stride, uint32_t lifetime, const GridSeq& q,
+                                hipStream_t s);
 hipError_t launch_grid_u32(uint32_t* hist, uint32_t* marks, uint8_t* out8, uint64_t ncells,
                            uint32_t lifetime, const GridSeq& q, hipStream_t s);
 hipError_t launch_widen_grid(const uint8_t* grid8, uint32_t* hist, uint64_t ncells,
@@ -100,7 +104,9 @@ size_t voxelize_group_tiles(uint32_t nmax);
 
 // multi-GPU occupancy marks: export = copy of the mark bitmask, import = OR of nranks masks
 hipError_t launch_export_marks(const uint32_t* marks, uint64_t words, uint32_t* bits, hipStream_t s);
+hipError_t launch_take_marks(uint32_t* marks, uint64_t words, uint32_t* bits, hipStream_t s);
+// nranks masks of `words` words, mask r at bits + r * stride
 hipError_t launch_import_marks(uint32_t* marks, uint64_t words, const uint32_t* bits,
-                               uint32_t nranks, hipStream_t s);
+                               uint32_t nranks, uint64_t stride, hipStream_t s);
 
 }  // namespace gdf

@@ -95,7 +95,9 @@ EXPORTED = [
     "gdf_get_point_count", "gdf_download_points", "gdf_download_voxel_coords",
     "gdf_download_voxelized_points", "gdf_download_occupancy_grid", "gdf_get_grid_size",
     "gdf_get_device_results", "gdf_process_frame", "gdf_export_occupancy_marks",
-    "gdf_import_occupancy_marks", "gdf_set_profiling", "gdf_get_kernel_times", "gdf_set_debug", "gdf_debug_stage_masks", "gdf_debug_rollbuffer",
+    "gdf_import_occupancy_marks", "gdf_take_occupancy_marks", "gdf_import_occupancy_marks_strided",
+    "gdf_voxel_occupancy_grid_batch",
+    "gdf_set_profiling", "gdf_get_kernel_times", "gdf_set_debug", "gdf_debug_stage_masks", "gdf_debug_rollbuffer",
     "gdf_debug_historic_grid",
     # include/gdf_driver.h: the component's depth loop in C++ over the C-ABI
     "gdf_run_depth_stream",
@@ -155,6 +157,9 @@ def load_library(path: str = LIB_PATH):
         "gdf_process_frame": (i32, [vp, P(FrameParams), P(FrameResult)]),
         "gdf_export_occupancy_marks": (i32, [vp, vp, u64]),
         "gdf_import_occupancy_marks": (i32, [vp, vp, u64, u32]),
+        "gdf_take_occupancy_marks": (i32, [vp, vp, u64]),
+        "gdf_import_occupancy_marks_strided": (i32, [vp, vp, u64, u32, u64]),
+        "gdf_voxel_occupancy_grid_batch": (i32, [vp, vp, u64, u32, u32, u64, u64, u32]),
         "gdf_set_profiling": (i32, [vp, i32]),
         "gdf_get_kernel_times": (i32, [vp, vp, vp, i32]),
         "gdf_set_debug": (i32, [vp, i32]),
@@ -469,9 +474,24 @@ class GPUDepthmapFusion:
     def export_marks(self, dev_ptr: int, words: int):
         self._check(self._lib.gdf_export_occupancy_marks(self._h, C.c_void_p(dev_ptr), words))
 
-    def import_marks(self, dev_ptr: int, words: int, nranks: int):
-        self._check(self._lib.gdf_import_occupancy_marks(self._h, C.c_void_p(dev_ptr), words,
-                                                         nranks))
+    def import_marks(self, dev_ptr: int, words: int, nranks: int, rank_stride: int = 0):
+        if rank_stride:
+            self._check(self._lib.gdf_import_occupancy_marks_strided(
+                self._h, C.c_void_p(dev_ptr), words, nranks, rank_stride))
+        else:
+            self._check(self._lib.gdf_import_occupancy_marks(self._h, C.c_void_p(dev_ptr), words,
+                                                             nranks))
+
+    def voxelOccupancyGridBatch(self, dev_ptr: int, words: int, nranks: int, nframes: int,
+                                frame_stride: int, rank_stride: int, lifetime: int):
+        """nframes grid updates in one pass from all-gathered mark masks (batched exchange)."""
+        self._check(self._lib.gdf_voxel_occupancy_grid_batch(
+            self._h, C.c_void_p(dev_ptr), words, nranks, nframes, frame_stride, rank_stride,
+            lifetime))
+
+    def take_marks(self, dev_ptr: int, words: int):
+        """Export the marks of the frame just processed and clear them (batched exchange)."""
+        self._check(self._lib.gdf_take_occupancy_marks(self._h, C.c_void_p(dev_ptr), words))
 
     # ---- whole frame ----
     def set_profiling(self, on: bool = True):

@@ -77,3 +77,44 @@ class DeviceMarkExchange:
         self.eng.export_marks(self.local.data_ptr(), self.words)
         dist.all_gather_into_tensor(self.gathered, self.local)
         self.eng.import_marks(self.gathered.data_ptr(), self.words, self.world)
+
+
+class BatchedMarkExchange:
+    """The same exchange for `batch` frames per collective, with the engine's frames pipelined
+    (gdf_set_pipeline_depth) instead of serialised behind a per-frame all-gather.
+
+    Per frame (processed with defer_occupancy_grid): take() moves the frame's marks into slot i of
+    a [batch, words] buffer and clears them in the engine.  flush(lifetime): one all-gather of the
+    [batch, words] buffers of all ranks ([rank, batch, words]), then, in frame order, the union
+    of frame i (masks at stride batch * words) is imported and the grid updated - the grids after
+    every frame are those of the per-frame exchange (occupancy union + in-order updates)."""
+
+    def __init__(self, engine, ncells: int, world: int, batch: int):
+        import torch
+        self.eng = engine
+        self.words = words_for(ncells)
+        self.world = world
+        self.batch = batch
+        self.local = torch.zeros(batch * self.words, dtype=torch.int32, device="cuda")
+        self.gathered = torch.zeros(world * batch * self.words, dtype=torch.int32, device="cuda")
+        self.n = 0
+
+    def take(self):
+        self.eng.take_marks(self.local.data_ptr() + 4 * self.n * self.words, self.words)
+        self.n += 1
+
+    def full(self) -> bool:
+        return self.n == self.batch
+
+    def flush(self, lifetime: int):
+        import torch
+        import torch.distributed as dist
+        if self.n == 0:
+            return
+        self.eng.synchronize()  # the takes (engine streams) before the collective (torch stream)
+        dist.all_gather_into_tensor(self.gathered, self.local)
+        torch.cuda.current_stream().synchronize()  # the collective before the imports
+        # the frames' grid updates in one pass (gdf_voxel_occupancy_grid_batch)
+        self.eng.voxelOccupancyGridBatch(self.gathered.data_ptr(), self.words, self.world, self.n,
+                                         self.words, self.batch * self.words, lifetime)
+        self.n = 0

@@ -553,3 +553,58 @@ def test_large_rollbuffer_window_properties(Engine):
     assert len(gpu.downloadVoxelizedPoints()) == len(np.unique(c))
     grid = gpu.downloadVoxelOccupancyGrid().reshape(-1)
     assert np.array_equal(np.flatnonzero(grid == p.occupancy_lifetime), np.unique(c))
+
+
+def test_batched_mark_exchange_pipelined(Engine):
+    """Batched multi-GPU exchange on one device: two engines (one camera each, 3 frames in
+    flight) process 7 frames with deferred grids, take (export + clear) their marks into
+    [batch, words] buffers, then import each frame's union from the concatenated
+    [rank, batch, words] masks (stride batch * words) and update in frame order; every rank's
+    grid equals the host history of the union, and the u32 history of a per-frame engine."""
+    from ros_gpu_depthmap_fusion_amd import hiprt, multi
+    p = ComponentParams()
+    p.occupancy_lifetime = 5
+    cams = [synth.make_camera(k, 160, 120) for k in range(2)]
+    gpus = [Engine() for _ in cams]
+    for g in gpus:
+        g.set_pipeline_depth(3)
+    orcs = [OracleFusion(threads=4) for _ in cams]
+    batch, nframes = 4, 7
+    hist = None
+    done = 0
+    while done < nframes:
+        nb = min(batch, nframes - done)
+        bufs, unions = [], []
+        for k, (c, g, o) in enumerate(zip(cams, gpus, orcs)):
+            (_, _, _), ncells = (None, None, None), None
+            local = None
+            for i in range(nb):
+                f = done + i
+                args = [cam_args(c, synth.depth_frame(c, k, f))]
+                run_fused(g, args, p, defer_occupancy_grid=True, synchronous=False)
+                run_fused(o, args, p)
+                _, ncells = g.grid_size()
+                nw = multi.words_for(ncells)
+                if local is None:
+                    local = hiprt.DeviceArray(batch * nw * 4)
+                g.take_marks(local.ptr + 4 * i * nw, nw)
+                m = np.zeros(ncells, bool)
+                m[o.downloadVoxelCoords()] = True
+                if k == 0:
+                    unions.append(m)
+                else:
+                    unions[i] |= m
+            g.synchronize()
+            bufs.append(local.to_numpy(np.uint32, batch * nw))
+        both = hiprt.DeviceArray.from_numpy(np.concatenate(bufs))
+        for i in range(nb):
+            hist = np.zeros(ncells, np.uint32) if hist is None else hist
+            hist = multi.historic_update(hist, unions[i], p.occupancy_lifetime)
+            for g in gpus:
+                g.import_marks(both.ptr + 4 * i * nw, nw, 2, rank_stride=batch * nw)
+                g.voxelOccupancyGrid(p.occupancy_lifetime)
+        for k, g in enumerate(gpus):
+            np.testing.assert_array_equal(g.downloadVoxelOccupancyGrid().reshape(-1),
+                                          (hist & 0xFF).astype(np.uint8),
+                                          err_msg=f"frames {done}..{done + nb} rank {k}")
+        done += nb
