@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--pipeline", type=int, default=3,
                     help="frames in flight on one GPU (engine slots, gdf_set_pipeline_depth); "
                          "N > 1 runs on torch's stream with depth 1")
-    ap.add_argument("--exchange-batch", type=int, default=8,
+    ap.add_argument("--exchange-batch", type=int, default=16,
                     help="N > 1: frames per occupancy-mark all-gather (multi.BatchedMarkExchange; "
                          "1 = one collective per frame on torch's stream, no pipelining)")
     ap.add_argument("--no-cpu-baseline", action="store_true")

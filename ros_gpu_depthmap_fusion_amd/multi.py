@@ -85,9 +85,9 @@ class BatchedMarkExchange:
 
     Per frame (processed with defer_occupancy_grid): take() moves the frame's marks into slot i of
     a [batch, words] buffer and clears them in the engine.  flush(lifetime): one all-gather of the
-    [batch, words] buffers of all ranks ([rank, batch, words]), then, in frame order, the union
-    of frame i (masks at stride batch * words) is imported and the grid updated - the grids after
-    every frame are those of the per-frame exchange (occupancy union + in-order updates)."""
+    [batch, words] buffers of all ranks ([rank, batch, words]), then the batch's grid updates in
+    ONE pass, frame after frame in registers (union of frame i: the masks at stride
+    batch * words) - the grid equals that of the per-frame exchange."""
 
     def __init__(self, engine, ncells: int, world: int, batch: int):
         import torch
