@@ -274,6 +274,9 @@ def main():
                        "cameras_per_gpu": K, "points_per_frame_after_crop": round(n_avg),
                        "voxels_per_frame": round(g_avg), "grid_cells": ncells,
                        "frames_in_flight": depth,
+                       "exchange": ("sparse mark pairs (cap %d words/frame), %d dense-fallback "
+                                    "batches" % (marks.cap, marks.dense_batches)
+                                    if batched else None),
                        "parallelism": ("camera-per-GPU x%d, occupancy-mark all-gather every %d "
                                        "frame(s)" % (world, args.exchange_batch if batched else 1))
                        if dist is not None else "single GPU"},

@@ -1661,6 +1661,29 @@ int gdf_take_occupancy_marks(gdf_engine* e, uint32_t* bits, uint64_t words) {
     });
 }
 
+int gdf_take_occupancy_marks_sparse(gdf_engine* e, uint32_t* bits, uint64_t words,
+                                    uint32_t* pairs, uint32_t cap) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        if (!e->grid_set || !bits || !pairs) fail(GDF_ERR_STATE, "no voxel grid");
+        if (words < (e->ncells + 31) / 32) fail(GDF_ERR_CAPACITY, "mark bitmask too small");
+        HIPCHK(launch_take_marks_sparse(marks_ptr(e), mark_words(e), bits, pairs, cap, e->s()));
+        e->sl().marks_set = false;
+    });
+}
+
+int gdf_union_occupancy_pairs(gdf_engine* e, uint32_t* union_bits, uint64_t words,
+                              const uint32_t* pairs, uint32_t nranks, uint32_t nframes,
+                              uint64_t record_words) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        if (!e->grid_set || !union_bits || (!pairs && nranks * nframes)) fail(GDF_ERR_STATE, "no voxel grid");
+        if (words < (e->ncells + 31) / 32) fail(GDF_ERR_CAPACITY, "union bitmask too small");
+        HIPCHK(launch_union_pairs(union_bits, mark_words(e), pairs, nranks, nframes, record_words,
+                                  e->s()));
+    });
+}
+
 int gdf_voxel_occupancy_grid_batch(gdf_engine* e, const uint32_t* bits, uint64_t words,
                                    uint32_t nranks, uint32_t nframes, uint64_t frame_stride_words,
                                    uint64_t rank_stride_words, uint32_t lifetime) {

@@ -2029,6 +2029,75 @@ __global__ __launch_bounds__(256) void k_take_marks(uint32_t* __restrict__ marks
     }
 }
 
+// take + sparse form: besides the bitmask, the non-zero words as (index, word) pairs -
+// pairs[0] = number of non-zero words (may exceed cap: then only the bitmask is complete),
+// pairs[1 + 2k], pairs[2 + 2k] = k-th pair (any order; OR-merged on import).  pairs[0] must be 0
+// on entry.
+__global__ __launch_bounds__(256) void k_take_marks_sparse(uint32_t* __restrict__ marks,
+                                                           uint32_t* __restrict__ bits,
+                                                           uint64_t words,
+                                                           uint32_t* __restrict__ pairs,
+                                                           uint32_t cap) {
+    const int lane = threadIdx.x & 63;
+    for (uint64_t base = blockIdx.x * (uint64_t)blockDim.x; base < words;
+         base += (uint64_t)gridDim.x * blockDim.x) {  // wave-uniform
+        const uint64_t w = base + threadIdx.x;
+        const uint32_t v = w < words ? marks[w] : 0u;
+        if (w < words) {
+            bits[w] = v;
+            if (v) marks[w] = 0u;
+        }
+        const unsigned long long nz = __ballot(v != 0u);
+        if (!nz) continue;
+        uint32_t first = 0;
+        if (lane == 0) first = atomicAdd(pairs, (uint32_t)__popcll(nz));
+        first = __shfl(first, 0, 64);
+        if (v) {
+            const uint32_t k = first + (uint32_t)__popcll(nz & lanemask_lt());
+            if (k < cap) {
+                pairs[1 + 2 * k] = (uint32_t)w;
+                pairs[2 + 2 * k] = v;
+            }
+        }
+    }
+}
+
+// OR the pairs of `nranks` x `nframes` sparse masks (record r, f at pairs + (r * nframes + f) *
+// rec_words) into union[f * words + index]; union zeroed on entry.  Every record fits its cap.
+__global__ __launch_bounds__(256) void k_union_pairs(uint32_t* __restrict__ uni, uint64_t words,
+                                                     const uint32_t* __restrict__ pairs,
+                                                     uint32_t nranks, uint32_t nframes,
+                                                     uint64_t rec_words) {
+    const uint32_t rec = blockIdx.y;  // r * nframes + f
+    const uint32_t f = rec % nframes;
+    const uint32_t* p = pairs + (uint64_t)rec * rec_words;
+    const uint32_t n = p[0];
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+        const uint32_t idx = p[1 + 2 * k], v = p[2 + 2 * k];
+        if (idx < words) atomicOr(uni + (uint64_t)f * words + idx, v);
+    }
+    (void)nranks;
+}
+
+hipError_t launch_take_marks_sparse(uint32_t* marks, uint64_t words, uint32_t* bits,
+                                    uint32_t* pairs, uint32_t cap, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(pairs, 0, 4, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_take_marks_sparse, dim3(grid_blocks(words, 256)), dim3(256), 0, s, marks,
+                       bits, words, pairs, cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_union_pairs(uint32_t* uni, uint64_t words, const uint32_t* pairs,
+                              uint32_t nranks, uint32_t nframes, uint64_t rec_words,
+                              hipStream_t s) {
+    hipError_t e = hipMemsetAsync(uni, 0, (size_t)nframes * words * 4, s);
+    if (e != hipSuccess || nranks * nframes == 0) return e;
+    hipLaunchKernelGGL(k_union_pairs, dim3(8, nranks * nframes), dim3(256), 0, s, uni, words,
+                       pairs, nranks, nframes, rec_words);
+    return hipGetLastError();
+}
+
 hipError_t launch_export_marks(const uint32_t* marks, uint64_t words, uint32_t* bits,
                                hipStream_t s) {
     return hipMemcpyAsync(bits, marks, words * 4, hipMemcpyDeviceToDevice, s);

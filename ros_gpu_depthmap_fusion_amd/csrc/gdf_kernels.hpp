@@ -105,6 +105,11 @@ size_t voxelize_group_tiles(uint32_t nmax);
 // multi-GPU occupancy marks: export = copy of the mark bitmask, import = OR of nranks masks
 hipError_t launch_export_marks(const uint32_t* marks, uint64_t words, uint32_t* bits, hipStream_t s);
 hipError_t launch_take_marks(uint32_t* marks, uint64_t words, uint32_t* bits, hipStream_t s);
+hipError_t launch_take_marks_sparse(uint32_t* marks, uint64_t words, uint32_t* bits,
+                                    uint32_t* pairs, uint32_t cap, hipStream_t s);
+hipError_t launch_union_pairs(uint32_t* uni, uint64_t words, const uint32_t* pairs,
+                              uint32_t nranks, uint32_t nframes, uint64_t rec_words,
+                              hipStream_t s);
 // nranks masks of `words` words, mask r at bits + r * stride
 hipError_t launch_import_marks(uint32_t* marks, uint64_t words, const uint32_t* bits,
                                uint32_t nranks, uint64_t stride, hipStream_t s);

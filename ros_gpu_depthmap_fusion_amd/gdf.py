@@ -96,7 +96,7 @@ EXPORTED = [
     "gdf_download_voxelized_points", "gdf_download_occupancy_grid", "gdf_get_grid_size",
     "gdf_get_device_results", "gdf_process_frame", "gdf_export_occupancy_marks",
     "gdf_import_occupancy_marks", "gdf_take_occupancy_marks", "gdf_import_occupancy_marks_strided",
-    "gdf_voxel_occupancy_grid_batch",
+    "gdf_voxel_occupancy_grid_batch", "gdf_take_occupancy_marks_sparse", "gdf_union_occupancy_pairs",
     "gdf_set_profiling", "gdf_get_kernel_times", "gdf_set_debug", "gdf_debug_stage_masks", "gdf_debug_rollbuffer",
     "gdf_debug_historic_grid",
     # include/gdf_driver.h: the component's depth loop in C++ over the C-ABI
@@ -160,6 +160,8 @@ def load_library(path: str = LIB_PATH):
         "gdf_take_occupancy_marks": (i32, [vp, vp, u64]),
         "gdf_import_occupancy_marks_strided": (i32, [vp, vp, u64, u32, u64]),
         "gdf_voxel_occupancy_grid_batch": (i32, [vp, vp, u64, u32, u32, u64, u64, u32]),
+        "gdf_take_occupancy_marks_sparse": (i32, [vp, vp, u64, vp, u32]),
+        "gdf_union_occupancy_pairs": (i32, [vp, vp, u64, vp, u32, u32, u64]),
         "gdf_set_profiling": (i32, [vp, i32]),
         "gdf_get_kernel_times": (i32, [vp, vp, vp, i32]),
         "gdf_set_debug": (i32, [vp, i32]),
@@ -488,6 +490,17 @@ class GPUDepthmapFusion:
         self._check(self._lib.gdf_voxel_occupancy_grid_batch(
             self._h, C.c_void_p(dev_ptr), words, nranks, nframes, frame_stride, rank_stride,
             lifetime))
+
+    def take_marks_sparse(self, dev_ptr: int, words: int, pairs_ptr: int, cap: int):
+        """take_marks plus the non-zero words as (index, word) pairs (pairs[0] = count)."""
+        self._check(self._lib.gdf_take_occupancy_marks_sparse(
+            self._h, C.c_void_p(dev_ptr), words, C.c_void_p(pairs_ptr), cap))
+
+    def union_pairs(self, union_ptr: int, words: int, pairs_ptr: int, nranks: int, nframes: int,
+                    record_words: int):
+        self._check(self._lib.gdf_union_occupancy_pairs(
+            self._h, C.c_void_p(union_ptr), words, C.c_void_p(pairs_ptr), nranks, nframes,
+            record_words))
 
     def take_marks(self, dev_ptr: int, words: int):
         """Export the marks of the frame just processed and clear them (batched exchange)."""

@@ -89,7 +89,7 @@ class BatchedMarkExchange:
     ONE pass, frame after frame in registers (union of frame i: the masks at stride
     batch * words) - the grid equals that of the per-frame exchange."""
 
-    def __init__(self, engine, ncells: int, world: int, batch: int):
+    def __init__(self, engine, ncells: int, world: int, batch: int, sparse_cap: int = -1):
         import torch
         self.eng = engine
         self.words = words_for(ncells)
@@ -97,10 +97,24 @@ class BatchedMarkExchange:
         self.batch = batch
         self.local = torch.zeros(batch * self.words, dtype=torch.int32, device="cuda")
         self.gathered = torch.zeros(world * batch * self.words, dtype=torch.int32, device="cuda")
+        # sparse records: the non-zero mark words as (index, word) pairs (gdf_take_occupancy_marks
+        # _sparse); the bitmasks travel only when some rank's frame has more than `cap`
+        self.cap = max(1024, self.words // 16) if sparse_cap < 0 else sparse_cap
+        self.rec = 1 + 2 * self.cap
+        if self.cap:
+            self.pairs = torch.zeros(batch * self.rec, dtype=torch.int32, device="cuda")
+            self.gpairs = torch.zeros(world * batch * self.rec, dtype=torch.int32, device="cuda")
+            self.union = torch.zeros(batch * self.words, dtype=torch.int32, device="cuda")
         self.n = 0
+        self.dense_batches = 0
 
     def take(self):
-        self.eng.take_marks(self.local.data_ptr() + 4 * self.n * self.words, self.words)
+        dst = self.local.data_ptr() + 4 * self.n * self.words
+        if self.cap:
+            self.eng.take_marks_sparse(dst, self.words,
+                                       self.pairs.data_ptr() + 4 * self.n * self.rec, self.cap)
+        else:
+            self.eng.take_marks(dst, self.words)
         self.n += 1
 
     def full(self) -> bool:
@@ -112,9 +126,22 @@ class BatchedMarkExchange:
         if self.n == 0:
             return
         self.eng.synchronize()  # the takes (engine streams) before the collective (torch stream)
-        dist.all_gather_into_tensor(self.gathered, self.local)
-        torch.cuda.current_stream().synchronize()  # the collective before the imports
-        # the frames' grid updates in one pass (gdf_voxel_occupancy_grid_batch)
-        self.eng.voxelOccupancyGridBatch(self.gathered.data_ptr(), self.words, self.world, self.n,
-                                         self.words, self.batch * self.words, lifetime)
+        dense = not self.cap
+        if self.cap:
+            dist.all_gather_into_tensor(self.gpairs, self.pairs)
+            counts = self.gpairs.view(self.world, self.batch, self.rec)[:, :self.n, 0]
+            dense = bool((counts > self.cap).any().item())  # same answer on every rank
+        if dense:
+            self.dense_batches += 1
+            dist.all_gather_into_tensor(self.gathered, self.local)
+            torch.cuda.current_stream().synchronize()  # the collective before the update
+            self.eng.voxelOccupancyGridBatch(self.gathered.data_ptr(), self.words, self.world,
+                                             self.n, self.words, self.batch * self.words,
+                                             lifetime)
+        else:
+            torch.cuda.current_stream().synchronize()
+            self.eng.union_pairs(self.union.data_ptr(), self.words, self.gpairs.data_ptr(),
+                                 self.world, self.batch, self.rec)
+            self.eng.voxelOccupancyGridBatch(self.union.data_ptr(), self.words, 1, self.n,
+                                             self.words, self.batch * self.words, lifetime)
         self.n = 0

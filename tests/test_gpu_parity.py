@@ -608,3 +608,49 @@ def test_batched_mark_exchange_pipelined(Engine):
                                           (hist & 0xFF).astype(np.uint8),
                                           err_msg=f"frames {done}..{done + nb} rank {k}")
         done += nb
+
+
+def test_sparse_mark_pairs_and_union(Engine):
+    """take_marks_sparse: the pairs are exactly the non-zero words of the taken bitmask (any
+    order), the engine's marks are cleared; union_pairs of two records ORs them; an over-cap
+    record reports its full count (the caller then falls back to the bitmasks)."""
+    from ros_gpu_depthmap_fusion_amd import hiprt, multi
+    p = ComponentParams()
+    gpu = Engine()
+    recs, masks = [], []
+    cap = 4096
+    for k in range(2):
+        cam = synth.make_camera(k, 200, 150)
+        run_fused(gpu, [cam_args(cam, synth.depth_frame(cam, k, 3))], p, defer_occupancy_grid=True)
+        _, ncells = gpu.grid_size()
+        nw = multi.words_for(ncells)
+        bits = hiprt.DeviceArray(nw * 4)
+        pairs = hiprt.DeviceArray((1 + 2 * cap) * 4)
+        gpu.take_marks_sparse(bits.ptr, nw, pairs.ptr, cap)
+        gpu.synchronize()
+        b = bits.to_numpy(np.uint32, nw)
+        pr = pairs.to_numpy(np.uint32, 1 + 2 * cap)
+        nz = np.flatnonzero(b)
+        assert pr[0] == len(nz) <= cap
+        idx, val = pr[1:1 + 2 * pr[0]:2], pr[2:2 + 2 * pr[0]:2]
+        order = np.argsort(idx)
+        np.testing.assert_array_equal(idx[order], nz)
+        np.testing.assert_array_equal(val[order], b[nz])
+        recs.append(pr)
+        masks.append(b)
+        # marks were cleared: a second take finds none
+        gpu.take_marks_sparse(bits.ptr, nw, pairs.ptr, cap)
+        gpu.synchronize()
+        assert pairs.to_numpy(np.uint32, 1)[0] == 0 and not bits.to_numpy(np.uint32, nw).any()
+    both = hiprt.DeviceArray.from_numpy(np.concatenate(recs))
+    uni = hiprt.DeviceArray(nw * 4)
+    gpu.union_pairs(uni.ptr, nw, both.ptr, 2, 1, 1 + 2 * cap)
+    gpu.synchronize()
+    np.testing.assert_array_equal(uni.to_numpy(np.uint32, nw), masks[0] | masks[1])
+    # over cap: count is complete, the pairs stop at cap
+    cam = synth.make_camera(0, 200, 150)
+    run_fused(gpu, [cam_args(cam, synth.depth_frame(cam, 0, 4))], p, defer_occupancy_grid=True)
+    small = hiprt.DeviceArray((1 + 2 * 8) * 4)
+    gpu.take_marks_sparse(bits.ptr, nw, small.ptr, 8)
+    gpu.synchronize()
+    assert small.to_numpy(np.uint32, 1)[0] == np.count_nonzero(bits.to_numpy(np.uint32, nw)) > 8
