@@ -206,6 +206,7 @@ struct Slot {
     uint32_t dbg_count = 0;
     DevBuf d_ka, d_kb, d_va, d_vb, d_sstatus, d_sgstatus, d_gstatus, d_ggstatus, d_vox;
     DevBuf d_gcnt, d_goff;          // group starts per tile + their scan (large frames)
+    DevBuf d_bigq, d_bigcnt;        // long voxels queued for k_group_big (large frames)
     bool vox_valid = false;
     DevBuf d_markbits;              // this frame's occupancy marks (1 bit per cell)
     uint32_t marks_gen = ~0u;
@@ -996,6 +997,8 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime) 
     const uint32_t gtiles = (uint32_t)voxelize_group_tiles(nmax);
     e->sl().d_gcnt.ensure((size_t)gtiles * 4);
     e->sl().d_goff.ensure(seg_offsets_words(gtiles) * 4);
+    e->sl().d_bigq.ensure((size_t)(gtiles + 2048) * 16);  // <= 1 long voxel per tile
+    e->sl().d_bigcnt.ensure(2048 * 4);
     VoxelizeArgs v;
     std::memset(&v, 0, sizeof(v));
     v.keys = e->sl().d_coords.as<uint32_t>();
@@ -1020,6 +1023,8 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime) 
     // (each tile publishes 256 look-back words: 2 KiB per 1 Ki keys at PT=4)
     v.group_counts = e->sl().d_gcnt.as<uint32_t>();
     v.group_offsets = e->sl().d_goff.as<uint32_t>();
+    v.bigq = e->sl().d_bigq.as<uint4>();
+    v.bigcnt = e->sl().d_bigcnt.as<uint32_t>();
     v.sort_pt = e->sort_pt ? e->sort_pt : nmax <= (1u << 20) ? 4 : nmax <= (1u << 24) ? 8 : 16;
     v.err = e->sl().d_misc.as<uint32_t>() + kErr;
     v.out = e->sl().d_vox.as<float4>();

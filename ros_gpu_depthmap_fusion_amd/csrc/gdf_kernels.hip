@@ -1710,9 +1710,10 @@ __global__ __launch_bounds__(kGroupThreads) __attribute__((amdgpu_waves_per_eu(8
     const uint32_t* __restrict__ count, const float4* __restrict__ pts, float* __restrict__ out,
     uint32_t* __restrict__ out_count, unsigned long long* status, unsigned long long* gstatus,
     uint32_t* tile_ctr, uint32_t* epoch_word, uint32_t* err, uint32_t* hist, int average,
-    VoxelParams vp, uint32_t* marks, const uint32_t* tile_base) {
+    VoxelParams vp, uint32_t* marks, const uint32_t* tile_base, uint4* __restrict__ bigq,
+    uint32_t* __restrict__ bigcnt, uint32_t bigcap) {
     __shared__ uint32_t s_wave[4];
-    __shared__ uint32_t s_tile, s_epoch, s_excl, s_nbig;
+    __shared__ uint32_t s_tile, s_epoch, s_excl, s_nbig, s_nq;
     __shared__ uint32_t s_start[kGroupThreads + 1];
     __shared__ uint32_t s_big[kGroupThreads];
     __shared__ float4 s_buf[4][kSumChunk];
@@ -1730,6 +1731,7 @@ __global__ __launch_bounds__(kGroupThreads) __attribute__((amdgpu_waves_per_eu(8
     const Tickets tk = tickets(ntiles, gridDim.x);
     if (!tile_base && blockIdx.x >= tk.nblk) return;
     if (!tile_base && threadIdx.x == 0) s_epoch = read_epoch(epoch_word);
+    if (threadIdx.x == 0) s_nq = 0;
     uint32_t walk = blockIdx.x;
     for (bool first = true;; first = false) {  // persistent
     if (!first && !tile_base && tk.oneshot) return;
@@ -1745,7 +1747,10 @@ __global__ __launch_bounds__(kGroupThreads) __attribute__((amdgpu_waves_per_eu(8
     walk += gridDim.x;
     __syncthreads();
     const uint32_t tile = s_tile, epoch = s_epoch;
-    if (tile >= ntiles) return;  // block-uniform
+    if (tile >= ntiles) {  // block-uniform
+        if (bigq && threadIdx.x == 0) bigcnt[blockIdx.x] = s_nq;
+        return;
+    }
     const uint32_t i = tile * kGroupThreads + threadIdx.x;
     const uint32_t tend = min(n, (tile + 1) * kGroupThreads);
     const uint32_t key = i < n ? keys[i] : 0u;
@@ -1846,6 +1851,12 @@ __global__ __launch_bounds__(kGroupThreads) __attribute__((amdgpu_waves_per_eu(8
             }
             const float fc = (float)(e - s);
             *reinterpret_cast<float4*>(o) = make_float4(ax / fc, ay / fc, az / fc, aw);
+        } else if (bigq && e - S0 > staged) {
+            // a voxel reaching past the staged points (at most the tile's last group): summed
+            // by k_group_big, so this block's other waves do not wait at the tile barrier for
+            // its chain (a block walks ~20 tiles; a voxel can hold 10^4 points)
+            bigq[(size_t)blockIdx.x * bigcap + s_nq] = make_uint4(g, s, e, 0u);
+            s_nq = s_nq + 1u;
         } else {
             s_big[atomicAdd(&s_nbig, 1u)] = threadIdx.x;
         }
@@ -1918,6 +1929,74 @@ __global__ __launch_bounds__(kGroupThreads) __attribute__((amdgpu_waves_per_eu(8
     }
 }
 
+// The long voxels queued by k_group (large frames): one wave per voxel, independent of tiles and
+// block barriers; the same sequential f32 sum in index order as k_group's wave path.
+__global__ __launch_bounds__(256) void k_group_big(const uint32_t* __restrict__ vals,
+                                                   const float4* __restrict__ pts,
+                                                   float* __restrict__ out,
+                                                   const uint4* __restrict__ bigq,
+                                                   const uint32_t* __restrict__ bigcnt,
+                                                   uint32_t nblocks, uint32_t bigcap) {
+    __shared__ float4 s_buf[4][kSumChunk];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint64_t nslots = (uint64_t)nblocks * bigcap;
+    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t slot = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wid; slot < nslots;
+         slot += waves) {  // wave-uniform
+        const uint32_t b = (uint32_t)(slot / bigcap), k = (uint32_t)(slot % bigcap);
+        if (k >= bigcnt[b]) continue;
+        const uint4 q = bigq[slot];
+        const uint32_t g = q.x, s = q.y, e = q.z;
+        float acc = 0.0f;
+        // point indices two chunks ahead, points one chunk ahead of the chunk being summed: the
+        // chain never waits on an index load
+        constexpr int Q = kSumChunk / 64;
+        uint32_t v1[Q], v2[Q];
+        float4 r[Q];
+#pragma unroll
+        for (int qq = 0; qq < Q; ++qq) {
+            const uint32_t k0 = s + qq * 64 + lane;
+            r[qq] = k0 < e ? pts[vals[k0]] : make_float4(0.f, 0.f, 0.f, 0.f);
+            const uint32_t k1 = k0 + kSumChunk, k2 = k0 + 2 * kSumChunk;
+            v1[qq] = k1 < e ? vals[k1] : 0xFFFFFFFFu;
+            v2[qq] = k2 < e ? vals[k2] : 0xFFFFFFFFu;
+        }
+        for (uint32_t c = s; c < e; c += kSumChunk) {
+#pragma unroll
+            for (int qq = 0; qq < Q; ++qq) {
+                s_buf[wid][qq * 64 + lane] = r[qq];
+                r[qq] = v1[qq] != 0xFFFFFFFFu ? pts[v1[qq]] : make_float4(0.f, 0.f, 0.f, 0.f);
+                v1[qq] = v2[qq];
+                const uint32_t k3 = c + 3 * kSumChunk + qq * 64 + lane;
+                v2[qq] = k3 < e ? vals[k3] : 0xFFFFFFFFu;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (lane < 4) {
+                const float* comp = reinterpret_cast<const float*>(&s_buf[wid][0]) + lane;
+                const uint32_t m = (e - c) < (uint32_t)kSumChunk ? (e - c) : (uint32_t)kSumChunk;
+                uint32_t j = 0;
+                for (; j + 16 <= m; j += 16) {
+                    float t[16];
+#pragma unroll
+                    for (int qq = 0; qq < 16; ++qq) t[qq] = comp[4 * (j + qq)];
+#pragma unroll
+                    for (int qq = 0; qq < 16; ++qq) acc = acc + t[qq];
+                }
+                for (; j < m; ++j) acc = acc + comp[4 * j];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        if (lane < 4) {
+            const float fc = (float)(e - s);
+            out[4 * (size_t)g + lane] = lane < 3 ? acc / fc : acc;
+        }
+    }
+}
+
 size_t voxelize_status_words(uint32_t nmax) {
     return (size_t)((nmax + kSortThreads * 4 - 1) / (kSortThreads * 4) + 1) * 256;
 }
@@ -1977,6 +2056,8 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
     const uint32_t group_tiles = std::min<uint32_t>(max_tiles, kPersistBlocks);
     HookScope hs(hook, GDF_KERNEL_GROUP);
     const uint32_t* tile_base = nullptr;
+    const uint32_t bigcap = (max_tiles + std::max<uint32_t>(group_tiles, 1u) - 1) /
+                            std::max<uint32_t>(group_tiles, 1u);  // tiles per block (walk)
     if (a.group_counts && max_tiles > kGroupScanTiles) {
         // many tiles: their group-id offsets from a count + scan instead of one ticket each
         // (a single ticket counter serves ~10^2 draws per microsecond)
@@ -1998,7 +2079,13 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
                        vin, a.count, a.pts, reinterpret_cast<float*>(a.out), a.out_count,
                        a.gstatus, a.ggstatus, reinterpret_cast<uint32_t*>(a.ctrs + kCtrGroup),
                        reinterpret_cast<uint32_t*>(a.ctrs + kCtrEpoch), a.err, a.hist, a.average,
-                       a.vp, a.group_marks, tile_base);
+                       a.vp, a.group_marks, tile_base, tile_base ? a.bigq : nullptr,
+                       a.bigcnt, bigcap);
+    if (tile_base && a.bigq && a.average) {
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_group_big, dim3(2048), dim3(256), 0, s, vin, a.pts,
+                           reinterpret_cast<float*>(a.out), a.bigq, a.bigcnt, group_tiles, bigcap);
+    }
     return hipGetLastError();
 }
 

@@ -90,6 +90,8 @@ struct VoxelizeArgs {
     uint32_t* group_marks;          // optional: k_group sets the occupancy mark of every voxel
     uint32_t* group_counts;         // [group tiles] group starts per tile (large frames)
     uint32_t* group_offsets;        // [seg_offsets_words(group tiles)] their scan
+    uint4* bigq;                    // [group blocks * tiles per block] long voxels (large frames)
+    uint32_t* bigcnt;               // [group blocks] queued per block
     GridSeq gseq;                   // engine order of the fused grid update (frame pipelining)
     uint64_t ncells;
     uint32_t lifetime;
