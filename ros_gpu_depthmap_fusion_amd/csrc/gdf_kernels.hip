@@ -998,7 +998,8 @@ __global__ __launch_bounds__(1024) void k_sel(FrameArgs a) {
     // block-uniform, read once into scalar registers, and the stage bits are computed without
     // branches; a tile reaching into the next sequence takes the per-point lookup
     const bool one_seq = si0 + kSelSegs * B <= g.next;
-    for (uint32_t j = i; j < (1u << kMarkCacheBits); j += B) s_mark[j] = 0xFFFFFFFFu;
+    if (a.marks)  // (rollbuffer frames of processFrame take their marks from the voxel groups)
+        for (uint32_t j = i; j < (1u << kMarkCacheBits); j += B) s_mark[j] = 0xFFFFFFFFu;
     uint32_t bits[kSelSegs];
     if (one_seq) {
         const gptr<const float> Tc = G(a.tfc + 16 * (size_t)g.tf0);
