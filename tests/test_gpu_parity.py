@@ -555,7 +555,8 @@ def test_large_rollbuffer_window_properties(Engine):
     assert np.array_equal(np.flatnonzero(grid == p.occupancy_lifetime), np.unique(c))
 
 
-def test_batched_mark_exchange_pipelined(Engine):
+@pytest.mark.parametrize("lifetime", [5, 300])
+def test_batched_mark_exchange_pipelined(Engine, lifetime):
     """Batched multi-GPU exchange on one device: two engines (one camera each, 3 frames in
     flight) process 7 frames with deferred grids, take (export + clear) their marks into
     [batch, words] buffers, then import each frame's union from the concatenated
@@ -563,7 +564,7 @@ def test_batched_mark_exchange_pipelined(Engine):
     grid equals the host history of the union, and the u32 history of a per-frame engine."""
     from ros_gpu_depthmap_fusion_amd import hiprt, multi
     p = ComponentParams()
-    p.occupancy_lifetime = 5
+    p.occupancy_lifetime = lifetime  # 300: the u32 history (frame-by-frame inside the batch call)
     cams = [synth.make_camera(k, 160, 120) for k in range(2)]
     gpus = [Engine() for _ in cams]
     for g in gpus:
