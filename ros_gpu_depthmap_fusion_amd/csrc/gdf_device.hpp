@@ -20,6 +20,7 @@ constexpr uint32_t kFusedPrefixSegs = 4096;  // up to this many segments k_emit 
 constexpr uint32_t kSelSegs = 8;      // rollbuffer points per k_sel thread (default; 4, 8, 16)
 constexpr uint32_t kSelThreads = 512; // k_sel block (default): a tile is segs * threads points
 constexpr int kSortThreads = 256;
+constexpr int kSortGroup = 8;         // radix tiles per look-back group (group granules: tiles / 8)
 // the voxel-key digit histogram is accumulated into kHistReps replicas of [4 passes][256 digits]
 // (block b adds into replica b % kHistReps): same-address atomics from hundreds of blocks
 // serialise at the memory-side atomic unit; the sort pass sums the replicas of its digit

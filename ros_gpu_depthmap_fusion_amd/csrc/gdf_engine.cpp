@@ -990,7 +990,7 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime) 
     e->sl().d_va.ensure((size_t)nmax * 4);
     e->sl().d_vb.ensure((size_t)nmax * 4);
     e->sl().d_sstatus.ensure_zero(voxelize_status_words(nmax) * 8, e->s());
-    e->sl().d_sgstatus.ensure_zero((voxelize_status_words(nmax) / 16 + 256) * 8, e->s());
+    e->sl().d_sgstatus.ensure_zero((voxelize_status_words(nmax) / kSortGroup + 256) * 8, e->s());
     e->sl().d_gstatus.ensure_zero(voxelize_group_tiles(nmax) * 8, e->s());
     e->sl().d_ggstatus.ensure_zero((voxelize_group_tiles(nmax) / 64 + 2) * 8, e->s());
     e->sl().d_vox.ensure((size_t)nmax * 16);

@@ -218,8 +218,8 @@ __device__ __forceinline__ uint32_t lookback2_wave(unsigned long long* tstat,
 }
 
 // The same two-level scheme with one channel per THREAD (the 256 digits of a radix pass):
-// groups of 16 tiles, 16 independent polls per round trip.
-constexpr int kSortGroup = 16;
+// groups of kSortGroup (8) tiles, 8 independent polls per round trip (8 rather than 16: 45 fewer
+// VGPRs in the radix pass, occupancy 4 -> 6 waves/SIMD at 4 keys per thread).
 __device__ __forceinline__ uint32_t lookback2_chan(unsigned long long* tstat,
                                                    unsigned long long* gstat, uint32_t tile,
                                                    uint32_t ntiles, uint32_t chan, uint32_t agg,
