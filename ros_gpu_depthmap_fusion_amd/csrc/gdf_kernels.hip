@@ -919,6 +919,9 @@ __global__ __launch_bounds__(1024) void k_emit(FrameArgs a) {
     int k = 0;
     for (int c = 0; c < a.ncams; ++c)
         if (cams[c].emit && s >= cams[c].seg0 && s < cams[c].seg0 + cams[c].nseg) k = c;
+    // block-uniform camera: its descriptor (device copy beyond kArgCams cameras) is read with
+    // scalar loads, not once per lane
+    k = __builtin_amdgcn_readfirstlane(k);
     const uint32_t j = s - cams[k].seg0;
     const uint32_t y = j / cams[k].nchunk;
     const uint32_t x0 = (j - y * cams[k].nchunk) * cams[k].segw;
