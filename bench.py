@@ -7,19 +7,30 @@ cells 0.1/0.1/0.12 -> 400x400x21 = 3.36 M cells; voxelize with averaging; lifeti
 A step = one full frame of GPUDepthmapFusionComponent::processDepthmaps on the GPU: fused
 convert+flying+crop+ordered compaction+voxel keys+occupancy marks, GPU voxelize (radix sort +
 ordered means), historic-grid update.  Frames are device-resident (a ring of distinct frames
-generated once and uploaded before timing).
+generated once and uploaded before timing).  The default frames are the realistic-density set
+(synth.dense_frame: ~65 % of the pixels survive the flying-pixel filter); `--workload stress` is
+round 1's independent-noise set.
+
+Before the timed region every engine slot has captured its frame graph (`prime`, independent of
+--warmup), so the steady state does not depend on --steps / --warmup.
+
+N = 1 also reports, in "secondary", the same line for 720p and 4K depth, the stress frames, the
+C2 frame with a host-resident depth map (pinned, H2D overlapped: `value_h2d`), and C3 (720p +
+256-sequence rollbuffer window, tools/bench_c3.py) - each with the roofline of its dominant kernel.
 
 N > 1 (torchrun, one rank per GPU over RCCL): rank k owns camera k (weak scaling).  The shared
 voxel grid needs one real exchange per frame: the per-rank occupancy marks (1 bit per cell) are
-all-gathered and OR-merged before every rank's identical historic-grid update.  Frames stay
-pipelined on every rank; the marks of `--exchange-batch` frames travel in one all-gather and the
-grid updates then run in frame order (the grids after every frame equal the per-frame exchange's).
+all-gathered and OR-merged before every rank's identical historic-grid update.  `--exchange-batch
+1` (default) exchanges every frame, as the reference component updates and downloads the grid per
+frame (component.cpp:297,306); B > 1 is the deferred-grid mode (the grid is brought up to date
+every B frames, labelled as such in `config`).
 
 Prints ONE JSON line (rank 0).
 """
 import argparse
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -28,6 +39,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Mpoints/s end-to-end depth→fused voxel grid @1/2/4/8 GPU; % HBM roofline"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+SINGLE_SLOTS = ("mask", "scan", "emit", "sort", "group", "grid", "sel")
 
 
 def parse():
@@ -37,6 +49,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
+    ap.add_argument("--workload", choices=("dense", "stress"), default="dense")
     ap.add_argument("--ring", type=int, default=8, help="distinct device-resident frames")
     ap.add_argument("--cameras", type=int, default=1,
                     help="cameras per GPU (one frame = one depth map of each; camera ids "
@@ -44,14 +57,213 @@ def parse():
     ap.add_argument("--pipeline", type=int, default=3,
                     help="frames in flight on one GPU (engine slots, gdf_set_pipeline_depth); "
                          "N > 1 runs on torch's stream with depth 1")
-    ap.add_argument("--exchange-batch", type=int, default=16,
-                    help="N > 1: frames per occupancy-mark all-gather (multi.BatchedMarkExchange; "
-                         "1 = one collective per frame on torch's stream, no pipelining)")
+    ap.add_argument("--exchange-batch", type=int, default=1,
+                    help="N > 1: frames per occupancy-mark all-gather (1 = every frame, the "
+                         "reference's per-frame grid; B > 1 = deferred grid, B frames per "
+                         "all-gather)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=3.0, help="per CPU run (5 runs)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="do not bracket launches with HIP events (for rocprofv3 runs)")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="N = 1: skip the 720p / 4K / stress / H2D / C3 lines")
+    ap.add_argument("--c3-window", type=int, default=256)
     return ap.parse_args()
+
+
+def model_bytes(P, n_avg, g_avg, ncells):
+    """Algorithmic HBM bytes per launch of each kernel: the bytes the algorithm
+    must move once, not the cache traffic of an implementation."""
+    tiles = (P + 255) // 256
+    return {
+        "mask": 3.0 * P,                           # u16 depth in, u8 stage bits out
+        "scan": 8.0 * tiles,
+        "emit": 1.0 * P + 22.0 * n_avg,            # stage in, depth of kept px, xyzw + key out
+        # 3 radix passes (key only in, key+index out; then key+index both ways) + the grid
+        # update carried by the first pass, averaged per launch
+        "sort": (12.0 * n_avg + 16.0 * n_avg * 2 + 2.0 * ncells) / 3.0,
+        # sorted keys + indices + gathered points in, means out
+        "group": 24.0 * n_avg + 16.0 * g_avg,
+        "grid": 2.0 * ncells,
+    }
+
+
+def roofline_from(ktimes, kt_steps, mb, pmc_key):
+    """The dominant kernel (largest total time per step) of an event-timed pass, its average
+    launch duration and algorithmic bytes per launch."""
+    singles = [k for k in SINGLE_SLOTS if ktimes[k][1] and k in mb]
+    per_step = {k: ktimes[k][0] / kt_steps for k in singles}
+    slot = max(singles, key=lambda k: per_step[k])
+    ms, n = ktimes[slot]
+    # An event pair costs stream time of its own.  An empty pair (slot event_floor, recorded over
+    # the same frames) spans two record packets, a bracketed kernel carries one of them: half the
+    # empty-pair time is subtracted (calibrated against rocprofv3 kernel-trace durations of the
+    # same command, profiles/).
+    fl_ms, fl_n = ktimes.get("event_floor", (0.0, 0))
+    floor_s = fl_ms / 1e3 / fl_n if fl_n else 0.0
+    raw_s = ms / 1e3 / max(n, 1)
+    avg_s = max(raw_s - 0.5 * floor_s, 1e-9)
+    achieved = mb[slot] / avg_s / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            rec = json.load(open(pmc)).get(pmc_key, {}).get(slot)
+            traffic = rec.get("hbm_bytes_per_launch") if rec else None
+        except Exception:
+            traffic = None
+    return {
+        "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
+        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic,
+        "kernel": slot, "avg_launch_us": round(avg_s * 1e6, 3),
+        "event_raw_us": round(raw_s * 1e6, 3), "event_floor_us": round(floor_s * 1e6, 3),
+        "launches_per_step": round(n / kt_steps, 3),
+        "bytes_per_launch": round(mb[slot]),
+        "per_kernel_us": {k: round(ktimes[k][0] * 1e3 / ktimes[k][1], 3) for k in singles},
+    }
+
+
+class DepthStream:
+    """One GPU's camera stream: device-resident frames, the engine, the component loop."""
+
+    def __init__(self, eng, W, H, K, rank, workload, ring, host_frames=False):
+        import numpy as np
+        from ros_gpu_depthmap_fusion_amd import hiprt, synth
+        self.W, self.H, self.K, self.ring = W, H, K, ring
+        self.P = W * H * K
+        self.eng = eng
+        gen = synth.WORKLOADS[workload]
+        self.cams = [synth.make_camera(rank * K + k, W, H) for k in range(K)]
+        self.frames = [[gen(c, rank * K + k, f) for f in range(ring)]
+                       for k, c in enumerate(self.cams)]
+        self.dframes = [[hiprt.DeviceArray.from_numpy(f) for f in fr] for fr in self.frames]
+        self.host = None
+        if host_frames:  # pinned host copies: the H2D-inclusive path
+            self.host = [[hiprt.PinnedArray.from_numpy(f) for f in fr] for fr in self.frames]
+        self.scam = [eng.make_stream_camera(
+            [d.ptr for d in (self.host[k] if host_frames else self.dframes[k])], W, H,
+            *c.intrinsics(), c.T_world, c.T_crop) for k, c in enumerate(self.cams)]
+        self.np = np
+
+    def counts(self, params):
+        """Per-frame point / voxel counts (byte model), one synchronous pass over the ring."""
+        npts, nvox = [], []
+        for i in range(self.ring):
+            self.eng.clear()
+            for k, c in enumerate(self.cams):
+                self.eng.addDepthmapDevice(self.dframes[k][i].ptr, self.W, self.H,
+                                           *c.intrinsics(), c.T_world, c.T_crop)
+            r = self.eng.processFrame(params, synchronous=True)
+            npts.append(r.num_points)
+            nvox.append(r.num_voxelized)
+        return npts, nvox
+
+    def run(self, pc, first, count):
+        if self.host is not None:
+            self.eng.run_host_stream(self.scam, pc, first, count)
+        else:
+            self.eng.run_depth_stream(self.scam, pc, first, count)
+
+
+def time_single(st, params, steps, warmup, depth, kernel_timing, pmc_key):
+    """Steady-state single-GPU line of one DepthStream: prime (every slot's graph captured),
+    warm-up, K timed frames, then the event-timed pass for the roofline."""
+    import numpy as np
+    eng = st.eng
+    npts, nvox = st.counts(params)
+    (gx, gy, gz), ncells = eng.grid_size()
+    eng.set_pipeline_depth(depth)
+    pc = params.to_c(None, None, False, False)
+    # prime: a slot captures its graph on its second steady frame; 2 rounds over the slots + 1
+    prime = 2 * depth + 2
+    st.run(pc, 0, prime)
+    st.run(pc, prime, warmup)
+    eng.synchronize()
+    t0 = time.perf_counter()
+    st.run(pc, prime + warmup, steps)
+    eng.synchronize()
+    elapsed = time.perf_counter() - t0
+    idx = [(prime + warmup + i) % st.ring for i in range(steps)]
+    n_avg = float(np.mean([npts[i] for i in idx]))
+    g_avg = float(np.mean([nvox[i] for i in idx]))
+    mb = model_bytes(st.P, n_avg, g_avg, ncells)
+    roof = None
+    if kernel_timing:
+        kt_steps = min(steps, 200)
+        eng.set_pipeline_depth(1)  # one frame in flight: launch durations without overlap
+        eng.set_profiling(True)
+        st.run(pc, prime + warmup, kt_steps)
+        eng.synchronize()
+        kt = eng.kernel_times()
+        eng.set_profiling(False)
+        roof = roofline_from(kt, kt_steps, mb, pmc_key)
+    survey = 2.0 * st.P + 24.0 * n_avg + 9.0 * ncells  # SURVEY.md §8(d) B_alg per frame
+    return {
+        "value": round(st.P * steps / elapsed / 1e6, 3), "ms_per_step": round(elapsed / steps * 1e3, 5),
+        "steps": steps, "warmup": warmup, "prime": prime,
+        "points_per_frame_after_crop": round(n_avg), "voxels_per_frame": round(g_avg),
+        "survival_after_crop": round(n_avg / st.P, 4),
+        "grid": [gx, gy, gz], "grid_cells": ncells, "frames_in_flight": depth,
+        "step_survey_bytes": round(survey),
+        "step_survey_GBps": round(survey * steps / elapsed / 1e9, 2),
+        "step_survey_frac": round(survey * steps / elapsed / 1e9 / HBM_PEAK_GBPS, 4),
+        "roofline": roof,
+    }
+
+
+def cpu_baseline(st, params, seconds):
+    """The C restatement (oracle/gdf_oracle.c, OpenMP) on the host's cores: median of 5 runs of
+    `seconds` each over the same frames (SURVEY.md §8(d) protocol)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import OracleFusion  # cpu_baseline leg only
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or 1
+    env_t = os.environ.get("OMP_NUM_THREADS")
+    threads = min(affinity, int(env_t)) if env_t and env_t.isdigit() else affinity
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    orc = OracleFusion(threads=threads)
+
+    def frame(i):
+        orc.clear()
+        for k, c in enumerate(st.cams):
+            orc.addDepthmap(st.frames[k][i % st.ring], *c.intrinsics(), c.T_world, c.T_crop)
+        orc.processFrame(params)
+
+    for i in range(3):  # warm-up
+        frame(i)
+    rates, total_frames = [], 0
+    for run in range(5):
+        done, t0 = 0, time.perf_counter()
+        while True:
+            frame(done)
+            done += 1
+            t = time.perf_counter() - t0
+            if t >= seconds or done >= 4000:
+                break
+        rates.append(done * st.P / t / 1e6)
+        total_frames += done
+    return {"value": round(statistics.median(rates), 3), "unit": "Mpoints/s", "cores": threads,
+            "kind": "port", "threads": threads, "nproc": os.cpu_count(),
+            "affinity_cpus": affinity, "cpu_model": model,
+            "runs_Mpoints_s": [round(r, 2) for r in rates],
+            "sample": f"median of 5 runs x {seconds:.0f} s ({total_frames} frames) of the same "
+                      f"{st.W}x{st.H} frames through the C restatement (oracle/gdf_oracle.c, "
+                      f"-O3 -ffp-contract=off, OpenMP {threads} threads)"}
+
+
+def workload_name(W, H, K, wl):
+    cams = "" if K == 1 else f"{K}x"
+    return (f"{cams}{W}x{H} u16 depth ({wl} frames), launch defaults (F=4 thr 0.3, crop/voxel "
+            f"-10..30/-20..20/-1..1.5, cells 0.1/0.1/0.12, voxelize average, lifetime 10)")
 
 
 def main():
@@ -68,72 +280,82 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         world = dist.get_world_size()
     import numpy as np
-    from ros_gpu_depthmap_fusion_amd import build_library, hiprt, synth
+    from ros_gpu_depthmap_fusion_amd import build_library, hiprt
     from ros_gpu_depthmap_fusion_amd.gdf import ComponentParams, GPUDepthmapFusion
 
     build_library()
     hiprt.set_device(local_rank)
-    W, H = args.width, args.height
-    K = args.cameras
-    P = W * H * K
-    cams = [synth.make_camera(rank * K + k, W, H) for k in range(K)]
-    frames = [[synth.depth_frame(c, rank * K + k, f) for f in range(args.ring)]
-              for k, c in enumerate(cams)]
-    dframes = [[hiprt.DeviceArray.from_numpy(f) for f in fr] for fr in frames]
+    W, H, K = args.width, args.height, args.cameras
     params = ComponentParams()
     eng = GPUDepthmapFusion(local_rank)
+    st = DepthStream(eng, W, H, K, rank, args.workload, args.ring)
+    P = st.P
+    pmc_key = f"{W}x{H}/{args.workload}"
 
-    batched = dist is not None and args.exchange_batch > 1
-    if dist is not None and not batched:
-        import torch
-        stream = torch.cuda.current_stream()
-        eng.set_stream(stream.cuda_stream)
-
-    def add(i):
-        eng.clear()
-        for k, c in enumerate(cams):
-            eng.addDepthmapDevice(dframes[k][i % args.ring].ptr, W, H, *c.intrinsics(), c.T_world,
-                                  c.T_crop)
-
-    # per-frame point counts (for the algorithmic byte model), one synchronous pass over the ring
-    npts, nvox = [], []
-    for i in range(args.ring):
-        add(i)
-        r = eng.processFrame(params, synchronous=True)
-        npts.append(r.num_points)
-        nvox.append(r.num_voxelized)
-    (gx, gy, gz), ncells = eng.grid_size()
-
-    depth = 1
-    if dist is not None and not batched:
-        from ros_gpu_depthmap_fusion_amd.multi import DeviceMarkExchange
-        marks = DeviceMarkExchange(eng, ncells, world)
+    if dist is None:
+        line = time_single(st, params, args.steps, args.warmup, max(1, min(4, args.pipeline)),
+                           not args.no_kernel_timing, pmc_key)
+        cfg_extra = {"parallelism": "single GPU", "exchange": None}
     else:
+        line, cfg_extra = time_multi(args, st, params, dist, world, pmc_key)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(st, params, args.cpu_seconds)
+
+    secondary = None
+    if rank == 0 and world == 1 and not args.no_secondary:
+        secondary = run_secondary(args, params)
+
+    if rank == 0:
+        roof = line.pop("roofline")
+        out = {
+            "metric": METRIC, "value": line.pop("value"), "unit": "Mpoints/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": line.pop("ms_per_step"),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (ray-cast analytic scene, %s frames; device-resident ring of %d "
+                    "frames)" % (args.workload, args.ring),
+            "config": dict({"workload": "C2: " + workload_name(W, H, K, args.workload),
+                            "cameras_per_gpu": K}, **line, **cfg_extra),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        if secondary is not None:
+            out["secondary"] = secondary
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def time_multi(args, st, params, dist, world, pmc_key):
+    """N > 1: every rank runs its camera; the occupancy marks are exchanged over RCCL."""
+    import numpy as np
+    import torch
+    eng = st.eng
+    npts, nvox = st.counts(params)
+    (gx, gy, gz), ncells = eng.grid_size()
+    batched = args.exchange_batch > 1
+    depth = 1
+    if batched:
+        from ros_gpu_depthmap_fusion_amd.multi import BatchedMarkExchange
         depth = max(1, min(4, args.pipeline))
         eng.set_pipeline_depth(depth)
-        if batched:
-            from ros_gpu_depthmap_fusion_amd.multi import BatchedMarkExchange
-            marks = BatchedMarkExchange(eng, ncells, world, args.exchange_batch)
-
-    pc_plain = params.to_c(None, None, False, False)
+        marks = BatchedMarkExchange(eng, ncells, world, args.exchange_batch)
+    else:
+        from ros_gpu_depthmap_fusion_amd.multi import DeviceMarkExchange
+        eng.set_stream(torch.cuda.current_stream().cuda_stream)
+        marks = DeviceMarkExchange(eng, ncells, world)
     pc_defer = params.to_c(None, None, False, True)
 
-    # the component's per-frame loop runs in C++ (gdf_run_depth_stream: clear + addDepthmapDevice
-    # + gdf_process_frame per frame), as the ROS component would drive the engine
-    scam = [eng.make_stream_camera([d.ptr for d in dframes[k]], W, H, *c.intrinsics(),
-                                   c.T_world, c.T_crop) for k, c in enumerate(cams)]
-
     def run(first, count):
-        if dist is None:
-            eng.run_depth_stream(scam, pc_plain, first, count)
-            return
         for i in range(first, first + count):
-            eng.run_depth_stream(scam, pc_defer, i, 1)
-            if batched:  # occupancy union over RCCL, `exchange_batch` frames per all-gather
+            st.run(pc_defer, i, 1)
+            if batched:
                 marks.take()
                 if marks.full():
                     marks.flush(params.occupancy_lifetime)
-            else:  # one all-gather per frame (multi.py)
+            else:
                 marks.exchange()
                 eng.voxelOccupancyGrid(params.occupancy_lifetime)
         if batched:
@@ -141,152 +363,86 @@ def main():
 
     def barrier_sync():
         eng.synchronize()
-        if dist is not None:
-            torch.cuda.synchronize()
-            dist.barrier()
-            torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
 
-    run(0, args.warmup)
+    prime = 2 * depth + 2
+    run(0, prime + args.warmup)
     barrier_sync()
     t0 = time.perf_counter()
-    run(args.warmup, args.steps)
+    run(prime + args.warmup, args.steps)
     barrier_sync()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    # per-kernel durations: a separate pass over the same frames with an HIP event pair around
-    # every launch on the engine stream (kept out of the timed region: the extra event records
-    # cost host time)
-    ktimes = None
-    if not args.no_kernel_timing:
-        kt_steps = min(args.steps, 200)
-        if dist is None or batched:
-            eng.set_pipeline_depth(1)  # one frame in flight: launch durations without overlap
-        eng.set_profiling(True)
-        run(args.warmup, kt_steps)
-        barrier_sync()
-        ktimes = eng.kernel_times()
-        eng.set_profiling(False)
-
-    ms_per_step = elapsed / args.steps * 1e3
-    value = world * P * args.steps / elapsed / 1e6
-    # frames used in the timed region, for the byte model
-    idx = [(args.warmup + i) % args.ring for i in range(args.steps)]
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    idx = [(prime + args.warmup + i) % st.ring for i in range(args.steps)]
     n_avg = float(np.mean([npts[i] for i in idx]))
     g_avg = float(np.mean([nvox[i] for i in idx]))
-    tiles = (P + 255) // 256
-    # algorithmic HBM bytes per launch of each kernel (DESIGN.md "Kernels and their rooflines"):
-    # the bytes the algorithm must move once, not the cache traffic of an implementation
-    model_bytes = {
-        "mask": 3.0 * P,                           # u16 depth in, u8 stage bits out
-        "scan": 8.0 * tiles,
-        "emit": 1.0 * P + 22.0 * n_avg,            # stage in, depth of kept px, xyzw + key out
-        # 3 radix passes (key only in, key+index out; then key+index both ways) + the grid
-        # update carried by the first pass, averaged per launch
-        "sort": (12.0 * n_avg + 16.0 * n_avg * 2 + 2.0 * ncells) / 3.0,
-        # sorted keys + indices + gathered points in, means out
-        "group": 24.0 * n_avg + 16.0 * g_avg,
-        "grid": 2.0 * ncells,
+    line = {
+        "value": round(world * st.P * args.steps / elapsed / 1e6, 3),
+        "ms_per_step": round(elapsed / args.steps * 1e3, 5), "prime": prime,
+        "points_per_frame_after_crop": round(n_avg), "voxels_per_frame": round(g_avg),
+        "grid": [gx, gy, gz], "grid_cells": ncells, "frames_in_flight": depth,
+        "roofline": None,
     }
-    survey_bytes = 2.0 * P + 24.0 * n_avg + 9.0 * ncells  # SURVEY.md §8(d) B_alg per frame
+    if not args.no_kernel_timing:
+        kt_steps = min(args.steps, 200)
+        if batched:
+            eng.set_pipeline_depth(1)
+        eng.set_profiling(True)
+        run(prime + args.warmup, kt_steps)
+        barrier_sync()
+        kt = eng.kernel_times()
+        eng.set_profiling(False)
+        line["roofline"] = roofline_from(kt, kt_steps, model_bytes(st.P, n_avg, g_avg, ncells),
+                                         pmc_key)
+    cfg = {"parallelism": "camera-per-GPU x%d, occupancy-mark all-gather %s" % (
+               world, "every frame" if not batched else
+               "every %d frames (deferred grid)" % args.exchange_batch),
+           "exchange": ("sparse mark pairs (cap %d words/frame), %d dense-fallback batches" %
+                        (marks.cap, marks.dense_batches)) if batched else "bitmask per frame"}
+    return line, cfg
 
-    roofline = None
-    if ktimes:
-        singles = [k for k in ("mask", "scan", "emit", "sort", "group", "grid")
-                   if ktimes[k][1]]
-        per_step = {k: ktimes[k][0] / kt_steps for k in singles}  # ms per step
-        slot = max(singles, key=lambda k: per_step[k])
-        ms, n = ktimes[slot]
-        # An event pair costs stream time of its own.  An empty pair (slot event_floor, recorded
-        # over the same frames) spans two record packets, a bracketed kernel carries one of them:
-        # half the empty-pair time is subtracted (calibrated against rocprofv3 kernel-trace
-        # durations of the same command, profiles/r01/).
-        fl_ms, fl_n = ktimes.get("event_floor", (0.0, 0))
-        floor_s = fl_ms / 1e3 / fl_n if fl_n else 0.0
-        raw_s = ms / 1e3 / max(n, 1)
-        avg_s = max(raw_s - 0.5 * floor_s, 1e-9)
-        achieved = model_bytes[slot] / avg_s / 1e9
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
-            try:
-                rec = json.load(open(pmc)).get(slot)
-                if rec and rec.get("workload") == f"{W}x{H}":
-                    traffic = rec.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        roofline = {
-            "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic,
-            "kernel": slot, "avg_launch_us": round(avg_s * 1e6, 3),
-            "event_raw_us": round(raw_s * 1e6, 3), "event_floor_us": round(floor_s * 1e6, 3),
-            "launches_per_step": round(n / kt_steps, 3),
-            "bytes_per_launch": round(model_bytes[slot]),
-            "per_kernel_us": {k: round(ktimes[k][0] * 1e3 / ktimes[k][1], 3) for k in singles},
-            "step_survey_bytes": round(survey_bytes),
-            "step_survey_GBps": round(survey_bytes * args.steps / elapsed / 1e9, 2),
-        }
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        from oracle import OracleFusion  # cpu_baseline leg only
-        threads = min(16, os.cpu_count() or 1)
-        orc = OracleFusion(threads=threads)
-        done, t_cpu = 0, 0.0
-        for i in range(2):  # warm-up
-            orc.clear()
-            for k, c in enumerate(cams):
-                orc.addDepthmap(frames[k][i % args.ring], *c.intrinsics(), c.T_world, c.T_crop)
-            orc.processFrame(params)
-        tc0 = time.perf_counter()
-        while True:
-            orc.clear()
-            for k, c in enumerate(cams):
-                orc.addDepthmap(frames[k][done % args.ring], *c.intrinsics(), c.T_world,
-                                c.T_crop)
-            orc.processFrame(params)
-            done += 1
-            t_cpu = time.perf_counter() - tc0
-            if t_cpu >= args.cpu_seconds or done >= 2000:
-                break
-        cpu = {"value": round(done * P / t_cpu / 1e6, 3), "unit": "Mpoints/s", "cores": threads,
-               "kind": "port",
-               "sample": f"{done} frames of the same {W}x{H} C2 workload through the C "
-                         f"restatement (oracle/gdf_oracle.c, OpenMP {threads} threads), "
-                         f"{t_cpu:.1f} s"}
-
-    if rank == 0:
-        out = {
-            "metric": METRIC, "value": round(value, 3), "unit": "Mpoints/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 5),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (ray-cast analytic scene, counter-hash noise/holes; "
-                    "device-resident ring of %d frames)" % args.ring,
-            "config": {"workload": "C2: %dx%d u16 depth stream per GPU, launch defaults "
-                                   "(F=4 thr 0.3, crop/voxel -10..30/-20..20/-1..1.5, "
-                                   "cells 0.1/0.1/0.12 -> %dx%dx%d, voxelize average, "
-                                   "lifetime 10)" % (W, H, gx, gy, gz),
-                       "cameras_per_gpu": K, "points_per_frame_after_crop": round(n_avg),
-                       "voxels_per_frame": round(g_avg), "grid_cells": ncells,
-                       "frames_in_flight": depth,
-                       "exchange": ("sparse mark pairs (cap %d words/frame), %d dense-fallback "
-                                    "batches" % (marks.cap, marks.dense_batches)
-                                    if batched else None),
-                       "parallelism": ("camera-per-GPU x%d, occupancy-mark all-gather every %d "
-                                       "frame(s)" % (world, args.exchange_batch if batched else 1))
-                       if dist is not None else "single GPU"},
-            "roofline": roofline,
-            "cpu_baseline": cpu,
-        }
-        print(json.dumps(out))
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
+def run_secondary(args, params):
+    """N = 1 only: the other single-GPU configurations, each with its own roofline."""
+    from ros_gpu_depthmap_fusion_amd.gdf import GPUDepthmapFusion
+    out = {}
+    steps = max(args.steps, 50)
+    warm = max(args.warmup, 10)
+    kt = not args.no_kernel_timing
+    for name, (W, H, wl, ring, st_steps) in {
+            "720p": (1280, 720, "dense", 4, steps),
+            "4k": (3840, 2160, "dense", 2, max(20, steps // 4)),
+            "vga_stress": (640, 480, "stress", 8, steps)}.items():
+        eng = GPUDepthmapFusion(0)
+        st = DepthStream(eng, W, H, 1, 0, wl, ring)
+        r = time_single(st, params, st_steps, warm, max(1, min(4, args.pipeline)), kt,
+                        f"{W}x{H}/{wl}")
+        r["workload"] = workload_name(W, H, 1, wl)
+        out[name] = r
+        del st
+        eng.close()
+    # host-resident depth maps (pinned, uploaded on a copy stream overlapped with compute)
+    eng = GPUDepthmapFusion(0)
+    st = DepthStream(eng, args.width, args.height, 1, 0, args.workload, args.ring,
+                     host_frames=True)
+    r = time_single(st, params, steps, warm, max(1, min(4, args.pipeline)), False, "")
+    r["workload"] = "C2 with host (pinned) depth maps: " + workload_name(
+        args.width, args.height, 1, args.workload)
+    r["value_h2d"] = r.pop("value")
+    out["vga_h2d"] = r
+    del st
+    eng.close()
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from bench_c3 import run_c3
+        out["c3"] = run_c3(window=args.c3_window, steps=20, ring=4, profile_steps=5)
+    except Exception as exc:  # reported, not hidden
+        out["c3"] = {"error": repr(exc)}
+    return out
 
 
 if __name__ == "__main__":

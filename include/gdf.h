@@ -247,15 +247,17 @@ int gdf_import_occupancy_marks_strided(gdf_engine* engine, const uint32_t* devic
 /* Sparse form of the take (the marks are ~1-2 % of the cells): besides the bitmask, the
  * non-zero words as (index, word) pairs in `pairs` (device, 1 + 2 * cap words): pairs[0] = their
  * number (> cap: only the bitmask is complete, exchange the bitmasks), then the pairs.
- * gdf_union_occupancy_pairs ORs nranks x nframes such records (record r, f at
- * pairs + (r * nframes + f) * record_words, all within their cap) into
- * union_bits[f * words + i] (zeroed first), the input of gdf_voxel_occupancy_grid_batch with
- * one rank. */
+ * gdf_union_occupancy_pairs ORs nranks x nframes such records - record (r, f) at
+ * pairs + (r * frames_per_rank + f) * record_words, f < nframes <= frames_per_rank (a partial
+ * batch of an all-gathered [rank, batch, record] buffer), each read up to its cap
+ * (record_words - 1) / 2 - into union_bits[f * words + i] (zeroed first), the input of
+ * gdf_voxel_occupancy_grid_batch with one rank. */
 int gdf_take_occupancy_marks_sparse(gdf_engine* engine, uint32_t* device_bitmask, uint64_t words,
                                     uint32_t* device_pairs, uint32_t cap);
 int gdf_union_occupancy_pairs(gdf_engine* engine, uint32_t* device_union_bitmasks, uint64_t words,
                               const uint32_t* device_pairs, uint32_t num_ranks,
-                              uint32_t num_frames, uint64_t record_words);
+                              uint32_t num_frames, uint32_t frames_per_rank,
+                              uint64_t record_words);
 int gdf_voxel_occupancy_grid_batch(gdf_engine* engine, const uint32_t* device_bitmasks,
                                    uint64_t words, uint32_t num_ranks, uint32_t num_frames,
                                    uint64_t frame_stride_words, uint64_t rank_stride_words,

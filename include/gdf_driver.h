@@ -19,7 +19,7 @@ extern "C" {
 /* One camera of the stream: a ring of `ring` device depth maps (width*height uint16 each) with
  * the camera's intrinsics and row-major transforms (the arguments of gdf_add_depthmap_device). */
 typedef struct gdf_stream_camera {
-    const uint16_t* const* frames;  /* host array of `ring` DEVICE pointers */
+    const uint16_t* const* frames;  /* host array of `ring` DEVICE (host: gdf_run_host_stream) pointers */
     uint32_t ring;
     uint32_t width, height;
     float depth_scale, fx, fy, cx, cy;
@@ -34,6 +34,14 @@ typedef struct gdf_stream_camera {
 int gdf_run_depth_stream(gdf_engine* engine, const gdf_stream_camera* cameras,
                          uint32_t num_cameras, const gdf_frame_params* params, uint64_t first,
                          uint64_t count);
+
+/* The same loop for HOST depth maps (frames[] are host pointers, gdf_add_depthmap): each frame's
+ * maps are copied to the device on the frame slot's stream (pinned memory directly, pageable
+ * memory through the slot's pinned staging), overlapping the kernels of the frames in flight
+ * (gdf_set_pipeline_depth).  The H2D-inclusive form of gdf_run_depth_stream. */
+int gdf_run_host_stream(gdf_engine* engine, const gdf_stream_camera* cameras,
+                        uint32_t num_cameras, const gdf_frame_params* params, uint64_t first,
+                        uint64_t count);
 
 #ifdef __cplusplus
 }

@@ -193,6 +193,10 @@ constexpr int kMaxPipe = 4;
 struct Slot {
     hipStream_t own = nullptr;
     DevBuf d_depth;                 // host depth maps uploaded for this frame
+    void* h_stage = nullptr;        // pinned staging of pageable host depth maps
+    size_t h_stage_bytes = 0;
+    hipEvent_t h2d_done = nullptr;  // the slot's last staged copy has been read
+    bool h2d_pending = false;
     DevBuf d_camdesc;
     DevBuf d_ctrs;                  // tile tickets of the look-back launches
     DevBuf d_khist;                 // digit histogram of the voxel keys [4*256]
@@ -265,6 +269,7 @@ struct gdf_engine {
     uint32_t mask_blocks = 0;       // compaction segments over the emitting cameras
     uint32_t max_segw = 0;          // widest segment (sizes k_mask's LDS band)
     bool depth_uploaded = false;
+    std::vector<std::pair<const void*, bool>> pinned_cache;  // is_pinned answers, most recent last
 
     // new sequences on the device
     DevBuf d_new;
@@ -719,10 +724,67 @@ void ensure_table(gdf_engine* e, size_t slot, const Cam& c) {
     t.valid = true;
 }
 
+// true when `p` is page-locked host memory (hipHostMalloc / hipHostRegister): the DMA engine reads
+// it directly, asynchronously.  The answer is cached for the last pointers seen (a sensor driver
+// cycles through a few buffers).
+bool is_pinned(gdf_engine* e, const void* p) {
+    auto& cache = e->pinned_cache;
+    for (auto& kv : cache)
+        if (kv.first == p) return kv.second;
+    hipPointerAttribute_t attr{};
+    bool pinned = false;
+    if (hipPointerGetAttributes(&attr, p) == hipSuccess)
+        pinned = attr.type == hipMemoryTypeHost && attr.hostPointer != nullptr;
+    else
+        (void)hipGetLastError();  // pageable memory: not known to HIP
+    if (cache.size() >= 16) cache.erase(cache.begin());
+    cache.emplace_back(p, pinned);
+    return pinned;
+}
+
+// Host depth maps (the reference's blocking glBufferSubData, fusion.cpp:1583-1593) go to the
+// slot's device buffer with hipMemcpyAsync on the slot's own stream, so the copy of frame f+1
+// overlaps the kernels of frame f (another slot, another stream) with no cross-stream event.
+// Pinned sources are read in place by the DMA engine; pageable ones are first copied into the
+// slot's pinned staging buffer (after the slot's previous copy from it has finished), so the
+// caller's buffer is free again when gdf_upload_depthmaps returns, as in the reference.
+void upload_host_depth(gdf_engine* e, uint16_t* dst, const Cam& c, size_t& staged) {
+    Slot& q = e->sl();
+    const size_t bytes = (size_t)c.n * 2;
+    if (is_pinned(e, c.host)) {
+        HIPCHK(hipMemcpyAsync(dst, c.host, bytes, hipMemcpyHostToDevice, e->s()));
+        return;
+    }
+    if (q.h2d_pending) {  // the slot's previous frame may still read the staging
+        HIPCHK(hipEventSynchronize(q.h2d_done));
+        q.h2d_pending = false;
+    }
+    if (q.h_stage_bytes < staged + bytes) fail(GDF_ERR_STATE, "depth staging not sized");
+    uint8_t* s = static_cast<uint8_t*>(q.h_stage) + staged;
+    std::memcpy(s, c.host, bytes);
+    HIPCHK(hipMemcpyAsync(dst, s, bytes, hipMemcpyHostToDevice, e->s()));
+    staged += bytes;
+}
+
 void upload_depthmaps(gdf_engine* e) {  // fusion.cpp:1583-1593
-    uint64_t host_px = 0;
-    for (const Cam& c : e->cams) if (!c.dev) host_px += c.n;
+    uint64_t host_px = 0, paged_px = 0;
+    for (const Cam& c : e->cams)
+        if (!c.dev) {
+            host_px += c.n;
+            if (!is_pinned(e, c.host)) paged_px += c.n;
+        }
     if (host_px) e->sl().d_depth.ensure(host_px * 2);
+    if (paged_px && e->sl().h_stage_bytes < paged_px * 2) {  // grow the staging once per frame
+        Slot& q = e->sl();
+        if (q.h2d_pending) HIPCHK(hipEventSynchronize(q.h2d_done));
+        q.h2d_pending = false;
+        if (q.h_stage) HIPCHK(hipHostFree(q.h_stage));
+        q.h_stage = nullptr;
+        q.h_stage_bytes = 0;
+        HIPCHK(hipHostMalloc(&q.h_stage, paged_px * 2, hipHostMallocDefault));
+        q.h_stage_bytes = paged_px * 2;
+    }
+    size_t staged = 0;
     if (e->cams.size() + e->halo.size() > (size_t)kMaxCams) fail(GDF_ERR_ARG, "too many cameras (incl. halo)");
     e->h_cams.clear();
     e->mask_blocks = 0;
@@ -736,7 +798,7 @@ void upload_depthmaps(gdf_engine* e) {  // fusion.cpp:1583-1593
             d.depth = c.dev;
         } else {
             uint16_t* dst = e->sl().d_depth.as<uint16_t>() + hoff;
-            HIPCHK(hipMemcpyWithStream(dst, c.host, (size_t)c.n * 2, hipMemcpyHostToDevice, e->s()));
+            upload_host_depth(e, dst, c, staged);
             d.depth = dst;
             hoff += c.n;
         }
@@ -760,6 +822,12 @@ void upload_depthmaps(gdf_engine* e) {  // fusion.cpp:1583-1593
         std::memcpy(d.Tc, c.Tc, 64);
         e->h_cams.push_back(d);
         off += c.n;
+    }
+    if (staged) {  // the staging is free again once these copies have run
+        Slot& q = e->sl();
+        if (!q.h2d_done) HIPCHK(hipEventCreateWithFlags(&q.h2d_done, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(q.h2d_done, e->s()));
+        q.h2d_pending = true;
     }
     // halo cameras first (negative offsets), then the emitting cameras: sorted by offset
     std::vector<CamDesc> all = e->halo;
@@ -1261,6 +1329,8 @@ int gdf_destroy(gdf_engine* e) {
     for (Slot& sl : e->slots) {
         sl.graph.reset();
         if (sl.h_misc) (void)hipHostFree(sl.h_misc);
+        if (sl.h_stage) (void)hipHostFree(sl.h_stage);
+        if (sl.h2d_done) (void)hipEventDestroy(sl.h2d_done);
         if (sl.own) (void)hipStreamDestroy(sl.own);
     }
     delete e;
@@ -1679,13 +1749,15 @@ int gdf_take_occupancy_marks_sparse(gdf_engine* e, uint32_t* bits, uint64_t word
 
 int gdf_union_occupancy_pairs(gdf_engine* e, uint32_t* union_bits, uint64_t words,
                               const uint32_t* pairs, uint32_t nranks, uint32_t nframes,
-                              uint64_t record_words) {
+                              uint32_t frames_per_rank, uint64_t record_words) {
     ENGINE_OR_FAIL(e);
     return guarded(e, [&] {
         if (!e->grid_set || !union_bits || (!pairs && nranks * nframes)) fail(GDF_ERR_STATE, "no voxel grid");
         if (words < (e->ncells + 31) / 32) fail(GDF_ERR_CAPACITY, "union bitmask too small");
-        HIPCHK(launch_union_pairs(union_bits, mark_words(e), pairs, nranks, nframes, record_words,
-                                  e->s()));
+        if (nframes > frames_per_rank || (nframes && record_words < 3))
+            fail(GDF_ERR_ARG, "union pairs: nframes > frames_per_rank or records too small");
+        HIPCHK(launch_union_pairs(union_bits, mark_words(e), pairs, nranks, nframes,
+                                  frames_per_rank, record_words, e->s()));
     });
 }
 
@@ -1698,7 +1770,9 @@ int gdf_voxel_occupancy_grid_batch(gdf_engine* e, const uint32_t* bits, uint64_t
         if (words < (e->ncells + 31) / 32 || (nframes > 1 && frame_stride_words < words) ||
             (nranks > 1 && rank_stride_words < frame_stride_words * (nframes ? nframes : 1)))
             fail(GDF_ERR_CAPACITY, "mark bitmasks too small");
-        if (e->sl().marks_set) fail(GDF_ERR_STATE, "marks of a frame are pending (take them first)");
+        for (int i = 0; i < e->npipe; ++i)  // a frame in flight on any slot, marks not taken
+            if (e->slots[i].marks_set)
+                fail(GDF_ERR_STATE, "marks of a frame are pending (take them first)");
         widen_if_needed(e, lifetime, e->s());
         if (e->grid_mode == 0) {  // one pass for the batch
             ensure_misc(e);

@@ -2153,21 +2153,25 @@ __global__ __launch_bounds__(256) void k_take_marks_sparse(uint32_t* __restrict_
     }
 }
 
-// OR the pairs of `nranks` x `nframes` sparse masks (record r, f at pairs + (r * nframes + f) *
-// rec_words) into union[f * words + index]; union zeroed on entry.  Every record fits its cap.
+// OR the pairs of `nranks` x `nframes` sparse masks into union[f * words + index]; union zeroed
+// on entry.  Record (r, f) sits at pairs + (r * frames_per_rank + f) * rec_words (an all-gathered
+// [rank, batch, record] buffer of which the first nframes frames are live); a record holds at
+// most cap = (rec_words - 1) / 2 pairs, whatever its count word says (a count above cap means the
+// caller exchanged bitmasks instead, so such records are never visited - the cap only keeps a
+// stale record inside its own slot).
 __global__ __launch_bounds__(256) void k_union_pairs(uint32_t* __restrict__ uni, uint64_t words,
                                                      const uint32_t* __restrict__ pairs,
-                                                     uint32_t nranks, uint32_t nframes,
+                                                     uint32_t nframes, uint32_t frames_per_rank,
                                                      uint64_t rec_words) {
     const uint32_t rec = blockIdx.y;  // r * nframes + f
-    const uint32_t f = rec % nframes;
-    const uint32_t* p = pairs + (uint64_t)rec * rec_words;
-    const uint32_t n = p[0];
+    const uint32_t r = rec / nframes, f = rec % nframes;
+    const uint32_t* p = pairs + ((uint64_t)r * frames_per_rank + f) * rec_words;
+    const uint32_t cap = (uint32_t)((rec_words - 1) / 2);
+    const uint32_t n = min(p[0], cap);
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
         const uint32_t idx = p[1 + 2 * k], v = p[2 + 2 * k];
         if (idx < words) atomicOr(uni + (uint64_t)f * words + idx, v);
     }
-    (void)nranks;
 }
 
 hipError_t launch_take_marks_sparse(uint32_t* marks, uint64_t words, uint32_t* bits,
@@ -2180,12 +2184,12 @@ hipError_t launch_take_marks_sparse(uint32_t* marks, uint64_t words, uint32_t* b
 }
 
 hipError_t launch_union_pairs(uint32_t* uni, uint64_t words, const uint32_t* pairs,
-                              uint32_t nranks, uint32_t nframes, uint64_t rec_words,
-                              hipStream_t s) {
+                              uint32_t nranks, uint32_t nframes, uint32_t frames_per_rank,
+                              uint64_t rec_words, hipStream_t s) {
     hipError_t e = hipMemsetAsync(uni, 0, (size_t)nframes * words * 4, s);
-    if (e != hipSuccess || nranks * nframes == 0) return e;
+    if (e != hipSuccess || nranks * nframes == 0 || rec_words < 3) return e;
     hipLaunchKernelGGL(k_union_pairs, dim3(8, nranks * nframes), dim3(256), 0, s, uni, words,
-                       pairs, nranks, nframes, rec_words);
+                       pairs, nframes, frames_per_rank, rec_words);
     return hipGetLastError();
 }
 

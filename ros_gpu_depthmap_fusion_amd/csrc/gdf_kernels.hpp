@@ -110,8 +110,8 @@ hipError_t launch_take_marks(uint32_t* marks, uint64_t words, uint32_t* bits, hi
 hipError_t launch_take_marks_sparse(uint32_t* marks, uint64_t words, uint32_t* bits,
                                     uint32_t* pairs, uint32_t cap, hipStream_t s);
 hipError_t launch_union_pairs(uint32_t* uni, uint64_t words, const uint32_t* pairs,
-                              uint32_t nranks, uint32_t nframes, uint64_t rec_words,
-                              hipStream_t s);
+                              uint32_t nranks, uint32_t nframes, uint32_t frames_per_rank,
+                              uint64_t rec_words, hipStream_t s);
 // nranks masks of `words` words, mask r at bits + r * stride
 hipError_t launch_import_marks(uint32_t* marks, uint64_t words, const uint32_t* bits,
                                uint32_t nranks, uint64_t stride, hipStream_t s);

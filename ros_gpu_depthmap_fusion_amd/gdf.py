@@ -100,7 +100,7 @@ EXPORTED = [
     "gdf_set_profiling", "gdf_get_kernel_times", "gdf_set_debug", "gdf_debug_stage_masks", "gdf_debug_rollbuffer",
     "gdf_debug_historic_grid",
     # include/gdf_driver.h: the component's depth loop in C++ over the C-ABI
-    "gdf_run_depth_stream",
+    "gdf_run_depth_stream", "gdf_run_host_stream",
 ]
 
 
@@ -161,7 +161,7 @@ def load_library(path: str = LIB_PATH):
         "gdf_import_occupancy_marks_strided": (i32, [vp, vp, u64, u32, u64]),
         "gdf_voxel_occupancy_grid_batch": (i32, [vp, vp, u64, u32, u32, u64, u64, u32]),
         "gdf_take_occupancy_marks_sparse": (i32, [vp, vp, u64, vp, u32]),
-        "gdf_union_occupancy_pairs": (i32, [vp, vp, u64, vp, u32, u32, u64]),
+        "gdf_union_occupancy_pairs": (i32, [vp, vp, u64, vp, u32, u32, u32, u64]),
         "gdf_set_profiling": (i32, [vp, i32]),
         "gdf_get_kernel_times": (i32, [vp, vp, vp, i32]),
         "gdf_set_debug": (i32, [vp, i32]),
@@ -169,6 +169,7 @@ def load_library(path: str = LIB_PATH):
         "gdf_debug_rollbuffer": (i32, [vp, vp, vp, vp, u32, vp, u32]),
         "gdf_debug_historic_grid": (i32, [vp, vp, u64]),
         "gdf_run_depth_stream": (i32, [vp, P(StreamCamera), u32, P(FrameParams), u64, u64]),
+        "gdf_run_host_stream": (i32, [vp, P(StreamCamera), u32, P(FrameParams), u64, u64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -497,10 +498,12 @@ class GPUDepthmapFusion:
             self._h, C.c_void_p(dev_ptr), words, C.c_void_p(pairs_ptr), cap))
 
     def union_pairs(self, union_ptr: int, words: int, pairs_ptr: int, nranks: int, nframes: int,
-                    record_words: int):
+                    record_words: int, frames_per_rank: int = 0):
+        """OR the first `nframes` sparse records of every rank (records laid out
+        [rank, frames_per_rank, record_words]) into per-frame bitmasks."""
         self._check(self._lib.gdf_union_occupancy_pairs(
             self._h, C.c_void_p(union_ptr), words, C.c_void_p(pairs_ptr), nranks, nframes,
-            record_words))
+            frames_per_rank or nframes, record_words))
 
     def take_marks(self, dev_ptr: int, words: int):
         """Export the marks of the frame just processed and clear them (batched exchange)."""
@@ -544,6 +547,15 @@ class GPUDepthmapFusion:
         arr = (StreamCamera * len(cameras))(*cameras)
         self._check(self._lib.gdf_run_depth_stream(self._h, arr, len(cameras), C.byref(p),
                                                    first, count))
+
+    def run_host_stream(self, cameras: Sequence[StreamCamera], p: FrameParams, first: int,
+                        count: int):
+        """gdf_run_host_stream: the same loop with HOST depth maps (pinned: copied in place on the
+        slot's stream; pageable: through the slot's pinned staging), H2D overlapped with the
+        frames in flight."""
+        arr = (StreamCamera * len(cameras))(*cameras)
+        self._check(self._lib.gdf_run_host_stream(self._h, arr, len(cameras), C.byref(p),
+                                                  first, count))
 
     def processFramePrepared(self, p: FrameParams) -> FrameResult:
         """processFrame with parameters already converted by ComponentParams.to_c (a stream of

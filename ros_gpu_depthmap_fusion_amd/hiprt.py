@@ -28,6 +28,8 @@ def hip():
         _hip.hipEventSynchronize.argtypes = [C.c_void_p]
         _hip.hipEventElapsedTime.argtypes = [C.POINTER(C.c_float), C.c_void_p, C.c_void_p]
         _hip.hipEventDestroy.argtypes = [C.c_void_p]
+        _hip.hipHostMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t, C.c_uint]
+        _hip.hipHostFree.argtypes = [C.c_void_p]
     return _hip
 
 
@@ -76,6 +78,39 @@ class DeviceArray:
     def close(self):
         if self.ptr:
             hip().hipFree(C.c_void_p(self.ptr))
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class PinnedArray:
+    """Page-locked host memory (hipHostMalloc) holding a copy of a numpy array: a sensor driver's
+    DMA-able frame buffer.  `.ptr` is the host address, `.array` a numpy view of it."""
+
+    def __init__(self, nbytes: int):
+        p = C.c_void_p()
+        check(hip().hipHostMalloc(C.byref(p), max(int(nbytes), 1), 0), "hipHostMalloc")
+        self.ptr = p.value
+        self.nbytes = int(nbytes)
+        self.array = None
+
+    @classmethod
+    def from_numpy(cls, a: np.ndarray) -> "PinnedArray":
+        a = np.ascontiguousarray(a)
+        h = cls(a.nbytes)
+        buf = (C.c_char * a.nbytes).from_address(h.ptr)
+        h.array = np.frombuffer(buf, dtype=a.dtype).reshape(a.shape)
+        h.array[...] = a
+        return h
+
+    def close(self):
+        if self.ptr:
+            self.array = None
+            hip().hipHostFree(C.c_void_p(self.ptr))
             self.ptr = None
 
     def __del__(self):

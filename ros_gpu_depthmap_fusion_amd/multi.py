@@ -140,8 +140,9 @@ class BatchedMarkExchange:
                                              lifetime)
         else:
             torch.cuda.current_stream().synchronize()
+            # only the n live frames of the (possibly partial) batch; records at stride batch
             self.eng.union_pairs(self.union.data_ptr(), self.words, self.gpairs.data_ptr(),
-                                 self.world, self.batch, self.rec)
+                                 self.world, self.n, self.rec, frames_per_rank=self.batch)
             self.eng.voxelOccupancyGridBatch(self.union.data_ptr(), self.words, 1, self.n,
                                              self.words, self.batch * self.words, lifetime)
         self.n = 0

@@ -136,6 +136,66 @@ def depth_frame(cam: Camera, k: int, frame: int, seed: int = SEED_BASE + 2,
     return d.astype(np.uint16).reshape(H, W)
 
 
+def _value_noise(W: int, H: int, cells: int, key: np.uint64) -> np.ndarray:
+    """Smooth value noise in [-1, 1] over an H x W image: random values on a lattice of `cells`
+    cells across the image width (square cells, so the structure has the same angular size at
+    every resolution), smoothstep-interpolated."""
+    step = W / float(cells)
+    gx, gy = cells + 2, int(np.ceil(H / step)) + 2
+    node = np.arange(gx * gy, dtype=np.uint64)
+    lat = (2.0 * uniform01(splitmix64(key ^ node)) - 1.0).reshape(gy, gx)
+    fu = (np.arange(W, dtype=np.float64) + 0.5) / step
+    fv = (np.arange(H, dtype=np.float64) + 0.5) / step
+    iu, iv = np.floor(fu).astype(np.int64), np.floor(fv).astype(np.int64)
+    su, sv = fu - iu, fv - iv
+    su, sv = su * su * (3 - 2 * su), sv * sv * (3 - 2 * sv)
+    a = lat[iv][:, iu]
+    b = lat[iv][:, iu + 1]
+    c = lat[iv + 1][:, iu]
+    d = lat[iv + 1][:, iu + 1]
+    top = a + (b - a) * su[None, :]
+    bot = c + (d - c) * su[None, :]
+    return top + (bot - top) * sv[:, None]
+
+
+def dense_frame(cam: Camera, k: int, frame: int, seed: int = SEED_BASE + 2) -> np.ndarray:
+    """uint16 [H, W] depth in millimetres with sensor-like, spatially correlated errors: the
+    realistic-density workload of the benchmark (VERDICT r1 "What's weak" 4).
+
+    `depth_frame` draws independent ±1 % noise and 3 % holes per pixel; at 4K 1 % of the depth is
+    ~20x the lateral pixel spacing, every surface normal is noise and the flying-pixel filter
+    (filter_flying_pixels.glsl:135-165, F=4 thr 0.3) removes ~99.97 % of the pixels.  Here the
+    errors have a size in the image (fractions of the field of view), not in pixels:
+      - a smooth depth bias of ±0.2 % (value noise, 32 cells across the image);
+      - ±0.5 mm dither before the rounding to whole millimetres (the u16 quantisation);
+      - holes as blobs (value noise over 48 cells above a threshold, ~2 % of the image) plus a
+        0.02 % per-pixel dropout.
+    With the same analytic scene about 60-70 % of the pixels survive the launch-default filter at
+    VGA, 720p and 4K alike (tests/test_synth.py states the measured fractions)."""
+    H, W = cam.height, cam.width
+    v, u = np.mgrid[0:H, 0:W].astype(np.float64)
+    ro = np.stack([(u - cam.cx) / cam.fx, (v - cam.cy) / cam.fy, np.ones_like(u)], -1).reshape(-1, 3)
+    R = cam.T_world[:3, :3].astype(np.float64)
+    dirs = ro @ R.T
+    origin = cam.T_world[:3, 3].astype(np.float64)
+    t = _raycast(origin, dirs).reshape(H, W)
+    key = np.uint64(seed) ^ (np.uint64(k) << np.uint64(48)) ^ (np.uint64(frame) << np.uint64(32))
+    bias = _value_noise(W, H, 32, key ^ np.uint64(0xB1A5 << 16))
+    blobs = _value_noise(W, H, 48, key ^ np.uint64(0x401E << 16))
+    pix = np.arange(H * W, dtype=np.uint64)
+    h1 = splitmix64(key ^ pix).reshape(H, W)
+    h2 = splitmix64(h1)
+    dither = uniform01(h1) - 0.5
+    d = np.where(np.isfinite(t), t * 1000.0 * (1.0 + 0.002 * bias) + dither, 0.0)
+    d = np.rint(d)
+    d = np.where((d < 300) | (d > 12000), 0, d)
+    d = np.where((blobs > 0.80) | (uniform01(h2) < 2e-4), 0, d)
+    return d.astype(np.uint16)
+
+
+WORKLOADS = {"dense": dense_frame, "stress": depth_frame}
+
+
 def uniform_frame(cam: Camera, k: int, frame: int, seed: int = SEED_BASE + 9) -> np.ndarray:
     """Stress frame: uniform random u16 depth (flying pixels everywhere)."""
     pix = np.arange(cam.height * cam.width, dtype=np.uint64)

@@ -1,0 +1,236 @@
+"""GPU parity tests added in round 2: the realistic-density workload at VGA / 720p / 4K, host
+depth maps through the pinned / overlapped H2D path, the batched grid update and the sparse
+union of a partial batch, the full C3 window (256 x 720p sequences) and a window large enough to
+reach the multi-segment k_sel tiles and k_group_big against the oracle.
+
+Bar as in test_gpu_parity.py: bit-exact points, keys, voxel means, grids, history.
+"""
+import numpy as np
+import pytest
+
+from drive import bits, compare_results
+from oracle import OracleFusion
+from ros_gpu_depthmap_fusion_amd import hiprt, multi, synth
+from ros_gpu_depthmap_fusion_amd.gdf import ComponentParams
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def Engine(gpu_engine_factory):
+    return gpu_engine_factory
+
+
+def cam_args(cam, depth):
+    return (depth, *cam.intrinsics(), cam.T_world, cam.T_crop)
+
+
+def run_fused(eng, cams_frames, params, **kw):
+    eng.clear()
+    for c in cams_frames:
+        eng.addDepthmap(*c)
+    return eng.processFrame(params, **kw)
+
+
+@pytest.mark.parametrize("W,H,frames", [(640, 480, 3), (1280, 720, 2)])
+def test_dense_workload_parity(Engine, W, H, frames):
+    """C2 (and 720p) at the realistic density of the benchmark (synth.dense_frame, ~65 % of the
+    pixels survive the flying-pixel filter): everything bit-exact, frame after frame."""
+    p = ComponentParams()
+    gpu, orc = Engine(), OracleFusion(threads=8)
+    cam = synth.make_camera(0, W, H)
+    for f in range(frames):
+        args = [cam_args(cam, synth.dense_frame(cam, 0, f))]
+        r = run_fused(gpu, args, p)
+        run_fused(orc, args, p)
+        assert r.num_points == orc.point_count() > 0.3 * W * H
+        compare_results(gpu, orc, tag=f"{W}x{H} frame {f}")
+
+
+def test_dense_4k_frame_parity(Engine):
+    """A full 3840x2160 dense frame (3 M points after crop; 256-px compaction segments, 8-key
+    radix tiles, k_group over ~12 K tiles): bit-exact vs the oracle."""
+    p = ComponentParams()
+    gpu, orc = Engine(), OracleFusion(threads=16)
+    cam = synth.make_camera(0, 3840, 2160)
+    args = [cam_args(cam, synth.dense_frame(cam, 0, 0))]
+    r = run_fused(gpu, args, p)
+    run_fused(orc, args, p)
+    assert r.num_points == orc.point_count() > 2_000_000
+    compare_results(gpu, orc, tag="4k dense")
+
+
+@pytest.mark.parametrize("pinned", [True, False])
+def test_host_stream_overlapped_h2d(Engine, pinned):
+    """Host depth maps through gdf_run_host_stream with 3 frames in flight: pinned maps are read
+    in place on the slot's stream, pageable ones through the slot's pinned staging; the grid after
+    all frames and the last frame's outputs equal the oracle's.  The pageable source is
+    overwritten after the call returns (the staging copy was taken: borrowed-until-upload)."""
+    p = ComponentParams()
+    cam = synth.make_camera(0, 320, 240)
+    ring = [synth.dense_frame(cam, 0, f) for f in range(4)]
+    if pinned:
+        host = [hiprt.PinnedArray.from_numpy(f) for f in ring]
+        ptrs = [h.ptr for h in host]
+    else:
+        host = [f.copy() for f in ring]
+        ptrs = [h.ctypes.data for h in host]
+    gpu, orc = Engine(), OracleFusion(threads=8)
+    gpu.set_pipeline_depth(3)
+    sc = gpu.make_stream_camera(ptrs, 320, 240, *cam.intrinsics(), cam.T_world, cam.T_crop)
+    n = 11
+    gpu.run_host_stream([sc], p.to_c(None, None, False, False), 0, n)
+    if not pinned:
+        for h in host:
+            h[...] = 0  # the engine holds its own copies by now
+    gpu.synchronize()
+    for i in range(n):
+        run_fused(orc, [cam_args(cam, ring[i % 4])], p)
+    compare_results(gpu, orc, tag="host stream")
+
+
+@pytest.mark.parametrize("lifetime", [10, 300])
+def test_grid_batch_update_partial_batch(Engine, lifetime):
+    """gdf_voxel_occupancy_grid_batch on an all-gathered [rank, batch, words] buffer of a PARTIAL
+    batch (3 live frames of 4, the 4th holding stale garbage): lifetime 10 = the one-pass u8
+    kernel, 300 = the u32 frame-by-frame branch; the grid equals the host history of the
+    per-frame unions."""
+    p = ComponentParams()
+    p.occupancy_lifetime = lifetime
+    gpu = Engine()
+    cam = synth.make_camera(0, 160, 120)
+    run_fused(gpu, [cam_args(cam, synth.dense_frame(cam, 0, 0))], p, defer_occupancy_grid=True)
+    _, ncells = gpu.grid_size()
+    nw = multi.words_for(ncells)
+    # the frame's own marks are taken first (pending marks are refused)
+    sink = hiprt.DeviceArray(nw * 4)
+    gpu.take_marks(sink.ptr, nw)
+    gpu.synchronize()
+    rng = np.random.default_rng(lifetime)
+    world, batch, live = 2, 4, 3
+    masks = np.zeros((world, batch, nw), np.uint32)
+    for r in range(world):
+        for f in range(batch):
+            m = rng.random(ncells) < (0.003 if f < live else 0.5)  # frame 3: stale, dense
+            masks[r, f] = multi.pack_marks(m)
+    dev = hiprt.DeviceArray.from_numpy(masks.reshape(-1))
+    gpu.voxelOccupancyGridBatch(dev.ptr, nw, world, live, nw, batch * nw, lifetime)
+    hist = np.zeros(ncells, np.uint32)
+    for f in range(live):
+        u = multi.unpack_marks(masks[0, f] | masks[1, f], ncells)
+        hist = multi.historic_update(hist, u, lifetime)
+    np.testing.assert_array_equal(gpu.downloadVoxelOccupancyGrid(), (hist & 0xFF).astype(np.uint8))
+    np.testing.assert_array_equal(gpu.historic_grid(), hist)
+
+
+def test_union_pairs_partial_batch_skips_stale_records(Engine):
+    """A partial sparse batch (n = 2 live frames of batch 4): the stale records 2..3 carry counts
+    far above the cap (a previous, dense batch); union_pairs with frames_per_rank = 4 visits only
+    the live records and reads each record up to its own cap."""
+    gpu = Engine()
+    p = ComponentParams()
+    cam = synth.make_camera(0, 64, 48)
+    run_fused(gpu, [cam_args(cam, synth.dense_frame(cam, 0, 0))], p)
+    _, ncells = gpu.grid_size()
+    nw = multi.words_for(ncells)
+    cap, batch, live, world = 64, 4, 2, 2
+    rec = 1 + 2 * cap
+    buf = np.zeros((world, batch, rec), np.uint32)
+    want = np.zeros((live, nw), np.uint32)
+    rng = np.random.default_rng(7)
+    for r in range(world):
+        for f in range(batch):
+            if f < live:
+                k = int(rng.integers(1, cap))
+                idx = rng.choice(nw, k, replace=False).astype(np.uint32)
+                val = rng.integers(1, 2**32, k, dtype=np.uint64).astype(np.uint32)
+                buf[r, f, 0] = k
+                buf[r, f, 1:1 + 2 * k:2] = idx
+                buf[r, f, 2:2 + 2 * k:2] = val
+                np.bitwise_or.at(want[f], idx, val)
+            else:
+                buf[r, f, 0] = 10_000_000  # stale over-cap count
+                buf[r, f, 1:] = 0xFFFFFFFF
+    dev = hiprt.DeviceArray.from_numpy(buf.reshape(-1))
+    uni = hiprt.DeviceArray(batch * nw * 4)
+    gpu.union_pairs(uni.ptr, nw, dev.ptr, world, live, rec, frames_per_rank=batch)
+    gpu.synchronize()
+    np.testing.assert_array_equal(uni.to_numpy(np.uint32, live * nw).reshape(live, nw), want)
+
+
+def _window_frames(gpu, orc, lidar, cam, p, nseq, npf, seqs_host, seqs_dev, depth, sync_last):
+    for k in range(nseq):
+        s, ns = synth.sequence_time(k)
+        T = synth.move_transform(k)
+        if gpu is not None:
+            gpu.addPointSequenceDevice(seqs_dev[k % len(seqs_dev)].ptr, npf, 16, s, ns, T)
+        if orc is not None:
+            orc.addPointSequence(seqs_host[k % len(seqs_host)], s, ns, T)
+        for e in (gpu, orc):
+            if e is None:
+                continue
+            e.clear()
+            e.addDepthmap(*cam_args(cam, depth[k % len(depth)]))
+            if e is gpu:
+                r = e.processFrame(p, T_world_move=lidar.T_world, T_crop_move=lidar.T_crop,
+                                   synchronous=sync_last and k == nseq - 1)
+            else:
+                e.processFrame(p, T_world_move=lidar.T_world, T_crop_move=lidar.T_crop)
+    return r
+
+
+def test_rollbuffer_window_oracle_parity_large(Engine):
+    """Rollbuffer window of 14 sequences x 320x240 (dense) + a 320x240 depth map: ~1.1 M selected
+    points per frame - k_sel's multi-segment tiles (8 x 512 points), tiles straddling two
+    sequences, > 4096 group tiles (group-id offsets by count + scan) and voxels longer than the
+    512 staged points (k_group_big) - bit-exact vs the oracle on the last frames."""
+    p = ComponentParams()
+    p.ps_timespan = 13.5 / 30.0
+    lidar = synth.make_camera(1, 320, 240)
+    cam = synth.make_camera(0, 320, 240)
+    npf = 320 * 240
+    host = [np.concatenate([synth.back_project(lidar, synth.dense_frame(lidar, 1, f)),
+                            np.ones((npf, 1), np.float32)], 1) for f in range(3)]
+    dev = [hiprt.DeviceArray.from_numpy(h) for h in host]
+    depth = [synth.dense_frame(cam, 0, f) for f in range(3)]
+    gpu, orc = Engine(), OracleFusion(threads=16)
+    r = _window_frames(gpu, orc, lidar, cam, p, 18, npf, host, dev, depth, True)
+    st = gpu.rollbuffer_state()
+    assert st.selection_sequence_count == 14 and st.as_tuple() == orc.rollbuffer_state()
+    assert r.num_points_total == 15 * npf and r.num_points > 300_000
+    compare_results(gpu, orc, tag="window")
+
+
+def test_c3_full_window_properties(Engine):
+    """C3 at full size: 720p depth + a window of 256 sequences of 921 600 points (236 M selected
+    points per frame, 3.8 GB ring): the selection, one voxel mean per distinct key, the grid holds
+    exactly the frame's voxels at full lifetime, and the points are the oracle's for the depth
+    part (the first N_depth points; rollbuffer survivors follow in selection order)."""
+    p = ComponentParams()
+    W, H = 1280, 720
+    n = W * H
+    p.ps_timespan = 255.5 / 30.0
+    lidar = synth.make_camera(1, W, H)
+    cam = synth.make_camera(0, W, H)
+    seqs = [hiprt.DeviceArray.from_numpy(np.concatenate(
+        [synth.back_project(lidar, synth.dense_frame(lidar, 1, f)),
+         np.ones((n, 1), np.float32)], 1)) for f in range(2)]
+    depth = [synth.dense_frame(cam, 0, f) for f in range(2)]
+    gpu = Engine()
+    r = _window_frames(gpu, None, lidar, cam, p, 260, n, None, seqs, depth, True)
+    st = gpu.rollbuffer_state()
+    assert st.selection_sequence_count == 256 and st.selection_point_count == 256 * n
+    assert r.num_points_total == 257 * n
+    c = gpu.downloadVoxelCoords()
+    assert len(c) == r.num_points > 10_000_000
+    u = np.unique(c)
+    assert len(gpu.downloadVoxelizedPoints()) == len(u)
+    grid = gpu.downloadVoxelOccupancyGrid().reshape(-1)
+    assert np.array_equal(np.flatnonzero(grid == p.occupancy_lifetime), u)
+    orc = OracleFusion(threads=8)
+    orc.clear()
+    orc.addDepthmap(*cam_args(cam, depth[259 % 2]))
+    orc.processFrame(p)
+    nd = orc.point_count()
+    pts = gpu.downloadPoints()
+    assert np.array_equal(bits(pts[:nd]), bits(orc.downloadPoints()))

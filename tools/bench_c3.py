@@ -28,40 +28,31 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBPS = 8000.0
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--width", type=int, default=1280)
-    ap.add_argument("--height", type=int, default=720)
-    ap.add_argument("--window", type=int, default=256)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--ring", type=int, default=4, help="distinct device-resident sequences/frames")
-    ap.add_argument("--profile-steps", type=int, default=5)
-    ap.add_argument("--json", default=None)
-    ap.add_argument("--corners", action="store_true",
-                    help="voxelize without averaging (voxel corners; diagnostics)")
-    args = ap.parse_args()
-
+def run_c3(width=1280, height=720, window=256, steps=20, ring=4, profile_steps=5, corners=False,
+           workload="dense"):
+    """The C3 line as a dict (bench.py puts it into its "secondary" results)."""
     import numpy as np
     from ros_gpu_depthmap_fusion_amd import build_library, hiprt, synth
     from ros_gpu_depthmap_fusion_amd.gdf import ComponentParams, GPUDepthmapFusion
 
     build_library()
-    W, H = args.width, args.height
+    W, H = width, height
     P = W * H
+    gen = synth.WORKLOADS[workload]
     cam = synth.make_camera(0, W, H)        # depth camera
     lidar = synth.make_camera(1, W, H)      # the point-sequence source (another view)
     t0 = time.perf_counter()
-    depth = [hiprt.DeviceArray.from_numpy(synth.depth_frame(cam, 0, f)) for f in range(args.ring)]
+    depth = [hiprt.DeviceArray.from_numpy(gen(cam, 0, f)) for f in range(ring)]
     seqs = []
-    for f in range(args.ring):
-        xyz = synth.back_project(lidar, synth.depth_frame(lidar, 1, f))
+    for f in range(ring):
+        xyz = synth.back_project(lidar, gen(lidar, 1, f))
         rec = np.concatenate([xyz, np.ones((len(xyz), 1), np.float32)], 1)  # step 16
         seqs.append(hiprt.DeviceArray.from_numpy(np.ascontiguousarray(rec)))
     gen_s = time.perf_counter() - t0
 
     p = ComponentParams()
-    p.ps_timespan = (args.window - 0.5) / 30.0
-    p.voxel_average = not args.corners
+    p.ps_timespan = (window - 0.5) / 30.0
+    p.voxel_average = not corners
     eng = GPUDepthmapFusion(0)
     pc_async = p.to_c(lidar.T_world, lidar.T_crop, False, False)
     pc_sync = p.to_c(lidar.T_world, lidar.T_crop, True, False)
@@ -70,9 +61,9 @@ def main():
     def frame(pc):
         nonlocal k
         s, ns = synth.sequence_time(k)
-        eng.addPointSequenceDevice(seqs[k % args.ring].ptr, P, 16, s, ns, synth.move_transform(k))
+        eng.addPointSequenceDevice(seqs[k % ring].ptr, P, 16, s, ns, synth.move_transform(k))
         eng.clear()
-        eng.addDepthmapDevice(depth[k % args.ring].ptr, W, H, *cam.intrinsics(), cam.T_world,
+        eng.addDepthmapDevice(depth[k % ring].ptr, W, H, *cam.intrinsics(), cam.T_world,
                               cam.T_crop)
         r = eng.processFramePrepared(pc)
         k += 1
@@ -80,11 +71,11 @@ def main():
 
     # fill the window (untimed), then one synchronous frame for the counts
     t0 = time.perf_counter()
-    for i in range(args.window + 1):
+    for i in range(window + 1):
         frame(pc_async)
         if i % 32 == 0:
             eng.synchronize()
-            print(f"# fill {i}/{args.window} {time.perf_counter() - t0:.1f}s", file=sys.stderr,
+            print(f"# c3 fill {i}/{window} {time.perf_counter() - t0:.1f}s", file=sys.stderr,
                   flush=True)
     eng.synchronize()
     r = frame(pc_sync)
@@ -94,7 +85,7 @@ def main():
     (gx, gy, gz), ncells = eng.grid_size()
     probe = GPUDepthmapFusion(0)
     probe.clear()
-    probe.addDepthmapDevice(depth[(k - 1) % args.ring].ptr, W, H, *cam.intrinsics(), cam.T_world,
+    probe.addDepthmapDevice(depth[(k - 1) % ring].ptr, W, H, *cam.intrinsics(), cam.T_world,
                             cam.T_crop)
     N_depth = probe.processFrame(p).num_points
     probe.close()
@@ -104,21 +95,24 @@ def main():
                    "p99": int(np.percentile(gsz, 99)),
                    "points_in_groups_over_4096": int(gsz[gsz > 4096].sum())}
 
+    for _ in range(3):  # every graph / buffer of the steady state in place
+        frame(pc_async)
     eng.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         frame(pc_async)
     eng.synchronize()
     elapsed = time.perf_counter() - t0
 
     eng.set_profiling(True)
-    for _ in range(args.profile_steps):
+    for _ in range(profile_steps):
         frame(pc_async)
     eng.synchronize()
     kt = eng.kernel_times()
     eng.set_profiling(False)
+    eng.close()
 
-    ms = elapsed / args.steps * 1e3
+    ms = elapsed / steps * 1e3
     items = P + S
     seg = 1024
     # algorithmic HBM bytes per launch (SURVEY §8(d) + C3 terms)
@@ -137,21 +131,25 @@ def main():
         tot, n = kt[name]
         if n:
             per[name] = {"avg_us": round(tot * 1e3 / n, 2), "launches_per_frame":
-                         round(n / args.profile_steps, 2),
+                         round(n / profile_steps, 2),
                          "GBps": round(model[name] / (tot / 1e3 / n) / 1e9, 1)}
     dom = max(per, key=lambda q: per[q]["avg_us"] * per[q]["launches_per_frame"])
     achieved = per[dom]["GBps"]
-    out = {
-        "metric": "Mpoints/s depth pixels (C3: 720p + 256-sequence rollbuffer window)",
-        "value": round(P / (elapsed / args.steps) / 1e6, 3),
-        "unit": "Mpoints/s", "n_gpus": 1, "steps": args.steps, "ms_per_step": round(ms, 4),
+    # SURVEY §8(d) B_alg for C3: depth 2P + 24N + 9C, plus 24 n_new + 24 n_sel + 32 n_sel
+    survey = 2.0 * P + 24.0 * N + 9.0 * ncells + 24.0 * P + 56.0 * S
+    return {
+        "metric": "Mpoints/s depth pixels (C3: 720p + %d-sequence rollbuffer window)" % window,
+        "value": round(P / (elapsed / steps) / 1e6, 3),
+        "unit": "Mpoints/s", "n_gpus": 1, "steps": steps, "ms_per_step": round(ms, 4),
         "points_per_frame_total": items,
-        "total_points_Mps": round(items / (elapsed / args.steps) / 1e6, 1),
-        "dtype": "f32", "data": "synthetic (ray-cast scene; %d device-resident frames and "
-                                "sequences reused round-robin)" % args.ring,
+        "total_points_Mps": round(items / (elapsed / steps) / 1e6, 1),
+        "step_survey_bytes": round(survey),
+        "step_survey_frac": round(survey / (elapsed / steps) / 1e9 / HBM_PEAK_GBPS, 4),
+        "dtype": "f32", "data": "synthetic (ray-cast scene, %s frames; %d device-resident frames "
+                                "and sequences reused round-robin)" % (workload, ring),
         "config": {"workload": "C3: %dx%d depth + rollbuffer window of %d sequences of %d "
                                "points (timespan select, transform, crop, compaction, voxelize, "
-                               "grid %dx%dx%d)" % (W, H, args.window, P, gx, gy, gz),
+                               "grid %dx%dx%d)" % (W, H, window, P, gx, gy, gz),
                    "selected_points": S, "points_after_crop": N, "voxels": G,
                    "depth_points_after_crop": N_depth,
                    "points_per_voxel": group_sizes,
@@ -161,6 +159,23 @@ def main():
                      "per_kernel": per},
         "setup_s": round(gen_s, 1),
     }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--width", type=int, default=1280)
+    ap.add_argument("--height", type=int, default=720)
+    ap.add_argument("--window", type=int, default=256)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--ring", type=int, default=4, help="distinct device-resident sequences/frames")
+    ap.add_argument("--profile-steps", type=int, default=5)
+    ap.add_argument("--workload", choices=("dense", "stress"), default="dense")
+    ap.add_argument("--json", default=None)
+    ap.add_argument("--corners", action="store_true",
+                    help="voxelize without averaging (voxel corners; diagnostics)")
+    args = ap.parse_args()
+    out = run_c3(args.width, args.height, args.window, args.steps, args.ring, args.profile_steps,
+                 args.corners, args.workload)
     line = json.dumps(out)
     print(line)
     if args.json:
