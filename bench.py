@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--workload", choices=("dense", "stress"), default="dense")
     ap.add_argument("--ring", type=int, default=8, help="distinct device-resident frames")
+    ap.add_argument("--batch", type=int, default=4,
+                    help="frames per launch chain (gdf_next_frame_in_batch); a step is one "
+                         "batch, value counts every frame's pixels")
     ap.add_argument("--cameras", type=int, default=1,
                     help="cameras per GPU (one frame = one depth map of each; camera ids "
                          "rank*cameras + k)")
@@ -71,9 +74,12 @@ def parse():
     return ap.parse_args()
 
 
-def model_bytes(P, n_avg, g_avg, ncells):
+def model_bytes(P, n_avg, g_avg, ncells, B=1):
     """Algorithmic HBM bytes per launch of each kernel: the bytes the algorithm
-    must move once, not the cache traffic of an implementation."""
+    must move once, not the cache traffic of an implementation.  A launch of a B-frame batch
+    processes B frames (P, n, g per frame); its grid update reads and writes the grid once and
+    stores the B - 1 intermediate per-frame grids."""
+    P, n_avg, g_avg = B * P, B * n_avg, B * g_avg
     tiles = (P + 255) // 256
     return {
         "mask": 3.0 * P,                           # u16 depth in, u8 stage bits out
@@ -81,10 +87,10 @@ def model_bytes(P, n_avg, g_avg, ncells):
         "emit": 1.0 * P + 22.0 * n_avg,            # stage in, depth of kept px, xyzw + key out
         # 3 radix passes (key only in, key+index out; then key+index both ways) + the grid
         # update carried by the first pass, averaged per launch
-        "sort": (12.0 * n_avg + 16.0 * n_avg * 2 + 2.0 * ncells) / 3.0,
+        "sort": (12.0 * n_avg + 16.0 * n_avg * 2 + (B + 1.0) * ncells) / 3.0,
         # sorted keys + indices + gathered points in, means out
         "group": 24.0 * n_avg + 16.0 * g_avg,
-        "grid": 2.0 * ncells,
+        "grid": (B + 1.0) * ncells,
     }
 
 
@@ -158,16 +164,21 @@ class DepthStream:
             nvox.append(r.num_voxelized)
         return npts, nvox
 
-    def run(self, pc, first, count):
-        if self.host is not None:
+    def run(self, pc, first, count, batch=1):
+        """`count` steps of `batch` frames from frame `first * batch` on."""
+        if batch > 1:
+            self.eng.run_depth_stream_batched(self.scam, pc, first * batch, count, batch,
+                                              self.host is not None)
+        elif self.host is not None:
             self.eng.run_host_stream(self.scam, pc, first, count)
         else:
             self.eng.run_depth_stream(self.scam, pc, first, count)
 
 
-def time_single(st, params, steps, warmup, depth, kernel_timing, pmc_key):
+def time_single(st, params, steps, warmup, depth, kernel_timing, pmc_key, batch=1):
     """Steady-state single-GPU line of one DepthStream: prime (every slot's graph captured),
-    warm-up, K timed frames, then the event-timed pass for the roofline."""
+    warm-up, K timed steps (a step = one batch of `batch` frames), then the event-timed pass for
+    the roofline."""
     import numpy as np
     eng = st.eng
     npts, nvox = st.counts(params)
@@ -176,30 +187,33 @@ def time_single(st, params, steps, warmup, depth, kernel_timing, pmc_key):
     pc = params.to_c(None, None, False, False)
     # prime: a slot captures its graph on its second steady frame; 2 rounds over the slots + 1
     prime = 2 * depth + 2
-    st.run(pc, 0, prime)
-    st.run(pc, prime, warmup)
+    st.run(pc, 0, prime, batch)
+    st.run(pc, prime, warmup, batch)
     eng.synchronize()
     t0 = time.perf_counter()
-    st.run(pc, prime + warmup, steps)
+    st.run(pc, prime + warmup, steps, batch)
     eng.synchronize()
     elapsed = time.perf_counter() - t0
-    idx = [(prime + warmup + i) % st.ring for i in range(steps)]
+    idx = [((prime + warmup + i) * batch + j) % st.ring for i in range(steps) for j in range(batch)]
     n_avg = float(np.mean([npts[i] for i in idx]))
     g_avg = float(np.mean([nvox[i] for i in idx]))
-    mb = model_bytes(st.P, n_avg, g_avg, ncells)
+    mb = model_bytes(st.P, n_avg, g_avg, ncells, batch)
     roof = None
     if kernel_timing:
         kt_steps = min(steps, 200)
         eng.set_pipeline_depth(1)  # one frame in flight: launch durations without overlap
         eng.set_profiling(True)
-        st.run(pc, prime + warmup, kt_steps)
+        st.run(pc, prime + warmup, kt_steps, batch)
         eng.synchronize()
         kt = eng.kernel_times()
         eng.set_profiling(False)
         roof = roofline_from(kt, kt_steps, mb, pmc_key)
-    survey = 2.0 * st.P + 24.0 * n_avg + 9.0 * ncells  # SURVEY.md §8(d) B_alg per frame
+    # SURVEY.md §8(d) B_alg per frame, times the frames of a step
+    survey = batch * (2.0 * st.P + 24.0 * n_avg + 9.0 * ncells)
     return {
-        "value": round(st.P * steps / elapsed / 1e6, 3), "ms_per_step": round(elapsed / steps * 1e3, 5),
+        "value": round(st.P * batch * steps / elapsed / 1e6, 3),
+        "ms_per_step": round(elapsed / steps * 1e3, 5),
+        "frames_per_step": batch, "ms_per_frame": round(elapsed / steps / batch * 1e3, 5),
         "steps": steps, "warmup": warmup, "prime": prime,
         "points_per_frame_after_crop": round(n_avg), "voxels_per_frame": round(g_avg),
         "survival_after_crop": round(n_avg / st.P, 4),
@@ -294,7 +308,7 @@ def main():
 
     if dist is None:
         line = time_single(st, params, args.steps, args.warmup, max(1, min(4, args.pipeline)),
-                           not args.no_kernel_timing, pmc_key)
+                           not args.no_kernel_timing, pmc_key, max(1, args.batch))
         cfg_extra = {"parallelism": "single GPU", "exchange": None}
     else:
         line, cfg_extra = time_multi(args, st, params, dist, world, pmc_key)
@@ -315,7 +329,10 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (ray-cast analytic scene, %s frames; device-resident ring of %d "
                     "frames)" % (args.workload, args.ring),
-            "config": dict({"workload": "C2: " + workload_name(W, H, K, args.workload),
+            "config": dict({"workload": "C2: " + workload_name(W, H, K, args.workload) + (
+                                "; a step = a batch of %d frames through one launch chain "
+                                "(every frame's points, voxel means and grid)" % args.batch
+                                if args.batch > 1 and dist is None else ""),
                             "cameras_per_gpu": K}, **line, **cfg_extra),
             "roofline": roof,
             "cpu_baseline": cpu,
@@ -413,14 +430,16 @@ def run_secondary(args, params):
     steps = max(args.steps, 50)
     warm = max(args.warmup, 10)
     kt = not args.no_kernel_timing
-    for name, (W, H, wl, ring, st_steps) in {
-            "720p": (1280, 720, "dense", 4, steps),
-            "4k": (3840, 2160, "dense", 2, max(20, steps // 4)),
-            "vga_stress": (640, 480, "stress", 8, steps)}.items():
+    for name, (W, H, wl, ring, st_steps, B) in {
+            "vga_single_frame": (640, 480, "dense", 8, steps, 1),
+            "720p": (1280, 720, "dense", 4, steps, 4),
+            "720p_single_frame": (1280, 720, "dense", 4, steps, 1),
+            "4k": (3840, 2160, "dense", 2, max(20, steps // 4), 1),
+            "vga_stress": (640, 480, "stress", 8, steps, args.batch)}.items():
         eng = GPUDepthmapFusion(0)
         st = DepthStream(eng, W, H, 1, 0, wl, ring)
         r = time_single(st, params, st_steps, warm, max(1, min(4, args.pipeline)), kt,
-                        f"{W}x{H}/{wl}")
+                        f"{W}x{H}/{wl}", B)
         r["workload"] = workload_name(W, H, 1, wl)
         out[name] = r
         del st
@@ -429,7 +448,7 @@ def run_secondary(args, params):
     eng = GPUDepthmapFusion(0)
     st = DepthStream(eng, args.width, args.height, 1, 0, args.workload, args.ring,
                      host_frames=True)
-    r = time_single(st, params, steps, warm, max(1, min(4, args.pipeline)), False, "")
+    r = time_single(st, params, steps, warm, max(1, min(4, args.pipeline)), False, "", args.batch)
     r["workload"] = "C2 with host (pinned) depth maps: " + workload_name(
         args.width, args.height, 1, args.workload)
     r["value_h2d"] = r.pop("value")

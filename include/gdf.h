@@ -223,6 +223,25 @@ int gdf_get_device_results(gdf_engine* engine, const float** points, const uint3
 int gdf_process_frame(gdf_engine* engine, const gdf_frame_params* params,
                       gdf_frame_result* out_result);
 
+/* ---- multi-frame batches ------------------------------------------------------------------- */
+/* Several depth-only frames through ONE launch chain (the per-frame sequence of
+ * GPUDepthmapFusionComponent::processDepthmaps, component.cpp:92-300, applied to each frame; a
+ * throughput mode for streams whose frames are launch-latency bound on the GPU, e.g. VGA).
+ * After gdf_clear and the depth maps of frame 0, gdf_next_frame_in_batch starts frame 1 of the
+ * same batch, and so on (<= 16 frames, each with >= 1 depth map); gdf_process_frame then runs
+ * every frame: each frame's points, voxel keys, voxel means and grid update are exactly those of
+ * processing the frames one by one (flying-pixel neighbour reads stay inside their frame, the
+ * grid updates apply in frame order).  Results: the compacted points / keys / voxel means of all
+ * frames back to back, frame f at [point_start[f], point_start[f+1]) and
+ * [voxel_start[f], voxel_start[f+1]) (gdf_get_batch_ranges, nframes + 1 entries each); the u8
+ * grid after frame f from gdf_download_batch_occupancy_grid.  Not with point sequences, a
+ * deferred grid or lifetime > 255. */
+int gdf_next_frame_in_batch(gdf_engine* engine);
+int gdf_get_batch_ranges(gdf_engine* engine, uint32_t* point_start, uint32_t* voxel_start,
+                         uint32_t capacity, uint32_t* out_frames);
+int gdf_download_batch_occupancy_grid(gdf_engine* engine, uint32_t frame, uint8_t* out,
+                                      uint64_t capacity);
+
 /* ---- multi-GPU (one camera per rank) ------------------------------------------------------- */
 /* Per-frame occupancy marks of this rank as a bitmask of ceil(num_cells/32) uint32 words, and
  * the merge of all ranks' masks (bitwise OR of `num_ranks` masks laid out back to back, as

@@ -43,6 +43,13 @@ int gdf_run_host_stream(gdf_engine* engine, const gdf_stream_camera* cameras,
                         uint32_t num_cameras, const gdf_frame_params* params, uint64_t first,
                         uint64_t count);
 
+/* `batches` multi-frame batches of `batch` frames each (gdf_next_frame_in_batch, include/gdf.h):
+ * batch b holds frames first + b*batch .. first + (b+1)*batch - 1; host != 0 reads host depth
+ * maps like gdf_run_host_stream. */
+int gdf_run_depth_stream_batched(gdf_engine* engine, const gdf_stream_camera* cameras,
+                                 uint32_t num_cameras, const gdf_frame_params* params,
+                                 uint64_t first, uint64_t batches, uint32_t batch, int host);
+
 #ifdef __cplusplus
 }
 #endif

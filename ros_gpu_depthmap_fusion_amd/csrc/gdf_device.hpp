@@ -61,7 +61,7 @@ struct CamDesc {
     uint32_t seg0;          // first segment of this camera (emitting cameras)
     uint32_t nseg;          // H * nchunk
     uint32_t segw;          // pixels per segment (a multiple of 64, <= 1024)
-    uint32_t pad;
+    uint32_t frame;         // frame of a multi-frame batch (neighbour reads stay inside it)
     float Tw[16];           // row-major T_world
     float Tc[16];           // row-major T_crop
 };
@@ -129,6 +129,13 @@ struct FrameArgs {
     uint32_t* err;
     uint32_t* grid_seq_out;     // optional: k_mask stores grid_seq here (the fused grid update's
     uint32_t grid_seq;          // sequence number, read by the first sort pass of the frame)
+    // multi-frame batch (depth-only frames through one launch chain): frame f's points are
+    // [frame_pt_start[f], frame_pt_start[f + 1]) of the compacted output, its occupancy marks at
+    // marks + f * mark_words, its sort key = voxel key | f << frame_shift
+    uint32_t nframes;           // 1: a single frame
+    uint32_t frame_shift;       // bit width of the voxel keys (the frame index sits above)
+    uint64_t mark_words;        // words of one frame's mark bitmask
+    uint32_t* frame_pt_start;   // [nframes + 1], written by k_emit
 };
 static_assert(sizeof(FrameArgs) <= 4096, "kernel arguments are limited to 4 KiB");
 

@@ -6,20 +6,27 @@
 
 namespace {
 
+// `count` calls of gdf_process_frame, each over `batch` consecutive frames (gdf_next_frame_in_batch
+// between them); frame i takes frames[i % ring] of every camera
 int run_stream(gdf_engine* e, const gdf_stream_camera* cams, uint32_t ncams,
-               const gdf_frame_params* p, uint64_t first, uint64_t count, bool host) {
-    if (!e || !p || (ncams && !cams)) return GDF_ERR_ARG;
+               const gdf_frame_params* p, uint64_t first, uint64_t count, bool host,
+               uint32_t batch) {
+    if (!e || !p || (ncams && !cams) || batch == 0) return GDF_ERR_ARG;
     for (uint32_t k = 0; k < ncams; ++k)
         if (!cams[k].frames || cams[k].ring == 0) return GDF_ERR_ARG;
-    for (uint64_t i = first; i < first + count; ++i) {
+    for (uint64_t b = 0; b < count; ++b) {
         int rc = gdf_clear(e);
         if (rc) return rc;
-        for (uint32_t k = 0; k < ncams; ++k) {
-            const gdf_stream_camera& c = cams[k];
-            rc = (host ? gdf_add_depthmap : gdf_add_depthmap_device)(
-                e, c.frames[i % c.ring], c.width, c.height, c.depth_scale, c.fx, c.fy, c.cx, c.cy,
-                c.T_world, c.T_crop);
-            if (rc) return rc;
+        for (uint32_t j = 0; j < batch; ++j) {
+            const uint64_t i = first + b * batch + j;
+            if (j && (rc = gdf_next_frame_in_batch(e))) return rc;
+            for (uint32_t k = 0; k < ncams; ++k) {
+                const gdf_stream_camera& c = cams[k];
+                rc = (host ? gdf_add_depthmap : gdf_add_depthmap_device)(
+                    e, c.frames[i % c.ring], c.width, c.height, c.depth_scale, c.fx, c.fy, c.cx,
+                    c.cy, c.T_world, c.T_crop);
+                if (rc) return rc;
+            }
         }
         rc = gdf_process_frame(e, p, nullptr);
         if (rc) return rc;
@@ -31,10 +38,17 @@ int run_stream(gdf_engine* e, const gdf_stream_camera* cams, uint32_t ncams,
 
 extern "C" int gdf_run_depth_stream(gdf_engine* e, const gdf_stream_camera* cams, uint32_t ncams,
                                     const gdf_frame_params* p, uint64_t first, uint64_t count) {
-    return run_stream(e, cams, ncams, p, first, count, false);
+    return run_stream(e, cams, ncams, p, first, count, false, 1);
 }
 
 extern "C" int gdf_run_host_stream(gdf_engine* e, const gdf_stream_camera* cams, uint32_t ncams,
                                    const gdf_frame_params* p, uint64_t first, uint64_t count) {
-    return run_stream(e, cams, ncams, p, first, count, true);
+    return run_stream(e, cams, ncams, p, first, count, true, 1);
+}
+
+extern "C" int gdf_run_depth_stream_batched(gdf_engine* e, const gdf_stream_camera* cams,
+                                            uint32_t ncams, const gdf_frame_params* p,
+                                            uint64_t first, uint64_t batches, uint32_t batch,
+                                            int host) {
+    return run_stream(e, cams, ncams, p, first, batches, host != 0, batch);
 }

@@ -129,6 +129,7 @@ struct PsBuf {  // PointSequences, gpu_depthmap_fusion.h:206-217
 struct Cam {
     const uint16_t* host = nullptr;
     const uint16_t* dev = nullptr;
+    uint32_t frame = 0;  // frame of a multi-frame batch
     uint32_t W, H, n;
     float scale, fx, fy, cx, cy;
     float Tw[16], Tc[16];
@@ -212,8 +213,12 @@ struct Slot {
     DevBuf d_gcnt, d_goff;          // group starts per tile + their scan (large frames)
     DevBuf d_bigq, d_bigcnt;        // long voxels queued for k_group_big (large frames)
     bool vox_valid = false;
-    DevBuf d_markbits;              // this frame's occupancy marks (1 bit per cell)
+    DevBuf d_markbits;              // this frame's occupancy marks (1 bit per cell; per batch frame)
     uint32_t marks_gen = ~0u;
+    uint32_t marks_frames = 0;      // frames the zeroed mark buffer covers
+    DevBuf d_fstart, d_fvox;        // batch: first point / first voxel of each frame [nframes + 1]
+    DevBuf d_snap;                  // batch: the u8 grid after each frame but the last
+    uint32_t nframes = 1;           // frames of the slot's last processed batch
     uint32_t n_total = 0;
     // steady-state frame as a HIP graph (the fused frame + voxelize launches of this slot): one
     // graph launch and two kernel-node argument updates (depth pointers, grid ticket) per frame
@@ -262,6 +267,7 @@ struct gdf_engine {
 
     // frame inputs
     std::vector<Cam> cams;
+    uint32_t nframes = 1;           // frames of the batch being assembled (gdf_next_frame_in_batch)
     uint32_t depth_total = 0;
     std::vector<CamDesc> halo;      // halo cameras (multi-GPU), negative offsets
     std::vector<CamTable> tables = std::vector<CamTable>(kMaxCams);
@@ -269,7 +275,6 @@ struct gdf_engine {
     uint32_t mask_blocks = 0;       // compaction segments over the emitting cameras
     uint32_t max_segw = 0;          // widest segment (sizes k_mask's LDS band)
     bool depth_uploaded = false;
-    std::vector<std::pair<const void*, bool>> pinned_cache;  // is_pinned answers, most recent last
 
     // new sequences on the device
     DevBuf d_new;
@@ -451,6 +456,7 @@ void next_slot(gdf_engine* e) {
 // ---- frame inputs ---------------------------------------------------------------------------------
 void engine_clear(gdf_engine* e) {  // fusion.cpp:725-732
     next_slot(e);
+    e->nframes = 1;
     e->rb.selection_point_count = 0;
     e->rb.selection_sequence_count = 0;
     e->depth_total = 0;
@@ -472,6 +478,7 @@ void add_depthmap(gdf_engine* e, const uint16_t* host, const uint16_t* dev, uint
     Cam c;
     c.host = host;
     c.dev = dev;
+    c.frame = e->nframes - 1;
     c.W = W; c.H = H; c.n = W * H;
     c.scale = scale; c.fx = fx; c.fy = fy; c.cx = cx; c.cy = cy;
     std::memcpy(c.Tw, Tw, 64);
@@ -724,37 +731,17 @@ void ensure_table(gdf_engine* e, size_t slot, const Cam& c) {
     t.valid = true;
 }
 
-// true when `p` is page-locked host memory (hipHostMalloc / hipHostRegister): the DMA engine reads
-// it directly, asynchronously.  The answer is cached for the last pointers seen (a sensor driver
-// cycles through a few buffers).
-bool is_pinned(gdf_engine* e, const void* p) {
-    auto& cache = e->pinned_cache;
-    for (auto& kv : cache)
-        if (kv.first == p) return kv.second;
-    hipPointerAttribute_t attr{};
-    bool pinned = false;
-    if (hipPointerGetAttributes(&attr, p) == hipSuccess)
-        pinned = attr.type == hipMemoryTypeHost && attr.hostPointer != nullptr;
-    else
-        (void)hipGetLastError();  // pageable memory: not known to HIP
-    if (cache.size() >= 16) cache.erase(cache.begin());
-    cache.emplace_back(p, pinned);
-    return pinned;
-}
-
-// Host depth maps (the reference's blocking glBufferSubData, fusion.cpp:1583-1593) go to the
-// slot's device buffer with hipMemcpyAsync on the slot's own stream, so the copy of frame f+1
-// overlaps the kernels of frame f (another slot, another stream) with no cross-stream event.
-// Pinned sources are read in place by the DMA engine; pageable ones are first copied into the
-// slot's pinned staging buffer (after the slot's previous copy from it has finished), so the
-// caller's buffer is free again when gdf_upload_depthmaps returns, as in the reference.
+// Host depth maps (the reference's blocking glBufferSubData, fusion.cpp:1583-1593) are copied
+// into the slot's pinned staging buffer (after the slot's previous copy from it has finished) and
+// sent to the slot's device buffer with hipMemcpyAsync on the slot's own stream: the caller's
+// buffer is free again when gdf_upload_depthmaps returns, as in the reference, and the DMA of
+// frame f+1 overlaps the kernels of frame f (another slot, another stream) with no cross-stream
+// event.  (Measured on MI355X, tools/h2d_probe.py: a VGA frame costs +9 us per frame this way at
+// 3 frames in flight; a DMA straight from the caller's hipHostMalloc buffer was slower,
+// +160 us.)
 void upload_host_depth(gdf_engine* e, uint16_t* dst, const Cam& c, size_t& staged) {
     Slot& q = e->sl();
     const size_t bytes = (size_t)c.n * 2;
-    if (is_pinned(e, c.host)) {
-        HIPCHK(hipMemcpyAsync(dst, c.host, bytes, hipMemcpyHostToDevice, e->s()));
-        return;
-    }
     if (q.h2d_pending) {  // the slot's previous frame may still read the staging
         HIPCHK(hipEventSynchronize(q.h2d_done));
         q.h2d_pending = false;
@@ -767,22 +754,19 @@ void upload_host_depth(gdf_engine* e, uint16_t* dst, const Cam& c, size_t& stage
 }
 
 void upload_depthmaps(gdf_engine* e) {  // fusion.cpp:1583-1593
-    uint64_t host_px = 0, paged_px = 0;
+    uint64_t host_px = 0;
     for (const Cam& c : e->cams)
-        if (!c.dev) {
-            host_px += c.n;
-            if (!is_pinned(e, c.host)) paged_px += c.n;
-        }
+        if (!c.dev) host_px += c.n;
     if (host_px) e->sl().d_depth.ensure(host_px * 2);
-    if (paged_px && e->sl().h_stage_bytes < paged_px * 2) {  // grow the staging once per frame
+    if (host_px && e->sl().h_stage_bytes < host_px * 2) {  // grow the staging once per frame
         Slot& q = e->sl();
         if (q.h2d_pending) HIPCHK(hipEventSynchronize(q.h2d_done));
         q.h2d_pending = false;
         if (q.h_stage) HIPCHK(hipHostFree(q.h_stage));
         q.h_stage = nullptr;
         q.h_stage_bytes = 0;
-        HIPCHK(hipHostMalloc(&q.h_stage, paged_px * 2, hipHostMallocDefault));
-        q.h_stage_bytes = paged_px * 2;
+        HIPCHK(hipHostMalloc(&q.h_stage, host_px * 2, hipHostMallocDefault));
+        q.h_stage_bytes = host_px * 2;
     }
     size_t staged = 0;
     if (e->cams.size() + e->halo.size() > (size_t)kMaxCams) fail(GDF_ERR_ARG, "too many cameras (incl. halo)");
@@ -806,6 +790,7 @@ void upload_depthmaps(gdf_engine* e) {  // fusion.cpp:1583-1593
         d.xn = e->tables[e->halo.size() + k].xn.as<float>();
         d.yn = e->tables[e->halo.size() + k].yn.as<float>();
         d.W = c.W; d.H = c.H; d.n = c.n; d.emit = 1;
+        d.frame = c.frame;
         d.scale = c.scale;
         d.wmagic = ((1ull << 40) + c.W - 1) / c.W;
         // compaction segments: rows split into nchunk pieces of segw (a multiple of 64) pixels
@@ -839,12 +824,20 @@ void upload_depthmaps(gdf_engine* e) {  // fusion.cpp:1583-1593
 // the slot's mark bitmask exists and is zero for the current grid
 void ensure_marks(gdf_engine* e) {
     Slot& sl = e->sl();
-    if (sl.marks_gen == e->grid_gen) return;
-    const size_t bytes = (size_t)((e->ncells + 31) / 32) * 4;
+    if (sl.marks_gen == e->grid_gen && sl.marks_frames >= e->nframes) return;
+    const uint32_t nf = std::max(e->nframes, sl.marks_gen == e->grid_gen ? sl.marks_frames : 1u);
+    const size_t bytes = (size_t)((e->ncells + 31) / 32) * 4 * nf;
     sl.d_markbits.ensure(bytes);
     HIPCHK(hipMemsetAsync(sl.d_markbits.p, 0, bytes, e->s()));
     sl.marks_gen = e->grid_gen;
+    sl.marks_frames = nf;
 }
+
+// bits of the sort key: the voxel key, plus the frame index of a batch above it
+uint32_t frame_bits(const gdf_engine* e) {
+    return e->nframes > 1 ? 32u - (uint32_t)__builtin_clz(e->nframes - 1) : 0u;
+}
+uint32_t sort_bits(const gdf_engine* e) { return e->key_bits + frame_bits(e); }
 
 void set_grid(gdf_engine* e, const float* lo, const float* hi, const float* cs) {
     // shader grid size (fusion.cpp:1693-1698) and VoxelGridMeta (grid_meta.h:140-158) must agree
@@ -991,7 +984,7 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel) {
         // each flush their histogram with device-scope atomics; k_sort_hist counts those keys
         a.key_hist = a.total_segs <= kFusedPrefixSegs && !a.sel_tiles ? e->sl().d_khist.as<uint32_t>()
                                                                       : nullptr;
-        a.npasses = e->key_bits == 0 ? 1u : (e->key_bits + 7) / 8;
+        a.npasses = sort_bits(e) == 0 ? 1u : (sort_bits(e) + 7) / 8;
     }
     a.out_pts = e->sl().d_pts.as<float4>();
     a.out_coords = e->sl().d_coords.as<uint32_t>();
@@ -1021,6 +1014,14 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel) {
     }
     e->sl().dbg_count = e->sl().n_total;
     a.err = e->sl().d_misc.as<uint32_t>() + kErr;
+    a.nframes = e->nframes;
+    a.frame_shift = e->nframes > 1 ? e->key_bits : 0u;
+    a.mark_words = mark_words(e);
+    e->sl().nframes = e->nframes;
+    if (e->nframes > 1) {
+        e->sl().d_fstart.ensure((size_t)(e->nframes + 1) * 4);
+        a.frame_pt_start = e->sl().d_fstart.as<uint32_t>();
+    }
     return a;
 }
 
@@ -1073,7 +1074,7 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime) 
     v.pts = e->sl().d_pts.as<float4>();
     v.count = e->sl().d_misc.as<uint32_t>() + kCount;
     v.nmax = nmax;
-    v.key_bits = e->key_bits;
+    v.key_bits = sort_bits(e);
     v.average = average;
     v.hist_ready = e->sl().khist_pending ? 1 : 0;
     v.vp = e->vp;
@@ -1098,6 +1099,18 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime) 
     v.out = e->sl().d_vox.as<float4>();
     v.out_count = e->sl().d_misc.as<uint32_t>() + kVoxCount;
     if (e->sl().group_marks) v.group_marks = marks_ptr(e);
+    v.nframes = e->nframes;
+    v.frame_shift = e->nframes > 1 ? e->key_bits : 0u;
+    v.mark_words = mark_words(e);
+    if (e->nframes > 1) {
+        v.frame_pt_start = e->sl().d_fstart.as<uint32_t>();
+        e->sl().d_fvox.ensure((size_t)(e->nframes + 1) * 4);
+        v.frame_vox_start = e->sl().d_fvox.as<uint32_t>();
+        const uint64_t padded = (e->ncells + 31) / 32 * 32;
+        e->sl().d_snap.ensure((size_t)padded * (e->nframes - 1));
+        v.snapshots = e->sl().d_snap.as<uint8_t>();
+        v.snapshot_bytes = padded;
+    }
     if (fused_grid_lifetime >= 0 && !e->sl().group_marks) {  // processFrame: the grid update rides on the first sort pass
         v.grid8 = e->d_grid8.as<uint8_t>();
         v.marks = marks_ptr(e);
@@ -1651,6 +1664,16 @@ int gdf_process_frame(gdf_engine* e, const gdf_frame_params* p, gdf_frame_result
             if (r) *r = res;
             return;
         }
+        if (e->nframes > 1) {  // a multi-frame batch: depth-only frames through one launch chain
+            if (collected > 0 || e->rb.num_points > 0)
+                fail(GDF_ERR_STATE, "frame batches carry depth maps only (no point sequences)");
+            if (e->cams.empty() || e->cams.back().frame != e->nframes - 1)
+                fail(GDF_ERR_STATE, "every frame of a batch needs a depth map");
+            if (p->enable_voxel_filter && (p->defer_occupancy_grid || p->occupancy_lifetime > 255))
+                fail(GDF_ERR_STATE, "frame batches need the fused grid update (lifetime <= 255, "
+                                    "not deferred)");
+            if (e->nframes > kMaxCams) fail(GDF_ERR_ARG, "at most 16 frames per batch");
+        }
         res.processed = 1;
         upload_point_sequences(e);
         e->ps_filter_set = true;
@@ -1685,6 +1708,7 @@ int gdf_process_frame(gdf_engine* e, const gdf_frame_params* p, gdf_frame_result
         std::memcpy(e->hi, p->crop_max, 12);
         if (p->enable_voxel_filter) {
             set_grid(e, p->voxel_min, p->voxel_max, p->voxel_size);
+            if (sort_bits(e) > 32) fail(GDF_ERR_ARG, "voxel key + frame index exceed 32 bits");
             widen_if_needed(e, p->occupancy_lifetime, e->s());  // before marks are consumed
             if (!p->defer_occupancy_grid && e->grid_mode == 0) {
                 run_fused_frame(e, p->voxel_average, p->occupancy_lifetime);
@@ -1704,6 +1728,58 @@ int gdf_process_frame(gdf_engine* e, const gdf_frame_params* p, gdf_frame_result
             res.num_voxelized = p->enable_voxel_filter ? e->sl().h_misc[kVoxCount] : 0;
         }
         if (r) *r = res;
+    });
+}
+
+int gdf_next_frame_in_batch(gdf_engine* e) {
+    ENGINE_OR_FAIL(e);
+    return guarded(nullptr, [&] {
+        if (e->cams.empty() || e->cams.back().frame != e->nframes - 1)
+            fail(GDF_ERR_STATE, "the current frame of the batch has no depth map");
+        if (e->nframes >= (uint32_t)kMaxCams) fail(GDF_ERR_ARG, "at most 16 frames per batch");
+        e->nframes++;
+    });
+}
+
+int gdf_get_batch_ranges(gdf_engine* e, uint32_t* point_start, uint32_t* voxel_start,
+                         uint32_t capacity, uint32_t* out_frames) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        Slot& q = e->sl();
+        if (!q.compacted) fail(GDF_ERR_STATE, "no frame has run");
+        const uint32_t nf = q.nframes;
+        if (out_frames) *out_frames = nf;
+        if ((point_start || voxel_start) && capacity < nf + 1)
+            fail(GDF_ERR_CAPACITY, "batch ranges: need nframes + 1 entries");
+        e->read_misc();  // (synchronises the frame)
+        if (nf == 1) {
+            if (point_start) { point_start[0] = 0; point_start[1] = q.h_misc[kCount]; }
+            if (voxel_start) { voxel_start[0] = 0; voxel_start[1] = q.vox_valid ? q.h_misc[kVoxCount] : 0; }
+            return;
+        }
+        if (point_start)
+            HIPCHK(hipMemcpy(point_start, q.d_fstart.p, (nf + 1) * 4, hipMemcpyDeviceToHost));
+        if (voxel_start) {
+            if (q.vox_valid)
+                HIPCHK(hipMemcpy(voxel_start, q.d_fvox.p, (nf + 1) * 4, hipMemcpyDeviceToHost));
+            else
+                std::memset(voxel_start, 0, (nf + 1) * 4);
+        }
+    });
+}
+
+int gdf_download_batch_occupancy_grid(gdf_engine* e, uint32_t frame, uint8_t* out, uint64_t cap) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        Slot& q = e->sl();
+        if (!e->grid_set || !e->invoked_once) fail(GDF_ERR_STATE, "no voxelOccupancyGrid has run");
+        if (frame >= q.nframes) fail(GDF_ERR_ARG, "frame outside the batch");
+        if (!out || cap < e->ncells) fail(GDF_ERR_CAPACITY, "occupancy grid: buffer too small");
+        sync_all(e);
+        e->sync();
+        const uint8_t* src = frame + 1 == q.nframes ? grid_out_ptr(e)
+                                                    : q.d_snap.as<uint8_t>() + (size_t)frame * ((e->ncells + 31) / 32 * 32);
+        HIPCHK(hipMemcpy(out, src, e->ncells, hipMemcpyDeviceToHost));
     });
 }
 

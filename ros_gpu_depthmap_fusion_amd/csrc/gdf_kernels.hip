@@ -321,6 +321,10 @@ struct Nb {
 __device__ __forceinline__ Nb nb_load(const CamDesc* cams, int ncams, int k, int64_t gi) {
     int j = (gi >= cams[k].off && gi < cams[k].off + (int64_t)cams[k].n) ? k
                                                                           : find_cam(cams, ncams, gi);
+    // a batch of frames shares one index space: a camera's linear-index reads past its frame's
+    // first camera find the previous frame's last camera, which the reference (one frame per
+    // buffer) never sees - canonicalised as out of bounds like camera 0's
+    if (j >= 0 && cams[j].frame != cams[k].frame) j = -1;
     Nb r;
     r.d = 0;
     r.xn = r.yn = 0.0f;
@@ -833,8 +837,9 @@ __global__ __launch_bounds__(1024) void k_scan_counts(const uint32_t* __restrict
 // runs of equal keys among the valid lanes - the first lane of a run marks / counts
 constexpr int kMarkCacheBits = 9;
 
-__device__ __forceinline__ void mark_and_count(const FrameArgs& a, bool valid, uint32_t key,
-                                               uint32_t* s_hist, uint32_t* s_mark) {
+__device__ __forceinline__ void mark_and_count(const FrameArgs& a, uint32_t* marks, bool valid,
+                                               uint32_t key, uint32_t hkey, uint32_t* s_hist,
+                                               uint32_t* s_mark) {
     const int lane = threadIdx.x & 63;
     const unsigned long long ltm = lanemask_lt();
     const unsigned long long vm = __ballot(valid);
@@ -848,9 +853,9 @@ __device__ __forceinline__ void mark_and_count(const FrameArgs& a, bool valid, u
         // direct-mapped cache of marked keys (a lane only skips a key some lane wrote AFTER
         // issuing its atomic; collisions just mark again)
         uint32_t& slot = s_mark[(key * 0x9E3779B1u) >> (32 - kMarkCacheBits)];
-        if (a.marks && slot != key) {
+        if (marks && slot != key) {
             slot = key;
-            __hip_atomic_fetch_or(G(a.marks + (key >> 5)), 1u << (key & 31u), __ATOMIC_RELAXED,
+            __hip_atomic_fetch_or(G(marks + (key >> 5)), 1u << (key & 31u), __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT);
         }
         if (a.key_hist) {
@@ -859,7 +864,7 @@ __device__ __forceinline__ void mark_and_count(const FrameArgs& a, bool valid, u
                 after ? ((1ull << (__ffsll((long long)after) - 1)) - 1ull) : ~0ull;
             const uint32_t rl = (uint32_t)__popcll(vm & ~ltm & upto);
             for (uint32_t p = 0; p < a.npasses; ++p)
-                atomicAdd(&s_hist[p * 256 + ((key >> (8 * p)) & 0xFFu)], rl);
+                atomicAdd(&s_hist[p * 256 + ((hkey >> (8 * p)) & 0xFFu)], rl);
         }
     }
 }
@@ -940,6 +945,13 @@ __global__ __launch_bounds__(1024) void k_emit(FrameArgs a) {
     uint32_t tot;
     const uint32_t wpre = wave_prefix(a, s, tot);
     if (a.fused_prefix && s == gridDim.x - 1 && threadIdx.x == 0) *G(a.out_count) = base + tot;
+    const uint32_t fr = cams[k].frame;
+    if (a.frame_pt_start && threadIdx.x == 0) {  // point range of each frame of a batch
+        const bool first_of_frame =
+            s == cams[k].seg0 && (k == 0 || !cams[k - 1].emit || cams[k - 1].frame != fr);
+        if (first_of_frame) G(a.frame_pt_start)[fr] = base;
+        if (s == gridDim.x - 1) G(a.frame_pt_start)[a.nframes] = base + tot;
+    }
     const unsigned long long ltm = lanemask_lt();
     uint32_t key = 0xFFFFFFFFu;
     if (valid) {
@@ -957,7 +969,9 @@ __global__ __launch_bounds__(1024) void k_emit(FrameArgs a) {
             G(a.out_coords)[pos] = key;
         }
     }
-    if (a.do_voxel) mark_and_count(a, valid, key, s_hist, s_mark);
+    if (a.do_voxel)
+        mark_and_count(a, a.marks ? a.marks + (size_t)fr * a.mark_words : nullptr, valid, key,
+                       key | (fr << a.frame_shift), s_hist, s_mark);
     flush_hist(a, s_hist);
 }
 
@@ -1084,7 +1098,7 @@ __global__ __launch_bounds__(1024) void k_sel(FrameArgs a) {
                 G(a.sel_keys)[pos] = key;
             }
         }
-        if (a.do_voxel && a.marks) mark_and_count(a, valid, key, nullptr, s_mark);
+        if (a.do_voxel && a.marks) mark_and_count(a, a.marks, valid, key, key, nullptr, s_mark);
     }
 }
 
@@ -1357,6 +1371,40 @@ __device__ __forceinline__ void grid_u8_part(uint4* __restrict__ grid, uint32_t*
     }
 }
 
+// the grid updates of a batch of `nframes` frames, frame f's marks at marks + f * mark_words,
+// applied in frame order in registers (blocks [0, nblocks) of a launch); the grid after frame
+// f < nframes - 1 is also stored at snap + f * snap_stride (the per-frame u8 grid the reference
+// downloads every frame), the last one is the grid itself.  Marks are cleared.
+__device__ __forceinline__ void grid_u8_part_frames(uint4* __restrict__ grid,
+                                                    uint32_t* __restrict__ marks, uint64_t nwords,
+                                                    uint32_t L, uint32_t block, uint32_t nblocks,
+                                                    uint32_t nframes, uint64_t mark_words,
+                                                    uint4* __restrict__ snap,
+                                                    uint64_t snap_stride) {
+    for (uint64_t i = block * (uint64_t)blockDim.x + threadIdx.x; i < nwords;
+         i += (uint64_t)nblocks * blockDim.x) {
+        uint4 v0 = grid[2 * i], v1 = grid[2 * i + 1];
+        for (uint32_t f = 0; f < nframes; ++f) {
+            const uint32_t m = marks[f * mark_words + i];
+            v0.x = grid_word(v0.x, m, L);
+            v0.y = grid_word(v0.y, m >> 4, L);
+            v0.z = grid_word(v0.z, m >> 8, L);
+            v0.w = grid_word(v0.w, m >> 12, L);
+            v1.x = grid_word(v1.x, m >> 16, L);
+            v1.y = grid_word(v1.y, m >> 20, L);
+            v1.z = grid_word(v1.z, m >> 24, L);
+            v1.w = grid_word(v1.w, m >> 28, L);
+            if (m) marks[f * mark_words + i] = 0u;
+            if (f + 1 < nframes) {
+                snap[f * snap_stride + 2 * i] = v0;
+                snap[f * snap_stride + 2 * i + 1] = v1;
+            }
+        }
+        grid[2 * i] = v0;
+        grid[2 * i + 1] = v1;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_grid_u8(uint4* __restrict__ grid,
                                                  uint32_t* __restrict__ marks, uint64_t nwords,
                                                  uint32_t L, GridSeq q) {
@@ -1512,11 +1560,29 @@ hipError_t launch_scatter(const uint32_t* coords, const uint32_t* count, uint32_
 // them: large frames).  Keys of neighbouring points repeat, so each wave adds run lengths: the
 // first lane of a run of equal digits adds the run (few LDS atomics on hot bins); each thread
 // keeps 4 chunk loads in flight.
+// frame of compacted point `idx` in a batch: the number of frame starts (after frame 0) <= idx
+__device__ __forceinline__ uint32_t frame_of(const uint32_t* s_fstart, uint32_t nframes,
+                                             uint32_t idx) {
+    uint32_t f = 0;
+    for (uint32_t j = 1; j < nframes; ++j) f += idx >= s_fstart[j] ? 1u : 0u;
+    return f;
+}
+
+__device__ __forceinline__ void load_fstart(uint32_t* s_fstart, const uint32_t* fstart,
+                                            uint32_t nframes) {
+    if (nframes > 1)
+        for (uint32_t j = threadIdx.x; j <= nframes; j += blockDim.x) s_fstart[j] = fstart[j];
+}
+
 __global__ __launch_bounds__(256) void k_sort_hist(const uint32_t* __restrict__ keys,
                                                    const uint32_t* __restrict__ count,
-                                                   uint32_t npasses, uint32_t* __restrict__ hist) {
+                                                   uint32_t npasses, uint32_t* __restrict__ hist,
+                                                   uint32_t nframes, uint32_t fshift,
+                                                   const uint32_t* __restrict__ fstart) {
     __shared__ uint32_t s_h[4 * 256];
+    __shared__ uint32_t s_fstart[kMaxCams + 1];
     for (uint32_t i = threadIdx.x; i < 4 * 256; i += 256) s_h[i] = 0;
+    load_fstart(s_fstart, fstart, nframes);
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const uint32_t n = *count;
@@ -1527,6 +1593,7 @@ __global__ __launch_bounds__(256) void k_sort_hist(const uint32_t* __restrict__ 
         for (int q = 0; q < 4; ++q) {
             const uint32_t i = base + q * stride + threadIdx.x;
             k[q] = i < n ? keys[i] : 0u;
+            if (nframes > 1 && i < n) k[q] |= frame_of(s_fstart, nframes, i) << fshift;
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -1578,15 +1645,21 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
     const uint32_t* __restrict__ ghist, unsigned long long* status, unsigned long long* gstatus,
     uint32_t* tile_ctr, uint32_t* epoch_word, uint32_t* err, uint32_t shift, uint32_t dbits,
     uint32_t grid_block0, uint4* grid, uint32_t* marks, uint64_t grid_nwords, uint32_t lifetime,
-    GridSeq q) {
+    GridSeq q, uint32_t nframes, uint32_t fshift, const uint32_t* __restrict__ fstart,
+    uint64_t mark_words, uint4* snap, uint64_t snap_stride) {
     constexpr int kTile = kSortThreads * PT;
     if (blockIdx.x >= grid_block0) {  // fused historic-grid update (first pass only)
         const uint32_t f = grid_seq_enter(q);
-        grid_u8_part(grid, marks, grid_nwords, lifetime, blockIdx.x - grid_block0,
-                     gridDim.x - grid_block0);
+        if (nframes > 1)
+            grid_u8_part_frames(grid, marks, grid_nwords, lifetime, blockIdx.x - grid_block0,
+                                gridDim.x - grid_block0, nframes, mark_words, snap, snap_stride);
+        else
+            grid_u8_part(grid, marks, grid_nwords, lifetime, blockIdx.x - grid_block0,
+                         gridDim.x - grid_block0);
         grid_seq_leave(q, f, gridDim.x - grid_block0);
         return;
     }
+    __shared__ uint32_t s_fstart[kMaxCams + 1];
     __shared__ uint32_t s_cnt[4][256];
     __shared__ uint32_t s_base[256];
     __shared__ uint32_t s_excl[256];
@@ -1599,6 +1672,9 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
     const Tickets tk = tickets(ntiles, grid_block0);
     if (blockIdx.x >= tk.nblk) return;
     if (threadIdx.x == 0) s_epoch = read_epoch(epoch_word);
+    // first pass of a batch: the frame index joins the key above its voxel bits
+    const bool add_frame = nframes > 1 && vin == nullptr;
+    if (add_frame) load_fstart(s_fstart, fstart, nframes);
     // the digit bases do not depend on the tile
     s_base[threadIdx.x] = digit_base(ghist, s_wave);
     for (bool first = true;; first = false) {  // persistent: tiles in ticket order
@@ -1617,6 +1693,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
             const bool ok = idx < n;
             key[j] = ok ? kin[idx] : 0xFFFFFFFFu;
             val[j] = ok ? (vin ? vin[idx] : idx) : 0u;
+            if (add_frame && ok) key[j] |= frame_of(s_fstart, nframes, idx) << fshift;
         }
 #pragma unroll
         for (int j = 0; j < PT; ++j) {
@@ -1715,7 +1792,8 @@ __global__ __launch_bounds__(kGroupThreads) __attribute__((amdgpu_waves_per_eu(8
     uint32_t* __restrict__ out_count, unsigned long long* status, unsigned long long* gstatus,
     uint32_t* tile_ctr, uint32_t* epoch_word, uint32_t* err, uint32_t* hist, int average,
     VoxelParams vp, uint32_t* marks, const uint32_t* tile_base, uint4* __restrict__ bigq,
-    uint32_t* __restrict__ bigcnt, uint32_t bigcap) {
+    uint32_t* __restrict__ bigcnt, uint32_t bigcap, uint32_t nframes, uint32_t fshift,
+    uint32_t* __restrict__ fvox) {
     __shared__ uint32_t s_wave[4];
     __shared__ uint32_t s_tile, s_epoch, s_excl, s_nbig, s_nq;
     __shared__ uint32_t s_start[kGroupThreads + 1];
@@ -1725,9 +1803,13 @@ __global__ __launch_bounds__(kGroupThreads) __attribute__((amdgpu_waves_per_eu(8
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t n = *count;
     const uint32_t ntiles = (n + kGroupThreads - 1) / kGroupThreads;
+    // a batch's keys carry the frame above bit fshift: kmask strips it
+    const uint32_t kmask = nframes > 1 ? (1u << fshift) - 1u : 0xFFFFFFFFu;
     if (blockIdx.x == 0) {
         for (uint32_t i = threadIdx.x; i < kHistWords; i += kGroupThreads) hist[i] = 0;
         if (ntiles == 0 && threadIdx.x == 0) *out_count = 0;  // n == 0
+        if (ntiles == 0 && fvox)
+            for (uint32_t f = threadIdx.x; f <= nframes; f += kGroupThreads) fvox[f] = 0;
     }
     // tile_base (large frames): the group-id offset of every tile is known (k_group_count + scan),
     // so blocks walk the tiles by index with no ticket and no look-back; otherwise tickets +
@@ -1784,7 +1866,12 @@ __global__ __launch_bounds__(kGroupThreads) __attribute__((amdgpu_waves_per_eu(8
                                       : lookback2_wave(status, gstatus, tile, ntiles, total, epoch, err);
         if (lane == 0) {
             s_excl = ex;
-            if (tile == ntiles - 1) *out_count = ex + total;
+            if (tile == ntiles - 1) {
+                *out_count = ex + total;
+                if (fvox)  // frames after the last point's frame start at the end
+                    for (uint32_t f = (keys[n - 1] >> fshift) + 1; f <= nframes; ++f)
+                        fvox[f] = ex + total;
+            }
         }
     } else if (wid == 1 && total) {
         // end of the tile's last group = first index >= tend whose (sorted) key exceeds the
@@ -1824,12 +1911,17 @@ __global__ __launch_bounds__(kGroupThreads) __attribute__((amdgpu_waves_per_eu(8
         const uint32_t s = s_start[threadIdx.x], e = s_start[threadIdx.x + 1];
         float* o = out + 4 * (size_t)g;
         if (marks) {  // voxel_grid_occupancy_of_points: one mark per occupied voxel
-            const uint32_t key = keys[s];
+            const uint32_t key = keys[s] & kmask;
             atomicOr(marks + (key >> 5), 1u << (key & 31u));
+        }
+        if (fvox) {  // a batch: the first voxel of each frame (frames without points share it)
+            const uint32_t fc = keys[s] >> fshift;
+            const uint32_t f0 = s == 0 ? 0u : (keys[s - 1] >> fshift) + 1u;
+            for (uint32_t f = f0; f <= fc; ++f) fvox[f] = g;
         }
         if (!average) {
             float c[4];
-            group_corner(keys[s], vp, c);
+            group_corner(keys[s] & kmask, vp, c);
             *reinterpret_cast<float4*>(o) = make_float4(c[0], c[1], c[2], c[3]);
         } else if (e - S0 <= staged && e - s <= (uint32_t)kSmallGroup) {
             float ax = 0.f, ay = 0.f, az = 0.f, aw = 0.f;
@@ -2020,7 +2112,9 @@ static void launch_sort_pass(uint32_t tiles, hipStream_t s, const uint32_t* kin,
                        vout, a.count, a.hist + 256 * p, a.status, a.sgstatus,
                        reinterpret_cast<uint32_t*>(a.ctrs + kCtrSort0 + p),
                        reinterpret_cast<uint32_t*>(a.ctrs + kCtrEpoch), a.err, 8 * p, dbits, tiles,
-                       reinterpret_cast<uint4*>(a.grid8), a.marks, nwords, a.lifetime, a.gseq);
+                       reinterpret_cast<uint4*>(a.grid8), a.marks, nwords, a.lifetime, a.gseq,
+                       a.nframes, a.frame_shift, a.frame_pt_start, a.mark_words,
+                       reinterpret_cast<uint4*>(a.snapshots), a.snapshot_bytes / 16);
 }
 
 hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hook) {
@@ -2033,7 +2127,8 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
     if (!a.hist_ready) {
         unsigned hb = grid_blocks(a.nmax, 256 * 4);
         if (hb > 512) hb = 512;
-        hipLaunchKernelGGL(k_sort_hist, dim3(hb), dim3(256), 0, s, a.keys, a.count, npasses, a.hist);
+        hipLaunchKernelGGL(k_sort_hist, dim3(hb), dim3(256), 0, s, a.keys, a.count, npasses, a.hist,
+                           a.nframes, a.frame_shift, a.frame_pt_start);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     const uint32_t* kin = a.keys;
@@ -2084,7 +2179,7 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
                        a.gstatus, a.ggstatus, reinterpret_cast<uint32_t*>(a.ctrs + kCtrGroup),
                        reinterpret_cast<uint32_t*>(a.ctrs + kCtrEpoch), a.err, a.hist, a.average,
                        a.vp, a.group_marks, tile_base, tile_base ? a.bigq : nullptr,
-                       a.bigcnt, bigcap);
+                       a.bigcnt, bigcap, a.nframes, a.frame_shift, a.frame_vox_start);
     if (tile_base && a.bigq && a.average) {
         if ((e = hipGetLastError()) != hipSuccess) return e;
         hipLaunchKernelGGL(k_group_big, dim3(2048), dim3(256), 0, s, vin, a.pts,

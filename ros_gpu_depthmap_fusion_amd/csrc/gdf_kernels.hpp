@@ -93,6 +93,17 @@ struct VoxelizeArgs {
     uint4* bigq;                    // [group blocks * tiles per block] long voxels (large frames)
     uint32_t* bigcnt;               // [group blocks] queued per block
     GridSeq gseq;                   // engine order of the fused grid update (frame pipelining)
+    // multi-frame batch: keys of frame f (points [frame_pt_start[f], frame_pt_start[f+1])) sort
+    // as key | f << frame_shift; k_group writes the first voxel of each frame (frame_vox_start,
+    // nframes + 1 entries); the grid update applies the frames' marks (stride mark_words) in
+    // order and stores the grid after each frame but the last at snapshots + f * snapshot_bytes
+    uint32_t nframes;
+    uint32_t frame_shift;
+    const uint32_t* frame_pt_start;
+    uint32_t* frame_vox_start;
+    uint64_t mark_words;
+    uint8_t* snapshots;
+    uint64_t snapshot_bytes;
     uint64_t ncells;
     uint32_t lifetime;
     uint32_t* err;

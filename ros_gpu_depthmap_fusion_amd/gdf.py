@@ -100,7 +100,8 @@ EXPORTED = [
     "gdf_set_profiling", "gdf_get_kernel_times", "gdf_set_debug", "gdf_debug_stage_masks", "gdf_debug_rollbuffer",
     "gdf_debug_historic_grid",
     # include/gdf_driver.h: the component's depth loop in C++ over the C-ABI
-    "gdf_run_depth_stream", "gdf_run_host_stream",
+    "gdf_run_depth_stream", "gdf_run_host_stream", "gdf_run_depth_stream_batched",
+    "gdf_next_frame_in_batch", "gdf_get_batch_ranges", "gdf_download_batch_occupancy_grid",
 ]
 
 
@@ -170,6 +171,11 @@ def load_library(path: str = LIB_PATH):
         "gdf_debug_historic_grid": (i32, [vp, vp, u64]),
         "gdf_run_depth_stream": (i32, [vp, P(StreamCamera), u32, P(FrameParams), u64, u64]),
         "gdf_run_host_stream": (i32, [vp, P(StreamCamera), u32, P(FrameParams), u64, u64]),
+        "gdf_run_depth_stream_batched": (i32, [vp, P(StreamCamera), u32, P(FrameParams), u64,
+                                               u64, u32, i32]),
+        "gdf_next_frame_in_batch": (i32, [vp]),
+        "gdf_get_batch_ranges": (i32, [vp, vp, vp, u32, P(u32)]),
+        "gdf_download_batch_occupancy_grid": (i32, [vp, u32, vp, u64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -550,12 +556,41 @@ class GPUDepthmapFusion:
 
     def run_host_stream(self, cameras: Sequence[StreamCamera], p: FrameParams, first: int,
                         count: int):
-        """gdf_run_host_stream: the same loop with HOST depth maps (pinned: copied in place on the
-        slot's stream; pageable: through the slot's pinned staging), H2D overlapped with the
-        frames in flight."""
+        """gdf_run_host_stream: the same loop with HOST depth maps (copied through the slot's
+        pinned staging, H2D on the slot's stream, overlapped with the frames in flight)."""
         arr = (StreamCamera * len(cameras))(*cameras)
         self._check(self._lib.gdf_run_host_stream(self._h, arr, len(cameras), C.byref(p),
                                                   first, count))
+
+    def run_depth_stream_batched(self, cameras: Sequence[StreamCamera], p: FrameParams,
+                                 first: int, batches: int, batch: int, host: bool = False):
+        """gdf_run_depth_stream_batched: `batches` multi-frame batches of `batch` frames."""
+        arr = (StreamCamera * len(cameras))(*cameras)
+        self._check(self._lib.gdf_run_depth_stream_batched(self._h, arr, len(cameras), C.byref(p),
+                                                           first, batches, batch,
+                                                           1 if host else 0))
+
+    # ---- multi-frame batches ----
+    def nextFrameInBatch(self):
+        """The depth maps added from now on belong to the next frame of this batch."""
+        self._check(self._lib.gdf_next_frame_in_batch(self._h))
+
+    def batch_ranges(self):
+        """(point_start, voxel_start) arrays of nframes + 1 entries of the last batch."""
+        nf = C.c_uint32()
+        self._check(self._lib.gdf_get_batch_ranges(self._h, None, None, 0, C.byref(nf)))
+        ps = np.zeros(nf.value + 1, np.uint32)
+        vs = np.zeros(nf.value + 1, np.uint32)
+        self._check(self._lib.gdf_get_batch_ranges(self._h, _ptr(ps), _ptr(vs), nf.value + 1,
+                                                   C.byref(nf)))
+        return ps, vs
+
+    def downloadBatchVoxelOccupancyGrid(self, frame: int) -> np.ndarray:
+        _, nc = self.grid_size()
+        out = np.empty(max(nc, 1), np.uint8)
+        self._check(self._lib.gdf_download_batch_occupancy_grid(self._h, frame, _ptr(out),
+                                                                out.shape[0]))
+        return out[:nc]
 
     def processFramePrepared(self, p: FrameParams) -> FrameResult:
         """processFrame with parameters already converted by ComponentParams.to_c (a stream of

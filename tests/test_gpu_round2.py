@@ -15,6 +15,8 @@ from ros_gpu_depthmap_fusion_amd.gdf import ComponentParams
 
 pytestmark = pytest.mark.gpu
 
+EYE = np.eye(4, dtype=np.float32)
+
 
 @pytest.fixture(scope="module")
 def Engine(gpu_engine_factory):
@@ -234,3 +236,80 @@ def test_c3_full_window_properties(Engine):
     nd = orc.point_count()
     pts = gpu.downloadPoints()
     assert np.array_equal(bits(pts[:nd]), bits(orc.downloadPoints()))
+
+
+def _batch(gpu, frames_args, p, **kw):
+    gpu.clear()
+    for j, args in enumerate(frames_args):
+        if j:
+            gpu.nextFrameInBatch()
+        for a in args:
+            gpu.addDepthmap(*a)
+    return gpu.processFrame(p, **kw)
+
+
+@pytest.mark.parametrize("case", ["vga_b4", "two_cams_b3_codedefaults", "corners_b2_depth3"])
+def test_batched_frames_equal_frame_by_frame(Engine, case):
+    """Multi-frame batches (gdf_next_frame_in_batch): every frame's points, keys, voxel means and
+    the grid after every frame equal the oracle processing the frames one by one - incl. two
+    cameras per frame (cross-camera reads stay inside the frame), code defaults (F=1, rot45,
+    lifetime 1), voxel corners, and batches pipelined over 3 slots."""
+    if case == "vga_b4":
+        p, W, H, ncam, B, nb, depth = ComponentParams(), 640, 480, 1, 4, 3, 1
+    elif case == "two_cams_b3_codedefaults":
+        p = ComponentParams.code_defaults()
+        p.crop_min, p.crop_max = (-3, -3, -1), (6, 3, 2.5)
+        p.voxel_min, p.voxel_max = (-3, -3, -1), (6, 3, 2.5)
+        W, H, ncam, B, nb, depth = 200, 150, 2, 3, 3, 1
+    else:
+        p = ComponentParams()
+        p.voxel_average = False
+        W, H, ncam, B, nb, depth = 160, 120, 1, 2, 5, 3
+    cams = [synth.make_camera(k, W, H) for k in range(ncam)]
+    gpu, orc = Engine(), OracleFusion(threads=8)
+    gpu.set_pipeline_depth(depth)
+    f = 0
+    for b in range(nb):
+        frames = [[cam_args(c, synth.dense_frame(c, k, f + j)) for k, c in enumerate(cams)]
+                  for j in range(B)]
+        r = _batch(gpu, frames, p)
+        pts, keys, vox = gpu.downloadPoints(), gpu.downloadVoxelCoords(), gpu.downloadVoxelizedPoints()
+        ps, vs = gpu.batch_ranges()
+        assert len(ps) == B + 1 and ps[-1] == len(pts) == r.num_points and vs[-1] == len(vox)
+        for j in range(B):
+            run_fused(orc, frames[j], p)
+            tag = f"batch {b} frame {j}"
+            po = orc.downloadPoints()
+            assert ps[j + 1] - ps[j] == len(po), tag
+            assert np.array_equal(bits(pts[ps[j]:ps[j + 1]]), bits(po)), tag
+            np.testing.assert_array_equal(keys[ps[j]:ps[j + 1]], orc.downloadVoxelCoords(), tag)
+            vo = orc.downloadVoxelizedPoints()
+            assert vs[j + 1] - vs[j] == len(vo), tag
+            assert np.array_equal(bits(vox[vs[j]:vs[j + 1], :3]), bits(vo[:, :3])), tag
+            np.testing.assert_array_equal(gpu.downloadBatchVoxelOccupancyGrid(j),
+                                          orc.downloadVoxelOccupancyGrid(), tag)
+        np.testing.assert_array_equal(gpu.historic_grid(), orc.historic_grid())
+        f += B
+
+
+def test_batch_errors_fail_loudly(Engine):
+    """A batch frame without a depth map, point sequences in a batch, lifetime > 255."""
+    from ros_gpu_depthmap_fusion_amd.gdf import GDFError
+    p = ComponentParams()
+    cam = synth.make_camera(0, 64, 48)
+    gpu = Engine()
+    gpu.clear()
+    with pytest.raises(GDFError):
+        gpu.nextFrameInBatch()  # frame 0 has no depth map yet
+    gpu.addDepthmap(*cam_args(cam, synth.dense_frame(cam, 0, 0)))
+    gpu.nextFrameInBatch()
+    with pytest.raises(GDFError):
+        gpu.processFrame(p)  # frame 1 has no depth map
+    gpu.addDepthmap(*cam_args(cam, synth.dense_frame(cam, 0, 1)))
+    q = ComponentParams()
+    q.occupancy_lifetime = 300
+    with pytest.raises(GDFError):
+        gpu.processFrame(q)
+    gpu.addPointSequence(synth.back_project(cam, synth.dense_frame(cam, 0, 2)), 1000, 0, EYE)
+    with pytest.raises(GDFError):
+        gpu.processFrame(p)
