@@ -223,6 +223,20 @@ int gdf_get_device_results(gdf_engine* engine, const float** points, const uint3
 int gdf_process_frame(gdf_engine* engine, const gdf_frame_params* params,
                       gdf_frame_result* out_result);
 
+/* ---- orphan shaders of the reference (device buffers, the engine's stream) ------------------ */
+/* mask_dilate (shader/mask_dilate.glsl:40-67; never dispatched by the reference): for every pixel
+ * of a width x height u32 mask, a zero in the (2F+1)^2 window clipped to the image writes 0;
+ * as_written != 0 reproduces line 67 (the other pixels are written 0 too), as_written == 0 is the
+ * intended erosion (they keep their value).  F <= 16; in and out must not alias. */
+int gdf_mask_dilate(gdf_engine* engine, const uint32_t* in_mask_device, uint32_t* out_mask_device,
+                    uint32_t width, uint32_t height, uint32_t filter_size, int as_written);
+/* transform_points (shader/transform_points.glsl:37-54; orphan sibling of the indirect form the
+ * rollbuffer uses): out[i] = T * in[i] for i < num_items with mask[i] != 0 (float4 points,
+ * T row-major); other outputs are left unwritten. */
+int gdf_transform_points(gdf_engine* engine, const float* in_points_device,
+                         const uint32_t* mask_device, float* out_points_device, uint32_t num_items,
+                         const float T[16]);
+
 /* ---- multi-frame batches ------------------------------------------------------------------- */
 /* Several depth-only frames through ONE launch chain (the per-frame sequence of
  * GPUDepthmapFusionComponent::processDepthmaps, component.cpp:92-300, applied to each frame; a

@@ -841,3 +841,33 @@ uint32_t orc_rollbuffer_b(orc_state* s, const float** pts, const uint32_t** mask
     *nseq = s->hB_s;
     return s->rb_pts;
 }
+
+/* ---- orphan shaders ------------------------------------------------ */
+/* sh/mask_dilate.glsl:40-67, see gdf_oracle.h.  get_pixel (:33-38): x = mod(idx, width),
+ * y = idx / width; the loops run dx outer, dy inner (:48-66). */
+void orc_mask_dilate(const uint32_t* in_mask, uint32_t* out_mask, uint32_t W, uint32_t H,
+                     uint32_t F, int as_written) {
+    const int64_t f = (int64_t)F;
+    for (uint32_t y = 0; y < H; ++y)
+        for (uint32_t x = 0; x < W; ++x) {
+            const size_t idx = (size_t)y * W + x;
+            uint32_t out = as_written ? 0u : in_mask[idx];
+            for (int64_t dx = -f; dx <= f && out; ++dx) {
+                const uint32_t xx = x + (uint32_t)dx;  /* uint wrap: negative -> >= W */
+                if (xx >= W) continue;
+                for (int64_t dy = -f; dy <= f; ++dy) {
+                    const uint32_t yy = y + (uint32_t)dy;
+                    if (yy >= H) continue;
+                    if (in_mask[(size_t)yy * W + xx] == 0) { out = 0; break; }
+                }
+            }
+            out_mask[idx] = out;
+        }
+}
+
+/* sh/transform_points.glsl:45-53 */
+void orc_transform_points(const float* in, const uint32_t* mask, float* out, uint32_t n,
+                          const float T[16]) {
+    for (uint32_t i = 0; i < n; ++i)
+        if (mask[i] != 0) mat_vec(T, in + 4 * (size_t)i, out + 4 * (size_t)i);
+}

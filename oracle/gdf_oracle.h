@@ -113,6 +113,20 @@ uint32_t orc_rollbuffer_b(orc_state* s, const float** pts, const uint32_t** mask
                           const uint32_t** seq_idx, const uint32_t** headers, uint32_t* nseq);
 
 /* standalone primitives for tests */
+/* sh/mask_dilate.glsl:40-67 (orphan in the reference: never dispatched).  For every pixel of a
+ * width x height mask (u32 per pixel, at in_mask / out_mask):  the (2F+1)^2 window clipped to the
+ * image (the GLSL's `pixel.x + dx < 0` is unsigned arithmetic: never true, but a negative sum
+ * wraps to >= width and is skipped by the second check, so the clip is exact);  a zero in the
+ * window writes 0 and returns (:58-63).  as_written != 0: line 67 writes 0 for the pixels that
+ * pass too (the mask is cleared everywhere); as_written == 0: the intended erosion, the pixel
+ * keeps its input value. */
+void orc_mask_dilate(const uint32_t* in_mask, uint32_t* out_mask, uint32_t width,
+                     uint32_t height, uint32_t filter_size, int as_written);
+/* sh/transform_points.glsl:37-54 (orphan sibling of transform_points_indirect): for i < n with
+ * mask[i] != 0, out[i] = T * in[i] (T row-major, the reference's `point * transform`); other
+ * outputs are left unwritten. */
+void orc_transform_points(const float* in_points, const uint32_t* mask, float* out_points,
+                          uint32_t n, const float T[16]);
 void orc_stable_sort_keys(const uint32_t* keys, uint32_t n, uint32_t* out_sorted_idx,
                           uint32_t* out_sorted_keys);
 

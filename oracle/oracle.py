@@ -88,6 +88,8 @@ def load():
         "orc_rollbuffer_state": (None, [vp, vp]),
         "orc_rollbuffer_b": (u32, [vp, P(vp), P(vp), P(vp), P(vp), P(u32)]),
         "orc_stable_sort_keys": (None, [vp, u32, vp, vp]),
+        "orc_mask_dilate": (None, [vp, vp, u32, u32, u32, i32]),
+        "orc_transform_points": (None, [vp, vp, vp, u32, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -322,6 +324,26 @@ def stable_sort_keys(keys: np.ndarray):
     sk = np.empty(len(k), np.uint32)
     lib.orc_stable_sort_keys(_p(k), len(k), _p(idx), _p(sk))
     return idx, sk
+
+
+def mask_dilate(mask: np.ndarray, filter_size: int, as_written: bool = False) -> np.ndarray:
+    """sh/mask_dilate.glsl:40-67 on an (H, W) u32 mask (see gdf_oracle.h)."""
+    lib = load()
+    m = np.ascontiguousarray(mask, np.uint32)
+    H, W = m.shape
+    out = np.empty_like(m)
+    lib.orc_mask_dilate(_p(m), _p(out), W, H, filter_size, 1 if as_written else 0)
+    return out
+
+
+def transform_points(points: np.ndarray, mask: np.ndarray, T, out: np.ndarray) -> np.ndarray:
+    """sh/transform_points.glsl:37-54: out[i] = T * points[i] where mask[i] != 0 (others kept)."""
+    lib = load()
+    pts = np.ascontiguousarray(points, np.float32)
+    m = np.ascontiguousarray(mask, np.uint32)
+    o = np.ascontiguousarray(out, np.float32).copy()
+    lib.orc_transform_points(_p(pts), _p(m), _p(o), len(pts), _p(_m(T)))
+    return o
 
 
 def ros_time_minus(sec, nsec, seconds):

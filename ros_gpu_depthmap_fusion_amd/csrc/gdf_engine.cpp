@@ -1731,6 +1731,27 @@ int gdf_process_frame(gdf_engine* e, const gdf_frame_params* p, gdf_frame_result
     });
 }
 
+int gdf_mask_dilate(gdf_engine* e, const uint32_t* in, uint32_t* out, uint32_t W, uint32_t H,
+                    uint32_t F, int as_written) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        if ((!in || !out) && (uint64_t)W * H) fail(GDF_ERR_ARG, "mask_dilate: null mask");
+        if (in == out && (uint64_t)W * H) fail(GDF_ERR_ARG, "mask_dilate: in-place is not supported");
+        if (F > kDilateMaxF) fail(GDF_ERR_ARG, "mask_dilate: filter size above 16");
+        HIPCHK(launch_mask_dilate(in, out, W, H, F, as_written, e->s()));
+    });
+}
+
+int gdf_transform_points(gdf_engine* e, const float* in, const uint32_t* mask, float* out,
+                         uint32_t n, const float T[16]) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        if (!T || (n && (!in || !mask || !out))) fail(GDF_ERR_ARG, "transform_points: null argument");
+        HIPCHK(launch_transform_points(reinterpret_cast<const float4*>(in), mask,
+                                       reinterpret_cast<float4*>(out), n, T, e->s()));
+    });
+}
+
 int gdf_next_frame_in_batch(gdf_engine* e) {
     ENGINE_OR_FAIL(e);
     return guarded(nullptr, [&] {

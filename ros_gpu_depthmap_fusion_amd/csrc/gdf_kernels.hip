@@ -2188,6 +2188,79 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
     return hipGetLastError();
 }
 
+// ---- orphan shaders of the reference --------------------------------------
+// mask_dilate (sh/mask_dilate.glsl:40-67): per pixel, a zero anywhere in the (2F+1)^2 window
+// (clipped to the image) writes 0; as written the shader writes 0 for the other pixels too
+// (:67), the intended erosion keeps the pixel's value.  The window AND is separable: a block
+// stages a (16 + 2F) x (64 + 2F) tile of "non-zero" bytes in LDS (outside the image = 1: those
+// neighbours are skipped), ANDs along rows, then along columns - O(F) per pixel, not O(F^2).
+constexpr uint32_t kDilTW = 64, kDilTH = 16;
+
+__global__ __launch_bounds__(256) void k_mask_dilate(const uint32_t* __restrict__ in,
+                                                     uint32_t* __restrict__ out, uint32_t W,
+                                                     uint32_t H, uint32_t F, int as_written) {
+    __shared__ uint8_t s_in[(kDilTH + 2 * kDilateMaxF) * (kDilTW + 2 * kDilateMaxF)];
+    __shared__ uint8_t s_h[(kDilTH + 2 * kDilateMaxF) * kDilTW];
+    const uint32_t x0 = blockIdx.x * kDilTW, y0 = blockIdx.y * kDilTH;
+    const uint32_t cols = kDilTW + 2 * F, rows = kDilTH + 2 * F;
+    for (uint32_t e = threadIdx.x; e < rows * cols; e += blockDim.x) {
+        const uint32_t r = e / cols, c = e - r * cols;
+        const int64_t gx = (int64_t)x0 - F + c, gy = (int64_t)y0 - F + r;
+        uint8_t v = 1;
+        if (gx >= 0 && gx < W && gy >= 0 && gy < H) v = in[(size_t)gy * W + gx] != 0u;
+        s_in[e] = v;
+    }
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < rows * kDilTW; e += blockDim.x) {
+        const uint32_t r = e / kDilTW, c = e - r * kDilTW;
+        const uint8_t* row = s_in + r * cols + c;
+        uint8_t a = 1;
+        for (uint32_t k = 0; k <= 2 * F; ++k) a &= row[k];
+        s_h[e] = a;
+    }
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < kDilTH * kDilTW; e += blockDim.x) {
+        const uint32_t ty = e / kDilTW, tx = e - ty * kDilTW;
+        const uint32_t x = x0 + tx, y = y0 + ty;
+        if (x >= W || y >= H) continue;
+        uint8_t a = 1;
+        for (uint32_t k = 0; k <= 2 * F; ++k) a &= s_h[(ty + k) * kDilTW + tx];
+        const size_t idx = (size_t)y * W + x;
+        out[idx] = (as_written || !a) ? 0u : in[idx];
+    }
+}
+
+hipError_t launch_mask_dilate(const uint32_t* in, uint32_t* out, uint32_t W, uint32_t H,
+                              uint32_t F, int as_written, hipStream_t s) {
+    if (W == 0 || H == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mask_dilate, dim3((W + kDilTW - 1) / kDilTW, (H + kDilTH - 1) / kDilTH),
+                       dim3(256), 0, s, in, out, W, H, F, as_written);
+    return hipGetLastError();
+}
+
+// transform_points (sh/transform_points.glsl:37-54): out[i] = T * in[i] where mask[i] != 0
+__global__ __launch_bounds__(256) void k_transform_points(const float4* __restrict__ in,
+                                                          const uint32_t* __restrict__ mask,
+                                                          float4* __restrict__ out, uint32_t n,
+                                                          Mat4 T) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        if (mask[i] == 0u) continue;
+        const float4 p = in[i];
+        out[i] = make_float4(mrow(T.m + 0, p.x, p.y, p.z, p.w), mrow(T.m + 4, p.x, p.y, p.z, p.w),
+                             mrow(T.m + 8, p.x, p.y, p.z, p.w), mrow(T.m + 12, p.x, p.y, p.z, p.w));
+    }
+}
+
+hipError_t launch_transform_points(const float4* in, const uint32_t* mask, float4* out, uint32_t n,
+                                   const float* T, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    Mat4 m;
+    for (int i = 0; i < 16; ++i) m.m[i] = T[i];
+    hipLaunchKernelGGL(k_transform_points, dim3(grid_blocks(n, 256)), dim3(256), 0, s, in, mask,
+                       out, n, m);
+    return hipGetLastError();
+}
+
 // ---- multi-GPU occupancy marks -------------------------------------------------------------------
 // The engine's marks already are the exchange format (1 bit per cell): export is a copy, import
 // ORs the all-gathered masks of every rank into them.

@@ -115,6 +115,15 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
 size_t voxelize_status_words(uint32_t nmax);
 size_t voxelize_group_tiles(uint32_t nmax);
 
+// orphan shaders: mask_dilate (F <= kDilateMaxF) and single-matrix transform_points
+hipError_t launch_mask_dilate(const uint32_t* in, uint32_t* out, uint32_t W, uint32_t H,
+                              uint32_t F, int as_written, hipStream_t s);
+struct Mat4 {
+    float m[16];
+};
+hipError_t launch_transform_points(const float4* in, const uint32_t* mask, float4* out, uint32_t n,
+                                   const float* T, hipStream_t s);
+
 // multi-GPU occupancy marks: export = copy of the mark bitmask, import = OR of nranks masks
 hipError_t launch_export_marks(const uint32_t* marks, uint64_t words, uint32_t* bits, hipStream_t s);
 hipError_t launch_take_marks(uint32_t* marks, uint64_t words, uint32_t* bits, hipStream_t s);

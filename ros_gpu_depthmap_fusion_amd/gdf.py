@@ -102,6 +102,7 @@ EXPORTED = [
     # include/gdf_driver.h: the component's depth loop in C++ over the C-ABI
     "gdf_run_depth_stream", "gdf_run_host_stream", "gdf_run_depth_stream_batched",
     "gdf_next_frame_in_batch", "gdf_get_batch_ranges", "gdf_download_batch_occupancy_grid",
+    "gdf_mask_dilate", "gdf_transform_points",
 ]
 
 
@@ -174,6 +175,8 @@ def load_library(path: str = LIB_PATH):
         "gdf_run_depth_stream_batched": (i32, [vp, P(StreamCamera), u32, P(FrameParams), u64,
                                                u64, u32, i32]),
         "gdf_next_frame_in_batch": (i32, [vp]),
+        "gdf_mask_dilate": (i32, [vp, vp, vp, u32, u32, u32, i32]),
+        "gdf_transform_points": (i32, [vp, vp, vp, vp, u32, vp]),
         "gdf_get_batch_ranges": (i32, [vp, vp, vp, u32, P(u32)]),
         "gdf_download_batch_occupancy_grid": (i32, [vp, u32, vp, u64]),
     }
@@ -569,6 +572,21 @@ class GPUDepthmapFusion:
         self._check(self._lib.gdf_run_depth_stream_batched(self._h, arr, len(cameras), C.byref(p),
                                                            first, batches, batch,
                                                            1 if host else 0))
+
+    # ---- orphan shaders (device buffers) ----
+    def maskDilate(self, in_ptr: int, out_ptr: int, width: int, height: int, filter_size: int,
+                   as_written: bool = False):
+        """sh/mask_dilate.glsl on device u32 masks (intended erosion, or as written)."""
+        self._check(self._lib.gdf_mask_dilate(self._h, C.c_void_p(in_ptr), C.c_void_p(out_ptr),
+                                              width, height, filter_size, 1 if as_written else 0))
+
+    def transformPoints(self, in_ptr: int, mask_ptr: int, out_ptr: int, num_items: int,
+                        transform):
+        """sh/transform_points.glsl on device float4 points + u32 mask."""
+        t = _mat(transform)
+        self._check(self._lib.gdf_transform_points(self._h, C.c_void_p(in_ptr),
+                                                   C.c_void_p(mask_ptr), C.c_void_p(out_ptr),
+                                                   num_items, _ptr(t)))
 
     # ---- multi-frame batches ----
     def nextFrameInBatch(self):

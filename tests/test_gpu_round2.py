@@ -313,3 +313,42 @@ def test_batch_errors_fail_loudly(Engine):
     gpu.addPointSequence(synth.back_project(cam, synth.dense_frame(cam, 0, 2)), 1000, 0, EYE)
     with pytest.raises(GDFError):
         gpu.processFrame(p)
+
+
+@pytest.mark.parametrize("W,H", [(1, 1), (37, 23), (640, 480), (1280, 720)])
+def test_mask_dilate_matches_oracle(Engine, W, H):
+    """gdf_mask_dilate (LDS-staged separable window AND) vs the oracle's literal restatement of
+    mask_dilate.glsl:40-67, intended erosion and as written, F = 0..16."""
+    from oracle import mask_dilate
+    rng = np.random.default_rng(W * H)
+    m = ((rng.random((H, W)) < 0.995) * rng.integers(1, 2**32, (H, W), dtype=np.uint64))
+    m = m.astype(np.uint32)
+    gpu = Engine()
+    din = hiprt.DeviceArray.from_numpy(m)
+    dout = hiprt.DeviceArray(m.nbytes)
+    for F in (0, 1, 4, 16):
+        for aw in (False, True):
+            hiprt.check(hiprt.hip().hipMemset(dout.ptr, 0xAB, m.nbytes))
+            gpu.maskDilate(din.ptr, dout.ptr, W, H, F, aw)
+            gpu.synchronize()
+            got = dout.to_numpy(np.uint32, W * H).reshape(H, W)
+            np.testing.assert_array_equal(got, mask_dilate(m, F, aw), f"F={F} as_written={aw}")
+
+
+def test_transform_points_matches_oracle(Engine):
+    """gdf_transform_points vs transform_points.glsl restated: bit-exact where mask != 0,
+    untouched elsewhere."""
+    from oracle import transform_points
+    rng = np.random.default_rng(5)
+    n = 300_001
+    pts = (rng.standard_normal((n, 4)) * 7).astype(np.float32)
+    mask = (rng.random(n) < 0.6).astype(np.uint32) * rng.integers(1, 9, n).astype(np.uint32)
+    T = synth.make_camera(3, 64, 48).T_world
+    init = np.full((n, 4), np.float32(-1.25))
+    gpu = Engine()
+    dp, dm, do = (hiprt.DeviceArray.from_numpy(a) for a in (pts, mask, init))
+    gpu.transformPoints(dp.ptr, dm.ptr, do.ptr, n, T)
+    gpu.synchronize()
+    got = do.to_numpy(np.float32, 4 * n).reshape(n, 4)
+    want = transform_points(pts, mask, T, init)
+    assert np.array_equal(bits(got), bits(want))
