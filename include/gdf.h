@@ -92,6 +92,10 @@ typedef struct gdf_frame_params {
     int32_t synchronous;                /* 1: wait for the frame and fill the host mirrors
                                            (m_points / m_points_voxelized / m_occupancyGrid),
                                            0: enqueue only (results stay on the device)      */
+    int32_t defer_voxelize;             /* 1: compute the voxel keys and occupancy marks but no
+                                           voxelize: the caller exchanges the (point, key) lists
+                                           across ranks and voxelizes them with
+                                           gdf_voxelize_points (multi-GPU fused cloud)        */
 } gdf_frame_params;
 
 /* What gdf_process_frame produced (counts are only valid when synchronous != 0). */
@@ -142,6 +146,16 @@ int gdf_clear(gdf_engine* engine);
 int gdf_add_depthmap(gdf_engine* engine, const uint16_t* depth, uint32_t width, uint32_t height,
                      float depth_scale, float fx, float fy, float cx, float cy,
                      const float T_world[16], const float T_crop[16]);
+/* Multi-GPU (one camera per rank): the camera that precedes this engine's first camera in the
+ * reference's concatenated buffer (rank k-1's camera), of which only the last `tail_pixels`
+ * depth values are given (device memory; >= F rows + F pixels of this engine's first camera).
+ * The flying-pixel reads of the first camera's top rows land there exactly as in the
+ * reference's single buffer; the halo camera emits no points.  Call after
+ * gdf_clear, before the depth maps; borrowed like gdf_add_depthmap_device's pointer. */
+int gdf_add_halo_depthmap_device(gdf_engine* engine, const uint16_t* tail_device,
+                                 uint32_t tail_pixels, uint32_t width, uint32_t height,
+                                 float depth_scale, float fx, float fy, float cx, float cy,
+                                 const float T_world[16], const float T_crop[16]);
 /* Same, for a depth map already resident in device memory of this engine's GPU (no copy). */
 int gdf_add_depthmap_device(gdf_engine* engine, const uint16_t* depth_device, uint32_t width,
                             uint32_t height, float depth_scale, float fx, float fy, float cx,
@@ -295,6 +309,20 @@ int gdf_voxel_occupancy_grid_batch(gdf_engine* engine, const uint32_t* device_bi
                                    uint64_t words, uint32_t num_ranks, uint32_t num_frames,
                                    uint64_t frame_stride_words, uint64_t rank_stride_words,
                                    uint32_t lifetime);
+
+/* Fused voxel cloud across ranks (the reference voxelizes the points of ALL cameras in one
+ * stable sort, fusion.cpp:1743-1756): gdf_partition_points splits the frame's compacted
+ * (point, key) list (gdf_process_frame with defer_voxelize = 1) by voxel-key range - part
+ * p = floor(key * nparts / num_cells) - into part-major send buffers (device, >= the frame's
+ * points), stable inside each part, with part_counts[p] (device, nparts words).  After an
+ * all-to-all (rank r receives part r of every rank, in rank order = camera order) each rank
+ * calls gdf_voxelize_points on what it received: its key range of m_points_voxelized, equal to
+ * the single-engine result over all cameras (gdf_download_voxelized_points). */
+int gdf_partition_points(gdf_engine* engine, uint32_t nparts, float* send_points_device,
+                         uint32_t* send_keys_device, uint32_t capacity,
+                         uint32_t* part_counts_device);
+int gdf_voxelize_points(gdf_engine* engine, const float* points_device,
+                        const uint32_t* keys_device, uint32_t count, int average_voxels);
 
 /* ---- live kernel timing (HIP events on the engine stream) ------------------------------------ */
 enum gdf_kernel_slot {

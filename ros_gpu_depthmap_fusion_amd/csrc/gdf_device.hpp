@@ -30,6 +30,7 @@ constexpr int kGroupThreads = 256;
 constexpr int kSumChunk = 128;                               // points per wave gather chunk
 constexpr uint32_t kSpinLimit = 1u << 26;                   // bounded look-back spins
 constexpr uint32_t kDilateMaxF = 16;                        // mask_dilate window radius limit
+constexpr uint32_t kMaxParts = 16;                          // ranks of the fused-cloud partition
 
 // Device-wide counters: monotonically increasing tile tickets (the host passes each launch's
 // base, so no per-launch memset) and the global digit histogram of the voxel keys.

@@ -177,7 +177,7 @@ bool ros_time_minus(uint32_t sec, uint32_t nsec, double seconds, uint32_t* os, u
 
 enum MiscSlot {
     kCount = 0, kTileCtr = 1, kErr = 2, kVoxCount = 3, kGridTicket = 4, kDepthCount = 5,
-    kSelTotal = 6, kMiscWords = 16
+    kSelTotal = 6, kPartTotal = 7, kRecvCount = 8, kMiscWords = 16
 };
 
 }  // namespace
@@ -218,6 +218,7 @@ struct Slot {
     uint32_t marks_frames = 0;      // frames the zeroed mark buffer covers
     DevBuf d_fstart, d_fvox;        // batch: first point / first voxel of each frame [nframes + 1]
     DevBuf d_snap;                  // batch: the u8 grid after each frame but the last
+    DevBuf d_pcnt, d_poff;          // multi-GPU key-range partition workspace
     uint32_t nframes = 1;           // frames of the slot's last processed batch
     uint32_t n_total = 0;
     // steady-state frame as a HIP graph (the fused frame + voxelize launches of this slot): one
@@ -269,7 +270,9 @@ struct gdf_engine {
     std::vector<Cam> cams;
     uint32_t nframes = 1;           // frames of the batch being assembled (gdf_next_frame_in_batch)
     uint32_t depth_total = 0;
-    std::vector<CamDesc> halo;      // halo cameras (multi-GPU), negative offsets
+    std::vector<CamDesc> halo;      // halo cameras (multi-GPU), negative offsets (built per frame)
+    std::vector<Cam> halo_cams;     // gdf_add_halo_depthmap_device inputs of this frame
+    std::vector<uint32_t> halo_tail;  // pixels present at the end of each halo camera
     std::vector<CamTable> tables = std::vector<CamTable>(kMaxCams);
     std::vector<CamDesc> h_cams;
     uint32_t mask_blocks = 0;       // compaction segments over the emitting cameras
@@ -461,6 +464,8 @@ void engine_clear(gdf_engine* e) {  // fusion.cpp:725-732
     e->rb.selection_sequence_count = 0;
     e->depth_total = 0;
     e->cams.clear();
+    e->halo_cams.clear();
+    e->halo_tail.clear();
     e->depth_uploaded = false;
     e->converted = e->flying_set = e->crop_set = false;
     e->prepared = e->sel_inserted = false;
@@ -769,7 +774,33 @@ void upload_depthmaps(gdf_engine* e) {  // fusion.cpp:1583-1593
         q.h_stage_bytes = host_px * 2;
     }
     size_t staged = 0;
-    if (e->cams.size() + e->halo.size() > (size_t)kMaxCams) fail(GDF_ERR_ARG, "too many cameras (incl. halo)");
+    if (e->cams.size() + e->halo_cams.size() > (size_t)kMaxCams) fail(GDF_ERR_ARG, "too many cameras (incl. halo)");
+    // halo cameras (multi-GPU): the cameras that precede this engine's first one in the
+    // reference's concatenated buffer, at negative offsets; only their last `tail` pixels exist
+    // (a virtual base pointer: the flying-pixel reads reach back at most F rows + F pixels,
+    // checked in frame_args)
+    e->halo.clear();
+    {
+        int64_t hoff = 0;
+        for (size_t j = e->halo_cams.size(); j-- > 0;) hoff -= (int64_t)e->halo_cams[j].n;
+        for (size_t j = 0; j < e->halo_cams.size(); ++j) {
+            const Cam& c = e->halo_cams[j];
+            CamDesc d{};
+            d.off = hoff;
+            d.depth = c.dev - (c.n - e->halo_tail[j]);
+            ensure_table(e, j, c);
+            d.xn = e->tables[j].xn.as<float>();
+            d.yn = e->tables[j].yn.as<float>();
+            d.W = c.W; d.H = c.H; d.n = c.n; d.emit = 0;
+            d.scale = c.scale;
+            d.wmagic = ((1ull << 40) + c.W - 1) / c.W;
+            d.frame = 0;
+            std::memcpy(d.Tw, c.Tw, 64);
+            std::memcpy(d.Tc, c.Tc, 64);
+            e->halo.push_back(d);
+            hoff += c.n;
+        }
+    }
     e->h_cams.clear();
     e->mask_blocks = 0;
     e->max_segw = 0;
@@ -1014,6 +1045,14 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel) {
     }
     e->sl().dbg_count = e->sl().n_total;
     a.err = e->sl().d_misc.as<uint32_t>() + kErr;
+    if (!e->halo_cams.empty() && a.do_flying && !e->cams.empty()) {
+        const uint64_t reach = (uint64_t)a.F * e->cams[0].W + a.F;  // deepest read into the halo
+        if (reach > e->halo_cams[0].n)
+            fail(GDF_ERR_ARG, "halo camera shorter than F rows of the first camera (reads would "
+                              "reach the camera before it)");
+        if (e->halo_tail[0] < reach)
+            fail(GDF_ERR_ARG, "halo depth map tail shorter than F rows + F pixels of the first camera");
+    }
     a.nframes = e->nframes;
     a.frame_shift = e->nframes > 1 ? e->key_bits : 0u;
     a.mark_words = mark_words(e);
@@ -1049,9 +1088,19 @@ void compute_voxel_coords(gdf_engine* e, const float* lo, const float* hi, const
     e->sl().marks_set = false;
 }
 
-VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime) {  // fusion.cpp:1743-1756
-    if (!e->grid_set || !e->sl().coords_valid) fail(GDF_ERR_STATE, "voxelize before computeVoxelCoords");
-    const uint32_t nmax = std::max<uint32_t>(e->sl().n_total, 1);
+// an external (point, key) list to voxelize instead of the frame's compaction (multi-GPU fused
+// cloud: the lists all-to-all'ed by key range)
+struct VoxSource {
+    const float4* pts = nullptr;
+    const uint32_t* keys = nullptr;
+    uint32_t n = 0;
+};
+
+VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime,
+                           const VoxSource* src = nullptr) {  // fusion.cpp:1743-1756
+    if (!e->grid_set || (!src && !e->sl().coords_valid))
+        fail(GDF_ERR_STATE, "voxelize before computeVoxelCoords");
+    const uint32_t nmax = std::max<uint32_t>(src ? src->n : e->sl().n_total, 1);
     if (nmax >= (1u << 31)) fail(GDF_ERR_CAPACITY, "voxelize supports < 2^31 points");
     ensure_misc(e);
     e->sl().d_ka.ensure((size_t)nmax * 4);
@@ -1073,10 +1122,15 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime) 
     v.keys = e->sl().d_coords.as<uint32_t>();
     v.pts = e->sl().d_pts.as<float4>();
     v.count = e->sl().d_misc.as<uint32_t>() + kCount;
+    if (src) {
+        v.keys = src->keys;
+        v.pts = src->pts;
+        v.count = e->sl().d_misc.as<uint32_t>() + kRecvCount;
+    }
     v.nmax = nmax;
     v.key_bits = sort_bits(e);
     v.average = average;
-    v.hist_ready = e->sl().khist_pending ? 1 : 0;
+    v.hist_ready = e->sl().khist_pending && !src ? 1 : 0;
     v.vp = e->vp;
     v.keys_a = e->sl().d_ka.as<uint32_t>();
     v.keys_b = e->sl().d_kb.as<uint32_t>();
@@ -1431,6 +1485,28 @@ int gdf_add_depthmap_device(gdf_engine* e, const uint16_t* depth, uint32_t W, ui
     return guarded(e, [&] { add_depthmap(e, nullptr, depth, W, H, scale, fx, fy, cx, cy, Tw, Tc); });
 }
 
+int gdf_add_halo_depthmap_device(gdf_engine* e, const uint16_t* tail, uint32_t tail_pixels,
+                                 uint32_t W, uint32_t H, float scale, float fx, float fy, float cx,
+                                 float cy, const float Tw[16], const float Tc[16]) {
+    ENGINE_OR_FAIL(e);
+    return guarded(nullptr, [&] {
+        if (!tail || !Tw || !Tc || W == 0 || H == 0 || tail_pixels == 0 ||
+            (uint64_t)tail_pixels > (uint64_t)W * H)
+            fail(GDF_ERR_ARG, "halo depth map: bad argument");
+        if (!e->halo_cams.empty()) fail(GDF_ERR_STATE, "one halo camera per frame");
+        if (!e->cams.empty()) fail(GDF_ERR_STATE, "the halo camera comes before the depth maps");
+        Cam c;
+        c.dev = tail;
+        c.W = W; c.H = H; c.n = W * H;
+        c.scale = scale; c.fx = fx; c.fy = fy; c.cx = cx; c.cy = cy;
+        std::memcpy(c.Tw, Tw, 64);
+        std::memcpy(c.Tc, Tc, 64);
+        e->halo_cams.push_back(c);
+        e->halo_tail.push_back(tail_pixels);
+        e->depth_uploaded = false;
+    });
+}
+
 int gdf_add_point_sequence(gdf_engine* e, const void* rec, uint32_t n, uint32_t step,
                            uint32_t sec, uint32_t nsec, const float Tm[16]) {
     ENGINE_OR_FAIL(e);
@@ -1710,7 +1786,10 @@ int gdf_process_frame(gdf_engine* e, const gdf_frame_params* p, gdf_frame_result
             set_grid(e, p->voxel_min, p->voxel_max, p->voxel_size);
             if (sort_bits(e) > 32) fail(GDF_ERR_ARG, "voxel key + frame index exceed 32 bits");
             widen_if_needed(e, p->occupancy_lifetime, e->s());  // before marks are consumed
-            if (!p->defer_occupancy_grid && e->grid_mode == 0) {
+            if (p->defer_voxelize) {  // keys + marks only (multi-GPU fused cloud)
+                run_frame(e, true);
+                if (!p->defer_occupancy_grid) occupancy_grid(e, p->occupancy_lifetime, e->s());
+            } else if (!p->defer_occupancy_grid && e->grid_mode == 0) {
                 run_fused_frame(e, p->voxel_average, p->occupancy_lifetime);
             } else {
                 run_frame(e, true);
@@ -1725,7 +1804,7 @@ int gdf_process_frame(gdf_engine* e, const gdf_frame_params* p, gdf_frame_result
         if (p->synchronous) {
             e->read_misc();
             res.num_points = e->sl().h_misc[kCount];
-            res.num_voxelized = p->enable_voxel_filter ? e->sl().h_misc[kVoxCount] : 0;
+            res.num_voxelized = p->enable_voxel_filter && !p->defer_voxelize ? e->sl().h_misc[kVoxCount] : 0;
         }
         if (r) *r = res;
     });
@@ -1749,6 +1828,48 @@ int gdf_transform_points(gdf_engine* e, const float* in, const uint32_t* mask, f
         if (!T || (n && (!in || !mask || !out))) fail(GDF_ERR_ARG, "transform_points: null argument");
         HIPCHK(launch_transform_points(reinterpret_cast<const float4*>(in), mask,
                                        reinterpret_cast<float4*>(out), n, T, e->s()));
+    });
+}
+
+int gdf_partition_points(gdf_engine* e, uint32_t nparts, float* send_pts, uint32_t* send_keys,
+                         uint32_t capacity, uint32_t* part_counts) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        Slot& q = e->sl();
+        if (!e->grid_set || !q.coords_valid) fail(GDF_ERR_STATE, "partition needs the voxel keys of a frame");
+        if (nparts == 0 || nparts > kMaxParts) fail(GDF_ERR_ARG, "partition: 1..16 parts");
+        if (!send_pts || !send_keys || !part_counts) fail(GDF_ERR_ARG, "partition: null buffer");
+        if (capacity < q.n_total) fail(GDF_ERR_CAPACITY, "partition: send buffers smaller than the frame");
+        ensure_misc(e);
+        const uint32_t nmax = std::max<uint32_t>(q.n_total, 1);
+        const uint32_t m = nparts * std::max<uint32_t>(part_tiles(nmax), 1u);
+        q.d_pcnt.ensure((size_t)m * 4);
+        q.d_poff.ensure(seg_offsets_words(m) * 4);
+        HIPCHK(launch_partition(q.d_pts.as<float4>(), q.d_coords.as<uint32_t>(),
+                                q.d_misc.as<uint32_t>() + kCount, nmax, nparts, e->ncells,
+                                q.d_pcnt.as<uint32_t>(), q.d_poff.as<uint32_t>(),
+                                q.d_misc.as<uint32_t>() + kPartTotal,
+                                reinterpret_cast<float4*>(send_pts), send_keys, part_counts, e->s()));
+    });
+}
+
+int gdf_voxelize_points(gdf_engine* e, const float* pts, const uint32_t* keys, uint32_t n,
+                        int average) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        if (!e->grid_set) fail(GDF_ERR_STATE, "voxelize_points needs the voxel grid of a frame");
+        if (n && (!pts || !keys)) fail(GDF_ERR_ARG, "voxelize_points: null list");
+        ensure_misc(e);
+        HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(e->sl().d_misc.as<uint32_t>() + kRecvCount),
+                                 (int)n, 1, e->s()));
+        VoxSource src;
+        src.pts = reinterpret_cast<const float4*>(pts);
+        src.keys = keys;
+        src.n = n;
+        const VoxelizeArgs v = voxelize_args(e, average, -1, &src);
+        e->timed(GDF_KERNEL_VOXELIZE, [&] { HIPCHK(launch_voxelize(v, e->s(), e->hook_ptr())); });
+        e->sl().khist_pending = false;
+        e->sl().vox_valid = true;
     });
 }
 

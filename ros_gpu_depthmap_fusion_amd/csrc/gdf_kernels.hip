@@ -2261,6 +2261,138 @@ hipError_t launch_transform_points(const float4* in, const uint32_t* mask, float
     return hipGetLastError();
 }
 
+// ---- multi-GPU fused cloud: stable partition of the compacted (point, key) list by key range -----
+// part(key) = floor(key * nparts / ncells): rank j owns the keys [ceil(j C / np), ceil((j+1) C / np)),
+// so after an all-to-all every rank holds, in rank (= camera) order and pixel order within a
+// camera, exactly the points of its key range - the stable order the reference's single voxelize
+// sees for them (fusion.cpp:1743-1756 over the concatenated cameras).  Tiles of 1024 items: counts
+// per (part, tile) dest-major, scanned by k_scan_*, then a stable scatter (wave ballots on the
+// 4-bit part, per-wave counters in LDS).
+constexpr uint32_t kPartTile = 1024;
+
+__device__ __forceinline__ uint32_t part_of(uint32_t key, uint32_t nparts, uint64_t ncells) {
+    const uint64_t p = (uint64_t)key * nparts / ncells;
+    return p < nparts ? (uint32_t)p : nparts - 1u;
+}
+
+__global__ __launch_bounds__(256) void k_part_count(const uint32_t* __restrict__ keys,
+                                                    const uint32_t* __restrict__ count,
+                                                    uint32_t nparts, uint64_t ncells,
+                                                    uint32_t ntiles, uint32_t* __restrict__ counts) {
+    __shared__ uint32_t s_c[kMaxParts];
+    const uint32_t n = *count;
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {  // block-uniform
+        if (threadIdx.x < kMaxParts) s_c[threadIdx.x] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t i = t * kPartTile + q * 256 + threadIdx.x;
+            if (i < n) atomicAdd(&s_c[part_of(keys[i], nparts, ncells)], 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x < nparts) counts[threadIdx.x * ntiles + t] = s_c[threadIdx.x];
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void k_part_scatter(const float4* __restrict__ pts,
+                                                      const uint32_t* __restrict__ keys,
+                                                      const uint32_t* __restrict__ count,
+                                                      uint32_t nparts, uint64_t ncells,
+                                                      uint32_t ntiles,
+                                                      const uint32_t* __restrict__ offsets,
+                                                      const uint32_t* __restrict__ total,
+                                                      float4* __restrict__ out_pts,
+                                                      uint32_t* __restrict__ out_keys,
+                                                      uint32_t* __restrict__ part_counts) {
+    __shared__ uint32_t s_w[4][kMaxParts];  // per-wave running counts (slot-major order)
+    __shared__ uint32_t s_base[kMaxParts];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t n = *count;
+    if (blockIdx.x == 0 && threadIdx.x < nparts) {
+        const uint32_t a = offsets[threadIdx.x * ntiles];
+        const uint32_t b = threadIdx.x + 1 < nparts ? offsets[(threadIdx.x + 1) * ntiles] : *total;
+        part_counts[threadIdx.x] = b - a;
+    }
+    const unsigned long long ltm = lanemask_lt();
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {  // block-uniform
+        if (threadIdx.x < 4 * kMaxParts) (&s_w[0][0])[threadIdx.x] = 0;
+        if (threadIdx.x < nparts) s_base[threadIdx.x] = offsets[threadIdx.x * ntiles + t];
+        __syncthreads();
+        // wave w owns items [t*1024 + w*256, + 256) in 4 slots of 64: stable within the tile
+        uint32_t part[4], rank[4], key[4];
+        float4 p[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t i = t * kPartTile + w * 256 + q * 64 + lane;
+            const bool ok = i < n;
+            key[q] = ok ? keys[i] : 0u;
+            if (ok) p[q] = pts[i];
+            part[q] = ok ? part_of(key[q], nparts, ncells) : 0u;
+            unsigned long long m = __ballot(ok);
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const bool bit = (part[q] >> b) & 1u;
+                const unsigned long long bb = __ballot(bit);
+                m &= bit ? bb : ~bb;
+            }
+            const uint32_t before = (uint32_t)__popcll(m & ltm);
+            const uint32_t base = ok ? s_w[w][part[q]] : 0u;
+            rank[q] = base + before;
+            __builtin_amdgcn_wave_barrier();
+            if (ok && before == 0) s_w[w][part[q]] = base + (uint32_t)__popcll(m);
+            __builtin_amdgcn_wave_barrier();
+        }
+        __syncthreads();
+        // waves before this one in the tile
+        if (threadIdx.x < nparts) {
+            uint32_t run = 0;
+            for (int ww = 0; ww < 4; ++ww) {
+                const uint32_t c = s_w[ww][threadIdx.x];
+                s_w[ww][threadIdx.x] = run;
+                run += c;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t i = t * kPartTile + w * 256 + q * 64 + lane;
+            if (i < n) {
+                const uint32_t pos = s_base[part[q]] + s_w[w][part[q]] + rank[q];
+                out_pts[pos] = p[q];
+                out_keys[pos] = key[q];
+            }
+        }
+        __syncthreads();
+    }
+}
+
+uint32_t part_tiles(uint32_t nmax) { return (nmax + kPartTile - 1) / kPartTile; }
+
+hipError_t launch_partition(const float4* pts, const uint32_t* keys, const uint32_t* count,
+                            uint32_t nmax, uint32_t nparts, uint64_t ncells, uint32_t* counts,
+                            uint32_t* offsets, uint32_t* total, float4* out_pts,
+                            uint32_t* out_keys, uint32_t* part_counts, hipStream_t s) {
+    const uint32_t ntiles = std::max<uint32_t>(part_tiles(nmax), 1u);
+    const uint32_t blocks = std::min<uint32_t>(ntiles, 2048u);
+    hipLaunchKernelGGL(k_part_count, dim3(blocks), dim3(256), 0, s, keys, count, nparts, ncells,
+                       ntiles, counts);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const uint32_t m = nparts * ntiles;
+    const uint32_t chunks = (m + 4095u) / 4096u;
+    uint32_t* partial = offsets + scan_partials_offset(m);
+    hipLaunchKernelGGL(k_scan_reduce, dim3(chunks), dim3(1024), 0, s, counts, m, partial,
+                       (const uint32_t*)nullptr, 1u);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_scan_counts, dim3(chunks), dim3(1024), 0, s, counts, m, offsets, total,
+                       partial, (const uint32_t*)nullptr, 1u);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_part_scatter, dim3(blocks), dim3(256), 0, s, pts, keys, count, nparts,
+                       ncells, ntiles, offsets, total, out_pts, out_keys, part_counts);
+    return hipGetLastError();
+}
+
 // ---- multi-GPU occupancy marks -------------------------------------------------------------------
 // The engine's marks already are the exchange format (1 bit per cell): export is a copy, import
 // ORs the all-gathered masks of every rank into them.

@@ -49,6 +49,7 @@ class FrameParams(C.Structure):
         ("enable_voxel_filter", C.c_int32), ("voxel_min", _f3), ("voxel_max", _f3),
         ("voxel_size", _f3), ("voxel_average", C.c_int32), ("occupancy_lifetime", C.c_uint32),
         ("defer_occupancy_grid", C.c_int32), ("synchronous", C.c_int32),
+        ("defer_voxelize", C.c_int32),
     ]
 
 
@@ -102,7 +103,8 @@ EXPORTED = [
     # include/gdf_driver.h: the component's depth loop in C++ over the C-ABI
     "gdf_run_depth_stream", "gdf_run_host_stream", "gdf_run_depth_stream_batched",
     "gdf_next_frame_in_batch", "gdf_get_batch_ranges", "gdf_download_batch_occupancy_grid",
-    "gdf_mask_dilate", "gdf_transform_points",
+    "gdf_mask_dilate", "gdf_transform_points", "gdf_add_halo_depthmap_device",
+    "gdf_partition_points", "gdf_voxelize_points",
 ]
 
 
@@ -176,6 +178,9 @@ def load_library(path: str = LIB_PATH):
                                                u64, u32, i32]),
         "gdf_next_frame_in_batch": (i32, [vp]),
         "gdf_mask_dilate": (i32, [vp, vp, vp, u32, u32, u32, i32]),
+        "gdf_add_halo_depthmap_device": (i32, [vp, vp, u32, u32, u32, f, f, f, f, f, vp, vp]),
+        "gdf_partition_points": (i32, [vp, u32, vp, vp, u32, vp]),
+        "gdf_voxelize_points": (i32, [vp, vp, vp, u32, i32]),
         "gdf_transform_points": (i32, [vp, vp, vp, vp, u32, vp]),
         "gdf_get_batch_ranges": (i32, [vp, vp, vp, u32, P(u32)]),
         "gdf_download_batch_occupancy_grid": (i32, [vp, u32, vp, u64]),
@@ -230,7 +235,7 @@ class ComponentParams:
                                occupancy_lifetime=1)
 
     def to_c(self, T_world_move=None, T_crop_move=None, synchronous=True,
-             defer_occupancy_grid=False) -> FrameParams:
+             defer_occupancy_grid=False, defer_voxelize=False) -> FrameParams:
         p = FrameParams()
         p.ps_filter_threshold = self.ps_filter_threshold
         p.ps_filter_size = self.ps_filter_size
@@ -252,6 +257,7 @@ class ComponentParams:
         p.occupancy_lifetime = self.occupancy_lifetime
         p.defer_occupancy_grid = 1 if defer_occupancy_grid else 0
         p.synchronous = 1 if synchronous else 0
+        p.defer_voxelize = 1 if defer_voxelize else 0
         return p
 
 
@@ -343,6 +349,16 @@ class GPUDepthmapFusion:
         self._check(self._lib.gdf_add_point_sequence_device(
             self._h, C.c_void_p(dev_ptr), num_points, point_step, timestampSec, timestampNSec,
             _ptr(tm)))
+
+    def addHaloDepthmapDevice(self, tail_ptr: int, tail_pixels: int, width: int, height: int,
+                              depthScale: float, fx: float, fy: float, cx: float, cy: float,
+                              transform_world, transform_crop):
+        """Multi-GPU: the last `tail_pixels` depth values of the camera before this engine's
+        first one (rank k-1), read by the flying-pixel filter's top-row wraps."""
+        tw, tc = _mat(transform_world), _mat(transform_crop)
+        self._check(self._lib.gdf_add_halo_depthmap_device(
+            self._h, C.c_void_p(tail_ptr), tail_pixels, width, height, depthScale, fx, fy, cx, cy,
+            _ptr(tw), _ptr(tc)))
 
     def numCollectedPointSequencePoints(self) -> int:
         n = C.c_uint32()
@@ -531,8 +547,10 @@ class GPUDepthmapFusion:
         return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(KERNEL_SLOTS)}
 
     def processFrame(self, params: ComponentParams, T_world_move=None, T_crop_move=None,
-                     synchronous: bool = True, defer_occupancy_grid: bool = False) -> FrameResult:
-        p = params.to_c(T_world_move, T_crop_move, synchronous, defer_occupancy_grid)
+                     synchronous: bool = True, defer_occupancy_grid: bool = False,
+                     defer_voxelize: bool = False) -> FrameResult:
+        p = params.to_c(T_world_move, T_crop_move, synchronous, defer_occupancy_grid,
+                        defer_voxelize)
         return self.processFramePrepared(p)
 
     def make_stream_camera(self, dev_ptrs: Sequence[int], width: int, height: int,
@@ -572,6 +590,20 @@ class GPUDepthmapFusion:
         self._check(self._lib.gdf_run_depth_stream_batched(self._h, arr, len(cameras), C.byref(p),
                                                            first, batches, batch,
                                                            1 if host else 0))
+
+    # ---- multi-GPU fused cloud ----
+    def partition_points(self, nparts: int, send_pts_ptr: int, send_keys_ptr: int,
+                         capacity: int, part_counts_ptr: int):
+        """Split the frame's (point, key) list by voxel-key range into part-major buffers."""
+        self._check(self._lib.gdf_partition_points(self._h, nparts, C.c_void_p(send_pts_ptr),
+                                                   C.c_void_p(send_keys_ptr), capacity,
+                                                   C.c_void_p(part_counts_ptr)))
+
+    def voxelize_points(self, pts_ptr: int, keys_ptr: int, count: int, average: bool = True):
+        """Voxelize an external (point, key) list (what this rank received)."""
+        self._check(self._lib.gdf_voxelize_points(self._h, C.c_void_p(pts_ptr),
+                                                  C.c_void_p(keys_ptr), count,
+                                                  1 if average else 0))
 
     # ---- orphan shaders (device buffers) ----
     def maskDilate(self, in_ptr: int, out_ptr: int, width: int, height: int, filter_size: int,

@@ -146,3 +146,172 @@ class BatchedMarkExchange:
             self.eng.voxelOccupancyGridBatch(self.union.data_ptr(), self.words, 1, self.n,
                                              self.words, self.batch * self.words, lifetime)
         self.n = 0
+
+
+# ---- fused voxel cloud across ranks -----------------------------------------
+# The reference voxelizes the points of ALL cameras in one stable sort
+# (src/gpu_depthmap_fusion.cpp:1743-1756, cameras concatenated at :1583-1626).  With one camera
+# per rank the equal result is reached by one all-to-all of the compacted (point, key) lists by
+# voxel-key range (gdf_partition_points): rank j receives the points of keys
+# [ceil(j C / N), ceil((j+1) C / N)) from every rank, in rank order = camera order, pixel order
+# inside each camera - the stable order of the single sort restricted to its key range - and
+# voxelizes them (gdf_voxelize_points).  Each point crosses the fabric once (all-to-all), not N-1
+# times (the all-gather the north star names).  The F-row halo: rank k's flying-pixel filter
+# reads the last F rows + F pixels of camera k-1 at its top border; the ranks
+# all-gather those tails (F*W + F depth values each) before the frame.
+
+def part_of_keys(keys: np.ndarray, nparts: int, ncells: int) -> np.ndarray:
+    """Key-range owner of each key: floor(key * nparts / ncells) (k_part_count's rule)."""
+    return np.minimum((keys.astype(np.uint64) * np.uint64(nparts)) // np.uint64(ncells),
+                      nparts - 1).astype(np.int64)
+
+
+def halo_pixels(F: int, width: int) -> int:
+    """Depth values of camera k-1 that camera k's filter reads: F rows + F pixels."""
+    return int(F) * int(width) + int(F)
+
+
+def all_gather_tails(tail, group=None):
+    """Every rank's depth tail (equal sizes) -> list indexed by rank."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    parts = [torch.empty_like(tail) for _ in range(world)]
+    dist.all_gather(parts, tail, group=group)
+    return parts
+
+
+def exchange_points(send_pts, send_keys, counts, group=None):
+    """All-to-all of part-major (point, key) send buffers: counts[j] items go to rank j.
+    Returns (recv_pts [n, 4] float32, recv_keys [n] int32, recv_counts) in source-rank order.
+    Tensors live on the collective's device (cuda for nccl, cpu for gloo)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    dev = send_pts.device
+    c = torch.as_tensor(counts, dtype=torch.int64, device=dev)
+    rc = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_to_all_single(rc, c, group=group)
+    rcounts = [int(x) for x in rc.cpu().tolist()]
+    scounts = [int(x) for x in c.cpu().tolist()]
+    n = sum(rcounts)
+    rp = torch.empty((n, 4), dtype=torch.float32, device=dev)
+    rk = torch.empty(n, dtype=torch.int32, device=dev)
+    m = sum(scounts)
+    dist.all_to_all_single(rp, send_pts[:m], output_split_sizes=rcounts,
+                           input_split_sizes=scounts, group=group)
+    dist.all_to_all_single(rk, send_keys[:m], output_split_sizes=rcounts,
+                           input_split_sizes=scounts, group=group)
+    return rp, rk, rcounts
+
+
+class FusedCloudRank:
+    """One rank of the multi-GPU frame with the reference's fused output, over a GPU engine.
+
+    Per frame: (halo) all-gather of the depth tails -> the rank's camera with camera k-1's tail
+    as halo -> compaction + keys + marks (defer_voxelize, deferred grid) -> occupancy-mark union
+    (all-gather + OR) and the identical grid update on every rank -> key-range partition ->
+    all-to-all -> voxelize of the rank's key range.  Collectives run on torch tensors of `dev`
+    ("cuda": RCCL, the engine on torch's stream; "cpu": gloo, staged through host copies)."""
+
+    def __init__(self, engine, cams, rank: int, world: int, params, dev: str = "cuda"):
+        import torch
+        from . import hiprt
+        self.eng, self.cams, self.rank, self.world, self.p = engine, cams, rank, world, params
+        self.dev = dev
+        self.hiprt = hiprt
+        if dev == "cuda":
+            engine.set_stream(torch.cuda.current_stream().cuda_stream)
+        self.F = params.flying_filter_size
+        # every rank sends the same number of tail values: the deepest read of any camera
+        self.Lmax = max(halo_pixels(self.F, cams[k].width) for k in range(world))
+        if any(cams[k].width * cams[k].height < self.Lmax for k in range(world)):
+            raise ValueError("fused multi-GPU frames need cameras taller than F rows")
+        self.pc = params.to_c(None, None, False, True, True)
+
+    def frame(self, depth_ptr: int, tail_src_ptr: int):
+        """One frame: depth_ptr = this rank's depth map (device), tail_src_ptr = its last
+        Lmax depth values (device, the halo the next rank needs)."""
+        import numpy as np
+        import torch
+        import torch.distributed as dist
+        h = self.hiprt
+        eng, c = self.eng, self.cams[self.rank]
+        halo = None
+        if self.F > 0 and self.world > 1:
+            # all ranks send Lmax values (the tail of their camera); rank k uses rank k-1's
+            if self.dev == "cuda":
+                tail = torch.empty(self.Lmax, dtype=torch.int16, device="cuda")
+                h.check(h.hip().hipMemcpy(tail.data_ptr(), tail_src_ptr, 2 * self.Lmax, h.D2D),
+                        "tail")
+                parts = all_gather_tails(tail)
+                halo = parts[self.rank - 1] if self.rank > 0 else None
+                halo_ptr = halo.data_ptr() if halo is not None else 0
+            else:
+                tail = torch.from_numpy(_d2h(h, tail_src_ptr, np.int16, self.Lmax))
+                parts = all_gather_tails(tail)
+                if self.rank > 0:
+                    halo = h.DeviceArray.from_numpy(parts[self.rank - 1].numpy())
+                    halo_ptr = halo.ptr
+        eng.clear()
+        if self.rank > 0 and halo is not None:
+            pc = self.cams[self.rank - 1]
+            n = pc.width * pc.height
+            take = min(self.Lmax, n)
+            # the received tail holds camera k-1's last Lmax values (or all of a smaller camera)
+            eng.addHaloDepthmapDevice(halo_ptr + 2 * (self.Lmax - take), take, pc.width,
+                                      pc.height, *pc.intrinsics(), pc.T_world, pc.T_crop)
+        eng.addDepthmapDevice(depth_ptr, c.width, c.height, *c.intrinsics(), c.T_world, c.T_crop)
+        eng.processFramePrepared(self.pc)
+        _, ncells = eng.grid_size()
+        words = words_for(ncells)
+        # occupancy union (every rank the same grid)
+        if self.dev == "cuda":
+            local = torch.empty(words, dtype=torch.int32, device="cuda")
+            gathered = torch.empty(self.world * words, dtype=torch.int32, device="cuda")
+            eng.export_marks(local.data_ptr(), words)
+            dist.all_gather_into_tensor(gathered, local)
+            eng.import_marks(gathered.data_ptr(), words, self.world)
+        else:
+            dl = h.DeviceArray(words * 4)
+            eng.export_marks(dl.ptr, words)
+            eng.synchronize()
+            local = torch.from_numpy(dl.to_numpy(np.int32, words))
+            parts = [torch.empty_like(local) for _ in range(self.world)]
+            dist.all_gather(parts, local)
+            dg = h.DeviceArray.from_numpy(torch.cat(parts).numpy())
+            eng.import_marks(dg.ptr, words, self.world)
+        eng.voxelOccupancyGrid(self.p.occupancy_lifetime)
+        # key-range partition + all-to-all + voxelize of this rank's range
+        n_total = max(c.width * c.height, 1)
+        if self.dev == "cuda":
+            sp = torch.empty((n_total, 4), dtype=torch.float32, device="cuda")
+            sk = torch.empty(n_total, dtype=torch.int32, device="cuda")
+            cnt = torch.empty(self.world, dtype=torch.int32, device="cuda")
+            eng.partition_points(self.world, sp.data_ptr(), sk.data_ptr(), n_total, cnt.data_ptr())
+            counts = cnt.cpu().tolist()
+            rp, rk, rc = exchange_points(sp, sk, counts)
+            eng.voxelize_points(rp.data_ptr(), rk.data_ptr(), int(sum(rc)), self.p.voxel_average)
+            self._keep = (rp, rk)
+        else:
+            dsp, dsk, dcnt = h.DeviceArray(n_total * 16), h.DeviceArray(n_total * 4), h.DeviceArray(64)
+            eng.partition_points(self.world, dsp.ptr, dsk.ptr, n_total, dcnt.ptr)
+            eng.synchronize()
+            counts = dcnt.to_numpy(np.uint32, self.world).tolist()
+            m = int(sum(counts))
+            sp = torch.from_numpy(dsp.to_numpy(np.float32, 4 * max(m, 1))[:4 * m].reshape(m, 4))
+            sk = torch.from_numpy(dsk.to_numpy(np.int32, max(m, 1))[:m])
+            rp, rk, rc = exchange_points(sp, sk, counts)
+            n = int(sum(rc))
+            drp = h.DeviceArray.from_numpy(rp.numpy()) if n else None
+            drk = h.DeviceArray.from_numpy(rk.numpy()) if n else None
+            eng.voxelize_points(drp.ptr if n else 0, drk.ptr if n else 0, n, self.p.voxel_average)
+            eng.synchronize()
+            self._keep = (drp, drk)
+        return counts
+
+
+def _d2h(h, ptr, dtype, count):
+    out = np.empty(count, dtype)
+    h.check(h.hip().hipMemcpy(out.ctypes.data, ptr, out.nbytes, h.D2H), "D2H")
+    return out

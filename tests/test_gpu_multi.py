@@ -1,0 +1,81 @@
+"""Multi-rank fused cloud through the HIP kernels: two processes on the one GPU of the box, gloo
+collectives (host-staged), each rank a GPUDepthmapFusion with its camera (camera k-1's depth
+tail as halo, gdf_add_halo_depthmap_device), the key-range partition (gdf_partition_points), the
+all-to-all, gdf_voxelize_points, the occupancy-mark union: the ranks' voxel ranges concatenated
+equal ONE oracle engine over both cameras bit for bit, and every rank holds its grid."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+from ros_gpu_depthmap_fusion_amd import synth  # noqa: E402
+from ros_gpu_depthmap_fusion_amd.gdf import ComponentParams  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+W, H, FRAMES = 160, 120, 3
+
+
+def params(F):
+    p = ComponentParams()
+    p.flying_filter_size = F
+    p.voxel_min, p.voxel_max = (-8.0, -8.0, -1.0), (8.0, 8.0, 2.0)
+    p.crop_min, p.crop_max = p.voxel_min, p.voxel_max
+    return p
+
+
+def _rank(rank, world, port, F, out_dir):
+    import torch.distributed as dist
+    from ros_gpu_depthmap_fusion_amd import build_library, hiprt, multi
+    from ros_gpu_depthmap_fusion_amd.gdf import GPUDepthmapFusion
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    build_library()
+    p = params(F)
+    cams = [synth.make_camera(k, W, H) for k in range(world)]
+    eng = GPUDepthmapFusion(0)
+    fr = multi.FusedCloudRank(eng, cams, rank, world, p, dev="cpu")
+    n = W * H
+    for f in range(FRAMES):
+        d = hiprt.DeviceArray.from_numpy(synth.dense_frame(cams[rank], rank, f))
+        fr.frame(d.ptr, d.ptr + 2 * (n - fr.Lmax))
+        np.save(os.path.join(out_dir, f"vox_r{rank}_f{f}.npy"), eng.downloadVoxelizedPoints()[:, :3])
+        np.save(os.path.join(out_dir, f"grid_r{rank}_f{f}.npy"), eng.downloadVoxelOccupancyGrid())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("F", [0, 4])
+def test_two_rank_fused_cloud_hip(tmp_path, F):
+    from oracle import OracleFusion
+    world = 2
+    mp.start_processes(_rank, args=(world, _free_port(), F, str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    p = params(F)
+    cams = [synth.make_camera(k, W, H) for k in range(world)]
+    orc = OracleFusion(threads=4)
+    for f in range(FRAMES):
+        orc.clear()
+        for k, c in enumerate(cams):
+            orc.addDepthmap(synth.dense_frame(c, k, f), *c.intrinsics(), c.T_world, c.T_crop)
+        orc.processFrame(p)
+        want = orc.downloadVoxelizedPoints()[:, :3]
+        got = np.concatenate([np.load(tmp_path / f"vox_r{r}_f{f}.npy") for r in range(world)])
+        assert len(got) == len(want) > 0, f"frame {f}"
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), f"frame {f}"
+        for r in range(world):
+            np.testing.assert_array_equal(np.load(tmp_path / f"grid_r{r}_f{f}.npy"),
+                                          orc.downloadVoxelOccupancyGrid(), f"frame {f} rank {r}")
