@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--pipeline", type=int, default=3,
                     help="frames in flight on one GPU (engine slots, gdf_set_pipeline_depth); "
                          "N > 1 runs on torch's stream with depth 1")
+    ap.add_argument("--multi-mode", choices=("fused", "marks"), default="fused",
+                    help="N > 1: fused = the reference's output over all cameras (halo, mark "
+                         "union, key-range all-to-all + voxelize); marks = occupancy union only")
     ap.add_argument("--exchange-batch", type=int, default=1,
                     help="N > 1: frames per occupancy-mark all-gather (1 = every frame, the "
                          "reference's per-frame grid; B > 1 = deferred grid, B frames per "
@@ -346,37 +349,55 @@ def main():
 
 
 def time_multi(args, st, params, dist, world, pmc_key):
-    """N > 1: every rank runs its camera; the occupancy marks are exchanged over RCCL."""
+    """N > 1: every rank runs its camera.  Mode "fused" (default): the reference's output over
+    all cameras - camera k-1's depth tail as halo (all-gather), occupancy-mark union (all-gather
+    + OR, every rank the same grid), key-range all-to-all of the (point, key) lists and the
+    voxelize of each rank's range (multi.FusedCloudRank).  Mode "marks": only the occupancy union
+    (voxel means per camera), `--exchange-batch` frames per all-gather."""
     import numpy as np
     import torch
     eng = st.eng
     npts, nvox = st.counts(params)
     (gx, gy, gz), ncells = eng.grid_size()
-    batched = args.exchange_batch > 1
     depth = 1
-    if batched:
-        from ros_gpu_depthmap_fusion_amd.multi import BatchedMarkExchange
-        depth = max(1, min(4, args.pipeline))
-        eng.set_pipeline_depth(depth)
-        marks = BatchedMarkExchange(eng, ncells, world, args.exchange_batch)
-    else:
-        from ros_gpu_depthmap_fusion_amd.multi import DeviceMarkExchange
-        eng.set_stream(torch.cuda.current_stream().cuda_stream)
-        marks = DeviceMarkExchange(eng, ncells, world)
-    pc_defer = params.to_c(None, None, False, True)
+    fused = args.multi_mode == "fused"
+    if fused:
+        from ros_gpu_depthmap_fusion_amd import synth
+        from ros_gpu_depthmap_fusion_amd.multi import FusedCloudRank
+        rank = dist.get_rank()
+        cams = [synth.make_camera(k, st.W, st.H) for k in range(world)]
+        fr = FusedCloudRank(eng, cams, rank, world, params, dev="cuda")
+        n = st.W * st.H
 
-    def run(first, count):
-        for i in range(first, first + count):
-            st.run(pc_defer, i, 1)
-            if batched:
-                marks.take()
-                if marks.full():
-                    marks.flush(params.occupancy_lifetime)
-            else:
-                marks.exchange()
-                eng.voxelOccupancyGrid(params.occupancy_lifetime)
+        def run(first, count):
+            for i in range(first, first + count):
+                d = st.dframes[0][i % st.ring].ptr
+                fr.frame(d, d + 2 * (n - fr.Lmax))
+    else:
+        batched = args.exchange_batch > 1
         if batched:
-            marks.flush(params.occupancy_lifetime)
+            from ros_gpu_depthmap_fusion_amd.multi import BatchedMarkExchange
+            depth = max(1, min(4, args.pipeline))
+            eng.set_pipeline_depth(depth)
+            marks = BatchedMarkExchange(eng, ncells, world, args.exchange_batch)
+        else:
+            from ros_gpu_depthmap_fusion_amd.multi import DeviceMarkExchange
+            eng.set_stream(torch.cuda.current_stream().cuda_stream)
+            marks = DeviceMarkExchange(eng, ncells, world)
+        pc_defer = params.to_c(None, None, False, True)
+
+        def run(first, count):
+            for i in range(first, first + count):
+                st.run(pc_defer, i, 1)
+                if batched:
+                    marks.take()
+                    if marks.full():
+                        marks.flush(params.occupancy_lifetime)
+                else:
+                    marks.exchange()
+                    eng.voxelOccupancyGrid(params.occupancy_lifetime)
+            if batched:
+                marks.flush(params.occupancy_lifetime)
 
     def barrier_sync():
         eng.synchronize()
@@ -405,8 +426,8 @@ def time_multi(args, st, params, dist, world, pmc_key):
         "roofline": None,
     }
     if not args.no_kernel_timing:
-        kt_steps = min(args.steps, 200)
-        if batched:
+        kt_steps = min(args.steps, 100)
+        if depth > 1:
             eng.set_pipeline_depth(1)
         eng.set_profiling(True)
         run(prime + args.warmup, kt_steps)
@@ -415,11 +436,19 @@ def time_multi(args, st, params, dist, world, pmc_key):
         eng.set_profiling(False)
         line["roofline"] = roofline_from(kt, kt_steps, model_bytes(st.P, n_avg, g_avg, ncells),
                                          pmc_key)
-    cfg = {"parallelism": "camera-per-GPU x%d, occupancy-mark all-gather %s" % (
-               world, "every frame" if not batched else
-               "every %d frames (deferred grid)" % args.exchange_batch),
-           "exchange": ("sparse mark pairs (cap %d words/frame), %d dense-fallback batches" %
-                        (marks.cap, marks.dense_batches)) if batched else "bitmask per frame"}
+    if fused:
+        cfg = {"parallelism": "camera-per-GPU x%d; per frame: depth-tail halo all-gather, "
+                              "occupancy-mark all-gather, key-range all-to-all of the (point, "
+                              "key) lists, voxelize per key range (fused cloud = one engine over "
+                              "all cameras)" % world,
+               "exchange": "halo %d px + %d-word marks + points all-to-all per frame" % (
+                   fr.Lmax, (ncells + 31) // 32)}
+    else:
+        cfg = {"parallelism": "camera-per-GPU x%d, occupancy-mark all-gather %s (voxel means per "
+                              "camera)" % (world, "every frame" if not batched else
+                                           "every %d frames (deferred grid)" % args.exchange_batch),
+               "exchange": ("sparse mark pairs (cap %d words/frame), %d dense-fallback batches" %
+                            (marks.cap, marks.dense_batches)) if batched else "bitmask per frame"}
     return line, cfg
 
 

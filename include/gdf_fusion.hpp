@@ -12,11 +12,21 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <cstring>
 #include <stdexcept>
 #include <string>
 #include <vector>
 
 #include "gdf.h"
+
+// The component calls glMemoryBarrier(GL_ALL_BARRIER_BITS) between the engine calls
+// (component.cpp:164-309, 12 sites); ordering is the HIP stream's here, so without a GL header
+// these are no-ops (SURVEY.md §8(b) "GL leakage into caller").
+#ifndef GL_ALL_BARRIER_BITS
+#define GL_ALL_BARRIER_BITS 0xFFFFFFFFu
+#define GL_SHADER_STORAGE_BARRIER_BIT 0x00002000u
+inline void glMemoryBarrier(unsigned int) {}
+#endif
 
 namespace gdf {
 

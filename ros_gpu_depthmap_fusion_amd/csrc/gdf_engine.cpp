@@ -1860,6 +1860,10 @@ int gdf_voxelize_points(gdf_engine* e, const float* pts, const uint32_t* keys, u
         if (!e->grid_set) fail(GDF_ERR_STATE, "voxelize_points needs the voxel grid of a frame");
         if (n && (!pts || !keys)) fail(GDF_ERR_ARG, "voxelize_points: null list");
         ensure_misc(e);
+        if (e->sl().khist_pending) {  // the frame's compaction counted ITS keys' digits: not these
+            HIPCHK(hipMemsetAsync(e->sl().d_khist.p, 0, kHistWords * 4, e->s()));
+            e->sl().khist_pending = false;
+        }
         HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(e->sl().d_misc.as<uint32_t>() + kRecvCount),
                                  (int)n, 1, e->s()));
         VoxSource src;

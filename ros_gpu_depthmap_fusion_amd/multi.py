@@ -240,15 +240,16 @@ class FusedCloudRank:
         halo = None
         if self.F > 0 and self.world > 1:
             # all ranks send Lmax values (the tail of their camera); rank k uses rank k-1's
+            # (bytes: gloo has no 16-bit integer collectives)
             if self.dev == "cuda":
-                tail = torch.empty(self.Lmax, dtype=torch.int16, device="cuda")
+                tail = torch.empty(2 * self.Lmax, dtype=torch.uint8, device="cuda")
                 h.check(h.hip().hipMemcpy(tail.data_ptr(), tail_src_ptr, 2 * self.Lmax, h.D2D),
                         "tail")
                 parts = all_gather_tails(tail)
                 halo = parts[self.rank - 1] if self.rank > 0 else None
                 halo_ptr = halo.data_ptr() if halo is not None else 0
             else:
-                tail = torch.from_numpy(_d2h(h, tail_src_ptr, np.int16, self.Lmax))
+                tail = torch.from_numpy(_d2h(h, tail_src_ptr, np.uint8, 2 * self.Lmax))
                 parts = all_gather_tails(tail)
                 if self.rank > 0:
                     halo = h.DeviceArray.from_numpy(parts[self.rank - 1].numpy())

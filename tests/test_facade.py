@@ -1,5 +1,7 @@
 """The C++ facade (include/gdf_fusion.hpp) compiles against the reference component's call
-sequence and links against libgdf.so (CPU-only check: nothing is run)."""
+sequence and links against libgdf.so (nothing is run here: tests/test_facade_gpu.py runs the
+component sequence on the GPU), and the facade fixture (tests/golden/facade) is what the oracle
+computes for its inputs."""
 import os
 import subprocess
 
@@ -18,3 +20,24 @@ def test_facade_compiles_and_links(tmp_path):
            "-Wl,--allow-shlib-undefined", "-o", str(out)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+    cmd[6] = os.path.join(ROOT, "tests", "facade_component.cpp")
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+def test_facade_fixture_pinned_by_oracle():
+    import sys
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import make_facade_golden as g
+    fix = os.path.join(ROOT, "tests", "golden", "facade")
+    for f, o in enumerate(g.oracle_outputs()):
+        for name, arr, dt in (("points", o["points"], "<f4"), ("coords", o["coords"], "<u4"),
+                              ("voxelized", o["voxelized"][:, :3], "<f4"),
+                              ("grid", o["grid"], "u1")):
+            want = np.fromfile(os.path.join(fix, f"{name}{f}.bin"), dt)
+            assert np.array_equal(np.ascontiguousarray(arr, dt).reshape(-1).view(np.uint8),
+                                  want.view(np.uint8)), f"frame {f} {name}"
+        _, _, depth, cloud, _, _, _ = g.inputs(f)
+        np.testing.assert_array_equal(np.fromfile(os.path.join(fix, f"depth{f}.bin"), "<u2"),
+                                      depth.reshape(-1))

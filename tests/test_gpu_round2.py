@@ -329,6 +329,7 @@ def test_mask_dilate_matches_oracle(Engine, W, H):
     for F in (0, 1, 4, 16):
         for aw in (False, True):
             hiprt.check(hiprt.hip().hipMemset(dout.ptr, 0xAB, m.nbytes))
+            hiprt.synchronize()  # (the engine's stream does not wait for the null stream)
             gpu.maskDilate(din.ptr, dout.ptr, W, H, F, aw)
             gpu.synchronize()
             got = dout.to_numpy(np.uint32, W * H).reshape(H, W)
