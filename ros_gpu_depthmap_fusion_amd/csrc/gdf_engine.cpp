@@ -1359,6 +1359,8 @@ int gdf_create(int device, gdf_engine** out) {
     int rc = guarded(e, [&] {
         create_slot(e->slots[0]);
         if (const char* v = std::getenv("GDF_SORT_PT")) e->sort_pt = std::atoi(v);  // tuning knob
+        if (const char* v = std::getenv("GDF_GROUP_SCAN_TILES"))                   // tuning knob
+            g_group_scan_tiles = (uint32_t)std::max(1, std::atoi(v));
         if (const char* v = std::getenv("GDF_SEG_ITEMS")) {  // tuning knob
             const uint32_t si = (uint32_t)std::atoi(v);
             if (si >= 64 && si <= kSegItems && si % 64 == 0) e->seg_items = si;

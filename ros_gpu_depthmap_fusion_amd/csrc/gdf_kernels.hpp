@@ -113,6 +113,8 @@ struct VoxelizeArgs {
 };
 hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hook = nullptr);
 size_t voxelize_status_words(uint32_t nmax);
+// capacity (256-key tiles) above which k_group takes its group-id offsets from count + scan
+extern uint32_t g_group_scan_tiles;
 size_t voxelize_group_tiles(uint32_t nmax);
 
 // orphan shaders: mask_dilate (F <= kDilateMaxF) and single-matrix transform_points

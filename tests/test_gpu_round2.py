@@ -182,12 +182,13 @@ def _window_frames(gpu, orc, lidar, cam, p, nseq, npf, seqs_host, seqs_dev, dept
 
 
 def test_rollbuffer_window_oracle_parity_large(Engine):
-    """Rollbuffer window of 14 sequences x 320x240 (dense) + a 320x240 depth map: ~1.1 M selected
+    """Rollbuffer window of 28 sequences x 320x240 (dense) + a 320x240 depth map: 2.2 M selected
     points per frame - k_sel's multi-segment tiles (8 x 512 points), tiles straddling two
-    sequences, > 4096 group tiles (group-id offsets by count + scan) and voxels longer than the
-    512 staged points (k_group_big) - bit-exact vs the oracle on the last frames."""
+    sequences, > 8192 group tiles of capacity (group-id offsets by count + scan) and voxels
+    longer than the 512 staged points (k_group_big) - bit-exact vs the oracle on the last
+    frames."""
     p = ComponentParams()
-    p.ps_timespan = 13.5 / 30.0
+    p.ps_timespan = 27.5 / 30.0
     lidar = synth.make_camera(1, 320, 240)
     cam = synth.make_camera(0, 320, 240)
     npf = 320 * 240
@@ -196,10 +197,10 @@ def test_rollbuffer_window_oracle_parity_large(Engine):
     dev = [hiprt.DeviceArray.from_numpy(h) for h in host]
     depth = [synth.dense_frame(cam, 0, f) for f in range(3)]
     gpu, orc = Engine(), OracleFusion(threads=16)
-    r = _window_frames(gpu, orc, lidar, cam, p, 18, npf, host, dev, depth, True)
+    r = _window_frames(gpu, orc, lidar, cam, p, 31, npf, host, dev, depth, True)
     st = gpu.rollbuffer_state()
-    assert st.selection_sequence_count == 14 and st.as_tuple() == orc.rollbuffer_state()
-    assert r.num_points_total == 15 * npf and r.num_points > 300_000
+    assert st.selection_sequence_count == 28 and st.as_tuple() == orc.rollbuffer_state()
+    assert r.num_points_total == 29 * npf and r.num_points > 600_000
     compare_results(gpu, orc, tag="window")
 
 
