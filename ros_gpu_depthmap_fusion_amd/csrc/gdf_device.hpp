@@ -35,7 +35,8 @@ constexpr uint32_t kMaxParts = 16;                          // ranks of the fuse
 // Device-wide counters: monotonically increasing tile tickets (the host passes each launch's
 // base, so no per-launch memset) and the global digit histogram of the voxel keys.
 // per-stream device counters (u64 words, low 32 bits used): tile tickets, look-back epoch
-enum CounterSlot { kCtrSel = 0, kCtrSort0 = 1, kCtrGroup = 5, kCtrEpoch = 6, kCtrSlots = 8 };
+enum CounterSlot { kCtrSel = 0, kCtrSort0 = 1, kCtrGroup = 5, kCtrEpoch = 6, kCtrExpand = 7,
+                   kCtrSlots = 8 };
 
 // engine-order of historic-grid updates across streams (grid_seq_enter / grid_seq_leave)
 struct GridSeq {
@@ -111,6 +112,7 @@ struct FrameArgs {
     // voxel keys + occupancy marks (compute_voxel_coords + voxel_grid_occupancy_of_points)
     int32_t do_voxel;
     float vlo[3], vcs[3], gmax[3];
+    float vrcs[3];              // RN(1 / vcs) (voxel_key's fast quotient)
     uint32_t gs[3];
     uint32_t* marks;            // occupancy mark bitmask (cell c -> bit c % 32 of word c / 32)
     uint32_t* key_hist;         // optional [npasses*256] digit histogram of the keys
@@ -138,6 +140,15 @@ struct FrameArgs {
     uint32_t frame_shift;       // bit width of the voxel keys (the frame index sits above)
     uint64_t mark_words;        // words of one frame's mark bitmask
     uint32_t* frame_pt_start;   // [nframes + 1], written by k_emit
+    // runs of equal voxel keys (depth-only frames): k_mask counts the runs among the kept pixels
+    // of each wave (a run = consecutive kept lanes with one key; the voxelize then sorts runs,
+    // not points), k_emit writes each run's sort key and first point
+    int32_t run_mode;
+    uint32_t* wave_runs;        // [total_segs * 16] runs per (segment, wave)
+    uint32_t* run_keys;         // [runs] key | frame << frame_shift
+    uint32_t* run_start;        // [runs + 1] first point of each run; [runs] = points
+    uint32_t* run_count;        // runs of the frame (device)
+    uint32_t* scan_total;       // scratch total of the segment-count scan
 };
 static_assert(sizeof(FrameArgs) <= 4096, "kernel arguments are limited to 4 KiB");
 
@@ -176,13 +187,27 @@ __device__ __forceinline__ void cam_point(const CamDesc& c, uint32_t local, uint
     z = zz;
 }
 
-// sh/compute_voxel_coords.glsl:44-53: clamp-then-floor per axis, x fastest
+// sh/compute_voxel_coords.glsl:44-53: clamp-then-floor per axis, x fastest, of the correctly
+// rounded quotient (p - lo) / cs.  Only the floor of the clamped quotient matters, so the
+// quotient is first taken as (p - lo) * rcp(cs) (rcs = RN(1/cs), host-computed): its relative
+// error is <= 3 * 2^-24, and unless it lies within 2^-20 (relative) of an integer - where the
+// exact quotient could floor (or clamp, at the integers 0 and gs - 1) differently - the floor is
+// the same.  Those rare lanes (wave-uniform branch) divide exactly.
+__device__ __forceinline__ float voxel_axis(float p, float lo, float cs, float rcs) {
+    const float d = p - lo;
+    const float q = d * rcs;
+    const float r = rintf(q);
+    if (__builtin_expect(fabsf(q - r) <= fabsf(q) * 9.5367431640625e-07f, 0))  // 2^-20
+        return d / cs;
+    return q;
+}
+
 __device__ __forceinline__ uint32_t voxel_key(float px, float py, float pz, const float* vlo,
-                                              const float* vcs, const float* gmax,
-                                              const uint32_t* gs) {
-    float fx = (px - vlo[0]) / vcs[0];
-    float fy = (py - vlo[1]) / vcs[1];
-    float fz = (pz - vlo[2]) / vcs[2];
+                                              const float* vcs, const float* vrcs,
+                                              const float* gmax, const uint32_t* gs) {
+    float fx = voxel_axis(px, vlo[0], vcs[0], vrcs[0]);
+    float fy = voxel_axis(py, vlo[1], vcs[1], vrcs[1]);
+    float fz = voxel_axis(pz, vlo[2], vcs[2], vrcs[2]);
     fx = fminf(fmaxf(fx, 0.0f), gmax[0]);
     fy = fminf(fmaxf(fy, 0.0f), gmax[1]);
     fz = fminf(fmaxf(fz, 0.0f), gmax[2]);

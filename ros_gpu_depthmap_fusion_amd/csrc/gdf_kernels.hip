@@ -368,17 +368,22 @@ struct SegGeo {
     uint32_t item0;   // first item (global point index)
 };
 
-__device__ __forceinline__ SegGeo seg_geo(const CamDesc* cams, int ncams, uint32_t s) {
+// (P: an LDS copy of the descriptors, or the global / kernel-argument table read with scalar
+// loads - the segment is block-uniform)
+template <class P>
+__device__ __forceinline__ SegGeo seg_geo(P cams, int ncams, uint32_t s) {
     SegGeo g{0, 0, 0, 0, 0};
     for (int c = 0; c < ncams; ++c)
         if (cams[c].emit && s >= cams[c].seg0 && s < cams[c].seg0 + cams[c].nseg) g.k = c;
-    const CamDesc& c = cams[g.k];
-    const uint32_t i = s - c.seg0;
-    g.y = i / c.nchunk;
-    const uint32_t j = i - g.y * c.nchunk;
-    g.x0 = j * c.segw;
-    g.len = min(c.segw, c.W - g.x0);
-    g.item0 = (uint32_t)c.off + g.y * c.W + g.x0;
+    g.k = __builtin_amdgcn_readfirstlane(g.k);
+    const uint32_t seg0 = cams[g.k].seg0, nchunk = cams[g.k].nchunk, segw = cams[g.k].segw;
+    const uint32_t W = cams[g.k].W;
+    const uint32_t i = s - seg0;
+    g.y = i / nchunk;
+    const uint32_t j = i - g.y * nchunk;
+    g.x0 = j * segw;
+    g.len = min(segw, W - g.x0);
+    g.item0 = (uint32_t)cams[g.k].off + g.y * W + g.x0;
     return g;
 }
 
@@ -633,6 +638,8 @@ __global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
     __shared__ float s_yn[2 * kHalo + 1];
     __shared__ int s_rowoff[2 * kHalo + 1];
     __shared__ uint32_t s_cnt[16];
+    __shared__ uint32_t s_rcnt[16];
+    __shared__ uint32_t s_hist[4 * 256];  // run-key digit histogram (run mode)
     extern __shared__ uint4 s_dyn[];  // band rows (a.band_rowb bytes each), then xn
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int nwaves = blockDim.x >> 6;
@@ -641,13 +648,21 @@ __global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
     const uint32_t n = gridDim.x, q8 = n / 8, r8 = n % 8, xcd = blockIdx.x % 8;
     const uint32_t s = xcd * q8 + min(xcd, r8) + blockIdx.x / 8;
     if (a.grid_seq_out && blockIdx.x == 0 && threadIdx.x == 0) *a.grid_seq_out = a.grid_seq;
-    load_cams(a, s_cams);
-    __syncthreads();
     uint32_t bits = 0;
+    uint32_t rkey = 0xFFFFFFFFu;  // run mode: sort key of a kept pixel
     const uint32_t i = threadIdx.x;
+    if (a.run_mode && a.key_hist)
+        for (uint32_t j = threadIdx.x; j < a.npasses * 256; j += blockDim.x) s_hist[j] = 0;
     {
-        const SegGeo sg = seg_geo(s_cams, a.ncams, s);
-        const CamDesc& c = s_cams[sg.k];
+        // the block's camera from the descriptor table with scalar loads, so the band loads
+        // issue at once; the LDS copy of all descriptors (neighbour lookups) overlaps them
+        const gptr<const CamDesc> gcam = G(cam_table(a));
+        const SegGeo sg = seg_geo(gcam, a.ncams, s);
+        struct {
+            const uint16_t* depth;
+            const float *xn, *yn;
+            uint32_t W, H;
+        } c = {gcam[sg.k].depth, gcam[sg.k].xn, gcam[sg.k].yn, gcam[sg.k].W, gcam[sg.k].H};
         const int h = a.do_flying ? (int)min(a.F, (uint32_t)kHalo) : 0;
         const uint32_t ca = sg.x0 >= (uint32_t)h ? sg.x0 - h : 0u;
         const uint32_t cb = min(c.W, sg.x0 + sg.len + h);
@@ -683,6 +698,7 @@ __global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
             const int gyi = (int)sg.y - h + (int)i;
             s_yn[i] = (gyi >= 0 && gyi < (int)c.H) ? G(c.yn)[gyi] : 0.0f;
         }
+        load_cams(a, s_cams);
         if (rok) {
 #pragma unroll
             for (int q = 0; q < 3; ++q) {
@@ -718,6 +734,14 @@ __global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
             else
                 bits = depth_bits<ROT45, false>(a, s_cams, sg.k, t, s_yn, sg.x0 + i, sg.y, i < sg.len);
             if (a.dbg && i < sg.len) G(a.dbg)[sg.item0 + i] = (uint8_t)bits;
+            if (a.run_mode && (bits & 4u)) {  // the voxel key k_emit will compute (same f32 ops)
+                const CamDesc& cd = s_cams[sg.k];
+                const P3 p = band_pt(t, h, sg.x0 + i, s_yn[h], cd.scale);
+                const float wx = mrow(cd.Tw + 0, p.x, p.y, p.z, 1.0f);
+                const float wy = mrow(cd.Tw + 4, p.x, p.y, p.z, 1.0f);
+                const float wz = mrow(cd.Tw + 8, p.x, p.y, p.z, 1.0f);
+                rkey = voxel_key(wx, wy, wz, a.vlo, a.vcs, a.vrcs, a.gmax, a.gs) | (cd.frame << a.frame_shift);
+            }
         }
     }
     const unsigned long long m = __ballot((bits & 4u) != 0u);
@@ -725,11 +749,35 @@ __global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
         G(a.vbits)[(size_t)s * 16 + wid] = m;
         s_cnt[wid] = (uint32_t)__popcll(m);
     }
+    if (a.run_mode) {  // runs of equal keys among the wave's kept lanes (k_emit's leaders)
+        const unsigned long long below = m & lanemask_lt();
+        const int prev = below ? 63 - __clzll((long long)below) : -1;
+        const uint32_t pkey = __shfl(rkey, prev < 0 ? 0 : prev, 64);
+        const bool leader = ((bits & 4u) != 0u) && (prev < 0 || pkey != rkey);
+        const unsigned long long lm = __ballot(leader);
+        if (lane == 0) {
+            G(a.wave_runs)[(size_t)s * 16 + wid] = (uint32_t)__popcll(lm);
+            s_rcnt[wid] = (uint32_t)__popcll(lm);
+        }
+        if (leader && a.key_hist)
+            for (uint32_t p = 0; p < a.npasses; ++p)
+                atomicAdd(&s_hist[p * 256 + ((rkey >> (8 * p)) & 0xFFu)], 1u);
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint32_t t = 0;
+        uint32_t t = 0, r = 0;
         for (int w = 0; w < nwaves; ++w) t += s_cnt[w];
         G(a.seg_counts)[s] = t;
+        if (a.run_mode) {
+            for (int w = 0; w < nwaves; ++w) r += s_rcnt[w];
+            G(a.seg_counts)[a.total_segs + s] = r;  // run counts follow the point counts
+        }
+    }
+    if (a.run_mode && a.key_hist) {
+        const gptr<uint32_t> rep = G(a.key_hist + (blockIdx.x % kHistReps) * 1024u);
+        for (uint32_t j = threadIdx.x; j < a.npasses * 256; j += blockDim.x)
+            if (s_hist[j])
+                __hip_atomic_fetch_add(rep + j, s_hist[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -858,7 +906,7 @@ __device__ __forceinline__ void mark_and_count(const FrameArgs& a, uint32_t* mar
             __hip_atomic_fetch_or(G(marks + (key >> 5)), 1u << (key & 31u), __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (a.key_hist) {
+        if (a.key_hist && s_hist) {
             const unsigned long long after = lm & ~(ltm | (1ull << lane));
             const unsigned long long upto =
                 after ? ((1ull << (__ffsll((long long)after) - 1)) - 1ull) : ~0ull;
@@ -879,12 +927,22 @@ __device__ __forceinline__ void flush_hist(const FrameArgs& a, uint32_t* s_hist)
 }
 
 // sum of the counts of segments [0, s) by the block (fused-prefix form), into s_red per wave
+// (run mode: the run counts of those segments too, into s_red + 16)
 __device__ __forceinline__ void prefix_partials(const FrameArgs& a, uint32_t s, uint32_t* s_red) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint32_t sum = 0;
-    for (uint32_t t = threadIdx.x; t < s; t += blockDim.x) sum += G(a.seg_counts)[t];
-    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
-    if (lane == 0) s_red[wid] = sum;
+    uint32_t sum = 0, rsum = 0;
+    for (uint32_t t = threadIdx.x; t < s; t += blockDim.x) {
+        sum += G(a.seg_counts)[t];
+        if (a.run_mode) rsum += G(a.seg_counts)[a.total_segs + t];
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        sum += __shfl_xor(sum, o, 64);
+        rsum += __shfl_xor(rsum, o, 64);
+    }
+    if (lane == 0) {
+        s_red[wid] = sum;
+        s_red[16 + wid] = rsum;
+    }
 }
 
 // prefix of the valid counts of the waves before this one in segment s (uniform word loads)
@@ -909,14 +967,15 @@ __device__ __forceinline__ uint32_t wave_prefix(const FrameArgs& a, uint32_t s, 
 // segments) or k_scan_counts' result.
 __global__ __launch_bounds__(1024) void k_emit(FrameArgs a) {
     __shared__ uint32_t s_hist[4 * 256];
-    __shared__ uint32_t s_red[16];
+    __shared__ uint32_t s_red[32];
     __shared__ uint32_t s_mark[1u << kMarkCacheBits];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int nwaves = blockDim.x >> 6;
     const uint32_t s = blockIdx.x;
     for (uint32_t j = threadIdx.x; j < (1u << kMarkCacheBits); j += blockDim.x) s_mark[j] = 0xFFFFFFFFu;
     const gptr<const CamDesc> cams = G(cam_table(a));
-    if (a.key_hist)
+    const bool hist = a.key_hist && !a.run_mode;  // (run mode: k_mask counted the run keys)
+    if (hist)
         for (uint32_t i = threadIdx.x; i < a.npasses * 256; i += blockDim.x) s_hist[i] = 0;
     if (a.fused_prefix) prefix_partials(a, s, s_red);
     // the segment's geometry and the thread's item source, loaded before the barrier
@@ -931,20 +990,46 @@ __global__ __launch_bounds__(1024) void k_emit(FrameArgs a) {
     const uint32_t y = j / cams[k].nchunk;
     const uint32_t x0 = (j - y * cams[k].nchunk) * cams[k].segw;
     const uint32_t len = min(cams[k].segw, cams[k].W - x0);
+    // the validity word, the depth and the column's ray factor are independent loads: all in
+    // flight together (the depth of a pixel the crop dropped is read for nothing - it is in L2
+    // from k_mask - instead of waiting for the validity word first)
     const unsigned long long m = G(a.vbits)[(size_t)s * 16 + wid];
-    const bool valid = i < len && ((m >> lane) & 1ull);
     uint32_t dval = 0;
-    if (valid) dval = G(cams[k].depth)[y * cams[k].W + x0 + i];
-    __syncthreads();
-    uint32_t base = 0;
-    if (a.fused_prefix) {
-        for (int w = 0; w < nwaves; ++w) base += s_red[w];
-    } else {
-        base = G(a.seg_offsets)[s];
+    float xnv = 0.0f;
+    if (i < len) {
+        dval = G(cams[k].depth)[y * cams[k].W + x0 + i];
+        xnv = G(cams[k].xn)[x0 + i];
     }
+    const float ynv = G(cams[k].yn)[y];
+    const bool valid = i < len && ((m >> lane) & 1ull);
     uint32_t tot;
     const uint32_t wpre = wave_prefix(a, s, tot);
-    if (a.fused_prefix && s == gridDim.x - 1 && threadIdx.x == 0) *G(a.out_count) = base + tot;
+    const uint32_t sbase = a.fused_prefix ? 0u : G(a.seg_offsets)[s];
+    // run mode: this segment's first run (the scan over points then runs: minus all points)
+    uint32_t rbase = 0, rwpre = 0, rtot = 0;
+    if (a.run_mode) {
+        if (!a.fused_prefix)
+            rbase = G(a.seg_offsets)[a.total_segs + s] - G(a.seg_offsets)[a.total_segs];
+        for (int w = 0; w < nwaves; ++w) {
+            const uint32_t rc = G(a.wave_runs)[(size_t)s * 16 + w];
+            rwpre += (w < wid) ? rc : 0u;
+            rtot += rc;
+        }
+    }
+    __syncthreads();
+    uint32_t base = sbase;
+    if (a.fused_prefix)
+        for (int w = 0; w < nwaves; ++w) {
+            base += s_red[w];
+            rbase += s_red[16 + w];
+        }
+    if (s == gridDim.x - 1 && threadIdx.x == 0) {
+        *G(a.out_count) = base + tot;
+        if (a.run_mode) {  // the runs' end sentinel and count
+            G(a.run_start)[rbase + rtot] = base + tot;
+            *G(a.run_count) = rbase + rtot;
+        }
+    }
     const uint32_t fr = cams[k].frame;
     if (a.frame_pt_start && threadIdx.x == 0) {  // point range of each frame of a batch
         const bool first_of_frame =
@@ -958,21 +1043,34 @@ __global__ __launch_bounds__(1024) void k_emit(FrameArgs a) {
         const uint32_t pos = base + wpre + (uint32_t)__popcll(m & ltm);
         const uint32_t x = x0 + i;
         const float zz = (float)dval * cams[k].scale;
-        const float px = G(cams[k].xn)[x] * zz, py = G(cams[k].yn)[y] * zz, pz = zz;
+        const float px = xnv * zz, py = ynv * zz, pz = zz;
+        (void)x;
         const float4 w = make_float4(mrow(cams[k].Tw + 0, px, py, pz, 1.0f),
                                      mrow(cams[k].Tw + 4, px, py, pz, 1.0f),
                                      mrow(cams[k].Tw + 8, px, py, pz, 1.0f),
                                      mrow(cams[k].Tw + 12, px, py, pz, 1.0f));
         gst4(a.out_pts, pos, w);
         if (a.do_voxel) {
-            key = voxel_key(w.x, w.y, w.z, a.vlo, a.vcs, a.gmax, a.gs);
+            key = voxel_key(w.x, w.y, w.z, a.vlo, a.vcs, a.vrcs, a.gmax, a.gs);
             G(a.out_coords)[pos] = key;
+        }
+    }
+    if (a.run_mode) {  // run leaders: the sort key and first point of each run (k_mask's runs)
+        const unsigned long long below = m & ltm;
+        const int prev = below ? 63 - __clzll((long long)below) : -1;
+        const uint32_t pkey = __shfl(key, prev < 0 ? 0 : prev, 64);
+        const bool leader = valid && (prev < 0 || pkey != key);
+        const unsigned long long lm = __ballot(leader);
+        if (leader) {
+            const uint32_t ri = rbase + rwpre + (uint32_t)__popcll(lm & ltm);
+            G(a.run_keys)[ri] = key | (fr << a.frame_shift);
+            G(a.run_start)[ri] = base + wpre + (uint32_t)__popcll(m & ltm);
         }
     }
     if (a.do_voxel)
         mark_and_count(a, a.marks ? a.marks + (size_t)fr * a.mark_words : nullptr, valid, key,
-                       key | (fr << a.frame_shift), s_hist, s_mark);
-    flush_hist(a, s_hist);
+                       key | (fr << a.frame_shift), hist ? s_hist : nullptr, s_mark);
+    if (hist) flush_hist(a, s_hist);
 }
 
 // Selected rollbuffer points (insertSelectedPointSequence + transformPointSequence + crop +
@@ -1094,7 +1192,7 @@ __global__ __launch_bounds__(1024) void k_sel(FrameArgs a) {
             }
             gst4(a.sel_pts, pos, w);
             if (a.do_voxel) {
-                key = voxel_key(w.x, w.y, w.z, a.vlo, a.vcs, a.gmax, a.gs);
+                key = voxel_key(w.x, w.y, w.z, a.vlo, a.vcs, a.vrcs, a.gmax, a.gs);
                 G(a.sel_keys)[pos] = key;
             }
         }
@@ -1150,15 +1248,18 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
                 hipLaunchKernelGGL(k_mask<false>, dim3(a.total_segs), dim3(a.seg_threads), lds, s, a);
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
-        if (!a.fused_prefix) {
+        if (!a.fused_prefix) {  // (run mode: the point counts, then the run counts)
             HookScope hs(hook, GDF_KERNEL_SCAN);
-            const uint32_t chunks = (a.total_segs + 4095u) / 4096u;
-            uint32_t* partial = a.seg_offsets + scan_partials_offset(a.total_segs);
-            hipLaunchKernelGGL(k_scan_reduce, dim3(chunks), dim3(1024), 0, s, a.seg_counts,
-                               a.total_segs, partial, nullptr, 1u);
-            if ((e = hipGetLastError()) != hipSuccess) return e;
-            hipLaunchKernelGGL(k_scan_counts, dim3(chunks), dim3(1024), 0, s, a.seg_counts,
-                               a.total_segs, a.seg_offsets, a.out_count, partial, nullptr, 1u);
+            const uint32_t m = a.run_mode ? 2u * a.total_segs : a.total_segs;
+            const uint32_t chunks = (m + 4095u) / 4096u;
+            uint32_t* partial = a.seg_offsets + scan_partials_offset(m);
+            if (chunks > 1) {
+                hipLaunchKernelGGL(k_scan_reduce, dim3(chunks), dim3(1024), 0, s, a.seg_counts, m,
+                                   partial, nullptr, 1u);
+                if ((e = hipGetLastError()) != hipSuccess) return e;
+            }
+            hipLaunchKernelGGL(k_scan_counts, dim3(chunks), dim3(1024), 0, s, a.seg_counts, m,
+                               a.seg_offsets, a.scan_total, partial, nullptr, 1u);
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
         HookScope hs(hook, GDF_KERNEL_EMIT);
@@ -1529,7 +1630,7 @@ __global__ __launch_bounds__(256) void k_coords(const float4* __restrict__ pts,
     const uint32_t n = *count;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const float4 p = pts[i];
-        coords[i] = voxel_key(p.x, p.y, p.z, v.vlo, v.vcs, v.gmax, v.gs);
+        coords[i] = voxel_key(p.x, p.y, p.z, v.vlo, v.vcs, v.vrcs, v.gmax, v.gs);
     }
 }
 
@@ -1584,7 +1685,7 @@ __global__ __launch_bounds__(256) void k_sort_hist(const uint32_t* __restrict__ 
     __shared__ uint32_t s_h[4 * 256];
     __shared__ uint32_t s_fstart[kMaxCams + 1];
     for (uint32_t i = threadIdx.x; i < 4 * 256; i += 256) s_h[i] = 0;
-    load_fstart(s_fstart, fstart, nframes);
+    if (fstart) load_fstart(s_fstart, fstart, nframes);
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const uint32_t n = *count;
@@ -1595,7 +1696,7 @@ __global__ __launch_bounds__(256) void k_sort_hist(const uint32_t* __restrict__ 
         for (int q = 0; q < 4; ++q) {
             const uint32_t i = base + q * stride + threadIdx.x;
             k[q] = i < n ? keys[i] : 0u;
-            if (nframes > 1 && i < n) k[q] |= frame_of(s_fstart, nframes, i) << fshift;
+            if (nframes > 1 && fstart && i < n) k[q] |= frame_of(s_fstart, nframes, i) << fshift;
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -1675,7 +1776,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
     if (blockIdx.x >= tk.nblk) return;
     if (threadIdx.x == 0) s_epoch = read_epoch(epoch_word);
     // first pass of a batch: the frame index joins the key above its voxel bits
-    const bool add_frame = nframes > 1 && vin == nullptr;
+    const bool add_frame = nframes > 1 && vin == nullptr && fstart != nullptr;
     if (add_frame) load_fstart(s_fstart, fstart, nframes);
     // the digit bases do not depend on the tile
     s_base[threadIdx.x] = digit_base(ghist, s_wave);
@@ -2099,6 +2200,67 @@ __global__ __launch_bounds__(256) void k_group_big(const uint32_t* __restrict__ 
     }
 }
 
+// Runs of equal keys back to points: the sorted (run key, run) pairs become the sorted (key, point)
+// order k_group consumes - run r's points start[r] .. start[r+1]-1 in a row, keys repeated.
+// Tiles of 256 runs: block scan of the run lengths + ticketed decoupled look-back for the tile's
+// first point; the tile's points are written cooperatively (binary search of the run in LDS), so
+// the stores are coalesced.
+__global__ __launch_bounds__(256) void k_expand(const uint32_t* __restrict__ rkeys,
+                                                const uint32_t* __restrict__ rvals,
+                                                const uint32_t* __restrict__ rcount,
+                                                const uint32_t* __restrict__ run_start,
+                                                uint32_t* __restrict__ okeys,
+                                                uint32_t* __restrict__ ovals,
+                                                unsigned long long* status,
+                                                unsigned long long* gstatus, uint32_t* tile_ctr,
+                                                uint32_t* epoch_word, uint32_t* err) {
+    __shared__ uint32_t s_off[257], s_ps[256], s_key[256];
+    __shared__ uint32_t s_wave[4], s_tile, s_epoch, s_base;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t R = *rcount;
+    const uint32_t ntiles = (R + 255u) / 256u;
+    const Tickets tk = tickets(ntiles, gridDim.x);
+    if (blockIdx.x >= tk.nblk) return;
+    if (threadIdx.x == 0) s_epoch = read_epoch(epoch_word);
+    for (bool first = true;; first = false) {  // persistent: tiles in ticket order
+        if (!first && tk.oneshot) return;
+        if (threadIdx.x == 0) s_tile = next_ticket(tile_ctr, tk, epoch_word, s_epoch);
+        __syncthreads();
+        const uint32_t tile = s_tile, epoch = s_epoch;
+        if (tile >= ntiles) return;  // block-uniform
+        const uint32_t i = tile * 256u + threadIdx.x;
+        uint32_t key = 0, ps = 0, len = 0;
+        if (i < R) {
+            key = rkeys[i];
+            const uint32_t v = rvals[i];
+            ps = run_start[v];
+            len = run_start[v + 1] - ps;
+        }
+        uint32_t total;
+        const uint32_t off = block_exclusive_scan(len, total, s_wave);
+        s_off[threadIdx.x] = off;
+        s_ps[threadIdx.x] = ps;
+        s_key[threadIdx.x] = key;
+        if (threadIdx.x == 0) s_off[256] = total;
+        if (wid == 0) {
+            const uint32_t ex = lookback2_wave(status, gstatus, tile, ntiles, total, epoch, err);
+            if (lane == 0) s_base = ex;
+        }
+        __syncthreads();
+        const uint32_t base = s_base;
+        for (uint32_t q = threadIdx.x; q < total; q += 256u) {
+            uint32_t lo = 0, hi = 256;  // last run with s_off <= q (a run holds >= 1 point)
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_off[mid] <= q) lo = mid; else hi = mid;
+            }
+            okeys[base + q] = s_key[lo];
+            ovals[base + q] = s_ps[lo] + (q - s_off[lo]);
+        }
+        __syncthreads();  // LDS reused by the next tile
+    }
+}
+
 size_t voxelize_status_words(uint32_t nmax) {
     return (size_t)((nmax + kSortThreads * 4 - 1) / (kSortThreads * 4) + 1) * 256;
 }
@@ -2141,6 +2303,7 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
     const uint32_t* vin = nullptr;
     uint32_t* kbuf[2] = {a.keys_a, a.keys_b};
     uint32_t* vbuf[2] = {a.vals_a, a.vals_b};
+    const bool runs = a.run_start != nullptr;  // keys are run keys: sort runs, then expand
     for (uint32_t p = 0; p < npasses; ++p) {
         const uint32_t remaining = a.key_bits > 8 * p ? a.key_bits - 8 * p : 0u;
         const uint32_t dbits = remaining >= 8 ? 8u : (remaining ? remaining : 1u);
@@ -2157,6 +2320,20 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
         kin = kbuf[p & 1];
         vin = vbuf[p & 1];
     }
+    const uint32_t* gcount = a.count;  // items of the group phase
+    if (runs) {
+        HookScope hs(hook, GDF_KERNEL_SORT);  // (accounted with the sort: the last step of it)
+        const uint32_t max_rt = std::min<uint32_t>((a.nmax + 255u) / 256u, kPersistBlocks);
+        hipLaunchKernelGGL(k_expand, dim3(std::max<uint32_t>(max_rt, 1u)), dim3(256), 0, s, kin,
+                           vin, a.count, a.run_start, kbuf[npasses & 1], vbuf[npasses & 1],
+                           a.gstatus, a.ggstatus,
+                           reinterpret_cast<uint32_t*>(a.ctrs + kCtrExpand),
+                           reinterpret_cast<uint32_t*>(a.ctrs + kCtrEpoch), a.err);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        kin = kbuf[npasses & 1];
+        vin = vbuf[npasses & 1];
+        gcount = a.point_count;
+    }
     const uint32_t max_tiles = (a.nmax + kGroupThreads - 1) / kGroupThreads;
     const uint32_t group_tiles = std::min<uint32_t>(max_tiles, kPersistBlocks);
     HookScope hs(hook, GDF_KERNEL_GROUP);
@@ -2166,24 +2343,24 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
     if (a.group_counts && max_tiles > g_group_scan_tiles) {
         // many tiles: their group-id offsets from a count + scan instead of one ticket each
         // (a single ticket counter serves ~10^2 draws per microsecond)
-        hipLaunchKernelGGL(k_group_count, dim3(group_tiles), dim3(256), 0, s, kin, a.count,
+        hipLaunchKernelGGL(k_group_count, dim3(group_tiles), dim3(256), 0, s, kin, gcount,
                            a.group_counts);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         const uint32_t chunks = (max_tiles + 4095u) / 4096u;
         uint32_t* partial = a.group_offsets + scan_partials_offset(max_tiles);
         if (chunks > 1) {  // (one chunk: k_scan_counts reads no partials)
             hipLaunchKernelGGL(k_scan_reduce, dim3(chunks), dim3(1024), 0, s, a.group_counts,
-                               max_tiles, partial, a.count, (uint32_t)kGroupThreads);
+                               max_tiles, partial, gcount, (uint32_t)kGroupThreads);
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
         hipLaunchKernelGGL(k_scan_counts, dim3(chunks), dim3(1024), 0, s, a.group_counts,
-                           max_tiles, a.group_offsets, (uint32_t*)nullptr, partial, a.count,
+                           max_tiles, a.group_offsets, (uint32_t*)nullptr, partial, gcount,
                            (uint32_t)kGroupThreads);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         tile_base = a.group_offsets;
     }
     hipLaunchKernelGGL(k_group, dim3(group_tiles ? group_tiles : 1), dim3(kGroupThreads), 0, s, kin,
-                       vin, a.count, a.pts, reinterpret_cast<float*>(a.out), a.out_count,
+                       vin, gcount, a.pts, reinterpret_cast<float*>(a.out), a.out_count,
                        a.gstatus, a.ggstatus, reinterpret_cast<uint32_t*>(a.ctrs + kCtrGroup),
                        reinterpret_cast<uint32_t*>(a.ctrs + kCtrEpoch), a.err, a.hist, a.average,
                        a.vp, a.group_marks, tile_base, tile_base ? a.bigq : nullptr,

@@ -16,6 +16,7 @@ struct LaunchHook {
 struct VoxelParams {
     float vlo[3], vcs[3], gmax[3];
     uint32_t gs[3];
+    float vrcs[3];  // RN(1 / vcs)
 };
 
 // per-camera ray factors xn[u] = (u - cx)/fx, yn[v] = (v - cy)/fy
@@ -104,6 +105,11 @@ struct VoxelizeArgs {
     uint64_t mark_words;
     uint8_t* snapshots;
     uint64_t snapshot_bytes;
+    // runs of equal keys (depth-only frames): keys / count are the run keys / run count, the
+    // sort orders runs, k_expand turns them back into the sorted (key, point) order over
+    // point_count points (run r = points run_start[r] .. run_start[r+1]-1)
+    const uint32_t* run_start;
+    const uint32_t* point_count;
     uint64_t ncells;
     uint32_t lifetime;
     uint32_t* err;

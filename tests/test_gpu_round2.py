@@ -354,3 +354,32 @@ def test_transform_points_matches_oracle(Engine):
     got = do.to_numpy(np.float32, 4 * n).reshape(n, 4)
     want = transform_points(pts, mask, T, init)
     assert np.array_equal(bits(got), bits(want))
+
+
+def test_run_mode_small_frames_forced(Engine, monkeypatch):
+    """The runs-of-equal-keys voxelize (on by default from 2 Mi pixels, 4K is covered above) at
+    small sizes through GDF_FORCE_RUNS: single frames with two cameras (the runs stop at camera
+    borders), a 3-frame batch (frame bits in the run keys), voxel corners - bit-exact."""
+    monkeypatch.setenv("GDF_FORCE_RUNS", "1")
+    gpu, orc = Engine(), OracleFusion(threads=8)
+    cams = [synth.make_camera(k, 320, 240) for k in range(2)]
+    for avg in (True, False):
+        p = ComponentParams()
+        p.voxel_average = avg
+        for f in range(2):
+            args = [cam_args(c, synth.dense_frame(c, k, f)) for k, c in enumerate(cams)]
+            run_fused(gpu, args, p)
+            run_fused(orc, args, p)
+            compare_results(gpu, orc, tag=f"avg={avg} frame {f}")
+    p = ComponentParams()
+    frames = [[cam_args(cams[0], synth.dense_frame(cams[0], 0, 10 + j))] for j in range(3)]
+    _batch(gpu, frames, p)
+    pts, vox = gpu.downloadPoints(), gpu.downloadVoxelizedPoints()
+    ps, vs = gpu.batch_ranges()
+    for j in range(3):
+        run_fused(orc, frames[j], p)
+        assert np.array_equal(bits(pts[ps[j]:ps[j + 1]]), bits(orc.downloadPoints()))
+        assert np.array_equal(bits(vox[vs[j]:vs[j + 1], :3]),
+                              bits(orc.downloadVoxelizedPoints()[:, :3]))
+        np.testing.assert_array_equal(gpu.downloadBatchVoxelOccupancyGrid(j),
+                                      orc.downloadVoxelOccupancyGrid())
