@@ -149,6 +149,9 @@ struct FrameArgs {
     uint32_t* run_start;        // [runs + 1] first point of each run; [runs] = points
     uint32_t* run_count;        // runs of the frame (device)
     uint32_t* scan_total;       // scratch total of the segment-count scan
+    uint32_t* sel_runkeys;      // run mode with rollbuffer points: staged run records per tile
+    uint32_t* sel_runstart;     //   (tile-local first point)
+    uint32_t* run_total;        // runs of depth + rollbuffer points (k_sel_place)
 };
 static_assert(sizeof(FrameArgs) <= 4096, "kernel arguments are limited to 4 KiB");
 

@@ -177,7 +177,7 @@ bool ros_time_minus(uint32_t sec, uint32_t nsec, double seconds, uint32_t* os, u
 
 enum MiscSlot {
     kCount = 0, kTileCtr = 1, kErr = 2, kVoxCount = 3, kGridTicket = 4, kDepthCount = 5,
-    kSelTotal = 6, kPartTotal = 7, kRecvCount = 8, kRunCount = 9, kScanTotal = 10, kMiscWords = 16
+    kSelTotal = 6, kPartTotal = 7, kRecvCount = 8, kRunCount = 9, kScanTotal = 10, kRunTotal = 11, kMiscWords = 16
 };
 
 }  // namespace
@@ -204,6 +204,7 @@ struct Slot {
     bool khist_pending = false;     // accumulated by the fused compaction, not yet consumed
     DevBuf d_pts, d_coords, d_stage, d_vbits, d_tcounts, d_toffsets;
     DevBuf d_selpts, d_selkeys, d_selcnt, d_seloff;  // rollbuffer compaction (k_sel)
+    DevBuf d_selrk, d_selrs;                         // k_sel's staged runs (run mode)
     DevBuf d_misc;
     uint32_t* h_misc = nullptr;     // pinned
     bool compacted = false, coords_valid = false, marks_set = false;
@@ -219,7 +220,8 @@ struct Slot {
     DevBuf d_fstart, d_fvox;        // batch: first point / first voxel of each frame [nframes + 1]
     DevBuf d_snap;                  // batch: the u8 grid after each frame but the last
     DevBuf d_pcnt, d_poff;          // multi-GPU key-range partition workspace
-    DevBuf d_wruns, d_runkeys, d_runstart;  // runs of equal keys (depth-only frames)
+    DevBuf d_wruns, d_runkeys, d_runstart;  // runs of equal keys
+    bool runs_sel = false;          // ... counted in kRunTotal (frame with rollbuffer points)
     bool runs_valid = false;        // this frame's voxelize may sort runs
     uint32_t nframes = 1;           // frames of the slot's last processed batch
     uint32_t n_total = 0;
@@ -974,8 +976,8 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel) {
         Slot& q = e->sl();
         q.d_selpts.ensure((size_t)a.sel_tiles * a.sel_tile * 16);
         q.d_selkeys.ensure((size_t)a.sel_tiles * a.sel_tile * 4);
-        q.d_selcnt.ensure((size_t)a.sel_tiles * 4);
-        q.d_seloff.ensure(seg_offsets_words(a.sel_tiles) * 4);
+        q.d_selcnt.ensure((size_t)a.sel_tiles * 2 * 4);  // point counts, then run counts
+        q.d_seloff.ensure(seg_offsets_words(2 * a.sel_tiles) * 4);
         a.sel_counts = q.d_selcnt.as<uint32_t>();
         a.sel_offsets = q.d_seloff.as<uint32_t>();
         a.sel_pts = q.d_selpts.as<float4>();
@@ -1027,12 +1029,15 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel) {
         // counts the runs and their key digits (one flush per segment: few runs, few bins)
         // (measured on MI355X, dense frames: 4K 18.2 -> 24.0 Gpoints/s; at VGA the extra key in
         // k_mask costs what the shorter sort saves, so frames under 2 Mi pixels sort points)
-        a.run_mode = e->use_runs && !a.sel_tiles && a.total_segs &&
-                             (e->force_runs || a.depth_total >= (1u << 21)) ? 1 : 0;
+        // Rollbuffer windows (10^7 points re-observing the same voxels) always sort runs: k_sel
+        // counts them per tile.
+        a.run_mode = e->use_runs && (a.sel_tiles || (a.total_segs && (e->force_runs ||
+                                                                      a.depth_total >= (1u << 21))))
+                         ? 1 : 0;
         // the run-key digits: k_mask's per-segment flush while there are few segments; above,
         // k_sort_hist over the runs (tens of thousands of flushes contend at the atomic units)
         if (a.run_mode)
-            a.key_hist = a.total_segs <= kFusedPrefixSegs && !e->run_hist_in_sort
+            a.key_hist = a.total_segs <= kFusedPrefixSegs && !e->run_hist_in_sort && !a.sel_tiles
                              ? e->sl().d_khist.as<uint32_t>() : nullptr;
     }
     a.out_pts = e->sl().d_pts.as<float4>();
@@ -1055,7 +1060,15 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel) {
         a.run_keys = q.d_runkeys.as<uint32_t>();
         a.run_start = q.d_runstart.as<uint32_t>();
         a.run_count = q.d_misc.as<uint32_t>() + kRunCount;
+        if (a.sel_tiles) {
+            q.d_selrk.ensure((size_t)a.sel_tiles * a.sel_tile * 4);
+            q.d_selrs.ensure((size_t)a.sel_tiles * a.sel_tile * 4);
+            a.sel_runkeys = q.d_selrk.as<uint32_t>();
+            a.sel_runstart = q.d_selrs.as<uint32_t>();
+            a.run_total = q.d_misc.as<uint32_t>() + kRunTotal;
+        }
     }
+    e->sl().runs_sel = a.run_mode && a.sel_tiles;
     a.vbits = e->sl().d_vbits.as<unsigned long long>();
     a.seg_counts = e->sl().d_tcounts.as<uint32_t>();
     a.seg_offsets = e->sl().d_toffsets.as<uint32_t>();
@@ -1159,7 +1172,7 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime,
         v.count = e->sl().d_misc.as<uint32_t>() + kRecvCount;
     } else if (e->sl().runs_valid) {  // sort the frame's runs of equal keys, then expand
         v.keys = e->sl().d_runkeys.as<uint32_t>();
-        v.count = e->sl().d_misc.as<uint32_t>() + kRunCount;
+        v.count = e->sl().d_misc.as<uint32_t>() + (e->sl().runs_sel ? kRunTotal : kRunCount);
         v.run_start = e->sl().d_runstart.as<uint32_t>();
         v.point_count = e->sl().d_misc.as<uint32_t>() + kCount;
     }

@@ -1085,6 +1085,7 @@ template <uint32_t kSegs>
 __global__ __launch_bounds__(1024) void k_sel(FrameArgs a) {
     constexpr uint32_t kSelSegs = kSegs;
     __shared__ uint32_t s_wc[kSelSegs * 16];  // kept items per (segment j, wave w), j-major
+    __shared__ uint32_t s_rc[kSelSegs * 16];  // run mode: runs per (segment j, wave w)
     static_assert(kSelSegs * 16 <= 256, "k_sel scan covers 256 entries");
     __shared__ uint32_t s_mark[1u << kMarkCacheBits];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1140,6 +1141,18 @@ __global__ __launch_bounds__(1024) void k_sel(FrameArgs a) {
         }
     }
     uint32_t keep = 0;  // bit j: item j of this thread survives the crop
+    const unsigned long long ltm = lanemask_lt();
+    const gptr<const float> T0 = G(a.tfw + 16 * (size_t)g.tf0);
+    // the world point of selected item j (transform_points_indirect, world matrix)
+    auto world = [&](uint32_t j) {
+        const uint32_t si = si0 + j * B + i;
+        const float x = p[j].x, y = p[j].y, z = p[j].z;
+        const gptr<const float> Tw =
+            one_seq || si < g.next ? T0 : G(a.tfw + 16 * (size_t)sel_tf(a, si));
+        return make_float4(mrow(Tw + 0, x, y, z, 1.0f), mrow(Tw + 4, x, y, z, 1.0f),
+                           mrow(Tw + 8, x, y, z, 1.0f), mrow(Tw + 12, x, y, z, 1.0f));
+    };
+    uint32_t rlead = 0;  // run mode: bit j - item j starts a run of equal keys in its wave
 #pragma unroll
     for (uint32_t j = 0; j < kSelSegs; ++j) {
         const uint32_t si = si0 + j * B + i;
@@ -1147,30 +1160,44 @@ __global__ __launch_bounds__(1024) void k_sel(FrameArgs a) {
         keep |= ((bits[j] >> 2) & 1u) << j;
         const unsigned long long m = __ballot((bits[j] & 4u) != 0u);
         if (lane == 0) s_wc[j * nwaves + wid] = (uint32_t)__popcll(m);
+        if (a.run_mode) {
+            uint32_t key = 0xFFFFFFFFu;
+            if (bits[j] & 4u) {
+                const float4 w = world(j);
+                key = voxel_key(w.x, w.y, w.z, a.vlo, a.vcs, a.vrcs, a.gmax, a.gs);
+            }
+            const unsigned long long below = m & ltm;
+            const int prev = below ? 63 - __clzll((long long)below) : -1;
+            const uint32_t pkey = __shfl(key, prev < 0 ? 0 : prev, 64);
+            const bool leader = ((bits[j] & 4u) != 0u) && (prev < 0 || pkey != key);
+            rlead |= (uint32_t)leader << j;
+            const unsigned long long lm = __ballot(leader);
+            if (lane == 0) s_rc[j * nwaves + wid] = (uint32_t)__popcll(lm);
+        }
     }
     __syncthreads();
-    // exclusive scan of the (segment, wave) counts in item order by wave 0 (<= 256 entries)
+    // exclusive scans of the (segment, wave) counts in item order: points by wave 0, runs by
+    // wave 1 (<= 256 entries each)
     const uint32_t ne = kSelSegs * (uint32_t)nwaves;
-    if (wid == 0) {
+    if (wid == 0 || (wid == 1 && a.run_mode)) {
+        uint32_t* sc = wid == 0 ? s_wc : s_rc;
         uint32_t carry = 0;
         for (uint32_t e0 = 0; e0 < ne; e0 += 64) {  // uniform
             const uint32_t e = e0 + (uint32_t)lane;
-            const uint32_t v = e < ne ? s_wc[e] : 0u;
+            const uint32_t v = e < ne ? sc[e] : 0u;
             uint32_t x = v;
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
                 const uint32_t y = __shfl_up(x, o, 64);
                 if (lane >= o) x += y;
             }
-            if (e < ne) s_wc[e] = carry + x - v;
+            if (e < ne) sc[e] = carry + x - v;
             carry += __shfl(x, 63, 64);
         }
-        if (lane == 0) G(a.sel_counts)[tile] = carry;
+        if (lane == 0) G(a.sel_counts)[(wid == 0 ? 0u : a.sel_tiles) + tile] = carry;
     }
     __syncthreads();
     const uint64_t base = (uint64_t)tile * kSelSegs * B;  // the tile's staging slots
-    const unsigned long long ltm = lanemask_lt();
-    const gptr<const float> T0 = G(a.tfw + 16 * (size_t)g.tf0);
 #pragma unroll
     for (uint32_t j = 0; j < kSelSegs; ++j) {
         const bool valid = (keep >> j) & 1u;
@@ -1178,22 +1205,22 @@ __global__ __launch_bounds__(1024) void k_sel(FrameArgs a) {
         if (!m) continue;  // wave-uniform
         uint32_t key = 0xFFFFFFFFu;
         if (valid) {
-            const uint32_t si = si0 + j * B + i;
-            const uint64_t pos = base + s_wc[j * nwaves + wid] + (uint32_t)__popcll(m & ltm);
-            const float x = p[j].x, y = p[j].y, z = p[j].z;
-            float4 w;
-            if (one_seq) {
-                w = make_float4(mrow(T0 + 0, x, y, z, 1.0f), mrow(T0 + 4, x, y, z, 1.0f),
-                                mrow(T0 + 8, x, y, z, 1.0f), mrow(T0 + 12, x, y, z, 1.0f));
-            } else {  // (rare: a tile reaching into the next sequence)
-                const gptr<const float> Tw = si < g.next ? T0 : G(a.tfw + 16 * (size_t)sel_tf(a, si));
-                w = make_float4(mrow(Tw + 0, x, y, z, 1.0f), mrow(Tw + 4, x, y, z, 1.0f),
-                                mrow(Tw + 8, x, y, z, 1.0f), mrow(Tw + 12, x, y, z, 1.0f));
-            }
+            const uint32_t local = s_wc[j * nwaves + wid] + (uint32_t)__popcll(m & ltm);
+            const uint64_t pos = base + local;
+            const float4 w = world(j);
             gst4(a.sel_pts, pos, w);
             if (a.do_voxel) {
                 key = voxel_key(w.x, w.y, w.z, a.vlo, a.vcs, a.vrcs, a.gmax, a.gs);
                 G(a.sel_keys)[pos] = key;
+            }
+        }
+        if (a.run_mode) {  // the run records at tile-local run ranks: key, tile-local first point
+            const bool lead = (rlead >> j) & 1u;
+            const unsigned long long lm = __ballot(lead);
+            if (lead) {
+                const uint64_t rpos = base + s_rc[j * nwaves + wid] + (uint32_t)__popcll(lm & ltm);
+                G(a.sel_runkeys)[rpos] = key;
+                G(a.sel_runstart)[rpos] = s_wc[j * nwaves + wid] + (uint32_t)__popcll(m & ltm);
             }
         }
         if (a.do_voxel && a.marks) mark_and_count(a, a.marks, valid, key, key, nullptr, s_mark);
@@ -1203,9 +1230,23 @@ __global__ __launch_bounds__(1024) void k_sel(FrameArgs a) {
 // Each tile's staged survivors behind the depth survivors, at the tile's scanned offset
 // (m_points order: depth points first, fusion.cpp:1525,1559), and the frame's total count.
 // A persistent grid walks the tiles; empty tiles cost one load.
+// Run mode: the tiles' run records behind the depth runs (run r of tile t at depth runs + the
+// tile's scanned run offset; its first point at the tile's placed offset + its tile-local
+// start), the frame's run count and the runs' end sentinel.  The counts were scanned as
+// [points of every tile | runs of every tile]: a tile's run offset is its scanned value minus
+// the selection's points.
 __global__ __launch_bounds__(256) void k_sel_place(FrameArgs a) {
     const uint32_t d = *G(a.out_count);
-    if (blockIdx.x == 0 && threadIdx.x == 0) *G(a.final_count) = d + *G(a.sel_total);
+    const uint32_t selp = a.run_mode ? G(a.sel_offsets)[a.sel_tiles] : *G(a.sel_total);
+    const uint32_t rd = a.run_mode ? *G(a.run_count) : 0u;  // depth runs (k_emit)
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        *G(a.final_count) = d + selp;
+        if (a.run_mode) {
+            const uint32_t rtot = rd + (*G(a.sel_total) - selp);
+            *G(a.run_total) = rtot;
+            G(a.run_start)[rtot] = d + selp;
+        }
+    }
     const uint32_t tile_items = a.sel_tile;
     for (uint32_t t = blockIdx.x; t < a.sel_tiles; t += gridDim.x) {
         const uint32_t c = G(a.sel_counts)[t];
@@ -1215,6 +1256,14 @@ __global__ __launch_bounds__(256) void k_sel_place(FrameArgs a) {
         for (uint32_t r = threadIdx.x; r < c; r += blockDim.x) {
             gst4(a.out_pts, (uint64_t)o + r, gld4(a.sel_pts, src + r));
             if (a.do_voxel) G(a.out_coords)[o + r] = G(a.sel_keys)[src + r];
+        }
+        if (a.run_mode) {
+            const uint32_t cr = G(a.sel_counts)[a.sel_tiles + t];
+            const uint32_t ro = rd + (G(a.sel_offsets)[a.sel_tiles + t] - selp);
+            for (uint32_t r = threadIdx.x; r < cr; r += blockDim.x) {
+                G(a.run_keys)[ro + r] = G(a.sel_runkeys)[src + r];
+                G(a.run_start)[ro + r] = o + G(a.sel_runstart)[src + r];
+            }
         }
     }
 }
@@ -1234,6 +1283,7 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
     hipError_t e;
     if (a.total_segs == 0) {  // no depth survivors to count
         if ((e = hipMemsetAsync(a.out_count, 0, 4, s)) != hipSuccess) return e;
+        if (a.run_mode && (e = hipMemsetAsync(a.run_count, 0, 4, s)) != hipSuccess) return e;
         if (a.grid_seq_out && !a.sel_tiles &&  // no kernel of this frame stores the ticket
             (e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(a.grid_seq_out),
                                    (int)a.grid_seq, 1, s)) != hipSuccess)
@@ -1276,15 +1326,16 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
         else
             hipLaunchKernelGGL(k_sel<8>, dim3(a.sel_tiles), dim3(thr), 0, s, a);
         if ((e = hipGetLastError()) != hipSuccess) return e;
-        const uint32_t chunks = (a.sel_tiles + 4095u) / 4096u;
-        uint32_t* partial = a.sel_offsets + scan_partials_offset(a.sel_tiles);
+        const uint32_t sm = a.run_mode ? 2u * a.sel_tiles : a.sel_tiles;  // (+ run counts)
+        const uint32_t chunks = (sm + 4095u) / 4096u;
+        uint32_t* partial = a.sel_offsets + scan_partials_offset(sm);
         if (chunks > 1) {
-            hipLaunchKernelGGL(k_scan_reduce, dim3(chunks), dim3(1024), 0, s, a.sel_counts,
-                               a.sel_tiles, partial, nullptr, 1u);
+            hipLaunchKernelGGL(k_scan_reduce, dim3(chunks), dim3(1024), 0, s, a.sel_counts, sm,
+                               partial, nullptr, 1u);
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
-        hipLaunchKernelGGL(k_scan_counts, dim3(chunks), dim3(1024), 0, s, a.sel_counts,
-                           a.sel_tiles, a.sel_offsets, a.sel_total, partial, nullptr, 1u);
+        hipLaunchKernelGGL(k_scan_counts, dim3(chunks), dim3(1024), 0, s, a.sel_counts, sm,
+                           a.sel_offsets, a.sel_total, partial, nullptr, 1u);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         hipLaunchKernelGGL(k_sel_place, dim3(std::min<uint32_t>(a.sel_tiles, 4096u)), dim3(256), 0,
                            s, a);
