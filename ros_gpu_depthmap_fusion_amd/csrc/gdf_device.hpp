@@ -35,8 +35,9 @@ constexpr uint32_t kMaxParts = 16;                          // ranks of the fuse
 // Device-wide counters: monotonically increasing tile tickets (the host passes each launch's
 // base, so no per-launch memset) and the global digit histogram of the voxel keys.
 // per-stream device counters (u64 words, low 32 bits used): tile tickets, look-back epoch
-enum CounterSlot { kCtrSel = 0, kCtrSort0 = 1, kCtrGroup = 5, kCtrEpoch = 6, kCtrExpand = 7,
-                   kCtrSlots = 8 };
+enum CounterSlot { kCtrSel = 0, kCtrSort0 = 1, kCtrGroup = 5, kCtrEpoch = 6,
+                   kCtrRunQueue = 7,  // (+ word 8) run-group queue: appends, draws, blocks done
+                   kCtrSlots = 9 };
 
 // engine-order of historic-grid updates across streams (grid_seq_enter / grid_seq_leave)
 struct GridSeq {
@@ -98,16 +99,15 @@ struct FrameArgs {
     const uint32_t* seg_tf;     // transform index of that sequence
     const float* tfw;           // row-major T_world_move·T_move per selected sequence
     const float* tfc;
-    // rollbuffer compaction (k_sel): tiles of kSelSegs * kSelThreads points, survivors staged at
-    // tile-local ranks, then placed by tile offsets (k_sel_place) behind the depth points
+    // rollbuffer compaction (k_sel): tiles of kSelSegs * kSelThreads points in ticket order, their
+    // survivors placed behind the depth points by decoupled look-backs over the tiles
     uint32_t sel_tiles;
     uint32_t sel_tile;          // points per tile = sel_segs * k_sel block size
     uint32_t sel_segs;
-    uint32_t* sel_counts;       // [sel_tiles] survivors per tile
-    uint32_t* sel_offsets;      // [seg_offsets_words(sel_tiles)] exclusive scan (+ scan partials)
-    float4* sel_pts;            // staged survivors: tile t's at [t * tile, + count) ...
-    uint32_t* sel_keys;         // ... and their voxel keys
-    uint32_t* sel_total;        // survivors of the selection
+    unsigned long long* sel_status;  // look-back granules: 2 channels (points, runs) x
+                                     // 2 * (tiles + tiles / 64 + 2) words (tiles, then groups)
+    uint32_t* sel_ctr;          // tile tickets
+    uint32_t* epoch_word;       // look-back epoch (shared with the voxelize launches)
     uint32_t* final_count;      // depth + rollbuffer survivors (out_count then holds the depth part)
     // voxel keys + occupancy marks (compute_voxel_coords + voxel_grid_occupancy_of_points)
     int32_t do_voxel;
@@ -149,9 +149,7 @@ struct FrameArgs {
     uint32_t* run_start;        // [runs + 1] first point of each run; [runs] = points
     uint32_t* run_count;        // runs of the frame (device)
     uint32_t* scan_total;       // scratch total of the segment-count scan
-    uint32_t* sel_runkeys;      // run mode with rollbuffer points: staged run records per tile
-    uint32_t* sel_runstart;     //   (tile-local first point)
-    uint32_t* run_total;        // runs of depth + rollbuffer points (k_sel_place)
+    uint32_t* run_total;        // runs of depth + rollbuffer points (k_sel's last tile)
 };
 static_assert(sizeof(FrameArgs) <= 4096, "kernel arguments are limited to 4 KiB");
 

@@ -203,8 +203,7 @@ struct Slot {
     DevBuf d_khist;                 // digit histogram of the voxel keys [4*256]
     bool khist_pending = false;     // accumulated by the fused compaction, not yet consumed
     DevBuf d_pts, d_coords, d_stage, d_vbits, d_tcounts, d_toffsets;
-    DevBuf d_selpts, d_selkeys, d_selcnt, d_seloff;  // rollbuffer compaction (k_sel)
-    DevBuf d_selrk, d_selrs;                         // k_sel's staged runs (run mode)
+    DevBuf d_selstat;  // k_sel's look-back granules
     DevBuf d_misc;
     uint32_t* h_misc = nullptr;     // pinned
     bool compacted = false, coords_valid = false, marks_set = false;
@@ -974,15 +973,11 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel) {
     a.sel_tiles = (uint32_t)(((uint64_t)sel + a.sel_tile - 1) / a.sel_tile);
     if (a.sel_tiles) {  // rollbuffer compaction (k_sel) + placement behind the depth points
         Slot& q = e->sl();
-        q.d_selpts.ensure((size_t)a.sel_tiles * a.sel_tile * 16);
-        q.d_selkeys.ensure((size_t)a.sel_tiles * a.sel_tile * 4);
-        q.d_selcnt.ensure((size_t)a.sel_tiles * 2 * 4);  // point counts, then run counts
-        q.d_seloff.ensure(seg_offsets_words(2 * a.sel_tiles) * 4);
-        a.sel_counts = q.d_selcnt.as<uint32_t>();
-        a.sel_offsets = q.d_seloff.as<uint32_t>();
-        a.sel_pts = q.d_selpts.as<float4>();
-        a.sel_keys = q.d_selkeys.as<uint32_t>();
-        a.sel_total = q.d_misc.as<uint32_t>() + kSelTotal;
+        // (epoch-tagged granules: zeroed once when allocated, never between frames)
+        q.d_selstat.ensure_zero((size_t)4 * (a.sel_tiles + a.sel_tiles / 64 + 2) * 8, e->s());
+        a.sel_status = q.d_selstat.as<unsigned long long>();
+        a.sel_ctr = reinterpret_cast<uint32_t*>(q.d_ctrs.as<unsigned long long>() + kCtrSel);
+        a.epoch_word = reinterpret_cast<uint32_t*>(q.d_ctrs.as<unsigned long long>() + kCtrEpoch);
     }
     a.do_flying = e->flying_set ? 1 : 0;
     a.F = e->F;
@@ -1042,7 +1037,7 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel) {
     }
     a.out_pts = e->sl().d_pts.as<float4>();
     a.out_coords = e->sl().d_coords.as<uint32_t>();
-    // with rollbuffer points the depth compaction counts into kDepthCount and k_sel_place writes
+    // with rollbuffer points the depth compaction counts into kDepthCount and k_sel writes
     // the frame's total
     a.out_count = e->sl().d_misc.as<uint32_t>() + (a.sel_tiles ? kDepthCount : kCount);
     a.final_count = e->sl().d_misc.as<uint32_t>() + kCount;
@@ -1060,13 +1055,7 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel) {
         a.run_keys = q.d_runkeys.as<uint32_t>();
         a.run_start = q.d_runstart.as<uint32_t>();
         a.run_count = q.d_misc.as<uint32_t>() + kRunCount;
-        if (a.sel_tiles) {
-            q.d_selrk.ensure((size_t)a.sel_tiles * a.sel_tile * 4);
-            q.d_selrs.ensure((size_t)a.sel_tiles * a.sel_tile * 4);
-            a.sel_runkeys = q.d_selrk.as<uint32_t>();
-            a.sel_runstart = q.d_selrs.as<uint32_t>();
-            a.run_total = q.d_misc.as<uint32_t>() + kRunTotal;
-        }
+        if (a.sel_tiles) a.run_total = q.d_misc.as<uint32_t>() + kRunTotal;
     }
     e->sl().runs_sel = a.run_mode && a.sel_tiles;
     a.vbits = e->sl().d_vbits.as<unsigned long long>();
@@ -1159,7 +1148,11 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime,
     const uint32_t gtiles = (uint32_t)voxelize_group_tiles(nmax);
     e->sl().d_gcnt.ensure((size_t)gtiles * 4);
     e->sl().d_goff.ensure(seg_offsets_words(gtiles) * 4);
-    e->sl().d_bigq.ensure((size_t)(gtiles + 2048) * 16);  // <= 1 long voxel per tile
+    // point mode: <= 1 long voxel per tile; run mode: one queue entry per long group, at most
+    // one per voxel of the batch
+    const uint64_t qcap = std::min<uint64_t>(nmax, (uint64_t)std::max<uint32_t>(e->nframes, 1) * e->ncells);
+    const uint64_t bigq_n = std::max<uint64_t>((uint64_t)gtiles + 2048, qcap);
+    e->sl().d_bigq.ensure((size_t)bigq_n * 16);
     e->sl().d_bigcnt.ensure(2048 * 4);
     VoxelizeArgs v;
     std::memset(&v, 0, sizeof(v));
@@ -1196,6 +1189,7 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime,
     v.group_counts = e->sl().d_gcnt.as<uint32_t>();
     v.group_offsets = e->sl().d_goff.as<uint32_t>();
     v.bigq = e->sl().d_bigq.as<uint4>();
+    v.bigq_cap = (uint32_t)std::min<uint64_t>(bigq_n, 0xFFFFFFFFu);
     v.bigcnt = e->sl().d_bigcnt.as<uint32_t>();
     v.sort_pt = e->sort_pt ? e->sort_pt : nmax <= (1u << 20) ? 4 : nmax <= (1u << 24) ? 8 : 16;
     v.err = e->sl().d_misc.as<uint32_t>() + kErr;
@@ -1410,6 +1404,10 @@ int gdf_create(int device, gdf_engine** out) {
         if (const char* v = std::getenv("GDF_SORT_PT")) e->sort_pt = std::atoi(v);  // tuning knob
         if (const char* v = std::getenv("GDF_GROUP_SCAN_TILES"))                   // tuning knob
             g_group_scan_tiles = (uint32_t)std::max(1, std::atoi(v));
+        if (const char* v = std::getenv("GDF_RUN_STAGE"))  // tuning knob: 512 or 2048
+            g_run_stage = (uint32_t)std::max(1, std::atoi(v));
+        if (const char* v = std::getenv("GDF_RUN_INBLOCK"))  // tuning knob
+            g_run_inblock = (uint32_t)std::max(0, std::atoi(v));
         if (const char* v = std::getenv("GDF_SEG_ITEMS")) {  // tuning knob
             const uint32_t si = (uint32_t)std::atoi(v);
             if (si >= 64 && si <= kSegItems && si % 64 == 0) e->seg_items = si;
@@ -1417,7 +1415,7 @@ int gdf_create(int device, gdf_engine** out) {
         if (const char* v = std::getenv("GDF_SEL_SHAPE")) {  // tuning knob: "segs,threads"
             unsigned sg = 0, th = 0;
             if (std::sscanf(v, "%u,%u", &sg, &th) == 2 && (sg == 4 || sg == 8 || sg == 16) &&
-                th >= 64 && th <= 1024 && th % 64 == 0 && sg * (th / 64) <= 256) {
+                th >= 128 && th <= 1024 && th % 64 == 0 && sg * (th / 64) <= 256) {
                 e->sel_segs = sg;
                 e->sel_threads = th;
             }

@@ -1076,11 +1076,12 @@ __global__ __launch_bounds__(1024) void k_emit(FrameArgs a) {
 // Selected rollbuffer points (insertSelectedPointSequence + transformPointSequence + crop +
 // applyPointMask + computeVoxelCoords + occupancy marks for the rollbuffer part).  The window is
 // large (10^8 points) and mostly cropped away: each block owns a tile of kSelSegs x blockDim
-// consecutive selected points, reads them once, and writes its survivors (world point + voxel
-// key) at tile-local ranks of a staging area plus the tile's survivor count - no tickets, no
-// look-back, no second read of the window.  After the scan of the tile counts, k_sel_place moves
-// each tile's survivors behind the depth points (whose count is known only after the depth
-// compaction), in selection order.  Stage bits go to the debug buffer as before.
+// consecutive selected points (tiles in ticket order), reads them once, counts its survivors
+// (and, run mode, their runs of equal keys), resolves the survivors / runs before it by two
+// decoupled look-backs (wave 0: points, wave 1: runs) and writes its survivors (world point +
+// voxel key) and run records straight to their place behind the depth compaction's - one pass
+// over the window, in selection order.  The last tile writes the frame's totals.  Stage bits go
+// to the debug buffer as before.
 template <uint32_t kSegs>
 __global__ __launch_bounds__(1024) void k_sel(FrameArgs a) {
     constexpr uint32_t kSelSegs = kSegs;
@@ -1088,10 +1089,18 @@ __global__ __launch_bounds__(1024) void k_sel(FrameArgs a) {
     __shared__ uint32_t s_rc[kSelSegs * 16];  // run mode: runs per (segment j, wave w)
     static_assert(kSelSegs * 16 <= 256, "k_sel scan covers 256 entries");
     __shared__ uint32_t s_mark[1u << kMarkCacheBits];
+    __shared__ uint32_t s_tile, s_epoch, s_tot[2], s_ex[2];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int nwaves = blockDim.x >> 6;
     const uint32_t B = blockDim.x, i = threadIdx.x;
-    const uint32_t tile = blockIdx.x;
+    const Tickets tk = tickets(a.sel_tiles, gridDim.x);  // (one tile per block: oneshot)
+    if (i == 0) {
+        const uint32_t ep = read_epoch(a.epoch_word);
+        s_epoch = ep;
+        s_tile = next_ticket(a.sel_ctr, tk, a.epoch_word, ep);
+    }
+    __syncthreads();
+    const uint32_t tile = s_tile, epoch = s_epoch;
     if (a.grid_seq_out && tile == 0 && i == 0) *a.grid_seq_out = a.grid_seq;  // (as k_mask)
     const uint32_t si0 = tile * kSelSegs * B;
     // the ring loads first (their slots need no search; 32-bit slot arithmetic: ring_cap < 2^32),
@@ -1194,77 +1203,53 @@ __global__ __launch_bounds__(1024) void k_sel(FrameArgs a) {
             if (e < ne) sc[e] = carry + x - v;
             carry += __shfl(x, 63, 64);
         }
-        if (lane == 0) G(a.sel_counts)[(wid == 0 ? 0u : a.sel_tiles) + tile] = carry;
+        // the survivors (runs) of the tiles before this one
+        const uint32_t words = a.sel_tiles + a.sel_tiles / 64u + 2u;
+        unsigned long long* st = a.sel_status + (wid == 0 ? 0u : 2u * (size_t)words);
+        const uint32_t ex =
+            lookback2_wave(st, st + words, tile, a.sel_tiles, carry, epoch, a.err);
+        if (lane == 0) {
+            s_tot[wid] = carry;
+            s_ex[wid] = ex;
+        }
     }
     __syncthreads();
-    const uint64_t base = (uint64_t)tile * kSelSegs * B;  // the tile's staging slots
+    const uint32_t d = *G(a.out_count);                    // depth survivors (k_emit)
+    const uint32_t rd = a.run_mode ? *G(a.run_count) : 0u;  // depth runs
+    const uint32_t pbase = d + s_ex[0], rbase = rd + (a.run_mode ? s_ex[1] : 0u);
+    if (tile == a.sel_tiles - 1u && i == 0) {  // the frame's totals
+        *G(a.final_count) = pbase + s_tot[0];
+        if (a.run_mode) {
+            const uint32_t rtot = rbase + s_tot[1];
+            *G(a.run_total) = rtot;
+            G(a.run_start)[rtot] = pbase + s_tot[0];
+        }
+    }
 #pragma unroll
     for (uint32_t j = 0; j < kSelSegs; ++j) {
         const bool valid = (keep >> j) & 1u;
         const unsigned long long m = __ballot(valid);
         if (!m) continue;  // wave-uniform
         uint32_t key = 0xFFFFFFFFu;
+        const uint32_t pos = pbase + s_wc[j * nwaves + wid] + (uint32_t)__popcll(m & ltm);
         if (valid) {
-            const uint32_t local = s_wc[j * nwaves + wid] + (uint32_t)__popcll(m & ltm);
-            const uint64_t pos = base + local;
             const float4 w = world(j);
-            gst4(a.sel_pts, pos, w);
+            gst4(a.out_pts, pos, w);
             if (a.do_voxel) {
                 key = voxel_key(w.x, w.y, w.z, a.vlo, a.vcs, a.vrcs, a.gmax, a.gs);
-                G(a.sel_keys)[pos] = key;
+                G(a.out_coords)[pos] = key;
             }
         }
-        if (a.run_mode) {  // the run records at tile-local run ranks: key, tile-local first point
+        if (a.run_mode) {  // the run records: key, first point
             const bool lead = (rlead >> j) & 1u;
             const unsigned long long lm = __ballot(lead);
             if (lead) {
-                const uint64_t rpos = base + s_rc[j * nwaves + wid] + (uint32_t)__popcll(lm & ltm);
-                G(a.sel_runkeys)[rpos] = key;
-                G(a.sel_runstart)[rpos] = s_wc[j * nwaves + wid] + (uint32_t)__popcll(m & ltm);
+                const uint32_t rpos = rbase + s_rc[j * nwaves + wid] + (uint32_t)__popcll(lm & ltm);
+                G(a.run_keys)[rpos] = key;
+                G(a.run_start)[rpos] = pos;
             }
         }
         if (a.do_voxel && a.marks) mark_and_count(a, a.marks, valid, key, key, nullptr, s_mark);
-    }
-}
-
-// Each tile's staged survivors behind the depth survivors, at the tile's scanned offset
-// (m_points order: depth points first, fusion.cpp:1525,1559), and the frame's total count.
-// A persistent grid walks the tiles; empty tiles cost one load.
-// Run mode: the tiles' run records behind the depth runs (run r of tile t at depth runs + the
-// tile's scanned run offset; its first point at the tile's placed offset + its tile-local
-// start), the frame's run count and the runs' end sentinel.  The counts were scanned as
-// [points of every tile | runs of every tile]: a tile's run offset is its scanned value minus
-// the selection's points.
-__global__ __launch_bounds__(256) void k_sel_place(FrameArgs a) {
-    const uint32_t d = *G(a.out_count);
-    const uint32_t selp = a.run_mode ? G(a.sel_offsets)[a.sel_tiles] : *G(a.sel_total);
-    const uint32_t rd = a.run_mode ? *G(a.run_count) : 0u;  // depth runs (k_emit)
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        *G(a.final_count) = d + selp;
-        if (a.run_mode) {
-            const uint32_t rtot = rd + (*G(a.sel_total) - selp);
-            *G(a.run_total) = rtot;
-            G(a.run_start)[rtot] = d + selp;
-        }
-    }
-    const uint32_t tile_items = a.sel_tile;
-    for (uint32_t t = blockIdx.x; t < a.sel_tiles; t += gridDim.x) {
-        const uint32_t c = G(a.sel_counts)[t];
-        if (!c) continue;
-        const uint32_t o = d + G(a.sel_offsets)[t];
-        const uint64_t src = (uint64_t)t * tile_items;
-        for (uint32_t r = threadIdx.x; r < c; r += blockDim.x) {
-            gst4(a.out_pts, (uint64_t)o + r, gld4(a.sel_pts, src + r));
-            if (a.do_voxel) G(a.out_coords)[o + r] = G(a.sel_keys)[src + r];
-        }
-        if (a.run_mode) {
-            const uint32_t cr = G(a.sel_counts)[a.sel_tiles + t];
-            const uint32_t ro = rd + (G(a.sel_offsets)[a.sel_tiles + t] - selp);
-            for (uint32_t r = threadIdx.x; r < cr; r += blockDim.x) {
-                G(a.run_keys)[ro + r] = G(a.sel_runkeys)[src + r];
-                G(a.run_start)[ro + r] = o + G(a.sel_runstart)[src + r];
-            }
-        }
     }
 }
 
@@ -1316,7 +1301,7 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
         hipLaunchKernelGGL(k_emit, dim3(a.total_segs), dim3(a.seg_threads), 0, s, a);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    if (a.sel_tiles) {  // rollbuffer points: survivors per tile, tile offsets, placement
+    if (a.sel_tiles) {  // rollbuffer points: one pass, behind the depth survivors
         HookScope hs(hook, GDF_KERNEL_SEL);
         const uint32_t thr = a.sel_tile / a.sel_segs;
         if (a.sel_segs == 4)
@@ -1325,20 +1310,6 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
             hipLaunchKernelGGL(k_sel<16>, dim3(a.sel_tiles), dim3(thr), 0, s, a);
         else
             hipLaunchKernelGGL(k_sel<8>, dim3(a.sel_tiles), dim3(thr), 0, s, a);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        const uint32_t sm = a.run_mode ? 2u * a.sel_tiles : a.sel_tiles;  // (+ run counts)
-        const uint32_t chunks = (sm + 4095u) / 4096u;
-        uint32_t* partial = a.sel_offsets + scan_partials_offset(sm);
-        if (chunks > 1) {
-            hipLaunchKernelGGL(k_scan_reduce, dim3(chunks), dim3(1024), 0, s, a.sel_counts, sm,
-                               partial, nullptr, 1u);
-            if ((e = hipGetLastError()) != hipSuccess) return e;
-        }
-        hipLaunchKernelGGL(k_scan_counts, dim3(chunks), dim3(1024), 0, s, a.sel_counts, sm,
-                           a.sel_offsets, a.sel_total, partial, nullptr, 1u);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        hipLaunchKernelGGL(k_sel_place, dim3(std::min<uint32_t>(a.sel_tiles, 4096u)), dim3(256), 0,
-                           s, a);
     }
     return hipGetLastError();
 }
@@ -1348,7 +1319,6 @@ const void* frame_kernel(int which, int rot45) {
     if (which == 2) return reinterpret_cast<const void*>(&k_sel<8>);
     if (which == 4) return reinterpret_cast<const void*>(&k_sel<4>);
     if (which == 5) return reinterpret_cast<const void*>(&k_sel<16>);
-    if (which == 3) return reinterpret_cast<const void*>(&k_sel_place);
     return rot45 ? reinterpret_cast<const void*>(&k_mask<true>)
                  : reinterpret_cast<const void*>(&k_mask<false>);
 }
@@ -1913,6 +1883,68 @@ constexpr uint32_t kPersistBlocks = 2048;  // blocks of a persistent sort / grou
 uint32_t g_group_scan_tiles = 1024;
 constexpr int kSmallGroup = 16;  // groups summed by one thread; longer ones by a wave
 
+// acc + comp[0] + comp[S] + ... + comp[(n-1) S], in order (one component chain of a voxel sum; S =
+// 4: AoS float4 points, S = 1: one component's row).  Blocks of 16 values alternate between two
+// register sets: the next block is read while the current one is added, so the LDS latency stays
+// off the dependent chain.  The reads run up to 16 values past n: every LDS buffer read this way
+// carries kChainPad values of padding.
+constexpr uint32_t kChainPad = 16;
+
+template <int S, int B>
+__device__ __forceinline__ void lds_block(const float* comp, uint32_t k, float (&t)[B]) {
+    if (S == 1) {
+#pragma unroll
+        for (int q = 0; q < B / 4; ++q) {
+            const float4 v = *reinterpret_cast<const float4*>(comp + k + 4 * q);
+            t[4 * q] = v.x;
+            t[4 * q + 1] = v.y;
+            t[4 * q + 2] = v.z;
+            t[4 * q + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < B; ++q) t[q] = comp[S * (k + q)];
+    }
+}
+
+// (the asm pins the sum here: without it the compiler sinks the additions below later reads and
+// keeps hundreds of values live)
+template <int B>
+__device__ __forceinline__ float add_block(float acc, const float (&t)[B]) {
+#pragma unroll
+    for (int q = 0; q < B; ++q) acc = acc + t[q];
+    asm volatile("" : "+v"(acc));
+    return acc;
+}
+
+// blocks of B = 16 values from component rows (S = 1, b128 reads), 8 from AoS points (S = 4: the
+// kernels using them run at 8 waves per SIMD, 64 VGPRs)
+template <int S>
+__device__ __forceinline__ float lds_chain(const float* comp, uint32_t n, float acc) {
+    constexpr int B = S == 1 ? 16 : 8;
+    static_assert(B <= (int)kChainPad, "the read-ahead stays inside the padding");
+    float a[B], b[B];
+    uint32_t k = 0;
+    lds_block<S, B>(comp, 0, a);
+#pragma unroll 1
+    for (; k + 2 * B <= n; k += 2 * B) {
+        lds_block<S, B>(comp, k + B, b);
+        asm volatile("" ::: "memory");  // (the reads issue before the adds they overlap)
+        __builtin_amdgcn_sched_barrier(0);
+        acc = add_block<B>(acc, a);
+        lds_block<S, B>(comp, k + 2 * B, a);
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        acc = add_block<B>(acc, b);
+    }
+    if (k + B <= n) {
+        acc = add_block<B>(acc, a);
+        k += B;
+    }
+    for (; k < n; ++k) acc = acc + comp[S * k];
+    return acc;
+}
+
 // Group starts per tile of kGroupThreads sorted keys (large frames: the tiles' group-id offsets
 // then come from a scan of these counts instead of tickets and look-back in k_group).
 __global__ __launch_bounds__(256) void k_group_count(const uint32_t* __restrict__ keys,
@@ -1944,7 +1976,7 @@ __device__ __forceinline__ void group_corner(uint32_t key, const VoxelParams& vp
     o[3] = 0.0f;
 }
 
-__global__ __launch_bounds__(kGroupThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_group(
+__global__ __launch_bounds__(kGroupThreads) __attribute__((amdgpu_waves_per_eu(7, 8))) void k_group(
     const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
     const uint32_t* __restrict__ count, const float4* __restrict__ pts, float* __restrict__ out,
     uint32_t* __restrict__ out_count, unsigned long long* status, unsigned long long* gstatus,
@@ -1956,8 +1988,8 @@ __global__ __launch_bounds__(kGroupThreads) __attribute__((amdgpu_waves_per_eu(8
     __shared__ uint32_t s_tile, s_epoch, s_excl, s_nbig, s_nq;
     __shared__ uint32_t s_start[kGroupThreads + 1];
     __shared__ uint32_t s_big[kGroupThreads];
-    __shared__ float4 s_buf[4][kSumChunk];
-    __shared__ float4 s_pts[kStagePts];
+    __shared__ float4 s_buf[4][kSumChunk + kChainPad];
+    __shared__ float4 s_pts[kStagePts + kChainPad];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t n = *count;
     const uint32_t ntiles = (n + kGroupThreads - 1) / kGroupThreads;
@@ -2124,16 +2156,8 @@ __global__ __launch_bounds__(kGroupThreads) __attribute__((amdgpu_waves_per_eu(8
         float acc = 0.0f;
         if (e - S0 <= staged) {  // staged: lanes 0..3 run the component chains from LDS
             if (lane < 4) {
-                const float* comp = reinterpret_cast<const float*>(s_pts) + lane;
-                uint32_t j = s - S0;
-                for (; j + 16 <= e - S0; j += 16) {
-                    float t[16];
-#pragma unroll
-                    for (int q = 0; q < 16; ++q) t[q] = comp[4 * (j + q)];
-#pragma unroll
-                    for (int q = 0; q < 16; ++q) acc = acc + t[q];
-                }
-                for (; j < e - S0; ++j) acc = acc + comp[4 * j];
+                const float* comp = reinterpret_cast<const float*>(s_pts) + lane + 4 * (s - S0);
+                acc = lds_chain<4>(comp, e - s, acc);
                 const float fc = (float)(e - s);
                 out[4 * (size_t)g + lane] = lane < 3 ? acc / fc : acc;
             }
@@ -2160,15 +2184,7 @@ __global__ __launch_bounds__(kGroupThreads) __attribute__((amdgpu_waves_per_eu(8
             if (lane < 4) {
                 const float* comp = reinterpret_cast<const float*>(&s_buf[wid][0]) + lane;
                 const uint32_t m = (e - c) < (uint32_t)kSumChunk ? (e - c) : (uint32_t)kSumChunk;
-                uint32_t j = 0;
-                for (; j + 16 <= m; j += 16) {
-                    float t[16];
-#pragma unroll
-                    for (int q = 0; q < 16; ++q) t[q] = comp[4 * (j + q)];
-#pragma unroll
-                    for (int q = 0; q < 16; ++q) acc = acc + t[q];
-                }
-                for (; j < m; ++j) acc = acc + comp[4 * j];
+                acc = lds_chain<4>(comp, m, acc);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -2191,7 +2207,7 @@ __global__ __launch_bounds__(256) void k_group_big(const uint32_t* __restrict__ 
                                                    const uint4* __restrict__ bigq,
                                                    const uint32_t* __restrict__ bigcnt,
                                                    uint32_t nblocks, uint32_t bigcap) {
-    __shared__ float4 s_buf[4][kSumChunk];
+    __shared__ float4 s_buf[4][kSumChunk + kChainPad];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint64_t nslots = (uint64_t)nblocks * bigcap;
     const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
@@ -2230,15 +2246,7 @@ __global__ __launch_bounds__(256) void k_group_big(const uint32_t* __restrict__ 
             if (lane < 4) {
                 const float* comp = reinterpret_cast<const float*>(&s_buf[wid][0]) + lane;
                 const uint32_t m = (e - c) < (uint32_t)kSumChunk ? (e - c) : (uint32_t)kSumChunk;
-                uint32_t j = 0;
-                for (; j + 16 <= m; j += 16) {
-                    float t[16];
-#pragma unroll
-                    for (int qq = 0; qq < 16; ++qq) t[qq] = comp[4 * (j + qq)];
-#pragma unroll
-                    for (int qq = 0; qq < 16; ++qq) acc = acc + t[qq];
-                }
-                for (; j < m; ++j) acc = acc + comp[4 * j];
+                acc = lds_chain<4>(comp, m, acc);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -2251,64 +2259,432 @@ __global__ __launch_bounds__(256) void k_group_big(const uint32_t* __restrict__ 
     }
 }
 
-// Runs of equal keys back to points: the sorted (run key, run) pairs become the sorted (key, point)
-// order k_group consumes - run r's points start[r] .. start[r+1]-1 in a row, keys repeated.
-// Tiles of 256 runs: block scan of the run lengths + ticketed decoupled look-back for the tile's
-// first point; the tile's points are written cooperatively (binary search of the run in LDS), so
-// the stores are coalesced.
-__global__ __launch_bounds__(256) void k_expand(const uint32_t* __restrict__ rkeys,
-                                                const uint32_t* __restrict__ rvals,
-                                                const uint32_t* __restrict__ rcount,
-                                                const uint32_t* __restrict__ run_start,
-                                                uint32_t* __restrict__ okeys,
-                                                uint32_t* __restrict__ ovals,
-                                                unsigned long long* status,
-                                                unsigned long long* gstatus, uint32_t* tile_ctr,
-                                                uint32_t* epoch_word, uint32_t* err) {
-    __shared__ uint32_t s_off[257], s_ps[256], s_key[256];
-    __shared__ uint32_t s_wave[4], s_tile, s_epoch, s_base;
+// ---- voxel groups over sorted RUNS (run mode) ---------------------------------------------------
+// The sort ordered runs of equal keys (run r = points run_start[r] .. run_start[r+1]-1, contiguous
+// in the compaction); a voxel group is a maximal sequence of sorted runs with one key and its
+// points are the concatenation of its runs' points - the same stable index order the reference
+// sums in (inc/voxelize.h:29-35), read as contiguous ranges with no per-point (key, index) list.
+// k_group_runs: points of a tile's groups staged in LDS (template: 512 or 2048), and the size up to
+// which a staged group is summed in-block (larger ones are queued); tuning knobs GDF_RUN_STAGE,
+// GDF_RUN_INBLOCK
+uint32_t g_run_stage = 512;
+uint32_t g_run_inblock = 512;
+constexpr int kRunQ = 4;        // a streamed chunk: 64 x kRunQ points per wave step
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Wave64 inclusive scans on DPP (row shifts inside the 16-lane rows, then the row broadcasts of
+// lanes 15 and 31): six dependent VALU steps, no LDS round trips.
+__device__ __forceinline__ int dpp_max_scan(int v) {  // (values >= -1)
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x111, 0xf, 0xf, false));  // row_shr:1
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x112, 0xf, 0xf, false));  // row_shr:2
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x114, 0xf, 0xf, false));  // row_shr:4
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x118, 0xf, 0xf, false));  // row_shr:8
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return v;
+}
+__device__ __forceinline__ uint32_t dpp_sum_scan(uint32_t x) {
+    int v = (int)x;
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
+    return (uint32_t)v;
+}
+
+struct RunRec {
+    uint32_t ps, len;
+};
+
+// One wave sums the points of sorted runs [rs, re) in order: batches of 64 runs (one per lane;
+// the records rps / rlen - first point, length - are indexed by sorted run, contiguous, and read
+// two batches ahead), their points streamed in chunks of 64 x kRunQ positions - position -> run by
+// a max-scan of the runs' first positions - loaded coalesced one chunk ahead (across batch
+// boundaries too), transposed into LDS per component, and added by lanes 0..3, one component chain
+// each (the reference's sequential f32 sum).  Returns lane c's component sum; npts = the group's
+// points (wave-uniform).
+struct RunBatch {
+    uint32_t ps, off, len;  // run `lane` of the batch: first point, first batch position, length
+    uint32_t T;             // the batch's points (wave-uniform)
+    int carry;              // run of the last fetched position
+};
+
+__device__ __forceinline__ RunBatch run_batch(const RunRec& r) {
+    const uint32_t x = dpp_sum_scan(r.len);
+    return RunBatch{r.ps, x - r.len, r.len, (uint32_t)__builtin_amdgcn_readlane((int)x, 63), 0};
+}
+
+__device__ __forceinline__ RunRec run_rec(const uint32_t* __restrict__ rps,
+                                          const uint32_t* __restrict__ rlen, uint32_t r, bool ok) {
+    return ok ? RunRec{rps[r], rlen[r]} : RunRec{0u, 0u};
+}
+
+// The points at batch positions c + 64 q + lane (q < kRunQ), in two steps: run_marks writes the
+// first position of every run inside the chunk, run_row(q) max-scans row q of the marks (the row
+// carries chain through cy) and loads its points - branch-free (positions past the batch load
+// point 0 and read as zero), so the rows interleave with the chain additions.
+__device__ __forceinline__ void run_marks(const RunBatch& bt, uint32_t c, int* s_mark) {
+    constexpr uint32_t CH = 64u * kRunQ;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int q = 0; q < kRunQ; ++q) s_mark[64 * q + lane] = -1;
+    wave_sync();
+    if (bt.len && bt.off >= c && bt.off < c + CH) s_mark[bt.off - c] = lane;
+    wave_sync();
+}
+
+__device__ __forceinline__ float4 run_row(const RunBatch& bt, uint32_t c, int q, const int* s_mark,
+                                          int& cy, const float4* __restrict__ pts) {
+    const int lane = threadIdx.x & 63;
+    int m = dpp_max_scan(s_mark[64 * q + lane]);
+    const int rowmax = __builtin_amdgcn_readlane(m, 63);
+    m = max(m, cy);
+    cy = max(cy, rowmax);
+    const uint32_t mps = __shfl(bt.ps, m, 64), moff = __shfl(bt.off, m, 64);
+    const uint32_t pos = c + 64u * q + (uint32_t)lane;
+    const bool ok = pos < bt.T;
+    const float4 v = pts[ok ? mps + (pos - moff) : 0u];
+    return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+__device__ __forceinline__ void run_fetch(RunBatch& bt, uint32_t c, const float4* __restrict__ pts,
+                                          int* s_mark, float4 (&p)[kRunQ]) {
+    run_marks(bt, c, s_mark);
+    int cy = bt.carry;
+#pragma unroll
+    for (int q = 0; q < kRunQ; ++q) p[q] = run_row(bt, c, q, s_mark, cy, pts);
+    bt.carry = cy;
+}
+
+
+
+__device__ __forceinline__ float wave_stream_sum(const uint32_t* __restrict__ rps,
+                                                 const uint32_t* __restrict__ rlen, uint32_t rs,
+                                                 uint32_t re, const float4* __restrict__ pts,
+                                                 float* s_soa, int* s_mark, uint32_t& npts) {
+    constexpr uint32_t CH = 64u * kRunQ, CHP = CH + kChainPad;  // (component rows, padded)
+    static_assert(CH == 256, "the interleaved chain below covers 4 rows of 64");
+    const int lane = threadIdx.x & 63;
+    float acc = 0.0f;
+    npts = 0;
+    const uint32_t r0 = rs + (uint32_t)lane;
+    RunBatch cur = run_batch(run_rec(rps, rlen, r0, r0 < re));
+    RunRec rec1 = run_rec(rps, rlen, r0 + 64u, r0 + 64u < re);    // batch 1
+    RunRec rec2 = run_rec(rps, rlen, r0 + 128u, r0 + 128u < re);  // batch 2
+    float4 p[kRunQ];
+    run_fetch(cur, 0, pts, s_mark, p);  // (every run holds >= 1 point)
+    // every lane runs the chain of component lane & 3 (lanes 0..3 hold the result): no exec mask
+    // splits the chain from the next chunk's fetch, which is interleaved with it row by row
+    const float* comp = s_soa + (uint32_t)(lane & 3) * CHP;
+    uint32_t rb = rs, c = 0;
+    while (true) {  // wave-uniform: one chunk per iteration
+#pragma unroll
+        for (int q = 0; q < kRunQ; ++q) {
+            s_soa[0 * CHP + 64 * q + lane] = p[q].x;
+            s_soa[1 * CHP + 64 * q + lane] = p[q].y;
+            s_soa[2 * CHP + 64 * q + lane] = p[q].z;
+            s_soa[3 * CHP + 64 * q + lane] = p[q].w;
+        }
+        wave_sync();
+        const uint32_t n = min(CH, cur.T - c);
+        // the next chunk, loaded while the chains run: the rest of this batch, or the next batch's
+        // first chunk (whose records were read two batches ago); none: T = 0, nothing is loaded
+        const bool more = c + CH < cur.T;
+        const bool next_batch = !more && rb + 64u < re;
+        RunBatch fb = cur;
+        uint32_t cn = c + CH;
+        if (next_batch) {
+            fb = run_batch(rec1);
+            rec1 = rec2;
+            const uint32_t r3 = rb + 192u + (uint32_t)lane;
+            rec2 = run_rec(rps, rlen, r3, r3 < re);
+            cn = 0;
+        } else if (!more) {
+            fb.T = 0;
+        }
+        run_marks(fb, cn, s_mark);
+        int cy = fb.carry;
+        if (n == CH) {  // a full chunk: 4 x (64 additions, then one row of the next chunk's loads)
+            float ta[16], tb[16];
+            lds_block<1, 16>(comp, 0, ta);
+#pragma unroll
+            for (int q = 0; q < kRunQ; ++q) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const uint32_t k = 64u * q + 32u * h;
+                    lds_block<1, 16>(comp, k + 16, tb);
+                    asm volatile("" ::: "memory");  // (reads stay where they are issued)
+                    __builtin_amdgcn_sched_barrier(0);
+                    acc = add_block<16>(acc, ta);
+                    lds_block<1, 16>(comp, k + 32, ta);  // (the last reads the padding)
+                    asm volatile("" ::: "memory");
+                    __builtin_amdgcn_sched_barrier(0);
+                    acc = add_block<16>(acc, tb);
+                }
+                p[q] = run_row(fb, cn, q, s_mark, cy, pts);
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < kRunQ; ++q) p[q] = run_row(fb, cn, q, s_mark, cy, pts);
+            acc = lds_chain<1>(comp, n, acc);
+        }
+        fb.carry = cy;
+        wave_sync();  // the chains have read the chunk before the next one is written
+        npts += n;
+        if (more) {
+            cur = fb;
+            c += CH;
+        } else if (next_batch) {
+            rb += 64u;
+            cur = fb;
+            c = 0;
+        } else {
+            break;
+        }
+    }
+    return acc;
+}
+
+// Groups of one tile of 256 sorted runs: group starts (key != previous run's key), group ids by a
+// block scan plus the tile's offset (count + scan, or tickets + look-back as k_group), the end of
+// the tile's last group (a search of the run keys past the tile).  The points of the tile's groups
+// are staged (up to kRunStage from the first group start); groups of <= kSmallGroup staged points
+// are summed by their thread, longer staged ones by a wave from LDS, and the others (past the
+// staged points, or continuing past the tile) are queued for k_group_runs_big - one append per
+// group, so a block never waits on a long chain.  Marks, frame voxel starts and corners as k_group.
+template <int kRunStage>
+__global__ __launch_bounds__(kGroupThreads) void k_group_runs(
+    const uint32_t* __restrict__ keys, const uint32_t* __restrict__ rvals,
+    const uint32_t* __restrict__ count, const uint32_t* __restrict__ run_start,
+    const float4* __restrict__ pts, float* __restrict__ out, uint32_t* __restrict__ out_count,
+    unsigned long long* status, unsigned long long* gstatus, uint32_t* tile_ctr,
+    uint32_t* epoch_word, uint32_t* err, uint32_t* hist, int average, VoxelParams vp,
+    uint32_t* marks, const uint32_t* tile_base, uint4* __restrict__ bigq, uint32_t bigq_cap,
+    uint32_t* __restrict__ qctr, uint32_t nframes, uint32_t fshift, uint32_t* __restrict__ fvox,
+    uint32_t inblock_max, uint32_t* __restrict__ rps, uint32_t* __restrict__ rlen) {
+    __shared__ uint32_t s_wave[4];
+    __shared__ uint32_t s_tile, s_epoch, s_excl, s_nbig, s_nq, s_qbase, s_wend;
+    __shared__ uint32_t s_start[kGroupThreads + 1];  // group starts (run index); [total] = end
+    __shared__ uint32_t s_ps[kGroupThreads];
+    __shared__ uint32_t s_off[kGroupThreads + 1];  // exclusive scan of the tile's run lengths
+    __shared__ uint32_t s_big[kGroupThreads];
+    __shared__ float4 s_pts[kRunStage + kChainPad];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint32_t R = *rcount;
-    const uint32_t ntiles = (R + 255u) / 256u;
+    const uint32_t n = *count;  // runs
+    const uint32_t ntiles = (n + kGroupThreads - 1) / kGroupThreads;
+    const uint32_t kmask = nframes > 1 ? (1u << fshift) - 1u : 0xFFFFFFFFu;
+    if (blockIdx.x == 0) {
+        for (uint32_t i = threadIdx.x; i < kHistWords; i += kGroupThreads) hist[i] = 0;
+        if (ntiles == 0 && threadIdx.x == 0) *out_count = 0;
+        if (ntiles == 0 && fvox)
+            for (uint32_t f = threadIdx.x; f <= nframes; f += kGroupThreads) fvox[f] = 0;
+    }
     const Tickets tk = tickets(ntiles, gridDim.x);
-    if (blockIdx.x >= tk.nblk) return;
-    if (threadIdx.x == 0) s_epoch = read_epoch(epoch_word);
-    for (bool first = true;; first = false) {  // persistent: tiles in ticket order
-        if (!first && tk.oneshot) return;
-        if (threadIdx.x == 0) s_tile = next_ticket(tile_ctr, tk, epoch_word, s_epoch);
+    if (!tile_base && blockIdx.x >= tk.nblk) return;
+    if (!tile_base && threadIdx.x == 0) s_epoch = read_epoch(epoch_word);
+    uint32_t walk = blockIdx.x;
+    for (bool first = true;; first = false) {  // persistent
+        if (!first && !tile_base && tk.oneshot) return;
+        if (threadIdx.x == 0) {
+            if (tile_base) {
+                s_tile = walk;
+                s_excl = walk < ntiles ? tile_base[walk] : 0u;
+            } else {
+                s_tile = next_ticket(tile_ctr, tk, epoch_word, s_epoch);
+            }
+            s_nbig = 0;
+            s_nq = 0;
+            s_wend = 0;
+        }
+        walk += gridDim.x;
         __syncthreads();
         const uint32_t tile = s_tile, epoch = s_epoch;
         if (tile >= ntiles) return;  // block-uniform
-        const uint32_t i = tile * 256u + threadIdx.x;
-        uint32_t key = 0, ps = 0, len = 0;
-        if (i < R) {
-            key = rkeys[i];
+        const uint32_t t0 = tile * kGroupThreads;
+        const uint32_t i = t0 + threadIdx.x;
+        const uint32_t tend = min(n, t0 + kGroupThreads);
+        const uint32_t key = i < n ? keys[i] : 0u;
+        const uint32_t prev = (i < n && i > 0) ? keys[i - 1] : ~key;
+        const bool start = i < n && (i == 0 || key != prev);
+        RunRec rr{0u, 0u};
+        if (average && i < n) {  // (and the sorted run records for k_group_runs_big)
             const uint32_t v = rvals[i];
-            ps = run_start[v];
-            len = run_start[v + 1] - ps;
+            rr.ps = run_start[v];
+            rr.len = run_start[v + 1] - rr.ps;
+            rps[i] = rr.ps;
+            rlen[i] = rr.len;
         }
-        uint32_t total;
-        const uint32_t off = block_exclusive_scan(len, total, s_wave);
-        s_off[threadIdx.x] = off;
-        s_ps[threadIdx.x] = ps;
-        s_key[threadIdx.x] = key;
-        if (threadIdx.x == 0) s_off[256] = total;
+        uint32_t total, ptotal;
+        const uint32_t local = block_exclusive_scan(start ? 1u : 0u, total, s_wave);
+        if (start) s_start[local] = i;
+        const uint32_t poff = block_exclusive_scan(rr.len, ptotal, s_wave);
+        s_ps[threadIdx.x] = rr.ps;
+        s_off[threadIdx.x] = poff;
+        if (threadIdx.x == 0) s_off[kGroupThreads] = ptotal;
+        __syncthreads();
         if (wid == 0) {
-            const uint32_t ex = lookback2_wave(status, gstatus, tile, ntiles, total, epoch, err);
-            if (lane == 0) s_base = ex;
+            const uint32_t ex = tile_base ? s_excl
+                                          : lookback2_wave(status, gstatus, tile, ntiles, total, epoch, err);
+            if (lane == 0) {
+                s_excl = ex;
+                if (tile == ntiles - 1) {
+                    *out_count = ex + total;
+                    if (fvox)
+                        for (uint32_t f = (keys[n - 1] >> fshift) + 1; f <= nframes; ++f)
+                            fvox[f] = ex + total;
+                }
+            }
+        } else if (wid == 1 && total) {  // end of the tile's last group (as k_group, over runs)
+            const uint32_t lastkey = keys[tend - 1];
+            uint32_t lo = tend, hi = n;
+            while (lo < hi) {
+                const uint32_t len = hi - lo;
+                const uint32_t step = len <= 64u || lo == tend ? 1u : (len + 63u) / 64u;
+                const uint32_t j = lo + (uint32_t)lane * step;
+                const unsigned long long ch = __ballot(j < hi && keys[j] > lastkey);
+                if (ch) {
+                    const uint32_t f = (uint32_t)(__ffsll((long long)ch) - 1);
+                    hi = lo + f * step;
+                    if (step == 1u) break;
+                    lo = f ? lo + (f - 1u) * step + 1u : lo;
+                } else {
+                    const uint32_t lastp = lo + min(63u, (len - 1u) / step) * step;
+                    lo = lastp + 1u;
+                }
+            }
+            if (lane == 0) s_start[total] = hi;
+        }
+        // the groups summed in-block: inside the tile, <= kRunInBlock points, ending within
+        // kRunStage positions of the first group start; their points are staged (positions of the
+        // tile's run stream up to the last such group's end; position -> run by a binary search
+        // of the run offsets), the other groups are queued
+        const uint32_t W0 = total ? s_off[s_start[0] - t0] : 0u;
+        __syncthreads();  // (the last group's end, s_start[total])
+        bool inblock = false;
+        if (threadIdx.x < total && average) {
+            const uint32_t s = s_start[threadIdx.x], e = s_start[threadIdx.x + 1];
+            if (e <= tend) {
+                const uint32_t ge = s_off[e - t0] - W0;
+                inblock = ge <= (uint32_t)kRunStage && ge - (s_off[s - t0] - W0) <= inblock_max;
+                if (inblock) atomicMax(&s_wend, ge);
+            }
         }
         __syncthreads();
-        const uint32_t base = s_base;
-        for (uint32_t q = threadIdx.x; q < total; q += 256u) {
-            uint32_t lo = 0, hi = 256;  // last run with s_off <= q (a run holds >= 1 point)
+        const uint32_t staged = s_wend;
+        for (uint32_t k = threadIdx.x; k < staged; k += kGroupThreads) {
+            const uint32_t q = W0 + k;
+            uint32_t lo = 0, hi = kGroupThreads;  // last run with s_off <= q
             while (hi - lo > 1) {
                 const uint32_t mid = (lo + hi) >> 1;
                 if (s_off[mid] <= q) lo = mid; else hi = mid;
             }
-            okeys[base + q] = s_key[lo];
-            ovals[base + q] = s_ps[lo] + (q - s_off[lo]);
+            s_pts[k] = pts[s_ps[lo] + (q - s_off[lo])];
+        }
+        __syncthreads();
+        if (total == 0) continue;  // block-uniform
+        uint32_t qlocal = 0xFFFFFFFFu;  // this thread's group in the tile's queue appends
+        if (threadIdx.x < total && average && !inblock) qlocal = atomicAdd(&s_nq, 1u);
+        __syncthreads();
+        if (threadIdx.x == 0 && s_nq) s_qbase = atomicAdd(qctr, s_nq);  // one append per tile
+        __syncthreads();
+        if (threadIdx.x < total) {
+            const uint32_t g = s_excl + threadIdx.x;
+            const uint32_t s = s_start[threadIdx.x], e = s_start[threadIdx.x + 1];
+            float* o = out + 4 * (size_t)g;
+            if (marks) {
+                const uint32_t k = keys[s] & kmask;
+                atomicOr(marks + (k >> 5), 1u << (k & 31u));
+            }
+            if (fvox) {
+                const uint32_t fc = keys[s] >> fshift;
+                const uint32_t f0 = s == 0 ? 0u : (keys[s - 1] >> fshift) + 1u;
+                for (uint32_t f = f0; f <= fc; ++f) fvox[f] = g;
+            }
+            const uint32_t g0 = s_off[s - t0] - W0;  // staged positions of the group
+            const uint32_t g1 = e <= tend ? s_off[e - t0] - W0 : 0xFFFFFFFFu;
+            if (!average) {
+                float c[4];
+                group_corner(keys[s] & kmask, vp, c);
+                *reinterpret_cast<float4*>(o) = make_float4(c[0], c[1], c[2], c[3]);
+            } else if (qlocal != 0xFFFFFFFFu) {  // past the staged points: k_group_runs_big
+                const uint32_t slot = s_qbase + qlocal;
+                if (slot < bigq_cap) bigq[slot] = make_uint4(g, s, e, 0u);
+                else atomicOr(err, 8u);
+            } else if (g1 - g0 <= (uint32_t)kSmallGroup) {
+                float ax = 0.f, ay = 0.f, az = 0.f, aw = 0.f;
+                for (uint32_t k = g0; k < g1; ++k) {
+                    const float4 q = s_pts[k];
+                    ax = ax + q.x;
+                    ay = ay + q.y;
+                    az = az + q.z;
+                    aw = aw + q.w;
+                }
+                const float fc = (float)(g1 - g0);
+                *reinterpret_cast<float4*>(o) = make_float4(ax / fc, ay / fc, az / fc, aw);
+            } else {
+                s_big[atomicAdd(&s_nbig, 1u)] = threadIdx.x;
+            }
+        }
+        __syncthreads();
+        const uint32_t nbig = s_nbig;
+        for (uint32_t bi = wid; bi < nbig; bi += kGroupThreads / 64) {  // staged: chains from LDS
+            const uint32_t li = s_big[bi];
+            const uint32_t g = s_excl + li;
+            const uint32_t s = s_start[li], e = s_start[li + 1];
+            const uint32_t g0 = s_off[s - t0] - W0, g1 = s_off[e - t0] - W0;
+            if (lane < 4) {
+                const float* comp = reinterpret_cast<const float*>(s_pts) + lane + 4 * g0;
+                const float acc = lds_chain<4>(comp, g1 - g0, 0.0f);
+                out[4 * (size_t)g + lane] = lane < 3 ? acc / (float)(g1 - g0) : acc;
+            }
         }
         __syncthreads();  // LDS reused by the next tile
+    }
+}
+
+// The groups queued by k_group_runs: wave w of the grid takes queue slot w, then draws further
+// slots (qctr[1]) while any remain - no draw at all when the queue fits the grid - and streams the
+// runs of each (records rps / rlen by sorted run, written by k_group_runs) from global memory
+// (wave_stream_sum).  The last block to finish resets the counters (qctr[2] counts finished
+// blocks) for the next voxelize; the queue was complete when this launch began.  20 KiB of LDS
+// and <= 64 VGPRs per 4-wave block: 8 waves per SIMD stream at once.
+__global__ __launch_bounds__(256) void k_group_runs_big(const uint32_t* __restrict__ rps,
+                                                        const uint32_t* __restrict__ rlen,
+                                                        const float4* __restrict__ pts,
+                                                        float* __restrict__ out,
+                                                        const uint4* __restrict__ bigq,
+                                                        uint32_t bigq_cap, uint32_t* qctr) {
+    constexpr uint32_t CH = 64u * kRunQ;
+    __shared__ __attribute__((aligned(16))) float s_soa[4][4 * (CH + kChainPad)];
+    __shared__ int s_mk[4][CH];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t nq = min(__hip_atomic_load(qctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), bigq_cap);
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    uint32_t t = blockIdx.x * (blockDim.x >> 6) + wid;
+    while (t < nq) {  // wave-uniform
+        const uint4 q = bigq[t];
+        uint32_t np = 0;
+        const float acc = wave_stream_sum(rps, rlen, q.y, q.z, pts, s_soa[wid], s_mk[wid], np);
+        if (lane < 4) out[4 * (size_t)q.x + lane] = lane < 3 ? acc / (float)np : acc;
+        if (nq <= waves) break;
+        uint32_t d = 0;
+        if (lane == 0) d = atomicAdd(qctr + 1, 1u);
+        d = __shfl(d, 0, 64);
+        if (d >= nq - waves) break;
+        t = waves + d;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && atomicAdd(qctr + 2, 1u) == gridDim.x - 1u) {  // last block out
+        qctr[0] = 0u;
+        qctr[1] = 0u;
+        qctr[2] = 0u;
     }
 }
 
@@ -2371,20 +2747,7 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
         kin = kbuf[p & 1];
         vin = vbuf[p & 1];
     }
-    const uint32_t* gcount = a.count;  // items of the group phase
-    if (runs) {
-        HookScope hs(hook, GDF_KERNEL_SORT);  // (accounted with the sort: the last step of it)
-        const uint32_t max_rt = std::min<uint32_t>((a.nmax + 255u) / 256u, kPersistBlocks);
-        hipLaunchKernelGGL(k_expand, dim3(std::max<uint32_t>(max_rt, 1u)), dim3(256), 0, s, kin,
-                           vin, a.count, a.run_start, kbuf[npasses & 1], vbuf[npasses & 1],
-                           a.gstatus, a.ggstatus,
-                           reinterpret_cast<uint32_t*>(a.ctrs + kCtrExpand),
-                           reinterpret_cast<uint32_t*>(a.ctrs + kCtrEpoch), a.err);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        kin = kbuf[npasses & 1];
-        vin = vbuf[npasses & 1];
-        gcount = a.point_count;
-    }
+    const uint32_t* gcount = a.count;  // items of the group phase (points, or runs)
     const uint32_t max_tiles = (a.nmax + kGroupThreads - 1) / kGroupThreads;
     const uint32_t group_tiles = std::min<uint32_t>(max_tiles, kPersistBlocks);
     HookScope hs(hook, GDF_KERNEL_GROUP);
@@ -2409,6 +2772,26 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
                            (uint32_t)kGroupThreads);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         tile_base = a.group_offsets;
+    }
+    if (runs) {  // groups of sorted runs; the long ones by k_group_runs_big
+        const uint32_t gb = std::max<uint32_t>(group_tiles, 1u);
+        uint32_t* qctr = reinterpret_cast<uint32_t*>(a.ctrs + kCtrRunQueue);
+        auto kg = g_run_stage >= 2048 ? k_group_runs<2048> : k_group_runs<512>;
+        hipLaunchKernelGGL(kg, dim3(gb), dim3(kGroupThreads), 0, s, kin, vin, gcount,
+                           a.run_start, a.pts, reinterpret_cast<float*>(a.out), a.out_count,
+                           a.gstatus, a.ggstatus, reinterpret_cast<uint32_t*>(a.ctrs + kCtrGroup),
+                           reinterpret_cast<uint32_t*>(a.ctrs + kCtrEpoch), a.err, a.hist,
+                           a.average, a.vp, a.group_marks, tile_base, a.bigq, a.bigq_cap, qctr,
+                           a.nframes, a.frame_shift, a.frame_vox_start,
+                           std::min<uint32_t>(g_run_inblock, g_run_stage >= 2048 ? 2048u : 512u),
+                           kbuf[npasses & 1], vbuf[npasses & 1]);  // (free after the sort)
+        if (a.average) {
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            hipLaunchKernelGGL(k_group_runs_big, dim3(2048), dim3(256), 0, s, kbuf[npasses & 1],
+                               vbuf[npasses & 1], a.pts, reinterpret_cast<float*>(a.out), a.bigq,
+                               a.bigq_cap, qctr);
+        }
+        return hipGetLastError();
     }
     hipLaunchKernelGGL(k_group, dim3(group_tiles ? group_tiles : 1), dim3(kGroupThreads), 0, s, kin,
                        vin, gcount, a.pts, reinterpret_cast<float*>(a.out), a.out_count,

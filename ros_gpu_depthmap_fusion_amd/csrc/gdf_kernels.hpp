@@ -32,7 +32,7 @@ inline uint32_t scan_partials_offset(uint32_t segs) { return (segs + 63u) & ~63u
 inline size_t seg_offsets_words(uint32_t segs) {
     return scan_partials_offset(segs) + (segs + 4095u) / 4096u + 1u;
 }
-// the compaction kernels (0: k_mask, 1: k_emit, 2/4/5: k_sel<8/4/16>, 3: k_sel_place) as launched for
+// the compaction kernels (0: k_mask, 1: k_emit, 2/4/5: k_sel<8/4/16>, 3: none) as launched for
 // `rot45` (graph node lookup)
 const void* frame_kernel(int which, int rot45);
 
@@ -92,6 +92,7 @@ struct VoxelizeArgs {
     uint32_t* group_counts;         // [group tiles] group starts per tile (large frames)
     uint32_t* group_offsets;        // [seg_offsets_words(group tiles)] their scan
     uint4* bigq;                    // [group blocks * tiles per block] long voxels (large frames)
+    uint32_t bigq_cap;              // run mode: one queue of bigq_cap groups (kCtrRunQueue counts)
     uint32_t* bigcnt;               // [group blocks] queued per block
     GridSeq gseq;                   // engine order of the fused grid update (frame pipelining)
     // multi-frame batch: keys of frame f (points [frame_pt_start[f], frame_pt_start[f+1])) sort
@@ -105,9 +106,9 @@ struct VoxelizeArgs {
     uint64_t mark_words;
     uint8_t* snapshots;
     uint64_t snapshot_bytes;
-    // runs of equal keys (depth-only frames): keys / count are the run keys / run count, the
-    // sort orders runs, k_expand turns them back into the sorted (key, point) order over
-    // point_count points (run r = points run_start[r] .. run_start[r+1]-1)
+    // runs of equal keys: keys / count are the run keys / run count, the sort orders runs and
+    // k_group_runs groups them (run r = points run_start[r] .. run_start[r+1]-1; point_count:
+    // the points)
     const uint32_t* run_start;
     const uint32_t* point_count;
     uint64_t ncells;
@@ -121,6 +122,8 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
 size_t voxelize_status_words(uint32_t nmax);
 // capacity (256-key tiles) above which k_group takes its group-id offsets from count + scan
 extern uint32_t g_group_scan_tiles;
+// k_group_runs staging (512 or 2048 points) and in-block group size limit
+extern uint32_t g_run_stage, g_run_inblock;
 size_t voxelize_group_tiles(uint32_t nmax);
 
 // orphan shaders: mask_dilate (F <= kDilateMaxF) and single-matrix transform_points

@@ -119,8 +119,8 @@ def run_c3(width=1280, height=720, window=256, steps=20, ring=4, profile_steps=5
     model = {
         "mask": 3.0 * P,                                         # depth in, stage bits out
         "emit": 1.0 * P + 22.0 * N_depth,                        # depth survivors: point + key
-        # selected ring points in once, survivors staged (point + key) and placed (read + write)
-        "sel": 16.0 * S + 20.0 * N_sel * 3,
+        # selected ring points in once, survivors (point + key) written once at their place
+        "sel": 16.0 * S + 20.0 * N_sel,
         "sort": (12.0 * N + 16.0 * N * 2 + 2.0 * ncells) / 3.0,
         "group": 24.0 * N + 16.0 * G,
         "ps_insert": 32.0 * P,                                   # new sequence in, ring out
@@ -133,8 +133,8 @@ def run_c3(width=1280, height=720, window=256, steps=20, ring=4, profile_steps=5
             per[name] = {"avg_us": round(tot * 1e3 / n, 2), "launches_per_frame":
                          round(n / profile_steps, 2),
                          "GBps": round(model[name] / (tot / 1e3 / n) / 1e9, 1)}
-    dom = max(per, key=lambda q: per[q]["avg_us"] * per[q]["launches_per_frame"])
-    achieved = per[dom]["GBps"]
+    dom = max(per, key=lambda q: per[q]["avg_us"] * per[q]["launches_per_frame"]) if per else None
+    achieved = per[dom]["GBps"] if per else 0.0
     # SURVEY §8(d) B_alg for C3: depth 2P + 24N + 9C, plus 24 n_new + 24 n_sel + 32 n_sel
     survey = 2.0 * P + 24.0 * N + 9.0 * ncells + 24.0 * P + 56.0 * S
     return {
