@@ -1770,8 +1770,13 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
     uint32_t* tile_ctr, uint32_t* epoch_word, uint32_t* err, uint32_t shift, uint32_t dbits,
     uint32_t grid_block0, uint4* grid, uint32_t* marks, uint64_t grid_nwords, uint32_t lifetime,
     GridSeq q, uint32_t nframes, uint32_t fshift, const uint32_t* __restrict__ fstart,
-    uint64_t mark_words, uint4* snap, uint64_t snap_stride) {
+    uint64_t mark_words, uint4* snap, uint64_t snap_stride, uint32_t* qreset) {
     constexpr int kTile = kSortThreads * PT;
+    // (first pass: the run-group queue counters start from zero for this voxelize's k_group_runs)
+    if (qreset && blockIdx.x == 0 && threadIdx.x == 0) {
+        qreset[0] = 0u;
+        qreset[1] = 0u;
+    }
     if (blockIdx.x >= grid_block0) {  // fused historic-grid update (first pass only)
         const uint32_t f = grid_seq_enter(q);
         if (nframes > 1)
@@ -2267,8 +2272,9 @@ __global__ __launch_bounds__(256) void k_group_big(const uint32_t* __restrict__ 
 // k_group_runs: points of a tile's groups staged in LDS (template: 512 or 2048), and the size up to
 // which a staged group is summed in-block (larger ones are queued); tuning knobs GDF_RUN_STAGE,
 // GDF_RUN_INBLOCK
-uint32_t g_run_stage = 512;
-uint32_t g_run_inblock = 512;
+uint32_t g_run_stage = 2048;
+uint32_t g_run_inblock = 256;
+uint32_t g_run_big_blocks = 1024;  // k_group_runs_big grid (tuning knob GDF_RUN_BIG_BLOCKS)
 constexpr int kRunQ = 4;        // a streamed chunk: 64 x kRunQ points per wave step
 
 __device__ __forceinline__ void wave_sync() {
@@ -2652,9 +2658,8 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
 // The groups queued by k_group_runs: wave w of the grid takes queue slot w, then draws further
 // slots (qctr[1]) while any remain - no draw at all when the queue fits the grid - and streams the
 // runs of each (records rps / rlen by sorted run, written by k_group_runs) from global memory
-// (wave_stream_sum).  The last block to finish resets the counters (qctr[2] counts finished
-// blocks) for the next voxelize; the queue was complete when this launch began.  20 KiB of LDS
-// and <= 64 VGPRs per 4-wave block: 8 waves per SIMD stream at once.
+// (wave_stream_sum).  The queue was complete when this launch began; the first sort pass of the
+// next voxelize zeroes the counters.
 __global__ __launch_bounds__(256) void k_group_runs_big(const uint32_t* __restrict__ rps,
                                                         const uint32_t* __restrict__ rlen,
                                                         const float4* __restrict__ pts,
@@ -2680,12 +2685,6 @@ __global__ __launch_bounds__(256) void k_group_runs_big(const uint32_t* __restri
         if (d >= nq - waves) break;
         t = waves + d;
     }
-    __syncthreads();
-    if (threadIdx.x == 0 && atomicAdd(qctr + 2, 1u) == gridDim.x - 1u) {  // last block out
-        qctr[0] = 0u;
-        qctr[1] = 0u;
-        qctr[2] = 0u;
-    }
 }
 
 size_t voxelize_status_words(uint32_t nmax) {
@@ -2709,7 +2708,8 @@ static void launch_sort_pass(uint32_t tiles, hipStream_t s, const uint32_t* kin,
                        reinterpret_cast<uint32_t*>(a.ctrs + kCtrEpoch), a.err, 8 * p, dbits, tiles,
                        reinterpret_cast<uint4*>(a.grid8), a.marks, nwords, a.lifetime, a.gseq,
                        a.nframes, a.frame_shift, a.frame_pt_start, a.mark_words,
-                       reinterpret_cast<uint4*>(a.snapshots), a.snapshot_bytes / 16);
+                       reinterpret_cast<uint4*>(a.snapshots), a.snapshot_bytes / 16,
+                       p == 0 ? reinterpret_cast<uint32_t*>(a.ctrs + kCtrRunQueue) : nullptr);
 }
 
 hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hook) {
@@ -2787,7 +2787,7 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
                            kbuf[npasses & 1], vbuf[npasses & 1]);  // (free after the sort)
         if (a.average) {
             if ((e = hipGetLastError()) != hipSuccess) return e;
-            hipLaunchKernelGGL(k_group_runs_big, dim3(2048), dim3(256), 0, s, kbuf[npasses & 1],
+            hipLaunchKernelGGL(k_group_runs_big, dim3(g_run_big_blocks), dim3(256), 0, s, kbuf[npasses & 1],
                                vbuf[npasses & 1], a.pts, reinterpret_cast<float*>(a.out), a.bigq,
                                a.bigq_cap, qctr);
         }
