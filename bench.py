@@ -50,8 +50,8 @@ def parse():
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--workload", choices=("dense", "stress"), default="dense")
-    ap.add_argument("--ring", type=int, default=8, help="distinct device-resident frames")
-    ap.add_argument("--batch", type=int, default=4,
+    ap.add_argument("--ring", type=int, default=32, help="distinct device-resident frames")
+    ap.add_argument("--batch", type=int, default=8,
                     help="frames per launch chain (gdf_next_frame_in_batch); a step is one "
                          "batch, value counts every frame's pixels")
     ap.add_argument("--cameras", type=int, default=1,
@@ -461,6 +461,7 @@ def run_secondary(args, params):
     kt = not args.no_kernel_timing
     for name, (W, H, wl, ring, st_steps, B) in {
             "vga_single_frame": (640, 480, "dense", 8, steps, 1),
+            "vga_batch4": (640, 480, "dense", 32, steps, 4),
             "720p": (1280, 720, "dense", 4, steps, 4),
             "720p_single_frame": (1280, 720, "dense", 4, steps, 1),
             "4k": (3840, 2160, "dense", 2, max(20, steps // 4), 1),

@@ -831,9 +831,11 @@ void upload_depthmaps(gdf_engine* e) {  // fusion.cpp:1583-1593
         d.scale = c.scale;
         d.wmagic = ((1ull << 40) + c.W - 1) / c.W;
         // compaction segments: rows split into nchunk pieces of segw (a multiple of 64) pixels
-        // segment width: whole rows (up to 1024 px) for small frames, 256 px for frames over
-        // 2 Mi pixels, where more, smaller blocks per CU hide the band loads (4K: +20 %)
-        const uint32_t seg_items = e->seg_items ? e->seg_items : (e->depth_total > (1u << 21) ? 256u : kSegItems);
+        // segment width: whole rows (up to 1024 px) for small frames, 256 px for frames (or
+        // batches) over 1 Mi pixels, where more, smaller blocks per CU hide the band loads
+        // (measured on MI355X, dense frames, mask + emit: 4K 1024 -> 256 px 311 -> 237 us,
+        // 720p x4 140 -> 107 us; 128 px and 64 px lose again in the mask)
+        const uint32_t seg_items = e->seg_items ? e->seg_items : (e->depth_total > (1u << 20) ? 256u : kSegItems);
         d.nchunk = (c.W + seg_items - 1) / seg_items;
         d.segw = ((c.W + d.nchunk - 1) / d.nchunk + 63) / 64 * 64;
         d.nseg = c.H * d.nchunk;
@@ -1022,12 +1024,13 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel) {
         a.npasses = sort_bits(e) == 0 ? 1u : (sort_bits(e) + 7) / 8;
         // depth-only frames sort runs of equal keys (8-20x fewer items on dense frames); k_mask
         // counts the runs and their key digits (one flush per segment: few runs, few bins)
-        // (measured on MI355X, dense frames: 4K 18.2 -> 24.0 Gpoints/s; at VGA the extra key in
-        // k_mask costs what the shorter sort saves, so frames under 2 Mi pixels sort points)
+        // (measured on MI355X, dense frames: 4K 18.2 -> 24.0 Gpoints/s, a batch of four VGA frames
+        // 14.6 -> 16.8; a single VGA frame (0.3 Mi pixels) gains nothing: the extra key in k_mask
+        // costs what the shorter sort saves, so frames under 1 Mi pixels sort points)
         // Rollbuffer windows (10^7 points re-observing the same voxels) always sort runs: k_sel
         // counts them per tile.
         a.run_mode = e->use_runs && (a.sel_tiles || (a.total_segs && (e->force_runs ||
-                                                                      a.depth_total >= (1u << 21))))
+                                                                      a.depth_total >= (1u << 20))))
                          ? 1 : 0;
         // the run-key digits: k_mask's per-segment flush while there are few segments; above,
         // k_sort_hist over the runs (tens of thousands of flushes contend at the atomic units)
