@@ -77,22 +77,26 @@ def parse():
     return ap.parse_args()
 
 
-def model_bytes(P, n_avg, g_avg, ncells, B=1):
+def model_bytes(P, n_avg, g_avg, ncells, B=1, s_avg=None, runs=False):
     """Algorithmic HBM bytes per launch of each kernel: the bytes the algorithm
     must move once, not the cache traffic of an implementation.  A launch of a B-frame batch
     processes B frames (P, n, g per frame); its grid update reads and writes the grid once and
-    stores the B - 1 intermediate per-frame grids."""
+    stores the B - 1 intermediate per-frame grids.  s_avg: the items the voxelize sorts per
+    frame - the points, or (runs) the runs of equal voxel keys, which the sort and the group
+    phase then move instead of points."""
     P, n_avg, g_avg = B * P, B * n_avg, B * g_avg
+    s_items = B * (s_avg if s_avg is not None else n_avg / B)
     tiles = (P + 255) // 256
     return {
         "mask": 3.0 * P,                           # u16 depth in, u8 stage bits out
         "scan": 8.0 * tiles,
-        "emit": 1.0 * P + 22.0 * n_avg,            # stage in, depth of kept px, xyzw + key out
-        # 3 radix passes (key only in, key+index out; then key+index both ways) + the grid
-        # update carried by the first pass, averaged per launch
-        "sort": (12.0 * n_avg + 16.0 * n_avg * 2 + (B + 1.0) * ncells) / 3.0,
-        # sorted keys + indices + gathered points in, means out
-        "group": 24.0 * n_avg + 16.0 * g_avg,
+        # stage in, depth of kept px, xyzw + key out (+ key and first point of each run)
+        "emit": 1.0 * P + 22.0 * n_avg + (8.0 * s_items if runs else 0.0),
+        # 3 radix passes over the sorted items (key only in, key+index out; then key+index both
+        # ways) + the grid update carried by the first pass, averaged per launch
+        "sort": (12.0 * s_items + 16.0 * s_items * 2 + (B + 1.0) * ncells) / 3.0,
+        # sorted keys + indices (+ the runs' point ranges) in, points in, means out
+        "group": (16.0 * n_avg + 16.0 * s_items if runs else 24.0 * n_avg) + 16.0 * g_avg,
         "grid": (B + 1.0) * ncells,
     }
 
@@ -167,6 +171,20 @@ class DepthStream:
             nvox.append(r.num_voxelized)
         return npts, nvox
 
+    def sort_items(self, params, batch):
+        """Items one batch's voxelize sorts per frame (runs of equal keys in run mode), from one
+        synchronous batched frame, and whether they are runs."""
+        self.eng.clear()
+        for j in range(batch):
+            if j:
+                self.eng.nextFrameInBatch()
+            for k, c in enumerate(self.cams):
+                self.eng.addDepthmapDevice(self.dframes[k][j % self.ring].ptr, self.W, self.H,
+                                           *c.intrinsics(), c.T_world, c.T_crop)
+        self.eng.processFrame(params, synchronous=True)
+        items, runs = self.eng.last_sort_items()
+        return items / batch, runs
+
     def run(self, pc, first, count, batch=1):
         """`count` steps of `batch` frames from frame `first * batch` on."""
         if batch > 1:
@@ -200,7 +218,8 @@ def time_single(st, params, steps, warmup, depth, kernel_timing, pmc_key, batch=
     idx = [((prime + warmup + i) * batch + j) % st.ring for i in range(steps) for j in range(batch)]
     n_avg = float(np.mean([npts[i] for i in idx]))
     g_avg = float(np.mean([nvox[i] for i in idx]))
-    mb = model_bytes(st.P, n_avg, g_avg, ncells, batch)
+    s_avg, runs = st.sort_items(params, batch)
+    mb = model_bytes(st.P, n_avg, g_avg, ncells, batch, s_avg, runs)
     roof = None
     if kernel_timing:
         kt_steps = min(steps, 200)
@@ -307,7 +326,7 @@ def main():
     eng = GPUDepthmapFusion(local_rank)
     st = DepthStream(eng, W, H, K, rank, args.workload, args.ring)
     P = st.P
-    pmc_key = f"{W}x{H}/{args.workload}"
+    pmc_key = f"{W}x{H}/{args.workload}" + (f"/b{args.batch}" if args.batch > 1 else "")
 
     if dist is None:
         line = time_single(st, params, args.steps, args.warmup, max(1, min(4, args.pipeline)),
@@ -469,7 +488,7 @@ def run_secondary(args, params):
         eng = GPUDepthmapFusion(0)
         st = DepthStream(eng, W, H, 1, 0, wl, ring)
         r = time_single(st, params, st_steps, warm, max(1, min(4, args.pipeline)), kt,
-                        f"{W}x{H}/{wl}", B)
+                        f"{W}x{H}/{wl}" + (f"/b{B}" if B > 1 else ""), B)
         r["workload"] = workload_name(W, H, 1, wl)
         out[name] = r
         del st

@@ -237,6 +237,10 @@ int gdf_get_device_results(gdf_engine* engine, const float** points, const uint3
 int gdf_process_frame(gdf_engine* engine, const gdf_frame_params* params,
                       gdf_frame_result* out_result);
 
+/* Instrumentation (no reference counterpart): the items the last synchronous gdf_process_frame's
+ * voxelize sorted - runs of equal voxel keys (*runs = 1) or points (*runs = 0). */
+int gdf_last_sort_items(gdf_engine* engine, uint32_t* items, int* runs);
+
 /* ---- orphan shaders of the reference (device buffers, the engine's stream) ------------------ */
 /* mask_dilate (shader/mask_dilate.glsl:40-67; never dispatched by the reference): for every pixel
  * of a width x height u32 mask, a zero in the (2F+1)^2 window clipped to the image writes 0;

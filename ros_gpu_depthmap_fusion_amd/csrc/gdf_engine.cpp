@@ -279,6 +279,8 @@ struct gdf_engine {
     std::vector<CamTable> tables = std::vector<CamTable>(kMaxCams);
     std::vector<CamDesc> h_cams;
     uint32_t mask_blocks = 0;       // compaction segments over the emitting cameras
+    uint32_t last_sort_items = 0;   // items the last synchronous frame's voxelize sorted
+    bool last_sort_runs = false;    // ... runs of equal keys (else points)
     uint32_t max_segw = 0;          // widest segment (sizes k_mask's LDS band)
     bool depth_uploaded = false;
 
@@ -1859,9 +1861,21 @@ int gdf_process_frame(gdf_engine* e, const gdf_frame_params* p, gdf_frame_result
             e->read_misc();
             res.num_points = e->sl().h_misc[kCount];
             res.num_voxelized = p->enable_voxel_filter && !p->defer_voxelize ? e->sl().h_misc[kVoxCount] : 0;
+            // what the voxelize sorted: runs of equal keys, or points
+            const bool runs = e->sl().runs_valid && p->enable_voxel_filter && !p->defer_voxelize;
+            e->last_sort_runs = runs;
+            e->last_sort_items = runs ? e->sl().h_misc[e->sl().runs_sel ? kRunTotal : kRunCount]
+                                      : res.num_points;
         }
         if (r) *r = res;
     });
+}
+
+int gdf_last_sort_items(gdf_engine* e, uint32_t* items, int* runs) {
+    ENGINE_OR_FAIL(e);
+    if (items) *items = e->last_sort_items;
+    if (runs) *runs = e->last_sort_runs ? 1 : 0;
+    return GDF_OK;
 }
 
 int gdf_mask_dilate(gdf_engine* e, const uint32_t* in, uint32_t* out, uint32_t W, uint32_t H,

@@ -104,7 +104,7 @@ EXPORTED = [
     "gdf_run_depth_stream", "gdf_run_host_stream", "gdf_run_depth_stream_batched",
     "gdf_next_frame_in_batch", "gdf_get_batch_ranges", "gdf_download_batch_occupancy_grid",
     "gdf_mask_dilate", "gdf_transform_points", "gdf_add_halo_depthmap_device",
-    "gdf_partition_points", "gdf_voxelize_points",
+    "gdf_partition_points", "gdf_voxelize_points", "gdf_last_sort_items",
 ]
 
 
@@ -184,6 +184,7 @@ def load_library(path: str = LIB_PATH):
         "gdf_transform_points": (i32, [vp, vp, vp, vp, u32, vp]),
         "gdf_get_batch_ranges": (i32, [vp, vp, vp, u32, P(u32)]),
         "gdf_download_batch_occupancy_grid": (i32, [vp, u32, vp, u64]),
+        "gdf_last_sort_items": (i32, [vp, P(u32), P(i32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -641,6 +642,13 @@ class GPUDepthmapFusion:
         self._check(self._lib.gdf_download_batch_occupancy_grid(self._h, frame, _ptr(out),
                                                                 out.shape[0]))
         return out[:nc]
+
+    def last_sort_items(self):
+        """(items, runs): what the last synchronous processFrame's voxelize sorted - runs of
+        equal voxel keys (runs True) or points (instrumentation; include/gdf.h)."""
+        n, r = C.c_uint32(0), C.c_int(0)
+        self._check(self._lib.gdf_last_sort_items(self._h, C.byref(n), C.byref(r)))
+        return n.value, bool(r.value)
 
     def processFramePrepared(self, p: FrameParams) -> FrameResult:
         """processFrame with parameters already converted by ComponentParams.to_c (a stream of

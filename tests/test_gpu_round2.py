@@ -383,3 +383,21 @@ def test_run_mode_small_frames_forced(Engine, monkeypatch):
                               bits(orc.downloadVoxelizedPoints()[:, :3]))
         np.testing.assert_array_equal(gpu.downloadBatchVoxelOccupancyGrid(j),
                                       orc.downloadVoxelOccupancyGrid())
+
+
+@pytest.mark.gpu
+def test_last_sort_items_reports_runs(Engine, monkeypatch):
+    """gdf_last_sort_items (the bench's byte model): points when the voxelize sorts points, the
+    runs of equal keys (fewer, >= the voxels) when it sorts runs; counts of a synchronous frame."""
+    cam = synth.make_camera(0, 320, 240)
+    args = [cam_args(cam, synth.dense_frame(cam, 0, 3))]
+    p = ComponentParams()
+    gpu = Engine()
+    r = run_fused(gpu, args, p)
+    items, runs = gpu.last_sort_items()
+    assert not runs and items == r.num_points
+    monkeypatch.setenv("GDF_FORCE_RUNS", "1")
+    gpu2 = Engine()
+    r2 = run_fused(gpu2, args, p)
+    items2, runs2 = gpu2.last_sort_items()
+    assert runs2 and r2.num_voxelized <= items2 < r2.num_points

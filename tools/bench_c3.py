@@ -81,6 +81,7 @@ def run_c3(width=1280, height=720, window=256, steps=20, ring=4, profile_steps=5
     r = frame(pc_sync)
     st = eng.rollbuffer_state()
     S, N, G = st.selection_point_count, r.num_points, r.num_voxelized
+    NS, runs = eng.last_sort_items()  # what the voxelize sorts: runs of equal keys, or points
     # survivors of the depth part alone (a frame with the depth map only, no selection)
     (gx, gy, gz), ncells = eng.grid_size()
     probe = GPUDepthmapFusion(0)
@@ -121,8 +122,8 @@ def run_c3(width=1280, height=720, window=256, steps=20, ring=4, profile_steps=5
         "emit": 1.0 * P + 22.0 * N_depth,                        # depth survivors: point + key
         # selected ring points in once, survivors (point + key) written once at their place
         "sel": 16.0 * S + 20.0 * N_sel,
-        "sort": (12.0 * N + 16.0 * N * 2 + 2.0 * ncells) / 3.0,
-        "group": 24.0 * N + 16.0 * G,
+        "sort": (12.0 * NS + 16.0 * NS * 2 + 2.0 * ncells) / 3.0,
+        "group": (16.0 * N + 16.0 * NS if runs else 24.0 * N) + 16.0 * G,
         "ps_insert": 32.0 * P,                                   # new sequence in, ring out
         "scan": 8.0 * (items / seg),
     }
@@ -151,6 +152,7 @@ def run_c3(width=1280, height=720, window=256, steps=20, ring=4, profile_steps=5
                                "points (timespan select, transform, crop, compaction, voxelize, "
                                "grid %dx%dx%d)" % (W, H, window, P, gx, gy, gz),
                    "selected_points": S, "points_after_crop": N, "voxels": G,
+                   "sorted_items": NS, "sorted_items_are_runs": runs,
                    "depth_points_after_crop": N_depth,
                    "points_per_voxel": group_sizes,
                    "grid_cells": ncells},

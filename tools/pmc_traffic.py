@@ -8,7 +8,7 @@ FETCH_SIZE / WRITE_SIZE are in KiB.  gfx950 correction (same guide, "HBM"): FETC
 taken as is.  Both are calibrated only for 16-B-per-lane streams: narrower access widths (the
 2-B depth loads of k_mask) are reported with the same rule and flagged as uncalibrated.
 
-    python tools/pmc_traffic.py FETCH.csv WRITE.csv --workload 640x480/dense [--out profiles/pmc_traffic.json]
+    python tools/pmc_traffic.py FETCH.csv WRITE.csv --workload 640x480/dense/b8 [--out profiles/pmc_traffic.json]
 
 The output maps workload -> kernel slot -> bytes per launch (bench.py reads the entry of its
 own workload; a launch of a multi-frame batch covers the batch).
@@ -19,8 +19,9 @@ import csv
 import json
 
 SLOT = {"k_mask": "mask", "k_emit": "emit", "k_sort_pass": "sort", "k_group": "group",
+        "k_group_runs": "group", "k_group_big": "group_big", "k_group_runs_big": "group_big",
         "k_scan_counts": "scan", "k_grid_u8": "grid", "k_grid_u32": "grid", "k_sel": "sel",
-        "k_sel_place": "sel_place", "k_sort_hist": "sort_hist", "k_group_count": "group_count"}
+        "k_sort_hist": "sort_hist", "k_group_count": "group_count"}
 
 
 def per_kernel(path, counter):
