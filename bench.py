@@ -67,6 +67,9 @@ def parse():
                     help="N > 1: frames per occupancy-mark all-gather (1 = every frame, the "
                          "reference's per-frame grid; B > 1 = deferred grid, B frames per "
                          "all-gather)")
+    ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                    help="N > 1: RCCL (default) or gloo with host-staged tensors (smoke runs of "
+                         "several ranks on one GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=3.0, help="per CPU run (5 runs)")
     ap.add_argument("--no-kernel-timing", action="store_true",
@@ -312,8 +315,13 @@ def main():
         import torch.distributed as dist
         rank = int(os.environ.get("RANK", "0"))
         local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.dist_backend == "gloo":  # (host-staged collectives: a smoke run of N ranks on
+            local_rank %= max(1, torch.cuda.device_count())  # fewer GPUs)
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         world = dist.get_world_size()
     import numpy as np
     from ros_gpu_depthmap_fusion_amd import build_library, hiprt
@@ -354,7 +362,8 @@ def main():
             "config": dict({"workload": "C2: " + workload_name(W, H, K, args.workload) + (
                                 "; a step = a batch of %d frames through one launch chain "
                                 "(every frame's points, voxel means and grid)" % args.batch
-                                if args.batch > 1 and dist is None else ""),
+                                if args.batch > 1 and (dist is None or args.multi_mode == "fused")
+                                else ""),
                             "cameras_per_gpu": K}, **line, **cfg_extra),
             "roofline": roof,
             "cpu_baseline": cpu,
@@ -385,13 +394,19 @@ def time_multi(args, st, params, dist, world, pmc_key):
         from ros_gpu_depthmap_fusion_amd.multi import FusedCloudRank
         rank = dist.get_rank()
         cams = [synth.make_camera(k, st.W, st.H) for k in range(world)]
-        fr = FusedCloudRank(eng, cams, rank, world, params, dev="cuda")
+        fr = FusedCloudRank(eng, cams, rank, world, params,
+                            dev="cuda" if args.dist_backend == "nccl" else "cpu")
         n = st.W * st.H
+        B = max(1, args.batch)
 
         def run(first, count):
             for i in range(first, first + count):
-                d = st.dframes[0][i % st.ring].ptr
-                fr.frame(d, d + 2 * (n - fr.Lmax))
+                if B > 1:  # a step = B frames through one launch chain and one exchange
+                    ds = [st.dframes[0][(i * B + j) % st.ring].ptr for j in range(B)]
+                    fr.batch(ds, [d + 2 * (n - fr.Lmax) for d in ds])
+                else:
+                    d = st.dframes[0][i % st.ring].ptr
+                    fr.frame(d, d + 2 * (n - fr.Lmax))
     else:
         batched = args.exchange_batch > 1
         if batched:
@@ -431,14 +446,18 @@ def time_multi(args, st, params, dist, world, pmc_key):
     run(prime + args.warmup, args.steps)
     barrier_sync()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    t = torch.tensor([elapsed], dtype=torch.float64,
+                     device="cuda" if args.dist_backend == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    idx = [(prime + args.warmup + i) % st.ring for i in range(args.steps)]
+    fpb = max(1, args.batch) if fused else 1  # frames per step
+    idx = [((prime + args.warmup + i) * fpb + j) % st.ring for i in range(args.steps)
+           for j in range(fpb)]
     n_avg = float(np.mean([npts[i] for i in idx]))
     g_avg = float(np.mean([nvox[i] for i in idx]))
     line = {
-        "value": round(world * st.P * args.steps / elapsed / 1e6, 3),
+        "value": round(world * st.P * fpb * args.steps / elapsed / 1e6, 3),
+        "frames_per_step": fpb,
         "ms_per_step": round(elapsed / args.steps * 1e3, 5), "prime": prime,
         "points_per_frame_after_crop": round(n_avg), "voxels_per_frame": round(g_avg),
         "grid": [gx, gy, gz], "grid_cells": ncells, "frames_in_flight": depth,
@@ -453,15 +472,16 @@ def time_multi(args, st, params, dist, world, pmc_key):
         barrier_sync()
         kt = eng.kernel_times()
         eng.set_profiling(False)
-        line["roofline"] = roofline_from(kt, kt_steps, model_bytes(st.P, n_avg, g_avg, ncells),
+        line["roofline"] = roofline_from(kt, kt_steps, model_bytes(st.P, n_avg, g_avg, ncells, fpb),
                                          pmc_key)
     if fused:
-        cfg = {"parallelism": "camera-per-GPU x%d; per frame: depth-tail halo all-gather, "
-                              "occupancy-mark all-gather, key-range all-to-all of the (point, "
-                              "key) lists, voxelize per key range (fused cloud = one engine over "
-                              "all cameras)" % world,
-               "exchange": "halo %d px + %d-word marks + points all-to-all per frame" % (
-                   fr.Lmax, (ncells + 31) // 32)}
+        cfg = {"parallelism": "camera-per-GPU x%d; per step of %d frames (one launch chain): "
+                              "depth-tail halo all-gather, occupancy-mark all-gather + batched "
+                              "grid update, key-range all-to-all of the (point, frame | key) "
+                              "lists, voxelize per key range (fused cloud = one engine over all "
+                              "cameras, per frame)" % (world, fpb),
+               "exchange": "per step of %d frames: halo %d px + %d-word marks per frame, one "
+                           "points all-to-all" % (fpb, fr.Lmax, (ncells + 31) // 32)}
     else:
         cfg = {"parallelism": "camera-per-GPU x%d, occupancy-mark all-gather %s (voxel means per "
                               "camera)" % (world, "every frame" if not batched else

@@ -279,6 +279,7 @@ struct gdf_engine {
     std::vector<CamTable> tables = std::vector<CamTable>(kMaxCams);
     std::vector<CamDesc> h_cams;
     uint32_t mask_blocks = 0;       // compaction segments over the emitting cameras
+    uint64_t index_end = 0;         // end of the cameras' index space (halo gaps included)
     uint32_t last_sort_items = 0;   // items the last synchronous frame's voxelize sorted
     bool last_sort_runs = false;    // ... runs of equal keys (else points)
     uint32_t max_segw = 0;          // widest segment (sizes k_mask's LDS band)
@@ -787,36 +788,46 @@ void upload_depthmaps(gdf_engine* e) {  // fusion.cpp:1583-1593
     // reference's concatenated buffer, at negative offsets; only their last `tail` pixels exist
     // (a virtual base pointer: the flying-pixel reads reach back at most F rows + F pixels,
     // checked in frame_args)
+    // Index space: a frame's halo camera sits right before the frame's first depth map (frame 0's
+    // at negative offsets, later frames' in a gap after the previous frame's cameras), so every
+    // frame's top-border reads resolve exactly as in the reference's concatenated buffer.
     e->halo.clear();
-    {
-        int64_t hoff = 0;
-        for (size_t j = e->halo_cams.size(); j-- > 0;) hoff -= (int64_t)e->halo_cams[j].n;
-        for (size_t j = 0; j < e->halo_cams.size(); ++j) {
-            const Cam& c = e->halo_cams[j];
-            CamDesc d{};
-            d.off = hoff;
-            d.depth = c.dev - (c.n - e->halo_tail[j]);
-            ensure_table(e, j, c);
-            d.xn = e->tables[j].xn.as<float>();
-            d.yn = e->tables[j].yn.as<float>();
-            d.W = c.W; d.H = c.H; d.n = c.n; d.emit = 0;
-            d.scale = c.scale;
-            d.wmagic = ((1ull << 40) + c.W - 1) / c.W;
-            d.frame = 0;
-            std::memcpy(d.Tw, c.Tw, 64);
-            std::memcpy(d.Tc, c.Tc, 64);
-            e->halo.push_back(d);
-            hoff += c.n;
-        }
-    }
+    auto halo_desc = [&](size_t j, int64_t off) {
+        const Cam& c = e->halo_cams[j];
+        CamDesc d{};
+        d.off = off;
+        d.depth = c.dev - (c.n - e->halo_tail[j]);
+        ensure_table(e, j, c);
+        d.xn = e->tables[j].xn.as<float>();
+        d.yn = e->tables[j].yn.as<float>();
+        d.W = c.W; d.H = c.H; d.n = c.n; d.emit = 0;
+        d.scale = c.scale;
+        d.wmagic = ((1ull << 40) + c.W - 1) / c.W;
+        d.frame = c.frame;
+        std::memcpy(d.Tw, c.Tw, 64);
+        std::memcpy(d.Tc, c.Tc, 64);
+        return d;
+    };
     e->h_cams.clear();
     e->mask_blocks = 0;
     e->max_segw = 0;
-    uint64_t off = 0, hoff = 0;
+    int64_t off = 0;
+    uint64_t hoff = 0;
+    size_t hj = 0;  // next halo camera (in frame order)
+    std::vector<CamDesc> ordered;  // halo of frame f, then frame f's depth maps
     for (size_t k = 0; k < e->cams.size(); ++k) {
         const Cam& c = e->cams[k];
+        if (hj < e->halo_cams.size() && e->halo_cams[hj].frame == c.frame &&
+            (k == 0 || e->cams[k - 1].frame != c.frame)) {
+            const int64_t hn = (int64_t)e->halo_cams[hj].n;
+            const int64_t hstart = hj == 0 && k == 0 ? -hn : off;
+            ordered.push_back(halo_desc(hj, hstart));
+            e->halo.push_back(ordered.back());
+            if (hstart >= 0) off += hn;  // (later frames: the halo takes a gap in the index space)
+            ++hj;
+        }
         CamDesc d{};
-        d.off = (int64_t)off;
+        d.off = off;
         if (c.dev) {
             d.depth = c.dev;
         } else {
@@ -825,9 +836,9 @@ void upload_depthmaps(gdf_engine* e) {  // fusion.cpp:1583-1593
             d.depth = dst;
             hoff += c.n;
         }
-        ensure_table(e, e->halo.size() + k, c);
-        d.xn = e->tables[e->halo.size() + k].xn.as<float>();
-        d.yn = e->tables[e->halo.size() + k].yn.as<float>();
+        ensure_table(e, e->halo_cams.size() + k, c);
+        d.xn = e->tables[e->halo_cams.size() + k].xn.as<float>();
+        d.yn = e->tables[e->halo_cams.size() + k].yn.as<float>();
         d.W = c.W; d.H = c.H; d.n = c.n; d.emit = 1;
         d.frame = c.frame;
         d.scale = c.scale;
@@ -847,18 +858,20 @@ void upload_depthmaps(gdf_engine* e) {  // fusion.cpp:1583-1593
         std::memcpy(d.Tw, c.Tw, 64);
         std::memcpy(d.Tc, c.Tc, 64);
         e->h_cams.push_back(d);
+        ordered.push_back(d);
         off += c.n;
     }
+    if (hj != e->halo_cams.size()) fail(GDF_ERR_STATE, "a halo camera without a depth map in its frame");
+    e->index_end = (uint64_t)std::max<int64_t>(off, 0);
     if (staged) {  // the staging is free again once these copies have run
         Slot& q = e->sl();
         if (!q.h2d_done) HIPCHK(hipEventCreateWithFlags(&q.h2d_done, hipEventDisableTiming));
         HIPCHK(hipEventRecord(q.h2d_done, e->s()));
         q.h2d_pending = true;
     }
-    // halo cameras first (negative offsets), then the emitting cameras: sorted by offset
-    std::vector<CamDesc> all = e->halo;
-    all.insert(all.end(), e->h_cams.begin(), e->h_cams.end());
-    e->h_cams = all;
+    // every frame's halo right before the frame's depth maps: sorted by offset (k_emit finds a
+    // frame's first camera by its predecessor)
+    e->h_cams = ordered;
     e->depth_uploaded = true;
 }
 
@@ -1075,19 +1088,25 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel) {
         a.band_rowb = ((cols * 2 + 15) / 16 + 1) * 16;
         a.band_lds = (2 * h + 1) * a.band_rowb + (a.seg_threads * 2) * 4;
     }
-    if (e->debug) {
-        e->sl().d_stage.ensure((size_t)std::max<uint32_t>(e->sl().n_total, 1));
+    if (e->debug) {  // (stage bits by global index: halo gaps included)
+        e->sl().d_stage.ensure(std::max<size_t>({(size_t)e->sl().n_total, (size_t)e->index_end + sel, 1}));
         a.dbg = e->sl().d_stage.as<uint8_t>();
     }
     e->sl().dbg_count = e->sl().n_total;
     a.err = e->sl().d_misc.as<uint32_t>() + kErr;
     if (!e->halo_cams.empty() && a.do_flying && !e->cams.empty()) {
-        const uint64_t reach = (uint64_t)a.F * e->cams[0].W + a.F;  // deepest read into the halo
-        if (reach > e->halo_cams[0].n)
-            fail(GDF_ERR_ARG, "halo camera shorter than F rows of the first camera (reads would "
-                              "reach the camera before it)");
-        if (e->halo_tail[0] < reach)
-            fail(GDF_ERR_ARG, "halo depth map tail shorter than F rows + F pixels of the first camera");
+        for (size_t j = 0; j < e->halo_cams.size(); ++j) {  // each halo against its frame's camera
+            const Cam* first = nullptr;
+            for (const Cam& c : e->cams)
+                if (c.frame == e->halo_cams[j].frame) { first = &c; break; }
+            if (!first) continue;
+            const uint64_t reach = (uint64_t)a.F * first->W + a.F;  // deepest read into the halo
+            if (reach > e->halo_cams[j].n)
+                fail(GDF_ERR_ARG, "halo camera shorter than F rows of the frame's first camera "
+                                  "(reads would reach the camera before it)");
+            if (e->halo_tail[j] < reach)
+                fail(GDF_ERR_ARG, "halo depth map tail shorter than F rows + F pixels of the frame's first camera");
+        }
     }
     a.nframes = e->nframes;
     a.frame_shift = e->nframes > 1 ? e->key_bits : 0u;
@@ -1205,7 +1224,9 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime,
     v.frame_shift = e->nframes > 1 ? e->key_bits : 0u;
     v.mark_words = mark_words(e);
     if (e->nframes > 1) {
-        v.frame_pt_start = v.run_start ? nullptr : e->sl().d_fstart.as<uint32_t>();
+        // (frame bits from the point ranges - not for runs, whose keys carry them, nor for an
+        // external list, whose keys carry them too: gdf_partition_points of a batch)
+        v.frame_pt_start = v.run_start || src ? nullptr : e->sl().d_fstart.as<uint32_t>();
         e->sl().d_fvox.ensure((size_t)(e->nframes + 1) * 4);
         v.frame_vox_start = e->sl().d_fvox.as<uint32_t>();
         const uint64_t padded = (e->ncells + 31) / 32 * 32;
@@ -1549,9 +1570,13 @@ int gdf_add_halo_depthmap_device(gdf_engine* e, const uint16_t* tail, uint32_t t
         if (!tail || !Tw || !Tc || W == 0 || H == 0 || tail_pixels == 0 ||
             (uint64_t)tail_pixels > (uint64_t)W * H)
             fail(GDF_ERR_ARG, "halo depth map: bad argument");
-        if (!e->halo_cams.empty()) fail(GDF_ERR_STATE, "one halo camera per frame");
-        if (!e->cams.empty()) fail(GDF_ERR_STATE, "the halo camera comes before the depth maps");
+        const uint32_t fr = e->nframes - 1;  // the current frame of a batch
+        if (!e->halo_cams.empty() && e->halo_cams.back().frame == fr)
+            fail(GDF_ERR_STATE, "one halo camera per frame");
+        if (!e->cams.empty() && e->cams.back().frame == fr)
+            fail(GDF_ERR_STATE, "the halo camera comes before the frame's depth maps");
         Cam c;
+        c.frame = fr;
         c.dev = tail;
         c.W = W; c.H = H; c.n = W * H;
         c.scale = scale; c.fx = fx; c.fy = fy; c.cx = cx; c.cy = cy;
@@ -1801,9 +1826,13 @@ int gdf_process_frame(gdf_engine* e, const gdf_frame_params* p, gdf_frame_result
                 fail(GDF_ERR_STATE, "frame batches carry depth maps only (no point sequences)");
             if (e->cams.empty() || e->cams.back().frame != e->nframes - 1)
                 fail(GDF_ERR_STATE, "every frame of a batch needs a depth map");
-            if (p->enable_voxel_filter && (p->defer_occupancy_grid || p->occupancy_lifetime > 255))
+            if (p->enable_voxel_filter && !p->defer_voxelize &&
+                (p->defer_occupancy_grid || p->occupancy_lifetime > 255))
                 fail(GDF_ERR_STATE, "frame batches need the fused grid update (lifetime <= 255, "
                                     "not deferred)");
+            if (p->enable_voxel_filter && p->defer_voxelize && !p->defer_occupancy_grid)
+                fail(GDF_ERR_STATE, "a batch with deferred voxelize defers its grid update too "
+                                    "(gdf_take_occupancy_marks + gdf_voxel_occupancy_grid_batch)");
             if (e->nframes > kMaxCams) fail(GDF_ERR_ARG, "at most 16 frames per batch");
         }
         res.processed = 1;
@@ -1917,7 +1946,9 @@ int gdf_partition_points(gdf_engine* e, uint32_t nparts, float* send_pts, uint32
                                 q.d_misc.as<uint32_t>() + kCount, nmax, nparts, e->ncells,
                                 q.d_pcnt.as<uint32_t>(), q.d_poff.as<uint32_t>(),
                                 q.d_misc.as<uint32_t>() + kPartTotal,
-                                reinterpret_cast<float4*>(send_pts), send_keys, part_counts, e->s()));
+                                reinterpret_cast<float4*>(send_pts), send_keys, part_counts, e->s(),
+                                q.nframes > 1 ? q.d_fstart.as<uint32_t>() : nullptr, q.nframes,
+                                q.nframes > 1 ? e->key_bits : 0u));
     });
 }
 
@@ -2021,7 +2052,10 @@ int gdf_take_occupancy_marks(gdf_engine* e, uint32_t* bits, uint64_t words) {
     return guarded(e, [&] {
         if (!e->grid_set || !bits) fail(GDF_ERR_STATE, "no voxel grid");
         if (words < (e->ncells + 31) / 32) fail(GDF_ERR_CAPACITY, "mark bitmask too small");
-        HIPCHK(launch_take_marks(marks_ptr(e), mark_words(e), bits, e->s()));
+        // a batch: every frame's marks when the buffer holds them (frame f at f * mark words)
+        const uint64_t nf = e->sl().nframes > 1 && words >= e->sl().nframes * mark_words(e)
+                                ? e->sl().nframes : 1;
+        HIPCHK(launch_take_marks(marks_ptr(e), mark_words(e) * nf, bits, e->s()));
         e->sl().marks_set = false;
     });
 }

@@ -2923,9 +2923,15 @@ __global__ __launch_bounds__(256) void k_part_scatter(const float4* __restrict__
                                                       const uint32_t* __restrict__ total,
                                                       float4* __restrict__ out_pts,
                                                       uint32_t* __restrict__ out_keys,
-                                                      uint32_t* __restrict__ part_counts) {
+                                                      uint32_t* __restrict__ part_counts,
+                                                      const uint32_t* __restrict__ fstart,
+                                                      uint32_t nframes, uint32_t fshift) {
     __shared__ uint32_t s_w[4][kMaxParts];  // per-wave running counts (slot-major order)
     __shared__ uint32_t s_base[kMaxParts];
+    __shared__ uint32_t s_fstart[kMaxCams + 1];
+    // a batch (fstart): the sent key carries the point's frame above the voxel key, the part
+    // comes from the voxel key alone
+    if (fstart) load_fstart(s_fstart, fstart, nframes);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t n = *count;
     if (blockIdx.x == 0 && threadIdx.x < nparts) {
@@ -2979,7 +2985,7 @@ __global__ __launch_bounds__(256) void k_part_scatter(const float4* __restrict__
             if (i < n) {
                 const uint32_t pos = s_base[part[q]] + s_w[w][part[q]] + rank[q];
                 out_pts[pos] = p[q];
-                out_keys[pos] = key[q];
+                out_keys[pos] = fstart ? key[q] | (frame_of(s_fstart, nframes, i) << fshift) : key[q];
             }
         }
         __syncthreads();
@@ -2991,7 +2997,8 @@ uint32_t part_tiles(uint32_t nmax) { return (nmax + kPartTile - 1) / kPartTile; 
 hipError_t launch_partition(const float4* pts, const uint32_t* keys, const uint32_t* count,
                             uint32_t nmax, uint32_t nparts, uint64_t ncells, uint32_t* counts,
                             uint32_t* offsets, uint32_t* total, float4* out_pts,
-                            uint32_t* out_keys, uint32_t* part_counts, hipStream_t s) {
+                            uint32_t* out_keys, uint32_t* part_counts, hipStream_t s,
+                            const uint32_t* fstart, uint32_t nframes, uint32_t fshift) {
     const uint32_t ntiles = std::max<uint32_t>(part_tiles(nmax), 1u);
     const uint32_t blocks = std::min<uint32_t>(ntiles, 2048u);
     hipLaunchKernelGGL(k_part_count, dim3(blocks), dim3(256), 0, s, keys, count, nparts, ncells,
@@ -3010,7 +3017,8 @@ hipError_t launch_partition(const float4* pts, const uint32_t* keys, const uint3
                        partial, (const uint32_t*)nullptr, 1u);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(k_part_scatter, dim3(blocks), dim3(256), 0, s, pts, keys, count, nparts,
-                       ncells, ntiles, offsets, total, out_pts, out_keys, part_counts);
+                       ncells, ntiles, offsets, total, out_pts, out_keys, part_counts, fstart,
+                       nframes, fshift);
     return hipGetLastError();
 }
 

@@ -136,14 +136,17 @@ hipError_t launch_transform_points(const float4* in, const uint32_t* mask, float
                                    const float* T, hipStream_t s);
 
 // multi-GPU fused cloud: stable partition of (points, keys)[*count] into nparts key ranges,
-// part-major into out_pts / out_keys; part_counts[p] = items of part p (device).  Workspace:
+// part-major into out_pts / out_keys; part_counts[p] = items of part p (device).  A batch
+// (fstart: the frames' point starts): the sent keys carry the frame index above bit fshift.  Workspace:
 // counts [nparts * part_tiles(nmax)], offsets [seg_offsets_words(nparts * part_tiles(nmax))],
 // total [1].
 uint32_t part_tiles(uint32_t nmax);
 hipError_t launch_partition(const float4* pts, const uint32_t* keys, const uint32_t* count,
                             uint32_t nmax, uint32_t nparts, uint64_t ncells, uint32_t* counts,
                             uint32_t* offsets, uint32_t* total, float4* out_pts,
-                            uint32_t* out_keys, uint32_t* part_counts, hipStream_t s);
+                            uint32_t* out_keys, uint32_t* part_counts, hipStream_t s,
+                            const uint32_t* fstart = nullptr, uint32_t nframes = 1,
+                            uint32_t fshift = 0);
 
 // multi-GPU occupancy marks: export = copy of the mark bitmask, import = OR of nranks masks
 hipError_t launch_export_marks(const uint32_t* marks, uint64_t words, uint32_t* bits, hipStream_t s);

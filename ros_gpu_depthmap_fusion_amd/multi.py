@@ -312,6 +312,103 @@ class FusedCloudRank:
         return counts
 
 
+    def batch(self, depth_ptrs, tail_src_ptrs):
+        """B frames through one launch chain and ONE exchange (the bench's batched steps): every
+        rank's B tails in one all-gather (frame j's halo before frame j's depth map), the batch's
+        compaction, the B frames' marks in one all-gather and one batched grid update
+        (gdf_voxel_occupancy_grid_batch: frame by frame in order), the (point, frame | key)
+        lists partitioned by voxel-key range and exchanged once, and one voxelize of the rank's
+        range - frame f's voxels of this range are eng.batch_ranges()[1][f:f+2]."""
+        import numpy as np
+        import torch
+        import torch.distributed as dist
+        h = self.hiprt
+        eng, c = self.eng, self.cams[self.rank]
+        B = len(depth_ptrs)
+        L2 = 2 * self.Lmax
+        halo_ptr = None
+        keep = []
+        if self.F > 0 and self.world > 1:
+            if self.dev == "cuda":
+                tail = torch.empty(B * L2, dtype=torch.uint8, device="cuda")
+                for j, src in enumerate(tail_src_ptrs):
+                    h.check(h.hip().hipMemcpy(tail.data_ptr() + j * L2, src, L2, h.D2D), "tail")
+                parts = all_gather_tails(tail)
+                if self.rank > 0:
+                    keep.append(parts[self.rank - 1])
+                    halo_ptr = parts[self.rank - 1].data_ptr()
+            else:
+                tail = torch.from_numpy(np.concatenate(
+                    [_d2h(h, src, np.uint8, L2) for src in tail_src_ptrs]))
+                parts = all_gather_tails(tail)
+                if self.rank > 0:
+                    dh = h.DeviceArray.from_numpy(parts[self.rank - 1].numpy())
+                    keep.append(dh)
+                    halo_ptr = dh.ptr
+        eng.clear()
+        for j in range(B):
+            if j:
+                eng.nextFrameInBatch()
+            if halo_ptr is not None:
+                pc = self.cams[self.rank - 1]
+                take = min(self.Lmax, pc.width * pc.height)
+                eng.addHaloDepthmapDevice(halo_ptr + j * L2 + 2 * (self.Lmax - take), take,
+                                          pc.width, pc.height, *pc.intrinsics(), pc.T_world,
+                                          pc.T_crop)
+            eng.addDepthmapDevice(depth_ptrs[j], c.width, c.height, *c.intrinsics(), c.T_world,
+                                  c.T_crop)
+        eng.processFramePrepared(self.pc)
+        _, ncells = eng.grid_size()
+        words = words_for(ncells)
+        if self.dev == "cuda":
+            local = torch.empty(B * words, dtype=torch.int32, device="cuda")
+            gathered = torch.empty(self.world * B * words, dtype=torch.int32, device="cuda")
+            eng.take_marks(local.data_ptr(), B * words)
+            dist.all_gather_into_tensor(gathered, local)
+            eng.voxelOccupancyGridBatch(gathered.data_ptr(), words, self.world, B, words,
+                                        B * words, self.p.occupancy_lifetime)
+            keep.append(gathered)
+        else:
+            dl = h.DeviceArray(B * words * 4)
+            eng.take_marks(dl.ptr, B * words)
+            eng.synchronize()
+            local = torch.from_numpy(dl.to_numpy(np.int32, B * words))
+            parts = [torch.empty_like(local) for _ in range(self.world)]
+            dist.all_gather(parts, local)
+            dg = h.DeviceArray.from_numpy(torch.cat(parts).numpy())
+            eng.voxelOccupancyGridBatch(dg.ptr, words, self.world, B, words, B * words,
+                                        self.p.occupancy_lifetime)
+            eng.synchronize()
+            keep.append(dg)
+        n_total = max(B * c.width * c.height, 1)
+        if self.dev == "cuda":
+            sp = torch.empty((n_total, 4), dtype=torch.float32, device="cuda")
+            sk = torch.empty(n_total, dtype=torch.int32, device="cuda")
+            cnt = torch.empty(self.world, dtype=torch.int32, device="cuda")
+            eng.partition_points(self.world, sp.data_ptr(), sk.data_ptr(), n_total, cnt.data_ptr())
+            counts = cnt.cpu().tolist()
+            rp, rk, rc = exchange_points(sp, sk, counts)
+            eng.voxelize_points(rp.data_ptr(), rk.data_ptr(), int(sum(rc)), self.p.voxel_average)
+            keep += [rp, rk]
+        else:
+            dsp, dsk, dcnt = h.DeviceArray(n_total * 16), h.DeviceArray(n_total * 4), h.DeviceArray(64)
+            eng.partition_points(self.world, dsp.ptr, dsk.ptr, n_total, dcnt.ptr)
+            eng.synchronize()
+            counts = dcnt.to_numpy(np.uint32, self.world).tolist()
+            m = int(sum(counts))
+            sp = torch.from_numpy(dsp.to_numpy(np.float32, 4 * max(m, 1))[:4 * m].reshape(m, 4))
+            sk = torch.from_numpy(dsk.to_numpy(np.int32, max(m, 1))[:m])
+            rp, rk, rc = exchange_points(sp, sk, counts)
+            n = int(sum(rc))
+            drp = h.DeviceArray.from_numpy(rp.numpy()) if n else None
+            drk = h.DeviceArray.from_numpy(rk.numpy()) if n else None
+            eng.voxelize_points(drp.ptr if n else 0, drk.ptr if n else 0, n, self.p.voxel_average)
+            eng.synchronize()
+            keep += [drp, drk]
+        self._keep = keep
+        return counts
+
+
 def _d2h(h, ptr, dtype, count):
     out = np.empty(count, dtype)
     h.check(h.hip().hipMemcpy(out.ctypes.data, ptr, out.nbytes, h.D2H), "D2H")

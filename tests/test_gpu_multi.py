@@ -79,3 +79,54 @@ def test_two_rank_fused_cloud_hip(tmp_path, F):
         for r in range(world):
             np.testing.assert_array_equal(np.load(tmp_path / f"grid_r{r}_f{f}.npy"),
                                           orc.downloadVoxelOccupancyGrid(), f"frame {f} rank {r}")
+
+
+def _rank_batch(rank, world, port, F, out_dir):
+    import torch.distributed as dist
+    from ros_gpu_depthmap_fusion_amd import build_library, hiprt, multi
+    from ros_gpu_depthmap_fusion_amd.gdf import GPUDepthmapFusion
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    build_library()
+    p = params(F)
+    cams = [synth.make_camera(k, W, H) for k in range(world)]
+    eng = GPUDepthmapFusion(0)
+    fr = multi.FusedCloudRank(eng, cams, rank, world, p, dev="cpu")
+    n = W * H
+    ds = [hiprt.DeviceArray.from_numpy(synth.dense_frame(cams[rank], rank, f)) for f in range(FRAMES)]
+    fr.batch([d.ptr for d in ds], [d.ptr + 2 * (n - fr.Lmax) for d in ds])
+    vox = eng.downloadVoxelizedPoints()[:, :3]
+    _, vs = eng.batch_ranges()
+    for f in range(FRAMES):
+        np.save(os.path.join(out_dir, f"bvox_r{rank}_f{f}.npy"), vox[vs[f]:vs[f + 1]])
+    np.save(os.path.join(out_dir, f"bgrid_r{rank}.npy"), eng.downloadVoxelOccupancyGrid())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("F", [0, 4])
+def test_two_rank_fused_cloud_hip_batch(tmp_path, F):
+    """FusedCloudRank.batch: the three frames of each rank in one launch chain and one exchange
+    (a halo per frame, the frames' marks in one all-gather + one batched grid update, the
+    (point, frame | key) lists partitioned by key range): per frame, the ranks' voxel ranges
+    concatenated equal one oracle engine over both cameras, and the grid after the batch equals
+    the oracle's after the three frames - bit for bit."""
+    from oracle import OracleFusion
+    world = 2
+    mp.start_processes(_rank_batch, args=(world, _free_port(), F, str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    p = params(F)
+    cams = [synth.make_camera(k, W, H) for k in range(world)]
+    orc = OracleFusion(threads=4)
+    for f in range(FRAMES):
+        orc.clear()
+        for k, c in enumerate(cams):
+            orc.addDepthmap(synth.dense_frame(c, k, f), *c.intrinsics(), c.T_world, c.T_crop)
+        orc.processFrame(p)
+        want = orc.downloadVoxelizedPoints()[:, :3]
+        got = np.concatenate([np.load(tmp_path / f"bvox_r{r}_f{f}.npy") for r in range(world)])
+        assert len(got) == len(want) > 0, f"frame {f}"
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), f"frame {f}"
+    for r in range(world):
+        np.testing.assert_array_equal(np.load(tmp_path / f"bgrid_r{r}.npy"),
+                                      orc.downloadVoxelOccupancyGrid(), f"rank {r}")
