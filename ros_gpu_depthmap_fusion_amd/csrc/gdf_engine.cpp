@@ -1321,7 +1321,8 @@ void run_fused_frame(gdf_engine* e, int average, uint32_t lifetime) {
         HIPCHK(hipGraphGetNodes(G.g, nullptr, &nn));
         std::vector<hipGraphNode_t> nodes(nn);
         HIPCHK(hipGraphGetNodes(G.g, nodes.data(), &nn));
-        const void* fk[6] = {frame_kernel(0, a.rot45), frame_kernel(1, a.rot45), frame_kernel(2, a.rot45),
+        const void* fk[6] = {frame_kernel(0, a.rot45, a.do_flying ? a.F : 0u), frame_kernel(1, a.rot45),
+                             frame_kernel(2, a.rot45),
                              frame_kernel(3, a.rot45), frame_kernel(4, a.rot45),
                              frame_kernel(5, a.rot45)};  // (the count scans take no FrameArgs)
         G.frame_nodes.clear();

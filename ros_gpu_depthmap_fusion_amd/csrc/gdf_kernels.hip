@@ -473,7 +473,9 @@ __device__ __forceinline__ bool ring_pass(const P3& u, const P3& d, const P3& l,
 // Stage bits of pixel (x, y) of camera k (band row h = the pixel's row).  Rings are evaluated
 // without per-lane early exit (the reference's first-failure return only decides the same AND);
 // the wave leaves the ring loop once none of its lanes is still valid.
-template <bool ROT45, bool INTERIOR>
+// FT > 0: the ring count F as a compile-time constant (the launch default F = 4): unrolled rings,
+// no per-ring loop bookkeeping; FT = 0: a.F at run time.
+template <bool ROT45, bool INTERIOR, uint32_t FT>
 __device__ __forceinline__ uint32_t depth_bits(const FrameArgs& a, const CamDesc* cams, int k,
                                                const Band& t, const float* s_yn, uint32_t x,
                                                uint32_t y, bool in) {
@@ -489,7 +491,9 @@ __device__ __forceinline__ uint32_t depth_bits(const FrameArgs& a, const CamDesc
         const float rr = __builtin_amdgcn_rsqf(pp);
         const float nax = -(p.x * rr), nay = -(p.y * rr), naz = -(p.z * rr);
         const int64_t g = c.off + (int64_t)y * c.W + x;
-        for (uint32_t i = 1; i <= a.F; ++i) {
+        const uint32_t FF = FT ? FT : a.F;
+#pragma unroll
+        for (uint32_t i = 1; i <= FF; ++i) {
             if (!__ballot(fly)) break;  // wave-uniform exit
             fly = fly & (x + i <= c.W - 1) & (y + i <= c.H - 1);  // bounds (:60)
             const int ii = (int)i;
@@ -632,7 +636,7 @@ __device__ __forceinline__ void load_cams(const FrameArgs& a, CamDesc* s_cams) {
 // Pass 1 of the ordered compaction (apply_point_mask.glsl:42-55 made stable): one block per
 // segment, one item per thread (blockDim = a.seg_threads >= every segment's length).  The ballot
 // of wave w's valid bits is word w of the segment's 16-word bitmask.
-template <bool ROT45>
+template <bool ROT45, uint32_t FT>
 __global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
     __shared__ CamDesc s_cams[kMaxCams];
     __shared__ float s_yn[2 * kHalo + 1];
@@ -730,9 +734,9 @@ __global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
         if (64u * (uint32_t)wid < sg.len) {  // wave-uniform
             const uint32_t xw0 = sg.x0 + 64u * wid;  // x of the wave's lane 0
             if (!a.do_flying || (xw0 >= a.F && sg.y >= a.F && a.F <= (uint32_t)h))
-                bits = depth_bits<ROT45, true>(a, s_cams, sg.k, t, s_yn, sg.x0 + i, sg.y, i < sg.len);
+                bits = depth_bits<ROT45, true, FT>(a, s_cams, sg.k, t, s_yn, sg.x0 + i, sg.y, i < sg.len);
             else
-                bits = depth_bits<ROT45, false>(a, s_cams, sg.k, t, s_yn, sg.x0 + i, sg.y, i < sg.len);
+                bits = depth_bits<ROT45, false, FT>(a, s_cams, sg.k, t, s_yn, sg.x0 + i, sg.y, i < sg.len);
             if (a.dbg && i < sg.len) G(a.dbg)[sg.item0 + i] = (uint8_t)bits;
             if (a.run_mode && (bits & 4u)) {  // the voxel key k_emit will compute (same f32 ops)
                 const CamDesc& cd = s_cams[sg.k];
@@ -1277,10 +1281,15 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
         {
             HookScope hs(hook, GDF_KERNEL_MASK);
             const size_t lds = (size_t)a.band_lds;
-            if (a.rot45)
-                hipLaunchKernelGGL(k_mask<true>, dim3(a.total_segs), dim3(a.seg_threads), lds, s, a);
+            const void* km = frame_kernel(0, a.rot45, a.do_flying ? a.F : 0u);
+            if (km == reinterpret_cast<const void*>(&k_mask<true, 4>))
+                hipLaunchKernelGGL((k_mask<true, 4>), dim3(a.total_segs), dim3(a.seg_threads), lds, s, a);
+            else if (km == reinterpret_cast<const void*>(&k_mask<false, 4>))
+                hipLaunchKernelGGL((k_mask<false, 4>), dim3(a.total_segs), dim3(a.seg_threads), lds, s, a);
+            else if (a.rot45)
+                hipLaunchKernelGGL((k_mask<true, 0>), dim3(a.total_segs), dim3(a.seg_threads), lds, s, a);
             else
-                hipLaunchKernelGGL(k_mask<false>, dim3(a.total_segs), dim3(a.seg_threads), lds, s, a);
+                hipLaunchKernelGGL((k_mask<false, 0>), dim3(a.total_segs), dim3(a.seg_threads), lds, s, a);
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
         if (!a.fused_prefix) {  // (run mode: the point counts, then the run counts)
@@ -1314,13 +1323,16 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
     return hipGetLastError();
 }
 
-const void* frame_kernel(int which, int rot45) {
+const void* frame_kernel(int which, int rot45, uint32_t F) {
     if (which == 1) return reinterpret_cast<const void*>(&k_emit);
     if (which == 2) return reinterpret_cast<const void*>(&k_sel<8>);
     if (which == 4) return reinterpret_cast<const void*>(&k_sel<4>);
     if (which == 5) return reinterpret_cast<const void*>(&k_sel<16>);
-    return rot45 ? reinterpret_cast<const void*>(&k_mask<true>)
-                 : reinterpret_cast<const void*>(&k_mask<false>);
+    if (F == 4)  // the launch default: rings unrolled
+        return rot45 ? reinterpret_cast<const void*>(&k_mask<true, 4>)
+                     : reinterpret_cast<const void*>(&k_mask<false, 4>);
+    return rot45 ? reinterpret_cast<const void*>(&k_mask<true, 0>)
+                 : reinterpret_cast<const void*>(&k_mask<false, 0>);
 }
 
 // per-camera ray factors (sh/convert_depthmap_to_points.glsl:68-69), one f32 division each
