@@ -313,6 +313,7 @@ struct gdf_engine {
 
     int sort_pt = 0;  // radix keys per thread (4, 8, 16); 0: chosen by frame capacity
     uint32_t sel_segs = kSelSegs, sel_threads = kSelThreads;  // k_sel tile shape
+    bool sel_shape_set = false;     // GDF_SEL_SHAPE given (else the shape follows the window)
     uint32_t seg_items = 0;  // max pixels per depth compaction segment (64..1024); 0: by frame size
     bool use_graphs = !getenv("GDF_NO_GRAPHS");  // gdf_set_graphs
     bool use_runs = !getenv("GDF_NO_RUNS");      // voxelize runs of equal keys (depth frames)
@@ -985,8 +986,12 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel) {
     // one item per thread: blocks as wide as the widest segment
     a.seg_threads = e->max_segw ? std::max<uint32_t>(64, e->max_segw) : kSegItems;
     a.total_segs = a.depth_segs;
-    a.sel_segs = e->sel_segs;
-    a.sel_tile = e->sel_segs * e->sel_threads;
+    // k_sel tiles: 4 K points; 16 K for windows over 16 Mi points, whose ~10^4..10^5 tiles would
+    // otherwise queue on the one ticket counter (measured on MI355X, C3's 236 M-point window:
+    // 57.6 K tiles 2.92 ms, 14.4 K tiles 2.11 ms per frame)
+    const bool big_window = !e->sel_shape_set && sel > (1u << 24);
+    a.sel_segs = big_window ? 16u : e->sel_segs;
+    a.sel_tile = big_window ? 16u * 1024u : e->sel_segs * e->sel_threads;
     a.sel_tiles = (uint32_t)(((uint64_t)sel + a.sel_tile - 1) / a.sel_tile);
     if (a.sel_tiles) {  // rollbuffer compaction (k_sel) + placement behind the depth points
         Slot& q = e->sl();
@@ -1447,6 +1452,7 @@ int gdf_create(int device, gdf_engine** out) {
                 th >= 128 && th <= 1024 && th % 64 == 0 && sg * (th / 64) <= 256) {
                 e->sel_segs = sg;
                 e->sel_threads = th;
+                e->sel_shape_set = true;
             }
         }
         ensure_misc(e);
