@@ -2287,7 +2287,8 @@ __global__ __launch_bounds__(256) void k_group_big(const uint32_t* __restrict__ 
 uint32_t g_run_stage = 2048;
 uint32_t g_run_inblock = 256;
 uint32_t g_run_big_blocks = 1024;  // k_group_runs_big grid (tuning knob GDF_RUN_BIG_BLOCKS)
-constexpr int kRunQ = 4;        // a streamed chunk: 64 x kRunQ points per wave step
+uint32_t g_run_q16 = 0;  // 1 K-point chunks in k_group_runs_big (tuning knob GDF_RUN_Q16)
+// a streamed chunk: 64 x Q points per wave step (Q = 4, 4 waves per block; Q = 16, one wave)
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -2323,7 +2324,7 @@ struct RunRec {
 
 // One wave sums the points of sorted runs [rs, re) in order: batches of 64 runs (one per lane;
 // the records rps / rlen - first point, length - are indexed by sorted run, contiguous, and read
-// two batches ahead), their points streamed in chunks of 64 x kRunQ positions - position -> run by
+// two batches ahead), their points streamed in chunks of 64 x Q positions - position -> run by
 // a max-scan of the runs' first positions - loaded coalesced one chunk ahead (across batch
 // boundaries too), transposed into LDS per component, and added by lanes 0..3, one component chain
 // each (the reference's sequential f32 sum).  Returns lane c's component sum; npts = the group's
@@ -2344,15 +2345,16 @@ __device__ __forceinline__ RunRec run_rec(const uint32_t* __restrict__ rps,
     return ok ? RunRec{rps[r], rlen[r]} : RunRec{0u, 0u};
 }
 
-// The points at batch positions c + 64 q + lane (q < kRunQ), in two steps: run_marks writes the
+// The points at batch positions c + 64 q + lane (q < Q), in two steps: run_marks writes the
 // first position of every run inside the chunk, run_row(q) max-scans row q of the marks (the row
 // carries chain through cy) and loads its points - branch-free (positions past the batch load
 // point 0 and read as zero), so the rows interleave with the chain additions.
+template <int Q>
 __device__ __forceinline__ void run_marks(const RunBatch& bt, uint32_t c, int* s_mark) {
-    constexpr uint32_t CH = 64u * kRunQ;
+    constexpr uint32_t CH = 64u * Q;
     const int lane = threadIdx.x & 63;
 #pragma unroll
-    for (int q = 0; q < kRunQ; ++q) s_mark[64 * q + lane] = -1;
+    for (int q = 0; q < Q; ++q) s_mark[64 * q + lane] = -1;
     wave_sync();
     if (bt.len && bt.off >= c && bt.off < c + CH) s_mark[bt.off - c] = lane;
     wave_sync();
@@ -2372,23 +2374,24 @@ __device__ __forceinline__ float4 run_row(const RunBatch& bt, uint32_t c, int q,
     return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
+template <int Q>
 __device__ __forceinline__ void run_fetch(RunBatch& bt, uint32_t c, const float4* __restrict__ pts,
-                                          int* s_mark, float4 (&p)[kRunQ]) {
-    run_marks(bt, c, s_mark);
+                                          int* s_mark, float4 (&p)[Q]) {
+    run_marks<Q>(bt, c, s_mark);
     int cy = bt.carry;
 #pragma unroll
-    for (int q = 0; q < kRunQ; ++q) p[q] = run_row(bt, c, q, s_mark, cy, pts);
+    for (int q = 0; q < Q; ++q) p[q] = run_row(bt, c, q, s_mark, cy, pts);
     bt.carry = cy;
 }
 
 
 
+template <int Q>
 __device__ __forceinline__ float wave_stream_sum(const uint32_t* __restrict__ rps,
                                                  const uint32_t* __restrict__ rlen, uint32_t rs,
                                                  uint32_t re, const float4* __restrict__ pts,
                                                  float* s_soa, int* s_mark, uint32_t& npts) {
-    constexpr uint32_t CH = 64u * kRunQ, CHP = CH + kChainPad;  // (component rows, padded)
-    static_assert(CH == 256, "the interleaved chain below covers 4 rows of 64");
+    constexpr uint32_t CH = 64u * Q, CHP = CH + kChainPad;  // (component rows, padded)
     const int lane = threadIdx.x & 63;
     float acc = 0.0f;
     npts = 0;
@@ -2396,15 +2399,15 @@ __device__ __forceinline__ float wave_stream_sum(const uint32_t* __restrict__ rp
     RunBatch cur = run_batch(run_rec(rps, rlen, r0, r0 < re));
     RunRec rec1 = run_rec(rps, rlen, r0 + 64u, r0 + 64u < re);    // batch 1
     RunRec rec2 = run_rec(rps, rlen, r0 + 128u, r0 + 128u < re);  // batch 2
-    float4 p[kRunQ];
-    run_fetch(cur, 0, pts, s_mark, p);  // (every run holds >= 1 point)
+    float4 p[Q];
+    run_fetch<Q>(cur, 0, pts, s_mark, p);  // (every run holds >= 1 point)
     // every lane runs the chain of component lane & 3 (lanes 0..3 hold the result): no exec mask
     // splits the chain from the next chunk's fetch, which is interleaved with it row by row
     const float* comp = s_soa + (uint32_t)(lane & 3) * CHP;
     uint32_t rb = rs, c = 0;
     while (true) {  // wave-uniform: one chunk per iteration
 #pragma unroll
-        for (int q = 0; q < kRunQ; ++q) {
+        for (int q = 0; q < Q; ++q) {
             s_soa[0 * CHP + 64 * q + lane] = p[q].x;
             s_soa[1 * CHP + 64 * q + lane] = p[q].y;
             s_soa[2 * CHP + 64 * q + lane] = p[q].z;
@@ -2427,13 +2430,13 @@ __device__ __forceinline__ float wave_stream_sum(const uint32_t* __restrict__ rp
         } else if (!more) {
             fb.T = 0;
         }
-        run_marks(fb, cn, s_mark);
+        run_marks<Q>(fb, cn, s_mark);
         int cy = fb.carry;
-        if (n == CH) {  // a full chunk: 4 x (64 additions, then one row of the next chunk's loads)
+        if (n == CH) {  // a full chunk: Q x (64 additions, then one row of the next chunk's loads)
             float ta[16], tb[16];
             lds_block<1, 16>(comp, 0, ta);
 #pragma unroll
-            for (int q = 0; q < kRunQ; ++q) {
+            for (int q = 0; q < Q; ++q) {
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     const uint32_t k = 64u * q + 32u * h;
@@ -2450,7 +2453,7 @@ __device__ __forceinline__ float wave_stream_sum(const uint32_t* __restrict__ rp
             }
         } else {
 #pragma unroll
-            for (int q = 0; q < kRunQ; ++q) p[q] = run_row(fb, cn, q, s_mark, cy, pts);
+            for (int q = 0; q < Q; ++q) p[q] = run_row(fb, cn, q, s_mark, cy, pts);
             acc = lds_chain<1>(comp, n, acc);
         }
         fb.carry = cy;
@@ -2672,23 +2675,28 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
 // runs of each (records rps / rlen by sorted run, written by k_group_runs) from global memory
 // (wave_stream_sum).  The queue was complete when this launch began; the first sort pass of the
 // next voxelize zeroes the counters.
-__global__ __launch_bounds__(256) void k_group_runs_big(const uint32_t* __restrict__ rps,
+template <int Q, int WPB>
+__global__ __launch_bounds__(64 * WPB) void k_group_runs_big(const uint32_t* __restrict__ rps,
                                                         const uint32_t* __restrict__ rlen,
                                                         const float4* __restrict__ pts,
                                                         float* __restrict__ out,
                                                         const uint4* __restrict__ bigq,
                                                         uint32_t bigq_cap, uint32_t* qctr) {
-    constexpr uint32_t CH = 64u * kRunQ;
-    __shared__ __attribute__((aligned(16))) float s_soa[4][4 * (CH + kChainPad)];
-    __shared__ int s_mk[4][CH];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    constexpr uint32_t CH = 64u * Q;
+    // WPB waves per block (Q = 16: one - a long chunk's 20 KB of LDS allocated per wave)
+    __shared__ __attribute__((aligned(16))) float s_soa[WPB][4 * (CH + kChainPad)];
+    __shared__ int s_mk[WPB][CH];
+    const int lane = threadIdx.x & 63, wid = WPB == 1 ? 0 : (int)(threadIdx.x >> 6);
     const uint32_t nq = min(__hip_atomic_load(qctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), bigq_cap);
     const uint32_t waves = gridDim.x * (blockDim.x >> 6);
     uint32_t t = blockIdx.x * (blockDim.x >> 6) + wid;
+    // one queue slot per draw: queued groups range over 10^3x in length (C3: up to 139 K points),
+    // and draws of 8 consecutive slots (neighbouring keys, similar lengths) measured 1.7 -> 2.8 ms
+    // of tail imbalance on the C3 window
     while (t < nq) {  // wave-uniform
         const uint4 q = bigq[t];
         uint32_t np = 0;
-        const float acc = wave_stream_sum(rps, rlen, q.y, q.z, pts, s_soa[wid], s_mk[wid], np);
+        const float acc = wave_stream_sum<Q>(rps, rlen, q.y, q.z, pts, s_soa[wid], s_mk[wid], np);
         if (lane < 4) out[4 * (size_t)q.x + lane] = lane < 3 ? acc / (float)np : acc;
         if (nq <= waves) break;
         uint32_t d = 0;
@@ -2799,7 +2807,12 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
                            kbuf[npasses & 1], vbuf[npasses & 1]);  // (free after the sort)
         if (a.average) {
             if ((e = hipGetLastError()) != hipSuccess) return e;
-            hipLaunchKernelGGL(k_group_runs_big, dim3(g_run_big_blocks), dim3(256), 0, s, kbuf[npasses & 1],
+            if (g_run_q16)
+                hipLaunchKernelGGL((k_group_runs_big<16, 1>), dim3(4 * g_run_big_blocks), dim3(64), 0,
+                                   s, kbuf[npasses & 1], vbuf[npasses & 1], a.pts,
+                                   reinterpret_cast<float*>(a.out), a.bigq, a.bigq_cap, qctr);
+            else
+                hipLaunchKernelGGL((k_group_runs_big<4, 4>), dim3(g_run_big_blocks), dim3(256), 0, s, kbuf[npasses & 1],
                                vbuf[npasses & 1], a.pts, reinterpret_cast<float*>(a.out), a.bigq,
                                a.bigq_cap, qctr);
         }
