@@ -120,6 +120,8 @@ int gdf_version(int* major, int* minor);
  * the engine's own stream. */
 int gdf_set_stream(gdf_engine* engine, void* hip_stream);
 int gdf_synchronize(gdf_engine* engine);
+/* The stream the engine's current frame is enqueued on (for consumers ordered after it). */
+int gdf_get_stream(gdf_engine* engine, void** out_stream);
 /* Frame pipelining (1..4, default 1): gdf_clear starts a frame on the next of `depth` slots,
  * each with its own stream and per-frame buffers, so a frame's compaction overlaps the previous
  * frame's sort / grouping.  Shared state stays ordered: grid updates run in frame order, frames

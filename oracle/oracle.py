@@ -90,6 +90,8 @@ def load():
         "orc_stable_sort_keys": (None, [vp, u32, vp, vp]),
         "orc_mask_dilate": (None, [vp, vp, u32, u32, u32, i32]),
         "orc_transform_points": (None, [vp, vp, vp, u32, vp]),
+        "orc_seg_run": (vp, [vp, u32, u32, u32]), "orc_seg_counts": (None, [vp, vp]),
+        "orc_seg_get": (None, [vp] + [vp] * 11), "orc_seg_free": (None, [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -381,3 +383,30 @@ class RefRadix:
                                   C.byref(ng))
         g = ng.value
         return si[:n], sk[:n], gs[:g], gz[:g], gv[:g]
+
+
+def object_segmentation_front(grid: np.ndarray) -> dict:
+    """labelVoxels + layers connections + mergeLabelsAcrossLayers (oracle/seg_oracle.c) on a u8
+    grid [layers, height, width]; flat arrays with the keys of gdf.Segmenter.results()."""
+    lib = load()
+    g = np.ascontiguousarray(grid, np.uint8)
+    L, H, W = g.shape
+    h = lib.orc_seg_run(_p(g), W, H, L)
+    try:
+        c = np.zeros(5, np.uint64)
+        lib.orc_seg_counts(h, _p(c))
+        T, NC, NP, CB, nobj = (int(v) for v in c)
+        r = dict(labels=np.zeros((L, H, W), np.uint16), num_labels=np.zeros(L, np.uint32),
+                 stats=np.zeros((T, 5), np.int32), centroids=np.zeros((T, 2), np.float64),
+                 labels_to_contours=np.zeros(T, np.int32),
+                 contours_per_layer=np.zeros(L, np.uint32), contour_sizes=np.zeros(NC, np.uint32),
+                 contour_points=np.zeros((NP, 2), np.int32), connections=np.zeros(CB, np.uint8),
+                 connection_starts=np.zeros(max(L - 1, 0), np.uint64),
+                 merged=np.zeros(T, np.uint32), num_objects=nobj)
+        lib.orc_seg_get(h, *[_p(r[k]) for k in (
+            "labels", "num_labels", "stats", "centroids", "labels_to_contours",
+            "contours_per_layer", "contour_sizes", "contour_points", "connections",
+            "connection_starts", "merged")])
+        return r
+    finally:
+        lib.orc_seg_free(h)

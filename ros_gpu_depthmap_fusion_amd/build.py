@@ -8,7 +8,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB_PATH = os.path.join(PKG, "lib", "libgdf.so")
-SOURCES = ["gdf_kernels.hip", "gdf_engine.cpp", "gdf_driver.cpp"]
+SOURCES = ["gdf_kernels.hip", "gdf_segment.hip", "gdf_engine.cpp", "gdf_driver.cpp"]
 HEADERS = ["gdf_device.hpp", "gdf_kernels.hpp"]
 
 # Float contract of SURVEY.md Appendix A: no FMA contraction, correctly rounded / and sqrt.
@@ -26,7 +26,7 @@ def _stale(out: str, deps) -> bool:
 
 def build_library(force: bool = False, verbose: bool = False) -> str:
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
-    deps += [os.path.join(ROOT, "include", h) for h in ("gdf.h", "gdf_driver.h")]
+    deps += [os.path.join(ROOT, "include", h) for h in ("gdf.h", "gdf_driver.h", "gdf_segment.h")]
     if not force and not _stale(LIB_PATH, deps):
         return LIB_PATH
     os.makedirs(os.path.dirname(LIB_PATH), exist_ok=True)

@@ -28,8 +28,14 @@
 using namespace gdf;
 
 namespace {
-
 thread_local std::string g_last_error;
+}  // namespace
+
+namespace gdf {
+void set_last_error(const std::string& msg) { g_last_error = msg; }
+}  // namespace gdf
+
+namespace {
 
 struct GdfError {
     int code;
@@ -1415,6 +1421,13 @@ int guarded(gdf_engine* e, F&& f) {
 extern "C" {
 
 const char* gdf_last_error(void) { return g_last_error.c_str(); }
+
+int gdf_get_stream(gdf_engine* e, void** out) {
+    ENGINE_OR_FAIL(e);
+    if (!out) return GDF_ERR_ARG;
+    *out = static_cast<void*>(e->s());
+    return GDF_OK;
+}
 
 int gdf_version(int* major, int* minor) {
     if (major) *major = GDF_VERSION_MAJOR;

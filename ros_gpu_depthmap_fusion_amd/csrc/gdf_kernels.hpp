@@ -4,7 +4,12 @@
 #include "gdf.h"
 #include "gdf_device.hpp"
 
+#include <string>
+
 namespace gdf {
+
+// the calling thread's gdf_last_error() message (gdf_engine.cpp), for the other C-ABI sources
+void set_last_error(const std::string& msg);
 
 // Optional per-launch callbacks (the engine records HIP event pairs when profiling).
 struct LaunchHook {

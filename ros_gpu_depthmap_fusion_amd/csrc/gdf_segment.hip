@@ -1,0 +1,1028 @@
+// gdf_segment.hip — GPU object-segmentation front end for gfx950.
+//
+// The reference runs this step on the CPU with OpenCV after downloading the u8 occupancy grid
+// (GPUDepthmapFusion::labelVoxels, src/gpu_depthmap_fusion.cpp:1872-2011: per z-layer
+// connectedComponentsWithStats(8, CV_16U) + findContours(RETR_EXTERNAL, CHAIN_APPROX_NONE)),
+// then uploads the labels again for the layer-connection shader (:2013-2241,
+// shader/layers_connections.glsl:96-122).  Here the grid never leaves the device:
+//
+//   k_cc_local    one workgroup per 16x16 tile of 2x2 pixel blocks: block foreground bits and
+//                 a union-find over the tile in LDS (8-adjacency between blocks, roots = the
+//                 smallest block index, i.e. the first block in block-raster order);
+//   k_cc_merge    unions across tile borders with global atomicMin (lock-free union-find);
+//   k_cc_flatten  every block points at its root;
+//   k_cc_rank     one workgroup per layer: roots ranked in block order -> label = rank + 1
+//                 (OpenCV's BBDT order: components by their first 2x2 block);
+//   k_cc_pixels   one wave per 64 columns x 8 rows: u16 labels, per-label stats accumulated per
+//                 run of equal labels in a row (ballot masks: min/max/area/sum of x from the mask
+//                 bits, no per-pixel atomics; background and the last foreground label cached
+//                 across rows), the layer connection bytes (one store per distinct pair);
+//   k_cc_finish   stats rows {LEFT, TOP, WIDTH, HEIGHT, AREA} and double centroids;
+//   k_cc_contours one wave per layer: the layer (1-pixel zero border) staged in LDS as int8, the
+//                 raster scan of cvFindNextContour in 64-pixel ballot steps, Suzuki-Abe border
+//                 following of each external start (marks 2 / -126, 8-neighbour masks), chain
+//                 codes out (expanded into points on download);
+//   k_cc_l2c      labelsToContours (fusion.cpp:1941-1952), findContours order = reverse discovery.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "gdf.h"
+#include "gdf_segment.h"
+#include "gdf_kernels.hpp"
+
+namespace {
+
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr uint32_t kTile = 16;       // blocks per tile side (k_cc_local / k_cc_merge)
+constexpr uint32_t kRowsPerWave = 8;  // k_cc_pixels
+constexpr uint32_t kStatWords = 6;    // minx, miny, maxx, maxy, area, first (raster index)
+constexpr size_t kLdsMax = 160 * 1024;
+
+// ---- block connectivity -------------------------------------------------------------------------
+// bits of a 2x2 block: 1 = (2bx, 2by), 2 = (2bx+1, 2by), 4 = (2bx, 2by+1), 8 = (2bx+1, 2by+1)
+__device__ __forceinline__ uint32_t block_bits(const uint8_t* __restrict__ lay, uint32_t W,
+                                               uint32_t H, uint32_t bx, uint32_t by) {
+    const uint32_t x = 2 * bx, y = 2 * by;
+    const uint8_t* r0 = lay + (size_t)y * W;
+    uint32_t b = r0[x] ? 1u : 0u;
+    if (x + 1 < W && r0[x + 1]) b |= 2u;
+    if (y + 1 < H) {
+        const uint8_t* r1 = r0 + W;
+        if (r1[x]) b |= 4u;
+        if (x + 1 < W && r1[x + 1]) b |= 8u;
+    }
+    return b;
+}
+// 8-adjacent foreground pixels between block b and its neighbour n: 0 left, 1 up, 2 up-left,
+// 3 up-right
+__device__ __forceinline__ bool linked(uint32_t b, uint32_t n, int dir) {
+    switch (dir) {
+        case 0: return (b & 5u) && (n & 10u);
+        case 1: return (b & 3u) && (n & 12u);
+        case 2: return (b & 1u) && (n & 8u);
+        default: return (b & 2u) && (n & 4u);
+    }
+}
+
+// lock-free union-find (roots = minimum index; a parent is always smaller than its child)
+template <int kScope>
+__device__ __forceinline__ uint32_t uf_find(uint32_t* par, uint32_t x) {
+    uint32_t p = __hip_atomic_load(par + x, __ATOMIC_RELAXED, kScope);
+    while (p != x) {
+        x = p;
+        p = __hip_atomic_load(par + x, __ATOMIC_RELAXED, kScope);
+    }
+    return x;
+}
+template <int kScope>
+__device__ __forceinline__ void uf_unite(uint32_t* par, uint32_t a, uint32_t b) {
+    while (true) {
+        a = uf_find<kScope>(par, a);
+        b = uf_find<kScope>(par, b);
+        if (a == b) return;
+        if (a < b) {
+            const uint32_t old = __hip_atomic_fetch_min(par + b, a, __ATOMIC_RELAXED, kScope);
+            if (old == b) return;
+            b = old;
+        } else {
+            const uint32_t old = __hip_atomic_fetch_min(par + a, b, __ATOMIC_RELAXED, kScope);
+            if (old == a) return;
+            a = old;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_cc_local(const uint8_t* __restrict__ grid, uint32_t W,
+                                                  uint32_t H, uint32_t BW, uint32_t BH,
+                                                  uint32_t* __restrict__ par,
+                                                  uint8_t* __restrict__ bits) {
+    __shared__ uint32_t s_par[kTile * kTile];
+    __shared__ uint8_t s_bits[kTile * kTile];
+    const uint32_t l = threadIdx.x, lx = l % kTile, ly = l / kTile;
+    const uint32_t bx = blockIdx.x * kTile + lx, by = blockIdx.y * kTile + ly, z = blockIdx.z;
+    const bool in = bx < BW && by < BH;
+    const uint32_t b = in ? block_bits(grid + (size_t)z * W * H, W, H, bx, by) : 0u;
+    s_bits[l] = (uint8_t)b;
+    s_par[l] = b ? l : kNone;
+    __syncthreads();
+    if (b) {
+        if (lx > 0 && linked(b, s_bits[l - 1], 0)) uf_unite<__HIP_MEMORY_SCOPE_WORKGROUP>(s_par, l, l - 1);
+        if (ly > 0) {
+            if (linked(b, s_bits[l - kTile], 1)) uf_unite<__HIP_MEMORY_SCOPE_WORKGROUP>(s_par, l, l - kTile);
+            if (lx > 0 && linked(b, s_bits[l - kTile - 1], 2))
+                uf_unite<__HIP_MEMORY_SCOPE_WORKGROUP>(s_par, l, l - kTile - 1);
+            if (lx + 1 < kTile && linked(b, s_bits[l - kTile + 1], 3))
+                uf_unite<__HIP_MEMORY_SCOPE_WORKGROUP>(s_par, l, l - kTile + 1);
+        }
+    }
+    __syncthreads();
+    if (!in) return;
+    const size_t nbl = (size_t)BW * BH;
+    const size_t g = (size_t)z * nbl + (size_t)by * BW + bx;
+    uint32_t out = kNone;
+    if (b) {  // the tile root (smallest local index = smallest global index of the tile part)
+        const uint32_t r = uf_find<__HIP_MEMORY_SCOPE_WORKGROUP>(s_par, l);
+        out = (uint32_t)(z * nbl + (size_t)(blockIdx.y * kTile + r / kTile) * BW +
+                         blockIdx.x * kTile + r % kTile);
+    }
+    par[g] = out;
+    bits[g] = (uint8_t)b;
+}
+
+__global__ __launch_bounds__(256) void k_cc_merge(const uint8_t* __restrict__ bits, uint32_t BW,
+                                                  uint32_t BH, uint32_t* par) {
+    const uint32_t l = threadIdx.x, lx = l % kTile, ly = l / kTile;
+    const uint32_t bx = blockIdx.x * kTile + lx, by = blockIdx.y * kTile + ly, z = blockIdx.z;
+    if (bx >= BW || by >= BH) return;
+    const uint32_t g = (uint32_t)(z * (size_t)BW * BH + (size_t)by * BW + bx);
+    const uint32_t b = bits[g];
+    if (!b) return;
+    // neighbours (left, up, up-left, up-right) that lie in another tile
+    if (lx == 0 && bx > 0 && linked(b, bits[g - 1], 0)) uf_unite<__HIP_MEMORY_SCOPE_AGENT>(par, g, g - 1);
+    if (by == 0) return;
+    if (ly == 0 && linked(b, bits[g - BW], 1)) uf_unite<__HIP_MEMORY_SCOPE_AGENT>(par, g, g - BW);
+    if (bx > 0 && (lx == 0 || ly == 0) && linked(b, bits[g - BW - 1], 2))
+        uf_unite<__HIP_MEMORY_SCOPE_AGENT>(par, g, g - BW - 1);
+    if (bx + 1 < BW && (lx + 1 == kTile || ly == 0) && linked(b, bits[g - BW + 1], 3))
+        uf_unite<__HIP_MEMORY_SCOPE_AGENT>(par, g, g - BW + 1);
+}
+
+__global__ __launch_bounds__(256) void k_cc_flatten(uint32_t* par, uint32_t nb) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= nb) return;
+    if (par[i] == kNone) return;
+    par[i] = uf_find<__HIP_MEMORY_SCOPE_AGENT>(par, i);
+}
+
+// one workgroup per layer: roots ranked in block order
+__global__ __launch_bounds__(1024) void k_cc_rank(const uint32_t* __restrict__ par, uint32_t nbl,
+                                                  uint32_t* __restrict__ blabel,
+                                                  uint32_t* __restrict__ nlabels) {
+    __shared__ uint32_t s_w[16];
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6, z = blockIdx.x;
+    const uint32_t base = z * nbl, per = (nbl + 1023) / 1024;
+    const uint32_t b0 = min(t * per, nbl), b1 = min(b0 + per, nbl);
+    uint32_t cnt = 0;
+    for (uint32_t i = b0; i < b1; ++i) cnt += par[base + i] == base + i;
+    // block exclusive scan: waves by DPP-free shuffles, then the 16 wave totals
+    uint32_t v = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(v, d, 64);
+        if ((int)lane >= d) v += o;
+    }
+    if (lane == 63) s_w[w] = v;
+    __syncthreads();
+    uint32_t woff = 0, tot = 0;
+    for (uint32_t k = 0; k < 16; ++k) {
+        const uint32_t x = s_w[k];
+        woff += k < w ? x : 0u;
+        tot += x;
+    }
+    uint32_t r = woff + v - cnt;
+    for (uint32_t i = b0; i < b1; ++i)
+        if (par[base + i] == base + i) blabel[base + i] = 1 + r++;
+    if (t == 0) nlabels[z] = 1 + tot;
+}
+
+struct SegArgs {
+    const uint8_t* grid;
+    uint32_t W, H, L, BW, nbl;
+    const uint32_t* par;
+    const uint32_t* blabel;
+    const uint32_t* lstart;
+    const uint32_t* nlab;
+    const uint64_t* cstart;
+    uint16_t* labels;
+    int32_t* st;      // [T][kStatWords]
+    unsigned long long* sums;  // [T][2]
+    uint8_t* conn;
+    int do_conn;
+};
+
+__device__ __forceinline__ uint32_t pixel_label(const SegArgs& a, uint32_t z, uint32_t x,
+                                                uint32_t y) {
+    return a.blabel[a.par[(size_t)z * a.nbl + (size_t)(y >> 1) * a.BW + (x >> 1)]];
+}
+
+// sum of the positions of the set bits of a 64-bit lane mask
+__device__ __forceinline__ uint32_t bit_pos_sum(uint64_t m) {
+    return (uint32_t)__popcll(m & 0xAAAAAAAAAAAAAAAAull) +
+           2u * (uint32_t)__popcll(m & 0xCCCCCCCCCCCCCCCCull) +
+           4u * (uint32_t)__popcll(m & 0xF0F0F0F0F0F0F0F0ull) +
+           8u * (uint32_t)__popcll(m & 0xFF00FF00FF00FF00ull) +
+           16u * (uint32_t)__popcll(m & 0xFFFF0000FFFF0000ull) +
+           32u * (uint32_t)__popcll(m & 0xFFFFFFFF00000000ull);
+}
+
+struct StatAcc {  // wave-uniform partial stats of one label
+    uint32_t label;
+    int32_t minx, miny, maxx, maxy;
+    uint32_t area, first;
+    unsigned long long sx, sy;
+};
+
+__device__ __forceinline__ void acc_reset(StatAcc& s, uint32_t label) {
+    s.label = label;
+    s.minx = INT_MAX; s.miny = INT_MAX; s.maxx = INT_MIN; s.maxy = INT_MIN;
+    s.area = 0; s.first = kNone; s.sx = 0; s.sy = 0;
+}
+__device__ __forceinline__ void acc_add(StatAcc& s, int32_t mnx, int32_t mxx, int32_t y,
+                                        uint32_t cnt, uint32_t first, unsigned long long sx) {
+    s.minx = min(s.minx, mnx);
+    s.maxx = max(s.maxx, mxx);
+    s.miny = min(s.miny, y);
+    s.maxy = max(s.maxy, y);
+    s.area += cnt;
+    s.first = min(s.first, first);
+    s.sx += sx;
+    s.sy += (unsigned long long)cnt * (uint32_t)y;
+}
+__device__ __forceinline__ void acc_flush(const StatAcc& s, const SegArgs& a, uint32_t ls) {
+    if (s.label == kNone || s.area == 0) return;
+    if ((threadIdx.x & 63) != 0) return;
+    int32_t* st = a.st + (size_t)(ls + s.label) * kStatWords;
+    atomicMin(st + 0, s.minx);
+    atomicMin(st + 1, s.miny);
+    atomicMax(st + 2, s.maxx);
+    atomicMax(st + 3, s.maxy);
+    atomicAdd(reinterpret_cast<uint32_t*>(st + 4), s.area);
+    atomicMin(reinterpret_cast<uint32_t*>(st + 5), s.first);
+    atomicAdd(a.sums + 2 * (size_t)(ls + s.label), s.sx);
+    atomicAdd(a.sums + 2 * (size_t)(ls + s.label) + 1, s.sy);
+}
+
+__global__ __launch_bounds__(64) void k_cc_pixels(SegArgs a) {
+    const uint32_t lane = threadIdx.x, x0 = blockIdx.x * 64, x = x0 + lane;
+    const uint32_t y0 = blockIdx.y * kRowsPerWave, z = blockIdx.z;
+    const bool inx = x < a.W;
+    const size_t LS = (size_t)a.W * a.H;
+    const uint8_t* lay = a.grid + z * LS;
+    const uint32_t ls = a.lstart[z];
+    const bool conn = a.do_conn && z + 1 < a.L;
+    const uint32_t nb = conn ? a.nlab[z + 1] : 0u;
+    uint8_t* cm = conn ? a.conn + a.cstart[z] : nullptr;
+    StatAcc bg, fg;
+    acc_reset(bg, 0);
+    acc_reset(fg, kNone);
+    uint32_t lastA = kNone, lastB = kNone;
+    for (uint32_t r = 0; r < kRowsPerWave; ++r) {
+        const uint32_t y = y0 + r;
+        if (y >= a.H) break;
+        const size_t p = (size_t)y * a.W + x;
+        uint32_t lab = 0;
+        if (inx && lay[p]) lab = pixel_label(a, z, x, y);
+        if (inx) a.labels[z * LS + p] = (uint16_t)lab;
+        uint64_t act = __ballot(inx);
+        while (act) {  // runs of equal labels in this row segment (wave-uniform)
+            const uint32_t L0 = __shfl(lab, __ffsll((long long)act) - 1, 64);
+            const uint64_t m = __ballot(inx && lab == L0);
+            act &= ~m;
+            const uint32_t cnt = (uint32_t)__popcll(m);
+            const int32_t mnx = (int32_t)(x0 + __ffsll((long long)m) - 1);
+            const int32_t mxx = (int32_t)(x0 + 63 - __clzll((long long)m));
+            const unsigned long long sx = (unsigned long long)cnt * x0 + bit_pos_sum(m);
+            const uint32_t first = y * a.W + (uint32_t)mnx;
+            if (L0 == 0) {
+                acc_add(bg, mnx, mxx, (int32_t)y, cnt, first, sx);
+            } else {
+                if (fg.label != L0) {
+                    acc_flush(fg, a, ls);
+                    acc_reset(fg, L0);
+                }
+                acc_add(fg, mnx, mxx, (int32_t)y, cnt, first, sx);
+            }
+        }
+        if (conn) {  // layers_connections.glsl:96-122 (neighbors_size 0)
+            uint32_t lb = 0;
+            if (inx && lay[LS + p]) lb = pixel_label(a, z + 1, x, y);
+            uint64_t act2 = __ballot(inx);
+            while (act2) {
+                const int ld = __ffsll((long long)act2) - 1;
+                const uint32_t A = __shfl(lab, ld, 64), B = __shfl(lb, ld, 64);
+                act2 &= ~__ballot(inx && lab == A && lb == B);
+                if (A != lastA || B != lastB) {
+                    if (lane == 0) cm[(size_t)A * nb + B] = 1;
+                    lastA = A;
+                    lastB = B;
+                }
+            }
+        }
+    }
+    acc_flush(bg, a, ls);
+    acc_flush(fg, a, ls);
+}
+
+__global__ __launch_bounds__(256) void k_cc_init_stats(int32_t* st, unsigned long long* sums,
+                                                       uint32_t T) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= T) return;
+    int32_t* s = st + (size_t)i * kStatWords;
+    s[0] = INT_MAX; s[1] = INT_MAX; s[2] = INT_MIN; s[3] = INT_MIN; s[4] = 0; s[5] = -1;
+    sums[2 * (size_t)i] = 0;
+    sums[2 * (size_t)i + 1] = 0;
+}
+
+// CCStatsOp::finish: WIDTH = right - left + 1 (int wrap for an empty label), centroid = sum / area
+__global__ __launch_bounds__(256) void k_cc_finish(const int32_t* __restrict__ st,
+                                                   const unsigned long long* __restrict__ sums,
+                                                   uint32_t T, int32_t* __restrict__ stats5,
+                                                   double* __restrict__ cent,
+                                                   int32_t* __restrict__ l2c) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= T) return;
+    const int32_t* s = st + (size_t)i * kStatWords;
+    int32_t* o = stats5 + 5 * (size_t)i;
+    o[0] = s[0];
+    o[1] = s[1];
+    o[2] = (int32_t)((uint32_t)s[2] - (uint32_t)s[0] + 1u);
+    o[3] = (int32_t)((uint32_t)s[3] - (uint32_t)s[1] + 1u);
+    o[4] = s[4];
+    const double area = (double)(uint32_t)s[4];
+    cent[2 * (size_t)i] = (double)sums[2 * (size_t)i] / area;
+    cent[2 * (size_t)i + 1] = (double)sums[2 * (size_t)i + 1] / area;
+    l2c[i] = -1;
+}
+
+// ---- findContours(RETR_EXTERNAL, CHAIN_APPROX_NONE) per layer -------------------------------------
+// chain code s: 0 (+1, 0), 1 (+1, -1), 2 (0, -1), 3 (-1, -1), 4 (-1, 0), 5 (-1, +1), 6 (0, +1),
+// 7 (+1, +1) - icvCodeDeltas; dx + 1 / dy + 1 packed 2 bits per code
+__device__ __forceinline__ int code_dx(int s) { return (int)((0x901Au >> (2 * s)) & 3u) - 1; }
+__device__ __forceinline__ int code_dy(int s) { return (int)((0xA901u >> (2 * s)) & 3u) - 1; }
+
+template <bool kLds>
+struct Img {
+    int8_t* p;
+    __device__ __forceinline__ int get(int i) const {
+        if (kLds) return p[i];
+        return __hip_atomic_load(p + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __device__ __forceinline__ void set(int i, int8_t v) const {
+        if (kLds) p[i] = v;
+        else __hip_atomic_store(p + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+};
+
+// non-zero 8-neighbours of pixel i, bit s for code s (zero-ness never changes while marking)
+template <bool kLds>
+__device__ __forceinline__ uint32_t nb_mask(const Img<kLds>& im, int i, int Wp) {
+    uint32_t m = 0;
+    m |= (im.get(i + 1) != 0) ? 1u : 0u;
+    m |= (im.get(i - Wp + 1) != 0) ? 2u : 0u;
+    m |= (im.get(i - Wp) != 0) ? 4u : 0u;
+    m |= (im.get(i - Wp - 1) != 0) ? 8u : 0u;
+    m |= (im.get(i - 1) != 0) ? 16u : 0u;
+    m |= (im.get(i + Wp - 1) != 0) ? 32u : 0u;
+    m |= (im.get(i + Wp) != 0) ? 64u : 0u;
+    m |= (im.get(i + Wp + 1) != 0) ? 128u : 0u;
+    return m;
+}
+
+// icvFetchContour of an outer border (is_hole = 0, nbd = 2) from padded pixel (x0, y0); writes one
+// chain code per written point (the last one leads back to the start); returns the point count
+template <bool kLds>
+__device__ uint32_t fetch_outer(const Img<kLds>& im, int Wp, int x0, int y0, uint8_t* codes,
+                                uint64_t cap, uint64_t& cpos, bool& overflow) {
+    const int i0 = y0 * Wp + x0;
+    const uint32_t m0 = nb_mask(im, i0, Wp);
+    // clockwise from code 3 down to 5 (code 4, the scan's zero predecessor, ends the search)
+    int s = -1;
+    for (int k = 3; k >= -3; --k) {
+        const int c = k & 7;
+        if (m0 & (1u << c)) { s = c; break; }
+    }
+    if (s < 0) {  // single point
+        im.set(i0, (int8_t)(2 | -128));
+        return 1;
+    }
+    const int i1 = i0 + code_dy(s) * Wp + code_dx(s);
+    int i3 = i0;
+    uint32_t npts = 0;
+    for (;;) {
+        const int s_end = s;
+        const uint32_t m = nb_mask(im, i3, Wp);
+        // counter-clockwise from s_end + 1: first non-zero neighbour
+        const uint32_t rot = ((m | (m << 8)) >> (s_end + 1)) & 0xFFu;
+        s = (s_end + 1 + (int)__builtin_ctz(rot)) & 7;  // rot != 0: the previous pixel is set
+        const int i4 = i3 + code_dy(s) * Wp + code_dx(s);
+        if ((unsigned)(s - 1) < (unsigned)s_end) im.set(i3, (int8_t)(2 | -128));
+        else if (im.get(i3) == 1) im.set(i3, 2);
+        ++npts;
+        if (cpos < cap) {
+            if ((threadIdx.x & 63) == 0) codes[cpos] = (uint8_t)s;
+            ++cpos;
+        } else {
+            overflow = true;
+            return npts;
+        }
+        if (i4 == i0 && i3 == i1) break;
+        i3 = i4;
+        s = (s + 4) & 7;
+    }
+    return npts;
+}
+
+// one workgroup per layer (8 waves stage the image, wave 0 scans); rec[4 * d] = {x, y, first
+// code, points} of the d-th DISCOVERED contour.  Image layout (LDS, or the global scratch):
+// Wp x Hp int8 pixels, then Hp row flags (row has a non-zero pixel: an all-zero row holds no
+// transition of the scan and is skipped; marking never makes a zero non-zero).
+constexpr int kContourThreads = 512;
+template <bool kLds>
+__global__ __launch_bounds__(kContourThreads) void k_cc_contours(
+    const uint8_t* __restrict__ grid, uint32_t W, uint32_t H, int8_t* gscratch,
+    uint8_t* __restrict__ codes, uint64_t code_cap, uint32_t* __restrict__ rec, uint32_t rec_cap,
+    uint32_t* __restrict__ ncont, uint32_t* __restrict__ err) {
+    extern __shared__ int8_t s_img[];
+    const uint32_t z = blockIdx.x;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int Wp = (int)W + 2, Hp = (int)H + 2;
+    const Img<kLds> im{kLds ? s_img : gscratch + (size_t)z * ((size_t)Wp * Hp + Hp)};
+    const int rowflag = Wp * Hp;
+    const uint8_t* lay = grid + (size_t)z * W * H;
+    // binarised copy with a zero border (copyMakeBorder + threshold), 8 loads in flight per lane
+    for (int y = wv; y < Hp; y += kContourThreads / 64) {
+        const bool iny = y >= 1 && y <= (int)H;
+        const uint8_t* src = lay + (size_t)(y - 1) * W - 1;
+        bool any = false;
+        for (int x0 = 0; x0 < Wp; x0 += 512) {
+            int8_t v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int x = x0 + 64 * k + lane;
+                v[k] = (iny && x >= 1 && x <= (int)W && src[x]) ? 1 : 0;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int x = x0 + 64 * k + lane;
+                if (x < Wp) im.set(y * Wp + x, v[k]);
+                any |= v[k] != 0;
+            }
+        }
+        const bool nz = __ballot(any) != 0;
+        if (lane == 0) im.set(rowflag + y, nz ? 1 : 0);
+    }
+    __syncthreads();
+    if (wv != 0) return;  // the raster scan is sequential: one wave
+    uint8_t* cz = codes + (size_t)z * code_cap;
+    uint32_t* rz = rec + (size_t)z * rec_cap * 4;
+    uint64_t cpos = 0;
+    uint32_t nc = 0;
+    bool overflow = false;
+    for (int y = 1; y < Hp - 1 && !overflow; ++y) {  // cvFindNextContour, mode RETR_EXTERNAL
+        if (!im.get(rowflag + y)) continue;
+        const int rb = y * Wp;
+        int x = 1, prev = 0, lnbd = 0;
+        while (true) {
+            // skip the run of `prev` (64 pixels per ballot)
+            int xn = x;
+            while (xn < Wp - 1) {
+                const int xi = xn + lane;
+                const int v = xi < Wp - 1 ? im.get(rb + xi) : prev;
+                const uint64_t m = __ballot(v != prev);
+                if (m) {
+                    xn += __ffsll((long long)m) - 1;
+                    break;
+                }
+                xn += 64;
+            }
+            if (xn >= Wp - 1) break;
+            x = xn;
+            const int p = im.get(rb + x);
+            bool trace = false;
+            if (prev == 0 && p == 1) {
+                trace = im.get(rb + lnbd) <= 0;
+            } else if (p == 0 && prev >= 1) {  // a hole border start: skipped, lnbd moves
+                if (prev & -2) lnbd = x - 1;
+            }
+            if (trace) {
+                if (nc >= rec_cap) {
+                    overflow = true;
+                    break;
+                }
+                const uint64_t c0 = cpos;
+                const uint32_t np = fetch_outer(im, Wp, x, y, cz, code_cap, cpos, overflow);
+                if (lane == 0) {
+                    rz[4 * nc + 0] = (uint32_t)(x - 1);
+                    rz[4 * nc + 1] = (uint32_t)(y - 1);
+                    rz[4 * nc + 2] = (uint32_t)c0;
+                    rz[4 * nc + 3] = np;
+                }
+                ++nc;
+                if (overflow) break;
+                prev = im.get(rb + x);  // the scan resumes after the (now marked) start pixel
+                ++x;
+                continue;
+            }
+            prev = p;
+            if (prev & -2) lnbd = x;
+            ++x;
+        }
+    }
+    if (lane == 0) {
+        ncont[z] = nc;
+        if (overflow) atomicOr(err, 1u);
+    }
+}
+
+// labelsToContours: contour j (findContours order) = discovered contour nc - 1 - j
+__global__ __launch_bounds__(256) void k_cc_l2c(const uint32_t* __restrict__ rec, uint32_t rec_cap,
+                                                const uint32_t* __restrict__ ncont,
+                                                const uint16_t* __restrict__ labels, uint32_t W,
+                                                uint32_t H, const uint32_t* __restrict__ lstart,
+                                                int32_t* __restrict__ l2c) {
+    const uint32_t z = blockIdx.x, nc = ncont[z];
+    const uint32_t* rz = rec + (size_t)z * rec_cap * 4;
+    for (uint32_t d = threadIdx.x; d < nc; d += 256) {
+        const uint32_t x = rz[4 * d], y = rz[4 * d + 1];
+        const uint32_t lab = labels[(size_t)z * W * H + (size_t)y * W + x];
+        l2c[lstart[z] + lab] = (int32_t)(nc - 1 - d);
+    }
+}
+
+// ---- host ------------------------------------------------------------------------------------------
+struct GpuBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    GpuBuf() = default;
+    GpuBuf(const GpuBuf&) = delete;
+    GpuBuf& operator=(const GpuBuf&) = delete;
+    ~GpuBuf() {
+        if (p) (void)hipFree(p);
+    }
+    hipError_t ensure(size_t need) {
+        if (need <= bytes) return hipSuccess;
+        size_t nb = std::max(need, bytes + bytes / 2);
+        nb = (nb + 255) & ~size_t(255);
+        if (p) {
+            hipError_t e = hipDeviceSynchronize();
+            if (e != hipSuccess) return e;
+            (void)hipFree(p);
+            p = nullptr;
+            bytes = 0;
+        }
+        hipError_t e = hipMalloc(&p, nb);
+        if (e == hipSuccess) bytes = nb;
+        return e;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+struct SegError {
+    int code;
+    std::string msg;
+};
+[[noreturn]] void seg_fail(int code, const std::string& m) { throw SegError{code, m}; }
+#define SEGCHK(expr)                                                                          \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess)                                                                 \
+            seg_fail(GDF_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));         \
+    } while (0)
+
+}  // namespace
+
+struct gdf_segmenter {
+    int device = 0;
+    hipStream_t own = nullptr, user = nullptr;
+    hipStream_t s() const { return user ? user : own; }
+    uint32_t W = 0, H = 0, L = 0, flags = 0;
+    bool have = false;
+    GpuBuf par, bits, blabel, nlab, lstart, cstart, labels, st, sums, stats5, cent, l2c, conn;
+    GpuBuf codes, rec, ncont, err, scratch;
+    uint64_t code_cap = 0;
+    uint32_t rec_cap = 0;
+    std::vector<uint32_t> h_nlab, h_lstart;
+    std::vector<uint64_t> h_cstart;
+    uint32_t total = 0;
+    uint64_t conn_bytes = 0;
+    // contours resolved on the host (after the first query)
+    bool contours_read = false;
+    std::vector<uint32_t> h_ncont, h_rec;
+    std::vector<uint8_t> h_codes;
+    uint64_t total_points = 0;
+    uint32_t total_contours = 0;
+};
+
+namespace {
+
+template <class F>
+int seg_guarded(F&& f) {
+    try {
+        f();
+        return GDF_OK;
+    } catch (const SegError& e) {
+        gdf::set_last_error(e.msg);
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        gdf::set_last_error("host allocation failed");
+        return GDF_ERR_NOMEM;
+    } catch (...) {
+        gdf::set_last_error("unknown error");
+        return GDF_ERR_HIP;
+    }
+}
+
+void run_label_layers(gdf_segmenter* g, const uint8_t* grid, uint32_t W, uint32_t H, uint32_t L,
+                      uint32_t flags, hipStream_t s) {
+    if (!grid || W == 0 || H == 0 || L == 0) seg_fail(GDF_ERR_ARG, "empty grid");
+    if (W > 65534 || H > 65534) seg_fail(GDF_ERR_ARG, "layers wider or taller than 65534 cells");
+    const uint32_t BW = (W + 1) / 2, BH = (H + 1) / 2;
+    const uint64_t nbl = (uint64_t)BW * BH, nb = nbl * L;
+    if (nb >= 0xFFFFFFF0ull) seg_fail(GDF_ERR_ARG, "grid too large for 32-bit block indices");
+    g->have = false;
+    g->contours_read = false;
+    SEGCHK(g->par.ensure(nb * 4));
+    SEGCHK(g->bits.ensure(nb));
+    SEGCHK(g->blabel.ensure(nb * 4));
+    SEGCHK(g->nlab.ensure((size_t)L * 4));
+    const dim3 tiles((BW + kTile - 1) / kTile, (BH + kTile - 1) / kTile, L);
+    hipLaunchKernelGGL(k_cc_local, tiles, dim3(256), 0, s, grid, W, H, BW, BH,
+                       g->par.as<uint32_t>(), g->bits.as<uint8_t>());
+    hipLaunchKernelGGL(k_cc_merge, tiles, dim3(256), 0, s, g->bits.as<const uint8_t>(), BW, BH,
+                       g->par.as<uint32_t>());
+    hipLaunchKernelGGL(k_cc_flatten, dim3((uint32_t)((nb + 255) / 256)), dim3(256), 0, s,
+                       g->par.as<uint32_t>(), (uint32_t)nb);
+    hipLaunchKernelGGL(k_cc_rank, dim3(L), dim3(1024), 0, s, g->par.as<const uint32_t>(),
+                       (uint32_t)nbl, g->blabel.as<uint32_t>(), g->nlab.as<uint32_t>());
+    SEGCHK(hipGetLastError());
+    g->h_nlab.assign(L, 0);
+    SEGCHK(hipMemcpyAsync(g->h_nlab.data(), g->nlab.p, (size_t)L * 4, hipMemcpyDeviceToHost, s));
+    SEGCHK(hipStreamSynchronize(s));
+    g->h_lstart.assign(L, 0);
+    g->h_cstart.assign(L, 0);
+    uint64_t T = 0, cb = 0;
+    for (uint32_t i = 0; i < L; ++i) {
+        if (g->h_nlab[i] > 65536u)
+            seg_fail(GDF_ERR_CAPACITY, "more than 65535 components in a layer (CV_16U labels)");
+        g->h_lstart[i] = (uint32_t)T;
+        T += g->h_nlab[i];
+    }
+    const bool do_conn = (flags & GDF_SEG_CONNECTIONS) != 0;
+    if (do_conn)
+        for (uint32_t i = 0; i + 1 < L; ++i) {
+            g->h_cstart[i] = cb;
+            cb += (uint64_t)g->h_nlab[i] * g->h_nlab[i + 1];
+        }
+    if (cb > (1ull << 32)) seg_fail(GDF_ERR_CAPACITY, "layer connection matrices exceed 4 GiB");
+    g->total = (uint32_t)T;
+    g->conn_bytes = cb;
+    SEGCHK(g->lstart.ensure((size_t)L * 4));
+    SEGCHK(g->cstart.ensure((size_t)L * 8));
+    SEGCHK(g->labels.ensure((size_t)W * H * L * 2));
+    SEGCHK(g->st.ensure(T * kStatWords * 4));
+    SEGCHK(g->sums.ensure(T * 16));
+    SEGCHK(g->stats5.ensure(T * 20));
+    SEGCHK(g->cent.ensure(T * 16));
+    SEGCHK(g->l2c.ensure(T * 4));
+    SEGCHK(g->conn.ensure(std::max<uint64_t>(cb, 1)));
+    SEGCHK(hipMemcpyAsync(g->lstart.p, g->h_lstart.data(), (size_t)L * 4, hipMemcpyHostToDevice, s));
+    SEGCHK(hipMemcpyAsync(g->cstart.p, g->h_cstart.data(), (size_t)L * 8, hipMemcpyHostToDevice, s));
+    if (cb) SEGCHK(hipMemsetAsync(g->conn.p, 0, cb, s));  // prepareLayersConnections' clear
+    const uint32_t tb = (uint32_t)((T + 255) / 256);
+    hipLaunchKernelGGL(k_cc_init_stats, dim3(tb), dim3(256), 0, s, g->st.as<int32_t>(),
+                       g->sums.as<unsigned long long>(), (uint32_t)T);
+    SegArgs a{grid, W, H, L, BW, (uint32_t)nbl, g->par.as<const uint32_t>(),
+              g->blabel.as<const uint32_t>(), g->lstart.as<const uint32_t>(),
+              g->nlab.as<const uint32_t>(), g->cstart.as<const uint64_t>(),
+              g->labels.as<uint16_t>(), g->st.as<int32_t>(), g->sums.as<unsigned long long>(),
+              g->conn.as<uint8_t>(), do_conn ? 1 : 0};
+    hipLaunchKernelGGL(k_cc_pixels, dim3((W + 63) / 64, (H + kRowsPerWave - 1) / kRowsPerWave, L),
+                       dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_cc_finish, dim3(tb), dim3(256), 0, s, g->st.as<const int32_t>(),
+                       g->sums.as<const unsigned long long>(), (uint32_t)T,
+                       g->stats5.as<int32_t>(), g->cent.as<double>(), g->l2c.as<int32_t>());
+    SEGCHK(hipGetLastError());
+    if (flags & GDF_SEG_CONTOURS) {
+        const uint64_t Wp = W + 2, Hp = H + 2, img = Wp * Hp + Hp;  // + row flags
+        g->rec_cap = (uint32_t)(((uint64_t)(W + 1) / 2) * H + 1);
+        g->code_cap = 8ull * W * H + 64;
+        SEGCHK(g->codes.ensure(g->code_cap * L));
+        SEGCHK(g->rec.ensure((size_t)g->rec_cap * 16 * L));
+        SEGCHK(g->ncont.ensure((size_t)L * 4));
+        SEGCHK(g->err.ensure(4));
+        SEGCHK(hipMemsetAsync(g->err.p, 0, 4, s));
+        bool lds = img <= kLdsMax;
+        if (lds) {
+            static bool attr_set = false;
+            if (!attr_set) {
+                lds = hipFuncSetAttribute((const void*)k_cc_contours<true>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)kLdsMax) == hipSuccess;
+                attr_set = lds;
+            }
+        }
+        if (lds) {
+            hipLaunchKernelGGL(k_cc_contours<true>, dim3(L), dim3(kContourThreads), (size_t)img, s, grid, W, H,
+                               nullptr, g->codes.as<uint8_t>(), g->code_cap, g->rec.as<uint32_t>(),
+                               g->rec_cap, g->ncont.as<uint32_t>(), g->err.as<uint32_t>());
+        } else {
+            SEGCHK(g->scratch.ensure(img * L));
+            hipLaunchKernelGGL(k_cc_contours<false>, dim3(L), dim3(kContourThreads), 0, s, grid, W, H,
+                               g->scratch.as<int8_t>(), g->codes.as<uint8_t>(), g->code_cap,
+                               g->rec.as<uint32_t>(), g->rec_cap, g->ncont.as<uint32_t>(),
+                               g->err.as<uint32_t>());
+        }
+        hipLaunchKernelGGL(k_cc_l2c, dim3(L), dim3(256), 0, s, g->rec.as<const uint32_t>(),
+                           g->rec_cap, g->ncont.as<const uint32_t>(),
+                           g->labels.as<const uint16_t>(), W, H, g->lstart.as<const uint32_t>(),
+                           g->l2c.as<int32_t>());
+        SEGCHK(hipGetLastError());
+    }
+    g->W = W;
+    g->H = H;
+    g->L = L;
+    g->flags = flags;
+    g->have = true;
+}
+
+void need_result(gdf_segmenter* g) {
+    if (!g->have) seg_fail(GDF_ERR_STATE, "no segmentation result (call gdf_seg_label_layers)");
+}
+
+// contour records and chain codes to the host (once per result)
+void read_contours(gdf_segmenter* g) {
+    need_result(g);
+    if (!(g->flags & GDF_SEG_CONTOURS)) seg_fail(GDF_ERR_STATE, "contours were not requested");
+    if (g->contours_read) return;
+    const hipStream_t s = g->s();
+    uint32_t err = 0;
+    g->h_ncont.assign(g->L, 0);
+    SEGCHK(hipMemcpyAsync(&err, g->err.p, 4, hipMemcpyDeviceToHost, s));
+    SEGCHK(hipMemcpyAsync(g->h_ncont.data(), g->ncont.p, (size_t)g->L * 4, hipMemcpyDeviceToHost, s));
+    SEGCHK(hipStreamSynchronize(s));
+    if (err) seg_fail(GDF_ERR_CAPACITY, "contour capacity exceeded");
+    g->h_rec.assign((size_t)g->rec_cap * 4 * g->L, 0);
+    g->total_contours = 0;
+    g->total_points = 0;
+    uint64_t code_bytes = 0;
+    for (uint32_t z = 0; z < g->L; ++z) {
+        const uint32_t n = g->h_ncont[z];
+        if (n)
+            SEGCHK(hipMemcpyAsync(g->h_rec.data() + (size_t)z * g->rec_cap * 4,
+                                  g->rec.as<uint32_t>() + (size_t)z * g->rec_cap * 4,
+                                  (size_t)n * 16, hipMemcpyDeviceToHost, s));
+    }
+    SEGCHK(hipStreamSynchronize(s));
+    std::vector<uint64_t> used(g->L, 0);
+    for (uint32_t z = 0; z < g->L; ++z) {
+        const uint32_t n = g->h_ncont[z];
+        const uint32_t* r = g->h_rec.data() + (size_t)z * g->rec_cap * 4;
+        for (uint32_t d = 0; d < n; ++d) g->total_points += r[4 * d + 3];
+        if (n) used[z] = (uint64_t)r[4 * (n - 1) + 2] + r[4 * (n - 1) + 3];
+        g->total_contours += n;
+        code_bytes = std::max(code_bytes, used[z]);
+    }
+    g->h_codes.assign((size_t)g->code_cap * g->L, 0);
+    for (uint32_t z = 0; z < g->L; ++z)
+        if (used[z])
+            SEGCHK(hipMemcpyAsync(g->h_codes.data() + (size_t)z * g->code_cap,
+                                  g->codes.as<uint8_t>() + (size_t)z * g->code_cap, used[z],
+                                  hipMemcpyDeviceToHost, s));
+    SEGCHK(hipStreamSynchronize(s));
+    g->contours_read = true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gdf_seg_create(int device, gdf_segmenter** out) {
+    if (!out) return GDF_ERR_ARG;
+    return seg_guarded([&] {
+        SEGCHK(hipSetDevice(device));
+        auto* g = new gdf_segmenter();
+        g->device = device;
+        hipError_t e = hipStreamCreateWithFlags(&g->own, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            delete g;
+            SEGCHK(e);
+        }
+        *out = g;
+    });
+}
+
+int gdf_seg_destroy(gdf_segmenter* g) {
+    if (!g) return GDF_OK;
+    (void)hipSetDevice(g->device);
+    (void)hipStreamSynchronize(g->s());
+    if (g->own) (void)hipStreamDestroy(g->own);
+    delete g;
+    return GDF_OK;
+}
+
+int gdf_seg_set_stream(gdf_segmenter* g, void* stream) {
+    if (!g) return GDF_ERR_ARG;
+    g->user = static_cast<hipStream_t>(stream);
+    return GDF_OK;
+}
+
+int gdf_seg_label_layers(gdf_segmenter* g, const uint8_t* grid, uint32_t W, uint32_t H,
+                         uint32_t L, uint32_t flags) {
+    if (!g) return GDF_ERR_ARG;
+    return seg_guarded([&] {
+        SEGCHK(hipSetDevice(g->device));
+        run_label_layers(g, grid, W, H, L, flags, g->s());
+    });
+}
+
+int gdf_seg_label_engine_grid(gdf_segmenter* g, gdf_engine* e, uint32_t flags) {
+    if (!g || !e) return GDF_ERR_ARG;
+    const uint8_t* occ = nullptr;
+    uint32_t gs[3] = {0, 0, 0};
+    uint64_t nc = 0;
+    void* st = nullptr;
+    int rc = gdf_get_device_results(e, nullptr, nullptr, nullptr, &occ);
+    if (rc == GDF_OK) rc = gdf_get_grid_size(e, gs, &nc);
+    if (rc == GDF_OK) rc = gdf_get_stream(e, &st);
+    if (rc != GDF_OK) return rc;
+    if (!occ) {
+        gdf::set_last_error("the engine has no occupancy grid yet");
+        return GDF_ERR_STATE;
+    }
+    return seg_guarded([&] {
+        SEGCHK(hipSetDevice(g->device));
+        run_label_layers(g, occ, gs[0], gs[1], gs[2], flags, static_cast<hipStream_t>(st));
+        // later downloads on the segmenter's stream must follow the engine stream's work
+        if (static_cast<hipStream_t>(st) != g->s()) SEGCHK(hipStreamSynchronize(static_cast<hipStream_t>(st)));
+    });
+}
+
+int gdf_seg_get_counts(gdf_segmenter* g, gdf_seg_counts* out) {
+    if (!g || !out) return GDF_ERR_ARG;
+    return seg_guarded([&] {
+        need_result(g);
+        if (g->flags & GDF_SEG_CONTOURS) read_contours(g);
+        out->width = g->W;
+        out->height = g->H;
+        out->layers = g->L;
+        out->total_labels = g->total;
+        out->total_contours = g->total_contours;
+        out->total_contour_points = g->total_points;
+        out->connection_bytes = g->conn_bytes;
+    });
+}
+
+int gdf_seg_download_labels(gdf_segmenter* g, uint16_t* out, uint64_t cap) {
+    if (!g || !out) return GDF_ERR_ARG;
+    return seg_guarded([&] {
+        need_result(g);
+        const uint64_t n = (uint64_t)g->W * g->H * g->L;
+        if (cap < n) seg_fail(GDF_ERR_CAPACITY, "labels capacity too small");
+        SEGCHK(hipMemcpyAsync(out, g->labels.p, n * 2, hipMemcpyDeviceToHost, g->s()));
+        SEGCHK(hipStreamSynchronize(g->s()));
+    });
+}
+
+int gdf_seg_download_num_labels(gdf_segmenter* g, uint32_t* out, uint32_t cap) {
+    if (!g || !out) return GDF_ERR_ARG;
+    return seg_guarded([&] {
+        need_result(g);
+        if (cap < g->L) seg_fail(GDF_ERR_CAPACITY, "num_labels capacity too small");
+        std::memcpy(out, g->h_nlab.data(), (size_t)g->L * 4);
+    });
+}
+
+int gdf_seg_download_stats(gdf_segmenter* g, int32_t* stats5, double* cent, uint32_t cap) {
+    if (!g) return GDF_ERR_ARG;
+    return seg_guarded([&] {
+        need_result(g);
+        if (cap < g->total) seg_fail(GDF_ERR_CAPACITY, "stats capacity too small");
+        if (stats5)
+            SEGCHK(hipMemcpyAsync(stats5, g->stats5.p, (size_t)g->total * 20, hipMemcpyDeviceToHost, g->s()));
+        if (cent)
+            SEGCHK(hipMemcpyAsync(cent, g->cent.p, (size_t)g->total * 16, hipMemcpyDeviceToHost, g->s()));
+        SEGCHK(hipStreamSynchronize(g->s()));
+    });
+}
+
+int gdf_seg_download_connections(gdf_segmenter* g, uint8_t* out, uint64_t cap, uint64_t* starts,
+                                 uint32_t starts_cap) {
+    if (!g) return GDF_ERR_ARG;
+    return seg_guarded([&] {
+        need_result(g);
+        if (!(g->flags & GDF_SEG_CONNECTIONS)) seg_fail(GDF_ERR_STATE, "connections were not requested");
+        if (out) {
+            if (cap < g->conn_bytes) seg_fail(GDF_ERR_CAPACITY, "connections capacity too small");
+            if (g->conn_bytes)
+                SEGCHK(hipMemcpyAsync(out, g->conn.p, g->conn_bytes, hipMemcpyDeviceToHost, g->s()));
+            SEGCHK(hipStreamSynchronize(g->s()));
+        }
+        if (starts) {
+            const uint32_t n = g->L ? g->L - 1 : 0;
+            if (starts_cap < n) seg_fail(GDF_ERR_CAPACITY, "starts capacity too small");
+            std::memcpy(starts, g->h_cstart.data(), (size_t)n * 8);
+        }
+    });
+}
+
+int gdf_seg_download_contours(gdf_segmenter* g, int32_t* l2c, uint32_t* per_layer,
+                              uint32_t* sizes, int32_t* pts, uint64_t pts_cap) {
+    if (!g) return GDF_ERR_ARG;
+    return seg_guarded([&] {
+        read_contours(g);
+        if (l2c) {
+            SEGCHK(hipMemcpyAsync(l2c, g->l2c.p, (size_t)g->total * 4, hipMemcpyDeviceToHost, g->s()));
+            SEGCHK(hipStreamSynchronize(g->s()));
+        }
+        if (per_layer) std::memcpy(per_layer, g->h_ncont.data(), (size_t)g->L * 4);
+        if (pts && pts_cap < g->total_points) seg_fail(GDF_ERR_CAPACITY, "points capacity too small");
+        uint64_t q = 0;
+        uint32_t c = 0;
+        for (uint32_t z = 0; z < g->L; ++z) {
+            const uint32_t n = g->h_ncont[z];
+            const uint32_t* r = g->h_rec.data() + (size_t)z * g->rec_cap * 4;
+            const uint8_t* cz = g->h_codes.data() + (size_t)z * g->code_cap;
+            for (uint32_t j = 0; j < n; ++j) {  // findContours order = reverse discovery
+                const uint32_t d = n - 1 - j;
+                const uint32_t np = r[4 * d + 3];
+                if (sizes) sizes[c] = np;
+                ++c;
+                if (!pts) continue;
+                int32_t x = (int32_t)r[4 * d], y = (int32_t)r[4 * d + 1];
+                const uint8_t* cc = cz + r[4 * d + 2];
+                static const int dx[8] = {1, 1, 0, -1, -1, -1, 0, 1};
+                static const int dy[8] = {0, -1, -1, -1, 0, 1, 1, 1};
+                for (uint32_t k = 0; k < np; ++k) {
+                    pts[2 * q] = x;
+                    pts[2 * q + 1] = y;
+                    ++q;
+                    if (k + 1 < np) {
+                        x += dx[cc[k] & 7];
+                        y += dy[cc[k] & 7];
+                    }
+                }
+            }
+        }
+    });
+}
+
+// mergeLabelsAcrossLayers (fusion.cpp:2243-2361): bottom-up then top-down min propagation of the
+// sequential global labels over the connection matrices (background only with background), then
+// UIntGrouper order: merged id = rank of the propagated id among the distinct ones.
+int gdf_seg_merge_labels(gdf_segmenter* g, uint32_t* merged, uint32_t cap, uint32_t* nobj) {
+    if (!g) return GDF_ERR_ARG;
+    return seg_guarded([&] {
+        need_result(g);
+        if (!(g->flags & GDF_SEG_CONNECTIONS)) seg_fail(GDF_ERR_STATE, "connections were not requested");
+        if (merged && cap < g->total) seg_fail(GDF_ERR_CAPACITY, "merged capacity too small");
+        std::vector<uint8_t> conn(g->conn_bytes);
+        if (g->conn_bytes) {
+            SEGCHK(hipMemcpyAsync(conn.data(), g->conn.p, g->conn_bytes, hipMemcpyDeviceToHost, g->s()));
+            SEGCHK(hipStreamSynchronize(g->s()));
+        }
+        const uint32_t L = g->L;
+        std::vector<uint32_t> gl(g->total);
+        for (uint32_t k = 0; k < g->total; ++k) gl[k] = k;
+        auto pass = [&](uint32_t la, uint32_t lb, bool up) {
+            const uint32_t nA = g->h_nlab[la], nB = g->h_nlab[lb];
+            const uint8_t* m = conn.data() + g->h_cstart[la];
+            if (up) {  // layer b takes the lowest label of its connected labels in layer a
+                for (uint32_t b = 0; b < nB; ++b) {
+                    uint32_t& v = gl[g->h_lstart[lb] + b];
+                    for (uint32_t a = 0; a < nA; ++a)
+                        if ((a == 0) == (b == 0) && m[(size_t)a * nB + b])
+                            v = std::min(v, gl[g->h_lstart[la] + a]);
+                }
+            } else {
+                for (uint32_t a = 0; a < nA; ++a) {
+                    uint32_t& v = gl[g->h_lstart[la] + a];
+                    for (uint32_t b = 0; b < nB; ++b)
+                        if ((a == 0) == (b == 0) && m[(size_t)a * nB + b])
+                            v = std::min(v, gl[g->h_lstart[lb] + b]);
+                }
+            }
+        };
+        for (uint32_t i = 0; i + 1 < L; ++i) pass(i, i + 1, true);
+        for (uint32_t i = 0; i + 1 < L; ++i) pass(L - 2 - i, L - 1 - i, false);
+        std::vector<uint32_t> rank(g->total, kNone);
+        for (uint32_t k = 0; k < g->total; ++k) rank[gl[k]] = 0;  // gl[k] <= k < total
+        uint32_t next = 0;
+        for (uint32_t v = 0; v < g->total; ++v)
+            if (rank[v] == 0) rank[v] = next++;
+        if (merged)
+            for (uint32_t k = 0; k < g->total; ++k) merged[k] = rank[gl[k]];
+        if (nobj) *nobj = next;
+    });
+}
+
+int gdf_seg_get_device_results(gdf_segmenter* g, const uint16_t** labels, const int32_t** stats5,
+                               const double** cent, const uint8_t** conn) {
+    if (!g) return GDF_ERR_ARG;
+    if (!g->have) {
+        gdf::set_last_error("no segmentation result");
+        return GDF_ERR_STATE;
+    }
+    if (labels) *labels = g->labels.as<const uint16_t>();
+    if (stats5) *stats5 = g->stats5.as<const int32_t>();
+    if (cent) *cent = g->cent.as<const double>();
+    if (conn) *conn = g->conn.as<const uint8_t>();
+    return GDF_OK;
+}
+
+}  // extern "C"

@@ -74,6 +74,13 @@ class FrameResult(C.Structure):
                 ("latest_time_nsec", C.c_uint32)]
 
 
+class SegCounts(C.Structure):
+    """gdf_seg_counts (include/gdf_segment.h)."""
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("layers", C.c_uint32),
+                ("total_labels", C.c_uint32), ("total_contours", C.c_uint32),
+                ("total_contour_points", C.c_uint64), ("connection_bytes", C.c_uint64)]
+
+
 class GDFError(RuntimeError):
     def __init__(self, status: int, msg: str):
         super().__init__(f"{STATUS_NAMES.get(status, status)}: {msg}")
@@ -104,7 +111,12 @@ EXPORTED = [
     "gdf_run_depth_stream", "gdf_run_host_stream", "gdf_run_depth_stream_batched",
     "gdf_next_frame_in_batch", "gdf_get_batch_ranges", "gdf_download_batch_occupancy_grid",
     "gdf_mask_dilate", "gdf_transform_points", "gdf_add_halo_depthmap_device",
-    "gdf_partition_points", "gdf_voxelize_points", "gdf_last_sort_items",
+    "gdf_partition_points", "gdf_voxelize_points", "gdf_last_sort_items", "gdf_get_stream",
+    # include/gdf_segment.h: the GPU object-segmentation front end
+    "gdf_seg_create", "gdf_seg_destroy", "gdf_seg_set_stream", "gdf_seg_label_layers",
+    "gdf_seg_label_engine_grid", "gdf_seg_get_counts", "gdf_seg_download_labels",
+    "gdf_seg_download_num_labels", "gdf_seg_download_stats", "gdf_seg_download_connections",
+    "gdf_seg_download_contours", "gdf_seg_merge_labels", "gdf_seg_get_device_results",
 ]
 
 
@@ -185,6 +197,20 @@ def load_library(path: str = LIB_PATH):
         "gdf_get_batch_ranges": (i32, [vp, vp, vp, u32, P(u32)]),
         "gdf_download_batch_occupancy_grid": (i32, [vp, u32, vp, u64]),
         "gdf_last_sort_items": (i32, [vp, P(u32), P(i32)]),
+        "gdf_get_stream": (i32, [vp, P(vp)]),
+        "gdf_seg_create": (i32, [i32, P(vp)]),
+        "gdf_seg_destroy": (i32, [vp]),
+        "gdf_seg_set_stream": (i32, [vp, vp]),
+        "gdf_seg_label_layers": (i32, [vp, vp, u32, u32, u32, u32]),
+        "gdf_seg_label_engine_grid": (i32, [vp, vp, u32]),
+        "gdf_seg_get_counts": (i32, [vp, P(SegCounts)]),
+        "gdf_seg_download_labels": (i32, [vp, vp, u64]),
+        "gdf_seg_download_num_labels": (i32, [vp, vp, u32]),
+        "gdf_seg_download_stats": (i32, [vp, vp, vp, u32]),
+        "gdf_seg_download_connections": (i32, [vp, vp, u64, vp, u32]),
+        "gdf_seg_download_contours": (i32, [vp, vp, vp, vp, vp, u64]),
+        "gdf_seg_merge_labels": (i32, [vp, vp, u32, P(u32)]),
+        "gdf_seg_get_device_results": (i32, [vp, P(vp), P(vp), P(vp), P(vp)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -656,4 +682,87 @@ class GPUDepthmapFusion:
         r = FrameResult()
         self._check(self._lib.gdf_process_frame(self._h, C.byref(p), C.byref(r)))
         self._keep = []
+        return r
+
+
+# segmentation flags (include/gdf_segment.h)
+SEG_CONTOURS, SEG_CONNECTIONS, SEG_ALL = 1, 2, 3
+
+
+class Segmenter:
+    """GPU object-segmentation front end (include/gdf_segment.h): labelVoxels +
+    layers connections + mergeLabelsAcrossLayers of the reference's objectSegmentation
+    (src/gpu_depthmap_fusion.cpp:1872-2361) on a device u8 grid [layers, height, width]."""
+
+    def __init__(self, device: int = 0, lib_path: str = LIB_PATH):
+        self._lib = load_library(lib_path)
+        h = C.c_void_p()
+        self._check(self._lib.gdf_seg_create(device, C.byref(h)))
+        self._h = h
+
+    def _check(self, rc: int):
+        if rc != GDF_OK:
+            raise GDFError(rc, (self._lib.gdf_last_error() or b"").decode())
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.gdf_seg_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_ptr: int):
+        self._check(self._lib.gdf_seg_set_stream(self._h, C.c_void_p(stream_ptr)))
+
+    def label_layers(self, grid_ptr: int, width: int, height: int, layers: int,
+                     flags: int = SEG_ALL):
+        """objectSegmentation front end on a device grid (a torch uint8 tensor's data_ptr())."""
+        self._check(self._lib.gdf_seg_label_layers(self._h, C.c_void_p(grid_ptr), width, height,
+                                                   layers, flags))
+
+    def label_engine_grid(self, engine: "GPUDepthmapFusion", flags: int = SEG_ALL):
+        """The same on the engine's current occupancy grid (after voxelOccupancyGrid)."""
+        self._check(self._lib.gdf_seg_label_engine_grid(self._h, engine._h, flags))
+
+    def counts(self) -> SegCounts:
+        c = SegCounts()
+        self._check(self._lib.gdf_seg_get_counts(self._h, C.byref(c)))
+        return c
+
+    def results(self, contours: bool = True, connections: bool = True) -> dict:
+        """Every output as flat arrays with the keys of oracle.object_segmentation_front."""
+        c = self.counts()
+        L, H, W, T = c.layers, c.height, c.width, c.total_labels
+        r = {}
+        r["labels"] = np.zeros((L, H, W), np.uint16)
+        self._check(self._lib.gdf_seg_download_labels(self._h, _ptr(r["labels"]), L * H * W))
+        r["num_labels"] = np.zeros(L, np.uint32)
+        self._check(self._lib.gdf_seg_download_num_labels(self._h, _ptr(r["num_labels"]), L))
+        r["stats"] = np.zeros((T, 5), np.int32)
+        r["centroids"] = np.zeros((T, 2), np.float64)
+        self._check(self._lib.gdf_seg_download_stats(self._h, _ptr(r["stats"]),
+                                                     _ptr(r["centroids"]), T))
+        if contours:
+            r["labels_to_contours"] = np.zeros(T, np.int32)
+            r["contours_per_layer"] = np.zeros(L, np.uint32)
+            r["contour_sizes"] = np.zeros(c.total_contours, np.uint32)
+            r["contour_points"] = np.zeros((c.total_contour_points, 2), np.int32)
+            self._check(self._lib.gdf_seg_download_contours(
+                self._h, _ptr(r["labels_to_contours"]), _ptr(r["contours_per_layer"]),
+                _ptr(r["contour_sizes"]), _ptr(r["contour_points"]), c.total_contour_points))
+        if connections:
+            r["connections"] = np.zeros(c.connection_bytes, np.uint8)
+            r["connection_starts"] = np.zeros(max(L - 1, 0), np.uint64)
+            self._check(self._lib.gdf_seg_download_connections(
+                self._h, _ptr(r["connections"]), c.connection_bytes,
+                _ptr(r["connection_starts"]), max(L - 1, 0)))
+            r["merged"] = np.zeros(T, np.uint32)
+            nobj = C.c_uint32(0)
+            self._check(self._lib.gdf_seg_merge_labels(self._h, _ptr(r["merged"]), T,
+                                                       C.byref(nobj)))
+            r["num_objects"] = nobj.value
         return r
