@@ -530,6 +530,11 @@ def run_secondary(args, params):
         out["c3"] = run_c3(window=args.c3_window, steps=20, ring=4, profile_steps=5)
     except Exception as exc:  # reported, not hidden
         out["c3"] = {"error": repr(exc)}
+    try:  # objectSegmentation front end on the grid of the C2-style stream
+        from bench_seg import run_seg
+        out["segmentation"] = run_seg(frames=16, reps=20)
+    except Exception as exc:
+        out["segmentation"] = {"error": repr(exc)}
     return out
 
 

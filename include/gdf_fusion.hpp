@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "gdf.h"
+#include "gdf_segment.h"
 
 // The component calls glMemoryBarrier(GL_ALL_BARRIER_BITS) between the engine calls
 // (component.cpp:164-309, 12 sites); ordering is the HIP stream's here, so without a GL header
@@ -44,8 +45,11 @@ struct MeasureTime {
 
 class GPUDepthmapFusion {
 public:
-    explicit GPUDepthmapFusion(int device = 0) { check(gdf_create(device, &h_)); }
-    ~GPUDepthmapFusion() { gdf_destroy(h_); }
+    explicit GPUDepthmapFusion(int device = 0) : device_(device) { check(gdf_create(device, &h_)); }
+    ~GPUDepthmapFusion() {
+        if (seg_) gdf_seg_destroy(seg_);
+        gdf_destroy(h_);
+    }
     GPUDepthmapFusion(const GPUDepthmapFusion&) = delete;
     GPUDepthmapFusion& operator=(const GPUDepthmapFusion&) = delete;
 
@@ -210,6 +214,82 @@ public:
         return r;
     }
 
+    // ---- object segmentation front end (fusion.cpp:1872-2361) on the GPU ----------------------
+    // labelVoxels (:1872-2011): labels, stats, centroids, contours and labelsToContours of every
+    // z-layer of the current occupancy grid (the grid stays on the device; downloadVoxel-
+    // OccupancyGrid is not needed for it) + the layer connection matrices (:2075-2214)
+    void labelVoxels() {
+        if (!seg_) check(gdf_seg_create(device_, &seg_));
+        check(gdf_seg_label_engine_grid(seg_, h_, GDF_SEG_ALL));
+        gdf_seg_counts c{};
+        check(gdf_seg_get_counts(seg_, &c));
+        const uint32_t L = c.layers, T = c.total_labels;
+        m_ccLabeledLayersData.resize((size_t)c.width * c.height * L);
+        check(gdf_seg_download_labels(seg_, m_ccLabeledLayersData.data(), m_ccLabeledLayersData.size()));
+        m_ccNumLabelsPerLayer.resize(L);
+        check(gdf_seg_download_num_labels(seg_, m_ccNumLabelsPerLayer.data(), L));
+        m_ccStatsData.resize((size_t)T * 5);
+        m_ccCentroidsData.resize((size_t)T * 2);
+        check(gdf_seg_download_stats(seg_, m_ccStatsData.data(), m_ccCentroidsData.data(), T));
+        m_ccStatsDataStarts.resize(L);
+        m_ccCentroidsDataStarts.resize(L);
+        m_ccLabelsLayerStarts.resize(L);
+        for (uint32_t i = 0, t = 0; i < L; t += m_ccNumLabelsPerLayer[i++]) {
+            m_ccLabelsLayerStarts[i] = t;
+            m_ccStatsDataStarts[i] = 5 * (int)t;
+            m_ccCentroidsDataStarts[i] = 2 * (int)t;
+        }
+        std::vector<int32_t> l2c(T), pts(2 * c.total_contour_points);
+        std::vector<uint32_t> per(L), sizes(c.total_contours);
+        check(gdf_seg_download_contours(seg_, l2c.data(), per.data(), sizes.data(), pts.data(),
+                                        c.total_contour_points));
+        m_labelsToContoursPerLayer.assign(L, {});
+        m_contoursPerLayer.assign(L, {});
+        size_t q = 0, k = 0;
+        for (uint32_t i = 0; i < L; ++i) {
+            const uint32_t t0 = m_ccLabelsLayerStarts[i];
+            m_labelsToContoursPerLayer[i].assign(l2c.begin() + t0,
+                                                 l2c.begin() + t0 + m_ccNumLabelsPerLayer[i]);
+            m_contoursPerLayer[i].resize(per[i]);
+            for (uint32_t j = 0; j < per[i]; ++j, ++k)
+                for (uint32_t n = 0; n < sizes[k]; ++n, ++q)
+                    m_contoursPerLayer[i][j].push_back(Point{pts[2 * q], pts[2 * q + 1]});
+        }
+        m_ccLayersConnectionsData.resize(c.connection_bytes);
+        m_ccLayersConnectionsDataStarts.resize(L ? L - 1 : 0);
+        check(gdf_seg_download_connections(seg_, m_ccLayersConnectionsData.data(),
+                                           m_ccLayersConnectionsData.size(),
+                                           m_ccLayersConnectionsDataStarts.data(),
+                                           (uint32_t)m_ccLayersConnectionsDataStarts.size()));
+    }
+    // the label upload, connection-matrix preparation and the layers_connections dispatch are
+    // part of labelVoxels here (the labels never leave the device)
+    void uploadVoxelLabels() {}
+    void prepareLayersConnections() {}
+    void computeLayersConnections() {}
+    void downloadLayersConnections() {}
+    // mergeLabelsAcrossLayers (:2243-2361): m_ccLabelsMerged / Layer / Local per global label
+    void mergeLabelsAcrossLayers() {
+        const size_t T = m_ccStatsData.size() / 5;
+        m_ccLabelsMerged.resize(T);
+        uint32_t nobj = 0;
+        check(gdf_seg_merge_labels(seg_, m_ccLabelsMerged.data(), (uint32_t)T, &nobj));
+        m_ccLabelsLayer.resize(T);
+        m_ccLabelsLocal.resize(T);
+        for (uint32_t i = 0, t = 0; i < m_ccNumLabelsPerLayer.size(); ++i)
+            for (uint32_t k = 0; k < m_ccNumLabelsPerLayer[i]; ++k, ++t) {
+                m_ccLabelsLayer[t] = i;
+                m_ccLabelsLocal[t] = k;
+            }
+        m_ccNumObjects = nobj;
+    }
+    // objectSegmentation (:2552-2575) up to the merged labels; createCCObjects and the tracking
+    // that consume them stay out of scope
+    void objectSegmentation() {
+        labelVoxels();
+        mergeLabelsAcrossLayers();
+    }
+
     gdf_rollbuffer_state rollbufferState() {
         gdf_rollbuffer_state s{};
         check(gdf_get_rollbuffer_state(h_, &s));
@@ -231,6 +311,22 @@ public:
     uint32_t m_rollBufferSelectionSequenceStart = 0, m_rollBufferSelectionSequenceCount = 0;
     uint32_t m_rollBufferEarliestTimeSec = 0, m_rollBufferEarliestTimeNSec = 0;
     uint32_t m_rollBufferLastTimeSec = 0, m_rollBufferLastTimeNSec = 0;
+    // segmentation members (gpu_depthmap_fusion.h:328-341, 511-518), flat like their *Data
+    // storage; cv::Mat_ views of them are (rows, cols, pointer) over these vectors
+    struct Point {  // cv::Point
+        int x, y;
+    };
+    std::vector<uint16_t> m_ccLabeledLayersData;
+    std::vector<uint32_t> m_ccNumLabelsPerLayer;
+    std::vector<int32_t> m_ccStatsData;
+    std::vector<double> m_ccCentroidsData;
+    std::vector<int> m_ccStatsDataStarts, m_ccCentroidsDataStarts;
+    std::vector<std::vector<int>> m_labelsToContoursPerLayer;
+    std::vector<std::vector<std::vector<Point>>> m_contoursPerLayer;
+    std::vector<uint8_t> m_ccLayersConnectionsData;
+    std::vector<uint64_t> m_ccLayersConnectionsDataStarts;
+    std::vector<uint32_t> m_ccLabelsMerged, m_ccLabelsLayer, m_ccLabelsLocal, m_ccLabelsLayerStarts;
+    uint32_t m_ccNumObjects = 0;
 
 private:
     void syncRollbuffer() {
@@ -255,6 +351,8 @@ private:
         return n;
     }
     gdf_engine* h_ = nullptr;
+    gdf_segmenter* seg_ = nullptr;
+    int device_ = 0;
     float lo_[3] = {0, 0, 0}, cs_[3] = {1, 1, 1};
     uint32_t gridSize_[3] = {0, 0, 0};
 };

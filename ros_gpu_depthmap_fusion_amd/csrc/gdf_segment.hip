@@ -27,6 +27,8 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -203,7 +205,9 @@ struct SegArgs {
     unsigned long long* sums;  // [T][2]
     uint8_t* conn;
     int do_conn;
+    unsigned long long* bgpart;  // [L][waves of the layer][kBgWords]: background partials
 };
+constexpr uint32_t kBgWords = 5;
 
 __device__ __forceinline__ uint32_t pixel_label(const SegArgs& a, uint32_t z, uint32_t x,
                                                 uint32_t y) {
@@ -314,8 +318,73 @@ __global__ __launch_bounds__(64) void k_cc_pixels(SegArgs a) {
             }
         }
     }
-    acc_flush(bg, a, ls);
+    // the background label is in every wave: partials (no atomics), reduced per layer by
+    // k_cc_bg_reduce; kBgWords u64 per wave: {minx | miny}, {maxx | maxy}, {area | first}, sx, sy
+    if (lane == 0) {
+        unsigned long long* bp =
+            a.bgpart + kBgWords * ((size_t)(z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x);
+        bp[0] = ((unsigned long long)(uint32_t)bg.minx << 32) | (uint32_t)bg.miny;
+        bp[1] = ((unsigned long long)(uint32_t)bg.maxx << 32) | (uint32_t)bg.maxy;
+        bp[2] = ((unsigned long long)bg.area << 32) | bg.first;
+        bp[3] = bg.sx;
+        bp[4] = bg.sy;
+    }
     acc_flush(fg, a, ls);
+}
+
+// one workgroup per layer: the background label's stats from the k_cc_pixels partials
+__global__ __launch_bounds__(256) void k_cc_bg_reduce(const unsigned long long* __restrict__ bgpart,
+                                                      uint32_t waves_per_layer,
+                                                      const uint32_t* __restrict__ lstart,
+                                                      int32_t* __restrict__ st,
+                                                      unsigned long long* __restrict__ sums) {
+    __shared__ int32_t s_i[4][8];
+    __shared__ uint32_t s_u[2][8];
+    __shared__ unsigned long long s_s[2][8];
+    const uint32_t z = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+    int32_t mnx = INT_MAX, mny = INT_MAX, mxx = INT_MIN, mxy = INT_MIN;
+    uint32_t area = 0, first = kNone;
+    unsigned long long sx = 0, sy = 0;
+    const unsigned long long* bp = bgpart + (size_t)z * waves_per_layer * kBgWords;
+    for (uint32_t i = t; i < waves_per_layer; i += 256) {
+        const unsigned long long* q = bp + (size_t)i * kBgWords;
+        const unsigned long long a0 = q[0], a1 = q[1], a2 = q[2];
+        mnx = min(mnx, (int32_t)(a0 >> 32));
+        mny = min(mny, (int32_t)(uint32_t)a0);
+        mxx = max(mxx, (int32_t)(a1 >> 32));
+        mxy = max(mxy, (int32_t)(uint32_t)a1);
+        area += (uint32_t)(a2 >> 32);
+        first = min(first, (uint32_t)a2);
+        sx += q[3];
+        sy += q[4];
+    }
+    for (int d = 32; d >= 1; d >>= 1) {
+        mnx = min(mnx, __shfl_xor(mnx, d, 64));
+        mny = min(mny, __shfl_xor(mny, d, 64));
+        mxx = max(mxx, __shfl_xor(mxx, d, 64));
+        mxy = max(mxy, __shfl_xor(mxy, d, 64));
+        area += __shfl_xor(area, d, 64);
+        first = min(first, (uint32_t)__shfl_xor((int)first, d, 64));
+        sx += __shfl_xor(sx, d, 64);
+        sy += __shfl_xor(sy, d, 64);
+    }
+    if (lane == 0) {
+        s_i[0][w] = mnx; s_i[1][w] = mny; s_i[2][w] = mxx; s_i[3][w] = mxy;
+        s_u[0][w] = area; s_u[1][w] = first;
+        s_s[0][w] = sx; s_s[1][w] = sy;
+    }
+    __syncthreads();
+    if (t != 0) return;
+    for (int k = 1; k < 4; ++k) {
+        mnx = min(mnx, s_i[0][k]); mny = min(mny, s_i[1][k]);
+        mxx = max(mxx, s_i[2][k]); mxy = max(mxy, s_i[3][k]);
+        area += s_u[0][k]; first = min(first, s_u[1][k]);
+        sx += s_s[0][k]; sy += s_s[1][k];
+    }
+    int32_t* o = st + (size_t)lstart[z] * kStatWords;  // label 0 of layer z
+    o[0] = mnx; o[1] = mny; o[2] = mxx; o[3] = mxy; o[4] = (int32_t)area; o[5] = (int32_t)first;
+    sums[2 * (size_t)lstart[z]] = sx;
+    sums[2 * (size_t)lstart[z] + 1] = sy;
 }
 
 __global__ __launch_bounds__(256) void k_cc_init_stats(int32_t* st, unsigned long long* sums,
@@ -362,64 +431,81 @@ struct Img {
         if (kLds) return p[i];
         return __hip_atomic_load(p + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+    // 4 pixels at a 4-aligned index
+    __device__ __forceinline__ uint32_t get4(int i) const {
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(p + i);
+        if (kLds) return *q;
+        return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     __device__ __forceinline__ void set(int i, int8_t v) const {
-        if (kLds) p[i] = v;
-        else __hip_atomic_store(p + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (kLds) {
+            p[i] = v;
+        } else {
+            __hip_atomic_store(p + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __threadfence_block();
+        }
+    }
+    __device__ __forceinline__ void zero4(int i) const {
+        uint32_t* q = reinterpret_cast<uint32_t*>(p + i);
+        if (kLds) *q = 0u;
+        else __hip_atomic_store(q, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 };
 
-// non-zero 8-neighbours of pixel i, bit s for code s (zero-ness never changes while marking)
+__device__ __forceinline__ int rdlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ int byte_at(uint32_t w, int k) { return (int)(int8_t)(w >> (8 * k)); }
+
+// The 3x3 neighbourhood of pixel i in ONE lane-parallel read: lane k < 8 reads the neighbour of
+// chain code k, lane 8 the pixel itself.  Returns the non-zero mask of the 8 neighbours (bit s =
+// code s; zero-ness never changes while marking) and the centre value.
 template <bool kLds>
-__device__ __forceinline__ uint32_t nb_mask(const Img<kLds>& im, int i, int Wp) {
-    uint32_t m = 0;
-    m |= (im.get(i + 1) != 0) ? 1u : 0u;
-    m |= (im.get(i - Wp + 1) != 0) ? 2u : 0u;
-    m |= (im.get(i - Wp) != 0) ? 4u : 0u;
-    m |= (im.get(i - Wp - 1) != 0) ? 8u : 0u;
-    m |= (im.get(i - 1) != 0) ? 16u : 0u;
-    m |= (im.get(i + Wp - 1) != 0) ? 32u : 0u;
-    m |= (im.get(i + Wp) != 0) ? 64u : 0u;
-    m |= (im.get(i + Wp + 1) != 0) ? 128u : 0u;
-    return m;
+__device__ __forceinline__ uint32_t nbhd(const Img<kLds>& im, int i, int P, int lane, int& centre) {
+    const int off = lane < 8 ? code_dy(lane) * P + code_dx(lane) : 0;
+    const int v = lane < 9 ? im.get(i + off) : 0;
+    centre = rdlane(v, 8);
+    return (uint32_t)(__ballot(v != 0) & 0xFFu);
 }
 
-// icvFetchContour of an outer border (is_hole = 0, nbd = 2) from padded pixel (x0, y0); writes one
-// chain code per written point (the last one leads back to the start); returns the point count
+// icvFetchContour of an outer border (is_hole = 0, nbd = 2) from padded pixel i0 (row pitch P;
+// wave-uniform control, one LDS read per step); lane 0 writes the marks and one chain code per
+// written point (the last one leads back to the start).  Returns the point count.
 template <bool kLds>
-__device__ uint32_t fetch_outer(const Img<kLds>& im, int Wp, int x0, int y0, uint8_t* codes,
-                                uint64_t cap, uint64_t& cpos, bool& overflow) {
-    const int i0 = y0 * Wp + x0;
-    const uint32_t m0 = nb_mask(im, i0, Wp);
-    // clockwise from code 3 down to 5 (code 4, the scan's zero predecessor, ends the search)
-    int s = -1;
-    for (int k = 3; k >= -3; --k) {
-        const int c = k & 7;
-        if (m0 & (1u << c)) { s = c; break; }
-    }
-    if (s < 0) {  // single point
-        im.set(i0, (int8_t)(2 | -128));
+__device__ __forceinline__ uint32_t fetch_outer(const Img<kLds>& im, int P, int i0, int lane,
+                                                uint8_t* codes, uint64_t cap, uint64_t& cpos,
+                                                bool& overflow) {
+    int c0;
+    const uint32_t m0 = nbhd(im, i0, P, lane, c0);
+    // clockwise from code 3 down to 5 (code 4, the scan's zero predecessor, ends the search):
+    // cw bit k = m0 bit of code (3 - k) & 7 for k = 0..6
+    const uint32_t cw = ((m0 >> 3) & 1u) | ((m0 >> 1) & 2u) | ((m0 << 1) & 4u) | ((m0 << 3) & 8u) |
+                        ((m0 >> 3) & 16u) | ((m0 >> 1) & 32u) | ((m0 << 1) & 64u);
+    if (cw == 0) {  // single point
+        if (lane == 0) im.set(i0, (int8_t)(2 | -128));
         return 1;
     }
-    const int i1 = i0 + code_dy(s) * Wp + code_dx(s);
+    int s = (3 - (int)__builtin_ctz(cw)) & 7;
+    const int i1 = i0 + code_dy(s) * P + code_dx(s);
     int i3 = i0;
     uint32_t npts = 0;
     for (;;) {
         const int s_end = s;
-        const uint32_t m = nb_mask(im, i3, Wp);
-        // counter-clockwise from s_end + 1: first non-zero neighbour
+        int c3;
+        const uint32_t m = nbhd(im, i3, P, lane, c3);
+        // counter-clockwise from s_end + 1: first non-zero neighbour (the previous pixel is one)
         const uint32_t rot = ((m | (m << 8)) >> (s_end + 1)) & 0xFFu;
-        s = (s_end + 1 + (int)__builtin_ctz(rot)) & 7;  // rot != 0: the previous pixel is set
-        const int i4 = i3 + code_dy(s) * Wp + code_dx(s);
-        if ((unsigned)(s - 1) < (unsigned)s_end) im.set(i3, (int8_t)(2 | -128));
-        else if (im.get(i3) == 1) im.set(i3, 2);
+        s = (s_end + 1 + (int)__builtin_ctz(rot)) & 7;
+        const int i4 = i3 + code_dy(s) * P + code_dx(s);
+        if (lane == 0) {
+            if ((unsigned)(s - 1) < (unsigned)s_end) im.set(i3, (int8_t)(2 | -128));
+            else if (c3 == 1) im.set(i3, 2);
+        }
         ++npts;
-        if (cpos < cap) {
-            if ((threadIdx.x & 63) == 0) codes[cpos] = (uint8_t)s;
-            ++cpos;
-        } else {
+        if (cpos >= cap) {
             overflow = true;
             return npts;
         }
+        if (lane == 0) codes[cpos] = (uint8_t)s;
+        ++cpos;
         if (i4 == i0 && i3 == i1) break;
         i3 = i4;
         s = (s + 4) & 7;
@@ -427,105 +513,173 @@ __device__ uint32_t fetch_outer(const Img<kLds>& im, int Wp, int x0, int y0, uin
     return npts;
 }
 
+__host__ __device__ inline int contour_pitch(uint32_t W) { return (int)((W + 2 + 3) & ~3u); }
+__host__ __device__ inline size_t contour_image_bytes(uint32_t W, uint32_t H) {
+    return (size_t)contour_pitch(W) * (H + 2) + (((H + 2) + 3) & ~3u);
+}
+
 // one workgroup per layer (8 waves stage the image, wave 0 scans); rec[4 * d] = {x, y, first
-// code, points} of the d-th DISCOVERED contour.  Image layout (LDS, or the global scratch):
-// Wp x Hp int8 pixels, then Hp row flags (row has a non-zero pixel: an all-zero row holds no
-// transition of the scan and is skipped; marking never makes a zero non-zero).
+// code, points} of the d-th DISCOVERED contour.  Image (LDS, or the global scratch): Hp rows of
+// P = roundup4(W + 2) int8 pixels (zero border), then Hp row flags (row has a non-zero pixel: an
+// all-zero row holds no transition of the scan and is skipped; marking never zeroes a pixel).
 constexpr int kContourThreads = 512;
 template <bool kLds>
 __global__ __launch_bounds__(kContourThreads) void k_cc_contours(
     const uint8_t* __restrict__ grid, uint32_t W, uint32_t H, int8_t* gscratch,
     uint8_t* __restrict__ codes, uint64_t code_cap, uint32_t* __restrict__ rec, uint32_t rec_cap,
-    uint32_t* __restrict__ ncont, uint32_t* __restrict__ err) {
+    uint32_t* __restrict__ ncont, uint32_t* __restrict__ err, unsigned long long* tdbg) {
     extern __shared__ int8_t s_img[];
     const uint32_t z = blockIdx.x;
+    const unsigned long long t_start = wall_clock64();
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int Wp = (int)W + 2, Hp = (int)H + 2;
-    const Img<kLds> im{kLds ? s_img : gscratch + (size_t)z * ((size_t)Wp * Hp + Hp)};
-    const int rowflag = Wp * Hp;
+    const int Wp = (int)W + 2, Hp = (int)H + 2, P = contour_pitch(W);
+    const int total = (int)contour_image_bytes(W, H);
+    const Img<kLds> im{kLds ? s_img : gscratch + (size_t)z * total};
+    const int rowflag = P * Hp;
+    // 1. zero image (with its border) and row flags
+    for (int i = 4 * threadIdx.x; i < total; i += 4 * kContourThreads) im.zero4(i);
+    __syncthreads();
+    // 2. scatter the layer's non-zero cells (binarised: copyMakeBorder + threshold); most 16-byte
+    //    chunks of an occupancy grid are zero and write nothing
     const uint8_t* lay = grid + (size_t)z * W * H;
-    // binarised copy with a zero border (copyMakeBorder + threshold), 8 loads in flight per lane
-    for (int y = wv; y < Hp; y += kContourThreads / 64) {
-        const bool iny = y >= 1 && y <= (int)H;
-        const uint8_t* src = lay + (size_t)(y - 1) * W - 1;
-        bool any = false;
-        for (int x0 = 0; x0 < Wp; x0 += 512) {
-            int8_t v[8];
+    const uint32_t n = W * H;
+    uint32_t done = 0;
+    if ((reinterpret_cast<uintptr_t>(lay) & 15u) == 0) {
+        const uint4* v4 = reinterpret_cast<const uint4*>(lay);
+        const uint32_t n16 = n / 16;
+        for (uint32_t c0 = threadIdx.x; c0 < n16; c0 += 4 * kContourThreads) {
+            uint4 q[4];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const int x = x0 + 64 * k + lane;
-                v[k] = (iny && x >= 1 && x <= (int)W && src[x]) ? 1 : 0;
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t c = c0 + k * kContourThreads;
+                q[k] = c < n16 ? v4[c] : make_uint4(0, 0, 0, 0);
             }
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const int x = x0 + 64 * k + lane;
-                if (x < Wp) im.set(y * Wp + x, v[k]);
-                any |= v[k] != 0;
+            for (int k = 0; k < 4; ++k) {
+                if ((q[k].x | q[k].y | q[k].z | q[k].w) == 0) continue;
+                uint32_t i = (c0 + k * kContourThreads) * 16, y = i / W, x = i - y * W;
+                const uint32_t w4[4] = {q[k].x, q[k].y, q[k].z, q[k].w};
+                for (int b = 0; b < 16; ++b) {
+                    if ((w4[b >> 2] >> (8 * (b & 3))) & 0xFFu) {
+                        im.set((int)(y + 1) * P + (int)x + 1, 1);
+                        im.set(rowflag + (int)y + 1, 1);
+                    }
+                    if (++x == W) {
+                        x = 0;
+                        ++y;
+                    }
+                }
             }
         }
-        const bool nz = __ballot(any) != 0;
-        if (lane == 0) im.set(rowflag + y, nz ? 1 : 0);
+        done = n16 * 16;
     }
+    for (uint32_t i = done + threadIdx.x; i < n; i += kContourThreads)
+        if (lay[i]) {
+            const uint32_t y = i / W, x = i - y * W;
+            im.set((int)(y + 1) * P + (int)x + 1, 1);
+            im.set(rowflag + (int)y + 1, 1);
+        }
     __syncthreads();
     if (wv != 0) return;  // the raster scan is sequential: one wave
+    const unsigned long long t_staged = wall_clock64();
     uint8_t* cz = codes + (size_t)z * code_cap;
     uint32_t* rz = rec + (size_t)z * rec_cap * 4;
     uint64_t cpos = 0;
     uint32_t nc = 0;
     bool overflow = false;
-    for (int y = 1; y < Hp - 1 && !overflow; ++y) {  // cvFindNextContour, mode RETR_EXTERNAL
-        if (!im.get(rowflag + y)) continue;
-        const int rb = y * Wp;
-        int x = 1, prev = 0, lnbd = 0;
-        while (true) {
-            // skip the run of `prev` (64 pixels per ballot)
-            int xn = x;
-            while (xn < Wp - 1) {
-                const int xi = xn + lane;
-                const int v = xi < Wp - 1 ? im.get(rb + xi) : prev;
-                const uint64_t m = __ballot(v != prev);
-                if (m) {
-                    xn += __ffsll((long long)m) - 1;
-                    break;
+    // 3. cvFindNextContour (mode RETR_EXTERNAL) over the non-empty rows, 64 flags per read; a row
+    //    is read 256 pixels per step (4 per lane), its transitions walked in registers
+    for (int yb = 1; yb < Hp - 1 && !overflow; yb += 64) {
+        uint64_t rows = __ballot(yb + lane < Hp - 1 && im.get(rowflag + yb + lane) != 0);
+        while (rows && !overflow) {
+            const int y = yb + (int)__builtin_ctzll(rows);
+            rows &= rows - 1;
+            const int rb = y * P;
+            int x = 1, lnbd = 0, lnbd_val = 0;  // lnbd: the row's last marked run start (0: border)
+            for (int cb = 0; cb < Wp - 1 && !overflow; cb += 256) {
+            reload:
+                const int q = cb + 4 * lane;  // this lane's 4 pixels [q, q + 4)
+                const uint32_t w = q < P ? im.get4(rb + q) : 0u;
+                const uint32_t pw = (q >= 4 && q - 4 < P) ? im.get4(rb + q - 4) : 0u;
+                // transitions of the run skip at positions [x, Wp - 2]: img[X] != img[X - 1]
+                uint64_t T[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int pos = q + k;
+                    const int left = k ? byte_at(w, k - 1) : byte_at(pw, 3);
+                    T[k] = __ballot(pos >= x && pos <= Wp - 2 && byte_at(w, k) != left);
                 }
-                xn += 64;
-            }
-            if (xn >= Wp - 1) break;
-            x = xn;
-            const int p = im.get(rb + x);
-            bool trace = false;
-            if (prev == 0 && p == 1) {
-                trace = im.get(rb + lnbd) <= 0;
-            } else if (p == 0 && prev >= 1) {  // a hole border start: skipped, lnbd moves
-                if (prev & -2) lnbd = x - 1;
-            }
-            if (trace) {
-                if (nc >= rec_cap) {
-                    overflow = true;
-                    break;
+                while (T[0] | T[1] | T[2] | T[3]) {
+                    // the next transition in position order: lane-major, then byte
+                    int best = 1 << 30, bk = 0;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        if (T[k]) {
+                            const int c = 4 * (int)__builtin_ctzll(T[k]) + k;
+                            if (c < best) {
+                                best = c;
+                                bk = k;
+                            }
+                        }
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        if (k == bk) T[k] &= T[k] - 1;
+                    const int X = cb + best, bl = best >> 2;
+                    const uint32_t wl = (uint32_t)rdlane((int)w, bl);
+                    const int p = byte_at(wl, bk);
+                    const int prev = bk ? byte_at(wl, bk - 1) : byte_at((uint32_t)rdlane((int)pw, bl), 3);
+                    if (prev == 0 && p == 1) {
+                        int lv = lnbd_val;
+                        if (lnbd >= cb) {
+                            const int o = lnbd - cb;
+                            lv = byte_at((uint32_t)rdlane((int)w, o >> 2), o & 3);
+                        }
+                        if (lv <= 0) {  // an external border start: trace it
+                            if (nc >= rec_cap) {
+                                overflow = true;
+                                break;
+                            }
+                            const uint64_t c0 = cpos;
+                            const uint32_t np = fetch_outer(im, P, rb + X, lane, cz, code_cap, cpos,
+                                                            overflow);
+                            if (lane == 0) {
+                                rz[4 * nc + 0] = (uint32_t)(X - 1);
+                                rz[4 * nc + 1] = (uint32_t)(y - 1);
+                                rz[4 * nc + 2] = (uint32_t)c0;
+                                rz[4 * nc + 3] = np;
+                            }
+                            ++nc;
+                            if (overflow) break;
+                            // the scan resumes at X + 1 with prev = the marked start (no lnbd
+                            // update); the trace may have re-marked pixels of this row
+                            if (lnbd < cb) lnbd_val = im.get(rb + lnbd);
+                            x = X + 1;
+                            goto reload;
+                        }
+                    } else if (p == 0 && prev >= 1) {  // a hole border start: skipped
+                        if (prev & -2) {
+                            lnbd = X - 1;
+                            lnbd_val = prev;
+                        }
+                    }
+                    if (p & -2) {  // resume: lnbd follows marked runs
+                        lnbd = X;
+                        lnbd_val = p;
+                    }
                 }
-                const uint64_t c0 = cpos;
-                const uint32_t np = fetch_outer(im, Wp, x, y, cz, code_cap, cpos, overflow);
-                if (lane == 0) {
-                    rz[4 * nc + 0] = (uint32_t)(x - 1);
-                    rz[4 * nc + 1] = (uint32_t)(y - 1);
-                    rz[4 * nc + 2] = (uint32_t)c0;
-                    rz[4 * nc + 3] = np;
-                }
-                ++nc;
-                if (overflow) break;
-                prev = im.get(rb + x);  // the scan resumes after the (now marked) start pixel
-                ++x;
-                continue;
+                x = max(x, cb + 256);
             }
-            prev = p;
-            if (prev & -2) lnbd = x;
-            ++x;
         }
     }
     if (lane == 0) {
         ncont[z] = nc;
         if (overflow) atomicOr(err, 1u);
+        if (tdbg) {  // GDF_SEG_DEBUG: phase times (100 MHz wall clock) and chain codes per layer
+            tdbg[4 * z + 0] = t_staged - t_start;
+            tdbg[4 * z + 1] = wall_clock64() - t_staged;
+            tdbg[4 * z + 2] = cpos;
+            tdbg[4 * z + 3] = nc;
+        }
     }
 }
 
@@ -590,11 +744,13 @@ struct SegError {
 struct gdf_segmenter {
     int device = 0;
     hipStream_t own = nullptr, user = nullptr;
+    hipStream_t side = nullptr;  // the contour scan runs here, concurrently with the labelling
+    hipEvent_t ev_ready = nullptr, ev_contours = nullptr;
     hipStream_t s() const { return user ? user : own; }
     uint32_t W = 0, H = 0, L = 0, flags = 0;
     bool have = false;
     GpuBuf par, bits, blabel, nlab, lstart, cstart, labels, st, sums, stats5, cent, l2c, conn;
-    GpuBuf codes, rec, ncont, err, scratch;
+    GpuBuf codes, rec, ncont, err, scratch, bgpart, tdbg;
     uint64_t code_cap = 0;
     uint32_t rec_cap = 0;
     std::vector<uint32_t> h_nlab, h_lstart;
@@ -628,6 +784,60 @@ int seg_guarded(F&& f) {
     }
 }
 
+// findContours of every layer on the segmenter's second stream, ordered after the work already
+// on `s` (the grid producer); g->ev_contours marks its end
+void launch_contours(gdf_segmenter* g, const uint8_t* grid, uint32_t W, uint32_t H, uint32_t L,
+                     hipStream_t s) {
+    const hipStream_t s2 = g->side;
+    SEGCHK(hipEventRecord(g->ev_ready, s));
+    SEGCHK(hipStreamWaitEvent(s2, g->ev_ready, 0));
+    const uint64_t img = contour_image_bytes(W, H);  // pixels (pitch roundup4(W + 2)) + row flags
+    g->rec_cap = (uint32_t)(((uint64_t)(W + 1) / 2) * H + 1);
+    g->code_cap = 8ull * W * H + 64;
+    SEGCHK(g->codes.ensure(g->code_cap * L));
+    SEGCHK(g->rec.ensure((size_t)g->rec_cap * 16 * L));
+    SEGCHK(g->ncont.ensure((size_t)L * 4));
+    SEGCHK(g->err.ensure(4));
+    SEGCHK(hipMemsetAsync(g->err.p, 0, 4, s2));
+    unsigned long long* tdbg = nullptr;
+    static const bool dbg = std::getenv("GDF_SEG_DEBUG") != nullptr;
+    if (dbg) {
+        SEGCHK(g->tdbg.ensure((size_t)L * 32));
+        tdbg = g->tdbg.as<unsigned long long>();
+    }
+    bool lds = img <= kLdsMax;
+    if (lds) {
+        static bool attr_set = false;
+        if (!attr_set) {
+            lds = hipFuncSetAttribute((const void*)k_cc_contours<true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)kLdsMax) == hipSuccess;
+            attr_set = lds;
+        }
+    }
+    if (lds) {
+        hipLaunchKernelGGL(k_cc_contours<true>, dim3(L), dim3(kContourThreads), (size_t)img, s2, grid, W, H,
+                           nullptr, g->codes.as<uint8_t>(), g->code_cap, g->rec.as<uint32_t>(),
+                           g->rec_cap, g->ncont.as<uint32_t>(), g->err.as<uint32_t>(), tdbg);
+    } else {
+        SEGCHK(g->scratch.ensure(img * L));
+        hipLaunchKernelGGL(k_cc_contours<false>, dim3(L), dim3(kContourThreads), 0, s2, grid, W, H,
+                           g->scratch.as<int8_t>(), g->codes.as<uint8_t>(), g->code_cap,
+                           g->rec.as<uint32_t>(), g->rec_cap, g->ncont.as<uint32_t>(),
+                           g->err.as<uint32_t>(), tdbg);
+    }
+    if (dbg) {
+        std::vector<unsigned long long> h((size_t)L * 4);
+        SEGCHK(hipMemcpyAsync(h.data(), tdbg, h.size() * 8, hipMemcpyDeviceToHost, s2));
+        SEGCHK(hipStreamSynchronize(s2));
+        for (uint32_t z = 0; z < L; ++z)
+            std::fprintf(stderr, "seg contours layer %u: stage %.1f us, scan+trace %.1f us, %llu codes, %llu contours\n",
+                         z, h[4 * z] / 100.0, h[4 * z + 1] / 100.0, h[4 * z + 2], h[4 * z + 3]);
+    }
+    SEGCHK(hipGetLastError());
+    SEGCHK(hipEventRecord(g->ev_contours, s2));
+}
+
 void run_label_layers(gdf_segmenter* g, const uint8_t* grid, uint32_t W, uint32_t H, uint32_t L,
                       uint32_t flags, hipStream_t s) {
     if (!grid || W == 0 || H == 0 || L == 0) seg_fail(GDF_ERR_ARG, "empty grid");
@@ -641,6 +851,7 @@ void run_label_layers(gdf_segmenter* g, const uint8_t* grid, uint32_t W, uint32_
     SEGCHK(g->bits.ensure(nb));
     SEGCHK(g->blabel.ensure(nb * 4));
     SEGCHK(g->nlab.ensure((size_t)L * 4));
+    if (flags & GDF_SEG_CONTOURS) launch_contours(g, grid, W, H, L, s);
     const dim3 tiles((BW + kTile - 1) / kTile, (BH + kTile - 1) / kTile, L);
     hipLaunchKernelGGL(k_cc_local, tiles, dim3(256), 0, s, grid, W, H, BW, BH,
                        g->par.as<uint32_t>(), g->bits.as<uint8_t>());
@@ -691,43 +902,24 @@ void run_label_layers(gdf_segmenter* g, const uint8_t* grid, uint32_t W, uint32_
               g->blabel.as<const uint32_t>(), g->lstart.as<const uint32_t>(),
               g->nlab.as<const uint32_t>(), g->cstart.as<const uint64_t>(),
               g->labels.as<uint16_t>(), g->st.as<int32_t>(), g->sums.as<unsigned long long>(),
-              g->conn.as<uint8_t>(), do_conn ? 1 : 0};
-    hipLaunchKernelGGL(k_cc_pixels, dim3((W + 63) / 64, (H + kRowsPerWave - 1) / kRowsPerWave, L),
-                       dim3(64), 0, s, a);
+              g->conn.as<uint8_t>(), do_conn ? 1 : 0, nullptr};
+    const dim3 pgrid((W + 63) / 64, (H + kRowsPerWave - 1) / kRowsPerWave, L);
+    const uint32_t wpl = pgrid.x * pgrid.y;
+    SEGCHK(g->bgpart.ensure((size_t)wpl * L * kBgWords * 8));
+    a.bgpart = g->bgpart.as<unsigned long long>();
+    hipLaunchKernelGGL(k_cc_pixels, pgrid, dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_cc_bg_reduce, dim3(L), dim3(256), 0, s,
+                       g->bgpart.as<const unsigned long long>(), wpl,
+                       g->lstart.as<const uint32_t>(), g->st.as<int32_t>(),
+                       g->sums.as<unsigned long long>());
     hipLaunchKernelGGL(k_cc_finish, dim3(tb), dim3(256), 0, s, g->st.as<const int32_t>(),
                        g->sums.as<const unsigned long long>(), (uint32_t)T,
                        g->stats5.as<int32_t>(), g->cent.as<double>(), g->l2c.as<int32_t>());
     SEGCHK(hipGetLastError());
     if (flags & GDF_SEG_CONTOURS) {
-        const uint64_t Wp = W + 2, Hp = H + 2, img = Wp * Hp + Hp;  // + row flags
-        g->rec_cap = (uint32_t)(((uint64_t)(W + 1) / 2) * H + 1);
-        g->code_cap = 8ull * W * H + 64;
-        SEGCHK(g->codes.ensure(g->code_cap * L));
-        SEGCHK(g->rec.ensure((size_t)g->rec_cap * 16 * L));
-        SEGCHK(g->ncont.ensure((size_t)L * 4));
-        SEGCHK(g->err.ensure(4));
-        SEGCHK(hipMemsetAsync(g->err.p, 0, 4, s));
-        bool lds = img <= kLdsMax;
-        if (lds) {
-            static bool attr_set = false;
-            if (!attr_set) {
-                lds = hipFuncSetAttribute((const void*)k_cc_contours<true>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize,
-                                          (int)kLdsMax) == hipSuccess;
-                attr_set = lds;
-            }
-        }
-        if (lds) {
-            hipLaunchKernelGGL(k_cc_contours<true>, dim3(L), dim3(kContourThreads), (size_t)img, s, grid, W, H,
-                               nullptr, g->codes.as<uint8_t>(), g->code_cap, g->rec.as<uint32_t>(),
-                               g->rec_cap, g->ncont.as<uint32_t>(), g->err.as<uint32_t>());
-        } else {
-            SEGCHK(g->scratch.ensure(img * L));
-            hipLaunchKernelGGL(k_cc_contours<false>, dim3(L), dim3(kContourThreads), 0, s, grid, W, H,
-                               g->scratch.as<int8_t>(), g->codes.as<uint8_t>(), g->code_cap,
-                               g->rec.as<uint32_t>(), g->rec_cap, g->ncont.as<uint32_t>(),
-                               g->err.as<uint32_t>());
-        }
+        // the contour scan (one workgroup per layer, the longest kernel) ran concurrently on the
+        // second stream since the start of this call
+        SEGCHK(hipStreamWaitEvent(s, g->ev_contours, 0));
         hipLaunchKernelGGL(k_cc_l2c, dim3(L), dim3(256), 0, s, g->rec.as<const uint32_t>(),
                            g->rec_cap, g->ncont.as<const uint32_t>(),
                            g->labels.as<const uint16_t>(), W, H, g->lstart.as<const uint32_t>(),
@@ -799,6 +991,9 @@ int gdf_seg_create(int device, gdf_segmenter** out) {
         auto* g = new gdf_segmenter();
         g->device = device;
         hipError_t e = hipStreamCreateWithFlags(&g->own, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&g->side, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&g->ev_ready, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&g->ev_contours, hipEventDisableTiming);
         if (e != hipSuccess) {
             delete g;
             SEGCHK(e);
@@ -811,7 +1006,11 @@ int gdf_seg_destroy(gdf_segmenter* g) {
     if (!g) return GDF_OK;
     (void)hipSetDevice(g->device);
     (void)hipStreamSynchronize(g->s());
+    if (g->side) (void)hipStreamSynchronize(g->side);
     if (g->own) (void)hipStreamDestroy(g->own);
+    if (g->side) (void)hipStreamDestroy(g->side);
+    if (g->ev_ready) (void)hipEventDestroy(g->ev_ready);
+    if (g->ev_contours) (void)hipEventDestroy(g->ev_contours);
     delete g;
     return GDF_OK;
 }

@@ -173,6 +173,8 @@ int main(int argc, char** argv) {
             m_fusion->voxelOccupancyGrid(lifetime);
             glMemoryBarrier(GL_ALL_BARRIER_BITS);
             m_fusion->downloadVoxelOccupancyGrid();
+            glMemoryBarrier(GL_ALL_BARRIER_BITS);
+            m_fusion->objectSegmentation();  // component.cpp:313-316 (front end + label merge)
         }
         const std::string s = std::to_string(f);
         write_bin(out + "/points" + s + ".bin", reinterpret_cast<const float*>(m_fusion->m_points.data()),
@@ -188,6 +190,30 @@ int main(int argc, char** argv) {
         write_bin(out + "/voxelized" + s + ".bin", vox.data(), vox.size());
         write_bin(out + "/grid" + s + ".bin", m_fusion->m_occupancyGrid.data(),
                   m_fusion->m_occupancyGrid.size());
+        uint32_t gs[3];
+        uint64_t cells = 0;
+        if (gdf_get_grid_size(m_fusion->handle(), gs, &cells) == GDF_OK) {
+            FILE* fh = std::fopen((out + "/gridsize" + s + ".txt").c_str(), "w");
+            std::fprintf(fh, "%u %u %u\n", gs[0], gs[1], gs[2]);
+            std::fclose(fh);
+        }
+        write_bin(out + "/labels" + s + ".bin", m_fusion->m_ccLabeledLayersData.data(),
+                  m_fusion->m_ccLabeledLayersData.size());
+        write_bin(out + "/stats" + s + ".bin", m_fusion->m_ccStatsData.data(),
+                  m_fusion->m_ccStatsData.size());
+        write_bin(out + "/merged" + s + ".bin", m_fusion->m_ccLabelsMerged.data(),
+                  m_fusion->m_ccLabelsMerged.size());
+        std::vector<int32_t> l2c;
+        for (const auto& v : m_fusion->m_labelsToContoursPerLayer) l2c.insert(l2c.end(), v.begin(), v.end());
+        write_bin(out + "/l2c" + s + ".bin", l2c.data(), l2c.size());
+        std::vector<int32_t> cpts;
+        for (const auto& layer : m_fusion->m_contoursPerLayer)
+            for (const auto& c : layer)
+                for (const auto& p : c) {
+                    cpts.push_back(p.x);
+                    cpts.push_back(p.y);
+                }
+        write_bin(out + "/contours" + s + ".bin", cpts.data(), cpts.size());
         std::printf("frame %d: %d points, %zu voxels, rollbuffer %u points\n", f,
                     m_fusion->m_numPoints, m_fusion->m_points_voxelized.size(),
                     m_fusion->m_rollBufferNumPoints);

@@ -1,7 +1,8 @@
 """The C++ facade (include/gdf_fusion.hpp) driven on the GPU in the reference component's exact
 call order (tests/facade_component.cpp, component.cpp:92-300): m_points, m_voxelCoords,
 m_points_voxelized and m_occupancyGrid after each of three frames (depth map + point sequence)
-equal the oracle's outputs committed in tests/golden/facade bit for bit."""
+equal the oracle's outputs committed in tests/golden/facade bit for bit, and objectSegmentation's
+labels / stats / contours / merged labels equal the oracle's on that grid."""
 import os
 import subprocess
 
@@ -38,3 +39,13 @@ def test_facade_component_sequence_on_gpu(tmp_path, gpu_engine_factory):
             want = np.fromfile(os.path.join(FIX, f"{name}{f}.bin"), dt)
             got = np.fromfile(outd / f"{name}{f}.bin", dt)
             assert len(want) > 0 and np.array_equal(got, want), f"frame {f} {name}"
+        # objectSegmentation front end (labelVoxels + mergeLabelsAcrossLayers) on that grid
+        import oracle
+        gx, gy, gz = (int(v) for v in open(outd / f"gridsize{f}.txt").read().split())
+        grid = np.fromfile(os.path.join(FIX, f"grid{f}.bin"), "u1").reshape(gz, gy, gx)
+        o = oracle.object_segmentation_front(grid)
+        for name, dt, key in (("labels", "<u2", "labels"), ("stats", "<i4", "stats"),
+                              ("merged", "<u4", "merged"), ("l2c", "<i4", "labels_to_contours"),
+                              ("contours", "<i4", "contour_points")):
+            got = np.fromfile(outd / f"{name}{f}.bin", dt)
+            assert np.array_equal(got, o[key].reshape(-1)), f"frame {f} {name}"

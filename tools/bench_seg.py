@@ -16,22 +16,18 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--frames", type=int, default=16)
-    ap.add_argument("--reps", type=int, default=50)
-    ap.add_argument("--cameras", type=int, default=4)
-    ap.add_argument("--json", default=None)
-    a = ap.parse_args()
+def run_seg(frames=16, reps=50, cameras=4, cpu=True):
+    """The segmentation front end on the C2-style grid: ms per call for the label/stat pass, with
+    the connection matrices, and with contours; the oracle's single-thread CPU time beside it."""
     import torch
     from ros_gpu_depthmap_fusion_amd import build_library, synth
     from ros_gpu_depthmap_fusion_amd.gdf import ComponentParams, GPUDepthmapFusion, Segmenter
     build_library()
     eng = GPUDepthmapFusion(0)
     p = ComponentParams()
-    for f in range(a.frames):
+    for f in range(frames):
         eng.clear()
-        for k in range(a.cameras):
+        for k in range(cameras):
             cam = synth.make_camera(k, 640, 480)
             eng.addDepthmap(synth.dense_frame(cam, f, k), *cam.intrinsics(), cam.T_world,
                             cam.T_crop)
@@ -39,7 +35,7 @@ def main():
     grid = eng.downloadVoxelOccupancyGrid()
     gs, nc = eng.grid_size()
     seg = Segmenter(0)
-    out = {"workload": f"occupancy grid after {a.frames} frames of {a.cameras} dense VGA cameras "
+    out = {"workload": f"occupancy grid after {frames} frames of {cameras} dense VGA cameras "
                        f"(launch defaults, grid {gs[0]}x{gs[1]}x{gs[2]})",
            "occupied_cells": int((grid > 0).sum())}
     for name, flags in (("labels_stats", 0), ("labels_stats_connections", 2), ("all", 3)):
@@ -47,10 +43,10 @@ def main():
             seg.label_engine_grid(eng, flags)
             torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(a.reps):
+        for _ in range(reps):
             seg.label_engine_grid(eng, flags)
         torch.cuda.synchronize()
-        out[f"ms_{name}"] = round((time.perf_counter() - t0) / a.reps * 1e3, 4)
+        out[f"ms_{name}"] = round((time.perf_counter() - t0) / reps * 1e3, 4)
     t0 = time.perf_counter()
     r = seg.results()
     out["ms_download_and_merge"] = round((time.perf_counter() - t0) * 1e3, 3)
@@ -58,15 +54,30 @@ def main():
     out.update(total_labels=int(c.total_labels), contours=int(c.total_contours),
                contour_points=int(c.total_contour_points),
                connection_bytes=int(c.connection_bytes), objects=int(r["num_objects"]))
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle  # the checker / CPU baseline only
-    g3 = grid.reshape(gs[2], gs[1], gs[0])
-    t0 = time.perf_counter()
-    o = oracle.object_segmentation_front(g3)
-    out["cpu_oracle_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
-    same = all(np.array_equal(np.nan_to_num(np.asarray(r[k])), np.nan_to_num(np.asarray(o[k])))
-               for k in r)
-    out["bit_exact_vs_oracle"] = bool(same)
+    if cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle  # the checker / CPU baseline only
+        g3 = grid.reshape(gs[2], gs[1], gs[0])
+        t0 = time.perf_counter()
+        o = oracle.object_segmentation_front(g3)
+        out["cpu_baseline"] = {"ms": round((time.perf_counter() - t0) * 1e3, 3), "threads": 1,
+                               "kind": "port", "sample": "the same grid through oracle/seg_oracle.c"}
+        same = all(np.array_equal(np.nan_to_num(np.asarray(r[k])),
+                                  np.nan_to_num(np.asarray(o[k]))) for k in r)
+        out["bit_exact_vs_oracle"] = bool(same)
+    seg.close()
+    eng.close()
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=16)
+    ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--cameras", type=int, default=4)
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    out = run_seg(a.frames, a.reps, a.cameras)
     line = json.dumps(out)
     print(line)
     if a.json:
