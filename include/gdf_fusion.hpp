@@ -283,11 +283,23 @@ public:
             }
         m_ccNumObjects = nobj;
     }
-    // objectSegmentation (:2552-2575) up to the merged labels; createCCObjects and the tracking
-    // that consume them stay out of scope
+    // createCCObjects (:2364-2550) without the OpenCV shapes: the objects' aggregate fields and
+    // their components (global label indices, grouped)
+    void createCCObjects() {
+        uint32_t n = 0;
+        check(gdf_seg_create_objects(seg_, lo_, cs_, nullptr, 0, nullptr, 0, &n));
+        m_ccObjects.resize(n);
+        m_ccObjectComponents.resize(m_ccLabelsMerged.size());
+        check(gdf_seg_create_objects(seg_, lo_, cs_, m_ccObjects.data(), n,
+                                     m_ccObjectComponents.data(),
+                                     (uint32_t)m_ccObjectComponents.size(), &n));
+    }
+    // objectSegmentation (:2552-2575); the shapes and objectTracking stay out of scope
+    // 
     void objectSegmentation() {
         labelVoxels();
         mergeLabelsAcrossLayers();
+        createCCObjects();
     }
 
     gdf_rollbuffer_state rollbufferState() {
@@ -327,6 +339,8 @@ public:
     std::vector<uint64_t> m_ccLayersConnectionsDataStarts;
     std::vector<uint32_t> m_ccLabelsMerged, m_ccLabelsLayer, m_ccLabelsLocal, m_ccLabelsLayerStarts;
     uint32_t m_ccNumObjects = 0;
+    std::vector<gdf_cc_object> m_ccObjects;
+    std::vector<uint32_t> m_ccObjectComponents;
 
 private:
     void syncRollbuffer() {

@@ -6,7 +6,8 @@
  * reference), uploadVoxelLabels (:2013-2073), prepareLayersConnections (:2075-2151),
  * computeLayersConnections (:2200-2214, shader/layers_connections.glsl:96-122) and
  * downloadLayersConnections (:2215-2241), plus mergeLabelsAcrossLayers (:2243-2361, host).
- * createCCObjects / objectTracking (:2364-2944) stay out of scope.
+ * createCCObjects (:2364-2550) without its OpenCV shapes, and objectTracking (:2727-2944), stay out
+ * of scope; gdf_seg_create_objects gives the objects' aggregate fields.
  *
  * Input: a device u8 occupancy grid of `layers` z-layers of height x width cells, x fastest
  * (m_occupancyGrid; layer i is the cv::Mat_<uint8_t>(height, width) view m_occupancyLayers[i],
@@ -82,6 +83,24 @@ int gdf_seg_download_contours(gdf_segmenter* seg, int32_t* labels_to_contours,
  * as in m_ccLabelsMergedGrouper); needs GDF_SEG_CONNECTIONS */
 int gdf_seg_merge_labels(gdf_segmenter* seg, uint32_t* merged, uint32_t capacity,
                          uint32_t* num_objects);
+/* createCCObjects (fusion.cpp:2364-2550) without the OpenCV shapes (minAreaRect /
+ * minEnclosingCircle of the contours, SURVEY §8(f) rank 4, out of scope): one record per merged
+ * object, in merged-label order (background objects included, as m_ccObjects), with the
+ * reference's float/int arithmetic; `components` receives every object's global label indices in
+ * grouped order (UIntGrouper: ascending index), object i's at [first_component,
+ * first_component + num_components).  lower / cell_size: the grid's GridMeta lower bound and
+ * cell size (voxelCoordToWorldCoord, fusion.cpp:1720-1730).  Needs gdf_seg_merge_labels' inputs
+ * (GDF_SEG_CONNECTIONS) and GDF_SEG_CONTOURS for the contour point counts. */
+typedef struct gdf_cc_object {
+    uint32_t label, num_components, num_layers, first_component;
+    float centroid[2];                        /* mean of the components' centroids (cv::Point2f) */
+    int32_t min_voxel[3], max_voxel[3], aabb_voxel[3];
+    float center_voxel[3], center_world[3], min_world[3], max_world[3], aabb_world[3];
+    uint32_t num_contour_points;              /* points of the components' external contours */
+} gdf_cc_object;
+int gdf_seg_create_objects(gdf_segmenter* seg, const float lower[3], const float cell_size[3],
+                           gdf_cc_object* objects, uint32_t capacity, uint32_t* components,
+                           uint32_t components_capacity, uint32_t* num_objects);
 /* device pointers of the results (valid until the next gdf_seg_label_*) */
 int gdf_seg_get_device_results(gdf_segmenter* seg, const uint16_t** labels, const int32_t** stats5,
                                const double** centroids2, const uint8_t** connections);

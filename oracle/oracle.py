@@ -410,3 +410,74 @@ def object_segmentation_front(grid: np.ndarray) -> dict:
         return r
     finally:
         lib.orc_seg_free(h)
+
+
+def create_cc_objects(front: dict, lower, cell_size):
+    """createCCObjects (src/gpu_depthmap_fusion.cpp:2364-2550) without the OpenCV shapes, from the
+    result of object_segmentation_front: per merged object (UIntGrouper order) the reference's
+    float / int arithmetic - centroid += (double) x / num_components into a cv::Point2f (:2409),
+    min / max voxel coords from the stats (:2397-2418), center = vec3(max + min) * 0.5f (:2421),
+    voxelCoordToWorldCoord x * cs + lb in f32 (:1720-1730), aabb and num_layers (:2427-2430),
+    and the contour points of the components (:2439-2460).  Returns (columns, components)."""
+    f32 = np.float32
+    merged = front["merged"].astype(np.int64)
+    nl = front["num_labels"].astype(np.int64)
+    layer = np.repeat(np.arange(len(nl)), nl)
+    order = np.argsort(merged, kind="stable")
+    n = int(front["num_objects"])
+    sizes_by_layer, q = [], 0
+    for z, c in enumerate(front["contours_per_layer"].astype(int)):
+        sizes_by_layer.append(front["contour_sizes"][q:q + c])
+        q += c
+    lo = [f32(v) for v in lower]
+    cs = [f32(v) for v in cell_size]
+
+    def world(v):
+        return [f32(f32(v[d]) * cs[d]) + lo[d] for d in range(3)]
+
+    cols = {k: [] for k in ("label", "num_components", "num_layers", "first_component",
+                            "centroid", "min_voxel", "max_voxel", "aabb_voxel", "center_voxel",
+                            "center_world", "min_world", "max_world", "aabb_world",
+                            "num_contour_points")}
+    first = 0
+    for i in range(n):
+        idxs = order[first:first + int(np.count_nonzero(merged == i))]
+        nc = len(idxs)
+        cx = cy = f32(0.0)
+        mn, mx, pts = [0, 0, 0], [0, 0, 0], 0
+        for k, idx in enumerate(idxs):
+            left, top, w, h, _ = (int(v) for v in front["stats"][idx])
+            x, y = (float(v) for v in front["centroids"][idx])
+            z = int(layer[idx])
+            cx = f32(float(cx) + x / nc)
+            cy = f32(float(cy) + y / nc)
+            for d, lo_v, hi_v in ((0, left, left + w), (1, top, top + h), (2, z, z)):
+                if k == 0 or lo_v < mn[d]:
+                    mn[d] = lo_v
+                if k == 0 or hi_v > mx[d]:
+                    mx[d] = hi_v
+            c = int(front["labels_to_contours"][idx])
+            if c >= 0:
+                pts += int(sizes_by_layer[z][c])
+        center = [f32(f32(mx[d] + mn[d]) * f32(0.5)) for d in range(3)]
+        mnw, mxw = world(mn), world(mx)
+        cols["label"].append(i)
+        cols["num_components"].append(nc)
+        cols["num_layers"].append(1 + mx[2] - mn[2])
+        cols["first_component"].append(first)
+        cols["centroid"].append([cx, cy])
+        cols["min_voxel"].append(mn)
+        cols["max_voxel"].append(mx)
+        cols["aabb_voxel"].append([mx[d] - mn[d] for d in range(3)])
+        cols["center_voxel"].append(center)
+        cols["center_world"].append(world(center))
+        cols["min_world"].append(mnw)
+        cols["max_world"].append(mxw)
+        cols["aabb_world"].append([f32(mxw[d] - mnw[d]) for d in range(3)])
+        cols["num_contour_points"].append(pts)
+        first += nc
+    dt = {"centroid": np.float32, "center_voxel": np.float32, "center_world": np.float32,
+          "min_world": np.float32, "max_world": np.float32, "aabb_world": np.float32,
+          "min_voxel": np.int32, "max_voxel": np.int32, "aabb_voxel": np.int32}
+    out = {k: np.array(v, dtype=dt.get(k, np.uint32)) for k, v in cols.items()}
+    return out, order.astype(np.uint32)

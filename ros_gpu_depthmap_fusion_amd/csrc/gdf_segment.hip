@@ -1161,15 +1161,15 @@ int gdf_seg_download_contours(gdf_segmenter* g, int32_t* l2c, uint32_t* per_laye
     });
 }
 
+}  // extern "C"
+
+namespace {
+
 // mergeLabelsAcrossLayers (fusion.cpp:2243-2361): bottom-up then top-down min propagation of the
 // sequential global labels over the connection matrices (background only with background), then
 // UIntGrouper order: merged id = rank of the propagated id among the distinct ones.
-int gdf_seg_merge_labels(gdf_segmenter* g, uint32_t* merged, uint32_t cap, uint32_t* nobj) {
-    if (!g) return GDF_ERR_ARG;
-    return seg_guarded([&] {
-        need_result(g);
-        if (!(g->flags & GDF_SEG_CONNECTIONS)) seg_fail(GDF_ERR_STATE, "connections were not requested");
-        if (merged && cap < g->total) seg_fail(GDF_ERR_CAPACITY, "merged capacity too small");
+uint32_t merge_labels(gdf_segmenter* g, uint32_t* merged) {
+    {
         std::vector<uint8_t> conn(g->conn_bytes);
         if (g->conn_bytes) {
             SEGCHK(hipMemcpyAsync(conn.data(), g->conn.p, g->conn_bytes, hipMemcpyDeviceToHost, g->s()));
@@ -1204,9 +1204,117 @@ int gdf_seg_merge_labels(gdf_segmenter* g, uint32_t* merged, uint32_t cap, uint3
         uint32_t next = 0;
         for (uint32_t v = 0; v < g->total; ++v)
             if (rank[v] == 0) rank[v] = next++;
-        if (merged)
-            for (uint32_t k = 0; k < g->total; ++k) merged[k] = rank[gl[k]];
-        if (nobj) *nobj = next;
+        for (uint32_t k = 0; k < g->total; ++k) merged[k] = rank[gl[k]];
+        return next;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int gdf_seg_merge_labels(gdf_segmenter* g, uint32_t* merged, uint32_t cap, uint32_t* nobj) {
+    if (!g) return GDF_ERR_ARG;
+    return seg_guarded([&] {
+        need_result(g);
+        if (!(g->flags & GDF_SEG_CONNECTIONS)) seg_fail(GDF_ERR_STATE, "connections were not requested");
+        if (merged && cap < g->total) seg_fail(GDF_ERR_CAPACITY, "merged capacity too small");
+        std::vector<uint32_t> m(g->total);
+        const uint32_t n = merge_labels(g, m.data());
+        if (merged) std::copy(m.begin(), m.end(), merged);
+        if (nobj) *nobj = n;
+    });
+}
+
+int gdf_seg_create_objects(gdf_segmenter* g, const float lower[3], const float cs[3],
+                           gdf_cc_object* objs, uint32_t cap, uint32_t* comps, uint32_t comps_cap,
+                           uint32_t* nobj) {
+    if (!g || !lower || !cs) return GDF_ERR_ARG;
+    return seg_guarded([&] {
+        need_result(g);
+        if (!(g->flags & GDF_SEG_CONNECTIONS)) seg_fail(GDF_ERR_STATE, "connections were not requested");
+        const uint32_t T = g->total;
+        std::vector<uint32_t> merged(T);
+        const uint32_t n = merge_labels(g, merged.data());
+        if (nobj) *nobj = n;
+        if (!objs && !comps) return;
+        if (objs && cap < n) seg_fail(GDF_ERR_CAPACITY, "objects capacity too small");
+        if (comps && comps_cap < T) seg_fail(GDF_ERR_CAPACITY, "components capacity too small");
+        std::vector<int32_t> st((size_t)T * 5);
+        std::vector<double> ce((size_t)T * 2);
+        SEGCHK(hipMemcpyAsync(st.data(), g->stats5.p, (size_t)T * 20, hipMemcpyDeviceToHost, g->s()));
+        SEGCHK(hipMemcpyAsync(ce.data(), g->cent.p, (size_t)T * 16, hipMemcpyDeviceToHost, g->s()));
+        std::vector<int32_t> l2c(T, -1);
+        if (g->flags & GDF_SEG_CONTOURS) {
+            read_contours(g);
+            SEGCHK(hipMemcpyAsync(l2c.data(), g->l2c.p, (size_t)T * 4, hipMemcpyDeviceToHost, g->s()));
+        }
+        SEGCHK(hipStreamSynchronize(g->s()));
+        // contour sizes in findContours order, per layer
+        std::vector<std::vector<uint32_t>> csize(g->L);
+        if (g->flags & GDF_SEG_CONTOURS)
+            for (uint32_t z = 0; z < g->L; ++z) {
+                const uint32_t nc = g->h_ncont[z];
+                const uint32_t* r = g->h_rec.data() + (size_t)z * g->rec_cap * 4;
+                for (uint32_t j = 0; j < nc; ++j) csize[z].push_back(r[4 * (nc - 1 - j) + 3]);
+            }
+        std::vector<uint32_t> layer(T), local(T);
+        for (uint32_t z = 0, t = 0; z < g->L; ++z)
+            for (uint32_t k = 0; k < g->h_nlab[z]; ++k, ++t) {
+                layer[t] = z;
+                local[t] = k;
+            }
+        // UIntGrouper over the merged ids: stable counting sort
+        std::vector<uint32_t> start(n + 1, 0), order(T);
+        for (uint32_t k = 0; k < T; ++k) ++start[merged[k] + 1];
+        for (uint32_t i = 0; i < n; ++i) start[i + 1] += start[i];
+        {
+            std::vector<uint32_t> ptr(start.begin(), start.end() - 1);
+            for (uint32_t k = 0; k < T; ++k) order[ptr[merged[k]]++] = k;
+        }
+        if (comps) std::copy(order.begin(), order.end(), comps);
+        if (!objs) return;
+        auto world = [&](float x, float y, float z, float* o) {  // voxelCoordToWorldCoord
+            o[0] = x * cs[0] + lower[0];
+            o[1] = y * cs[1] + lower[1];
+            o[2] = z * cs[2] + lower[2];
+        };
+        for (uint32_t i = 0; i < n; ++i) {
+            gdf_cc_object& ob = objs[i];
+            std::memset(&ob, 0, sizeof(ob));
+            const uint32_t nc = start[i + 1] - start[i];
+            ob.num_components = nc;
+            ob.first_component = start[i];
+            ob.label = merged[order[start[i]]];
+            float cx = 0.0f, cy = 0.0f;  // cv::Point2f += double / uint
+            for (uint32_t k = 0; k < nc; ++k) {
+                const uint32_t idx = order[start[i] + k], z = layer[idx];
+                const int32_t* sr = st.data() + 5 * (size_t)idx;
+                const double x = ce[2 * (size_t)idx], y = ce[2 * (size_t)idx + 1];
+                const int32_t right = sr[0] + sr[2], bottom = sr[1] + sr[3];
+                cx = (float)((double)cx + x / nc);
+                cy = (float)((double)cy + y / nc);
+                if (k == 0 || sr[0] < ob.min_voxel[0]) ob.min_voxel[0] = sr[0];
+                if (k == 0 || sr[1] < ob.min_voxel[1]) ob.min_voxel[1] = sr[1];
+                if (k == 0 || z < (uint32_t)ob.min_voxel[2]) ob.min_voxel[2] = (int32_t)z;
+                if (k == 0 || right > ob.max_voxel[0]) ob.max_voxel[0] = right;
+                if (k == 0 || bottom > ob.max_voxel[1]) ob.max_voxel[1] = bottom;
+                if (k == 0 || z > (uint32_t)ob.max_voxel[2]) ob.max_voxel[2] = (int32_t)z;
+                const int32_t c = l2c[idx];
+                if (c >= 0) ob.num_contour_points += csize[z][(size_t)c];
+            }
+            ob.centroid[0] = cx;
+            ob.centroid[1] = cy;
+            for (int d = 0; d < 3; ++d) {
+                ob.center_voxel[d] = (float)(ob.max_voxel[d] + ob.min_voxel[d]) * 0.5f;
+                ob.aabb_voxel[d] = ob.max_voxel[d] - ob.min_voxel[d];
+            }
+            world(ob.center_voxel[0], ob.center_voxel[1], ob.center_voxel[2], ob.center_world);
+            world((float)ob.min_voxel[0], (float)ob.min_voxel[1], (float)ob.min_voxel[2], ob.min_world);
+            world((float)ob.max_voxel[0], (float)ob.max_voxel[1], (float)ob.max_voxel[2], ob.max_world);
+            for (int d = 0; d < 3; ++d) ob.aabb_world[d] = ob.max_world[d] - ob.min_world[d];
+            ob.num_layers = (uint32_t)(1 + ob.aabb_voxel[2]);
+        }
     });
 }
 

@@ -81,6 +81,24 @@ class SegCounts(C.Structure):
                 ("total_contour_points", C.c_uint64), ("connection_bytes", C.c_uint64)]
 
 
+class CCObject(C.Structure):
+    """gdf_cc_object (include/gdf_segment.h): createCCObjects' aggregate fields."""
+    _fields_ = [("label", C.c_uint32), ("num_components", C.c_uint32),
+                ("num_layers", C.c_uint32), ("first_component", C.c_uint32),
+                ("centroid", C.c_float * 2), ("min_voxel", C.c_int32 * 3),
+                ("max_voxel", C.c_int32 * 3), ("aabb_voxel", C.c_int32 * 3),
+                ("center_voxel", C.c_float * 3), ("center_world", C.c_float * 3),
+                ("min_world", C.c_float * 3), ("max_world", C.c_float * 3),
+                ("aabb_world", C.c_float * 3), ("num_contour_points", C.c_uint32)]
+
+
+def cc_objects_as_dict(objs) -> dict:
+    """Columns of a CCObject array (the layout oracle.create_cc_objects returns)."""
+    names = [n for n, _ in CCObject._fields_]
+    return {n: np.array([np.ctypeslib.as_array(getattr(o, n)) if hasattr(getattr(o, n), "_length_")
+                         else getattr(o, n) for o in objs]) for n in names}
+
+
 class GDFError(RuntimeError):
     def __init__(self, status: int, msg: str):
         super().__init__(f"{STATUS_NAMES.get(status, status)}: {msg}")
@@ -117,6 +135,7 @@ EXPORTED = [
     "gdf_seg_label_engine_grid", "gdf_seg_get_counts", "gdf_seg_download_labels",
     "gdf_seg_download_num_labels", "gdf_seg_download_stats", "gdf_seg_download_connections",
     "gdf_seg_download_contours", "gdf_seg_merge_labels", "gdf_seg_get_device_results",
+    "gdf_seg_create_objects",
 ]
 
 
@@ -211,6 +230,7 @@ def load_library(path: str = LIB_PATH):
         "gdf_seg_download_contours": (i32, [vp, vp, vp, vp, vp, u64]),
         "gdf_seg_merge_labels": (i32, [vp, vp, u32, P(u32)]),
         "gdf_seg_get_device_results": (i32, [vp, P(vp), P(vp), P(vp), P(vp)]),
+        "gdf_seg_create_objects": (i32, [vp, vp, vp, vp, u32, vp, u32, P(u32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -766,3 +786,16 @@ class Segmenter:
                                                        C.byref(nobj)))
             r["num_objects"] = nobj.value
         return r
+
+    def create_objects(self, lower, cell_size):
+        """createCCObjects' aggregate fields (no OpenCV shapes): (columns dict, components)."""
+        lo, cs = _vec3(lower), _vec3(cell_size)
+        n = C.c_uint32(0)
+        self._check(self._lib.gdf_seg_create_objects(self._h, _ptr(lo), _ptr(cs), None, 0, None,
+                                                     0, C.byref(n)))
+        objs = (CCObject * max(n.value, 1))()
+        T = self.counts().total_labels
+        comps = np.zeros(T, np.uint32)
+        self._check(self._lib.gdf_seg_create_objects(self._h, _ptr(lo), _ptr(cs), objs, n.value,
+                                                     _ptr(comps), T, C.byref(n)))
+        return cc_objects_as_dict(objs[:n.value]), comps

@@ -203,6 +203,10 @@ int main(int argc, char** argv) {
                   m_fusion->m_ccStatsData.size());
         write_bin(out + "/merged" + s + ".bin", m_fusion->m_ccLabelsMerged.data(),
                   m_fusion->m_ccLabelsMerged.size());
+        std::vector<int32_t> objmin;
+        for (const gdf_cc_object& o : m_fusion->m_ccObjects)
+            objmin.insert(objmin.end(), o.min_voxel, o.min_voxel + 3);
+        write_bin(out + "/objmin" + s + ".bin", objmin.data(), objmin.size());
         std::vector<int32_t> l2c;
         for (const auto& v : m_fusion->m_labelsToContoursPerLayer) l2c.insert(l2c.end(), v.begin(), v.end());
         write_bin(out + "/l2c" + s + ".bin", l2c.data(), l2c.size());

@@ -49,3 +49,6 @@ def test_facade_component_sequence_on_gpu(tmp_path, gpu_engine_factory):
                               ("contours", "<i4", "contour_points")):
             got = np.fromfile(outd / f"{name}{f}.bin", dt)
             assert np.array_equal(got, o[key].reshape(-1)), f"frame {f} {name}"
+        objs, _ = oracle.create_cc_objects(o, (-10, -20, -1), (0.1, 0.1, 0.12))
+        got = np.fromfile(outd / f"objmin{f}.bin", "<i4")
+        assert np.array_equal(got, objs["min_voxel"].reshape(-1)), f"frame {f} objects"

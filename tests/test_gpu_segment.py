@@ -88,3 +88,21 @@ def test_engine_occupancy_grid(seg, gpu_engine_factory):
     o = oracle_mod.object_segmentation_front(grid.reshape(gs[2], gs[1], gs[0]))
     assert_same(r, o)
     assert r["num_objects"] > 2
+    assert_objects(seg, o, p.voxel_min, p.voxel_size)
+
+
+def assert_objects(seg, r, lower=(-10, -20, -1), cs=(0.1, 0.1, 0.12)):
+    go, gc = seg.create_objects(lower, cs)
+    oo, oc = oracle_mod.create_cc_objects(r, lower, cs)
+    assert np.array_equal(gc, oc)
+    for k in oo:
+        assert np.array_equal(np.asarray(go[k]).reshape(oo[k].shape), oo[k]), k
+
+
+@pytest.mark.parametrize("shape,density,seed", [((3, 70, 64), 0.4, 3), ((21, 120, 100), 0.35, 12)])
+def test_cc_objects_match_oracle(seg, shape, density, seed):
+    rng = np.random.default_rng(seed)
+    g = blobs(rng, *shape, density)
+    r = gpu_front(seg, g)
+    assert_objects(seg, oracle_mod.object_segmentation_front(g))
+    assert r["num_objects"] > 3

@@ -163,3 +163,23 @@ def test_connections_and_merge_across_layers():
     assert r["merged"].tolist() == [0, 1, 2, 0, 1, 0, 3]
     assert r["num_objects"] == 4
     assert_same(r, seg_ref.front_end(g))
+
+
+def test_cc_objects_aggregate_fields():
+    g = np.zeros((3, 6, 6), np.uint8)
+    g[0, 0:2, 0:2] = 1
+    g[1, 1:3, 1:3] = 1
+    g[2, 5, 5] = 1
+    g[0, 4:6, 4:6] = 1
+    r = front(g)
+    o, comps = oracle_mod.create_cc_objects(r, (-10, -20, -1), (0.1, 0.1, 0.12))
+    assert o["num_components"].tolist() == [3, 2, 1, 1]
+    assert comps.tolist() == [0, 3, 5, 1, 4, 2, 6]  # grouped global labels, ascending per object
+    # object 1 = A (layer 0, x,y 0..1) + the layer-1 blob (1..2): right/bottom = left + width
+    assert o["min_voxel"][1].tolist() == [0, 0, 0] and o["max_voxel"][1].tolist() == [3, 3, 1]
+    assert o["num_layers"].tolist() == [3, 2, 1, 1]
+    assert o["centroid"][1].tolist() == [1.0, 1.0]       # (0.5 + 1.5) / 2
+    assert o["center_voxel"][1].tolist() == [1.5, 1.5, 0.5]
+    assert o["num_contour_points"].tolist() == [0, 8, 4, 1]
+    f = np.float32
+    assert o["min_world"][2][0] == f(f(4) * f(0.1)) + f(-10)
