@@ -491,6 +491,45 @@ def time_multi(args, st, params, dist, world, pmc_key):
     return line, cfg
 
 
+def run_alternating(args, params, steps, warm):
+    """C2 batches with two parameter sets alternating step by step: graphs on (per-slot graph
+    cache) vs direct launches (graphs off)."""
+    import copy
+    from ros_gpu_depthmap_fusion_amd.gdf import GPUDepthmapFusion
+    p2 = copy.copy(params)
+    p2.flying_threshold = params.flying_threshold + 0.01
+    pcs = [params.to_c(None, None, False, False), p2.to_c(None, None, False, False)]
+    batch = 1  # the component's frame-by-frame flow (batches take direct launches anyway)
+    r = {"workload": "C2 single VGA frames (3 in flight), flying threshold %.2f / %.2f alternating "
+                     "every frame" % (params.flying_threshold, p2.flying_threshold)}
+    for graphs in (True, False):
+        eng = GPUDepthmapFusion(0)
+        st = DepthStream(eng, args.width, args.height, 1, 0, args.workload, args.ring)
+        st.counts(params)
+        eng.set_graphs(graphs)
+        depth = max(1, min(4, args.pipeline))
+        eng.set_pipeline_depth(depth)
+        prime = 4 * depth + 4
+        c0 = eng.graph_stats()
+        eng.run_depth_stream_alternating(st.scam, pcs, 0, prime + warm, batch)
+        eng.synchronize()
+        t0 = time.perf_counter()
+        eng.run_depth_stream_alternating(st.scam, pcs, prime + warm, steps, batch)
+        eng.synchronize()
+        el = time.perf_counter() - t0
+        key = "graph_cache" if graphs else "direct_launches"
+        r[key] = {"value": round(st.P * batch * steps / el / 1e6, 3),
+                  "ms_per_step": round(el / steps * 1e3, 5)}
+        if graphs:
+            c1 = eng.graph_stats()
+            r[key]["graph_captures_replays"] = [c1[0] - c0[0], c1[1] - c0[1]]
+        del st
+        eng.close()
+    r["value"] = r["graph_cache"]["value"]
+    r["ms_per_step"] = r["graph_cache"]["ms_per_step"]
+    return r
+
+
 def run_secondary(args, params):
     """N = 1 only: the other single-GPU configurations, each with its own roofline."""
     from ros_gpu_depthmap_fusion_amd.gdf import GPUDepthmapFusion
@@ -513,6 +552,9 @@ def run_secondary(args, params):
         out[name] = r
         del st
         eng.close()
+    # runtime parameter changes (component.cpp:970-990): two flying-pixel thresholds alternating
+    # every step - one cached graph per (slot, set) - and the same stream with graphs off
+    out["vga_alternating_params"] = run_alternating(args, params, steps, warm)
     # host-resident depth maps (pinned, uploaded on a copy stream overlapped with compute)
     eng = GPUDepthmapFusion(0)
     st = DepthStream(eng, args.width, args.height, 1, 0, args.workload, args.ring,

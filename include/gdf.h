@@ -239,6 +239,9 @@ int gdf_get_device_results(gdf_engine* engine, const float** points, const uint3
 int gdf_process_frame(gdf_engine* engine, const gdf_frame_params* params,
                       gdf_frame_result* out_result);
 
+/* Instrumentation (no reference counterpart): frame-graph captures and replays so far (every slot;
+ * each slot keeps the graphs of up to 4 launch-argument sets, least recently used evicted). */
+int gdf_get_graph_stats(gdf_engine* engine, uint64_t* captures, uint64_t* replays);
 /* Instrumentation (no reference counterpart): the items the last synchronous gdf_process_frame's
  * voxelize sorted - runs of equal voxel keys (*runs = 1) or points (*runs = 0). */
 int gdf_last_sort_items(gdf_engine* engine, uint32_t* items, int* runs);

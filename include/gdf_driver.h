@@ -50,6 +50,14 @@ int gdf_run_depth_stream_batched(gdf_engine* engine, const gdf_stream_camera* ca
                                  uint32_t num_cameras, const gdf_frame_params* params,
                                  uint64_t first, uint64_t batches, uint32_t batch, int host);
 
+/* gdf_run_depth_stream_batched with the parameter set changing every step: step b of the call
+ * uses params[(first + b) % nparams] (a component whose runtime config topics change the
+ * filter parameters between frames, component.cpp:970-990; measures the graph cache). */
+int gdf_run_depth_stream_alternating(gdf_engine* engine, const gdf_stream_camera* cameras,
+                                     uint32_t num_cameras, const gdf_frame_params* params,
+                                     uint32_t nparams, uint64_t first, uint64_t batches,
+                                     uint32_t batch);
+
 #ifdef __cplusplus
 }
 #endif

@@ -8,10 +8,11 @@ namespace {
 
 // `count` calls of gdf_process_frame, each over `batch` consecutive frames (gdf_next_frame_in_batch
 // between them); frame i takes frames[i % ring] of every camera
+// (step b takes parameter set p[(first + b) % nparams])
 int run_stream(gdf_engine* e, const gdf_stream_camera* cams, uint32_t ncams,
                const gdf_frame_params* p, uint64_t first, uint64_t count, bool host,
-               uint32_t batch) {
-    if (!e || !p || (ncams && !cams) || batch == 0) return GDF_ERR_ARG;
+               uint32_t batch, uint32_t nparams = 1) {
+    if (!e || !p || (ncams && !cams) || batch == 0 || nparams == 0) return GDF_ERR_ARG;
     for (uint32_t k = 0; k < ncams; ++k)
         if (!cams[k].frames || cams[k].ring == 0) return GDF_ERR_ARG;
     for (uint64_t b = 0; b < count; ++b) {
@@ -28,7 +29,7 @@ int run_stream(gdf_engine* e, const gdf_stream_camera* cams, uint32_t ncams,
                 if (rc) return rc;
             }
         }
-        rc = gdf_process_frame(e, p, nullptr);
+        rc = gdf_process_frame(e, p + (first + b) % nparams, nullptr);
         if (rc) return rc;
     }
     return GDF_OK;
@@ -51,4 +52,11 @@ extern "C" int gdf_run_depth_stream_batched(gdf_engine* e, const gdf_stream_came
                                             uint64_t first, uint64_t batches, uint32_t batch,
                                             int host) {
     return run_stream(e, cams, ncams, p, first, batches, host != 0, batch);
+}
+
+extern "C" int gdf_run_depth_stream_alternating(gdf_engine* e, const gdf_stream_camera* cams,
+                                                uint32_t ncams, const gdf_frame_params* params,
+                                                uint32_t nparams, uint64_t first,
+                                                uint64_t batches, uint32_t batch) {
+    return run_stream(e, cams, ncams, params, first, batches, false, batch, nparams);
 }

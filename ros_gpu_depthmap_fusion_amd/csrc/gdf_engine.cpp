@@ -230,11 +230,15 @@ struct Slot {
     bool runs_valid = false;        // this frame's voxelize may sort runs
     uint32_t nframes = 1;           // frames of the slot's last processed batch
     uint32_t n_total = 0;
-    // steady-state frame as a HIP graph (the fused frame + voxelize launches of this slot): one
+    // steady-state frames as HIP graphs (the fused frame + voxelize launches of this slot): one
     // graph launch and two kernel-node argument updates (depth pointers, grid ticket) per frame
-    // instead of six direct launches.  Replayed while the frame's launch arguments - minus those
-    // two fields - stay what they were at capture; captured once they repeat on two frames.
-    struct Graph {
+    // instead of six direct launches.  A graph is replayed while the frame's launch arguments -
+    // minus those two fields - equal its capture's; captured once they repeat on two frames.  Up to
+    // kGraphCache argument sets per slot keep their graphs (least recently used evicted), so a
+    // caller alternating between parameter sets (e.g. the component's runtime config topics,
+    // component.cpp:970-990) replays instead of re-capturing.
+    static constexpr int kGraphCache = 4;
+    struct GraphEntry {
         hipGraph_t g = nullptr;
         hipGraphExec_t x = nullptr;
         // the compaction kernel nodes (k_mask, k_emit, k_emit_sel): they take the FrameArgs
@@ -242,16 +246,29 @@ struct Slot {
         FrameArgs key_a;
         VoxelizeArgs key_v;
         bool valid = false;
-        FrameArgs cand_a;
-        VoxelizeArgs cand_v;
-        bool cand = false;
+        uint64_t used = 0;  // last use (Graphs::tick)
         void reset() {
             if (x) (void)hipGraphExecDestroy(x);
             if (g) (void)hipGraphDestroy(g);
             x = nullptr;
             g = nullptr;
-            valid = cand = false;
+            valid = false;
+            used = 0;
             frame_nodes.clear();
+        }
+    };
+    struct Graphs {
+        GraphEntry e[kGraphCache];
+        // argument sets seen once (direct launches): a second sighting captures
+        FrameArgs cand_a[kGraphCache];
+        VoxelizeArgs cand_v[kGraphCache];
+        bool cand[kGraphCache] = {};
+        int cand_next = 0;
+        uint64_t tick = 0;
+        uint64_t captures = 0, replays = 0;  // instrumentation (gdf_get_graph_stats)
+        void reset() {
+            for (GraphEntry& x : e) x.reset();
+            for (bool& c : cand) c = false;
         }
     } graph;
 };
@@ -1295,7 +1312,7 @@ void run_fused_frame(gdf_engine* e, int average, uint32_t lifetime) {
     const FrameArgs a = frame_args(e, true);
     frame_launched(e, true, a.key_hist != nullptr, a.run_mode != 0);  // (the launches below follow)
     const VoxelizeArgs v = voxelize_args(e, average, (int)lifetime);
-    Slot::Graph& G = e->sl().graph;
+    Slot::Graphs& G = e->sl().graph;
     // (a frame without compaction kernels stores its grid ticket with a memset: not replayable)
     if (e->sl().group_marks) {  // rollbuffer frame: marks from the voxel groups, then the grid
         e->timed(GDF_KERNEL_FRAME, [&] { HIPCHK(launch_frame(a, e->s(), e->hook_ptr())); });
@@ -1307,18 +1324,40 @@ void run_fused_frame(gdf_engine* e, int average, uint32_t lifetime) {
     const bool eligible = e->use_graphs && !e->profiling && !e->debug && a.ncams <= kArgCams &&
                           !e->user_stream && a.total_segs;
     hipStream_t st = e->s();
-    if (eligible && G.valid && same_key(a, v, G.key_a, G.key_v)) {
+    Slot::GraphEntry* hit = nullptr;
+    if (eligible)
+        for (Slot::GraphEntry& x : G.e)
+            if (x.valid && same_key(a, v, x.key_a, x.key_v)) hit = &x;
+    int seen = -1;
+    if (eligible && !hit)
+        for (int c = 0; c < Slot::kGraphCache; ++c)
+            if (G.cand[c] && same_key(a, v, G.cand_a[c], G.cand_v[c])) seen = c;
+    if (hit) {
         void* args[] = {const_cast<FrameArgs*>(&a)};
-        for (auto& np : G.frame_nodes) {
+        for (auto& np : hit->frame_nodes) {
             hipKernelNodeParams kp = np.second;
             kp.kernelParams = args;
-            HIPCHK(hipGraphExecKernelNodeSetParams(G.x, np.first, &kp));
+            HIPCHK(hipGraphExecKernelNodeSetParams(hit->x, np.first, &kp));
         }
-        HIPCHK(hipGraphLaunch(G.x, st));
-    } else if (eligible && G.cand && same_key(a, v, G.cand_a, G.cand_v)) {
-        // the arguments repeated: capture this frame's launches and replay from now on
-        if (G.x) HIPCHK(hipStreamSynchronize(st));  // no launch of the old graph in flight
-        G.reset();
+        HIPCHK(hipGraphLaunch(hit->x, st));
+        hit->used = ++G.tick;
+        ++G.replays;
+    } else if (seen >= 0) {
+        // the arguments repeated: capture this frame's launches and replay from now on, into a
+        // free entry or the least recently used one
+        Slot::GraphEntry* slot = nullptr;
+        for (Slot::GraphEntry& x : G.e)
+            if (!x.valid) {
+                slot = &x;
+                break;
+            }
+        if (!slot) {
+            slot = &G.e[0];
+            for (Slot::GraphEntry& x : G.e)
+                if (x.used < slot->used) slot = &x;
+        }
+        if (slot->valid) HIPCHK(hipStreamSynchronize(st));  // no launch of the evicted graph in flight
+        slot->reset();
         HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
         hipError_t e1 = launch_frame(a, st, nullptr);
         hipError_t e2 = e1 == hipSuccess ? launch_voxelize(v, st, nullptr) : e1;
@@ -1326,17 +1365,17 @@ void run_fused_frame(gdf_engine* e, int average, uint32_t lifetime) {
         hipError_t e3 = hipStreamEndCapture(st, &g);
         HIPCHK(e2);
         HIPCHK(e3);
-        G.g = g;
-        HIPCHK(hipGraphInstantiate(&G.x, G.g, nullptr, nullptr, 0));
+        slot->g = g;
+        HIPCHK(hipGraphInstantiate(&slot->x, slot->g, nullptr, nullptr, 0));
         size_t nn = 0;
-        HIPCHK(hipGraphGetNodes(G.g, nullptr, &nn));
+        HIPCHK(hipGraphGetNodes(slot->g, nullptr, &nn));
         std::vector<hipGraphNode_t> nodes(nn);
-        HIPCHK(hipGraphGetNodes(G.g, nodes.data(), &nn));
+        HIPCHK(hipGraphGetNodes(slot->g, nodes.data(), &nn));
         const void* fk[6] = {frame_kernel(0, a.rot45, a.do_flying ? a.F : 0u), frame_kernel(1, a.rot45),
                              frame_kernel(2, a.rot45),
                              frame_kernel(3, a.rot45), frame_kernel(4, a.rot45),
                              frame_kernel(5, a.rot45)};  // (the count scans take no FrameArgs)
-        G.frame_nodes.clear();
+        slot->frame_nodes.clear();
         for (hipGraphNode_t n : nodes) {
             hipGraphNodeType t;
             HIPCHK(hipGraphNodeGetType(n, &t));
@@ -1344,18 +1383,23 @@ void run_fused_frame(gdf_engine* e, int average, uint32_t lifetime) {
             hipKernelNodeParams kp{};
             HIPCHK(hipGraphKernelNodeGetParams(n, &kp));
             if (std::find(fk, fk + 6, kp.func) != fk + 6)
-                G.frame_nodes.emplace_back(n, kp);
+                slot->frame_nodes.emplace_back(n, kp);
         }
-        if (G.frame_nodes.empty()) fail(GDF_ERR_HIP, "frame graph: compaction kernels not found");
-        graph_key(a, G.key_a);
-        G.key_v = v;
-        G.valid = true;
-        HIPCHK(hipGraphLaunch(G.x, st));
+        if (slot->frame_nodes.empty()) fail(GDF_ERR_HIP, "frame graph: compaction kernels not found");
+        graph_key(a, slot->key_a);
+        slot->key_v = v;
+        slot->valid = true;
+        slot->used = ++G.tick;
+        G.cand[seen] = false;
+        ++G.captures;
+        HIPCHK(hipGraphLaunch(slot->x, st));
     } else {
         if (eligible) {
-            graph_key(a, G.cand_a);
-            G.cand_v = v;
-            G.cand = true;
+            const int c = G.cand_next;
+            G.cand_next = (c + 1) % Slot::kGraphCache;
+            graph_key(a, G.cand_a[c]);
+            G.cand_v[c] = v;
+            G.cand[c] = true;
         }
         if (e->profiling) e->timed(GDF_KERNEL_EVENT_FLOOR, [] {});
         e->timed(GDF_KERNEL_FRAME, [&] { HIPCHK(launch_frame(a, st, e->hook_ptr())); });
@@ -1421,6 +1465,18 @@ int guarded(gdf_engine* e, F&& f) {
 extern "C" {
 
 const char* gdf_last_error(void) { return g_last_error.c_str(); }
+
+int gdf_get_graph_stats(gdf_engine* e, uint64_t* captures, uint64_t* replays) {
+    ENGINE_OR_FAIL(e);
+    uint64_t c = 0, r = 0;
+    for (const Slot& sl : e->slots) {
+        c += sl.graph.captures;
+        r += sl.graph.replays;
+    }
+    if (captures) *captures = c;
+    if (replays) *replays = r;
+    return GDF_OK;
+}
 
 int gdf_get_stream(gdf_engine* e, void** out) {
     ENGINE_OR_FAIL(e);

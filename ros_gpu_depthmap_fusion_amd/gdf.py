@@ -127,9 +127,11 @@ EXPORTED = [
     "gdf_debug_historic_grid",
     # include/gdf_driver.h: the component's depth loop in C++ over the C-ABI
     "gdf_run_depth_stream", "gdf_run_host_stream", "gdf_run_depth_stream_batched",
+    "gdf_run_depth_stream_alternating",
     "gdf_next_frame_in_batch", "gdf_get_batch_ranges", "gdf_download_batch_occupancy_grid",
     "gdf_mask_dilate", "gdf_transform_points", "gdf_add_halo_depthmap_device",
     "gdf_partition_points", "gdf_voxelize_points", "gdf_last_sort_items", "gdf_get_stream",
+    "gdf_get_graph_stats",
     # include/gdf_segment.h: the GPU object-segmentation front end
     "gdf_seg_create", "gdf_seg_destroy", "gdf_seg_set_stream", "gdf_seg_label_layers",
     "gdf_seg_label_engine_grid", "gdf_seg_get_counts", "gdf_seg_download_labels",
@@ -207,6 +209,8 @@ def load_library(path: str = LIB_PATH):
         "gdf_run_host_stream": (i32, [vp, P(StreamCamera), u32, P(FrameParams), u64, u64]),
         "gdf_run_depth_stream_batched": (i32, [vp, P(StreamCamera), u32, P(FrameParams), u64,
                                                u64, u32, i32]),
+        "gdf_run_depth_stream_alternating": (i32, [vp, P(StreamCamera), u32, vp, u32, u64, u64,
+                                                   u32]),
         "gdf_next_frame_in_batch": (i32, [vp]),
         "gdf_mask_dilate": (i32, [vp, vp, vp, u32, u32, u32, i32]),
         "gdf_add_halo_depthmap_device": (i32, [vp, vp, u32, u32, u32, f, f, f, f, f, vp, vp]),
@@ -217,6 +221,7 @@ def load_library(path: str = LIB_PATH):
         "gdf_download_batch_occupancy_grid": (i32, [vp, u32, vp, u64]),
         "gdf_last_sort_items": (i32, [vp, P(u32), P(i32)]),
         "gdf_get_stream": (i32, [vp, P(vp)]),
+        "gdf_get_graph_stats": (i32, [vp, P(u64), P(u64)]),
         "gdf_seg_create": (i32, [i32, P(vp)]),
         "gdf_seg_destroy": (i32, [vp]),
         "gdf_seg_set_stream": (i32, [vp, vp]),
@@ -638,6 +643,15 @@ class GPUDepthmapFusion:
                                                            first, batches, batch,
                                                            1 if host else 0))
 
+    def run_depth_stream_alternating(self, cameras: Sequence[StreamCamera],
+                                     params: Sequence[FrameParams], first: int, batches: int,
+                                     batch: int):
+        """gdf_run_depth_stream_alternating: step b uses params[(first + b) % len(params)]."""
+        arr = (StreamCamera * len(cameras))(*cameras)
+        ps = (FrameParams * len(params))(*params)
+        self._check(self._lib.gdf_run_depth_stream_alternating(self._h, arr, len(cameras), ps,
+                                                               len(params), first, batches, batch))
+
     # ---- multi-GPU fused cloud ----
     def partition_points(self, nparts: int, send_pts_ptr: int, send_keys_ptr: int,
                          capacity: int, part_counts_ptr: int):
@@ -688,6 +702,12 @@ class GPUDepthmapFusion:
         self._check(self._lib.gdf_download_batch_occupancy_grid(self._h, frame, _ptr(out),
                                                                 out.shape[0]))
         return out[:nc]
+
+    def graph_stats(self):
+        """(captures, replays) of the slots' frame graphs (instrumentation; include/gdf.h)."""
+        c, r = C.c_uint64(0), C.c_uint64(0)
+        self._check(self._lib.gdf_get_graph_stats(self._h, C.byref(c), C.byref(r)))
+        return c.value, r.value
 
     def last_sort_items(self):
         """(items, runs): what the last synchronous processFrame's voxelize sorted - runs of

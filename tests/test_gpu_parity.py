@@ -655,3 +655,45 @@ def test_sparse_mark_pairs_and_union(Engine):
     gpu.take_marks_sparse(bits.ptr, nw, small.ptr, 8)
     gpu.synchronize()
     assert small.to_numpy(np.uint32, 1)[0] == np.count_nonzero(bits.to_numpy(np.uint32, nw)) > 8
+
+
+def test_graph_cache_alternating_parameters(Engine):
+    """A caller alternating between parameter sets every frame (the component's runtime config
+    topics, component.cpp:970-990) replays one cached graph per set and slot instead of
+    re-capturing: frame by frame equal to direct launches, the grid equal to the oracle's, and
+    each (slot, set) captured once."""
+    from ros_gpu_depthmap_fusion_amd import hiprt
+    cams = synth.cameras(2, 160, 120)
+    ring = 5
+    host = [[synth.dense_frame(c, f, k) for f in range(ring)] for k, c in enumerate(cams)]
+    dev = [[hiprt.DeviceArray.from_numpy(d) for d in h] for h in host]
+    sets = [ComponentParams(), ComponentParams(flying_threshold=0.35),
+            ComponentParams(voxel_average=False)]
+    direct, graph = Engine(), Engine()
+    direct.set_graphs(False)
+    graph.set_graphs(True)
+    for e in (direct, graph):
+        e.set_pipeline_depth(3)
+    orc = OracleFusion(threads=4)
+    nframes = 36
+    for f in range(nframes):
+        p = sets[f % 2] if f < 24 else sets[f % 3]
+        for e in (direct, graph):
+            e.clear()
+            for k, c in enumerate(cams):
+                e.addDepthmapDevice(dev[k][f % ring].ptr, c.width, c.height, *c.intrinsics(),
+                                    c.T_world, c.T_crop)
+            e.processFrame(p, synchronous=False)
+        run_fused(orc, [cam_args(c, host[k][f % ring]) for k, c in enumerate(cams)], p)
+        if f % 6 == 5:
+            direct.synchronize()
+            graph.synchronize()
+            for a, b in zip(_gpu_outputs(direct), _gpu_outputs(graph)):
+                np.testing.assert_array_equal(bits(a) if a.dtype == np.float32 else a,
+                                              bits(b) if b.dtype == np.float32 else b,
+                                              err_msg=f"frame {f}")
+    graph.synchronize()
+    np.testing.assert_array_equal(graph.historic_grid(), orc.historic_grid())
+    captures, replays = graph.graph_stats()
+    assert captures <= 3 * 3, captures   # <= one per (slot, parameter set)
+    assert replays >= nframes - 2 * 3 * 3 - 3 * 3, replays
