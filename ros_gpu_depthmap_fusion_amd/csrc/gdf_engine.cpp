@@ -1587,6 +1587,7 @@ int gdf_set_pipeline_depth(gdf_engine* e, int depth) {
     }
     return guarded(e, [&] {
         if (e->user_stream && depth > 1) fail(GDF_ERR_STATE, "pipelining needs the engine's own streams");
+        if (depth == e->npipe) return;  // unchanged: no drain, the grid sequence continues
         sync_all(e);
         for (int i = 0; i < depth; ++i) create_slot(e->slots[i]);
         // a configuration call between frames: the next frame starts on slot 0 (a shallower
