@@ -2287,7 +2287,11 @@ __global__ __launch_bounds__(256) void k_group_big(const uint32_t* __restrict__ 
 uint32_t g_run_stage = 2048;
 uint32_t g_run_inblock = 256;
 uint32_t g_run_big_blocks = 1024;  // k_group_runs_big grid (tuning knob GDF_RUN_BIG_BLOCKS)
-uint32_t g_run_q16 = 0;  // 1 K-point chunks in k_group_runs_big (tuning knob GDF_RUN_Q16)
+// 1 K-point chunks in k_group_runs_big: 0 never, 1 always, 2 (default) for single depth-only
+// frames - whose long voxels reach ~20 K points at 4K (4K group phase 154 -> 142 us) - while
+// batches (shorter voxels: VGA x8 42 -> 49 us) and rollbuffer windows keep 256-point chunks
+// (tuning knob GDF_RUN_Q16)
+uint32_t g_run_q16 = 2;
 // a streamed chunk: 64 x Q points per wave step (Q = 4, 4 waves per block; Q = 16, one wave)
 
 __device__ __forceinline__ void wave_sync() {
@@ -2807,7 +2811,9 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
                            kbuf[npasses & 1], vbuf[npasses & 1]);  // (free after the sort)
         if (a.average) {
             if ((e = hipGetLastError()) != hipSuccess) return e;
-            if (g_run_q16)
+            const bool q16 = g_run_q16 == 1 ||
+                             (g_run_q16 == 2 && a.nframes <= 1 && a.group_marks == nullptr);
+            if (q16)
                 hipLaunchKernelGGL((k_group_runs_big<16, 1>), dim3(4 * g_run_big_blocks), dim3(64), 0,
                                    s, kbuf[npasses & 1], vbuf[npasses & 1], a.pts,
                                    reinterpret_cast<float*>(a.out), a.bigq, a.bigq_cap, qctr);
