@@ -161,34 +161,37 @@ __global__ __launch_bounds__(256) void k_cc_flatten(uint32_t* par, uint32_t nb) 
     par[i] = uf_find<__HIP_MEMORY_SCOPE_AGENT>(par, i);
 }
 
-// one workgroup per layer: roots ranked in block order
+// one workgroup per layer: roots ranked in block order.  Wave w owns a contiguous range of the
+// layer's blocks and walks it 64 blocks per step (coalesced; ballot + popcount), twice: counts,
+// then - after a scan of the 16 wave totals - the labels.
 __global__ __launch_bounds__(1024) void k_cc_rank(const uint32_t* __restrict__ par, uint32_t nbl,
                                                   uint32_t* __restrict__ blabel,
                                                   uint32_t* __restrict__ nlabels) {
     __shared__ uint32_t s_w[16];
     const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6, z = blockIdx.x;
-    const uint32_t base = z * nbl, per = (nbl + 1023) / 1024;
-    const uint32_t b0 = min(t * per, nbl), b1 = min(b0 + per, nbl);
+    const uint32_t base = z * nbl;
+    const uint32_t per = ((nbl + 15) / 16 + 63) / 64 * 64;  // blocks per wave, whole steps
+    const uint32_t b0 = min(w * per, nbl), b1 = min(b0 + per, nbl);
+    const unsigned long long ltm = (1ull << lane) - 1ull;
     uint32_t cnt = 0;
-    for (uint32_t i = b0; i < b1; ++i) cnt += par[base + i] == base + i;
-    // block exclusive scan: waves by DPP-free shuffles, then the 16 wave totals
-    uint32_t v = cnt;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = __shfl_up(v, d, 64);
-        if ((int)lane >= d) v += o;
+    for (uint32_t i = b0 + lane; i - lane < b1; i += 64) {  // (i - lane: wave-uniform)
+        const bool root = i < b1 && par[base + i] == base + i;
+        cnt += (uint32_t)__popcll(__ballot(root));
     }
-    if (lane == 63) s_w[w] = v;
+    if (lane == 0) s_w[w] = cnt;
     __syncthreads();
-    uint32_t woff = 0, tot = 0;
+    uint32_t r = 0, tot = 0;
     for (uint32_t k = 0; k < 16; ++k) {
         const uint32_t x = s_w[k];
-        woff += k < w ? x : 0u;
+        r += k < w ? x : 0u;
         tot += x;
     }
-    uint32_t r = woff + v - cnt;
-    for (uint32_t i = b0; i < b1; ++i)
-        if (par[base + i] == base + i) blabel[base + i] = 1 + r++;
+    for (uint32_t i = b0 + lane; i - lane < b1; i += 64) {
+        const bool root = i < b1 && par[base + i] == base + i;
+        const unsigned long long m = __ballot(root);
+        if (root) blabel[base + i] = 1 + r + (uint32_t)__popcll(m & ltm);
+        r += (uint32_t)__popcll(m);
+    }
     if (t == 0) nlabels[z] = 1 + tot;
 }
 
