@@ -843,13 +843,13 @@ void launch_contours(gdf_segmenter* g, const uint8_t* grid, uint32_t W, uint32_t
 
 void run_label_layers(gdf_segmenter* g, const uint8_t* grid, uint32_t W, uint32_t H, uint32_t L,
                       uint32_t flags, hipStream_t s) {
+    g->have = false;  // (a failed call leaves no result behind)
+    g->contours_read = false;
     if (!grid || W == 0 || H == 0 || L == 0) seg_fail(GDF_ERR_ARG, "empty grid");
     if (W > 65534 || H > 65534) seg_fail(GDF_ERR_ARG, "layers wider or taller than 65534 cells");
     const uint32_t BW = (W + 1) / 2, BH = (H + 1) / 2;
     const uint64_t nbl = (uint64_t)BW * BH, nb = nbl * L;
     if (nb >= 0xFFFFFFF0ull) seg_fail(GDF_ERR_ARG, "grid too large for 32-bit block indices");
-    g->have = false;
-    g->contours_read = false;
     SEGCHK(g->par.ensure(nb * 4));
     SEGCHK(g->bits.ensure(nb));
     SEGCHK(g->blabel.ensure(nb * 4));

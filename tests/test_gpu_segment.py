@@ -106,3 +106,23 @@ def test_cc_objects_match_oracle(seg, shape, density, seed):
     r = gpu_front(seg, g)
     assert_objects(seg, oracle_mod.object_segmentation_front(g))
     assert r["num_objects"] > 3
+
+
+def test_errors_fail_loudly(seg):
+    import torch
+    from ros_gpu_depthmap_fusion_amd.gdf import GDFError
+    # more than 65535 components in a layer overflow the reference's CV_16U labels
+    g = np.zeros((1, 600, 600), np.uint8)
+    g[0, ::2, ::2] = 1  # 90 000 isolated cells
+    t = torch.from_numpy(g).cuda()
+    torch.cuda.synchronize()
+    with pytest.raises(GDFError, match="65535"):
+        seg.label_layers(t.data_ptr(), 600, 600, 1)
+    with pytest.raises(GDFError):
+        seg.counts()  # no result after a failed call
+    with pytest.raises(GDFError):
+        seg.label_layers(t.data_ptr(), 0, 600, 1)
+    # the segmenter stays usable
+    g2 = np.zeros((2, 30, 20), np.uint8)
+    g2[:, 3:9, 4:7] = 5
+    assert_same(gpu_front(seg, g2), oracle_mod.object_segmentation_front(g2))
