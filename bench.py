@@ -80,6 +80,17 @@ def parse():
     return ap.parse_args()
 
 
+def radix_passes(ncells, B=1):
+    """Radix passes of the voxelize sort (gdf_device.hpp radix_passes): the voxel-key bits plus
+    the frame bits of a batch, 8-bit digits, a 9-bit last digit when that saves a pass (<= 25)."""
+    bits = max(int(ncells - 1).bit_length(), 0) + (int(B - 1).bit_length() if B > 1 else 0)
+    if bits == 0:
+        return 1
+    if bits <= 25:
+        return 1 if bits <= 9 else (bits + 6) // 8
+    return (bits + 7) // 8
+
+
 def model_bytes(P, n_avg, g_avg, ncells, B=1, s_avg=None, runs=False):
     """Algorithmic HBM bytes per launch of each kernel: the bytes the algorithm
     must move once, not the cache traffic of an implementation.  A launch of a B-frame batch
@@ -90,14 +101,15 @@ def model_bytes(P, n_avg, g_avg, ncells, B=1, s_avg=None, runs=False):
     P, n_avg, g_avg = B * P, B * n_avg, B * g_avg
     s_items = B * (s_avg if s_avg is not None else n_avg / B)
     tiles = (P + 255) // 256
+    npass = radix_passes(ncells, B)
     return {
         "mask": 3.0 * P,                           # u16 depth in, u8 stage bits out
         "scan": 8.0 * tiles,
         # stage in, depth of kept px, xyzw + key out (+ key and first point of each run)
         "emit": 1.0 * P + 22.0 * n_avg + (8.0 * s_items if runs else 0.0),
-        # 3 radix passes over the sorted items (key only in, key+index out; then key+index both
+        # radix passes over the sorted items (key only in, key+index out; then key+index both
         # ways) + the grid update carried by the first pass, averaged per launch
-        "sort": (12.0 * s_items + 16.0 * s_items * 2 + (B + 1.0) * ncells) / 3.0,
+        "sort": (12.0 * s_items + 16.0 * s_items * (npass - 1) + (B + 1.0) * ncells) / npass,
         # sorted keys + indices (+ the runs' point ranges) in, points in, means out
         "group": (16.0 * n_avg + 16.0 * s_items if runs else 24.0 * n_avg) + 16.0 * g_avg,
         "grid": (B + 1.0) * ncells,

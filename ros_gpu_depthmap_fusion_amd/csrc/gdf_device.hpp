@@ -26,6 +26,26 @@ constexpr int kSortGroup = 8;         // radix tiles per look-back group (group 
 // serialise at the memory-side atomic unit; the sort pass sums the replicas of its digit
 constexpr int kHistReps = 16;
 constexpr int kHistWords = kHistReps * 4 * 256;
+
+// Radix passes over a key of `bits` bits: 8-bit digits, except that up to 25 bits the LAST pass
+// takes a 9-bit digit when that saves a pass (25 = 22 voxel-key bits + 3 frame bits of an 8-frame
+// batch: 3 passes instead of 4; 17 and 9 likewise).  Pass p's histogram lives at [p*256, ...):
+// the 9-bit last digit of pass 2 fills [512, 1024), still inside a replica's 1024 words.
+__host__ __device__ constexpr uint32_t radix_passes(uint32_t bits) {
+    return bits == 0 ? 1u : bits <= 25 ? (bits <= 9 ? 1u : (bits + 6) / 8) : (bits + 7) / 8;
+}
+__host__ __device__ constexpr bool radix_wide_last(uint32_t bits) {
+    return bits >= 9 && bits <= 25 && bits % 8 == 1;
+}
+// digit of pass p (of np passes): a 9-bit mask on the last of <= 3 passes is exact for every key
+// (an 8-bit last digit has bit 8 clear: the key has no bits there)
+__host__ __device__ constexpr uint32_t radix_digit(uint32_t key, uint32_t p, uint32_t np) {
+    return (key >> (8u * p)) & ((p + 1u == np && np <= 3u) ? 0x1FFu : 0xFFu);
+}
+// histogram words a producer clears / flushes for np passes
+__host__ __device__ constexpr uint32_t radix_hist_span(uint32_t np) {
+    return np <= 3u ? (np + 1u) * 256u : 1024u;
+}
 constexpr int kGroupThreads = 256;
 constexpr int kSumChunk = 128;                               // points per wave gather chunk
 constexpr uint32_t kSpinLimit = 1u << 26;                   // bounded look-back spins

@@ -1064,7 +1064,7 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel) {
         // each flush their histogram with device-scope atomics; k_sort_hist counts those keys
         a.key_hist = a.total_segs <= kFusedPrefixSegs && !a.sel_tiles ? e->sl().d_khist.as<uint32_t>()
                                                                       : nullptr;
-        a.npasses = sort_bits(e) == 0 ? 1u : (sort_bits(e) + 7) / 8;
+        a.npasses = radix_passes(sort_bits(e));
         // depth-only frames sort runs of equal keys (8-20x fewer items on dense frames); k_mask
         // counts the runs and their key digits (one flush per segment: few runs, few bins)
         // (measured on MI355X, dense frames: 4K 18.2 -> 24.0 Gpoints/s, a batch of four VGA frames
@@ -1192,8 +1192,9 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime,
     e->sl().d_kb.ensure((size_t)nmax * 4);
     e->sl().d_va.ensure((size_t)nmax * 4);
     e->sl().d_vb.ensure((size_t)nmax * 4);
-    e->sl().d_sstatus.ensure_zero(voxelize_status_words(nmax) * 8, e->s());
-    e->sl().d_sgstatus.ensure_zero((voxelize_status_words(nmax) / kSortGroup + 256) * 8, e->s());
+    const size_t swords = voxelize_status_words(nmax, sort_bits(e));
+    e->sl().d_sstatus.ensure_zero(swords * 8, e->s());
+    e->sl().d_sgstatus.ensure_zero((swords / kSortGroup + 512) * 8, e->s());
     e->sl().d_gstatus.ensure_zero(voxelize_group_tiles(nmax) * 8, e->s());
     e->sl().d_ggstatus.ensure_zero((voxelize_group_tiles(nmax) / 64 + 2) * 8, e->s());
     e->sl().d_vox.ensure((size_t)nmax * 16);

@@ -217,87 +217,102 @@ __device__ __forceinline__ uint32_t lookback2_wave(unsigned long long* tstat,
     return gpre + in_excl;
 }
 
-// The same two-level scheme with one channel per THREAD (the 256 digits of a radix pass):
-// groups of kSortGroup (8) tiles, 8 independent polls per round trip (8 rather than 16: 45 fewer
-// VGPRs in the radix pass, occupancy 4 -> 6 waves/SIMD at 4 keys per thread).
-__device__ __forceinline__ uint32_t lookback2_chan(unsigned long long* tstat,
-                                                   unsigned long long* gstat, uint32_t tile,
-                                                   uint32_t ntiles, uint32_t chan, uint32_t agg,
-                                                   uint32_t epoch, uint32_t* err) {
+// The same two-level scheme with R channels per THREAD (the 256 R digits of a radix pass; channel
+// r of thread t is t + 256 r): groups of kSortGroup (8) tiles, 8 independent polls per round trip
+// (8 rather than 16: 45 fewer VGPRs in the radix pass, occupancy 4 -> 6 waves/SIMD at 4 keys per
+// thread).  All R aggregates are published before the first poll.
+template <int R>
+__device__ __forceinline__ void lookback2_chans(unsigned long long* tstat, unsigned long long* gstat,
+                                                uint32_t tile, uint32_t ntiles, const uint32_t* agg,
+                                                uint32_t* excl, uint32_t epoch, uint32_t* err) {
+    constexpr uint32_t kCh = 256u * R;
+    const uint32_t t = threadIdx.x;
     const unsigned long long fagg = 2ull * epoch, fincl = 2ull * epoch + 1ull;
     const uint32_t G = tile / kSortGroup, first = G * kSortGroup, pos = tile - first;
     const uint32_t last = (first + kSortGroup - 1u < ntiles - 1u) ? first + kSortGroup - 1u
                                                                    : ntiles - 1u;
-    __hip_atomic_store(&tstat[(size_t)tile * 256 + chan], (fagg << 32) | agg, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        __hip_atomic_store(&tstat[(size_t)tile * kCh + t + 256u * r], (fagg << 32) | agg[r],
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint32_t spins = 0;
-    uint32_t in_excl = 0;
-    if (pos > 0) {
-        while (true) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t chan = t + 256u * r;
+        uint32_t in_excl = 0;
+        if (pos > 0) {
+            while (true) {
+                unsigned long long sv[kSortGroup];
+#pragma unroll
+                for (int q = 0; q < kSortGroup; ++q)
+                    sv[q] = ((uint32_t)q < pos)
+                                ? __hip_atomic_load(&tstat[(size_t)(first + q) * kCh + chan],
+                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                : (fagg << 32);
+                bool wait = false;
+                uint32_t v = 0;
+#pragma unroll
+                for (int q = 0; q < kSortGroup; ++q) {
+                    wait |= (sv[q] >> 32) < fagg;
+                    v += (uint32_t)q < pos ? (uint32_t)sv[q] : 0u;
+                }
+                if (wait) {
+                    if (++spins > kSpinLimit) {
+                        atomicOr(err, 2u);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                in_excl = v;
+                break;
+            }
+        }
+        excl[r] = in_excl;  // (within the group; the groups' prefix is added below)
+    }
+    if (tile == last)
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            __hip_atomic_store(&gstat[(size_t)G * kCh + t + 256u * r], (fagg << 32) | (excl[r] + agg[r]),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t chan = t + 256u * r;
+        uint32_t gpre = 0;
+        int64_t j = (int64_t)G - 1;
+        while (j >= 0) {
             unsigned long long sv[kSortGroup];
 #pragma unroll
             for (int q = 0; q < kSortGroup; ++q)
-                sv[q] = ((uint32_t)q < pos)
-                            ? __hip_atomic_load(&tstat[(size_t)(first + q) * 256 + chan],
-                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                            : (fagg << 32);
-            bool wait = false;
-            uint32_t v = 0;
-#pragma unroll
-            for (int q = 0; q < kSortGroup; ++q) {
-                wait |= (sv[q] >> 32) < fagg;
-                v += (uint32_t)q < pos ? (uint32_t)sv[q] : 0u;
+                sv[q] = (j - q >= 0) ? __hip_atomic_load(&gstat[(size_t)(j - q) * kCh + chan],
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                     : (fincl << 32);
+            int q = 0;
+            bool done = false;
+            for (; q < kSortGroup; ++q) {
+                const unsigned long long flag = sv[q] >> 32;
+                if (flag < fagg) break;
+                gpre += (uint32_t)sv[q];
+                if (flag == fincl) {
+                    done = true;
+                    break;
+                }
             }
-            if (wait) {
+            if (done) break;
+            j -= q;
+            if (q < kSortGroup) {
                 if (++spins > kSpinLimit) {
                     atomicOr(err, 2u);
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
-                continue;
             }
-            in_excl = v;
-            break;
         }
+        if (tile == last)
+            __hip_atomic_store(&gstat[(size_t)G * kCh + chan], (fincl << 32) | (gpre + excl[r] + agg[r]),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        excl[r] += gpre;
     }
-    const uint32_t gtotal = in_excl + agg;
-    if (tile == last)
-        __hip_atomic_store(&gstat[(size_t)G * 256 + chan], (fagg << 32) | gtotal,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint32_t gpre = 0;
-    int64_t j = (int64_t)G - 1;
-    while (j >= 0) {
-        unsigned long long sv[kSortGroup];
-#pragma unroll
-        for (int q = 0; q < kSortGroup; ++q)
-            sv[q] = (j - q >= 0) ? __hip_atomic_load(&gstat[(size_t)(j - q) * 256 + chan],
-                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                 : (fincl << 32);
-        int q = 0;
-        bool done = false;
-        for (; q < kSortGroup; ++q) {
-            const unsigned long long flag = sv[q] >> 32;
-            if (flag < fagg) break;
-            gpre += (uint32_t)sv[q];
-            if (flag == fincl) {
-                done = true;
-                break;
-            }
-        }
-        if (done) break;
-        j -= q;
-        if (q < kSortGroup) {
-            if (++spins > kSpinLimit) {
-                atomicOr(err, 2u);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    if (tile == last)
-        __hip_atomic_store(&gstat[(size_t)G * 256 + chan], (fincl << 32) | (gpre + gtotal),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return gpre + in_excl;
 }
 
 // ---- fused frame kernel ------------------------------------------------------------------------
@@ -656,7 +671,7 @@ __global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
     uint32_t rkey = 0xFFFFFFFFu;  // run mode: sort key of a kept pixel
     const uint32_t i = threadIdx.x;
     if (a.run_mode && a.key_hist)
-        for (uint32_t j = threadIdx.x; j < a.npasses * 256; j += blockDim.x) s_hist[j] = 0;
+        for (uint32_t j = threadIdx.x; j < radix_hist_span(a.npasses); j += blockDim.x) s_hist[j] = 0;
     {
         // the block's camera from the descriptor table with scalar loads, so the band loads
         // issue at once; the LDS copy of all descriptors (neighbour lookups) overlaps them
@@ -765,7 +780,7 @@ __global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
         }
         if (leader && a.key_hist)
             for (uint32_t p = 0; p < a.npasses; ++p)
-                atomicAdd(&s_hist[p * 256 + ((rkey >> (8 * p)) & 0xFFu)], 1u);
+                atomicAdd(&s_hist[p * 256 + radix_digit(rkey, p, a.npasses)], 1u);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -779,7 +794,7 @@ __global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
     }
     if (a.run_mode && a.key_hist) {
         const gptr<uint32_t> rep = G(a.key_hist + (blockIdx.x % kHistReps) * 1024u);
-        for (uint32_t j = threadIdx.x; j < a.npasses * 256; j += blockDim.x)
+        for (uint32_t j = threadIdx.x; j < radix_hist_span(a.npasses); j += blockDim.x)
             if (s_hist[j])
                 __hip_atomic_fetch_add(rep + j, s_hist[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -916,7 +931,7 @@ __device__ __forceinline__ void mark_and_count(const FrameArgs& a, uint32_t* mar
                 after ? ((1ull << (__ffsll((long long)after) - 1)) - 1ull) : ~0ull;
             const uint32_t rl = (uint32_t)__popcll(vm & ~ltm & upto);
             for (uint32_t p = 0; p < a.npasses; ++p)
-                atomicAdd(&s_hist[p * 256 + ((hkey >> (8 * p)) & 0xFFu)], rl);
+                atomicAdd(&s_hist[p * 256 + radix_digit(hkey, p, a.npasses)], rl);
         }
     }
 }
@@ -925,7 +940,7 @@ __device__ __forceinline__ void flush_hist(const FrameArgs& a, uint32_t* s_hist)
     if (!a.key_hist) return;
     __syncthreads();
     const gptr<uint32_t> rep = G(a.key_hist + (blockIdx.x % kHistReps) * 1024u);
-    for (uint32_t j = threadIdx.x; j < a.npasses * 256; j += blockDim.x)
+    for (uint32_t j = threadIdx.x; j < radix_hist_span(a.npasses); j += blockDim.x)
         if (s_hist[j])
             __hip_atomic_fetch_add(rep + j, s_hist[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -980,7 +995,7 @@ __global__ __launch_bounds__(1024) void k_emit(FrameArgs a) {
     const gptr<const CamDesc> cams = G(cam_table(a));
     const bool hist = a.key_hist && !a.run_mode;  // (run mode: k_mask counted the run keys)
     if (hist)
-        for (uint32_t i = threadIdx.x; i < a.npasses * 256; i += blockDim.x) s_hist[i] = 0;
+        for (uint32_t i = threadIdx.x; i < radix_hist_span(a.npasses); i += blockDim.x) s_hist[i] = 0;
     if (a.fused_prefix) prefix_partials(a, s, s_red);
     // the segment's geometry and the thread's item source, loaded before the barrier
     const uint32_t i = threadIdx.x;
@@ -1738,7 +1753,7 @@ __global__ __launch_bounds__(256) void k_sort_hist(const uint32_t* __restrict__ 
             if (!vm) break;
             const uint32_t nv = (uint32_t)__popcll(vm);
             for (uint32_t p = 0; p < npasses; ++p) {
-                const uint32_t d = (k[q] >> (8 * p)) & 0xFFu;
+                const uint32_t d = radix_digit(k[q], p, npasses);
                 const uint32_t pd = __shfl_up(d, 1, 64);
                 const bool leader = (uint32_t)lane < nv && (lane == 0 || pd != d);
                 const unsigned long long lm = __ballot(leader);
@@ -1752,7 +1767,7 @@ __global__ __launch_bounds__(256) void k_sort_hist(const uint32_t* __restrict__ 
     }
     __syncthreads();
     uint32_t* rep = hist + (blockIdx.x % kHistReps) * 1024u;
-    for (uint32_t i = threadIdx.x; i < npasses * 256; i += 256)
+    for (uint32_t i = threadIdx.x; i < radix_hist_span(npasses); i += 256)
         if (s_h[i]) atomicAdd(&rep[i], s_h[i]);
 }
 
@@ -1770,11 +1785,27 @@ __device__ __forceinline__ uint32_t digit_base(const uint32_t* ghist, uint32_t* 
     return block_exclusive_scan(v, total, s_wave);
 }
 
-// Stable scatter of one 8-bit digit.  Tile = 256 threads x PT keys: wave w owns keys
+// the same for a 512-digit pass: thread t holds digits 2t and 2t+1
+__device__ __forceinline__ void digit_base512(const uint32_t* ghist, uint32_t* s_wave, uint32_t* s_base) {
+    const uint32_t d = 2u * threadIdx.x;
+    uint32_t v0 = 0, v1 = 0;
+#pragma unroll
+    for (int r = 0; r < kHistReps; ++r) {
+        v0 += ghist[r * 1024 + d];
+        v1 += ghist[r * 1024 + d + 1];
+    }
+    uint32_t total;
+    const uint32_t e = block_exclusive_scan(v0 + v1, total, s_wave);
+    s_base[d] = e;
+    s_base[d + 1] = e + v0;
+}
+
+// Stable scatter of one 8-bit (NB = 256) or 9-bit (NB = 512, the last pass of a 25-bit batch key)
+// digit.  Tile = 256 threads x PT keys: wave w owns keys
 // [w*64*PT, (w+1)*64*PT) of the tile in slot-major order (slot j, lane l -> w*64*PT + j*64 + l),
 // so ranking the slots in order with wave ballots keeps the sort stable.  Per-digit tile offsets
 // come from a decoupled look-back over epoch-tagged {flag, count} granules.
-template <int PT>
+template <int PT, int NB>
 __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
     uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, const uint32_t* __restrict__ count,
@@ -1801,9 +1832,10 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
         return;
     }
     __shared__ uint32_t s_fstart[kMaxCams + 1];
-    __shared__ uint32_t s_cnt[4][256];
-    __shared__ uint32_t s_base[256];
-    __shared__ uint32_t s_excl[256];
+    constexpr int R = NB / 256;  // digits per thread in the offset phase
+    __shared__ uint32_t s_cnt[4][NB];
+    __shared__ uint32_t s_base[NB];
+    __shared__ uint32_t s_excl[NB];
     __shared__ uint32_t s_wave[4];
     __shared__ uint32_t s_tile, s_epoch;
     const uint32_t n = *count;
@@ -1817,11 +1849,14 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
     const bool add_frame = nframes > 1 && vin == nullptr && fstart != nullptr;
     if (add_frame) load_fstart(s_fstart, fstart, nframes);
     // the digit bases do not depend on the tile
-    s_base[threadIdx.x] = digit_base(ghist, s_wave);
+    if constexpr (NB == 256)
+        s_base[threadIdx.x] = digit_base(ghist, s_wave);
+    else
+        digit_base512(ghist, s_wave, s_base);
     for (bool first = true;; first = false) {  // persistent: tiles in ticket order
         if (!first && tk.oneshot) return;
         if (threadIdx.x == 0) s_tile = next_ticket(tile_ctr, tk, epoch_word, s_epoch);
-        for (uint32_t i = threadIdx.x; i < 4 * 256; i += kSortThreads) (&s_cnt[0][0])[i] = 0;
+        for (uint32_t i = threadIdx.x; i < 4 * NB; i += kSortThreads) (&s_cnt[0][0])[i] = 0;
         __syncthreads();
         const uint32_t tile = s_tile, epoch = s_epoch;
         if (tile >= ntiles) return;  // block-uniform
@@ -1840,7 +1875,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
         for (int j = 0; j < PT; ++j) {
             const uint32_t idx = wbase + j * 64 + lane;
             const bool ok = idx < n;
-            const uint32_t d = (key[j] >> shift) & 0xFFu;
+            const uint32_t d = (key[j] >> shift) & (NB - 1u);
             unsigned long long m = __ballot(ok);
             for (uint32_t b = 0; b < dbits; ++b) {
                 const bool bit = (d >> b) & 1u;
@@ -1856,21 +1891,27 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
             __builtin_amdgcn_wave_barrier();
         }
         __syncthreads();
-        const uint32_t d = threadIdx.x;
-        uint32_t tot = 0;
+        uint32_t tot[R], ex[R];
 #pragma unroll
-        for (int ww = 0; ww < 4; ++ww) {
-            const uint32_t c = s_cnt[ww][d];
-            s_cnt[ww][d] = tot;
-            tot += c;
+        for (int r = 0; r < R; ++r) {
+            const uint32_t d = threadIdx.x + 256u * r;
+            tot[r] = 0;
+#pragma unroll
+            for (int ww = 0; ww < 4; ++ww) {
+                const uint32_t c = s_cnt[ww][d];
+                s_cnt[ww][d] = tot[r];
+                tot[r] += c;
+            }
         }
-        s_excl[d] = lookback2_chan(status, gstatus, tile, ntiles, d, tot, epoch, err);
+        lookback2_chans<R>(status, gstatus, tile, ntiles, tot, ex, epoch, err);
+#pragma unroll
+        for (int r = 0; r < R; ++r) s_excl[threadIdx.x + 256u * r] = ex[r];
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < PT; ++j) {
             const uint32_t idx = wbase + j * 64 + lane;
             if (idx < n) {
-                const uint32_t dd = (key[j] >> shift) & 0xFFu;
+                const uint32_t dd = (key[j] >> shift) & (NB - 1u);
                 const uint32_t pos = s_base[dd] + s_excl[dd] + s_cnt[w][dd] + rank[j];
                 kout[pos] = key[j];
                 vout[pos] = val[j];
@@ -2711,14 +2752,15 @@ __global__ __launch_bounds__(64 * WPB) void k_group_runs_big(const uint32_t* __r
     }
 }
 
-size_t voxelize_status_words(uint32_t nmax) {
-    return (size_t)((nmax + kSortThreads * 4 - 1) / (kSortThreads * 4) + 1) * 256;
+size_t voxelize_status_words(uint32_t nmax, uint32_t key_bits) {  // (tiles of >= 4 keys per thread)
+    return (size_t)((nmax + kSortThreads * 4 - 1) / (kSortThreads * 4) + 1) *
+           (radix_wide_last(key_bits) ? 512 : 256);
 }
 size_t voxelize_group_tiles(uint32_t nmax) {
     return (size_t)((nmax + kGroupThreads - 1) / kGroupThreads + 1);
 }
 
-template <int PT>
+template <int PT, int NB>
 static void launch_sort_pass(uint32_t tiles, hipStream_t s, const uint32_t* kin, const uint32_t* vin,
                              uint32_t* kout, uint32_t* vout, const VoxelizeArgs& a, uint32_t p,
                              uint32_t dbits) {
@@ -2726,7 +2768,7 @@ static void launch_sort_pass(uint32_t tiles, hipStream_t s, const uint32_t* kin,
     const bool g = p == 0 && a.grid8 != nullptr;
     const uint64_t nwords = g ? (a.ncells + 31) / 32 : 0;
     const uint32_t gb = g ? grid_blocks(nwords, 256 * 2) : 0;
-    hipLaunchKernelGGL(k_sort_pass<PT>, dim3(tiles + gb), dim3(kSortThreads), 0, s, kin, vin, kout,
+    hipLaunchKernelGGL((k_sort_pass<PT, NB>), dim3(tiles + gb), dim3(kSortThreads), 0, s, kin, vin, kout,
                        vout, a.count, a.hist + 256 * p, a.status, a.sgstatus,
                        reinterpret_cast<uint32_t*>(a.ctrs + kCtrSort0 + p),
                        reinterpret_cast<uint32_t*>(a.ctrs + kCtrEpoch), a.err, 8 * p, dbits, tiles,
@@ -2737,7 +2779,7 @@ static void launch_sort_pass(uint32_t tiles, hipStream_t s, const uint32_t* kin,
 }
 
 hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hook) {
-    const uint32_t npasses = a.key_bits == 0 ? 1u : (a.key_bits + 7) / 8;
+    const uint32_t npasses = radix_passes(a.key_bits);
     const int pt = a.sort_pt == 4 || a.sort_pt == 8 ? a.sort_pt : 16;
     const uint32_t tile = kSortThreads * pt;
     // persistent blocks (ticket loop): at most kPersistBlocks, fewer when the capacity is small
@@ -2757,15 +2799,24 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
     const bool runs = a.run_start != nullptr;  // keys are run keys: sort runs, then expand
     for (uint32_t p = 0; p < npasses; ++p) {
         const uint32_t remaining = a.key_bits > 8 * p ? a.key_bits - 8 * p : 0u;
-        const uint32_t dbits = remaining >= 8 ? 8u : (remaining ? remaining : 1u);
+        // (a 9-bit last digit: radix_wide_last)
+        const bool wide = p + 1 == npasses && remaining == 9;
+        const uint32_t dbits = wide ? 9u : remaining >= 8 ? 8u : (remaining ? remaining : 1u);
         if (sort_tiles) {
             HookScope hs(hook, GDF_KERNEL_SORT);
-            if (pt == 4)
-                launch_sort_pass<4>(sort_tiles, s, kin, vin, kbuf[p & 1], vbuf[p & 1], a, p, dbits);
+            if (wide) {
+                if (pt == 4)
+                    launch_sort_pass<4, 512>(sort_tiles, s, kin, vin, kbuf[p & 1], vbuf[p & 1], a, p, dbits);
+                else if (pt == 8)
+                    launch_sort_pass<8, 512>(sort_tiles, s, kin, vin, kbuf[p & 1], vbuf[p & 1], a, p, dbits);
+                else
+                    launch_sort_pass<16, 512>(sort_tiles, s, kin, vin, kbuf[p & 1], vbuf[p & 1], a, p, dbits);
+            } else if (pt == 4)
+                launch_sort_pass<4, 256>(sort_tiles, s, kin, vin, kbuf[p & 1], vbuf[p & 1], a, p, dbits);
             else if (pt == 8)
-                launch_sort_pass<8>(sort_tiles, s, kin, vin, kbuf[p & 1], vbuf[p & 1], a, p, dbits);
+                launch_sort_pass<8, 256>(sort_tiles, s, kin, vin, kbuf[p & 1], vbuf[p & 1], a, p, dbits);
             else
-                launch_sort_pass<16>(sort_tiles, s, kin, vin, kbuf[p & 1], vbuf[p & 1], a, p, dbits);
+                launch_sort_pass<16, 256>(sort_tiles, s, kin, vin, kbuf[p & 1], vbuf[p & 1], a, p, dbits);
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
         kin = kbuf[p & 1];

@@ -124,7 +124,7 @@ struct VoxelizeArgs {
     uint32_t* out_count;
 };
 hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hook = nullptr);
-size_t voxelize_status_words(uint32_t nmax);
+size_t voxelize_status_words(uint32_t nmax, uint32_t key_bits);
 // capacity (256-key tiles) above which k_group takes its group-id offsets from count + scan
 extern uint32_t g_group_scan_tiles;
 // k_group_runs staging (512 or 2048 points) and in-block group size limit

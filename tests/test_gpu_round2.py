@@ -249,14 +249,21 @@ def _batch(gpu, frames_args, p, **kw):
     return gpu.processFrame(p, **kw)
 
 
-@pytest.mark.parametrize("case", ["vga_b4", "two_cams_b3_codedefaults", "corners_b2_depth3"])
+@pytest.mark.parametrize("case", ["vga_b4", "two_cams_b3_codedefaults", "corners_b2_depth3",
+                                  "vga_b8_runs", "small_b8_points"])
 def test_batched_frames_equal_frame_by_frame(Engine, case):
     """Multi-frame batches (gdf_next_frame_in_batch): every frame's points, keys, voxel means and
     the grid after every frame equal the oracle processing the frames one by one - incl. two
     cameras per frame (cross-camera reads stay inside the frame), code defaults (F=1, rot45,
-    lifetime 1), voxel corners, and batches pipelined over 3 slots."""
+    lifetime 1), voxel corners, and batches pipelined over 3 slots.  Batches of 8 frames at the
+    launch-default grid sort 25-bit keys (22 voxel bits + 3 frame bits) in 3 radix passes with a
+    9-bit last digit: over runs of equal keys (VGA, 2.4 Mi pixels per batch) and over points."""
     if case == "vga_b4":
         p, W, H, ncam, B, nb, depth = ComponentParams(), 640, 480, 1, 4, 3, 1
+    elif case == "vga_b8_runs":
+        p, W, H, ncam, B, nb, depth = ComponentParams(), 640, 480, 1, 8, 2, 2
+    elif case == "small_b8_points":
+        p, W, H, ncam, B, nb, depth = ComponentParams(), 160, 120, 1, 8, 2, 1
     elif case == "two_cams_b3_codedefaults":
         p = ComponentParams.code_defaults()
         p.crop_min, p.crop_max = (-3, -3, -1), (6, 3, 2.5)
@@ -383,6 +390,24 @@ def test_run_mode_small_frames_forced(Engine, monkeypatch):
                               bits(orc.downloadVoxelizedPoints()[:, :3]))
         np.testing.assert_array_equal(gpu.downloadBatchVoxelOccupancyGrid(j),
                                       orc.downloadVoxelOccupancyGrid())
+
+
+@pytest.mark.parametrize("cells,runs", [((0.4, 0.4, 0.25), False), ((0.4, 0.4, 0.25), True),
+                                         ((4.0, 4.0, 0.5), False), ((4.0, 4.0, 0.5), True)])
+def test_wide_last_radix_digit_single_frames(Engine, monkeypatch, cells, runs):
+    """Grids of 17-bit keys (100x100x10 cells: passes of 8 + 9 bits) and 9-bit keys (10x10x5:
+    one 9-bit pass) - points and runs of equal keys, voxel means and grid bit-exact."""
+    if runs:
+        monkeypatch.setenv("GDF_FORCE_RUNS", "1")
+    p = ComponentParams()
+    p.voxel_size = cells
+    gpu, orc = Engine(), OracleFusion(threads=8)
+    cam = synth.make_camera(0, 320, 240)
+    for f in range(2):
+        args = [cam_args(cam, synth.dense_frame(cam, 0, f))]
+        run_fused(gpu, args, p)
+        run_fused(orc, args, p)
+        compare_results(gpu, orc, tag=f"cells {cells} runs={runs} frame {f}")
 
 
 @pytest.mark.gpu
