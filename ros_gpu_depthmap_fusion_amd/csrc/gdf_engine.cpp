@@ -1114,7 +1114,7 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel) {
         const uint32_t h = a.do_flying ? std::min<uint32_t>(a.F, kHalo) : 0u;
         const uint32_t cols = e->max_segw + 2 * h;
         a.band_rowb = ((cols * 2 + 15) / 16 + 1) * 16;
-        a.band_lds = (2 * h + 1) * a.band_rowb + (a.seg_threads * 2) * 4;
+        a.band_lds = (2 * h + 1) * a.band_rowb + (kHalo + a.seg_threads * 2) * 4;
     }
     if (e->debug) {  // (stage bits by global index: halo gaps included)
         e->sl().d_stage.ensure(std::max<size_t>({(size_t)e->sl().n_total, (size_t)e->index_end + sel, 1}));

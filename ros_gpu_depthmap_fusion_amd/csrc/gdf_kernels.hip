@@ -485,12 +485,29 @@ __device__ __forceinline__ bool ring_pass(const P3& u, const P3& d, const P3& l,
     return nz & pass;
 }
 
+// signed column x (>= -h on a row-start segment's own band row: the previous row's end)
+__device__ __forceinline__ P3 band_pt_s(const Band& t, int r, int x, float yn, float scale) {
+    const uint32_t d = *reinterpret_cast<const uint16_t*>(t.b + t.rowoff[r] + 2 * x);
+    const float zz = (float)d * scale;
+    P3 p;
+    p.x = t.xn[x - (int)t.ca] * zz;
+    p.y = yn * zz;
+    p.z = zz;
+    p.v = d != 0u;
+    return p;
+}
+
+// waves of k_mask: every neighbour in the band (kInterior); a row-start wave of a segment with
+// x0 = 0, y >= F: left neighbours of lanes x < i wrap to the previous row's end, staged in front
+// of the pixel's band row (kRowStart); anything else reads the wrapping neighbours globally
+constexpr int kGeneral = 0, kInterior = 1, kRowStart = 2;
+
 // Stage bits of pixel (x, y) of camera k (band row h = the pixel's row).  Rings are evaluated
 // without per-lane early exit (the reference's first-failure return only decides the same AND);
 // the wave leaves the ring loop once none of its lanes is still valid.
 // FT > 0: the ring count F as a compile-time constant (the launch default F = 4): unrolled rings,
 // no per-ring loop bookkeeping; FT = 0: a.F at run time.
-template <bool ROT45, bool INTERIOR, uint32_t FT>
+template <bool ROT45, int MODE, uint32_t FT>
 __device__ __forceinline__ uint32_t depth_bits(const FrameArgs& a, const CamDesc* cams, int k,
                                                const Band& t, const float* s_yn, uint32_t x,
                                                uint32_t y, bool in) {
@@ -513,7 +530,8 @@ __device__ __forceinline__ uint32_t depth_bits(const FrameArgs& a, const CamDesc
             fly = fly & (x + i <= c.W - 1) & (y + i <= c.H - 1);  // bounds (:60)
             const int ii = (int)i;
             const int64_t gw = (int64_t)i * c.W;
-            // INTERIOR (wave-uniform: every lane has x >= F, y >= F, F <= h): all in the band
+            // kInterior (wave-uniform: every lane has x >= F, y >= F, F <= h): all in the band
+            constexpr bool INTERIOR = MODE != kGeneral;
             const bool L = INTERIOR || ii <= h;  // ring inside the band (uniform)
             const bool yw = !INTERIOR && y < i;  // up neighbours leave the camera (uniform)
             const bool xw = !INTERIOR && x < i;  // left neighbours wrap to the previous row
@@ -523,7 +541,10 @@ __device__ __forceinline__ uint32_t depth_bits(const FrameArgs& a, const CamDesc
             n0 = (L && !yw) ? band_pt(t, h - ii, xs, s_yn[h - ii], scale)
                             : glb_pt(cams, a.ncams, k, g - gw);
             n1 = L ? band_pt(t, h + ii, xs, s_yn[h + ii], scale) : glb_pt(cams, a.ncams, k, g + gw);
-            n2 = (L && !xw) ? band_pt(t, h, xl, s_yn[h], scale) : glb_pt(cams, a.ncams, k, g - ii);
+            if (MODE == kRowStart)  // x < i: pixel (W - i + x, y - 1), its depth before column 0
+                n2 = band_pt_s(t, h, (int)x - ii, x < i ? s_yn[h - 1] : s_yn[h], scale);
+            else
+                n2 = (L && !xw) ? band_pt(t, h, xl, s_yn[h], scale) : glb_pt(cams, a.ncams, k, g - ii);
             n3 = L ? band_pt(t, h, xr, s_yn[h], scale) : glb_pt(cams, a.ncams, k, g + ii);
             fly = fly & ring_pass(n0, n1, n2, n3, a.thr, nax, nay, naz, p.x, p.y, p.z, fly);
             if (ROT45) {  // up (x-i, y-i), down (x+i, y+i), left (x-i, y+i), right (x+i, y-i)
@@ -687,7 +708,13 @@ __global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
         const uint32_t cb = min(c.W, sg.x0 + sg.len + h);
         const uint32_t nrows = 2 * h + 1;
         uint8_t* band = reinterpret_cast<uint8_t*>(s_dyn);
-        float* s_xn = reinterpret_cast<float*>(band + (size_t)nrows * a.band_rowb);
+        // (kHalo floats before s_xn: the ray factors of the last h columns, s_xn[-j] = xn[W - j],
+        // read by the left neighbours that wrap to the previous row's end)
+        float* s_xn = reinterpret_cast<float*>(band + (size_t)nrows * a.band_rowb) + kHalo;
+        // A row-start segment (x0 = 0, rows y >= h, W >= h): the pixel's own band row also stages
+        // the h pixels before column 0 in linear order - the previous row's end, which the
+        // reference's linear index x - i reaches for x < i (filter_flying_pixels.glsl:63-73)
+        const bool wrap = a.do_flying && sg.x0 == 0 && sg.y >= (uint32_t)h && c.W >= (uint32_t)h && h > 0;
         // stage the band: 16-byte chunks, the row's first chunk aligned down (same 16-B line as
         // a needed byte, so never outside the allocation's pages); all loads before any store
         typedef uint32_t u4v __attribute__((ext_vector_type(4)));
@@ -700,8 +727,10 @@ __global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
         uintptr_t a16 = 0, first = 0;
         const int gy = (int)sg.y - h + (int)r;
         const bool rok = r < nrows && gy >= 0 && gy < (int)c.H;
+        uintptr_t col0 = 0;  // address of column ca
         if (rok) {
-            first = dbase + 2 * ((uintptr_t)gy * c.W + ca);
+            col0 = dbase + 2 * ((uintptr_t)gy * c.W + ca);
+            first = col0 - (wrap && r == (uint32_t)h ? 2 * (uintptr_t)h : 0);
             const uintptr_t last = dbase + 2 * ((uintptr_t)gy * c.W + cb);  // exclusive
             a16 = first & ~(uintptr_t)15;
             n16 = min((uint32_t)((last - a16 + 15) / 16), nch);
@@ -717,6 +746,8 @@ __global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
             const int gyi = (int)sg.y - h + (int)i;
             s_yn[i] = (gyi >= 0 && gyi < (int)c.H) ? G(c.yn)[gyi] : 0.0f;
         }
+        float xwv = 0.0f;
+        if (wrap && i < (uint32_t)h) xwv = G(c.xn)[c.W - 1 - i];
         load_cams(a, s_cams);
         if (rok) {
 #pragma unroll
@@ -726,7 +757,7 @@ __global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
             }
         }
         if (lane == 0 && r < nrows)  // rows outside the camera: any in-bounds offset (never live)
-            s_rowoff[r] = (int)(r * a.band_rowb) - 2 * (int)ca + (rok ? (int)(first - a16) : 0);
+            s_rowoff[r] = (int)(r * a.band_rowb) - 2 * (int)ca + (rok ? (int)(col0 - a16) : 0);
         // bands taller than the block's waves (few waves, big F): remaining rows, plain loop
         for (uint32_t rr = (uint32_t)nwaves + r; rr < nrows; rr += (uint32_t)nwaves) {
             const int gy2 = (int)sg.y - h + (int)rr;
@@ -734,7 +765,7 @@ __global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
             uintptr_t f2 = 0, b2 = 0;
             if (ok2) {
                 f2 = dbase + 2 * ((uintptr_t)gy2 * c.W + ca);
-                b2 = f2 & ~(uintptr_t)15;
+                b2 = (f2 - (wrap && rr == (uint32_t)h ? 2 * (uintptr_t)h : 0)) & ~(uintptr_t)15;
                 const uint32_t m16 = min((uint32_t)((dbase + 2 * ((uintptr_t)gy2 * c.W + cb) - b2 + 15) / 16), nch);
                 for (uint32_t ch = (uint32_t)lane; ch < m16; ch += 64)
                     *reinterpret_cast<u4v*>(band + rr * a.band_rowb + 16 * ch) =
@@ -744,14 +775,17 @@ __global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
         }
         if (ca + i < cb) s_xn[i] = xv0;
         if (ca + i + blockDim.x < cb) s_xn[i + blockDim.x] = xv1;
+        if (wrap && i < (uint32_t)h) s_xn[-1 - (int)i] = xwv;
         __syncthreads();
         const Band t{band, s_xn, s_rowoff, ca, h};
         if (64u * (uint32_t)wid < sg.len) {  // wave-uniform
             const uint32_t xw0 = sg.x0 + 64u * wid;  // x of the wave's lane 0
             if (!a.do_flying || (xw0 >= a.F && sg.y >= a.F && a.F <= (uint32_t)h))
-                bits = depth_bits<ROT45, true, FT>(a, s_cams, sg.k, t, s_yn, sg.x0 + i, sg.y, i < sg.len);
+                bits = depth_bits<ROT45, kInterior, FT>(a, s_cams, sg.k, t, s_yn, sg.x0 + i, sg.y, i < sg.len);
+            else if (!ROT45 && wrap && a.F <= (uint32_t)h)  // (wrap: y >= h = F)
+                bits = depth_bits<ROT45, kRowStart, FT>(a, s_cams, sg.k, t, s_yn, sg.x0 + i, sg.y, i < sg.len);
             else
-                bits = depth_bits<ROT45, false, FT>(a, s_cams, sg.k, t, s_yn, sg.x0 + i, sg.y, i < sg.len);
+                bits = depth_bits<ROT45, kGeneral, FT>(a, s_cams, sg.k, t, s_yn, sg.x0 + i, sg.y, i < sg.len);
             if (a.dbg && i < sg.len) G(a.dbg)[sg.item0 + i] = (uint8_t)bits;
             if (a.run_mode && (bits & 4u)) {  // the voxel key k_emit will compute (same f32 ops)
                 const CamDesc& cd = s_cams[sg.k];
