@@ -130,3 +130,57 @@ def test_two_rank_fused_cloud_hip_batch(tmp_path, F):
     for r in range(world):
         np.testing.assert_array_equal(np.load(tmp_path / f"bgrid_r{r}.npy"),
                                       orc.downloadVoxelOccupancyGrid(), f"rank {r}")
+
+
+def _rank_cfg(rank, world, port, W_, H_, frames, out_dir):
+    """One rank of a C4 / C5-shaped run: launch-default parameters (F = 4, the 400x400x21 grid),
+    camera `rank` at W_ x H_; saves its depth frames for the oracle and its outputs."""
+    import torch.distributed as dist
+    from ros_gpu_depthmap_fusion_amd import build_library, hiprt, multi
+    from ros_gpu_depthmap_fusion_amd.gdf import GPUDepthmapFusion
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    build_library()
+    p = ComponentParams()
+    cams = [synth.make_camera(k, W_, H_) for k in range(world)]
+    eng = GPUDepthmapFusion(0)
+    fr = multi.FusedCloudRank(eng, cams, rank, world, p, dev="cpu")
+    n = W_ * H_
+    for f in range(frames):
+        depth = synth.dense_frame(cams[rank], rank, f)
+        np.save(os.path.join(out_dir, f"depth_r{rank}_f{f}.npy"), depth)
+        d = hiprt.DeviceArray.from_numpy(depth)
+        fr.frame(d.ptr, d.ptr + 2 * (n - fr.Lmax))
+        np.save(os.path.join(out_dir, f"vox_r{rank}_f{f}.npy"), eng.downloadVoxelizedPoints()[:, :3])
+        np.save(os.path.join(out_dir, f"grid_r{rank}_f{f}.npy"), eng.downloadVoxelOccupancyGrid())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("cfg", ["C4", "C5"])
+def test_fused_cloud_survey_configs(tmp_path, cfg):
+    """SURVEY §8(d) C4 (4 x 720p, 4 ranks) and C5 (8 x 4K, 8 ranks) shapes as processes on the
+    one GPU of the box (gloo, host-staged): launch-default parameters, the halo, the key-range
+    all-to-all and the mark union - the ranks' voxel ranges concatenated equal ONE oracle engine
+    over all cameras bit for bit, and every rank's grid equals the oracle's."""
+    from oracle import OracleFusion
+    world, W_, H_, frames = (4, 1280, 720, 2) if cfg == "C4" else (8, 3840, 2160, 1)
+    mp.start_processes(_rank_cfg, args=(world, _free_port(), W_, H_, frames, str(tmp_path)),
+                       nprocs=world, join=True, start_method="spawn")
+    p = ComponentParams()
+    cams = [synth.make_camera(k, W_, H_) for k in range(world)]
+    orc = OracleFusion(threads=8)
+    for f in range(frames):
+        orc.clear()
+        for k, c in enumerate(cams):
+            orc.addDepthmap(np.load(tmp_path / f"depth_r{k}_f{f}.npy"), *c.intrinsics(), c.T_world,
+                            c.T_crop)
+        orc.processFrame(p)
+        want = orc.downloadVoxelizedPoints()[:, :3]
+        got = np.concatenate([np.load(tmp_path / f"vox_r{r}_f{f}.npy") for r in range(world)])
+        assert len(got) == len(want) > 0, f"{cfg} frame {f}"
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), f"{cfg} frame {f}"
+        g = orc.downloadVoxelOccupancyGrid()
+        for r in range(world):
+            np.testing.assert_array_equal(np.load(tmp_path / f"grid_r{r}_f{f}.npy"), g,
+                                          f"{cfg} frame {f} rank {r}")
