@@ -81,7 +81,7 @@ def test_two_rank_fused_cloud_hip(tmp_path, F):
                                           orc.downloadVoxelOccupancyGrid(), f"frame {f} rank {r}")
 
 
-def _rank_batch(rank, world, port, F, out_dir):
+def _rank_batch(rank, world, port, F, out_dir, nf=FRAMES):
     import torch.distributed as dist
     from ros_gpu_depthmap_fusion_amd import build_library, hiprt, multi
     from ros_gpu_depthmap_fusion_amd.gdf import GPUDepthmapFusion
@@ -93,32 +93,33 @@ def _rank_batch(rank, world, port, F, out_dir):
     eng = GPUDepthmapFusion(0)
     fr = multi.FusedCloudRank(eng, cams, rank, world, p, dev="cpu")
     n = W * H
-    ds = [hiprt.DeviceArray.from_numpy(synth.dense_frame(cams[rank], rank, f)) for f in range(FRAMES)]
+    ds = [hiprt.DeviceArray.from_numpy(synth.dense_frame(cams[rank], rank, f)) for f in range(nf)]
     fr.batch([d.ptr for d in ds], [d.ptr + 2 * (n - fr.Lmax) for d in ds])
     vox = eng.downloadVoxelizedPoints()[:, :3]
     _, vs = eng.batch_ranges()
-    for f in range(FRAMES):
+    for f in range(nf):
         np.save(os.path.join(out_dir, f"bvox_r{rank}_f{f}.npy"), vox[vs[f]:vs[f + 1]])
     np.save(os.path.join(out_dir, f"bgrid_r{rank}.npy"), eng.downloadVoxelOccupancyGrid())
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("F", [0, 4])
-def test_two_rank_fused_cloud_hip_batch(tmp_path, F):
+@pytest.mark.parametrize("F,nf", [(0, FRAMES), (4, FRAMES), (4, 8)])
+def test_two_rank_fused_cloud_hip_batch(tmp_path, F, nf):
     """FusedCloudRank.batch: the three frames of each rank in one launch chain and one exchange
     (a halo per frame, the frames' marks in one all-gather + one batched grid update, the
     (point, frame | key) lists partitioned by key range): per frame, the ranks' voxel ranges
     concatenated equal one oracle engine over both cameras, and the grid after the batch equals
-    the oracle's after the three frames - bit for bit."""
+    the oracle's after the three frames - bit for bit.  8 frames: (frame | key) keys of 25 bits,
+    sorted by gdf_voxelize_points in 3 passes with a 9-bit last digit."""
     from oracle import OracleFusion
     world = 2
-    mp.start_processes(_rank_batch, args=(world, _free_port(), F, str(tmp_path)), nprocs=world,
+    mp.start_processes(_rank_batch, args=(world, _free_port(), F, str(tmp_path), nf), nprocs=world,
                        join=True, start_method="spawn")
     p = params(F)
     cams = [synth.make_camera(k, W, H) for k in range(world)]
     orc = OracleFusion(threads=4)
-    for f in range(FRAMES):
+    for f in range(nf):
         orc.clear()
         for k, c in enumerate(cams):
             orc.addDepthmap(synth.dense_frame(c, k, f), *c.intrinsics(), c.T_world, c.T_crop)
