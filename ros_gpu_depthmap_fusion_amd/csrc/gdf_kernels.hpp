@@ -40,6 +40,8 @@ inline size_t seg_offsets_words(uint32_t segs) {
 // the compaction kernels (0: k_mask, 1: k_emit, 2/4/5: k_sel<8/4/16>, 3: none) as launched for
 // `rot45` and flying-pixel rings F (0: no filter) (graph node lookup)
 const void* frame_kernel(int which, int rot45, uint32_t F = 0);
+const void* mask_kernel(const FrameArgs& a);  // the compaction pass-1 kernel launch_frame uses
+extern uint32_t g_mask_px2;
 
 // filter_point_sequence + insert into the rollbuffer ring (w = mask)
 hipError_t launch_ps_filter_insert(const float4* new_pts, uint32_t n, int do_filter, float thr,
