@@ -1508,7 +1508,7 @@ int gdf_create(int device, gdf_engine** out) {
             g_group_scan_tiles = (uint32_t)std::max(1, std::atoi(v));
         if (const char* v = std::getenv("GDF_RUN_STAGE"))  // tuning knob: 512 or 2048
             g_run_stage = (uint32_t)std::max(1, std::atoi(v));
-        if (const char* v = std::getenv("GDF_MASK_PX2"))  // tuning knob
+        if (const char* v = std::getenv("GDF_MASK_PX"))  // tuning knob: pixels per k_mask thread
             g_mask_px2 = (uint32_t)std::atoi(v);
         if (const char* v = std::getenv("GDF_RUN_Q16"))  // tuning knob
             g_run_q16 = (uint32_t)std::atoi(v);

@@ -834,72 +834,75 @@ __global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
     }
 }
 
-// Two pixels per thread, ring by ring in lockstep (F = 4, no rot45): pixel A = x (k_mask's
-// kInterior / kRowStart wave of the first 128 columns of a segment), pixel B = x + 128 (always
-// interior when A's row is).  One wave-uniform ring exit and one exact-fallback ballot per ring
-// serve both pixels; the arithmetic of each pixel is depth_bits' (same operations, same order).
-template <int AMODE>
-__device__ __forceinline__ void depth_bits2(const FrameArgs& a, const CamDesc* cams, int k,
-                                            const Band& t, const float* s_yn, uint32_t xa,
-                                            uint32_t xb, uint32_t y, bool ina, bool inb,
-                                            uint32_t& ba, uint32_t& bb) {
+// PX pixels per thread, ring by ring in lockstep (F = 4, no rot45): pixel j of thread i is
+// x0 + i + j * blockDim (blockDim = 256 / PX).  Pixel 0 is k_mask's kInterior / kRowStart wave
+// of the segment's first columns, the others are interior whenever pixel 0's row is.  One
+// wave-uniform ring exit and the exact-fallback ballots of a ring serve all PX pixels; the
+// arithmetic of each pixel is depth_bits' (same operations, same order).
+template <int AMODE, int PX>
+__device__ __forceinline__ void depth_bits_px(const FrameArgs& a, const CamDesc* cams, int k,
+                                              const Band& t, const float* s_yn, const uint32_t* x,
+                                              uint32_t y, const bool* in, uint32_t* bits) {
     const CamDesc& c = cams[k];
     const int h = t.h;
     const float scale = c.scale;
-    const P3 pa = ina ? band_pt(t, h, xa, s_yn[h], scale) : P3{0.f, 0.f, 0.f, false};
-    const P3 pb = inb ? band_pt(t, h, xb, s_yn[h], scale) : P3{0.f, 0.f, 0.f, false};
-    const bool conva = ina & pa.v, convb = inb & pb.v;
-    bool flya = conva, flyb = convb;
-    {
-        const float ppa = dot3(pa.x, pa.y, pa.z, pa.x, pa.y, pa.z);
-        const float ppb = dot3(pb.x, pb.y, pb.z, pb.x, pb.y, pb.z);
-        flya = flya & !beyond_max_distance(ppa);
-        flyb = flyb & !beyond_max_distance(ppb);
-        const float rra = __builtin_amdgcn_rsqf(ppa), rrb = __builtin_amdgcn_rsqf(ppb);
-        const float nax = -(pa.x * rra), nay = -(pa.y * rra), naz = -(pa.z * rra);
-        const float nbx = -(pb.x * rrb), nby = -(pb.y * rrb), nbz = -(pb.z * rrb);
+    P3 p[PX];
+    bool conv[PX], fly[PX];
+    float nx[PX], ny[PX], nz[PX];
 #pragma unroll
-        for (uint32_t i = 1; i <= 4; ++i) {
-            if (!__ballot(flya | flyb)) break;  // wave-uniform exit
-            flya = flya & (xa + i <= c.W - 1) & (y + i <= c.H - 1);
-            flyb = flyb & (xb + i <= c.W - 1) & (y + i <= c.H - 1);
-            const int ii = (int)i;
-            const P3 a0 = band_pt(t, h - ii, xa, s_yn[h - ii], scale);
-            const P3 a1 = band_pt(t, h + ii, xa, s_yn[h + ii], scale);
-            const P3 a2 = AMODE == kRowStart
-                              ? band_pt_s(t, h, (int)xa - ii, xa < i ? s_yn[h - 1] : s_yn[h], scale)
-                              : band_pt(t, h, xa - i, s_yn[h], scale);
-            const P3 a3 = band_pt(t, h, xa + i, s_yn[h], scale);
-            const P3 b0 = band_pt(t, h - ii, xb, s_yn[h - ii], scale);
-            const P3 b1 = band_pt(t, h + ii, xb, s_yn[h + ii], scale);
-            const P3 b2 = band_pt(t, h, xb - i, s_yn[h], scale);
-            const P3 b3 = band_pt(t, h, xb + i, s_yn[h], scale);
-            flya = flya & ring_pass(a0, a1, a2, a3, a.thr, nax, nay, naz, pa.x, pa.y, pa.z, flya);
-            flyb = flyb & ring_pass(b0, b1, b2, b3, a.thr, nbx, nby, nbz, pb.x, pb.y, pb.z, flyb);
+    for (int j = 0; j < PX; ++j) {
+        p[j] = in[j] ? band_pt(t, h, x[j], s_yn[h], scale) : P3{0.f, 0.f, 0.f, false};
+        conv[j] = in[j] & p[j].v;
+        const float pp = dot3(p[j].x, p[j].y, p[j].z, p[j].x, p[j].y, p[j].z);
+        fly[j] = conv[j] & !beyond_max_distance(pp);
+        const float rr = __builtin_amdgcn_rsqf(pp);
+        nx[j] = -(p[j].x * rr);
+        ny[j] = -(p[j].y * rr);
+        nz[j] = -(p[j].z * rr);
+    }
+#pragma unroll
+    for (uint32_t i = 1; i <= 4; ++i) {
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < PX; ++j) any |= fly[j];
+        if (!__ballot(any)) break;  // wave-uniform exit
+        const int ii = (int)i;
+#pragma unroll
+        for (int j = 0; j < PX; ++j) {
+            fly[j] = fly[j] & (x[j] + i <= c.W - 1) & (y + i <= c.H - 1);
+            const P3 n0 = band_pt(t, h - ii, x[j], s_yn[h - ii], scale);
+            const P3 n1 = band_pt(t, h + ii, x[j], s_yn[h + ii], scale);
+            const P3 n2 = (AMODE == kRowStart && j == 0)
+                              ? band_pt_s(t, h, (int)x[j] - ii, x[j] < i ? s_yn[h - 1] : s_yn[h], scale)
+                              : band_pt(t, h, x[j] - i, s_yn[h], scale);
+            const P3 n3 = band_pt(t, h, x[j] + i, s_yn[h], scale);
+            fly[j] = fly[j] & ring_pass(n0, n1, n2, n3, a.thr, nx[j], ny[j], nz[j], p[j].x, p[j].y,
+                                        p[j].z, fly[j]);
         }
     }
-    bool cropa = true, cropb = true;
-    if (a.do_crop) {
-        const float qax = mrow(c.Tc + 0, pa.x, pa.y, pa.z, 1.0f);
-        const float qay = mrow(c.Tc + 4, pa.x, pa.y, pa.z, 1.0f);
-        const float qaz = mrow(c.Tc + 8, pa.x, pa.y, pa.z, 1.0f);
-        const float qbx = mrow(c.Tc + 0, pb.x, pb.y, pb.z, 1.0f);
-        const float qby = mrow(c.Tc + 4, pb.x, pb.y, pb.z, 1.0f);
-        const float qbz = mrow(c.Tc + 8, pb.x, pb.y, pb.z, 1.0f);
-        cropa = !((qax < a.lo[0]) | (qax > a.hi[0]) | (qay < a.lo[1]) | (qay > a.hi[1]) |
-                  (qaz < a.lo[2]) | (qaz > a.hi[2]));
-        cropb = !((qbx < a.lo[0]) | (qbx > a.hi[0]) | (qby < a.lo[1]) | (qby > a.hi[1]) |
-                  (qbz < a.lo[2]) | (qbz > a.hi[2]));
+#pragma unroll
+    for (int j = 0; j < PX; ++j) {
+        bool crop = true;
+        if (a.do_crop) {
+            const float qx = mrow(c.Tc + 0, p[j].x, p[j].y, p[j].z, 1.0f);
+            const float qy = mrow(c.Tc + 4, p[j].x, p[j].y, p[j].z, 1.0f);
+            const float qz = mrow(c.Tc + 8, p[j].x, p[j].y, p[j].z, 1.0f);
+            crop = !((qx < a.lo[0]) | (qx > a.hi[0]) | (qy < a.lo[1]) | (qy > a.hi[1]) |
+                     (qz < a.lo[2]) | (qz > a.hi[2]));
+        }
+        bits[j] = (uint32_t)conv[j] | ((uint32_t)fly[j] << 1) | ((uint32_t)(fly[j] & crop) << 2);
     }
-    ba = (uint32_t)conva | ((uint32_t)flya << 1) | ((uint32_t)(flya & cropa) << 2);
-    bb = (uint32_t)convb | ((uint32_t)flyb << 1) | ((uint32_t)(flyb & cropb) << 2);
 }
 
-// k_mask with two pixels per thread (x, x + 128) for 256-pixel segments at F = 4 without rot45:
-// 128 threads per segment, the same band in LDS, the same outputs (validity word w from pixel A of
-// wave w, word w + 2 from pixel B; counts, runs, run-key histogram).  No debug stage bits (the
-// engine launches k_mask for those).
-__global__ __launch_bounds__(128) void k_mask2(FrameArgs a) {
+// k_mask with PX pixels per thread (x + j * 256 / PX) for 256-pixel segments at F = 4 without
+// rot45: 256 / PX threads per segment, the same band in LDS, the same outputs (validity word
+// w + j * waves from pixel j of wave w; counts, runs, run-key histogram).  No debug stage bits
+// (the engine launches k_mask for those).
+template <int PX>
+__global__ __launch_bounds__(256 / PX) void k_mask_px(FrameArgs a) {
+    constexpr int NT = 256 / PX, NW = NT / 64;           // threads, waves
+    constexpr int QR = (2 * 4 + 1 + NW - 1) / NW;        // band rows per wave (h = 4)
+    constexpr int QX = (256 + 2 * 4 + NT - 1) / NT;      // ray factors per thread
     __shared__ CamDesc s_cams[kMaxCams];
     __shared__ float s_yn[2 * kHalo + 1];
     __shared__ int s_rowoff[2 * kHalo + 1];
@@ -911,11 +914,15 @@ __global__ __launch_bounds__(128) void k_mask2(FrameArgs a) {
     const uint32_t n = gridDim.x, q8 = n / 8, r8 = n % 8, xcd = blockIdx.x % 8;
     const uint32_t s = xcd * q8 + min(xcd, r8) + blockIdx.x / 8;
     if (a.grid_seq_out && blockIdx.x == 0 && threadIdx.x == 0) *a.grid_seq_out = a.grid_seq;
-    uint32_t bits[2] = {0u, 0u};
-    uint32_t rkey[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
+    uint32_t bits[PX], rkey[PX];
+#pragma unroll
+    for (int j = 0; j < PX; ++j) {
+        bits[j] = 0u;
+        rkey[j] = 0xFFFFFFFFu;
+    }
     const uint32_t i = threadIdx.x;
     if (a.run_mode && a.key_hist)
-        for (uint32_t j = threadIdx.x; j < radix_hist_span(a.npasses); j += blockDim.x) s_hist[j] = 0;
+        for (uint32_t j = threadIdx.x; j < radix_hist_span(a.npasses); j += NT) s_hist[j] = 0;
     {
         const gptr<const CamDesc> gcam = G(cam_table(a));
         const SegGeo sg = seg_geo(gcam, a.ncams, s);
@@ -924,24 +931,24 @@ __global__ __launch_bounds__(128) void k_mask2(FrameArgs a) {
             const float *xn, *yn;
             uint32_t W, H;
         } c = {gcam[sg.k].depth, gcam[sg.k].xn, gcam[sg.k].yn, gcam[sg.k].W, gcam[sg.k].H};
-        const int h = (int)min(a.F, (uint32_t)kHalo);  // (do_flying: the launch checks it)
+        const int h = 4;  // (F = 4: the launch checks it)
         const uint32_t ca = sg.x0 >= (uint32_t)h ? sg.x0 - h : 0u;
         const uint32_t cb = min(c.W, sg.x0 + sg.len + h);
         const uint32_t nrows = 2 * h + 1;
         uint8_t* band = reinterpret_cast<uint8_t*>(s_dyn);
         float* s_xn = reinterpret_cast<float*>(band + (size_t)nrows * a.band_rowb) + kHalo;
-        const bool wrap = sg.x0 == 0 && sg.y >= (uint32_t)h && c.W >= (uint32_t)h && h > 0;
+        const bool wrap = sg.x0 == 0 && sg.y >= (uint32_t)h && c.W >= (uint32_t)h;
         typedef uint32_t u4v __attribute__((ext_vector_type(4)));
         const uintptr_t dbase = reinterpret_cast<uintptr_t>(c.depth);
         const uint32_t nch = a.band_rowb / 16;  // <= 64 (the launch checks it): one chunk per lane
-        // rows wid, wid + 2, ... (<= 5 per wave at h = 4): every load before any store
-        u4v v[5];
-        uintptr_t a16[5], col0[5];
-        uint32_t n16[5];
-        bool rok[5];
+        // rows wid, wid + NW, ...: every load before any store
+        u4v v[QR];
+        uintptr_t a16[QR], col0[QR];
+        uint32_t n16[QR];
+        bool rok[QR];
 #pragma unroll
-        for (int q = 0; q < 5; ++q) {
-            const uint32_t r = (uint32_t)wid + 2u * q;
+        for (int q = 0; q < QR; ++q) {
+            const uint32_t r = (uint32_t)wid + (uint32_t)NW * q;
             const int gy = (int)sg.y - h + (int)r;
             rok[q] = r < nrows && gy >= 0 && gy < (int)c.H;
             n16[q] = 0;
@@ -955,10 +962,10 @@ __global__ __launch_bounds__(128) void k_mask2(FrameArgs a) {
                 if ((uint32_t)lane < n16[q]) v[q] = *(gptr<const u4v>)(a16[q] + 16 * (uintptr_t)lane);
             }
         }
-        float xv[3] = {0.0f, 0.0f, 0.0f};
+        float xv[QX];
 #pragma unroll
-        for (int q = 0; q < 3; ++q)
-            if (ca + i + 128u * q < cb) xv[q] = G(c.xn)[ca + i + 128u * q];
+        for (int q = 0; q < QX; ++q)
+            xv[q] = ca + i + (uint32_t)NT * q < cb ? G(c.xn)[ca + i + (uint32_t)NT * q] : 0.0f;
         if (i < nrows) {
             const int gyi = (int)sg.y - h + (int)i;
             s_yn[i] = (gyi >= 0 && gyi < (int)c.H) ? G(c.yn)[gyi] : 0.0f;
@@ -967,8 +974,8 @@ __global__ __launch_bounds__(128) void k_mask2(FrameArgs a) {
         if (wrap && i < (uint32_t)h) xwv = G(c.xn)[c.W - 1 - i];
         load_cams(a, s_cams);
 #pragma unroll
-        for (int q = 0; q < 5; ++q) {
-            const uint32_t r = (uint32_t)wid + 2u * q;
+        for (int q = 0; q < QR; ++q) {
+            const uint32_t r = (uint32_t)wid + (uint32_t)NW * q;
             if (r < nrows) {
                 if (rok[q] && (uint32_t)lane < n16[q])
                     *reinterpret_cast<u4v*>(band + r * a.band_rowb + 16 * lane) = v[q];
@@ -977,42 +984,47 @@ __global__ __launch_bounds__(128) void k_mask2(FrameArgs a) {
             }
         }
 #pragma unroll
-        for (int q = 0; q < 3; ++q)
-            if (ca + i + 128u * q < cb) s_xn[i + 128u * q] = xv[q];
+        for (int q = 0; q < QX; ++q)
+            if (ca + i + (uint32_t)NT * q < cb) s_xn[i + (uint32_t)NT * q] = xv[q];
         if (wrap && i < (uint32_t)h) s_xn[-1 - (int)i] = xwv;
         __syncthreads();
         const Band t{band, s_xn, s_rowoff, ca, h};
         if (64u * (uint32_t)wid < sg.len) {  // wave-uniform
             const uint32_t xw0 = sg.x0 + 64u * wid;
-            const uint32_t xa = sg.x0 + i, xb = sg.x0 + 128u + i;
-            const bool ina = i < sg.len, inb = 128u + i < sg.len;
-            if (sg.y >= a.F && a.F <= (uint32_t)h && xw0 >= a.F)
-                depth_bits2<kInterior>(a, s_cams, sg.k, t, s_yn, xa, xb, sg.y, ina, inb, bits[0], bits[1]);
-            else if (wrap && a.F <= (uint32_t)h)
-                depth_bits2<kRowStart>(a, s_cams, sg.k, t, s_yn, xa, xb, sg.y, ina, inb, bits[0], bits[1]);
-            else {
-                bits[0] = depth_bits<false, kGeneral, 4>(a, s_cams, sg.k, t, s_yn, xa, sg.y, ina);
-                bits[1] = depth_bits<false, kGeneral, 4>(a, s_cams, sg.k, t, s_yn, xb, sg.y, inb);
+            uint32_t x[PX];
+            bool in[PX];
+#pragma unroll
+            for (int j = 0; j < PX; ++j) {
+                x[j] = sg.x0 + i + (uint32_t)NT * j;
+                in[j] = i + (uint32_t)NT * j < sg.len;
             }
+            if (sg.y >= 4u && xw0 >= 4u)
+                depth_bits_px<kInterior, PX>(a, s_cams, sg.k, t, s_yn, x, sg.y, in, bits);
+            else if (wrap)
+                depth_bits_px<kRowStart, PX>(a, s_cams, sg.k, t, s_yn, x, sg.y, in, bits);
+            else
+#pragma unroll
+                for (int j = 0; j < PX; ++j)
+                    bits[j] = depth_bits<false, kGeneral, 4>(a, s_cams, sg.k, t, s_yn, x[j], sg.y, in[j]);
             if (a.run_mode) {
                 const CamDesc& cd = s_cams[sg.k];
 #pragma unroll
-                for (int q = 0; q < 2; ++q)
-                    if (bits[q] & 4u) {  // the voxel key k_emit will compute (same f32 ops)
-                        const P3 p = band_pt(t, h, q ? xb : xa, s_yn[h], cd.scale);
+                for (int j = 0; j < PX; ++j)
+                    if (bits[j] & 4u) {  // the voxel key k_emit will compute (same f32 ops)
+                        const P3 p = band_pt(t, h, x[j], s_yn[h], cd.scale);
                         const float wx = mrow(cd.Tw + 0, p.x, p.y, p.z, 1.0f);
                         const float wy = mrow(cd.Tw + 4, p.x, p.y, p.z, 1.0f);
                         const float wz = mrow(cd.Tw + 8, p.x, p.y, p.z, 1.0f);
-                        rkey[q] = voxel_key(wx, wy, wz, a.vlo, a.vcs, a.vrcs, a.gmax, a.gs) |
+                        rkey[j] = voxel_key(wx, wy, wz, a.vlo, a.vcs, a.vrcs, a.gmax, a.gs) |
                                   (cd.frame << a.frame_shift);
                     }
             }
         }
     }
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const uint32_t word = (uint32_t)wid + 2u * q;
-        const unsigned long long m = __ballot((bits[q] & 4u) != 0u);
+    for (int j = 0; j < PX; ++j) {
+        const uint32_t word = (uint32_t)wid + (uint32_t)NW * j;
+        const unsigned long long m = __ballot((bits[j] & 4u) != 0u);
         if (lane == 0) {
             G(a.vbits)[(size_t)s * 16 + word] = m;
             s_cnt[word] = (uint32_t)__popcll(m);
@@ -1020,8 +1032,8 @@ __global__ __launch_bounds__(128) void k_mask2(FrameArgs a) {
         if (a.run_mode) {
             const unsigned long long below = m & lanemask_lt();
             const int prev = below ? 63 - __clzll((long long)below) : -1;
-            const uint32_t pkey = __shfl(rkey[q], prev < 0 ? 0 : prev, 64);
-            const bool leader = ((bits[q] & 4u) != 0u) && (prev < 0 || pkey != rkey[q]);
+            const uint32_t pkey = __shfl(rkey[j], prev < 0 ? 0 : prev, 64);
+            const bool leader = ((bits[j] & 4u) != 0u) && (prev < 0 || pkey != rkey[j]);
             const unsigned long long lm = __ballot(leader);
             if (lane == 0) {
                 G(a.wave_runs)[(size_t)s * 16 + word] = (uint32_t)__popcll(lm);
@@ -1029,7 +1041,7 @@ __global__ __launch_bounds__(128) void k_mask2(FrameArgs a) {
             }
             if (leader && a.key_hist)
                 for (uint32_t p = 0; p < a.npasses; ++p)
-                    atomicAdd(&s_hist[p * 256 + radix_digit(rkey[q], p, a.npasses)], 1u);
+                    atomicAdd(&s_hist[p * 256 + radix_digit(rkey[j], p, a.npasses)], 1u);
         }
     }
     __syncthreads();
@@ -1044,7 +1056,7 @@ __global__ __launch_bounds__(128) void k_mask2(FrameArgs a) {
     }
     if (a.run_mode && a.key_hist) {
         const gptr<uint32_t> rep = G(a.key_hist + (blockIdx.x % kHistReps) * 1024u);
-        for (uint32_t j = threadIdx.x; j < radix_hist_span(a.npasses); j += blockDim.x)
+        for (uint32_t j = threadIdx.x; j < radix_hist_span(a.npasses); j += NT)
             if (s_hist[j])
                 __hip_atomic_fetch_add(rep + j, s_hist[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -1572,8 +1584,10 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
             HookScope hs(hook, GDF_KERNEL_MASK);
             const size_t lds = (size_t)a.band_lds;
             const void* km = mask_kernel(a);
-            if (km == reinterpret_cast<const void*>(&k_mask2))
-                hipLaunchKernelGGL(k_mask2, dim3(a.total_segs), dim3(128), lds, s, a);
+            if (km == reinterpret_cast<const void*>(&k_mask_px<2>))
+                hipLaunchKernelGGL(k_mask_px<2>, dim3(a.total_segs), dim3(128), lds, s, a);
+            else if (km == reinterpret_cast<const void*>(&k_mask_px<4>))
+                hipLaunchKernelGGL(k_mask_px<4>, dim3(a.total_segs), dim3(64), lds, s, a);
             else if (km == reinterpret_cast<const void*>(&k_mask<true, 4>))
                 hipLaunchKernelGGL((k_mask<true, 4>), dim3(a.total_segs), dim3(a.seg_threads), lds, s, a);
             else if (km == reinterpret_cast<const void*>(&k_mask<false, 4>))
@@ -1607,15 +1621,16 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
     return hipGetLastError();
 }
 
-// k_mask2 (two pixels per thread) serves 256-pixel segments at F = 4 without rot45 unless
-// g_mask_px2 is cleared (tuning knob GDF_MASK_PX2=0); k_mask everything else.  Measured on MI355X
-// (A/B on one box, dense frames): VGA 8-frame batches 22.1 -> 23.7, 720p 4-frame batches
-// 29.8 -> 32.6, 4K 30.9 -> 32.4 Gpoints/s
-uint32_t g_mask_px2 = 1;
+// k_mask_px (g_mask_px = 2 or 4 pixels per thread) serves 256-pixel segments at F = 4 without
+// rot45 (tuning knob GDF_MASK_PX; 0 or 1: k_mask); k_mask everything else.  Measured on MI355X
+// (A/B on one box, dense frames, 2 pixels per thread vs k_mask): VGA 8-frame batches
+// 22.1 -> 23.7, 720p 4-frame batches 29.8 -> 32.6, 4K 30.9 -> 32.4 Gpoints/s
+uint32_t g_mask_px2 = 2;
 const void* mask_kernel(const FrameArgs& a) {
-    if (g_mask_px2 && a.do_flying && a.F == 4 && !a.rot45 && a.seg_threads == 256 && !a.dbg &&
+    if (g_mask_px2 >= 2 && a.do_flying && a.F == 4 && !a.rot45 && a.seg_threads == 256 && !a.dbg &&
         a.band_rowb <= 64 * 16)
-        return reinterpret_cast<const void*>(&k_mask2);
+        return g_mask_px2 >= 4 ? reinterpret_cast<const void*>(&k_mask_px<4>)
+                               : reinterpret_cast<const void*>(&k_mask_px<2>);
     return frame_kernel(0, a.rot45, a.do_flying ? a.F : 0u);
 }
 
