@@ -145,15 +145,15 @@ def roofline_from(ktimes, kt_steps, mb, pmc_key):
     if slot == "mask" and os.path.exists(sq):
         # k_mask is bound by neither HBM nor MFMA: its VALU issue rate beside the HBM fraction.
         # VALU instructions per wave from the committed SQ counters of this workload
-        # (profiles/pmc_sq.json), one wave per 64 pixels of the launch (mb["mask"] = 3 B per
-        # pixel), a wave64 VALU instruction issues in 2 cycles on a SIMD (MI355X_MICROARCH.md),
-        # 1024 SIMDs at 2.4 GHz.
+        # (profiles/pmc_sq.json), one wave per 64 x (pixels per thread) pixels of the launch
+        # (mb["mask"] = 3 B per pixel), a wave64 VALU instruction issues in 2 cycles on a SIMD
+        # (MI355X_MICROARCH.md), 1024 SIMDs at 2.4 GHz.
         try:
             rec = json.load(open(sq)).get(pmc_key, {}).get("mask")
         except Exception:
             rec = None
         if rec:
-            waves = mb["mask"] / 3.0 / 64.0
+            waves = mb["mask"] / 3.0 / rec.get("pixels_per_wave", 64)
             issue = waves * rec["valu_per_wave"] * 2.0 / (1024 * 2.4e9 * avg_s)
             valu = {"insts_per_wave": rec["valu_per_wave"], "waves_per_launch": round(waves),
                     "issue_frac": round(issue, 4), "wait_frac": rec["wait_frac"],

@@ -18,7 +18,7 @@ import collections
 import csv
 import json
 
-SLOT = {"k_mask": "mask", "k_emit": "emit", "k_sort_pass": "sort", "k_group": "group",
+SLOT = {"k_mask": "mask", "k_mask_px": "mask", "k_emit": "emit", "k_sort_pass": "sort", "k_group": "group",
         "k_group_runs": "group", "k_group_big": "group_big", "k_group_runs_big": "group_big",
         "k_scan_counts": "scan", "k_grid_u8": "grid", "k_grid_u32": "grid", "k_sel": "sel",
         "k_sort_hist": "sort_hist", "k_group_count": "group_count"}
