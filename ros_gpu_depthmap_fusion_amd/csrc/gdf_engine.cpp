@@ -1372,7 +1372,7 @@ void run_fused_frame(gdf_engine* e, int average, uint32_t lifetime) {
         HIPCHK(hipGraphGetNodes(slot->g, nullptr, &nn));
         std::vector<hipGraphNode_t> nodes(nn);
         HIPCHK(hipGraphGetNodes(slot->g, nodes.data(), &nn));
-        const void* fk[6] = {mask_kernel(a), frame_kernel(1, a.rot45),
+        const void* fk[6] = {mask_kernel(a), emit_kernel(a),
                              frame_kernel(2, a.rot45),
                              frame_kernel(3, a.rot45), frame_kernel(4, a.rot45),
                              frame_kernel(5, a.rot45)};  // (the count scans take no FrameArgs)
@@ -1508,6 +1508,8 @@ int gdf_create(int device, gdf_engine** out) {
             g_group_scan_tiles = (uint32_t)std::max(1, std::atoi(v));
         if (const char* v = std::getenv("GDF_RUN_STAGE"))  // tuning knob: 512 or 2048
             g_run_stage = (uint32_t)std::max(1, std::atoi(v));
+        if (const char* v = std::getenv("GDF_EMIT_PX2"))  // tuning knob
+            g_emit_px2 = (uint32_t)std::atoi(v);
         if (const char* v = std::getenv("GDF_MASK_PX"))  // tuning knob: pixels per k_mask thread
             g_mask_px2 = (uint32_t)std::atoi(v);
         if (const char* v = std::getenv("GDF_RUN_Q16"))  // tuning knob

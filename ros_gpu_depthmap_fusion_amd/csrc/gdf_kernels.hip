@@ -1379,6 +1379,125 @@ __global__ __launch_bounds__(1024) void k_emit(FrameArgs a) {
     if (hist) flush_hist(a, s_hist);
 }
 
+// k_emit for 256-pixel segments with two pixels per thread (x, x + 128; 128 threads per
+// segment, k_mask_px's layout: pixel j of wave w is validity word w + 2j): the block's scalar
+// work (camera lookup, counts and run prefixes of the segment's words) is shared by twice the
+// pixels per wave.  Same outputs in the same order as k_emit.
+__global__ __launch_bounds__(128) void k_emit_px2(FrameArgs a) {
+    __shared__ uint32_t s_hist[4 * 256];
+    __shared__ uint32_t s_red[32];
+    __shared__ uint32_t s_mark[1u << kMarkCacheBits];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    constexpr int NW = 2;
+    const uint32_t s = blockIdx.x;
+    for (uint32_t j = threadIdx.x; j < (1u << kMarkCacheBits); j += 128) s_mark[j] = 0xFFFFFFFFu;
+    const gptr<const CamDesc> cams = G(cam_table(a));
+    const bool hist = a.key_hist && !a.run_mode;
+    if (hist)
+        for (uint32_t i = threadIdx.x; i < radix_hist_span(a.npasses); i += 128) s_hist[i] = 0;
+    if (a.fused_prefix) prefix_partials(a, s, s_red);
+    const uint32_t i = threadIdx.x;
+    int k = 0;
+    for (int c = 0; c < a.ncams; ++c)
+        if (cams[c].emit && s >= cams[c].seg0 && s < cams[c].seg0 + cams[c].nseg) k = c;
+    k = __builtin_amdgcn_readfirstlane(k);
+    const uint32_t j = s - cams[k].seg0;
+    const uint32_t y = j / cams[k].nchunk;
+    const uint32_t x0 = (j - y * cams[k].nchunk) * cams[k].segw;
+    const uint32_t len = min(cams[k].segw, cams[k].W - x0);
+    uint64_t m[2];
+    uint32_t dval[2] = {0u, 0u};
+    float xnv[2] = {0.0f, 0.0f};
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        m[q] = G(a.vbits)[(size_t)s * 16 + wid + NW * q];
+        const uint32_t ii = i + 128u * q;
+        if (ii < len) {
+            dval[q] = G(cams[k].depth)[y * cams[k].W + x0 + ii];
+            xnv[q] = G(cams[k].xn)[x0 + ii];
+        }
+    }
+    const float ynv = G(cams[k].yn)[y];
+    // counts (and runs) of the segment's 4 words: the prefix of each of this thread's words
+    uint32_t pc[4], rc[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int w = 0; w < 4; ++w) pc[w] = (uint32_t)__popcll(G(a.vbits)[(size_t)s * 16 + w]);
+    const uint32_t sbase = a.fused_prefix ? 0u : G(a.seg_offsets)[s];
+    uint32_t rbase = 0;
+    if (a.run_mode) {
+        if (!a.fused_prefix)
+            rbase = G(a.seg_offsets)[a.total_segs + s] - G(a.seg_offsets)[a.total_segs];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) rc[w] = G(a.wave_runs)[(size_t)s * 16 + w];
+    }
+    __syncthreads();
+    uint32_t base = sbase;
+    if (a.fused_prefix)
+        for (int w = 0; w < NW; ++w) {
+            base += s_red[w];
+            rbase += s_red[16 + w];
+        }
+    const uint32_t tot = pc[0] + pc[1] + pc[2] + pc[3];
+    const uint32_t rtot = rc[0] + rc[1] + rc[2] + rc[3];
+    if (s == gridDim.x - 1 && threadIdx.x == 0) {
+        *G(a.out_count) = base + tot;
+        if (a.run_mode) {
+            G(a.run_start)[rbase + rtot] = base + tot;
+            *G(a.run_count) = rbase + rtot;
+        }
+    }
+    const uint32_t fr = cams[k].frame;
+    if (a.frame_pt_start && threadIdx.x == 0) {
+        const bool first_of_frame =
+            s == cams[k].seg0 && (k == 0 || !cams[k - 1].emit || cams[k - 1].frame != fr);
+        if (first_of_frame) G(a.frame_pt_start)[fr] = base;
+        if (s == gridDim.x - 1) G(a.frame_pt_start)[a.nframes] = base + tot;
+    }
+    const unsigned long long ltm = lanemask_lt();
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const uint32_t word = (uint32_t)wid + NW * q;
+        uint32_t wpre = 0, rwpre = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            wpre += (uint32_t)w < word ? pc[w] : 0u;
+            rwpre += (uint32_t)w < word ? rc[w] : 0u;
+        }
+        const bool valid = i + 128u * q < len && ((m[q] >> lane) & 1ull);
+        uint32_t key = 0xFFFFFFFFu;
+        if (valid) {
+            const uint32_t pos = base + wpre + (uint32_t)__popcll(m[q] & ltm);
+            const float zz = (float)dval[q] * cams[k].scale;
+            const float px = xnv[q] * zz, py = ynv * zz, pz = zz;
+            const float4 w4 = make_float4(mrow(cams[k].Tw + 0, px, py, pz, 1.0f),
+                                          mrow(cams[k].Tw + 4, px, py, pz, 1.0f),
+                                          mrow(cams[k].Tw + 8, px, py, pz, 1.0f),
+                                          mrow(cams[k].Tw + 12, px, py, pz, 1.0f));
+            gst4(a.out_pts, pos, w4);
+            if (a.do_voxel) {
+                key = voxel_key(w4.x, w4.y, w4.z, a.vlo, a.vcs, a.vrcs, a.gmax, a.gs);
+                G(a.out_coords)[pos] = key;
+            }
+        }
+        if (a.run_mode) {
+            const unsigned long long below = m[q] & ltm;
+            const int prev = below ? 63 - __clzll((long long)below) : -1;
+            const uint32_t pkey = __shfl(key, prev < 0 ? 0 : prev, 64);
+            const bool leader = valid && (prev < 0 || pkey != key);
+            const unsigned long long lm = __ballot(leader);
+            if (leader) {
+                const uint32_t ri = rbase + rwpre + (uint32_t)__popcll(lm & ltm);
+                G(a.run_keys)[ri] = key | (fr << a.frame_shift);
+                G(a.run_start)[ri] = base + wpre + (uint32_t)__popcll(m[q] & ltm);
+            }
+        }
+        if (a.do_voxel)
+            mark_and_count(a, a.marks ? a.marks + (size_t)fr * a.mark_words : nullptr, valid, key,
+                           key | (fr << a.frame_shift), hist ? s_hist : nullptr, s_mark);
+    }
+    if (hist) flush_hist(a, s_hist);
+}
+
 // Selected rollbuffer points (insertSelectedPointSequence + transformPointSequence + crop +
 // applyPointMask + computeVoxelCoords + occupancy marks for the rollbuffer part).  The window is
 // large (10^8 points) and mostly cropped away: each block owns a tile of kSelSegs x blockDim
@@ -1605,7 +1724,10 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
                 return e;
         }
         HookScope hs(hook, GDF_KERNEL_EMIT);
-        hipLaunchKernelGGL(k_emit, dim3(a.total_segs), dim3(a.seg_threads), 0, s, a);
+        if (emit_kernel(a) == reinterpret_cast<const void*>(&k_emit_px2))
+            hipLaunchKernelGGL(k_emit_px2, dim3(a.total_segs), dim3(128), 0, s, a);
+        else
+            hipLaunchKernelGGL(k_emit, dim3(a.total_segs), dim3(a.seg_threads), 0, s, a);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (a.sel_tiles) {  // rollbuffer points: one pass, behind the depth survivors
@@ -1632,6 +1754,14 @@ const void* mask_kernel(const FrameArgs& a) {
         return g_mask_px2 >= 4 ? reinterpret_cast<const void*>(&k_mask_px<4>)
                                : reinterpret_cast<const void*>(&k_mask_px<2>);
     return frame_kernel(0, a.rot45, a.do_flying ? a.F : 0u);
+}
+
+// k_emit_px2 (two pixels per thread) for 256-pixel segments unless g_emit_px2 is cleared (tuning
+// knob GDF_EMIT_PX2=0)
+uint32_t g_emit_px2 = 1;
+const void* emit_kernel(const FrameArgs& a) {
+    if (g_emit_px2 && a.seg_threads == 256) return reinterpret_cast<const void*>(&k_emit_px2);
+    return reinterpret_cast<const void*>(&k_emit);
 }
 
 const void* frame_kernel(int which, int rot45, uint32_t F) {

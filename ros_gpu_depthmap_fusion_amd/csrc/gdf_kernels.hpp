@@ -42,6 +42,8 @@ inline size_t seg_offsets_words(uint32_t segs) {
 const void* frame_kernel(int which, int rot45, uint32_t F = 0);
 const void* mask_kernel(const FrameArgs& a);  // the compaction pass-1 kernel launch_frame uses
 extern uint32_t g_mask_px2;
+const void* emit_kernel(const FrameArgs& a);  // the compaction pass-2 kernel launch_frame uses
+extern uint32_t g_emit_px2;
 
 // filter_point_sequence + insert into the rollbuffer ring (w = mask)
 hipError_t launch_ps_filter_insert(const float4* new_pts, uint32_t n, int do_filter, float thr,
