@@ -11,7 +11,7 @@ import csv
 import json
 
 SLOT = {"k_mask": ("mask", 64), "k_mask_px<2>": ("mask", 128), "k_mask_px<4>": ("mask", 256),
-        "k_emit": ("emit", 64), "k_sort_pass<8, 256>": ("sort", 64),
+        "k_emit_px2": ("emit", 128), "k_emit": ("emit_1px", 64), "k_sort_pass<8, 256>": ("sort", 64),
         "k_sort_pass<8, 512>": ("sort_wide", 64)}
 
 
