@@ -898,16 +898,18 @@ __device__ __forceinline__ void depth_bits_px(const FrameArgs& a, const CamDesc*
 // rot45: 256 / PX threads per segment, the same band in LDS, the same outputs (validity word
 // w + j * waves from pixel j of wave w; counts, runs, run-key histogram).  No debug stage bits
 // (the engine launches k_mask for those).
-template <int PX>
-__global__ __launch_bounds__(256 / PX) void k_mask_px(FrameArgs a) {
-    constexpr int NT = 256 / PX, NW = NT / 64;           // threads, waves
+template <int PX, int SEGW>
+__global__ __launch_bounds__(SEGW / PX) void k_mask_px(FrameArgs a) {
+    constexpr int NT = SEGW / PX, NW = NT / 64;          // threads, waves
+    constexpr int NWORDS = SEGW / 64;                    // validity words of a segment
     constexpr int QR = (2 * 4 + 1 + NW - 1) / NW;        // band rows per wave (h = 4)
-    constexpr int QX = (256 + 2 * 4 + NT - 1) / NT;      // ray factors per thread
+    constexpr int QX = (SEGW + 2 * 4 + NT - 1) / NT;     // ray factors per thread
+    constexpr int QC = (((SEGW + 8) * 2 + 15) / 16 + 1 + 63) / 64;  // 16-B chunks per lane and row
     __shared__ CamDesc s_cams[kMaxCams];
     __shared__ float s_yn[2 * kHalo + 1];
     __shared__ int s_rowoff[2 * kHalo + 1];
-    __shared__ uint32_t s_cnt[4];
-    __shared__ uint32_t s_rcnt[4];
+    __shared__ uint32_t s_cnt[NWORDS];
+    __shared__ uint32_t s_rcnt[NWORDS];
     __shared__ uint32_t s_hist[4 * 256];
     extern __shared__ uint4 s_dyn[];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -940,9 +942,9 @@ __global__ __launch_bounds__(256 / PX) void k_mask_px(FrameArgs a) {
         const bool wrap = sg.x0 == 0 && sg.y >= (uint32_t)h && c.W >= (uint32_t)h;
         typedef uint32_t u4v __attribute__((ext_vector_type(4)));
         const uintptr_t dbase = reinterpret_cast<uintptr_t>(c.depth);
-        const uint32_t nch = a.band_rowb / 16;  // <= 64 (the launch checks it): one chunk per lane
+        const uint32_t nch = a.band_rowb / 16;  // <= 64 QC (the launch checks it)
         // rows wid, wid + NW, ...: every load before any store
-        u4v v[QR];
+        u4v v[QR][QC];
         uintptr_t a16[QR], col0[QR];
         uint32_t n16[QR];
         bool rok[QR];
@@ -959,7 +961,11 @@ __global__ __launch_bounds__(256 / PX) void k_mask_px(FrameArgs a) {
                 const uintptr_t last = dbase + 2 * ((uintptr_t)gy * c.W + cb);
                 a16[q] = first & ~(uintptr_t)15;
                 n16[q] = min((uint32_t)((last - a16[q] + 15) / 16), nch);
-                if ((uint32_t)lane < n16[q]) v[q] = *(gptr<const u4v>)(a16[q] + 16 * (uintptr_t)lane);
+#pragma unroll
+                for (int cq = 0; cq < QC; ++cq) {
+                    const uint32_t ch = (uint32_t)lane + 64u * cq;
+                    if (ch < n16[q]) v[q][cq] = *(gptr<const u4v>)(a16[q] + 16 * (uintptr_t)ch);
+                }
             }
         }
         float xv[QX];
@@ -977,8 +983,12 @@ __global__ __launch_bounds__(256 / PX) void k_mask_px(FrameArgs a) {
         for (int q = 0; q < QR; ++q) {
             const uint32_t r = (uint32_t)wid + (uint32_t)NW * q;
             if (r < nrows) {
-                if (rok[q] && (uint32_t)lane < n16[q])
-                    *reinterpret_cast<u4v*>(band + r * a.band_rowb + 16 * lane) = v[q];
+#pragma unroll
+                for (int cq = 0; cq < QC; ++cq) {
+                    const uint32_t ch = (uint32_t)lane + 64u * cq;
+                    if (rok[q] && ch < n16[q])
+                        *reinterpret_cast<u4v*>(band + r * a.band_rowb + 16 * ch) = v[q][cq];
+                }
                 if (lane == 0)
                     s_rowoff[r] = (int)(r * a.band_rowb) - 2 * (int)ca + (rok[q] ? (int)(col0[q] - a16[q]) : 0);
             }
@@ -1047,10 +1057,10 @@ __global__ __launch_bounds__(256 / PX) void k_mask_px(FrameArgs a) {
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t tt = 0, r = 0;
-        for (int w = 0; w < 4; ++w) tt += s_cnt[w];
+        for (int w = 0; w < NWORDS; ++w) tt += s_cnt[w];
         G(a.seg_counts)[s] = tt;
         if (a.run_mode) {
-            for (int w = 0; w < 4; ++w) r += s_rcnt[w];
+            for (int w = 0; w < NWORDS; ++w) r += s_rcnt[w];
             G(a.seg_counts)[a.total_segs + s] = r;
         }
     }
@@ -1383,18 +1393,19 @@ __global__ __launch_bounds__(1024) void k_emit(FrameArgs a) {
 // segment, k_mask_px's layout: pixel j of wave w is validity word w + 2j): the block's scalar
 // work (camera lookup, counts and run prefixes of the segment's words) is shared by twice the
 // pixels per wave.  Same outputs in the same order as k_emit.
-__global__ __launch_bounds__(128) void k_emit_px2(FrameArgs a) {
+template <int SEGW>
+__global__ __launch_bounds__(SEGW / 2) void k_emit_px2(FrameArgs a) {
     __shared__ uint32_t s_hist[4 * 256];
     __shared__ uint32_t s_red[32];
     __shared__ uint32_t s_mark[1u << kMarkCacheBits];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    constexpr int NW = 2;
+    constexpr int NT = SEGW / 2, NW = NT / 64, NWORDS = SEGW / 64;
     const uint32_t s = blockIdx.x;
-    for (uint32_t j = threadIdx.x; j < (1u << kMarkCacheBits); j += 128) s_mark[j] = 0xFFFFFFFFu;
+    for (uint32_t j = threadIdx.x; j < (1u << kMarkCacheBits); j += NT) s_mark[j] = 0xFFFFFFFFu;
     const gptr<const CamDesc> cams = G(cam_table(a));
     const bool hist = a.key_hist && !a.run_mode;
     if (hist)
-        for (uint32_t i = threadIdx.x; i < radix_hist_span(a.npasses); i += 128) s_hist[i] = 0;
+        for (uint32_t i = threadIdx.x; i < radix_hist_span(a.npasses); i += NT) s_hist[i] = 0;
     if (a.fused_prefix) prefix_partials(a, s, s_red);
     const uint32_t i = threadIdx.x;
     int k = 0;
@@ -1411,7 +1422,7 @@ __global__ __launch_bounds__(128) void k_emit_px2(FrameArgs a) {
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         m[q] = G(a.vbits)[(size_t)s * 16 + wid + NW * q];
-        const uint32_t ii = i + 128u * q;
+        const uint32_t ii = i + (uint32_t)NT * q;
         if (ii < len) {
             dval[q] = G(cams[k].depth)[y * cams[k].W + x0 + ii];
             xnv[q] = G(cams[k].xn)[x0 + ii];
@@ -1419,16 +1430,19 @@ __global__ __launch_bounds__(128) void k_emit_px2(FrameArgs a) {
     }
     const float ynv = G(cams[k].yn)[y];
     // counts (and runs) of the segment's 4 words: the prefix of each of this thread's words
-    uint32_t pc[4], rc[4] = {0u, 0u, 0u, 0u};
+    uint32_t pc[NWORDS], rc[NWORDS];
 #pragma unroll
-    for (int w = 0; w < 4; ++w) pc[w] = (uint32_t)__popcll(G(a.vbits)[(size_t)s * 16 + w]);
+    for (int w = 0; w < NWORDS; ++w) {
+        pc[w] = (uint32_t)__popcll(G(a.vbits)[(size_t)s * 16 + w]);
+        rc[w] = 0u;
+    }
     const uint32_t sbase = a.fused_prefix ? 0u : G(a.seg_offsets)[s];
     uint32_t rbase = 0;
     if (a.run_mode) {
         if (!a.fused_prefix)
             rbase = G(a.seg_offsets)[a.total_segs + s] - G(a.seg_offsets)[a.total_segs];
 #pragma unroll
-        for (int w = 0; w < 4; ++w) rc[w] = G(a.wave_runs)[(size_t)s * 16 + w];
+        for (int w = 0; w < NWORDS; ++w) rc[w] = G(a.wave_runs)[(size_t)s * 16 + w];
     }
     __syncthreads();
     uint32_t base = sbase;
@@ -1437,8 +1451,12 @@ __global__ __launch_bounds__(128) void k_emit_px2(FrameArgs a) {
             base += s_red[w];
             rbase += s_red[16 + w];
         }
-    const uint32_t tot = pc[0] + pc[1] + pc[2] + pc[3];
-    const uint32_t rtot = rc[0] + rc[1] + rc[2] + rc[3];
+    uint32_t tot = 0, rtot = 0;
+#pragma unroll
+    for (int w = 0; w < NWORDS; ++w) {
+        tot += pc[w];
+        rtot += rc[w];
+    }
     if (s == gridDim.x - 1 && threadIdx.x == 0) {
         *G(a.out_count) = base + tot;
         if (a.run_mode) {
@@ -1459,11 +1477,11 @@ __global__ __launch_bounds__(128) void k_emit_px2(FrameArgs a) {
         const uint32_t word = (uint32_t)wid + NW * q;
         uint32_t wpre = 0, rwpre = 0;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
+        for (int w = 0; w < NWORDS; ++w) {
             wpre += (uint32_t)w < word ? pc[w] : 0u;
             rwpre += (uint32_t)w < word ? rc[w] : 0u;
         }
-        const bool valid = i + 128u * q < len && ((m[q] >> lane) & 1ull);
+        const bool valid = i + (uint32_t)NT * q < len && ((m[q] >> lane) & 1ull);
         uint32_t key = 0xFFFFFFFFu;
         if (valid) {
             const uint32_t pos = base + wpre + (uint32_t)__popcll(m[q] & ltm);
@@ -1703,10 +1721,12 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
             HookScope hs(hook, GDF_KERNEL_MASK);
             const size_t lds = (size_t)a.band_lds;
             const void* km = mask_kernel(a);
-            if (km == reinterpret_cast<const void*>(&k_mask_px<2>))
-                hipLaunchKernelGGL(k_mask_px<2>, dim3(a.total_segs), dim3(128), lds, s, a);
-            else if (km == reinterpret_cast<const void*>(&k_mask_px<4>))
-                hipLaunchKernelGGL(k_mask_px<4>, dim3(a.total_segs), dim3(64), lds, s, a);
+            if (km == reinterpret_cast<const void*>(&k_mask_px<2, 256>))
+                hipLaunchKernelGGL((k_mask_px<2, 256>), dim3(a.total_segs), dim3(128), lds, s, a);
+            else if (km == reinterpret_cast<const void*>(&k_mask_px<4, 256>))
+                hipLaunchKernelGGL((k_mask_px<4, 256>), dim3(a.total_segs), dim3(64), lds, s, a);
+            else if (km == reinterpret_cast<const void*>(&k_mask_px<2, 640>))
+                hipLaunchKernelGGL((k_mask_px<2, 640>), dim3(a.total_segs), dim3(320), lds, s, a);
             else if (km == reinterpret_cast<const void*>(&k_mask<true, 4>))
                 hipLaunchKernelGGL((k_mask<true, 4>), dim3(a.total_segs), dim3(a.seg_threads), lds, s, a);
             else if (km == reinterpret_cast<const void*>(&k_mask<false, 4>))
@@ -1724,8 +1744,11 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
                 return e;
         }
         HookScope hs(hook, GDF_KERNEL_EMIT);
-        if (emit_kernel(a) == reinterpret_cast<const void*>(&k_emit_px2))
-            hipLaunchKernelGGL(k_emit_px2, dim3(a.total_segs), dim3(128), 0, s, a);
+        const void* ke = emit_kernel(a);
+        if (ke == reinterpret_cast<const void*>(&k_emit_px2<256>))
+            hipLaunchKernelGGL(k_emit_px2<256>, dim3(a.total_segs), dim3(128), 0, s, a);
+        else if (ke == reinterpret_cast<const void*>(&k_emit_px2<640>))
+            hipLaunchKernelGGL(k_emit_px2<640>, dim3(a.total_segs), dim3(320), 0, s, a);
         else
             hipLaunchKernelGGL(k_emit, dim3(a.total_segs), dim3(a.seg_threads), 0, s, a);
         if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -1743,6 +1766,11 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
     return hipGetLastError();
 }
 
+// 640-pixel segments (single frames under 1 Mi pixels): two pixels per thread only from this many
+// segments (measured on MI355X, A/B on one box: 720p single frames, 1440 segments, 13.7 -> 14.4-14.9
+// Gpoints/s; VGA single frames, 480 segments = 2400 waves of 320 threads, 8.3 -> 7.6-8.1)
+constexpr uint32_t kPx640MinSegs = 1024;
+
 // k_mask_px (g_mask_px = 2 or 4 pixels per thread) serves 256-pixel segments at F = 4 without
 // rot45 (tuning knob GDF_MASK_PX; 0 or 1: k_mask); k_mask everything else.  Measured on MI355X
 // (A/B on one box, dense frames, 2 pixels per thread vs k_mask): VGA 8-frame batches
@@ -1751,16 +1779,23 @@ uint32_t g_mask_px2 = 2;
 const void* mask_kernel(const FrameArgs& a) {
     if (g_mask_px2 >= 2 && a.do_flying && a.F == 4 && !a.rot45 && a.seg_threads == 256 && !a.dbg &&
         a.band_rowb <= 64 * 16)
-        return g_mask_px2 >= 4 ? reinterpret_cast<const void*>(&k_mask_px<4>)
-                               : reinterpret_cast<const void*>(&k_mask_px<2>);
+        return g_mask_px2 >= 4 ? reinterpret_cast<const void*>(&k_mask_px<4, 256>)
+                               : reinterpret_cast<const void*>(&k_mask_px<2, 256>);
+    // (half 720p rows: single frames under 1 Mi pixels with enough segments to fill the chip)
+    if (g_mask_px2 >= 2 && a.do_flying && a.F == 4 && !a.rot45 && a.seg_threads == 640 && !a.dbg &&
+        a.band_rowb <= 2 * 64 * 16 && a.total_segs >= kPx640MinSegs)
+        return reinterpret_cast<const void*>(&k_mask_px<2, 640>);
     return frame_kernel(0, a.rot45, a.do_flying ? a.F : 0u);
 }
+
 
 // k_emit_px2 (two pixels per thread) for 256-pixel segments unless g_emit_px2 is cleared (tuning
 // knob GDF_EMIT_PX2=0)
 uint32_t g_emit_px2 = 1;
 const void* emit_kernel(const FrameArgs& a) {
-    if (g_emit_px2 && a.seg_threads == 256) return reinterpret_cast<const void*>(&k_emit_px2);
+    if (g_emit_px2 && a.seg_threads == 256) return reinterpret_cast<const void*>(&k_emit_px2<256>);
+    if (g_emit_px2 && a.seg_threads == 640 && a.total_segs >= kPx640MinSegs)
+        return reinterpret_cast<const void*>(&k_emit_px2<640>);
     return reinterpret_cast<const void*>(&k_emit);
 }
 
