@@ -565,7 +565,9 @@ def run_secondary(args, params):
     """N = 1 only: the other single-GPU configurations, each with its own roofline."""
     from ros_gpu_depthmap_fusion_amd.gdf import GPUDepthmapFusion
     out = {}
-    steps = max(args.steps, 50)
+    # (at least 200 steps: a 50-step single-frame line times ~2 ms and moves by tens of % with
+    # host launch jitter)
+    steps = max(args.steps, 200)
     warm = max(args.warmup, 10)
     kt = not args.no_kernel_timing
     for name, (W, H, wl, ring, st_steps, B) in {
