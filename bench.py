@@ -230,6 +230,19 @@ class DepthStream:
             self.eng.run_depth_stream(self.scam, pc, first, count)
 
 
+SETTLE_S = 0.25
+
+
+def settle(eng, run_some, seconds=SETTLE_S):
+    """Untimed steps for `seconds` of wall time before the warm-up: the GPU's clocks and power
+    state ramp up under sustained load, and a short timed region (the driver's 20 steps of a
+    batch are ~2 ms) must not start on a GPU that was idle a moment ago."""
+    t = time.perf_counter()
+    while time.perf_counter() - t < seconds:
+        run_some()
+    eng.synchronize()
+
+
 def time_single(st, params, steps, warmup, depth, kernel_timing, pmc_key, batch=1):
     """Steady-state single-GPU line of one DepthStream: prime (every slot's graph captured),
     warm-up, K timed steps (a step = one batch of `batch` frames), then the event-timed pass for
@@ -243,6 +256,7 @@ def time_single(st, params, steps, warmup, depth, kernel_timing, pmc_key, batch=
     # prime: a slot captures its graph on its second steady frame; 2 rounds over the slots + 1
     prime = 2 * depth + 2
     st.run(pc, 0, prime, batch)
+    settle(eng, lambda: st.run(pc, 0, 2 * depth + 2, batch))
     st.run(pc, prime, warmup, batch)
     eng.synchronize()
     t0 = time.perf_counter()
@@ -471,7 +485,11 @@ def time_multi(args, st, params, dist, world, pmc_key):
         torch.cuda.synchronize()
 
     prime = 2 * depth + 2
-    run(0, prime + args.warmup)
+    run(0, prime)
+    # (the settle of time_single, as a fixed step count: every rank must run the same number of
+    # exchanges)
+    run(0, 200)
+    run(prime, args.warmup)
     barrier_sync()
     t0 = time.perf_counter()
     run(prime + args.warmup, args.steps)
