@@ -30,8 +30,12 @@
 extern "C" {
 #endif
 
+/* ABI version: gdf_frame_params and the signatures below are exactly those of this version; a
+ * caller checks gdf_version() against the header it was built with (the Python binding and the
+ * C++ facade do).  0.2: gdf_frame_params.defer_voxelize, frames_per_rank of
+ * gdf_union_occupancy_pairs; 0.3: batched take / sparse per-frame grids. */
 #define GDF_VERSION_MAJOR 0
-#define GDF_VERSION_MINOR 1
+#define GDF_VERSION_MINOR 3
 
 #define GDF_MAX_CAMERAS 16
 
@@ -271,8 +275,11 @@ int gdf_transform_points(gdf_engine* engine, const float* in_points_device,
  * grid updates apply in frame order).  Results: the compacted points / keys / voxel means of all
  * frames back to back, frame f at [point_start[f], point_start[f+1]) and
  * [voxel_start[f], voxel_start[f+1]) (gdf_get_batch_ranges, nframes + 1 entries each); the u8
- * grid after frame f from gdf_download_batch_occupancy_grid.  Not with point sequences, a
- * deferred grid or lifetime > 255. */
+ * grid after frame f from gdf_download_batch_occupancy_grid (the batch's grid update keeps the
+ * frames' grids as sparse snapshots).  Not with point sequences; the grid update is the fused
+ * one (lifetime <= 255), or - deferred voxelize + deferred grid, the multi-GPU exchange -
+ * gdf_voxel_occupancy_grid_batch after gdf_take_occupancy_marks, whose u32 history branch
+ * (lifetime > 255) keeps no per-frame grids (their download fails with GDF_ERR_STATE). */
 int gdf_next_frame_in_batch(gdf_engine* engine);
 int gdf_get_batch_ranges(gdf_engine* engine, uint32_t* point_start, uint32_t* voxel_start,
                          uint32_t capacity, uint32_t* out_frames);
@@ -291,7 +298,9 @@ int gdf_import_occupancy_marks(gdf_engine* engine, const uint32_t* device_bitmas
  * the engine can run the next frames; once the masks of a batch are all-gathered, each frame's
  * union is imported in frame order - mask r of that frame at device_bitmasks + r *
  * rank_stride_words - and followed by its gdf_voxel_occupancy_grid.  Same grids as the per-frame
- * exchange. */
+ * exchange.  A multi-frame batch (gdf_next_frame_in_batch) takes every frame's marks at once -
+ * frame f at device_bitmask + f * words - and needs words >= num_frames * ceil(num_cells/32)
+ * (GDF_ERR_CAPACITY otherwise: a partial take would leave frames' marks set). */
 int gdf_take_occupancy_marks(gdf_engine* engine, uint32_t* device_bitmask, uint64_t words);
 int gdf_import_occupancy_marks_strided(gdf_engine* engine, const uint32_t* device_bitmasks,
                                        uint64_t words, uint32_t num_ranks,
@@ -307,7 +316,8 @@ int gdf_import_occupancy_marks_strided(gdf_engine* engine, const uint32_t* devic
  * pairs + (r * frames_per_rank + f) * record_words, f < nframes <= frames_per_rank (a partial
  * batch of an all-gathered [rank, batch, record] buffer), each read up to its cap
  * (record_words - 1) / 2 - into union_bits[f * words + i] (zeroed first), the input of
- * gdf_voxel_occupancy_grid_batch with one rank. */
+ * gdf_voxel_occupancy_grid_batch with one rank.  Single frames only (GDF_ERR_STATE for a
+ * multi-frame batch: take its marks with gdf_take_occupancy_marks). */
 int gdf_take_occupancy_marks_sparse(gdf_engine* engine, uint32_t* device_bitmask, uint64_t words,
                                     uint32_t* device_pairs, uint32_t cap);
 int gdf_union_occupancy_pairs(gdf_engine* engine, uint32_t* device_union_bitmasks, uint64_t words,

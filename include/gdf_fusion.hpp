@@ -21,12 +21,19 @@
 #include "gdf_segment.h"
 
 // The component calls glMemoryBarrier(GL_ALL_BARRIER_BITS) between the engine calls
-// (component.cpp:164-309, 12 sites); ordering is the HIP stream's here, so without a GL header
-// these are no-ops (SURVEY.md §8(b) "GL leakage into caller").
-#ifndef GL_ALL_BARRIER_BITS
+// (component.cpp:164-309, 12 sites); ordering is the HIP stream's here, so they are no-ops
+// (SURVEY.md §8(b) "GL leakage into caller").  The no-op lives in namespace gdf; a build without
+// any GL header defines GDF_GL_BARRIER_STUB before including this header to also get the global
+// glMemoryBarrier / GL_* names the component's source uses (a GL header, when present, provides
+// them itself - no clash whatever the include order).
+namespace gdf {
+constexpr unsigned int kAllBarrierBits = 0xFFFFFFFFu;
+inline void glMemoryBarrier(unsigned int) {}
+}  // namespace gdf
+#if defined(GDF_GL_BARRIER_STUB) && !defined(GL_ALL_BARRIER_BITS)
 #define GL_ALL_BARRIER_BITS 0xFFFFFFFFu
 #define GL_SHADER_STORAGE_BARRIER_BIT 0x00002000u
-inline void glMemoryBarrier(unsigned int) {}
+using gdf::glMemoryBarrier;
 #endif
 
 namespace gdf {
@@ -45,7 +52,14 @@ struct MeasureTime {
 
 class GPUDepthmapFusion {
 public:
-    explicit GPUDepthmapFusion(int device = 0) : device_(device) { check(gdf_create(device, &h_)); }
+    explicit GPUDepthmapFusion(int device = 0) : device_(device) {
+        int major = -1, minor = -1;  // the library's ABI is the one this header describes
+        gdf_version(&major, &minor);
+        if (major != GDF_VERSION_MAJOR || minor != GDF_VERSION_MINOR)
+            throw std::runtime_error("gdf: libgdf ABI " + std::to_string(major) + "." +
+                                     std::to_string(minor) + " differs from gdf.h");
+        check(gdf_create(device, &h_));
+    }
     ~GPUDepthmapFusion() {
         if (seg_) gdf_seg_destroy(seg_);
         gdf_destroy(h_);

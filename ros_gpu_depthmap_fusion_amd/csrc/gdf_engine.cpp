@@ -223,7 +223,11 @@ struct Slot {
     uint32_t marks_gen = ~0u;
     uint32_t marks_frames = 0;      // frames the zeroed mark buffer covers
     DevBuf d_fstart, d_fvox;        // batch: first point / first voxel of each frame [nframes + 1]
-    DevBuf d_snap;                  // batch: the u8 grid after each frame but the last
+    // batch: sparse snapshots of the u8 grid after each frame but the last (SnapArgs), valid
+    // when this batch's grid update wrote them (snap_blocks: that update's grid size)
+    DevBuf d_snap_idx, d_snap_data, d_snap_cnt;
+    bool snap_valid = false;
+    uint32_t snap_blocks = 0, snap_frames = 0;
     DevBuf d_pcnt, d_poff;          // multi-GPU key-range partition workspace
     DevBuf d_wruns, d_runkeys, d_runstart;  // runs of equal keys
     bool runs_sel = false;          // ... counted in kRunTotal (frame with rollbuffer points)
@@ -353,6 +357,7 @@ struct gdf_engine {
     uint32_t key_bits = 0;
     VoxelParams vp{};
     DevBuf d_grid8, d_hist32, d_out8;
+    DevBuf d_snap_dense;  // a batch frame's grid expanded from its sparse snapshot (download)
     DevBuf d_gridctl;               // GridSeq counters [0] updates done, [1] blocks finished
     uint32_t grid_ticket = 0;       // sequence number of the next grid update
     uint32_t grid_gen = 0;          // bumped when the grid is (re)allocated: slots re-zero marks
@@ -1140,6 +1145,7 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel) {
     a.frame_shift = e->nframes > 1 ? e->key_bits : 0u;
     a.mark_words = mark_words(e);
     e->sl().nframes = e->nframes;
+    e->sl().snap_valid = false;  // (set by this batch's grid update when it keeps the frames' grids)
     if (e->nframes > 1) {
         e->sl().d_fstart.ensure((size_t)(e->nframes + 1) * 4);
         a.frame_pt_start = e->sl().d_fstart.as<uint32_t>();
@@ -1180,6 +1186,22 @@ struct VoxSource {
     const uint32_t* keys = nullptr;
     uint32_t n = 0;
 };
+
+// the slot's sparse snapshot buffers for a grid update of `nblocks` blocks over `nframes` frames
+// (the batch's frames but the last are kept); marks the slot's snapshots valid
+SnapArgs snap_args(gdf_engine* e, uint32_t nblocks, uint32_t nframes) {
+    Slot& q = e->sl();
+    uint32_t W = 0, seg = 0;
+    snap_dims(e->ncells, nblocks, &W, &seg);
+    const size_t entries = (size_t)W * seg * (nframes - 1);
+    q.d_snap_idx.ensure(entries * 4);
+    q.d_snap_data.ensure(entries * 32);
+    q.d_snap_cnt.ensure((size_t)W * (nframes - 1) * 4);
+    q.snap_valid = true;
+    q.snap_blocks = nblocks;
+    q.snap_frames = nframes;
+    return SnapArgs{q.d_snap_idx.as<uint32_t>(), q.d_snap_data.as<uint4>(), q.d_snap_cnt.as<uint32_t>()};
+}
 
 VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime,
                            const VoxSource* src = nullptr) {  // fusion.cpp:1743-1756
@@ -1258,10 +1280,6 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime,
         v.frame_pt_start = v.run_start || src ? nullptr : e->sl().d_fstart.as<uint32_t>();
         e->sl().d_fvox.ensure((size_t)(e->nframes + 1) * 4);
         v.frame_vox_start = e->sl().d_fvox.as<uint32_t>();
-        const uint64_t padded = (e->ncells + 31) / 32 * 32;
-        e->sl().d_snap.ensure((size_t)padded * (e->nframes - 1));
-        v.snapshots = e->sl().d_snap.as<uint8_t>();
-        v.snapshot_bytes = padded;
     }
     if (fused_grid_lifetime >= 0 && !e->sl().group_marks) {  // processFrame: the grid update rides on the first sort pass
         v.grid8 = e->d_grid8.as<uint8_t>();
@@ -1271,6 +1289,7 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime,
         // the ticket was stored by this frame's k_mask (run_frame: grid_seq = grid_ticket)
         v.gseq = e->grid_seq(0, e->sl().d_misc.as<uint32_t>() + kGridTicket);
         e->grid_ticket++;
+        if (e->nframes > 1) v.snap = snap_args(e, fused_grid_blocks(e->ncells), e->nframes);
     }
     return v;
 }
@@ -2106,8 +2125,19 @@ int gdf_download_batch_occupancy_grid(gdf_engine* e, uint32_t frame, uint8_t* ou
         if (!out || cap < e->ncells) fail(GDF_ERR_CAPACITY, "occupancy grid: buffer too small");
         sync_all(e);
         e->sync();
-        const uint8_t* src = frame + 1 == q.nframes ? grid_out_ptr(e)
-                                                    : q.d_snap.as<uint8_t>() + (size_t)frame * ((e->ncells + 31) / 32 * 32);
+        const uint8_t* src = grid_out_ptr(e);
+        if (frame + 1 < q.nframes) {  // the batch's grid update kept sparse snapshots
+            if (!q.snap_valid || frame + 1 >= q.snap_frames)
+                fail(GDF_ERR_STATE, "the batch's grid update kept no per-frame grids (u32 history, "
+                                    "or a deferred grid update that has not run)");
+            e->d_snap_dense.ensure((e->ncells + 31) / 32 * 32);
+            const SnapArgs sn{q.d_snap_idx.as<uint32_t>(), q.d_snap_data.as<uint4>(),
+                              q.d_snap_cnt.as<uint32_t>()};
+            HIPCHK(launch_snap_expand(sn, frame, q.snap_blocks, e->ncells,
+                                      e->d_snap_dense.as<uint8_t>(), e->s()));
+            e->sync();
+            src = e->d_snap_dense.as<uint8_t>();
+        }
         HIPCHK(hipMemcpy(out, src, e->ncells, hipMemcpyDeviceToHost));
     });
 }
@@ -2136,9 +2166,12 @@ int gdf_take_occupancy_marks(gdf_engine* e, uint32_t* bits, uint64_t words) {
     return guarded(e, [&] {
         if (!e->grid_set || !bits) fail(GDF_ERR_STATE, "no voxel grid");
         if (words < (e->ncells + 31) / 32) fail(GDF_ERR_CAPACITY, "mark bitmask too small");
-        // a batch: every frame's marks when the buffer holds them (frame f at f * mark words)
-        const uint64_t nf = e->sl().nframes > 1 && words >= e->sl().nframes * mark_words(e)
-                                ? e->sl().nframes : 1;
+        // a batch: every frame's marks (frame f at f * mark words); taking only some would leave
+        // the others' bits set for the slot's next batch
+        const uint64_t nf = e->sl().nframes;
+        if (nf > 1 && words < nf * mark_words(e))
+            fail(GDF_ERR_CAPACITY, "take marks of a batch: the buffer must hold every frame's "
+                                   "marks (nframes * mark words)");
         HIPCHK(launch_take_marks(marks_ptr(e), mark_words(e) * nf, bits, e->s()));
         e->sl().marks_set = false;
     });
@@ -2150,6 +2183,8 @@ int gdf_take_occupancy_marks_sparse(gdf_engine* e, uint32_t* bits, uint64_t word
     return guarded(e, [&] {
         if (!e->grid_set || !bits || !pairs) fail(GDF_ERR_STATE, "no voxel grid");
         if (words < (e->ncells + 31) / 32) fail(GDF_ERR_CAPACITY, "mark bitmask too small");
+        if (e->sl().nframes > 1)
+            fail(GDF_ERR_STATE, "sparse take of a batch's marks: use gdf_take_occupancy_marks");
         HIPCHK(launch_take_marks_sparse(marks_ptr(e), mark_words(e), bits, pairs, cap, e->s()));
         e->sl().marks_set = false;
     });
@@ -2185,12 +2220,15 @@ int gdf_voxel_occupancy_grid_batch(gdf_engine* e, const uint32_t* bits, uint64_t
         if (e->grid_mode == 0) {  // one pass for the batch
             ensure_misc(e);
             const GridSeq q = e->grid_seq(e->grid_ticket++);
+            const SnapArgs sn = nframes > 1 ? snap_args(e, batch_grid_blocks(e->ncells), nframes)
+                                             : SnapArgs{nullptr, nullptr, nullptr};
             e->timed_on(GDF_KERNEL_GRID, e->s(), [&] {
                 HIPCHK(launch_grid_u8_batch(e->d_grid8.as<uint8_t>(), bits, e->ncells, nranks,
                                             nframes, frame_stride_words, rank_stride_words,
-                                            lifetime, q, e->s()));
+                                            lifetime, q, sn, e->s()));
             });
-        } else {  // general history: frame by frame
+        } else {  // general history: frame by frame (no per-frame grids kept)
+            e->sl().snap_valid = false;
             for (uint32_t f = 0; f < nframes; ++f) {
                 HIPCHK(launch_import_marks(marks_ptr(e), mark_words(e), bits + f * frame_stride_words,
                                            nranks, rank_stride_words, e->s()));

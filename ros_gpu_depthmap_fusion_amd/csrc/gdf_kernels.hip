@@ -1983,21 +1983,52 @@ __device__ __forceinline__ void grid_u8_part(uint4* __restrict__ grid, uint32_t*
     }
 }
 
+// Sparse per-frame grid snapshots of a batch (the u8 grid the reference downloads after every
+// frame, fusion.cpp:1824-1839): the grid after frame f < nframes - 1 is kept as the list of its
+// NON-ZERO 32-cell groups (word index + 32 bytes), written by the grid update itself.  A dense
+// copy per frame would write (B - 1) C bytes per batch (23.5 MB at B = 8 and the launch-default
+// grid) to serve a download that may never come; the groups a launch-default frame keeps
+// non-zero (its last `lifetime` frames' voxels) are ~1 % of them.  Every wave of the update owns a
+// segment of snap.seg entries per frame, compacted by ballot (no atomics); snap.cnt[f * W + w]
+// is wave w's count.  gdf_download_batch_occupancy_grid expands a frame with k_snap_expand.
+__device__ __forceinline__ void snap_layout(uint64_t nwords, uint32_t nblocks, uint32_t& waves,
+                                            uint32_t& seg) {
+    const uint64_t stride = (uint64_t)nblocks * 256u;
+    waves = nblocks * 4u;
+    seg = (uint32_t)((nwords + stride - 1) / stride) * 64u;
+}
+
 // the grid updates of a batch of `nframes` frames, frame f's marks at marks + f * mark_words,
-// applied in frame order in registers (blocks [0, nblocks) of a launch); the grid after frame
-// f < nframes - 1 is also stored at snap + f * snap_stride (the per-frame u8 grid the reference
-// downloads every frame), the last one is the grid itself.  Marks are cleared.
-__device__ __forceinline__ void grid_u8_part_frames(uint4* __restrict__ grid,
-                                                    uint32_t* __restrict__ marks, uint64_t nwords,
-                                                    uint32_t L, uint32_t block, uint32_t nblocks,
-                                                    uint32_t nframes, uint64_t mark_words,
-                                                    uint4* __restrict__ snap,
-                                                    uint64_t snap_stride) {
-    for (uint64_t i = block * (uint64_t)blockDim.x + threadIdx.x; i < nwords;
-         i += (uint64_t)nblocks * blockDim.x) {
-        uint4 v0 = grid[2 * i], v1 = grid[2 * i + 1];
+// applied in frame order in registers (blocks [0, nblocks) of a launch, 256 threads); the grid
+// after frame f < nframes - 1 goes to the sparse snapshots, the last one is the grid itself.
+// Marks are cleared.
+// (mk(f, i): the marks word i of frame f - read and cleared, or OR-ed over ranks)
+template <class Marks>
+__device__ __forceinline__ void grid_u8_frames(uint4* __restrict__ grid, uint64_t nwords,
+                                               uint32_t L, uint32_t block, uint32_t nblocks,
+                                               uint32_t nframes, const Marks& mk,
+                                               const SnapArgs& sn) {
+    __shared__ uint32_t s_sc[4][kMaxCams];  // per wave: snapshot entries so far, per frame
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t W, seg;
+    snap_layout(nwords, nblocks, W, seg);
+    const uint32_t wave = block * 4u + wid;
+    if (lane < (uint32_t)kMaxCams) s_sc[wid][lane] = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint64_t stride = (uint64_t)nblocks * blockDim.x;
+    for (uint64_t i0 = (uint64_t)block * blockDim.x + (threadIdx.x & ~63u); i0 < nwords;
+         i0 += stride) {  // wave-uniform
+        const uint64_t i = i0 + lane;
+        const bool act = i < nwords;
+        uint4 v0 = make_uint4(0u, 0u, 0u, 0u), v1 = v0;
+        if (act) {
+            v0 = grid[2 * i];
+            v1 = grid[2 * i + 1];
+        }
         for (uint32_t f = 0; f < nframes; ++f) {
-            const uint32_t m = marks[f * mark_words + i];
+            const uint32_t m = act ? mk(f, i) : 0u;
             v0.x = grid_word(v0.x, m, L);
             v0.y = grid_word(v0.y, m >> 4, L);
             v0.z = grid_word(v0.z, m >> 8, L);
@@ -2006,15 +2037,81 @@ __device__ __forceinline__ void grid_u8_part_frames(uint4* __restrict__ grid,
             v1.y = grid_word(v1.y, m >> 20, L);
             v1.z = grid_word(v1.z, m >> 24, L);
             v1.w = grid_word(v1.w, m >> 28, L);
-            if (m) marks[f * mark_words + i] = 0u;
-            if (f + 1 < nframes) {
-                snap[f * snap_stride + 2 * i] = v0;
-                snap[f * snap_stride + 2 * i + 1] = v1;
+            if (f + 1 < nframes && sn.idx) {
+                const bool nz = act && ((v0.x | v0.y | v0.z | v0.w | v1.x | v1.y | v1.z | v1.w) != 0u);
+                const unsigned long long b = __ballot(nz);
+                if (b) {  // wave-uniform
+                    const uint32_t base = s_sc[wid][f];
+                    if (nz) {
+                        const uint64_t e = ((uint64_t)f * W + wave) * seg + base +
+                                           (uint32_t)__popcll(b & lanemask_lt());
+                        sn.idx[e] = (uint32_t)i;
+                        sn.data[2 * e] = v0;
+                        sn.data[2 * e + 1] = v1;
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    if (lane == 0) s_sc[wid][f] = base + (uint32_t)__popcll(b);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                }
             }
         }
-        grid[2 * i] = v0;
-        grid[2 * i + 1] = v1;
+        if (act) {
+            grid[2 * i] = v0;
+            grid[2 * i + 1] = v1;
+        }
     }
+    if (sn.idx && lane + 1 < nframes) sn.cnt[(uint64_t)lane * W + wave] = s_sc[wid][lane];
+}
+
+__device__ __forceinline__ void grid_u8_part_frames(uint4* __restrict__ grid,
+                                                    uint32_t* __restrict__ marks, uint64_t nwords,
+                                                    uint32_t L, uint32_t block, uint32_t nblocks,
+                                                    uint32_t nframes, uint64_t mark_words,
+                                                    const SnapArgs& sn) {
+    grid_u8_frames(grid, nwords, L, block, nblocks, nframes,
+                   [&](uint32_t f, uint64_t i) {
+                       const uint32_t m = marks[f * mark_words + i];
+                       if (m) marks[f * mark_words + i] = 0u;
+                       return m;
+                   },
+                   sn);
+}
+
+// frame f's sparse snapshot into a zeroed dense u8 grid: one block per update wave
+__global__ __launch_bounds__(256) void k_snap_expand(const uint32_t* __restrict__ idx,
+                                                     const uint4* __restrict__ data,
+                                                     const uint32_t* __restrict__ cnt, uint32_t f,
+                                                     uint32_t W, uint32_t seg,
+                                                     uint4* __restrict__ out) {
+    const uint32_t w = blockIdx.x;
+    const uint32_t n = cnt[(uint64_t)f * W + w];
+    const uint64_t e0 = ((uint64_t)f * W + w) * seg;
+    for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
+        const uint32_t i = idx[e0 + j];
+        out[2 * (uint64_t)i] = data[2 * (e0 + j)];
+        out[2 * (uint64_t)i + 1] = data[2 * (e0 + j) + 1];
+    }
+}
+
+void snap_dims(uint64_t ncells, uint32_t nblocks, uint32_t* waves, uint32_t* seg) {
+    const uint64_t nwords = (ncells + 31) / 32;
+    const uint64_t stride = (uint64_t)nblocks * 256u;
+    *waves = nblocks * 4u;
+    *seg = (uint32_t)((nwords + stride - 1) / stride) * 64u;
+}
+
+hipError_t launch_snap_expand(const SnapArgs& sn, uint32_t frame, uint32_t nblocks,
+                              uint64_t ncells, uint8_t* out, hipStream_t s) {
+    uint32_t W, seg;
+    snap_dims(ncells, nblocks, &W, &seg);
+    hipError_t e = hipMemsetAsync(out, 0, (ncells + 31) / 32 * 32, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_snap_expand, dim3(W), dim3(256), 0, s, sn.idx, sn.data, sn.cnt, frame, W,
+                       seg, reinterpret_cast<uint4*>(out));
+    return hipGetLastError();
 }
 
 __global__ __launch_bounds__(256) void k_grid_u8(uint4* __restrict__ grid,
@@ -2042,43 +2139,36 @@ hipError_t launch_grid_u8(uint8_t* grid, uint32_t* marks, uint64_t ncells, uint3
 
 // nframes consecutive grid updates in one pass (batched multi-GPU exchange): frame f's marks are
 // the OR over ranks of bits[r * rank_stride + f * frame_stride + word]; the updates are applied
-// in frame order in registers, so the grid equals nframes sequential k_grid_u8 updates
+// in frame order in registers, so the grid equals nframes sequential k_grid_u8 updates; sparse
+// snapshots of the frames but the last as the fused pass writes them
 __global__ __launch_bounds__(256) void k_grid_u8_batch(uint4* __restrict__ grid,
                                                        const uint32_t* __restrict__ bits,
                                                        uint64_t nwords, uint32_t nranks,
                                                        uint32_t nframes, uint64_t frame_stride,
                                                        uint64_t rank_stride, uint32_t L,
-                                                       GridSeq q) {
+                                                       GridSeq q, SnapArgs sn) {
     const uint32_t f0 = grid_seq_enter(q);
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nwords;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        uint4 v0 = grid[2 * i], v1 = grid[2 * i + 1];
-        for (uint32_t f = 0; f < nframes; ++f) {
-            uint32_t m = 0;
-            for (uint32_t r = 0; r < nranks; ++r) m |= bits[r * rank_stride + f * frame_stride + i];
-            v0.x = grid_word(v0.x, m, L);
-            v0.y = grid_word(v0.y, m >> 4, L);
-            v0.z = grid_word(v0.z, m >> 8, L);
-            v0.w = grid_word(v0.w, m >> 12, L);
-            v1.x = grid_word(v1.x, m >> 16, L);
-            v1.y = grid_word(v1.y, m >> 20, L);
-            v1.z = grid_word(v1.z, m >> 24, L);
-            v1.w = grid_word(v1.w, m >> 28, L);
-        }
-        grid[2 * i] = v0;
-        grid[2 * i + 1] = v1;
-    }
+    grid_u8_frames(grid, nwords, L, blockIdx.x, gridDim.x, nframes,
+                   [&](uint32_t f, uint64_t i) {
+                       uint32_t m = 0;
+                       for (uint32_t r = 0; r < nranks; ++r) m |= bits[r * rank_stride + f * frame_stride + i];
+                       return m;
+                   },
+                   sn);
     grid_seq_leave(q, f0, gridDim.x);
 }
+
+uint32_t fused_grid_blocks(uint64_t ncells) { return grid_blocks((ncells + 31) / 32, 256 * 2); }
+uint32_t batch_grid_blocks(uint64_t ncells) { return grid_blocks((ncells + 31) / 32, 256); }
 
 hipError_t launch_grid_u8_batch(uint8_t* grid, const uint32_t* bits, uint64_t ncells,
                                 uint32_t nranks, uint32_t nframes, uint64_t frame_stride,
                                 uint64_t rank_stride, uint32_t lifetime, const GridSeq& q,
-                                hipStream_t s) {
+                                const SnapArgs& snap, hipStream_t s) {
     const uint64_t nwords = (ncells + 31) / 32;
-    hipLaunchKernelGGL(k_grid_u8_batch, dim3(grid_blocks(nwords, 256)), dim3(256), 0, s,
+    hipLaunchKernelGGL(k_grid_u8_batch, dim3(batch_grid_blocks(ncells)), dim3(256), 0, s,
                        reinterpret_cast<uint4*>(grid), bits, nwords, nranks, nframes,
-                       frame_stride, rank_stride, lifetime, q);
+                       frame_stride, rank_stride, lifetime, q, snap);
     return hipGetLastError();
 }
 
@@ -2274,7 +2364,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
     uint32_t* tile_ctr, uint32_t* epoch_word, uint32_t* err, uint32_t shift, uint32_t dbits,
     uint32_t grid_block0, uint4* grid, uint32_t* marks, uint64_t grid_nwords, uint32_t lifetime,
     GridSeq q, uint32_t nframes, uint32_t fshift, const uint32_t* __restrict__ fstart,
-    uint64_t mark_words, uint4* snap, uint64_t snap_stride, uint32_t* qreset) {
+    uint64_t mark_words, SnapArgs snap, uint32_t* qreset) {
     constexpr int kTile = kSortThreads * PT;
     // (first pass: the run-group queue counters start from zero for this voxelize's k_group_runs)
     if (qreset && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -2285,7 +2375,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
         const uint32_t f = grid_seq_enter(q);
         if (nframes > 1)
             grid_u8_part_frames(grid, marks, grid_nwords, lifetime, blockIdx.x - grid_block0,
-                                gridDim.x - grid_block0, nframes, mark_words, snap, snap_stride);
+                                gridDim.x - grid_block0, nframes, mark_words, snap);
         else
             grid_u8_part(grid, marks, grid_nwords, lifetime, blockIdx.x - grid_block0,
                          gridDim.x - grid_block0);
@@ -2402,66 +2492,196 @@ constexpr uint32_t kPersistBlocks = 2048;  // blocks of a persistent sort / grou
 uint32_t g_group_scan_tiles = 1024;
 constexpr int kSmallGroup = 16;  // groups summed by one thread; longer ones by a wave
 
-// acc + comp[0] + comp[S] + ... + comp[(n-1) S], in order (one component chain of a voxel sum; S =
-// 4: AoS float4 points, S = 1: one component's row).  Blocks of 16 values alternate between two
-// register sets: the next block is read while the current one is added, so the LDS latency stays
-// off the dependent chain.  The reads run up to 16 values past n: every LDS buffer read this way
-// carries kChainPad values of padding.
-constexpr uint32_t kChainPad = 16;
+constexpr uint32_t kChainPad = 16;  // LDS padding of staged point buffers
 
-template <int S, int B>
-__device__ __forceinline__ void lds_block(const float* comp, uint32_t k, float (&t)[B]) {
-    if (S == 1) {
+// ---- the voxel sum: the sequential f32 chain, evaluated 64 terms at a time ----------------------
+// The reference sums a voxel's points one after the other (inc/voxelize.h:29-35:
+// s_k = fl(s_{k-1} + x_k), round-to-nearest-even), a dependent chain that cannot be reassociated in
+// general.  It can, however, be evaluated EXACTLY in parallel over stretches where every rounding
+// lands on one fixed grid:
+//   let u be a power of two with s = m u (m integer) and y_k = x_k / u (exact scaling).  If the
+//   exact value v_k = s_{k-1} + x_k lies strictly inside a binade whose ulp is u, then
+//   fl(v_k) = s_{k-1} + u rint(y_k) unless y_k is a tie (fraction exactly 1/2, whose rounding
+//   depends on the parity of s_{k-1}/u); if y_k is an integer and |m + sum| <= 2^24 the sum is
+//   exactly representable, so fl(v_k) = v_k whatever its binade.
+// With u = ulp(s) (binade exponent E = ex - 127, u = 2^(ex - 150)) a row of 64 terms becomes
+// integer arithmetic: t_k = rint(y_k) (int32), an inclusive wave scan P_k = m + t_1 + ... + t_k,
+// and a per-lane validity test - rounding steps need 2^23 < |P_k| < 2^24 (then |v_k| is inside
+// (2^23 u, 2^24 u) since |v_k - P_k u| < u/2), exact steps need |P_k| <= 2^24, ties and
+// |y_k| > 2^24 (inf, NaN) fail.  The first failing lane L ends the stretch: the prefix [b, L) is
+// committed as s = P_{L-1} u (exact), term L is added by one ordinary f32 add (the reference's own
+// operation: a binade crossing, a tie, a NaN ...), and a new stretch starts at L + 1 with the new
+// ulp.  A zero, subnormal-range or non-finite s takes single f32 adds until it leaves that range.
+// The result is bit-identical to the sequential chain for every input (the model and the bit-exact
+// GPU tests: tests/test_gpu_round3.py); a voxel sum grows monotonically for most voxels, so a
+// stretch fails about once per doubling of the sum (~log2(n) extra stretches per voxel).
+__device__ __forceinline__ float bcast_f(float v, uint32_t l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ float uniform_f(float v) {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+// wave64 inclusive sum scan on DPP (row shifts, then the row broadcasts of lanes 15 and 31)
+__device__ __forceinline__ int dpp_iscan(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
+}
+// four independent scans step by step (the DPP hazard gaps of one scan hold the others' steps)
+__device__ __forceinline__ void dpp_iscan4(int (&v)[4]) {
 #pragma unroll
-        for (int q = 0; q < B / 4; ++q) {
-            const float4 v = *reinterpret_cast<const float4*>(comp + k + 4 * q);
-            t[4 * q] = v.x;
-            t[4 * q + 1] = v.y;
-            t[4 * q + 2] = v.z;
-            t[4 * q + 3] = v.w;
+    for (int c = 0; c < 4; ++c) v[c] += __builtin_amdgcn_update_dpp(0, v[c], 0x111, 0xf, 0xf, false);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] += __builtin_amdgcn_update_dpp(0, v[c], 0x112, 0xf, 0xf, false);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] += __builtin_amdgcn_update_dpp(0, v[c], 0x114, 0xf, 0xf, false);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] += __builtin_amdgcn_update_dpp(0, v[c], 0x118, 0xf, 0xf, false);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] += __builtin_amdgcn_update_dpp(0, v[c], 0x142, 0xa, 0xf, false);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] += __builtin_amdgcn_update_dpp(0, v[c], 0x143, 0xc, 0xf, false);
+}
+__device__ __forceinline__ bool spec_ok_s(float s) {  // s admits a stretch: normal, ulp(s) normal
+    const uint32_t ex = ((uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(s)) >> 23) & 255u;
+    return ex >= 24u && ex != 255u;
+}
+// One stretch over lanes [b, nv) from s (spec_ok_s(s)): the failing-lane ballot, P (lane-wise
+// prefix in units of u) and u.  Branch-free (non-short-circuit & / |): no exec-mask splits.
+__device__ __forceinline__ unsigned long long spec_try(float s, float x, uint32_t b, uint32_t nv,
+                                                       int& P, float& u) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t ex = ((uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(s)) >> 23) & 255u;
+    const float scale = __uint_as_float((277u - ex) << 23);  // 2^(150 - ex) = 1 / u
+    u = __uint_as_float((ex - 23u) << 23);
+    const int m = __builtin_amdgcn_readfirstlane((int)(s * scale));
+    const float y = x * scale;
+    const float r = __builtin_rintf(y);
+    const bool in = (lane >= b) & (lane < nv);
+    const bool fin = (__builtin_fabsf(y) <= 16777216.0f) & (__builtin_fabsf(y - r) != 0.5f);
+    P = m + dpp_iscan((in & fin) ? (int)r : 0);
+    const uint32_t aP = (uint32_t)__builtin_abs(P);
+    const bool exact = y == r;
+    const bool ok = fin & ((exact & (aP <= 16777216u)) | (!exact & (aP - 8388609u <= 8388606u)));
+    return __ballot(in & !ok);
+}
+// One component, general path: s + x_b + ... + x_{nv-1} by stretches, with single f32 adds
+// while s is not admissible and at every failing lane.
+__device__ __forceinline__ float chain_row(float s, float x, uint32_t b, uint32_t nv) {
+    while (b < nv) {  // wave-uniform
+        if (!spec_ok_s(s)) {
+            s = uniform_f(s + bcast_f(x, b));
+            ++b;
+            continue;
         }
-    } else {
-#pragma unroll
-        for (int q = 0; q < B; ++q) t[q] = comp[S * (k + q)];
+        int P;
+        float u;
+        const unsigned long long bad = spec_try(s, x, b, nv, P, u);
+        const uint32_t L = bad ? (uint32_t)__builtin_ctzll(bad) : nv;
+        if (L > b) s = uniform_f((float)__builtin_amdgcn_readlane(P, L - 1) * u);
+        if (L >= nv) break;
+        s = uniform_f(s + bcast_f(x, L));
+        b = L + 1;
     }
+    return s;
 }
-
-// (the asm pins the sum here: without it the compiler sinks the additions below later reads and
-// keeps hundreds of values live)
-template <int B>
-__device__ __forceinline__ float add_block(float acc, const float (&t)[B]) {
+// s[c] + x_c of lanes 0..nv-1, in lane order, for the four components of a row of points
+// (wave-uniform s; lanes >= nv ignored).  The common case - one stretch per component - runs the
+// four scans side by side; a component whose stretch fails (a binade crossing, a tie, a zero
+// sum ...) is redone from the row start by chain_row, one component at a time (one copy of the
+// general path: the kernels stay small enough for the instruction cache).
+__device__ __forceinline__ void row_sum4(float (&s)[4], const float4& p, uint32_t nv) {
+    const float x[4] = {p.x, p.y, p.z, p.w};
+    uint32_t redo = 0xFu;
+    if (spec_ok_s(s[0]) && spec_ok_s(s[1]) && spec_ok_s(s[2]) && spec_ok_s(s[3])) {
+        // spec_try for the four components in phases, so their scans interleave
+        const uint32_t lane = threadIdx.x & 63;
+        const bool in = lane < nv;
+        int P[4], m[4];
+        float u[4], y[4], r[4];
+        bool fin[4];
 #pragma unroll
-    for (int q = 0; q < B; ++q) acc = acc + t[q];
-    asm volatile("" : "+v"(acc));
-    return acc;
-}
-
-// blocks of B = 16 values from component rows (S = 1, b128 reads), 8 from AoS points (S = 4: the
-// kernels using them run at 8 waves per SIMD, 64 VGPRs)
-template <int S>
-__device__ __forceinline__ float lds_chain(const float* comp, uint32_t n, float acc) {
-    constexpr int B = S == 1 ? 16 : 8;
-    static_assert(B <= (int)kChainPad, "the read-ahead stays inside the padding");
-    float a[B], b[B];
-    uint32_t k = 0;
-    lds_block<S, B>(comp, 0, a);
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t ex = ((uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(s[c])) >> 23) & 255u;
+            const float scale = __uint_as_float((277u - ex) << 23);
+            u[c] = __uint_as_float((ex - 23u) << 23);
+            m[c] = __builtin_amdgcn_readfirstlane((int)(s[c] * scale));
+            y[c] = x[c] * scale;
+            r[c] = __builtin_rintf(y[c]);
+            fin[c] = (__builtin_fabsf(y[c]) <= 16777216.0f) & (__builtin_fabsf(y[c] - r[c]) != 0.5f);
+            P[c] = (in & fin[c]) ? (int)r[c] : 0;
+        }
+        dpp_iscan4(P);
+        redo = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            P[c] += m[c];
+            const uint32_t aP = (uint32_t)__builtin_abs(P[c]);
+            const bool exact = y[c] == r[c];
+            const bool ok = fin[c] & ((exact & (aP <= 16777216u)) | (!exact & (aP - 8388609u <= 8388606u)));
+            if (__ballot(in & !ok)) redo |= 1u << c;
+            else s[c] = uniform_f((float)__builtin_amdgcn_readlane(P[c], 63) * u[c]);
+        }
+    }
+    if (redo) {
 #pragma unroll 1
-    for (; k + 2 * B <= n; k += 2 * B) {
-        lds_block<S, B>(comp, k + B, b);
-        asm volatile("" ::: "memory");  // (the reads issue before the adds they overlap)
-        __builtin_amdgcn_sched_barrier(0);
-        acc = add_block<B>(acc, a);
-        lds_block<S, B>(comp, k + 2 * B, a);
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        acc = add_block<B>(acc, b);
+        for (uint32_t c = 0; c < 4; ++c) {
+            if (!((redo >> c) & 1u)) continue;
+            const float xc = c == 0 ? x[0] : c == 1 ? x[1] : c == 2 ? x[2] : x[3];
+            const float sc = c == 0 ? s[0] : c == 1 ? s[1] : c == 2 ? s[2] : s[3];
+            const float r = chain_row(sc, xc, 0, nv);
+            s[0] = c == 0 ? r : s[0];
+            s[1] = c == 1 ? r : s[1];
+            s[2] = c == 2 ? r : s[2];
+            s[3] = c == 3 ? r : s[3];
+        }
     }
-    if (k + B <= n) {
-        acc = add_block<B>(acc, a);
-        k += B;
+}
+// The voxel output of lanes 0..3 (component lane): x/y/z divided by the count, w the plain sum.
+__device__ __forceinline__ void store_mean(float* o, const float (&s)[4], uint32_t cnt) {
+    const int lane = threadIdx.x & 63;
+    if (lane < 4) {
+        const float v = lane == 0 ? s[0] : lane == 1 ? s[1] : lane == 2 ? s[2] : s[3];
+        o[lane] = lane < 3 ? v / (float)cnt : v;
     }
-    for (; k < n; ++k) acc = acc + comp[S * k];
-    return acc;
+}
+// A group of cnt points from a float4 AoS LDS buffer (staged groups), rows of 64.
+__device__ __forceinline__ void lds_group_sum(const float4* pts, uint32_t cnt, float (&s)[4]) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll 1
+    for (uint32_t r = 0; r < cnt; r += 64) {
+        const uint32_t nv = min(64u, cnt - r);
+        const float4 p = (uint32_t)lane < nv ? pts[r + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+        row_sum4(s, p, nv);
+    }
+}
+
+// A group's points pts[vals[k]], k in [s, e), gathered in rows of 64 (points mode): the gathers
+// run kAhead rows ahead of the row being summed.
+constexpr int kAhead = 4;
+__device__ __forceinline__ float4 gather_pt(const uint32_t* __restrict__ vals,
+                                            const float4* __restrict__ pts, uint32_t k, uint32_t e) {
+    return k < e ? pts[vals[k]] : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+__device__ __forceinline__ void gather_group_sum(const uint32_t* __restrict__ vals,
+                                                 const float4* __restrict__ pts, uint32_t s,
+                                                 uint32_t e, float (&sum)[4]) {
+    const uint32_t lane = threadIdx.x & 63;
+    float4 r[kAhead];
+#pragma unroll
+    for (int q = 0; q < kAhead; ++q) r[q] = gather_pt(vals, pts, s + 64u * q + lane, e);
+#pragma unroll 1
+    for (uint32_t c = s; c < e; c += 64) {
+        const float4 cur = r[0];
+#pragma unroll
+        for (int q = 0; q + 1 < kAhead; ++q) r[q] = r[q + 1];
+        r[kAhead - 1] = gather_pt(vals, pts, c + 64u * kAhead + lane, e);
+        row_sum4(sum, cur, min(64u, e - c));
+    }
 }
 
 // Group starts per tile of kGroupThreads sorted keys (large frames: the tiles' group-id offsets
@@ -2507,7 +2727,6 @@ __global__ __launch_bounds__(kGroupThreads) __attribute__((amdgpu_waves_per_eu(7
     __shared__ uint32_t s_tile, s_epoch, s_excl, s_nbig, s_nq;
     __shared__ uint32_t s_start[kGroupThreads + 1];
     __shared__ uint32_t s_big[kGroupThreads];
-    __shared__ float4 s_buf[4][kSumChunk + kChainPad];
     __shared__ float4 s_pts[kStagePts + kChainPad];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t n = *count;
@@ -2672,47 +2891,10 @@ __global__ __launch_bounds__(kGroupThreads) __attribute__((amdgpu_waves_per_eu(7
         const uint32_t li = s_big[b];
         const uint32_t g = s_excl + li;
         const uint32_t s = s_start[li], e = s_start[li + 1];
-        float acc = 0.0f;
-        if (e - S0 <= staged) {  // staged: lanes 0..3 run the component chains from LDS
-            if (lane < 4) {
-                const float* comp = reinterpret_cast<const float*>(s_pts) + lane + 4 * (s - S0);
-                acc = lds_chain<4>(comp, e - s, acc);
-                const float fc = (float)(e - s);
-                out[4 * (size_t)g + lane] = lane < 3 ? acc / fc : acc;
-            }
-            continue;
-        }
-        float4 r[kSumChunk / 64];
-#pragma unroll
-        for (int q = 0; q < kSumChunk / 64; ++q) {
-            const uint32_t k = s + q * 64 + lane;
-            r[q] = k < e ? pts[vals[k]] : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-        for (uint32_t c = s; c < e; c += kSumChunk) {
-#pragma unroll
-            for (int q = 0; q < kSumChunk / 64; ++q) s_buf[wid][q * 64 + lane] = r[q];
-            const uint32_t cn = c + kSumChunk;
-#pragma unroll
-            for (int q = 0; q < kSumChunk / 64; ++q) {
-                const uint32_t k = cn + q * 64 + lane;
-                r[q] = k < e ? pts[vals[k]] : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (lane < 4) {
-                const float* comp = reinterpret_cast<const float*>(&s_buf[wid][0]) + lane;
-                const uint32_t m = (e - c) < (uint32_t)kSumChunk ? (e - c) : (uint32_t)kSumChunk;
-                acc = lds_chain<4>(comp, m, acc);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-        if (lane < 4) {
-            const float fc = (float)(e - s);
-            out[4 * (size_t)g + lane] = lane < 3 ? acc / fc : acc;
-        }
+        float sum[4] = {0.f, 0.f, 0.f, 0.f};
+        if (e - S0 <= staged) lds_group_sum(s_pts + (s - S0), e - s, sum);  // staged
+        else gather_group_sum(vals, pts, s, e, sum);
+        store_mean(out + 4 * (size_t)g, sum, e - s);
     }
     __syncthreads();  // LDS reused by the next tile
     }
@@ -2726,8 +2908,7 @@ __global__ __launch_bounds__(256) void k_group_big(const uint32_t* __restrict__ 
                                                    const uint4* __restrict__ bigq,
                                                    const uint32_t* __restrict__ bigcnt,
                                                    uint32_t nblocks, uint32_t bigcap) {
-    __shared__ float4 s_buf[4][kSumChunk + kChainPad];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int wid = threadIdx.x >> 6;
     const uint64_t nslots = (uint64_t)nblocks * bigcap;
     const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     for (uint64_t slot = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wid; slot < nslots;
@@ -2735,46 +2916,9 @@ __global__ __launch_bounds__(256) void k_group_big(const uint32_t* __restrict__ 
         const uint32_t b = (uint32_t)(slot / bigcap), k = (uint32_t)(slot % bigcap);
         if (k >= bigcnt[b]) continue;
         const uint4 q = bigq[slot];
-        const uint32_t g = q.x, s = q.y, e = q.z;
-        float acc = 0.0f;
-        // point indices two chunks ahead, points one chunk ahead of the chunk being summed: the
-        // chain never waits on an index load
-        constexpr int Q = kSumChunk / 64;
-        uint32_t v1[Q], v2[Q];
-        float4 r[Q];
-#pragma unroll
-        for (int qq = 0; qq < Q; ++qq) {
-            const uint32_t k0 = s + qq * 64 + lane;
-            r[qq] = k0 < e ? pts[vals[k0]] : make_float4(0.f, 0.f, 0.f, 0.f);
-            const uint32_t k1 = k0 + kSumChunk, k2 = k0 + 2 * kSumChunk;
-            v1[qq] = k1 < e ? vals[k1] : 0xFFFFFFFFu;
-            v2[qq] = k2 < e ? vals[k2] : 0xFFFFFFFFu;
-        }
-        for (uint32_t c = s; c < e; c += kSumChunk) {
-#pragma unroll
-            for (int qq = 0; qq < Q; ++qq) {
-                s_buf[wid][qq * 64 + lane] = r[qq];
-                r[qq] = v1[qq] != 0xFFFFFFFFu ? pts[v1[qq]] : make_float4(0.f, 0.f, 0.f, 0.f);
-                v1[qq] = v2[qq];
-                const uint32_t k3 = c + 3 * kSumChunk + qq * 64 + lane;
-                v2[qq] = k3 < e ? vals[k3] : 0xFFFFFFFFu;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (lane < 4) {
-                const float* comp = reinterpret_cast<const float*>(&s_buf[wid][0]) + lane;
-                const uint32_t m = (e - c) < (uint32_t)kSumChunk ? (e - c) : (uint32_t)kSumChunk;
-                acc = lds_chain<4>(comp, m, acc);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-        if (lane < 4) {
-            const float fc = (float)(e - s);
-            out[4 * (size_t)g + lane] = lane < 3 ? acc / fc : acc;
-        }
+        float sum[4] = {0.f, 0.f, 0.f, 0.f};
+        gather_group_sum(vals, pts, q.y, q.z, sum);
+        store_mean(out + 4 * (size_t)q.x, sum, q.z - q.y);
     }
 }
 
@@ -2813,16 +2957,7 @@ __device__ __forceinline__ int dpp_max_scan(int v) {  // (values >= -1)
     v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
     return v;
 }
-__device__ __forceinline__ uint32_t dpp_sum_scan(uint32_t x) {
-    int v = (int)x;
-    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
-    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
-    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
-    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
-    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
-    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
-    return (uint32_t)v;
-}
+__device__ __forceinline__ uint32_t dpp_sum_scan(uint32_t x) { return (uint32_t)dpp_iscan((int)x); }
 
 struct RunRec {
     uint32_t ps, len;
@@ -2893,13 +3028,13 @@ __device__ __forceinline__ void run_fetch(RunBatch& bt, uint32_t c, const float4
 
 
 template <int Q>
-__device__ __forceinline__ float wave_stream_sum(const uint32_t* __restrict__ rps,
-                                                 const uint32_t* __restrict__ rlen, uint32_t rs,
-                                                 uint32_t re, const float4* __restrict__ pts,
-                                                 float* s_soa, int* s_mark, uint32_t& npts) {
-    constexpr uint32_t CH = 64u * Q, CHP = CH + kChainPad;  // (component rows, padded)
+__device__ __forceinline__ void wave_stream_sum(const uint32_t* __restrict__ rps,
+                                                const uint32_t* __restrict__ rlen, uint32_t rs,
+                                                uint32_t re, const float4* __restrict__ pts,
+                                                int* s_mark, float4* s_chunk, float (&sum)[4],
+                                                uint32_t& npts) {
+    constexpr uint32_t CH = 64u * Q;
     const int lane = threadIdx.x & 63;
-    float acc = 0.0f;
     npts = 0;
     const uint32_t r0 = rs + (uint32_t)lane;
     RunBatch cur = run_batch(run_rec(rps, rlen, r0, r0 < re));
@@ -2907,22 +3042,13 @@ __device__ __forceinline__ float wave_stream_sum(const uint32_t* __restrict__ rp
     RunRec rec2 = run_rec(rps, rlen, r0 + 128u, r0 + 128u < re);  // batch 2
     float4 p[Q];
     run_fetch<Q>(cur, 0, pts, s_mark, p);  // (every run holds >= 1 point)
-    // every lane runs the chain of component lane & 3 (lanes 0..3 hold the result): no exec mask
-    // splits the chain from the next chunk's fetch, which is interleaved with it row by row
-    const float* comp = s_soa + (uint32_t)(lane & 3) * CHP;
     uint32_t rb = rs, c = 0;
     while (true) {  // wave-uniform: one chunk per iteration
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            s_soa[0 * CHP + 64 * q + lane] = p[q].x;
-            s_soa[1 * CHP + 64 * q + lane] = p[q].y;
-            s_soa[2 * CHP + 64 * q + lane] = p[q].z;
-            s_soa[3 * CHP + 64 * q + lane] = p[q].w;
-        }
-        wave_sync();
         const uint32_t n = min(CH, cur.T - c);
-        // the next chunk, loaded while the chains run: the rest of this batch, or the next batch's
-        // first chunk (whose records were read two batches ago); none: T = 0, nothing is loaded
+#pragma unroll
+        for (int q = 0; q < Q; ++q) s_chunk[64 * q + lane] = p[q];
+        // the next chunk, loaded while this one is summed: the rest of this batch, or the next
+        // batch's first chunk (whose records were read two batches ago); none: T = 0
         const bool more = c + CH < cur.T;
         const bool next_batch = !more && rb + 64u < re;
         RunBatch fb = cur;
@@ -2936,34 +3062,11 @@ __device__ __forceinline__ float wave_stream_sum(const uint32_t* __restrict__ rp
         } else if (!more) {
             fb.T = 0;
         }
-        run_marks<Q>(fb, cn, s_mark);
-        int cy = fb.carry;
-        if (n == CH) {  // a full chunk: Q x (64 additions, then one row of the next chunk's loads)
-            float ta[16], tb[16];
-            lds_block<1, 16>(comp, 0, ta);
-#pragma unroll
-            for (int q = 0; q < Q; ++q) {
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const uint32_t k = 64u * q + 32u * h;
-                    lds_block<1, 16>(comp, k + 16, tb);
-                    asm volatile("" ::: "memory");  // (reads stay where they are issued)
-                    __builtin_amdgcn_sched_barrier(0);
-                    acc = add_block<16>(acc, ta);
-                    lds_block<1, 16>(comp, k + 32, ta);  // (the last reads the padding)
-                    asm volatile("" ::: "memory");
-                    __builtin_amdgcn_sched_barrier(0);
-                    acc = add_block<16>(acc, tb);
-                }
-                p[q] = run_row(fb, cn, q, s_mark, cy, pts);
-            }
-        } else {
-#pragma unroll
-            for (int q = 0; q < Q; ++q) p[q] = run_row(fb, cn, q, s_mark, cy, pts);
-            acc = lds_chain<1>(comp, n, acc);
-        }
-        fb.carry = cy;
-        wave_sync();  // the chains have read the chunk before the next one is written
+        run_fetch<Q>(fb, cn, pts, s_mark, p);  // (its marks' wave_sync also orders s_chunk)
+#pragma unroll 1
+        for (uint32_t r = 0; r < n; r += 64)  // this chunk's rows from LDS
+            row_sum4(sum, s_chunk[r + (uint32_t)lane], min(64u, n - r));
+        wave_sync();  // the rows are read before the next chunk is written
         npts += n;
         if (more) {
             cur = fb;
@@ -2976,7 +3079,6 @@ __device__ __forceinline__ float wave_stream_sum(const uint32_t* __restrict__ rp
             break;
         }
     }
-    return acc;
 }
 
 // Groups of one tile of 256 sorted runs: group starts (key != previous run's key), group ids by a
@@ -3166,11 +3268,9 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
             const uint32_t g = s_excl + li;
             const uint32_t s = s_start[li], e = s_start[li + 1];
             const uint32_t g0 = s_off[s - t0] - W0, g1 = s_off[e - t0] - W0;
-            if (lane < 4) {
-                const float* comp = reinterpret_cast<const float*>(s_pts) + lane + 4 * g0;
-                const float acc = lds_chain<4>(comp, g1 - g0, 0.0f);
-                out[4 * (size_t)g + lane] = lane < 3 ? acc / (float)(g1 - g0) : acc;
-            }
+            float sum[4] = {0.f, 0.f, 0.f, 0.f};
+            lds_group_sum(s_pts + g0, g1 - g0, sum);
+            store_mean(out + 4 * (size_t)g, sum, g1 - g0);
         }
         __syncthreads();  // LDS reused by the next tile
     }
@@ -3189,9 +3289,9 @@ __global__ __launch_bounds__(64 * WPB) void k_group_runs_big(const uint32_t* __r
                                                         const uint4* __restrict__ bigq,
                                                         uint32_t bigq_cap, uint32_t* qctr) {
     constexpr uint32_t CH = 64u * Q;
-    // WPB waves per block (Q = 16: one - a long chunk's 20 KB of LDS allocated per wave)
-    __shared__ __attribute__((aligned(16))) float s_soa[WPB][4 * (CH + kChainPad)];
+    // WPB waves per block; a wave's run marks and points of one chunk in LDS
     __shared__ int s_mk[WPB][CH];
+    __shared__ float4 s_ck[WPB][CH];
     const int lane = threadIdx.x & 63, wid = WPB == 1 ? 0 : (int)(threadIdx.x >> 6);
     const uint32_t nq = min(__hip_atomic_load(qctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), bigq_cap);
     const uint32_t waves = gridDim.x * (blockDim.x >> 6);
@@ -3202,8 +3302,9 @@ __global__ __launch_bounds__(64 * WPB) void k_group_runs_big(const uint32_t* __r
     while (t < nq) {  // wave-uniform
         const uint4 q = bigq[t];
         uint32_t np = 0;
-        const float acc = wave_stream_sum<Q>(rps, rlen, q.y, q.z, pts, s_soa[wid], s_mk[wid], np);
-        if (lane < 4) out[4 * (size_t)q.x + lane] = lane < 3 ? acc / (float)np : acc;
+        float sum[4] = {0.f, 0.f, 0.f, 0.f};
+        wave_stream_sum<Q>(rps, rlen, q.y, q.z, pts, s_mk[wid], s_ck[wid], sum, np);
+        store_mean(out + 4 * (size_t)q.x, sum, np);
         if (nq <= waves) break;
         uint32_t d = 0;
         if (lane == 0) d = atomicAdd(qctr + 1, 1u);
@@ -3228,14 +3329,14 @@ static void launch_sort_pass(uint32_t tiles, hipStream_t s, const uint32_t* kin,
     // the first pass also carries the historic-grid update in extra blocks
     const bool g = p == 0 && a.grid8 != nullptr;
     const uint64_t nwords = g ? (a.ncells + 31) / 32 : 0;
-    const uint32_t gb = g ? grid_blocks(nwords, 256 * 2) : 0;
+    const uint32_t gb = g ? fused_grid_blocks(a.ncells) : 0;
     hipLaunchKernelGGL((k_sort_pass<PT, NB>), dim3(tiles + gb), dim3(kSortThreads), 0, s, kin, vin, kout,
                        vout, a.count, a.hist + 256 * p, a.status, a.sgstatus,
                        reinterpret_cast<uint32_t*>(a.ctrs + kCtrSort0 + p),
                        reinterpret_cast<uint32_t*>(a.ctrs + kCtrEpoch), a.err, 8 * p, dbits, tiles,
                        reinterpret_cast<uint4*>(a.grid8), a.marks, nwords, a.lifetime, a.gseq,
                        a.nframes, a.frame_shift, a.frame_pt_start, a.mark_words,
-                       reinterpret_cast<uint4*>(a.snapshots), a.snapshot_bytes / 16,
+                       a.snap,
                        p == 0 ? reinterpret_cast<uint32_t*>(a.ctrs + kCtrRunQueue) : nullptr);
 }
 

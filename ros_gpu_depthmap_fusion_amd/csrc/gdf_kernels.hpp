@@ -53,6 +53,24 @@ hipError_t launch_ps_filter_insert(const float4* new_pts, uint32_t n, int do_fil
 hipError_t launch_gather_records(const void* rec, uint32_t n, uint32_t step, float4* out,
                                  hipStream_t s);
 
+// sparse per-frame u8 grid snapshots of a batch (the non-zero 32-cell groups of the grid after
+// each frame but the last), written by the batched grid update; layout per update launch of
+// `nblocks` 256-thread blocks: snap_dims (W wave segments of `seg` entries per frame), entry e =
+// (word index idx[e], 32 bytes data[2e], data[2e + 1]), counts cnt[f * W + w]
+struct SnapArgs {
+    uint32_t* idx;
+    uint4* data;
+    uint32_t* cnt;
+};
+void snap_dims(uint64_t ncells, uint32_t nblocks, uint32_t* waves, uint32_t* seg);
+// blocks of the grid update that the first sort pass carries (for the snapshot layout)
+uint32_t fused_grid_blocks(uint64_t ncells);
+// blocks of k_grid_u8_batch
+uint32_t batch_grid_blocks(uint64_t ncells);
+// frame `frame`'s snapshot expanded into a dense u8 grid (out: padded to 32 bytes)
+hipError_t launch_snap_expand(const SnapArgs& sn, uint32_t frame, uint32_t nblocks,
+                              uint64_t ncells, uint8_t* out, hipStream_t s);
+
 // historic grid update from the frame's mark bitmask (cleared on the way): u8 grid = history for
 // lifetime <= 255; the general u32 history with a separate u8 output grid beyond
 // (q: engine order of grid updates across streams, see GridSeq)
@@ -61,7 +79,7 @@ hipError_t launch_grid_u8(uint8_t* grid, uint32_t* marks, uint64_t ncells, uint3
 hipError_t launch_grid_u8_batch(uint8_t* grid, const uint32_t* bits, uint64_t ncells,
                                 uint32_t nranks, uint32_t nframes, uint64_t frame_stride,
                                 uint64_t rank_stride, uint32_t lifetime, const GridSeq& q,
-                                hipStream_t s);
+                                const SnapArgs& snap, hipStream_t s);
 hipError_t launch_grid_u32(uint32_t* hist, uint32_t* marks, uint8_t* out8, uint64_t ncells,
                            uint32_t lifetime, const GridSeq& q, hipStream_t s);
 hipError_t launch_widen_grid(const uint8_t* grid8, uint32_t* hist, uint64_t ncells,
@@ -107,14 +125,13 @@ struct VoxelizeArgs {
     // multi-frame batch: keys of frame f (points [frame_pt_start[f], frame_pt_start[f+1])) sort
     // as key | f << frame_shift; k_group writes the first voxel of each frame (frame_vox_start,
     // nframes + 1 entries); the grid update applies the frames' marks (stride mark_words) in
-    // order and stores the grid after each frame but the last at snapshots + f * snapshot_bytes
+    // order and writes the sparse snapshots of the grid after each frame but the last (snap)
     uint32_t nframes;
     uint32_t frame_shift;
     const uint32_t* frame_pt_start;
     uint32_t* frame_vox_start;
     uint64_t mark_words;
-    uint8_t* snapshots;
-    uint64_t snapshot_bytes;
+    SnapArgs snap;
     // runs of equal keys: keys / count are the run keys / run count, the sort orders runs and
     // k_group_runs groups them (run r = points run_start[r] .. run_start[r+1]-1; point_count:
     // the points)

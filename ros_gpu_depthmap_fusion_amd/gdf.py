@@ -141,6 +141,9 @@ EXPORTED = [
 ]
 
 
+ABI_VERSION = (0, 3)  # include/gdf.h GDF_VERSION_MAJOR / _MINOR
+
+
 def load_library(path: str = LIB_PATH):
     """Load libgdf.so (raises if it was not built: there is no fallback path)."""
     global _lib
@@ -241,6 +244,11 @@ def load_library(path: str = LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    major, minor = C.c_int(), C.c_int()
+    lib.gdf_version(C.byref(major), C.byref(minor))
+    if (major.value, minor.value) != ABI_VERSION:  # the structs below are those of ABI_VERSION
+        raise GDFError(-2, f"{path}: ABI {major.value}.{minor.value}, binding expects "
+                           f"{ABI_VERSION[0]}.{ABI_VERSION[1]} (rebuild the library)")
     _lib = lib
     return lib
 

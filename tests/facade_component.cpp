@@ -16,6 +16,7 @@
 #include <string>
 #include <vector>
 
+#define GDF_GL_BARRIER_STUB  // no GL header in this build: the component's barrier lines compile as no-ops
 #include "gdf_fusion.hpp"
 
 namespace cv {

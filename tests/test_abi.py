@@ -39,7 +39,7 @@ def test_library_loads_and_reports_version():
     lib = load_library()
     a, b = ctypes.c_int(), ctypes.c_int()
     assert lib.gdf_version(ctypes.byref(a), ctypes.byref(b)) == 0
-    assert (a.value, b.value) == (0, 1)
+    assert (a.value, b.value) == (0, 3)
     # null-handle calls fail cleanly with GDF_ERR_ARG, no GPU touched
     assert lib.gdf_clear(None) == -1
     assert b"null engine" in lib.gdf_last_error()
