@@ -70,6 +70,11 @@ def parse():
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
                     help="N > 1: RCCL (default) or gloo with host-staged tensors (smoke runs of "
                          "several ranks on one GPU)")
+    ap.add_argument("--dist", action="store_true",
+                    help="the multi-GPU (torch.distributed) path even at one rank (RCCL at world 1)")
+    ap.add_argument("--publish", action="store_true",
+                    help="fused mode: gather the fused voxel cloud to rank 0 every step (the "
+                         "component publishes it every frame)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=3.0, help="per CPU run (5 runs)")
     ap.add_argument("--no-kernel-timing", action="store_true",
@@ -335,13 +340,31 @@ def cpu_baseline(st, params, seconds):
                 break
         rates.append(done * st.P / t / 1e6)
         total_frames += done
-    return {"value": round(statistics.median(rates), 3), "unit": "Mpoints/s", "cores": threads,
-            "kind": "port", "threads": threads, "nproc": os.cpu_count(),
-            "affinity_cpus": affinity, "cpu_model": model,
-            "runs_Mpoints_s": [round(r, 2) for r in rates],
+    out = {"value": round(statistics.median(rates), 3), "unit": "Mpoints/s", "cores": threads,
+           "kind": "port", "threads": threads, "nproc": os.cpu_count(),
+           "affinity_cpus": affinity, "cpu_model": model,
+           "runs_Mpoints_s": [round(r, 2) for r in rates],
             "sample": f"median of 5 runs x {seconds:.0f} s ({total_frames} frames) of the same "
                       f"{st.W}x{st.H} frames through the C restatement (oracle/gdf_oracle.c, "
-                      f"-O3 -ffp-contract=off, OpenMP {threads} threads)"}
+                      f"-O3 -ffp-contract=off, OpenMP {threads} threads = the pool's "
+                      f"OMP_NUM_THREADS share of this GPU's host)"}
+    if affinity > threads:  # and every CPU of the host (nproc), a short sample
+        orc.set_threads(affinity)
+        frame(0)
+        rates_all = []
+        for run in range(3):
+            done, t0 = 0, time.perf_counter()
+            while True:
+                frame(done)
+                done += 1
+                t = time.perf_counter() - t0
+                if t >= 1.0 or done >= 4000:
+                    break
+            rates_all.append(done * st.P / t / 1e6)
+        out["all_cpus"] = {"value": round(statistics.median(rates_all), 3), "threads": affinity,
+                           "runs_Mpoints_s": [round(r, 2) for r in rates_all],
+                           "sample": "median of 3 runs x 1 s, OpenMP %d threads" % affinity}
+    return out
 
 
 def workload_name(W, H, K, wl):
@@ -355,7 +378,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     dist = None
     rank, local_rank = 0, 0
-    if args.gpus > 1 or world > 1:
+    if args.gpus > 1 or world > 1 or args.dist:
         import torch
         import torch.distributed as dist
         rank = int(os.environ.get("RANK", "0"))
@@ -444,6 +467,8 @@ def time_multi(args, st, params, dist, world, pmc_key):
         n = st.W * st.H
         B = max(1, args.batch)
 
+        from ros_gpu_depthmap_fusion_amd.multi import gather_fused_cloud
+
         def run(first, count):
             for i in range(first, first + count):
                 if B > 1:  # a step = B frames through one launch chain and one exchange
@@ -452,6 +477,8 @@ def time_multi(args, st, params, dist, world, pmc_key):
                 else:
                     d = st.dframes[0][i % st.ring].ptr
                     fr.frame(d, d + 2 * (n - fr.Lmax))
+                if args.publish:  # the fused cloud of the step on the publishing rank
+                    gather_fused_cloud(fr, root=0)
     else:
         batched = args.exchange_batch > 1
         if batched:
@@ -528,7 +555,8 @@ def time_multi(args, st, params, dist, world, pmc_key):
                               "depth-tail halo all-gather, occupancy-mark all-gather + batched "
                               "grid update, key-range all-to-all of the (point, frame | key) "
                               "lists, voxelize per key range (fused cloud = one engine over all "
-                              "cameras, per frame)" % (world, fpb),
+                              "cameras, per frame)%s" % (world, fpb, "; fused cloud gathered "
+                                                        "to rank 0 every step" if args.publish else ""),
                "exchange": "per step of %d frames: halo %d px + %d-word marks per frame, one "
                            "points all-to-all" % (fpb, fr.Lmax, (ncells + 31) // 32)}
     else:
@@ -579,6 +607,44 @@ def run_alternating(args, params, steps, warm):
     return r
 
 
+def run_component_sync(args, params, frames=300, warm=20):
+    """The reference component's per-frame sequence, synchronous, one frame at a time
+    (GPUDepthmapFusionComponent::processDepthmaps, component.cpp:92-306): a host depth image
+    (cv_bridge) -> addDepthmap -> the frame (uploadDepthmaps ... voxelOccupancyGrid) -> the
+    downloads the component makes every frame: downloadPoints, downloadVoxelCoords, the voxelized
+    points (published as out/Points, component.cpp:389-461) and downloadVoxelOccupancyGrid.  The
+    latency per frame (median, p99) and the rate of one such stream."""
+    import numpy as np
+    from ros_gpu_depthmap_fusion_amd import synth
+    from ros_gpu_depthmap_fusion_amd.gdf import GPUDepthmapFusion
+    W, H = args.width, args.height
+    eng = GPUDepthmapFusion(0)
+    cam = synth.make_camera(0, W, H)
+    ring = [synth.WORKLOADS[args.workload](cam, 0, f) for f in range(8)]
+    lat = []
+    for i in range(warm + frames):
+        t0 = time.perf_counter()
+        eng.clear()
+        eng.addDepthmap(ring[i % len(ring)], *cam.intrinsics(), cam.T_world, cam.T_crop)
+        eng.processFrame(params, synchronous=True)
+        pts = eng.downloadPoints()
+        keys = eng.downloadVoxelCoords()
+        vox = eng.downloadVoxelizedPoints()
+        grid = eng.downloadVoxelOccupancyGrid()
+        if i >= warm:
+            lat.append(time.perf_counter() - t0)
+    eng.close()
+    lat = np.array(lat)
+    return {"workload": "C2 component-equivalent: one %dx%d host depth frame at a time, "
+                        "synchronous, with the per-frame downloads (points, voxel coords, "
+                        "voxelized points, u8 grid)" % (W, H),
+            "value": round(W * H * len(lat) / lat.sum() / 1e6, 3),
+            "latency_ms_median": round(float(np.median(lat)) * 1e3, 4),
+            "latency_ms_p99": round(float(np.percentile(lat, 99)) * 1e3, 4),
+            "frames": len(lat),
+            "download_bytes_per_frame": int(pts.nbytes + keys.nbytes + vox.nbytes + grid.nbytes)}
+
+
 def run_secondary(args, params):
     """N = 1 only: the other single-GPU configurations, each with its own roofline."""
     from ros_gpu_depthmap_fusion_amd.gdf import GPUDepthmapFusion
@@ -617,6 +683,7 @@ def run_secondary(args, params):
     out["vga_h2d"] = r
     del st
     eng.close()
+    out["component_sync"] = run_component_sync(args, params)
     try:
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         from bench_c3 import run_c3

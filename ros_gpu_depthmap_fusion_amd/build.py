@@ -9,7 +9,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB_PATH = os.path.join(PKG, "lib", "libgdf.so")
 SOURCES = ["gdf_kernels.hip", "gdf_segment.hip", "gdf_engine.cpp", "gdf_driver.cpp"]
-HEADERS = ["gdf_device.hpp", "gdf_kernels.hpp"]
+HEADERS = ["gdf_device.hpp", "gdf_kernels.hpp", "gdf_voxsum.hpp"]
 
 # Float contract of SURVEY.md Appendix A: no FMA contraction, correctly rounded / and sqrt.
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
@@ -24,19 +24,26 @@ def _stale(out: str, deps) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_library(force: bool = False, verbose: bool = False) -> str:
+TRACE_LIB_PATH = os.path.join(PKG, "lib", "libgdf_trace.so")
+
+
+def build_library(force: bool = False, verbose: bool = False, trace: bool = False) -> str:
+    """libgdf.so; trace=True: the diagnostic variant libgdf_trace.so (-DGDF_TRACE_GROUPS: per-group
+    timings of the voxel-sum kernel, read by tools/group_trace.py - never the product library)."""
+    out = TRACE_LIB_PATH if trace else LIB_PATH
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
     deps += [os.path.join(ROOT, "include", h) for h in ("gdf.h", "gdf_driver.h", "gdf_segment.h")]
-    if not force and not _stale(LIB_PATH, deps):
-        return LIB_PATH
-    os.makedirs(os.path.dirname(LIB_PATH), exist_ok=True)
+    if not force and not _stale(out, deps):
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, *HIPCC_FLAGS, "-I" + os.path.join(ROOT, "include"), "-I" + CSRC,
-           "-o", LIB_PATH + ".tmp", *[os.path.join(CSRC, f) for f in SOURCES]]
+    cmd = [hipcc, *HIPCC_FLAGS, *(["-DGDF_TRACE_GROUPS"] if trace else []),
+           "-I" + os.path.join(ROOT, "include"), "-I" + CSRC,
+           "-o", out + ".tmp", *[os.path.join(CSRC, f) for f in SOURCES]]
     if verbose:
         print(" ".join(cmd))
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("hipcc failed:\n" + r.stdout + r.stderr)
-    os.replace(LIB_PATH + ".tmp", LIB_PATH)
-    return LIB_PATH
+    os.replace(out + ".tmp", out)
+    return out

@@ -10,6 +10,7 @@
 //                      / uints_to_chars.glsl:31-50, fused into one pass over the cells
 //   k_sort_*, k_group  inc/voxelize.h:74-105 + radix_grouper.h + radix_sort.h (GPU version)
 #include "gdf_kernels.hpp"
+#include "gdf_voxsum.hpp"  // the voxel sum (row_sum4): exact integer stretches
 
 #include <algorithm>
 
@@ -2494,194 +2495,19 @@ constexpr int kSmallGroup = 16;  // groups summed by one thread; longer ones by 
 
 constexpr uint32_t kChainPad = 16;  // LDS padding of staged point buffers
 
-// ---- the voxel sum: the sequential f32 chain, evaluated 64 terms at a time ----------------------
-// The reference sums a voxel's points one after the other (inc/voxelize.h:29-35:
-// s_k = fl(s_{k-1} + x_k), round-to-nearest-even), a dependent chain that cannot be reassociated in
-// general.  It can, however, be evaluated EXACTLY in parallel over stretches where every rounding
-// lands on one fixed grid:
-//   let u be a power of two with s = m u (m integer) and y_k = x_k / u (exact scaling).  If the
-//   exact value v_k = s_{k-1} + x_k lies strictly inside a binade whose ulp is u, then
-//   fl(v_k) = s_{k-1} + u rint(y_k) unless y_k is a tie (fraction exactly 1/2, whose rounding
-//   depends on the parity of s_{k-1}/u); if y_k is an integer and |m + sum| <= 2^24 the sum is
-//   exactly representable, so fl(v_k) = v_k whatever its binade.
-// With u = ulp(s) (binade exponent E = ex - 127, u = 2^(ex - 150)) a row of 64 terms becomes
-// integer arithmetic: t_k = rint(y_k) (int32), an inclusive wave scan P_k = m + t_1 + ... + t_k,
-// and a per-lane validity test - rounding steps need 2^23 < |P_k| < 2^24 (then |v_k| is inside
-// (2^23 u, 2^24 u) since |v_k - P_k u| < u/2), exact steps need |P_k| <= 2^24, ties and
-// |y_k| > 2^24 (inf, NaN) fail.  The first failing lane L ends the stretch: the prefix [b, L) is
-// committed as s = P_{L-1} u (exact), term L is added by one ordinary f32 add (the reference's own
-// operation: a binade crossing, a tie, a NaN ...), and a new stretch starts at L + 1 with the new
-// ulp.  A zero, subnormal-range or non-finite s takes single f32 adds until it leaves that range.
-// The result is bit-identical to the sequential chain for every input (the model and the bit-exact
-// GPU tests: tests/test_gpu_round3.py); a voxel sum grows monotonically for most voxels, so a
-// stretch fails about once per doubling of the sum (~log2(n) extra stretches per voxel).
-__device__ __forceinline__ float bcast_f(float v, uint32_t l) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+// Voxel sums, one component per wave (gdf_voxsum.hpp): wave c of a 4-wave group sums component c.
+// A staged group of cnt points (float4 AoS in LDS)
+__device__ __forceinline__ float lds_group_comp(const float4* pts, uint32_t c, uint32_t cnt) {
+    const float* f = reinterpret_cast<const float*>(pts) + c;
+    return comp_stretch_sum<4>([&](uint32_t i) { return f[4 * i]; }, 0, cnt, 0.0f);
 }
-__device__ __forceinline__ float uniform_f(float v) {
-    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
-}
-// wave64 inclusive sum scan on DPP (row shifts, then the row broadcasts of lanes 15 and 31)
-__device__ __forceinline__ int dpp_iscan(int v) {
-    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
-    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
-    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);  // row_shr:4
-    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);  // row_shr:8
-    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
-    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
-    return v;
-}
-// four independent scans step by step (the DPP hazard gaps of one scan hold the others' steps)
-__device__ __forceinline__ void dpp_iscan4(int (&v)[4]) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) v[c] += __builtin_amdgcn_update_dpp(0, v[c], 0x111, 0xf, 0xf, false);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) v[c] += __builtin_amdgcn_update_dpp(0, v[c], 0x112, 0xf, 0xf, false);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) v[c] += __builtin_amdgcn_update_dpp(0, v[c], 0x114, 0xf, 0xf, false);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) v[c] += __builtin_amdgcn_update_dpp(0, v[c], 0x118, 0xf, 0xf, false);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) v[c] += __builtin_amdgcn_update_dpp(0, v[c], 0x142, 0xa, 0xf, false);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) v[c] += __builtin_amdgcn_update_dpp(0, v[c], 0x143, 0xc, 0xf, false);
-}
-__device__ __forceinline__ bool spec_ok_s(float s) {  // s admits a stretch: normal, ulp(s) normal
-    const uint32_t ex = ((uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(s)) >> 23) & 255u;
-    return ex >= 24u && ex != 255u;
-}
-// One stretch over lanes [b, nv) from s (spec_ok_s(s)): the failing-lane ballot, P (lane-wise
-// prefix in units of u) and u.  Branch-free (non-short-circuit & / |): no exec-mask splits.
-__device__ __forceinline__ unsigned long long spec_try(float s, float x, uint32_t b, uint32_t nv,
-                                                       int& P, float& u) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t ex = ((uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(s)) >> 23) & 255u;
-    const float scale = __uint_as_float((277u - ex) << 23);  // 2^(150 - ex) = 1 / u
-    u = __uint_as_float((ex - 23u) << 23);
-    const int m = __builtin_amdgcn_readfirstlane((int)(s * scale));
-    const float y = x * scale;
-    const float r = __builtin_rintf(y);
-    const bool in = (lane >= b) & (lane < nv);
-    const bool fin = (__builtin_fabsf(y) <= 16777216.0f) & (__builtin_fabsf(y - r) != 0.5f);
-    P = m + dpp_iscan((in & fin) ? (int)r : 0);
-    const uint32_t aP = (uint32_t)__builtin_abs(P);
-    const bool exact = y == r;
-    const bool ok = fin & ((exact & (aP <= 16777216u)) | (!exact & (aP - 8388609u <= 8388606u)));
-    return __ballot(in & !ok);
-}
-// One component, general path: s + x_b + ... + x_{nv-1} by stretches, with single f32 adds
-// while s is not admissible and at every failing lane.
-__device__ __forceinline__ float chain_row(float s, float x, uint32_t b, uint32_t nv) {
-    while (b < nv) {  // wave-uniform
-        if (!spec_ok_s(s)) {
-            s = uniform_f(s + bcast_f(x, b));
-            ++b;
-            continue;
-        }
-        int P;
-        float u;
-        const unsigned long long bad = spec_try(s, x, b, nv, P, u);
-        const uint32_t L = bad ? (uint32_t)__builtin_ctzll(bad) : nv;
-        if (L > b) s = uniform_f((float)__builtin_amdgcn_readlane(P, L - 1) * u);
-        if (L >= nv) break;
-        s = uniform_f(s + bcast_f(x, L));
-        b = L + 1;
-    }
-    return s;
-}
-// s[c] + x_c of lanes 0..nv-1, in lane order, for the four components of a row of points
-// (wave-uniform s; lanes >= nv ignored).  The common case - one stretch per component - runs the
-// four scans side by side; a component whose stretch fails (a binade crossing, a tie, a zero
-// sum ...) is redone from the row start by chain_row, one component at a time (one copy of the
-// general path: the kernels stay small enough for the instruction cache).
-__device__ __forceinline__ void row_sum4(float (&s)[4], const float4& p, uint32_t nv) {
-    const float x[4] = {p.x, p.y, p.z, p.w};
-    uint32_t redo = 0xFu;
-    if (spec_ok_s(s[0]) && spec_ok_s(s[1]) && spec_ok_s(s[2]) && spec_ok_s(s[3])) {
-        // spec_try for the four components in phases, so their scans interleave
-        const uint32_t lane = threadIdx.x & 63;
-        const bool in = lane < nv;
-        int P[4], m[4];
-        float u[4], y[4], r[4];
-        bool fin[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const uint32_t ex = ((uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(s[c])) >> 23) & 255u;
-            const float scale = __uint_as_float((277u - ex) << 23);
-            u[c] = __uint_as_float((ex - 23u) << 23);
-            m[c] = __builtin_amdgcn_readfirstlane((int)(s[c] * scale));
-            y[c] = x[c] * scale;
-            r[c] = __builtin_rintf(y[c]);
-            fin[c] = (__builtin_fabsf(y[c]) <= 16777216.0f) & (__builtin_fabsf(y[c] - r[c]) != 0.5f);
-            P[c] = (in & fin[c]) ? (int)r[c] : 0;
-        }
-        dpp_iscan4(P);
-        redo = 0;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            P[c] += m[c];
-            const uint32_t aP = (uint32_t)__builtin_abs(P[c]);
-            const bool exact = y[c] == r[c];
-            const bool ok = fin[c] & ((exact & (aP <= 16777216u)) | (!exact & (aP - 8388609u <= 8388606u)));
-            if (__ballot(in & !ok)) redo |= 1u << c;
-            else s[c] = uniform_f((float)__builtin_amdgcn_readlane(P[c], 63) * u[c]);
-        }
-    }
-    if (redo) {
-#pragma unroll 1
-        for (uint32_t c = 0; c < 4; ++c) {
-            if (!((redo >> c) & 1u)) continue;
-            const float xc = c == 0 ? x[0] : c == 1 ? x[1] : c == 2 ? x[2] : x[3];
-            const float sc = c == 0 ? s[0] : c == 1 ? s[1] : c == 2 ? s[2] : s[3];
-            const float r = chain_row(sc, xc, 0, nv);
-            s[0] = c == 0 ? r : s[0];
-            s[1] = c == 1 ? r : s[1];
-            s[2] = c == 2 ? r : s[2];
-            s[3] = c == 3 ? r : s[3];
-        }
-    }
-}
-// The voxel output of lanes 0..3 (component lane): x/y/z divided by the count, w the plain sum.
-__device__ __forceinline__ void store_mean(float* o, const float (&s)[4], uint32_t cnt) {
-    const int lane = threadIdx.x & 63;
-    if (lane < 4) {
-        const float v = lane == 0 ? s[0] : lane == 1 ? s[1] : lane == 2 ? s[2] : s[3];
-        o[lane] = lane < 3 ? v / (float)cnt : v;
-    }
-}
-// A group of cnt points from a float4 AoS LDS buffer (staged groups), rows of 64.
-__device__ __forceinline__ void lds_group_sum(const float4* pts, uint32_t cnt, float (&s)[4]) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll 1
-    for (uint32_t r = 0; r < cnt; r += 64) {
-        const uint32_t nv = min(64u, cnt - r);
-        const float4 p = (uint32_t)lane < nv ? pts[r + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
-        row_sum4(s, p, nv);
-    }
-}
-
-// A group's points pts[vals[k]], k in [s, e), gathered in rows of 64 (points mode): the gathers
-// run kAhead rows ahead of the row being summed.
-constexpr int kAhead = 4;
-__device__ __forceinline__ float4 gather_pt(const uint32_t* __restrict__ vals,
-                                            const float4* __restrict__ pts, uint32_t k, uint32_t e) {
-    return k < e ? pts[vals[k]] : make_float4(0.f, 0.f, 0.f, 0.f);
-}
-__device__ __forceinline__ void gather_group_sum(const uint32_t* __restrict__ vals,
-                                                 const float4* __restrict__ pts, uint32_t s,
-                                                 uint32_t e, float (&sum)[4]) {
-    const uint32_t lane = threadIdx.x & 63;
-    float4 r[kAhead];
-#pragma unroll
-    for (int q = 0; q < kAhead; ++q) r[q] = gather_pt(vals, pts, s + 64u * q + lane, e);
-#pragma unroll 1
-    for (uint32_t c = s; c < e; c += 64) {
-        const float4 cur = r[0];
-#pragma unroll
-        for (int q = 0; q + 1 < kAhead; ++q) r[q] = r[q + 1];
-        r[kAhead - 1] = gather_pt(vals, pts, c + 64u * kAhead + lane, e);
-        row_sum4(sum, cur, min(64u, e - c));
-    }
+// a group's points pts[vals[k]], k in [s, e) (points mode), gathered from global memory
+__device__ __forceinline__ float gather_group_comp(const uint32_t* __restrict__ vals,
+                                                   const float4* __restrict__ pts, uint32_t c,
+                                                   uint32_t s, uint32_t e) {
+    const float* f = reinterpret_cast<const float*>(pts) + c;
+    return comp_stretch_sum<4>([&](uint32_t i) { return f[4 * (size_t)vals[s + i]]; }, 0, e - s,
+                               0.0f);
 }
 
 // Group starts per tile of kGroupThreads sorted keys (large frames: the tiles' group-id offsets
@@ -2887,38 +2713,34 @@ __global__ __launch_bounds__(kGroupThreads) __attribute__((amdgpu_waves_per_eu(7
     }
     __syncthreads();
     const uint32_t nbig = s_nbig;
-    for (uint32_t b = wid; b < nbig; b += kGroupThreads / 64) {
+    for (uint32_t b = 0; b < nbig; ++b) {  // every group by the 4 waves, wave = component
         const uint32_t li = s_big[b];
         const uint32_t g = s_excl + li;
         const uint32_t s = s_start[li], e = s_start[li + 1];
-        float sum[4] = {0.f, 0.f, 0.f, 0.f};
-        if (e - S0 <= staged) lds_group_sum(s_pts + (s - S0), e - s, sum);  // staged
-        else gather_group_sum(vals, pts, s, e, sum);
-        store_mean(out + 4 * (size_t)g, sum, e - s);
+        const float sum = e - S0 <= staged ? lds_group_comp(s_pts + (s - S0), wid, e - s)  // staged
+                                           : gather_group_comp(vals, pts, wid, s, e);
+        store_comp_mean(out + 4 * (size_t)g, wid, sum, e - s);
     }
     __syncthreads();  // LDS reused by the next tile
     }
 }
 
-// The long voxels queued by k_group (large frames): one wave per voxel, independent of tiles and
-// block barriers; the same sequential f32 sum in index order as k_group's wave path.
+// The long voxels queued by k_group (large frames): one block (4 waves, one per component) per
+// voxel, independent of tiles and block barriers; the same sums as k_group's wave path.
 __global__ __launch_bounds__(256) void k_group_big(const uint32_t* __restrict__ vals,
                                                    const float4* __restrict__ pts,
                                                    float* __restrict__ out,
                                                    const uint4* __restrict__ bigq,
                                                    const uint32_t* __restrict__ bigcnt,
                                                    uint32_t nblocks, uint32_t bigcap) {
-    const int wid = threadIdx.x >> 6;
+    const uint32_t wid = threadIdx.x >> 6;  // (the component)
     const uint64_t nslots = (uint64_t)nblocks * bigcap;
-    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    for (uint64_t slot = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wid; slot < nslots;
-         slot += waves) {  // wave-uniform
+    for (uint64_t slot = blockIdx.x; slot < nslots; slot += gridDim.x) {  // block-uniform
         const uint32_t b = (uint32_t)(slot / bigcap), k = (uint32_t)(slot % bigcap);
         if (k >= bigcnt[b]) continue;
         const uint4 q = bigq[slot];
-        float sum[4] = {0.f, 0.f, 0.f, 0.f};
-        gather_group_sum(vals, pts, q.y, q.z, sum);
-        store_mean(out + 4 * (size_t)q.x, sum, q.z - q.y);
+        const float sum = gather_group_comp(vals, pts, wid, q.y, q.z);
+        store_comp_mean(out + 4 * (size_t)q.x, wid, sum, q.z - q.y);
     }
 }
 
@@ -2933,12 +2755,10 @@ __global__ __launch_bounds__(256) void k_group_big(const uint32_t* __restrict__ 
 uint32_t g_run_stage = 2048;
 uint32_t g_run_inblock = 256;
 uint32_t g_run_big_blocks = 1024;  // k_group_runs_big grid (tuning knob GDF_RUN_BIG_BLOCKS)
-// 1 K-point chunks in k_group_runs_big: 0 never, 1 always, 2 (default) for single depth-only
-// frames - whose long voxels reach ~20 K points at 4K (4K group phase 154 -> 142 us) - while
-// batches (shorter voxels: VGA x8 42 -> 49 us) and rollbuffer windows keep 256-point chunks
-// (tuning knob GDF_RUN_Q16)
+// chunks of k_group_runs_big (one 4-wave block per queued group): 1 K points (Q = 16) or 512
+// (Q = 8); 0 never 1 K, 1 always, 2 (default) for single depth-only frames, whose long voxels
+// reach ~20 K points at 4K (tuning knob GDF_RUN_Q16)
 uint32_t g_run_q16 = 2;
-// a streamed chunk: 64 x Q points per wave step (Q = 4, 4 waves per block; Q = 16, one wave)
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -2963,22 +2783,20 @@ struct RunRec {
     uint32_t ps, len;
 };
 
-// One wave sums the points of sorted runs [rs, re) in order: batches of 64 runs (one per lane;
+// A group's points stream through a 4-wave block in order: batches of 64 sorted runs (one per lane;
 // the records rps / rlen - first point, length - are indexed by sorted run, contiguous, and read
-// two batches ahead), their points streamed in chunks of 64 x Q positions - position -> run by
-// a max-scan of the runs' first positions - loaded coalesced one chunk ahead (across batch
-// boundaries too), transposed into LDS per component, and added by lanes 0..3, one component chain
-// each (the reference's sequential f32 sum).  Returns lane c's component sum; npts = the group's
-// points (wave-uniform).
+// two batches ahead), their points in chunks of 64 x Q positions - position -> run by a max-scan of
+// the runs' first positions - loaded coalesced one chunk ahead (across batch boundaries too); wave w
+// loads rows w, w + 4, ... of a chunk, the block transposes the chunk into LDS per component and
+// wave c sums component c (gdf_voxsum.hpp) - the reference's sequential f32 sum, in stable order.
 struct RunBatch {
     uint32_t ps, off, len;  // run `lane` of the batch: first point, first batch position, length
     uint32_t T;             // the batch's points (wave-uniform)
-    int carry;              // run of the last fetched position
 };
 
 __device__ __forceinline__ RunBatch run_batch(const RunRec& r) {
     const uint32_t x = dpp_sum_scan(r.len);
-    return RunBatch{r.ps, x - r.len, r.len, (uint32_t)__builtin_amdgcn_readlane((int)x, 63), 0};
+    return RunBatch{r.ps, x - r.len, r.len, (uint32_t)__builtin_amdgcn_readlane((int)x, 63)};
 }
 
 __device__ __forceinline__ RunRec run_rec(const uint32_t* __restrict__ rps,
@@ -2986,67 +2804,77 @@ __device__ __forceinline__ RunRec run_rec(const uint32_t* __restrict__ rps,
     return ok ? RunRec{rps[r], rlen[r]} : RunRec{0u, 0u};
 }
 
-// The points at batch positions c + 64 q + lane (q < Q), in two steps: run_marks writes the
-// first position of every run inside the chunk, run_row(q) max-scans row q of the marks (the row
-// carries chain through cy) and loads its points - branch-free (positions past the batch load
-// point 0 and read as zero), so the rows interleave with the chain additions.
+// This wave's rows q = wid + 4 i of the chunk at batch position c: the first positions of the runs
+// starting in them marked in s_mark (rows are disjoint between the waves), each row max-scanned,
+// carried in by the last run starting before the row (a ballot count: every run holds >= 1
+// point, so the runs' first positions increase with the lane); positions past the batch read 0.
 template <int Q>
-__device__ __forceinline__ void run_marks(const RunBatch& bt, uint32_t c, int* s_mark) {
+__device__ __forceinline__ void fetch_rows4(const RunBatch& bt, uint32_t c, int* s_mark,
+                                            const float4* __restrict__ pts, float4 (&p)[Q / 4]) {
     constexpr uint32_t CH = 64u * Q;
-    const int lane = threadIdx.x & 63;
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
-    for (int q = 0; q < Q; ++q) s_mark[64 * q + lane] = -1;
+    for (int i = 0; i < Q / 4; ++i) s_mark[64u * (wid + 4u * i) + lane] = -1;
     wave_sync();
-    if (bt.len && bt.off >= c && bt.off < c + CH) s_mark[bt.off - c] = lane;
+    if (bt.len && bt.off >= c && bt.off < c + CH && (((bt.off - c) >> 6) & 3u) == wid)
+        s_mark[bt.off - c] = (int)lane;
     wave_sync();
-}
-
-__device__ __forceinline__ float4 run_row(const RunBatch& bt, uint32_t c, int q, const int* s_mark,
-                                          int& cy, const float4* __restrict__ pts) {
-    const int lane = threadIdx.x & 63;
-    int m = dpp_max_scan(s_mark[64 * q + lane]);
-    const int rowmax = __builtin_amdgcn_readlane(m, 63);
-    m = max(m, cy);
-    cy = max(cy, rowmax);
-    const uint32_t mps = __shfl(bt.ps, m, 64), moff = __shfl(bt.off, m, 64);
-    const uint32_t pos = c + 64u * q + (uint32_t)lane;
-    const bool ok = pos < bt.T;
-    const float4 v = pts[ok ? mps + (pos - moff) : 0u];
-    return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-}
-
-template <int Q>
-__device__ __forceinline__ void run_fetch(RunBatch& bt, uint32_t c, const float4* __restrict__ pts,
-                                          int* s_mark, float4 (&p)[Q]) {
-    run_marks<Q>(bt, c, s_mark);
-    int cy = bt.carry;
 #pragma unroll
-    for (int q = 0; q < Q; ++q) p[q] = run_row(bt, c, q, s_mark, cy, pts);
-    bt.carry = cy;
+    for (int i = 0; i < Q / 4; ++i) {
+        const uint32_t q = wid + 4u * i;
+        const uint32_t pos0 = c + 64u * q;
+        const int carry = (int)__popcll(__ballot(bt.len != 0u && bt.off < pos0)) - 1;
+        const int m = max(dpp_max_scan(s_mark[64u * q + lane]), carry);
+        const uint32_t mps = __shfl(bt.ps, m, 64), moff = __shfl(bt.off, m, 64);
+        const uint32_t pos = pos0 + lane;
+        const bool ok = pos < bt.T;
+        const float4 v = pts[ok ? mps + (pos - moff) : 0u];
+        p[i] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
 }
 
+#ifdef GDF_TRACE_GROUPS
+// (diagnostic build, tools/group_trace.py) per queued group: wall clock start / end, points,
+// chunks, cycles in the sums / at the barriers / in the fetches, and the CU it ran on
+constexpr uint32_t kTraceSlots = 1u << 16;
+__device__ unsigned long long g_gtrace[kTraceSlots][8];
+#define GDF_TCLK(var) const unsigned long long var = clock64()
+#else
+#define GDF_TCLK(var)
+#endif
 
-
+// The sum of component wid of sorted runs [rs, re) (one 4-wave block); npts = the group's points.
 template <int Q>
-__device__ __forceinline__ void wave_stream_sum(const uint32_t* __restrict__ rps,
-                                                const uint32_t* __restrict__ rlen, uint32_t rs,
-                                                uint32_t re, const float4* __restrict__ pts,
-                                                int* s_mark, float4* s_chunk, float (&sum)[4],
-                                                uint32_t& npts) {
+__device__ __forceinline__ float block_stream_sum(const uint32_t* __restrict__ rps,
+                                                  const uint32_t* __restrict__ rlen, uint32_t rs,
+                                                  uint32_t re, const float4* __restrict__ pts,
+                                                  int* s_mark, float (*s_soa)[kRowStride * Q],
+                                                  uint32_t& npts, unsigned long long* tr) {
+    static_assert(Q % 4 == 0 && Q <= 16, "rows_chunk_sum takes up to 16 rows");
     constexpr uint32_t CH = 64u * Q;
-    const int lane = threadIdx.x & 63;
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     npts = 0;
-    const uint32_t r0 = rs + (uint32_t)lane;
+    float s = 0.0f;
+    const uint32_t r0 = rs + lane;
     RunBatch cur = run_batch(run_rec(rps, rlen, r0, r0 < re));
     RunRec rec1 = run_rec(rps, rlen, r0 + 64u, r0 + 64u < re);    // batch 1
     RunRec rec2 = run_rec(rps, rlen, r0 + 128u, r0 + 128u < re);  // batch 2
-    float4 p[Q];
-    run_fetch<Q>(cur, 0, pts, s_mark, p);  // (every run holds >= 1 point)
+    float4 p[Q / 4];
+    fetch_rows4<Q>(cur, 0, s_mark, pts, p);
     uint32_t rb = rs, c = 0;
-    while (true) {  // wave-uniform: one chunk per iteration
+    while (true) {  // block-uniform: one chunk per iteration
         const uint32_t n = min(CH, cur.T - c);
+        GDF_TCLK(b0);
+        __syncthreads();  // every wave has summed the previous chunk
+        GDF_TCLK(b1);
 #pragma unroll
-        for (int q = 0; q < Q; ++q) s_chunk[64 * q + lane] = p[q];
+        for (int i = 0; i < Q / 4; ++i) {
+            const uint32_t k = kRowStride * (wid + 4u * i) + lane;
+            s_soa[0][k] = p[i].x;
+            s_soa[1][k] = p[i].y;
+            s_soa[2][k] = p[i].z;
+            s_soa[3][k] = p[i].w;
+        }
         // the next chunk, loaded while this one is summed: the rest of this batch, or the next
         // batch's first chunk (whose records were read two batches ago); none: T = 0
         const bool more = c + CH < cur.T;
@@ -3056,17 +2884,30 @@ __device__ __forceinline__ void wave_stream_sum(const uint32_t* __restrict__ rps
         if (next_batch) {
             fb = run_batch(rec1);
             rec1 = rec2;
-            const uint32_t r3 = rb + 192u + (uint32_t)lane;
+            const uint32_t r3 = rb + 192u + lane;
             rec2 = run_rec(rps, rlen, r3, r3 < re);
             cn = 0;
         } else if (!more) {
             fb.T = 0;
         }
-        run_fetch<Q>(fb, cn, pts, s_mark, p);  // (its marks' wave_sync also orders s_chunk)
-#pragma unroll 1
-        for (uint32_t r = 0; r < n; r += 64)  // this chunk's rows from LDS
-            row_sum4(sum, s_chunk[r + (uint32_t)lane], min(64u, n - r));
-        wave_sync();  // the rows are read before the next chunk is written
+        GDF_TCLK(b2);
+        __syncthreads();  // the chunk is in LDS
+        GDF_TCLK(b3);
+        if (more || next_batch) fetch_rows4<Q>(fb, cn, s_mark, pts, p);
+        GDF_TCLK(b4);
+        s = rows_chunk_sum(s_soa[wid], n, s);
+        GDF_TCLK(b5);
+#ifdef GDF_TRACE_GROUPS
+        if (tr) {
+            tr[0] += (b1 - b0) + (b3 - b2);  // barriers
+            tr[1] += b2 - b1;                // LDS stores (waits for the loads)
+            tr[2] += b4 - b3;                // fetch issue
+            tr[3] += b5 - b4;                // sum
+            tr[4] += 1;
+        }
+#else
+        (void)tr;
+#endif
         npts += n;
         if (more) {
             cur = fb;
@@ -3079,6 +2920,7 @@ __device__ __forceinline__ void wave_stream_sum(const uint32_t* __restrict__ rps
             break;
         }
     }
+    return s;
 }
 
 // Groups of one tile of 256 sorted runs: group starts (key != previous run's key), group ids by a
@@ -3263,56 +3105,84 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
         }
         __syncthreads();
         const uint32_t nbig = s_nbig;
-        for (uint32_t bi = wid; bi < nbig; bi += kGroupThreads / 64) {  // staged: chains from LDS
+        for (uint32_t bi = 0; bi < nbig; ++bi) {  // staged: the 4 waves, wave = component
             const uint32_t li = s_big[bi];
             const uint32_t g = s_excl + li;
             const uint32_t s = s_start[li], e = s_start[li + 1];
             const uint32_t g0 = s_off[s - t0] - W0, g1 = s_off[e - t0] - W0;
-            float sum[4] = {0.f, 0.f, 0.f, 0.f};
-            lds_group_sum(s_pts + g0, g1 - g0, sum);
-            store_mean(out + 4 * (size_t)g, sum, g1 - g0);
+            store_comp_mean(out + 4 * (size_t)g, wid, lds_group_comp(s_pts + g0, wid, g1 - g0),
+                            g1 - g0);
         }
         __syncthreads();  // LDS reused by the next tile
     }
 }
 
-// The groups queued by k_group_runs: wave w of the grid takes queue slot w, then draws further
+// The groups queued by k_group_runs: block b of the grid takes queue slot b, then draws further
 // slots (qctr[1]) while any remain - no draw at all when the queue fits the grid - and streams the
 // runs of each (records rps / rlen by sorted run, written by k_group_runs) from global memory
-// (wave_stream_sum).  The queue was complete when this launch began; the first sort pass of the
+// (block_stream_sum).  The queue was complete when this launch began; the first sort pass of the
 // next voxelize zeroes the counters.
-template <int Q, int WPB>
-__global__ __launch_bounds__(64 * WPB) void k_group_runs_big(const uint32_t* __restrict__ rps,
-                                                        const uint32_t* __restrict__ rlen,
-                                                        const float4* __restrict__ pts,
-                                                        float* __restrict__ out,
-                                                        const uint4* __restrict__ bigq,
-                                                        uint32_t bigq_cap, uint32_t* qctr) {
-    constexpr uint32_t CH = 64u * Q;
-    // WPB waves per block; a wave's run marks and points of one chunk in LDS
-    __shared__ int s_mk[WPB][CH];
-    __shared__ float4 s_ck[WPB][CH];
-    const int lane = threadIdx.x & 63, wid = WPB == 1 ? 0 : (int)(threadIdx.x >> 6);
+template <int Q>
+__global__ __launch_bounds__(256) void k_group_runs_big(const uint32_t* __restrict__ rps,
+                                                       const uint32_t* __restrict__ rlen,
+                                                       const float4* __restrict__ pts,
+                                                       float* __restrict__ out,
+                                                       const uint4* __restrict__ bigq,
+                                                       uint32_t bigq_cap, uint32_t* qctr) {
+    __shared__ int s_mark[64 * Q];
+    __shared__ __attribute__((aligned(16))) float s_soa[4][kRowStride * Q];
+    __shared__ uint32_t s_t;
+    const uint32_t wid = threadIdx.x >> 6;  // (the component)
     const uint32_t nq = min(__hip_atomic_load(qctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), bigq_cap);
-    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
-    uint32_t t = blockIdx.x * (blockDim.x >> 6) + wid;
+    uint32_t t = blockIdx.x;
     // one queue slot per draw: queued groups range over 10^3x in length (C3: up to 139 K points),
     // and draws of 8 consecutive slots (neighbouring keys, similar lengths) measured 1.7 -> 2.8 ms
     // of tail imbalance on the C3 window
-    while (t < nq) {  // wave-uniform
+    while (t < nq) {  // block-uniform
         const uint4 q = bigq[t];
         uint32_t np = 0;
-        float sum[4] = {0.f, 0.f, 0.f, 0.f};
-        wave_stream_sum<Q>(rps, rlen, q.y, q.z, pts, s_mk[wid], s_ck[wid], sum, np);
-        store_mean(out + 4 * (size_t)q.x, sum, np);
-        if (nq <= waves) break;
-        uint32_t d = 0;
-        if (lane == 0) d = atomicAdd(qctr + 1, 1u);
-        d = __shfl(d, 0, 64);
-        if (d >= nq - waves) break;
-        t = waves + d;
+#ifdef GDF_TRACE_GROUPS
+        unsigned long long tr[5] = {0, 0, 0, 0, 0};
+        const unsigned long long w0 = wall_clock64(), c0 = clock64();
+        const float sum = block_stream_sum<Q>(rps, rlen, q.y, q.z, pts, s_mark, s_soa, np, tr);
+        if (threadIdx.x == 128 && t < kTraceSlots) {  // (wave 2: z)
+            unsigned long long* g = g_gtrace[t];
+            g[0] = w0;
+            g[1] = wall_clock64();
+            g[2] = ((unsigned long long)np << 32) | (unsigned)tr[4];
+            g[3] = clock64() - c0;
+            g[4] = tr[0];
+            g[5] = tr[1];
+            g[6] = tr[2];
+            // HW_ID (hwreg 4: wave, simd, pipe, cu, sh, se) and XCC_ID (hwreg 20) bits 0..15
+            const unsigned long long hw = (unsigned)__builtin_amdgcn_s_getreg(4 | (15 << 11)) & 0xFFFFu;
+            const unsigned long long xcc = (unsigned)__builtin_amdgcn_s_getreg(20 | (15 << 11)) & 0xFu;
+            g[7] = tr[3] | (hw << 40) | (xcc << 56);
+        }
+#else
+        const float sum = block_stream_sum<Q>(rps, rlen, q.y, q.z, pts, s_mark, s_soa, np, nullptr);
+#endif
+        store_comp_mean(out + 4 * (size_t)q.x, wid, sum, np);
+        if (nq <= gridDim.x) break;
+        if (threadIdx.x == 0) s_t = atomicAdd(qctr + 1, 1u);
+        __syncthreads();
+        const uint32_t d = s_t;
+        __syncthreads();
+        if (d >= nq - gridDim.x) break;
+        t = gridDim.x + d;
     }
 }
+
+#ifdef GDF_TRACE_GROUPS
+extern "C" int gdf_debug_group_trace(void* dst, size_t bytes) {  // (diagnostic build only)
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_gtrace), std::min(bytes, sizeof(g_gtrace)), 0,
+                                    hipMemcpyDeviceToHost);
+}
+extern "C" int gdf_debug_group_trace_clear() {
+    static unsigned long long zero[kTraceSlots][8];
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_gtrace), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
+}
+#endif
 
 size_t voxelize_status_words(uint32_t nmax, uint32_t key_bits) {  // (tiles of >= 4 keys per thread)
     return (size_t)((nmax + kSortThreads * 4 - 1) / (kSortThreads * 4) + 1) *
@@ -3419,13 +3289,13 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
             const bool q16 = g_run_q16 == 1 ||
                              (g_run_q16 == 2 && a.nframes <= 1 && a.group_marks == nullptr);
             if (q16)
-                hipLaunchKernelGGL((k_group_runs_big<16, 1>), dim3(4 * g_run_big_blocks), dim3(64), 0,
-                                   s, kbuf[npasses & 1], vbuf[npasses & 1], a.pts,
+                hipLaunchKernelGGL((k_group_runs_big<16>), dim3(g_run_big_blocks), dim3(256), 0, s,
+                                   kbuf[npasses & 1], vbuf[npasses & 1], a.pts,
                                    reinterpret_cast<float*>(a.out), a.bigq, a.bigq_cap, qctr);
             else
-                hipLaunchKernelGGL((k_group_runs_big<4, 4>), dim3(g_run_big_blocks), dim3(256), 0, s, kbuf[npasses & 1],
-                               vbuf[npasses & 1], a.pts, reinterpret_cast<float*>(a.out), a.bigq,
-                               a.bigq_cap, qctr);
+                hipLaunchKernelGGL((k_group_runs_big<8>), dim3(g_run_big_blocks), dim3(256), 0, s,
+                                   kbuf[npasses & 1], vbuf[npasses & 1], a.pts,
+                                   reinterpret_cast<float*>(a.out), a.bigq, a.bigq_cap, qctr);
         }
         return hipGetLastError();
     }

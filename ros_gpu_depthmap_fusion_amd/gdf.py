@@ -508,6 +508,12 @@ class GPUDepthmapFusion:
                                                         C.byref(cnt)))
         return out[:cnt.value]
 
+    def voxelized_count(self) -> int:
+        """Voxels of the last voxelize (waits for the engine's stream)."""
+        cnt = C.c_uint32()
+        self._check(self._lib.gdf_download_voxelized_points(self._h, None, 0, C.byref(cnt)))
+        return cnt.value
+
     def downloadVoxelizedPoints(self) -> np.ndarray:
         cnt = C.c_uint32()
         self._check(self._lib.gdf_download_voxelized_points(self._h, None, 0, C.byref(cnt)))

@@ -21,6 +21,7 @@ def hip():
         _hip.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
         _hip.hipFree.argtypes = [C.c_void_p]
         _hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        _hip.hipMemcpyAsync.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
         _hip.hipMemset.argtypes = [C.c_void_p, C.c_int, C.c_size_t]
         _hip.hipSetDevice.argtypes = [C.c_int]
         _hip.hipEventCreate.argtypes = [C.POINTER(C.c_void_p)]
@@ -46,6 +47,12 @@ def device_count() -> int:
 
 def set_device(d: int):
     check(hip().hipSetDevice(d), "hipSetDevice")
+
+
+def copy_async(dst: int, src: int, nbytes: int, kind: int, stream: int):
+    """hipMemcpyAsync on `stream` (ordered with the engine / torch work of that stream)."""
+    check(hip().hipMemcpyAsync(C.c_void_p(dst), C.c_void_p(src), int(nbytes), kind,
+                               C.c_void_p(stream)), "hipMemcpyAsync")
 
 
 def synchronize():

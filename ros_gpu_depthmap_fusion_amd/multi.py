@@ -205,6 +205,29 @@ def exchange_points(send_pts, send_keys, counts, group=None):
     return rp, rk, rcounts
 
 
+def exchange_points_dev(send_pts, send_keys, send_counts, group=None):
+    """exchange_points for device tensors with the send counts still on the device (the
+    partition's output): the counts' all-to-all runs on the device and ONE host read brings both
+    the send and the receive split sizes (one synchronisation of the stream per exchange)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    dev = send_pts.device
+    c = send_counts.to(torch.int64)
+    rc = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_to_all_single(rc, c, group=group)
+    both = torch.cat([c, rc]).cpu().tolist()  # the one host synchronisation
+    scounts, rcounts = [int(x) for x in both[:world]], [int(x) for x in both[world:]]
+    n, m = sum(rcounts), sum(scounts)
+    rp = torch.empty((n, 4), dtype=torch.float32, device=dev)
+    rk = torch.empty(n, dtype=torch.int32, device=dev)
+    dist.all_to_all_single(rp, send_pts[:m], output_split_sizes=rcounts,
+                           input_split_sizes=scounts, group=group)
+    dist.all_to_all_single(rk, send_keys[:m], output_split_sizes=rcounts,
+                           input_split_sizes=scounts, group=group)
+    return rp, rk, rcounts, scounts
+
+
 class FusedCloudRank:
     """One rank of the multi-GPU frame with the reference's fused output, over a GPU engine.
 
@@ -243,8 +266,8 @@ class FusedCloudRank:
             # (bytes: gloo has no 16-bit integer collectives)
             if self.dev == "cuda":
                 tail = torch.empty(2 * self.Lmax, dtype=torch.uint8, device="cuda")
-                h.check(h.hip().hipMemcpy(tail.data_ptr(), tail_src_ptr, 2 * self.Lmax, h.D2D),
-                        "tail")
+                h.copy_async(tail.data_ptr(), tail_src_ptr, 2 * self.Lmax, h.D2D,
+                             torch.cuda.current_stream().cuda_stream)
                 parts = all_gather_tails(tail)
                 halo = parts[self.rank - 1] if self.rank > 0 else None
                 halo_ptr = halo.data_ptr() if halo is not None else 0
@@ -290,8 +313,7 @@ class FusedCloudRank:
             sk = torch.empty(n_total, dtype=torch.int32, device="cuda")
             cnt = torch.empty(self.world, dtype=torch.int32, device="cuda")
             eng.partition_points(self.world, sp.data_ptr(), sk.data_ptr(), n_total, cnt.data_ptr())
-            counts = cnt.cpu().tolist()
-            rp, rk, rc = exchange_points(sp, sk, counts)
+            rp, rk, rc, counts = exchange_points_dev(sp, sk, cnt)
             eng.voxelize_points(rp.data_ptr(), rk.data_ptr(), int(sum(rc)), self.p.voxel_average)
             self._keep = (rp, rk)
         else:
@@ -331,8 +353,9 @@ class FusedCloudRank:
         if self.F > 0 and self.world > 1:
             if self.dev == "cuda":
                 tail = torch.empty(B * L2, dtype=torch.uint8, device="cuda")
+                stream = torch.cuda.current_stream().cuda_stream
                 for j, src in enumerate(tail_src_ptrs):
-                    h.check(h.hip().hipMemcpy(tail.data_ptr() + j * L2, src, L2, h.D2D), "tail")
+                    h.copy_async(tail.data_ptr() + j * L2, src, L2, h.D2D, stream)
                 parts = all_gather_tails(tail)
                 if self.rank > 0:
                     keep.append(parts[self.rank - 1])
@@ -386,8 +409,7 @@ class FusedCloudRank:
             sk = torch.empty(n_total, dtype=torch.int32, device="cuda")
             cnt = torch.empty(self.world, dtype=torch.int32, device="cuda")
             eng.partition_points(self.world, sp.data_ptr(), sk.data_ptr(), n_total, cnt.data_ptr())
-            counts = cnt.cpu().tolist()
-            rp, rk, rc = exchange_points(sp, sk, counts)
+            rp, rk, rc, counts = exchange_points_dev(sp, sk, cnt)
             eng.voxelize_points(rp.data_ptr(), rk.data_ptr(), int(sum(rc)), self.p.voxel_average)
             keep += [rp, rk]
         else:
@@ -407,6 +429,45 @@ class FusedCloudRank:
             keep += [drp, drk]
         self._keep = keep
         return counts
+
+
+def gather_fused_cloud(rank_obj, root: int = 0):
+    """The fused voxel cloud on rank `root`: every rank's voxels (its key range of the frame's -
+    or the batch's - m_points_voxelized) concatenated in rank order, which is ascending key order,
+    i.e. the reference's single voxelize over all cameras (fusion.cpp:1743-1756) as the component
+    publishes it (component.cpp:389-461).  Returns an (n, 4) float32 tensor on root (device for
+    "cuda", host for "cpu"), None elsewhere.  One count all-gather (one host read) + one gather
+    of the padded voxel lists."""
+    import torch
+    import torch.distributed as dist
+    eng, world, dev = rank_obj.eng, rank_obj.world, rank_obj.dev
+    h = rank_obj.hiprt
+    rank = dist.get_rank()
+    if dev == "cuda":
+        n = eng.voxelized_count()  # (reads the engine's count: the stream has run voxelize)
+        cnt = torch.tensor([n], dtype=torch.int64, device="cuda")
+        allc = torch.empty(world, dtype=torch.int64, device="cuda")
+        dist.all_gather_into_tensor(allc, cnt)
+        counts = [int(x) for x in allc.cpu().tolist()]
+        mx = max(max(counts), 1)
+        mine = torch.zeros((mx, 4), dtype=torch.float32, device="cuda")
+        if n:
+            vptr = eng.device_results()[2]
+            h.copy_async(mine.data_ptr(), vptr, 16 * n, h.D2D, torch.cuda.current_stream().cuda_stream)
+    else:
+        vox = eng.downloadVoxelizedPoints()
+        n = len(vox)
+        allc = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(allc, torch.tensor([n], dtype=torch.int64))
+        counts = [int(x.item()) for x in allc]
+        mx = max(max(counts), 1)
+        mine = torch.zeros((mx, 4), dtype=torch.float32)
+        mine[:n] = torch.from_numpy(vox)
+    parts = [torch.empty_like(mine) for _ in range(world)] if rank == root else None
+    dist.gather(mine, parts, dst=root)
+    if rank != root:
+        return None
+    return torch.cat([parts[r][:counts[r]] for r in range(world)])
 
 
 def _d2h(h, ptr, dtype, count):

@@ -48,6 +48,11 @@ def _rank(rank, world, port, F, out_dir):
         fr.frame(d.ptr, d.ptr + 2 * (n - fr.Lmax))
         np.save(os.path.join(out_dir, f"vox_r{rank}_f{f}.npy"), eng.downloadVoxelizedPoints()[:, :3])
         np.save(os.path.join(out_dir, f"grid_r{rank}_f{f}.npy"), eng.downloadVoxelOccupancyGrid())
+        pub = multi.gather_fused_cloud(fr, root=0)  # the publishing rank's fused cloud
+        if rank == 0:
+            np.save(os.path.join(out_dir, f"pub_f{f}.npy"), pub.numpy()[:, :3])
+        else:
+            assert pub is None
     dist.barrier()
     dist.destroy_process_group()
 
@@ -76,6 +81,8 @@ def test_two_rank_fused_cloud_hip(tmp_path, F):
         got = np.concatenate([np.load(tmp_path / f"vox_r{r}_f{f}.npy") for r in range(world)])
         assert len(got) == len(want) > 0, f"frame {f}"
         assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), f"frame {f}"
+        pub = np.load(tmp_path / f"pub_f{f}.npy")  # gathered on rank 0 = the single engine's
+        assert np.array_equal(pub.view(np.uint32), want.view(np.uint32)), f"published frame {f}"
         for r in range(world):
             np.testing.assert_array_equal(np.load(tmp_path / f"grid_r{r}_f{f}.npy"),
                                           orc.downloadVoxelOccupancyGrid(), f"frame {f} rank {r}")
@@ -185,3 +192,65 @@ def test_fused_cloud_survey_configs(tmp_path, cfg):
         for r in range(world):
             np.testing.assert_array_equal(np.load(tmp_path / f"grid_r{r}_f{f}.npy"), g,
                                           f"{cfg} frame {f} rank {r}")
+
+
+def _rank_nccl(rank, world, port, out_dir):
+    """One process, RCCL (backend "nccl") at world 1: FusedCloudRank(dev="cuda") with the engine
+    on torch's stream - the device collectives (all-gather of marks, all-to-all of counts and of
+    the (point, key) lists, the gather of the fused cloud) over RCCL, frame by frame and per
+    batch."""
+    import torch
+    import torch.distributed as dist
+    from ros_gpu_depthmap_fusion_amd import build_library, hiprt, multi
+    from ros_gpu_depthmap_fusion_amd.gdf import GPUDepthmapFusion
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    build_library()
+    p = ComponentParams()
+    cams = [synth.make_camera(k, W, H) for k in range(world)]
+    eng = GPUDepthmapFusion(0)
+    fr = multi.FusedCloudRank(eng, cams, rank, world, p, dev="cuda")
+    n = W * H
+    ds = [hiprt.DeviceArray.from_numpy(synth.dense_frame(cams[rank], rank, f)) for f in range(4)]
+    for f in range(2):
+        fr.frame(ds[f].ptr, ds[f].ptr + 2 * (n - fr.Lmax))
+        torch.cuda.synchronize()
+        np.save(os.path.join(out_dir, f"nvox_f{f}.npy"), eng.downloadVoxelizedPoints()[:, :3])
+        np.save(os.path.join(out_dir, f"ngrid_f{f}.npy"), eng.downloadVoxelOccupancyGrid())
+        np.save(os.path.join(out_dir, f"npub_f{f}.npy"),
+                multi.gather_fused_cloud(fr, root=0).cpu().numpy()[:, :3])
+    fr.batch([d.ptr for d in ds[2:]], [d.ptr + 2 * (n - fr.Lmax) for d in ds[2:]])
+    torch.cuda.synchronize()
+    vox = eng.downloadVoxelizedPoints()[:, :3]
+    _, vs = eng.batch_ranges()
+    for j in range(2):
+        np.save(os.path.join(out_dir, f"nvox_f{2 + j}.npy"), vox[vs[j]:vs[j + 1]])
+    np.save(os.path.join(out_dir, "ngrid_f3.npy"), eng.downloadVoxelOccupancyGrid())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_rccl_fused_cloud_world1(tmp_path):
+    """The RCCL branch of FusedCloudRank (dev="cuda", backend nccl) on the box's GPU at world 1:
+    two frames one by one, then a 2-frame batch - voxel means, grids and the gathered publishing
+    cloud equal the oracle bit for bit."""
+    from oracle import OracleFusion
+    mp.start_processes(_rank_nccl, args=(1, _free_port(), str(tmp_path)), nprocs=1, join=True,
+                       start_method="spawn")
+    p = ComponentParams()
+    cam = synth.make_camera(0, W, H)
+    orc = OracleFusion(threads=4)
+    for f in range(4):
+        orc.clear()
+        orc.addDepthmap(synth.dense_frame(cam, 0, f), *cam.intrinsics(), cam.T_world, cam.T_crop)
+        orc.processFrame(p)
+        want = orc.downloadVoxelizedPoints()[:, :3]
+        got = np.load(tmp_path / f"nvox_f{f}.npy")
+        assert len(got) == len(want) > 0 and np.array_equal(got.view(np.uint32), want.view(np.uint32)), f
+        if f < 2:
+            pub = np.load(tmp_path / f"npub_f{f}.npy")
+            assert np.array_equal(pub.view(np.uint32), want.view(np.uint32)), f"published {f}"
+        if f != 2:
+            np.testing.assert_array_equal(np.load(tmp_path / f"ngrid_f{f}.npy"),
+                                          orc.downloadVoxelOccupancyGrid(), f"frame {f}")

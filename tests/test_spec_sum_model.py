@@ -1,12 +1,12 @@
-"""CPU check of the voxel-sum algorithm the GPU kernels use (tests/spec_sum_model.py restates
-gdf_kernels.hip spec_try / spec_finish / row_sum4): the stretch evaluation equals the
+"""CPU check of the voxel-sum algorithms the GPU kernels use (tests/spec_sum_model.py restates
+gdf_voxsum.hpp comp_stretch_sum and rows_chunk_sum): the stretch evaluation equals the
 reference's sequential f32 chain (inc/voxelize.h:29-35) bit for bit on adversarial inputs -
 ties at every binade, sums crossing zero, exact cancellation, subnormals, huge terms, inf/NaN,
 long monotone sums - and on the points of a real dense frame's voxels."""
 import numpy as np
 import pytest
 
-from spec_sum_model import group_sum, sequential_sum
+from spec_sum_model import cursor_sum, group_sum, rows_sum, sequential_sum
 
 f32 = np.float32
 
@@ -49,6 +49,10 @@ def cases():
 def test_stretch_sum_equals_sequential_chain(name):
     x = cases()[name]
     assert same(group_sum(x), sequential_sum(x)), name
+    for R in (1, 2, 4):  # the GPU's cursor form
+        assert same(cursor_sum(x, R), sequential_sum(x)), (name, R)
+    for NR in (16, 8, 1):  # the row form (k_group_runs_big)
+        assert same(rows_sum(x, NR), sequential_sum(x)), (name, NR)
 
 
 def test_random_prefixes_and_row_offsets():
@@ -60,6 +64,8 @@ def test_random_prefixes_and_row_offsets():
              np.round(rng.normal(0, 5, 200)) * 2.0 ** -3][dist].astype(f32)
         for n in range(0, 201, 7):
             assert same(group_sum(x[:n]), sequential_sum(x[:n])), (dist, n)
+            assert same(cursor_sum(x[:n], 2), sequential_sum(x[:n])), (dist, n)
+            assert same(rows_sum(x[:n], 1), sequential_sum(x[:n])), (dist, n)
 
 
 def test_dense_frame_voxels_match_and_stretches_are_few():
@@ -86,6 +92,8 @@ def test_dense_frame_voxels_match_and_stretches_are_few():
         for c in range(4):
             stats = long_stats if e - a >= 256 else None
             s = group_sum(ps[a:e, c], stats)
+            if e - a >= 64:
+                assert same(rows_sum(ps[a:e, c]), s)
             want = V[g, c] * f32(e - a) if c < 3 else V[g, c]
             if c == 3:
                 assert same(s, want)

@@ -1,6 +1,6 @@
 """Runs one fused-frame configuration for N frames (profiling driver for rocprofv3 / PMC).
 
-    python tools/frame_driver.py W H F ROT45(0/1) [frames]
+    python tools/frame_driver.py W H F ROT45(0/1) [frames] [dense|stress]
 """
 import os
 import sys
@@ -13,16 +13,17 @@ from ros_gpu_depthmap_fusion_amd.gdf import ComponentParams, GPUDepthmapFusion  
 def main():
     W, H, F, rot = (int(x) for x in sys.argv[1:5])
     frames = int(sys.argv[5]) if len(sys.argv) > 5 else 50
+    gen = synth.WORKLOADS[sys.argv[6] if len(sys.argv) > 6 else "stress"]
     build_library()
     cam = synth.make_camera(0, W, H)
-    dframes = [hiprt.DeviceArray.from_numpy(synth.depth_frame(cam, 0, f)) for f in range(4)]
+    dframes = [hiprt.DeviceArray.from_numpy(gen(cam, 0, f)) for f in range(2)]
     eng = GPUDepthmapFusion(0)
     p = ComponentParams()
     p.flying_filter_size, p.flying_rot45 = F, bool(rot)
     pc = p.to_c(None, None, False, False)
     for i in range(frames):
         eng.clear()
-        eng.addDepthmapDevice(dframes[i % 4].ptr, W, H, *cam.intrinsics(), cam.T_world, cam.T_crop)
+        eng.addDepthmapDevice(dframes[i % 2].ptr, W, H, *cam.intrinsics(), cam.T_world, cam.T_crop)
         eng.processFramePrepared(pc)
     eng.synchronize()
 
