@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "gdf.h"
+#include "gdf_objects.hpp"
 #include "gdf_segment.h"
 
 // The component calls glMemoryBarrier(GL_ALL_BARRIER_BITS) between the engine calls
@@ -214,9 +215,20 @@ public:
         check(gdf_download_points(h_, reinterpret_cast<float*>(m_points.data()), n, &n));
         m_points.resize(n);
     }
-    // GridMeta::worldCoord: lower corner of voxel (x, y, z)
-    vec4 voxelCoordToWorldCoord(float x, float y, float z) const {
-        return vec4{x * cs_[0] + lo_[0], y * cs_[1] + lo_[1], z * cs_[2] + lo_[2], 1.0f};
+    // the mapped variant (fusion.cpp:2952-2966): the points in host memory until unmap
+    void* downloadPoints(int& count_out) {
+        downloadPoints();
+        count_out = (int)m_points.size();
+        return m_points.data();
+    }
+    void unmap() {}
+    // voxelCoordToWorldCoord / worldCoordToVoxelCoord (gpu_depthmap_fusion.cpp:1720-1741): the
+    // lower corner of voxel (x, y, z), and back (glm::vec3 arithmetic in f32)
+    vec3 voxelCoordToWorldCoord(float x, float y, float z) const {
+        return vec3(x * cs_[0] + lo_[0], y * cs_[1] + lo_[1], z * cs_[2] + lo_[2]);
+    }
+    vec3 worldCoordToVoxelCoord(float x, float y, float z) const {
+        return vec3((x - lo_[0]) / cs_[0], (y - lo_[1]) / cs_[1], (z - lo_[2]) / cs_[2]);
     }
 
     // the component's whole per-frame sequence as one call (gdf_process_frame)
@@ -275,6 +287,22 @@ public:
                                            m_ccLayersConnectionsData.size(),
                                            m_ccLayersConnectionsDataStarts.data(),
                                            (uint32_t)m_ccLayersConnectionsDataStarts.size()));
+        // the cv::Mat_ views of the reference (fusion.cpp:1915, 2004-2010, 2108-2111)
+        m_ccLabeledLayers.resize(L);
+        m_ccStats.resize(L);
+        m_ccCentroids.resize(L);
+        for (uint32_t i = 0; i < L; ++i) {
+            m_ccLabeledLayers[i] = Mat_<uint16_t>((int)c.height, (int)c.width,
+                                                  m_ccLabeledLayersData.data() + (size_t)i * c.width * c.height);
+            const int nl = (int)m_ccNumLabelsPerLayer[i];
+            m_ccStats[i] = Mat_<int32_t>(nl, 5, m_ccStatsData.data() + m_ccStatsDataStarts[i]);
+            m_ccCentroids[i] = Mat_<double>(nl, 2, m_ccCentroidsData.data() + m_ccCentroidsDataStarts[i]);
+        }
+        m_ccLayersConnections.resize(L ? L - 1 : 0);
+        for (uint32_t i = 0; i + 1 < L; ++i)
+            m_ccLayersConnections[i] = Mat_<uint8_t>(
+                (int)m_ccNumLabelsPerLayer[i], (int)m_ccNumLabelsPerLayer[i + 1],
+                m_ccLayersConnectionsData.data() + m_ccLayersConnectionsDataStarts[i]);
     }
     // the label upload, connection-matrix preparation and the layers_connections dispatch are
     // part of labelVoxels here (the labels never leave the device)
@@ -297,24 +325,29 @@ public:
             }
         m_ccNumObjects = nobj;
     }
-    // createCCObjects (:2364-2550) without the OpenCV shapes: the objects' aggregate fields and
-    // their components (global label indices, grouped)
+    // createCCObjects (:2364-2550): the objects' aggregate fields and their components (global
+    // label indices, grouped) from the GPU (gdf_seg_create_objects), then on the host each
+    // component's contour in voxel and world coordinates, the per-layer and top-view point sets
+    // and the minimal shapes (gdf_objects.hpp) of components, layers and top view
     void createCCObjects() {
         uint32_t n = 0;
         check(gdf_seg_create_objects(seg_, lo_, cs_, nullptr, 0, nullptr, 0, &n));
-        m_ccObjects.resize(n);
+        m_ccObjectRecords.resize(n);
         m_ccObjectComponents.resize(m_ccLabelsMerged.size());
-        check(gdf_seg_create_objects(seg_, lo_, cs_, m_ccObjects.data(), n,
+        check(gdf_seg_create_objects(seg_, lo_, cs_, m_ccObjectRecords.data(), n,
                                      m_ccObjectComponents.data(),
                                      (uint32_t)m_ccObjectComponents.size(), &n));
+        m_ccObjects.assign(n, CCObject());
+        for (uint32_t i = 0; i < n; ++i) build_object(m_ccObjectRecords[i], m_ccObjects[i]);
     }
-    // objectSegmentation (:2552-2575); the shapes and objectTracking stay out of scope
-    // 
+    // objectSegmentation (:2552-2575)
     void objectSegmentation() {
         labelVoxels();
         mergeLabelsAcrossLayers();
         createCCObjects();
     }
+    // objectTracking (:2727-2944): associates m_ccObjects with m_ccObjectTracks
+    void objectTracking(float min_area) { object_tracking(m_ccObjects, m_ccObjectTracks, min_area); }
 
     gdf_rollbuffer_state rollbufferState() {
         gdf_rollbuffer_state s{};
@@ -339,9 +372,6 @@ public:
     uint32_t m_rollBufferLastTimeSec = 0, m_rollBufferLastTimeNSec = 0;
     // segmentation members (gpu_depthmap_fusion.h:328-341, 511-518), flat like their *Data
     // storage; cv::Mat_ views of them are (rows, cols, pointer) over these vectors
-    struct Point {  // cv::Point
-        int x, y;
-    };
     std::vector<uint16_t> m_ccLabeledLayersData;
     std::vector<uint32_t> m_ccNumLabelsPerLayer;
     std::vector<int32_t> m_ccStatsData;
@@ -353,10 +383,63 @@ public:
     std::vector<uint64_t> m_ccLayersConnectionsDataStarts;
     std::vector<uint32_t> m_ccLabelsMerged, m_ccLabelsLayer, m_ccLabelsLocal, m_ccLabelsLayerStarts;
     uint32_t m_ccNumObjects = 0;
-    std::vector<gdf_cc_object> m_ccObjects;
+    // cv::Mat_ views over the *Data vectors (gpu_depthmap_fusion.h:328-333), valid until the next
+    // labelVoxels
+    std::vector<Mat_<uint16_t>> m_ccLabeledLayers;
+    std::vector<Mat_<int32_t>> m_ccStats;
+    std::vector<Mat_<double>> m_ccCentroids;
+    std::vector<Mat_<uint8_t>> m_ccLayersConnections;
+    std::vector<CCObject> m_ccObjects;            // (gpu_depthmap_fusion.h:342)
+    std::vector<CCObjectTrack> m_ccObjectTracks;  // (gpu_depthmap_fusion.h:343)
+    std::vector<gdf_cc_object> m_ccObjectRecords;  // the GPU's aggregates behind m_ccObjects
     std::vector<uint32_t> m_ccObjectComponents;
 
 private:
+    // one CCObject from the GPU record + the contours (fusion.cpp:2371-2537)
+    void build_object(const gdf_cc_object& R, CCObject& obj) const {
+        obj.centroid = Point2f(R.centroid[0], R.centroid[1]);
+        obj.label = R.label;
+        obj.num_components = R.num_components;
+        obj.num_layers = R.num_layers;
+        obj.min_coord.voxel = ivec3(R.min_voxel[0], R.min_voxel[1], R.min_voxel[2]);
+        obj.max_coord.voxel = ivec3(R.max_voxel[0], R.max_voxel[1], R.max_voxel[2]);
+        obj.aabb_size.voxel = ivec3(R.aabb_voxel[0], R.aabb_voxel[1], R.aabb_voxel[2]);
+        obj.center_coord.voxel = vec3(R.center_voxel[0], R.center_voxel[1], R.center_voxel[2]);
+        obj.center_coord.world = vec3(R.center_world[0], R.center_world[1], R.center_world[2]);
+        obj.min_coord.world = vec3(R.min_world[0], R.min_world[1], R.min_world[2]);
+        obj.max_coord.world = vec3(R.max_world[0], R.max_world[1], R.max_world[2]);
+        obj.aabb_size.world = vec3(R.aabb_world[0], R.aabb_world[1], R.aabb_world[2]);
+        obj.components.assign(R.num_components, CCObject::Component());
+        obj.layers.assign(R.num_layers, CCObject::Layer());
+        for (uint32_t k = 0; k < R.num_components; ++k) {
+            const uint32_t idx = m_ccObjectComponents[R.first_component + k];
+            const uint32_t layer = m_ccLabelsLayer[idx], local = m_ccLabelsLocal[idx];
+            const int ci = m_labelsToContoursPerLayer[layer][local];
+            if (ci < 0) continue;
+            const std::vector<Point>& contour = m_contoursPerLayer[layer][ci];
+            CCObject::Component& cmp = obj.components[k];
+            CCObject::Layer& ly = obj.layers[layer - (uint32_t)obj.min_coord.voxel.z];
+            for (const Point& p : contour) {
+                const vec3 w = voxelCoordToWorldCoord((float)p.x, (float)p.y, (float)layer);
+                cmp.contour3d.voxel.push_back(vec3((float)p.x, (float)p.y, (float)layer));
+                cmp.contour3d.world.push_back(w);
+                cmp.contour2d.voxel.push_back(Point2f((float)p.x, (float)p.y));
+                cmp.contour2d.world.push_back(Point2f(w.x, w.y));
+                ly.points2d.voxel.push_back(cmp.contour2d.voxel.back());
+                ly.points2d.world.push_back(cmp.contour2d.world.back());
+                obj.topview.points2d.world.push_back(cmp.contour2d.world.back());
+                obj.topview.points2d.voxel.push_back(cmp.contour2d.voxel.back());
+            }
+            cmp.shapes.voxel = CCObject::MinShapes(cmp.contour2d.voxel);
+            cmp.shapes.world = CCObject::MinShapes(cmp.contour2d.world);
+        }
+        for (CCObject::Layer& ly : obj.layers) {
+            ly.shapes.voxel = CCObject::MinShapes(ly.points2d.voxel);
+            ly.shapes.world = CCObject::MinShapes(ly.points2d.world);
+        }
+        obj.topview.shapes.voxel = CCObject::MinShapes(obj.topview.points2d.voxel);
+        obj.topview.shapes.world = CCObject::MinShapes(obj.topview.points2d.world);
+    }
     void syncRollbuffer() {
         const gdf_rollbuffer_state r = rollbufferState();
         m_rollBufferNumPoints = r.num_points;

@@ -2494,6 +2494,7 @@ uint32_t g_group_scan_tiles = 1024;
 constexpr int kSmallGroup = 16;  // groups summed by one thread; longer ones by a wave
 
 constexpr uint32_t kChainPad = 16;  // LDS padding of staged point buffers
+constexpr uint32_t kExtraRuns = 64;  // runs past a k_group_runs tile read for its last group
 
 // Voxel sums, one component per wave (gdf_voxsum.hpp): wave c of a 4-wave group sums component c.
 // A staged group of cnt points (float4 AoS in LDS)
@@ -2753,7 +2754,7 @@ __global__ __launch_bounds__(256) void k_group_big(const uint32_t* __restrict__ 
 // which a staged group is summed in-block (larger ones are queued); tuning knobs GDF_RUN_STAGE,
 // GDF_RUN_INBLOCK
 uint32_t g_run_stage = 2048;
-uint32_t g_run_inblock = 256;
+uint32_t g_run_inblock = 2048;
 uint32_t g_run_big_blocks = 1024;  // k_group_runs_big grid (tuning knob GDF_RUN_BIG_BLOCKS)
 // chunks of k_group_runs_big (one 4-wave block per queued group): 1 K points (Q = 16) or 512
 // (Q = 8); 0 never 1 K, 1 always, 2 (default) for single depth-only frames, whose long voxels
@@ -2766,70 +2767,136 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Wave64 inclusive scans on DPP (row shifts inside the 16-lane rows, then the row broadcasts of
-// lanes 15 and 31): six dependent VALU steps, no LDS round trips.
-__device__ __forceinline__ int dpp_max_scan(int v) {  // (values >= -1)
-    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x111, 0xf, 0xf, false));  // row_shr:1
-    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x112, 0xf, 0xf, false));  // row_shr:2
-    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x114, 0xf, 0xf, false));  // row_shr:4
-    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x118, 0xf, 0xf, false));  // row_shr:8
-    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
-    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
-    return v;
-}
+// Wave64 inclusive sum scan on DPP (gdf_voxsum.hpp dpp_iscan).
 __device__ __forceinline__ uint32_t dpp_sum_scan(uint32_t x) { return (uint32_t)dpp_iscan((int)x); }
 
 struct RunRec {
     uint32_t ps, len;
 };
 
-// A group's points stream through a 4-wave block in order: batches of 64 sorted runs (one per lane;
-// the records rps / rlen - first point, length - are indexed by sorted run, contiguous, and read
-// two batches ahead), their points in chunks of 64 x Q positions - position -> run by a max-scan of
-// the runs' first positions - loaded coalesced one chunk ahead (across batch boundaries too); wave w
-// loads rows w, w + 4, ... of a chunk, the block transposes the chunk into LDS per component and
-// wave c sums component c (gdf_voxsum.hpp) - the reference's sequential f32 sum, in stable order.
+// A group's points stream through a 4-wave block in order: batches of 256 sorted runs (4 per lane,
+// runs 4 l .. 4 l + 3 in lane l; the records rps / rlen - first point, length - are indexed by
+// sorted run, contiguous, and read two batches ahead), their points in chunks of 64 x Q positions
+// - position -> run by a max-scan of the runs' first positions - loaded coalesced one chunk ahead
+// (across batch boundaries too); wave w loads rows w, w + 4, ... of a chunk, the block transposes
+// the chunk into LDS rows per component and wave c sums component c (gdf_voxsum.hpp
+// rows_chunk_sum) - the reference's sequential f32 sum, in stable order.  256-run batches keep
+// chunks nearly full where runs are short (4K frames: ~100 points per run of a long voxel, C3
+// windows ~11): a chunk never spans two batches.
+constexpr int kRunsPerLane = 4;
+struct RunRecs {
+    uint32_t ps[kRunsPerLane], len[kRunsPerLane];
+};
 struct RunBatch {
-    uint32_t ps, off, len;  // run `lane` of the batch: first point, first batch position, length
-    uint32_t T;             // the batch's points (wave-uniform)
+    uint32_t off[kRunsPerLane], len[kRunsPerLane];  // runs 4 lane + j: first batch position, length
+    uint32_t base[kRunsPerLane];                    // first point - first batch position
+    uint32_t T;                                     // the batch's points (wave-uniform)
 };
 
-__device__ __forceinline__ RunBatch run_batch(const RunRec& r) {
-    const uint32_t x = dpp_sum_scan(r.len);
-    return RunBatch{r.ps, x - r.len, r.len, (uint32_t)__builtin_amdgcn_readlane((int)x, 63)};
+__device__ __forceinline__ RunBatch run_batch(const RunRecs& r) {
+    RunBatch b;
+    uint32_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < kRunsPerLane; ++j) {
+        b.off[j] = acc;
+        acc += r.len[j];
+    }
+    const uint32_t x = dpp_sum_scan(acc);
+#pragma unroll
+    for (int j = 0; j < kRunsPerLane; ++j) {
+        b.off[j] += x - acc;
+        b.len[j] = r.len[j];
+        b.base[j] = r.ps[j] - b.off[j];
+    }
+    b.T = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+    return b;
 }
 
-__device__ __forceinline__ RunRec run_rec(const uint32_t* __restrict__ rps,
-                                          const uint32_t* __restrict__ rlen, uint32_t r, bool ok) {
-    return ok ? RunRec{rps[r], rlen[r]} : RunRec{0u, 0u};
+__device__ __forceinline__ RunRecs run_recs(const uint32_t* __restrict__ rps,
+                                            const uint32_t* __restrict__ rlen, uint32_t r0,
+                                            uint32_t re) {
+    RunRecs q;
+    const uint32_t r = r0 + kRunsPerLane * (threadIdx.x & 63);
+#pragma unroll
+    for (int j = 0; j < kRunsPerLane; ++j) {
+        const bool ok = r + j < re;
+        q.ps[j] = ok ? rps[r + j] : 0u;
+        q.len[j] = ok ? rlen[r + j] : 0u;
+    }
+    return q;
 }
 
-// This wave's rows q = wid + 4 i of the chunk at batch position c: the first positions of the runs
-// starting in them marked in s_mark (rows are disjoint between the waves), each row max-scanned,
-// carried in by the last run starting before the row (a ballot count: every run holds >= 1
-// point, so the runs' first positions increase with the lane); positions past the batch read 0.
+// This wave's copy of a batch's run bases (s_base[wave][run]) for fetch_rows4.
+__device__ __forceinline__ void put_bases(const RunBatch& bt, uint32_t* s_base) {
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < kRunsPerLane; ++j) s_base[kRunsPerLane * lane + j] = bt.base[j];
+}
+
+// N independent inclusive wave64 max-scans on DPP, step by step (values >= -1: row shifts inside
+// the 16-lane rows, then the row broadcasts of lanes 15 and 31)
+template <int N>
+__device__ __forceinline__ void dpp_max_scan_n(int (&v)[N]) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = max(v[i], __builtin_amdgcn_update_dpp(-1, v[i], 0x111, 0xf, 0xf, false));
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = max(v[i], __builtin_amdgcn_update_dpp(-1, v[i], 0x112, 0xf, 0xf, false));
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = max(v[i], __builtin_amdgcn_update_dpp(-1, v[i], 0x114, 0xf, 0xf, false));
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = max(v[i], __builtin_amdgcn_update_dpp(-1, v[i], 0x118, 0xf, 0xf, false));
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = max(v[i], __builtin_amdgcn_update_dpp(-1, v[i], 0x142, 0xa, 0xf, false));
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = max(v[i], __builtin_amdgcn_update_dpp(-1, v[i], 0x143, 0xc, 0xf, false));
+}
+
+// This wave's Q / 4 consecutive rows of the chunk at batch position c: the first positions of the
+// runs starting in them marked in s_mark (disjoint between the waves; a run outside them marks a
+// scratch slot past the chunk - no branches), the rows max-scanned side by side, the first one
+// carried in by the last run starting before it (a ballot count: every run holds >= 1 point, so
+// the runs' first positions increase with the run index) and each next one by the row before; a
+// position's point is base[run] + position (s_base: this wave's copy of the batch's bases).
+// Positions past the batch load point 0 (never summed), and no select touches the loaded values:
+// the loads stay in flight until the chunk is stored.
 template <int Q>
 __device__ __forceinline__ void fetch_rows4(const RunBatch& bt, uint32_t c, int* s_mark,
-                                            const float4* __restrict__ pts, float4 (&p)[Q / 4]) {
+                                            const uint32_t* s_base, const float4* __restrict__ pts,
+                                            float4 (&p)[Q / 4]) {
+    constexpr int RPW = Q / 4;  // rows per wave
     constexpr uint32_t CH = 64u * Q;
     const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t row0 = wid * RPW, pos_w = c + 64u * row0;
 #pragma unroll
-    for (int i = 0; i < Q / 4; ++i) s_mark[64u * (wid + 4u * i) + lane] = -1;
-    wave_sync();
-    if (bt.len && bt.off >= c && bt.off < c + CH && (((bt.off - c) >> 6) & 3u) == wid)
-        s_mark[bt.off - c] = (int)lane;
+    for (int i = 0; i < RPW; ++i) s_mark[64u * (row0 + i) + lane] = -1;
     wave_sync();
 #pragma unroll
-    for (int i = 0; i < Q / 4; ++i) {
-        const uint32_t q = wid + 4u * i;
-        const uint32_t pos0 = c + 64u * q;
-        const int carry = (int)__popcll(__ballot(bt.len != 0u && bt.off < pos0)) - 1;
-        const int m = max(dpp_max_scan(s_mark[64u * q + lane]), carry);
-        const uint32_t mps = __shfl(bt.ps, m, 64), moff = __shfl(bt.off, m, 64);
-        const uint32_t pos = pos0 + lane;
-        const bool ok = pos < bt.T;
-        const float4 v = pts[ok ? mps + (pos - moff) : 0u];
-        p[i] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int j = 0; j < kRunsPerLane; ++j) {
+        const uint32_t o = bt.off[j];
+        const bool mine = bt.len[j] != 0u && o - pos_w < 64u * RPW;
+        s_mark[mine ? o - c : CH + lane] = (int)(kRunsPerLane * lane + j);
+    }
+    wave_sync();
+    int before = 0;
+#pragma unroll
+    for (int j = 0; j < kRunsPerLane; ++j)
+        before += (int)__popcll(__ballot(bt.len[j] != 0u && bt.off[j] < pos_w));
+    int mk[RPW];
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) mk[i] = s_mark[64u * (row0 + i) + lane];
+    dpp_max_scan_n<RPW>(mk);
+    int carry = before - 1;  // (wave-uniform)
+    uint32_t b[RPW];
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+        const int m = max(mk[i], carry);
+        carry = max(carry, __builtin_amdgcn_readlane(mk[i], 63));
+        b[i] = s_base[max(m, 0)];
+    }
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+        const uint32_t pos = pos_w + 64u * i + lane;
+        p[i] = pts[pos < bt.T ? b[i] + pos : 0u];
     }
 }
 
@@ -2848,19 +2915,21 @@ template <int Q>
 __device__ __forceinline__ float block_stream_sum(const uint32_t* __restrict__ rps,
                                                   const uint32_t* __restrict__ rlen, uint32_t rs,
                                                   uint32_t re, const float4* __restrict__ pts,
-                                                  int* s_mark, float (*s_soa)[kRowStride * Q],
-                                                  uint32_t& npts, unsigned long long* tr) {
+                                                  int* s_mark, uint32_t* s_base,
+                                                  float (*s_soa)[kRowStride * Q], uint32_t& npts,
+                                                  unsigned long long* tr) {
     static_assert(Q % 4 == 0 && Q <= 16, "rows_chunk_sum takes up to 16 rows");
-    constexpr uint32_t CH = 64u * Q;
-    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    constexpr uint32_t CH = 64u * Q, NB = 64u * kRunsPerLane;  // chunk points, batch runs
+    const uint32_t wid = threadIdx.x >> 6;
     npts = 0;
     float s = 0.0f;
-    const uint32_t r0 = rs + lane;
-    RunBatch cur = run_batch(run_rec(rps, rlen, r0, r0 < re));
-    RunRec rec1 = run_rec(rps, rlen, r0 + 64u, r0 + 64u < re);    // batch 1
-    RunRec rec2 = run_rec(rps, rlen, r0 + 128u, r0 + 128u < re);  // batch 2
+    RunBatch cur = run_batch(run_recs(rps, rlen, rs, re));
+    RunRecs rec1 = run_recs(rps, rlen, rs + NB, re);      // batch 1
+    RunRecs rec2 = run_recs(rps, rlen, rs + 2u * NB, re);  // batch 2
     float4 p[Q / 4];
-    fetch_rows4<Q>(cur, 0, s_mark, pts, p);
+    put_bases(cur, s_base);
+    wave_sync();
+    fetch_rows4<Q>(cur, 0, s_mark, s_base, pts, p);
     uint32_t rb = rs, c = 0;
     while (true) {  // block-uniform: one chunk per iteration
         const uint32_t n = min(CH, cur.T - c);
@@ -2869,7 +2938,7 @@ __device__ __forceinline__ float block_stream_sum(const uint32_t* __restrict__ r
         GDF_TCLK(b1);
 #pragma unroll
         for (int i = 0; i < Q / 4; ++i) {
-            const uint32_t k = kRowStride * (wid + 4u * i) + lane;
+            const uint32_t k = kRowStride * (wid * (Q / 4) + i) + (threadIdx.x & 63);
             s_soa[0][k] = p[i].x;
             s_soa[1][k] = p[i].y;
             s_soa[2][k] = p[i].z;
@@ -2878,14 +2947,13 @@ __device__ __forceinline__ float block_stream_sum(const uint32_t* __restrict__ r
         // the next chunk, loaded while this one is summed: the rest of this batch, or the next
         // batch's first chunk (whose records were read two batches ago); none: T = 0
         const bool more = c + CH < cur.T;
-        const bool next_batch = !more && rb + 64u < re;
+        const bool next_batch = !more && rb + NB < re;
         RunBatch fb = cur;
         uint32_t cn = c + CH;
         if (next_batch) {
             fb = run_batch(rec1);
             rec1 = rec2;
-            const uint32_t r3 = rb + 192u + lane;
-            rec2 = run_rec(rps, rlen, r3, r3 < re);
+            rec2 = run_recs(rps, rlen, rb + 3u * NB, re);
             cn = 0;
         } else if (!more) {
             fb.T = 0;
@@ -2893,7 +2961,11 @@ __device__ __forceinline__ float block_stream_sum(const uint32_t* __restrict__ r
         GDF_TCLK(b2);
         __syncthreads();  // the chunk is in LDS
         GDF_TCLK(b3);
-        if (more || next_batch) fetch_rows4<Q>(fb, cn, s_mark, pts, p);
+        if (next_batch) {
+            put_bases(fb, s_base);
+            wave_sync();
+        }
+        if (more || next_batch) fetch_rows4<Q>(fb, cn, s_mark, s_base, pts, p);
         GDF_TCLK(b4);
         s = rows_chunk_sum(s_soa[wid], n, s);
         GDF_TCLK(b5);
@@ -2913,7 +2985,7 @@ __device__ __forceinline__ float block_stream_sum(const uint32_t* __restrict__ r
             cur = fb;
             c += CH;
         } else if (next_batch) {
-            rb += 64u;
+            rb += NB;
             cur = fb;
             c = 0;
         } else {
@@ -2941,13 +3013,17 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
     uint32_t* __restrict__ qctr, uint32_t nframes, uint32_t fshift, uint32_t* __restrict__ fvox,
     uint32_t inblock_max, uint32_t* __restrict__ rps, uint32_t* __restrict__ rlen) {
     __shared__ uint32_t s_wave[4];
-    __shared__ uint32_t s_tile, s_epoch, s_excl, s_nbig, s_nq, s_qbase, s_wend;
+    __shared__ uint32_t s_tile, s_epoch, s_excl, s_nbig, s_nq, s_qbase, s_wend, s_nx;
     __shared__ uint32_t s_start[kGroupThreads + 1];  // group starts (run index); [total] = end
-    __shared__ uint32_t s_ps[kGroupThreads];
-    __shared__ uint32_t s_off[kGroupThreads + 1];  // exclusive scan of the tile's run lengths
+    // the tile's runs, then up to kExtraRuns runs of the next tiles (the rest of the tile's last
+    // group): first points and the exclusive scan of their lengths
+    __shared__ uint32_t s_ps[kGroupThreads + kExtraRuns];
+    __shared__ uint32_t s_off[kGroupThreads + kExtraRuns + 1];
     __shared__ uint32_t s_big[kGroupThreads];
     __shared__ float4 s_pts[kRunStage + kChainPad];
+    __shared__ __attribute__((aligned(16))) float s_wsoa[4][kWaveSoa];  // wave_group_sum chunks
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    wave_soa_init(s_wsoa[wid]);
     const uint32_t n = *count;  // runs
     const uint32_t ntiles = (n + kGroupThreads - 1) / kGroupThreads;
     const uint32_t kmask = nframes > 1 ? (1u << fshift) - 1u : 0xFFFFFFFFu;
@@ -2973,6 +3049,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
             s_nbig = 0;
             s_nq = 0;
             s_wend = 0;
+            s_nx = 0;
         }
         walk += gridDim.x;
         __syncthreads();
@@ -3030,6 +3107,23 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
                     lo = lastp + 1u;
                 }
             }
+            // the rest of a last group continuing past the tile, when short: its runs' records
+            // (the tile is full here) - so a group is queued only when long
+            if (average && hi > tend && hi - tend <= kExtraRuns) {
+                const uint32_t nx = hi - tend;
+                uint32_t ps = 0, len = 0;
+                if ((uint32_t)lane < nx) {
+                    const uint32_t v = rvals[tend + lane];
+                    ps = run_start[v];
+                    len = run_start[v + 1] - ps;
+                }
+                const uint32_t inc = dpp_sum_scan(len);
+                if ((uint32_t)lane < nx) {
+                    s_ps[kGroupThreads + lane] = ps;
+                    s_off[kGroupThreads + 1 + lane] = ptotal + inc;
+                }
+                if (lane == 0) s_nx = nx;
+            }
             if (lane == 0) s_start[total] = hi;
         }
         // the groups summed in-block: inside the tile, <= kRunInBlock points, ending within
@@ -3037,11 +3131,12 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
         // tile's run stream up to the last such group's end; position -> run by a binary search
         // of the run offsets), the other groups are queued
         const uint32_t W0 = total ? s_off[s_start[0] - t0] : 0u;
-        __syncthreads();  // (the last group's end, s_start[total])
+        __syncthreads();  // (the last group's end, s_start[total]; the extra runs)
+        const uint32_t rend = tend + s_nx;  // runs with records here
         bool inblock = false;
         if (threadIdx.x < total && average) {
             const uint32_t s = s_start[threadIdx.x], e = s_start[threadIdx.x + 1];
-            if (e <= tend) {
+            if (e <= rend) {
                 const uint32_t ge = s_off[e - t0] - W0;
                 inblock = ge <= (uint32_t)kRunStage && ge - (s_off[s - t0] - W0) <= inblock_max;
                 if (inblock) atomicMax(&s_wend, ge);
@@ -3051,7 +3146,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
         const uint32_t staged = s_wend;
         for (uint32_t k = threadIdx.x; k < staged; k += kGroupThreads) {
             const uint32_t q = W0 + k;
-            uint32_t lo = 0, hi = kGroupThreads;  // last run with s_off <= q
+            uint32_t lo = 0, hi = kGroupThreads + s_nx;  // last run with s_off <= q
             while (hi - lo > 1) {
                 const uint32_t mid = (lo + hi) >> 1;
                 if (s_off[mid] <= q) lo = mid; else hi = mid;
@@ -3079,7 +3174,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
                 for (uint32_t f = f0; f <= fc; ++f) fvox[f] = g;
             }
             const uint32_t g0 = s_off[s - t0] - W0;  // staged positions of the group
-            const uint32_t g1 = e <= tend ? s_off[e - t0] - W0 : 0xFFFFFFFFu;
+            const uint32_t g1 = e <= rend ? s_off[e - t0] - W0 : 0xFFFFFFFFu;
             if (!average) {
                 float c[4];
                 group_corner(keys[s] & kmask, vp, c);
@@ -3105,13 +3200,16 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
         }
         __syncthreads();
         const uint32_t nbig = s_nbig;
-        for (uint32_t bi = 0; bi < nbig; ++bi) {  // staged: the 4 waves, wave = component
+        for (uint32_t bi = wid; bi < nbig; bi += 4) {  // staged: a wave per group, all components
             const uint32_t li = s_big[bi];
             const uint32_t g = s_excl + li;
             const uint32_t s = s_start[li], e = s_start[li + 1];
             const uint32_t g0 = s_off[s - t0] - W0, g1 = s_off[e - t0] - W0;
-            store_comp_mean(out + 4 * (size_t)g, wid, lds_group_comp(s_pts + g0, wid, g1 - g0),
-                            g1 - g0);
+            const float sum = wave_group_sum(s_pts + g0, g1 - g0, s_wsoa[wid]);
+            if ((lane & 15) == 0) {
+                const uint32_t c = (uint32_t)lane >> 4;
+                out[4 * (size_t)g + c] = c < 3 ? sum / (float)(g1 - g0) : sum;
+            }
         }
         __syncthreads();  // LDS reused by the next tile
     }
@@ -3129,7 +3227,8 @@ __global__ __launch_bounds__(256) void k_group_runs_big(const uint32_t* __restri
                                                        float* __restrict__ out,
                                                        const uint4* __restrict__ bigq,
                                                        uint32_t bigq_cap, uint32_t* qctr) {
-    __shared__ int s_mark[64 * Q];
+    __shared__ int s_mark[64 * Q + 64];  // (+ a scratch row: marks of runs outside a wave's rows)
+    __shared__ uint32_t s_base[4][64 * kRunsPerLane];  // (a copy per wave)
     __shared__ __attribute__((aligned(16))) float s_soa[4][kRowStride * Q];
     __shared__ uint32_t s_t;
     const uint32_t wid = threadIdx.x >> 6;  // (the component)
@@ -3144,7 +3243,7 @@ __global__ __launch_bounds__(256) void k_group_runs_big(const uint32_t* __restri
 #ifdef GDF_TRACE_GROUPS
         unsigned long long tr[5] = {0, 0, 0, 0, 0};
         const unsigned long long w0 = wall_clock64(), c0 = clock64();
-        const float sum = block_stream_sum<Q>(rps, rlen, q.y, q.z, pts, s_mark, s_soa, np, tr);
+        const float sum = block_stream_sum<Q>(rps, rlen, q.y, q.z, pts, s_mark, s_base[wid], s_soa, np, tr);
         if (threadIdx.x == 128 && t < kTraceSlots) {  // (wave 2: z)
             unsigned long long* g = g_gtrace[t];
             g[0] = w0;
@@ -3160,7 +3259,8 @@ __global__ __launch_bounds__(256) void k_group_runs_big(const uint32_t* __restri
             g[7] = tr[3] | (hw << 40) | (xcc << 56);
         }
 #else
-        const float sum = block_stream_sum<Q>(rps, rlen, q.y, q.z, pts, s_mark, s_soa, np, nullptr);
+        const float sum = block_stream_sum<Q>(rps, rlen, q.y, q.z, pts, s_mark, s_base[wid], s_soa, np,
+                                                   nullptr);
 #endif
         store_comp_mean(out + 4 * (size_t)q.x, wid, sum, np);
         if (nq <= gridDim.x) break;

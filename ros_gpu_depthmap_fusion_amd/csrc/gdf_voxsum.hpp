@@ -233,10 +233,10 @@ __device__ __forceinline__ float comp_stretch_sum(const Get& get, uint32_t pos, 
 // ... + t_k, t = rint(x / u)) lies in [2^23 + 1, 2^24 - 1] (sign of O), which for a whole row holds
 // iff the row's smallest and largest running prefix do.  Rows are independent given u, so:
 //  1. every lane takes 16 values of one row (lanes 4r .. 4r + 3: row r), sums them loosely and
-//     the wave scans the sums: s + the rows before row r is a GUESS of s at row r's start, whose
+//     the wave scans the sums: s + the rows up to row r is a GUESS of s at row r's end, whose
 //     binade gives the row's u (a wrong guess only costs the row its integer path);
 //  2. per value y = x / u, t = rint(y) clamped to +-2^24 (any |t| >= 2^23 leaves the binade, and
-//     the clamp keeps every int32 sum below 2^31), the tie / NaN flag |y - t| >= 1/2, the running
+//     the clamp keeps every int32 sum below 2^31), the tie flag |y - t| >= 1/2, the running
 //     P with its min and max; the 4 parts of a row combine by quad DPP (offsets by a quad scan);
 //  3. from the exact s: the rows' totals are scanned, a row is taken when its guessed binade is
 //     s's, it has no tie / NaN and O + min P, O + max P stay in range - the ballot's first other
@@ -259,45 +259,71 @@ __device__ __forceinline__ float dpp_iscan_f(float f) {  // inclusive wave64 sum
     return __int_as_float(v);
 }
 
-// s + the n <= 1024 values of one component staged as rows (row q at comp + q kRowStride).
-__device__ __forceinline__ float rows_chunk_sum(const float* __restrict__ comp, uint32_t n, float s) {
-    constexpr uint32_t V = 16;  // values per lane
-    constexpr int A = 8388609, B = 16777215;
-    const uint32_t lane = threadIdx.x & 63, r = lane >> 2, h = lane & 3;
-    const uint32_t nrows = (n + 63u) >> 6;
+__device__ __forceinline__ float dpp_iscan16_f(float f) {  // inclusive scans of the 16-lane rows
+    int v = __float_as_int(f);
+    v = __float_as_int(__int_as_float(v) + __int_as_float(__builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false)));
+    v = __float_as_int(__int_as_float(v) + __int_as_float(__builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false)));
+    v = __float_as_int(__int_as_float(v) + __int_as_float(__builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false)));
+    v = __float_as_int(__int_as_float(v) + __int_as_float(__builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false)));
+    return __int_as_float(v);
+}
+__device__ __forceinline__ int dpp_iscan16(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
+    return v;
+}
+
+// Steps 1 and 2 for the quad of this lane (part h = lane & 3 of a row: 16 values at src, 16-byte
+// aligned; vc of them valid when `partial`, the rest read as -0.0): the row's guessed binade exr,
+// its total T and prefix min / max, and whether it is free of ties (rowfree, on the quad's lane 3).
+// SEG: the guess scans the 16-lane DPP rows (4 independent sums of 4 rows each) instead of the wave.
+struct RowInfo {
+    uint32_t exr;
+    int T, rmn, rmx;
+    bool rowfree;
+};
+template <bool SEG>
+__device__ __forceinline__ RowInfo row_info(const float* __restrict__ src, int vc, bool partial,
+                                            float s) {
+    constexpr int V = 16;
+    const uint32_t h = threadIdx.x & 3;
     float x[V];
-    const float4* src = reinterpret_cast<const float4*>(comp + r * kRowStride + h * V);
+    const float4* s4 = reinterpret_cast<const float4*>(src);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const float4 v = src[i];
+        const float4 v = s4[i];
         x[4 * i] = v.x;
         x[4 * i + 1] = v.y;
         x[4 * i + 2] = v.z;
         x[4 * i + 3] = v.w;
     }
-    if (n < 64u * 16u) {  // (wave-uniform) a partial chunk: values past n read as -0.0
-        const int vc = (int)n - (int)(r * 64u + h * V);
+    if (partial) {  // (wave-uniform)
 #pragma unroll
-        for (int i = 0; i < (int)V; ++i) x[i] = i < vc ? x[i] : -0.0f;
+        for (int i = 0; i < V; ++i) x[i] = i < vc ? x[i] : -0.0f;
     }
-    // 1. the guess of s at the row's start -> the row's binade
+    // 1. the guess: s + the rows up to this one (loose) - the binade at the row's end, which a NaN
+    // or inf term of the row or before it makes non-finite: such rows never take the integer path
     float q[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) q[i] = (x[i] + x[i + 4]) + (x[i + 8] + x[i + 12]);
     const float qs = (q[0] + q[1]) + (q[2] + q[3]);
-    const float before = dpp_iscan_f(qs) - qs;  // (lane 4r: the rows before r)
-    const float guess = s + __int_as_float(GDF_QPERM(__float_as_int(before), 0x00));
-    const uint32_t exr = (__float_as_uint(guess) >> 23) & 255u;
-    const uint32_t e = min(max(exr, 24u), 254u);
+    const float inc = SEG ? dpp_iscan16_f(qs) : dpp_iscan_f(qs);
+    const float guess = s + __int_as_float(GDF_QPERM(__float_as_int(inc), 0xFF));
+    RowInfo ri;
+    ri.exr = (__float_as_uint(guess) >> 23) & 255u;
+    const uint32_t e = min(max(ri.exr, 24u), 254u);
     const float scale = __uint_as_float((277u - e) << 23);
-    // 2. integer terms, running prefix with its min / max, tie / NaN flag
+    // 2. integer terms, running prefix with its min / max, tie flag
     int P = 0, mn = 0x7FFFFFFF, mx = -0x7FFFFFFF - 1;
-    uint32_t dm = 0;
+    float dmf = 0.0f;  // max |y - t|: 1/2 only for a tie (>= 1/2 for an overflow to inf; NaN:
+                       // the guess above)
 #pragma unroll
-    for (int i = 0; i < (int)V; ++i) {
+    for (int i = 0; i < V; ++i) {
         const float y = x[i] * scale;
         const float t = __builtin_amdgcn_fmed3f(__builtin_rintf(y), -16777216.0f, 16777216.0f);
-        dm = max(dm, __float_as_uint(y - t) & 0x7FFFFFFFu);
+        dmf = __builtin_fmaxf(dmf, __builtin_fabsf(y - t));
         P += (int)t;
         mn = min(mn, P);
         mx = max(mx, P);
@@ -311,10 +337,23 @@ __device__ __forceinline__ float rows_chunk_sum(const float* __restrict__ comp, 
     rmn = min(rmn, GDF_QPERM(rmn, 0x4E));  // [2,3,0,1]
     rmx = max(rmx, GDF_QPERM(rmx, 0xB1));
     rmx = max(rmx, GDF_QPERM(rmx, 0x4E));
+    uint32_t dm = __float_as_uint(dmf);  // (>= 0: ordered as unsigned)
     dm = max(dm, (uint32_t)GDF_QPERM((int)dm, 0xB1));
     dm = max(dm, (uint32_t)GDF_QPERM((int)dm, 0x4E));
-    const int T = GDF_QPERM(Pi, 0xFF);  // the row's total (lane 4r + 3's inclusive)
-    const bool rowfree = h == 3u && dm <= 0x3EFFFFFFu;
+    ri.T = GDF_QPERM(Pi, 0xFF);  // the row's total (lane 4r + 3's inclusive)
+    ri.rmn = rmn;
+    ri.rmx = rmx;
+    ri.rowfree = h == 3u && dm <= 0x3EFFFFFFu;
+    return ri;
+}
+
+// s + the n <= 1024 values of one component staged as rows (row q at comp + q kRowStride).
+__device__ __forceinline__ float rows_chunk_sum(const float* __restrict__ comp, uint32_t n, float s) {
+    constexpr int A = 8388609, B = 16777215;
+    const uint32_t lane = threadIdx.x & 63, r = lane >> 2, h = lane & 3;
+    const uint32_t nrows = (n + 63u) >> 6;
+    const RowInfo ri = row_info<false>(comp + r * kRowStride + h * 16u,
+                                       (int)n - (int)(r * 64u + h * 16u), n < 64u * 16u, s);
     // 3. the rows from the exact s
     auto get = [&](uint32_t i) { return comp[(i >> 6) * kRowStride + (i & 63u)]; };
     uint32_t cur = 0;
@@ -327,11 +366,11 @@ __device__ __forceinline__ float rows_chunk_sum(const float* __restrict__ comp, 
             const float u = __uint_as_float((ex - 23u) << 23);
             const int O0 = __builtin_amdgcn_readfirstlane((int)(s * sc));
             const bool act = h == 3u && r >= cur && r < nrows;
-            const int Tm = act ? T : 0;
+            const int Tm = act ? ri.T : 0;
             const int inc = dpp_iscan(Tm);
             const int Ob = O0 + inc - Tm;  // O at the row's start
             const int lo = O0 > 0 ? A : -B, hi = O0 > 0 ? B : -A;
-            const bool ok = rowfree && exr == ex && Ob + rmn >= lo && Ob + rmx <= hi;
+            const bool ok = ri.rowfree && ri.exr == ex && Ob + ri.rmn >= lo && Ob + ri.rmx <= hi;
             const unsigned long long bad = __ballot(act && !ok);
             f = bad ? (uint32_t)__builtin_ctzll(bad) >> 2 : nrows;
             if (f > cur) s = (float)(O0 + __builtin_amdgcn_readlane(inc, 4u * f - 1u)) * u;
@@ -340,6 +379,98 @@ __device__ __forceinline__ float rows_chunk_sum(const float* __restrict__ comp, 
         GDF_VOXSUM_PROBE(3);
         s = uniform_f(serial_row(get, 64u * f, n, s));
         cur = f + 1u;
+    }
+    return s;
+}
+
+// ---- the 4 components side by side: a voxel of up to 256 values per chunk in ONE wave ----------
+// Lanes 16 c .. 16 c + 15 (DPP row c) sum component c: quad (c, r) row r of 4, the guess scanned
+// within the DPP row, step 3 for the 4 components at once (per-lane s, uniform in a DPP row; the
+// ballot's 16-bit segment c gives component c's first failing row), their chain rows together
+// (components without one add the wave's -0.0 row).  No barrier anywhere: a block's waves sum
+// different voxels (k_group_runs).  Chunk layout (kWaveSoa floats per wave): component c's rows
+// at c * kWaveCompStride, row r at + r kRowStride, row 4 all -0.0 (written once).
+constexpr uint32_t kWaveCompStride = 5 * kRowStride;
+constexpr uint32_t kWaveSoa = 4 * kWaveCompStride;
+
+__device__ __forceinline__ void wave_soa_init(float* wsoa) {  // the -0.0 rows
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) wsoa[c * kWaveCompStride + 4 * kRowStride + lane] = -0.0f;
+}
+
+// s (this lane's component) + the chunk's n <= 256 values (rows past n hold -0.0).
+__device__ __forceinline__ float rows4c_chunk(const float* __restrict__ wsoa, uint32_t n, float s) {
+    constexpr int A = 8388609, B = 16777215;
+    const uint32_t lane = threadIdx.x & 63, c = lane >> 4, r = (lane >> 2) & 3, h = lane & 3;
+    const float* comp = wsoa + c * kWaveCompStride;
+    const uint32_t nrows = (n + 63u) >> 6;
+    const RowInfo ri = row_info<true>(comp + r * kRowStride + h * 16u, 0, false, s);
+    uint32_t cur = 0;  // (per component)
+#pragma unroll 1
+    while (true) {
+        const bool pending = cur < nrows;
+        if (__ballot(pending) == 0) break;  // (wave-uniform)
+        const uint32_t ex = (__float_as_uint(s) >> 23) & 255u;
+        const bool adm = pending && ex >= 24u && ex != 255u;
+        const uint32_t ec = min(max(ex, 24u), 254u);
+        const float sc = __uint_as_float((277u - ec) << 23);
+        const float u = __uint_as_float((ec - 23u) << 23);
+        const int O0 = (int)(s * sc);
+        const bool act = adm && h == 3u && r >= cur && r < nrows;
+        const int Tm = act ? ri.T : 0;
+        const int inc = dpp_iscan16(Tm);
+        const int Ob = O0 + inc - Tm;
+        const int lo = O0 > 0 ? A : -B, hi = O0 > 0 ? B : -A;
+        const bool ok = ri.rowfree && ri.exr == ex && Ob + ri.rmn >= lo && Ob + ri.rmx <= hi;
+        const unsigned long long bad = __ballot(act && !ok);
+        const uint32_t seg = (uint32_t)(bad >> (lane & 48u)) & 0xFFFFu;
+        const uint32_t f = !pending ? nrows : !adm ? cur : seg ? (uint32_t)__builtin_ctz(seg) >> 2 : nrows;
+        // commit rows [cur, f): component c's inclusive total through row f - 1
+        const int at = __shfl(inc, (int)((lane & 48u) + 4u * max(f, 1u) - 1u), 64);
+        if (adm && f > cur) s = (float)(O0 + at) * u;
+        // row f by the chain (components without one: the -0.0 row)
+        const bool chain = pending && f < nrows;
+        if (__ballot(chain)) {  // (wave-uniform)
+            GDF_VOXSUM_PROBE(3);
+            const float4* rp = reinterpret_cast<const float4*>(comp + (chain ? f : 4u) * kRowStride);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const float4 v = rp[k];
+                s = s + v.x;
+                s = s + v.y;
+                s = s + v.z;
+                s = s + v.w;
+            }
+        }
+        cur = chain ? f + 1u : pending ? nrows : cur;
+    }
+    return s;
+}
+
+// A voxel's cnt points staged in LDS (float4, AoS) summed by one wave in chunks of 256 through
+// wsoa (kWaveSoa floats, wave_soa_init'ed): the lane's component (lane >> 4) of the sum.
+__device__ __forceinline__ float wave_group_sum(const float4* gp, uint32_t cnt, float* wsoa) {
+    const uint32_t lane = threadIdx.x & 63;
+    float s = 0.0f;
+#pragma unroll 1
+    for (uint32_t c0 = 0; c0 < cnt; c0 += 256u) {
+        const uint32_t n = min(256u, cnt - c0);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // (the previous chunk is read)
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t i = 64u * k + lane;
+            const float4 v = i < n ? gp[c0 + i] : make_float4(-0.0f, -0.0f, -0.0f, -0.0f);
+            wsoa[0 * kWaveCompStride + k * kRowStride + lane] = v.x;
+            wsoa[1 * kWaveCompStride + k * kRowStride + lane] = v.y;
+            wsoa[2 * kWaveCompStride + k * kRowStride + lane] = v.z;
+            wsoa[3 * kWaveCompStride + k * kRowStride + lane] = v.w;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        s = rows4c_chunk(wsoa, n, s);
     }
     return s;
 }

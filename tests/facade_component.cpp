@@ -175,7 +175,8 @@ int main(int argc, char** argv) {
             glMemoryBarrier(GL_ALL_BARRIER_BITS);
             m_fusion->downloadVoxelOccupancyGrid();
             glMemoryBarrier(GL_ALL_BARRIER_BITS);
-            m_fusion->objectSegmentation();  // component.cpp:313-316 (front end + label merge)
+            m_fusion->objectSegmentation();  // component.cpp:313-323
+            m_fusion->objectTracking(0.1f);
         }
         const std::string s = std::to_string(f);
         write_bin(out + "/points" + s + ".bin", reinterpret_cast<const float*>(m_fusion->m_points.data()),
@@ -205,8 +206,8 @@ int main(int argc, char** argv) {
         write_bin(out + "/merged" + s + ".bin", m_fusion->m_ccLabelsMerged.data(),
                   m_fusion->m_ccLabelsMerged.size());
         std::vector<int32_t> objmin;
-        for (const gdf_cc_object& o : m_fusion->m_ccObjects)
-            objmin.insert(objmin.end(), o.min_voxel, o.min_voxel + 3);
+        for (const gdf::CCObject& o : m_fusion->m_ccObjects)
+            for (int i = 0; i < 3; ++i) objmin.push_back(o.min_coord.voxel[i]);
         write_bin(out + "/objmin" + s + ".bin", objmin.data(), objmin.size());
         std::vector<int32_t> l2c;
         for (const auto& v : m_fusion->m_labelsToContoursPerLayer) l2c.insert(l2c.end(), v.begin(), v.end());

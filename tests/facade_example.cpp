@@ -56,9 +56,31 @@ int run_component_frame(gdf::GPUDepthmapFusion& f, const cv::Mat_<uint16_t>& dep
     f.voxelOccupancyGrid(10);
     f.downloadVoxelOccupancyGrid();
     f.downloadPoints();
-    const gdf::vec4 c = f.voxelCoordToWorldCoord(1, 2, 3);
+    const gdf::vec3 c = f.voxelCoordToWorldCoord(1, 2, 3);
+    const gdf::vec3 v = f.worldCoordToVoxelCoord(c[0], c[1], c[2]);
+    // the segmentation / tracking members the component reads (component.cpp:313-342, 541-632,
+    // 731-962)
+    f.objectSegmentation();
+    f.objectTracking(0.1f);
+    int acc = 0;
+    for (size_t i = 0; i < f.m_ccCentroids.size(); ++i)
+        for (int k = 1; k < f.m_ccCentroids[i].rows; ++k)
+            acc += (int)f.voxelCoordToWorldCoord((float)f.m_ccCentroids[i](k, 0),
+                                                 (float)f.m_ccCentroids[i](k, 1), (float)i)[0];
+    if (!f.m_ccLayersConnections.empty() && f.m_ccLayersConnections[0].rows > 0)
+        acc += f.m_ccLayersConnections[0].at<uint8_t>(0, 0);
+    for (const auto& obj : f.m_ccObjects) {
+        gdf::Point2f p[4];
+        obj.topview.shapes.world.box.points(p);
+        acc += (int)obj.label + (int)obj.min_coord.world.z + (int)obj.max_coord.world.z +
+               (int)p[0].x + (int)obj.components.size();
+        for (const auto& cmp : obj.components) acc += (int)cmp.contour3d.world.size();
+    }
+    for (const auto& t : f.m_ccObjectTracks)
+        acc += (int)(t.score_filter.values[0] + gdf::norm(t.rrect_filter.rrect.center) +
+                     t.lastObject.max_coord.world.z);
     return f.m_numPoints + (int)f.m_points_voxelized.size() + (int)f.m_occupancyGrid.size() +
-           (int)c.x + (int)f.rollbufferState().num_seqs;
+           (int)c.x + (int)v.z + acc + (int)f.rollbufferState().num_seqs;
 }
 
 int main() { return 0; }

@@ -147,7 +147,8 @@ def sequential_sum(x):
 
 def rows_sum(x, NR=16, stats=None):
     """The GPU's row form (gdf_voxsum.hpp rows_chunk_sum): chunks of NR rows of 64 values; per row
-    a predicted binade (the f32 sum s plus the rows before it, summed loosely - a guess, checked),
+    a predicted binade (the f32 sum s plus the rows up to it, summed loosely - a guess, checked;
+    non-finite for a row holding or following a NaN / inf term),
     its integer terms t = rint(x / u) clamped to +-2^24, the row total T and the min / max of the
     row's running prefix, and whether any |x / u - t| >= 1/2 (tie / NaN).  Then, from the exact s,
     row after row while the binade of s equals the row's guess and every running value
@@ -165,7 +166,7 @@ def rows_sum(x, NR=16, stats=None):
         rows.reshape(-1)[:len(seg)] = seg
         with np.errstate(all="ignore"):
             rsum = rows.sum(axis=1, dtype=f32)
-            pred = (s + np.concatenate([[f32(0)], np.cumsum(rsum, dtype=f32)[:-1]])).astype(f32)
+            pred = (s + np.cumsum(rsum, dtype=f32)).astype(f32)
         exr = (pred.view(np.uint32) >> 23) & 255
         info = []
         for r in range(nrows):
@@ -175,7 +176,7 @@ def rows_sum(x, NR=16, stats=None):
                 y = (rows[r] * scale).astype(f32)
                 t = np.clip(np.rint(y), f32(-16777216.0), f32(16777216.0)).astype(f32)
                 d = np.abs((y - t).astype(f32))
-            fail = not bool(np.all(d < f32(0.5)))
+            fail = not bool(np.all(d[np.isfinite(rows[r])] < f32(0.5)))  # (NaN / inf: the guess)
             P = np.cumsum(np.where(np.isfinite(t), t, 0).astype(np.int64))
             info.append((int(exr[r]), fail, int(P[-1]), int(P.min()), int(P.max())))
         r = 0

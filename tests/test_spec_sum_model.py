@@ -51,7 +51,7 @@ def test_stretch_sum_equals_sequential_chain(name):
     assert same(group_sum(x), sequential_sum(x)), name
     for R in (1, 2, 4):  # the GPU's cursor form
         assert same(cursor_sum(x, R), sequential_sum(x)), (name, R)
-    for NR in (16, 8, 1):  # the row form (k_group_runs_big)
+    for NR in (16, 8, 4, 1):  # the row form (k_group_runs_big: 16 / 8 rows, wave_group_sum: 4)
         assert same(rows_sum(x, NR), sequential_sum(x)), (name, NR)
 
 

@@ -1,7 +1,7 @@
 """Per-group timings of the voxel-sum kernel (k_group_runs_big) from the diagnostic build
 libgdf_trace.so (built here by `python tools/group_trace.py --build`, run on the GPU box):
 
-    python tools/group_trace.py W H F [dense|stress] [frames_per_launch]
+    python tools/group_trace.py W H F [dense|stress] [frames_per_batch]
 
 prints the kernel's span, the longest groups (points, chunks, cycles at barriers / LDS stores /
 fetch issue / sums) and how the groups' start times spread."""
@@ -12,9 +12,9 @@ import sys
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from ros_gpu_depthmap_fusion_amd import hiprt, synth  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from ros_gpu_depthmap_fusion_amd.build import TRACE_LIB_PATH, build_library  # noqa: E402
-from ros_gpu_depthmap_fusion_amd.gdf import ComponentParams, GPUDepthmapFusion  # noqa: E402
+import frame_driver  # noqa: E402
 
 SLOTS = 1 << 16
 
@@ -24,27 +24,24 @@ def main():
         print(build_library(trace=True))
         return
     W, H, F = (int(x) for x in sys.argv[1:4])
-    gen = synth.WORKLOADS[sys.argv[4] if len(sys.argv) > 4 else "dense"]
-    cam = synth.make_camera(0, W, H)
-    dframes = [hiprt.DeviceArray.from_numpy(gen(cam, 0, f)) for f in range(2)]
-    eng = GPUDepthmapFusion(0, lib_path=TRACE_LIB_PATH)
+    workload = sys.argv[4] if len(sys.argv) > 4 else "dense"
+    batch = int(sys.argv[5]) if len(sys.argv) > 5 else 1
+    eng, step = frame_driver.make(W, H, F, 0, workload, TRACE_LIB_PATH)
     lib = eng._lib
-    p = ComponentParams()
-    p.flying_filter_size = F
-    pc = p.to_c(None, None, False, False)
     for i in range(4):
         if i == 3:
             eng.synchronize()
             assert lib.gdf_debug_group_trace_clear() == 0
-        eng.clear()
-        eng.addDepthmapDevice(dframes[i % 2].ptr, W, H, *cam.intrinsics(), cam.T_world, cam.T_crop)
-        eng.processFramePrepared(pc)
+        step(i, batch)
     eng.synchronize()
     buf = np.zeros((SLOTS, 8), np.uint64)
     assert lib.gdf_debug_group_trace(buf.ctypes.data_as(C.c_void_p), C.c_size_t(buf.nbytes)) == 0
     used = buf[:, 0] != 0
     g = buf[used]
     slots = np.flatnonzero(used)
+    if len(g) == 0:
+        print("no queued groups (every group summed in k_group_runs)")
+        return
     w0, w1 = g[:, 0].astype(np.int64), g[:, 1].astype(np.int64)
     t0 = w0.min()
     npts = (g[:, 2] >> np.uint64(32)).astype(np.int64)
