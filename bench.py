@@ -300,6 +300,15 @@ def time_single(st, params, steps, warmup, depth, kernel_timing, pmc_key, batch=
     }
 
 
+def cgroup_cpu_quota():
+    """CPUs this process may use per the cgroup v2 cpu.max (None: unlimited / unknown)."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(st, params, seconds):
     """The C restatement (oracle/gdf_oracle.c, OpenMP) on the host's cores: median of 5 runs of
     `seconds` each over the same frames (SURVEY.md §8(d) protocol)."""
@@ -348,7 +357,15 @@ def cpu_baseline(st, params, seconds):
                       f"{st.W}x{st.H} frames through the C restatement (oracle/gdf_oracle.c, "
                       f"-O3 -ffp-contract=off, OpenMP {threads} threads = the pool's "
                       f"OMP_NUM_THREADS share of this GPU's host)"}
-    if affinity > threads:  # and every CPU of the host (nproc), a short sample
+    quota = cgroup_cpu_quota()
+    if quota is not None:
+        out["cgroup_cpu_quota"] = round(quota, 2)
+    if quota is not None and quota < affinity and quota <= threads * 1.05:
+        # the CPUs beyond the quota only time-slice it (a 256-thread run under a 16-CPU quota
+        # measured 0.41 Mpoints/s, 160x below the 16-thread run)
+        out["all_cpus"] = {"skipped": "cgroup cpu.max quota of %.1f CPUs: the %d-thread run "
+                                      "already uses this host's whole CPU allowance" % (quota, threads)}
+    elif affinity > threads:  # and every CPU of the host (nproc), a short sample
         orc.set_threads(affinity)
         frame(0)
         rates_all = []

@@ -36,8 +36,8 @@ int gdf_run_depth_stream(gdf_engine* engine, const gdf_stream_camera* cameras,
                          uint64_t count);
 
 /* The same loop for HOST depth maps (frames[] are host pointers, gdf_add_depthmap): each frame's
- * maps are copied to the device on the frame slot's stream (pinned memory directly, pageable
- * memory through the slot's pinned staging), overlapping the kernels of the frames in flight
+ * maps (pinned or pageable alike) are copied into the frame slot's pinned staging by a few host
+ * threads and sent to the device on the slot's stream, overlapping the kernels of the frames in flight
  * (gdf_set_pipeline_depth).  The H2D-inclusive form of gdf_run_depth_stream. */
 int gdf_run_host_stream(gdf_engine* engine, const gdf_stream_camera* cameras,
                         uint32_t num_cameras, const gdf_frame_params* params, uint64_t first,

@@ -2491,7 +2491,53 @@ constexpr uint32_t kPersistBlocks = 2048;  // blocks of a persistent sort / grou
 // group phase 1.7x faster through count + scan than through the look-back chain; one VGA frame,
 // 1.2 K tiles of capacity, 4 % faster per frame)
 uint32_t g_group_scan_tiles = 1024;
-constexpr int kSmallGroup = 16;  // groups summed by one thread; longer ones by a wave
+// Staged groups of up to g_small_group points are summed by their own thread (thread_group_sum:
+// the four component chains side by side, one group per lane, the groups of a tile in parallel);
+// longer ones by a wave (gdf_voxsum.hpp's stretch sums: a wave per group, serial over a block's
+// groups).  Tuning knob GDF_SMALL_GROUP.
+uint32_t g_small_group = 256;
+
+// p[0] + ... + p[n-1] per component, in order, by one thread: blocks of 4 points alternate between
+// two register sets, the next block read while the current one is added (LDS latency off the
+// add chains).  Reads stay inside [0, n) (no padding needed).
+__device__ __forceinline__ float4 thread_group_sum(const float4* p, uint32_t n) {
+    float ax = 0.f, ay = 0.f, az = 0.f, aw = 0.f;
+    auto add = [&](const float4& q) {
+        ax = ax + q.x;
+        ay = ay + q.y;
+        az = az + q.z;
+        aw = aw + q.w;
+    };
+    uint32_t k = 0;
+    if (n >= 8) {
+        float4 a[4], b[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[q] = p[q];
+#pragma unroll 1
+        for (; k + 8 <= n; k += 8) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) b[q] = p[k + 4 + q];
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) add(a[q]);
+            const uint32_t kn = k + 8 + 4 <= n ? k + 8 : k;  // (in range; unused past the loop)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) a[q] = p[kn + q];
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) add(b[q]);
+        }
+        if (k + 4 <= n) {  // a[] holds points k .. k+3 exactly when k + 4 <= n here
+#pragma unroll
+            for (int q = 0; q < 4; ++q) add(a[q]);
+            k += 4;
+        }
+    }
+    for (; k < n; ++k) add(p[k]);
+    return make_float4(ax, ay, az, aw);
+}
 
 constexpr uint32_t kChainPad = 16;  // LDS padding of staged point buffers
 constexpr uint32_t kExtraRuns = 64;  // runs past a k_group_runs tile read for its last group
@@ -2549,7 +2595,7 @@ __global__ __launch_bounds__(kGroupThreads) __attribute__((amdgpu_waves_per_eu(7
     uint32_t* tile_ctr, uint32_t* epoch_word, uint32_t* err, uint32_t* hist, int average,
     VoxelParams vp, uint32_t* marks, const uint32_t* tile_base, uint4* __restrict__ bigq,
     uint32_t* __restrict__ bigcnt, uint32_t bigcap, uint32_t nframes, uint32_t fshift,
-    uint32_t* __restrict__ fvox) {
+    uint32_t* __restrict__ fvox, uint32_t small_max) {
     __shared__ uint32_t s_wave[4];
     __shared__ uint32_t s_tile, s_epoch, s_excl, s_nbig, s_nq;
     __shared__ uint32_t s_start[kGroupThreads + 1];
@@ -2678,30 +2724,10 @@ __global__ __launch_bounds__(kGroupThreads) __attribute__((amdgpu_waves_per_eu(7
             float c[4];
             group_corner(keys[s] & kmask, vp, c);
             *reinterpret_cast<float4*>(o) = make_float4(c[0], c[1], c[2], c[3]);
-        } else if (e - S0 <= staged && e - s <= (uint32_t)kSmallGroup) {
-            float ax = 0.f, ay = 0.f, az = 0.f, aw = 0.f;
-            uint32_t k = s - S0;
-            for (; k + 4 <= e - S0; k += 4) {
-                float4 p[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) p[q] = s_pts[k + q];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    ax = ax + p[q].x;
-                    ay = ay + p[q].y;
-                    az = az + p[q].z;
-                    aw = aw + p[q].w;
-                }
-            }
-            for (; k < e - S0; ++k) {
-                const float4 p = s_pts[k];
-                ax = ax + p.x;
-                ay = ay + p.y;
-                az = az + p.z;
-                aw = aw + p.w;
-            }
+        } else if (e - S0 <= staged && e - s <= small_max) {
+            const float4 a = thread_group_sum(s_pts + (s - S0), e - s);
             const float fc = (float)(e - s);
-            *reinterpret_cast<float4*>(o) = make_float4(ax / fc, ay / fc, az / fc, aw);
+            *reinterpret_cast<float4*>(o) = make_float4(a.x / fc, a.y / fc, a.z / fc, a.w);
         } else if (bigq && e - S0 > staged) {
             // a voxel reaching past the staged points (at most the tile's last group): summed
             // by k_group_big, so this block's other waves do not wait at the tile barrier for
@@ -2755,6 +2781,7 @@ __global__ __launch_bounds__(256) void k_group_big(const uint32_t* __restrict__ 
 // GDF_RUN_INBLOCK
 uint32_t g_run_stage = 2048;
 uint32_t g_run_inblock = 2048;
+uint32_t g_run_wave = 0;  // staged groups above g_small_group by a wave in k_group_runs (GDF_RUN_WAVE)
 uint32_t g_run_big_blocks = 1024;  // k_group_runs_big grid (tuning knob GDF_RUN_BIG_BLOCKS)
 // chunks of k_group_runs_big (one 4-wave block per queued group): 1 K points (Q = 16) or 512
 // (Q = 8); 0 never 1 K, 1 always, 2 (default) for single depth-only frames, whose long voxels
@@ -2998,11 +3025,13 @@ __device__ __forceinline__ float block_stream_sum(const uint32_t* __restrict__ r
 // Groups of one tile of 256 sorted runs: group starts (key != previous run's key), group ids by a
 // block scan plus the tile's offset (count + scan, or tickets + look-back as k_group), the end of
 // the tile's last group (a search of the run keys past the tile).  The points of the tile's groups
-// are staged (up to kRunStage from the first group start); groups of <= kSmallGroup staged points
+// are staged (up to kRunStage from the first group start); groups of <= small_max staged points
 // are summed by their thread, longer staged ones by a wave from LDS, and the others (past the
 // staged points, or continuing past the tile) are queued for k_group_runs_big - one append per
 // group, so a block never waits on a long chain.  Marks, frame voxel starts and corners as k_group.
-template <int kRunStage>
+// WAVE = false (default): staged groups above small_max are queued like the unstaged ones, and the
+// block needs no per-wave transpose buffers (37.6 instead of 59.4 KB of LDS: 4 blocks per CU, not 2).
+template <int kRunStage, bool WAVE>
 __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
     const uint32_t* __restrict__ keys, const uint32_t* __restrict__ rvals,
     const uint32_t* __restrict__ count, const uint32_t* __restrict__ run_start,
@@ -3011,7 +3040,8 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
     uint32_t* epoch_word, uint32_t* err, uint32_t* hist, int average, VoxelParams vp,
     uint32_t* marks, const uint32_t* tile_base, uint4* __restrict__ bigq, uint32_t bigq_cap,
     uint32_t* __restrict__ qctr, uint32_t nframes, uint32_t fshift, uint32_t* __restrict__ fvox,
-    uint32_t inblock_max, uint32_t* __restrict__ rps, uint32_t* __restrict__ rlen) {
+    uint32_t inblock_max, uint32_t* __restrict__ rps, uint32_t* __restrict__ rlen,
+    uint32_t small_max) {
     __shared__ uint32_t s_wave[4];
     __shared__ uint32_t s_tile, s_epoch, s_excl, s_nbig, s_nq, s_qbase, s_wend, s_nx;
     __shared__ uint32_t s_start[kGroupThreads + 1];  // group starts (run index); [total] = end
@@ -3021,9 +3051,10 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
     __shared__ uint32_t s_off[kGroupThreads + kExtraRuns + 1];
     __shared__ uint32_t s_big[kGroupThreads];
     __shared__ float4 s_pts[kRunStage + kChainPad];
-    __shared__ __attribute__((aligned(16))) float s_wsoa[4][kWaveSoa];  // wave_group_sum chunks
+    __shared__ __attribute__((aligned(16))) float s_wsoa[WAVE ? 4 : 1][WAVE ? kWaveSoa : 4];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    wave_soa_init(s_wsoa[wid]);
+    if (WAVE) wave_soa_init(s_wsoa[wid]);
+    if (!WAVE) inblock_max = min(inblock_max, small_max);  // longer groups: k_group_runs_big
     const uint32_t n = *count;  // runs
     const uint32_t ntiles = (n + kGroupThreads - 1) / kGroupThreads;
     const uint32_t kmask = nframes > 1 ? (1u << fshift) - 1u : 0xFFFFFFFFu;
@@ -3183,29 +3214,22 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
                 const uint32_t slot = s_qbase + qlocal;
                 if (slot < bigq_cap) bigq[slot] = make_uint4(g, s, e, 0u);
                 else atomicOr(err, 8u);
-            } else if (g1 - g0 <= (uint32_t)kSmallGroup) {
-                float ax = 0.f, ay = 0.f, az = 0.f, aw = 0.f;
-                for (uint32_t k = g0; k < g1; ++k) {
-                    const float4 q = s_pts[k];
-                    ax = ax + q.x;
-                    ay = ay + q.y;
-                    az = az + q.z;
-                    aw = aw + q.w;
-                }
+            } else if (g1 - g0 <= small_max) {
+                const float4 a = thread_group_sum(s_pts + g0, g1 - g0);
                 const float fc = (float)(g1 - g0);
-                *reinterpret_cast<float4*>(o) = make_float4(ax / fc, ay / fc, az / fc, aw);
+                *reinterpret_cast<float4*>(o) = make_float4(a.x / fc, a.y / fc, a.z / fc, a.w);
             } else {
                 s_big[atomicAdd(&s_nbig, 1u)] = threadIdx.x;
             }
         }
         __syncthreads();
-        const uint32_t nbig = s_nbig;
+        const uint32_t nbig = WAVE ? s_nbig : 0u;
         for (uint32_t bi = wid; bi < nbig; bi += 4) {  // staged: a wave per group, all components
             const uint32_t li = s_big[bi];
             const uint32_t g = s_excl + li;
             const uint32_t s = s_start[li], e = s_start[li + 1];
             const uint32_t g0 = s_off[s - t0] - W0, g1 = s_off[e - t0] - W0;
-            const float sum = wave_group_sum(s_pts + g0, g1 - g0, s_wsoa[wid]);
+            const float sum = wave_group_sum(s_pts + g0, g1 - g0, s_wsoa[WAVE ? wid : 0]);
             if ((lane & 15) == 0) {
                 const uint32_t c = (uint32_t)lane >> 4;
                 out[4 * (size_t)g + c] = c < 3 ? sum / (float)(g1 - g0) : sum;
@@ -3375,7 +3399,8 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
     if (runs) {  // groups of sorted runs; the long ones by k_group_runs_big
         const uint32_t gb = std::max<uint32_t>(group_tiles, 1u);
         uint32_t* qctr = reinterpret_cast<uint32_t*>(a.ctrs + kCtrRunQueue);
-        auto kg = g_run_stage >= 2048 ? k_group_runs<2048> : k_group_runs<512>;
+        auto kg = g_run_wave ? (g_run_stage >= 2048 ? k_group_runs<2048, true> : k_group_runs<512, true>)
+                             : (g_run_stage >= 2048 ? k_group_runs<2048, false> : k_group_runs<512, false>);
         hipLaunchKernelGGL(kg, dim3(gb), dim3(kGroupThreads), 0, s, kin, vin, gcount,
                            a.run_start, a.pts, reinterpret_cast<float*>(a.out), a.out_count,
                            a.gstatus, a.ggstatus, reinterpret_cast<uint32_t*>(a.ctrs + kCtrGroup),
@@ -3383,7 +3408,7 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
                            a.average, a.vp, a.group_marks, tile_base, a.bigq, a.bigq_cap, qctr,
                            a.nframes, a.frame_shift, a.frame_vox_start,
                            std::min<uint32_t>(g_run_inblock, g_run_stage >= 2048 ? 2048u : 512u),
-                           kbuf[npasses & 1], vbuf[npasses & 1]);  // (free after the sort)
+                           kbuf[npasses & 1], vbuf[npasses & 1], g_small_group);  // (free after the sort)
         if (a.average) {
             if ((e = hipGetLastError()) != hipSuccess) return e;
             const bool q16 = g_run_q16 == 1 ||
@@ -3404,7 +3429,8 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
                        a.gstatus, a.ggstatus, reinterpret_cast<uint32_t*>(a.ctrs + kCtrGroup),
                        reinterpret_cast<uint32_t*>(a.ctrs + kCtrEpoch), a.err, a.hist, a.average,
                        a.vp, a.group_marks, tile_base, tile_base ? a.bigq : nullptr,
-                       a.bigcnt, bigcap, a.nframes, a.frame_shift, a.frame_vox_start);
+                       a.bigcnt, bigcap, a.nframes, a.frame_shift, a.frame_vox_start,
+                       g_small_group);
     if (tile_base && a.bigq && a.average) {
         if ((e = hipGetLastError()) != hipSuccess) return e;
         hipLaunchKernelGGL(k_group_big, dim3(2048), dim3(256), 0, s, vin, a.pts,

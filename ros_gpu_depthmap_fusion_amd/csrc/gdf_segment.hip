@@ -686,6 +686,47 @@ __global__ __launch_bounds__(kContourThreads) void k_cc_contours(
     }
 }
 
+// The contours of all layers packed back to back for ONE download each of records and chain
+// codes: block z places layer z's records at roff[z] = the records of the layers before it and
+// its codes at coff[z] (a layer's codes end where its last record's end: start + length);
+// hdr = roff[0..L] then coff[0..L].
+__global__ __launch_bounds__(256) void k_cc_pack_contours(
+    const uint32_t* __restrict__ rec, uint32_t rec_cap, const uint8_t* __restrict__ codes,
+    uint64_t code_cap, const uint32_t* __restrict__ ncont, uint32_t L,
+    uint32_t* __restrict__ prec, uint8_t* __restrict__ pcodes, unsigned long long* __restrict__ hdr) {
+    __shared__ unsigned long long s_r, s_c;
+    const uint32_t z = blockIdx.x, t = threadIdx.x;
+    if (t == 0) s_r = s_c = 0;
+    __syncthreads();
+    unsigned long long r = 0, c = 0;
+    for (uint32_t q = t; q < z + (z + 1 == L ? 1u : 0u); q += 256) {  // (the last block: all L)
+        const uint32_t n = min(ncont[q], rec_cap);  // (clamps: a capacity error is reported)
+        if (q < z) r += n;
+        if (q < z && n) {
+            const uint32_t* last = rec + ((size_t)q * rec_cap + n - 1) * 4;
+            c += min((unsigned long long)last[2] + last[3], (unsigned long long)code_cap);
+        }
+    }
+    if (r) atomicAdd(&s_r, r);
+    if (c) atomicAdd(&s_c, c);
+    __syncthreads();
+    const uint32_t n = min(ncont[z], rec_cap);
+    const unsigned long long roff = s_r, coff = s_c;
+    const uint32_t* rz = rec + (size_t)z * rec_cap * 4;
+    for (uint32_t i = t; i < 4 * n; i += 256) prec[roff * 4 + i] = rz[i];
+    const uint64_t used = n ? min((uint64_t)rz[4 * (n - 1) + 2] + rz[4 * (n - 1) + 3], code_cap) : 0;
+    const uint8_t* cz = codes + (size_t)z * code_cap;
+    for (uint64_t i = t; i < used; i += 256) pcodes[coff + i] = cz[i];
+    if (t == 0) {
+        hdr[z] = roff;
+        hdr[L + 1 + z] = coff;
+        if (z + 1 == L) {
+            hdr[L] = roff + n;
+            hdr[2 * L + 1] = coff + used;
+        }
+    }
+}
+
 // labelsToContours: contour j (findContours order) = discovered contour nc - 1 - j
 __global__ __launch_bounds__(256) void k_cc_l2c(const uint32_t* __restrict__ rec, uint32_t rec_cap,
                                                 const uint32_t* __restrict__ ncont,
@@ -699,6 +740,75 @@ __global__ __launch_bounds__(256) void k_cc_l2c(const uint32_t* __restrict__ rec
         const uint32_t lab = labels[(size_t)z * W * H + (size_t)y * W + x];
         l2c[lstart[z] + lab] = (int32_t)(nc - 1 - d);
     }
+}
+
+// mergeLabelsAcrossLayers (fusion.cpp:2243-2361) on the device, one workgroup: the sequential
+// global labels gl[k] = k are min-propagated bottom-up (layer i+1 takes the smallest label of the
+// connected labels of layer i), then top-down, over the numA x numB connection matrices
+// (background connects only with background), and numbered in UIntGrouper order: merged[k] = the
+// rank of gl[k] among the distinct propagated values (gl[k] <= k, so a flag per value and one
+// scan).  A pass is parallel over the labels it writes (each reads only the finished neighbour
+// layer), so the result is the host loop's; passes are separated by barriers.
+constexpr uint32_t kMergeThreads = 1024;
+__global__ __launch_bounds__(kMergeThreads) void k_cc_merge_layers(
+    const uint8_t* __restrict__ conn, const uint64_t* __restrict__ cstart,
+    const uint32_t* __restrict__ nlab, const uint32_t* __restrict__ lstart, uint32_t L,
+    uint32_t T, uint32_t* __restrict__ gl, uint32_t* __restrict__ flag,
+    uint32_t* __restrict__ merged, uint32_t* __restrict__ nobj) {
+    const uint32_t t = threadIdx.x;
+    for (uint32_t k = t; k < T; k += kMergeThreads) {
+        gl[k] = k;
+        flag[k] = 0;
+    }
+    __syncthreads();
+    for (uint32_t i = 0; i + 1 < L; ++i) {  // bottom-up: layer i+1 from layer i
+        const uint32_t nA = nlab[i], nB = nlab[i + 1], sa = lstart[i], sb = lstart[i + 1];
+        const uint8_t* m = conn + cstart[i];
+        for (uint32_t b = t; b < nB; b += kMergeThreads) {
+            uint32_t v = gl[sb + b];
+            for (uint32_t a = b == 0 ? 0 : 1; a < (b == 0 ? 1u : nA); ++a)
+                if (m[(size_t)a * nB + b]) v = min(v, gl[sa + a]);
+            gl[sb + b] = v;
+        }
+        __syncthreads();
+    }
+    for (uint32_t j = 0; j + 1 < L; ++j) {  // top-down: layer i from layer i+1
+        const uint32_t i = L - 2 - j;
+        const uint32_t nA = nlab[i], nB = nlab[i + 1], sa = lstart[i], sb = lstart[i + 1];
+        const uint8_t* m = conn + cstart[i];
+        for (uint32_t a = t; a < nA; a += kMergeThreads) {
+            uint32_t v = gl[sa + a];
+            const uint8_t* row = m + (size_t)a * nB;
+            for (uint32_t b = a == 0 ? 0 : 1; b < (a == 0 ? 1u : nB); ++b)
+                if (row[b]) v = min(v, gl[sb + b]);
+            gl[sa + a] = v;
+        }
+        __syncthreads();
+    }
+    for (uint32_t k = t; k < T; k += kMergeThreads) flag[gl[k]] = 1;
+    __syncthreads();
+    // exclusive scan of the flags in chunks of kMergeThreads (flag[v] becomes v's rank)
+    __shared__ uint32_t wsum[kMergeThreads / 64];
+    __shared__ uint32_t carry;
+    if (t == 0) carry = 0;
+    __syncthreads();
+    const uint32_t lane = t & 63, w = t >> 6;
+    for (uint32_t base = 0; base < T; base += kMergeThreads) {
+        const uint32_t k = base + t;
+        const uint32_t f = k < T ? flag[k] : 0;
+        const uint64_t bal = __ballot(f != 0);
+        const uint32_t below = __popcll(bal & ((1ull << lane) - 1));
+        if (lane == 63) wsum[w] = below + f;
+        __syncthreads();
+        uint32_t pre = carry;
+        for (uint32_t q = 0; q < w; ++q) pre += wsum[q];
+        if (k < T) flag[k] = pre + below;
+        __syncthreads();
+        if (t == kMergeThreads - 1) carry = pre + below + f;
+        __syncthreads();
+    }
+    for (uint32_t k = t; k < T; k += kMergeThreads) merged[k] = flag[gl[k]];
+    if (t == 0) *nobj = carry;
 }
 
 // ---- host ------------------------------------------------------------------------------------------
@@ -754,6 +864,8 @@ struct gdf_segmenter {
     bool have = false;
     GpuBuf par, bits, blabel, nlab, lstart, cstart, labels, st, sums, stats5, cent, l2c, conn;
     GpuBuf codes, rec, ncont, err, scratch, bgpart, tdbg;
+    GpuBuf mgl, mflag, mout;      // label merge (k_cc_merge_layers)
+    GpuBuf prec, pcodes, phdr;    // packed contours (k_cc_pack_contours)
     uint64_t code_cap = 0;
     uint32_t rec_cap = 0;
     std::vector<uint32_t> h_nlab, h_lstart;
@@ -763,6 +875,7 @@ struct gdf_segmenter {
     // contours resolved on the host (after the first query)
     bool contours_read = false;
     std::vector<uint32_t> h_ncont, h_rec;
+    std::vector<uint64_t> h_roff, h_coff;  // per-layer offsets into h_rec (records) / h_codes
     std::vector<uint8_t> h_codes;
     uint64_t total_points = 0;
     uint32_t total_contours = 0;
@@ -946,40 +1059,37 @@ void read_contours(gdf_segmenter* g) {
     if (!(g->flags & GDF_SEG_CONTOURS)) seg_fail(GDF_ERR_STATE, "contours were not requested");
     if (g->contours_read) return;
     const hipStream_t s = g->s();
+    // compact host copies (k_cc_pack_contours): layer z's records at h_roff[z], its chain codes
+    // at h_coff[z] - one download of each
+    const uint32_t L = g->L;
+    SEGCHK(g->prec.ensure(g->rec.bytes));
+    SEGCHK(g->pcodes.ensure(g->codes.bytes));
+    SEGCHK(g->phdr.ensure((size_t)(2 * L + 2) * 8));
+    hipLaunchKernelGGL(k_cc_pack_contours, dim3(L), dim3(256), 0, s, g->rec.as<const uint32_t>(),
+                       g->rec_cap, g->codes.as<const uint8_t>(), g->code_cap,
+                       g->ncont.as<const uint32_t>(), L, g->prec.as<uint32_t>(),
+                       g->pcodes.as<uint8_t>(), g->phdr.as<unsigned long long>());
+    SEGCHK(hipGetLastError());
+    std::vector<unsigned long long> hdr(2 * (size_t)L + 2);
     uint32_t err = 0;
-    g->h_ncont.assign(g->L, 0);
+    g->h_ncont.assign(L, 0);
     SEGCHK(hipMemcpyAsync(&err, g->err.p, 4, hipMemcpyDeviceToHost, s));
-    SEGCHK(hipMemcpyAsync(g->h_ncont.data(), g->ncont.p, (size_t)g->L * 4, hipMemcpyDeviceToHost, s));
+    SEGCHK(hipMemcpyAsync(g->h_ncont.data(), g->ncont.p, (size_t)L * 4, hipMemcpyDeviceToHost, s));
+    SEGCHK(hipMemcpyAsync(hdr.data(), g->phdr.p, hdr.size() * 8, hipMemcpyDeviceToHost, s));
     SEGCHK(hipStreamSynchronize(s));
     if (err) seg_fail(GDF_ERR_CAPACITY, "contour capacity exceeded");
-    g->h_rec.assign((size_t)g->rec_cap * 4 * g->L, 0);
-    g->total_contours = 0;
+    g->h_roff.assign(hdr.begin(), hdr.begin() + L + 1);
+    g->h_coff.assign(hdr.begin() + L + 1, hdr.end());
+    g->h_rec.resize(g->h_roff[L] * 4);
+    g->h_codes.resize(g->h_coff[L]);
+    if (!g->h_rec.empty())
+        SEGCHK(hipMemcpyAsync(g->h_rec.data(), g->prec.p, g->h_rec.size() * 4, hipMemcpyDeviceToHost, s));
+    if (!g->h_codes.empty())
+        SEGCHK(hipMemcpyAsync(g->h_codes.data(), g->pcodes.p, g->h_codes.size(), hipMemcpyDeviceToHost, s));
+    SEGCHK(hipStreamSynchronize(s));
+    g->total_contours = (uint32_t)g->h_roff[L];
     g->total_points = 0;
-    uint64_t code_bytes = 0;
-    for (uint32_t z = 0; z < g->L; ++z) {
-        const uint32_t n = g->h_ncont[z];
-        if (n)
-            SEGCHK(hipMemcpyAsync(g->h_rec.data() + (size_t)z * g->rec_cap * 4,
-                                  g->rec.as<uint32_t>() + (size_t)z * g->rec_cap * 4,
-                                  (size_t)n * 16, hipMemcpyDeviceToHost, s));
-    }
-    SEGCHK(hipStreamSynchronize(s));
-    std::vector<uint64_t> used(g->L, 0);
-    for (uint32_t z = 0; z < g->L; ++z) {
-        const uint32_t n = g->h_ncont[z];
-        const uint32_t* r = g->h_rec.data() + (size_t)z * g->rec_cap * 4;
-        for (uint32_t d = 0; d < n; ++d) g->total_points += r[4 * d + 3];
-        if (n) used[z] = (uint64_t)r[4 * (n - 1) + 2] + r[4 * (n - 1) + 3];
-        g->total_contours += n;
-        code_bytes = std::max(code_bytes, used[z]);
-    }
-    g->h_codes.assign((size_t)g->code_cap * g->L, 0);
-    for (uint32_t z = 0; z < g->L; ++z)
-        if (used[z])
-            SEGCHK(hipMemcpyAsync(g->h_codes.data() + (size_t)z * g->code_cap,
-                                  g->codes.as<uint8_t>() + (size_t)z * g->code_cap, used[z],
-                                  hipMemcpyDeviceToHost, s));
-    SEGCHK(hipStreamSynchronize(s));
+    for (size_t d = 0; d < g->h_roff[L]; ++d) g->total_points += g->h_rec[4 * d + 3];
     g->contours_read = true;
 }
 
@@ -1138,8 +1248,8 @@ int gdf_seg_download_contours(gdf_segmenter* g, int32_t* l2c, uint32_t* per_laye
         uint32_t c = 0;
         for (uint32_t z = 0; z < g->L; ++z) {
             const uint32_t n = g->h_ncont[z];
-            const uint32_t* r = g->h_rec.data() + (size_t)z * g->rec_cap * 4;
-            const uint8_t* cz = g->h_codes.data() + (size_t)z * g->code_cap;
+            const uint32_t* r = g->h_rec.data() + g->h_roff[z] * 4;
+            const uint8_t* cz = g->h_codes.data() + g->h_coff[z];
             for (uint32_t j = 0; j < n; ++j) {  // findContours order = reverse discovery
                 const uint32_t d = n - 1 - j;
                 const uint32_t np = r[4 * d + 3];
@@ -1168,48 +1278,25 @@ int gdf_seg_download_contours(gdf_segmenter* g, int32_t* l2c, uint32_t* per_laye
 
 namespace {
 
-// mergeLabelsAcrossLayers (fusion.cpp:2243-2361): bottom-up then top-down min propagation of the
-// sequential global labels over the connection matrices (background only with background), then
-// UIntGrouper order: merged id = rank of the propagated id among the distinct ones.
+// mergeLabelsAcrossLayers (fusion.cpp:2243-2361) by k_cc_merge_layers on the segmenter's stream:
+// the connection matrices stay on the device, only the merged ids (4 B per label) come back.
 uint32_t merge_labels(gdf_segmenter* g, uint32_t* merged) {
-    {
-        std::vector<uint8_t> conn(g->conn_bytes);
-        if (g->conn_bytes) {
-            SEGCHK(hipMemcpyAsync(conn.data(), g->conn.p, g->conn_bytes, hipMemcpyDeviceToHost, g->s()));
-            SEGCHK(hipStreamSynchronize(g->s()));
-        }
-        const uint32_t L = g->L;
-        std::vector<uint32_t> gl(g->total);
-        for (uint32_t k = 0; k < g->total; ++k) gl[k] = k;
-        auto pass = [&](uint32_t la, uint32_t lb, bool up) {
-            const uint32_t nA = g->h_nlab[la], nB = g->h_nlab[lb];
-            const uint8_t* m = conn.data() + g->h_cstart[la];
-            if (up) {  // layer b takes the lowest label of its connected labels in layer a
-                for (uint32_t b = 0; b < nB; ++b) {
-                    uint32_t& v = gl[g->h_lstart[lb] + b];
-                    for (uint32_t a = 0; a < nA; ++a)
-                        if ((a == 0) == (b == 0) && m[(size_t)a * nB + b])
-                            v = std::min(v, gl[g->h_lstart[la] + a]);
-                }
-            } else {
-                for (uint32_t a = 0; a < nA; ++a) {
-                    uint32_t& v = gl[g->h_lstart[la] + a];
-                    for (uint32_t b = 0; b < nB; ++b)
-                        if ((a == 0) == (b == 0) && m[(size_t)a * nB + b])
-                            v = std::min(v, gl[g->h_lstart[lb] + b]);
-                }
-            }
-        };
-        for (uint32_t i = 0; i + 1 < L; ++i) pass(i, i + 1, true);
-        for (uint32_t i = 0; i + 1 < L; ++i) pass(L - 2 - i, L - 1 - i, false);
-        std::vector<uint32_t> rank(g->total, kNone);
-        for (uint32_t k = 0; k < g->total; ++k) rank[gl[k]] = 0;  // gl[k] <= k < total
-        uint32_t next = 0;
-        for (uint32_t v = 0; v < g->total; ++v)
-            if (rank[v] == 0) rank[v] = next++;
-        for (uint32_t k = 0; k < g->total; ++k) merged[k] = rank[gl[k]];
-        return next;
-    }
+    const hipStream_t s = g->s();
+    const uint32_t T = g->total;
+    SEGCHK(g->mgl.ensure((size_t)std::max(T, 1u) * 4));
+    SEGCHK(g->mflag.ensure((size_t)std::max(T, 1u) * 4));
+    SEGCHK(g->mout.ensure((size_t)std::max(T, 1u) * 4 + 4));
+    uint32_t* out = g->mout.as<uint32_t>();
+    hipLaunchKernelGGL(k_cc_merge_layers, dim3(1), dim3(kMergeThreads), 0, s,
+                       g->conn.as<const uint8_t>(), g->cstart.as<const uint64_t>(),
+                       g->nlab.as<const uint32_t>(), g->lstart.as<const uint32_t>(), g->L, T,
+                       g->mgl.as<uint32_t>(), g->mflag.as<uint32_t>(), out, out + T);
+    SEGCHK(hipGetLastError());
+    uint32_t n = 0;
+    if (T) SEGCHK(hipMemcpyAsync(merged, out, (size_t)T * 4, hipMemcpyDeviceToHost, s));
+    SEGCHK(hipMemcpyAsync(&n, out + T, 4, hipMemcpyDeviceToHost, s));
+    SEGCHK(hipStreamSynchronize(s));
+    return n;
 }
 
 }  // namespace
@@ -1258,7 +1345,7 @@ int gdf_seg_create_objects(gdf_segmenter* g, const float lower[3], const float c
         if (g->flags & GDF_SEG_CONTOURS)
             for (uint32_t z = 0; z < g->L; ++z) {
                 const uint32_t nc = g->h_ncont[z];
-                const uint32_t* r = g->h_rec.data() + (size_t)z * g->rec_cap * 4;
+                const uint32_t* r = g->h_rec.data() + g->h_roff[z] * 4;
                 for (uint32_t j = 0; j < nc; ++j) csize[z].push_back(r[4 * (nc - 1 - j) + 3]);
             }
         std::vector<uint32_t> layer(T), local(T);

@@ -821,6 +821,14 @@ class Segmenter:
             r["num_objects"] = nobj.value
         return r
 
+    def merge_labels(self):
+        """mergeLabelsAcrossLayers (fusion.cpp:2243-2361, on the device): (merged ids [T], n)."""
+        T = self.counts().total_labels
+        merged = np.zeros(T, np.uint32)
+        nobj = C.c_uint32(0)
+        self._check(self._lib.gdf_seg_merge_labels(self._h, _ptr(merged), T, C.byref(nobj)))
+        return merged, nobj.value
+
     def create_objects(self, lower, cell_size):
         """createCCObjects' aggregate fields (no OpenCV shapes): (columns dict, components)."""
         lo, cs = _vec3(lower), _vec3(cell_size)

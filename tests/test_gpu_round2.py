@@ -62,14 +62,15 @@ def test_dense_4k_frame_parity(Engine):
     compare_results(gpu, orc, tag="4k dense")
 
 
-@pytest.mark.parametrize("pinned", [True, False])
-def test_host_stream_overlapped_h2d(Engine, pinned):
-    """Host depth maps through gdf_run_host_stream with 3 frames in flight: pinned maps are read
-    in place on the slot's stream, pageable ones through the slot's pinned staging; the grid after
-    all frames and the last frame's outputs equal the oracle's.  The pageable source is
-    overwritten after the call returns (the staging copy was taken: borrowed-until-upload)."""
+@pytest.mark.parametrize("pinned,W,H", [(True, 320, 240), (False, 320, 240), (False, 1280, 720)])
+def test_host_stream_overlapped_h2d(Engine, pinned, W, H):
+    """Host depth maps through gdf_run_host_stream with 3 frames in flight: every host map (pinned
+    or pageable) is copied into the slot's pinned staging - 720p maps (1.8 MB) in 256 KB chunks by
+    the staging threads - and sent on the slot's stream; the grid after all frames and the last
+    frame's outputs equal the oracle's.  The pageable source is overwritten after the call
+    returns (the staging copy was taken: borrowed-until-upload)."""
     p = ComponentParams()
-    cam = synth.make_camera(0, 320, 240)
+    cam = synth.make_camera(0, W, H)
     ring = [synth.dense_frame(cam, 0, f) for f in range(4)]
     if pinned:
         host = [hiprt.PinnedArray.from_numpy(f) for f in ring]
@@ -79,7 +80,7 @@ def test_host_stream_overlapped_h2d(Engine, pinned):
         ptrs = [h.ctypes.data for h in host]
     gpu, orc = Engine(), OracleFusion(threads=8)
     gpu.set_pipeline_depth(3)
-    sc = gpu.make_stream_camera(ptrs, 320, 240, *cam.intrinsics(), cam.T_world, cam.T_crop)
+    sc = gpu.make_stream_camera(ptrs, W, H, *cam.intrinsics(), cam.T_world, cam.T_crop)
     n = 11
     gpu.run_host_stream([sc], p.to_c(None, None, False, False), 0, n)
     if not pinned:

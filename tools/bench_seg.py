@@ -47,9 +47,24 @@ def run_seg(frames=16, reps=50, cameras=4, cpu=True):
             seg.label_engine_grid(eng, flags)
         torch.cuda.synchronize()
         out[f"ms_{name}"] = round((time.perf_counter() - t0) / reps * 1e3, 4)
-    t0 = time.perf_counter()
-    r = seg.results()
-    out["ms_download_and_merge"] = round((time.perf_counter() - t0) * 1e3, 3)
+    # the label merge alone (k_cc_merge_layers + the merged ids' D2H), and every output to the
+    # host (labels 2 B per cell, stats, contours, connections, merge) after a fresh labelling
+    tm, td = [], []
+    for _ in range(max(3, reps // 2)):
+        seg.label_engine_grid(eng, 2)  # (no contours: counts() then reads no contour records)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        seg.merge_labels()
+        tm.append(time.perf_counter() - t0)
+        seg.label_engine_grid(eng, 3)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        r = seg.results()
+        td.append(time.perf_counter() - t0)
+    out["ms_merge"] = round(float(np.median(tm)) * 1e3, 4)
+    out["ms_download_all"] = round(float(np.median(td)) * 1e3, 4)
+    out["download_all_bytes"] = int(sum(np.asarray(v).nbytes for v in r.values()
+                                        if isinstance(v, np.ndarray)))
     c = seg.counts()
     out.update(total_labels=int(c.total_labels), contours=int(c.total_contours),
                contour_points=int(c.total_contour_points),
