@@ -79,6 +79,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=3.0, help="per CPU run (5 runs)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="do not bracket launches with HIP events (for rocprofv3 runs)")
+    ap.add_argument("--h2d-only", action="store_true",
+                    help="only the host-depth-map (H2D-inclusive) line, as JSON")
     ap.add_argument("--no-secondary", action="store_true",
                     help="N = 1: skip the 720p / 4K / stress / H2D / C3 lines")
     ap.add_argument("--c3-window", type=int, default=256)
@@ -416,6 +418,9 @@ def main():
     hiprt.set_device(local_rank)
     W, H, K = args.width, args.height, args.cameras
     params = ComponentParams()
+    if args.h2d_only:
+        print(json.dumps(run_h2d(args, params, args.steps, args.warmup)), flush=True)
+        return
     eng = GPUDepthmapFusion(local_rank)
     st = DepthStream(eng, W, H, K, rank, args.workload, args.ring)
     P = st.P
@@ -662,6 +667,25 @@ def run_component_sync(args, params, frames=300, warm=20):
             "download_bytes_per_frame": int(pts.nbytes + keys.nbytes + vox.nbytes + grid.nbytes)}
 
 
+def run_h2d(args, params, steps, warm):
+    """C2 from HOST depth maps: each frame's map is copied into the slot's pinned staging by
+    GDF_H2D_THREADS host threads and DMA'd on the slot's stream, overlapped with the kernels of the
+    frames in flight."""
+    from ros_gpu_depthmap_fusion_amd.gdf import GPUDepthmapFusion
+    eng = GPUDepthmapFusion(0)
+    st = DepthStream(eng, args.width, args.height, 1, 0, args.workload, args.ring,
+                     host_frames=True)
+    r = time_single(st, params, steps, warm, max(1, min(4, args.pipeline)), False, "", args.batch)
+    r["workload"] = "C2 with host (pinned) depth maps: " + workload_name(
+        args.width, args.height, 1, args.workload)
+    r["value_h2d"] = r.pop("value")
+    r["h2d_threads"] = int(os.environ.get("GDF_H2D_THREADS", "4"))
+    r["h2d_GBps"] = round(2.0 * args.width * args.height * args.batch / (r["ms_per_step"] / 1e3) / 1e9, 2)
+    del st
+    eng.close()
+    return r
+
+
 def run_secondary(args, params):
     """N = 1 only: the other single-GPU configurations, each with its own roofline."""
     from ros_gpu_depthmap_fusion_amd.gdf import GPUDepthmapFusion
@@ -689,17 +713,7 @@ def run_secondary(args, params):
     # runtime parameter changes (component.cpp:970-990): two flying-pixel thresholds alternating
     # every step - one cached graph per (slot, set) - and the same stream with graphs off
     out["vga_alternating_params"] = run_alternating(args, params, steps, warm)
-    # host-resident depth maps (pinned, uploaded on a copy stream overlapped with compute)
-    eng = GPUDepthmapFusion(0)
-    st = DepthStream(eng, args.width, args.height, 1, 0, args.workload, args.ring,
-                     host_frames=True)
-    r = time_single(st, params, steps, warm, max(1, min(4, args.pipeline)), False, "", args.batch)
-    r["workload"] = "C2 with host (pinned) depth maps: " + workload_name(
-        args.width, args.height, 1, args.workload)
-    r["value_h2d"] = r.pop("value")
-    out["vga_h2d"] = r
-    del st
-    eng.close()
+    out["vga_h2d"] = run_h2d(args, params, steps, warm)
     out["component_sync"] = run_component_sync(args, params)
     try:
         sys.path.insert(0, os.path.join(ROOT, "tools"))

@@ -57,7 +57,9 @@ struct GdfError {
 // Host -> pinned-staging copies of host depth maps, split over worker threads: one thread's
 // memcpy (~8-15 GB/s, box-dependent) bounded the host-map line at half the device-map rate
 // (VERDICT r2 weak #11).  The caller works too; workers are created on first use and block on a
-// condition variable between calls.  Threads: GDF_H2D_THREADS (default 4, 1 = caller only).
+// condition variable between calls.  Threads: GDF_H2D_THREADS (default 1 = the caller only:
+// measured on MI355X, 8-frame VGA batches, 1 / 4 / 8 threads 14.3 / 12.9 / 13.0 Gpoints/s - the
+// DMA at ~27 GB/s, not the copy, bounds the host-map line on that box).
 class StagingCopier {
   public:
     struct Job {
@@ -105,7 +107,7 @@ class StagingCopier {
     unsigned threads() {
         if (!nthreads_) {
             const char* s = std::getenv("GDF_H2D_THREADS");
-            const int v = s ? std::atoi(s) : 4;
+            const int v = s ? std::atoi(s) : 1;
             nthreads_ = (unsigned)std::max(1, std::min(v, 16));
         }
         return nthreads_;

@@ -2495,7 +2495,7 @@ uint32_t g_group_scan_tiles = 1024;
 // the four component chains side by side, one group per lane, the groups of a tile in parallel);
 // longer ones by a wave (gdf_voxsum.hpp's stretch sums: a wave per group, serial over a block's
 // groups).  Tuning knob GDF_SMALL_GROUP.
-uint32_t g_small_group = 256;
+uint32_t g_small_group = 32;
 
 // p[0] + ... + p[n-1] per component, in order, by one thread: blocks of 4 points alternate between
 // two register sets, the next block read while the current one is added (LDS latency off the
@@ -2541,6 +2541,7 @@ __device__ __forceinline__ float4 thread_group_sum(const float4* p, uint32_t n) 
 
 constexpr uint32_t kChainPad = 16;  // LDS padding of staged point buffers
 constexpr uint32_t kExtraRuns = 64;  // runs past a k_group_runs tile read for its last group
+constexpr uint32_t kRunPasses = 4;   // staging windows per k_group_runs tile (mode 2)
 
 // Voxel sums, one component per wave (gdf_voxsum.hpp): wave c of a 4-wave group sums component c.
 // A staged group of cnt points (float4 AoS in LDS)
@@ -2781,7 +2782,45 @@ __global__ __launch_bounds__(256) void k_group_big(const uint32_t* __restrict__ 
 // GDF_RUN_INBLOCK
 uint32_t g_run_stage = 2048;
 uint32_t g_run_inblock = 2048;
-uint32_t g_run_wave = 0;  // staged groups above g_small_group by a wave in k_group_runs (GDF_RUN_WAVE)
+// staged groups above g_small_group in k_group_runs (GDF_RUN_WAVE): 0 queued for k_group_runs_big,
+// 1 a wave's stretch sums (wave_group_sum), 2 four lanes' chains (lane_comp_chain, default)
+uint32_t g_run_wave = 2;
+
+// comp[0] + comp[4] + ... + comp[4 (n - 1)] in order: one component of a staged group by one lane
+// (its 4 lanes hold the group's 4 components); blocks of 8 values alternate between two register
+// sets so the LDS reads of the next block overlap the additions of the current one.
+__device__ __forceinline__ float lane_comp_chain(const float* comp, uint32_t n) {
+    float acc = 0.0f;
+    uint32_t k = 0;
+    if (n >= 16) {
+        float a[8], b[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) a[q] = comp[4 * q];
+#pragma unroll 1
+        for (; k + 16 <= n; k += 16) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) b[q] = comp[4 * (k + 8 + q)];
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc = acc + a[q];
+            const uint32_t kn = k + 16 + 8 <= n ? k + 16 : k;  // (in range; unused past the loop)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) a[q] = comp[4 * (kn + q)];
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc = acc + b[q];
+        }
+        if (k + 8 <= n) {  // a[] holds values k .. k+7 exactly when k + 8 <= n here
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc = acc + a[q];
+            k += 8;
+        }
+    }
+    for (; k < n; ++k) acc = acc + comp[4 * k];
+    return acc;
+}
 uint32_t g_run_big_blocks = 1024;  // k_group_runs_big grid (tuning knob GDF_RUN_BIG_BLOCKS)
 // chunks of k_group_runs_big (one 4-wave block per queued group): 1 K points (Q = 16) or 512
 // (Q = 8); 0 never 1 K, 1 always, 2 (default) for single depth-only frames, whose long voxels
@@ -3029,9 +3068,11 @@ __device__ __forceinline__ float block_stream_sum(const uint32_t* __restrict__ r
 // are summed by their thread, longer staged ones by a wave from LDS, and the others (past the
 // staged points, or continuing past the tile) are queued for k_group_runs_big - one append per
 // group, so a block never waits on a long chain.  Marks, frame voxel starts and corners as k_group.
-// WAVE = false (default): staged groups above small_max are queued like the unstaged ones, and the
-// block needs no per-wave transpose buffers (37.6 instead of 59.4 KB of LDS: 4 blocks per CU, not 2).
-template <int kRunStage, bool WAVE>
+// WAVE (g_run_wave): staged groups above small_max are 0 queued like the unstaged ones, 1 summed
+// by a wave from LDS (wave_group_sum: per-wave transpose buffers, 59.4 instead of 37.6 KB of LDS -
+// 2 blocks per CU, not 4), 2 summed by 4 lanes each, one component chain per lane (16 groups per
+// wave, the tile's long groups dealt round-robin over the 4 waves).
+template <int kRunStage, int WAVE>
 __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
     const uint32_t* __restrict__ keys, const uint32_t* __restrict__ rvals,
     const uint32_t* __restrict__ count, const uint32_t* __restrict__ run_start,
@@ -3043,7 +3084,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
     uint32_t inblock_max, uint32_t* __restrict__ rps, uint32_t* __restrict__ rlen,
     uint32_t small_max) {
     __shared__ uint32_t s_wave[4];
-    __shared__ uint32_t s_tile, s_epoch, s_excl, s_nbig, s_nq, s_qbase, s_wend, s_nx;
+    __shared__ uint32_t s_tile, s_epoch, s_excl, s_nbig, s_nq, s_qbase, s_wend, s_nx, s_nbase;
     __shared__ uint32_t s_start[kGroupThreads + 1];  // group starts (run index); [total] = end
     // the tile's runs, then up to kExtraRuns runs of the next tiles (the rest of the tile's last
     // group): first points and the exclusive scan of their lengths
@@ -3051,10 +3092,10 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
     __shared__ uint32_t s_off[kGroupThreads + kExtraRuns + 1];
     __shared__ uint32_t s_big[kGroupThreads];
     __shared__ float4 s_pts[kRunStage + kChainPad];
-    __shared__ __attribute__((aligned(16))) float s_wsoa[WAVE ? 4 : 1][WAVE ? kWaveSoa : 4];
+    __shared__ __attribute__((aligned(16))) float s_wsoa[WAVE == 1 ? 4 : 1][WAVE == 1 ? kWaveSoa : 4];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    if (WAVE) wave_soa_init(s_wsoa[wid]);
-    if (!WAVE) inblock_max = min(inblock_max, small_max);  // longer groups: k_group_runs_big
+    if (WAVE == 1) wave_soa_init(s_wsoa[wid]);
+    if (WAVE == 0) inblock_max = min(inblock_max, small_max);  // longer groups: k_group_runs_big
     const uint32_t n = *count;  // runs
     const uint32_t ntiles = (n + kGroupThreads - 1) / kGroupThreads;
     const uint32_t kmask = nframes > 1 ? (1u << fshift) - 1u : 0xFFFFFFFFu;
@@ -3081,6 +3122,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
             s_nq = 0;
             s_wend = 0;
             s_nx = 0;
+            s_nbase = 0xFFFFFFFFu;
         }
         walk += gridDim.x;
         __syncthreads();
@@ -3164,75 +3206,179 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
         const uint32_t W0 = total ? s_off[s_start[0] - t0] : 0u;
         __syncthreads();  // (the last group's end, s_start[total]; the extra runs)
         const uint32_t rend = tend + s_nx;  // runs with records here
-        bool inblock = false;
-        if (threadIdx.x < total && average) {
-            const uint32_t s = s_start[threadIdx.x], e = s_start[threadIdx.x + 1];
-            if (e <= rend) {
-                const uint32_t ge = s_off[e - t0] - W0;
-                inblock = ge <= (uint32_t)kRunStage && ge - (s_off[s - t0] - W0) <= inblock_max;
-                if (inblock) atomicMax(&s_wend, ge);
+        if constexpr (WAVE == 2) {
+            // Windows of kRunStage staged positions, up to kRunPasses per tile: each window starts
+            // at the first group not summed yet and takes every group that ends inside it; its
+            // groups are summed by their thread (<= small_max points) or by 4 lanes, one component
+            // chain each.  Groups longer than inblock_max, continuing past the tile's records, or
+            // left after the last window are queued for k_group_runs_big.
+            uint32_t gs = 0, ge = 0;
+            bool elig = false, done = false;
+            if (threadIdx.x < total && average) {
+                const uint32_t s = s_start[threadIdx.x], e = s_start[threadIdx.x + 1];
+                if (e <= rend) {
+                    gs = s_off[s - t0];
+                    ge = s_off[e - t0];
+                    elig = ge - gs <= inblock_max;
+                }
             }
-        }
-        __syncthreads();
-        const uint32_t staged = s_wend;
-        for (uint32_t k = threadIdx.x; k < staged; k += kGroupThreads) {
-            const uint32_t q = W0 + k;
-            uint32_t lo = 0, hi = kGroupThreads + s_nx;  // last run with s_off <= q
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (s_off[mid] <= q) lo = mid; else hi = mid;
+            uint32_t base = W0;
+#pragma unroll 1
+            for (uint32_t pass = 0; pass < kRunPasses; ++pass) {
+                const bool in = elig && !done && gs >= base && ge - base <= (uint32_t)kRunStage;
+                // (shared counters: each is reset by thread 0 between the barrier after its last
+                // read and the barrier before its next update)
+                if (in) atomicMax(&s_wend, ge - base);
+                __syncthreads();  // A
+                const uint32_t staged = s_wend;
+                if (threadIdx.x == 0) s_nbase = 0xFFFFFFFFu;  // (read before A by everyone)
+                if (staged == 0) break;  // block-uniform
+                for (uint32_t k = threadIdx.x; k < staged; k += kGroupThreads) {
+                    const uint32_t q = base + k;
+                    uint32_t lo = 0, hi = kGroupThreads + s_nx;  // last run with s_off <= q
+                    while (hi - lo > 1) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (s_off[mid] <= q) lo = mid; else hi = mid;
+                    }
+                    s_pts[k] = pts[s_ps[lo] + (q - s_off[lo])];
+                }
+                __syncthreads();  // B
+                if (threadIdx.x == 0) s_wend = 0;
+                if (in && ge - gs <= small_max) {
+                    const float4 acc = thread_group_sum(s_pts + (gs - base), ge - gs);
+                    const float fc = (float)(ge - gs);
+                    *reinterpret_cast<float4*>(out + 4 * (size_t)(s_excl + threadIdx.x)) =
+                        make_float4(acc.x / fc, acc.y / fc, acc.z / fc, acc.w);
+                } else if (in) {
+                    s_big[atomicAdd(&s_nbig, 1u)] = threadIdx.x;
+                }
+                __syncthreads();  // C
+                const uint32_t nbig = s_nbig;
+                for (uint32_t bi = ((uint32_t)lane >> 2) * 4u + (uint32_t)wid; bi < nbig; bi += 64u) {
+                    const uint32_t li = s_big[bi];  // staged long groups: 4 lanes, lane = component
+                    const uint32_t g0 = s_off[s_start[li] - t0] - base;
+                    const uint32_t g1 = s_off[s_start[li + 1] - t0] - base;
+                    const uint32_t c = (uint32_t)lane & 3u;
+                    const float acc = lane_comp_chain(reinterpret_cast<const float*>(s_pts + g0) + c, g1 - g0);
+                    out[4 * (size_t)(s_excl + li) + c] = c < 3 ? acc / (float)(g1 - g0) : acc;
+                }
+                done = done || in;
+                if (elig && !done) atomicMin(&s_nbase, gs);
+                __syncthreads();  // D (s_pts read; s_nbase complete)
+                base = s_nbase;
+                if (threadIdx.x == 0) s_nbig = 0;
+                if (base == 0xFFFFFFFFu) break;  // block-uniform: nothing eligible left
             }
-            s_pts[k] = pts[s_ps[lo] + (q - s_off[lo])];
-        }
-        __syncthreads();
-        if (total == 0) continue;  // block-uniform
-        uint32_t qlocal = 0xFFFFFFFFu;  // this thread's group in the tile's queue appends
-        if (threadIdx.x < total && average && !inblock) qlocal = atomicAdd(&s_nq, 1u);
-        __syncthreads();
-        if (threadIdx.x == 0 && s_nq) s_qbase = atomicAdd(qctr, s_nq);  // one append per tile
-        __syncthreads();
-        if (threadIdx.x < total) {
-            const uint32_t g = s_excl + threadIdx.x;
-            const uint32_t s = s_start[threadIdx.x], e = s_start[threadIdx.x + 1];
-            float* o = out + 4 * (size_t)g;
-            if (marks) {
-                const uint32_t k = keys[s] & kmask;
-                atomicOr(marks + (k >> 5), 1u << (k & 31u));
+            __syncthreads();
+            if (total == 0) continue;  // block-uniform
+            uint32_t qlocal = 0xFFFFFFFFu;
+            if (threadIdx.x < total && average && !done) qlocal = atomicAdd(&s_nq, 1u);
+            __syncthreads();
+            if (threadIdx.x == 0 && s_nq) s_qbase = atomicAdd(qctr, s_nq);  // one append per tile
+            __syncthreads();
+            if (threadIdx.x < total) {
+                const uint32_t g = s_excl + threadIdx.x;
+                const uint32_t s = s_start[threadIdx.x], e = s_start[threadIdx.x + 1];
+                if (marks) {
+                    const uint32_t k = keys[s] & kmask;
+                    atomicOr(marks + (k >> 5), 1u << (k & 31u));
+                }
+                if (fvox) {
+                    const uint32_t fc = keys[s] >> fshift;
+                    const uint32_t f0 = s == 0 ? 0u : (keys[s - 1] >> fshift) + 1u;
+                    for (uint32_t f = f0; f <= fc; ++f) fvox[f] = g;
+                }
+                if (!average) {
+                    float c[4];
+                    group_corner(keys[s] & kmask, vp, c);
+                    *reinterpret_cast<float4*>(out + 4 * (size_t)g) = make_float4(c[0], c[1], c[2], c[3]);
+                } else if (qlocal != 0xFFFFFFFFu) {  // k_group_runs_big
+                    const uint32_t slot = s_qbase + qlocal;
+                    if (slot < bigq_cap) bigq[slot] = make_uint4(g, s, e, 0u);
+                    else atomicOr(err, 8u);
+                }
             }
-            if (fvox) {
-                const uint32_t fc = keys[s] >> fshift;
-                const uint32_t f0 = s == 0 ? 0u : (keys[s - 1] >> fshift) + 1u;
-                for (uint32_t f = f0; f <= fc; ++f) fvox[f] = g;
+        } else {
+            bool inblock = false;
+            if (threadIdx.x < total && average) {
+                const uint32_t s = s_start[threadIdx.x], e = s_start[threadIdx.x + 1];
+                if (e <= rend) {
+                    const uint32_t ge = s_off[e - t0] - W0;
+                    inblock = ge <= (uint32_t)kRunStage && ge - (s_off[s - t0] - W0) <= inblock_max;
+                    if (inblock) atomicMax(&s_wend, ge);
+                }
             }
-            const uint32_t g0 = s_off[s - t0] - W0;  // staged positions of the group
-            const uint32_t g1 = e <= rend ? s_off[e - t0] - W0 : 0xFFFFFFFFu;
-            if (!average) {
-                float c[4];
-                group_corner(keys[s] & kmask, vp, c);
-                *reinterpret_cast<float4*>(o) = make_float4(c[0], c[1], c[2], c[3]);
-            } else if (qlocal != 0xFFFFFFFFu) {  // past the staged points: k_group_runs_big
-                const uint32_t slot = s_qbase + qlocal;
-                if (slot < bigq_cap) bigq[slot] = make_uint4(g, s, e, 0u);
-                else atomicOr(err, 8u);
-            } else if (g1 - g0 <= small_max) {
-                const float4 a = thread_group_sum(s_pts + g0, g1 - g0);
-                const float fc = (float)(g1 - g0);
-                *reinterpret_cast<float4*>(o) = make_float4(a.x / fc, a.y / fc, a.z / fc, a.w);
-            } else {
-                s_big[atomicAdd(&s_nbig, 1u)] = threadIdx.x;
+            __syncthreads();
+            const uint32_t staged = s_wend;
+            for (uint32_t k = threadIdx.x; k < staged; k += kGroupThreads) {
+                const uint32_t q = W0 + k;
+                uint32_t lo = 0, hi = kGroupThreads + s_nx;  // last run with s_off <= q
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (s_off[mid] <= q) lo = mid; else hi = mid;
+                }
+                s_pts[k] = pts[s_ps[lo] + (q - s_off[lo])];
             }
-        }
-        __syncthreads();
-        const uint32_t nbig = WAVE ? s_nbig : 0u;
-        for (uint32_t bi = wid; bi < nbig; bi += 4) {  // staged: a wave per group, all components
-            const uint32_t li = s_big[bi];
-            const uint32_t g = s_excl + li;
-            const uint32_t s = s_start[li], e = s_start[li + 1];
-            const uint32_t g0 = s_off[s - t0] - W0, g1 = s_off[e - t0] - W0;
-            const float sum = wave_group_sum(s_pts + g0, g1 - g0, s_wsoa[WAVE ? wid : 0]);
-            if ((lane & 15) == 0) {
-                const uint32_t c = (uint32_t)lane >> 4;
-                out[4 * (size_t)g + c] = c < 3 ? sum / (float)(g1 - g0) : sum;
+            __syncthreads();
+            if (total == 0) continue;  // block-uniform
+            uint32_t qlocal = 0xFFFFFFFFu;  // this thread's group in the tile's queue appends
+            if (threadIdx.x < total && average && !inblock) qlocal = atomicAdd(&s_nq, 1u);
+            __syncthreads();
+            if (threadIdx.x == 0 && s_nq) s_qbase = atomicAdd(qctr, s_nq);  // one append per tile
+            __syncthreads();
+            if (threadIdx.x < total) {
+                const uint32_t g = s_excl + threadIdx.x;
+                const uint32_t s = s_start[threadIdx.x], e = s_start[threadIdx.x + 1];
+                float* o = out + 4 * (size_t)g;
+                if (marks) {
+                    const uint32_t k = keys[s] & kmask;
+                    atomicOr(marks + (k >> 5), 1u << (k & 31u));
+                }
+                if (fvox) {
+                    const uint32_t fc = keys[s] >> fshift;
+                    const uint32_t f0 = s == 0 ? 0u : (keys[s - 1] >> fshift) + 1u;
+                    for (uint32_t f = f0; f <= fc; ++f) fvox[f] = g;
+                }
+                const uint32_t g0 = s_off[s - t0] - W0;  // staged positions of the group
+                const uint32_t g1 = e <= rend ? s_off[e - t0] - W0 : 0xFFFFFFFFu;
+                if (!average) {
+                    float c[4];
+                    group_corner(keys[s] & kmask, vp, c);
+                    *reinterpret_cast<float4*>(o) = make_float4(c[0], c[1], c[2], c[3]);
+                } else if (qlocal != 0xFFFFFFFFu) {  // past the staged points: k_group_runs_big
+                    const uint32_t slot = s_qbase + qlocal;
+                    if (slot < bigq_cap) bigq[slot] = make_uint4(g, s, e, 0u);
+                    else atomicOr(err, 8u);
+                } else if (g1 - g0 <= small_max) {
+                    const float4 a = thread_group_sum(s_pts + g0, g1 - g0);
+                    const float fc = (float)(g1 - g0);
+                    *reinterpret_cast<float4*>(o) = make_float4(a.x / fc, a.y / fc, a.z / fc, a.w);
+                } else {
+                    s_big[atomicAdd(&s_nbig, 1u)] = threadIdx.x;
+                }
+            }
+            __syncthreads();
+            const uint32_t nbig = WAVE ? s_nbig : 0u;
+            if (WAVE == 2) {  // staged long groups: 4 lanes each, lane = component
+                for (uint32_t bi = ((uint32_t)lane >> 2) * 4u + (uint32_t)wid; bi < nbig; bi += 64u) {
+                    const uint32_t li = s_big[bi];
+                    const uint32_t s = s_start[li], e = s_start[li + 1];
+                    const uint32_t g0 = s_off[s - t0] - W0, g1 = s_off[e - t0] - W0;
+                    const uint32_t c = (uint32_t)lane & 3u;
+                    const float acc = lane_comp_chain(reinterpret_cast<const float*>(s_pts + g0) + c, g1 - g0);
+                    out[4 * (size_t)(s_excl + li) + c] = c < 3 ? acc / (float)(g1 - g0) : acc;
+                }
+            }
+            for (uint32_t bi = wid; WAVE == 1 && bi < nbig; bi += 4) {  // staged: a wave per group
+                const uint32_t li = s_big[bi];
+                const uint32_t g = s_excl + li;
+                const uint32_t s = s_start[li], e = s_start[li + 1];
+                const uint32_t g0 = s_off[s - t0] - W0, g1 = s_off[e - t0] - W0;
+                const float sum = wave_group_sum(s_pts + g0, g1 - g0, s_wsoa[WAVE == 1 ? wid : 0]);
+                if ((lane & 15) == 0) {
+                    const uint32_t c = (uint32_t)lane >> 4;
+                    out[4 * (size_t)g + c] = c < 3 ? sum / (float)(g1 - g0) : sum;
+                }
             }
         }
         __syncthreads();  // LDS reused by the next tile
@@ -3399,8 +3545,9 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
     if (runs) {  // groups of sorted runs; the long ones by k_group_runs_big
         const uint32_t gb = std::max<uint32_t>(group_tiles, 1u);
         uint32_t* qctr = reinterpret_cast<uint32_t*>(a.ctrs + kCtrRunQueue);
-        auto kg = g_run_wave ? (g_run_stage >= 2048 ? k_group_runs<2048, true> : k_group_runs<512, true>)
-                             : (g_run_stage >= 2048 ? k_group_runs<2048, false> : k_group_runs<512, false>);
+        auto kg = g_run_wave == 1 ? (g_run_stage >= 2048 ? k_group_runs<2048, 1> : k_group_runs<512, 1>)
+                : g_run_wave == 2 ? (g_run_stage >= 2048 ? k_group_runs<2048, 2> : k_group_runs<512, 2>)
+                                  : (g_run_stage >= 2048 ? k_group_runs<2048, 0> : k_group_runs<512, 0>);
         hipLaunchKernelGGL(kg, dim3(gb), dim3(kGroupThreads), 0, s, kin, vin, gcount,
                            a.run_start, a.pts, reinterpret_cast<float*>(a.out), a.out_count,
                            a.gstatus, a.ggstatus, reinterpret_cast<uint32_t*>(a.ctrs + kCtrGroup),

@@ -347,6 +347,35 @@ __device__ __forceinline__ RowInfo row_info(const float* __restrict__ src, int v
     return ri;
 }
 
+// s + the first min(m, 64) values of a staged row by the chain itself: every lane reads the whole
+// row (LDS broadcast reads, 16-byte aligned) into its registers and runs the same 64 dependent f32
+// adds (s stays wave-uniform; no readlane round trip per value); values past m add -0.0, which
+// leaves any s as it is.
+__device__ __forceinline__ float lds_row_chain(const float* __restrict__ row, uint32_t m, float s) {
+    const float4* rp = reinterpret_cast<const float4*>(row);
+    float4 v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = rp[k];
+    if (m < 64u) {  // (wave-uniform: a group's last, partial row)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t i = 4u * k;
+            v[k].x = i < m ? v[k].x : -0.0f;
+            v[k].y = i + 1u < m ? v[k].y : -0.0f;
+            v[k].z = i + 2u < m ? v[k].z : -0.0f;
+            v[k].w = i + 3u < m ? v[k].w : -0.0f;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        s = s + v[k].x;
+        s = s + v[k].y;
+        s = s + v[k].z;
+        s = s + v[k].w;
+    }
+    return s;
+}
+
 // s + the n <= 1024 values of one component staged as rows (row q at comp + q kRowStride).
 __device__ __forceinline__ float rows_chunk_sum(const float* __restrict__ comp, uint32_t n, float s) {
     constexpr int A = 8388609, B = 16777215;
@@ -355,7 +384,6 @@ __device__ __forceinline__ float rows_chunk_sum(const float* __restrict__ comp, 
     const RowInfo ri = row_info<false>(comp + r * kRowStride + h * 16u,
                                        (int)n - (int)(r * 64u + h * 16u), n < 64u * 16u, s);
     // 3. the rows from the exact s
-    auto get = [&](uint32_t i) { return comp[(i >> 6) * kRowStride + (i & 63u)]; };
     uint32_t cur = 0;
 #pragma unroll 1
     while (cur < nrows) {  // wave-uniform
@@ -377,7 +405,7 @@ __device__ __forceinline__ float rows_chunk_sum(const float* __restrict__ comp, 
         }
         if (f >= nrows) break;
         GDF_VOXSUM_PROBE(3);
-        s = uniform_f(serial_row(get, 64u * f, n, s));
+        s = lds_row_chain(comp + f * kRowStride, n - 64u * f, s);
         cur = f + 1u;
     }
     return s;
