@@ -1647,6 +1647,8 @@ int gdf_create(int device, gdf_engine** out) {
             g_run_big_blocks = (uint32_t)std::max(1, std::atoi(v));
         if (const char* v = std::getenv("GDF_RUN_INBLOCK"))  // tuning knob
             g_run_inblock = (uint32_t)std::max(0, std::atoi(v));
+        if (const char* v = std::getenv("GDF_POINTS_LANE"))  // tuning knob
+            g_points_lane = (uint32_t)std::atoi(v);
         if (const char* v = std::getenv("GDF_RUN_WAVE"))  // tuning knob
             g_run_wave = (uint32_t)std::atoi(v);
         if (const char* v = std::getenv("GDF_SMALL_GROUP"))  // tuning knob

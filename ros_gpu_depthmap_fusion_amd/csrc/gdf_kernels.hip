@@ -2496,6 +2496,7 @@ uint32_t g_group_scan_tiles = 1024;
 // longer ones by a wave (gdf_voxsum.hpp's stretch sums: a wave per group, serial over a block's
 // groups).  Tuning knob GDF_SMALL_GROUP.
 uint32_t g_small_group = 32;
+uint32_t g_points_lane = 1;  // k_group: staged long groups by 4-lane chains (GDF_POINTS_LANE)
 
 // p[0] + ... + p[n-1] per component, in order, by one thread: blocks of 4 points alternate between
 // two register sets, the next block read while the current one is added (LDS latency off the
@@ -2542,6 +2543,42 @@ __device__ __forceinline__ float4 thread_group_sum(const float4* p, uint32_t n) 
 constexpr uint32_t kChainPad = 16;  // LDS padding of staged point buffers
 constexpr uint32_t kExtraRuns = 64;  // runs past a k_group_runs tile read for its last group
 constexpr uint32_t kRunPasses = 4;   // staging windows per k_group_runs tile (mode 2)
+
+// comp[0] + comp[4] + ... + comp[4 (n - 1)] in order: one component of a staged group by one lane
+// (its 4 lanes hold the group's 4 components); blocks of 8 values alternate between two register
+// sets so the LDS reads of the next block overlap the additions of the current one.
+__device__ __forceinline__ float lane_comp_chain(const float* comp, uint32_t n) {
+    float acc = 0.0f;
+    uint32_t k = 0;
+    if (n >= 16) {
+        float a[8], b[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) a[q] = comp[4 * q];
+#pragma unroll 1
+        for (; k + 16 <= n; k += 16) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) b[q] = comp[4 * (k + 8 + q)];
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc = acc + a[q];
+            const uint32_t kn = k + 16 + 8 <= n ? k + 16 : k;  // (in range; unused past the loop)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) a[q] = comp[4 * (kn + q)];
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc = acc + b[q];
+        }
+        if (k + 8 <= n) {  // a[] holds values k .. k+7 exactly when k + 8 <= n here
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc = acc + a[q];
+            k += 8;
+        }
+    }
+    for (; k < n; ++k) acc = acc + comp[4 * k];
+    return acc;
+}
 
 // Voxel sums, one component per wave (gdf_voxsum.hpp): wave c of a 4-wave group sums component c.
 // A staged group of cnt points (float4 AoS in LDS)
@@ -2596,7 +2633,7 @@ __global__ __launch_bounds__(kGroupThreads) __attribute__((amdgpu_waves_per_eu(7
     uint32_t* tile_ctr, uint32_t* epoch_word, uint32_t* err, uint32_t* hist, int average,
     VoxelParams vp, uint32_t* marks, const uint32_t* tile_base, uint4* __restrict__ bigq,
     uint32_t* __restrict__ bigcnt, uint32_t bigcap, uint32_t nframes, uint32_t fshift,
-    uint32_t* __restrict__ fvox, uint32_t small_max) {
+    uint32_t* __restrict__ fvox, uint32_t small_max, uint32_t lane_chains) {
     __shared__ uint32_t s_wave[4];
     __shared__ uint32_t s_tile, s_epoch, s_excl, s_nbig, s_nq;
     __shared__ uint32_t s_start[kGroupThreads + 1];
@@ -2741,13 +2778,23 @@ __global__ __launch_bounds__(kGroupThreads) __attribute__((amdgpu_waves_per_eu(7
     }
     __syncthreads();
     const uint32_t nbig = s_nbig;
-    for (uint32_t b = 0; b < nbig; ++b) {  // every group by the 4 waves, wave = component
+    // staged long groups: 4 lanes each, one component chain per lane (16 groups per wave), or
+    // (lane_chains = 0) the 4 waves' stretch sums, wave = component
+    for (uint32_t b = ((uint32_t)lane >> 2) * 4u + (uint32_t)wid; lane_chains && b < nbig; b += 64u) {
         const uint32_t li = s_big[b];
-        const uint32_t g = s_excl + li;
         const uint32_t s = s_start[li], e = s_start[li + 1];
-        const float sum = e - S0 <= staged ? lds_group_comp(s_pts + (s - S0), wid, e - s)  // staged
+        if (e - S0 > staged) continue;
+        const uint32_t c = (uint32_t)lane & 3u;
+        const float acc = lane_comp_chain(reinterpret_cast<const float*>(s_pts + (s - S0)) + c, e - s);
+        out[4 * (size_t)(s_excl + li) + c] = c < 3 ? acc / (float)(e - s) : acc;
+    }
+    for (uint32_t b = 0; b < nbig; ++b) {  // groups past the staged points: the 4 waves, wave = component
+        const uint32_t li = s_big[b];
+        const uint32_t s = s_start[li], e = s_start[li + 1];
+        if (lane_chains && e - S0 <= staged) continue;  // (block-uniform)
+        const float sum = e - S0 <= staged ? lds_group_comp(s_pts + (s - S0), wid, e - s)
                                            : gather_group_comp(vals, pts, wid, s, e);
-        store_comp_mean(out + 4 * (size_t)g, wid, sum, e - s);
+        store_comp_mean(out + 4 * (size_t)(s_excl + li), wid, sum, e - s);
     }
     __syncthreads();  // LDS reused by the next tile
     }
@@ -2781,46 +2828,11 @@ __global__ __launch_bounds__(256) void k_group_big(const uint32_t* __restrict__ 
 // which a staged group is summed in-block (larger ones are queued); tuning knobs GDF_RUN_STAGE,
 // GDF_RUN_INBLOCK
 uint32_t g_run_stage = 2048;
-uint32_t g_run_inblock = 2048;
+uint32_t g_run_inblock = 1024;  // (measured: C2 / 720p x4 / 4K best or within noise of best at 1024)
 // staged groups above g_small_group in k_group_runs (GDF_RUN_WAVE): 0 queued for k_group_runs_big,
 // 1 a wave's stretch sums (wave_group_sum), 2 four lanes' chains (lane_comp_chain, default)
 uint32_t g_run_wave = 2;
 
-// comp[0] + comp[4] + ... + comp[4 (n - 1)] in order: one component of a staged group by one lane
-// (its 4 lanes hold the group's 4 components); blocks of 8 values alternate between two register
-// sets so the LDS reads of the next block overlap the additions of the current one.
-__device__ __forceinline__ float lane_comp_chain(const float* comp, uint32_t n) {
-    float acc = 0.0f;
-    uint32_t k = 0;
-    if (n >= 16) {
-        float a[8], b[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) a[q] = comp[4 * q];
-#pragma unroll 1
-        for (; k + 16 <= n; k += 16) {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) b[q] = comp[4 * (k + 8 + q)];
-            asm volatile("" ::: "memory");
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int q = 0; q < 8; ++q) acc = acc + a[q];
-            const uint32_t kn = k + 16 + 8 <= n ? k + 16 : k;  // (in range; unused past the loop)
-#pragma unroll
-            for (int q = 0; q < 8; ++q) a[q] = comp[4 * (kn + q)];
-            asm volatile("" ::: "memory");
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int q = 0; q < 8; ++q) acc = acc + b[q];
-        }
-        if (k + 8 <= n) {  // a[] holds values k .. k+7 exactly when k + 8 <= n here
-#pragma unroll
-            for (int q = 0; q < 8; ++q) acc = acc + a[q];
-            k += 8;
-        }
-    }
-    for (; k < n; ++k) acc = acc + comp[4 * k];
-    return acc;
-}
 uint32_t g_run_big_blocks = 1024;  // k_group_runs_big grid (tuning knob GDF_RUN_BIG_BLOCKS)
 // chunks of k_group_runs_big (one 4-wave block per queued group): 1 K points (Q = 16) or 512
 // (Q = 8); 0 never 1 K, 1 always, 2 (default) for single depth-only frames, whose long voxels
@@ -3385,9 +3397,8 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
     }
 }
 
-// The groups queued by k_group_runs: block b of the grid takes queue slot b, then draws further
-// slots (qctr[1]) while any remain - no draw at all when the queue fits the grid - and streams the
-// runs of each (records rps / rlen by sorted run, written by k_group_runs) from global memory
+// The groups queued by k_group_runs: every block draws queue slots from a counter (qctr[1]) while
+// any remain and streams the runs of each (records rps / rlen by sorted run, written by k_group_runs) from global memory
 // (block_stream_sum).  The queue was complete when this launch began; the first sort pass of the
 // next voxelize zeroes the counters.
 template <int Q>
@@ -3403,10 +3414,16 @@ __global__ __launch_bounds__(256) void k_group_runs_big(const uint32_t* __restri
     __shared__ uint32_t s_t;
     const uint32_t wid = threadIdx.x >> 6;  // (the component)
     const uint32_t nq = min(__hip_atomic_load(qctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), bigq_cap);
-    uint32_t t = blockIdx.x;
-    // one queue slot per draw: queued groups range over 10^3x in length (C3: up to 139 K points),
-    // and draws of 8 consecutive slots (neighbouring keys, similar lengths) measured 1.7 -> 2.8 ms
-    // of tail imbalance on the C3 window
+    // every slot is drawn from the counter, the first one too: a block that is not resident yet
+    // (the grid exceeds what fits on the chip) must not hold a slot - with slot b fixed to block b,
+    // the C3 window's 100 K-point groups in slots ~800-1000 started only when the rest of the
+    // queue was drained (1.0 ms into a 1.7 ms kernel, tools/group_trace.py --c3).  One slot per
+    // draw: queued groups range over 10^3x in length (C3: up to 139 K points), and draws of 8
+    // consecutive slots measured 1.7 -> 2.8 ms of tail imbalance on the C3 window.
+    if (threadIdx.x == 0) s_t = atomicAdd(qctr + 1, 1u);
+    __syncthreads();
+    uint32_t t = s_t;
+    __syncthreads();
     while (t < nq) {  // block-uniform
         const uint4 q = bigq[t];
         uint32_t np = 0;
@@ -3433,13 +3450,10 @@ __global__ __launch_bounds__(256) void k_group_runs_big(const uint32_t* __restri
                                                    nullptr);
 #endif
         store_comp_mean(out + 4 * (size_t)q.x, wid, sum, np);
-        if (nq <= gridDim.x) break;
         if (threadIdx.x == 0) s_t = atomicAdd(qctr + 1, 1u);
         __syncthreads();
-        const uint32_t d = s_t;
+        t = s_t;
         __syncthreads();
-        if (d >= nq - gridDim.x) break;
-        t = gridDim.x + d;
     }
 }
 
@@ -3577,7 +3591,7 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
                        reinterpret_cast<uint32_t*>(a.ctrs + kCtrEpoch), a.err, a.hist, a.average,
                        a.vp, a.group_marks, tile_base, tile_base ? a.bigq : nullptr,
                        a.bigcnt, bigcap, a.nframes, a.frame_shift, a.frame_vox_start,
-                       g_small_group);
+                       g_small_group, g_points_lane);
     if (tile_base && a.bigq && a.average) {
         if ((e = hipGetLastError()) != hipSuccess) return e;
         hipLaunchKernelGGL(k_group_big, dim3(2048), dim3(256), 0, s, vin, a.pts,

@@ -2,6 +2,7 @@
 libgdf_trace.so (built here by `python tools/group_trace.py --build`, run on the GPU box):
 
     python tools/group_trace.py W H F [dense|stress] [frames_per_batch]
+    python tools/group_trace.py --c3 WINDOW      (720p depth + a WINDOW-sequence rollbuffer)
 
 prints the kernel's span, the longest groups (points, chunks, cycles at barriers / LDS stores /
 fetch issue / sums) and how the groups' start times spread."""
@@ -19,17 +20,48 @@ import frame_driver  # noqa: E402
 SLOTS = 1 << 16
 
 
+def make_c3(window):
+    """bench_c3's frames (720p depth + rollbuffer of `window` 720p sequences) on the trace build."""
+    from ros_gpu_depthmap_fusion_amd import hiprt, synth
+    from ros_gpu_depthmap_fusion_amd.gdf import ComponentParams, GPUDepthmapFusion
+    W, H = 1280, 720
+    cam, lidar = synth.make_camera(0, W, H), synth.make_camera(1, W, H)
+    depth = [hiprt.DeviceArray.from_numpy(synth.dense_frame(cam, 0, f)) for f in range(2)]
+    seqs = []
+    for f in range(2):
+        xyz = synth.back_project(lidar, synth.dense_frame(lidar, 1, f))
+        seqs.append(hiprt.DeviceArray.from_numpy(
+            np.ascontiguousarray(np.concatenate([xyz, np.ones((len(xyz), 1), np.float32)], 1))))
+    p = ComponentParams()
+    p.ps_timespan = (window - 0.5) / 30.0
+    pc = p.to_c(lidar.T_world, lidar.T_crop, False, False)
+    eng = GPUDepthmapFusion(0, lib_path=TRACE_LIB_PATH)
+
+    def step(k, batch=1):
+        s_, ns = synth.sequence_time(k)
+        eng.addPointSequenceDevice(seqs[k % 2].ptr, W * H, 16, s_, ns, synth.move_transform(k))
+        eng.clear()
+        eng.addDepthmapDevice(depth[k % 2].ptr, W, H, *cam.intrinsics(), cam.T_world, cam.T_crop)
+        eng.processFramePrepared(pc)
+    return eng, step
+
+
 def main():
     if sys.argv[1] == "--build":
         print(build_library(trace=True))
         return
-    W, H, F = (int(x) for x in sys.argv[1:4])
-    workload = sys.argv[4] if len(sys.argv) > 4 else "dense"
-    batch = int(sys.argv[5]) if len(sys.argv) > 5 else 1
-    eng, step = frame_driver.make(W, H, F, 0, workload, TRACE_LIB_PATH)
+    if sys.argv[1] == "--c3":
+        eng, step = make_c3(int(sys.argv[2]))
+        nsteps, batch = int(sys.argv[2]) + 2, 1
+    else:
+        W, H, F = (int(x) for x in sys.argv[1:4])
+        workload = sys.argv[4] if len(sys.argv) > 4 else "dense"
+        batch = int(sys.argv[5]) if len(sys.argv) > 5 else 1
+        eng, step = frame_driver.make(W, H, F, 0, workload, TRACE_LIB_PATH)
+        nsteps = 4
     lib = eng._lib
-    for i in range(4):
-        if i == 3:
+    for i in range(nsteps):
+        if i == nsteps - 1:
             eng.synchronize()
             assert lib.gdf_debug_group_trace_clear() == 0
         step(i, batch)
