@@ -2496,7 +2496,8 @@ uint32_t g_group_scan_tiles = 1024;
 // longer ones by a wave (gdf_voxsum.hpp's stretch sums: a wave per group, serial over a block's
 // groups).  Tuning knob GDF_SMALL_GROUP.
 uint32_t g_small_group = 32;
-uint32_t g_points_lane = 1;  // k_group: staged long groups by 4-lane chains (GDF_POINTS_LANE)
+uint32_t g_points_lane = 0;  // k_group: staged long groups by 4-lane chains (GDF_POINTS_LANE; measured
+                             // slower on single VGA / 720p frames: 5.7 / 9.9 vs 6.1 / 11.6 Gpoints/s)
 
 // p[0] + ... + p[n-1] per component, in order, by one thread: blocks of 4 points alternate between
 // two register sets, the next block read while the current one is added (LDS latency off the
@@ -2541,14 +2542,14 @@ __device__ __forceinline__ float4 thread_group_sum(const float4* p, uint32_t n) 
 }
 
 constexpr uint32_t kChainPad = 16;  // LDS padding of staged point buffers
+constexpr uint32_t kGatherChunk = 256;  // points per gathered chunk of a k_group wave
 constexpr uint32_t kExtraRuns = 64;  // runs past a k_group_runs tile read for its last group
 constexpr uint32_t kRunPasses = 4;   // staging windows per k_group_runs tile (mode 2)
 
 // comp[0] + comp[4] + ... + comp[4 (n - 1)] in order: one component of a staged group by one lane
 // (its 4 lanes hold the group's 4 components); blocks of 8 values alternate between two register
 // sets so the LDS reads of the next block overlap the additions of the current one.
-__device__ __forceinline__ float lane_comp_chain(const float* comp, uint32_t n) {
-    float acc = 0.0f;
+__device__ __forceinline__ float lane_comp_chain_from(const float* comp, uint32_t n, float acc) {
     uint32_t k = 0;
     if (n >= 16) {
         float a[8], b[8];
@@ -2578,6 +2579,16 @@ __device__ __forceinline__ float lane_comp_chain(const float* comp, uint32_t n) 
     }
     for (; k < n; ++k) acc = acc + comp[4 * k];
     return acc;
+}
+__device__ __forceinline__ float lane_comp_chain(const float* comp, uint32_t n) {
+    return lane_comp_chain_from(comp, n, 0.0f);
+}
+
+// (the wave's LDS writes visible to its own lanes)
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // Voxel sums, one component per wave (gdf_voxsum.hpp): wave c of a 4-wave group sums component c.
@@ -2639,6 +2650,7 @@ __global__ __launch_bounds__(kGroupThreads) __attribute__((amdgpu_waves_per_eu(7
     __shared__ uint32_t s_start[kGroupThreads + 1];
     __shared__ uint32_t s_big[kGroupThreads];
     __shared__ float4 s_pts[kStagePts + kChainPad];
+    __shared__ float4 s_gbuf[4][kGatherChunk];  // per-wave chunks of gathered groups
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t n = *count;
     const uint32_t ntiles = (n + kGroupThreads - 1) / kGroupThreads;
@@ -2788,13 +2800,44 @@ __global__ __launch_bounds__(kGroupThreads) __attribute__((amdgpu_waves_per_eu(7
         const float acc = lane_comp_chain(reinterpret_cast<const float*>(s_pts + (s - S0)) + c, e - s);
         out[4 * (size_t)(s_excl + li) + c] = c < 3 ? acc / (float)(e - s) : acc;
     }
-    for (uint32_t b = 0; b < nbig; ++b) {  // groups past the staged points: the 4 waves, wave = component
+    for (uint32_t b = 0; !lane_chains && b < nbig; ++b) {  // staged: the 4 waves, wave = component
         const uint32_t li = s_big[b];
         const uint32_t s = s_start[li], e = s_start[li + 1];
-        if (lane_chains && e - S0 <= staged) continue;  // (block-uniform)
-        const float sum = e - S0 <= staged ? lds_group_comp(s_pts + (s - S0), wid, e - s)
-                                           : gather_group_comp(vals, pts, wid, s, e);
-        store_comp_mean(out + 4 * (size_t)(s_excl + li), wid, sum, e - s);
+        if (e - S0 > staged) continue;  // (block-uniform)
+        store_comp_mean(out + 4 * (size_t)(s_excl + li), wid,
+                        lds_group_comp(s_pts + (s - S0), wid, e - s), e - s);
+    }
+    // groups past the staged points (small frames: no queue): a wave per group, chunks of
+    // kGatherChunk points gathered through vals into the wave's LDS buffer - the next chunk's
+    // loads in flight while lanes 0..3 chain the current one, one component each
+    for (uint32_t b = wid; b < nbig; b += 4u) {
+        const uint32_t li = s_big[b];
+        const uint32_t s = s_start[li], e = s_start[li + 1];
+        if (e - S0 <= staged) continue;  // (wave-uniform)
+        float4 r[kGatherChunk / 64];
+#pragma unroll
+        for (int q = 0; q < (int)kGatherChunk / 64; ++q) {
+            const uint32_t k = s + q * 64u + (uint32_t)lane;
+            r[q] = k < e ? pts[vals[k]] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        float acc = 0.0f;
+#pragma unroll 1
+        for (uint32_t c = s; c < e; c += kGatherChunk) {
+#pragma unroll
+            for (int q = 0; q < (int)kGatherChunk / 64; ++q) s_gbuf[wid][q * 64 + lane] = r[q];
+            const uint32_t cn = c + kGatherChunk;
+#pragma unroll
+            for (int q = 0; q < (int)kGatherChunk / 64; ++q) {
+                const uint32_t k = cn + q * 64u + (uint32_t)lane;
+                r[q] = k < e ? pts[vals[k]] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+            wave_sync();
+            if (lane < 4)
+                acc = lane_comp_chain_from(reinterpret_cast<const float*>(&s_gbuf[wid][0]) + lane,
+                                           min(e - c, kGatherChunk), acc);
+            wave_sync();
+        }
+        if (lane < 4) out[4 * (size_t)(s_excl + li) + lane] = lane < 3 ? acc / (float)(e - s) : acc;
     }
     __syncthreads();  // LDS reused by the next tile
     }
@@ -2839,11 +2882,6 @@ uint32_t g_run_big_blocks = 1024;  // k_group_runs_big grid (tuning knob GDF_RUN
 // reach ~20 K points at 4K (tuning knob GDF_RUN_Q16)
 uint32_t g_run_q16 = 2;
 
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // Wave64 inclusive sum scan on DPP (gdf_voxsum.hpp dpp_iscan).
 __device__ __forceinline__ uint32_t dpp_sum_scan(uint32_t x) { return (uint32_t)dpp_iscan((int)x); }
@@ -3001,6 +3039,7 @@ __device__ __forceinline__ float block_stream_sum(const uint32_t* __restrict__ r
     const uint32_t wid = threadIdx.x >> 6;
     npts = 0;
     float s = 0.0f;
+    ChainMode cm;
     RunBatch cur = run_batch(run_recs(rps, rlen, rs, re));
     RunRecs rec1 = run_recs(rps, rlen, rs + NB, re);      // batch 1
     RunRecs rec2 = run_recs(rps, rlen, rs + 2u * NB, re);  // batch 2
@@ -3045,7 +3084,7 @@ __device__ __forceinline__ float block_stream_sum(const uint32_t* __restrict__ r
         }
         if (more || next_batch) fetch_rows4<Q>(fb, cn, s_mark, s_base, pts, p);
         GDF_TCLK(b4);
-        s = rows_chunk_sum(s_soa[wid], n, s);
+        s = rows_chunk_sum(s_soa[wid], n, s, cm);
         GDF_TCLK(b5);
 #ifdef GDF_TRACE_GROUPS
         if (tr) {

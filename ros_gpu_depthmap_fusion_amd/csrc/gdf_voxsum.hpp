@@ -376,8 +376,58 @@ __device__ __forceinline__ float lds_row_chain(const float* __restrict__ row, ui
     return s;
 }
 
-// s + the n <= 1024 values of one component staged as rows (row q at comp + q kRowStride).
-__device__ __forceinline__ float rows_chunk_sum(const float* __restrict__ comp, uint32_t n, float s) {
+// s + the n <= 1024 staged values by the chain alone (every lane the same adds, wave-uniform s):
+// half rows of 32 values alternate between two register sets, the next one read from LDS while
+// the current one is added; values past n add -0.0.
+__device__ __forceinline__ float rows_chain_all(const float* __restrict__ comp, uint32_t n, float s) {
+    const uint32_t nh = (n + 31u) >> 5;  // half rows
+    auto load = [&](uint32_t h, float4 (&v)[8]) {
+        const float4* rp = reinterpret_cast<const float4*>(comp + (h >> 1) * kRowStride + (h & 1u) * 32u);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = rp[k];
+    };
+    auto add = [&](uint32_t h, float4 (&v)[8]) {
+        const uint32_t m = n - 32u * h;  // values of this half row (>= 1)
+        if (m < 32u) {  // (wave-uniform: the chunk's last, partial half row)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t i = 4u * k;
+                v[k].x = i < m ? v[k].x : -0.0f;
+                v[k].y = i + 1u < m ? v[k].y : -0.0f;
+                v[k].z = i + 2u < m ? v[k].z : -0.0f;
+                v[k].w = i + 3u < m ? v[k].w : -0.0f;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            s = s + v[k].x;
+            s = s + v[k].y;
+            s = s + v[k].z;
+            s = s + v[k].w;
+        }
+        asm volatile("" : "+v"(s));
+    };
+    float4 a[8], b[8];
+    load(0, a);
+    uint32_t h = 0;
+#pragma unroll 1
+    for (; h + 2 <= nh; h += 2) {
+        load(h + 1, b);
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        add(h, a);
+        if (h + 2 < nh) load(h + 2, a);
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        add(h + 1, b);
+    }
+    if (h < nh) add(h, a);
+    return s;
+}
+
+// The stretch form; nchain counts the rows run by the chain.
+__device__ __forceinline__ float rows_chunk_sum_stretch(const float* __restrict__ comp, uint32_t n,
+                                                       float s, uint32_t& nchain) {
     constexpr int A = 8388609, B = 16777215;
     const uint32_t lane = threadIdx.x & 63, r = lane >> 2, h = lane & 3;
     const uint32_t nrows = (n + 63u) >> 6;
@@ -406,7 +456,36 @@ __device__ __forceinline__ float rows_chunk_sum(const float* __restrict__ comp, 
         if (f >= nrows) break;
         GDF_VOXSUM_PROBE(3);
         s = lds_row_chain(comp + f * kRowStride, n - 64u * f, s);
+        ++nchain;
         cur = f + 1u;
+    }
+    return s;
+}
+
+// Per component wave, across the chunks of a group: chunks to run by the chain alone (low byte)
+// and the backoff level (next byte).  A stretch chunk that ran at least half of its rows (>= 4)
+// as chain rows - a sum walking around zero, the C3 window's z - makes the next 2, 4, ... 16
+// chunks plain chains (~4 cycles per value instead of a row attempt per row); a stretch chunk
+// with fewer chain rows resets the backoff.  Either way the sum is the sequential chain's.
+struct ChainMode {
+    uint32_t left = 0, level = 0;
+};
+
+// s + the n <= 1024 values of one component staged as rows (row q at comp + q kRowStride).
+__device__ __forceinline__ float rows_chunk_sum(const float* __restrict__ comp, uint32_t n, float s,
+                                               ChainMode& cm) {
+    if (cm.left) {  // (wave-uniform)
+        --cm.left;
+        return rows_chain_all(comp, n, s);
+    }
+    uint32_t nchain = 0;
+    s = rows_chunk_sum_stretch(comp, n, s, nchain);
+    const uint32_t nrows = (n + 63u) >> 6;
+    if (nrows >= 4u && 2u * nchain >= nrows) {
+        cm.left = 2u << min(cm.level, 3u);
+        cm.level = min(cm.level + 1u, 3u);
+    } else {
+        cm.level = 0;
     }
     return s;
 }

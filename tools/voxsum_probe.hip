@@ -63,6 +63,7 @@ __global__ __launch_bounds__(256) void k_rows(const float4* __restrict__ pts, ui
     __shared__ __attribute__((aligned(16))) float s_soa[4][16 * gdf::kRowStride];
     const uint32_t w = threadIdx.x >> 6;
     float s = 0.0f;
+    gdf::ChainMode cm;
     unsigned long long t = 0;
     for (uint32_t c = 0; c < n; c += 1024) {
         __syncthreads();
@@ -76,7 +77,7 @@ __global__ __launch_bounds__(256) void k_rows(const float4* __restrict__ pts, ui
         }
         __syncthreads();
         const unsigned long long t0 = clock64();
-        s = gdf::rows_chunk_sum(s_soa[w], min(1024u, n - c), s);
+        s = gdf::rows_chunk_sum(s_soa[w], min(1024u, n - c), s, cm);
         t += clock64() - t0;
     }
     if ((threadIdx.x & 63) == 0) {
