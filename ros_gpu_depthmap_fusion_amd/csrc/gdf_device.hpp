@@ -56,8 +56,9 @@ constexpr uint32_t kMaxParts = 16;                          // ranks of the fuse
 // base, so no per-launch memset) and the global digit histogram of the voxel keys.
 // per-stream device counters (u64 words, low 32 bits used): tile tickets, look-back epoch
 enum CounterSlot { kCtrSel = 0, kCtrSort0 = 1, kCtrGroup = 5, kCtrEpoch = 6,
-                   kCtrRunQueue = 7,  // run-group queue: appends, draws (two u32)
-                   kCtrSlots = 8 };
+                   kCtrRunQueue = 7,  // run-group queue: appends, draws, huge appends (u32 each,
+                                      // over words 7 and 8)
+                   kCtrSlots = 9 };
 
 // engine-order of historic-grid updates across streams (grid_seq_enter / grid_seq_leave)
 struct GridSeq {

@@ -2371,6 +2371,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
     if (qreset && blockIdx.x == 0 && threadIdx.x == 0) {
         qreset[0] = 0u;
         qreset[1] = 0u;
+        qreset[2] = 0u;
     }
     if (blockIdx.x >= grid_block0) {  // fused historic-grid update (first pass only)
         const uint32_t f = grid_seq_enter(q);
@@ -2545,6 +2546,7 @@ constexpr uint32_t kChainPad = 16;  // LDS padding of staged point buffers
 constexpr uint32_t kGatherChunk = 256;  // points per gathered chunk of a k_group wave
 constexpr uint32_t kExtraRuns = 64;  // runs past a k_group_runs tile read for its last group
 constexpr uint32_t kRunPasses = 4;   // staging windows per k_group_runs tile (mode 2)
+constexpr uint32_t kHugeGroup = 8192;  // queued groups drawn first by k_group_runs_big (points)
 
 // comp[0] + comp[4] + ... + comp[4 (n - 1)] in order: one component of a staged group by one lane
 // (its 4 lanes hold the group's 4 components); blocks of 8 values alternate between two register
@@ -3136,6 +3138,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
     uint32_t small_max) {
     __shared__ uint32_t s_wave[4];
     __shared__ uint32_t s_tile, s_epoch, s_excl, s_nbig, s_nq, s_qbase, s_wend, s_nx, s_nbase;
+    __shared__ uint32_t s_nh, s_hbase;
     __shared__ uint32_t s_start[kGroupThreads + 1];  // group starts (run index); [total] = end
     // the tile's runs, then up to kExtraRuns runs of the next tiles (the rest of the tile's last
     // group): first points and the exclusive scan of their lengths
@@ -3174,6 +3177,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
             s_wend = 0;
             s_nx = 0;
             s_nbase = 0xFFFFFFFFu;
+            s_nh = 0;
         }
         walk += gridDim.x;
         __syncthreads();
@@ -3322,10 +3326,19 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
             }
             __syncthreads();
             if (total == 0) continue;  // block-uniform
-            uint32_t qlocal = 0xFFFFFFFFu;
-            if (threadIdx.x < total && average && !done) qlocal = atomicAdd(&s_nq, 1u);
+            // queued groups: huge ones (>= kHugeGroup points, or continuing past the tile) into
+            // the region at the top of the queue that k_group_runs_big draws first (longest
+            // first bounds the tail: the C3 window's 10^5-point groups otherwise start late)
+            uint32_t qlocal = 0xFFFFFFFFu, hlocal = 0xFFFFFFFFu;
+            if (threadIdx.x < total && average && !done) {
+                const uint32_t e = s_start[threadIdx.x + 1];
+                const bool huge = e > rend || ge - gs >= kHugeGroup;
+                if (huge) hlocal = atomicAdd(&s_nh, 1u);
+                else qlocal = atomicAdd(&s_nq, 1u);
+            }
             __syncthreads();
             if (threadIdx.x == 0 && s_nq) s_qbase = atomicAdd(qctr, s_nq);  // one append per tile
+            if (threadIdx.x == 64 && s_nh) s_hbase = atomicAdd(qctr + 2, s_nh);
             __syncthreads();
             if (threadIdx.x < total) {
                 const uint32_t g = s_excl + threadIdx.x;
@@ -3346,6 +3359,10 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
                 } else if (qlocal != 0xFFFFFFFFu) {  // k_group_runs_big
                     const uint32_t slot = s_qbase + qlocal;
                     if (slot < bigq_cap) bigq[slot] = make_uint4(g, s, e, 0u);
+                    else atomicOr(err, 8u);
+                } else if (hlocal != 0xFFFFFFFFu) {  // from the top (the regions never meet: the
+                    const uint32_t h = s_hbase + hlocal;  // queue holds every group, bigq_cap >= groups)
+                    if (h < bigq_cap) bigq[bigq_cap - 1u - h] = make_uint4(g, s, e, 0u);
                     else atomicOr(err, 8u);
                 }
             }
@@ -3436,8 +3453,8 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
     }
 }
 
-// The groups queued by k_group_runs: every block draws queue slots from a counter (qctr[1]) while
-// any remain and streams the runs of each (records rps / rlen by sorted run, written by k_group_runs) from global memory
+// The groups queued by k_group_runs: block b of a resident-sized grid takes queue slot b, then
+// draws further slots (qctr[1]) while any remain and streams the runs of each (records rps / rlen by sorted run, written by k_group_runs) from global memory
 // (block_stream_sum).  The queue was complete when this launch began; the first sort pass of the
 // next voxelize zeroes the counters.
 template <int Q>
@@ -3452,19 +3469,22 @@ __global__ __launch_bounds__(256) void k_group_runs_big(const uint32_t* __restri
     __shared__ __attribute__((aligned(16))) float s_soa[4][kRowStride * Q];
     __shared__ uint32_t s_t;
     const uint32_t wid = threadIdx.x >> 6;  // (the component)
-    const uint32_t nq = min(__hip_atomic_load(qctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), bigq_cap);
-    // every slot is drawn from the counter, the first one too: a block that is not resident yet
-    // (the grid exceeds what fits on the chip) must not hold a slot - with slot b fixed to block b,
-    // the C3 window's 100 K-point groups in slots ~800-1000 started only when the rest of the
-    // queue was drained (1.0 ms into a 1.7 ms kernel, tools/group_trace.py --c3).  One slot per
-    // draw: queued groups range over 10^3x in length (C3: up to 139 K points), and draws of 8
-    // consecutive slots measured 1.7 -> 2.8 ms of tail imbalance on the C3 window.
-    if (threadIdx.x == 0) s_t = atomicAdd(qctr + 1, 1u);
-    __syncthreads();
-    uint32_t t = s_t;
-    __syncthreads();
+    // logical slot j: the huge region (appended from the top, drawn first), then the others
+    const uint32_t na = __hip_atomic_load(qctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t nh = __hip_atomic_load(qctr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t nq = min(na + nh, bigq_cap);
+    auto slot_of = [&](uint32_t j) { return j < nh ? bigq_cap - 1u - j : j - nh; };
+    // Block b takes slot b, then draws further slots from the counter.  The grid is sized to the
+    // blocks the chip holds at once (launch_voxelize): a block that is not resident yet must not
+    // hold a slot - with 1024 blocks, the C3 window's 100 K-point groups in slots ~800-1000
+    // started only when the rest of the queue was drained (1.0 ms into a 1.7 ms kernel,
+    // tools/group_trace.py --c3); drawing the first slot from the counter too serialised 10^3
+    // atomics at the start (4K: groups starting up to 13 us late, an empty queue 14 us).  One
+    // slot per draw: queued groups range over 10^3x in length (C3: up to 139 K points), and draws
+    // of 8 consecutive slots measured 1.7 -> 2.8 ms of tail imbalance on the C3 window.
+    uint32_t t = blockIdx.x;
     while (t < nq) {  // block-uniform
-        const uint4 q = bigq[t];
+        const uint4 q = bigq[slot_of(t)];
         uint32_t np = 0;
 #ifdef GDF_TRACE_GROUPS
         unsigned long long tr[5] = {0, 0, 0, 0, 0};
@@ -3489,10 +3509,13 @@ __global__ __launch_bounds__(256) void k_group_runs_big(const uint32_t* __restri
                                                    nullptr);
 #endif
         store_comp_mean(out + 4 * (size_t)q.x, wid, sum, np);
+        if (nq <= gridDim.x) break;
         if (threadIdx.x == 0) s_t = atomicAdd(qctr + 1, 1u);
         __syncthreads();
-        t = s_t;
+        const uint32_t d = s_t;
         __syncthreads();
+        if (d >= nq - gridDim.x) break;
+        t = gridDim.x + d;
     }
 }
 
@@ -3613,12 +3636,25 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
             if ((e = hipGetLastError()) != hipSuccess) return e;
             const bool q16 = g_run_q16 == 1 ||
                              (g_run_q16 == 2 && a.nframes <= 1 && a.group_marks == nullptr);
+            static uint32_t resident[2] = {0, 0};  // blocks of <8> / <16> the chip holds at once
+            uint32_t& rb = resident[q16 ? 1 : 0];
+            if (!rb) {
+                int per_cu = 0, cus = 0, dev = 0;
+                (void)hipGetDevice(&dev);
+                (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+                (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                    &per_cu, q16 ? reinterpret_cast<const void*>(&k_group_runs_big<16>)
+                                 : reinterpret_cast<const void*>(&k_group_runs_big<8>), 256, 0);
+                // (the API can report one block per CU too many, MI355X_MICROARCH.md)
+                rb = per_cu > 1 && cus > 0 ? (uint32_t)((per_cu - 1) * cus) : 256u;
+            }
+            const uint32_t big_blocks = std::min(g_run_big_blocks, rb);
             if (q16)
-                hipLaunchKernelGGL((k_group_runs_big<16>), dim3(g_run_big_blocks), dim3(256), 0, s,
+                hipLaunchKernelGGL((k_group_runs_big<16>), dim3(big_blocks), dim3(256), 0, s,
                                    kbuf[npasses & 1], vbuf[npasses & 1], a.pts,
                                    reinterpret_cast<float*>(a.out), a.bigq, a.bigq_cap, qctr);
             else
-                hipLaunchKernelGGL((k_group_runs_big<8>), dim3(g_run_big_blocks), dim3(256), 0, s,
+                hipLaunchKernelGGL((k_group_runs_big<8>), dim3(big_blocks), dim3(256), 0, s,
                                    kbuf[npasses & 1], vbuf[npasses & 1], a.pts,
                                    reinterpret_cast<float*>(a.out), a.bigq, a.bigq_cap, qctr);
         }
