@@ -2546,7 +2546,7 @@ constexpr uint32_t kChainPad = 16;  // LDS padding of staged point buffers
 constexpr uint32_t kGatherChunk = 256;  // points per gathered chunk of a k_group wave
 constexpr uint32_t kExtraRuns = 64;  // runs past a k_group_runs tile read for its last group
 constexpr uint32_t kRunPasses = 4;   // staging windows per k_group_runs tile (mode 2)
-constexpr uint32_t kHugeGroup = 8192;  // queued groups drawn first by k_group_runs_big (points)
+constexpr uint32_t kHugeGroup = 32768;  // queued groups drawn first by k_group_runs_big (points)
 
 // comp[0] + comp[4] + ... + comp[4 (n - 1)] in order: one component of a staged group by one lane
 // (its 4 lanes hold the group's 4 components); blocks of 8 values alternate between two register
@@ -2880,8 +2880,9 @@ uint32_t g_run_wave = 2;
 
 uint32_t g_run_big_blocks = 1024;  // k_group_runs_big grid (tuning knob GDF_RUN_BIG_BLOCKS)
 // chunks of k_group_runs_big (one 4-wave block per queued group): 1 K points (Q = 16) or 512
-// (Q = 8); 0 never 1 K, 1 always, 2 (default) for single depth-only frames, whose long voxels
-// reach ~20 K points at 4K (tuning knob GDF_RUN_Q16)
+// (Q = 8); 0 never 1 K, 1 always, 2 (default) for single frames - 4K depth frames (voxels of
+// ~20 K points) and rollbuffer windows (C3: 4.72 -> 4.49 ms per frame with 1 K chunks) - and 512
+// for multi-frame batches (tuning knob GDF_RUN_Q16)
 uint32_t g_run_q16 = 2;
 
 
@@ -3326,13 +3327,17 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
             }
             __syncthreads();
             if (total == 0) continue;  // block-uniform
-            // queued groups: huge ones (>= kHugeGroup points, or continuing past the tile) into
-            // the region at the top of the queue that k_group_runs_big draws first (longest
-            // first bounds the tail: the C3 window's 10^5-point groups otherwise start late)
+            // queued groups: huge ones (>= kHugeGroup points) into the region at the top of the
+            // queue that k_group_runs_big draws first (longest first bounds the tail: the C3
+            // window's 10^5-point groups otherwise start late).  A group continuing past the
+            // tile's records is sized by its runs times the tile's mean run length (an estimate:
+            // it only orders the queue).
             uint32_t qlocal = 0xFFFFFFFFu, hlocal = 0xFFFFFFFFu;
             if (threadIdx.x < total && average && !done) {
-                const uint32_t e = s_start[threadIdx.x + 1];
-                const bool huge = e > rend || ge - gs >= kHugeGroup;
+                const uint32_t s = s_start[threadIdx.x], e = s_start[threadIdx.x + 1];
+                const uint64_t est = e > rend ? (uint64_t)(e - s) * s_off[kGroupThreads] / kGroupThreads
+                                              : (uint64_t)(ge - gs);
+                const bool huge = est >= kHugeGroup;
                 if (huge) hlocal = atomicAdd(&s_nh, 1u);
                 else qlocal = atomicAdd(&s_nq, 1u);
             }
@@ -3635,7 +3640,7 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
         if (a.average) {
             if ((e = hipGetLastError()) != hipSuccess) return e;
             const bool q16 = g_run_q16 == 1 ||
-                             (g_run_q16 == 2 && a.nframes <= 1 && a.group_marks == nullptr);
+                             (g_run_q16 == 2 && a.nframes <= 1);
             static uint32_t resident[2] = {0, 0};  // blocks of <8> / <16> the chip holds at once
             uint32_t& rb = resident[q16 ? 1 : 0];
             if (!rb) {
