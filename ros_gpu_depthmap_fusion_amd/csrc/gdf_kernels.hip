@@ -3330,12 +3330,14 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
             // queued groups: huge ones (>= kHugeGroup points) into the region at the top of the
             // queue that k_group_runs_big draws first (longest first bounds the tail: the C3
             // window's 10^5-point groups otherwise start late).  A group continuing past the
-            // tile's records is sized by its runs times the tile's mean run length (an estimate:
-            // it only orders the queue).
+            // tile's records is sized by its runs times the mean length of its own runs inside the
+            // tile (an estimate: it only orders the queue; the tile's other groups can have much
+            // shorter runs).
             uint32_t qlocal = 0xFFFFFFFFu, hlocal = 0xFFFFFFFFu;
             if (threadIdx.x < total && average && !done) {
                 const uint32_t s = s_start[threadIdx.x], e = s_start[threadIdx.x + 1];
-                const uint64_t est = e > rend ? (uint64_t)(e - s) * s_off[kGroupThreads] / kGroupThreads
+                const uint32_t nin = tend - s, pin = s_off[tend - t0] - s_off[s - t0];
+                const uint64_t est = e > rend ? (uint64_t)(e - s) * pin / max(nin, 1u)
                                               : (uint64_t)(ge - gs);
                 const bool huge = est >= kHugeGroup;
                 if (huge) hlocal = atomicAdd(&s_nh, 1u);

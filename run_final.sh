@@ -11,3 +11,4 @@ timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/write -o run --output-forma
 timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d $O/t4k -o run --output-format csv -- python3 bench.py --steps 50 --warmup 5 --width 3840 --height 2160 --batch 1 --ring 2 --no-secondary --no-cpu-baseline --no-kernel-timing > $O/t4k.log 2>&1 || exit 1
 timeout -k 10 150 python tools/group_trace.py --c3 256 > $O/gtrace_c3.txt 2>&1 || exit 1
 timeout -k 10 120 python tools/group_trace.py 3840 2160 4 dense > $O/gtrace_4k.txt 2>&1 || exit 1
+timeout -k 10 180 python tools/bench_c3.py --steps 10 --json $O/c3.json > /dev/null 2>> $O/err.log || exit 1
