@@ -2547,6 +2547,7 @@ constexpr uint32_t kGatherChunk = 256;  // points per gathered chunk of a k_grou
 constexpr uint32_t kExtraRuns = 64;  // runs past a k_group_runs tile read for its last group
 constexpr uint32_t kRunPasses = 4;   // staging windows per k_group_runs tile (mode 2)
 constexpr uint32_t kHugeGroup = 32768;  // queued groups drawn first by k_group_runs_big (points)
+constexpr uint32_t kHugeRuns = 2048;    // ... or runs (a crossing group's point estimate can be low)
 
 // comp[0] + comp[4] + ... + comp[4 (n - 1)] in order: one component of a staged group by one lane
 // (its 4 lanes hold the group's 4 components); blocks of 8 values alternate between two register
@@ -3339,7 +3340,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
                 const uint32_t nin = tend - s, pin = s_off[tend - t0] - s_off[s - t0];
                 const uint64_t est = e > rend ? (uint64_t)(e - s) * pin / max(nin, 1u)
                                               : (uint64_t)(ge - gs);
-                const bool huge = est >= kHugeGroup;
+                const bool huge = est >= kHugeGroup || e - s >= kHugeRuns;
                 if (huge) hlocal = atomicAdd(&s_nh, 1u);
                 else qlocal = atomicAdd(&s_nq, 1u);
             }
@@ -3481,6 +3482,14 @@ __global__ __launch_bounds__(256) void k_group_runs_big(const uint32_t* __restri
     const uint32_t nh = __hip_atomic_load(qctr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t nq = min(na + nh, bigq_cap);
     auto slot_of = [&](uint32_t j) { return j < nh ? bigq_cap - 1u - j : j - nh; };
+#ifdef GDF_TRACE_GROUPS
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // (the queue's two regions, in the last slot)
+        g_gtrace[kTraceSlots - 1][0] = 0;
+        g_gtrace[kTraceSlots - 1][1] = na;
+        g_gtrace[kTraceSlots - 1][2] = nh;
+        g_gtrace[kTraceSlots - 1][3] = bigq_cap;
+    }
+#endif
     // Block b takes slot b, then draws further slots from the counter.  The grid is sized to the
     // blocks the chip holds at once (launch_voxelize): a block that is not resident yet must not
     // hold a slot - with 1024 blocks, the C3 window's 100 K-point groups in slots ~800-1000

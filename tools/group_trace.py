@@ -68,6 +68,8 @@ def main():
     eng.synchronize()
     buf = np.zeros((SLOTS, 8), np.uint64)
     assert lib.gdf_debug_group_trace(buf.ctypes.data_as(C.c_void_p), C.c_size_t(buf.nbytes)) == 0
+    print(f"queue: normal {int(buf[-1, 1])}  huge-first {int(buf[-1, 2])}  capacity {int(buf[-1, 3])}")
+    buf[-1] = 0
     used = buf[:, 0] != 0
     g = buf[used]
     slots = np.flatnonzero(used)
