@@ -392,8 +392,21 @@ def workload_name(W, H, K, wl):
             f"-10..30/-20..20/-1..1.5, cells 0.1/0.1/0.12, voxelize average, lifetime 10)")
 
 
+_JSON_FD = None  # the process's original stdout (the one JSON line goes there)
+
+
+def emit(obj):
+    os.write(_JSON_FD if _JSON_FD is not None else 1, (json.dumps(obj) + "\n").encode())
+
+
 def main():
+    # Library chatter on stdout (RCCL's version banner at communicator creation, ...) would break
+    # the one-JSON-line contract: fd 1 points at stderr for the run, the line goes to the original.
+    global _JSON_FD
     args = parse()
+    sys.stdout.flush()
+    _JSON_FD = os.dup(1)
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     dist = None
     rank, local_rank = 0, 0
@@ -419,7 +432,7 @@ def main():
     W, H, K = args.width, args.height, args.cameras
     params = ComponentParams()
     if args.h2d_only:
-        print(json.dumps(run_h2d(args, params, args.steps, args.warmup)), flush=True)
+        emit(run_h2d(args, params, args.steps, args.warmup))
         return
     eng = GPUDepthmapFusion(local_rank)
     st = DepthStream(eng, W, H, K, rank, args.workload, args.ring)
@@ -460,7 +473,7 @@ def main():
         }
         if secondary is not None:
             out["secondary"] = secondary
-        print(json.dumps(out), flush=True)
+        emit(out)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
