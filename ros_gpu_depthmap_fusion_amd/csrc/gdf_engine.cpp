@@ -20,6 +20,7 @@
 #include <cstdlib>
 #include <atomic>
 #include <condition_variable>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -84,25 +85,34 @@ class StagingCopier {
             for (const Job& j : jobs) std::memcpy(j.dst, j.src, j.bytes);
             return;
         }
-        std::unique_lock<std::mutex> lk(m_);
-        if (th_.empty())
-            for (unsigned i = 1; i < nt; ++i) th_.emplace_back([this] { worker(); });
-        chunks_.clear();
+        // one generation per call: its own chunk list, captured by the workers under the lock, so
+        // a worker that wakes late (after this call returned) holds the OLD list - already fully
+        // claimed - and can never read the next call's list while it is being built
+        auto g = std::make_shared<Gen>();
         for (const Job& j : jobs)
             for (size_t o = 0; o < j.bytes; o += kChunk)
-                chunks_.push_back({j.dst + o, j.src + o, std::min(kChunk, j.bytes - o)});
-        next_.store(0);
-        left_ = chunks_.size();
-        ++gen_;
-        lk.unlock();
+                g->chunks.push_back({j.dst + o, j.src + o, std::min(kChunk, j.bytes - o)});
+        g->left = g->chunks.size();
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            if (th_.empty())
+                for (unsigned i = 1; i < nt; ++i) th_.emplace_back([this] { worker(); });
+            cur_ = g;
+            ++gen_;
+        }
         cv_.notify_all();
-        work();
-        lk.lock();
-        // (and no worker still inside work(): the next call rebuilds chunks_)
-        done_cv_.wait(lk, [this] { return left_ == 0 && busy_ == 0; });
+        work(*g);
+        std::unique_lock<std::mutex> lk(m_);
+        done_cv_.wait(lk, [&] { return g->left == 0; });  // every chunk copied
+        cur_.reset();
     }
 
   private:
+    struct Gen {
+        std::vector<Job> chunks;  // fixed once published
+        std::atomic<size_t> next{0};
+        size_t left = 0;          // chunks not yet copied (guarded by m_)
+    };
     static constexpr size_t kChunk = 256 << 10;
     unsigned threads() {
         if (!nthreads_) {
@@ -112,37 +122,34 @@ class StagingCopier {
         }
         return nthreads_;
     }
-    void work() {  // claim chunks until none is left (caller and workers alike)
+    void work(Gen& g) {  // claim chunks until none is left (caller and workers alike)
         size_t done = 0;
-        for (size_t i; (i = next_.fetch_add(1)) < chunks_.size(); ++done)
-            std::memcpy(chunks_[i].dst, chunks_[i].src, chunks_[i].bytes);
+        for (size_t i; (i = g.next.fetch_add(1)) < g.chunks.size(); ++done)
+            std::memcpy(g.chunks[i].dst, g.chunks[i].src, g.chunks[i].bytes);
+        if (!done) return;
         std::lock_guard<std::mutex> lk(m_);
-        left_ -= done;
-        if (left_ == 0) done_cv_.notify_all();
+        g.left -= done;
+        if (g.left == 0) done_cv_.notify_all();
     }
     void worker() {
         uint64_t seen = 0;
         for (;;) {
+            std::shared_ptr<Gen> g;
             {
                 std::unique_lock<std::mutex> lk(m_);
                 cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
                 if (stop_) return;
                 seen = gen_;
-                ++busy_;
+                g = cur_;
             }
-            work();
-            std::lock_guard<std::mutex> lk(m_);
-            if (--busy_ == 0 && left_ == 0) done_cv_.notify_all();
+            if (g) work(*g);
         }
     }
     unsigned nthreads_ = 0;
     std::vector<std::thread> th_;
     std::mutex m_;
     std::condition_variable cv_, done_cv_;
-    std::vector<Job> chunks_;
-    std::atomic<size_t> next_{0};
-    size_t left_ = 0;
-    unsigned busy_ = 0;
+    std::shared_ptr<Gen> cur_;
     uint64_t gen_ = 0;
     bool stop_ = false;
 };
@@ -1103,7 +1110,7 @@ void ensure_misc(gdf_engine* e) {
 
 // Arguments of the fused compaction launch: convert + flying + crop + selected-point transform +
 // ordered compaction (+ voxel keys and occupancy marks when fused_voxel).
-FrameArgs frame_args(gdf_engine* e, bool fused_voxel) {
+FrameArgs frame_args(gdf_engine* e, bool fused_voxel, bool compaction_marks = false) {
     if (!e->prepared) prepare_buffers(e);
     if (!e->depth_uploaded) upload_depthmaps(e);
     ensure_misc(e);
@@ -1156,11 +1163,13 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel) {
     a.tfw = e->d_tfw.as<float>();
     a.tfc = e->d_tfc.as<float>();
     a.do_voxel = fused_voxel ? 1 : 0;
-    e->sl().group_marks = fused_voxel && a.sel_tiles;
+    e->sl().group_marks = fused_voxel && a.sel_tiles && !compaction_marks;
     if (fused_voxel) {
         // With rollbuffer points (10^7 survivors of a window that re-observes the same voxels) the
         // occupancy marks come from the voxel groups after the sort - one per voxel - instead of
         // device-scope atomics per run of survivors; the grid update is then its own launch.
+        // A frame whose voxelize is deferred (multi-GPU: the rank with the rollbuffer sends its
+        // points away to the key-range owners) has no local groups: k_sel marks them itself.
         // Otherwise: marks from the compaction, and the sequence number the grid update fused
         // into the first radix pass will take.
         if (!e->sl().group_marks) {
@@ -1272,8 +1281,8 @@ void frame_launched(gdf_engine* e, bool fused_voxel, bool key_hist, bool runs = 
     e->sl().vox_valid = false;
 }
 
-void run_frame(gdf_engine* e, bool fused_voxel) {
-    const FrameArgs a = frame_args(e, fused_voxel);
+void run_frame(gdf_engine* e, bool fused_voxel, bool compaction_marks = false) {
+    const FrameArgs a = frame_args(e, fused_voxel, compaction_marks);
     if (e->profiling) e->timed(GDF_KERNEL_EVENT_FLOOR, [] {});  // calibrates the event overhead
     e->timed(GDF_KERNEL_FRAME, [&] { HIPCHK(launch_frame(a, e->s(), e->hook_ptr())); });
     frame_launched(e, fused_voxel, a.key_hist != nullptr, a.run_mode != 0);
@@ -2091,7 +2100,7 @@ int gdf_process_frame(gdf_engine* e, const gdf_frame_params* p, gdf_frame_result
             if (sort_bits(e) > 32) fail(GDF_ERR_ARG, "voxel key + frame index exceed 32 bits");
             widen_if_needed(e, p->occupancy_lifetime, e->s());  // before marks are consumed
             if (p->defer_voxelize) {  // keys + marks only (multi-GPU fused cloud)
-                run_frame(e, true);
+                run_frame(e, true, true);
                 if (!p->defer_occupancy_grid) occupancy_grid(e, p->occupancy_lifetime, e->s());
             } else if (!p->defer_occupancy_grid && e->grid_mode == 0) {
                 run_fused_frame(e, p->voxel_average, p->occupancy_lifetime);
@@ -2333,16 +2342,27 @@ int gdf_voxel_occupancy_grid_batch(gdf_engine* e, const uint32_t* bits, uint64_t
             if (e->slots[i].marks_set)
                 fail(GDF_ERR_STATE, "marks of a frame are pending (take them first)");
         widen_if_needed(e, lifetime, e->s());
-        if (e->grid_mode == 0) {  // one pass for the batch
+        if (e->grid_mode == 0) {  // one pass per <= kMaxCams frames
             ensure_misc(e);
-            const GridSeq q = e->grid_seq(e->grid_ticket++);
-            const SnapArgs sn = nframes > 1 ? snap_args(e, batch_grid_blocks(e->ncells), nframes)
-                                             : SnapArgs{nullptr, nullptr, nullptr};
-            e->timed_on(GDF_KERNEL_GRID, e->s(), [&] {
-                HIPCHK(launch_grid_u8_batch(e->d_grid8.as<uint8_t>(), bits, e->ncells, nranks,
-                                            nframes, frame_stride_words, rank_stride_words,
-                                            lifetime, q, sn, e->s()));
-            });
+            // per-frame snapshots only for the slot's own multi-frame batch (<= kMaxCams frames,
+            // downloadable with gdf_download_batch_occupancy_grid); the frames of a deferred
+            // single-frame exchange (BatchedMarkExchange) can never be downloaded one by one, and
+            // the kernel's per-wave snapshot counters hold kMaxCams frames
+            const bool snaps = nframes > 1 && e->sl().nframes == nframes && nframes <= (uint32_t)kMaxCams;
+            e->sl().snap_valid = false;
+            const SnapArgs sn = snaps ? snap_args(e, batch_grid_blocks(e->ncells), nframes)
+                                      : SnapArgs{nullptr, nullptr, nullptr};
+            for (uint32_t f0 = 0; f0 < nframes || f0 == 0; f0 += (uint32_t)kMaxCams) {
+                const uint32_t nf = std::min<uint32_t>(nframes - f0, (uint32_t)kMaxCams);
+                const GridSeq q = e->grid_seq(e->grid_ticket++);
+                e->timed_on(GDF_KERNEL_GRID, e->s(), [&] {
+                    HIPCHK(launch_grid_u8_batch(e->d_grid8.as<uint8_t>(),
+                                                bits ? bits + (uint64_t)f0 * frame_stride_words : bits,
+                                                e->ncells, nranks, nf, frame_stride_words,
+                                                rank_stride_words, lifetime, q, sn, e->s()));
+                });
+                if (nframes == 0) break;
+            }
         } else {  // general history: frame by frame (no per-frame grids kept)
             e->sl().snap_valid = false;
             for (uint32_t f = 0; f < nframes; ++f) {

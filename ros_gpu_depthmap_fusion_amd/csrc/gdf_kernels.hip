@@ -9,6 +9,7 @@
 //   k_grid_*           zero_uints / decrement_uints.glsl:31-51 / max_with_uints_times_scalar.glsl:36-46
 //                      / uints_to_chars.glsl:31-50, fused into one pass over the cells
 //   k_sort_*, k_group  inc/voxelize.h:74-105 + radix_grouper.h + radix_sort.h (GPU version)
+#include <atomic>
 #include "gdf_kernels.hpp"
 #include "gdf_voxsum.hpp"  // the voxel sum (row_sum4): exact integer stretches
 
@@ -2011,6 +2012,8 @@ __device__ __forceinline__ void grid_u8_frames(uint4* __restrict__ grid, uint64_
                                                const SnapArgs& sn) {
     __shared__ uint32_t s_sc[4][kMaxCams];  // per wave: snapshot entries so far, per frame
     const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    // (the host passes snapshots only for <= kMaxCams frames; anything else keeps none)
+    const bool keep_snaps = sn.idx != nullptr && nframes <= (uint32_t)kMaxCams;
     uint32_t W, seg;
     snap_layout(nwords, nblocks, W, seg);
     const uint32_t wave = block * 4u + wid;
@@ -2038,7 +2041,7 @@ __device__ __forceinline__ void grid_u8_frames(uint4* __restrict__ grid, uint64_
             v1.y = grid_word(v1.y, m >> 20, L);
             v1.z = grid_word(v1.z, m >> 24, L);
             v1.w = grid_word(v1.w, m >> 28, L);
-            if (f + 1 < nframes && sn.idx) {
+            if (f + 1 < nframes && keep_snaps) {
                 const bool nz = act && ((v0.x | v0.y | v0.z | v0.w | v1.x | v1.y | v1.z | v1.w) != 0u);
                 const unsigned long long b = __ballot(nz);
                 if (b) {  // wave-uniform
@@ -2064,7 +2067,7 @@ __device__ __forceinline__ void grid_u8_frames(uint4* __restrict__ grid, uint64_
             grid[2 * i + 1] = v1;
         }
     }
-    if (sn.idx && lane + 1 < nframes) sn.cnt[(uint64_t)lane * W + wave] = s_sc[wid][lane];
+    if (keep_snaps && lane + 1 < nframes) sn.cnt[(uint64_t)lane * W + wave] = s_sc[wid][lane];
 }
 
 __device__ __forceinline__ void grid_u8_part_frames(uint4* __restrict__ grid,
@@ -3572,6 +3575,28 @@ static void launch_sort_pass(uint32_t tiles, hipStream_t s, const uint32_t* kin,
                        p == 0 ? reinterpret_cast<uint32_t*>(a.ctrs + kCtrRunQueue) : nullptr);
 }
 
+// Blocks of k_group_runs_big<8> / <16> the current device holds at once, cached per device (an
+// engine is bound to one device, but a process may drive several; the value is computed once per
+// device and kernel variant, races only recompute the same number)
+static uint32_t resident_big_blocks(bool q16) {
+    constexpr int kDev = 64;
+    static std::atomic<uint32_t> cache[kDev][2];
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::atomic<uint32_t>* slot = dev >= 0 && dev < kDev ? &cache[dev][q16 ? 1 : 0] : nullptr;
+    uint32_t rb = slot ? slot->load(std::memory_order_relaxed) : 0u;
+    if (rb) return rb;
+    int per_cu = 0, cus = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, q16 ? reinterpret_cast<const void*>(&k_group_runs_big<16>)
+                     : reinterpret_cast<const void*>(&k_group_runs_big<8>), 256, 0);
+    // (the API can report one block per CU too many, MI355X_MICROARCH.md)
+    rb = per_cu > 1 && cus > 0 ? (uint32_t)((per_cu - 1) * cus) : 256u;
+    if (slot) slot->store(rb, std::memory_order_relaxed);
+    return rb;
+}
+
 hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hook) {
     const uint32_t npasses = radix_passes(a.key_bits);
     const int pt = a.sort_pt == 4 || a.sort_pt == 8 ? a.sort_pt : 16;
@@ -3652,18 +3677,7 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
             if ((e = hipGetLastError()) != hipSuccess) return e;
             const bool q16 = g_run_q16 == 1 ||
                              (g_run_q16 == 2 && a.nframes <= 1);
-            static uint32_t resident[2] = {0, 0};  // blocks of <8> / <16> the chip holds at once
-            uint32_t& rb = resident[q16 ? 1 : 0];
-            if (!rb) {
-                int per_cu = 0, cus = 0, dev = 0;
-                (void)hipGetDevice(&dev);
-                (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-                (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                    &per_cu, q16 ? reinterpret_cast<const void*>(&k_group_runs_big<16>)
-                                 : reinterpret_cast<const void*>(&k_group_runs_big<8>), 256, 0);
-                // (the API can report one block per CU too many, MI355X_MICROARCH.md)
-                rb = per_cu > 1 && cus > 0 ? (uint32_t)((per_cu - 1) * cus) : 256u;
-            }
+            const uint32_t rb = resident_big_blocks(q16);
             const uint32_t big_blocks = std::min(g_run_big_blocks, rb);
             if (q16)
                 hipLaunchKernelGGL((k_group_runs_big<16>), dim3(big_blocks), dim3(256), 0, s,

@@ -431,7 +431,11 @@ __device__ __forceinline__ float rows_chunk_sum_stretch(const float* __restrict_
     constexpr int A = 8388609, B = 16777215;
     const uint32_t lane = threadIdx.x & 63, r = lane >> 2, h = lane & 3;
     const uint32_t nrows = (n + 63u) >> 6;
-    const RowInfo ri = row_info<false>(comp + r * kRowStride + h * 16u,
+    // lanes of rows past the chunk's last read row 0 (their values are masked to -0.0 by the
+    // negative count): no lane reads outside its component's rows (a k_group_runs_big<8> wave
+    // owns 8 rows, not 16)
+    const uint32_t rr = r < nrows ? r : 0u;
+    const RowInfo ri = row_info<false>(comp + rr * kRowStride + h * 16u,
                                        (int)n - (int)(r * 64u + h * 16u), n < 64u * 16u, s);
     // 3. the rows from the exact s
     uint32_t cur = 0;

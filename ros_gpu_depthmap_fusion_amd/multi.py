@@ -251,10 +251,37 @@ class FusedCloudRank:
         if any(cams[k].width * cams[k].height < self.Lmax for k in range(world)):
             raise ValueError("fused multi-GPU frames need cameras taller than F rows")
         self.pc = params.to_c(None, None, False, True, True)
+        # The rollbuffer (point sequences, SURVEY §8(e): a single stream) lives on the LAST rank:
+        # the reference appends the selected rollbuffer points after every camera's pixels, at
+        # offset sum(P) (fusion.cpp:1509-1581, offsets :1525 / :1559), and sorts them together
+        # with the depth points in one voxelize (:1743-1756).  The last rank compacts [its camera's
+        # pixels, then the selected rollbuffer points] and partitions that list stably by key
+        # range, so every key-range owner receives, in rank order, [camera 0 .. camera N-1 pixels,
+        # rollbuffer points] - the reference's buffer order restricted to its range.
+        self.rollbuffer_rank = world - 1
+        self.has_rollbuffer = rank == self.rollbuffer_rank
+        self._pc_move = {}  # to_c of the frames with move transforms (rollbuffer rank)
 
-    def frame(self, depth_ptr: int, tail_src_ptr: int):
+    def frame_params(self, move=None):
+        """The frame's gdf_frame_params: `move` = (T_world_move, T_crop_move) when the component's
+        tf lookup of the move frame succeeded (component.cpp:192-197) - used by the rollbuffer
+        rank only (the other ranks hold no point sequences)."""
+        if move is None or not self.has_rollbuffer:
+            return self.pc
+        key = tuple(np.asarray(move[0], np.float32).ravel()) + tuple(np.asarray(move[1], np.float32).ravel())
+        pc = self._pc_move.get(key)
+        if pc is None:
+            if len(self._pc_move) > 64:
+                self._pc_move.clear()
+            pc = self._pc_move[key] = self.p.to_c(move[0], move[1], False, True, True)
+        return pc
+
+    def frame(self, depth_ptr: int, tail_src_ptr: int, move=None):
         """One frame: depth_ptr = this rank's depth map (device), tail_src_ptr = its last
-        Lmax depth values (device, the halo the next rank needs)."""
+        Lmax depth values (device, the halo the next rank needs).  On the rollbuffer rank the
+        point sequences added to the engine since the last frame (addPointSequence[Device]) are
+        ingested, rolled and - with `move` - selected, transformed, cropped and compacted behind
+        the camera's points."""
         import numpy as np
         import torch
         import torch.distributed as dist
@@ -286,7 +313,7 @@ class FusedCloudRank:
             eng.addHaloDepthmapDevice(halo_ptr + 2 * (self.Lmax - take), take, pc.width,
                                       pc.height, *pc.intrinsics(), pc.T_world, pc.T_crop)
         eng.addDepthmapDevice(depth_ptr, c.width, c.height, *c.intrinsics(), c.T_world, c.T_crop)
-        eng.processFramePrepared(self.pc)
+        res = eng.processFramePrepared(self.frame_params(move))
         _, ncells = eng.grid_size()
         words = words_for(ncells)
         # occupancy union (every rank the same grid)
@@ -306,8 +333,9 @@ class FusedCloudRank:
             dg = h.DeviceArray.from_numpy(torch.cat(parts).numpy())
             eng.import_marks(dg.ptr, words, self.world)
         eng.voxelOccupancyGrid(self.p.occupancy_lifetime)
-        # key-range partition + all-to-all + voxelize of this rank's range
-        n_total = max(c.width * c.height, 1)
+        # key-range partition + all-to-all + voxelize of this rank's range (send buffers for the
+        # frame's depth pixels + selected rollbuffer points)
+        n_total = max(int(res.num_points_total), 1)
         if self.dev == "cuda":
             sp = torch.empty((n_total, 4), dtype=torch.float32, device="cuda")
             sk = torch.empty(n_total, dtype=torch.int32, device="cuda")

@@ -254,3 +254,93 @@ def test_rccl_fused_cloud_world1(tmp_path):
         if f != 2:
             np.testing.assert_array_equal(np.load(tmp_path / f"ngrid_f{f}.npy"),
                                           orc.downloadVoxelOccupancyGrid(), f"frame {f}")
+
+
+# ---- the rollbuffer leg: point sequences on the last rank -----------------
+def _rank_rb(rank, world, port, W_, H_, LW, LH, first, win, frames, out_dir, launch_defaults):
+    """One rank of a fused run WITH the rollbuffer: the last rank ingests the point sequences of
+    fused_ref.schedule (device PointCloud2 records, gdf_add_point_sequence_device) and sends its
+    selected points behind its camera's (multi.FusedCloudRank.frame(move=...))."""
+    import torch.distributed as dist
+    import fused_ref
+    from ros_gpu_depthmap_fusion_amd import build_library, hiprt, multi
+    from ros_gpu_depthmap_fusion_amd.gdf import GPUDepthmapFusion
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    build_library()
+    p = ComponentParams() if launch_defaults else params(4)
+    p.ps_timespan = (win - 0.5) / 30.0
+    cams = [synth.make_camera(k, W_, H_) for k in range(world)]
+    eng = GPUDepthmapFusion(0)
+    fr = multi.FusedCloudRank(eng, cams, rank, world, p, dev="cpu")
+    n = W_ * H_
+    lidar = fused_ref.lidar_camera(LW, LH)
+    recs = None
+    if fr.has_rollbuffer:
+        recs = [hiprt.DeviceArray.from_numpy(fused_ref.sequence_records(lidar, k)) for k in range(2)]
+    sched = fused_ref.schedule(first, frames)
+    for f in range(frames):
+        depth = synth.dense_frame(cams[rank], rank, f)
+        move = None
+        if fr.has_rollbuffer:
+            for k in sched[f]:
+                eng.addPointSequenceDevice(recs[k % 2].ptr, LW * LH, 16, *synth.sequence_time(k),
+                                           synth.move_transform(k))
+            move = (lidar.T_world, lidar.T_crop)
+        d = hiprt.DeviceArray.from_numpy(depth)
+        fr.frame(d.ptr, d.ptr + 2 * (n - fr.Lmax), move=move)
+        np.save(os.path.join(out_dir, f"vox_r{rank}_f{f}.npy"), eng.downloadVoxelizedPoints()[:, :3])
+        np.save(os.path.join(out_dir, f"grid_r{rank}_f{f}.npy"), eng.downloadVoxelOccupancyGrid())
+        if fr.has_rollbuffer:
+            np.save(os.path.join(out_dir, f"rb_f{f}.npy"), np.array(eng.rollbuffer_state().as_tuple()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _oracle_rb(world, W_, H_, LW, LH, first, win, frames, launch_defaults, threads):
+    """The single oracle engine over all cameras + the same point sequences, per frame:
+    (voxel means, u8 grid, rollbuffer state)."""
+    import fused_ref
+    from oracle import OracleFusion
+    p = ComponentParams() if launch_defaults else params(4)
+    p.ps_timespan = (win - 0.5) / 30.0
+    cams = [synth.make_camera(k, W_, H_) for k in range(world)]
+    lidar = fused_ref.lidar_camera(LW, LH)
+    recs = [fused_ref.sequence_records(lidar, k) for k in range(2)]
+    orc = OracleFusion(threads=threads)
+    for f, seqs in enumerate(fused_ref.schedule(first, frames)):
+        for k in seqs:
+            orc.addPointSequence(recs[k % 2], *synth.sequence_time(k), synth.move_transform(k))
+        orc.clear()
+        for k, c in enumerate(cams):
+            orc.addDepthmap(synth.dense_frame(c, k, f), *c.intrinsics(), c.T_world, c.T_crop)
+        orc.processFrame(p, T_world_move=lidar.T_world, T_crop_move=lidar.T_crop)
+        yield orc.downloadVoxelizedPoints()[:, :3], orc.downloadVoxelOccupancyGrid(), orc.rollbuffer_state()
+
+
+@pytest.mark.parametrize("cfg", ["small", "C5"])
+def test_fused_cloud_rollbuffer_leg(tmp_path, cfg):
+    """The multi-GPU fused cloud WITH the rollbuffer on the last rank, through the HIP kernels
+    (processes on the one GPU, gloo): per frame the ranks' voxel ranges concatenated equal ONE
+    oracle engine over all cameras + the rollbuffer (its selected points at offset sum(P),
+    fusion.cpp:1509-1581, sorted with the depth points, :1743-1756) bit for bit; every rank's grid
+    and the rollbuffer rank's state equal the oracle's.  "small": 3 ranks x 160x120, F = 4,
+    sequences of 80x60 points, window 3, 5 frames (rolls from frame 2).  "C5": 8 ranks x 4K at
+    launch defaults + a window of 8 x 720p sequences (7.4 M selected points; frame 1 rolls the
+    oldest out)."""
+    if cfg == "small":
+        world, W_, H_, LW, LH, first, win, frames, ld, th = 3, 160, 120, 80, 60, 2, 3, 5, False, 4
+    else:
+        world, W_, H_, LW, LH, first, win, frames, ld, th = 8, 3840, 2160, 1280, 720, 8, 8, 2, True, 16
+    mp.start_processes(_rank_rb, args=(world, _free_port(), W_, H_, LW, LH, first, win, frames,
+                                       str(tmp_path), ld), nprocs=world, join=True,
+                       start_method="spawn")
+    for f, (want, grid, st) in enumerate(_oracle_rb(world, W_, H_, LW, LH, first, win, frames, ld, th)):
+        assert st[3] > 0, f"frame {f}: rollbuffer points selected"
+        assert tuple(np.load(tmp_path / f"rb_f{f}.npy").tolist()) == tuple(st), f"{cfg} frame {f} state"
+        got = np.concatenate([np.load(tmp_path / f"vox_r{r}_f{f}.npy") for r in range(world)])
+        assert len(got) == len(want) > 0, f"{cfg} frame {f}"
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), f"{cfg} frame {f}"
+        for r in range(world):
+            np.testing.assert_array_equal(np.load(tmp_path / f"grid_r{r}_f{f}.npy"), grid,
+                                          f"{cfg} frame {f} rank {r}")

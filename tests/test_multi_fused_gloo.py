@@ -3,7 +3,11 @@ one camera (the oracle as its engine, camera k-1's tail as halo), the compacted 
 lists are all-to-all'ed by voxel-key range (multi.exchange_points), each rank voxelizes its range;
 the concatenated ranges equal ONE engine over all cameras (src/gpu_depthmap_fusion.cpp:1743-1756)
 bit for bit - at F = 0 and at F = 4, where camera k's top rows read camera k-1 -
-and the occupancy union gives every rank the single engine's grid."""
+and the occupancy union gives every rank the single engine's grid.  With the rollbuffer leg the
+last rank also ingests point sequences (filter, insert, roll, select, transform, crop) and sends
+its selected points after its camera's: the fused cloud is the single engine's over all cameras
+AND the rollbuffer (fusion.cpp:1509-1581: the selection sits at offset sum(P), after every
+camera)."""
 import os
 import socket
 import sys
@@ -32,19 +36,41 @@ def params(F):
     return p
 
 
-def _rank(rank, world, port, F, out_dir):
+RB_FRAMES, RB_FIRST, RB_WIN = 4, 2, 3  # rollbuffer leg: frames, sequences at frame 0, window
+
+
+def rb_params(F):
+    p = params(F)
+    p.ps_timespan = (RB_WIN - 0.5) / 30.0  # the window keeps RB_WIN sequences
+    return p
+
+
+def _rank(rank, world, port, F, out_dir, rollbuffer=False):
     import torch
     import torch.distributed as dist
     import fused_ref
     from oracle import OracleFusion
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    p = params(F)
+    p = rb_params(F) if rollbuffer else params(F)
     cams = [synth.make_camera(k, W, H) for k in range(world)]
     orc = OracleFusion()
     hist = None
-    for f in range(FRAMES):
-        pts, keys = fused_ref.rank_points(orc, cams, rank, f, p, halo=F > 0)
+    lidar = fused_ref.lidar_camera(W // 2, H // 2)
+    frames = RB_FRAMES if rollbuffer else FRAMES
+    sched = fused_ref.schedule(RB_FIRST, frames)
+    for f in range(frames):
+        move = None
+        if rollbuffer and rank == world - 1:  # the rollbuffer rank (multi.FusedCloudRank)
+            for k in sched[f]:
+                orc.addPointSequence(fused_ref.sequence_records(lidar, k), *synth.sequence_time(k),
+                                     synth.move_transform(k))
+            move = (lidar.T_world, lidar.T_crop)
+        pts, keys = fused_ref.rank_points(orc, cams, rank, f, p, halo=F > 0, move=move)
+        if move is not None:
+            np.save(os.path.join(out_dir, f"rb_f{f}.npy"), np.array(orc.rollbuffer_state()))
+            np.save(os.path.join(out_dir, f"rbsel_f{f}.npy"),
+                    np.array([orc.rollbuffer_state()[3], len(keys)]))
         ncells = int(np.prod(orc.grid_size()))
         sp, sk, counts = fused_ref.partition(pts, keys, world, ncells)
         rp, rk, rc = multi.exchange_points(torch.from_numpy(np.ascontiguousarray(sp)),
@@ -70,6 +96,51 @@ def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("world,F", [(2, 4), (3, 4)])
+def test_fused_cloud_with_rollbuffer_equals_single_engine(tmp_path, world, F):
+    """The rollbuffer leg: the last rank ingests the point sequences and
+    appends its selected points behind its camera's; per frame the ranks' voxel ranges
+    concatenated equal ONE engine over all cameras + the rollbuffer bit for bit, every rank's grid
+    equals its grid, and the rollbuffer rank's state equals its state (frames 2 and 3 roll)."""
+    import fused_ref
+    from oracle import OracleFusion
+    mp.start_processes(_rank, args=(world, _free_port(), F, str(tmp_path), True), nprocs=world,
+                       join=True, start_method="spawn")
+    p = rb_params(F)
+    cams = [synth.make_camera(k, W, H) for k in range(world)]
+    lidar = fused_ref.lidar_camera(W // 2, H // 2)
+    sched = fused_ref.schedule(RB_FIRST, RB_FRAMES)
+    orc = OracleFusion()
+    for f in range(RB_FRAMES):
+        for k in sched[f]:
+            orc.addPointSequence(fused_ref.sequence_records(lidar, k), *synth.sequence_time(k),
+                                 synth.move_transform(k))
+        orc.clear()
+        for k, c in enumerate(cams):
+            orc.addDepthmap(synth.dense_frame(c, k, f), *c.intrinsics(), c.T_world, c.T_crop)
+        orc.processFrame(p, T_world_move=lidar.T_world, T_crop_move=lidar.T_crop)
+        st = orc.rollbuffer_state()
+        assert st[3] > 0, "the frame selected rollbuffer points"
+        assert tuple(np.load(tmp_path / f"rb_f{f}.npy").tolist()) == tuple(st), f"frame {f} state"
+        sel, kept = np.load(tmp_path / f"rbsel_f{f}.npy").tolist()
+        assert kept > 0
+        want = orc.downloadVoxelizedPoints()[:, :3]
+        got = np.concatenate([np.load(tmp_path / f"vox_r{r}_f{f}.npy") for r in range(world)])
+        assert len(got) == len(want) > 0, f"frame {f}"
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), f"frame {f}"
+        g = orc.historic_grid().reshape(-1)
+        for r in range(world):
+            np.testing.assert_array_equal(np.load(tmp_path / f"grid_r{r}_f{f}.npy"), g)
+    # the rollbuffer actually moved the result: without it the fused cloud differs
+    orc2 = OracleFusion()
+    orc2.clear()
+    for k, c in enumerate(cams):
+        orc2.addDepthmap(synth.dense_frame(c, k, RB_FRAMES - 1), *c.intrinsics(), c.T_world, c.T_crop)
+    orc2.processFrame(p)
+    assert len(orc2.downloadVoxelizedPoints()) != len(want) or not np.array_equal(
+        orc2.downloadVoxelizedPoints()[:, :3].view(np.uint32), want.view(np.uint32))
 
 
 @pytest.mark.parametrize("world,F", [(2, 0), (2, 4), (3, 4)])
