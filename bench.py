@@ -98,17 +98,26 @@ def radix_passes(ncells, B=1):
     return (bits + 7) // 8
 
 
-def model_bytes(P, n_avg, g_avg, ncells, B=1, s_avg=None, runs=False):
-    """Algorithmic HBM bytes per launch of each kernel (DESIGN.md §4): the bytes the algorithm
+def grid_update_bytes(ncells, B=1, snap_bytes=0.0):
+    """Algorithmic bytes of one (batched) grid update: the u8 grid read and written once, each
+    frame's 1-bit marks read, and the sparse snapshots of the frames but the last (4-B index +
+    32 B per non-zero 32-cell group) - not dense per-frame grids."""
+    return 2.0 * ncells + B * ncells / 8.0 + snap_bytes
+
+
+def model_bytes(P, n_avg, g_avg, ncells, B=1, s_avg=None, runs=False, snap_bytes=0.0):
+    """Algorithmic HBM bytes per launch of each kernel (DESIGN.md §5): the bytes the algorithm
     must move once, not the cache traffic of an implementation.  A launch of a B-frame batch
-    processes B frames (P, n, g per frame); its grid update reads and writes the grid once and
-    stores the B - 1 intermediate per-frame grids.  s_avg: the items the voxelize sorts per
-    frame - the points, or (runs) the runs of equal voxel keys, which the sort and the group
-    phase then move instead of points."""
+    processes B frames (P, n, g per frame); its grid update (carried by the first radix pass)
+    reads and writes the grid once, reads the B frames' marks and writes the sparse snapshots of
+    the B - 1 intermediate grids (snap_bytes, counted from the frames' grids).  s_avg: the items
+    the voxelize sorts per frame - the points, or (runs) the runs of equal voxel keys, which the
+    sort and the group phase then move instead of points."""
     P, n_avg, g_avg = B * P, B * n_avg, B * g_avg
     s_items = B * (s_avg if s_avg is not None else n_avg / B)
     tiles = (P + 255) // 256
     npass = radix_passes(ncells, B)
+    grid = grid_update_bytes(ncells, B, snap_bytes)
     return {
         "mask": 3.0 * P,                           # u16 depth in, u8 stage bits out
         "scan": 8.0 * tiles,
@@ -116,10 +125,10 @@ def model_bytes(P, n_avg, g_avg, ncells, B=1, s_avg=None, runs=False):
         "emit": 1.0 * P + 22.0 * n_avg + (8.0 * s_items if runs else 0.0),
         # radix passes over the sorted items (key only in, key+index out; then key+index both
         # ways) + the grid update carried by the first pass, averaged per launch
-        "sort": (12.0 * s_items + 16.0 * s_items * (npass - 1) + (B + 1.0) * ncells) / npass,
+        "sort": (12.0 * s_items + 16.0 * s_items * (npass - 1) + grid) / npass,
         # sorted keys + indices (+ the runs' point ranges) in, points in, means out
         "group": (16.0 * n_avg + 16.0 * s_items if runs else 24.0 * n_avg) + 16.0 * g_avg,
-        "grid": (B + 1.0) * ncells,
+        "grid": grid,
     }
 
 
@@ -139,14 +148,12 @@ def roofline_from(ktimes, kt_steps, mb, pmc_key):
     raw_s = ms / 1e3 / max(n, 1)
     avg_s = max(raw_s - 0.5 * floor_s, 1e-9)
     achieved = mb[slot] / avg_s / 1e9
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
-        try:
-            rec = json.load(open(pmc)).get(pmc_key, {}).get(slot)
-            traffic = rec.get("hbm_bytes_per_launch") if rec else None
-        except Exception:
-            traffic = None
+    traffic, traffic_src = None, None
+    rec = pmc_record(pmc_key).get(slot)
+    if rec:
+        traffic = rec.get("hbm_bytes_per_launch")
+        traffic_src = {"kernels": rec.get("kernels"), "dispatches": rec.get("dispatches"),
+                       "source": "profiles/pmc_traffic.json[%s]" % pmc_key}
     valu = None
     sq = os.path.join(ROOT, "profiles", "pmc_sq.json")
     if slot == "mask" and os.path.exists(sq):
@@ -169,12 +176,23 @@ def roofline_from(ktimes, kt_steps, mb, pmc_key):
         "valu": valu,
         "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic,
+        "traffic_src": traffic_src,
         "kernel": slot, "avg_launch_us": round(avg_s * 1e6, 3),
         "event_raw_us": round(raw_s * 1e6, 3), "event_floor_us": round(floor_s * 1e6, 3),
         "launches_per_step": round(n / kt_steps, 3),
         "bytes_per_launch": round(mb[slot]),
         "per_kernel_us": {k: round(ktimes[k][0] * 1e3 / ktimes[k][1], 3) for k in singles},
     }
+
+
+def pmc_record(pmc_key):
+    """The committed PMC traffic of a workload (tools/pmc_traffic.py): {slot: record, "_step":
+    bytes per bench step}; {} when none was recorded."""
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        return json.load(open(pmc)).get(pmc_key, {}) or {}
+    except (OSError, ValueError):
+        return {}
 
 
 class DepthStream:
@@ -224,7 +242,15 @@ class DepthStream:
                                            *c.intrinsics(), c.T_world, c.T_crop)
         self.eng.processFrame(params, synchronous=True)
         items, runs = self.eng.last_sort_items()
-        return items / batch, runs
+        # the batch's sparse grid snapshots (frames but the last): 36 B per non-zero 32-cell group
+        np = self.np
+        snap = 0
+        for f in range(batch - 1):
+            g = self.eng.downloadBatchVoxelOccupancyGrid(f)
+            pad = (-len(g)) % 32
+            g32 = np.concatenate([g, np.zeros(pad, np.uint8)]).reshape(-1, 32)
+            snap += 36 * int(np.count_nonzero(g32.any(axis=1)))
+        return items / batch, runs, snap
 
     def run(self, pc, first, count, batch=1):
         """`count` steps of `batch` frames from frame `first * batch` on."""
@@ -273,8 +299,8 @@ def time_single(st, params, steps, warmup, depth, kernel_timing, pmc_key, batch=
     idx = [((prime + warmup + i) * batch + j) % st.ring for i in range(steps) for j in range(batch)]
     n_avg = float(np.mean([npts[i] for i in idx]))
     g_avg = float(np.mean([nvox[i] for i in idx]))
-    s_avg, runs = st.sort_items(params, batch)
-    mb = model_bytes(st.P, n_avg, g_avg, ncells, batch, s_avg, runs)
+    s_avg, runs, snap = st.sort_items(params, batch)
+    mb = model_bytes(st.P, n_avg, g_avg, ncells, batch, s_avg, runs, snap)
     roof = None
     if kernel_timing:
         kt_steps = min(steps, 200)
@@ -287,6 +313,14 @@ def time_single(st, params, steps, warmup, depth, kernel_timing, pmc_key, batch=
         roof = roofline_from(kt, kt_steps, mb, pmc_key)
     # SURVEY.md §8(d) B_alg per frame, times the frames of a step
     survey = batch * (2.0 * st.P + 24.0 * n_avg + 9.0 * ncells)
+    # bytes the step actually moves (PMC FETCH x2 + WRITE of every kernel of a steady step, one
+    # batch in flight, profiles/pmc_traffic.json) over the measured step time
+    step_pmc = pmc_record(pmc_key).get("_step", {}).get("hbm_bytes_per_step")
+    pmc_line = {}
+    if step_pmc:
+        gbps = step_pmc * steps / elapsed / 1e9
+        pmc_line = {"step_pmc_bytes": step_pmc, "step_pmc_GBps": round(gbps, 2),
+                    "step_pmc_frac": round(gbps / HBM_PEAK_GBPS, 4)}
     return {
         "value": round(st.P * batch * steps / elapsed / 1e6, 3),
         "ms_per_step": round(elapsed / steps * 1e3, 5),
@@ -298,6 +332,9 @@ def time_single(st, params, steps, warmup, depth, kernel_timing, pmc_key, batch=
         "step_survey_bytes": round(survey),
         "step_survey_GBps": round(survey * steps / elapsed / 1e9, 2),
         "step_survey_frac": round(survey * steps / elapsed / 1e9 / HBM_PEAK_GBPS, 4),
+        "step_survey_note": "SURVEY 8(d) B_alg (counts a u32 history this build never moves)",
+        **pmc_line,
+        "model_bytes_per_launch": {k: round(v) for k, v in mb.items()},
         "roofline": roof,
     }
 
