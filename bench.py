@@ -84,6 +84,9 @@ def parse():
     ap.add_argument("--no-secondary", action="store_true",
                     help="N = 1: skip the 720p / 4K / stress / H2D / C3 lines")
     ap.add_argument("--c3-window", type=int, default=256)
+    ap.add_argument("--rb-window", type=int, default=0,
+                    help="N > 1 fused mode: the last rank also runs a rollbuffer of this many "
+                         "720p point sequences, one new sequence per step (C5 with its rollbuffer)")
     return ap.parse_args()
 
 
@@ -529,28 +532,38 @@ def time_multi(args, st, params, dist, world, pmc_key):
     (gx, gy, gz), ncells = eng.grid_size()
     depth = 1
     fused = args.multi_mode == "fused"
+    rb = None
     if fused:
         from ros_gpu_depthmap_fusion_amd import synth
-        from ros_gpu_depthmap_fusion_amd.multi import FusedCloudRank
+        from ros_gpu_depthmap_fusion_amd.multi import FusedCloudRank, gather_fused_cloud
         rank = dist.get_rank()
         cams = [synth.make_camera(k, st.W, st.H) for k in range(world)]
-        fr = FusedCloudRank(eng, cams, rank, world, params,
-                            dev="cuda" if args.dist_backend == "nccl" else "cpu")
+        cuda = args.dist_backend == "nccl"
+        # pipelined steps (RCCL): `--pipeline` batches in the engine's slots, a step's points
+        # exchange finished while the next step computes
+        fr = FusedCloudRank(eng, cams, rank, world, params, dev="cuda" if cuda else "cpu",
+                            depth=max(1, min(4, args.pipeline)) if cuda else 1)
+        depth = fr.depth
         n = st.W * st.H
         B = max(1, args.batch)
+        if args.rb_window:
+            if B != 1:
+                raise SystemExit("--rb-window: frames carrying point sequences run one per step "
+                                 "(--batch 1)")
+            rb = RollbufferFeed(eng, args.rb_window, params) if fr.has_rollbuffer else None
+            params.ps_timespan = (args.rb_window - 0.5) / 30.0
+            fr.p = params
+            fr.pc = params.to_c(None, None, False, True, True)
+            fr._pc_move.clear()
 
-        from ros_gpu_depthmap_fusion_amd.multi import gather_fused_cloud
+        def ptrs(i):
+            return [st.dframes[0][(i * B + j) % st.ring].ptr for j in range(B)]
 
         def run(first, count):
-            for i in range(first, first + count):
-                if B > 1:  # a step = B frames through one launch chain and one exchange
-                    ds = [st.dframes[0][(i * B + j) % st.ring].ptr for j in range(B)]
-                    fr.batch(ds, [d + 2 * (n - fr.Lmax) for d in ds])
-                else:
-                    d = st.dframes[0][i % st.ring].ptr
-                    fr.frame(d, d + 2 * (n - fr.Lmax))
-                if args.publish:  # the fused cloud of the step on the publishing rank
-                    gather_fused_cloud(fr, root=0)
+            fr.run(count, lambda i: ptrs(first + i),
+                   lambda i: [d + 2 * (n - fr.Lmax) for d in ptrs(first + i)],
+                   move_of=(lambda i: rb.feed(first + i)) if rb is not None else None,
+                   on_finish=(lambda j: gather_fused_cloud(fr, root=0)) if args.publish else None)
     else:
         batched = args.exchange_batch > 1
         if batched:
@@ -584,6 +597,8 @@ def time_multi(args, st, params, dist, world, pmc_key):
         torch.cuda.synchronize()
 
     prime = 2 * depth + 2
+    if rb is not None:
+        rb.fill()  # the window's sequences before the first timed step
     run(0, prime)
     # (the settle of time_single, as a fixed step count: every rank must run the same number of
     # exchanges)
@@ -596,8 +611,10 @@ def time_multi(args, st, params, dist, world, pmc_key):
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64,
                      device="cuda" if args.dist_backend == "nccl" else "cpu")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    allt = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(allt, t)
+    per_rank = [round(float(x.item()) / args.steps * 1e3, 5) for x in allt]
+    elapsed = max(float(x.item()) for x in allt)  # (the max over ranks)
     fpb = max(1, args.batch) if fused else 1  # frames per step
     idx = [((prime + args.warmup + i) * fpb + j) % st.ring for i in range(args.steps)
            for j in range(fpb)]
@@ -609,12 +626,21 @@ def time_multi(args, st, params, dist, world, pmc_key):
         "ms_per_step": round(elapsed / args.steps * 1e3, 5), "prime": prime,
         "points_per_frame_after_crop": round(n_avg), "voxels_per_frame": round(g_avg),
         "grid": [gx, gy, gz], "grid_cells": ncells, "frames_in_flight": depth,
+        "ms_per_step_per_rank": per_rank,
         "roofline": None,
     }
+    if rb is not None or (fused and args.rb_window):
+        line["rollbuffer"] = {"window_sequences": args.rb_window, "rank": world - 1,
+                              "sequence_points": RollbufferFeed.POINTS,
+                              "note": "the last rank holds the rollbuffer (SURVEY 8(e)); "
+                                      "ms_per_step_per_rank shows the imbalance"}
     if not args.no_kernel_timing:
         kt_steps = min(args.steps, 100)
         if depth > 1:
+            eng.synchronize()
             eng.set_pipeline_depth(1)
+            if fused:
+                fr.depth = 1
         eng.set_profiling(True)
         run(prime + args.warmup, kt_steps)
         barrier_sync()
@@ -638,6 +664,39 @@ def time_multi(args, st, params, dist, world, pmc_key):
                "exchange": ("sparse mark pairs (cap %d words/frame), %d dense-fallback batches" %
                             (marks.cap, marks.dense_batches)) if batched else "bitmask per frame"}
     return line, cfg
+
+
+class RollbufferFeed:
+    """The point-sequence stream of the rollbuffer rank (C5 "full rollbuffer"): C3's sequences -
+    a 720p lidar frame back-projected, 921 600 points, T_move(k) = 0.01 k m along x, 30 per
+    second - device-resident PointCloud2 records (two, alternated) added one per step; fill()
+    ingests a full window first."""
+    POINTS = 1280 * 720
+
+    def __init__(self, eng, window, params):
+        import numpy as np
+        from ros_gpu_depthmap_fusion_amd import hiprt, synth
+        self.eng, self.window, self.synth = eng, window, synth
+        self.lidar = synth.make_camera(1, 1280, 720)
+        recs = [np.concatenate([synth.back_project(self.lidar, synth.dense_frame(self.lidar, 1, f)),
+                                np.ones((self.POINTS, 1), np.float32)], 1) for f in range(2)]
+        self.dev = [hiprt.DeviceArray.from_numpy(r) for r in recs]
+        self.k = 0
+
+    def _add(self):
+        s, ns = self.synth.sequence_time(self.k)
+        self.eng.addPointSequenceDevice(self.dev[self.k % 2].ptr, self.POINTS, 16, s, ns,
+                                        self.synth.move_transform(self.k))
+        self.k += 1
+
+    def fill(self):
+        for _ in range(self.window - 1):
+            self._add()
+
+    def feed(self, i):
+        """Step i: one new sequence, and the move transforms of the frame."""
+        self._add()
+        return (self.lidar.T_world, self.lidar.T_crop)
 
 
 def run_alternating(args, params, steps, warm):

@@ -33,9 +33,10 @@ extern "C" {
 /* ABI version: gdf_frame_params and the signatures below are exactly those of this version; a
  * caller checks gdf_version() against the header it was built with (the Python binding and the
  * C++ facade do).  0.2: gdf_frame_params.defer_voxelize, frames_per_rank of
- * gdf_union_occupancy_pairs; 0.3: batched take / sparse per-frame grids. */
+ * gdf_union_occupancy_pairs; 0.3: batched take / sparse per-frame grids; 0.4: slot selection
+ * (gdf_get_slot / gdf_select_slot), build provenance (gdf_build_info). */
 #define GDF_VERSION_MAJOR 0
-#define GDF_VERSION_MINOR 3
+#define GDF_VERSION_MINOR 4
 
 #define GDF_MAX_CAMERAS 16
 
@@ -120,6 +121,9 @@ int gdf_create(int device, gdf_engine** out_engine);
 int gdf_destroy(gdf_engine* engine);
 const char* gdf_last_error(void);
 int gdf_version(int* major, int* minor);
+/* Build provenance (no reference counterpart): "source_sha=<digest of the sources the library
+ * was compiled from>;built_on=<host>;built_at=<UTC time>" - which build a process loaded. */
+const char* gdf_build_info(void);
 /* Use a caller-owned hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL restores
  * the engine's own stream. */
 int gdf_set_stream(gdf_engine* engine, void* hip_stream);
@@ -133,6 +137,15 @@ int gdf_get_stream(gdf_engine* engine, void** out_stream);
  * frame are read (downloads, gdf_get_device_results) before the next gdf_clear.  Call between
  * frames; not available with gdf_set_stream. */
 int gdf_set_pipeline_depth(gdf_engine* engine, int depth);
+/* The slot the engine's calls address (after gdf_clear: the new frame's), and its re-selection:
+ * the follow-up calls of a frame still resident in its slot (gdf_take_occupancy_marks,
+ * gdf_partition_points, gdf_voxelize_points, downloads) after later frames were started on other
+ * slots - the multi-GPU exchange finishes batch b while batch b + 1 computes.  gdf_get_stream then
+ * names that slot's stream.  The next gdf_clear continues the rotation after the most recently
+ * cleared slot, whatever slot is selected.  (No reference counterpart: the reference runs one
+ * frame at a time.) */
+int gdf_get_slot(gdf_engine* engine, int* slot);
+int gdf_select_slot(gdf_engine* engine, int slot);
 /* Steady-state frames of gdf_process_frame as HIP graphs (default on; env GDF_NO_GRAPHS turns
  * the default off): when a slot's frame repeats the launch arguments of its previous frame (all
  * but the depth pointers and the grid ticket) the frame's launches are captured once and then

@@ -286,7 +286,8 @@ bool ros_time_minus(uint32_t sec, uint32_t nsec, double seconds, uint32_t* os, u
 
 enum MiscSlot {
     kCount = 0, kTileCtr = 1, kErr = 2, kVoxCount = 3, kGridTicket = 4, kDepthCount = 5,
-    kSelTotal = 6, kPartTotal = 7, kRecvCount = 8, kRunCount = 9, kScanTotal = 10, kRunTotal = 11, kMiscWords = 16
+    kSelTotal = 6, kPartTotal = 7, kRecvCount = 8, kRunCount = 9, kScanTotal = 10, kRunTotal = 11,
+    kRecvRuns = 12, kMiscWords = 16
 };
 
 }  // namespace
@@ -332,6 +333,7 @@ struct Slot {
     bool snap_valid = false;
     uint32_t snap_blocks = 0, snap_frames = 0;
     DevBuf d_pcnt, d_poff;          // multi-GPU key-range partition workspace
+    DevBuf d_xcnt, d_xoff, d_xrk, d_xrs;  // runs of a received (point, key) list
     DevBuf d_wruns, d_runkeys, d_runstart;  // runs of equal keys
     bool runs_sel = false;          // ... counted in kRunTotal (frame with rollbuffer points)
     bool runs_valid = false;        // this frame's voxelize may sort runs
@@ -386,6 +388,7 @@ struct gdf_engine {
     // frame slots: per-frame buffers on their own streams (pipeline depth 1..kMaxPipe)
     Slot slots[kMaxPipe];
     int cur = 0;
+    int ring = 0;  // slot of the most recent gdf_clear (gdf_select_slot moves cur, not ring)
     int npipe = 1;
     hipStream_t user_stream = nullptr;  // gdf_set_stream: single slot on the caller's stream
     bool serialized = false;            // this frame already waits for the previous one
@@ -450,6 +453,7 @@ struct gdf_engine {
     bool use_runs = !getenv("GDF_NO_RUNS");      // voxelize runs of equal keys (depth frames)
     bool force_runs = getenv("GDF_FORCE_RUNS") != nullptr;    // tuning knob: runs at every size
     bool run_hist_in_sort = getenv("GDF_RUN_HIST_SORT") != nullptr;  // tuning knob
+    bool xruns = !getenv("GDF_NO_XRUNS");  // voxelize_points sorts the received list's runs
 
     // compaction outputs
 
@@ -594,7 +598,8 @@ void sync_all(gdf_engine* e) {
 // frame boundary (gdf_clear): the next frame goes to the next slot
 void next_slot(gdf_engine* e) {
     if (e->npipe <= 1) return;
-    e->cur = (e->cur + 1) % e->npipe;
+    e->ring = (e->ring + 1) % e->npipe;
+    e->cur = e->ring;
     e->serialized = false;
 }
 
@@ -1196,8 +1201,11 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel, bool compaction_marks = fa
         // costs what the shorter sort saves, so frames under 1 Mi pixels sort points)
         // Rollbuffer windows (10^7 points re-observing the same voxels) always sort runs: k_sel
         // counts them per tile.
-        a.run_mode = e->use_runs && (a.sel_tiles || (a.total_segs && (e->force_runs ||
-                                                                      a.depth_total >= (1u << 20))))
+        // (a deferred voxelize - the multi-GPU exchange - sorts what the rank RECEIVES, whose runs
+        // gdf_voxelize_points finds itself: the compaction counts none)
+        a.run_mode = e->use_runs && !compaction_marks &&
+                             (a.sel_tiles || (a.total_segs && (e->force_runs ||
+                                                               a.depth_total >= (1u << 20))))
                          ? 1 : 0;
         // the run-key digits: k_mask's per-segment flush while there are few segments; above,
         // k_sort_hist over the runs (tens of thousands of flushes contend at the atomic units)
@@ -1304,6 +1312,8 @@ struct VoxSource {
     const float4* pts = nullptr;
     const uint32_t* keys = nullptr;
     uint32_t n = 0;
+    const uint32_t* run_keys = nullptr;  // its runs of equal keys (launch_xruns), or none
+    const uint32_t* run_start = nullptr;
 };
 
 // the slot's sparse snapshot buffers for a grid update of `nblocks` blocks over `nframes` frames
@@ -1353,7 +1363,13 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime,
     v.keys = e->sl().d_coords.as<uint32_t>();
     v.pts = e->sl().d_pts.as<float4>();
     v.count = e->sl().d_misc.as<uint32_t>() + kCount;
-    if (src) {
+    if (src && src->run_keys) {  // the received list's runs (gdf_voxelize_points)
+        v.keys = src->run_keys;
+        v.pts = src->pts;
+        v.count = e->sl().d_misc.as<uint32_t>() + kRecvRuns;
+        v.run_start = src->run_start;
+        v.point_count = e->sl().d_misc.as<uint32_t>() + kRecvCount;
+    } else if (src) {
         v.keys = src->keys;
         v.pts = src->pts;
         v.count = e->sl().d_misc.as<uint32_t>() + kRecvCount;
@@ -1715,8 +1731,29 @@ int gdf_set_stream(gdf_engine* e, void* stream) {
         e->user_stream = static_cast<hipStream_t>(stream);
         if (stream) {  // the caller orders frames on its own stream: one slot
             e->npipe = 1;
-            e->cur = 0;
+            e->cur = e->ring = 0;
         }
+    });
+}
+
+#ifndef GDF_BUILD_INFO
+#define GDF_BUILD_INFO "source_sha=unknown"
+#endif
+const char* gdf_build_info(void) { return GDF_BUILD_INFO; }
+
+int gdf_get_slot(gdf_engine* e, int* slot) {
+    ENGINE_OR_FAIL(e);
+    if (!slot) return GDF_ERR_ARG;
+    *slot = e->cur;
+    return GDF_OK;
+}
+
+int gdf_select_slot(gdf_engine* e, int slot) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        if (slot < 0 || slot >= e->npipe) fail(GDF_ERR_ARG, "select_slot: no such pipeline slot");
+        e->cur = slot;
+        e->serialized = false;
     });
 }
 
@@ -1742,6 +1779,7 @@ int gdf_set_pipeline_depth(gdf_engine* e, int depth) {
         // a configuration call between frames: the next frame starts on slot 0 (a shallower
         // pipeline does not keep the results of the frame that was current)
         if (e->cur >= depth) e->cur = 0;
+        e->ring = e->cur;
         if (e->grid_alloc) {  // restart the grid-update sequence (nothing in flight)
             HIPCHK(hipMemset(e->d_gridctl.p, 0, 64));
             e->grid_ticket = 0;
@@ -2197,6 +2235,19 @@ int gdf_voxelize_points(gdf_engine* e, const float* pts, const uint32_t* keys, u
         src.pts = reinterpret_cast<const float4*>(pts);
         src.keys = keys;
         src.n = n;
+        if (e->xruns && n) {  // sort the list's runs of equal keys, not its points
+            Slot& q = e->sl();
+            const uint32_t tiles = std::max<uint32_t>(xrun_tiles(n), 1u);
+            q.d_xcnt.ensure((size_t)tiles * 4);
+            q.d_xoff.ensure(seg_offsets_words(tiles) * 4);
+            q.d_xrk.ensure((size_t)n * 4);
+            q.d_xrs.ensure(((size_t)n + 1) * 4);
+            HIPCHK(launch_xruns(keys, q.d_misc.as<uint32_t>() + kRecvCount, n, q.d_xcnt.as<uint32_t>(),
+                                q.d_xoff.as<uint32_t>(), q.d_xrk.as<uint32_t>(), q.d_xrs.as<uint32_t>(),
+                                q.d_misc.as<uint32_t>() + kRecvRuns, e->s()));
+            src.run_keys = q.d_xrk.as<uint32_t>();
+            src.run_start = q.d_xrs.as<uint32_t>();
+        }
         const VoxelizeArgs v = voxelize_args(e, average, -1, &src);
         e->timed(GDF_KERNEL_VOXELIZE, [&] { HIPCHK(launch_voxelize(v, e->s(), e->hook_ptr())); });
         e->sl().khist_pending = false;

@@ -3911,6 +3911,113 @@ hipError_t launch_partition(const float4* pts, const uint32_t* keys, const uint3
     return hipGetLastError();
 }
 
+// ---- runs of equal keys in an external (point, key) list -----------------------------------------
+// What a rank received in the fused-cloud exchange (every source's points of the rank's key range,
+// stable) keeps each camera's runs of equal keys (consecutive kept pixels of one voxel, ~10 points
+// each on dense frames): found here, the voxelize sorts runs instead of points (k_group_runs sums
+// each voxel's runs in run order = point order, the same sequential chain).  Tiles of 4096 keys,
+// 16 contiguous keys per thread; a leader is a key that differs from the one before it.  Counts
+// per tile -> launch_scan -> emit (run key, first point); the last tile closes run_start[R] = n.
+constexpr uint32_t kXRunTile = 4096;
+
+__device__ __forceinline__ uint32_t xrun_leaders(const uint32_t* __restrict__ keys, uint32_t n,
+                                                 uint32_t i0, bool vec, uint32_t (&k)[16]) {
+    if (vec && i0 + 16u <= n) {
+        const uint4* k4 = reinterpret_cast<const uint4*>(keys + i0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint4 v = k4[q];
+            k[4 * q] = v.x;
+            k[4 * q + 1] = v.y;
+            k[4 * q + 2] = v.z;
+            k[4 * q + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) k[j] = i0 + j < n ? keys[i0 + j] : 0u;
+    }
+    if (i0 >= n) return 0u;
+    uint32_t prev = i0 ? keys[i0 - 1] : ~k[0];
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        m |= (uint32_t)((i0 + j < n) & (k[j] != prev)) << j;
+        prev = k[j];
+    }
+    return m;
+}
+
+__global__ __launch_bounds__(256) void k_xruns_count(const uint32_t* __restrict__ keys,
+                                                     const uint32_t* __restrict__ count,
+                                                     uint32_t nmax, int vec,
+                                                     uint32_t* __restrict__ tcounts) {
+    __shared__ uint32_t s_w[4];
+    const uint32_t n = min(*count, nmax);
+    if (blockIdx.x * kXRunTile >= n) return;  // (tiles past n are not scanned)
+    uint32_t k[16];
+    const uint32_t m = xrun_leaders(keys, n, blockIdx.x * kXRunTile + threadIdx.x * 16u, vec != 0, k);
+    uint32_t c = (uint32_t)__popc(m);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) tcounts[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+
+__global__ __launch_bounds__(256) void k_xruns_emit(const uint32_t* __restrict__ keys,
+                                                    const uint32_t* __restrict__ count,
+                                                    uint32_t nmax, int vec,
+                                                    const uint32_t* __restrict__ offsets,
+                                                    const uint32_t* __restrict__ total,
+                                                    uint32_t* __restrict__ run_keys,
+                                                    uint32_t* __restrict__ run_start) {
+    __shared__ uint32_t s_w[4];
+    const uint32_t n = min(*count, nmax);
+    const uint32_t last = n ? (n - 1u) / kXRunTile : 0u;  // the tile that closes the run list
+    if (blockIdx.x > last) return;
+    if (blockIdx.x == last && threadIdx.x == 0) run_start[*total] = n;
+    if (n == 0) return;
+    const uint32_t i0 = blockIdx.x * kXRunTile + threadIdx.x * 16u;
+    uint32_t k[16];
+    uint32_t m = xrun_leaders(keys, n, i0, vec != 0, k);
+    const uint32_t c = (uint32_t)__popc(m);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t x = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_w[wid] = x;
+    __syncthreads();
+    uint32_t pos = offsets[blockIdx.x] + x - c;
+    for (int w = 0; w < wid; ++w) pos += s_w[w];
+    while (m) {
+        const int j = __builtin_ctz(m);
+        m &= m - 1u;
+        run_keys[pos] = k[j];
+        run_start[pos] = i0 + (uint32_t)j;
+        ++pos;
+    }
+}
+
+uint32_t xrun_tiles(uint32_t nmax) { return (nmax + kXRunTile - 1) / kXRunTile; }
+
+hipError_t launch_xruns(const uint32_t* keys, const uint32_t* count, uint32_t nmax,
+                        uint32_t* tcounts, uint32_t* offsets, uint32_t* run_keys,
+                        uint32_t* run_start, uint32_t* run_total, hipStream_t s) {
+    const uint32_t tiles = std::max<uint32_t>(xrun_tiles(nmax), 1u);
+    const int vec = (reinterpret_cast<uintptr_t>(keys) & 15u) == 0;
+    hipLaunchKernelGGL(k_xruns_count, dim3(tiles), dim3(256), 0, s, keys, count, nmax, vec, tcounts);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if ((e = launch_scan(tcounts, tiles, offsets, run_total, count, kXRunTile, s)) != hipSuccess)
+        return e;
+    hipLaunchKernelGGL(k_xruns_emit, dim3(tiles), dim3(256), 0, s, keys, count, nmax, vec, offsets,
+                       (const uint32_t*)run_total, run_keys, run_start);
+    return hipGetLastError();
+}
+
 // ---- multi-GPU occupancy marks -------------------------------------------------------------------
 // The engine's marks already are the exchange format (1 bit per cell): export is a copy, import
 // ORs the all-gathered masks of every rank into them.

@@ -174,6 +174,14 @@ hipError_t launch_partition(const float4* pts, const uint32_t* keys, const uint3
                             const uint32_t* fstart = nullptr, uint32_t nframes = 1,
                             uint32_t fshift = 0);
 
+// runs of equal keys in an external key list of *count (<= nmax) keys (the multi-GPU receive
+// buffer): run_keys[r], run_start[r] (first item; run_start[R] = n), *run_total = R.  Workspace:
+// tcounts [xrun_tiles(nmax)], offsets [seg_offsets_words(xrun_tiles(nmax))].
+uint32_t xrun_tiles(uint32_t nmax);
+hipError_t launch_xruns(const uint32_t* keys, const uint32_t* count, uint32_t nmax,
+                        uint32_t* tcounts, uint32_t* offsets, uint32_t* run_keys,
+                        uint32_t* run_start, uint32_t* run_total, hipStream_t s);
+
 // multi-GPU occupancy marks: export = copy of the mark bitmask, import = OR of nranks masks
 hipError_t launch_export_marks(const uint32_t* marks, uint64_t words, uint32_t* bits, hipStream_t s);
 hipError_t launch_take_marks(uint32_t* marks, uint64_t words, uint32_t* bits, hipStream_t s);

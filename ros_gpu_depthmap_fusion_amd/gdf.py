@@ -131,7 +131,7 @@ EXPORTED = [
     "gdf_next_frame_in_batch", "gdf_get_batch_ranges", "gdf_download_batch_occupancy_grid",
     "gdf_mask_dilate", "gdf_transform_points", "gdf_add_halo_depthmap_device",
     "gdf_partition_points", "gdf_voxelize_points", "gdf_last_sort_items", "gdf_get_stream",
-    "gdf_get_graph_stats",
+    "gdf_get_graph_stats", "gdf_get_slot", "gdf_select_slot", "gdf_build_info",
     # include/gdf_segment.h: the GPU object-segmentation front end
     "gdf_seg_create", "gdf_seg_destroy", "gdf_seg_set_stream", "gdf_seg_label_layers",
     "gdf_seg_label_engine_grid", "gdf_seg_get_counts", "gdf_seg_download_labels",
@@ -141,7 +141,7 @@ EXPORTED = [
 ]
 
 
-ABI_VERSION = (0, 3)  # include/gdf.h GDF_VERSION_MAJOR / _MINOR
+ABI_VERSION = (0, 4)  # include/gdf.h GDF_VERSION_MAJOR / _MINOR
 
 
 def load_library(path: str = LIB_PATH):
@@ -225,6 +225,9 @@ def load_library(path: str = LIB_PATH):
         "gdf_last_sort_items": (i32, [vp, P(u32), P(i32)]),
         "gdf_get_stream": (i32, [vp, P(vp)]),
         "gdf_get_graph_stats": (i32, [vp, P(u64), P(u64)]),
+        "gdf_get_slot": (i32, [vp, P(i32)]),
+        "gdf_select_slot": (i32, [vp, i32]),
+        "gdf_build_info": (C.c_char_p, []),
         "gdf_seg_create": (i32, [i32, P(vp)]),
         "gdf_seg_destroy": (i32, [vp]),
         "gdf_seg_set_stream": (i32, [vp, vp]),
@@ -249,8 +252,26 @@ def load_library(path: str = LIB_PATH):
     if (major.value, minor.value) != ABI_VERSION:  # the structs below are those of ABI_VERSION
         raise GDFError(-2, f"{path}: ABI {major.value}.{minor.value}, binding expects "
                            f"{ABI_VERSION[0]}.{ABI_VERSION[1]} (rebuild the library)")
+    info = build_info(lib)
+    from .build import source_digest
+    want = source_digest()
+    if want is not None and info.get("source_sha") != want:  # sources present: must match
+        raise GDFError(-2, f"{path} was built from other sources (library {info.get('source_sha')}, "
+                           f"tree {want}): rebuild it (build_library())")
     _lib = lib
     return lib
+
+
+def build_info(lib=None) -> dict:
+    """Provenance stamped into libgdf.so at compile time (gdf_build_info): the digest of the
+    sources it was built from, the host that compiled it and when."""
+    lib = lib or load_library()
+    out = {}
+    for kv in lib.gdf_build_info().decode().split(";"):
+        if "=" in kv:
+            k, v = kv.split("=", 1)
+            out[k] = v
+    return out
 
 
 def _ptr(a: Optional[np.ndarray]):
@@ -364,6 +385,22 @@ class GPUDepthmapFusion:
 
     def synchronize(self):
         self._check(self._lib.gdf_synchronize(self._h))
+
+    def slot(self) -> int:
+        """The pipeline slot the engine's calls address (gdf_get_slot)."""
+        k = C.c_int(0)
+        self._check(self._lib.gdf_get_slot(self._h, C.byref(k)))
+        return k.value
+
+    def select_slot(self, slot: int):
+        """Address the frame still resident in `slot` (gdf_select_slot)."""
+        self._check(self._lib.gdf_select_slot(self._h, slot))
+
+    def stream(self) -> int:
+        """The HIP stream of the addressed slot (gdf_get_stream), as an integer handle."""
+        s = C.c_void_p()
+        self._check(self._lib.gdf_get_stream(self._h, C.byref(s)))
+        return s.value or 0
 
     def set_debug(self, on: bool = True):
         self._check(self._lib.gdf_set_debug(self._h, 1 if on else 0))

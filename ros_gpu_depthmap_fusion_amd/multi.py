@@ -228,23 +228,82 @@ def exchange_points_dev(send_pts, send_keys, send_counts, group=None):
     return rp, rk, rcounts, scounts
 
 
+class _SlotExchange:
+    """Device / pinned buffers of the batch in flight on one engine slot (RCCL path): kept for the
+    rank's lifetime so a collective on the slot's stream never reads memory the caching allocator
+    handed to someone else; grown (after the slot's stream drained) when a batch needs more."""
+
+    def __init__(self, world: int):
+        import torch
+        self.world = world
+        self.cap = 0          # send capacity (points)
+        self.rcap = 0         # receive capacity (points)
+        self.mcap = 0         # mark words
+        self.tcap = 0         # halo tail bytes
+        self.cnt = torch.zeros(world, dtype=torch.int32, device="cuda")
+        self.c64 = torch.zeros(world, dtype=torch.int64, device="cuda")
+        self.rc = torch.zeros(world, dtype=torch.int64, device="cuda")
+        self.host = torch.zeros(2 * world, dtype=torch.int64, pin_memory=True)
+        self.ev = torch.cuda.Event()
+        self.pending = False
+
+    def ensure(self, stream, n_send=0, n_recv=0, mark_words=0, tail_bytes=0):
+        import torch
+        grow = (n_send > self.cap or n_recv > self.rcap or mark_words > self.mcap or
+                tail_bytes > self.tcap)
+        if not grow:
+            return
+        stream.synchronize()  # the slot's previous batch no longer reads the old buffers
+        if n_send > self.cap:
+            self.cap = max(n_send, self.cap + self.cap // 2)
+            self.sp = torch.empty((self.cap, 4), dtype=torch.float32, device="cuda")
+            self.sk = torch.empty(self.cap, dtype=torch.int32, device="cuda")
+        if n_recv > self.rcap:
+            self.rcap = max(n_recv, self.rcap + self.rcap // 2)
+            self.rp = torch.empty((self.rcap, 4), dtype=torch.float32, device="cuda")
+            self.rk = torch.empty(self.rcap, dtype=torch.int32, device="cuda")
+        if mark_words > self.mcap:
+            self.mcap = mark_words
+            self.local = torch.empty(mark_words, dtype=torch.int32, device="cuda")
+            self.gathered = torch.empty(self.world * mark_words, dtype=torch.int32, device="cuda")
+        if tail_bytes > self.tcap:
+            self.tcap = tail_bytes
+            self.tail = torch.empty(tail_bytes, dtype=torch.uint8, device="cuda")
+            self.tails = torch.empty(self.world * tail_bytes, dtype=torch.uint8, device="cuda")
+
+
 class FusedCloudRank:
     """One rank of the multi-GPU frame with the reference's fused output, over a GPU engine.
 
-    Per frame: (halo) all-gather of the depth tails -> the rank's camera with camera k-1's tail
-    as halo -> compaction + keys + marks (defer_voxelize, deferred grid) -> occupancy-mark union
-    (all-gather + OR) and the identical grid update on every rank -> key-range partition ->
-    all-to-all -> voxelize of the rank's key range.  Collectives run on torch tensors of `dev`
-    ("cuda": RCCL, the engine on torch's stream; "cpu": gloo, staged through host copies)."""
+    Per step (one frame, or a batch of B frames through one launch chain): (halo) all-gather of
+    the depth tails -> the rank's camera with camera k-1's tail as halo -> compaction + keys +
+    marks (defer_voxelize, deferred grid) -> occupancy-mark union (all-gather) and the identical
+    batched grid update on every rank -> key-range partition -> all-to-all -> voxelize of the
+    rank's key range (the received list's runs of equal keys).  Collectives run on torch tensors
+    of `dev` ("cuda": RCCL; "cpu": gloo, staged through host copies).
 
-    def __init__(self, engine, cams, rank: int, world: int, params, dev: str = "cuda"):
+    RCCL path, pipelined (start / finish): the engine keeps `depth` batches in its pipeline slots,
+    each slot's work and collectives on the slot's own stream.  start() runs a batch up to the
+    all-to-all of its split sizes and queues their copy to pinned memory; finish() - called after
+    the NEXT batch was started, so the GPU is busy while the host reads the sizes - runs the
+    points all-to-all and the voxelize on the batch's slot.  The points travel on a second
+    communicator (its own RCCL stream), so batch b's exchange never queues behind batch b + 1's
+    mark / count collectives."""
+
+    def __init__(self, engine, cams, rank: int, world: int, params, dev: str = "cuda",
+                 depth: int = 1):
         import torch
+        import torch.distributed as dist
         from . import hiprt
         self.eng, self.cams, self.rank, self.world, self.p = engine, cams, rank, world, params
         self.dev = dev
         self.hiprt = hiprt
+        self.depth = max(1, int(depth)) if dev == "cuda" else 1
         if dev == "cuda":
-            engine.set_stream(torch.cuda.current_stream().cuda_stream)
+            engine.set_pipeline_depth(self.depth)
+            self.slots = {}
+            # the points' communicator: its own RCCL stream (see the class docstring)
+            self.pg_points = dist.new_group(list(range(world))) if world > 1 else None
         self.F = params.flying_filter_size
         # every rank sends the same number of tail values: the deepest read of any camera
         self.Lmax = max(halo_pixels(self.F, cams[k].width) for k in range(world))
@@ -261,6 +320,8 @@ class FusedCloudRank:
         self.rollbuffer_rank = world - 1
         self.has_rollbuffer = rank == self.rollbuffer_rank
         self._pc_move = {}  # to_c of the frames with move transforms (rollbuffer rank)
+        self._staged = {}   # gloo path: the host-staged lists of a started batch
+        self._keep = []
 
     def frame_params(self, move=None):
         """The frame's gdf_frame_params: `move` = (T_world_move, T_crop_move) when the component's
@@ -276,187 +337,191 @@ class FusedCloudRank:
             pc = self._pc_move[key] = self.p.to_c(move[0], move[1], False, True, True)
         return pc
 
+    # ---- one step, synchronous -------------------------------------------------------------------
     def frame(self, depth_ptr: int, tail_src_ptr: int, move=None):
         """One frame: depth_ptr = this rank's depth map (device), tail_src_ptr = its last
         Lmax depth values (device, the halo the next rank needs).  On the rollbuffer rank the
         point sequences added to the engine since the last frame (addPointSequence[Device]) are
         ingested, rolled and - with `move` - selected, transformed, cropped and compacted behind
-        the camera's points."""
-        import numpy as np
-        import torch
-        import torch.distributed as dist
-        h = self.hiprt
-        eng, c = self.eng, self.cams[self.rank]
-        halo = None
-        if self.F > 0 and self.world > 1:
-            # all ranks send Lmax values (the tail of their camera); rank k uses rank k-1's
-            # (bytes: gloo has no 16-bit integer collectives)
-            if self.dev == "cuda":
-                tail = torch.empty(2 * self.Lmax, dtype=torch.uint8, device="cuda")
-                h.copy_async(tail.data_ptr(), tail_src_ptr, 2 * self.Lmax, h.D2D,
-                             torch.cuda.current_stream().cuda_stream)
-                parts = all_gather_tails(tail)
-                halo = parts[self.rank - 1] if self.rank > 0 else None
-                halo_ptr = halo.data_ptr() if halo is not None else 0
-            else:
-                tail = torch.from_numpy(_d2h(h, tail_src_ptr, np.uint8, 2 * self.Lmax))
-                parts = all_gather_tails(tail)
-                if self.rank > 0:
-                    halo = h.DeviceArray.from_numpy(parts[self.rank - 1].numpy())
-                    halo_ptr = halo.ptr
-        eng.clear()
-        if self.rank > 0 and halo is not None:
-            pc = self.cams[self.rank - 1]
-            n = pc.width * pc.height
-            take = min(self.Lmax, n)
-            # the received tail holds camera k-1's last Lmax values (or all of a smaller camera)
-            eng.addHaloDepthmapDevice(halo_ptr + 2 * (self.Lmax - take), take, pc.width,
-                                      pc.height, *pc.intrinsics(), pc.T_world, pc.T_crop)
-        eng.addDepthmapDevice(depth_ptr, c.width, c.height, *c.intrinsics(), c.T_world, c.T_crop)
-        res = eng.processFramePrepared(self.frame_params(move))
-        _, ncells = eng.grid_size()
-        words = words_for(ncells)
-        # occupancy union (every rank the same grid)
-        if self.dev == "cuda":
-            local = torch.empty(words, dtype=torch.int32, device="cuda")
-            gathered = torch.empty(self.world * words, dtype=torch.int32, device="cuda")
-            eng.export_marks(local.data_ptr(), words)
-            dist.all_gather_into_tensor(gathered, local)
-            eng.import_marks(gathered.data_ptr(), words, self.world)
-        else:
-            dl = h.DeviceArray(words * 4)
-            eng.export_marks(dl.ptr, words)
-            eng.synchronize()
-            local = torch.from_numpy(dl.to_numpy(np.int32, words))
-            parts = [torch.empty_like(local) for _ in range(self.world)]
-            dist.all_gather(parts, local)
-            dg = h.DeviceArray.from_numpy(torch.cat(parts).numpy())
-            eng.import_marks(dg.ptr, words, self.world)
-        eng.voxelOccupancyGrid(self.p.occupancy_lifetime)
-        # key-range partition + all-to-all + voxelize of this rank's range (send buffers for the
-        # frame's depth pixels + selected rollbuffer points)
-        n_total = max(int(res.num_points_total), 1)
-        if self.dev == "cuda":
-            sp = torch.empty((n_total, 4), dtype=torch.float32, device="cuda")
-            sk = torch.empty(n_total, dtype=torch.int32, device="cuda")
-            cnt = torch.empty(self.world, dtype=torch.int32, device="cuda")
-            eng.partition_points(self.world, sp.data_ptr(), sk.data_ptr(), n_total, cnt.data_ptr())
-            rp, rk, rc, counts = exchange_points_dev(sp, sk, cnt)
-            eng.voxelize_points(rp.data_ptr(), rk.data_ptr(), int(sum(rc)), self.p.voxel_average)
-            self._keep = (rp, rk)
-        else:
-            dsp, dsk, dcnt = h.DeviceArray(n_total * 16), h.DeviceArray(n_total * 4), h.DeviceArray(64)
-            eng.partition_points(self.world, dsp.ptr, dsk.ptr, n_total, dcnt.ptr)
-            eng.synchronize()
-            counts = dcnt.to_numpy(np.uint32, self.world).tolist()
-            m = int(sum(counts))
-            sp = torch.from_numpy(dsp.to_numpy(np.float32, 4 * max(m, 1))[:4 * m].reshape(m, 4))
-            sk = torch.from_numpy(dsk.to_numpy(np.int32, max(m, 1))[:m])
-            rp, rk, rc = exchange_points(sp, sk, counts)
-            n = int(sum(rc))
-            drp = h.DeviceArray.from_numpy(rp.numpy()) if n else None
-            drk = h.DeviceArray.from_numpy(rk.numpy()) if n else None
-            eng.voxelize_points(drp.ptr if n else 0, drk.ptr if n else 0, n, self.p.voxel_average)
-            eng.synchronize()
-            self._keep = (drp, drk)
-        return counts
-
+        the camera's points.  Returns the send counts per rank."""
+        return self.finish(self.start([depth_ptr], [tail_src_ptr], move))
 
     def batch(self, depth_ptrs, tail_src_ptrs):
-        """B frames through one launch chain and ONE exchange (the bench's batched steps): every
-        rank's B tails in one all-gather (frame j's halo before frame j's depth map), the batch's
-        compaction, the B frames' marks in one all-gather and one batched grid update
-        (gdf_voxel_occupancy_grid_batch: frame by frame in order), the (point, frame | key)
-        lists partitioned by voxel-key range and exchanged once, and one voxelize of the rank's
-        range - frame f's voxels of this range are eng.batch_ranges()[1][f:f+2]."""
-        import numpy as np
+        """B frames through one launch chain and ONE exchange: every rank's B tails in one
+        all-gather (frame j's halo before frame j's depth map), the batch's compaction, the B
+        frames' marks in one all-gather and one batched grid update (frame by frame in order),
+        the (point, frame | key) lists partitioned by voxel-key range and exchanged once, and one
+        voxelize of the rank's range - frame f's voxels of this range are
+        eng.batch_ranges()[1][f:f+2]."""
+        return self.finish(self.start(depth_ptrs, tail_src_ptrs))
+
+    # ---- pipelined halves ---------------------------------------------------------------------
+    def _slot(self, k):
+        if k not in self.slots:
+            self.slots[k] = _SlotExchange(self.world)
+        return self.slots[k]
+
+    def start(self, depth_ptrs, tail_src_ptrs, move=None):
+        """Starts a step (1 frame or a batch) on the engine's next slot: everything up to the
+        split sizes of the points all-to-all.  Returns the slot for finish()."""
         import torch
         import torch.distributed as dist
         h = self.hiprt
         eng, c = self.eng, self.cams[self.rank]
         B = len(depth_ptrs)
         L2 = 2 * self.Lmax
-        halo_ptr = None
-        keep = []
-        if self.F > 0 and self.world > 1:
-            if self.dev == "cuda":
-                tail = torch.empty(B * L2, dtype=torch.uint8, device="cuda")
-                stream = torch.cuda.current_stream().cuda_stream
-                for j, src in enumerate(tail_src_ptrs):
-                    h.copy_async(tail.data_ptr() + j * L2, src, L2, h.D2D, stream)
-                parts = all_gather_tails(tail)
-                if self.rank > 0:
-                    keep.append(parts[self.rank - 1])
-                    halo_ptr = parts[self.rank - 1].data_ptr()
-            else:
-                tail = torch.from_numpy(np.concatenate(
-                    [_d2h(h, src, np.uint8, L2) for src in tail_src_ptrs]))
-                parts = all_gather_tails(tail)
-                if self.rank > 0:
-                    dh = h.DeviceArray.from_numpy(parts[self.rank - 1].numpy())
-                    keep.append(dh)
-                    halo_ptr = dh.ptr
+        halo = self.F > 0 and self.world > 1
         eng.clear()
-        for j in range(B):
-            if j:
-                eng.nextFrameInBatch()
-            if halo_ptr is not None:
-                pc = self.cams[self.rank - 1]
-                take = min(self.Lmax, pc.width * pc.height)
-                eng.addHaloDepthmapDevice(halo_ptr + j * L2 + 2 * (self.Lmax - take), take,
-                                          pc.width, pc.height, *pc.intrinsics(), pc.T_world,
-                                          pc.T_crop)
-            eng.addDepthmapDevice(depth_ptrs[j], c.width, c.height, *c.intrinsics(), c.T_world,
-                                  c.T_crop)
-        eng.processFramePrepared(self.pc)
-        _, ncells = eng.grid_size()
-        words = words_for(ncells)
+        k = eng.slot() if self.dev == "cuda" else 0
         if self.dev == "cuda":
-            local = torch.empty(B * words, dtype=torch.int32, device="cuda")
-            gathered = torch.empty(self.world * B * words, dtype=torch.int32, device="cuda")
-            eng.take_marks(local.data_ptr(), B * words)
-            dist.all_gather_into_tensor(gathered, local)
-            eng.voxelOccupancyGridBatch(gathered.data_ptr(), words, self.world, B, words,
-                                        B * words, self.p.occupancy_lifetime)
-            keep.append(gathered)
+            S = self._slot(k)
+            if S.pending:
+                raise RuntimeError("FusedCloudRank.start: the slot's previous step is unfinished")
+            st = torch.cuda.ExternalStream(eng.stream())
+            S.ensure(st, tail_bytes=B * L2 if halo else 0)
+            ctx = torch.cuda.stream(st)
         else:
-            dl = h.DeviceArray(B * words * 4)
-            eng.take_marks(dl.ptr, B * words)
-            eng.synchronize()
-            local = torch.from_numpy(dl.to_numpy(np.int32, B * words))
-            parts = [torch.empty_like(local) for _ in range(self.world)]
-            dist.all_gather(parts, local)
-            dg = h.DeviceArray.from_numpy(torch.cat(parts).numpy())
-            eng.voxelOccupancyGridBatch(dg.ptr, words, self.world, B, words, B * words,
-                                        self.p.occupancy_lifetime)
-            eng.synchronize()
-            keep.append(dg)
-        n_total = max(B * c.width * c.height, 1)
+            S, st, ctx = None, None, _nullctx()
+        with ctx:
+            halo_ptr = None
+            if halo:
+                # all ranks send Lmax values (the tail of their camera); rank k uses rank k-1's
+                # (bytes: gloo has no 16-bit integer collectives)
+                if self.dev == "cuda":
+                    for j, src in enumerate(tail_src_ptrs):
+                        h.copy_async(S.tail.data_ptr() + j * L2, src, L2, h.D2D, st.cuda_stream)
+                    dist.all_gather_into_tensor(S.tails[:self.world * B * L2], S.tail[:B * L2])
+                    if self.rank > 0:
+                        halo_ptr = S.tails.data_ptr() + (self.rank - 1) * B * L2
+                else:
+                    tail = torch.from_numpy(np.concatenate(
+                        [_d2h(h, src, np.uint8, L2) for src in tail_src_ptrs]))
+                    parts = all_gather_tails(tail)
+                    if self.rank > 0:
+                        dh = h.DeviceArray.from_numpy(parts[self.rank - 1].numpy())
+                        self._keep = [dh]
+                        halo_ptr = dh.ptr
+            for j in range(B):
+                if j:
+                    eng.nextFrameInBatch()
+                if halo_ptr is not None:
+                    pc_ = self.cams[self.rank - 1]
+                    take = min(self.Lmax, pc_.width * pc_.height)
+                    # the received tail holds camera k-1's last Lmax values (or all of a smaller one)
+                    eng.addHaloDepthmapDevice(halo_ptr + j * L2 + 2 * (self.Lmax - take), take,
+                                              pc_.width, pc_.height, *pc_.intrinsics(),
+                                              pc_.T_world, pc_.T_crop)
+                eng.addDepthmapDevice(depth_ptrs[j], c.width, c.height, *c.intrinsics(), c.T_world,
+                                      c.T_crop)
+            res = eng.processFramePrepared(self.frame_params(move) if B == 1 else self.pc)
+            _, ncells = eng.grid_size()
+            words = words_for(ncells)
+            n_total = max(int(res.num_points_total), 1)
+            if self.dev == "cuda":
+                S.ensure(st, n_send=n_total, mark_words=B * words)
+                # occupancy union: the B frames' marks of every rank, one batched grid update
+                eng.take_marks(S.local.data_ptr(), B * words)
+                dist.all_gather_into_tensor(S.gathered[:self.world * B * words], S.local[:B * words])
+                eng.voxelOccupancyGridBatch(S.gathered.data_ptr(), words, self.world, B, words,
+                                            B * words, self.p.occupancy_lifetime)
+                # key-range partition; the split sizes to the host without a stream sync
+                eng.partition_points(self.world, S.sp.data_ptr(), S.sk.data_ptr(), S.cap,
+                                     S.cnt.data_ptr())
+                S.c64.copy_(S.cnt)
+                dist.all_to_all_single(S.rc, S.c64)
+                S.host[:self.world].copy_(S.c64, non_blocking=True)
+                S.host[self.world:].copy_(S.rc, non_blocking=True)
+                S.ev.record(st)
+                S.pending = True
+            else:
+                dl = h.DeviceArray(B * words * 4)
+                eng.take_marks(dl.ptr, B * words)
+                eng.synchronize()
+                local = torch.from_numpy(dl.to_numpy(np.int32, B * words))
+                parts = [torch.empty_like(local) for _ in range(self.world)]
+                dist.all_gather(parts, local)
+                dg = h.DeviceArray.from_numpy(torch.cat(parts).numpy())
+                eng.voxelOccupancyGridBatch(dg.ptr, words, self.world, B, words, B * words,
+                                            self.p.occupancy_lifetime)
+                dsp, dsk, dcnt = h.DeviceArray(n_total * 16), h.DeviceArray(n_total * 4), h.DeviceArray(64)
+                eng.partition_points(self.world, dsp.ptr, dsk.ptr, n_total, dcnt.ptr)
+                eng.synchronize()
+                self._staged[k] = (dg, dsp, dsk, dcnt)
+        return k
+
+    def finish(self, k):
+        """The points all-to-all and the voxelize of the step started on slot k.  Returns the
+        send counts per rank."""
+        import torch
+        import torch.distributed as dist
+        h = self.hiprt
+        eng = self.eng
         if self.dev == "cuda":
-            sp = torch.empty((n_total, 4), dtype=torch.float32, device="cuda")
-            sk = torch.empty(n_total, dtype=torch.int32, device="cuda")
-            cnt = torch.empty(self.world, dtype=torch.int32, device="cuda")
-            eng.partition_points(self.world, sp.data_ptr(), sk.data_ptr(), n_total, cnt.data_ptr())
-            rp, rk, rc, counts = exchange_points_dev(sp, sk, cnt)
-            eng.voxelize_points(rp.data_ptr(), rk.data_ptr(), int(sum(rc)), self.p.voxel_average)
-            keep += [rp, rk]
-        else:
-            dsp, dsk, dcnt = h.DeviceArray(n_total * 16), h.DeviceArray(n_total * 4), h.DeviceArray(64)
-            eng.partition_points(self.world, dsp.ptr, dsk.ptr, n_total, dcnt.ptr)
-            eng.synchronize()
-            counts = dcnt.to_numpy(np.uint32, self.world).tolist()
-            m = int(sum(counts))
-            sp = torch.from_numpy(dsp.to_numpy(np.float32, 4 * max(m, 1))[:4 * m].reshape(m, 4))
-            sk = torch.from_numpy(dsk.to_numpy(np.int32, max(m, 1))[:m])
-            rp, rk, rc = exchange_points(sp, sk, counts)
-            n = int(sum(rc))
-            drp = h.DeviceArray.from_numpy(rp.numpy()) if n else None
-            drk = h.DeviceArray.from_numpy(rk.numpy()) if n else None
-            eng.voxelize_points(drp.ptr if n else 0, drk.ptr if n else 0, n, self.p.voxel_average)
-            eng.synchronize()
-            keep += [drp, drk]
-        self._keep = keep
+            eng.select_slot(k)
+            S = self.slots[k]
+            if not S.pending:
+                raise RuntimeError("FusedCloudRank.finish: no step in flight on this slot")
+            st = torch.cuda.ExternalStream(eng.stream())
+            S.ev.synchronize()  # (the slot's split sizes; the later slots keep the GPU busy)
+            both = S.host.tolist()
+            scounts = [int(x) for x in both[:self.world]]
+            rcounts = [int(x) for x in both[self.world:]]
+            n, m = sum(rcounts), sum(scounts)
+            S.ensure(st, n_recv=max(n, 1))
+            with torch.cuda.stream(st):
+                if self.world > 1 or n:
+                    dist.all_to_all_single(S.rp[:n], S.sp[:m], output_split_sizes=rcounts,
+                                           input_split_sizes=scounts, group=self.pg_points)
+                    dist.all_to_all_single(S.rk[:n], S.sk[:m], output_split_sizes=rcounts,
+                                           input_split_sizes=scounts, group=self.pg_points)
+                eng.voxelize_points(S.rp.data_ptr(), S.rk.data_ptr(), n, self.p.voxel_average)
+            S.pending = False
+            return scounts
+        dg, dsp, dsk, dcnt = self._staged.pop(k)
+        counts = dcnt.to_numpy(np.uint32, self.world).tolist()
+        m = int(sum(counts))
+        sp = torch.from_numpy(dsp.to_numpy(np.float32, 4 * max(m, 1))[:4 * m].reshape(m, 4))
+        sk = torch.from_numpy(dsk.to_numpy(np.int32, max(m, 1))[:m])
+        rp, rk, rc = exchange_points(sp, sk, counts)
+        n = int(sum(rc))
+        drp = h.DeviceArray.from_numpy(rp.numpy()) if n else None
+        drk = h.DeviceArray.from_numpy(rk.numpy()) if n else None
+        eng.voxelize_points(drp.ptr if n else 0, drk.ptr if n else 0, n, self.p.voxel_average)
+        eng.synchronize()
+        self._keep = [dg, drp, drk]
         return counts
+
+    def run(self, steps, depth_ptrs_of, tail_ptrs_of, move_of=None, on_finish=None):
+        """`steps` steps through the pipeline: step i's inputs from depth_ptrs_of(i) /
+        tail_ptrs_of(i) (/ move_of(i)); each step is finished right after the next one started
+        (the GPU computes step i + 1 while the host waits for step i's split sizes).
+        on_finish(i) runs after step i's finish (e.g. publishing its cloud)."""
+        pending = []
+        for i in range(steps):
+            if self.dev == "cuda" and len(pending) >= self.depth:
+                j, kk = pending.pop(0)  # (its slot comes round again)
+                self.finish(kk)
+                if on_finish:
+                    on_finish(j)
+            k = self.start(depth_ptrs_of(i), tail_ptrs_of(i), move_of(i) if move_of else None)
+            pending.append((i, k))
+            if self.dev != "cuda" or self.depth == 1 or len(pending) > 1:
+                j, kk = pending.pop(0)
+                self.finish(kk)
+                if on_finish:
+                    on_finish(j)
+        for j, kk in pending:
+            self.finish(kk)
+            if on_finish:
+                on_finish(j)
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
 
 
 def gather_fused_cloud(rank_obj, root: int = 0):

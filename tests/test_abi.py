@@ -39,7 +39,7 @@ def test_library_loads_and_reports_version():
     lib = load_library()
     a, b = ctypes.c_int(), ctypes.c_int()
     assert lib.gdf_version(ctypes.byref(a), ctypes.byref(b)) == 0
-    assert (a.value, b.value) == (0, 3)
+    assert (a.value, b.value) == (0, 4)
     # null-handle calls fail cleanly with GDF_ERR_ARG, no GPU touched
     assert lib.gdf_clear(None) == -1
     assert b"null engine" in lib.gdf_last_error()
@@ -49,3 +49,13 @@ def test_code_object_targets_gfx950():
     from ros_gpu_depthmap_fusion_amd import build_library
     data = open(build_library(), "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in data
+
+
+def test_build_provenance_matches_sources():
+    """libgdf.so carries the digest of the sources it was compiled from (gdf_build_info); the
+    binding refuses a library built from other sources (no stale build is ever loaded)."""
+    from ros_gpu_depthmap_fusion_amd.build import source_digest
+    from ros_gpu_depthmap_fusion_amd.gdf import build_info, load_library
+    info = build_info(load_library())
+    assert info["source_sha"] == source_digest()
+    assert info.get("built_on") and info.get("built_at")

@@ -344,3 +344,85 @@ def test_fused_cloud_rollbuffer_leg(tmp_path, cfg):
         for r in range(world):
             np.testing.assert_array_equal(np.load(tmp_path / f"grid_r{r}_f{f}.npy"), grid,
                                           f"{cfg} frame {f} rank {r}")
+
+
+# ---- the pipelined RCCL path: steps in the engine's slots ----------------
+def _rank_nccl_pipe(rank, world, port, out_dir, depth, rollbuffer):
+    """RCCL at world 1, FusedCloudRank(depth=3).run(): step i+1 starts (compaction, marks, grid
+    update, partition, split sizes) before step i's points all-to-all and voxelize - on the
+    slots' own streams, the points on their own communicator.  Batches of 2 frames, or (with the
+    rollbuffer) single frames each carrying one new point sequence."""
+    import torch
+    import torch.distributed as dist
+    import fused_ref
+    from ros_gpu_depthmap_fusion_amd import build_library, hiprt, multi
+    from ros_gpu_depthmap_fusion_amd.gdf import GPUDepthmapFusion
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    build_library()
+    p = ComponentParams()
+    p.ps_timespan = 2.5 / 30.0
+    cams = [synth.make_camera(k, W, H) for k in range(world)]
+    eng = GPUDepthmapFusion(0)
+    fr = multi.FusedCloudRank(eng, cams, rank, world, p, dev="cuda", depth=depth)
+    n = W * H
+    B = 1 if rollbuffer else 2
+    steps = 6
+    ds = [hiprt.DeviceArray.from_numpy(synth.dense_frame(cams[rank], rank, f)) for f in range(B * steps)]
+    lidar = fused_ref.lidar_camera(80, 60)
+    recs = [hiprt.DeviceArray.from_numpy(fused_ref.sequence_records(lidar, k)) for k in range(2)]
+
+    def move(i):
+        eng.addPointSequenceDevice(recs[i % 2].ptr, 80 * 60, 16, *synth.sequence_time(i),
+                                   synth.move_transform(i))
+        return (lidar.T_world, lidar.T_crop)
+
+    def done(i):
+        torch.cuda.synchronize()
+        vox = eng.downloadVoxelizedPoints()[:, :3]
+        _, vs = eng.batch_ranges()
+        for j in range(B):
+            np.save(os.path.join(out_dir, f"pvox_f{B * i + j}.npy"), vox[vs[j]:vs[j + 1]])
+        if rollbuffer:
+            np.save(os.path.join(out_dir, f"prb_f{i}.npy"), np.array(eng.rollbuffer_state().as_tuple()))
+
+    fr.run(steps, lambda i: [ds[B * i + j].ptr for j in range(B)],
+           lambda i: [ds[B * i + j].ptr + 2 * (n - fr.Lmax) for j in range(B)],
+           move_of=move if rollbuffer else None, on_finish=done)
+    torch.cuda.synchronize()
+    np.save(os.path.join(out_dir, "pgrid.npy"), eng.downloadVoxelOccupancyGrid())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("rollbuffer", [False, True])
+def test_rccl_pipelined_fused_cloud_world1(tmp_path, rollbuffer):
+    """The pipelined fused path (three steps in flight on the engine's slots, the points
+    all-to-all on a second communicator) under RCCL at world 1: every frame's voxel means, the
+    final grid and (rollbuffer) the rollbuffer state after every frame equal the oracle's bit for
+    bit."""
+    import fused_ref
+    from oracle import OracleFusion
+    mp.start_processes(_rank_nccl_pipe, args=(1, _free_port(), str(tmp_path), 3, rollbuffer),
+                       nprocs=1, join=True, start_method="spawn")
+    p = ComponentParams()
+    p.ps_timespan = 2.5 / 30.0
+    cam = synth.make_camera(0, W, H)
+    lidar = fused_ref.lidar_camera(80, 60)
+    recs = [fused_ref.sequence_records(lidar, k) for k in range(2)]
+    orc = OracleFusion(threads=4)
+    nf = 6 if rollbuffer else 12
+    for f in range(nf):
+        orc.clear()
+        orc.addDepthmap(synth.dense_frame(cam, 0, f), *cam.intrinsics(), cam.T_world, cam.T_crop)
+        if rollbuffer:
+            orc.addPointSequence(recs[f % 2], *synth.sequence_time(f), synth.move_transform(f))
+            orc.processFrame(p, T_world_move=lidar.T_world, T_crop_move=lidar.T_crop)
+            assert tuple(np.load(tmp_path / f"prb_f{f}.npy").tolist()) == tuple(orc.rollbuffer_state())
+        else:
+            orc.processFrame(p)
+        want = orc.downloadVoxelizedPoints()[:, :3]
+        got = np.load(tmp_path / f"pvox_f{f}.npy")
+        assert len(got) == len(want) > 0 and np.array_equal(got.view(np.uint32), want.view(np.uint32)), f
+    np.testing.assert_array_equal(np.load(tmp_path / "pgrid.npy"), orc.downloadVoxelOccupancyGrid())

@@ -79,16 +79,24 @@ def _nan_equal_bits(a, b):
     return (a.view(np.uint32) == b.view(np.uint32)) | both_nan
 
 
-def test_voxel_sums_adversarial_points_mode(Engine):
-    """gdf_voxelize_points (points mode: k_group in-thread / staged / gathered wave sums and, with
-    > 1 K tiles, k_group_big) on voxels built from the adversarial term lists of
-    tests/test_spec_sum_model.py - ties at every binade, sums through zero, exact cancellation,
+@pytest.mark.parametrize("xruns", [False, True])
+def test_voxel_sums_adversarial_points_mode(Engine, xruns):
+    """gdf_voxelize_points (points mode - GDF_NO_XRUNS: k_group in-thread / staged / gathered wave
+    sums and, with > 1 K tiles, k_group_big; or, by default, the received list's runs of equal
+    keys through k_group_runs / k_group_runs_big) on voxels built from the adversarial term lists
+    of tests/test_spec_sum_model.py - ties at every binade, sums through zero, exact cancellation,
     subnormals, overflow to inf, inf and NaN terms, 70 K ones - interleaved with 400 K ordinary
     points: every voxel mean equals the reference's sequential f32 chain (inc/voxelize.h:29-35),
     bit for bit (NaN: any NaN)."""
+    import os
     from test_spec_sum_model import cases
     from spec_sum_model import sequential_sum
-    gpu = Engine()
+    if not xruns:
+        os.environ["GDF_NO_XRUNS"] = "1"
+    try:
+        gpu = Engine()
+    finally:
+        os.environ.pop("GDF_NO_XRUNS", None)
     p = ComponentParams()
     cam = synth.make_camera(0, 64, 48)
     gpu.clear()
@@ -107,9 +115,17 @@ def test_voxel_sums_adversarial_points_mode(Engine):
     for j in range(3000):  # ordinary voxels, 1..400 points
         n = int(rng.integers(1, 400))
         groups.append((200_000 + 613 * j, rng.normal(0, 1, (n, 4)).astype(np.float32)))
-    # interleave the groups' points (each group keeps its own order: the stable sort restores it)
+    # interleave the groups' points (each group keeps its own order: the stable sort restores it);
+    # runs mode: blocks of consecutive points of one group (runs of 1..64 points)
     owner = np.concatenate([np.full(len(t), g) for g, (_, t) in enumerate(groups)])
     rng.shuffle(owner)
+    if xruns:
+        owner = np.sort(owner)
+        cut = np.cumsum(rng.integers(1, 65, len(owner)))
+        cut = cut[cut < len(owner)]
+        blocks = np.split(owner, cut)
+        rng.shuffle(blocks)
+        owner = np.concatenate(blocks)
     pos = np.zeros(len(groups), np.int64)
     pts = np.empty((len(owner), 4), np.float32)
     keys = np.empty(len(owner), np.uint32)
