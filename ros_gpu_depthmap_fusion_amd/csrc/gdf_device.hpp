@@ -17,6 +17,9 @@ constexpr int kArgCams = 4;           // camera descriptors passed in the kernel
 constexpr int kHalo = 8;              // band rows/columns staged around a segment: min(F, 8)
 constexpr uint32_t kSegItems = 1024;  // items per compaction segment (max)
 constexpr uint32_t kFusedPrefixSegs = 4096;  // up to this many segments k_emit sums the counts
+constexpr uint32_t kScanGroup = 64;          // segments per group of the in-kernel group scan
+constexpr uint32_t kMaxScanGroups = 4096;    // k_emit sums at most this many group totals
+constexpr uint32_t kMaxGroupScanTiles = 65536;  // group phase: in-kernel scan up to this many tiles
 constexpr uint32_t kSelSegs = 8;      // rollbuffer points per k_sel thread (default; 4, 8, 16)
 constexpr uint32_t kSelThreads = 512; // k_sel block (default): a tile is segs * threads points
 constexpr int kSortThreads = 256;
@@ -171,6 +174,13 @@ struct FrameArgs {
     uint32_t* run_count;        // runs of the frame (device)
     uint32_t* scan_total;       // scratch total of the segment-count scan
     uint32_t* run_total;        // runs of depth + rollbuffer points (k_sel's last tile)
+    // group scan (no scan launch, kFusedPrefixSegs < segments <= kScanGroup * kMaxScanGroups):
+    // the last k_mask block to finish in each group of kScanGroup segments scans the group's
+    // counts into group-local offsets (seg_offsets) and the group totals (grp_tot: point totals,
+    // then run totals); k_emit adds the totals of the groups before its own
+    uint32_t* grp_done;         // [groups] arrival counters (self-resetting)
+    uint32_t* grp_tot;          // [2 * groups]
+    int32_t mask_packed;        // k_mask_px<2>: both pixels of a thread in packed f32 ops
 };
 static_assert(sizeof(FrameArgs) <= 4096, "kernel arguments are limited to 4 KiB");
 

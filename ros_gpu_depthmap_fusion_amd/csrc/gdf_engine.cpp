@@ -334,6 +334,8 @@ struct Slot {
     uint32_t snap_blocks = 0, snap_frames = 0;
     DevBuf d_pcnt, d_poff;          // multi-GPU key-range partition workspace
     DevBuf d_xcnt, d_xoff, d_xrk, d_xrs;  // runs of a received (point, key) list
+    DevBuf d_grpdone, d_grptot;     // in-kernel group scan of the segment counts
+    DevBuf d_ggdone, d_ggtot;       // ... and of the group phase's tile counts
     DevBuf d_wruns, d_runkeys, d_runstart;  // runs of equal keys
     bool runs_sel = false;          // ... counted in kRunTotal (frame with rollbuffer points)
     bool runs_valid = false;        // this frame's voxelize may sort runs
@@ -454,6 +456,8 @@ struct gdf_engine {
     bool force_runs = getenv("GDF_FORCE_RUNS") != nullptr;    // tuning knob: runs at every size
     bool run_hist_in_sort = getenv("GDF_RUN_HIST_SORT") != nullptr;  // tuning knob
     bool xruns = !getenv("GDF_NO_XRUNS");  // voxelize_points sorts the received list's runs
+    bool group_scan = !getenv("GDF_NO_GROUP_SCAN");  // segment offsets without scan launches
+    bool mask_packed = !getenv("GDF_NO_MASK_PACKED");  // k_mask_px<2>: packed f32 pixel pairs
 
     // compaction outputs
 
@@ -1240,6 +1244,17 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel, bool compaction_marks = fa
     a.seg_counts = e->sl().d_tcounts.as<uint32_t>();
     a.seg_offsets = e->sl().d_toffsets.as<uint32_t>();
     a.fused_prefix = a.total_segs <= kFusedPrefixSegs ? 1 : 0;
+    a.mask_packed = e->mask_packed ? 1 : 0;
+    // above: the last k_mask block of each group of kScanGroup segments scans the group (no scan
+    // launches); k_emit sums the group totals before its own
+    const uint32_t ngroups = (a.total_segs + kScanGroup - 1) / kScanGroup;
+    if (!a.fused_prefix && e->group_scan && ngroups <= kMaxScanGroups) {
+        Slot& q = e->sl();
+        q.d_grpdone.ensure_zero((size_t)ngroups * 4, e->s());  // (self-resetting afterwards)
+        q.d_grptot.ensure((size_t)ngroups * 2 * 4);
+        a.grp_done = q.d_grpdone.as<uint32_t>();
+        a.grp_tot = q.d_grptot.as<uint32_t>();
+    }
     // k_mask's LDS band: 2h+1 rows of 16-B chunks covering segw + 2h columns (+1 chunk of
     // alignment), then the columns' ray factors
     {
@@ -1352,6 +1367,11 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime,
     const uint32_t gtiles = (uint32_t)voxelize_group_tiles(nmax);
     e->sl().d_gcnt.ensure((size_t)gtiles * 4);
     e->sl().d_goff.ensure(seg_offsets_words(gtiles) * 4);
+    if (e->group_scan) {  // k_group_count's own group scan (kernels skip it above their bound)
+        const size_t ng = ((size_t)gtiles + kScanGroup - 1) / kScanGroup;
+        e->sl().d_ggdone.ensure_zero(ng * 4, e->s());  // (self-resetting afterwards)
+        e->sl().d_ggtot.ensure(ng * 4);
+    }
     // point mode: <= 1 long voxel per tile; run mode: one queue entry per long group, at most
     // one per voxel of the batch
     const uint64_t qcap = std::min<uint64_t>(nmax, (uint64_t)std::max<uint32_t>(e->nframes, 1) * e->ncells);
@@ -1398,6 +1418,8 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime,
     // (each tile publishes 256 look-back words: 2 KiB per 1 Ki keys at PT=4)
     v.group_counts = e->sl().d_gcnt.as<uint32_t>();
     v.group_offsets = e->sl().d_goff.as<uint32_t>();
+    v.group_done = e->group_scan ? e->sl().d_ggdone.as<uint32_t>() : nullptr;
+    v.group_gtot = e->group_scan ? e->sl().d_ggtot.as<uint32_t>() : nullptr;
     v.bigq = e->sl().d_bigq.as<uint4>();
     v.bigq_cap = (uint32_t)std::min<uint64_t>(bigq_n, 0xFFFFFFFFu);
     v.bigcnt = e->sl().d_bigcnt.as<uint32_t>();

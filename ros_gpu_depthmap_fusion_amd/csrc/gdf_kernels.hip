@@ -671,6 +671,87 @@ __device__ __forceinline__ void load_cams(const FrameArgs& a, CamDesc* s_cams) {
     for (uint32_t w = threadIdx.x; w < words; w += blockDim.x) dst[w] = G(src)[w];
 }
 
+// In-kernel group scan of the segment counts (replaces k_scan_reduce + k_scan_counts above
+// kFusedPrefixSegs segments): after a block has written its counts, it counts itself in at its
+// group of kScanGroup consecutive segments; the group's last block (agent-scope release /
+// acquire: the blocks of a group may run on other XCDs) scans the group's point counts - and run
+// counts - into group-local exclusive offsets and writes the group totals, then re-arms the
+// counter for the next launch (graph replays included).  k_emit adds the totals of the groups
+// before its own (group_partials).
+// Generic form: entry `idx` of `nent` counts (cnt[q * stride + i] for series q < nser) was just
+// written by thread 0 of this block; the last arriver of idx's group scans the group.
+__device__ __forceinline__ void arrive_and_scan(uint32_t* done, const uint32_t* cnt, uint32_t* off,
+                                                uint32_t* gtot, uint32_t idx, uint32_t nent,
+                                                int nser, uint32_t stride, uint32_t* s_last) {
+    const uint32_t g = idx / kScanGroup;
+    const uint32_t s0 = g * kScanGroup;
+    const uint32_t n = min(kScanGroup, nent - s0);
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this block's counts
+        const uint32_t old = __hip_atomic_fetch_add(done + g, 1u, __ATOMIC_ACQ_REL,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+        *s_last = old + 1u == n ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!*s_last || threadIdx.x >= 64) return;  // block-uniform, then wave 0
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every block's counts of the group
+    const uint32_t lane = threadIdx.x;
+    const uint32_t ng = (nent + kScanGroup - 1) / kScanGroup;
+    for (int q = 0; q < nser; ++q) {  // (k_mask: point counts, then run counts)
+        const uint32_t base = q * stride;
+        const uint32_t v = lane < n ? __hip_atomic_load(cnt + base + s0 + lane, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT)
+                                    : 0u;
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= (uint32_t)o) x += y;
+        }
+        if (lane < n) G(off)[base + s0 + lane] = x - v;
+        if (lane == 63) G(gtot)[q * ng + g] = x;
+    }
+    if (lane == 0) __hip_atomic_store(done + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void group_scan_tail(const FrameArgs& a, uint32_t s) {
+    __shared__ uint32_t s_last;
+    if (!a.grp_done) return;
+    arrive_and_scan(a.grp_done, a.seg_counts, a.seg_offsets, a.grp_tot, s, a.total_segs,
+                    a.run_mode ? 2 : 1, a.total_segs, &s_last);
+}
+
+// the sum of the group totals gtot[0 .. idx / kScanGroup) by one wave (every lane gets it)
+__device__ __forceinline__ uint32_t wave_group_prefix(const uint32_t* gtot, uint32_t idx) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t sum = 0;
+    for (uint32_t t = lane; t < idx / kScanGroup; t += 64) sum += G(gtot)[t];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    return sum;
+}
+
+// sum of the totals of the groups before segment s's group (group-scan form), into s_red per
+// wave (run mode: the run totals too, into s_red + 16)
+__device__ __forceinline__ void group_partials(const FrameArgs& a, uint32_t s, uint32_t* s_red) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t g = s / kScanGroup;
+    const uint32_t ng = (a.total_segs + kScanGroup - 1) / kScanGroup;
+    uint32_t sum = 0, rsum = 0;
+    for (uint32_t t = threadIdx.x; t < g; t += blockDim.x) {
+        sum += G(a.grp_tot)[t];
+        if (a.run_mode) rsum += G(a.grp_tot)[ng + t];
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        sum += __shfl_xor(sum, o, 64);
+        rsum += __shfl_xor(rsum, o, 64);
+    }
+    if (lane == 0) {
+        s_red[wid] = sum;
+        s_red[16 + wid] = rsum;
+    }
+}
+
 // Pass 1 of the ordered compaction (apply_point_mask.glsl:42-55 made stable): one block per
 // segment, one item per thread (blockDim = a.seg_threads >= every segment's length).  The ballot
 // of wave w's valid bits is word w of the segment's 16-word bitmask.
@@ -834,6 +915,7 @@ __global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
             if (s_hist[j])
                 __hip_atomic_fetch_add(rep + j, s_hist[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    group_scan_tail(a, s);
 }
 
 // PX pixels per thread, ring by ring in lockstep (F = 4, no rot45): pixel j of thread i is
@@ -893,6 +975,120 @@ __device__ __forceinline__ void depth_bits_px(const FrameArgs& a, const CamDesc*
                      (qz < a.lo[2]) | (qz > a.hi[2]));
         }
         bits[j] = (uint32_t)conv[j] | ((uint32_t)fly[j] << 1) | ((uint32_t)(fly[j] & crop) << 2);
+    }
+}
+
+// ---- the two pixels of a thread in packed f32 (v_pk_mul_f32 / v_pk_add_f32) --------------------
+// depth_bits_px<AMODE, 2> with the arithmetic of BOTH pixels in one packed instruction per
+// operation: element 0 = pixel x, element 1 = pixel x + 128.  The packed ops round exactly like
+// the scalar ones (IEEE binary32, same denormal mode, no contraction: -ffp-contract=off), and
+// every operation keeps depth_bits' order, so the stage bits are bit-identical.
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+struct P3x2 {
+    f2v x, y, z;
+    bool v0, v1;
+};
+
+__device__ __forceinline__ f2v f2(float a, float b) {
+    f2v r;
+    r.x = a;
+    r.y = b;
+    return r;
+}
+
+// neighbours (col0, row r0) and (col1, row r1) from the band (rows may differ: kRowStart's wrap)
+__device__ __forceinline__ P3x2 band_pt2(const Band& t, int r0, int c0, int r1, int c1, f2v yn,
+                                         float scale) {
+    const uint32_t d0 = *reinterpret_cast<const uint16_t*>(t.b + t.rowoff[r0] + 2 * c0);
+    const uint32_t d1 = *reinterpret_cast<const uint16_t*>(t.b + t.rowoff[r1] + 2 * c1);
+    P3x2 p;
+    p.z = f2((float)d0, (float)d1) * f2(scale, scale);
+    p.x = f2(t.xn[c0 - (int)t.ca], t.xn[c1 - (int)t.ca]) * p.z;
+    p.y = yn * p.z;
+    p.v0 = d0 != 0u;
+    p.v1 = d1 != 0u;
+    return p;
+}
+
+__device__ __forceinline__ void ring_pass2(const P3x2& u, const P3x2& d, const P3x2& l,
+                                           const P3x2& r, float thr, f2v nax, f2v nay, f2v naz,
+                                           f2v px, f2v py, f2v pz, bool live0, bool live1,
+                                           bool& out0, bool& out1) {
+    const bool nz0 = u.v0 & d.v0 & l.v0 & r.v0;
+    const bool nz1 = u.v1 & d.v1 & l.v1 & r.v1;
+    const f2v ax = d.x - u.x, ay = d.y - u.y, az = d.z - u.z;  // dy = down - up
+    const f2v bx = r.x - l.x, by = r.y - l.y, bz = r.z - l.z;  // dx = right - left
+    const f2v cx = ay * bz - az * by;
+    const f2v cy = az * bx - ax * bz;
+    const f2v cz = ax * by - ay * bx;
+    const f2v dd = (cx * cx + cy * cy) + cz * cz;
+    const f2v dt = (cx * nax + cy * nay) + cz * naz;
+    const f2v cva = dt * f2(__builtin_amdgcn_rsqf(dd.x), __builtin_amdgcn_rsqf(dd.y));
+    const float hi_t = thr + 1e-5f, lo_t = thr - 1e-5f;
+    const bool n0 = (dd.x > 1e-30f) & (dd.x < 1e30f), n1 = (dd.y > 1e-30f) & (dd.y < 1e30f);
+    const bool hi0 = cva.x > hi_t, lo0 = cva.x < lo_t, hi1 = cva.y > hi_t, lo1 = cva.y < lo_t;
+    bool pass0 = n0 & hi0, pass1 = n1 & hi1;
+    const bool und0 = live0 & nz0 & !(n0 & (hi0 | lo0));
+    const bool und1 = live1 & nz1 & !(n1 & (hi1 | lo1));
+    if (__ballot(und0 | und1)) {  // rare, wave-uniform
+        if (und0) pass0 = surface_exact(cx.x, cy.x, cz.x, dd.x, thr, px.x, py.x, pz.x);
+        if (und1) pass1 = surface_exact(cx.y, cy.y, cz.y, dd.y, thr, px.y, py.y, pz.y);
+    }
+    out0 = nz0 & pass0;
+    out1 = nz1 & pass1;
+}
+
+template <int AMODE>
+__device__ __forceinline__ void depth_bits_px2(const FrameArgs& a, const CamDesc* cams, int k,
+                                               const Band& t, const float* s_yn, const uint32_t* x,
+                                               uint32_t y, const bool* in, uint32_t* bits) {
+    const CamDesc& c = cams[k];
+    const int h = t.h;
+    const float scale = c.scale;
+    const f2v ynh = f2(s_yn[h], s_yn[h]);
+    // the centre points (a pixel outside the segment reads column x0: defined, never used)
+    // (a pixel past the segment's end reads inside the band row's buffer; its point is zeroed)
+    P3x2 p = band_pt2(t, h, (int)x[0], h, (int)x[1], ynh, scale);
+    if (!in[0]) { p.x.x = 0.f; p.y.x = 0.f; p.z.x = 0.f; p.v0 = false; }
+    if (!in[1]) { p.x.y = 0.f; p.y.y = 0.f; p.z.y = 0.f; p.v1 = false; }
+    const bool conv0 = in[0] & p.v0, conv1 = in[1] & p.v1;
+    const f2v pp = (p.x * p.x + p.y * p.y) + p.z * p.z;
+    bool fly0 = conv0 & !beyond_max_distance(pp.x);
+    bool fly1 = conv1 & !beyond_max_distance(pp.y);
+    const f2v rr = f2(__builtin_amdgcn_rsqf(pp.x), __builtin_amdgcn_rsqf(pp.y));
+    const f2v nx = -(p.x * rr), ny = -(p.y * rr), nz = -(p.z * rr);
+    const int x0 = (int)x[0], x1 = (int)x[1];
+#pragma unroll
+    for (uint32_t i = 1; i <= 4; ++i) {
+        if (!__ballot(fly0 | fly1)) break;  // wave-uniform exit
+        const int ii = (int)i;
+        fly0 = fly0 & (x[0] + i <= c.W - 1) & (y + i <= c.H - 1);
+        fly1 = fly1 & (x[1] + i <= c.W - 1) & (y + i <= c.H - 1);
+        const P3x2 n0 = band_pt2(t, h - ii, x0, h - ii, x1, f2(s_yn[h - ii], s_yn[h - ii]), scale);
+        const P3x2 n1 = band_pt2(t, h + ii, x0, h + ii, x1, f2(s_yn[h + ii], s_yn[h + ii]), scale);
+        // left: kRowStart's pixel 0 may wrap to the previous row's end (staged before column 0)
+        const float ynl0 = (AMODE == kRowStart && x[0] < i) ? s_yn[h - 1] : s_yn[h];
+        const P3x2 n2 = band_pt2(t, h, x0 - ii, h, x1 - ii, f2(ynl0, s_yn[h]), scale);
+        const P3x2 n3 = band_pt2(t, h, x0 + ii, h, x1 + ii, ynh, scale);
+        bool r0, r1;
+        ring_pass2(n0, n1, n2, n3, a.thr, nx, ny, nz, p.x, p.y, p.z, fly0, fly1, r0, r1);
+        fly0 = fly0 & r0;
+        fly1 = fly1 & r1;
+    }
+    const bool fl[2] = {fly0, fly1}, cv[2] = {conv0, conv1};
+    const float qxv[2] = {p.x.x, p.x.y}, qyv[2] = {p.y.x, p.y.y}, qzv[2] = {p.z.x, p.z.y};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        bool crop = true;
+        if (a.do_crop) {
+            const float qx = mrow(c.Tc + 0, qxv[j], qyv[j], qzv[j], 1.0f);
+            const float qy = mrow(c.Tc + 4, qxv[j], qyv[j], qzv[j], 1.0f);
+            const float qz = mrow(c.Tc + 8, qxv[j], qyv[j], qzv[j], 1.0f);
+            crop = !((qx < a.lo[0]) | (qx > a.hi[0]) | (qy < a.lo[1]) | (qy > a.hi[1]) |
+                     (qz < a.lo[2]) | (qz > a.hi[2]));
+        }
+        bits[j] = (uint32_t)cv[j] | ((uint32_t)fl[j] << 1) | ((uint32_t)(fl[j] & crop) << 2);
     }
 }
 
@@ -1010,7 +1206,11 @@ __global__ __launch_bounds__(SEGW / PX) void k_mask_px(FrameArgs a) {
                 x[j] = sg.x0 + i + (uint32_t)NT * j;
                 in[j] = i + (uint32_t)NT * j < sg.len;
             }
-            if (sg.y >= 4u && xw0 >= 4u)
+            if (PX == 2 && a.mask_packed && sg.y >= 4u && xw0 >= 4u)
+                depth_bits_px2<kInterior>(a, s_cams, sg.k, t, s_yn, x, sg.y, in, bits);
+            else if (PX == 2 && a.mask_packed && wrap)
+                depth_bits_px2<kRowStart>(a, s_cams, sg.k, t, s_yn, x, sg.y, in, bits);
+            else if (sg.y >= 4u && xw0 >= 4u)
                 depth_bits_px<kInterior, PX>(a, s_cams, sg.k, t, s_yn, x, sg.y, in, bits);
             else if (wrap)
                 depth_bits_px<kRowStart, PX>(a, s_cams, sg.k, t, s_yn, x, sg.y, in, bits);
@@ -1072,6 +1272,7 @@ __global__ __launch_bounds__(SEGW / PX) void k_mask_px(FrameArgs a) {
             if (s_hist[j])
                 __hip_atomic_fetch_add(rep + j, s_hist[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    group_scan_tail(a, s);
 }
 
 // Exclusive scan of the segment counts by one workgroup (chunks of 4096 with a running carry);
@@ -1296,6 +1497,7 @@ __global__ __launch_bounds__(1024) void k_emit(FrameArgs a) {
     if (hist)
         for (uint32_t i = threadIdx.x; i < radix_hist_span(a.npasses); i += blockDim.x) s_hist[i] = 0;
     if (a.fused_prefix) prefix_partials(a, s, s_red);
+    else if (a.grp_tot) group_partials(a, s, s_red);
     // the segment's geometry and the thread's item source, loaded before the barrier
     const uint32_t i = threadIdx.x;
     int k = 0;
@@ -1326,8 +1528,9 @@ __global__ __launch_bounds__(1024) void k_emit(FrameArgs a) {
     // run mode: this segment's first run (the scan over points then runs: minus all points)
     uint32_t rbase = 0, rwpre = 0, rtot = 0;
     if (a.run_mode) {
-        if (!a.fused_prefix)
-            rbase = G(a.seg_offsets)[a.total_segs + s] - G(a.seg_offsets)[a.total_segs];
+        if (!a.fused_prefix)  // (group scan: offsets local to the group's runs)
+            rbase = G(a.seg_offsets)[a.total_segs + s] -
+                    (a.grp_tot ? 0u : G(a.seg_offsets)[a.total_segs]);
         for (int w = 0; w < nwaves; ++w) {
             const uint32_t rc = G(a.wave_runs)[(size_t)s * 16 + w];
             rwpre += (w < wid) ? rc : 0u;
@@ -1336,7 +1539,7 @@ __global__ __launch_bounds__(1024) void k_emit(FrameArgs a) {
     }
     __syncthreads();
     uint32_t base = sbase;
-    if (a.fused_prefix)
+    if (a.fused_prefix || a.grp_tot)
         for (int w = 0; w < nwaves; ++w) {
             base += s_red[w];
             rbase += s_red[16 + w];
@@ -1409,6 +1612,7 @@ __global__ __launch_bounds__(SEGW / 2) void k_emit_px2(FrameArgs a) {
     if (hist)
         for (uint32_t i = threadIdx.x; i < radix_hist_span(a.npasses); i += NT) s_hist[i] = 0;
     if (a.fused_prefix) prefix_partials(a, s, s_red);
+    else if (a.grp_tot) group_partials(a, s, s_red);
     const uint32_t i = threadIdx.x;
     int k = 0;
     for (int c = 0; c < a.ncams; ++c)
@@ -1441,14 +1645,15 @@ __global__ __launch_bounds__(SEGW / 2) void k_emit_px2(FrameArgs a) {
     const uint32_t sbase = a.fused_prefix ? 0u : G(a.seg_offsets)[s];
     uint32_t rbase = 0;
     if (a.run_mode) {
-        if (!a.fused_prefix)
-            rbase = G(a.seg_offsets)[a.total_segs + s] - G(a.seg_offsets)[a.total_segs];
+        if (!a.fused_prefix)  // (group scan: offsets local to the group's runs)
+            rbase = G(a.seg_offsets)[a.total_segs + s] -
+                    (a.grp_tot ? 0u : G(a.seg_offsets)[a.total_segs]);
 #pragma unroll
         for (int w = 0; w < NWORDS; ++w) rc[w] = G(a.wave_runs)[(size_t)s * 16 + w];
     }
     __syncthreads();
     uint32_t base = sbase;
-    if (a.fused_prefix)
+    if (a.fused_prefix || a.grp_tot)
         for (int w = 0; w < NW; ++w) {
             base += s_red[w];
             rbase += s_red[16 + w];
@@ -1739,7 +1944,7 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
                 hipLaunchKernelGGL((k_mask<false, 0>), dim3(a.total_segs), dim3(a.seg_threads), lds, s, a);
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
-        if (!a.fused_prefix) {  // (run mode: the point counts, then the run counts)
+        if (!a.fused_prefix && !a.grp_done) {  // (run mode: the point counts, then the run counts)
             HookScope hs(hook, GDF_KERNEL_SCAN);
             const uint32_t m = a.run_mode ? 2u * a.total_segs : a.total_segs;
             if ((e = launch_scan(a.seg_counts, m, a.seg_offsets, a.scan_total, nullptr, 1u, s)) != hipSuccess)
@@ -2614,10 +2819,15 @@ __device__ __forceinline__ float gather_group_comp(const uint32_t* __restrict__ 
 
 // Group starts per tile of kGroupThreads sorted keys (large frames: the tiles' group-id offsets
 // then come from a scan of these counts instead of tickets and look-back in k_group).
+// group starts per tile of the sorted keys; with gdone, also their group scan (arrive_and_scan:
+// local offsets into offsets[], group totals into gtot[]) - no scan launches
 __global__ __launch_bounds__(256) void k_group_count(const uint32_t* __restrict__ keys,
                                                      const uint32_t* __restrict__ count,
-                                                     uint32_t* __restrict__ counts) {
+                                                     uint32_t* __restrict__ counts,
+                                                     uint32_t* gdone, uint32_t* offsets,
+                                                     uint32_t* gtot) {
     __shared__ uint32_t s_w[4];
+    __shared__ uint32_t s_last;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t n = *count;
     const uint32_t ntiles = (n + kGroupThreads - 1) / kGroupThreads;
@@ -2629,6 +2839,7 @@ __global__ __launch_bounds__(256) void k_group_count(const uint32_t* __restrict_
         if (lane == 0) s_w[wid] = (uint32_t)__popcll(b);
         __syncthreads();
         if (threadIdx.x == 0) counts[t] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        if (gdone) arrive_and_scan(gdone, counts, offsets, gtot, t, ntiles, 1, 0u, &s_last);
         __syncthreads();
     }
 }
@@ -2650,7 +2861,8 @@ __global__ __launch_bounds__(kGroupThreads) __attribute__((amdgpu_waves_per_eu(7
     uint32_t* tile_ctr, uint32_t* epoch_word, uint32_t* err, uint32_t* hist, int average,
     VoxelParams vp, uint32_t* marks, const uint32_t* tile_base, uint4* __restrict__ bigq,
     uint32_t* __restrict__ bigcnt, uint32_t bigcap, uint32_t nframes, uint32_t fshift,
-    uint32_t* __restrict__ fvox, uint32_t small_max, uint32_t lane_chains) {
+    uint32_t* __restrict__ fvox, uint32_t small_max, uint32_t lane_chains,
+    const uint32_t* tile_gtot) {
     __shared__ uint32_t s_wave[4];
     __shared__ uint32_t s_tile, s_epoch, s_excl, s_nbig, s_nq;
     __shared__ uint32_t s_start[kGroupThreads + 1];
@@ -2678,10 +2890,13 @@ __global__ __launch_bounds__(kGroupThreads) __attribute__((amdgpu_waves_per_eu(7
     uint32_t walk = blockIdx.x;
     for (bool first = true;; first = false) {  // persistent
     if (!first && !tile_base && tk.oneshot) return;
+    // (group-scanned offsets: the group-local offset + the totals of the groups before)
+    const uint32_t gpre = tile_base && tile_gtot && wid == 0 && walk < ntiles
+                              ? wave_group_prefix(tile_gtot, walk) : 0u;
     if (threadIdx.x == 0) {
         if (tile_base) {
             s_tile = walk;
-            s_excl = walk < ntiles ? tile_base[walk] : 0u;
+            s_excl = walk < ntiles ? tile_base[walk] + gpre : 0u;
         } else {
             s_tile = next_ticket(tile_ctr, tk, epoch_word, s_epoch);
         }
@@ -3140,7 +3355,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
     uint32_t* marks, const uint32_t* tile_base, uint4* __restrict__ bigq, uint32_t bigq_cap,
     uint32_t* __restrict__ qctr, uint32_t nframes, uint32_t fshift, uint32_t* __restrict__ fvox,
     uint32_t inblock_max, uint32_t* __restrict__ rps, uint32_t* __restrict__ rlen,
-    uint32_t small_max) {
+    uint32_t small_max, const uint32_t* tile_gtot) {
     __shared__ uint32_t s_wave[4];
     __shared__ uint32_t s_tile, s_epoch, s_excl, s_nbig, s_nq, s_qbase, s_wend, s_nx, s_nbase;
     __shared__ uint32_t s_nh, s_hbase;
@@ -3170,10 +3385,13 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
     uint32_t walk = blockIdx.x;
     for (bool first = true;; first = false) {  // persistent
         if (!first && !tile_base && tk.oneshot) return;
+        // (group-scanned offsets: the group-local offset + the totals of the groups before)
+        const uint32_t gpre = tile_base && tile_gtot && wid == 0 && walk < ntiles
+                                  ? wave_group_prefix(tile_gtot, walk) : 0u;
         if (threadIdx.x == 0) {
             if (tile_base) {
                 s_tile = walk;
-                s_excl = walk < ntiles ? tile_base[walk] : 0u;
+                s_excl = walk < ntiles ? tile_base[walk] + gpre : 0u;
             } else {
                 s_tile = next_ticket(tile_ctr, tk, epoch_word, s_epoch);
             }
@@ -3646,18 +3864,24 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
     const uint32_t group_tiles = std::min<uint32_t>(max_tiles, kPersistBlocks);
     HookScope hs(hook, GDF_KERNEL_GROUP);
     const uint32_t* tile_base = nullptr;
+    const uint32_t* tile_gtot = nullptr;
     const uint32_t bigcap = (max_tiles + std::max<uint32_t>(group_tiles, 1u) - 1) /
                             std::max<uint32_t>(group_tiles, 1u);  // tiles per block (walk)
     if (a.group_counts && max_tiles > g_group_scan_tiles) {
         // many tiles: their group-id offsets from a count + scan instead of one ticket each
         // (a single ticket counter serves ~10^2 draws per microsecond)
+        // (up to kMaxGroupScanTiles tiles the count kernel scans its groups of kScanGroup tiles
+        // itself and the group kernels add the group totals: no scan launches)
+        const bool gscan = a.group_done && max_tiles <= kMaxGroupScanTiles;
         hipLaunchKernelGGL(k_group_count, dim3(group_tiles), dim3(256), 0, s, kin, gcount,
-                           a.group_counts);
+                           a.group_counts, gscan ? a.group_done : nullptr, a.group_offsets,
+                           a.group_gtot);
         if ((e = hipGetLastError()) != hipSuccess) return e;
-        if ((e = launch_scan(a.group_counts, max_tiles, a.group_offsets, nullptr, gcount,
-                             (uint32_t)kGroupThreads, s)) != hipSuccess)
+        if (!gscan && (e = launch_scan(a.group_counts, max_tiles, a.group_offsets, nullptr, gcount,
+                                       (uint32_t)kGroupThreads, s)) != hipSuccess)
             return e;
         tile_base = a.group_offsets;
+        tile_gtot = gscan ? a.group_gtot : nullptr;
     }
     if (runs) {  // groups of sorted runs; the long ones by k_group_runs_big
         const uint32_t gb = std::max<uint32_t>(group_tiles, 1u);
@@ -3672,7 +3896,8 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
                            a.average, a.vp, a.group_marks, tile_base, a.bigq, a.bigq_cap, qctr,
                            a.nframes, a.frame_shift, a.frame_vox_start,
                            std::min<uint32_t>(g_run_inblock, g_run_stage >= 2048 ? 2048u : 512u),
-                           kbuf[npasses & 1], vbuf[npasses & 1], g_small_group);  // (free after the sort)
+                           kbuf[npasses & 1], vbuf[npasses & 1], g_small_group,  // (free after the sort)
+                           tile_gtot);
         if (a.average) {
             if ((e = hipGetLastError()) != hipSuccess) return e;
             const bool q16 = g_run_q16 == 1 ||
@@ -3696,7 +3921,7 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
                        reinterpret_cast<uint32_t*>(a.ctrs + kCtrEpoch), a.err, a.hist, a.average,
                        a.vp, a.group_marks, tile_base, tile_base ? a.bigq : nullptr,
                        a.bigcnt, bigcap, a.nframes, a.frame_shift, a.frame_vox_start,
-                       g_small_group, g_points_lane);
+                       g_small_group, g_points_lane, tile_gtot);
     if (tile_base && a.bigq && a.average) {
         if ((e = hipGetLastError()) != hipSuccess) return e;
         hipLaunchKernelGGL(k_group_big, dim3(2048), dim3(256), 0, s, vin, a.pts,

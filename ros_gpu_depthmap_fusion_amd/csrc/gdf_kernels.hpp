@@ -118,6 +118,10 @@ struct VoxelizeArgs {
     uint32_t* group_marks;          // optional: k_group sets the occupancy mark of every voxel
     uint32_t* group_counts;         // [group tiles] group starts per tile (large frames)
     uint32_t* group_offsets;        // [seg_offsets_words(group tiles)] their scan
+    // optional: the scan inside k_group_count (arrive_and_scan, no scan launches) - arrival
+    // counters [group tiles / kScanGroup] (self-resetting) and group totals [same]
+    uint32_t* group_done;
+    uint32_t* group_gtot;
     uint4* bigq;                    // [group blocks * tiles per block] long voxels (large frames)
     uint32_t bigq_cap;              // run mode: one queue of bigq_cap groups (kCtrRunQueue counts)
     uint32_t* bigcnt;               // [group blocks] queued per block
