@@ -749,31 +749,45 @@ def run_component_sync(args, params, frames=300, warm=20):
     from ros_gpu_depthmap_fusion_amd import synth
     from ros_gpu_depthmap_fusion_amd.gdf import GPUDepthmapFusion
     W, H = args.width, args.height
-    eng = GPUDepthmapFusion(0)
     cam = synth.make_camera(0, W, H)
     ring = [synth.WORKLOADS[args.workload](cam, 0, f) for f in range(8)]
-    lat = []
-    for i in range(warm + frames):
-        t0 = time.perf_counter()
-        eng.clear()
-        eng.addDepthmap(ring[i % len(ring)], *cam.intrinsics(), cam.T_world, cam.T_crop)
-        eng.processFrame(params, synchronous=True)
-        pts = eng.downloadPoints()
-        keys = eng.downloadVoxelCoords()
-        vox = eng.downloadVoxelizedPoints()
-        grid = eng.downloadVoxelOccupancyGrid()
-        if i >= warm:
-            lat.append(time.perf_counter() - t0)
-    eng.close()
-    lat = np.array(lat)
+    pc = params.to_c(None, None, False)  # (the frame's wait is the download's)
+
+    def stream(per_call):
+        eng = GPUDepthmapFusion(0)
+        lat = []
+        for i in range(warm + frames):
+            t0 = time.perf_counter()
+            eng.clear()
+            eng.addDepthmap(ring[i % len(ring)], *cam.intrinsics(), cam.T_world, cam.T_crop)
+            if per_call:  # downloadPoints / downloadVoxelCoords / ... one call (and wait) each
+                eng.processFrame(params, synchronous=True)
+                out = [eng.downloadPoints(), eng.downloadVoxelCoords(),
+                       eng.downloadVoxelizedPoints(), eng.downloadVoxelOccupancyGrid()]
+            else:  # gdf_download_frame: the four copies into pinned mirrors, one wait
+                eng.processFramePrepared(pc)
+                out = list(eng.download_frame().values())
+            if i >= warm:
+                lat.append(time.perf_counter() - t0)
+        nbytes = int(sum(a.nbytes for a in out))
+        eng.close()
+        return np.array(lat), nbytes
+
+    lat, nbytes = stream(False)
+    lat_pc, _ = stream(True)
     return {"workload": "C2 component-equivalent: one %dx%d host depth frame at a time, "
                         "synchronous, with the per-frame downloads (points, voxel coords, "
-                        "voxelized points, u8 grid)" % (W, H),
+                        "voxelized points, u8 grid) through gdf_download_frame" % (W, H),
             "value": round(W * H * len(lat) / lat.sum() / 1e6, 3),
             "latency_ms_median": round(float(np.median(lat)) * 1e3, 4),
             "latency_ms_p99": round(float(np.percentile(lat, 99)) * 1e3, 4),
             "frames": len(lat),
-            "download_bytes_per_frame": int(pts.nbytes + keys.nbytes + vox.nbytes + grid.nbytes)}
+            "download_bytes_per_frame": nbytes,
+            "per_call_downloads": {
+                "latency_ms_median": round(float(np.median(lat_pc)) * 1e3, 4),
+                "latency_ms_p99": round(float(np.percentile(lat_pc, 99)) * 1e3, 4),
+                "note": "the same frames with the four per-call downloads (one wait each, "
+                        "pageable destinations)"}}
 
 
 def run_h2d(args, params, steps, warm):

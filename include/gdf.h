@@ -248,6 +248,28 @@ int gdf_get_grid_size(gdf_engine* engine, uint32_t grid_size[3], uint64_t* num_c
 int gdf_get_device_results(gdf_engine* engine, const float** points, const uint32_t** coords,
                            const float** voxelized, const uint8_t** occupancy);
 
+/* All of a frame's host-side outputs at once (the component downloads points, voxel coords, the
+ * voxelized cloud and the u8 grid every frame, component.cpp:297-401): the copies run on the
+ * frame's stream into engine-owned pinned host mirrors of the addressed slot, with one wait for
+ * them all; the pointers stay valid until the slot's next gdf_download_frame (or gdf_destroy).
+ * `what` is a mask of GDF_DL_*; members not asked for are NULL / 0.  (No single reference
+ * counterpart: it replaces downloadPoints + downloadVoxelCoords + the voxelized download +
+ * downloadVoxelOccupancyGrid, fusion.cpp:1712-1718, 1824-1839, 2946-2951.) */
+#define GDF_DL_POINTS 1u
+#define GDF_DL_COORDS 2u
+#define GDF_DL_VOXELIZED 4u
+#define GDF_DL_GRID 8u
+typedef struct gdf_host_frame {
+    const float* points;            /* float4[num_points]  (m_points)            */
+    const uint32_t* voxel_coords;   /* uint32[num_points]  (m_voxelCoords)       */
+    uint32_t num_points;
+    const float* voxelized;         /* float4[num_voxelized] (m_points_voxelized) */
+    uint32_t num_voxelized;
+    const uint8_t* occupancy;       /* uint8[num_cells]    (m_occupancyGrid)     */
+    uint64_t num_cells;
+} gdf_host_frame;
+int gdf_download_frame(gdf_engine* engine, uint32_t what, gdf_host_frame* out);
+
 /* ---- whole frame -------------------------------------------------------------------------- */
 /* The per-frame sequence of GPUDepthmapFusionComponent::processDepthmaps
  * (component.cpp:92-300) from uploadPointSequences through downloadVoxelOccupancyGrid, for the

@@ -335,6 +335,26 @@ struct Slot {
     DevBuf d_pcnt, d_poff;          // multi-GPU key-range partition workspace
     DevBuf d_xcnt, d_xoff, d_xrk, d_xrs;  // runs of a received (point, key) list
     DevBuf d_grpdone, d_grptot;     // in-kernel group scan of the segment counts
+    struct Pinned {                 // pinned host mirror (gdf_download_frame)
+        void* p = nullptr;
+        size_t bytes = 0;
+        void* ensure(size_t need) {
+            if (need <= bytes) return p;
+            if (p) (void)hipHostFree(p);
+            p = nullptr;
+            bytes = 0;
+            const size_t nb = std::max(need, bytes + bytes / 2);
+            if (hipHostMalloc(&p, nb, hipHostMallocDefault) != hipSuccess) {
+                p = nullptr;
+                return nullptr;
+            }
+            bytes = nb;
+            return p;
+        }
+        ~Pinned() {
+            if (p) (void)hipHostFree(p);
+        }
+    } h_pts, h_coords, h_vox, h_grid;
     DevBuf d_ggdone, d_ggtot;       // ... and of the group phase's tile counts
     DevBuf d_wruns, d_runkeys, d_runstart;  // runs of equal keys
     bool runs_sel = false;          // ... counted in kRunTotal (frame with rollbuffer points)
@@ -2070,6 +2090,47 @@ int gdf_download_occupancy_grid(gdf_engine* e, uint8_t* out, uint64_t cap) {
         sync_all(e);  // grid updates may still run on another slot's stream
         e->sync();
         HIPCHK(hipMemcpy(out, grid_out_ptr(e), e->ncells, hipMemcpyDeviceToHost));
+    });
+}
+
+int gdf_download_frame(gdf_engine* e, uint32_t what, gdf_host_frame* out) {
+    ENGINE_OR_FAIL(e);
+    if (!out) return GDF_ERR_ARG;
+    return guarded(e, [&] {
+        Slot& q = e->sl();
+        *out = gdf_host_frame{};
+        if ((what & (GDF_DL_POINTS | GDF_DL_COORDS)) && !q.compacted)
+            fail(GDF_ERR_STATE, "download_frame: no compaction has run");
+        if ((what & GDF_DL_COORDS) && !q.coords_valid) fail(GDF_ERR_STATE, "download_frame: no voxel coords");
+        if ((what & GDF_DL_VOXELIZED) && !q.vox_valid) fail(GDF_ERR_STATE, "download_frame: no voxelize has run");
+        if ((what & GDF_DL_GRID) && (!e->grid_set || !e->invoked_once))
+            fail(GDF_ERR_STATE, "download_frame: no voxelOccupancyGrid has run");
+        if (what & GDF_DL_GRID) sync_all(e);  // grid updates may still run on another slot's stream
+        e->read_misc();  // the counts (one wait)
+        const uint32_t n = q.h_misc[kCount], nv = q.h_misc[kVoxCount];
+        auto copy = [&](Slot::Pinned& m, const void* src, size_t bytes) -> void* {
+            void* dst = m.ensure(std::max<size_t>(bytes, 64));
+            if (!dst) fail(GDF_ERR_NOMEM, "pinned host mirror allocation failed");
+            if (bytes) HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, e->s()));
+            return dst;
+        };
+        if (what & GDF_DL_POINTS) {
+            out->points = static_cast<const float*>(copy(q.h_pts, q.d_pts.p, (size_t)n * 16));
+            out->num_points = n;
+        }
+        if (what & GDF_DL_COORDS) {
+            out->voxel_coords = static_cast<const uint32_t*>(copy(q.h_coords, q.d_coords.p, (size_t)n * 4));
+            out->num_points = n;
+        }
+        if (what & GDF_DL_VOXELIZED) {
+            out->voxelized = static_cast<const float*>(copy(q.h_vox, q.d_vox.p, (size_t)nv * 16));
+            out->num_voxelized = nv;
+        }
+        if (what & GDF_DL_GRID) {
+            out->occupancy = static_cast<const uint8_t*>(copy(q.h_grid, grid_out_ptr(e), e->ncells));
+            out->num_cells = e->ncells;
+        }
+        e->sync();  // every copy (the second wait)
     });
 }
 

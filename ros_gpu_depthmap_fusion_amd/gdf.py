@@ -74,6 +74,15 @@ class FrameResult(C.Structure):
                 ("latest_time_nsec", C.c_uint32)]
 
 
+class HostFrame(C.Structure):
+    _fields_ = [("points", C.c_void_p), ("voxel_coords", C.c_void_p), ("num_points", C.c_uint32),
+                ("voxelized", C.c_void_p), ("num_voxelized", C.c_uint32),
+                ("occupancy", C.c_void_p), ("num_cells", C.c_uint64)]
+
+
+DL_POINTS, DL_COORDS, DL_VOXELIZED, DL_GRID = 1, 2, 4, 8
+
+
 class SegCounts(C.Structure):
     """gdf_seg_counts (include/gdf_segment.h)."""
     _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("layers", C.c_uint32),
@@ -132,6 +141,7 @@ EXPORTED = [
     "gdf_mask_dilate", "gdf_transform_points", "gdf_add_halo_depthmap_device",
     "gdf_partition_points", "gdf_voxelize_points", "gdf_last_sort_items", "gdf_get_stream",
     "gdf_get_graph_stats", "gdf_get_slot", "gdf_select_slot", "gdf_build_info",
+    "gdf_download_frame",
     # include/gdf_segment.h: the GPU object-segmentation front end
     "gdf_seg_create", "gdf_seg_destroy", "gdf_seg_set_stream", "gdf_seg_label_layers",
     "gdf_seg_label_engine_grid", "gdf_seg_get_counts", "gdf_seg_download_labels",
@@ -228,6 +238,7 @@ def load_library(path: str = LIB_PATH):
         "gdf_get_slot": (i32, [vp, P(i32)]),
         "gdf_select_slot": (i32, [vp, i32]),
         "gdf_build_info": (C.c_char_p, []),
+        "gdf_download_frame": (i32, [vp, u32, P(HostFrame)]),
         "gdf_seg_create": (i32, [i32, P(vp)]),
         "gdf_seg_destroy": (i32, [vp]),
         "gdf_seg_set_stream": (i32, [vp, vp]),
@@ -529,6 +540,30 @@ class GPUDepthmapFusion:
         n = C.c_uint32()
         self._check(self._lib.gdf_get_point_count(self._h, C.byref(n)))
         return n.value
+
+    def download_frame(self, what: int = 15) -> dict:
+        """gdf_download_frame: the frame's points / voxel coords / voxelized cloud / u8 grid in
+        one pass into the engine's pinned host mirrors - numpy views of them (no copy), valid
+        until the slot's next download_frame."""
+        hf = HostFrame()
+        self._check(self._lib.gdf_download_frame(self._h, what, C.byref(hf)))
+
+        def view(ptr, ctype, count, shape):
+            if not ptr or count == 0:
+                return np.zeros(shape if count == 0 else (0,), dtype=np.dtype(ctype))
+            buf = (ctype * count).from_address(ptr)
+            return np.ctypeslib.as_array(buf).reshape(shape)
+        out = {}
+        if what & DL_POINTS:
+            out["points"] = view(hf.points, C.c_float, 4 * hf.num_points, (hf.num_points, 4))
+        if what & DL_COORDS:
+            out["voxel_coords"] = view(hf.voxel_coords, C.c_uint32, hf.num_points, (hf.num_points,))
+        if what & DL_VOXELIZED:
+            out["voxelized"] = view(hf.voxelized, C.c_float, 4 * hf.num_voxelized,
+                                    (hf.num_voxelized, 4))
+        if what & DL_GRID:
+            out["occupancy"] = view(hf.occupancy, C.c_uint8, hf.num_cells, (hf.num_cells,))
+        return out
 
     def downloadPoints(self) -> np.ndarray:
         n = self.point_count()
