@@ -1039,6 +1039,45 @@ __device__ __forceinline__ void ring_pass2(const P3x2& u, const P3x2& d, const P
     out1 = nz1 & pass1;
 }
 
+// the world rows of transform_points (mrow's order) for two pixels at once
+template <class P>
+__device__ __forceinline__ f2v mrow2(P m, f2v x, f2v y, f2v z) {
+    return ((f2(m[0], m[0]) * x + f2(m[1], m[1]) * y) + f2(m[2], m[2]) * z) +
+           f2(m[3], m[3]) * f2(1.0f, 1.0f);
+}
+
+// voxel_key of two points: the packed quotients, then per element voxel_axis' exact-division
+// guard, clamp and floor (the same operations as voxel_key)
+__device__ __forceinline__ float voxel_axis_fix(float q, float d, float cs) {
+    const float r = rintf(q);
+    if (__builtin_expect(fabsf(q - r) <= fabsf(q) * 9.5367431640625e-07f, 0)) return d / cs;  // 2^-20
+    return q;
+}
+__device__ __forceinline__ void voxel_key2(f2v px, f2v py, f2v pz, const float* vlo,
+                                           const float* vcs, const float* vrcs,
+                                           const float* gmax, const uint32_t* gs, uint32_t& k0,
+                                           uint32_t& k1) {
+    const f2v dx = px - f2(vlo[0], vlo[0]), dy = py - f2(vlo[1], vlo[1]), dz = pz - f2(vlo[2], vlo[2]);
+    const f2v qx = dx * f2(vrcs[0], vrcs[0]), qy = dy * f2(vrcs[1], vrcs[1]), qz = dz * f2(vrcs[2], vrcs[2]);
+    float f[2][3];
+    f[0][0] = voxel_axis_fix(qx.x, dx.x, vcs[0]);
+    f[1][0] = voxel_axis_fix(qx.y, dx.y, vcs[0]);
+    f[0][1] = voxel_axis_fix(qy.x, dy.x, vcs[1]);
+    f[1][1] = voxel_axis_fix(qy.y, dy.y, vcs[1]);
+    f[0][2] = voxel_axis_fix(qz.x, dz.x, vcs[2]);
+    f[1][2] = voxel_axis_fix(qz.y, dz.y, vcs[2]);
+    uint32_t k[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const uint32_t ux = (uint32_t)floorf(fminf(fmaxf(f[j][0], 0.0f), gmax[0]));
+        const uint32_t uy = (uint32_t)floorf(fminf(fmaxf(f[j][1], 0.0f), gmax[1]));
+        const uint32_t uz = (uint32_t)floorf(fminf(fmaxf(f[j][2], 0.0f), gmax[2]));
+        k[j] = ux + uy * gs[0] + uz * gs[0] * gs[1];
+    }
+    k0 = k[0];
+    k1 = k[1];
+}
+
 template <int AMODE>
 __device__ __forceinline__ void depth_bits_px2(const FrameArgs& a, const CamDesc* cams, int k,
                                                const Band& t, const float* s_yn, const uint32_t* x,
@@ -1218,7 +1257,19 @@ __global__ __launch_bounds__(SEGW / PX) void k_mask_px(FrameArgs a) {
 #pragma unroll
                 for (int j = 0; j < PX; ++j)
                     bits[j] = depth_bits<false, kGeneral, 4>(a, s_cams, sg.k, t, s_yn, x[j], sg.y, in[j]);
-            if (a.run_mode) {
+            if (a.run_mode && PX == 2 && a.mask_packed) {  // both pixels' keys in packed f32
+                const CamDesc& cd = s_cams[sg.k];
+                if ((bits[0] | bits[PX - 1]) & 4u) {
+                    const P3x2 p = band_pt2(t, h, (int)x[0], h, (int)x[PX - 1],
+                                            f2(s_yn[h], s_yn[h]), cd.scale);
+                    uint32_t k0, k1;
+                    voxel_key2(mrow2(cd.Tw + 0, p.x, p.y, p.z), mrow2(cd.Tw + 4, p.x, p.y, p.z),
+                               mrow2(cd.Tw + 8, p.x, p.y, p.z), a.vlo, a.vcs, a.vrcs, a.gmax, a.gs,
+                               k0, k1);
+                    if (bits[0] & 4u) rkey[0] = k0 | (cd.frame << a.frame_shift);
+                    if (bits[PX - 1] & 4u) rkey[PX - 1] = k1 | (cd.frame << a.frame_shift);
+                }
+            } else if (a.run_mode) {
                 const CamDesc& cd = s_cams[sg.k];
 #pragma unroll
                 for (int j = 0; j < PX; ++j)
@@ -1679,6 +1730,15 @@ __global__ __launch_bounds__(SEGW / 2) void k_emit_px2(FrameArgs a) {
         if (s == gridDim.x - 1) G(a.frame_pt_start)[a.nframes] = base + tot;
     }
     const unsigned long long ltm = lanemask_lt();
+    // the world points (and keys) of the thread's two pixels in packed f32 (the same operations
+    // as k_emit: convert, transform_points' rows, compute_voxel_coords)
+    const f2v zz2 = f2((float)dval[0], (float)dval[1]) * f2(cams[k].scale, cams[k].scale);
+    const f2v px2 = f2(xnv[0], xnv[1]) * zz2, py2 = f2(ynv, ynv) * zz2, pz2 = zz2;
+    const f2v wx2 = mrow2(cams[k].Tw + 0, px2, py2, pz2), wy2 = mrow2(cams[k].Tw + 4, px2, py2, pz2);
+    const f2v wz2 = mrow2(cams[k].Tw + 8, px2, py2, pz2), ww2 = mrow2(cams[k].Tw + 12, px2, py2, pz2);
+    uint32_t key2[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
+    if (a.do_voxel && (m[0] | m[1]))
+        voxel_key2(wx2, wy2, wz2, a.vlo, a.vcs, a.vrcs, a.gmax, a.gs, key2[0], key2[1]);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         const uint32_t word = (uint32_t)wid + NW * q;
@@ -1692,15 +1752,11 @@ __global__ __launch_bounds__(SEGW / 2) void k_emit_px2(FrameArgs a) {
         uint32_t key = 0xFFFFFFFFu;
         if (valid) {
             const uint32_t pos = base + wpre + (uint32_t)__popcll(m[q] & ltm);
-            const float zz = (float)dval[q] * cams[k].scale;
-            const float px = xnv[q] * zz, py = ynv * zz, pz = zz;
-            const float4 w4 = make_float4(mrow(cams[k].Tw + 0, px, py, pz, 1.0f),
-                                          mrow(cams[k].Tw + 4, px, py, pz, 1.0f),
-                                          mrow(cams[k].Tw + 8, px, py, pz, 1.0f),
-                                          mrow(cams[k].Tw + 12, px, py, pz, 1.0f));
+            const float4 w4 = q == 0 ? make_float4(wx2.x, wy2.x, wz2.x, ww2.x)
+                                     : make_float4(wx2.y, wy2.y, wz2.y, ww2.y);
             gst4(a.out_pts, pos, w4);
             if (a.do_voxel) {
-                key = voxel_key(w4.x, w4.y, w4.z, a.vlo, a.vcs, a.vrcs, a.gmax, a.gs);
+                key = key2[q];
                 G(a.out_coords)[pos] = key;
             }
         }
