@@ -69,6 +69,11 @@ struct GridSeq {
     const uint32_t* fptr;  // the update's sequence number on the device (or nullptr: use f)
     uint32_t f;
     uint32_t* err;
+    // optional delta of a single-frame u8 update (gdf_download_frame's grid): every 32-cell
+    // group whose bytes changed, as (word index, new 32 bytes) appended at *dcnt (zeroed before)
+    uint32_t* dcnt;
+    uint32_t* didx;
+    uint4* ddata;
 };
 
 // A halo camera (emit == 0, multi-GPU sharding) sits at a negative offset: its pixels are only

@@ -287,7 +287,7 @@ bool ros_time_minus(uint32_t sec, uint32_t nsec, double seconds, uint32_t* os, u
 enum MiscSlot {
     kCount = 0, kTileCtr = 1, kErr = 2, kVoxCount = 3, kGridTicket = 4, kDepthCount = 5,
     kSelTotal = 6, kPartTotal = 7, kRecvCount = 8, kRunCount = 9, kScanTotal = 10, kRunTotal = 11,
-    kRecvRuns = 12, kMiscWords = 16
+    kRecvRuns = 12, kDeltaCount = 13, kMiscWords = 16
 };
 
 }  // namespace
@@ -354,7 +354,10 @@ struct Slot {
         ~Pinned() {
             if (p) (void)hipHostFree(p);
         }
-    } h_pts, h_coords, h_vox, h_grid;
+    } h_pts, h_coords, h_vox, h_delta;
+    DevBuf d_didx, d_ddata;         // the grid delta of this slot's single-frame update
+    bool delta_valid = false;
+    uint32_t delta_ticket = 0;      // ... and that update's sequence number
     DevBuf d_ggdone, d_ggtot;       // ... and of the group phase's tile counts
     DevBuf d_wruns, d_runkeys, d_runstart;  // runs of equal keys
     bool runs_sel = false;          // ... counted in kRunTotal (frame with rollbuffer points)
@@ -478,6 +481,13 @@ struct gdf_engine {
     bool xruns = !getenv("GDF_NO_XRUNS");  // voxelize_points sorts the received list's runs
     bool group_scan = !getenv("GDF_NO_GROUP_SCAN");  // segment offsets without scan launches
     bool mask_packed = !getenv("GDF_NO_MASK_PACKED");  // k_mask_px<2>: packed f32 pixel pairs
+    // host mirror of the u8 grid (gdf_download_frame): after the first grid download, single-frame
+    // updates also list the 32-cell groups they changed, and the next download moves only those
+    bool grid_delta = false;
+    bool grid_delta_allowed = !getenv("GDF_NO_GRID_DELTA");
+    Slot::Pinned h_mirror;
+    bool mirror_valid = false;
+    uint32_t mirror_ticket = 0, mirror_gen = 0;
 
     // compaction outputs
 
@@ -1117,6 +1127,24 @@ uint64_t mark_words(const gdf_engine* e) { return (e->ncells + 31) / 32; }
 
 void ensure_misc(gdf_engine* e);
 
+// The delta outputs (changed 32-cell groups) of the single-frame u8 grid update about to be
+// issued with sequence number t on the current slot - once a grid download asked for them.
+void delta_args(gdf_engine* e, GridSeq& q, uint32_t t, bool single) {
+    Slot& sl = e->sl();
+    sl.delta_valid = false;
+    if (!e->grid_delta || !single || e->grid_mode != 0) return;
+    const uint64_t nw = mark_words(e);
+    sl.d_didx.ensure(nw * 4);
+    sl.d_ddata.ensure(nw * 32);
+    ensure_misc(e);
+    HIPCHK(hipMemsetAsync(sl.d_misc.as<uint32_t>() + kDeltaCount, 0, 4, e->s()));
+    q.dcnt = sl.d_misc.as<uint32_t>() + kDeltaCount;
+    q.didx = sl.d_didx.as<uint32_t>();
+    q.ddata = sl.d_ddata.as<uint4>();
+    sl.delta_valid = true;
+    sl.delta_ticket = t;
+}
+
 // switch to the general u32 history once a lifetime no longer fits the u8 grid
 void widen_if_needed(gdf_engine* e, uint32_t lifetime, hipStream_t st) {
     if (e->grid_mode != 0 || lifetime <= 255) return;
@@ -1465,6 +1493,7 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime,
         v.lifetime = (uint32_t)fused_grid_lifetime;
         // the ticket was stored by this frame's k_mask (run_frame: grid_seq = grid_ticket)
         v.gseq = e->grid_seq(0, e->sl().d_misc.as<uint32_t>() + kGridTicket);
+        delta_args(e, v.gseq, e->grid_ticket, e->nframes == 1);
         e->grid_ticket++;
         if (e->nframes > 1) v.snap = snap_args(e, fused_grid_blocks(e->ncells), e->nframes);
     }
@@ -1614,7 +1643,9 @@ void occupancy_grid(gdf_engine* e, uint32_t lifetime, hipStream_t st) {  // fusi
                               std::max<uint32_t>(e->sl().n_total, 1), marks_ptr(e), st));
     }
     ensure_misc(e);
-    const GridSeq q = e->grid_seq(e->grid_ticket++);
+    GridSeq q = e->grid_seq(e->grid_ticket);
+    delta_args(e, q, e->grid_ticket, st == e->s());
+    e->grid_ticket++;
     e->timed_on(GDF_KERNEL_GRID, st, [&] {
         if (e->grid_mode == 0)
             HIPCHK(launch_grid_u8(e->d_grid8.as<uint8_t>(), marks_ptr(e), e->ncells, lifetime, q, st));
@@ -2126,11 +2157,45 @@ int gdf_download_frame(gdf_engine* e, uint32_t what, gdf_host_frame* out) {
             out->voxelized = static_cast<const float*>(copy(q.h_vox, q.d_vox.p, (size_t)nv * 16));
             out->num_voxelized = nv;
         }
+        // the grid: into the engine's host mirror - only the groups the last update changed when
+        // the mirror holds the grid right before it (a frame-by-frame component), else all of it
+        bool apply_delta = false;
+        uint32_t nd = 0;
         if (what & GDF_DL_GRID) {
-            out->occupancy = static_cast<const uint8_t*>(copy(q.h_grid, grid_out_ptr(e), e->ncells));
+            const uint32_t latest = e->grid_ticket - 1u;
+            nd = q.h_misc[kDeltaCount];
+            apply_delta = q.delta_valid && q.delta_ticket == latest && e->mirror_valid &&
+                          e->mirror_gen == e->grid_gen && e->mirror_ticket + 1u == latest &&
+                          e->grid_mode == 0;
+            const size_t padded = (size_t)mark_words(e) * 32;
+            if (!e->h_mirror.ensure(padded)) fail(GDF_ERR_NOMEM, "pinned grid mirror allocation failed");
+            if (apply_delta) {
+                uint8_t* st = static_cast<uint8_t*>(q.h_delta.ensure((size_t)std::max<uint32_t>(nd, 1) * 36));
+                if (!st) fail(GDF_ERR_NOMEM, "pinned delta staging allocation failed");
+                if (nd) {
+                    HIPCHK(hipMemcpyAsync(st, q.d_didx.p, (size_t)nd * 4, hipMemcpyDeviceToHost, e->s()));
+                    HIPCHK(hipMemcpyAsync(st + (size_t)nd * 4, q.d_ddata.p, (size_t)nd * 32,
+                                          hipMemcpyDeviceToHost, e->s()));
+                }
+            } else {
+                HIPCHK(hipMemcpyAsync(e->h_mirror.p, grid_out_ptr(e), e->ncells, hipMemcpyDeviceToHost,
+                                      e->s()));
+            }
+            e->mirror_valid = true;
+            e->mirror_ticket = latest;
+            e->mirror_gen = e->grid_gen;
+            out->occupancy = static_cast<const uint8_t*>(e->h_mirror.p);
             out->num_cells = e->ncells;
         }
         e->sync();  // every copy (the second wait)
+        if (apply_delta && nd) {  // the changed groups into the mirror (32 bytes each)
+            const uint8_t* st = static_cast<const uint8_t*>(q.h_delta.p);
+            const uint32_t* idx = reinterpret_cast<const uint32_t*>(st);
+            const uint8_t* data = st + (size_t)nd * 4;
+            uint8_t* mir = static_cast<uint8_t*>(e->h_mirror.p);
+            for (uint32_t k = 0; k < nd; ++k) std::memcpy(mir + (size_t)idx[k] * 32, data + (size_t)k * 32, 32);
+        }
+        if ((what & GDF_DL_GRID) && e->grid_delta_allowed) e->grid_delta = true;  // from now on
     });
 }
 
@@ -2476,6 +2541,7 @@ int gdf_voxel_occupancy_grid_batch(gdf_engine* e, const uint32_t* bits, uint64_t
             if (e->slots[i].marks_set)
                 fail(GDF_ERR_STATE, "marks of a frame are pending (take them first)");
         widen_if_needed(e, lifetime, e->s());
+        e->sl().delta_valid = false;
         if (e->grid_mode == 0) {  // one pass per <= kMaxCams frames
             ensure_misc(e);
             // per-frame snapshots only for the slot's own multi-frame batch (<= kMaxCams frames,

@@ -2227,22 +2227,51 @@ __device__ __forceinline__ uint32_t grid_word(uint32_t w, uint32_t mb, uint32_t 
 // word) per thread and step; the grid allocation is padded to 32 bytes
 __device__ __forceinline__ void grid_u8_part(uint4* __restrict__ grid, uint32_t* __restrict__ marks,
                                              uint64_t nwords, uint32_t L, uint32_t block,
-                                             uint32_t nblocks) {
-    for (uint64_t i = block * (uint64_t)blockDim.x + threadIdx.x; i < nwords;
-         i += (uint64_t)nblocks * blockDim.x) {
-        uint4 v0 = grid[2 * i], v1 = grid[2 * i + 1];
-        const uint32_t m = marks[i];
-        v0.x = grid_word(v0.x, m, L);
-        v0.y = grid_word(v0.y, m >> 4, L);
-        v0.z = grid_word(v0.z, m >> 8, L);
-        v0.w = grid_word(v0.w, m >> 12, L);
-        v1.x = grid_word(v1.x, m >> 16, L);
-        v1.y = grid_word(v1.y, m >> 20, L);
-        v1.z = grid_word(v1.z, m >> 24, L);
-        v1.w = grid_word(v1.w, m >> 28, L);
-        grid[2 * i] = v0;
-        grid[2 * i + 1] = v1;
-        if (m) marks[i] = 0u;
+                                             uint32_t nblocks, const GridSeq& q) {
+    const uint64_t stride = (uint64_t)nblocks * blockDim.x;
+    // wave-uniform loop (the delta's ballots need every lane)
+    for (uint64_t i0 = block * (uint64_t)blockDim.x + (threadIdx.x & ~63u); i0 < nwords; i0 += stride) {
+        const uint64_t i = i0 + (threadIdx.x & 63u);
+        const bool act = i < nwords;
+        uint4 o0 = make_uint4(0u, 0u, 0u, 0u), o1 = o0;
+        uint32_t m = 0;
+        if (act) {
+            o0 = grid[2 * i];
+            o1 = grid[2 * i + 1];
+            m = marks[i];
+        }
+        uint4 v0, v1;
+        v0.x = grid_word(o0.x, m, L);
+        v0.y = grid_word(o0.y, m >> 4, L);
+        v0.z = grid_word(o0.z, m >> 8, L);
+        v0.w = grid_word(o0.w, m >> 12, L);
+        v1.x = grid_word(o1.x, m >> 16, L);
+        v1.y = grid_word(o1.y, m >> 20, L);
+        v1.z = grid_word(o1.z, m >> 24, L);
+        v1.w = grid_word(o1.w, m >> 28, L);
+        if (act) {
+            grid[2 * i] = v0;
+            grid[2 * i + 1] = v1;
+            if (m) marks[i] = 0u;
+        }
+        if (q.dcnt) {  // the changed groups (a frame: the grid's ~1-2 % non-zero cells)
+            const bool ch = act && ((o0.x ^ v0.x) | (o0.y ^ v0.y) | (o0.z ^ v0.z) | (o0.w ^ v0.w) |
+                                    (o1.x ^ v1.x) | (o1.y ^ v1.y) | (o1.z ^ v1.z) | (o1.w ^ v1.w)) != 0u;
+            const unsigned long long b = __ballot(ch);
+            if (b) {  // wave-uniform: one append per wave step
+                uint32_t base = 0;
+                if ((threadIdx.x & 63u) == 0)
+                    base = __hip_atomic_fetch_add(q.dcnt, (uint32_t)__popcll(b), __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+                base = __shfl(base, 0, 64);
+                if (ch) {
+                    const uint32_t e = base + (uint32_t)__popcll(b & lanemask_lt());
+                    q.didx[e] = (uint32_t)i;
+                    q.ddata[2 * (uint64_t)e] = v0;
+                    q.ddata[2 * (uint64_t)e + 1] = v1;
+                }
+            }
+        }
     }
 }
 
@@ -2383,7 +2412,7 @@ __global__ __launch_bounds__(256) void k_grid_u8(uint4* __restrict__ grid,
                                                  uint32_t* __restrict__ marks, uint64_t nwords,
                                                  uint32_t L, GridSeq q) {
     const uint32_t f = grid_seq_enter(q);
-    grid_u8_part(grid, marks, nwords, L, blockIdx.x, gridDim.x);
+    grid_u8_part(grid, marks, nwords, L, blockIdx.x, gridDim.x, q);
     grid_seq_leave(q, f, gridDim.x);
 }
 
@@ -2644,7 +2673,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
                                 gridDim.x - grid_block0, nframes, mark_words, snap);
         else
             grid_u8_part(grid, marks, grid_nwords, lifetime, blockIdx.x - grid_block0,
-                         gridDim.x - grid_block0);
+                         gridDim.x - grid_block0, q);
         grid_seq_leave(q, f, gridDim.x - grid_block0);
         return;
     }

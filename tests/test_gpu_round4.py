@@ -1,7 +1,10 @@
 """GPU tests added in round 4 (bar: bit-exact against the oracle, as test_gpu_parity.py).
 
 * gdf_download_frame (the component's four per-frame downloads in one pass into pinned host
-  mirrors) returns exactly what the per-call downloads return, and the oracle's outputs;
+  mirrors) returns exactly what the per-call downloads return, and the oracle's outputs - the
+  grid through its host mirror, updated from the changed 32-cell groups of each single-frame
+  update once the mirror holds the previous grid (full copies after batches, skipped downloads,
+  lifetime changes);
 * the packed-f32 two-pixel flying filter (k_mask_px<2>, default) and the in-kernel group scans
   (segment counts in k_mask, group starts in k_group_count, default) against their switched-off
   forms and the oracle, on 8-frame VGA batches (9600 segments: the group-scan range) and a 4K
@@ -67,6 +70,61 @@ def test_download_frame_equals_per_call_downloads(Engine):
         assert np.array_equal(d["voxelized"][:, :3].view(np.uint32), w.view(np.uint32))
     only = gpu.download_frame(8)  # the grid alone
     assert set(only) == {"occupancy"}
+
+
+def test_download_frame_grid_mirror_deltas(Engine):
+    """The grid mirror across single frames (delta path), a skipped download, a 3-frame batch
+    (full copy), a rollbuffer frame (k_grid_u8: delta), the stage-by-stage grid call and a
+    lifetime above 255 (u32 history: full copies): every downloaded grid equals the oracle's."""
+    p = ComponentParams()
+    cam = synth.make_camera(0, 320, 240)
+    lidar = synth.make_camera(1, 64, 48)
+    pts = synth.back_project(lidar, synth.dense_frame(lidar, 1, 0))
+    eye = np.eye(4, dtype=np.float32)
+    gpu, orc = Engine(), OracleFusion(threads=8)
+    f = 0
+
+    def frame(download=True, seq=False):
+        nonlocal f
+        for e in (gpu, orc):
+            if seq:
+                e.addPointSequence(pts, *synth.sequence_time(f), synth.move_transform(f))
+            e.clear()
+            e.addDepthmap(*cam_args(cam, synth.dense_frame(cam, 0, f)))
+            if seq:
+                e.processFrame(p, T_world_move=eye, T_crop_move=eye)
+            else:
+                e.processFrame(p)
+        f += 1
+        if download:
+            g = gpu.download_frame(8)["occupancy"]
+            assert np.array_equal(g, orc.downloadVoxelOccupancyGrid()), f"frame {f - 1}"
+
+    for _ in range(5):
+        frame()
+    frame(download=False)
+    frame()
+    frame()
+    # a batch of 3 frames (the batched update keeps no delta: the next download is a full copy)
+    gpu.clear()
+    for j in range(3):
+        if j:
+            gpu.nextFrameInBatch()
+        gpu.addDepthmap(*cam_args(cam, synth.dense_frame(cam, 0, f + j)))
+    gpu.processFrame(p)
+    for j in range(3):
+        orc.clear()
+        orc.addDepthmap(*cam_args(cam, synth.dense_frame(cam, 0, f + j)))
+        orc.processFrame(p)
+    f += 3
+    assert np.array_equal(gpu.download_frame(8)["occupancy"], orc.downloadVoxelOccupancyGrid())
+    frame()
+    frame(seq=True)  # rollbuffer frame: marks from the voxel groups, k_grid_u8 update
+    frame(seq=True)
+    frame()
+    p.occupancy_lifetime = 300  # u32 history from here on
+    frame()
+    frame()
 
 
 @pytest.mark.parametrize("knobs", [{}, {"GDF_NO_MASK_PACKED": "1"}, {"GDF_NO_GROUP_SCAN": "1"}])
