@@ -145,6 +145,11 @@ int gdf_set_pipeline_depth(gdf_engine* engine, int depth);
  * cleared slot, whatever slot is selected.  (No reference counterpart: the reference runs one
  * frame at a time.) */
 int gdf_get_slot(gdf_engine* engine, int* slot);
+/* The pipeline slots' streams from the caller (e.g. torch streams, so the caller's allocator and
+ * collectives share them): slot i runs on streams[i] (i < n; the others keep the engine's own);
+ * the engine synchronises but never destroys them.  n = 0 restores the engine's streams.  Not
+ * with gdf_set_stream. */
+int gdf_set_slot_streams(gdf_engine* engine, void* const* streams, int n);
 int gdf_select_slot(gdf_engine* engine, int slot);
 /* Steady-state frames of gdf_process_frame as HIP graphs (default on; env GDF_NO_GRAPHS turns
  * the default off): when a slot's frame repeats the launch arguments of its previous frame (all

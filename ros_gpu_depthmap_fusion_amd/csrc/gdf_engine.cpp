@@ -303,6 +303,8 @@ constexpr int kMaxPipe = 4;
 // ~20 us of GPU time per frame on this device (tools/graph_probe.hip).
 struct Slot {
     hipStream_t own = nullptr;
+    hipStream_t ext = nullptr;      // caller-owned stream of this slot (gdf_set_slot_streams)
+    hipStream_t stream() const { return ext ? ext : own; }
     DevBuf d_depth;                 // host depth maps uploaded for this frame
     void* h_stage = nullptr;        // pinned staging of pageable host depth maps
     size_t h_stage_bytes = 0;
@@ -519,7 +521,7 @@ struct gdf_engine {
     double prof_ms[GDF_KERNEL_SLOTS] = {};
     uint64_t prof_n[GDF_KERNEL_SLOTS] = {};
 
-    hipStream_t s() const { return user_stream ? user_stream : sl().own; }
+    hipStream_t s() const { return user_stream ? user_stream : sl().stream(); }
 
     hipEvent_t take_event() {
         if (!ev_pool.empty()) {
@@ -599,7 +601,7 @@ struct gdf_engine {
     void serialize() {
         if (npipe <= 1 || serialized) return;
         for (int i = 0; i < npipe; ++i)
-            if (i != cur && slots[i].own) HIPCHK(hipStreamSynchronize(slots[i].own));
+            if (i != cur && slots[i].stream()) HIPCHK(hipStreamSynchronize(slots[i].stream()));
         serialized = true;
     }
     // the ordering of one historic-grid update: ticket f (or the ticket the frame's k_mask stored)
@@ -626,7 +628,7 @@ void create_slot(Slot& sl) {
 void sync_all(gdf_engine* e) {
     if (e->user_stream) HIPCHK(hipStreamSynchronize(e->user_stream));
     for (Slot& sl : e->slots)
-        if (sl.own) HIPCHK(hipStreamSynchronize(sl.own));
+        if (sl.stream()) HIPCHK(hipStreamSynchronize(sl.stream()));
 }
 
 // frame boundary (gdf_clear): the next frame goes to the next slot
@@ -1780,7 +1782,7 @@ int gdf_destroy(gdf_engine* e) {
     (void)hipSetDevice(e->device);
     if (e->user_stream) (void)hipStreamSynchronize(e->user_stream);
     for (Slot& sl : e->slots)
-        if (sl.own) (void)hipStreamSynchronize(sl.own);
+        if (sl.stream()) (void)hipStreamSynchronize(sl.stream());
     for (auto& p : e->ev_pending) {
         (void)hipEventDestroy(p.a);
         (void)hipEventDestroy(p.b);
@@ -1827,6 +1829,19 @@ int gdf_select_slot(gdf_engine* e, int slot) {
         if (slot < 0 || slot >= e->npipe) fail(GDF_ERR_ARG, "select_slot: no such pipeline slot");
         e->cur = slot;
         e->serialized = false;
+    });
+}
+
+int gdf_set_slot_streams(gdf_engine* e, void* const* streams, int n) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        if (n < 0 || n > kMaxPipe || (n && !streams)) fail(GDF_ERR_ARG, "set_slot_streams: 0..4 streams");
+        if (e->user_stream) fail(GDF_ERR_STATE, "set_slot_streams: the engine runs on one caller stream");
+        sync_all(e);
+        for (int i = 0; i < kMaxPipe; ++i) {
+            create_slot(e->slots[i]);
+            e->slots[i].ext = i < n ? static_cast<hipStream_t>(streams[i]) : nullptr;
+        }
     });
 }
 

@@ -141,7 +141,7 @@ EXPORTED = [
     "gdf_mask_dilate", "gdf_transform_points", "gdf_add_halo_depthmap_device",
     "gdf_partition_points", "gdf_voxelize_points", "gdf_last_sort_items", "gdf_get_stream",
     "gdf_get_graph_stats", "gdf_get_slot", "gdf_select_slot", "gdf_build_info",
-    "gdf_download_frame",
+    "gdf_download_frame", "gdf_set_slot_streams",
     # include/gdf_segment.h: the GPU object-segmentation front end
     "gdf_seg_create", "gdf_seg_destroy", "gdf_seg_set_stream", "gdf_seg_label_layers",
     "gdf_seg_label_engine_grid", "gdf_seg_get_counts", "gdf_seg_download_labels",
@@ -239,6 +239,7 @@ def load_library(path: str = LIB_PATH):
         "gdf_select_slot": (i32, [vp, i32]),
         "gdf_build_info": (C.c_char_p, []),
         "gdf_download_frame": (i32, [vp, u32, P(HostFrame)]),
+        "gdf_set_slot_streams": (i32, [vp, vp, i32]),
         "gdf_seg_create": (i32, [i32, P(vp)]),
         "gdf_seg_destroy": (i32, [vp]),
         "gdf_seg_set_stream": (i32, [vp, vp]),
@@ -402,6 +403,11 @@ class GPUDepthmapFusion:
         k = C.c_int(0)
         self._check(self._lib.gdf_get_slot(self._h, C.byref(k)))
         return k.value
+
+    def set_slot_streams(self, streams: Sequence[int]):
+        """Run the pipeline slots on caller-owned streams (gdf_set_slot_streams)."""
+        arr = (C.c_void_p * max(len(streams), 1))(*[C.c_void_p(x) for x in streams])
+        self._check(self._lib.gdf_set_slot_streams(self._h, arr, len(streams)))
 
     def select_slot(self, slot: int):
         """Address the frame still resident in `slot` (gdf_select_slot)."""

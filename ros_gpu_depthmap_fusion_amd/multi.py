@@ -301,6 +301,10 @@ class FusedCloudRank:
         self.depth = max(1, int(depth)) if dev == "cuda" else 1
         if dev == "cuda":
             engine.set_pipeline_depth(self.depth)
+            # the slots run on torch streams: torch's allocator and the collectives issued on
+            # them see streams that live as long as the process (the engine never destroys them)
+            self.streams = [torch.cuda.Stream() for _ in range(self.depth)]
+            engine.set_slot_streams([st.cuda_stream for st in self.streams])
             self.slots = {}
             # the points' communicator: its own RCCL stream (see the class docstring)
             self.pg_points = dist.new_group(list(range(world))) if world > 1 else None
@@ -377,7 +381,7 @@ class FusedCloudRank:
             S = self._slot(k)
             if S.pending:
                 raise RuntimeError("FusedCloudRank.start: the slot's previous step is unfinished")
-            st = torch.cuda.ExternalStream(eng.stream())
+            st = self.streams[k]
             S.ensure(st, tail_bytes=B * L2 if halo else 0)
             ctx = torch.cuda.stream(st)
         else:
@@ -461,7 +465,7 @@ class FusedCloudRank:
             S = self.slots[k]
             if not S.pending:
                 raise RuntimeError("FusedCloudRank.finish: no step in flight on this slot")
-            st = torch.cuda.ExternalStream(eng.stream())
+            st = self.streams[k]
             S.ev.synchronize()  # (the slot's split sizes; the later slots keep the GPU busy)
             both = S.host.tolist()
             scounts = [int(x) for x in both[:self.world]]

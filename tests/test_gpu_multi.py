@@ -374,6 +374,11 @@ def _rank_nccl_pipe(rank, world, port, out_dir, depth, rollbuffer):
     recs = [hiprt.DeviceArray.from_numpy(fused_ref.sequence_records(lidar, k)) for k in range(2)]
 
     def move(i):
+        # (the rollbuffer is engine state, not slot state: frame i-1's state is the one in place
+        # right before step i starts - the steps after it may already have run when i-1 finishes)
+        if i:
+            np.save(os.path.join(out_dir, f"prb_f{i - 1}.npy"),
+                    np.array(eng.rollbuffer_state().as_tuple()))
         eng.addPointSequenceDevice(recs[i % 2].ptr, 80 * 60, 16, *synth.sequence_time(i),
                                    synth.move_transform(i))
         return (lidar.T_world, lidar.T_crop)
@@ -384,13 +389,13 @@ def _rank_nccl_pipe(rank, world, port, out_dir, depth, rollbuffer):
         _, vs = eng.batch_ranges()
         for j in range(B):
             np.save(os.path.join(out_dir, f"pvox_f{B * i + j}.npy"), vox[vs[j]:vs[j + 1]])
-        if rollbuffer:
-            np.save(os.path.join(out_dir, f"prb_f{i}.npy"), np.array(eng.rollbuffer_state().as_tuple()))
 
     fr.run(steps, lambda i: [ds[B * i + j].ptr for j in range(B)],
            lambda i: [ds[B * i + j].ptr + 2 * (n - fr.Lmax) for j in range(B)],
            move_of=move if rollbuffer else None, on_finish=done)
     torch.cuda.synchronize()
+    if rollbuffer:
+        np.save(os.path.join(out_dir, f"prb_f{steps - 1}.npy"), np.array(eng.rollbuffer_state().as_tuple()))
     np.save(os.path.join(out_dir, "pgrid.npy"), eng.downloadVoxelOccupancyGrid())
     dist.barrier()
     dist.destroy_process_group()
