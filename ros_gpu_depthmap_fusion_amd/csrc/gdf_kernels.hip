@@ -678,8 +678,12 @@ __device__ __forceinline__ void load_cams(const FrameArgs& a, CamDesc* s_cams) {
 // counts - into group-local exclusive offsets and writes the group totals, then re-arms the
 // counter for the next launch (graph replays included).  k_emit adds the totals of the groups
 // before its own (group_partials).
-// Generic form: entry `idx` of `nent` counts (cnt[q * stride + i] for series q < nser) was just
+// Generic form (counts stored by publish_count, from thread 0): entry `idx` of `nent` counts (cnt[q * stride + i] for series q < nser) was just
 // written by thread 0 of this block; the last arriver of idx's group scans the group.
+__device__ __forceinline__ void publish_count(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_store sc1
+}
+
 __device__ __forceinline__ void arrive_and_scan(uint32_t* done, const uint32_t* cnt, uint32_t* off,
                                                 uint32_t* gtot, uint32_t idx, uint32_t nent,
                                                 int nser, uint32_t stride, uint32_t* s_last) {
@@ -687,14 +691,16 @@ __device__ __forceinline__ void arrive_and_scan(uint32_t* done, const uint32_t* 
     const uint32_t s0 = g * kScanGroup;
     const uint32_t n = min(kScanGroup, nent - s0);
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this block's counts
-        const uint32_t old = __hip_atomic_fetch_add(done + g, 1u, __ATOMIC_ACQ_REL,
+        // write-through hand-off, no fences (an agent release here is an L2 write-back per block:
+        // 7x the whole kernel, measured): the counts were stored sc1 by this lane (publish_count),
+        // drained before the counter add; the last arriver reads them with sc1 loads
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t old = __hip_atomic_fetch_add(done + g, 1u, __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_AGENT);
         *s_last = old + 1u == n ? 1u : 0u;
     }
     __syncthreads();
     if (!*s_last || threadIdx.x >= 64) return;  // block-uniform, then wave 0
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every block's counts of the group
     const uint32_t lane = threadIdx.x;
     const uint32_t ng = (nent + kScanGroup - 1) / kScanGroup;
     for (int q = 0; q < nser; ++q) {  // (k_mask: point counts, then run counts)
@@ -903,10 +909,10 @@ __global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
     if (threadIdx.x == 0) {
         uint32_t t = 0, r = 0;
         for (int w = 0; w < nwaves; ++w) t += s_cnt[w];
-        G(a.seg_counts)[s] = t;
+        publish_count(a.seg_counts + s, t);
         if (a.run_mode) {
             for (int w = 0; w < nwaves; ++w) r += s_rcnt[w];
-            G(a.seg_counts)[a.total_segs + s] = r;  // run counts follow the point counts
+            publish_count(a.seg_counts + a.total_segs + s, r);  // run counts follow the point counts
         }
     }
     if (a.run_mode && a.key_hist) {
@@ -1311,10 +1317,10 @@ __global__ __launch_bounds__(SEGW / PX) void k_mask_px(FrameArgs a) {
     if (threadIdx.x == 0) {
         uint32_t tt = 0, r = 0;
         for (int w = 0; w < NWORDS; ++w) tt += s_cnt[w];
-        G(a.seg_counts)[s] = tt;
+        publish_count(a.seg_counts + s, tt);
         if (a.run_mode) {
             for (int w = 0; w < NWORDS; ++w) r += s_rcnt[w];
-            G(a.seg_counts)[a.total_segs + s] = r;
+            publish_count(a.seg_counts + a.total_segs + s, r);
         }
     }
     if (a.run_mode && a.key_hist) {
@@ -2923,7 +2929,7 @@ __global__ __launch_bounds__(256) void k_group_count(const uint32_t* __restrict_
         const unsigned long long b = __ballot(i < n && (i == 0 || key != prev));
         if (lane == 0) s_w[wid] = (uint32_t)__popcll(b);
         __syncthreads();
-        if (threadIdx.x == 0) counts[t] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        if (threadIdx.x == 0) publish_count(counts + t, s_w[0] + s_w[1] + s_w[2] + s_w[3]);
         if (gdone) arrive_and_scan(gdone, counts, offsets, gtot, t, ntiles, 1, 0u, &s_last);
         __syncthreads();
     }
