@@ -72,6 +72,9 @@ def parse():
                          "several ranks on one GPU)")
     ap.add_argument("--dist", action="store_true",
                     help="the multi-GPU (torch.distributed) path even at one rank (RCCL at world 1)")
+    ap.add_argument("--fused-impl", choices=("native", "python"), default="native",
+                    help="RCCL fused mode: the step in C++ with libgdf's own RCCL calls "
+                         "(gdf_fused_*, default) or multi.FusedCloudRank's torch collectives")
     ap.add_argument("--publish", action="store_true",
                     help="fused mode: gather the fused voxel cloud to rank 0 every step (the "
                          "component publishes it every frame)")
@@ -533,16 +536,22 @@ def time_multi(args, st, params, dist, world, pmc_key):
     depth = 1
     fused = args.multi_mode == "fused"
     rb = None
+    native = False
     if fused:
         from ros_gpu_depthmap_fusion_amd import synth
-        from ros_gpu_depthmap_fusion_amd.multi import FusedCloudRank, gather_fused_cloud
+        from ros_gpu_depthmap_fusion_amd.multi import (FusedCloudRank, NativeFusedRank,
+                                                       gather_fused_cloud)
         rank = dist.get_rank()
         cams = [synth.make_camera(k, st.W, st.H) for k in range(world)]
         cuda = args.dist_backend == "nccl"
+        native = cuda and args.fused_impl == "native"
         # pipelined steps (RCCL): `--pipeline` batches in the engine's slots, a step's points
         # exchange finished while the next step computes
-        fr = FusedCloudRank(eng, cams, rank, world, params, dev="cuda" if cuda else "cpu",
-                            depth=max(1, min(4, args.pipeline)) if cuda else 1)
+        if native:
+            fr = NativeFusedRank(eng, cams, rank, world, params, depth=max(1, min(4, args.pipeline)))
+        else:
+            fr = FusedCloudRank(eng, cams, rank, world, params, dev="cuda" if cuda else "cpu",
+                                depth=max(1, min(4, args.pipeline)) if cuda else 1)
         depth = fr.depth
         n = st.W * st.H
         B = max(1, args.batch)
@@ -559,7 +568,12 @@ def time_multi(args, st, params, dist, world, pmc_key):
         def ptrs(i):
             return [st.dframes[0][(i * B + j) % st.ring].ptr for j in range(B)]
 
+        ring = [d.ptr for d in st.dframes[0]]
+
         def run(first, count):
+            if native and rb is None and not args.publish:  # the C++ step loop (gdf_fused_run)
+                fr.run_stream(ring, first, count, B)
+                return
             fr.run(count, lambda i: ptrs(first + i),
                    lambda i: [d + 2 * (n - fr.Lmax) for d in ptrs(first + i)],
                    move_of=(lambda i: rb.feed(first + i)) if rb is not None else None,
@@ -648,13 +662,19 @@ def time_multi(args, st, params, dist, world, pmc_key):
         eng.set_profiling(False)
         line["roofline"] = roofline_from(kt, kt_steps, model_bytes(st.P, n_avg, g_avg, ncells, fpb),
                                          pmc_key)
+    if fused and native:
+        fr.close()  # (its communicators, before the process group goes)
     if fused:
         cfg = {"parallelism": "camera-per-GPU x%d; per step of %d frames (one launch chain): "
                               "depth-tail halo all-gather, occupancy-mark all-gather + batched "
                               "grid update, key-range all-to-all of the (point, frame | key) "
                               "lists, voxelize per key range (fused cloud = one engine over all "
-                              "cameras, per frame)%s" % (world, fpb, "; fused cloud gathered "
-                                                        "to rank 0 every step" if args.publish else ""),
+                              "cameras, per frame)%s%s" % (
+                                  world, fpb, "; fused cloud gathered to rank 0 every step"
+                                  if args.publish else "",
+                                  "; the step in C++ (gdf_fused_run), RCCL called from libgdf on "
+                                  "the slots' streams, two communicators" if native else
+                                  "; torch.distributed collectives (multi.FusedCloudRank)"),
                "exchange": "per step of %d frames: halo %d px + %d-word marks per frame, one "
                            "points all-to-all" % (fpb, fr.Lmax, (ncells + 31) // 32)}
     else:

@@ -382,6 +382,22 @@ int gdf_partition_points(gdf_engine* engine, uint32_t nparts, float* send_points
                          uint32_t* part_counts_device);
 int gdf_voxelize_points(gdf_engine* engine, const float* points_device,
                         const uint32_t* keys_device, uint32_t count, int average_voxels);
+/* The same exchange with RUNS instead of per-point keys: gdf_partition_runs writes the part-major
+ * points plus each part's runs of equal keys - consecutive points of one voxel (of one frame of a
+ * batch: the run keys carry the frame above the voxel key, as gdf_partition_points' keys) - as run
+ * keys and run starts relative to the part's first point; part_counts (device, 2 * nparts words):
+ * points per part, then runs per part.  A rank that received nsources such segments, concatenated
+ * in rank order (points of source q from point_base[q], its runs from run_base[q]; host arrays of
+ * nsources + 1 entries, the last the totals), calls gdf_voxelize_runs: the run starts are rebased
+ * in place (run_starts needs run_base[nsources] + 1 entries) and the voxelize sorts the runs - the
+ * same voxel means as gdf_voxelize_points over the same points. */
+int gdf_partition_runs(gdf_engine* engine, uint32_t nparts, float* send_points_device,
+                       uint32_t* send_run_keys_device, uint32_t* send_run_starts_device,
+                       uint32_t capacity, uint32_t* part_counts_device);
+int gdf_voxelize_runs(gdf_engine* engine, const float* points_device,
+                      const uint32_t* run_keys_device, uint32_t* run_starts_device,
+                      uint32_t nsources, const uint32_t* point_base, const uint32_t* run_base,
+                      int average_voxels);
 
 /* ---- live kernel timing (HIP events on the engine stream) ------------------------------------ */
 enum gdf_kernel_slot {

@@ -1,0 +1,79 @@
+/* gdf_fused.h — one rank of the multi-GPU fused cloud, the whole step in C++ over RCCL.
+ *
+ * Not a reference interface: the reference fuses every camera in ONE process
+ * (GPUDepthmapFusion::processFrame over all depth maps, src/gpu_depthmap_fusion.cpp:1583-1756;
+ * the buffer order [camera 0 .. camera N-1 pixels, rollbuffer points] at :1509-1581, one voxelize
+ * at :1743-1756).  Here each rank (one process per GPU) holds one camera; a step is
+ *   depth-tail halo all-gather (camera k reads camera k-1's last F rows + F pixels)
+ *   -> the rank's compaction + voxel keys + occupancy marks (gdf_process_frame, deferred)
+ *   -> occupancy-mark all-gather + the batched grid update (every rank the same grid)
+ *   -> key-range partition -> split-size all-gather -> (finish) the points / keys all-to-all as
+ *      grouped send / recv -> voxelize of the rank's key range (gdf_voxelize_points),
+ * with the collectives issued by this library on the engine slot's stream through RCCL
+ * (dlopen'ed: the caller names the librccl it already loaded - torch's - so one RCCL serves the
+ * process).  Everything runs through the public C-ABI of include/gdf.h; the Python
+ * FusedCloudRank (ros_gpu_depthmap_fusion_amd/multi.py) is the same protocol with torch
+ * collectives and is the one the gloo CPU tests drive.
+ *
+ * Two communicators: A carries the halo / marks / split sizes, B the points.  Operations on one
+ * communicator run in issue order, so B's all-to-all of step i never queues behind step i + 1's
+ * collectives on A (the step is pipelined: start(i + 1) is issued before finish(i)).
+ */
+#ifndef GDF_FUSED_H
+#define GDF_FUSED_H
+
+#include "gdf.h"
+#include "gdf_driver.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct gdf_fused gdf_fused;
+
+#define GDF_FUSED_ID_BYTES 256 /* two ncclUniqueId (communicators A and B) */
+
+/* Rank 0: the unique ids of the two communicators (GDF_FUSED_ID_BYTES bytes), to be broadcast to
+ * every rank before gdf_fused_create.  rccl_library: path of librccl.so (NULL: the one on the
+ * loader path). */
+int gdf_fused_unique_id(const char* rccl_library, uint8_t* id_out);
+
+/* Collective over the `world` ranks: creates the communicators on the engine's device and the
+ * per-slot exchange state.  cams[k] = camera k's geometry (width, height, intrinsics, T_world,
+ * T_crop; `frames`/`ring` unused) for k < world - this rank's camera is cams[rank].
+ * flying_filter_size sets the halo (F rows + F pixels of camera k-1).  The engine keeps its own
+ * slot streams and must outlive the rank (gdf_fused_destroy first). */
+int gdf_fused_create(gdf_engine* engine, const char* rccl_library, const uint8_t* id, int rank,
+                     int world, const gdf_stream_camera* cams, uint32_t flying_filter_size,
+                     gdf_fused** out);
+int gdf_fused_destroy(gdf_fused* rank);
+
+/* Depth values of the halo every rank sends (max over cameras of F * width + F). */
+int gdf_fused_halo_pixels(gdf_fused* rank, uint32_t* pixels);
+
+/* Starts a step of `nframes` frames (1..16) of this rank's camera - depth[j] = frame j's DEVICE
+ * depth map - on the engine's next slot: everything up to the split sizes (queued to pinned
+ * memory, no wait).  p: the frame's parameters (its defer / synchronous flags are overridden; a
+ * move transform - rollbuffer rank, single frames - is honoured as by gdf_process_frame).
+ * Point sequences added to the engine beforehand are ingested by this step.  *slot = the slot to
+ * pass to gdf_fused_finish. */
+int gdf_fused_start(gdf_fused* rank, const uint16_t* const* depth, uint32_t nframes,
+                    const gdf_frame_params* p, int* slot);
+/* Finishes the step started on `slot`: waits for its split sizes, runs the points all-to-all and
+ * the voxelize of the rank's key range (gdf_select_slot(slot) is left selected: the rank's voxels
+ * are that slot's results).  send_counts (world entries, may be NULL): points sent to each rank;
+ * recv_count (may be NULL): points received. */
+int gdf_fused_finish(gdf_fused* rank, int slot, uint32_t* send_counts, uint32_t* recv_count);
+
+/* `steps` pipelined steps of `batch` frames of this rank's camera from cam->frames (step s takes
+ * frames (first + s) * batch + j, modulo the ring): step s + 1 is started before step s is
+ * finished, `depth` steps in flight at most (the engine's pipeline depth is set to it).  Returns
+ * after the last step was finished (its work still queued: gdf_synchronize waits). */
+int gdf_fused_run(gdf_fused* rank, const gdf_stream_camera* cam, const gdf_frame_params* p,
+                  uint64_t first, uint64_t steps, uint32_t batch, int depth);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GDF_FUSED_H */

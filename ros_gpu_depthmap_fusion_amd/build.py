@@ -11,7 +11,8 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB_PATH = os.path.join(PKG, "lib", "libgdf.so")
-SOURCES = ["gdf_kernels.hip", "gdf_segment.hip", "gdf_engine.cpp", "gdf_driver.cpp"]
+SOURCES = ["gdf_kernels.hip", "gdf_segment.hip", "gdf_engine.cpp", "gdf_driver.cpp",
+           "gdf_fused.cpp"]
 HEADERS = ["gdf_device.hpp", "gdf_kernels.hpp", "gdf_voxsum.hpp"]
 
 # Float contract of SURVEY.md Appendix A: no FMA contraction, correctly rounded / and sqrt.
@@ -22,7 +23,7 @@ HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
 
 def _deps():
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
-    deps += [os.path.join(ROOT, "include", h) for h in ("gdf.h", "gdf_driver.h", "gdf_segment.h")]
+    deps += [os.path.join(ROOT, "include", h) for h in ("gdf.h", "gdf_driver.h", "gdf_segment.h", "gdf_fused.h")]
     return deps
 
 
@@ -67,7 +68,7 @@ def build_library(force: bool = False, verbose: bool = False, trace: bool = Fals
     cmd = [hipcc, *HIPCC_FLAGS, *(["-DGDF_TRACE_GROUPS"] if trace else []),
            '-DGDF_BUILD_INFO="%s"' % stamp,
            "-I" + os.path.join(ROOT, "include"), "-I" + CSRC,
-           "-o", out + ".tmp", *[os.path.join(CSRC, f) for f in SOURCES]]
+           "-o", out + ".tmp", *[os.path.join(CSRC, f) for f in SOURCES], "-ldl"]
     if verbose:
         print(" ".join(cmd))
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -2381,6 +2381,72 @@ int gdf_partition_points(gdf_engine* e, uint32_t nparts, float* send_pts, uint32
     });
 }
 
+int gdf_partition_runs(gdf_engine* e, uint32_t nparts, float* send_pts, uint32_t* send_run_keys,
+                       uint32_t* send_run_starts, uint32_t capacity, uint32_t* part_counts) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        Slot& q = e->sl();
+        if (!e->grid_set || !q.coords_valid) fail(GDF_ERR_STATE, "partition needs the voxel keys of a frame");
+        if (nparts == 0 || nparts > kMaxParts) fail(GDF_ERR_ARG, "partition: 1..16 parts");
+        if (!send_pts || !send_run_keys || !send_run_starts || !part_counts)
+            fail(GDF_ERR_ARG, "partition: null buffer");
+        if (capacity < q.n_total) fail(GDF_ERR_CAPACITY, "partition: send buffers smaller than the frame");
+        ensure_misc(e);
+        const uint32_t nmax = std::max<uint32_t>(q.n_total, 1);
+        const uint32_t m = 2 * nparts * std::max<uint32_t>(part_tiles(nmax), 1u);
+        q.d_pcnt.ensure((size_t)m * 4);
+        q.d_poff.ensure(seg_offsets_words(m) * 4);
+        HIPCHK(launch_partition(q.d_pts.as<float4>(), q.d_coords.as<uint32_t>(),
+                                q.d_misc.as<uint32_t>() + kCount, nmax, nparts, e->ncells,
+                                q.d_pcnt.as<uint32_t>(), q.d_poff.as<uint32_t>(),
+                                q.d_misc.as<uint32_t>() + kPartTotal,
+                                reinterpret_cast<float4*>(send_pts), nullptr, part_counts, e->s(),
+                                q.nframes > 1 ? q.d_fstart.as<uint32_t>() : nullptr, q.nframes,
+                                q.nframes > 1 ? e->key_bits : 0u, send_run_keys, send_run_starts));
+    });
+}
+
+int gdf_voxelize_runs(gdf_engine* e, const float* pts, const uint32_t* run_keys,
+                      uint32_t* run_starts, uint32_t nsources, const uint32_t* point_base,
+                      const uint32_t* run_base, int average) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        if (!e->grid_set) fail(GDF_ERR_STATE, "voxelize_runs needs the voxel grid of a frame");
+        if (nsources == 0 || nsources > kMaxParts || !point_base || !run_base)
+            fail(GDF_ERR_ARG, "voxelize_runs: 1..16 sources and their bases");
+        RebaseArgs rb;
+        std::memset(&rb, 0, sizeof(rb));
+        rb.nsrc = nsources;
+        for (uint32_t k = 0; k <= nsources; ++k) {
+            rb.point_base[k] = point_base[k];
+            rb.run_base[k] = run_base[k];
+            if (k && (point_base[k] < point_base[k - 1] || run_base[k] < run_base[k - 1]))
+                fail(GDF_ERR_ARG, "voxelize_runs: bases must not decrease");
+            if (k && (run_base[k] > run_base[k - 1]) != (point_base[k] > point_base[k - 1]))
+                fail(GDF_ERR_ARG, "voxelize_runs: a source has points without runs or runs without points");
+        }
+        const uint32_t n = point_base[nsources], R = run_base[nsources];
+        if (R && (!pts || !run_keys || !run_starts)) fail(GDF_ERR_ARG, "voxelize_runs: null list");
+        if (!run_starts) fail(GDF_ERR_ARG, "voxelize_runs: run_starts needs R + 1 entries");
+        ensure_misc(e);
+        if (e->sl().khist_pending) {  // the frame's compaction counted ITS keys' digits: not these
+            HIPCHK(hipMemsetAsync(e->sl().d_khist.p, 0, kHistWords * 4, e->s()));
+            e->sl().khist_pending = false;
+        }
+        uint32_t* misc = e->sl().d_misc.as<uint32_t>();
+        HIPCHK(launch_run_rebase(run_starts, rb, misc + kRecvCount, misc + kRecvRuns, e->s()));
+        VoxSource src;
+        src.pts = reinterpret_cast<const float4*>(pts);
+        src.keys = run_keys;
+        src.n = n;
+        src.run_keys = run_keys;
+        src.run_start = run_starts;
+        const VoxelizeArgs v = voxelize_args(e, average, -1, &src);
+        e->timed(GDF_KERNEL_VOXELIZE, [&] { HIPCHK(launch_voxelize(v, e->s(), e->hook_ptr())); });
+        e->sl().vox_valid = true;
+    });
+}
+
 int gdf_voxelize_points(gdf_engine* e, const float* pts, const uint32_t* keys, uint32_t n,
                         int average) {
     ENGINE_OR_FAIL(e);

@@ -2301,11 +2301,12 @@ __device__ __forceinline__ void snap_layout(uint64_t nwords, uint32_t nblocks, u
 // after frame f < nframes - 1 goes to the sparse snapshots, the last one is the grid itself.
 // Marks are cleared.
 // (mk(f, i): the marks word i of frame f - read and cleared, or OR-ed over ranks)
-template <class Marks>
+// (fill(i, mf): every frame's marks word i at once into mf[0 .. nframes), nframes <= kMaxCams)
+template <class Marks, class Fill>
 __device__ __forceinline__ void grid_u8_frames(uint4* __restrict__ grid, uint64_t nwords,
                                                uint32_t L, uint32_t block, uint32_t nblocks,
                                                uint32_t nframes, const Marks& mk,
-                                               const SnapArgs& sn) {
+                                               const SnapArgs& sn, const Fill& fill) {
     __shared__ uint32_t s_sc[4][kMaxCams];  // per wave: snapshot entries so far, per frame
     const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     // (the host passes snapshots only for <= kMaxCams frames; anything else keeps none)
@@ -2327,8 +2328,7 @@ __device__ __forceinline__ void grid_u8_frames(uint4* __restrict__ grid, uint64_
             v0 = grid[2 * i];
             v1 = grid[2 * i + 1];
         }
-        for (uint32_t f = 0; f < nframes; ++f) {
-            const uint32_t m = act ? mk(f, i) : 0u;
+        auto step = [&](uint32_t f, uint32_t m) {
             v0.x = grid_word(v0.x, m, L);
             v0.y = grid_word(v0.y, m >> 4, L);
             v0.z = grid_word(v0.z, m >> 8, L);
@@ -2357,6 +2357,21 @@ __device__ __forceinline__ void grid_u8_frames(uint4* __restrict__ grid, uint64_
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 }
             }
+        };
+        if (nframes <= (uint32_t)kMaxCams) {
+            // every frame's marks word first: the loads are in flight together, not one memory
+            // latency per frame (the batched update was ~B dependent round trips per word)
+            uint32_t mf[kMaxCams];
+#pragma unroll
+            for (uint32_t f = 0; f < (uint32_t)kMaxCams; ++f) mf[f] = 0u;
+            if (act) fill(i, mf);
+#pragma unroll
+            for (uint32_t f = 0; f < (uint32_t)kMaxCams; ++f) {
+                if (f >= nframes) break;
+                step(f, mf[f]);
+            }
+        } else {
+            for (uint32_t f = 0; f < nframes; ++f) step(f, act ? mk(f, i) : 0u);
         }
         if (act) {
             grid[2 * i] = v0;
@@ -2377,7 +2392,15 @@ __device__ __forceinline__ void grid_u8_part_frames(uint4* __restrict__ grid,
                        if (m) marks[f * mark_words + i] = 0u;
                        return m;
                    },
-                   sn);
+                   sn,
+                   [&](uint64_t i, uint32_t (&mf)[kMaxCams]) {
+#pragma unroll
+                       for (uint32_t f = 0; f < (uint32_t)kMaxCams; ++f)
+                           if (f < nframes) mf[f] = marks[f * mark_words + i];
+#pragma unroll
+                       for (uint32_t f = 0; f < (uint32_t)kMaxCams; ++f)
+                           if (f < nframes && mf[f]) marks[f * mark_words + i] = 0u;
+                   });
 }
 
 // frame f's sparse snapshot into a zeroed dense u8 grid: one block per update wave
@@ -2454,7 +2477,15 @@ __global__ __launch_bounds__(256) void k_grid_u8_batch(uint4* __restrict__ grid,
                        for (uint32_t r = 0; r < nranks; ++r) m |= bits[r * rank_stride + f * frame_stride + i];
                        return m;
                    },
-                   sn);
+                   sn,
+                   [&](uint64_t i, uint32_t (&mf)[kMaxCams]) {
+                       for (uint32_t r = 0; r < nranks; ++r) {  // (a rank's frames in flight together)
+                           const uint32_t* b = bits + r * rank_stride + i;
+#pragma unroll
+                           for (uint32_t f = 0; f < (uint32_t)kMaxCams; ++f)
+                               if (f < nframes) mf[f] |= b[f * frame_stride];
+                       }
+                   });
     grid_seq_leave(q, f0, gridDim.x);
 }
 
@@ -4108,26 +4139,67 @@ __device__ __forceinline__ uint32_t part_of(uint32_t key, uint32_t nparts, uint6
     return p < nparts ? (uint32_t)p : nparts - 1u;
 }
 
+// RUNS: the partition also cuts each part's points into runs of equal (frame | voxel) keys - a
+// run starts at a tile's first item or where the key differs from the item before it (equal keys
+// share a part, so a run never straddles parts) - and writes them part-major behind the points'
+// counts: run keys (with the frame bits) and run starts relative to the part's first point.  The
+// receiver then sorts runs, not points (gdf_voxelize_runs), and no per-point key travels.
+__device__ __forceinline__ uint32_t sent_key(const uint32_t* __restrict__ keys, uint32_t i,
+                                             const uint32_t* s_fstart, uint32_t nframes,
+                                             uint32_t fshift, bool batch) {
+    const uint32_t k = keys[i];
+    return batch ? k | (frame_of(s_fstart, nframes, i) << fshift) : k;
+}
+
+template <bool RUNS>
 __global__ __launch_bounds__(256) void k_part_count(const uint32_t* __restrict__ keys,
                                                     const uint32_t* __restrict__ count,
                                                     uint32_t nparts, uint64_t ncells,
-                                                    uint32_t ntiles, uint32_t* __restrict__ counts) {
-    __shared__ uint32_t s_c[kMaxParts];
+                                                    uint32_t ntiles, uint32_t* __restrict__ counts,
+                                                    const uint32_t* __restrict__ fstart,
+                                                    uint32_t nframes, uint32_t fshift) {
+    __shared__ uint32_t s_c[2 * kMaxParts];
+    __shared__ uint32_t s_fstart[kMaxCams + 1];
+    const bool batch = RUNS && fstart != nullptr && nframes > 1;
+    if (batch) load_fstart(s_fstart, fstart, nframes);
     const uint32_t n = *count;
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {  // block-uniform
-        if (threadIdx.x < kMaxParts) s_c[threadIdx.x] = 0;
+        if (threadIdx.x < 2 * kMaxParts) s_c[threadIdx.x] = 0;
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const uint32_t i = t * kPartTile + q * 256 + threadIdx.x;
-            if (i < n) atomicAdd(&s_c[part_of(keys[i], nparts, ncells)], 1u);
+            if (i < n) {
+                const uint32_t key = keys[i];
+                const uint32_t part = part_of(key, nparts, ncells);
+                atomicAdd(&s_c[part], 1u);
+                if (RUNS && (i == t * kPartTile ||
+                             sent_key(keys, i - 1, s_fstart, nframes, fshift, batch) !=
+                                 (batch ? key | (frame_of(s_fstart, nframes, i) << fshift) : key)))
+                    atomicAdd(&s_c[kMaxParts + part], 1u);
+            }
         }
         __syncthreads();
-        if (threadIdx.x < nparts) counts[threadIdx.x * ntiles + t] = s_c[threadIdx.x];
+        if (threadIdx.x < nparts) {
+            counts[threadIdx.x * ntiles + t] = s_c[threadIdx.x];
+            if (RUNS) counts[(nparts + threadIdx.x) * ntiles + t] = s_c[kMaxParts + threadIdx.x];
+        }
         __syncthreads();
     }
 }
 
+// lanes of this wave in the same part as this lane, among the lanes of `m`
+__device__ __forceinline__ unsigned long long same_part(unsigned long long m, uint32_t part) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const bool bit = (part >> b) & 1u;
+        const unsigned long long bb = __ballot(bit);
+        m &= bit ? bb : ~bb;
+    }
+    return m;
+}
+
+template <bool RUNS>
 __global__ __launch_bounds__(256) void k_part_scatter(const float4* __restrict__ pts,
                                                       const uint32_t* __restrict__ keys,
                                                       const uint32_t* __restrict__ count,
@@ -4139,27 +4211,50 @@ __global__ __launch_bounds__(256) void k_part_scatter(const float4* __restrict__
                                                       uint32_t* __restrict__ out_keys,
                                                       uint32_t* __restrict__ part_counts,
                                                       const uint32_t* __restrict__ fstart,
-                                                      uint32_t nframes, uint32_t fshift) {
+                                                      uint32_t nframes, uint32_t fshift,
+                                                      uint32_t* __restrict__ out_run_keys,
+                                                      uint32_t* __restrict__ out_run_start) {
     __shared__ uint32_t s_w[4][kMaxParts];  // per-wave running counts (slot-major order)
+    __shared__ uint32_t s_rw[4][kMaxParts];  // (runs)
     __shared__ uint32_t s_base[kMaxParts];
+    __shared__ uint32_t s_rbase[kMaxParts];
+    __shared__ uint32_t s_pfirst[kMaxParts];  // the part's first send position
     __shared__ uint32_t s_fstart[kMaxCams + 1];
     // a batch (fstart): the sent key carries the point's frame above the voxel key, the part
     // comes from the voxel key alone
-    if (fstart) load_fstart(s_fstart, fstart, nframes);
+    const bool batch = fstart != nullptr && nframes > 1;
+    if (batch) load_fstart(s_fstart, fstart, nframes);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t n = *count;
+    const uint32_t mp = nparts * ntiles;  // (RUNS: the run counts' offsets follow the points')
     if (blockIdx.x == 0 && threadIdx.x < nparts) {
         const uint32_t a = offsets[threadIdx.x * ntiles];
-        const uint32_t b = threadIdx.x + 1 < nparts ? offsets[(threadIdx.x + 1) * ntiles] : *total;
+        const uint32_t b = threadIdx.x + 1 < nparts ? offsets[(threadIdx.x + 1) * ntiles]
+                                                   : (RUNS ? offsets[mp] : *total);
         part_counts[threadIdx.x] = b - a;
+        if (RUNS) {
+            const uint32_t ra = offsets[mp + threadIdx.x * ntiles];
+            const uint32_t rb = threadIdx.x + 1 < nparts ? offsets[mp + (threadIdx.x + 1) * ntiles] : *total;
+            part_counts[nparts + threadIdx.x] = rb - ra;
+        }
     }
     const unsigned long long ltm = lanemask_lt();
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {  // block-uniform
-        if (threadIdx.x < 4 * kMaxParts) (&s_w[0][0])[threadIdx.x] = 0;
-        if (threadIdx.x < nparts) s_base[threadIdx.x] = offsets[threadIdx.x * ntiles + t];
+        if (threadIdx.x < 4 * kMaxParts) {
+            (&s_w[0][0])[threadIdx.x] = 0;
+            if (RUNS) (&s_rw[0][0])[threadIdx.x] = 0;
+        }
+        if (threadIdx.x < nparts) {
+            s_base[threadIdx.x] = offsets[threadIdx.x * ntiles + t];
+            if (RUNS) {
+                s_rbase[threadIdx.x] = offsets[mp + threadIdx.x * ntiles + t] - offsets[mp];
+                s_pfirst[threadIdx.x] = offsets[threadIdx.x * ntiles];
+            }
+        }
         __syncthreads();
         // wave w owns items [t*1024 + w*256, + 256) in 4 slots of 64: stable within the tile
-        uint32_t part[4], rank[4], key[4];
+        uint32_t part[4], rank[4], key[4], rrank[4];
+        bool lead[4];
         float4 p[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -4168,28 +4263,42 @@ __global__ __launch_bounds__(256) void k_part_scatter(const float4* __restrict__
             key[q] = ok ? keys[i] : 0u;
             if (ok) p[q] = pts[i];
             part[q] = ok ? part_of(key[q], nparts, ncells) : 0u;
-            unsigned long long m = __ballot(ok);
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const bool bit = (part[q] >> b) & 1u;
-                const unsigned long long bb = __ballot(bit);
-                m &= bit ? bb : ~bb;
-            }
+            if (batch && ok) key[q] |= frame_of(s_fstart, nframes, i) << fshift;
+            const unsigned long long m = same_part(__ballot(ok), part[q]);
             const uint32_t before = (uint32_t)__popcll(m & ltm);
             const uint32_t base = ok ? s_w[w][part[q]] : 0u;
             rank[q] = base + before;
-            __builtin_amdgcn_wave_barrier();
-            if (ok && before == 0) s_w[w][part[q]] = base + (uint32_t)__popcll(m);
+            if (RUNS) {
+                lead[q] = ok && (i == t * kPartTile ||
+                                 sent_key(keys, i - 1, s_fstart, nframes, fshift, batch) != key[q]);
+                const unsigned long long lm = same_part(__ballot(lead[q]), part[q]);
+                const uint32_t rbefore = (uint32_t)__popcll(lm & ltm);
+                const uint32_t rb0 = ok ? s_rw[w][part[q]] : 0u;
+                rrank[q] = rb0 + rbefore;
+                __builtin_amdgcn_wave_barrier();
+                if (ok && before == 0) {
+                    s_w[w][part[q]] = base + (uint32_t)__popcll(m);
+                    s_rw[w][part[q]] = rb0 + (uint32_t)__popcll(lm);
+                }
+            } else {
+                __builtin_amdgcn_wave_barrier();
+                if (ok && before == 0) s_w[w][part[q]] = base + (uint32_t)__popcll(m);
+            }
             __builtin_amdgcn_wave_barrier();
         }
         __syncthreads();
         // waves before this one in the tile
         if (threadIdx.x < nparts) {
-            uint32_t run = 0;
+            uint32_t run = 0, rrun = 0;
             for (int ww = 0; ww < 4; ++ww) {
                 const uint32_t c = s_w[ww][threadIdx.x];
                 s_w[ww][threadIdx.x] = run;
                 run += c;
+                if (RUNS) {
+                    const uint32_t rc = s_rw[ww][threadIdx.x];
+                    s_rw[ww][threadIdx.x] = rrun;
+                    rrun += rc;
+                }
             }
         }
         __syncthreads();
@@ -4199,7 +4308,12 @@ __global__ __launch_bounds__(256) void k_part_scatter(const float4* __restrict__
             if (i < n) {
                 const uint32_t pos = s_base[part[q]] + s_w[w][part[q]] + rank[q];
                 out_pts[pos] = p[q];
-                out_keys[pos] = fstart ? key[q] | (frame_of(s_fstart, nframes, i) << fshift) : key[q];
+                if (out_keys) out_keys[pos] = key[q];
+                if (RUNS && lead[q]) {
+                    const uint32_t rpos = s_rbase[part[q]] + s_rw[w][part[q]] + rrank[q];
+                    out_run_keys[rpos] = key[q];
+                    out_run_start[rpos] = pos - s_pfirst[part[q]];
+                }
             }
         }
         __syncthreads();
@@ -4212,18 +4326,57 @@ hipError_t launch_partition(const float4* pts, const uint32_t* keys, const uint3
                             uint32_t nmax, uint32_t nparts, uint64_t ncells, uint32_t* counts,
                             uint32_t* offsets, uint32_t* total, float4* out_pts,
                             uint32_t* out_keys, uint32_t* part_counts, hipStream_t s,
-                            const uint32_t* fstart, uint32_t nframes, uint32_t fshift) {
+                            const uint32_t* fstart, uint32_t nframes, uint32_t fshift,
+                            uint32_t* out_run_keys, uint32_t* out_run_start) {
     const uint32_t ntiles = std::max<uint32_t>(part_tiles(nmax), 1u);
     const uint32_t blocks = std::min<uint32_t>(ntiles, 2048u);
-    hipLaunchKernelGGL(k_part_count, dim3(blocks), dim3(256), 0, s, keys, count, nparts, ncells,
-                       ntiles, counts);
+    const bool runs = out_run_keys != nullptr;
+    if (runs)
+        hipLaunchKernelGGL(k_part_count<true>, dim3(blocks), dim3(256), 0, s, keys, count, nparts,
+                           ncells, ntiles, counts, fstart, nframes, fshift);
+    else
+        hipLaunchKernelGGL(k_part_count<false>, dim3(blocks), dim3(256), 0, s, keys, count, nparts,
+                           ncells, ntiles, counts, fstart, nframes, fshift);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    const uint32_t m = nparts * ntiles;
+    const uint32_t m = (runs ? 2u : 1u) * nparts * ntiles;
     if ((e = launch_scan(counts, m, offsets, total, nullptr, 1u, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_part_scatter, dim3(blocks), dim3(256), 0, s, pts, keys, count, nparts,
-                       ncells, ntiles, offsets, total, out_pts, out_keys, part_counts, fstart,
-                       nframes, fshift);
+    if (runs)
+        hipLaunchKernelGGL(k_part_scatter<true>, dim3(blocks), dim3(256), 0, s, pts, keys, count,
+                           nparts, ncells, ntiles, offsets, total, out_pts, out_keys, part_counts,
+                           fstart, nframes, fshift, out_run_keys, out_run_start);
+    else
+        hipLaunchKernelGGL(k_part_scatter<false>, dim3(blocks), dim3(256), 0, s, pts, keys, count,
+                           nparts, ncells, ntiles, offsets, total, out_pts, out_keys, part_counts,
+                           fstart, nframes, fshift, out_run_keys, out_run_start);
+    return hipGetLastError();
+}
+
+// The received run lists of gdf_voxelize_runs: source q's run starts are relative to its point
+// segment - add its point base; close the list (run_start[R] = n) and store the counts the
+// voxelize reads (misc words: points, runs).
+__global__ __launch_bounds__(256) void k_run_rebase(uint32_t* __restrict__ run_start, RebaseArgs r,
+                                                    uint32_t* __restrict__ n_points,
+                                                    uint32_t* __restrict__ n_runs) {
+    const uint32_t R = r.run_base[r.nsrc];
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < R) {
+        uint32_t q = 0;
+        while (q + 1 < r.nsrc && r.run_base[q + 1] <= i) ++q;
+        run_start[i] += r.point_base[q];
+    }
+    if (i == 0) {
+        run_start[R] = r.point_base[r.nsrc];
+        *n_points = r.point_base[r.nsrc];
+        *n_runs = R;
+    }
+}
+
+hipError_t launch_run_rebase(uint32_t* run_start, const RebaseArgs& r, uint32_t* n_points,
+                             uint32_t* n_runs, hipStream_t s) {
+    const uint32_t R = r.run_base[r.nsrc];
+    hipLaunchKernelGGL(k_run_rebase, dim3(std::max<uint32_t>((R + 255) / 256, 1u)), dim3(256), 0, s,
+                       run_start, r, n_points, n_runs);
     return hipGetLastError();
 }
 

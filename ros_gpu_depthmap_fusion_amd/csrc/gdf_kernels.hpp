@@ -170,13 +170,27 @@ hipError_t launch_transform_points(const float4* in, const uint32_t* mask, float
 // (fstart: the frames' point starts): the sent keys carry the frame index above bit fshift.  Workspace:
 // counts [nparts * part_tiles(nmax)], offsets [seg_offsets_words(nparts * part_tiles(nmax))],
 // total [1].
+// With out_run_keys (runs mode): also the part-major runs of equal sent keys (run keys, run
+// starts relative to the part's first point), part_counts[nparts + p] = runs of part p, counts /
+// offsets twice as long (points' tile counts, then the runs'); out_keys may be null.
 uint32_t part_tiles(uint32_t nmax);
 hipError_t launch_partition(const float4* pts, const uint32_t* keys, const uint32_t* count,
                             uint32_t nmax, uint32_t nparts, uint64_t ncells, uint32_t* counts,
                             uint32_t* offsets, uint32_t* total, float4* out_pts,
                             uint32_t* out_keys, uint32_t* part_counts, hipStream_t s,
                             const uint32_t* fstart = nullptr, uint32_t nframes = 1,
-                            uint32_t fshift = 0);
+                            uint32_t fshift = 0, uint32_t* out_run_keys = nullptr,
+                            uint32_t* out_run_start = nullptr);
+
+// gdf_voxelize_runs: nsrc received segments, source q's points from point_base[q] and runs from
+// run_base[q] (q <= nsrc: the totals)
+struct RebaseArgs {
+    uint32_t point_base[kMaxParts + 1];
+    uint32_t run_base[kMaxParts + 1];
+    uint32_t nsrc;
+};
+hipError_t launch_run_rebase(uint32_t* run_start, const RebaseArgs& r, uint32_t* n_points,
+                             uint32_t* n_runs, hipStream_t s);
 
 // runs of equal keys in an external key list of *count (<= nmax) keys (the multi-GPU receive
 // buffer): run_keys[r], run_start[r] (first item; run_start[R] = n), *run_total = R.  Workspace:

@@ -139,9 +139,12 @@ EXPORTED = [
     "gdf_run_depth_stream_alternating",
     "gdf_next_frame_in_batch", "gdf_get_batch_ranges", "gdf_download_batch_occupancy_grid",
     "gdf_mask_dilate", "gdf_transform_points", "gdf_add_halo_depthmap_device",
-    "gdf_partition_points", "gdf_voxelize_points", "gdf_last_sort_items", "gdf_get_stream",
+    "gdf_partition_points", "gdf_voxelize_points", "gdf_partition_runs", "gdf_voxelize_runs", "gdf_last_sort_items", "gdf_get_stream",
     "gdf_get_graph_stats", "gdf_get_slot", "gdf_select_slot", "gdf_build_info",
     "gdf_download_frame", "gdf_set_slot_streams",
+    # include/gdf_fused.h: a rank of the multi-GPU fused cloud in C++ over RCCL
+    "gdf_fused_unique_id", "gdf_fused_create", "gdf_fused_destroy", "gdf_fused_halo_pixels",
+    "gdf_fused_start", "gdf_fused_finish", "gdf_fused_run",
     # include/gdf_segment.h: the GPU object-segmentation front end
     "gdf_seg_create", "gdf_seg_destroy", "gdf_seg_set_stream", "gdf_seg_label_layers",
     "gdf_seg_label_engine_grid", "gdf_seg_get_counts", "gdf_seg_download_labels",
@@ -229,6 +232,8 @@ def load_library(path: str = LIB_PATH):
         "gdf_add_halo_depthmap_device": (i32, [vp, vp, u32, u32, u32, f, f, f, f, f, vp, vp]),
         "gdf_partition_points": (i32, [vp, u32, vp, vp, u32, vp]),
         "gdf_voxelize_points": (i32, [vp, vp, vp, u32, i32]),
+        "gdf_partition_runs": (i32, [vp, u32, vp, vp, vp, u32, vp]),
+        "gdf_voxelize_runs": (i32, [vp, vp, vp, vp, u32, vp, vp, i32]),
         "gdf_transform_points": (i32, [vp, vp, vp, vp, u32, vp]),
         "gdf_get_batch_ranges": (i32, [vp, vp, vp, u32, P(u32)]),
         "gdf_download_batch_occupancy_grid": (i32, [vp, u32, vp, u64]),
@@ -240,6 +245,13 @@ def load_library(path: str = LIB_PATH):
         "gdf_build_info": (C.c_char_p, []),
         "gdf_download_frame": (i32, [vp, u32, P(HostFrame)]),
         "gdf_set_slot_streams": (i32, [vp, vp, i32]),
+        "gdf_fused_unique_id": (i32, [C.c_char_p, vp]),
+        "gdf_fused_create": (i32, [vp, C.c_char_p, vp, i32, i32, P(StreamCamera), u32, P(vp)]),
+        "gdf_fused_destroy": (i32, [vp]),
+        "gdf_fused_halo_pixels": (i32, [vp, P(u32)]),
+        "gdf_fused_start": (i32, [vp, vp, u32, P(FrameParams), P(i32)]),
+        "gdf_fused_finish": (i32, [vp, i32, vp, P(u32)]),
+        "gdf_fused_run": (i32, [vp, P(StreamCamera), P(FrameParams), u64, u64, u32, i32]),
         "gdf_seg_create": (i32, [i32, P(vp)]),
         "gdf_seg_destroy": (i32, [vp]),
         "gdf_seg_set_stream": (i32, [vp, vp]),
@@ -757,6 +769,25 @@ class GPUDepthmapFusion:
         self._check(self._lib.gdf_voxelize_points(self._h, C.c_void_p(pts_ptr),
                                                   C.c_void_p(keys_ptr), count,
                                                   1 if average else 0))
+
+    def partition_runs(self, nparts: int, send_pts_ptr: int, send_run_keys_ptr: int,
+                       send_run_starts_ptr: int, capacity: int, part_counts_ptr: int):
+        """partition_points with runs of equal keys instead of per-point keys (gdf_partition_runs):
+        part_counts = points per part, then runs per part."""
+        self._check(self._lib.gdf_partition_runs(
+            self._h, nparts, C.c_void_p(send_pts_ptr), C.c_void_p(send_run_keys_ptr),
+            C.c_void_p(send_run_starts_ptr), capacity, C.c_void_p(part_counts_ptr)))
+
+    def voxelize_runs(self, pts_ptr: int, run_keys_ptr: int, run_starts_ptr: int,
+                      point_base, run_base, average: bool = True):
+        """Voxelize received run segments (gdf_voxelize_runs): point_base / run_base = the
+        sources' offsets, nsources + 1 entries each."""
+        pb = np.ascontiguousarray(point_base, np.uint32)
+        rb = np.ascontiguousarray(run_base, np.uint32)
+        self._check(self._lib.gdf_voxelize_runs(self._h, C.c_void_p(pts_ptr),
+                                                C.c_void_p(run_keys_ptr), C.c_void_p(run_starts_ptr),
+                                                len(pb) - 1, _ptr(pb), _ptr(rb),
+                                                1 if average else 0))
 
     # ---- orphan shaders (device buffers) ----
     def maskDilate(self, in_ptr: int, out_ptr: int, width: int, height: int, filter_size: int,

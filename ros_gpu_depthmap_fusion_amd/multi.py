@@ -13,6 +13,8 @@ GPU box, "gloo" for the CPU tests.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 
@@ -205,6 +207,31 @@ def exchange_points(send_pts, send_keys, counts, group=None):
     return rp, rk, rcounts
 
 
+def exchange_runs(send_pts, send_run_keys, send_run_starts, counts, runs, group=None):
+    """exchange_points for the run form (gdf_partition_runs): counts[j] points and runs[j] runs
+    go to rank j.  Returns (points, run keys, run starts, points per source, runs per source)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    mine = torch.tensor([[int(counts[j]), int(runs[j])] for j in range(world)], dtype=torch.int64)
+    got = torch.zeros_like(mine)
+    dist.all_to_all_single(got, mine, group=group)
+    rc = [int(x) for x in got[:, 0].tolist()]
+    rr = [int(x) for x in got[:, 1].tolist()]
+    sc = [int(x) for x in counts]
+    sr = [int(x) for x in runs]
+    rp = torch.empty((sum(rc), 4), dtype=torch.float32)
+    rk = torch.empty(sum(rr), dtype=torch.int32)
+    rs = torch.empty(sum(rr), dtype=torch.int32)
+    dist.all_to_all_single(rp, send_pts[:sum(sc)], output_split_sizes=rc, input_split_sizes=sc,
+                           group=group)
+    dist.all_to_all_single(rk, send_run_keys[:sum(sr)], output_split_sizes=rr,
+                           input_split_sizes=sr, group=group)
+    dist.all_to_all_single(rs, send_run_starts[:sum(sr)], output_split_sizes=rr,
+                           input_split_sizes=sr, group=group)
+    return rp, rk, rs, rc, rr
+
+
 def exchange_points_dev(send_pts, send_keys, send_counts, group=None):
     """exchange_points for device tensors with the send counts still on the device (the
     partition's output): the counts' all-to-all runs on the device and ONE host read brings both
@@ -240,10 +267,11 @@ class _SlotExchange:
         self.rcap = 0         # receive capacity (points)
         self.mcap = 0         # mark words
         self.tcap = 0         # halo tail bytes
-        self.cnt = torch.zeros(world, dtype=torch.int32, device="cuda")
-        self.c64 = torch.zeros(world, dtype=torch.int64, device="cuda")
-        self.rc = torch.zeros(world, dtype=torch.int64, device="cuda")
-        self.host = torch.zeros(2 * world, dtype=torch.int64, pin_memory=True)
+        # split sizes: (points, runs) per part - sent [world, 2], received [world, 2]
+        self.cnt = torch.zeros(2 * world, dtype=torch.int32, device="cuda")
+        self.c64 = torch.zeros((world, 2), dtype=torch.int64, device="cuda")
+        self.rc = torch.zeros((world, 2), dtype=torch.int64, device="cuda")
+        self.host = torch.zeros(4 * world, dtype=torch.int64, pin_memory=True)
         self.ev = torch.cuda.Event()
         self.pending = False
 
@@ -257,11 +285,13 @@ class _SlotExchange:
         if n_send > self.cap:
             self.cap = max(n_send, self.cap + self.cap // 2)
             self.sp = torch.empty((self.cap, 4), dtype=torch.float32, device="cuda")
-            self.sk = torch.empty(self.cap, dtype=torch.int32, device="cuda")
+            self.srk = torch.empty(self.cap, dtype=torch.int32, device="cuda")  # run keys
+            self.srs = torch.empty(self.cap, dtype=torch.int32, device="cuda")  # run starts
         if n_recv > self.rcap:
             self.rcap = max(n_recv, self.rcap + self.rcap // 2)
             self.rp = torch.empty((self.rcap, 4), dtype=torch.float32, device="cuda")
-            self.rk = torch.empty(self.rcap, dtype=torch.int32, device="cuda")
+            self.rrk = torch.empty(self.rcap, dtype=torch.int32, device="cuda")
+            self.rrs = torch.empty(self.rcap + 1, dtype=torch.int32, device="cuda")
         if mark_words > self.mcap:
             self.mcap = mark_words
             self.local = torch.empty(mark_words, dtype=torch.int32, device="cuda")
@@ -428,13 +458,14 @@ class FusedCloudRank:
                 dist.all_gather_into_tensor(S.gathered[:self.world * B * words], S.local[:B * words])
                 eng.voxelOccupancyGridBatch(S.gathered.data_ptr(), words, self.world, B, words,
                                             B * words, self.p.occupancy_lifetime)
-                # key-range partition; the split sizes to the host without a stream sync
-                eng.partition_points(self.world, S.sp.data_ptr(), S.sk.data_ptr(), S.cap,
-                                     S.cnt.data_ptr())
-                S.c64.copy_(S.cnt)
+                # key-range partition into points + runs of equal keys; the split sizes
+                # (points, runs) per part to the host without a stream sync
+                eng.partition_runs(self.world, S.sp.data_ptr(), S.srk.data_ptr(),
+                                   S.srs.data_ptr(), S.cap, S.cnt.data_ptr())
+                S.c64.copy_(S.cnt.view(2, self.world).t())
                 dist.all_to_all_single(S.rc, S.c64)
-                S.host[:self.world].copy_(S.c64, non_blocking=True)
-                S.host[self.world:].copy_(S.rc, non_blocking=True)
+                S.host[:2 * self.world].copy_(S.c64.view(-1), non_blocking=True)
+                S.host[2 * self.world:].copy_(S.rc.view(-1), non_blocking=True)
                 S.ev.record(st)
                 S.pending = True
             else:
@@ -447,10 +478,12 @@ class FusedCloudRank:
                 dg = h.DeviceArray.from_numpy(torch.cat(parts).numpy())
                 eng.voxelOccupancyGridBatch(dg.ptr, words, self.world, B, words, B * words,
                                             self.p.occupancy_lifetime)
-                dsp, dsk, dcnt = h.DeviceArray(n_total * 16), h.DeviceArray(n_total * 4), h.DeviceArray(64)
-                eng.partition_points(self.world, dsp.ptr, dsk.ptr, n_total, dcnt.ptr)
+                dsp, drk, drs = (h.DeviceArray(n_total * 16), h.DeviceArray(n_total * 4),
+                                 h.DeviceArray(n_total * 4))
+                dcnt = h.DeviceArray(2 * self.world * 4)
+                eng.partition_runs(self.world, dsp.ptr, drk.ptr, drs.ptr, n_total, dcnt.ptr)
                 eng.synchronize()
-                self._staged[k] = (dg, dsp, dsk, dcnt)
+                self._staged[k] = (dg, dsp, drk, drs, dcnt)
         return k
 
     def finish(self, k):
@@ -467,32 +500,42 @@ class FusedCloudRank:
                 raise RuntimeError("FusedCloudRank.finish: no step in flight on this slot")
             st = self.streams[k]
             S.ev.synchronize()  # (the slot's split sizes; the later slots keep the GPU busy)
-            both = S.host.tolist()
-            scounts = [int(x) for x in both[:self.world]]
-            rcounts = [int(x) for x in both[self.world:]]
-            n, m = sum(rcounts), sum(scounts)
+            both = [int(x) for x in S.host.tolist()]
+            W = self.world
+            scounts, sruns = both[0:2 * W:2], both[1:2 * W:2]
+            rcounts, rruns = both[2 * W::2], both[2 * W + 1::2]
+            n, m, R, M = sum(rcounts), sum(scounts), sum(rruns), sum(sruns)
             S.ensure(st, n_recv=max(n, 1))
             with torch.cuda.stream(st):
                 if self.world > 1 or n:
+                    g = self.pg_points
                     dist.all_to_all_single(S.rp[:n], S.sp[:m], output_split_sizes=rcounts,
-                                           input_split_sizes=scounts, group=self.pg_points)
-                    dist.all_to_all_single(S.rk[:n], S.sk[:m], output_split_sizes=rcounts,
-                                           input_split_sizes=scounts, group=self.pg_points)
-                eng.voxelize_points(S.rp.data_ptr(), S.rk.data_ptr(), n, self.p.voxel_average)
+                                           input_split_sizes=scounts, group=g)
+                    dist.all_to_all_single(S.rrk[:R], S.srk[:M], output_split_sizes=rruns,
+                                           input_split_sizes=sruns, group=g)
+                    dist.all_to_all_single(S.rrs[:R], S.srs[:M], output_split_sizes=rruns,
+                                           input_split_sizes=sruns, group=g)
+                eng.voxelize_runs(S.rp.data_ptr(), S.rrk.data_ptr(), S.rrs.data_ptr(),
+                                  np.cumsum([0] + rcounts), np.cumsum([0] + rruns),
+                                  self.p.voxel_average)
             S.pending = False
             return scounts
-        dg, dsp, dsk, dcnt = self._staged.pop(k)
-        counts = dcnt.to_numpy(np.uint32, self.world).tolist()
-        m = int(sum(counts))
+        dg, dsp, drk, drs, dcnt = self._staged.pop(k)
+        c = dcnt.to_numpy(np.uint32, 2 * self.world).tolist()
+        counts, runs = c[:self.world], c[self.world:]
+        m, M = int(sum(counts)), int(sum(runs))
         sp = torch.from_numpy(dsp.to_numpy(np.float32, 4 * max(m, 1))[:4 * m].reshape(m, 4))
-        sk = torch.from_numpy(dsk.to_numpy(np.int32, max(m, 1))[:m])
-        rp, rk, rc = exchange_points(sp, sk, counts)
-        n = int(sum(rc))
+        srk = torch.from_numpy(drk.to_numpy(np.int32, max(M, 1))[:M])
+        srs = torch.from_numpy(drs.to_numpy(np.int32, max(M, 1))[:M])
+        rp, rrk, rrs, rc, rr = exchange_runs(sp, srk, srs, counts, runs)
+        n, R = int(sum(rc)), int(sum(rr))
         drp = h.DeviceArray.from_numpy(rp.numpy()) if n else None
-        drk = h.DeviceArray.from_numpy(rk.numpy()) if n else None
-        eng.voxelize_points(drp.ptr if n else 0, drk.ptr if n else 0, n, self.p.voxel_average)
+        drk2 = h.DeviceArray.from_numpy(rrk.numpy()) if R else None
+        drs2 = h.DeviceArray.from_numpy(np.concatenate([rrs.numpy(), np.zeros(1, np.int32)]))
+        eng.voxelize_runs(drp.ptr if n else 0, drk2.ptr if R else 0, drs2.ptr,
+                          np.cumsum([0] + rc), np.cumsum([0] + rr), self.p.voxel_average)
         eng.synchronize()
-        self._keep = [dg, drp, drk]
+        self._keep = [dg, drp, drk2, drs2]
         return counts
 
     def run(self, steps, depth_ptrs_of, tail_ptrs_of, move_of=None, on_finish=None):
@@ -518,6 +561,116 @@ class FusedCloudRank:
             self.finish(kk)
             if on_finish:
                 on_finish(j)
+
+
+def rccl_library_path() -> str:
+    """The librccl torch loaded (torch/lib/librccl.so), so the C++ rank and torch share one RCCL."""
+    import torch
+    p = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    return p if os.path.exists(p) else "librccl.so"
+
+
+class NativeFusedRank:
+    """FusedCloudRank's RCCL path with the step in C++ (include/gdf_fused.h, csrc/gdf_fused.cpp):
+    the halo / mark / split-size all-gathers, the grid update, the partition and the grouped
+    send / recv of the (point, key) lists issued by libgdf on the engine slots' streams over two
+    RCCL communicators of its own (ids broadcast over the default process group) - no Python,
+    torch op or host copy between the launches of a step.  Same start / finish / run / frame /
+    batch interface and results as FusedCloudRank(dev="cuda")."""
+
+    def __init__(self, engine, cams, rank: int, world: int, params, depth: int = 1):
+        import ctypes as C
+        import torch.distributed as dist
+        from . import hiprt
+        from .gdf import StreamCamera
+        self.eng, self.cams, self.rank, self.world, self.p = engine, cams, rank, world, params
+        self.dev, self.hiprt = "cuda", hiprt
+        self.depth = max(1, min(4, int(depth)))
+        self._lib = engine._lib
+        self.F = params.flying_filter_size
+        path = rccl_library_path().encode()
+        ids = (C.c_uint8 * 256)()
+        if rank == 0:
+            engine._check(self._lib.gdf_fused_unique_id(path, ids))
+        obj = [bytes(ids)]
+        dist.broadcast_object_list(obj, src=0)
+        ids = (C.c_uint8 * 256).from_buffer_copy(obj[0])
+        sc = (StreamCamera * world)()
+        for k in range(world):
+            c = cams[k]
+            sc[k].ring, sc[k].width, sc[k].height = 0, c.width, c.height
+            sc[k].depth_scale, sc[k].fx, sc[k].fy, sc[k].cx, sc[k].cy = c.intrinsics()
+            sc[k].T_world[:] = np.asarray(c.T_world, np.float32).ravel().tolist()
+            sc[k].T_crop[:] = np.asarray(c.T_crop, np.float32).ravel().tolist()
+        self._cams_c = sc
+        h = C.c_void_p()
+        engine.set_pipeline_depth(self.depth)
+        engine._check(self._lib.gdf_fused_create(engine.handle, path, ids, rank, world, sc,
+                                                 self.F, C.byref(h)))
+        self._h = h
+        L = C.c_uint32()
+        engine._check(self._lib.gdf_fused_halo_pixels(h, C.byref(L)))
+        self.Lmax = L.value
+        self.pc = params.to_c(None, None, False, True, True)
+        self.rollbuffer_rank = world - 1
+        self.has_rollbuffer = rank == self.rollbuffer_rank
+        self._pc_move = {}
+
+    frame_params = FusedCloudRank.frame_params
+
+    def close(self):
+        """Destroys the C++ rank (its communicators, buffers); the engine stays."""
+        if getattr(self, "_h", None):
+            self._lib.gdf_fused_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def start(self, depth_ptrs, tail_src_ptrs=None, move=None):
+        """gdf_fused_start (the halo tails are the depth maps' last Lmax values: tail_src_ptrs is
+        accepted for FusedCloudRank's signature and not read)."""
+        import ctypes as C
+        arr = (C.c_void_p * len(depth_ptrs))(*depth_ptrs)
+        k = C.c_int()
+        p = self.frame_params(move) if len(depth_ptrs) == 1 else self.pc
+        self.eng._check(self._lib.gdf_fused_start(self._h, arr, len(depth_ptrs), C.byref(p),
+                                                  C.byref(k)))
+        return k.value
+
+    def finish(self, k):
+        import ctypes as C
+        sc = (C.c_uint32 * self.world)()
+        n = C.c_uint32()
+        self.eng._check(self._lib.gdf_fused_finish(self._h, k, sc, C.byref(n)))
+        return list(sc)
+
+    def frame(self, depth_ptr: int, tail_src_ptr: int = 0, move=None):
+        return self.finish(self.start([depth_ptr], None, move))
+
+    def batch(self, depth_ptrs, tail_src_ptrs=None):
+        return self.finish(self.start(depth_ptrs))
+
+    run = FusedCloudRank.run
+
+    def run_stream(self, frame_ptrs, first: int, steps: int, batch: int):
+        """gdf_fused_run: `steps` pipelined steps of `batch` frames from the device ring
+        frame_ptrs (step s takes frames (first + s) * batch + j), no Python per step."""
+        import ctypes as C
+        from .gdf import StreamCamera
+        c = self.cams[self.rank]
+        sc = StreamCamera()
+        arr = (C.c_void_p * len(frame_ptrs))(*frame_ptrs)
+        sc.frames = C.cast(arr, C.POINTER(C.c_void_p))
+        sc.ring, sc.width, sc.height = len(frame_ptrs), c.width, c.height
+        sc.depth_scale, sc.fx, sc.fy, sc.cx, sc.cy = c.intrinsics()
+        sc.T_world[:] = np.asarray(c.T_world, np.float32).ravel().tolist()
+        sc.T_crop[:] = np.asarray(c.T_crop, np.float32).ravel().tolist()
+        self.eng._check(self._lib.gdf_fused_run(self._h, C.byref(sc), C.byref(self.pc), first,
+                                                steps, batch, self.depth))
 
 
 class _nullctx:

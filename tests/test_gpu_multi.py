@@ -194,7 +194,7 @@ def test_fused_cloud_survey_configs(tmp_path, cfg):
                                           f"{cfg} frame {f} rank {r}")
 
 
-def _rank_nccl(rank, world, port, out_dir):
+def _rank_nccl(rank, world, port, out_dir, native=False):
     """One process, RCCL (backend "nccl") at world 1: FusedCloudRank(dev="cuda") with the engine
     on torch's stream - the device collectives (all-gather of marks, all-to-all of counts and of
     the (point, key) lists, the gather of the fused cloud) over RCCL, frame by frame and per
@@ -210,7 +210,8 @@ def _rank_nccl(rank, world, port, out_dir):
     p = ComponentParams()
     cams = [synth.make_camera(k, W, H) for k in range(world)]
     eng = GPUDepthmapFusion(0)
-    fr = multi.FusedCloudRank(eng, cams, rank, world, p, dev="cuda")
+    fr = (multi.NativeFusedRank(eng, cams, rank, world, p) if native else
+          multi.FusedCloudRank(eng, cams, rank, world, p, dev="cuda"))
     n = W * H
     ds = [hiprt.DeviceArray.from_numpy(synth.dense_frame(cams[rank], rank, f)) for f in range(4)]
     for f in range(2):
@@ -227,17 +228,21 @@ def _rank_nccl(rank, world, port, out_dir):
     for j in range(2):
         np.save(os.path.join(out_dir, f"nvox_f{2 + j}.npy"), vox[vs[j]:vs[j + 1]])
     np.save(os.path.join(out_dir, "ngrid_f3.npy"), eng.downloadVoxelOccupancyGrid())
+    if native:
+        fr.close()
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_rccl_fused_cloud_world1(tmp_path):
-    """The RCCL branch of FusedCloudRank (dev="cuda", backend nccl) on the box's GPU at world 1:
-    two frames one by one, then a 2-frame batch - voxel means, grids and the gathered publishing
-    cloud equal the oracle bit for bit."""
+@pytest.mark.parametrize("native", [False, True])
+def test_rccl_fused_cloud_world1(tmp_path, native):
+    """The RCCL branch of FusedCloudRank (dev="cuda", backend nccl) - and its C++ form
+    NativeFusedRank (gdf_fused_*, RCCL from libgdf) - on the box's GPU at world 1: two frames one
+    by one, then a 2-frame batch - voxel means, grids and the gathered publishing cloud equal the
+    oracle bit for bit."""
     from oracle import OracleFusion
-    mp.start_processes(_rank_nccl, args=(1, _free_port(), str(tmp_path)), nprocs=1, join=True,
-                       start_method="spawn")
+    mp.start_processes(_rank_nccl, args=(1, _free_port(), str(tmp_path), native), nprocs=1,
+                       join=True, start_method="spawn")
     p = ComponentParams()
     cam = synth.make_camera(0, W, H)
     orc = OracleFusion(threads=4)
@@ -347,7 +352,7 @@ def test_fused_cloud_rollbuffer_leg(tmp_path, cfg):
 
 
 # ---- the pipelined RCCL path: steps in the engine's slots ----------------
-def _rank_nccl_pipe(rank, world, port, out_dir, depth, rollbuffer):
+def _rank_nccl_pipe(rank, world, port, out_dir, depth, rollbuffer, native=False):
     """RCCL at world 1, FusedCloudRank(depth=3).run(): step i+1 starts (compaction, marks, grid
     update, partition, split sizes) before step i's points all-to-all and voxelize - on the
     slots' own streams, the points on their own communicator.  Batches of 2 frames, or (with the
@@ -365,7 +370,8 @@ def _rank_nccl_pipe(rank, world, port, out_dir, depth, rollbuffer):
     p.ps_timespan = 2.5 / 30.0
     cams = [synth.make_camera(k, W, H) for k in range(world)]
     eng = GPUDepthmapFusion(0)
-    fr = multi.FusedCloudRank(eng, cams, rank, world, p, dev="cuda", depth=depth)
+    fr = (multi.NativeFusedRank(eng, cams, rank, world, p, depth=depth) if native else
+          multi.FusedCloudRank(eng, cams, rank, world, p, dev="cuda", depth=depth))
     n = W * H
     B = 1 if rollbuffer else 2
     steps = 6
@@ -397,19 +403,26 @@ def _rank_nccl_pipe(rank, world, port, out_dir, depth, rollbuffer):
     if rollbuffer:
         np.save(os.path.join(out_dir, f"prb_f{steps - 1}.npy"), np.array(eng.rollbuffer_state().as_tuple()))
     np.save(os.path.join(out_dir, "pgrid.npy"), eng.downloadVoxelOccupancyGrid())
+    if native and not rollbuffer:  # and the C++ loop (gdf_fused_run) over the same frames
+        fr.run_stream([d.ptr for d in ds], 0, steps, B)
+        torch.cuda.synchronize()
+        np.save(os.path.join(out_dir, "pvox_run_last.npy"), eng.downloadVoxelizedPoints()[:, :3])
+    if native:
+        fr.close()
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("rollbuffer", [False, True])
-def test_rccl_pipelined_fused_cloud_world1(tmp_path, rollbuffer):
+@pytest.mark.parametrize("rollbuffer,native", [(False, False), (True, False), (False, True),
+                                                (True, True)])
+def test_rccl_pipelined_fused_cloud_world1(tmp_path, rollbuffer, native):
     """The pipelined fused path (three steps in flight on the engine's slots, the points
     all-to-all on a second communicator) under RCCL at world 1: every frame's voxel means, the
     final grid and (rollbuffer) the rollbuffer state after every frame equal the oracle's bit for
     bit."""
     import fused_ref
     from oracle import OracleFusion
-    mp.start_processes(_rank_nccl_pipe, args=(1, _free_port(), str(tmp_path), 3, rollbuffer),
+    mp.start_processes(_rank_nccl_pipe, args=(1, _free_port(), str(tmp_path), 3, rollbuffer, native),
                        nprocs=1, join=True, start_method="spawn")
     p = ComponentParams()
     p.ps_timespan = 2.5 / 30.0
@@ -431,3 +444,8 @@ def test_rccl_pipelined_fused_cloud_world1(tmp_path, rollbuffer):
         got = np.load(tmp_path / f"pvox_f{f}.npy")
         assert len(got) == len(want) > 0 and np.array_equal(got.view(np.uint32), want.view(np.uint32)), f
     np.testing.assert_array_equal(np.load(tmp_path / "pgrid.npy"), orc.downloadVoxelOccupancyGrid())
+    if native and not rollbuffer:  # gdf_fused_run over the same frames: its last step's
+        B = 2  # voxels = the last step's (voxel means depend on the step's frames only)
+        last = np.load(tmp_path / "pvox_run_last.npy")
+        want = np.concatenate([np.load(tmp_path / f"pvox_f{f}.npy") for f in range(nf - B, nf)])
+        assert np.array_equal(last.view(np.uint32), want.view(np.uint32))

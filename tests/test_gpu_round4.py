@@ -172,3 +172,66 @@ def test_4k_frame_knobs_match_oracle(Engine, knobs):
         e.addDepthmap(*cam_args(cam, synth.dense_frame(cam, 0, 0)))
         e.processFrame(p)
     compare_results(gpu, orc, tag=f"4K {knobs}")
+
+
+@pytest.mark.parametrize("nparts,B", [(1, 1), (3, 1), (5, 3), (16, 8)])
+def test_partition_runs_voxelize_runs_match_oracle(Engine, nparts, B):
+    """gdf_partition_runs (points + runs of equal frame|voxel keys, part-major) and
+    gdf_voxelize_runs per part, in one process: every part voxelized on its own, the parts'
+    voxels concatenated in part order, equal the oracle's voxel means of each frame bit for bit
+    (the fused cloud's key ranges without the transport).  Also: sources split at arbitrary
+    points of a part (several "ranks" sending one key range) rebase to the same result."""
+    from ros_gpu_depthmap_fusion_amd import hiprt
+    p = ComponentParams()
+    cam = synth.make_camera(0, 640, 480)
+    gpu, orc = Engine(), OracleFusion(threads=16)
+    frames = [synth.dense_frame(cam, 0, 11 + j) for j in range(B)]
+    gpu.clear()
+    for j in range(B):
+        if j:
+            gpu.nextFrameInBatch()
+        gpu.addDepthmap(*cam_args(cam, frames[j]))
+    res = gpu.processFrame(p, synchronous=True, defer_occupancy_grid=True, defer_voxelize=True)
+    n = int(gpu.downloadPoints().shape[0])
+    cap = int(res.num_points_total)  # (the send buffers hold the frame's pixels before compaction)
+    sp, srk, srs = hiprt.DeviceArray(16 * cap), hiprt.DeviceArray(4 * cap), hiprt.DeviceArray(4 * cap)
+    cnt = hiprt.DeviceArray(8 * nparts)
+    gpu.partition_runs(nparts, sp.ptr, srk.ptr, srs.ptr, cap, cnt.ptr)
+    gpu.synchronize()
+    c = cnt.to_numpy(np.uint32, 2 * nparts)
+    pts, runs = c[:nparts].astype(np.int64), c[nparts:].astype(np.int64)
+    assert pts.sum() == n and (runs <= pts).all() and ((runs > 0) == (pts > 0)).all()
+    P0, R0 = np.concatenate([[0], np.cumsum(pts)]), np.concatenate([[0], np.cumsum(runs)])
+    h_rs = srs.to_numpy(np.uint32, max(n, 1))
+    want = []
+    for j in range(B):
+        orc.clear()
+        orc.addDepthmap(*cam_args(cam, frames[j]))
+        orc.processFrame(p)
+        want.append(orc.downloadVoxelizedPoints()[:, :3])
+    got = [[] for _ in range(B)]
+    for q in range(nparts):
+        if pts[q] == 0:
+            continue
+        rs = h_rs[R0[q]:R0[q + 1]]
+        assert rs[0] == 0 and (np.diff(rs.astype(np.int64)) > 0).all() and rs[-1] < pts[q]
+        # the part as two sources split at a run boundary (a key range from two ranks)
+        cut = len(rs) // 2
+        pb = np.array([0, rs[cut], pts[q]] if cut else [0, pts[q]], np.uint32)
+        rb = np.array([0, cut, len(rs)] if cut else [0, len(rs)], np.uint32)
+        local = rs.astype(np.uint32).copy()
+        if cut:
+            local[cut:] -= rs[cut]
+        drs = hiprt.DeviceArray.from_numpy(np.concatenate([local, np.zeros(1, np.uint32)]))
+        gpu.voxelize_runs(sp.ptr + 16 * int(P0[q]), srk.ptr + 4 * int(R0[q]), drs.ptr, pb, rb)
+        vox = gpu.downloadVoxelizedPoints()[:, :3]
+        if B > 1:
+            _, vs = gpu.batch_ranges()
+            for j in range(B):
+                got[j].append(vox[vs[j]:vs[j + 1]])
+        else:
+            got[0].append(vox)
+    for j in range(B):
+        g = np.concatenate(got[j]) if got[j] else np.zeros((0, 3), np.float32)
+        assert len(g) == len(want[j]) > 0, (nparts, B, j)
+        assert np.array_equal(g.view(np.uint32), want[j].view(np.uint32)), (nparts, B, j)
