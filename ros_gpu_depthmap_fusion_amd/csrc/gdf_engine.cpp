@@ -356,7 +356,8 @@ struct Slot {
         ~Pinned() {
             if (p) (void)hipHostFree(p);
         }
-    } h_pts, h_coords, h_vox, h_delta;
+    } h_pts, h_coords, h_vox, h_delta, h_miscpf;
+    bool pf_valid = false;          // this slot's last frame wrote its downloads (k_download)
     DevBuf d_didx, d_ddata;         // the grid delta of this slot's single-frame update
     bool delta_valid = false;
     uint32_t delta_ticket = 0;      // ... and that update's sequence number
@@ -488,6 +489,10 @@ struct gdf_engine {
     bool grid_delta = false;
     bool grid_delta_allowed = !getenv("GDF_NO_GRID_DELTA");
     Slot::Pinned h_mirror;
+    // after a single-frame gdf_download_frame of points / coords / voxels: single frames end with
+    // k_download into the slot's pinned mirrors (the next download_frame waits once)
+    bool dl_prefetch = false;
+    bool dl_prefetch_allowed = !getenv("GDF_NO_DL_PREFETCH");
     bool mirror_valid = false;
     uint32_t mirror_ticket = 0, mirror_gen = 0;
 
@@ -642,6 +647,7 @@ void next_slot(gdf_engine* e) {
 // ---- frame inputs ---------------------------------------------------------------------------------
 void engine_clear(gdf_engine* e) {  // fusion.cpp:725-732
     next_slot(e);
+    e->sl().pf_valid = false;
     e->nframes = 1;
     e->rb.selection_point_count = 0;
     e->rb.selection_sequence_count = 0;
@@ -1355,6 +1361,7 @@ void frame_launched(gdf_engine* e, bool fused_voxel, bool key_hist, bool runs = 
 }
 
 void run_frame(gdf_engine* e, bool fused_voxel, bool compaction_marks = false) {
+    e->sl().pf_valid = false;
     const FrameArgs a = frame_args(e, fused_voxel, compaction_marks);
     if (e->profiling) e->timed(GDF_KERNEL_EVENT_FLOOR, [] {});  // calibrates the event overhead
     e->timed(GDF_KERNEL_FRAME, [&] { HIPCHK(launch_frame(a, e->s(), e->hook_ptr())); });
@@ -1514,6 +1521,7 @@ void voxelize_launched(gdf_engine* e, int fused_grid_lifetime) {
 }
 
 void voxelize(gdf_engine* e, int average, int fused_grid_lifetime = -1) {
+    e->sl().pf_valid = false;
     const VoxelizeArgs v = voxelize_args(e, average, fused_grid_lifetime);
     e->timed(GDF_KERNEL_VOXELIZE, [&] { HIPCHK(launch_voxelize(v, e->s(), e->hook_ptr())); });
     voxelize_launched(e, fused_grid_lifetime);
@@ -1536,6 +1544,41 @@ bool same_key(const FrameArgs& a, const VoxelizeArgs& v, const FrameArgs& ka, co
 
 // processFrame's fused frame (compaction + voxelize + grid update) on the slot's stream:
 // direct launches, or the slot's captured graph when the launch arguments repeat
+// gdf_download_frame prefetch: a single frame's downloads written by k_download at the end of
+// its launch chain (after the voxelize and the grid update it carries)
+void prefetch_downloads(gdf_engine* e, hipStream_t st) {
+    Slot& q = e->sl();
+    q.pf_valid = false;
+    if (!e->dl_prefetch || e->nframes != 1 || e->user_stream) return;
+    const uint32_t cap = std::max<uint32_t>(q.n_total, 1);
+    const uint32_t dcap = q.delta_valid ? (uint32_t)((mark_words(e) + 3) / 4 * 4) : 0u;
+    DlArgs d{};
+    d.misc = q.d_misc.as<uint32_t>();
+    d.misc_words = kMiscWords;
+    d.i_count = kCount;
+    d.i_vox = kVoxCount;
+    d.i_delta = kDeltaCount;
+    d.pts = q.d_pts.as<uint4>();
+    d.coords = q.d_coords.as<uint32_t>();
+    d.vox = q.d_vox.as<uint4>();
+    d.didx = q.d_didx.as<uint32_t>();
+    d.ddata = q.d_ddata.as<uint4>();
+    d.pts_cap = cap;
+    d.vox_cap = (uint32_t)std::min<size_t>(q.d_vox.bytes / 16, cap);
+    d.delta_cap = dcap;
+    d.h_misc = static_cast<uint32_t*>(q.h_miscpf.ensure(kMiscWords * 4));
+    d.h_pts = static_cast<uint4*>(q.h_pts.ensure((size_t)cap * 16));
+    d.h_coords = static_cast<uint32_t*>(q.h_coords.ensure((size_t)cap * 4));
+    d.h_vox = static_cast<uint4*>(q.h_vox.ensure((size_t)std::max<uint32_t>(d.vox_cap, 1) * 16));
+    uint8_t* hd = static_cast<uint8_t*>(q.h_delta.ensure((size_t)std::max<uint32_t>(dcap, 4) * 36));
+    if (!d.h_misc || !d.h_pts || !d.h_coords || !d.h_vox || !hd)
+        fail(GDF_ERR_NOMEM, "pinned download mirror allocation failed");
+    d.h_didx = reinterpret_cast<uint32_t*>(hd);
+    d.h_ddata = reinterpret_cast<uint4*>(hd + (size_t)dcap * 4);
+    HIPCHK(launch_download(d, st));
+    q.pf_valid = true;
+}
+
 void run_fused_frame(gdf_engine* e, int average, uint32_t lifetime) {
     const FrameArgs a = frame_args(e, true);
     frame_launched(e, true, a.key_hist != nullptr, a.run_mode != 0);  // (the launches below follow)
@@ -1634,9 +1677,11 @@ void run_fused_frame(gdf_engine* e, int average, uint32_t lifetime) {
         e->timed(GDF_KERNEL_VOXELIZE, [&] { HIPCHK(launch_voxelize(v, st, e->hook_ptr())); });
     }
     voxelize_launched(e, (int)lifetime);
+    prefetch_downloads(e, st);
 }
 
 void occupancy_grid(gdf_engine* e, uint32_t lifetime, hipStream_t st) {  // fusion.cpp:1757-1823
+    e->sl().pf_valid = false;
     if (!e->grid_set) fail(GDF_ERR_STATE, "voxelOccupancyGrid before computeVoxelCoords");
     widen_if_needed(e, lifetime, st);
     if (!e->sl().marks_set) {
@@ -1739,6 +1784,8 @@ int gdf_create(int device, gdf_engine** out) {
             g_run_stage = (uint32_t)std::max(1, std::atoi(v));
         if (const char* v = std::getenv("GDF_EMIT_PX2"))  // tuning knob
             g_emit_px2 = (uint32_t)std::atoi(v);
+        if (const char* v = std::getenv("GDF_GRID_WPT"))  // tuning knob: 1..8
+            g_grid_wpt = (uint32_t)std::min(8, std::max(1, std::atoi(v)));
         if (const char* v = std::getenv("GDF_MASK_PX"))  // tuning knob: pixels per k_mask thread
             g_mask_px2 = (uint32_t)std::atoi(v);
         if (const char* v = std::getenv("GDF_RUN_Q16"))  // tuning knob
@@ -2152,6 +2199,57 @@ int gdf_download_frame(gdf_engine* e, uint32_t what, gdf_host_frame* out) {
         if ((what & GDF_DL_GRID) && (!e->grid_set || !e->invoked_once))
             fail(GDF_ERR_STATE, "download_frame: no voxelOccupancyGrid has run");
         if (what & GDF_DL_GRID) sync_all(e);  // grid updates may still run on another slot's stream
+        if (q.pf_valid) {  // k_download wrote everything: the one wait
+            e->sync();
+            q.pf_valid = false;
+            const uint32_t* hm = static_cast<const uint32_t*>(q.h_miscpf.p);
+            if (hm[kErr]) {
+                HIPCHK(hipMemsetAsync(q.d_misc.as<uint32_t>() + kErr, 0, 4, e->s()));
+                fail(GDF_ERR_DEVICE, "device look-back spin limit expired (code " + std::to_string(hm[kErr]) + ")");
+            }
+            std::memcpy(q.h_misc, hm, kMiscWords * 4);
+            const uint32_t n = hm[kCount], nv = hm[kVoxCount];
+            if (what & GDF_DL_POINTS) {
+                out->points = static_cast<const float*>(q.h_pts.p);
+                out->num_points = n;
+            }
+            if (what & GDF_DL_COORDS) {
+                out->voxel_coords = static_cast<const uint32_t*>(q.h_coords.p);
+                out->num_points = n;
+            }
+            if (what & GDF_DL_VOXELIZED) {
+                out->voxelized = static_cast<const float*>(q.h_vox.p);
+                out->num_voxelized = nv;
+            }
+            if (what & GDF_DL_GRID) {
+                const uint32_t latest = e->grid_ticket - 1u;
+                const uint32_t nd = hm[kDeltaCount];
+                const uint32_t dcap = (uint32_t)((mark_words(e) + 3) / 4 * 4);
+                const bool apply = q.delta_valid && q.delta_ticket == latest && e->mirror_valid &&
+                                   e->mirror_gen == e->grid_gen && e->mirror_ticket + 1u == latest &&
+                                   e->grid_mode == 0 && nd <= dcap;
+                const size_t padded = (size_t)mark_words(e) * 32;
+                if (!e->h_mirror.ensure(padded)) fail(GDF_ERR_NOMEM, "pinned grid mirror allocation failed");
+                uint8_t* mir = static_cast<uint8_t*>(e->h_mirror.p);
+                if (apply) {
+                    const uint8_t* hd = static_cast<const uint8_t*>(q.h_delta.p);
+                    const uint32_t* idx = reinterpret_cast<const uint32_t*>(hd);
+                    const uint8_t* data = hd + (size_t)dcap * 4;
+                    for (uint32_t k = 0; k < nd; ++k)
+                        std::memcpy(mir + (size_t)idx[k] * 32, data + (size_t)k * 32, 32);
+                } else {
+                    HIPCHK(hipMemcpyAsync(mir, grid_out_ptr(e), e->ncells, hipMemcpyDeviceToHost, e->s()));
+                    e->sync();
+                }
+                e->mirror_valid = true;
+                e->mirror_ticket = latest;
+                e->mirror_gen = e->grid_gen;
+                out->occupancy = mir;
+                out->num_cells = e->ncells;
+                if (e->grid_delta_allowed) e->grid_delta = true;
+            }
+            return;
+        }
         e->read_misc();  // the counts (one wait)
         const uint32_t n = q.h_misc[kCount], nv = q.h_misc[kVoxCount];
         auto copy = [&](Slot::Pinned& m, const void* src, size_t bytes) -> void* {
@@ -2211,6 +2309,10 @@ int gdf_download_frame(gdf_engine* e, uint32_t what, gdf_host_frame* out) {
             for (uint32_t k = 0; k < nd; ++k) std::memcpy(mir + (size_t)idx[k] * 32, data + (size_t)k * 32, 32);
         }
         if ((what & GDF_DL_GRID) && e->grid_delta_allowed) e->grid_delta = true;  // from now on
+        // single frames: from now on the launch chain ends with k_download (prefetch)
+        if ((what & (GDF_DL_POINTS | GDF_DL_COORDS | GDF_DL_VOXELIZED)) && q.nframes == 1 &&
+            e->dl_prefetch_allowed)
+            e->dl_prefetch = true;
     });
 }
 
@@ -2433,6 +2535,7 @@ int gdf_voxelize_runs(gdf_engine* e, const float* pts, const uint32_t* run_keys,
             HIPCHK(hipMemsetAsync(e->sl().d_khist.p, 0, kHistWords * 4, e->s()));
             e->sl().khist_pending = false;
         }
+        e->sl().pf_valid = false;
         uint32_t* misc = e->sl().d_misc.as<uint32_t>();
         HIPCHK(launch_run_rebase(run_starts, rb, misc + kRecvCount, misc + kRecvRuns, e->s()));
         VoxSource src;
@@ -2458,6 +2561,7 @@ int gdf_voxelize_points(gdf_engine* e, const float* pts, const uint32_t* keys, u
             HIPCHK(hipMemsetAsync(e->sl().d_khist.p, 0, kHistWords * 4, e->s()));
             e->sl().khist_pending = false;
         }
+        e->sl().pf_valid = false;
         HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(e->sl().d_misc.as<uint32_t>() + kRecvCount),
                                  (int)n, 1, e->s()));
         VoxSource src;

@@ -2489,7 +2489,8 @@ __global__ __launch_bounds__(256) void k_grid_u8_batch(uint4* __restrict__ grid,
     grid_seq_leave(q, f0, gridDim.x);
 }
 
-uint32_t fused_grid_blocks(uint64_t ncells) { return grid_blocks((ncells + 31) / 32, 256 * 2); }
+uint32_t g_grid_wpt = 2;  // mark words per thread of the grid blocks carried by radix pass 1 (GDF_GRID_WPT)
+uint32_t fused_grid_blocks(uint64_t ncells) { return grid_blocks((ncells + 31) / 32, 256 * g_grid_wpt); }
 uint32_t batch_grid_blocks(uint64_t ncells) { return grid_blocks((ncells + 31) / 32, 256); }
 
 hipError_t launch_grid_u8_batch(uint8_t* grid, const uint32_t* bits, uint64_t ncells,
@@ -4349,6 +4350,31 @@ hipError_t launch_partition(const float4* pts, const uint32_t* keys, const uint3
         hipLaunchKernelGGL(k_part_scatter<false>, dim3(blocks), dim3(256), 0, s, pts, keys, count,
                            nparts, ncells, ntiles, offsets, total, out_pts, out_keys, part_counts,
                            fstart, nframes, fshift, out_run_keys, out_run_start);
+    return hipGetLastError();
+}
+
+// gdf_download_frame prefetch (DlArgs): one grid-stride pass over [counters | points | coords |
+// voxelized | delta indices | delta data], 16-B stores where the items are 16 B (the host link
+// takes coalesced wave stores at DMA-like rates).
+__global__ __launch_bounds__(256) void k_download(DlArgs d) {
+    const uint32_t n = min(d.misc[d.i_count], d.pts_cap);
+    const uint32_t nv = min(d.misc[d.i_vox], d.vox_cap);
+    const uint32_t nd = d.delta_cap ? min(d.misc[d.i_delta], d.delta_cap) : 0u;
+    const uint64_t e0 = d.misc_words, e1 = e0 + n, e2 = e1 + n, e3 = e2 + nv, e4 = e3 + nd,
+                   e5 = e4 + 2ull * nd;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < e5; i += stride) {
+        if (i < e0) d.h_misc[i] = d.misc[i];
+        else if (i < e1) d.h_pts[i - e0] = d.pts[i - e0];
+        else if (i < e2) d.h_coords[i - e1] = d.coords[i - e1];
+        else if (i < e3) d.h_vox[i - e2] = d.vox[i - e2];
+        else if (i < e4) d.h_didx[i - e3] = d.didx[i - e3];
+        else d.h_ddata[i - e4] = d.ddata[i - e4];
+    }
+}
+
+hipError_t launch_download(const DlArgs& d, hipStream_t s) {
+    hipLaunchKernelGGL(k_download, dim3(512), dim3(256), 0, s, d);
     return hipGetLastError();
 }
 

@@ -44,6 +44,7 @@ const void* mask_kernel(const FrameArgs& a);  // the compaction pass-1 kernel la
 extern uint32_t g_mask_px2;
 const void* emit_kernel(const FrameArgs& a);  // the compaction pass-2 kernel launch_frame uses
 extern uint32_t g_emit_px2;
+extern uint32_t g_grid_wpt;
 
 // filter_point_sequence + insert into the rollbuffer ring (w = mask)
 hipError_t launch_ps_filter_insert(const float4* new_pts, uint32_t n, int do_filter, float thr,
@@ -181,6 +182,29 @@ hipError_t launch_partition(const float4* pts, const uint32_t* keys, const uint3
                             const uint32_t* fstart = nullptr, uint32_t nframes = 1,
                             uint32_t fshift = 0, uint32_t* out_run_keys = nullptr,
                             uint32_t* out_run_start = nullptr);
+
+// gdf_download_frame's prefetch: a single-frame launch chain ends with ONE kernel that writes the
+// frame's downloads - the small counters, the points, voxel coords, voxelized points and the grid
+// delta, each of the size the counters name - straight into pinned (host-mapped) mirrors, so the
+// host waits once for the stream instead of reading the counts, then queueing the copies, then
+// waiting again.
+struct DlArgs {
+    const uint32_t* misc;
+    uint32_t misc_words, i_count, i_vox, i_delta;  // counter words: points, voxels, delta groups
+    const uint4* pts;
+    const uint32_t* coords;
+    const uint4* vox;
+    const uint32_t* didx;
+    const uint4* ddata;  // 2 per group
+    uint32_t pts_cap, vox_cap, delta_cap;
+    uint32_t* h_misc;
+    uint4* h_pts;
+    uint32_t* h_coords;
+    uint4* h_vox;
+    uint32_t* h_didx;
+    uint4* h_ddata;
+};
+hipError_t launch_download(const DlArgs& d, hipStream_t s);
 
 // gdf_voxelize_runs: nsrc received segments, source q's points from point_base[q] and runs from
 // run_base[q] (q <= nsrc: the totals)
