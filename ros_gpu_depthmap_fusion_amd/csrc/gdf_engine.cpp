@@ -358,6 +358,8 @@ struct Slot {
         }
     } h_pts, h_coords, h_vox, h_delta, h_miscpf;
     bool pf_valid = false;          // this slot's last frame wrote its downloads (k_download)
+    hipStream_t dl_aux = nullptr;   // k_download of the points / coords, after the compaction,
+    hipEvent_t dl_ev = nullptr;     // overlapping the voxelize (an event after the compaction)
     DevBuf d_didx, d_ddata;         // the grid delta of this slot's single-frame update
     bool delta_valid = false;
     uint32_t delta_ticket = 0;      // ... and that update's sequence number
@@ -493,6 +495,9 @@ struct gdf_engine {
     // k_download into the slot's pinned mirrors (the next download_frame waits once)
     bool dl_prefetch = false;
     bool dl_prefetch_allowed = !getenv("GDF_NO_DL_PREFETCH");
+    // tuning knob GDF_DL_FORK: the points / coords part on a second stream right after the
+    // compaction (direct launches) instead of in the chain's last kernel (graph replays)
+    bool dl_fork = getenv("GDF_DL_FORK") != nullptr;
     bool mirror_valid = false;
     uint32_t mirror_ticket = 0, mirror_gen = 0;
 
@@ -1546,12 +1551,33 @@ bool same_key(const FrameArgs& a, const VoxelizeArgs& v, const FrameArgs& ka, co
 // direct launches, or the slot's captured graph when the launch arguments repeat
 // gdf_download_frame prefetch: a single frame's downloads written by k_download at the end of
 // its launch chain (after the voxelize and the grid update it carries)
-void prefetch_downloads(gdf_engine* e, hipStream_t st) {
+bool prefetch_on(const gdf_engine* e) { return e->dl_prefetch && e->nframes == 1 && !e->user_stream; }
+bool prefetch_fork(const gdf_engine* e) { return prefetch_on(e) && e->dl_fork; }
+
+// parts: DL_POINTS on the slot's aux stream right after the compaction (overlaps the voxelize),
+// the rest at the end of the chain
+void prefetch_downloads(gdf_engine* e, hipStream_t st, uint32_t parts) {
     Slot& q = e->sl();
-    q.pf_valid = false;
-    if (!e->dl_prefetch || e->nframes != 1 || e->user_stream) return;
+    if (parts & DL_MISC) q.pf_valid = false;
+    if (!prefetch_on(e)) return;
+    if (parts == DL_POINTS) {  // (forked: its own stream after the compaction)
+        if (!q.dl_aux) {
+            HIPCHK(hipStreamCreateWithFlags(&q.dl_aux, hipStreamNonBlocking));
+            HIPCHK(hipEventCreateWithFlags(&q.dl_ev, hipEventDisableTiming));
+        }
+        HIPCHK(hipEventRecord(q.dl_ev, st));
+        HIPCHK(hipStreamWaitEvent(q.dl_aux, q.dl_ev, 0));
+        st = q.dl_aux;
+    }
     const uint32_t cap = std::max<uint32_t>(q.n_total, 1);
     const uint32_t dcap = q.delta_valid ? (uint32_t)((mark_words(e) + 3) / 4 * 4) : 0u;
+    // a mirror about to grow is freed first: no earlier k_download may still write it
+    if (q.h_pts.bytes < (size_t)cap * 16 || q.h_coords.bytes < (size_t)cap * 4 ||
+        q.h_vox.bytes < (size_t)cap * 16 || q.h_delta.bytes < (size_t)std::max<uint32_t>(dcap, 4) * 36 ||
+        q.h_miscpf.bytes < kMiscWords * 4) {
+        HIPCHK(hipStreamSynchronize(q.stream()));
+        if (q.dl_aux) HIPCHK(hipStreamSynchronize(q.dl_aux));
+    }
     DlArgs d{};
     d.misc = q.d_misc.as<uint32_t>();
     d.misc_words = kMiscWords;
@@ -1569,14 +1595,15 @@ void prefetch_downloads(gdf_engine* e, hipStream_t st) {
     d.h_misc = static_cast<uint32_t*>(q.h_miscpf.ensure(kMiscWords * 4));
     d.h_pts = static_cast<uint4*>(q.h_pts.ensure((size_t)cap * 16));
     d.h_coords = static_cast<uint32_t*>(q.h_coords.ensure((size_t)cap * 4));
-    d.h_vox = static_cast<uint4*>(q.h_vox.ensure((size_t)std::max<uint32_t>(d.vox_cap, 1) * 16));
+    d.h_vox = static_cast<uint4*>(q.h_vox.ensure((size_t)cap * 16));
     uint8_t* hd = static_cast<uint8_t*>(q.h_delta.ensure((size_t)std::max<uint32_t>(dcap, 4) * 36));
     if (!d.h_misc || !d.h_pts || !d.h_coords || !d.h_vox || !hd)
         fail(GDF_ERR_NOMEM, "pinned download mirror allocation failed");
     d.h_didx = reinterpret_cast<uint32_t*>(hd);
     d.h_ddata = reinterpret_cast<uint4*>(hd + (size_t)dcap * 4);
+    d.parts = parts;
     HIPCHK(launch_download(d, st));
-    q.pf_valid = true;
+    if (parts & DL_MISC) q.pf_valid = true;
 }
 
 void run_fused_frame(gdf_engine* e, int average, uint32_t lifetime) {
@@ -1592,8 +1619,9 @@ void run_fused_frame(gdf_engine* e, int average, uint32_t lifetime) {
         occupancy_grid(e, lifetime, e->s());
         return;
     }
+    // (a prefetching frame forks its points download after the compaction: direct launches)
     const bool eligible = e->use_graphs && !e->profiling && !e->debug && a.ncams <= kArgCams &&
-                          !e->user_stream && a.total_segs;
+                          !e->user_stream && a.total_segs && !prefetch_fork(e);
     hipStream_t st = e->s();
     Slot::GraphEntry* hit = nullptr;
     if (eligible)
@@ -1674,10 +1702,11 @@ void run_fused_frame(gdf_engine* e, int average, uint32_t lifetime) {
         }
         if (e->profiling) e->timed(GDF_KERNEL_EVENT_FLOOR, [] {});
         e->timed(GDF_KERNEL_FRAME, [&] { HIPCHK(launch_frame(a, st, e->hook_ptr())); });
+        if (prefetch_fork(e)) prefetch_downloads(e, st, DL_POINTS);
         e->timed(GDF_KERNEL_VOXELIZE, [&] { HIPCHK(launch_voxelize(v, st, e->hook_ptr())); });
     }
     voxelize_launched(e, (int)lifetime);
-    prefetch_downloads(e, st);
+    prefetch_downloads(e, st, DL_MISC | DL_VOX | DL_DELTA | (prefetch_fork(e) ? 0u : DL_POINTS));
 }
 
 void occupancy_grid(gdf_engine* e, uint32_t lifetime, hipStream_t st) {  // fusion.cpp:1757-1823
@@ -1837,6 +1866,11 @@ int gdf_destroy(gdf_engine* e) {
     for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
     for (Slot& sl : e->slots) {
         sl.graph.reset();
+        if (sl.dl_aux) {
+            (void)hipStreamSynchronize(sl.dl_aux);
+            (void)hipStreamDestroy(sl.dl_aux);
+        }
+        if (sl.dl_ev) (void)hipEventDestroy(sl.dl_ev);
         if (sl.h_misc) (void)hipHostFree(sl.h_misc);
         if (sl.h_stage) (void)hipHostFree(sl.h_stage);
         if (sl.h2d_done) (void)hipEventDestroy(sl.h2d_done);
@@ -2199,8 +2233,9 @@ int gdf_download_frame(gdf_engine* e, uint32_t what, gdf_host_frame* out) {
         if ((what & GDF_DL_GRID) && (!e->grid_set || !e->invoked_once))
             fail(GDF_ERR_STATE, "download_frame: no voxelOccupancyGrid has run");
         if (what & GDF_DL_GRID) sync_all(e);  // grid updates may still run on another slot's stream
-        if (q.pf_valid) {  // k_download wrote everything: the one wait
+        if (q.pf_valid) {  // k_download wrote everything: the one wait (and the aux stream's)
             e->sync();
+            if (q.dl_aux) HIPCHK(hipStreamSynchronize(q.dl_aux));
             q.pf_valid = false;
             const uint32_t* hm = static_cast<const uint32_t*>(q.h_miscpf.p);
             if (hm[kErr]) {

@@ -4357,10 +4357,11 @@ hipError_t launch_partition(const float4* pts, const uint32_t* keys, const uint3
 // voxelized | delta indices | delta data], 16-B stores where the items are 16 B (the host link
 // takes coalesced wave stores at DMA-like rates).
 __global__ __launch_bounds__(256) void k_download(DlArgs d) {
-    const uint32_t n = min(d.misc[d.i_count], d.pts_cap);
-    const uint32_t nv = min(d.misc[d.i_vox], d.vox_cap);
-    const uint32_t nd = d.delta_cap ? min(d.misc[d.i_delta], d.delta_cap) : 0u;
-    const uint64_t e0 = d.misc_words, e1 = e0 + n, e2 = e1 + n, e3 = e2 + nv, e4 = e3 + nd,
+    const uint32_t n = (d.parts & DL_POINTS) ? min(d.misc[d.i_count], d.pts_cap) : 0u;
+    const uint32_t nv = (d.parts & DL_VOX) ? min(d.misc[d.i_vox], d.vox_cap) : 0u;
+    const uint32_t nd = (d.parts & DL_DELTA) && d.delta_cap ? min(d.misc[d.i_delta], d.delta_cap) : 0u;
+    const uint64_t e0 = (d.parts & DL_MISC) ? d.misc_words : 0u, e1 = e0 + n, e2 = e1 + n,
+                   e3 = e2 + nv, e4 = e3 + nd,
                    e5 = e4 + 2ull * nd;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < e5; i += stride) {

@@ -203,7 +203,9 @@ struct DlArgs {
     uint4* h_vox;
     uint32_t* h_didx;
     uint4* h_ddata;
+    uint32_t parts;  // DL_* bits: which of the above this launch writes
 };
+enum : uint32_t { DL_MISC = 1, DL_POINTS = 2, DL_VOX = 4, DL_DELTA = 8 };
 hipError_t launch_download(const DlArgs& d, hipStream_t s);
 
 // gdf_voxelize_runs: nsrc received segments, source q's points from point_base[q] and runs from
