@@ -394,6 +394,16 @@ int gdf_voxelize_points(gdf_engine* engine, const float* points_device,
 int gdf_partition_runs(gdf_engine* engine, uint32_t nparts, float* send_points_device,
                        uint32_t* send_run_keys_device, uint32_t* send_run_starts_device,
                        uint32_t capacity, uint32_t* part_counts_device);
+/* gdf_partition_runs' send lists written by the next frame's compaction itself: arm before a
+ * gdf_process_frame with defer_voxelize (capacity >= that frame's pixels + selected points); that
+ * frame's k_mask / k_emit count and place every kept point and run per part (no compaction-order
+ * points, keys or runs: the frame's point / coords downloads are not available), or - frames the
+ * fused kernels do not cover (rollbuffer points, other segment shapes) - compact and then
+ * partition.  The same send lists and part_counts either way; disarmed after that frame
+ * (nparts = 0 disarms explicitly). */
+int gdf_set_emit_partition(gdf_engine* engine, uint32_t nparts, float* send_points_device,
+                           uint32_t* send_run_keys_device, uint32_t* send_run_starts_device,
+                           uint32_t capacity, uint32_t* part_counts_device);
 int gdf_voxelize_runs(gdf_engine* engine, const float* points_device,
                       const uint32_t* run_keys_device, uint32_t* run_starts_device,
                       uint32_t nsources, const uint32_t* point_base, const uint32_t* run_base,

@@ -186,6 +186,17 @@ struct FrameArgs {
     uint32_t* grp_done;         // [groups] arrival counters (self-resetting)
     uint32_t* grp_tot;          // [2 * groups]
     int32_t mask_packed;        // k_mask_px<2>: both pixels of a thread in packed f32 ops
+    // emit partition (multi-GPU fused cloud, gdf_set_emit_partition): the compaction writes the
+    // key-range partition itself - k_mask_px counts each segment's kept points and runs per part
+    // (seg_counts [2 * nparts][total_segs], one scan), k_emit_px2 writes every kept point and run
+    // record straight to its part: points part-major, run keys (with the frame) and run starts
+    // relative to the part's first point; no compaction-order points, keys or runs
+    uint32_t nparts;            // 0: off
+    uint64_t part_ncells;       // part of voxel key k: floor(k * nparts / part_ncells)
+    float4* part_pts;
+    uint32_t* part_run_keys;
+    uint32_t* part_run_starts;
+    uint32_t* part_counts;      // [2 * nparts]: points, then runs per part (device)
 };
 static_assert(sizeof(FrameArgs) <= 4096, "kernel arguments are limited to 4 KiB");
 

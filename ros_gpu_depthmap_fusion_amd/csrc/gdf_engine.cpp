@@ -358,6 +358,7 @@ struct Slot {
         }
     } h_pts, h_coords, h_vox, h_delta, h_miscpf;
     bool pf_valid = false;          // this slot's last frame wrote its downloads (k_download)
+    bool part_emitted = false;      // this slot's last compaction wrote the emit partition
     hipStream_t dl_aux = nullptr;   // k_download of the points / coords, after the compaction,
     hipEvent_t dl_ev = nullptr;     // overlapping the voxelize (an event after the compaction)
     DevBuf d_didx, d_ddata;         // the grid delta of this slot's single-frame update
@@ -494,6 +495,13 @@ struct gdf_engine {
     // after a single-frame gdf_download_frame of points / coords / voxels: single frames end with
     // k_download into the slot's pinned mirrors (the next download_frame waits once)
     bool dl_prefetch = false;
+    // gdf_set_emit_partition: the next deferred frame's send lists (device), armed until used
+    struct EmitPart {
+        uint32_t nparts = 0, cap = 0;
+        float* pts = nullptr;
+        uint32_t *run_keys = nullptr, *run_starts = nullptr, *counts = nullptr;
+    } epart;
+    bool emit_part = getenv("GDF_EMIT_PART") != nullptr;  // (else: compaction, then the partition pass)
     bool dl_prefetch_allowed = !getenv("GDF_NO_DL_PREFETCH");
     // tuning knob GDF_DL_FORK: the points / coords part on a second stream right after the
     // compaction (direct launches) instead of in the chain's last kernel (graph replays)
@@ -1347,6 +1355,34 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel, bool compaction_marks = fa
     a.nframes = e->nframes;
     a.frame_shift = e->nframes > 1 ? e->key_bits : 0u;
     a.mark_words = mark_words(e);
+    if (fused_voxel && compaction_marks && e->epart.nparts && e->emit_part && !a.sel_tiles &&
+        a.total_segs && !e->debug) {
+        // the compaction writes the key-range partition itself (k_mask_px + k_emit_px2 only;
+        // anything else compacts, then partitions: gdf_process_frame)
+        FrameArgs t = a;
+        t.run_mode = 1;
+        t.key_hist = nullptr;
+        t.fused_prefix = 0;
+        t.grp_done = t.grp_tot = nullptr;
+        if (emit_partition_kernels(t)) {
+            Slot& q = e->sl();
+            const uint32_t segs = std::max<uint32_t>(a.total_segs, 1);
+            const uint32_t P = e->epart.nparts;
+            q.d_tcounts.ensure((size_t)segs * 2 * P * 4);
+            q.d_toffsets.ensure(seg_offsets_words(2 * P * segs) * 4);
+            q.d_wruns.ensure((size_t)segs * 16 * 4);
+            t.seg_counts = q.d_tcounts.as<uint32_t>();
+            t.seg_offsets = q.d_toffsets.as<uint32_t>();
+            t.wave_runs = q.d_wruns.as<uint32_t>();
+            t.nparts = P;
+            t.part_ncells = e->ncells;
+            t.part_pts = reinterpret_cast<float4*>(e->epart.pts);
+            t.part_run_keys = e->epart.run_keys;
+            t.part_run_starts = e->epart.run_starts;
+            t.part_counts = e->epart.counts;
+            a = t;
+        }
+    }
     e->sl().nframes = e->nframes;
     e->sl().snap_valid = false;  // (set by this batch's grid update when it keeps the frames' grids)
     if (e->nframes > 1) {
@@ -1368,9 +1404,14 @@ void frame_launched(gdf_engine* e, bool fused_voxel, bool key_hist, bool runs = 
 void run_frame(gdf_engine* e, bool fused_voxel, bool compaction_marks = false) {
     e->sl().pf_valid = false;
     const FrameArgs a = frame_args(e, fused_voxel, compaction_marks);
+    e->sl().part_emitted = a.nparts != 0;
     if (e->profiling) e->timed(GDF_KERNEL_EVENT_FLOOR, [] {});  // calibrates the event overhead
     e->timed(GDF_KERNEL_FRAME, [&] { HIPCHK(launch_frame(a, e->s(), e->hook_ptr())); });
     frame_launched(e, fused_voxel, a.key_hist != nullptr, a.run_mode != 0);
+    if (a.nparts) {  // (the points went to the send lists only: no compaction-order outputs)
+        e->sl().coords_valid = false;
+        e->sl().runs_valid = false;
+    }
 }
 
 void compute_voxel_coords(gdf_engine* e, const float* lo, const float* hi, const float* cs) {
@@ -1762,6 +1803,30 @@ int guarded(gdf_engine* e, F&& f) {
             return GDF_ERR_ARG;                                             \
         }                                                                   \
     } while (0)
+
+void partition_runs(gdf_engine* e, uint32_t nparts, float* send_pts, uint32_t* send_run_keys,
+                    uint32_t* send_run_starts, uint32_t capacity, uint32_t* part_counts) {
+    {
+        Slot& q = e->sl();
+        if (!e->grid_set || !q.coords_valid) fail(GDF_ERR_STATE, "partition needs the voxel keys of a frame");
+        if (nparts == 0 || nparts > kMaxParts) fail(GDF_ERR_ARG, "partition: 1..16 parts");
+        if (!send_pts || !send_run_keys || !send_run_starts || !part_counts)
+            fail(GDF_ERR_ARG, "partition: null buffer");
+        if (capacity < q.n_total) fail(GDF_ERR_CAPACITY, "partition: send buffers smaller than the frame");
+        ensure_misc(e);
+        const uint32_t nmax = std::max<uint32_t>(q.n_total, 1);
+        const uint32_t m = 2 * nparts * std::max<uint32_t>(part_tiles(nmax), 1u);
+        q.d_pcnt.ensure((size_t)m * 4);
+        q.d_poff.ensure(seg_offsets_words(m) * 4);
+        HIPCHK(launch_partition(q.d_pts.as<float4>(), q.d_coords.as<uint32_t>(),
+                                q.d_misc.as<uint32_t>() + kCount, nmax, nparts, e->ncells,
+                                q.d_pcnt.as<uint32_t>(), q.d_poff.as<uint32_t>(),
+                                q.d_misc.as<uint32_t>() + kPartTotal,
+                                reinterpret_cast<float4*>(send_pts), nullptr, part_counts, e->s(),
+                                q.nframes > 1 ? q.d_fstart.as<uint32_t>() : nullptr, q.nframes,
+                                q.nframes > 1 ? e->key_bits : 0u, send_run_keys, send_run_starts));
+    }
+}
 
 }  // namespace
 
@@ -2438,7 +2503,13 @@ int gdf_process_frame(gdf_engine* e, const gdf_frame_params* p, gdf_frame_result
             if (sort_bits(e) > 32) fail(GDF_ERR_ARG, "voxel key + frame index exceed 32 bits");
             widen_if_needed(e, p->occupancy_lifetime, e->s());  // before marks are consumed
             if (p->defer_voxelize) {  // keys + marks only (multi-GPU fused cloud)
+                const gdf_engine::EmitPart ep = e->epart;
+                if (ep.nparts && ep.cap < e->sl().n_total)
+                    fail(GDF_ERR_CAPACITY, "emit partition: send lists smaller than the frame");
                 run_frame(e, true, true);
+                e->epart = gdf_engine::EmitPart{};  // (one frame)
+                if (ep.nparts && !e->sl().part_emitted)  // the compaction could not: a pass
+                    partition_runs(e, ep.nparts, ep.pts, ep.run_keys, ep.run_starts, ep.cap, ep.counts);
                 if (!p->defer_occupancy_grid) occupancy_grid(e, p->occupancy_lifetime, e->s());
             } else if (!p->defer_occupancy_grid && e->grid_mode == 0) {
                 run_fused_frame(e, p->voxel_average, p->occupancy_lifetime);
@@ -2518,30 +2589,30 @@ int gdf_partition_points(gdf_engine* e, uint32_t nparts, float* send_pts, uint32
     });
 }
 
+int gdf_set_emit_partition(gdf_engine* e, uint32_t nparts, float* send_pts, uint32_t* send_run_keys,
+                           uint32_t* send_run_starts, uint32_t capacity, uint32_t* part_counts) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        if (nparts > kMaxParts) fail(GDF_ERR_ARG, "emit partition: 0..16 parts");
+        if (nparts && (!send_pts || !send_run_keys || !send_run_starts || !part_counts))
+            fail(GDF_ERR_ARG, "emit partition: null buffer");
+        e->epart.nparts = nparts;
+        e->epart.cap = capacity;
+        e->epart.pts = send_pts;
+        e->epart.run_keys = send_run_keys;
+        e->epart.run_starts = send_run_starts;
+        e->epart.counts = part_counts;
+    });
+}
+
 int gdf_partition_runs(gdf_engine* e, uint32_t nparts, float* send_pts, uint32_t* send_run_keys,
                        uint32_t* send_run_starts, uint32_t capacity, uint32_t* part_counts) {
     ENGINE_OR_FAIL(e);
     return guarded(e, [&] {
-        Slot& q = e->sl();
-        if (!e->grid_set || !q.coords_valid) fail(GDF_ERR_STATE, "partition needs the voxel keys of a frame");
-        if (nparts == 0 || nparts > kMaxParts) fail(GDF_ERR_ARG, "partition: 1..16 parts");
-        if (!send_pts || !send_run_keys || !send_run_starts || !part_counts)
-            fail(GDF_ERR_ARG, "partition: null buffer");
-        if (capacity < q.n_total) fail(GDF_ERR_CAPACITY, "partition: send buffers smaller than the frame");
-        ensure_misc(e);
-        const uint32_t nmax = std::max<uint32_t>(q.n_total, 1);
-        const uint32_t m = 2 * nparts * std::max<uint32_t>(part_tiles(nmax), 1u);
-        q.d_pcnt.ensure((size_t)m * 4);
-        q.d_poff.ensure(seg_offsets_words(m) * 4);
-        HIPCHK(launch_partition(q.d_pts.as<float4>(), q.d_coords.as<uint32_t>(),
-                                q.d_misc.as<uint32_t>() + kCount, nmax, nparts, e->ncells,
-                                q.d_pcnt.as<uint32_t>(), q.d_poff.as<uint32_t>(),
-                                q.d_misc.as<uint32_t>() + kPartTotal,
-                                reinterpret_cast<float4*>(send_pts), nullptr, part_counts, e->s(),
-                                q.nframes > 1 ? q.d_fstart.as<uint32_t>() : nullptr, q.nframes,
-                                q.nframes > 1 ? e->key_bits : 0u, send_run_keys, send_run_starts));
+        partition_runs(e, nparts, send_pts, send_run_keys, send_run_starts, capacity, part_counts);
     });
 }
+
 
 int gdf_voxelize_runs(gdf_engine* e, const float* pts, const uint32_t* run_keys,
                       uint32_t* run_starts, uint32_t nsources, const uint32_t* point_base,

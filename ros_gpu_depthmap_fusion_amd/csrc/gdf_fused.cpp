@@ -222,30 +222,43 @@ void fused_start(gdf_fused* f, const uint16_t* const* depth, uint32_t B, const g
     q.defer_occupancy_grid = 1;
     q.defer_voxelize = 1;
     if (R != W - 1 || B > 1) q.move_transform_available = 0;  // the rollbuffer: last rank only
+    // the send lists, written by the compaction itself (gdf_set_emit_partition): sized for the
+    // step's pixels (+ halo) plus, on the rollbuffer rank, every point the window can select
+    uint32_t* cnt = S.cnt.ensure<uint32_t>((size_t)2 * W * 4, st);
+    uint32_t* cntall = S.cntall.ensure<uint32_t>((size_t)2 * W * W * 4, st);
+    size_t want = (size_t)B * c.width * c.height + (halo && R > 0 ? B * (size_t)f->Lmax : 0u);
+    if (R == W - 1 && B == 1 && p->move_transform_available) {  // + the window after the ingest
+        gdf_rollbuffer_state rs{};
+        gdfchk(gdf_get_rollbuffer_state(e, &rs));
+        uint32_t col = 0;
+        gdfchk(gdf_num_collected_point_sequence_points(e, &col));
+        want += (size_t)rs.num_points + col;
+    }
+    auto arm = [&](size_t cap) {
+        S.sp.ensure<float>(cap * 16, st);
+        S.srk.ensure<uint32_t>(cap * 4, st);
+        S.srs.ensure<uint32_t>(cap * 4, st);
+        const uint32_t have = (uint32_t)std::min<size_t>({S.sp.cap / 16, S.srk.cap / 4, S.srs.cap / 4});
+        gdfchk(gdf_set_emit_partition(e, W, S.sp.as<float>(), S.srk.as<uint32_t>(),
+                                      S.srs.as<uint32_t>(), have, cnt));
+    };
+    arm(std::max<size_t>(want, 1));
     gdf_frame_result res{};
     gdfchk(gdf_process_frame(e, &q, &res));
     uint32_t g[3];
     uint64_t ncells = 0;
     gdfchk(gdf_get_grid_size(e, g, &ncells));
     const uint64_t words = (ncells + 31) / 32;
-    const uint32_t n_total = std::max<uint32_t>(res.num_points_total, 1);
     uint32_t* local = S.local.ensure<uint32_t>(B * words * 4, st);
     uint32_t* gathered = S.gathered.ensure<uint32_t>((size_t)W * B * words * 4, st);
-    float* sp = S.sp.ensure<float>((size_t)n_total * 16, st);
-    uint32_t* srk = S.srk.ensure<uint32_t>((size_t)n_total * 4, st);
-    uint32_t* srs = S.srs.ensure<uint32_t>((size_t)n_total * 4, st);
-    uint32_t* cnt = S.cnt.ensure<uint32_t>((size_t)2 * W * 4, st);
-    uint32_t* cntall = S.cntall.ensure<uint32_t>((size_t)2 * W * W * 4, st);
     // occupancy union: the B frames' marks of every rank, one batched grid update
     gdfchk(gdf_take_occupancy_marks(e, local, B * words));
     ncclchk(r, r.all_gather(local, gathered, B * words, ncclUint32, f->comm_a, st),
             "ncclAllGather(marks)");
     gdfchk(gdf_voxel_occupancy_grid_batch(e, gathered, words, W, B, words, B * words,
                                           q.occupancy_lifetime));
-    // key-range partition into points + runs of equal keys; every rank's split sizes to pinned
-    // memory (no wait here)
-    const uint32_t cap = (uint32_t)std::min<size_t>({S.sp.cap / 16, S.srk.cap / 4, S.srs.cap / 4});
-    gdfchk(gdf_partition_runs(e, W, sp, srk, srs, cap, cnt));
+    // every rank's split sizes (the partition's, written with the compaction) to pinned memory
+    // (no wait here)
     ncclchk(r, r.all_gather(cnt, cntall, 2 * W, ncclUint32, f->comm_a, st), "ncclAllGather(counts)");
     hipchk(hipMemcpyAsync(S.host, cntall, (size_t)2 * W * W * 4, hipMemcpyDeviceToHost, st),
            "hipMemcpyAsync(counts)");

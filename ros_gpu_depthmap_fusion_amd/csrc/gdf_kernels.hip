@@ -1137,6 +1137,30 @@ __device__ __forceinline__ void depth_bits_px2(const FrameArgs& a, const CamDesc
     }
 }
 
+// emit partition: the part (key range) of voxel key k
+__device__ __forceinline__ uint32_t emit_part_of(uint32_t key, uint32_t nparts, uint64_t ncells) {
+    const uint64_t p = (uint64_t)key * nparts / ncells;
+    return p < nparts ? (uint32_t)p : nparts - 1u;
+}
+
+// the lanes of `m` whose part equals this lane's, per distinct part of the wave (wave-uniform
+// loop, one iteration per part present - usually one or two); cb(part, lanes) once per part
+template <class CB>
+__device__ __forceinline__ unsigned long long part_lanes(unsigned long long m, bool in, uint32_t part,
+                                                         const CB& cb) {
+    unsigned long long mine = 0;
+    unsigned long long rem = m;
+    while (rem) {
+        const int l = __ffsll((long long)rem) - 1;
+        const uint32_t p = __shfl(part, l, 64);
+        const unsigned long long pm = __ballot(in && part == p) & m;
+        if (in && part == p) mine = pm;
+        cb(p, pm);
+        rem &= ~pm;
+    }
+    return mine;
+}
+
 // k_mask with PX pixels per thread (x + j * 256 / PX) for 256-pixel segments at F = 4 without
 // rot45: 256 / PX threads per segment, the same band in LDS, the same outputs (validity word
 // w + j * waves from pixel j of wave w; counts, runs, run-key histogram).  No debug stage bits
@@ -1154,8 +1178,11 @@ __global__ __launch_bounds__(SEGW / PX) void k_mask_px(FrameArgs a) {
     __shared__ uint32_t s_cnt[NWORDS];
     __shared__ uint32_t s_rcnt[NWORDS];
     __shared__ uint32_t s_hist[4 * 256];
+    __shared__ uint32_t s_pc[2][NWORDS][kMaxParts];  // emit partition: points, runs per (word, part)
     extern __shared__ uint4 s_dyn[];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (a.nparts)
+        for (uint32_t j = threadIdx.x; j < 2u * NWORDS * kMaxParts; j += NT) (&s_pc[0][0][0])[j] = 0u;
     const uint32_t n = gridDim.x, q8 = n / 8, r8 = n % 8, xcd = blockIdx.x % 8;
     const uint32_t s = xcd * q8 + min(xcd, r8) + blockIdx.x / 8;
     if (a.grid_seq_out && blockIdx.x == 0 && threadIdx.x == 0) *a.grid_seq_out = a.grid_seq;
@@ -1311,10 +1338,28 @@ __global__ __launch_bounds__(SEGW / PX) void k_mask_px(FrameArgs a) {
             if (leader && a.key_hist)
                 for (uint32_t p = 0; p < a.npasses; ++p)
                     atomicAdd(&s_hist[p * 256 + radix_digit(rkey[j], p, a.npasses)], 1u);
+            if (a.nparts) {  // this word's kept points and runs per part
+                const bool kept = (bits[j] & 4u) != 0u;
+                const uint32_t vk = a.frame_shift ? rkey[j] & ((1u << a.frame_shift) - 1u) : rkey[j];
+                const uint32_t part = kept ? emit_part_of(vk, a.nparts, a.part_ncells) : 0u;
+                part_lanes(m, kept, part, [&](uint32_t p, unsigned long long pm) {
+                    if (lane == 0) {
+                        s_pc[0][word][p] = (uint32_t)__popcll(pm);
+                        s_pc[1][word][p] = (uint32_t)__popcll(pm & lm);
+                    }
+                });
+            }
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (a.nparts) {  // counts [points of part 0..P-1 | runs of part 0..P-1][segment]
+        if (threadIdx.x < 2u * a.nparts) {
+            const uint32_t kind = threadIdx.x / a.nparts, p = threadIdx.x % a.nparts;
+            uint32_t c = 0;
+            for (int w = 0; w < NWORDS; ++w) c += s_pc[kind][w][p];
+            G(a.seg_counts)[(size_t)threadIdx.x * a.total_segs + s] = c;
+        }
+    } else if (threadIdx.x == 0) {
         uint32_t tt = 0, r = 0;
         for (int w = 0; w < NWORDS; ++w) tt += s_cnt[w];
         publish_count(a.seg_counts + s, tt);
@@ -1655,6 +1700,116 @@ __global__ __launch_bounds__(1024) void k_emit(FrameArgs a) {
 // segment, k_mask_px's layout: pixel j of wave w is validity word w + 2j): the block's scalar
 // work (camera lookup, counts and run prefixes of the segment's words) is shared by twice the
 // pixels per wave.  Same outputs in the same order as k_emit.
+// k_emit_px2 under the emit partition (FrameArgs::nparts): the same points, keys and marks; each
+// kept point goes to its part (the segment's offset of the part from the one scan over [points
+// per part | runs per part][segment], then the part's earlier words, then its rank among the
+// word's lanes of that part), and each run (a kept pixel whose key differs from the kept pixel
+// before it in the word) to its part's run list.
+template <int SEGW>
+__device__ __forceinline__ void emit_px2_parts(const FrameArgs& a, uint32_t* s_mark) {
+    constexpr int NT = SEGW / 2, NW = NT / 64, NWORDS = SEGW / 64;
+    __shared__ uint32_t s_pc[2][NWORDS][kMaxParts];
+    __shared__ uint32_t s_off[2][kMaxParts], s_first[kMaxParts], s_tot;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t s = blockIdx.x, P = a.nparts, TS = a.total_segs;
+    for (uint32_t j = threadIdx.x; j < 2u * NWORDS * kMaxParts; j += NT) (&s_pc[0][0][0])[j] = 0u;
+    if (threadIdx.x < 2u * P) {
+        const uint32_t kind = threadIdx.x / P, p = threadIdx.x % P;
+        s_off[kind][p] = G(a.seg_offsets)[(size_t)threadIdx.x * TS + s];
+        if (kind == 0) s_first[p] = G(a.seg_offsets)[(size_t)p * TS];
+    }
+    if (threadIdx.x == 0) s_tot = G(a.seg_offsets)[(size_t)P * TS];  // (the kept points)
+    __syncthreads();  // (the zeroed counters and the mark cache before any wave writes them)
+    const gptr<const CamDesc> cams = G(cam_table(a));
+    const uint32_t i = threadIdx.x;
+    int k = 0;
+    for (int c = 0; c < a.ncams; ++c)
+        if (cams[c].emit && s >= cams[c].seg0 && s < cams[c].seg0 + cams[c].nseg) k = c;
+    k = __builtin_amdgcn_readfirstlane(k);
+    const uint32_t j = s - cams[k].seg0;
+    const uint32_t y = j / cams[k].nchunk;
+    const uint32_t x0 = (j - y * cams[k].nchunk) * cams[k].segw;
+    const uint32_t len = min(cams[k].segw, cams[k].W - x0);
+    uint64_t m[2];
+    uint32_t dval[2] = {0u, 0u};
+    float xnv[2] = {0.0f, 0.0f};
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        m[q] = G(a.vbits)[(size_t)s * 16 + wid + NW * q];
+        const uint32_t ii = i + (uint32_t)NT * q;
+        if (ii < len) {
+            dval[q] = G(cams[k].depth)[y * cams[k].W + x0 + ii];
+            xnv[q] = G(cams[k].xn)[x0 + ii];
+        }
+    }
+    const float ynv = G(cams[k].yn)[y];
+    const uint32_t fr = cams[k].frame;
+    const unsigned long long ltm = lanemask_lt();
+    const f2v zz2 = f2((float)dval[0], (float)dval[1]) * f2(cams[k].scale, cams[k].scale);
+    const f2v px2 = f2(xnv[0], xnv[1]) * zz2, py2 = f2(ynv, ynv) * zz2, pz2 = zz2;
+    const f2v wx2 = mrow2(cams[k].Tw + 0, px2, py2, pz2), wy2 = mrow2(cams[k].Tw + 4, px2, py2, pz2);
+    const f2v wz2 = mrow2(cams[k].Tw + 8, px2, py2, pz2), ww2 = mrow2(cams[k].Tw + 12, px2, py2, pz2);
+    uint32_t key2[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
+    if (m[0] | m[1]) voxel_key2(wx2, wy2, wz2, a.vlo, a.vcs, a.vrcs, a.gmax, a.gs, key2[0], key2[1]);
+    bool valid[2], lead[2];
+    uint32_t part[2];
+    unsigned long long mine[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const uint32_t word = (uint32_t)wid + NW * q;
+        valid[q] = i + (uint32_t)NT * q < len && ((m[q] >> lane) & 1ull);
+        const uint32_t key = valid[q] ? key2[q] : 0xFFFFFFFFu;
+        const unsigned long long below = m[q] & ltm;
+        const int prev = below ? 63 - __clzll((long long)below) : -1;
+        const uint32_t pkey = __shfl(key, prev < 0 ? 0 : prev, 64);
+        lead[q] = valid[q] && (prev < 0 || pkey != key);
+        const unsigned long long lm = __ballot(lead[q]);
+        part[q] = valid[q] ? emit_part_of(key2[q], P, a.part_ncells) : 0u;
+        mine[q] = part_lanes(m[q], valid[q], part[q], [&](uint32_t p, unsigned long long pm) {
+            if (lane == 0) {
+                s_pc[0][word][p] = (uint32_t)__popcll(pm);
+                s_pc[1][word][p] = (uint32_t)__popcll(pm & lm);
+            }
+        });
+        mine[q] &= valid[q] ? ~0ull : 0ull;
+        // (the leaders among this lane's part: runs ranked within the word)
+        if (!valid[q]) lead[q] = false;
+        mark_and_count(a, a.marks ? a.marks + (size_t)fr * a.mark_words : nullptr, valid[q], key,
+                       key | (fr << a.frame_shift), nullptr, s_mark);
+        (void)lm;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const uint32_t word = (uint32_t)wid + NW * q;
+        const unsigned long long lm = __ballot(lead[q]);
+        if (!valid[q]) continue;
+        const uint32_t p = part[q];
+        uint32_t wpre = 0, rwpre = 0;
+        for (uint32_t w = 0; w < word; ++w) {
+            wpre += s_pc[0][w][p];
+            rwpre += s_pc[1][w][p];
+        }
+        const uint32_t pos = s_off[0][p] + wpre + (uint32_t)__popcll(mine[q] & ltm);
+        const float4 w4 = q == 0 ? make_float4(wx2.x, wy2.x, wz2.x, ww2.x)
+                                 : make_float4(wx2.y, wy2.y, wz2.y, ww2.y);
+        gst4(a.part_pts, pos, w4);
+        if (lead[q]) {
+            const uint32_t rpos = s_off[1][p] - s_tot + rwpre + (uint32_t)__popcll(mine[q] & lm & ltm);
+            G(a.part_run_keys)[rpos] = key2[q] | (fr << a.frame_shift);
+            G(a.part_run_starts)[rpos] = pos - s_first[p];
+        }
+    }
+    if (s == gridDim.x - 1 && threadIdx.x < 2u * P) {  // the parts' sizes from the scan
+        const uint32_t kind = threadIdx.x / P, p = threadIdx.x % P;
+        const uint32_t a0 = G(a.seg_offsets)[(size_t)threadIdx.x * TS];
+        const uint32_t a1 = threadIdx.x + 1 < 2u * P ? G(a.seg_offsets)[(size_t)(threadIdx.x + 1) * TS]
+                                                     : *G(a.scan_total);
+        G(a.part_counts)[kind * P + p] = a1 - a0;
+        if (threadIdx.x == 0) *G(a.out_count) = s_tot;
+    }
+}
+
 template <int SEGW>
 __global__ __launch_bounds__(SEGW / 2) void k_emit_px2(FrameArgs a) {
     __shared__ uint32_t s_hist[4 * 256];
@@ -1663,6 +1818,11 @@ __global__ __launch_bounds__(SEGW / 2) void k_emit_px2(FrameArgs a) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     constexpr int NT = SEGW / 2, NW = NT / 64, NWORDS = SEGW / 64;
     const uint32_t s = blockIdx.x;
+    if (a.nparts) {
+        for (uint32_t j = threadIdx.x; j < (1u << kMarkCacheBits); j += NT) s_mark[j] = 0xFFFFFFFFu;
+        emit_px2_parts<SEGW>(a, s_mark);
+        return;
+    }
     for (uint32_t j = threadIdx.x; j < (1u << kMarkCacheBits); j += NT) s_mark[j] = 0xFFFFFFFFu;
     const gptr<const CamDesc> cams = G(cam_table(a));
     const bool hist = a.key_hist && !a.run_mode;
@@ -2008,7 +2168,8 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
         }
         if (!a.fused_prefix && !a.grp_done) {  // (run mode: the point counts, then the run counts)
             HookScope hs(hook, GDF_KERNEL_SCAN);
-            const uint32_t m = a.run_mode ? 2u * a.total_segs : a.total_segs;
+            const uint32_t m = a.nparts ? 2u * a.nparts * a.total_segs
+                                        : a.run_mode ? 2u * a.total_segs : a.total_segs;
             if ((e = launch_scan(a.seg_counts, m, a.seg_offsets, a.scan_total, nullptr, 1u, s)) != hipSuccess)
                 return e;
         }
@@ -2061,6 +2222,14 @@ const void* mask_kernel(const FrameArgs& a) {
 // k_emit_px2 (two pixels per thread) for 256-pixel segments unless g_emit_px2 is cleared (tuning
 // knob GDF_EMIT_PX2=0)
 uint32_t g_emit_px2 = 1;
+// the compaction kernels that write the emit partition (FrameArgs::nparts)
+bool emit_partition_kernels(const FrameArgs& a) {
+    const void* km = mask_kernel(a);
+    return (km == reinterpret_cast<const void*>(&k_mask_px<2, 256>) ||
+            km == reinterpret_cast<const void*>(&k_mask_px<4, 256>)) &&
+           emit_kernel(a) == reinterpret_cast<const void*>(&k_emit_px2<256>);
+}
+
 const void* emit_kernel(const FrameArgs& a) {
     if (g_emit_px2 && a.seg_threads == 256) return reinterpret_cast<const void*>(&k_emit_px2<256>);
     if (g_emit_px2 && a.seg_threads == 640 && a.total_segs >= kPx640MinSegs)

@@ -43,6 +43,7 @@ const void* frame_kernel(int which, int rot45, uint32_t F = 0);
 const void* mask_kernel(const FrameArgs& a);  // the compaction pass-1 kernel launch_frame uses
 extern uint32_t g_mask_px2;
 const void* emit_kernel(const FrameArgs& a);  // the compaction pass-2 kernel launch_frame uses
+bool emit_partition_kernels(const FrameArgs& a);
 extern uint32_t g_emit_px2;
 extern uint32_t g_grid_wpt;
 

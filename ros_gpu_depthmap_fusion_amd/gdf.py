@@ -139,7 +139,7 @@ EXPORTED = [
     "gdf_run_depth_stream_alternating",
     "gdf_next_frame_in_batch", "gdf_get_batch_ranges", "gdf_download_batch_occupancy_grid",
     "gdf_mask_dilate", "gdf_transform_points", "gdf_add_halo_depthmap_device",
-    "gdf_partition_points", "gdf_voxelize_points", "gdf_partition_runs", "gdf_voxelize_runs", "gdf_last_sort_items", "gdf_get_stream",
+    "gdf_partition_points", "gdf_voxelize_points", "gdf_partition_runs", "gdf_voxelize_runs", "gdf_set_emit_partition", "gdf_last_sort_items", "gdf_get_stream",
     "gdf_get_graph_stats", "gdf_get_slot", "gdf_select_slot", "gdf_build_info",
     "gdf_download_frame", "gdf_set_slot_streams",
     # include/gdf_fused.h: a rank of the multi-GPU fused cloud in C++ over RCCL
@@ -233,6 +233,7 @@ def load_library(path: str = LIB_PATH):
         "gdf_partition_points": (i32, [vp, u32, vp, vp, u32, vp]),
         "gdf_voxelize_points": (i32, [vp, vp, vp, u32, i32]),
         "gdf_partition_runs": (i32, [vp, u32, vp, vp, vp, u32, vp]),
+        "gdf_set_emit_partition": (i32, [vp, u32, vp, vp, vp, u32, vp]),
         "gdf_voxelize_runs": (i32, [vp, vp, vp, vp, u32, vp, vp, i32]),
         "gdf_transform_points": (i32, [vp, vp, vp, vp, u32, vp]),
         "gdf_get_batch_ranges": (i32, [vp, vp, vp, u32, P(u32)]),
@@ -775,6 +776,14 @@ class GPUDepthmapFusion:
         """partition_points with runs of equal keys instead of per-point keys (gdf_partition_runs):
         part_counts = points per part, then runs per part."""
         self._check(self._lib.gdf_partition_runs(
+            self._h, nparts, C.c_void_p(send_pts_ptr), C.c_void_p(send_run_keys_ptr),
+            C.c_void_p(send_run_starts_ptr), capacity, C.c_void_p(part_counts_ptr)))
+
+    def set_emit_partition(self, nparts: int, send_pts_ptr: int = 0, send_run_keys_ptr: int = 0,
+                           send_run_starts_ptr: int = 0, capacity: int = 0, part_counts_ptr: int = 0):
+        """The next deferred frame's compaction writes partition_runs' send lists itself
+        (gdf_set_emit_partition; nparts = 0 disarms)."""
+        self._check(self._lib.gdf_set_emit_partition(
             self._h, nparts, C.c_void_p(send_pts_ptr), C.c_void_p(send_run_keys_ptr),
             C.c_void_p(send_run_starts_ptr), capacity, C.c_void_p(part_counts_ptr)))
 

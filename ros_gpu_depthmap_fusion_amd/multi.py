@@ -447,21 +447,33 @@ class FusedCloudRank:
                                               pc_.T_world, pc_.T_crop)
                 eng.addDepthmapDevice(depth_ptrs[j], c.width, c.height, *c.intrinsics(), c.T_world,
                                       c.T_crop)
-            res = eng.processFramePrepared(self.frame_params(move) if B == 1 else self.pc)
+            pc = self.frame_params(move) if B == 1 else self.pc
+            # the send lists, written by the compaction itself (gdf_set_emit_partition): every
+            # pixel of the step, and on the rollbuffer rank every point the window can select
+            want = B * c.width * c.height
+            if self.has_rollbuffer and B == 1 and pc.move_transform_available:
+                want += (eng.rollbuffer_state().num_points +
+                         eng.numCollectedPointSequencePoints())
+            if self.dev == "cuda":
+                S.ensure(st, n_send=max(want, 1))
+                eng.set_emit_partition(self.world, S.sp.data_ptr(), S.srk.data_ptr(),
+                                       S.srs.data_ptr(), S.cap, S.cnt.data_ptr())
+            else:
+                dsp, drk, drs = (h.DeviceArray(max(want, 1) * 16), h.DeviceArray(max(want, 1) * 4),
+                                 h.DeviceArray(max(want, 1) * 4))
+                dcnt = h.DeviceArray(2 * self.world * 4)
+                eng.set_emit_partition(self.world, dsp.ptr, drk.ptr, drs.ptr, max(want, 1), dcnt.ptr)
+            res = eng.processFramePrepared(pc)
             _, ncells = eng.grid_size()
             words = words_for(ncells)
-            n_total = max(int(res.num_points_total), 1)
             if self.dev == "cuda":
-                S.ensure(st, n_send=n_total, mark_words=B * words)
+                S.ensure(st, mark_words=B * words)
                 # occupancy union: the B frames' marks of every rank, one batched grid update
                 eng.take_marks(S.local.data_ptr(), B * words)
                 dist.all_gather_into_tensor(S.gathered[:self.world * B * words], S.local[:B * words])
                 eng.voxelOccupancyGridBatch(S.gathered.data_ptr(), words, self.world, B, words,
                                             B * words, self.p.occupancy_lifetime)
-                # key-range partition into points + runs of equal keys; the split sizes
-                # (points, runs) per part to the host without a stream sync
-                eng.partition_runs(self.world, S.sp.data_ptr(), S.srk.data_ptr(),
-                                   S.srs.data_ptr(), S.cap, S.cnt.data_ptr())
+                # the split sizes (points, runs) per part to the host without a stream sync
                 S.c64.copy_(S.cnt.view(2, self.world).t())
                 dist.all_to_all_single(S.rc, S.c64)
                 S.host[:2 * self.world].copy_(S.c64.view(-1), non_blocking=True)
@@ -478,10 +490,6 @@ class FusedCloudRank:
                 dg = h.DeviceArray.from_numpy(torch.cat(parts).numpy())
                 eng.voxelOccupancyGridBatch(dg.ptr, words, self.world, B, words, B * words,
                                             self.p.occupancy_lifetime)
-                dsp, drk, drs = (h.DeviceArray(n_total * 16), h.DeviceArray(n_total * 4),
-                                 h.DeviceArray(n_total * 4))
-                dcnt = h.DeviceArray(2 * self.world * 4)
-                eng.partition_runs(self.world, dsp.ptr, drk.ptr, drs.ptr, n_total, dcnt.ptr)
                 eng.synchronize()
                 self._staged[k] = (dg, dsp, drk, drs, dcnt)
         return k

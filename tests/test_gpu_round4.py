@@ -174,13 +174,18 @@ def test_4k_frame_knobs_match_oracle(Engine, knobs):
     compare_results(gpu, orc, tag=f"4K {knobs}")
 
 
-@pytest.mark.parametrize("nparts,B", [(1, 1), (3, 1), (5, 3), (16, 8)])
-def test_partition_runs_voxelize_runs_match_oracle(Engine, nparts, B):
+@pytest.mark.parametrize("nparts,B,emit", [(1, 1, False), (3, 1, False), (5, 3, False),
+                                            (16, 8, False), (1, 8, True), (3, 8, True),
+                                            (8, 8, True), (16, 4, True), (3, 1, True)])
+def test_partition_runs_voxelize_runs_match_oracle(Engine, nparts, B, emit):
     """gdf_partition_runs (points + runs of equal frame|voxel keys, part-major) and
     gdf_voxelize_runs per part, in one process: every part voxelized on its own, the parts'
     voxels concatenated in part order, equal the oracle's voxel means of each frame bit for bit
     (the fused cloud's key ranges without the transport).  Also: sources split at arbitrary
-    points of a part (several "ranks" sending one key range) rebase to the same result."""
+    points of a part (several "ranks" sending one key range) rebase to the same result.  emit:
+    the same send lists from gdf_set_emit_partition (the compaction writes them: k_mask_px +
+    k_emit_px2 on the 256-pixel segments of frames over 1 Mi pixels; a single VGA frame takes the
+    compaction + partition pass)."""
     from ros_gpu_depthmap_fusion_amd import hiprt
     p = ComponentParams()
     cam = synth.make_camera(0, 640, 480)
@@ -191,16 +196,19 @@ def test_partition_runs_voxelize_runs_match_oracle(Engine, nparts, B):
         if j:
             gpu.nextFrameInBatch()
         gpu.addDepthmap(*cam_args(cam, frames[j]))
-    res = gpu.processFrame(p, synchronous=True, defer_occupancy_grid=True, defer_voxelize=True)
-    n = int(gpu.downloadPoints().shape[0])
-    cap = int(res.num_points_total)  # (the send buffers hold the frame's pixels before compaction)
+    cap = 640 * 480 * B  # (the send buffers hold the frame's pixels before compaction)
     sp, srk, srs = hiprt.DeviceArray(16 * cap), hiprt.DeviceArray(4 * cap), hiprt.DeviceArray(4 * cap)
     cnt = hiprt.DeviceArray(8 * nparts)
-    gpu.partition_runs(nparts, sp.ptr, srk.ptr, srs.ptr, cap, cnt.ptr)
+    if emit:
+        gpu.set_emit_partition(nparts, sp.ptr, srk.ptr, srs.ptr, cap, cnt.ptr)
+    gpu.processFrame(p, synchronous=True, defer_occupancy_grid=True, defer_voxelize=True)
+    if not emit:
+        gpu.partition_runs(nparts, sp.ptr, srk.ptr, srs.ptr, cap, cnt.ptr)
     gpu.synchronize()
     c = cnt.to_numpy(np.uint32, 2 * nparts)
     pts, runs = c[:nparts].astype(np.int64), c[nparts:].astype(np.int64)
-    assert pts.sum() == n and (runs <= pts).all() and ((runs > 0) == (pts > 0)).all()
+    n = int(pts.sum())
+    assert (runs <= pts).all() and ((runs > 0) == (pts > 0)).all()
     P0, R0 = np.concatenate([[0], np.cumsum(pts)]), np.concatenate([[0], np.cumsum(runs)])
     h_rs = srs.to_numpy(np.uint32, max(n, 1))
     want = []
