@@ -156,7 +156,8 @@ struct FrameArgs {
     uint32_t* seg_offsets;      // [total_segs] (k_scan_counts path)
     int32_t fused_prefix;       // k_emit sums the preceding segment counts itself
     uint32_t band_rowb;         // bytes per staged band row (16-B chunks)
-    uint32_t band_lds;          // dynamic LDS of k_mask: band rows + column ray factors
+    uint32_t band_lds;          // dynamic LDS of k_mask: band rows + column ray factors (+ hist)
+    uint32_t hist_lds;          // k_mask_px: byte offset of the run-key digit histogram in it
     uint32_t seg_threads;       // block size of k_mask / k_emit (>= every segment, 64-multiple)
     uint8_t* dbg;               // optional per-item stage bits
     uint32_t* err;

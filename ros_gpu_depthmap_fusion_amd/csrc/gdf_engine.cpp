@@ -501,7 +501,7 @@ struct gdf_engine {
         float* pts = nullptr;
         uint32_t *run_keys = nullptr, *run_starts = nullptr, *counts = nullptr;
     } epart;
-    bool emit_part = getenv("GDF_EMIT_PART") != nullptr;  // (else: compaction, then the partition pass)
+    bool emit_part = !getenv("GDF_NO_EMIT_PART");  // (else: compaction, then the partition pass)
     bool dl_prefetch_allowed = !getenv("GDF_NO_DL_PREFETCH");
     // tuning knob GDF_DL_FORK: the points / coords part on a second stream right after the
     // compaction (direct launches) instead of in the chain's last kernel (graph replays)
@@ -1331,6 +1331,8 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel, bool compaction_marks = fa
         const uint32_t cols = e->max_segw + 2 * h;
         a.band_rowb = ((cols * 2 + 15) / 16 + 1) * 16;
         a.band_lds = (2 * h + 1) * a.band_rowb + (kHalo + a.seg_threads * 2) * 4;
+        a.hist_lds = (a.band_lds + 15) & ~15u;  // (k_mask_px: the digit histogram, when counted)
+        if (a.run_mode && a.key_hist) a.band_lds = a.hist_lds + 4 * 256 * 4;
     }
     if (e->debug) {  // (stage bits by global index: halo gaps included)
         e->sl().d_stage.ensure(std::max<size_t>({(size_t)e->sl().n_total, (size_t)e->index_end + sel, 1}));

@@ -1172,14 +1172,17 @@ __global__ __launch_bounds__(SEGW / PX) void k_mask_px(FrameArgs a) {
     constexpr int QR = (2 * 4 + 1 + NW - 1) / NW;        // band rows per wave (h = 4)
     constexpr int QX = (SEGW + 2 * 4 + NT - 1) / NT;     // ray factors per thread
     constexpr int QC = (((SEGW + 8) * 2 + 15) / 16 + 1 + 63) / 64;  // 16-B chunks per lane and row
-    __shared__ CamDesc s_cams[kMaxCams];
+    // the segment's camera only (occupancy: 16 descriptors were 3.3 KB of LDS per block; the first
+    // rows' general path reads the others from the argument table)
+    __shared__ CamDesc s_cams[1];
     __shared__ float s_yn[2 * kHalo + 1];
     __shared__ int s_rowoff[2 * kHalo + 1];
     __shared__ uint32_t s_cnt[NWORDS];
     __shared__ uint32_t s_rcnt[NWORDS];
-    __shared__ uint32_t s_hist[4 * 256];
     __shared__ uint32_t s_pc[2][NWORDS][kMaxParts];  // emit partition: points, runs per (word, part)
     extern __shared__ uint4 s_dyn[];
+    // run-key digit histogram: dynamic LDS behind the band, only when the launch counts digits
+    uint32_t* s_hist = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(s_dyn) + a.hist_lds);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (a.nparts)
         for (uint32_t j = threadIdx.x; j < 2u * NWORDS * kMaxParts; j += NT) (&s_pc[0][0][0])[j] = 0u;
@@ -1248,7 +1251,11 @@ __global__ __launch_bounds__(SEGW / PX) void k_mask_px(FrameArgs a) {
         }
         float xwv = 0.0f;
         if (wrap && i < (uint32_t)h) xwv = G(c.xn)[c.W - 1 - i];
-        load_cams(a, s_cams);
+        {  // camera sg.k's descriptor into LDS
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(cam_table(a) + sg.k);
+            uint32_t* dst = reinterpret_cast<uint32_t*>(s_cams);
+            for (uint32_t w = threadIdx.x; w < (uint32_t)(sizeof(CamDesc) / 4); w += NT) dst[w] = G(src)[w];
+        }
 #pragma unroll
         for (int q = 0; q < QR; ++q) {
             const uint32_t r = (uint32_t)wid + (uint32_t)NW * q;
@@ -1279,19 +1286,19 @@ __global__ __launch_bounds__(SEGW / PX) void k_mask_px(FrameArgs a) {
                 in[j] = i + (uint32_t)NT * j < sg.len;
             }
             if (PX == 2 && a.mask_packed && sg.y >= 4u && xw0 >= 4u)
-                depth_bits_px2<kInterior>(a, s_cams, sg.k, t, s_yn, x, sg.y, in, bits);
+                depth_bits_px2<kInterior>(a, s_cams, 0, t, s_yn, x, sg.y, in, bits);
             else if (PX == 2 && a.mask_packed && wrap)
-                depth_bits_px2<kRowStart>(a, s_cams, sg.k, t, s_yn, x, sg.y, in, bits);
+                depth_bits_px2<kRowStart>(a, s_cams, 0, t, s_yn, x, sg.y, in, bits);
             else if (sg.y >= 4u && xw0 >= 4u)
-                depth_bits_px<kInterior, PX>(a, s_cams, sg.k, t, s_yn, x, sg.y, in, bits);
+                depth_bits_px<kInterior, PX>(a, s_cams, 0, t, s_yn, x, sg.y, in, bits);
             else if (wrap)
-                depth_bits_px<kRowStart, PX>(a, s_cams, sg.k, t, s_yn, x, sg.y, in, bits);
+                depth_bits_px<kRowStart, PX>(a, s_cams, 0, t, s_yn, x, sg.y, in, bits);
             else
 #pragma unroll
                 for (int j = 0; j < PX; ++j)
-                    bits[j] = depth_bits<false, kGeneral, 4>(a, s_cams, sg.k, t, s_yn, x[j], sg.y, in[j]);
+                    bits[j] = depth_bits<false, kGeneral, 4>(a, reinterpret_cast<const CamDesc*>(cam_table(a)), sg.k, t, s_yn, x[j], sg.y, in[j]);
             if (a.run_mode && PX == 2 && a.mask_packed) {  // both pixels' keys in packed f32
-                const CamDesc& cd = s_cams[sg.k];
+                const CamDesc& cd = s_cams[0];
                 if ((bits[0] | bits[PX - 1]) & 4u) {
                     const P3x2 p = band_pt2(t, h, (int)x[0], h, (int)x[PX - 1],
                                             f2(s_yn[h], s_yn[h]), cd.scale);
@@ -1303,7 +1310,7 @@ __global__ __launch_bounds__(SEGW / PX) void k_mask_px(FrameArgs a) {
                     if (bits[PX - 1] & 4u) rkey[PX - 1] = k1 | (cd.frame << a.frame_shift);
                 }
             } else if (a.run_mode) {
-                const CamDesc& cd = s_cams[sg.k];
+                const CamDesc& cd = s_cams[0];
 #pragma unroll
                 for (int j = 0; j < PX; ++j)
                     if (bits[j] & 4u) {  // the voxel key k_emit will compute (same f32 ops)
@@ -1818,11 +1825,6 @@ __global__ __launch_bounds__(SEGW / 2) void k_emit_px2(FrameArgs a) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     constexpr int NT = SEGW / 2, NW = NT / 64, NWORDS = SEGW / 64;
     const uint32_t s = blockIdx.x;
-    if (a.nparts) {
-        for (uint32_t j = threadIdx.x; j < (1u << kMarkCacheBits); j += NT) s_mark[j] = 0xFFFFFFFFu;
-        emit_px2_parts<SEGW>(a, s_mark);
-        return;
-    }
     for (uint32_t j = threadIdx.x; j < (1u << kMarkCacheBits); j += NT) s_mark[j] = 0xFFFFFFFFu;
     const gptr<const CamDesc> cams = G(cam_table(a));
     const bool hist = a.key_hist && !a.run_mode;
@@ -1943,6 +1945,15 @@ __global__ __launch_bounds__(SEGW / 2) void k_emit_px2(FrameArgs a) {
                            key | (fr << a.frame_shift), hist ? s_hist : nullptr, s_mark);
     }
     if (hist) flush_hist(a, s_hist);
+}
+
+// the emit partition's k_emit_px2 (its own kernel: the part bookkeeping's registers would otherwise
+// raise the plain kernel's VGPR count, 32 -> 54, and cost it 10 us per 8-frame batch)
+template <int SEGW>
+__global__ __launch_bounds__(SEGW / 2) void k_emit_px2_parts(FrameArgs a) {
+    __shared__ uint32_t s_mark[1u << kMarkCacheBits];
+    for (uint32_t j = threadIdx.x; j < (1u << kMarkCacheBits); j += SEGW / 2) s_mark[j] = 0xFFFFFFFFu;
+    emit_px2_parts<SEGW>(a, s_mark);
 }
 
 // Selected rollbuffer points (insertSelectedPointSequence + transformPointSequence + crop +
@@ -2175,7 +2186,9 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
         }
         HookScope hs(hook, GDF_KERNEL_EMIT);
         const void* ke = emit_kernel(a);
-        if (ke == reinterpret_cast<const void*>(&k_emit_px2<256>))
+        if (ke == reinterpret_cast<const void*>(&k_emit_px2_parts<256>))
+            hipLaunchKernelGGL(k_emit_px2_parts<256>, dim3(a.total_segs), dim3(128), 0, s, a);
+        else if (ke == reinterpret_cast<const void*>(&k_emit_px2<256>))
             hipLaunchKernelGGL(k_emit_px2<256>, dim3(a.total_segs), dim3(128), 0, s, a);
         else if (ke == reinterpret_cast<const void*>(&k_emit_px2<640>))
             hipLaunchKernelGGL(k_emit_px2<640>, dim3(a.total_segs), dim3(320), 0, s, a);
@@ -2225,12 +2238,15 @@ uint32_t g_emit_px2 = 1;
 // the compaction kernels that write the emit partition (FrameArgs::nparts)
 bool emit_partition_kernels(const FrameArgs& a) {
     const void* km = mask_kernel(a);
+    FrameArgs plain = a;
+    plain.nparts = 0;
     return (km == reinterpret_cast<const void*>(&k_mask_px<2, 256>) ||
             km == reinterpret_cast<const void*>(&k_mask_px<4, 256>)) &&
-           emit_kernel(a) == reinterpret_cast<const void*>(&k_emit_px2<256>);
+           emit_kernel(plain) == reinterpret_cast<const void*>(&k_emit_px2<256>);
 }
 
 const void* emit_kernel(const FrameArgs& a) {
+    if (a.nparts) return reinterpret_cast<const void*>(&k_emit_px2_parts<256>);
     if (g_emit_px2 && a.seg_threads == 256) return reinterpret_cast<const void*>(&k_emit_px2<256>);
     if (g_emit_px2 && a.seg_threads == 640 && a.total_segs >= kPx640MinSegs)
         return reinterpret_cast<const void*>(&k_emit_px2<640>);

@@ -10,9 +10,12 @@ import collections
 import csv
 import json
 
-SLOT = {"k_mask": ("mask", 64), "k_mask_px<2>": ("mask", 128), "k_mask_px<4>": ("mask", 256),
-        "k_emit_px2": ("emit", 128), "k_emit": ("emit_1px", 64), "k_sort_pass<8, 256>": ("sort", 64),
-        "k_sort_pass<8, 512>": ("sort_wide", 64)}
+# full kernel names (template arguments included): the timed batch kernels only, never averaged
+# with the single-frame variants of the bench's synchronous count pass
+SLOT = {"k_mask": ("mask", 64), "k_mask_px<2, 256>": ("mask", 128), "k_mask_px<4, 256>": ("mask", 256),
+        "k_mask_px<2, 640>": ("mask", 128), "k_emit_px2<256>": ("emit", 128), "k_emit": ("emit_1px", 64),
+        "k_sort_pass<8, 256>": ("sort", 64), "k_sort_pass<8, 512>": ("sort_wide", 64),
+        "k_group_runs<2048, 2>": ("group", 0)}
 
 
 def main():
