@@ -1880,6 +1880,8 @@ int gdf_create(int device, gdf_engine** out) {
             g_run_stage = (uint32_t)std::max(1, std::atoi(v));
         if (const char* v = std::getenv("GDF_EMIT_PX2"))  // tuning knob
             g_emit_px2 = (uint32_t)std::atoi(v);
+        if (const char* v = std::getenv("GDF_MASK_OCC8"))  // tuning knob
+            g_mask_occ8 = (uint32_t)std::atoi(v);
         if (const char* v = std::getenv("GDF_GRID_WPT"))  // tuning knob: 1..8
             g_grid_wpt = (uint32_t)std::min(8, std::max(1, std::atoi(v)));
         if (const char* v = std::getenv("GDF_MASK_PX"))  // tuning knob: pixels per k_mask thread

@@ -1166,7 +1166,7 @@ __device__ __forceinline__ unsigned long long part_lanes(unsigned long long m, b
 // w + j * waves from pixel j of wave w; counts, runs, run-key histogram).  No debug stage bits
 // (the engine launches k_mask for those).
 template <int PX, int SEGW>
-__global__ __launch_bounds__(SEGW / PX) void k_mask_px(FrameArgs a) {
+__device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
     constexpr int NT = SEGW / PX, NW = NT / 64;          // threads, waves
     constexpr int NWORDS = SEGW / 64;                    // validity words of a segment
     constexpr int QR = (2 * 4 + 1 + NW - 1) / NW;        // band rows per wave (h = 4)
@@ -1382,6 +1382,16 @@ __global__ __launch_bounds__(SEGW / PX) void k_mask_px(FrameArgs a) {
                 __hip_atomic_fetch_add(rep + j, s_hist[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     group_scan_tail(a, s);
+}
+
+template <int PX, int SEGW>
+__global__ __launch_bounds__(SEGW / PX) void k_mask_px(FrameArgs a) {
+    mask_px_body<PX, SEGW>(a);
+}
+// the same at 8 waves per SIMD (<= 64 VGPRs, a few spilled): tuning knob GDF_MASK_OCC8
+template <int PX, int SEGW>
+__global__ __launch_bounds__(SEGW / PX) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_mask_px_o8(FrameArgs a) {
+    mask_px_body<PX, SEGW>(a);
 }
 
 // Exclusive scan of the segment counts by one workgroup (chunks of 4096 with a running carry);
@@ -2163,6 +2173,8 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
             const void* km = mask_kernel(a);
             if (km == reinterpret_cast<const void*>(&k_mask_px<2, 256>))
                 hipLaunchKernelGGL((k_mask_px<2, 256>), dim3(a.total_segs), dim3(128), lds, s, a);
+            else if (km == reinterpret_cast<const void*>(&k_mask_px_o8<2, 256>))
+                hipLaunchKernelGGL((k_mask_px_o8<2, 256>), dim3(a.total_segs), dim3(128), lds, s, a);
             else if (km == reinterpret_cast<const void*>(&k_mask_px<4, 256>))
                 hipLaunchKernelGGL((k_mask_px<4, 256>), dim3(a.total_segs), dim3(64), lds, s, a);
             else if (km == reinterpret_cast<const void*>(&k_mask_px<2, 640>))
@@ -2219,10 +2231,12 @@ constexpr uint32_t kPx640MinSegs = 1024;
 // (A/B on one box, dense frames, 2 pixels per thread vs k_mask): VGA 8-frame batches
 // 22.1 -> 23.7, 720p 4-frame batches 29.8 -> 32.6, 4K 30.9 -> 32.4 Gpoints/s
 uint32_t g_mask_px2 = 2;
+uint32_t g_mask_occ8 = 1;  // k_mask_px<2, 256> at 8 waves per SIMD (GDF_MASK_OCC8=0: 7; +2.5 % on C2)
 const void* mask_kernel(const FrameArgs& a) {
     if (g_mask_px2 >= 2 && a.do_flying && a.F == 4 && !a.rot45 && a.seg_threads == 256 && !a.dbg &&
         a.band_rowb <= 64 * 16)
         return g_mask_px2 >= 4 ? reinterpret_cast<const void*>(&k_mask_px<4, 256>)
+               : g_mask_occ8   ? reinterpret_cast<const void*>(&k_mask_px_o8<2, 256>)
                                : reinterpret_cast<const void*>(&k_mask_px<2, 256>);
     // (half 720p rows: single frames under 1 Mi pixels with enough segments to fill the chip)
     if (g_mask_px2 >= 2 && a.do_flying && a.F == 4 && !a.rot45 && a.seg_threads == 640 && !a.dbg &&
@@ -2241,6 +2255,7 @@ bool emit_partition_kernels(const FrameArgs& a) {
     FrameArgs plain = a;
     plain.nparts = 0;
     return (km == reinterpret_cast<const void*>(&k_mask_px<2, 256>) ||
+            km == reinterpret_cast<const void*>(&k_mask_px_o8<2, 256>) ||
             km == reinterpret_cast<const void*>(&k_mask_px<4, 256>)) &&
            emit_kernel(plain) == reinterpret_cast<const void*>(&k_emit_px2<256>);
 }

@@ -46,6 +46,7 @@ const void* emit_kernel(const FrameArgs& a);  // the compaction pass-2 kernel la
 bool emit_partition_kernels(const FrameArgs& a);
 extern uint32_t g_emit_px2;
 extern uint32_t g_grid_wpt;
+extern uint32_t g_mask_occ8;
 
 // filter_point_sequence + insert into the rollbuffer ring (w = mask)
 hipError_t launch_ps_filter_insert(const float4* new_pts, uint32_t n, int do_filter, float thr,

@@ -12,7 +12,7 @@ import json
 
 # full kernel names (template arguments included): the timed batch kernels only, never averaged
 # with the single-frame variants of the bench's synchronous count pass
-SLOT = {"k_mask": ("mask", 64), "k_mask_px<2, 256>": ("mask", 128), "k_mask_px<4, 256>": ("mask", 256),
+SLOT = {"k_mask": ("mask", 64), "k_mask_px<2, 256>": ("mask", 128), "k_mask_px_o8<2, 256>": ("mask", 128), "k_mask_px<4, 256>": ("mask", 256),
         "k_mask_px<2, 640>": ("mask", 128), "k_emit_px2<256>": ("emit", 128), "k_emit": ("emit_1px", 64),
         "k_sort_pass<8, 256>": ("sort", 64), "k_sort_pass<8, 512>": ("sort_wide", 64),
         "k_group_runs<2048, 2>": ("group", 0)}

@@ -25,7 +25,7 @@ import csv
 import json
 
 # slot of bench.py's roofline (SINGLE_SLOTS) per kernel base name
-SLOT = {"k_mask": "mask", "k_mask_px": "mask", "k_emit": "emit", "k_emit_px2": "emit",
+SLOT = {"k_mask": "mask", "k_mask_px": "mask", "k_mask_px_o8": "mask", "k_emit": "emit", "k_emit_px2": "emit",
         "k_sort_pass": "sort", "k_group": "group", "k_group_runs": "group",
         "k_group_big": "group_big", "k_group_runs_big": "group_big", "k_scan_counts": "scan",
         "k_scan_reduce": "scan_reduce", "k_grid_u8": "grid", "k_grid_u32": "grid",
@@ -51,7 +51,7 @@ def load(path, counter):
 def steady(rows):
     """Dispatches from the first one of the most-dispatched compaction (mask) kernel on, and the
     name of that kernel."""
-    cnt = collections.Counter(n for _, n, _ in rows if n.split("<")[0] in ("k_mask", "k_mask_px"))
+    cnt = collections.Counter(n for _, n, _ in rows if n.split("<")[0] in ("k_mask", "k_mask_px", "k_mask_px_o8"))
     if not cnt:
         return rows, None
     mk = cnt.most_common(1)[0][0]
