@@ -13,7 +13,7 @@ namespace gdf {
 
 constexpr int kMaxCams = 16;          // GDF_MAX_CAMERAS
 constexpr int kFrameThreads = 256;    // k_mask / k_emit block: 4 waves, 4 items per thread
-constexpr int kArgCams = 4;           // camera descriptors passed in the kernel arguments
+constexpr int kArgCams = 8;           // camera descriptors passed in the kernel arguments
 constexpr int kHalo = 8;              // band rows/columns staged around a segment: min(F, 8)
 constexpr uint32_t kSegItems = 1024;  // items per compaction segment (max)
 constexpr uint32_t kFusedPrefixSegs = 4096;  // up to this many segments k_emit sums the counts

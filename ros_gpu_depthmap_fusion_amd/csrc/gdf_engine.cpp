@@ -1663,8 +1663,10 @@ void run_fused_frame(gdf_engine* e, int average, uint32_t lifetime) {
         return;
     }
     // (a prefetching frame forks its points download after the compaction: direct launches)
+    // (single frames only: a multi-frame batch launches directly - its replays measured 26.8 ->
+    // 25.9 Gpoints/s on the C2 line once 8 descriptors fit the argument table)
     const bool eligible = e->use_graphs && !e->profiling && !e->debug && a.ncams <= kArgCams &&
-                          !e->user_stream && a.total_segs && !prefetch_fork(e);
+                          !e->user_stream && a.total_segs && !prefetch_fork(e) && e->nframes == 1;
     hipStream_t st = e->s();
     Slot::GraphEntry* hit = nullptr;
     if (eligible)
