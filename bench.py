@@ -822,7 +822,7 @@ def run_h2d(args, params, steps, warm):
     r["workload"] = "C2 with host (pinned) depth maps: " + workload_name(
         args.width, args.height, 1, args.workload)
     r["value_h2d"] = r.pop("value")
-    r["h2d_threads"] = int(os.environ.get("GDF_H2D_THREADS", "1"))  # (the engine default)
+    r["h2d_threads"] = int(os.environ.get("GDF_H2D_THREADS", "4"))  # (the engine default)
     r["h2d_GBps"] = round(2.0 * args.width * args.height * args.batch / (r["ms_per_step"] / 1e3) / 1e9, 2)
     del st
     eng.close()

@@ -58,9 +58,11 @@ struct GdfError {
 // Host -> pinned-staging copies of host depth maps, split over worker threads: one thread's
 // memcpy (~8-15 GB/s, box-dependent) bounded the host-map line at half the device-map rate
 // (VERDICT r2 weak #11).  The caller works too; workers are created on first use and block on a
-// condition variable between calls.  Threads: GDF_H2D_THREADS (default 1 = the caller only:
-// measured on MI355X, 8-frame VGA batches, 1 / 4 / 8 threads 14.3 / 12.9 / 13.0 Gpoints/s - the
-// DMA at ~27 GB/s, not the copy, bounds the host-map line on that box).
+// condition variable between calls.  Threads: GDF_H2D_THREADS (default 4: the caller + 3
+// workers).  Round 3 measured no gain from threads (8 DMAs per batch with command gaps bounded
+// the line); with one coalesced DMA per batch (upload_depthmaps) the single-thread memcpy is the
+// bound - trace: 107-us DMA, next batch's DMA issued ~240 us later - and 1 / 4 / 8 threads give
+// 28.6 / 34.5 / 32.6 GB/s on one box (profiles/r04/h2d/).
 class StagingCopier {
   public:
     struct Job {
@@ -117,7 +119,7 @@ class StagingCopier {
     unsigned threads() {
         if (!nthreads_) {
             const char* s = std::getenv("GDF_H2D_THREADS");
-            const int v = s ? std::atoi(s) : 1;
+            const int v = s ? std::atoi(s) : 4;
             nthreads_ = (unsigned)std::max(1, std::min(v, 16));
         }
         return nthreads_;
@@ -484,6 +486,8 @@ struct gdf_engine {
     bool use_runs = !getenv("GDF_NO_RUNS");      // voxelize runs of equal keys (depth frames)
     bool force_runs = getenv("GDF_FORCE_RUNS") != nullptr;    // tuning knob: runs at every size
     bool run_hist_in_sort = getenv("GDF_RUN_HIST_SORT") != nullptr;  // tuning knob
+    bool run_hist_all = getenv("GDF_RUN_HIST_ALL") != nullptr;  // tuning knob: k_mask counts the
+                                                               // run digits at any segment count
     bool xruns = !getenv("GDF_NO_XRUNS");  // voxelize_points sorts the received list's runs
     bool group_scan = !getenv("GDF_NO_GROUP_SCAN");  // segment offsets without scan launches
     bool mask_packed = !getenv("GDF_NO_MASK_PACKED");  // k_mask_px<2>: packed f32 pixel pairs
@@ -1068,8 +1072,18 @@ void upload_depthmaps(gdf_engine* e) {  // fusion.cpp:1583-1593
         std::vector<StagingCopier::Job> jobs;
         for (const HostUpload& u : ups) jobs.push_back({u.stage, static_cast<const uint8_t*>(u.src), u.bytes});
         e->copier.run(jobs);
-        for (const HostUpload& u : ups)
-            HIPCHK(hipMemcpyAsync(u.dst, u.stage, u.bytes, hipMemcpyHostToDevice, e->s()));
+        // one DMA per contiguous run of staged maps (a batch's maps are staged and placed back to
+        // back): 8 VGA frames as one 4.9 MB copy instead of 8 copies with a command gap each
+        // (~8 us between 17-us copies in the trace, profiles/r04/h2d/)
+        for (size_t i = 0; i < ups.size();) {
+            size_t j = i + 1, bytes = ups[i].bytes;
+            while (j < ups.size() &&
+                   reinterpret_cast<uint8_t*>(ups[j].dst) == reinterpret_cast<uint8_t*>(ups[i].dst) + bytes &&
+                   ups[j].stage == ups[i].stage + bytes)
+                bytes += ups[j++].bytes;
+            HIPCHK(hipMemcpyAsync(ups[i].dst, ups[i].stage, bytes, hipMemcpyHostToDevice, e->s()));
+            i = j;
+        }
         Slot& q = e->sl();
         if (!q.h2d_done) HIPCHK(hipEventCreateWithFlags(&q.h2d_done, hipEventDisableTiming));
         HIPCHK(hipEventRecord(q.h2d_done, e->s()));
@@ -1283,7 +1297,8 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel, bool compaction_marks = fa
         // the run-key digits: k_mask's per-segment flush while there are few segments; above,
         // k_sort_hist over the runs (tens of thousands of flushes contend at the atomic units)
         if (a.run_mode)
-            a.key_hist = a.total_segs <= kFusedPrefixSegs && !e->run_hist_in_sort && !a.sel_tiles
+            a.key_hist = (a.total_segs <= kFusedPrefixSegs || e->run_hist_all) && !e->run_hist_in_sort &&
+                         !a.sel_tiles
                              ? e->sl().d_khist.as<uint32_t>() : nullptr;
     }
     a.out_pts = e->sl().d_pts.as<float4>();
