@@ -372,7 +372,8 @@ int gdf_voxel_occupancy_grid_batch(gdf_engine* engine, const uint32_t* device_bi
 /* Fused voxel cloud across ranks (the reference voxelizes the points of ALL cameras in one
  * stable sort, fusion.cpp:1743-1756): gdf_partition_points splits the frame's compacted
  * (point, key) list (gdf_process_frame with defer_voxelize = 1) by voxel-key range - part
- * p = floor(key * nparts / num_cells) - into part-major send buffers (device, >= the frame's
+ * p = min(floor(key / 32) / S, nparts - 1), S = ceil(ceil(num_cells / 32) / nparts): whole
+ * 32-cell occupancy-mark words per part - into part-major send buffers (device, >= the frame's
  * points), stable inside each part, with part_counts[p] (device, nparts words).  After an
  * all-to-all (rank r receives part r of every rank, in rank order = camera order) each rank
  * calls gdf_voxelize_points on what it received: its key range of m_points_voxelized, equal to
@@ -408,6 +409,15 @@ int gdf_voxelize_runs(gdf_engine* engine, const float* points_device,
                       const uint32_t* run_keys_device, uint32_t* run_starts_device,
                       uint32_t nsources, const uint32_t* point_base, const uint32_t* run_base,
                       int average_voxels);
+/* gdf_voxelize_runs that also ORs every voxel's occupancy mark into marks_device (device; frame f
+ * of a batch at f * frame_stride_words, >= the grid's mark words; the caller zeroes it).  With the
+ * word-range parts above, rank j's voxels mark exactly words [j S, (j + 1) S) of each frame, so an
+ * in-place all-gather of those slices is the union of every rank's marks (gdf_fused.cpp: 1 / W of
+ * the full bitmasks' all-gather volume), ready for gdf_voxel_occupancy_grid_batch. */
+int gdf_voxelize_runs_marked(gdf_engine* engine, const float* points_device,
+                             const uint32_t* run_keys_device, uint32_t* run_starts_device,
+                             uint32_t nsources, const uint32_t* point_base, const uint32_t* run_base,
+                             int average_voxels, uint32_t* marks_device, uint64_t frame_stride_words);
 
 /* ---- live kernel timing (HIP events on the engine stream) ------------------------------------ */
 enum gdf_kernel_slot {

@@ -2638,8 +2638,19 @@ int gdf_partition_runs(gdf_engine* e, uint32_t nparts, float* send_pts, uint32_t
 int gdf_voxelize_runs(gdf_engine* e, const float* pts, const uint32_t* run_keys,
                       uint32_t* run_starts, uint32_t nsources, const uint32_t* point_base,
                       const uint32_t* run_base, int average) {
+    return gdf_voxelize_runs_marked(e, pts, run_keys, run_starts, nsources, point_base, run_base,
+                                    average, nullptr, 0);
+}
+
+int gdf_voxelize_runs_marked(gdf_engine* e, const float* pts, const uint32_t* run_keys,
+                             uint32_t* run_starts, uint32_t nsources, const uint32_t* point_base,
+                             const uint32_t* run_base, int average, uint32_t* marks,
+                             uint64_t frame_stride_words) {
     ENGINE_OR_FAIL(e);
     return guarded(e, [&] {
+        if (marks && (frame_stride_words < mark_words(e) ||
+                      (e->nframes > 1 && frame_stride_words == 0)))
+            fail(GDF_ERR_CAPACITY, "voxelize_runs: a frame's marks need >= the grid's mark words");
         if (!e->grid_set) fail(GDF_ERR_STATE, "voxelize_runs needs the voxel grid of a frame");
         if (nsources == 0 || nsources > kMaxParts || !point_base || !run_base)
             fail(GDF_ERR_ARG, "voxelize_runs: 1..16 sources and their bases");
@@ -2671,7 +2682,11 @@ int gdf_voxelize_runs(gdf_engine* e, const float* pts, const uint32_t* run_keys,
         src.n = n;
         src.run_keys = run_keys;
         src.run_start = run_starts;
-        const VoxelizeArgs v = voxelize_args(e, average, -1, &src);
+        VoxelizeArgs v = voxelize_args(e, average, -1, &src);
+        if (marks) {  // every voxel's mark, frame f at f * stride (k_group_runs)
+            v.group_marks = marks;
+            v.group_mark_stride = frame_stride_words;
+        }
         e->timed(GDF_KERNEL_VOXELIZE, [&] { HIPCHK(launch_voxelize(v, e->s(), e->hook_ptr())); });
         e->sl().vox_valid = true;
     });

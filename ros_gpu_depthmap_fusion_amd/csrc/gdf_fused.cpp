@@ -130,7 +130,9 @@ struct DevBuf {
 
 struct SlotX {
     DevBuf tail, tails;       // this rank's halo tails, every rank's (all-gather)
-    DevBuf local, gathered;   // occupancy marks of the step's frames, every rank's
+    DevBuf local;             // the compaction's occupancy marks of the step's frames (discarded)
+    DevBuf gathered;          // the union of the step's marks: frame f at f * W * S words, rank
+                              // j's key range in words [j S, (j + 1) S) (voxelize + all-gather)
     // partitioned send lists (points, run keys, run starts), split sizes (points then runs per
     // part), every rank's split sizes
     DevBuf sp, srk, srs, cnt, cntall;
@@ -139,6 +141,7 @@ struct SlotX {
     hipEvent_t ev = nullptr;
     bool pending = false;
     int average = 1;  // the step's voxel_average
+    uint32_t nframes = 1, lifetime = 0;  // the step's batch and occupancy_lifetime
 };
 
 constexpr int kSlots = 4;  // the engine's pipeline depth is 1..4
@@ -249,14 +252,14 @@ void fused_start(gdf_fused* f, const uint16_t* const* depth, uint32_t B, const g
     uint64_t ncells = 0;
     gdfchk(gdf_get_grid_size(e, g, &ncells));
     const uint64_t words = (ncells + 31) / 32;
+    // The compaction's marks are not exchanged (W full bitmasks of B frames: 3.4 MB per rank and
+    // step at VGA x 8, received W - 1 times): the key-range voxelize of the finish marks every
+    // voxel of its range - whole mark words per range - and one in-place all-gather of those
+    // slices is the union (1 / W of the volume).  The frame's own marks are cleared here.
     uint32_t* local = S.local.ensure<uint32_t>(B * words * 4, st);
-    uint32_t* gathered = S.gathered.ensure<uint32_t>((size_t)W * B * words * 4, st);
-    // occupancy union: the B frames' marks of every rank, one batched grid update
     gdfchk(gdf_take_occupancy_marks(e, local, B * words));
-    ncclchk(r, r.all_gather(local, gathered, B * words, ncclUint32, f->comm_a, st),
-            "ncclAllGather(marks)");
-    gdfchk(gdf_voxel_occupancy_grid_batch(e, gathered, words, W, B, words, B * words,
-                                          q.occupancy_lifetime));
+    S.nframes = B;
+    S.lifetime = q.occupancy_lifetime;
     // every rank's split sizes (the partition's, written with the compaction) to pinned memory
     // (no wait here)
     ncclchk(r, r.all_gather(cnt, cntall, 2 * W, ncclUint32, f->comm_a, st), "ncclAllGather(counts)");
@@ -337,7 +340,26 @@ void fused_finish(gdf_fused* f, int slot, uint32_t* send_counts, uint32_t* recv_
         }
         ncclchk(r, r.group_end(), "ncclGroupEnd");
     }
-    gdfchk(gdf_voxelize_runs(e, rp, rrk, rrs, W, pbase, rbase, S.average));
+    // the voxel means of this rank's key range, every voxel's mark into slice R of its frame's
+    // union bitmask, the slices all-gathered in place, then the step's batched grid update
+    uint32_t g[3];
+    uint64_t ncells = 0;
+    gdfchk(gdf_get_grid_size(e, g, &ncells));
+    const uint64_t words = (ncells + 31) / 32;
+    const uint64_t Sw = (words + W - 1) / W;  // = part_slice_words(W, ncells), the partition's rule
+    const uint64_t stride = Sw * W;
+    uint32_t* uni = S.gathered.ensure<uint32_t>(S.nframes * stride * 4, st);
+    hipchk(hipMemsetAsync(uni, 0, S.nframes * stride * 4, st), "hipMemsetAsync(marks)");
+    gdfchk(gdf_voxelize_runs_marked(e, rp, rrk, rrs, W, pbase, rbase, S.average, uni, stride));
+    if (W > 1) {
+        ncclchk(r, r.group_start(), "ncclGroupStart");
+        for (uint32_t j = 0; j < S.nframes; ++j)
+            ncclchk(r, r.all_gather(uni + j * stride + (uint64_t)R * Sw, uni + j * stride, Sw, ncclUint32,
+                                    f->comm_a, st), "ncclAllGather(mark slices)");
+        ncclchk(r, r.group_end(), "ncclGroupEnd");
+    }
+    gdfchk(gdf_voxel_occupancy_grid_batch(e, uni, words, 1, S.nframes, stride, S.nframes * stride,
+                                          S.lifetime));
     if (send_counts)
         for (int q = 0; q < W; ++q) send_counts[q] = (uint32_t)pts_of(R, q);
     if (recv_count) *recv_count = (uint32_t)n;

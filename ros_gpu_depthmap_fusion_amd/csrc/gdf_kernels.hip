@@ -1137,10 +1137,10 @@ __device__ __forceinline__ void depth_bits_px2(const FrameArgs& a, const CamDesc
     }
 }
 
-// emit partition: the part (key range) of voxel key k
+// emit partition: the part (key range) of voxel key k (part_of below: whole occupancy-mark words)
 __device__ __forceinline__ uint32_t emit_part_of(uint32_t key, uint32_t nparts, uint64_t ncells) {
-    const uint64_t p = (uint64_t)key * nparts / ncells;
-    return p < nparts ? (uint32_t)p : nparts - 1u;
+    const uint32_t p = (key >> 5) / part_slice_words(nparts, ncells);
+    return p < nparts ? p : nparts - 1u;
 }
 
 // the lanes of `m` whose part equals this lane's, per distinct part of the wave (wave-uniform
@@ -3678,7 +3678,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
     uint32_t* marks, const uint32_t* tile_base, uint4* __restrict__ bigq, uint32_t bigq_cap,
     uint32_t* __restrict__ qctr, uint32_t nframes, uint32_t fshift, uint32_t* __restrict__ fvox,
     uint32_t inblock_max, uint32_t* __restrict__ rps, uint32_t* __restrict__ rlen,
-    uint32_t small_max, const uint32_t* tile_gtot) {
+    uint32_t small_max, const uint32_t* tile_gtot, uint64_t mark_stride) {
     __shared__ uint32_t s_wave[4];
     __shared__ uint32_t s_tile, s_epoch, s_excl, s_nbig, s_nq, s_qbase, s_wend, s_nx, s_nbase;
     __shared__ uint32_t s_nh, s_hbase;
@@ -3895,9 +3895,10 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
             if (threadIdx.x < total) {
                 const uint32_t g = s_excl + threadIdx.x;
                 const uint32_t s = s_start[threadIdx.x], e = s_start[threadIdx.x + 1];
-                if (marks) {
+                if (marks) {  // (mark_stride: a batch's frame f at f * mark_stride words)
                     const uint32_t k = keys[s] & kmask;
-                    atomicOr(marks + (k >> 5), 1u << (k & 31u));
+                    const uint64_t fo = mark_stride && nframes > 1 ? (uint64_t)(keys[s] >> fshift) * mark_stride : 0u;
+                    atomicOr(marks + fo + (k >> 5), 1u << (k & 31u));
                 }
                 if (fvox) {
                     const uint32_t fc = keys[s] >> fshift;
@@ -3950,9 +3951,10 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
                 const uint32_t g = s_excl + threadIdx.x;
                 const uint32_t s = s_start[threadIdx.x], e = s_start[threadIdx.x + 1];
                 float* o = out + 4 * (size_t)g;
-                if (marks) {
+                if (marks) {  // (mark_stride: a batch's frame f at f * mark_stride words)
                     const uint32_t k = keys[s] & kmask;
-                    atomicOr(marks + (k >> 5), 1u << (k & 31u));
+                    const uint64_t fo = mark_stride && nframes > 1 ? (uint64_t)(keys[s] >> fshift) * mark_stride : 0u;
+                    atomicOr(marks + fo + (k >> 5), 1u << (k & 31u));
                 }
                 if (fvox) {
                     const uint32_t fc = keys[s] >> fshift;
@@ -4220,7 +4222,7 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
                            a.nframes, a.frame_shift, a.frame_vox_start,
                            std::min<uint32_t>(g_run_inblock, g_run_stage >= 2048 ? 2048u : 512u),
                            kbuf[npasses & 1], vbuf[npasses & 1], g_small_group,  // (free after the sort)
-                           tile_gtot);
+                           tile_gtot, a.group_mark_stride);
         if (a.average) {
             if ((e = hipGetLastError()) != hipSuccess) return e;
             const bool q16 = g_run_q16 == 1 ||
@@ -4327,8 +4329,11 @@ hipError_t launch_transform_points(const float4* in, const uint32_t* mask, float
 }
 
 // ---- multi-GPU fused cloud: stable partition of the compacted (point, key) list by key range -----
-// part(key) = floor(key * nparts / ncells): rank j owns the keys [ceil(j C / np), ceil((j+1) C / np)),
-// so after an all-to-all every rank holds, in rank (= camera) order and pixel order within a
+// part(key) = min(floor((key / 32) / S), nparts - 1) with S = ceil(ceil(C / 32) / nparts) (part_slice_words):
+// rank j owns the keys of the occupancy-mark words [j S, (j + 1) S) - whole words, so the marks
+// of rank j's voxels fill exactly slice j of every frame's bitmask and one in-place all-gather of
+// equal slices is the union (gdf_fused.cpp) - and after an all-to-all every rank holds, in rank
+// (= camera) order and pixel order within a
 // camera, exactly the points of its key range - the stable order the reference's single voxelize
 // sees for them (fusion.cpp:1743-1756 over the concatenated cameras).  Tiles of 1024 items: counts
 // per (part, tile) dest-major, scanned by k_scan_*, then a stable scatter (wave ballots on the
@@ -4336,8 +4341,7 @@ hipError_t launch_transform_points(const float4* in, const uint32_t* mask, float
 constexpr uint32_t kPartTile = 1024;
 
 __device__ __forceinline__ uint32_t part_of(uint32_t key, uint32_t nparts, uint64_t ncells) {
-    const uint64_t p = (uint64_t)key * nparts / ncells;
-    return p < nparts ? (uint32_t)p : nparts - 1u;
+    return emit_part_of(key, nparts, ncells);
 }
 
 // RUNS: the partition also cuts each part's points into runs of equal (frame | voxel) keys - a

@@ -2,6 +2,12 @@
 #pragma once
 
 #include "gdf.h"
+
+// occupancy-mark words per key range of an nparts-way partition (the last range may be shorter):
+// the key-range rule of the multi-GPU exchange (gdf_kernels.hip part_of)
+__host__ __device__ inline uint32_t part_slice_words(uint32_t nparts, uint64_t ncells) {
+    return (uint32_t)(((ncells + 31) / 32 + nparts - 1) / nparts);
+}
 #include "gdf_device.hpp"
 
 #include <string>
@@ -119,6 +125,7 @@ struct VoxelizeArgs {
     uint8_t* grid8;
     uint32_t* marks;
     uint32_t* group_marks;          // optional: k_group sets the occupancy mark of every voxel
+    uint64_t group_mark_stride;     // k_group_runs: frame f's marks at f * stride words (0: one bitmask)
     uint32_t* group_counts;         // [group tiles] group starts per tile (large frames)
     uint32_t* group_offsets;        // [seg_offsets_words(group tiles)] their scan
     // optional: the scan inside k_group_count (arrive_and_scan, no scan launches) - arrival

@@ -139,7 +139,7 @@ EXPORTED = [
     "gdf_run_depth_stream_alternating",
     "gdf_next_frame_in_batch", "gdf_get_batch_ranges", "gdf_download_batch_occupancy_grid",
     "gdf_mask_dilate", "gdf_transform_points", "gdf_add_halo_depthmap_device",
-    "gdf_partition_points", "gdf_voxelize_points", "gdf_partition_runs", "gdf_voxelize_runs", "gdf_set_emit_partition", "gdf_last_sort_items", "gdf_get_stream",
+    "gdf_partition_points", "gdf_voxelize_points", "gdf_partition_runs", "gdf_voxelize_runs", "gdf_voxelize_runs_marked", "gdf_set_emit_partition", "gdf_last_sort_items", "gdf_get_stream",
     "gdf_get_graph_stats", "gdf_get_slot", "gdf_select_slot", "gdf_build_info",
     "gdf_download_frame", "gdf_set_slot_streams",
     # include/gdf_fused.h: a rank of the multi-GPU fused cloud in C++ over RCCL
@@ -235,6 +235,7 @@ def load_library(path: str = LIB_PATH):
         "gdf_partition_runs": (i32, [vp, u32, vp, vp, vp, u32, vp]),
         "gdf_set_emit_partition": (i32, [vp, u32, vp, vp, vp, u32, vp]),
         "gdf_voxelize_runs": (i32, [vp, vp, vp, vp, u32, vp, vp, i32]),
+        "gdf_voxelize_runs_marked": (i32, [vp, vp, vp, vp, u32, vp, vp, i32, vp, u64]),
         "gdf_transform_points": (i32, [vp, vp, vp, vp, u32, vp]),
         "gdf_get_batch_ranges": (i32, [vp, vp, vp, u32, P(u32)]),
         "gdf_download_batch_occupancy_grid": (i32, [vp, u32, vp, u64]),
@@ -797,6 +798,18 @@ class GPUDepthmapFusion:
                                                 C.c_void_p(run_keys_ptr), C.c_void_p(run_starts_ptr),
                                                 len(pb) - 1, _ptr(pb), _ptr(rb),
                                                 1 if average else 0))
+
+    def voxelize_runs_marked(self, pts_ptr: int, run_keys_ptr: int, run_starts_ptr: int,
+                             point_base, run_base, marks_ptr: int, frame_stride_words: int,
+                             average: bool = True):
+        """voxelize_runs that also ORs every voxel's occupancy mark into marks_ptr (device, frame
+        f at f * frame_stride_words, zeroed by the caller; gdf_voxelize_runs_marked)."""
+        pb = np.ascontiguousarray(point_base, np.uint32)
+        rb = np.ascontiguousarray(run_base, np.uint32)
+        self._check(self._lib.gdf_voxelize_runs_marked(
+            self._h, C.c_void_p(pts_ptr), C.c_void_p(run_keys_ptr), C.c_void_p(run_starts_ptr),
+            len(pb) - 1, _ptr(pb), _ptr(rb), 1 if average else 0, C.c_void_p(marks_ptr),
+            frame_stride_words))
 
     # ---- orphan shaders (device buffers) ----
     def maskDilate(self, in_ptr: int, out_ptr: int, width: int, height: int, filter_size: int,

@@ -162,10 +162,17 @@ class BatchedMarkExchange:
 # reads the last F rows + F pixels of camera k-1 at its top border; the ranks
 # all-gather those tails (F*W + F depth values each) before the frame.
 
+def part_slice_words(nparts: int, ncells: int) -> int:
+    """Occupancy-mark words per key range: ceil(ceil(ncells / 32) / nparts)."""
+    return ((ncells + 31) // 32 + nparts - 1) // nparts
+
+
 def part_of_keys(keys: np.ndarray, nparts: int, ncells: int) -> np.ndarray:
-    """Key-range owner of each key: floor(key * nparts / ncells) (k_part_count's rule)."""
-    return np.minimum((keys.astype(np.uint64) * np.uint64(nparts)) // np.uint64(ncells),
-                      nparts - 1).astype(np.int64)
+    """Key-range owner of each key: min((key // 32) // S, nparts - 1), S = part_slice_words
+    (k_part_count's rule: whole mark words per rank, so rank j's voxels mark exactly slice j of
+    each frame's occupancy bitmask)."""
+    S = np.uint64(part_slice_words(nparts, ncells))
+    return np.minimum((keys.astype(np.uint64) >> np.uint64(5)) // S, nparts - 1).astype(np.int64)
 
 
 def halo_pixels(F: int, width: int) -> int:

@@ -186,7 +186,7 @@ def test_partition_runs_voxelize_runs_match_oracle(Engine, nparts, B, emit):
     the same send lists from gdf_set_emit_partition (the compaction writes them: k_mask_px +
     k_emit_px2 on the 256-pixel segments of frames over 1 Mi pixels; a single VGA frame takes the
     compaction + partition pass)."""
-    from ros_gpu_depthmap_fusion_amd import hiprt
+    from ros_gpu_depthmap_fusion_amd import hiprt, multi
     p = ComponentParams()
     cam = synth.make_camera(0, 640, 480)
     gpu, orc = Engine(), OracleFusion(threads=16)
@@ -211,12 +211,21 @@ def test_partition_runs_voxelize_runs_match_oracle(Engine, nparts, B, emit):
     assert (runs <= pts).all() and ((runs > 0) == (pts > 0)).all()
     P0, R0 = np.concatenate([[0], np.cumsum(pts)]), np.concatenate([[0], np.cumsum(runs)])
     h_rs = srs.to_numpy(np.uint32, max(n, 1))
-    want = []
+    # every part's voxel marks (gdf_voxelize_runs_marked): frame j at j * stride words; part q's
+    # keys are whole mark words [q S, (q + 1) S) (the fused step all-gathers those slices)
+    ncells = int(gpu.grid_size()[1])
+    words = (ncells + 31) // 32
+    S = multi.part_slice_words(nparts, ncells)
+    stride = S * nparts
+    union = np.zeros((B, stride), np.uint32)
+    want, want_marks = [], np.zeros((B, words), np.uint32)
     for j in range(B):
         orc.clear()
         orc.addDepthmap(*cam_args(cam, frames[j]))
         orc.processFrame(p)
         want.append(orc.downloadVoxelizedPoints()[:, :3])
+        k = np.unique(orc.downloadVoxelCoords().astype(np.int64))
+        np.bitwise_or.at(want_marks[j], k >> 5, (np.uint32(1) << (k & 31).astype(np.uint32)))
     got = [[] for _ in range(B)]
     for q in range(nparts):
         if pts[q] == 0:
@@ -231,7 +240,15 @@ def test_partition_runs_voxelize_runs_match_oracle(Engine, nparts, B, emit):
         if cut:
             local[cut:] -= rs[cut]
         drs = hiprt.DeviceArray.from_numpy(np.concatenate([local, np.zeros(1, np.uint32)]))
-        gpu.voxelize_runs(sp.ptr + 16 * int(P0[q]), srk.ptr + 4 * int(R0[q]), drs.ptr, pb, rb)
+        dmk = hiprt.DeviceArray.from_numpy(np.zeros(B * stride, np.uint32))
+        gpu.voxelize_runs_marked(sp.ptr + 16 * int(P0[q]), srk.ptr + 4 * int(R0[q]), drs.ptr, pb, rb,
+                                 dmk.ptr, stride)
+        gpu.synchronize()
+        mk = dmk.to_numpy(np.uint32, B * stride).reshape(B, stride)
+        outside = np.ones(stride, bool)
+        outside[q * S:(q + 1) * S] = False
+        assert not mk[:, outside].any(), (nparts, B, q)
+        union |= mk
         vox = gpu.downloadVoxelizedPoints()[:, :3]
         if B > 1:
             _, vs = gpu.batch_ranges()
@@ -243,3 +260,5 @@ def test_partition_runs_voxelize_runs_match_oracle(Engine, nparts, B, emit):
         g = np.concatenate(got[j]) if got[j] else np.zeros((0, 3), np.float32)
         assert len(g) == len(want[j]) > 0, (nparts, B, j)
         assert np.array_equal(g.view(np.uint32), want[j].view(np.uint32)), (nparts, B, j)
+        assert np.array_equal(union[j, :words], want_marks[j]), (nparts, B, j)
+        assert not union[j, words:].any()

@@ -166,9 +166,17 @@ def test_fused_cloud_equals_single_engine(tmp_path, world, F):
 
 
 def test_key_range_partition_rule():
-    """part_of_keys = floor(key * N / C): contiguous ascending ranges covering every key."""
+    """part_of_keys: contiguous ascending ranges of whole 32-key mark words covering every key."""
     ncells = 3_360_000
     keys = np.arange(0, ncells, 997, dtype=np.uint32)
     for n in (1, 2, 3, 7, 8, 16):
         part = multi.part_of_keys(keys, n, ncells)
         assert part.min() == 0 and part.max() == n - 1 and (np.diff(part) >= 0).all()
+        S = multi.part_slice_words(n, ncells)
+        assert S * n * 32 >= ncells
+        word = np.arange((ncells + 31) // 32, dtype=np.uint32)
+        # every key of a word has the word's part, and part j = words [j S, (j + 1) S)
+        for off in (0, 17, 31):
+            k = np.minimum(word * 32 + off, ncells - 1).astype(np.uint32)
+            pk = multi.part_of_keys(k, n, ncells)
+            np.testing.assert_array_equal(pk[k // 32 == word], np.minimum(word // S, n - 1)[k // 32 == word])
