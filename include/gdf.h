@@ -405,6 +405,10 @@ int gdf_partition_runs(gdf_engine* engine, uint32_t nparts, float* send_points_d
 int gdf_set_emit_partition(gdf_engine* engine, uint32_t nparts, float* send_points_device,
                            uint32_t* send_run_keys_device, uint32_t* send_run_starts_device,
                            uint32_t capacity, uint32_t* part_counts_device);
+/* Whether a deferred frame armed with gdf_set_emit_partition sets its occupancy marks (default 1).
+ * 0: a caller that builds the union from gdf_voxelize_runs_marked skips the compaction's marks
+ * (and their clear) - the frame then has no marks to take. */
+int gdf_set_partition_marks(gdf_engine* engine, int enabled);
 int gdf_voxelize_runs(gdf_engine* engine, const float* points_device,
                       const uint32_t* run_keys_device, uint32_t* run_starts_device,
                       uint32_t nsources, const uint32_t* point_base, const uint32_t* run_base,

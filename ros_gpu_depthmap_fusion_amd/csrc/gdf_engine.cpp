@@ -506,6 +506,9 @@ struct gdf_engine {
         uint32_t *run_keys = nullptr, *run_starts = nullptr, *counts = nullptr;
     } epart;
     bool emit_part = !getenv("GDF_NO_EMIT_PART");  // (else: compaction, then the partition pass)
+    // a frame armed with gdf_set_emit_partition sets its occupancy marks (gdf_set_partition_marks:
+    // off when the caller builds the union from the key-range voxelize, gdf_voxelize_runs_marked)
+    bool part_marks = true;
     bool dl_prefetch_allowed = !getenv("GDF_NO_DL_PREFETCH");
     // tuning knob GDF_DL_FORK: the points / coords part on a second stream right after the
     // compaction (direct launches) instead of in the chain's last kernel (graph replays)
@@ -1267,7 +1270,7 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel, bool compaction_marks = fa
         if (!e->sl().group_marks) {
             a.grid_seq_out = e->sl().d_misc.as<uint32_t>() + kGridTicket;
             a.grid_seq = e->grid_ticket;
-            a.marks = marks_ptr(e);
+            if (!(compaction_marks && e->epart.nparts && !e->part_marks)) a.marks = marks_ptr(e);
         }
         std::memcpy(a.vlo, e->vp.vlo, 12);
         std::memcpy(a.vcs, e->vp.vcs, 12);
@@ -1425,6 +1428,7 @@ void run_frame(gdf_engine* e, bool fused_voxel, bool compaction_marks = false) {
     if (e->profiling) e->timed(GDF_KERNEL_EVENT_FLOOR, [] {});  // calibrates the event overhead
     e->timed(GDF_KERNEL_FRAME, [&] { HIPCHK(launch_frame(a, e->s(), e->hook_ptr())); });
     frame_launched(e, fused_voxel, a.key_hist != nullptr, a.run_mode != 0);
+    if (fused_voxel && !a.marks && !e->sl().group_marks) e->sl().marks_set = false;  // (no marks)
     if (a.nparts) {  // (the points went to the send lists only: no compaction-order outputs)
         e->sl().coords_valid = false;
         e->sl().runs_valid = false;
@@ -2624,6 +2628,11 @@ int gdf_set_emit_partition(gdf_engine* e, uint32_t nparts, float* send_pts, uint
         e->epart.run_starts = send_run_starts;
         e->epart.counts = part_counts;
     });
+}
+
+int gdf_set_partition_marks(gdf_engine* e, int enabled) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] { e->part_marks = enabled != 0; });
 }
 
 int gdf_partition_runs(gdf_engine* e, uint32_t nparts, float* send_pts, uint32_t* send_run_keys,

@@ -130,7 +130,6 @@ struct DevBuf {
 
 struct SlotX {
     DevBuf tail, tails;       // this rank's halo tails, every rank's (all-gather)
-    DevBuf local;             // the compaction's occupancy marks of the step's frames (discarded)
     DevBuf gathered;          // the union of the step's marks: frame f at f * W * S words, rank
                               // j's key range in words [j S, (j + 1) S) (voxelize + all-gather)
     // partitioned send lists (points, run keys, run starts), split sizes (points then runs per
@@ -158,9 +157,12 @@ struct gdf_fused {
     SlotX slots[kSlots];
 
     ~gdf_fused() {
-        if (e) gdf_synchronize(e);
+        if (e) {
+            gdf_synchronize(e);
+            gdf_set_partition_marks(e, 1);  // (the engine's default again)
+        }
         for (SlotX& s : slots) {
-            for (DevBuf* b : {&s.tail, &s.tails, &s.local, &s.gathered, &s.sp, &s.srk, &s.srs,
+            for (DevBuf* b : {&s.tail, &s.tails, &s.gathered, &s.sp, &s.srk, &s.srs,
                               &s.cnt, &s.cntall, &s.rp, &s.rrk, &s.rrs})
                 b->release();
             if (s.host) hipHostFree(s.host);
@@ -246,18 +248,13 @@ void fused_start(gdf_fused* f, const uint16_t* const* depth, uint32_t B, const g
                                       S.srs.as<uint32_t>(), have, cnt));
     };
     arm(std::max<size_t>(want, 1));
+    gdfchk(gdf_set_partition_marks(e, 0));
     gdf_frame_result res{};
     gdfchk(gdf_process_frame(e, &q, &res));
-    uint32_t g[3];
-    uint64_t ncells = 0;
-    gdfchk(gdf_get_grid_size(e, g, &ncells));
-    const uint64_t words = (ncells + 31) / 32;
-    // The compaction's marks are not exchanged (W full bitmasks of B frames: 3.4 MB per rank and
-    // step at VGA x 8, received W - 1 times): the key-range voxelize of the finish marks every
-    // voxel of its range - whole mark words per range - and one in-place all-gather of those
-    // slices is the union (1 / W of the volume).  The frame's own marks are cleared here.
-    uint32_t* local = S.local.ensure<uint32_t>(B * words * 4, st);
-    gdfchk(gdf_take_occupancy_marks(e, local, B * words));
+    // The compaction sets no marks (gdf_set_partition_marks(e, 0) before the frame): W full
+    // bitmasks of B frames (3.4 MB per rank and step at VGA x 8, received W - 1 times) would travel;
+    // instead the key-range voxelize of the finish marks every voxel of its range - whole mark
+    // words per range - and one in-place all-gather of those slices is the union (1 / W).
     S.nframes = B;
     S.lifetime = q.occupancy_lifetime;
     // every rank's split sizes (the partition's, written with the compaction) to pinned memory
