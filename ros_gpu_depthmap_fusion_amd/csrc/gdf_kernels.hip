@@ -2403,12 +2403,16 @@ __device__ __forceinline__ uint32_t grid_seq_enter(const GridSeq& q) {
     return s_f;
 }
 
+// COHERENT: the block wrote the grid with agent-coherent stores (grid_store): once they have
+// completed they are visible to every XCD, and no per-block L2 write-back (an agent release fence,
+// buffer_wbl2, issued by each of hundreds of blocks) is needed before the block counts itself in
+template <bool COHERENT = false>
 __device__ __forceinline__ void grid_seq_leave(const GridSeq& q, uint32_t f, uint32_t nblocks) {
     if (!q.ctl) return;
-    __builtin_amdgcn_s_waitcnt(0);  // this wave's grid stores have reached L2
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's grid stores have completed
     __syncthreads();
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // L2 write-back: visible to all XCDs
+        if (!COHERENT) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // L2 write-back: visible to all XCDs
         const uint32_t c = atomicAdd(&q.ctl[1], 1u);
         if (c == nblocks - 1u) {
             atomicExch(&q.ctl[1], 0u);
@@ -2431,6 +2435,14 @@ __device__ __forceinline__ uint32_t grid_word(uint32_t w, uint32_t mb, uint32_t 
 
 // blocks [0, nblocks) of a launch update the u8 grid: 32 cells (two 16-byte vectors and one mark
 // word) per thread and step; the grid allocation is padded to 32 bytes
+// two grid words of 16 cells each as agent-scope (sc1) 64-bit stores: coherent across the XCDs
+// without an L2 write-back (grid_seq_leave<true>)
+__device__ __forceinline__ void grid_store(uint4* grid, uint64_t j, const uint4& v) {
+    unsigned long long* p = reinterpret_cast<unsigned long long*>(grid + j);
+    __hip_atomic_store(p, ((unsigned long long)v.y << 32) | v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(p + 1, ((unsigned long long)v.w << 32) | v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ void grid_u8_part(uint4* __restrict__ grid, uint32_t* __restrict__ marks,
                                              uint64_t nwords, uint32_t L, uint32_t block,
                                              uint32_t nblocks, const GridSeq& q) {
@@ -2456,8 +2468,8 @@ __device__ __forceinline__ void grid_u8_part(uint4* __restrict__ grid, uint32_t*
         v1.z = grid_word(o1.z, m >> 24, L);
         v1.w = grid_word(o1.w, m >> 28, L);
         if (act) {
-            grid[2 * i] = v0;
-            grid[2 * i + 1] = v1;
+            grid_store(grid, 2 * i, v0);
+            grid_store(grid, 2 * i + 1, v1);
             if (m) marks[i] = 0u;
         }
         if (q.dcnt) {  // the changed groups (a frame: the grid's ~1-2 % non-zero cells)
@@ -2574,8 +2586,8 @@ __device__ __forceinline__ void grid_u8_frames(uint4* __restrict__ grid, uint64_
             for (uint32_t f = 0; f < nframes; ++f) step(f, act ? mk(f, i) : 0u);
         }
         if (act) {
-            grid[2 * i] = v0;
-            grid[2 * i + 1] = v1;
+            grid_store(grid, 2 * i, v0);
+            grid_store(grid, 2 * i + 1, v1);
         }
     }
     if (keep_snaps && lane + 1 < nframes) sn.cnt[(uint64_t)lane * W + wave] = s_sc[wid][lane];
@@ -2642,7 +2654,7 @@ __global__ __launch_bounds__(256) void k_grid_u8(uint4* __restrict__ grid,
                                                  uint32_t L, GridSeq q) {
     const uint32_t f = grid_seq_enter(q);
     grid_u8_part(grid, marks, nwords, L, blockIdx.x, gridDim.x, q);
-    grid_seq_leave(q, f, gridDim.x);
+    grid_seq_leave<true>(q, f, gridDim.x);
 }
 
 static unsigned grid_blocks(uint64_t work, unsigned per_block) {
@@ -2686,7 +2698,7 @@ __global__ __launch_bounds__(256) void k_grid_u8_batch(uint4* __restrict__ grid,
                                if (f < nframes) mf[f] |= b[f * frame_stride];
                        }
                    });
-    grid_seq_leave(q, f0, gridDim.x);
+    grid_seq_leave<true>(q, f0, gridDim.x);
 }
 
 uint32_t g_grid_wpt = 2;  // mark words per thread of the grid blocks carried by radix pass 1 (GDF_GRID_WPT)
@@ -2912,7 +2924,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
         else
             grid_u8_part(grid, marks, grid_nwords, lifetime, blockIdx.x - grid_block0,
                          gridDim.x - grid_block0, q);
-        grid_seq_leave(q, f, gridDim.x - grid_block0);
+        grid_seq_leave<true>(q, f, gridDim.x - grid_block0);
         return;
     }
     __shared__ uint32_t s_fstart[kMaxCams + 1];
