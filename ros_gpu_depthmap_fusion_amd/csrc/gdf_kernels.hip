@@ -2381,6 +2381,9 @@ hipError_t launch_gather_records(const void* rec, uint32_t n, uint32_t step, flo
 // streams (frame pipelining): update f waits until ctl[0] == f (updates completed), and the last
 // of its blocks to finish publishes ctl[0] = f + 1.  f comes from the host (the kernel argument,
 // or a per-slot word the frame's k_mask stored).  ctl == nullptr: no ordering (one stream).
+// COHERENT: the block reads the grid with agent-coherent loads (grid_load), so no per-block L2
+// invalidate (an agent acquire fence, buffer_inv) is needed after the wait
+template <bool COHERENT = false>
 __device__ __forceinline__ uint32_t grid_seq_enter(const GridSeq& q) {
     __shared__ uint32_t s_f;
     if (!q.ctl) return 0;
@@ -2396,7 +2399,7 @@ __device__ __forceinline__ uint32_t grid_seq_enter(const GridSeq& q) {
             }
             __builtin_amdgcn_s_sleep(8);
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the previous update's grid
+        if (!COHERENT) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the previous update's grid
         s_f = f;
     }
     __syncthreads();
@@ -2443,6 +2446,13 @@ __device__ __forceinline__ void grid_store(uint4* grid, uint64_t j, const uint4&
     __hip_atomic_store(p + 1, ((unsigned long long)v.w << 32) | v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+__device__ __forceinline__ uint4 grid_load(const uint4* grid, uint64_t j) {
+    const unsigned long long* p = reinterpret_cast<const unsigned long long*>(grid + j);
+    const unsigned long long a = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long b = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+}
+
 __device__ __forceinline__ void grid_u8_part(uint4* __restrict__ grid, uint32_t* __restrict__ marks,
                                              uint64_t nwords, uint32_t L, uint32_t block,
                                              uint32_t nblocks, const GridSeq& q) {
@@ -2454,8 +2464,8 @@ __device__ __forceinline__ void grid_u8_part(uint4* __restrict__ grid, uint32_t*
         uint4 o0 = make_uint4(0u, 0u, 0u, 0u), o1 = o0;
         uint32_t m = 0;
         if (act) {
-            o0 = grid[2 * i];
-            o1 = grid[2 * i + 1];
+            o0 = grid_load(grid, 2 * i);
+            o1 = grid_load(grid, 2 * i + 1);
             m = marks[i];
         }
         uint4 v0, v1;
@@ -2537,8 +2547,8 @@ __device__ __forceinline__ void grid_u8_frames(uint4* __restrict__ grid, uint64_
         const bool act = i < nwords;
         uint4 v0 = make_uint4(0u, 0u, 0u, 0u), v1 = v0;
         if (act) {
-            v0 = grid[2 * i];
-            v1 = grid[2 * i + 1];
+            v0 = grid_load(grid, 2 * i);
+            v1 = grid_load(grid, 2 * i + 1);
         }
         auto step = [&](uint32_t f, uint32_t m) {
             v0.x = grid_word(v0.x, m, L);
@@ -2652,7 +2662,7 @@ hipError_t launch_snap_expand(const SnapArgs& sn, uint32_t frame, uint32_t nbloc
 __global__ __launch_bounds__(256) void k_grid_u8(uint4* __restrict__ grid,
                                                  uint32_t* __restrict__ marks, uint64_t nwords,
                                                  uint32_t L, GridSeq q) {
-    const uint32_t f = grid_seq_enter(q);
+    const uint32_t f = grid_seq_enter<true>(q);
     grid_u8_part(grid, marks, nwords, L, blockIdx.x, gridDim.x, q);
     grid_seq_leave<true>(q, f, gridDim.x);
 }
@@ -2682,7 +2692,7 @@ __global__ __launch_bounds__(256) void k_grid_u8_batch(uint4* __restrict__ grid,
                                                        uint32_t nframes, uint64_t frame_stride,
                                                        uint64_t rank_stride, uint32_t L,
                                                        GridSeq q, SnapArgs sn) {
-    const uint32_t f0 = grid_seq_enter(q);
+    const uint32_t f0 = grid_seq_enter<true>(q);
     grid_u8_frames(grid, nwords, L, blockIdx.x, gridDim.x, nframes,
                    [&](uint32_t f, uint64_t i) {
                        uint32_t m = 0;
@@ -2917,7 +2927,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
         qreset[2] = 0u;
     }
     if (blockIdx.x >= grid_block0) {  // fused historic-grid update (first pass only)
-        const uint32_t f = grid_seq_enter(q);
+        const uint32_t f = grid_seq_enter<true>(q);
         if (nframes > 1)
             grid_u8_part_frames(grid, marks, grid_nwords, lifetime, blockIdx.x - grid_block0,
                                 gridDim.x - grid_block0, nframes, mark_words, snap);
