@@ -83,7 +83,9 @@ class StagingCopier {
         for (const Job& j : jobs) total += j.bytes;
         if (total == 0) return;
         const unsigned nt = threads();
-        if (nt <= 1 || total < 2 * kChunk) {
+        // (one frame - the synchronous component path - is copied by the caller alone: waking
+        // the workers costs more latency than they save on 0.6 MB; batches use them)
+        if (nt <= 1 || total < kMinParallel) {
             for (const Job& j : jobs) std::memcpy(j.dst, j.src, j.bytes);
             return;
         }
@@ -116,6 +118,7 @@ class StagingCopier {
         size_t left = 0;          // chunks not yet copied (guarded by m_)
     };
     static constexpr size_t kChunk = 256 << 10;
+    static constexpr size_t kMinParallel = 2 << 20;
     unsigned threads() {
         if (!nthreads_) {
             const char* s = std::getenv("GDF_H2D_THREADS");

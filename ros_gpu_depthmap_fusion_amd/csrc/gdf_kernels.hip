@@ -2446,6 +2446,76 @@ __device__ __forceinline__ void grid_store(uint4* grid, uint64_t j, const uint4&
     __hip_atomic_store(p + 1, ((unsigned long long)v.w << 32) | v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The wave's 64 grid words (2 KB from uint4 2 i0) through 2 KB of LDS per wave: two coalesced 1-KB
+// agent-coherent (sc1) buffer accesses per direction.  Per lane at a 32-B stride, the coherent
+// accesses reach memory sector by sector - four 8-B stores per 32-B sector measured the grid's
+// writes at ~4x its bytes (PMC WRITE_SIZE of the carrying radix pass).  Past the grid (the last
+// wave's idle lanes) the buffer range check returns 0 / drops the store.  Grids of 2 GB and more
+// take the per-lane form.
+__device__ __forceinline__ uint4* grid_xbuf() {
+    __shared__ uint4 s_gx[4][128];
+    return &s_gx[threadIdx.x >> 6][0];
+}
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+typedef uint32_t gx4 __attribute__((ext_vector_type(4)));
+constexpr int kCpolSc1 = 16;  // buffer cache policy: sc1 (agent scope)
+
+__device__ __forceinline__ uint4 grid_load(const uint4* grid, uint64_t j);
+__device__ __forceinline__ void grid_store(uint4* grid, uint64_t j, const uint4& v);
+
+__device__ __forceinline__ void grid_wave_load(const uint4* grid, uint64_t nwords, uint64_t i0,
+                                               uint4& v0, uint4& v1) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t bytes = nwords * 32u;
+    if (bytes < (1ull << 31)) {
+        uint4* sx = grid_xbuf();
+        const __amdgpu_buffer_rsrc_t r =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(grid), 0, (int)bytes, 0x00020000);
+        const uint32_t base = (uint32_t)(i0 * 32u) + lane * 16u;
+        const gx4 a = __builtin_amdgcn_raw_buffer_load_b128(r, base, 0, kCpolSc1);
+        const gx4 b = __builtin_amdgcn_raw_buffer_load_b128(r, base + 1024u, 0, kCpolSc1);
+        sx[lane] = make_uint4(a.x, a.y, a.z, a.w);
+        sx[64 + lane] = make_uint4(b.x, b.y, b.z, b.w);
+        wave_lds_sync();
+        v0 = sx[2 * lane];
+        v1 = sx[2 * lane + 1];
+        wave_lds_sync();  // (the buffer is free again)
+    } else if (i0 + lane < nwords) {
+        v0 = grid_load(grid, 2 * (i0 + lane));
+        v1 = grid_load(grid, 2 * (i0 + lane) + 1);
+    } else {
+        v0 = v1 = make_uint4(0u, 0u, 0u, 0u);
+    }
+}
+
+__device__ __forceinline__ void grid_wave_store(uint4* grid, uint64_t nwords, uint64_t i0,
+                                                const uint4& v0, const uint4& v1) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t bytes = nwords * 32u;
+    if (bytes < (1ull << 31)) {
+        uint4* sx = grid_xbuf();
+        sx[2 * lane] = v0;
+        sx[2 * lane + 1] = v1;
+        wave_lds_sync();
+        const uint4 a = sx[lane], b = sx[64 + lane];
+        wave_lds_sync();
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(grid, 0, (int)bytes, 0x00020000);
+        const uint32_t base = (uint32_t)(i0 * 32u) + lane * 16u;
+        gx4 va, vb;
+        va.x = a.x; va.y = a.y; va.z = a.z; va.w = a.w;
+        vb.x = b.x; vb.y = b.y; vb.z = b.z; vb.w = b.w;
+        __builtin_amdgcn_raw_buffer_store_b128(va, r, base, 0, kCpolSc1);
+        __builtin_amdgcn_raw_buffer_store_b128(vb, r, base + 1024u, 0, kCpolSc1);
+    } else if (i0 + lane < nwords) {
+        grid_store(grid, 2 * (i0 + lane), v0);
+        grid_store(grid, 2 * (i0 + lane) + 1, v1);
+    }
+}
+
 __device__ __forceinline__ uint4 grid_load(const uint4* grid, uint64_t j) {
     const unsigned long long* p = reinterpret_cast<const unsigned long long*>(grid + j);
     const unsigned long long a = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2463,11 +2533,8 @@ __device__ __forceinline__ void grid_u8_part(uint4* __restrict__ grid, uint32_t*
         const bool act = i < nwords;
         uint4 o0 = make_uint4(0u, 0u, 0u, 0u), o1 = o0;
         uint32_t m = 0;
-        if (act) {
-            o0 = grid_load(grid, 2 * i);
-            o1 = grid_load(grid, 2 * i + 1);
-            m = marks[i];
-        }
+        grid_wave_load(grid, nwords, i0, o0, o1);
+        if (act) m = marks[i];
         uint4 v0, v1;
         v0.x = grid_word(o0.x, m, L);
         v0.y = grid_word(o0.y, m >> 4, L);
@@ -2477,11 +2544,8 @@ __device__ __forceinline__ void grid_u8_part(uint4* __restrict__ grid, uint32_t*
         v1.y = grid_word(o1.y, m >> 20, L);
         v1.z = grid_word(o1.z, m >> 24, L);
         v1.w = grid_word(o1.w, m >> 28, L);
-        if (act) {
-            grid_store(grid, 2 * i, v0);
-            grid_store(grid, 2 * i + 1, v1);
-            if (m) marks[i] = 0u;
-        }
+        grid_wave_store(grid, nwords, i0, v0, v1);
+        if (act && m) marks[i] = 0u;
         if (q.dcnt) {  // the changed groups (a frame: the grid's ~1-2 % non-zero cells)
             const bool ch = act && ((o0.x ^ v0.x) | (o0.y ^ v0.y) | (o0.z ^ v0.z) | (o0.w ^ v0.w) |
                                     (o1.x ^ v1.x) | (o1.y ^ v1.y) | (o1.z ^ v1.z) | (o1.w ^ v1.w)) != 0u;
@@ -2546,10 +2610,7 @@ __device__ __forceinline__ void grid_u8_frames(uint4* __restrict__ grid, uint64_
         const uint64_t i = i0 + lane;
         const bool act = i < nwords;
         uint4 v0 = make_uint4(0u, 0u, 0u, 0u), v1 = v0;
-        if (act) {
-            v0 = grid_load(grid, 2 * i);
-            v1 = grid_load(grid, 2 * i + 1);
-        }
+        grid_wave_load(grid, nwords, i0, v0, v1);
         auto step = [&](uint32_t f, uint32_t m) {
             v0.x = grid_word(v0.x, m, L);
             v0.y = grid_word(v0.y, m >> 4, L);
@@ -2595,10 +2656,7 @@ __device__ __forceinline__ void grid_u8_frames(uint4* __restrict__ grid, uint64_
         } else {
             for (uint32_t f = 0; f < nframes; ++f) step(f, act ? mk(f, i) : 0u);
         }
-        if (act) {
-            grid_store(grid, 2 * i, v0);
-            grid_store(grid, 2 * i + 1, v1);
-        }
+        grid_wave_store(grid, nwords, i0, v0, v1);
     }
     if (keep_snaps && lane + 1 < nframes) sn.cnt[(uint64_t)lane * W + wave] = s_sc[wid][lane];
 }
