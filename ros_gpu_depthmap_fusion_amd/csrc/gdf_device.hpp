@@ -185,8 +185,7 @@ struct FrameArgs {
     // counts into group-local offsets (seg_offsets) and the group totals (grp_tot: point totals,
     // then run totals); k_emit adds the totals of the groups before its own
     uint32_t* grp_done;         // [groups] arrival counters (self-resetting)
-    uint32_t* grp_tot;          // [2 * groups] ([2 P * groups] in part mode)
-    uint32_t* grp_base;         // part mode: [2 P * groups] channel base + groups before (top-level scan)
+    uint32_t* grp_tot;          // [2 * groups]
     int32_t mask_packed;        // k_mask_px<2>: both pixels of a thread in packed f32 ops
     // emit partition (multi-GPU fused cloud, gdf_set_emit_partition): the compaction writes the
     // key-range partition itself - k_mask_px counts each segment's kept points and runs per part

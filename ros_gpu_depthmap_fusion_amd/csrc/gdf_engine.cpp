@@ -342,7 +342,6 @@ struct Slot {
     DevBuf d_pcnt, d_poff;          // multi-GPU key-range partition workspace
     DevBuf d_xcnt, d_xoff, d_xrk, d_xrs;  // runs of a received (point, key) list
     DevBuf d_grpdone, d_grptot;     // in-kernel group scan of the segment counts
-    DevBuf d_grpbase;               // (part mode: the top-level scan's group bases)
     struct Pinned {                 // pinned host mirror (gdf_download_frame)
         void* p = nullptr;
         size_t bytes = 0;
@@ -513,7 +512,6 @@ struct gdf_engine {
     // a frame armed with gdf_set_emit_partition sets its occupancy marks (gdf_set_partition_marks:
     // off when the caller builds the union from the key-range voxelize, gdf_voxelize_runs_marked)
     bool part_marks = true;
-    bool part_group_scan = !getenv("GDF_NO_PART_GROUP_SCAN");  // (else: the scan launches)
     bool dl_prefetch_allowed = !getenv("GDF_NO_DL_PREFETCH");
     // tuning knob GDF_DL_FORK: the points / coords part on a second stream right after the
     // compaction (direct launches) instead of in the chain's last kernel (graph replays)
@@ -1388,21 +1386,11 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel, bool compaction_marks = fa
         t.run_mode = 1;
         t.key_hist = nullptr;
         t.fused_prefix = 0;
-        t.grp_done = t.grp_tot = t.grp_base = nullptr;
+        t.grp_done = t.grp_tot = nullptr;
         if (emit_partition_kernels(t)) {
             Slot& q = e->sl();
             const uint32_t segs = std::max<uint32_t>(a.total_segs, 1);
             const uint32_t P = e->epart.nparts;
-            const uint32_t ng = (segs + kScanGroup - 1) / kScanGroup;
-            if (e->group_scan && e->part_group_scan && ng <= kMaxScanGroups) {
-                // the 2P series scanned in k_mask_px (two-level group hand-off), no scan launches
-                q.d_grpdone.ensure_zero((size_t)ng * 4, e->s());  // (self-resetting afterwards)
-                q.d_grptot.ensure((size_t)ng * 2 * P * 4);
-                q.d_grpbase.ensure((size_t)ng * 2 * P * 4);
-                t.grp_done = q.d_grpdone.as<uint32_t>();
-                t.grp_tot = q.d_grptot.as<uint32_t>();
-                t.grp_base = q.d_grpbase.as<uint32_t>();
-            }
             q.d_tcounts.ensure((size_t)segs * 2 * P * 4);
             q.d_toffsets.ensure(seg_offsets_words(2 * P * segs) * 4);
             q.d_wruns.ensure((size_t)segs * 16 * 4);

@@ -720,83 +720,9 @@ __device__ __forceinline__ void arrive_and_scan(uint32_t* done, const uint32_t* 
     if (lane == 0) __hip_atomic_store(done + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Part mode (the emit partition): the 2P series [points of part p | runs of part p][segment] in
-// channel-major order, scanned by the same group hand-off into group-local offsets and group
-// totals; k_part_base (one wave) then scans the group totals in channel order - one small launch
-// instead of k_scan_reduce + k_scan_counts.  The counts were
-// stored sc1 by threads < 2P, each drained by its own vmcnt(0) before the block barrier.
-struct PartScan {  // (the fields of FrameArgs the part-mode hand-off touches, by value)
-    uint32_t *done, *cnt, *off, *gtot, *gbase, *part_counts, *out_count;
-    uint32_t nparts, TS;
-};
-__device__ __forceinline__ void arrive_and_scan_parts(const PartScan& a, uint32_t s, uint32_t* s_last) {
-    const uint32_t nser = 2u * a.nparts, TS = a.TS;
-    const uint32_t ng = (TS + kScanGroup - 1) / kScanGroup;
-    const uint32_t g = s / kScanGroup, s0 = g * kScanGroup;
-    const uint32_t n = min(kScanGroup, TS - s0);
-    __syncthreads();  // (every count of this block has been stored and drained)
-    if (threadIdx.x == 0) {
-        const uint32_t old = __hip_atomic_fetch_add(a.done + g, 1u, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-        *s_last = old + 1u == n ? 1u : 0u;
-    }
-    __syncthreads();
-    if (!*s_last || threadIdx.x >= 64) return;  // block-uniform, then wave 0
-    const uint32_t lane = threadIdx.x;
-    for (uint32_t q = 0; q < nser; ++q) {
-        const uint32_t base = q * TS;
-        const uint32_t v = lane < n ? __hip_atomic_load(a.cnt + base + s0 + lane, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT)
-                                    : 0u;
-        uint32_t x = v;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o, 64);
-            if (lane >= (uint32_t)o) x += y;
-        }
-        if (lane < n) G(a.off)[base + s0 + lane] = x - v;
-        if (lane == 63) G(a.gtot)[q * ng + g] = x;
-    }
-    if (lane == 0) __hip_atomic_store(a.done + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// The top level of the part-mode scan (one wave, after k_mask_px): every channel's group totals
-// in channel order into gbase (channel base + the groups before), the parts' sizes and the kept
-// points.  (In k_mask_px itself, as a second hand-off, this loop made the compiler keep a private
-// copy of the 2 KB kernel-argument struct: 2.2 KB of scratch per lane.)
-__global__ __launch_bounds__(64) void k_part_base(PartScan a) {
-    const uint32_t lane = threadIdx.x;
-    const uint32_t nser = 2u * a.nparts;
-    const uint32_t ng = (a.TS + kScanGroup - 1) / kScanGroup;
-    uint32_t run = 0;
-    for (uint32_t q = 0; q < nser; ++q) {
-        const uint32_t before = run;
-        for (uint32_t t0 = 0; t0 < ng; t0 += 64) {
-            const uint32_t t = t0 + lane;
-            const uint32_t v = t < ng ? a.gtot[q * ng + t] : 0u;
-            uint32_t x = v;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = __shfl_up(x, o, 64);
-                if (lane >= (uint32_t)o) x += y;
-            }
-            if (t < ng) a.gbase[q * ng + t] = run + x - v;
-            run += __shfl(x, 63, 64);
-        }
-        if (lane == 0) a.part_counts[q] = run - before;
-        if (lane == 0 && q + 1 == a.nparts) *a.out_count = run;  // (the kept points)
-    }
-}
-
 __device__ __forceinline__ void group_scan_tail(const FrameArgs& a, uint32_t s) {
     __shared__ uint32_t s_last;
     if (!a.grp_done) return;
-    if (a.nparts && a.grp_base) {
-        const PartScan ps{a.grp_done, a.seg_counts, a.seg_offsets, a.grp_tot, a.grp_base, a.part_counts,
-                          a.out_count, a.nparts, a.total_segs};
-        arrive_and_scan_parts(ps, s, &s_last);
-        return;
-    }
     arrive_and_scan(a.grp_done, a.seg_counts, a.seg_offsets, a.grp_tot, s, a.total_segs,
                     a.run_mode ? 2 : 1, a.total_segs, &s_last);
 }
@@ -1438,14 +1364,7 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
             const uint32_t kind = threadIdx.x / a.nparts, p = threadIdx.x % a.nparts;
             uint32_t c = 0;
             for (int w = 0; w < NWORDS; ++w) c += s_pc[kind][w][p];
-            if (a.grp_done) {  // (the group scan's hand-off: stored sc1 and drained)
-                publish_count(a.seg_counts + (size_t)threadIdx.x * a.total_segs + s, c);
-                // (the builtin, not asm with a memory clobber: that would make the compiler keep
-                // a private copy of the 2 KB kernel-argument struct, 2.2 KB of scratch per lane)
-                __builtin_amdgcn_s_waitcnt(0);
-            } else {
-                G(a.seg_counts)[(size_t)threadIdx.x * a.total_segs + s] = c;
-            }
+            G(a.seg_counts)[(size_t)threadIdx.x * a.total_segs + s] = c;
         }
     } else if (threadIdx.x == 0) {
         uint32_t tt = 0, r = 0;
@@ -1811,19 +1730,12 @@ __device__ __forceinline__ void emit_px2_parts(const FrameArgs& a, uint32_t* s_m
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t s = blockIdx.x, P = a.nparts, TS = a.total_segs;
     for (uint32_t j = threadIdx.x; j < 2u * NWORDS * kMaxParts; j += NT) (&s_pc[0][0][0])[j] = 0u;
-    const uint32_t ng = (TS + kScanGroup - 1) / kScanGroup, gs = s / kScanGroup;
     if (threadIdx.x < 2u * P) {
         const uint32_t kind = threadIdx.x / P, p = threadIdx.x % P;
-        if (a.grp_base) {  // (in-kernel group scan: channel base + groups before + in-group offset)
-            s_off[kind][p] = G(a.grp_base)[(size_t)threadIdx.x * ng + gs] + G(a.seg_offsets)[(size_t)threadIdx.x * TS + s];
-            if (kind == 0) s_first[p] = G(a.grp_base)[(size_t)p * ng];
-        } else {
-            s_off[kind][p] = G(a.seg_offsets)[(size_t)threadIdx.x * TS + s];
-            if (kind == 0) s_first[p] = G(a.seg_offsets)[(size_t)p * TS];
-        }
+        s_off[kind][p] = G(a.seg_offsets)[(size_t)threadIdx.x * TS + s];
+        if (kind == 0) s_first[p] = G(a.seg_offsets)[(size_t)p * TS];
     }
-    if (threadIdx.x == 0)  // (the kept points)
-        s_tot = a.grp_base ? G(a.grp_base)[(size_t)P * ng] : G(a.seg_offsets)[(size_t)P * TS];
+    if (threadIdx.x == 0) s_tot = G(a.seg_offsets)[(size_t)P * TS];  // (the kept points)
     __syncthreads();  // (the zeroed counters and the mark cache before any wave writes them)
     const gptr<const CamDesc> cams = G(cam_table(a));
     const uint32_t i = threadIdx.x;
@@ -1905,7 +1817,7 @@ __device__ __forceinline__ void emit_px2_parts(const FrameArgs& a, uint32_t* s_m
             G(a.part_run_starts)[rpos] = pos - s_first[p];
         }
     }
-    if (!a.grp_base && s == gridDim.x - 1 && threadIdx.x < 2u * P) {  // the parts' sizes from the scan
+    if (s == gridDim.x - 1 && threadIdx.x < 2u * P) {  // the parts' sizes from the scan
         const uint32_t kind = threadIdx.x / P, p = threadIdx.x % P;
         const uint32_t a0 = G(a.seg_offsets)[(size_t)threadIdx.x * TS];
         const uint32_t a1 = threadIdx.x + 1 < 2u * P ? G(a.seg_offsets)[(size_t)(threadIdx.x + 1) * TS]
@@ -2277,13 +2189,7 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
                 hipLaunchKernelGGL((k_mask<false, 0>), dim3(a.total_segs), dim3(a.seg_threads), lds, s, a);
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
-        if (a.nparts && a.grp_base) {  // part mode: the top level of the in-kernel group scan
-            HookScope hs(hook, GDF_KERNEL_SCAN);
-            const PartScan ps{a.grp_done, a.seg_counts, a.seg_offsets, a.grp_tot, a.grp_base, a.part_counts,
-                              a.out_count, a.nparts, a.total_segs};
-            hipLaunchKernelGGL(k_part_base, dim3(1), dim3(64), 0, s, ps);
-            if ((e = hipGetLastError()) != hipSuccess) return e;
-        } else if (!a.fused_prefix && !a.grp_done) {  // (run mode: the point counts, then the run counts)
+        if (!a.fused_prefix && !a.grp_done) {  // (run mode: the point counts, then the run counts)
             HookScope hs(hook, GDF_KERNEL_SCAN);
             const uint32_t m = a.nparts ? 2u * a.nparts * a.total_segs
                                         : a.run_mode ? 2u * a.total_segs : a.total_segs;
