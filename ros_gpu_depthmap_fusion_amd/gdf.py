@@ -800,6 +800,11 @@ class GPUDepthmapFusion:
                                                 len(pb) - 1, _ptr(pb), _ptr(rb),
                                                 1 if average else 0))
 
+    def set_partition_marks(self, enabled: bool):
+        """Whether frames armed with set_emit_partition set their occupancy marks
+        (gdf_set_partition_marks; off when the union comes from voxelize_runs_marked)."""
+        self._check(self._lib.gdf_set_partition_marks(self._h, 1 if enabled else 0))
+
     def voxelize_runs_marked(self, pts_ptr: int, run_keys_ptr: int, run_starts_ptr: int,
                              point_base, run_base, marks_ptr: int, frame_stride_words: int,
                              average: bool = True):

@@ -328,7 +328,7 @@ class FusedCloudRank:
     mark / count collectives."""
 
     def __init__(self, engine, cams, rank: int, world: int, params, dev: str = "cuda",
-                 depth: int = 1):
+                 depth: int = 1, mark_slices: bool = False):
         import torch
         import torch.distributed as dist
         from . import hiprt
@@ -363,6 +363,12 @@ class FusedCloudRank:
         self._pc_move = {}  # to_c of the frames with move transforms (rollbuffer rank)
         self._staged = {}   # gloo path: the host-staged lists of a started batch
         self._keep = []
+        # gloo path: the occupancy union as the C++ step builds it (gdf_fused.cpp) - no compaction
+        # marks; the key-range voxelize marks its voxels (whole mark words per range,
+        # part_of_keys) and the ranks all-gather those slices, not their full bitmasks
+        self.mark_slices = bool(mark_slices) and dev != "cuda"
+        if hasattr(engine, "set_partition_marks"):  # (the CPU tests' oracle stand-in has none)
+            engine.set_partition_marks(not self.mark_slices)
 
     def frame_params(self, move=None):
         """The frame's gdf_frame_params: `move` = (T_world_move, T_crop_move) when the component's
@@ -487,6 +493,9 @@ class FusedCloudRank:
                 S.host[2 * self.world:].copy_(S.rc.view(-1), non_blocking=True)
                 S.ev.record(st)
                 S.pending = True
+            elif self.mark_slices:  # (the union after the voxelize: finish)
+                eng.synchronize()
+                self._staged[k] = ((B, words, ncells), dsp, drk, drs, dcnt)
             else:
                 dl = h.DeviceArray(B * words * 4)
                 eng.take_marks(dl.ptr, B * words)
@@ -547,10 +556,30 @@ class FusedCloudRank:
         drp = h.DeviceArray.from_numpy(rp.numpy()) if n else None
         drk2 = h.DeviceArray.from_numpy(rrk.numpy()) if R else None
         drs2 = h.DeviceArray.from_numpy(np.concatenate([rrs.numpy(), np.zeros(1, np.int32)]))
-        eng.voxelize_runs(drp.ptr if n else 0, drk2.ptr if R else 0, drs2.ptr,
-                          np.cumsum([0] + rc), np.cumsum([0] + rr), self.p.voxel_average)
+        if not self.mark_slices:
+            eng.voxelize_runs(drp.ptr if n else 0, drk2.ptr if R else 0, drs2.ptr,
+                              np.cumsum([0] + rc), np.cumsum([0] + rr), self.p.voxel_average)
+            eng.synchronize()
+            self._keep = [dg, drp, drk2, drs2]
+            return counts
+        B, words, ncells = dg
+        Sw = part_slice_words(self.world, ncells)
+        stride = Sw * self.world
+        dmk = h.DeviceArray.from_numpy(np.zeros(B * stride, np.uint32))
+        eng.voxelize_runs_marked(drp.ptr if n else 0, drk2.ptr if R else 0, drs2.ptr,
+                                 np.cumsum([0] + rc), np.cumsum([0] + rr), dmk.ptr, stride,
+                                 self.p.voxel_average)
         eng.synchronize()
-        self._keep = [dg, drp, drk2, drs2]
+        mk = dmk.to_numpy(np.uint32, B * stride).reshape(B, stride)
+        mine = torch.from_numpy(np.ascontiguousarray(
+            mk[:, self.rank * Sw:(self.rank + 1) * Sw]).view(np.int32))
+        parts = [torch.empty_like(mine) for _ in range(self.world)]
+        dist.all_gather(parts, mine)  # (each rank's slice of every frame)
+        union = np.concatenate([q.numpy().view(np.uint32) for q in parts], axis=1)
+        du = h.DeviceArray.from_numpy(np.ascontiguousarray(union))
+        eng.voxelOccupancyGridBatch(du.ptr, words, 1, B, stride, B * stride, self.p.occupancy_lifetime)
+        eng.synchronize()
+        self._keep = [du, dmk, drp, drk2, drs2]
         return counts
 
     def run(self, steps, depth_ptrs_of, tail_ptrs_of, move_of=None, on_finish=None):

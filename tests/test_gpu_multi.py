@@ -88,7 +88,7 @@ def test_two_rank_fused_cloud_hip(tmp_path, F):
                                           orc.downloadVoxelOccupancyGrid(), f"frame {f} rank {r}")
 
 
-def _rank_batch(rank, world, port, F, out_dir, nf=FRAMES):
+def _rank_batch(rank, world, port, F, out_dir, nf=FRAMES, mark_slices=False):
     import torch.distributed as dist
     from ros_gpu_depthmap_fusion_amd import build_library, hiprt, multi
     from ros_gpu_depthmap_fusion_amd.gdf import GPUDepthmapFusion
@@ -98,7 +98,7 @@ def _rank_batch(rank, world, port, F, out_dir, nf=FRAMES):
     p = params(F)
     cams = [synth.make_camera(k, W, H) for k in range(world)]
     eng = GPUDepthmapFusion(0)
-    fr = multi.FusedCloudRank(eng, cams, rank, world, p, dev="cpu")
+    fr = multi.FusedCloudRank(eng, cams, rank, world, p, dev="cpu", mark_slices=mark_slices)
     n = W * H
     ds = [hiprt.DeviceArray.from_numpy(synth.dense_frame(cams[rank], rank, f)) for f in range(nf)]
     fr.batch([d.ptr for d in ds], [d.ptr + 2 * (n - fr.Lmax) for d in ds])
@@ -111,18 +111,22 @@ def _rank_batch(rank, world, port, F, out_dir, nf=FRAMES):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("F,nf", [(0, FRAMES), (4, FRAMES), (4, 8)])
-def test_two_rank_fused_cloud_hip_batch(tmp_path, F, nf):
+@pytest.mark.parametrize("F,nf,slices", [(0, FRAMES, False), (4, FRAMES, False), (4, 8, False),
+                                          (4, FRAMES, True), (0, 8, True)])
+def test_two_rank_fused_cloud_hip_batch(tmp_path, F, nf, slices):
     """FusedCloudRank.batch: the three frames of each rank in one launch chain and one exchange
     (a halo per frame, the frames' marks in one all-gather + one batched grid update, the
     (point, frame | key) lists partitioned by key range): per frame, the ranks' voxel ranges
     concatenated equal one oracle engine over both cameras, and the grid after the batch equals
     the oracle's after the three frames - bit for bit.  8 frames: (frame | key) keys of 25 bits,
-    sorted by gdf_voxelize_points in 3 passes with a 9-bit last digit."""
+    sorted by gdf_voxelize_points in 3 passes with a 9-bit last digit.  slices: the occupancy
+    union as the C++ step builds it - no compaction marks, every rank's key-range voxelize marks
+    its voxels (gdf_voxelize_runs_marked) and the ranks all-gather their slices of the bitmasks -
+    at world 2 through the HIP kernels (RCCL cannot put two ranks on one GPU)."""
     from oracle import OracleFusion
     world = 2
-    mp.start_processes(_rank_batch, args=(world, _free_port(), F, str(tmp_path), nf), nprocs=world,
-                       join=True, start_method="spawn")
+    mp.start_processes(_rank_batch, args=(world, _free_port(), F, str(tmp_path), nf, slices),
+                       nprocs=world, join=True, start_method="spawn")
     p = params(F)
     cams = [synth.make_camera(k, W, H) for k in range(world)]
     orc = OracleFusion(threads=4)
