@@ -266,7 +266,8 @@ def test_rccl_fused_cloud_world1(tmp_path, native):
 
 
 # ---- the rollbuffer leg: point sequences on the last rank -----------------
-def _rank_rb(rank, world, port, W_, H_, LW, LH, first, win, frames, out_dir, launch_defaults):
+def _rank_rb(rank, world, port, W_, H_, LW, LH, first, win, frames, out_dir, launch_defaults,
+             mark_slices=False):
     """One rank of a fused run WITH the rollbuffer: the last rank ingests the point sequences of
     fused_ref.schedule (device PointCloud2 records, gdf_add_point_sequence_device) and sends its
     selected points behind its camera's (multi.FusedCloudRank.frame(move=...))."""
@@ -281,7 +282,7 @@ def _rank_rb(rank, world, port, W_, H_, LW, LH, first, win, frames, out_dir, lau
     p.ps_timespan = (win - 0.5) / 30.0
     cams = [synth.make_camera(k, W_, H_) for k in range(world)]
     eng = GPUDepthmapFusion(0)
-    fr = multi.FusedCloudRank(eng, cams, rank, world, p, dev="cpu")
+    fr = multi.FusedCloudRank(eng, cams, rank, world, p, dev="cpu", mark_slices=mark_slices)
     n = W_ * H_
     lidar = fused_ref.lidar_camera(LW, LH)
     recs = None
@@ -327,7 +328,7 @@ def _oracle_rb(world, W_, H_, LW, LH, first, win, frames, launch_defaults, threa
         yield orc.downloadVoxelizedPoints()[:, :3], orc.downloadVoxelOccupancyGrid(), orc.rollbuffer_state()
 
 
-@pytest.mark.parametrize("cfg", ["small", "C5"])
+@pytest.mark.parametrize("cfg", ["small", "small_slices", "C5"])
 def test_fused_cloud_rollbuffer_leg(tmp_path, cfg):
     """The multi-GPU fused cloud WITH the rollbuffer on the last rank, through the HIP kernels
     (processes on the one GPU, gloo): per frame the ranks' voxel ranges concatenated equal ONE
@@ -337,13 +338,13 @@ def test_fused_cloud_rollbuffer_leg(tmp_path, cfg):
     sequences of 80x60 points, window 3, 5 frames (rolls from frame 2).  "C5": 8 ranks x 4K at
     launch defaults + a window of 8 x 720p sequences (7.4 M selected points; frame 1 rolls the
     oldest out)."""
-    if cfg == "small":
+    if cfg in ("small", "small_slices"):
         world, W_, H_, LW, LH, first, win, frames, ld, th = 3, 160, 120, 80, 60, 2, 3, 5, False, 4
     else:
         world, W_, H_, LW, LH, first, win, frames, ld, th = 8, 3840, 2160, 1280, 720, 8, 8, 2, True, 16
     mp.start_processes(_rank_rb, args=(world, _free_port(), W_, H_, LW, LH, first, win, frames,
-                                       str(tmp_path), ld), nprocs=world, join=True,
-                       start_method="spawn")
+                                       str(tmp_path), ld, cfg == "small_slices"), nprocs=world,
+                       join=True, start_method="spawn")
     for f, (want, grid, st) in enumerate(_oracle_rb(world, W_, H_, LW, LH, first, win, frames, ld, th)):
         assert st[3] > 0, f"frame {f}: rollbuffer points selected"
         assert tuple(np.load(tmp_path / f"rb_f{f}.npy").tolist()) == tuple(st), f"{cfg} frame {f} state"
