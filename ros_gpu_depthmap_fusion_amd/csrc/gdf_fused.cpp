@@ -348,11 +348,12 @@ void fused_finish(gdf_fused* f, int slot, uint32_t* send_counts, uint32_t* recv_
     uint32_t* uni = S.gathered.ensure<uint32_t>(S.nframes * stride * 4, st);
     hipchk(hipMemsetAsync(uni, 0, S.nframes * stride * 4, st), "hipMemsetAsync(marks)");
     gdfchk(gdf_voxelize_runs_marked(e, rp, rrk, rrs, W, pbase, rbase, S.average, uni, stride));
-    if (W > 1) {
+    if (W > 1) {  // (on the points' communicator: the finish's collectives stay in step order,
+                  // never behind the next step's start collectives on comm_a)
         ncclchk(r, r.group_start(), "ncclGroupStart");
         for (uint32_t j = 0; j < S.nframes; ++j)
             ncclchk(r, r.all_gather(uni + j * stride + (uint64_t)R * Sw, uni + j * stride, Sw, ncclUint32,
-                                    f->comm_a, st), "ncclAllGather(mark slices)");
+                                    f->comm_b, st), "ncclAllGather(mark slices)");
         ncclchk(r, r.group_end(), "ncclGroupEnd");
     }
     gdfchk(gdf_voxel_occupancy_grid_batch(e, uni, words, 1, S.nframes, stride, S.nframes * stride,
