@@ -49,8 +49,10 @@ def main():
     a = ap.parse_args()
     s, d = a.src, a.dst
     os.makedirs(d, exist_ok=True)
-    for f in ("pytest_gpu.log", "smoke.log", "bench_20_5.json", "bench_300.json", "dist_n1.json", "c3.json"):
-        shutil.copy(os.path.join(s, f), os.path.join(d, f))
+    for f in ("pytest_gpu.log", "smoke.log", "bench_default.json", "bench_20_5.json", "bench_300.json",
+              "dist_n1.json", "c3.json"):
+        if os.path.exists(os.path.join(s, f)):
+            shutil.copy(os.path.join(s, f), os.path.join(d, f))
     for sub, name in (("trace", "c2_p1_kernel_stats.csv"), ("t4k", "4k_kernel_stats.csv"),
                       ("tdist", "dist_n1_kernel_stats.csv")):
         shutil.copy(os.path.join(s, sub, "run_kernel_stats.csv"), os.path.join(d, name))

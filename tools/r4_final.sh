@@ -1,5 +1,5 @@
-# Round-4 measurement set: bash tools/r4_final.sh <outdir> - GPU suite, smoke, the driver-style line
-# (20 / 5, every secondary), the 300-step line, the world-1 --dist (native) line, the kernel trace
+# Round-4 measurement set: bash tools/r4_final.sh <outdir> - GPU suite, smoke, the default line
+# (python bench.py: 300 / 30, every secondary), the short line (20 / 5), the 300-step line, the world-1 --dist (native) line, the kernel trace
 # of the C2 step with one batch in flight, PMC FETCH / WRITE / SQ passes of it, the 4K trace, the
 # world-1 --dist trace, the C3 line.
 set -o pipefail
@@ -7,6 +7,7 @@ cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=gpurun_out/${1:-r4final}; mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread --durations=15 > $O/pytest_gpu.log 2>&1 || exit 1
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
+timeout -k 10 600 python bench.py > $O/bench_default.json 2> $O/bench_default.err || exit 1
 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_20_5.json 2> $O/bench_20_5.err || exit 1
 timeout -k 10 150 python bench.py --gpus 1 --steps 300 --warmup 30 --no-secondary > $O/bench_300.json 2> $O/bench_300.err || exit 1
 timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 1 --dist --steps 100 --warmup 10 --no-secondary --no-cpu-baseline > $O/dist_n1.json 2> $O/dist_n1.err || exit 1
