@@ -87,6 +87,11 @@ def parse():
     ap.add_argument("--no-secondary", action="store_true",
                     help="N = 1: skip the 720p / 4K / stress / H2D / C3 lines")
     ap.add_argument("--c3-window", type=int, default=256)
+    ap.add_argument("--transport", choices=("rccl", "local"), default="rccl",
+                    help="N > 1 fused mode: rccl = one process per GPU (torchrun, or started by "
+                         "this script); local = N ranks of the C++ step in THIS process on one "
+                         "GPU (gdf_fused_local: one engine + host thread per rank, device copies "
+                         "as the collectives) - exercises the multi-rank step, not a scaling run")
     ap.add_argument("--rb-window", type=int, default=0,
                     help="N > 1 fused mode: the last rank also runs a rollbuffer of this many "
                          "720p point sequences, one new sequence per step (C5 with its rollbuffer)")
@@ -442,17 +447,38 @@ def emit(obj):
     os.write(_JSON_FD if _JSON_FD is not None else 1, (json.dumps(obj) + "\n").encode())
 
 
+def launch_ranks(args) -> int:
+    """`--gpus N` without a launcher: start N rank processes of this script under
+    torch.distributed.run (127.0.0.1 rendezvous) as CHILDREN - before this process touches a GPU -
+    and return their exit status (rank 0 prints the JSON line)."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node=%d" % args.gpus, "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "4"))
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     # Library chatter on stdout (RCCL's version banner at communicator creation, ...) would break
     # the one-JSON-line contract: fd 1 points at stderr for the run, the line goes to the original.
     global _JSON_FD
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and args.transport == "rccl":
+        sys.exit(launch_ranks(args))  # (no GPU call has been made in this process)
     sys.stdout.flush()
     _JSON_FD = os.dup(1)
     os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     dist = None
     rank, local_rank = 0, 0
+    if args.transport == "local" and args.gpus > 1:
+        emit(time_local(args))
+        return
     if args.gpus > 1 or world > 1 or args.dist:
         import torch
         import torch.distributed as dist
@@ -466,6 +492,8 @@ def main():
             torch.cuda.set_device(local_rank)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         world = dist.get_world_size()
+        if world != max(1, args.gpus):
+            raise SystemExit("bench: %d ranks started for --gpus %d" % (world, args.gpus))
     import numpy as np
     from ros_gpu_depthmap_fusion_amd import build_library, hiprt
     from ros_gpu_depthmap_fusion_amd.gdf import ComponentParams, GPUDepthmapFusion
@@ -662,7 +690,9 @@ def time_multi(args, st, params, dist, world, pmc_key):
         eng.set_profiling(False)
         line["roofline"] = roofline_from(kt, kt_steps, model_bytes(st.P, n_avg, g_avg, ncells, fpb),
                                          pmc_key)
+    transport_ranks = dist.get_world_size()
     if fused and native:
+        transport_ranks = fr.info()[2]  # (ncclCommCount of the step's points communicator)
         fr.close()  # (its communicators, before the process group goes)
     if fused:
         cfg = {"parallelism": "camera-per-GPU x%d; per step of %d frames (one launch chain): "
@@ -676,14 +706,70 @@ def time_multi(args, st, params, dist, world, pmc_key):
                                   "the slots' streams, two communicators" if native else
                                   "; torch.distributed collectives (multi.FusedCloudRank)"),
                "exchange": "per step of %d frames: halo %d px + %d-word marks per frame, one "
-                           "points all-to-all" % (fpb, fr.Lmax, (ncells + 31) // 32)}
+                           "points all-to-all" % (fpb, fr.Lmax, (ncells + 31) // 32),
+               "transport_ranks": transport_ranks}
     else:
         cfg = {"parallelism": "camera-per-GPU x%d, occupancy-mark all-gather %s (voxel means per "
                               "camera)" % (world, "every frame" if not batched else
                                            "every %d frames (deferred grid)" % args.exchange_batch),
                "exchange": ("sparse mark pairs (cap %d words/frame), %d dense-fallback batches" %
-                            (marks.cap, marks.dense_batches)) if batched else "bitmask per frame"}
+                            (marks.cap, marks.dense_batches)) if batched else "bitmask per frame",
+               "transport_ranks": transport_ranks}
     return line, cfg
+
+
+def time_local(args):
+    """`--transport local --gpus N`: N ranks of the C++ fused step (gdf_fused_run) in this process on
+    ONE GPU - one engine, one host thread and one camera each, the collectives as device copies
+    (multi.LocalFusedWorld).  The ranks share the GPU, so the rate is the step's throughput with N
+    cameras on one device, not a scaling number (n_gpus: 1)."""
+    import numpy as np
+    from ros_gpu_depthmap_fusion_amd import build_library, synth
+    from ros_gpu_depthmap_fusion_amd.gdf import ComponentParams, GPUDepthmapFusion
+    from ros_gpu_depthmap_fusion_amd.multi import LocalFusedWorld, NativeFusedRank
+    build_library()
+    N, W, H, B = args.gpus, args.width, args.height, max(1, args.batch)
+    params = ComponentParams()
+    depth = max(1, min(4, args.pipeline))
+    lw = LocalFusedWorld(N)
+    cams = [synth.make_camera(k, W, H) for k in range(N)]
+    streams = [DepthStream(GPUDepthmapFusion(0), W, H, 1, r, args.workload, args.ring)
+               for r in range(N)]
+    ranks = [NativeFusedRank(st.eng, cams, r, N, params, depth=depth, local=lw)
+             for r, st in enumerate(streams)]
+    info = ranks[0].info()
+    rings = [[d.ptr for d in st.dframes[0]] for st in streams]
+
+    def run(first, count):
+        lw.run(lambda r: ranks[r].run_stream(rings[r], first, count, B))
+        for st in streams:
+            st.eng.synchronize()
+
+    prime = 2 * depth + 2
+    run(0, prime + 100)
+    run(prime, args.warmup)
+    t0 = time.perf_counter()
+    run(prime + args.warmup, args.steps)
+    elapsed = time.perf_counter() - t0
+    for fr in ranks:
+        fr.close()
+    lw.close()
+    P = W * H
+    return {
+        "metric": METRIC, "value": round(N * P * B * args.steps / elapsed / 1e6, 3),
+        "unit": "Mpoints/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 5), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (ray-cast analytic scene, %s frames)" % args.workload,
+        "config": {"workload": "%d ranks x %s, a step = a batch of %d frames per rank" % (
+                       N, workload_name(W, H, 1, args.workload), B),
+                   "parallelism": "%d ranks of the C++ fused step (gdf_fused_run) in one process "
+                                  "on one GPU, in-process transport (%s, %d ranks)" % (
+                                      N, info[3], info[2]),
+                   "ranks": N, "frames_in_flight": depth,
+                   "note": "diagnostic: N cameras' fused step sharing ONE GPU, not a scaling run"},
+        "roofline": None, "cpu_baseline": None,
+    }
 
 
 class RollbufferFeed:

@@ -48,13 +48,37 @@ int gdf_fused_create(gdf_engine* engine, const char* rccl_library, const uint8_t
                      gdf_fused** out);
 int gdf_fused_destroy(gdf_fused* rank);
 
+/* In-process transport: `world` ranks of ONE process - one host thread and one engine each, on one
+ * device or several - with the step's collectives as device-to-device copies on the ranks' own
+ * streams (matched in issue order like RCCL's; the host only waits for every rank to ISSUE a
+ * collective, never for the GPU).  The same gdf_fused_start / finish / run as the RCCL ranks: this
+ * is how the multi-rank C++ step runs (and is tested) on a node with fewer GPUs than ranks, where
+ * RCCL refuses two ranks on one device.  A rank whose step fails aborts the world: the other
+ * ranks' pending and later collectives fail with GDF_ERR_STATE instead of waiting (so does a rank
+ * left waiting longer than GDF_LOCAL_TIMEOUT_S seconds, default 300).  Destroy every rank
+ * (gdf_fused_destroy) before the world. */
+typedef struct gdf_fused_local gdf_fused_local;
+int gdf_fused_local_create(int world, gdf_fused_local** out);
+int gdf_fused_local_destroy(gdf_fused_local* world);
+/* Not collective (no rendezvous): creates rank `rank` of the local world on `engine`; cams and
+ * flying_filter_size as for gdf_fused_create. */
+int gdf_fused_create_local(gdf_engine* engine, gdf_fused_local* world, int rank, int nranks,
+                           const gdf_stream_camera* cams, uint32_t flying_filter_size,
+                           gdf_fused** out);
+
+/* The rank, its world, the rank count its transport reports (RCCL: ncclCommCount of the points'
+ * communicator) and the transport's name ("rccl" / "local"; a static string). */
+int gdf_fused_info(gdf_fused* rank, int* rank_out, int* world, int* transport_ranks,
+                   const char** transport);
+
 /* Depth values of the halo every rank sends (max over cameras of F * width + F). */
 int gdf_fused_halo_pixels(gdf_fused* rank, uint32_t* pixels);
 
 /* Starts a step of `nframes` frames (1..16) of this rank's camera - depth[j] = frame j's DEVICE
  * depth map - on the engine's next slot: everything up to the split sizes (queued to pinned
  * memory, no wait).  p: the frame's parameters (its defer / synchronous flags are overridden; a
- * move transform - rollbuffer rank, single frames - is honoured as by gdf_process_frame).
+ * move transform - rollbuffer rank, single frames - is honoured as by gdf_process_frame; with
+ * nframes > 1 it is GDF_ERR_ARG: a batch carries no rollbuffer frame).
  * Point sequences added to the engine beforehand are ingested by this step.  *slot = the slot to
  * pass to gdf_fused_finish. */
 int gdf_fused_start(gdf_fused* rank, const uint16_t* const* depth, uint32_t nframes,
@@ -66,8 +90,8 @@ int gdf_fused_start(gdf_fused* rank, const uint16_t* const* depth, uint32_t nfra
 int gdf_fused_finish(gdf_fused* rank, int slot, uint32_t* send_counts, uint32_t* recv_count);
 
 /* `steps` pipelined steps of `batch` frames of this rank's camera from cam->frames (step s takes
- * frames (first + s) * batch + j, modulo the ring): step s + 1 is started before step s is
- * finished, `depth` steps in flight at most (the engine's pipeline depth is set to it).  Returns
+ * frames (first + s) * batch + j, modulo the ring): up to `depth` steps in flight (the engine's
+ * pipeline depth is set to it) - step s - depth + 1 is finished right after step s started.  Returns
  * after the last step was finished (its work still queued: gdf_synchronize waits). */
 int gdf_fused_run(gdf_fused* rank, const gdf_stream_camera* cam, const gdf_frame_params* p,
                   uint64_t first, uint64_t steps, uint32_t batch, int depth);

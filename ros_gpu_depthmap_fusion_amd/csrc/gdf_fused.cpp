@@ -10,8 +10,13 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -100,6 +105,242 @@ void ncclchk(const Rccl& r, ncclResult_t res, const char* what) {
     if (res != ncclSuccess) fail(GDF_ERR_HIP, std::string(what) + ": " + r.error_string(res));
 }
 
+// ---- the step's collectives -------------------------------------------------------------------
+// Everything the step exchanges goes through this interface: an all-gather of equal byte slices
+// (in place when send == recv + rank * bytes), point-to-point sends / receives, and groups (the
+// operations between group_start and group_end are issued as one, like ncclGroupStart/End).  Two
+// communicators: kHalo (halo tails, split sizes: the start) and kPoints (points, runs, mark
+// slices: the finish).  Every call is stream-ordered on `st` (the engine slot's stream).
+enum Comm { kHalo = 0, kPoints = 1 };
+
+struct Transport {
+    virtual ~Transport() = default;
+    virtual const char* kind() const = 0;
+    virtual int ranks() const = 0;  // the rank count the communicator reports
+    virtual void all_gather(const void* send, void* recv, size_t bytes, Comm c, hipStream_t st) = 0;
+    virtual void group_start(Comm c) = 0;
+    virtual void send(const void* buf, size_t bytes, int peer, Comm c, hipStream_t st) = 0;
+    virtual void recv(void* buf, size_t bytes, int peer, Comm c, hipStream_t st) = 0;
+    virtual void group_end(Comm c, hipStream_t st) = 0;
+    virtual void abort() {}
+    uint64_t calls = 0;  // collectives and groups issued (counted by the step)
+};
+
+// RCCL: two communicators of the transport's own, byte-typed transfers.
+struct RcclTransport final : Transport {
+    const Rccl* r = nullptr;
+    ncclComm_t comm[2] = {nullptr, nullptr};
+    int world = 1;
+    ~RcclTransport() override {
+        for (ncclComm_t c : comm)
+            if (c) r->comm_destroy(c);
+    }
+    const char* kind() const override { return "rccl"; }
+    int ranks() const override {
+        int n = 0;
+        using CountFn = ncclResult_t (*)(const ncclComm_t, int*);
+        auto fn = reinterpret_cast<CountFn>(dlsym(r->lib, "ncclCommCount"));
+        if (!fn || fn(comm[kPoints], &n) != ncclSuccess) return -1;
+        return n;
+    }
+    void all_gather(const void* send, void* recv, size_t bytes, Comm c, hipStream_t st) override {
+        ncclchk(*r, r->all_gather(send, recv, bytes, ncclUint8, comm[c], st), "ncclAllGather");
+    }
+    void group_start(Comm) override { ncclchk(*r, r->group_start(), "ncclGroupStart"); }
+    void send(const void* buf, size_t bytes, int peer, Comm c, hipStream_t st) override {
+        ncclchk(*r, r->send(buf, bytes, ncclUint8, peer, comm[c], st), "ncclSend");
+    }
+    void recv(void* buf, size_t bytes, int peer, Comm c, hipStream_t st) override {
+        ncclchk(*r, r->recv(buf, bytes, ncclUint8, peer, comm[c], st), "ncclRecv");
+    }
+    void group_end(Comm, hipStream_t) override { ncclchk(*r, r->group_end(), "ncclGroupEnd"); }
+};
+
+}  // namespace
+
+// In-process transport: `world` ranks of ONE process (one host thread and one engine each, on one
+// or several devices), exchanging through device-to-device copies on the ranks' own streams.  A
+// collective (or a group) is a round of its communicator; round k of communicator c is matched
+// across the ranks by their k-th call, like RCCL's issue order:
+//   1. each rank records `ready` on its stream (its sends are written) and posts its operations;
+//   2. host barrier: every rank posted round k;
+//   3. each rank copies what it receives, on ITS stream, behind the sender's `ready`;
+//   4. each rank records `done` (its reads are finished); host barrier;
+//   5. each rank's stream waits for every other rank's `done` before its buffers are reused.
+// The host only waits for the other ranks to ISSUE (not to finish): GPU work stays queued and the
+// steps stay pipelined.  A rank that fails aborts the world, so the others fail instead of waiting.
+struct gdf_fused_local {
+    struct Op {
+        int kind;  // 0 all-gather, 1 send, 2 recv
+        const void* src;
+        void* dst;
+        size_t bytes;
+        int peer;
+    };
+    struct Post {
+        std::vector<Op> ops;
+        hipEvent_t ready = nullptr, done = nullptr;
+    };
+    struct Round {
+        std::vector<Post> posts;
+        int arrived = 0, copied = 0, left = 0;
+    };
+    int world = 1;
+    std::mutex m;
+    std::condition_variable cv;
+    std::map<uint64_t, Round> rounds[2];
+    int refs = 0;  // ranks created on this world and not destroyed
+    bool aborted = false;
+    std::string abort_reason;
+    double timeout_s = 300.0;  // a rank that never arrives (a caller bug) ends the wait
+
+    template <class Pred>
+    void wait(std::unique_lock<std::mutex>& lk, Pred pred, const char* what) {
+        const auto until = std::chrono::steady_clock::now() +
+                           std::chrono::milliseconds((long long)(timeout_s * 1e3));
+        while (!pred()) {
+            if (aborted) fail(GDF_ERR_STATE, std::string("local transport aborted (") + abort_reason + ")");
+            if (cv.wait_until(lk, until) == std::cv_status::timeout && !pred()) {
+                aborted = true;
+                abort_reason = std::string("timeout at ") + what;
+                cv.notify_all();
+                fail(GDF_ERR_STATE, std::string("local transport: a rank did not reach ") + what);
+            }
+        }
+    }
+};
+
+namespace {
+
+struct LocalTransport final : Transport {
+    gdf_fused_local* w = nullptr;
+    int rank = 0;
+    uint64_t seq[2] = {0, 0};
+    hipEvent_t ready[2] = {nullptr, nullptr}, done[2] = {nullptr, nullptr};
+    bool grouped[2] = {false, false};
+    std::vector<gdf_fused_local::Op> ops[2];
+
+    LocalTransport(gdf_fused_local* world, int r) : w(world), rank(r) {
+        for (int c = 0; c < 2; ++c) {
+            hipchk(hipEventCreateWithFlags(&ready[c], hipEventDisableTiming), "hipEventCreate");
+            hipchk(hipEventCreateWithFlags(&done[c], hipEventDisableTiming), "hipEventCreate");
+        }
+    }
+    ~LocalTransport() override {
+        for (int c = 0; c < 2; ++c) {
+            if (ready[c]) (void)hipEventDestroy(ready[c]);
+            if (done[c]) (void)hipEventDestroy(done[c]);
+        }
+    }
+    const char* kind() const override { return "local"; }
+    int ranks() const override { return w->world; }
+    void abort() override {
+        std::lock_guard<std::mutex> lk(w->m);
+        if (!w->aborted) {
+            w->aborted = true;
+            w->abort_reason = "rank " + std::to_string(rank) + " failed";
+        }
+        w->cv.notify_all();
+    }
+    void all_gather(const void* send, void* recv, size_t bytes, Comm c, hipStream_t st) override {
+        ops[c].push_back({0, send, recv, bytes, -1});
+        if (!grouped[c]) run(c, st);
+    }
+    void group_start(Comm c) override {
+        if (grouped[c]) fail(GDF_ERR_STATE, "local transport: nested group");
+        grouped[c] = true;
+    }
+    void send(const void* buf, size_t bytes, int peer, Comm c, hipStream_t) override {
+        if (!grouped[c]) fail(GDF_ERR_STATE, "local transport: send outside a group");
+        ops[c].push_back({1, buf, nullptr, bytes, peer});
+    }
+    void recv(void* buf, size_t bytes, int peer, Comm c, hipStream_t) override {
+        if (!grouped[c]) fail(GDF_ERR_STATE, "local transport: recv outside a group");
+        ops[c].push_back({2, nullptr, buf, bytes, peer});
+    }
+    void group_end(Comm c, hipStream_t st) override {
+        if (!grouped[c]) fail(GDF_ERR_STATE, "local transport: group_end without group_start");
+        grouped[c] = false;
+        run(c, st);
+    }
+
+  private:
+    // one round (a collective, or a group of operations) of communicator c
+    void run(Comm c, hipStream_t st) {
+        std::vector<gdf_fused_local::Op> mine;
+        mine.swap(ops[c]);
+        const int W = w->world, R = rank;
+        const uint64_t k = seq[c]++;
+        hipchk(hipEventRecord(ready[c], st), "hipEventRecord(ready)");
+        gdf_fused_local::Round* rd = nullptr;
+        {
+            std::unique_lock<std::mutex> lk(w->m);
+            rd = &w->rounds[c][k];
+            if (rd->posts.empty()) rd->posts.resize(W);
+            rd->posts[R].ops = mine;
+            rd->posts[R].ready = ready[c];
+            rd->posts[R].done = done[c];
+            ++rd->arrived;
+            w->cv.notify_all();
+            w->wait(lk, [&] { return rd->arrived == W; }, "a collective");
+        }
+        // (the posts are written before the barrier and only read after it: no lock needed)
+        std::vector<char> waited(W, 0);
+        auto behind = [&](int q) {
+            if (!waited[q]) {
+                hipchk(hipStreamWaitEvent(st, rd->posts[q].ready, 0), "hipStreamWaitEvent(ready)");
+                waited[q] = 1;
+            }
+        };
+        auto copy = [&](void* dst, const void* src, size_t bytes) {
+            if (bytes && dst != src)
+                hipchk(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync(local)");
+        };
+        int ag = 0;  // the index of this all-gather among the round's all-gathers
+        std::vector<int> nrecv(W, 0);  // receives from each peer so far
+        for (const gdf_fused_local::Op& op : mine) {
+            if (op.kind == 0) {
+                for (int q = 0; q < W; ++q) {
+                    const gdf_fused_local::Op* o = nth(rd->posts[q].ops, 0, -1, ag);
+                    if (!o || o->bytes != op.bytes)
+                        fail(GDF_ERR_STATE, "local transport: all-gather sizes differ across ranks");
+                    uint8_t* dst = static_cast<uint8_t*>(op.dst) + (size_t)q * op.bytes;
+                    if (q != R) behind(q);
+                    copy(dst, o->src, op.bytes);  // (in place: the own slice is already there)
+                }
+                ++ag;
+            } else if (op.kind == 2) {
+                const int q = op.peer;
+                if (q < 0 || q >= W || q == R) fail(GDF_ERR_STATE, "local transport: bad receive peer");
+                const gdf_fused_local::Op* o = nth(rd->posts[q].ops, 1, R, nrecv[q]++);
+                if (!o) fail(GDF_ERR_STATE, "local transport: a receive without its send");
+                if (o->bytes != op.bytes) fail(GDF_ERR_STATE, "local transport: send / receive sizes differ");
+                behind(q);
+                copy(op.dst, o->src, op.bytes);
+            } else if (op.peer < 0 || op.peer >= W || op.peer == R) {
+                fail(GDF_ERR_STATE, "local transport: bad send peer");
+            }
+        }
+        hipchk(hipEventRecord(done[c], st), "hipEventRecord(done)");
+        {
+            std::unique_lock<std::mutex> lk(w->m);
+            ++rd->copied;
+            w->cv.notify_all();
+            w->wait(lk, [&] { return rd->copied == W; }, "the end of a collective");
+        }
+        for (int q = 0; q < W; ++q)  // (nobody writes over a buffer another rank still reads)
+            if (q != R) hipchk(hipStreamWaitEvent(st, rd->posts[q].done, 0), "hipStreamWaitEvent(done)");
+        std::lock_guard<std::mutex> lk(w->m);
+        if (++rd->left == W) w->rounds[c].erase(k);
+    }
+    // the n-th operation of `kind` (to `peer`, for sends) in a rank's list
+    static const gdf_fused_local::Op* nth(const std::vector<gdf_fused_local::Op>& v, int kind, int peer, int n) {
+        for (const gdf_fused_local::Op& o : v)
+            if (o.kind == kind && (kind != 1 || o.peer == peer) && n-- == 0) return &o;
+        return nullptr;
+    }
+};
+
 // ---- per-slot exchange state ------------------------------------------------------------------
 struct DevBuf {
     void* p = nullptr;
@@ -149,8 +390,8 @@ constexpr int kSlots = 4;  // the engine's pipeline depth is 1..4
 
 struct gdf_fused {
     gdf_engine* e = nullptr;
-    const Rccl* r = nullptr;
-    ncclComm_t comm_a = nullptr, comm_b = nullptr;
+    std::unique_ptr<Transport> x;  // RCCL, or the in-process transport of a gdf_fused_local
+    gdf_fused_local* local = nullptr;
     int rank = 0, world = 1;
     std::vector<gdf_stream_camera> cams;
     uint32_t F = 0, Lmax = 0;
@@ -168,9 +409,10 @@ struct gdf_fused {
             if (s.host) hipHostFree(s.host);
             if (s.ev) hipEventDestroy(s.ev);
         }
-        if (r) {
-            if (comm_a) r->comm_destroy(comm_a);
-            if (comm_b) r->comm_destroy(comm_b);
+        x.reset();
+        if (local) {
+            std::lock_guard<std::mutex> lk(local->m);
+            --local->refs;
         }
     }
 };
@@ -183,8 +425,12 @@ void fused_start(gdf_fused* f, const uint16_t* const* depth, uint32_t B, const g
     for (uint32_t j = 0; j < B; ++j)
         if (!depth[j]) fail(GDF_ERR_ARG, "fused start: null depth map");
     if (!p->enable_voxel_filter) fail(GDF_ERR_ARG, "fused start: the fused cloud needs the voxel filter");
+    // frames carrying the rollbuffer run one per step (the batched launch chain has no rollbuffer
+    // frame: a silent drop would lose the window's points)
+    if (B > 1 && p->move_transform_available)
+        fail(GDF_ERR_ARG, "fused start: a move transform (rollbuffer frame) needs nframes == 1");
     gdf_engine* e = f->e;
-    const Rccl& r = *f->r;
+    Transport& x = *f->x;
     gdfchk(gdf_clear(e));
     int slot = 0;
     gdfchk(gdf_get_slot(e, &slot));
@@ -206,8 +452,8 @@ void fused_start(gdf_fused* f, const uint16_t* const* depth, uint32_t B, const g
         for (uint32_t j = 0; j < B; ++j)
             hipchk(hipMemcpyAsync(tail + j * L2, depth[j] + (npx - f->Lmax), L2,
                                   hipMemcpyDeviceToDevice, st), "hipMemcpyAsync(tail)");
-        ncclchk(r, r.all_gather(tail, S.tails.as(), B * L2, ncclUint8, f->comm_a, st),
-                "ncclAllGather(tails)");
+        ++x.calls;
+        x.all_gather(tail, S.tails.as(), B * L2, kHalo, st);
     }
     for (uint32_t j = 0; j < B; ++j) {
         if (j) gdfchk(gdf_next_frame_in_batch(e));
@@ -226,7 +472,7 @@ void fused_start(gdf_fused* f, const uint16_t* const* depth, uint32_t B, const g
     q.synchronous = 0;
     q.defer_occupancy_grid = 1;
     q.defer_voxelize = 1;
-    if (R != W - 1 || B > 1) q.move_transform_available = 0;  // the rollbuffer: last rank only
+    if (R != W - 1) q.move_transform_available = 0;  // the rollbuffer: last rank only
     // the send lists, written by the compaction itself (gdf_set_emit_partition): sized for the
     // step's pixels (+ halo) plus, on the rollbuffer rank, every point the window can select
     uint32_t* cnt = S.cnt.ensure<uint32_t>((size_t)2 * W * 4, st);
@@ -259,7 +505,8 @@ void fused_start(gdf_fused* f, const uint16_t* const* depth, uint32_t B, const g
     S.lifetime = q.occupancy_lifetime;
     // every rank's split sizes (the partition's, written with the compaction) to pinned memory
     // (no wait here)
-    ncclchk(r, r.all_gather(cnt, cntall, 2 * W, ncclUint32, f->comm_a, st), "ncclAllGather(counts)");
+    ++x.calls;
+    x.all_gather(cnt, cntall, (size_t)2 * W * 4, kHalo, st);
     hipchk(hipMemcpyAsync(S.host, cntall, (size_t)2 * W * W * 4, hipMemcpyDeviceToHost, st),
            "hipMemcpyAsync(counts)");
     hipchk(hipEventRecord(S.ev, st), "hipEventRecord");
@@ -271,7 +518,7 @@ void fused_start(gdf_fused* f, const uint16_t* const* depth, uint32_t B, const g
 void fused_finish(gdf_fused* f, int slot, uint32_t* send_counts, uint32_t* recv_count) {
     if (slot < 0 || slot >= kSlots) fail(GDF_ERR_ARG, "fused finish: bad slot");
     gdf_engine* e = f->e;
-    const Rccl& r = *f->r;
+    Transport& x = *f->x;
     SlotX& S = f->slots[slot];
     if (!S.pending) fail(GDF_ERR_STATE, "fused finish: no step in flight on this slot");
     gdfchk(gdf_select_slot(e, slot));
@@ -313,29 +560,26 @@ void fused_finish(gdf_fused* f, int slot, uint32_t* send_counts, uint32_t* recv_
                               hipMemcpyDeviceToDevice, st), "hipMemcpyAsync(run starts)");
     }
     if (W > 1) {
-        ncclchk(r, r.group_start(), "ncclGroupStart");
+        ++x.calls;
+        x.group_start(kPoints);
         soff = sroff = 0;
         for (int q = 0; q < W; ++q) {
             const size_t sc = pts_of(R, q), sr = runs_of(R, q);
             const size_t rc = pts_of(q, R), rr = runs_of(q, R);
             if (q != R && sc) {
-                ncclchk(r, r.send(S.sp.as<float>() + 4 * soff, 4 * sc, ncclFloat32, q, f->comm_b, st),
-                        "ncclSend(points)");
-                ncclchk(r, r.send(S.srk.as<uint32_t>() + sroff, sr, ncclUint32, q, f->comm_b, st),
-                        "ncclSend(run keys)");
-                ncclchk(r, r.send(S.srs.as<uint32_t>() + sroff, sr, ncclUint32, q, f->comm_b, st),
-                        "ncclSend(run starts)");
+                x.send(S.sp.as<float>() + 4 * soff, 16 * sc, q, kPoints, st);
+                x.send(S.srk.as<uint32_t>() + sroff, 4 * sr, q, kPoints, st);
+                x.send(S.srs.as<uint32_t>() + sroff, 4 * sr, q, kPoints, st);
             }
             if (q != R && rc) {
-                ncclchk(r, r.recv(rp + 4 * (size_t)pbase[q], 4 * rc, ncclFloat32, q, f->comm_b, st),
-                        "ncclRecv(points)");
-                ncclchk(r, r.recv(rrk + rbase[q], rr, ncclUint32, q, f->comm_b, st), "ncclRecv(run keys)");
-                ncclchk(r, r.recv(rrs + rbase[q], rr, ncclUint32, q, f->comm_b, st), "ncclRecv(run starts)");
+                x.recv(rp + 4 * (size_t)pbase[q], 16 * rc, q, kPoints, st);
+                x.recv(rrk + rbase[q], 4 * rr, q, kPoints, st);
+                x.recv(rrs + rbase[q], 4 * rr, q, kPoints, st);
             }
             soff += sc;
             sroff += sr;
         }
-        ncclchk(r, r.group_end(), "ncclGroupEnd");
+        x.group_end(kPoints, st);
     }
     // the voxel means of this rank's key range, every voxel's mark into slice R of its frame's
     // union bitmask, the slices all-gathered in place, then the step's batched grid update
@@ -349,12 +593,12 @@ void fused_finish(gdf_fused* f, int slot, uint32_t* send_counts, uint32_t* recv_
     hipchk(hipMemsetAsync(uni, 0, S.nframes * stride * 4, st), "hipMemsetAsync(marks)");
     gdfchk(gdf_voxelize_runs_marked(e, rp, rrk, rrs, W, pbase, rbase, S.average, uni, stride));
     if (W > 1) {  // (on the points' communicator: the finish's collectives stay in step order,
-                  // never behind the next step's start collectives on comm_a)
-        ncclchk(r, r.group_start(), "ncclGroupStart");
+                  // never behind the next step's start collectives on the halo communicator)
+        ++x.calls;
+        x.group_start(kPoints);
         for (uint32_t j = 0; j < S.nframes; ++j)
-            ncclchk(r, r.all_gather(uni + j * stride + (uint64_t)R * Sw, uni + j * stride, Sw, ncclUint32,
-                                    f->comm_b, st), "ncclAllGather(mark slices)");
-        ncclchk(r, r.group_end(), "ncclGroupEnd");
+            x.all_gather(uni + j * stride + (uint64_t)R * Sw, uni + j * stride, Sw * 4, kPoints, st);
+        x.group_end(kPoints, st);
     }
     gdfchk(gdf_voxel_occupancy_grid_batch(e, uni, words, 1, S.nframes, stride, S.nframes * stride,
                                           S.lifetime));
@@ -362,6 +606,52 @@ void fused_finish(gdf_fused* f, int slot, uint32_t* send_counts, uint32_t* recv_
         for (int q = 0; q < W; ++q) send_counts[q] = (uint32_t)pts_of(R, q);
     if (recv_count) *recv_count = (uint32_t)n;
     S.pending = false;
+}
+
+}  // namespace
+
+namespace {
+
+// the state every transport shares: cameras, halo size, per-slot pinned split sizes and events
+gdf_fused* fused_new(gdf_engine* engine, int rank, int world, const gdf_stream_camera* cams,
+                     uint32_t flying_filter_size) {
+    std::unique_ptr<gdf_fused> f(new gdf_fused());
+    f->rank = rank;
+    f->world = world;
+    f->cams.assign(cams, cams + world);
+    f->F = flying_filter_size;
+    for (const gdf_stream_camera& c : f->cams)
+        f->Lmax = std::max<uint32_t>(f->Lmax, f->F * c.width + f->F);
+    for (const gdf_stream_camera& c : f->cams)
+        if ((uint64_t)c.width * c.height < f->Lmax)
+            fail(GDF_ERR_ARG, "fused multi-GPU frames need cameras taller than F rows");
+    for (SlotX& s : f->slots) {
+        hipchk(hipHostMalloc(reinterpret_cast<void**>(&s.host), (size_t)2 * world * world * 4,
+                             hipHostMallocDefault), "hipHostMalloc");
+        hipchk(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming), "hipEventCreate");
+    }
+    f->e = engine;  // (set last: the destructor of a half-made rank leaves the engine alone)
+    return f.release();
+}
+
+bool create_args_ok(gdf_engine* engine, const gdf_stream_camera* cams, gdf_fused** out, int rank,
+                    int world) {
+    if (!engine || !cams || !out || world < 1 || world > 16 || rank < 0 || rank >= world) {
+        gdf::set_last_error("fused create: engine, cameras, 0 <= rank < world <= 16");
+        return false;
+    }
+    *out = nullptr;
+    return true;
+}
+
+// A failed step aborts the in-process world, so the other ranks' threads fail instead of waiting;
+// an argument error raised before the step issued any collective leaves the world usable.
+template <class F>
+int step_guarded(gdf_fused* f, F&& fn) {
+    const uint64_t before = f->x ? f->x->calls : 0;
+    const int rc = guarded(fn);
+    if (rc != GDF_OK && f->x && (rc != GDF_ERR_ARG || f->x->calls != before)) f->x->abort();
+    return rc;
 }
 
 }  // namespace
@@ -383,42 +673,92 @@ int gdf_fused_unique_id(const char* rccl_library, uint8_t* id_out) {
 int gdf_fused_create(gdf_engine* engine, const char* rccl_library, const uint8_t* id, int rank,
                      int world, const gdf_stream_camera* cams, uint32_t flying_filter_size,
                      gdf_fused** out) {
-    if (!engine || !id || !cams || !out || world < 1 || world > 16 || rank < 0 || rank >= world) {
-        gdf::set_last_error("fused create: engine, ids, cameras, 0 <= rank < world <= 16");
+    if (!id || !create_args_ok(engine, cams, out, rank, world)) {
+        if (!id) gdf::set_last_error("fused create: null communicator ids");
         return GDF_ERR_ARG;
     }
-    *out = nullptr;
     gdf_fused* f = nullptr;
     const int rc = guarded([&] {
         const Rccl& r = rccl(rccl_library);
-        f = new gdf_fused();
-        f->e = engine;
-        f->rank = rank;
-        f->world = world;
-        f->cams.assign(cams, cams + world);
-        f->F = flying_filter_size;
-        for (const gdf_stream_camera& c : f->cams)
-            f->Lmax = std::max<uint32_t>(f->Lmax, f->F * c.width + f->F);
-        for (const gdf_stream_camera& c : f->cams)
-            if ((uint64_t)c.width * c.height < f->Lmax)
-                fail(GDF_ERR_ARG, "fused multi-GPU frames need cameras taller than F rows");
-        for (SlotX& s : f->slots) {
-            hipchk(hipHostMalloc(reinterpret_cast<void**>(&s.host), (size_t)2 * world * world * 4,
-                                 hipHostMallocDefault), "hipHostMalloc");
-            hipchk(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming), "hipEventCreate");
-        }
+        f = fused_new(engine, rank, world, cams, flying_filter_size);
+        std::unique_ptr<RcclTransport> t(new RcclTransport());
+        t->r = &r;
+        t->world = world;
         ncclUniqueId a, b;
         std::memcpy(&a, id, sizeof(a));
         std::memcpy(&b, id + sizeof(a), sizeof(b));
-        ncclchk(r, r.comm_init_rank(&f->comm_a, world, a, rank), "ncclCommInitRank(A)");
-        ncclchk(r, r.comm_init_rank(&f->comm_b, world, b, rank), "ncclCommInitRank(B)");
-        f->r = &r;
+        ncclchk(r, r.comm_init_rank(&t->comm[kHalo], world, a, rank), "ncclCommInitRank(halo)");
+        ncclchk(r, r.comm_init_rank(&t->comm[kPoints], world, b, rank), "ncclCommInitRank(points)");
+        f->x = std::move(t);
     });
     if (rc != GDF_OK) {
         delete f;
         return rc;
     }
     *out = f;
+    return GDF_OK;
+}
+
+int gdf_fused_local_create(int world, gdf_fused_local** out) {
+    if (!out || world < 1 || world > 16) {
+        gdf::set_last_error("fused local world: 1 <= world <= 16");
+        return GDF_ERR_ARG;
+    }
+    *out = nullptr;
+    return guarded([&] {
+        gdf_fused_local* w = new gdf_fused_local();
+        w->world = world;
+        if (const char* v = std::getenv("GDF_LOCAL_TIMEOUT_S")) w->timeout_s = std::atof(v);
+        *out = w;
+    });
+}
+
+int gdf_fused_local_destroy(gdf_fused_local* w) {
+    if (!w) return GDF_OK;
+    {
+        std::lock_guard<std::mutex> lk(w->m);
+        if (w->refs) {
+            gdf::set_last_error("fused local world: destroy its ranks first");
+            return GDF_ERR_STATE;
+        }
+    }
+    delete w;
+    return GDF_OK;
+}
+
+int gdf_fused_create_local(gdf_engine* engine, gdf_fused_local* w, int rank, int world,
+                           const gdf_stream_camera* cams, uint32_t flying_filter_size,
+                           gdf_fused** out) {
+    if (!w || !create_args_ok(engine, cams, out, rank, world)) {
+        if (!w) gdf::set_last_error("fused create: null local world");
+        return GDF_ERR_ARG;
+    }
+    if (world != w->world) {
+        gdf::set_last_error("fused create: world differs from the local world's");
+        return GDF_ERR_ARG;
+    }
+    gdf_fused* f = nullptr;
+    const int rc = guarded([&] {
+        f = fused_new(engine, rank, world, cams, flying_filter_size);
+        f->x.reset(new LocalTransport(w, rank));
+        std::lock_guard<std::mutex> lk(w->m);
+        ++w->refs;
+        f->local = w;
+    });
+    if (rc != GDF_OK) {
+        delete f;
+        return rc;
+    }
+    *out = f;
+    return GDF_OK;
+}
+
+int gdf_fused_info(gdf_fused* f, int* rank, int* world, int* transport_ranks, const char** transport) {
+    if (!f) return GDF_ERR_ARG;
+    if (rank) *rank = f->rank;
+    if (world) *world = f->world;
+    if (transport_ranks) *transport_ranks = f->x ? f->x->ranks() : -1;
+    if (transport) *transport = f->x ? f->x->kind() : "none";
     return GDF_OK;
 }
 
@@ -436,12 +776,12 @@ int gdf_fused_halo_pixels(gdf_fused* f, uint32_t* pixels) {
 int gdf_fused_start(gdf_fused* f, const uint16_t* const* depth, uint32_t nframes,
                     const gdf_frame_params* p, int* slot) {
     if (!f || !slot) return GDF_ERR_ARG;
-    return guarded([&] { fused_start(f, depth, nframes, p, slot); });
+    return step_guarded(f, [&] { fused_start(f, depth, nframes, p, slot); });
 }
 
 int gdf_fused_finish(gdf_fused* f, int slot, uint32_t* send_counts, uint32_t* recv_count) {
     if (!f) return GDF_ERR_ARG;
-    return guarded([&] { fused_finish(f, slot, send_counts, recv_count); });
+    return step_guarded(f, [&] { fused_finish(f, slot, send_counts, recv_count); });
 }
 
 int gdf_fused_run(gdf_fused* f, const gdf_stream_camera* cam, const gdf_frame_params* p,
@@ -449,22 +789,19 @@ int gdf_fused_run(gdf_fused* f, const gdf_stream_camera* cam, const gdf_frame_pa
     if (!f || !cam || !p || !cam->frames || cam->ring == 0 || batch == 0 || batch > 16 ||
         depth < 1 || depth > kSlots)
         return GDF_ERR_ARG;
-    return guarded([&] {
+    return step_guarded(f, [&] {
         gdfchk(gdf_set_pipeline_depth(f->e, depth));
         std::deque<int> pending;
         const uint16_t* ptrs[16];
         for (uint64_t s = 0; s < steps; ++s) {
-            if ((int)pending.size() >= depth) {  // (its slot comes round again)
-                fused_finish(f, pending.front(), nullptr, nullptr);
-                pending.pop_front();
-            }
             for (uint32_t j = 0; j < batch; ++j) ptrs[j] = cam->frames[((first + s) * batch + j) % cam->ring];
             int slot = 0;
             fused_start(f, ptrs, batch, p, &slot);
             pending.push_back(slot);
-            // step s - 1 is finished once step s is queued: the GPU computes s while the host
-            // waits for s - 1's split sizes
-            if (depth == 1 || pending.size() > 1) {
+            // `depth` steps in flight: the oldest is finished once the newest is queued (the GPU
+            // computes the later steps while the host waits for the oldest one's split sizes),
+            // and its slot is free again before the engine hands it out
+            if ((int)pending.size() >= depth) {
                 fused_finish(f, pending.front(), nullptr, nullptr);
                 pending.pop_front();
             }

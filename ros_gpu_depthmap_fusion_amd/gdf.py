@@ -144,7 +144,8 @@ EXPORTED = [
     "gdf_download_frame", "gdf_set_slot_streams",
     # include/gdf_fused.h: a rank of the multi-GPU fused cloud in C++ over RCCL
     "gdf_fused_unique_id", "gdf_fused_create", "gdf_fused_destroy", "gdf_fused_halo_pixels",
-    "gdf_fused_start", "gdf_fused_finish", "gdf_fused_run",
+    "gdf_fused_start", "gdf_fused_finish", "gdf_fused_run", "gdf_fused_local_create",
+    "gdf_fused_local_destroy", "gdf_fused_create_local", "gdf_fused_info",
     # include/gdf_segment.h: the GPU object-segmentation front end
     "gdf_seg_create", "gdf_seg_destroy", "gdf_seg_set_stream", "gdf_seg_label_layers",
     "gdf_seg_label_engine_grid", "gdf_seg_get_counts", "gdf_seg_download_labels",
@@ -255,6 +256,10 @@ def load_library(path: str = LIB_PATH):
         "gdf_fused_start": (i32, [vp, vp, u32, P(FrameParams), P(i32)]),
         "gdf_fused_finish": (i32, [vp, i32, vp, P(u32)]),
         "gdf_fused_run": (i32, [vp, P(StreamCamera), P(FrameParams), u64, u64, u32, i32]),
+        "gdf_fused_local_create": (i32, [i32, P(vp)]),
+        "gdf_fused_local_destroy": (i32, [vp]),
+        "gdf_fused_create_local": (i32, [vp, vp, i32, i32, P(StreamCamera), u32, P(vp)]),
+        "gdf_fused_info": (i32, [vp, P(i32), P(i32), P(i32), P(C.c_char_p)]),
         "gdf_seg_create": (i32, [i32, P(vp)]),
         "gdf_seg_destroy": (i32, [vp]),
         "gdf_seg_set_stream": (i32, [vp, vp]),

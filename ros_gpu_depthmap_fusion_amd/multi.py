@@ -584,19 +584,16 @@ class FusedCloudRank:
 
     def run(self, steps, depth_ptrs_of, tail_ptrs_of, move_of=None, on_finish=None):
         """`steps` steps through the pipeline: step i's inputs from depth_ptrs_of(i) /
-        tail_ptrs_of(i) (/ move_of(i)); each step is finished right after the next one started
-        (the GPU computes step i + 1 while the host waits for step i's split sizes).
+        tail_ptrs_of(i) (/ move_of(i)); up to `depth` steps in flight: step i - depth + 1 is
+        finished right after step i started (the GPU computes the later steps while the host waits
+        for the oldest one's split sizes).
         on_finish(i) runs after step i's finish (e.g. publishing its cloud)."""
         pending = []
+        depth = self.depth if self.dev == "cuda" else 1
         for i in range(steps):
-            if self.dev == "cuda" and len(pending) >= self.depth:
-                j, kk = pending.pop(0)  # (its slot comes round again)
-                self.finish(kk)
-                if on_finish:
-                    on_finish(j)
             k = self.start(depth_ptrs_of(i), tail_ptrs_of(i), move_of(i) if move_of else None)
             pending.append((i, k))
-            if self.dev != "cuda" or self.depth == 1 or len(pending) > 1:
+            if len(pending) >= depth:  # (`depth` steps in flight; the oldest one's slot is next)
                 j, kk = pending.pop(0)
                 self.finish(kk)
                 if on_finish:
@@ -605,6 +602,55 @@ class FusedCloudRank:
             self.finish(kk)
             if on_finish:
                 on_finish(j)
+
+
+class LocalFusedWorld:
+    """`world` ranks of the C++ fused step in ONE process (include/gdf_fused.h gdf_fused_local):
+    one engine and one host thread per rank, the step's collectives as device copies on the ranks'
+    streams.  The multi-rank C++ step on one GPU (RCCL refuses two ranks on one device); a rank is
+    NativeFusedRank(..., local=this)."""
+
+    def __init__(self, world: int, lib=None):
+        import ctypes as C
+        from .gdf import load_library
+        self._lib = lib or load_library()
+        self.world = world
+        h = C.c_void_p()
+        rc = self._lib.gdf_fused_local_create(world, C.byref(h))
+        if rc:
+            raise RuntimeError("gdf_fused_local_create: %d" % rc)
+        self.handle = h
+
+    def run(self, fn, timeout: float = 600.0):
+        """fn(rank) on `world` threads (ctypes drops the GIL inside the library calls); returns
+        their results in rank order, re-raises the first failure."""
+        import threading
+        out, err = [None] * self.world, [None] * self.world
+
+        def body(r):
+            try:
+                out[r] = fn(r)
+            except BaseException as e:  # noqa: BLE001 - handed to the caller
+                err[r] = e
+
+        ts = [threading.Thread(target=body, args=(r,), daemon=True) for r in range(self.world)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout)
+        if any(t.is_alive() for t in ts):
+            raise TimeoutError("local fused ranks still running after %.0f s" % timeout)
+        for e in err:
+            if e is not None:
+                raise e
+        return out
+
+    def close(self):
+        if getattr(self, "handle", None):
+            rc = self._lib.gdf_fused_local_destroy(self.handle)
+            if rc:
+                raise RuntimeError("gdf_fused_local_destroy: %d (ranks still alive)" % rc)
+            self.handle = None
 
 
 def rccl_library_path() -> str:
@@ -622,9 +668,11 @@ class NativeFusedRank:
     torch op or host copy between the launches of a step.  Same start / finish / run / frame /
     batch interface and results as FusedCloudRank(dev="cuda")."""
 
-    def __init__(self, engine, cams, rank: int, world: int, params, depth: int = 1):
+    def __init__(self, engine, cams, rank: int, world: int, params, depth: int = 1, local=None):
+        """local: a LocalFusedWorld - the rank is one of `world` ranks of THIS process (one host
+        thread and one engine each) exchanging through device copies (gdf_fused_create_local);
+        None: one rank per process over RCCL (ids broadcast over the default process group)."""
         import ctypes as C
-        import torch.distributed as dist
         from . import hiprt
         from .gdf import StreamCamera
         self.eng, self.cams, self.rank, self.world, self.p = engine, cams, rank, world, params
@@ -632,13 +680,6 @@ class NativeFusedRank:
         self.depth = max(1, min(4, int(depth)))
         self._lib = engine._lib
         self.F = params.flying_filter_size
-        path = rccl_library_path().encode()
-        ids = (C.c_uint8 * 256)()
-        if rank == 0:
-            engine._check(self._lib.gdf_fused_unique_id(path, ids))
-        obj = [bytes(ids)]
-        dist.broadcast_object_list(obj, src=0)
-        ids = (C.c_uint8 * 256).from_buffer_copy(obj[0])
         sc = (StreamCamera * world)()
         for k in range(world):
             c = cams[k]
@@ -649,8 +690,21 @@ class NativeFusedRank:
         self._cams_c = sc
         h = C.c_void_p()
         engine.set_pipeline_depth(self.depth)
-        engine._check(self._lib.gdf_fused_create(engine.handle, path, ids, rank, world, sc,
-                                                 self.F, C.byref(h)))
+        self.local = local
+        if local is not None:
+            engine._check(self._lib.gdf_fused_create_local(engine.handle, local.handle, rank, world,
+                                                           sc, self.F, C.byref(h)))
+        else:
+            import torch.distributed as dist
+            path = rccl_library_path().encode()
+            ids = (C.c_uint8 * 256)()
+            if rank == 0:
+                engine._check(self._lib.gdf_fused_unique_id(path, ids))
+            obj = [bytes(ids)]
+            dist.broadcast_object_list(obj, src=0)
+            ids = (C.c_uint8 * 256).from_buffer_copy(obj[0])
+            engine._check(self._lib.gdf_fused_create(engine.handle, path, ids, rank, world, sc,
+                                                     self.F, C.byref(h)))
         self._h = h
         L = C.c_uint32()
         engine._check(self._lib.gdf_fused_halo_pixels(h, C.byref(L)))
@@ -659,6 +713,14 @@ class NativeFusedRank:
         self.rollbuffer_rank = world - 1
         self.has_rollbuffer = rank == self.rollbuffer_rank
         self._pc_move = {}
+
+    def info(self):
+        """(rank, world, the rank count the transport reports, transport name)."""
+        import ctypes as C
+        r, w, n, k = C.c_int(), C.c_int(), C.c_int(), C.c_char_p()
+        self.eng._check(self._lib.gdf_fused_info(self._h, C.byref(r), C.byref(w), C.byref(n),
+                                                 C.byref(k)))
+        return r.value, w.value, n.value, k.value.decode()
 
     frame_params = FusedCloudRank.frame_params
 

@@ -59,3 +59,20 @@ def test_build_provenance_matches_sources():
     info = build_info(load_library())
     assert info["source_sha"] == source_digest()
     assert info.get("built_on") and info.get("built_at")
+
+
+def test_local_world_lifecycle_without_gpu():
+    """gdf_fused_local_create / _destroy (the in-process transport's world) touch no GPU: argument
+    checks, a world of 1..16 ranks, and gdf_fused_info / gdf_fused_create_local refusing nulls."""
+    import ctypes
+    from ros_gpu_depthmap_fusion_amd.gdf import load_library
+    lib = load_library()
+    h = ctypes.c_void_p()
+    assert lib.gdf_fused_local_create(0, ctypes.byref(h)) == -1
+    assert lib.gdf_fused_local_create(17, ctypes.byref(h)) == -1
+    assert lib.gdf_fused_local_create(4, ctypes.byref(h)) == 0 and h.value
+    out = ctypes.c_void_p()
+    assert lib.gdf_fused_create_local(None, h, 0, 4, None, 0, ctypes.byref(out)) == -1
+    assert lib.gdf_fused_info(None, None, None, None, None) == -1
+    assert lib.gdf_fused_local_destroy(h) == 0
+    assert lib.gdf_fused_local_destroy(None) == 0
