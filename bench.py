@@ -546,6 +546,7 @@ def main():
             out["secondary"] = secondary
         emit(out)
     if dist is not None:
+        eng.close()  # (the engine's streams before the process group: DESIGN.md §6, teardown)
         dist.barrier()
         dist.destroy_process_group()
 
@@ -693,7 +694,8 @@ def time_multi(args, st, params, dist, world, pmc_key):
     transport_ranks = dist.get_world_size()
     if fused and native:
         transport_ranks = fr.info()[2]  # (ncclCommCount of the step's points communicator)
-        fr.close()  # (its communicators, before the process group goes)
+    if fused:
+        fr.close()  # (its communicators / slot tensors, before the engine and the process group)
     if fused:
         cfg = {"parallelism": "camera-per-GPU x%d; per step of %d frames (one launch chain): "
                               "depth-tail halo all-gather, occupancy-mark all-gather + batched "

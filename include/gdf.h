@@ -256,8 +256,9 @@ int gdf_get_device_results(gdf_engine* engine, const float** points, const uint3
 /* All of a frame's host-side outputs at once (the component downloads points, voxel coords, the
  * voxelized cloud and the u8 grid every frame, component.cpp:297-401): the copies run on the
  * frame's stream into engine-owned pinned host mirrors of the addressed slot, with one wait for
- * them all; the pointers stay valid until the slot's next gdf_download_frame (or gdf_destroy).
- * `what` is a mask of GDF_DL_*; members not asked for are NULL / 0.  (No single reference
+ * them all; the pointers stay valid until the slot's next gdf_download_frame (or gdf_destroy):
+ * frames processed in between write their prefetched downloads into a second set of mirrors, never
+ * into the set last handed out.  `what` is a mask of GDF_DL_*; members not asked for are NULL / 0.  (No single reference
  * counterpart: it replaces downloadPoints + downloadVoxelCoords + the voxelized download +
  * downloadVoxelOccupancyGrid, fusion.cpp:1712-1718, 1824-1839, 2946-2951.) */
 #define GDF_DL_POINTS 1u

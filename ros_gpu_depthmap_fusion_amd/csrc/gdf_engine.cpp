@@ -361,7 +361,16 @@ struct Slot {
         ~Pinned() {
             if (p) (void)hipHostFree(p);
         }
-    } h_pts, h_coords, h_vox, h_delta, h_miscpf;
+    };
+    // Two sets of mirrors: gdf_download_frame hands out set `mir_out`, and the next downloads
+    // (k_download's prefetch, or the copies of a later gdf_download_frame) go to the other set,
+    // so the views a caller holds stay intact until its next gdf_download_frame (gdf.h).
+    struct Mirrors {
+        Pinned pts, coords, vox, delta, misc;
+    } mir[2];
+    int mir_out = -1;               // the set last handed out (-1: none)
+    int mir_pf = 0;                 // the set this slot's valid prefetch wrote
+    int mir_next() const { return mir_out == 0 ? 1 : 0; }
     bool pf_valid = false;          // this slot's last frame wrote its downloads (k_download)
     bool part_emitted = false;      // this slot's last compaction wrote the emit partition
     hipStream_t dl_aux = nullptr;   // k_download of the points / coords, after the compaction,
@@ -1636,10 +1645,12 @@ void prefetch_downloads(gdf_engine* e, hipStream_t st, uint32_t parts) {
     }
     const uint32_t cap = std::max<uint32_t>(q.n_total, 1);
     const uint32_t dcap = q.delta_valid ? (uint32_t)((mark_words(e) + 3) / 4 * 4) : 0u;
+    const int set = q.mir_next();  // (never the set the caller holds)
+    Slot::Mirrors& M = q.mir[set];
     // a mirror about to grow is freed first: no earlier k_download may still write it
-    if (q.h_pts.bytes < (size_t)cap * 16 || q.h_coords.bytes < (size_t)cap * 4 ||
-        q.h_vox.bytes < (size_t)cap * 16 || q.h_delta.bytes < (size_t)std::max<uint32_t>(dcap, 4) * 36 ||
-        q.h_miscpf.bytes < kMiscWords * 4) {
+    if (M.pts.bytes < (size_t)cap * 16 || M.coords.bytes < (size_t)cap * 4 ||
+        M.vox.bytes < (size_t)cap * 16 || M.delta.bytes < (size_t)std::max<uint32_t>(dcap, 4) * 36 ||
+        M.misc.bytes < kMiscWords * 4) {
         HIPCHK(hipStreamSynchronize(q.stream()));
         if (q.dl_aux) HIPCHK(hipStreamSynchronize(q.dl_aux));
     }
@@ -1657,18 +1668,21 @@ void prefetch_downloads(gdf_engine* e, hipStream_t st, uint32_t parts) {
     d.pts_cap = cap;
     d.vox_cap = (uint32_t)std::min<size_t>(q.d_vox.bytes / 16, cap);
     d.delta_cap = dcap;
-    d.h_misc = static_cast<uint32_t*>(q.h_miscpf.ensure(kMiscWords * 4));
-    d.h_pts = static_cast<uint4*>(q.h_pts.ensure((size_t)cap * 16));
-    d.h_coords = static_cast<uint32_t*>(q.h_coords.ensure((size_t)cap * 4));
-    d.h_vox = static_cast<uint4*>(q.h_vox.ensure((size_t)cap * 16));
-    uint8_t* hd = static_cast<uint8_t*>(q.h_delta.ensure((size_t)std::max<uint32_t>(dcap, 4) * 36));
+    d.h_misc = static_cast<uint32_t*>(M.misc.ensure(kMiscWords * 4));
+    d.h_pts = static_cast<uint4*>(M.pts.ensure((size_t)cap * 16));
+    d.h_coords = static_cast<uint32_t*>(M.coords.ensure((size_t)cap * 4));
+    d.h_vox = static_cast<uint4*>(M.vox.ensure((size_t)cap * 16));
+    uint8_t* hd = static_cast<uint8_t*>(M.delta.ensure((size_t)std::max<uint32_t>(dcap, 4) * 36));
     if (!d.h_misc || !d.h_pts || !d.h_coords || !d.h_vox || !hd)
         fail(GDF_ERR_NOMEM, "pinned download mirror allocation failed");
     d.h_didx = reinterpret_cast<uint32_t*>(hd);
     d.h_ddata = reinterpret_cast<uint4*>(hd + (size_t)dcap * 4);
     d.parts = parts;
     HIPCHK(launch_download(d, st));
-    if (parts & DL_MISC) q.pf_valid = true;
+    if (parts & DL_MISC) {
+        q.pf_valid = true;
+        q.mir_pf = set;
+    }
 }
 
 void run_fused_frame(gdf_engine* e, int average, uint32_t lifetime) {
@@ -2330,7 +2344,9 @@ int gdf_download_frame(gdf_engine* e, uint32_t what, gdf_host_frame* out) {
             e->sync();
             if (q.dl_aux) HIPCHK(hipStreamSynchronize(q.dl_aux));
             q.pf_valid = false;
-            const uint32_t* hm = static_cast<const uint32_t*>(q.h_miscpf.p);
+            Slot::Mirrors& M = q.mir[q.mir_pf];
+            q.mir_out = q.mir_pf;  // (handed out: the next prefetch writes the other set)
+            const uint32_t* hm = static_cast<const uint32_t*>(M.misc.p);
             if (hm[kErr]) {
                 HIPCHK(hipMemsetAsync(q.d_misc.as<uint32_t>() + kErr, 0, 4, e->s()));
                 fail(GDF_ERR_DEVICE, "device look-back spin limit expired (code " + std::to_string(hm[kErr]) + ")");
@@ -2338,15 +2354,15 @@ int gdf_download_frame(gdf_engine* e, uint32_t what, gdf_host_frame* out) {
             std::memcpy(q.h_misc, hm, kMiscWords * 4);
             const uint32_t n = hm[kCount], nv = hm[kVoxCount];
             if (what & GDF_DL_POINTS) {
-                out->points = static_cast<const float*>(q.h_pts.p);
+                out->points = static_cast<const float*>(M.pts.p);
                 out->num_points = n;
             }
             if (what & GDF_DL_COORDS) {
-                out->voxel_coords = static_cast<const uint32_t*>(q.h_coords.p);
+                out->voxel_coords = static_cast<const uint32_t*>(M.coords.p);
                 out->num_points = n;
             }
             if (what & GDF_DL_VOXELIZED) {
-                out->voxelized = static_cast<const float*>(q.h_vox.p);
+                out->voxelized = static_cast<const float*>(M.vox.p);
                 out->num_voxelized = nv;
             }
             if (what & GDF_DL_GRID) {
@@ -2360,7 +2376,7 @@ int gdf_download_frame(gdf_engine* e, uint32_t what, gdf_host_frame* out) {
                 if (!e->h_mirror.ensure(padded)) fail(GDF_ERR_NOMEM, "pinned grid mirror allocation failed");
                 uint8_t* mir = static_cast<uint8_t*>(e->h_mirror.p);
                 if (apply) {
-                    const uint8_t* hd = static_cast<const uint8_t*>(q.h_delta.p);
+                    const uint8_t* hd = static_cast<const uint8_t*>(M.delta.p);
                     const uint32_t* idx = reinterpret_cast<const uint32_t*>(hd);
                     const uint8_t* data = hd + (size_t)dcap * 4;
                     for (uint32_t k = 0; k < nd; ++k)
@@ -2380,6 +2396,8 @@ int gdf_download_frame(gdf_engine* e, uint32_t what, gdf_host_frame* out) {
         }
         e->read_misc();  // the counts (one wait)
         const uint32_t n = q.h_misc[kCount], nv = q.h_misc[kVoxCount];
+        Slot::Mirrors& M = q.mir[q.mir_next()];  // (not the set the caller still holds)
+        q.mir_out = q.mir_next();
         auto copy = [&](Slot::Pinned& m, const void* src, size_t bytes) -> void* {
             void* dst = m.ensure(std::max<size_t>(bytes, 64));
             if (!dst) fail(GDF_ERR_NOMEM, "pinned host mirror allocation failed");
@@ -2387,15 +2405,15 @@ int gdf_download_frame(gdf_engine* e, uint32_t what, gdf_host_frame* out) {
             return dst;
         };
         if (what & GDF_DL_POINTS) {
-            out->points = static_cast<const float*>(copy(q.h_pts, q.d_pts.p, (size_t)n * 16));
+            out->points = static_cast<const float*>(copy(M.pts, q.d_pts.p, (size_t)n * 16));
             out->num_points = n;
         }
         if (what & GDF_DL_COORDS) {
-            out->voxel_coords = static_cast<const uint32_t*>(copy(q.h_coords, q.d_coords.p, (size_t)n * 4));
+            out->voxel_coords = static_cast<const uint32_t*>(copy(M.coords, q.d_coords.p, (size_t)n * 4));
             out->num_points = n;
         }
         if (what & GDF_DL_VOXELIZED) {
-            out->voxelized = static_cast<const float*>(copy(q.h_vox, q.d_vox.p, (size_t)nv * 16));
+            out->voxelized = static_cast<const float*>(copy(M.vox, q.d_vox.p, (size_t)nv * 16));
             out->num_voxelized = nv;
         }
         // the grid: into the engine's host mirror - only the groups the last update changed when
@@ -2411,7 +2429,7 @@ int gdf_download_frame(gdf_engine* e, uint32_t what, gdf_host_frame* out) {
             const size_t padded = (size_t)mark_words(e) * 32;
             if (!e->h_mirror.ensure(padded)) fail(GDF_ERR_NOMEM, "pinned grid mirror allocation failed");
             if (apply_delta) {
-                uint8_t* st = static_cast<uint8_t*>(q.h_delta.ensure((size_t)std::max<uint32_t>(nd, 1) * 36));
+                uint8_t* st = static_cast<uint8_t*>(M.delta.ensure((size_t)std::max<uint32_t>(nd, 1) * 36));
                 if (!st) fail(GDF_ERR_NOMEM, "pinned delta staging allocation failed");
                 if (nd) {
                     HIPCHK(hipMemcpyAsync(st, q.d_didx.p, (size_t)nd * 4, hipMemcpyDeviceToHost, e->s()));
@@ -2430,7 +2448,7 @@ int gdf_download_frame(gdf_engine* e, uint32_t what, gdf_host_frame* out) {
         }
         e->sync();  // every copy (the second wait)
         if (apply_delta && nd) {  // the changed groups into the mirror (32 bytes each)
-            const uint8_t* st = static_cast<const uint8_t*>(q.h_delta.p);
+            const uint8_t* st = static_cast<const uint8_t*>(M.delta.p);
             const uint32_t* idx = reinterpret_cast<const uint32_t*>(st);
             const uint8_t* data = st + (size_t)nd * 4;
             uint8_t* mir = static_cast<uint8_t*>(e->h_mirror.p);
@@ -2468,6 +2486,12 @@ int gdf_get_device_results(gdf_engine* e, const float** pts, const uint32_t** co
 int gdf_process_frame(gdf_engine* e, const gdf_frame_params* p, gdf_frame_result* r) {
     ENGINE_OR_FAIL(e);
     if (!p) return GDF_ERR_ARG;
+    // gdf_set_emit_partition arms ONE frame: disarmed on every exit, failures included (a later
+    // frame must never write send lists into the caller's stale buffers)
+    struct Disarm {
+        gdf_engine* e;
+        ~Disarm() { e->epart = gdf_engine::EmitPart{}; }
+    } disarm{e};
     return guarded(e, [&] {
         gdf_frame_result res{};
         uint32_t collected;

@@ -11,6 +11,14 @@
 //   k_sort_*, k_group  inc/voxelize.h:74-105 + radix_grouper.h + radix_sort.h (GPU version)
 #include <atomic>
 #include "gdf_kernels.hpp"
+
+// The fence-free hand-offs (publish_count / arrive_and_scan, grid_seq_enter / grid_seq_leave
+// <COHERENT>) rely on gfx950's cache policy bits: cpol sc1 = agent-coherent (write-through past the
+// XCD's L2), with vmcnt(0) draining the stores.  The same bits mean something else on other
+// targets: device code is built for gfx950 only.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "gdf_kernels.hip targets gfx950 (CDNA4) only: its coherence hand-offs use gfx950 cache bits"
+#endif
 #include "gdf_voxsum.hpp"  // the voxel sum (row_sum4): exact integer stretches
 
 #include <algorithm>
@@ -659,8 +667,20 @@ __device__ __forceinline__ uint32_t sel_bits(const FrameArgs& a, const SelSeg& g
 }
 
 // Camera descriptors: kernel arguments for up to kArgCams cameras, else the device copy.
+// The kernel-argument table is addressed in the kernarg segment itself, never through `a`: the
+// callers read it with GLOBAL loads (G()), which is valid for the kernarg segment but not for a
+// private copy of the by-value struct - and the compiler may keep one (2.2 KB of scratch per
+// lane: an asm memory clobber in round 4, k_mask_px<4> always).  G() of a scratch address is an
+// address in the private aperture, not a global one: HSA_STATUS_ERROR_MEMORY_APERTURE_VIOLATION
+// (round 4's k_mask_px_o8 fault).  Every caller is a kernel whose only argument is
+// the FrameArgs, at offset 0 of the segment.
 __device__ __forceinline__ const CamDesc* cam_table(const FrameArgs& a) {
-    return a.ncams <= kArgCams ? a.cams : a.cams_dev;
+    if (a.ncams <= kArgCams) {
+        const char* ka = reinterpret_cast<const char*>(
+            (const void*)__builtin_amdgcn_kernarg_segment_ptr());
+        return reinterpret_cast<const CamDesc*>(ka + offsetof(FrameArgs, cams));
+    }
+    return a.cams_dev;
 }
 
 // block-wide copy of the camera descriptors into LDS
@@ -2408,7 +2428,10 @@ __device__ __forceinline__ uint32_t grid_seq_enter(const GridSeq& q) {
 
 // COHERENT: the block wrote the grid with agent-coherent stores (grid_store): once they have
 // completed they are visible to every XCD, and no per-block L2 write-back (an agent release fence,
-// buffer_wbl2, issued by each of hundreds of blocks) is needed before the block counts itself in
+// buffer_wbl2, issued by each of hundreds of blocks) is needed before the block counts itself in.
+// This covers ONLY the sc1 grid stores: the plain stores of the same blocks (a single frame's grid
+// delta, a batch's sparse snapshots) are read by later kernels of the SAME stream (k_download,
+// k_snap_expand), ordered by the kernel boundary's release, never by the next slot's update.
 template <bool COHERENT = false>
 __device__ __forceinline__ void grid_seq_leave(const GridSeq& q, uint32_t f, uint32_t nblocks) {
     if (!q.ctl) return;

@@ -328,7 +328,7 @@ class FusedCloudRank:
     mark / count collectives."""
 
     def __init__(self, engine, cams, rank: int, world: int, params, dev: str = "cuda",
-                 depth: int = 1, mark_slices: bool = False):
+                 depth: int = 1, mark_slices: bool = False, engine_streams: bool = False):
         import torch
         import torch.distributed as dist
         from . import hiprt
@@ -336,12 +336,23 @@ class FusedCloudRank:
         self.dev = dev
         self.hiprt = hiprt
         self.depth = max(1, int(depth)) if dev == "cuda" else 1
+        self.streams = None
+        self.engine_streams = False
         if dev == "cuda":
             engine.set_pipeline_depth(self.depth)
-            # the slots run on torch streams: torch's allocator and the collectives issued on
-            # them see streams that live as long as the process (the engine never destroys them)
-            self.streams = [torch.cuda.Stream() for _ in range(self.depth)]
-            engine.set_slot_streams([st.cuda_stream for st in self.streams])
+            # The slots' streams: torch streams by default (torch's allocator and the collectives
+            # issued on them see streams that live as long as the process), or the engine's own
+            # (engine_streams) wrapped as torch ExternalStreams.  Either way the slot tensors -
+            # allocated by torch's caching allocator ON those streams - must be released before
+            # the streams go: close() (then the engine's close) before destroy_process_group.
+            # Round 4's teardown SIGSEGV was exactly that order reversed: the rank's __dict__
+            # dropped the engine first (gdf_destroy: hipStreamDestroy of the slot streams), then
+            # the slot tensors, whose free path in the caching allocator used the destroyed
+            # streams (no Python frame on the faulthandler trace: a C-level tensor dealloc).
+            self.engine_streams = bool(engine_streams)
+            if not engine_streams:
+                self.streams = [torch.cuda.Stream() for _ in range(self.depth)]
+                engine.set_slot_streams([st.cuda_stream for st in self.streams])
             self.slots = {}
             # the points' communicator: its own RCCL stream (see the class docstring)
             self.pg_points = dist.new_group(list(range(world))) if world > 1 else None
@@ -369,6 +380,25 @@ class FusedCloudRank:
         self.mark_slices = bool(mark_slices) and dev != "cuda"
         if hasattr(engine, "set_partition_marks"):  # (the CPU tests' oracle stand-in has none)
             engine.set_partition_marks(not self.mark_slices)
+
+    def _slot_stream(self, k):
+        """Slot k's stream as a torch stream (the engine's slot k is the addressed slot)."""
+        import torch
+        if self.engine_streams:
+            return torch.cuda.ExternalStream(self.eng.stream())
+        return self.streams[k]
+
+    def close(self):
+        """Releases the slots' torch tensors (after their streams drained) and the streams, BEFORE
+        the engine (and the process group) go - see __init__.  The engine stays."""
+        import torch
+        if self.dev == "cuda":
+            self.eng.synchronize()
+            torch.cuda.synchronize()
+            self.slots = {}
+            self._keep = []
+            self._staged = {}
+            self.streams = None
 
     def frame_params(self, move=None):
         """The frame's gdf_frame_params: `move` = (T_world_move, T_crop_move) when the component's
@@ -424,7 +454,7 @@ class FusedCloudRank:
             S = self._slot(k)
             if S.pending:
                 raise RuntimeError("FusedCloudRank.start: the slot's previous step is unfinished")
-            st = self.streams[k]
+            st = self._slot_stream(k)
             S.ensure(st, tail_bytes=B * L2 if halo else 0)
             ctx = torch.cuda.stream(st)
         else:
@@ -522,7 +552,7 @@ class FusedCloudRank:
             S = self.slots[k]
             if not S.pending:
                 raise RuntimeError("FusedCloudRank.finish: no step in flight on this slot")
-            st = self.streams[k]
+            st = self._slot_stream(k)
             S.ev.synchronize()  # (the slot's split sizes; the later slots keep the GPU busy)
             both = [int(x) for x in S.host.tolist()]
             W = self.world

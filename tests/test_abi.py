@@ -76,3 +76,37 @@ def test_local_world_lifecycle_without_gpu():
     assert lib.gdf_fused_info(None, None, None, None, None) == -1
     assert lib.gdf_fused_local_destroy(h) == 0
     assert lib.gdf_fused_local_destroy(None) == 0
+
+
+def kernel_private_segments(lib_path):
+    """{kernel symbol: private_segment_fixed_size} of the gfx950 code object inside lib_path
+    (llvm-objcopy + clang-offload-bundler + llvm-readelf --notes from /opt/rocm/lib/llvm/bin)."""
+    import tempfile
+    llvm = "/opt/rocm/lib/llvm/bin"
+    with tempfile.TemporaryDirectory() as d:
+        fb, co = os.path.join(d, "fb.bin"), os.path.join(d, "gdf.co")
+        subprocess.run([f"{llvm}/llvm-objcopy", "--dump-section", f".hip_fatbin={fb}", lib_path],
+                       check=True, capture_output=True)
+        subprocess.run([f"{llvm}/clang-offload-bundler", "--unbundle", "--type=o",
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={fb}",
+                        f"--output={co}"], check=True, capture_output=True)
+        notes = subprocess.run([f"{llvm}/llvm-readelf", "--notes", co], check=True,
+                               capture_output=True, text=True).stdout
+    names = re.findall(r"^\s+\.name:\s+(\S+)\s*$", notes, re.M)
+    sizes = [int(x) for x in re.findall(r"\.private_segment_fixed_size:\s+(\d+)", notes)]
+    assert len(names) == len(sizes) > 20
+    return dict(zip(names, sizes))
+
+
+def test_no_kernel_keeps_a_private_copy_of_its_arguments():
+    """Round 4's k_mask_px_o8 fault: the compiler kept a private (scratch) copy of the 2 KB
+    by-value FrameArgs, and the kernels' global loads of the camera table then addressed scratch
+    (HSA_STATUS_ERROR_MEMORY_APERTURE_VIOLATION).  cam_table() now addresses the kernarg segment
+    itself; this pins the consequence: no kernel of the library spends more than 256 B of scratch
+    per lane (a copy of FrameArgs is > 2 KB; register spills of the frame kernels are <= 48 B)."""
+    from ros_gpu_depthmap_fusion_amd import build_library
+    sizes = kernel_private_segments(build_library())
+    frame = {k: v for k, v in sizes.items() if "FrameArgs" in k}
+    assert len(frame) >= 6
+    big = {k: v for k, v in sizes.items() if v > 256}
+    assert not big, big

@@ -198,7 +198,7 @@ def test_fused_cloud_survey_configs(tmp_path, cfg):
                                           f"{cfg} frame {f} rank {r}")
 
 
-def _rank_nccl(rank, world, port, out_dir, native=False):
+def _rank_nccl(rank, world, port, out_dir, native=False, engine_streams=False):
     """One process, RCCL (backend "nccl") at world 1: FusedCloudRank(dev="cuda") with the engine
     on torch's stream - the device collectives (all-gather of marks, all-to-all of counts and of
     the (point, key) lists, the gather of the fused cloud) over RCCL, frame by frame and per
@@ -215,7 +215,7 @@ def _rank_nccl(rank, world, port, out_dir, native=False):
     cams = [synth.make_camera(k, W, H) for k in range(world)]
     eng = GPUDepthmapFusion(0)
     fr = (multi.NativeFusedRank(eng, cams, rank, world, p) if native else
-          multi.FusedCloudRank(eng, cams, rank, world, p, dev="cuda"))
+          multi.FusedCloudRank(eng, cams, rank, world, p, dev="cuda", engine_streams=engine_streams))
     n = W * H
     ds = [hiprt.DeviceArray.from_numpy(synth.dense_frame(cams[rank], rank, f)) for f in range(4)]
     for f in range(2):
@@ -232,21 +232,24 @@ def _rank_nccl(rank, world, port, out_dir, native=False):
     for j in range(2):
         np.save(os.path.join(out_dir, f"nvox_f{2 + j}.npy"), vox[vs[j]:vs[j + 1]])
     np.save(os.path.join(out_dir, "ngrid_f3.npy"), eng.downloadVoxelOccupancyGrid())
-    if native:
-        fr.close()
+    # teardown in dependency order: the rank (its communicators / slot tensors), then the engine
+    # (its streams), then the process group - never the engine before what lives on its streams
+    fr.close()
+    eng.close()
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("native", [False, True])
-def test_rccl_fused_cloud_world1(tmp_path, native):
+@pytest.mark.parametrize("native,engine_streams", [(False, False), (True, False), (False, True)])
+def test_rccl_fused_cloud_world1(tmp_path, native, engine_streams):
     """The RCCL branch of FusedCloudRank (dev="cuda", backend nccl) - and its C++ form
     NativeFusedRank (gdf_fused_*, RCCL from libgdf) - on the box's GPU at world 1: two frames one
     by one, then a 2-frame batch - voxel means, grids and the gathered publishing cloud equal the
-    oracle bit for bit."""
+    oracle bit for bit.  engine_streams: the Python rank on the ENGINE's slot streams (round 4's
+    teardown SIGSEGV configuration), closed in dependency order."""
     from oracle import OracleFusion
-    mp.start_processes(_rank_nccl, args=(1, _free_port(), str(tmp_path), native), nprocs=1,
-                       join=True, start_method="spawn")
+    mp.start_processes(_rank_nccl, args=(1, _free_port(), str(tmp_path), native, engine_streams),
+                       nprocs=1, join=True, start_method="spawn")
     p = ComponentParams()
     cam = synth.make_camera(0, W, H)
     orc = OracleFusion(threads=4)
@@ -357,7 +360,8 @@ def test_fused_cloud_rollbuffer_leg(tmp_path, cfg):
 
 
 # ---- the pipelined RCCL path: steps in the engine's slots ----------------
-def _rank_nccl_pipe(rank, world, port, out_dir, depth, rollbuffer, native=False):
+def _rank_nccl_pipe(rank, world, port, out_dir, depth, rollbuffer, native=False,
+                    engine_streams=False):
     """RCCL at world 1, FusedCloudRank(depth=3).run(): step i+1 starts (compaction, marks, grid
     update, partition, split sizes) before step i's points all-to-all and voxelize - on the
     slots' own streams, the points on their own communicator.  Batches of 2 frames, or (with the
@@ -376,7 +380,8 @@ def _rank_nccl_pipe(rank, world, port, out_dir, depth, rollbuffer, native=False)
     cams = [synth.make_camera(k, W, H) for k in range(world)]
     eng = GPUDepthmapFusion(0)
     fr = (multi.NativeFusedRank(eng, cams, rank, world, p, depth=depth) if native else
-          multi.FusedCloudRank(eng, cams, rank, world, p, dev="cuda", depth=depth))
+          multi.FusedCloudRank(eng, cams, rank, world, p, dev="cuda", depth=depth,
+                               engine_streams=engine_streams))
     n = W * H
     B = 1 if rollbuffer else 2
     steps = 6
@@ -412,22 +417,24 @@ def _rank_nccl_pipe(rank, world, port, out_dir, depth, rollbuffer, native=False)
         fr.run_stream([d.ptr for d in ds], 0, steps, B)
         torch.cuda.synchronize()
         np.save(os.path.join(out_dir, "pvox_run_last.npy"), eng.downloadVoxelizedPoints()[:, :3])
-    if native:
-        fr.close()
+    fr.close()
+    eng.close()
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("rollbuffer,native", [(False, False), (True, False), (False, True),
-                                                (True, True)])
-def test_rccl_pipelined_fused_cloud_world1(tmp_path, rollbuffer, native):
+@pytest.mark.parametrize("rollbuffer,native,engine_streams",
+                         [(False, False, False), (True, False, False), (False, True, False),
+                          (True, True, False), (False, False, True), (True, False, True)])
+def test_rccl_pipelined_fused_cloud_world1(tmp_path, rollbuffer, native, engine_streams):
     """The pipelined fused path (three steps in flight on the engine's slots, the points
     all-to-all on a second communicator) under RCCL at world 1: every frame's voxel means, the
     final grid and (rollbuffer) the rollbuffer state after every frame equal the oracle's bit for
     bit."""
     import fused_ref
     from oracle import OracleFusion
-    mp.start_processes(_rank_nccl_pipe, args=(1, _free_port(), str(tmp_path), 3, rollbuffer, native),
+    mp.start_processes(_rank_nccl_pipe, args=(1, _free_port(), str(tmp_path), 3, rollbuffer, native,
+                                              engine_streams),
                        nprocs=1, join=True, start_method="spawn")
     p = ComponentParams()
     p.ps_timespan = 2.5 / 30.0
