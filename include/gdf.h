@@ -215,6 +215,22 @@ int gdf_insert_selected_point_sequence(gdf_engine* engine, const float T_world_m
 int gdf_transform_point_sequence(gdf_engine* engine);                    /* :1555-1581 */
 int gdf_get_rollbuffer_state(gdf_engine* engine, gdf_rollbuffer_state* out);
 
+/* Rollbuffer sharding (not in the reference: the multi-GPU window, include/gdf_fused.h).  Every
+ * shard is given EVERY point sequence (same order, same frames); sequence k (the k-th inserted
+ * since this call) keeps its points on shard (k / block) % nshards only, and enters the other
+ * shards' rollbuffers as a header without points.  So every shard rolls and selects the same
+ * sequences by time (rollPointSequenceRollbufferCPU / selectPointSequenceTimespanCPU depend only
+ * on the headers, fusion.cpp:1098-1217, 1358-1416) and holds ~1/nshards of the window; the shards'
+ * selected points, concatenated in gdf_get_rollbuffer_shard_order, are the unsharded selection
+ * (the point filter still sees every new point: its neighbours cross sequences).  The
+ * rollbuffer state then counts the shard's own points.  Set before the first sequence is
+ * inserted; nshards = 1: off. */
+int gdf_set_rollbuffer_shard(gdf_engine* engine, uint32_t shard, uint32_t nshards, uint32_t block);
+/* The shards in the order their selected points take in the unsharded selection (by their first
+ * selected sequence; shards holding none follow in shard order).  GDF_ERR_STATE when a shard
+ * holds two separate pieces of the selection (the window spans more than nshards blocks). */
+int gdf_get_rollbuffer_shard_order(gdf_engine* engine, uint32_t* order, uint32_t nshards);
+
 /* ---- depth chain ------------------------------------------------------------------------ */
 int gdf_upload_depthmaps(gdf_engine* engine);                            /* :1583-1593 */
 int gdf_convert_depthmaps(gdf_engine* engine);                           /* :1595-1628 */
@@ -406,6 +422,12 @@ int gdf_partition_runs(gdf_engine* engine, uint32_t nparts, float* send_points_d
 int gdf_set_emit_partition(gdf_engine* engine, uint32_t nparts, float* send_points_device,
                            uint32_t* send_run_keys_device, uint32_t* send_run_starts_device,
                            uint32_t capacity, uint32_t* part_counts_device);
+/* nseg = 2 for the armed frame: each part is cut into two buckets, [the frame's depth points | its
+ * selected rollbuffer points] (bucket b = part * 2 + segment, bucket-major send lists, run starts
+ * relative to the bucket's first point, part_counts [2 nparts points | 2 nparts runs]): the
+ * multi-GPU step places the rollbuffer segments of the ranks behind every rank's depth points
+ * (the reference's buffer order, fusion.cpp:1509-1581).  Disarmed (1) with the emit partition. */
+int gdf_set_partition_segments(gdf_engine* engine, uint32_t nseg);
 /* Whether a deferred frame armed with gdf_set_emit_partition sets its occupancy marks (default 1).
  * 0: a caller that builds the union from gdf_voxelize_runs_marked skips the compaction's marks
  * (and their clear) - the frame then has no marks to take. */

@@ -5,19 +5,21 @@
  * the buffer order [camera 0 .. camera N-1 pixels, rollbuffer points] at :1509-1581, one voxelize
  * at :1743-1756).  Here each rank (one process per GPU) holds one camera; a step is
  *   depth-tail halo all-gather (camera k reads camera k-1's last F rows + F pixels)
- *   -> the rank's compaction + voxel keys + occupancy marks (gdf_process_frame, deferred)
- *   -> occupancy-mark all-gather + the batched grid update (every rank the same grid)
- *   -> key-range partition -> split-size all-gather -> (finish) the points / keys all-to-all as
- *      grouped send / recv -> voxelize of the rank's key range (gdf_voxelize_points),
+ *   -> the rank's compaction + voxel keys (gdf_process_frame, deferred)
+ *   -> key-range partition (buckets [depth | rollbuffer] per range) -> split-size all-gather
+ *   -> (finish) the points / runs all-to-all as grouped send / recv -> voxelize of the rank's key
+ *      range (gdf_voxelize_runs_marked) -> mark-slice all-gather -> batched grid update,
  * with the collectives issued by this library on the engine slot's stream through RCCL
  * (dlopen'ed: the caller names the librccl it already loaded - torch's - so one RCCL serves the
  * process).  Everything runs through the public C-ABI of include/gdf.h; the Python
  * FusedCloudRank (ros_gpu_depthmap_fusion_amd/multi.py) is the same protocol with torch
  * collectives and is the one the gloo CPU tests drive.
  *
- * Two communicators: A carries the halo / marks / split sizes, B the points.  Operations on one
- * communicator run in issue order, so B's all-to-all of step i never queues behind step i + 1's
- * collectives on A (the step is pipelined: start(i + 1) is issued before finish(i)).
+ * Two communicators: A carries the halo tails / split sizes (the start), B the points, runs and
+ * mark slices (the finish).  Operations on one communicator run in issue order, so B's exchange of
+ * step i never queues behind step i + 1's collectives on A (the step is pipelined: start(i + 1) is
+ * issued before finish(i)).  The collectives go through a transport: RCCL (gdf_fused_create) or
+ * the in-process one below (gdf_fused_create_local).
  */
 #ifndef GDF_FUSED_H
 #define GDF_FUSED_H
@@ -70,6 +72,18 @@ int gdf_fused_create_local(gdf_engine* engine, gdf_fused_local* world, int rank,
  * communicator) and the transport's name ("rccl" / "local"; a static string). */
 int gdf_fused_info(gdf_fused* rank, int* rank_out, int* world, int* transport_ranks,
                    const char** transport);
+
+/* The rollbuffer window sharded over the ranks (block > 0; 0 = the last rank holds it, SURVEY
+ * 8(e)): every rank is given EVERY point sequence (gdf_add_point_sequence[_device] on each
+ * engine, same order) and keeps the points of the sequences k with (k / block) % world == rank
+ * (gdf_set_rollbuffer_shard); a rollbuffer step (nframes == 1, move transform) then selects, on
+ * every rank, its share of the window, and the exchange carries two buckets per key range - the
+ * rank's depth points, its rollbuffer points - which each owner places as [every rank's depth
+ * points, the rollbuffer segments in the selection's order] (the reference's buffer, fusion.cpp
+ * :1509-1581, restricted to the key range).  The window may span at most `world` blocks (else the
+ * step fails: GDF_ERR_STATE); block = ceil((window - 1) / (world - 1)) sequences guarantees it.
+ * Call before the first sequence is added. */
+int gdf_fused_set_rollbuffer_shard(gdf_fused* rank, uint32_t block);
 
 /* Depth values of the halo every rank sends (max over cameras of F * width + F). */
 int gdf_fused_halo_pixels(gdf_fused* rank, uint32_t* pixels);

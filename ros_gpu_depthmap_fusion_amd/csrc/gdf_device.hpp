@@ -54,6 +54,8 @@ constexpr int kSumChunk = 128;                               // points per wave 
 constexpr uint32_t kSpinLimit = 1u << 26;                   // bounded look-back spins
 constexpr uint32_t kDilateMaxF = 16;                        // mask_dilate window radius limit
 constexpr uint32_t kMaxParts = 16;                          // ranks of the fused-cloud partition
+constexpr uint32_t kMaxBuckets = 2 * kMaxParts;             // parts x segments [depth | rollbuffer]
+constexpr uint32_t kMaxSources = 2 * kMaxParts;             // received segments of gdf_voxelize_runs
 
 // Device-wide counters: monotonically increasing tile tickets (the host passes each launch's
 // base, so no per-launch memset) and the global digit histogram of the voxel keys.

@@ -206,6 +206,10 @@ struct CamTable {  // cached per-camera ray factors (xn per column, yn per row)
 struct Hdr {  // PointSequence, gpu_depthmap_fusion.h:178-204
     uint32_t sec, nsec, start, num;
     float T[16];
+    // (not in the reference) rollbuffer sharding, gdf_set_rollbuffer_shard: the sequence's arrival
+    // number and its point count before sharding (num = 0 for a sequence another shard holds)
+    uint64_t id = 0;
+    uint32_t num_global = 0;
 };
 
 // Where the points of collected sequences come from: a run of `n` points at collect offset `dst`,
@@ -372,6 +376,7 @@ struct Slot {
     int mir_pf = 0;                 // the set this slot's valid prefetch wrote
     int mir_next() const { return mir_out == 0 ? 1 : 0; }
     bool pf_valid = false;          // this slot's last frame wrote its downloads (k_download)
+    bool sel_frame = false;         // this slot's last frame compacted rollbuffer points (k_sel)
     bool part_emitted = false;      // this slot's last compaction wrote the emit partition
     hipStream_t dl_aux = nullptr;   // k_download of the points / coords, after the compaction,
     hipEvent_t dl_ev = nullptr;     // overlapping the voxelize (an event after the compaction)
@@ -476,6 +481,10 @@ struct gdf_engine {
     DevBuf d_ring;
     uint64_t ring_cap = 0, ring_head = 0;
     std::vector<Hdr> hdrA, hdrB;
+    // rollbuffer sharding (gdf_set_rollbuffer_shard): sequence id keeps its points on shard
+    // (id / shard_block) % nshards; every shard holds every header
+    uint32_t shard = 0, nshards = 1, shard_block = 1;
+    uint64_t seq_counter = 0;  // sequences inserted so far (their ids)
     gdf_rollbuffer_state rb{};
 
     // selected rollbuffer points
@@ -516,6 +525,7 @@ struct gdf_engine {
         uint32_t nparts = 0, cap = 0;
         float* pts = nullptr;
         uint32_t *run_keys = nullptr, *run_starts = nullptr, *counts = nullptr;
+        uint32_t nseg = 1;  // gdf_set_partition_segments: 2 = [depth | rollbuffer] buckets
     } epart;
     bool emit_part = !getenv("GDF_NO_EMIT_PART");  // (else: compaction, then the partition pass)
     // a frame armed with gdf_set_emit_partition sets its occupancy marks (gdf_set_partition_marks:
@@ -813,16 +823,38 @@ void insert_new_point_sequences(gdf_engine* e) {  // fusion.cpp:979-1087
     const uint32_t R = e->rb.num_points, S = e->rb.num_seqs;
     if (e->hdrB.size() < S) fail(GDF_ERR_STATE, "insert: rollbuffer headers out of sync");
     if ((uint64_t)R + e->n_new >= (1ull << 31)) fail(GDF_ERR_CAPACITY, "rollbuffer exceeds 2^31 points");
-    ensure_ring(e, (uint64_t)R + e->n_new);
-    if (e->n_new)
+    // sequence ids; a sharded engine keeps the points of its own sequences only (the filter still
+    // reads every new point: its neighbours cross sequences, filter_point_sequence.glsl:78-122)
+    uint32_t kept = 0;
+    std::vector<std::pair<uint32_t, uint32_t>> spans;  // own (first new point, count), merged
+    for (Hdr& h : e->new_hdrs) {
+        h.id = e->seq_counter++;
+        h.num_global = h.num;
+        const bool own = e->nshards <= 1 || (h.id / e->shard_block) % e->nshards == e->shard;
+        if (own && h.num) {
+            if (!spans.empty() && spans.back().first + spans.back().second == h.start)
+                spans.back().second += h.num;
+            else
+                spans.emplace_back(h.start, h.num);
+            kept += h.num;
+        }
+        if (!own) h.num = 0;
+    }
+    ensure_ring(e, (uint64_t)R + kept);
+    if (kept)
         e->timed(GDF_KERNEL_PS_INSERT, [&] {
-            HIPCHK(launch_ps_filter_insert(e->d_new.as<float4>(), e->n_new, e->ps_filter_set ? 1 : 0,
-                                           e->ps_thr, e->ps_F, e->d_ring.as<float4>(), e->ring_cap,
-                                           (e->ring_head + R) % e->ring_cap, e->s()));
+            uint32_t at = 0;
+            for (const auto& sp : spans) {
+                HIPCHK(launch_ps_filter_insert(e->d_new.as<float4>(), e->n_new, e->ps_filter_set ? 1 : 0,
+                                               e->ps_thr, e->ps_F, e->d_ring.as<float4>(), e->ring_cap,
+                                               (e->ring_head + R + at) % e->ring_cap, e->s(),
+                                               sp.first, sp.second));
+                at += sp.second;
+            }
         });
     e->hdrA.assign(e->hdrB.begin(), e->hdrB.begin() + S);
     e->hdrA.insert(e->hdrA.end(), e->new_hdrs.begin(), e->new_hdrs.end());
-    e->rb.num_points = R + e->n_new;
+    e->rb.num_points = R + kept;
     e->rb.num_seqs = S + (uint32_t)e->new_hdrs.size();
     if (!e->new_hdrs.empty()) {
         e->rb.last_time_sec = e->new_hdrs.back().sec;
@@ -915,6 +947,10 @@ void insert_selected(gdf_engine* e, const float* Twm, const float* Tcm) {  // fu
     if (cnt) {
         uint64_t cum = 0;
         int64_t s0 = -1;
+        if (e->nshards > 1) {  // the unsharded engine's s0: the first selected sequence with points
+            for (uint32_t j = ss; j < e->hdrB.size() && s0 < 0; ++j)
+                if (e->hdrB[j].num_global) s0 = j;
+        }
         for (uint32_t j = 0; j < e->hdrB.size(); ++j) {
             const uint64_t a = cum, b = cum + e->hdrB[j].num;
             cum = b;
@@ -1387,8 +1423,9 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel, bool compaction_marks = fa
     a.nframes = e->nframes;
     a.frame_shift = e->nframes > 1 ? e->key_bits : 0u;
     a.mark_words = mark_words(e);
+    e->sl().sel_frame = a.sel_tiles != 0;  // (the partition pass's [depth | rollbuffer] split)
     if (fused_voxel && compaction_marks && e->epart.nparts && e->emit_part && !a.sel_tiles &&
-        a.total_segs && !e->debug) {
+        e->epart.nseg == 1 && a.total_segs && !e->debug) {
         // the compaction writes the key-range partition itself (k_mask_px + k_emit_px2 only;
         // anything else compacts, then partitions: gdf_process_frame)
         FrameArgs t = a;
@@ -1844,18 +1881,24 @@ int guarded(gdf_engine* e, F&& f) {
         }                                                                   \
     } while (0)
 
+// nseg = 2: buckets [depth | rollbuffer] per part (the compacted depth points are the first
+// kDepthCount items of a frame with selected rollbuffer points, all of them otherwise)
 void partition_runs(gdf_engine* e, uint32_t nparts, float* send_pts, uint32_t* send_run_keys,
-                    uint32_t* send_run_starts, uint32_t capacity, uint32_t* part_counts) {
+                    uint32_t* send_run_starts, uint32_t capacity, uint32_t* part_counts,
+                    uint32_t nseg = 1) {
     {
         Slot& q = e->sl();
         if (!e->grid_set || !q.coords_valid) fail(GDF_ERR_STATE, "partition needs the voxel keys of a frame");
         if (nparts == 0 || nparts > kMaxParts) fail(GDF_ERR_ARG, "partition: 1..16 parts");
+        if (nseg != 1 && nseg != 2) fail(GDF_ERR_ARG, "partition: 1 or 2 segments");
         if (!send_pts || !send_run_keys || !send_run_starts || !part_counts)
             fail(GDF_ERR_ARG, "partition: null buffer");
         if (capacity < q.n_total) fail(GDF_ERR_CAPACITY, "partition: send buffers smaller than the frame");
         ensure_misc(e);
         const uint32_t nmax = std::max<uint32_t>(q.n_total, 1);
-        const uint32_t m = 2 * nparts * std::max<uint32_t>(part_tiles(nmax), 1u);
+        const uint32_t m = 2 * nparts * nseg * std::max<uint32_t>(part_tiles(nmax), 1u);
+        const uint32_t* split = nseg == 2 ? q.d_misc.as<uint32_t>() + (q.sel_frame ? kDepthCount : kCount)
+                                          : nullptr;
         q.d_pcnt.ensure((size_t)m * 4);
         q.d_poff.ensure(seg_offsets_words(m) * 4);
         HIPCHK(launch_partition(q.d_pts.as<float4>(), q.d_coords.as<uint32_t>(),
@@ -1864,7 +1907,8 @@ void partition_runs(gdf_engine* e, uint32_t nparts, float* send_pts, uint32_t* s
                                 q.d_misc.as<uint32_t>() + kPartTotal,
                                 reinterpret_cast<float4*>(send_pts), nullptr, part_counts, e->s(),
                                 q.nframes > 1 ? q.d_fstart.as<uint32_t>() : nullptr, q.nframes,
-                                q.nframes > 1 ? e->key_bits : 0u, send_run_keys, send_run_starts));
+                                q.nframes > 1 ? e->key_bits : 0u, send_run_keys, send_run_starts,
+                                split));
     }
 }
 
@@ -2202,6 +2246,53 @@ int gdf_get_rollbuffer_state(gdf_engine* e, gdf_rollbuffer_state* out) {
     if (!out) return GDF_ERR_ARG;
     *out = e->rb;
     return GDF_OK;
+}
+
+int gdf_set_rollbuffer_shard(gdf_engine* e, uint32_t shard, uint32_t nshards, uint32_t block) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        if (nshards == 0 || nshards > 16 || shard >= nshards || block == 0)
+            fail(GDF_ERR_ARG, "rollbuffer shard: 0 <= shard < nshards <= 16, block >= 1");
+        if (e->rb.num_seqs != 0 || !e->hdrB.empty())
+            fail(GDF_ERR_STATE, "rollbuffer shard: set before the first point sequence is inserted");
+        e->shard = shard;
+        e->nshards = nshards;
+        e->shard_block = block;
+        e->seq_counter = 0;
+    });
+}
+
+int gdf_get_rollbuffer_shard_order(gdf_engine* e, uint32_t* order, uint32_t nshards) {
+    ENGINE_OR_FAIL(e);
+    if (!order) return GDF_ERR_ARG;
+    return guarded(e, [&] {
+        if (nshards != e->nshards) fail(GDF_ERR_ARG, "rollbuffer shard order: nshards differs from the engine's");
+        const uint32_t ss = e->rb.selection_sequence_start, sc = e->rb.selection_sequence_count;
+        if (sc && (uint64_t)ss + sc > e->hdrB.size()) fail(GDF_ERR_STATE, "selection exceeds rollbuffer sequences");
+        std::vector<int64_t> first(nshards, -1);
+        std::vector<char> closed(nshards, 0);
+        int64_t cur = -1;
+        for (uint32_t j = ss; j < ss + sc; ++j) {
+            const Hdr& h = e->hdrB[j];
+            if (!h.num_global) continue;  // (no points on any shard)
+            const int64_t k = (int64_t)((h.id / e->shard_block) % e->nshards);
+            if (k == cur) continue;
+            if (cur >= 0) closed[cur] = 1;
+            if (closed[k])
+                fail(GDF_ERR_STATE, "rollbuffer shard order: a shard holds two separate pieces of the "
+                                    "selected window (the window spans more than nshards blocks: "
+                                    "raise the block size)");
+            first[k] = j;
+            cur = k;
+        }
+        std::vector<uint32_t> idx(nshards);
+        for (uint32_t k = 0; k < nshards; ++k) idx[k] = k;
+        std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) {
+            const int64_t fa = first[a] < 0 ? INT64_MAX : first[a], fb = first[b] < 0 ? INT64_MAX : first[b];
+            return fa < fb;
+        });
+        std::copy(idx.begin(), idx.end(), order);
+    });
 }
 
 int gdf_upload_depthmaps(gdf_engine* e) {
@@ -2561,7 +2652,8 @@ int gdf_process_frame(gdf_engine* e, const gdf_frame_params* p, gdf_frame_result
                 run_frame(e, true, true);
                 e->epart = gdf_engine::EmitPart{};  // (one frame)
                 if (ep.nparts && !e->sl().part_emitted)  // the compaction could not: a pass
-                    partition_runs(e, ep.nparts, ep.pts, ep.run_keys, ep.run_starts, ep.cap, ep.counts);
+                    partition_runs(e, ep.nparts, ep.pts, ep.run_keys, ep.run_starts, ep.cap, ep.counts,
+                                   ep.nseg);
                 if (!p->defer_occupancy_grid) occupancy_grid(e, p->occupancy_lifetime, e->s());
             } else if (!p->defer_occupancy_grid && e->grid_mode == 0) {
                 run_fused_frame(e, p->voxel_average, p->occupancy_lifetime);
@@ -2657,6 +2749,14 @@ int gdf_set_emit_partition(gdf_engine* e, uint32_t nparts, float* send_pts, uint
     });
 }
 
+int gdf_set_partition_segments(gdf_engine* e, uint32_t nseg) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        if (nseg != 1 && nseg != 2) fail(GDF_ERR_ARG, "partition segments: 1 or 2");
+        e->epart.nseg = nseg;
+    });
+}
+
 int gdf_set_partition_marks(gdf_engine* e, int enabled) {
     ENGINE_OR_FAIL(e);
     return guarded(e, [&] { e->part_marks = enabled != 0; });
@@ -2688,8 +2788,8 @@ int gdf_voxelize_runs_marked(gdf_engine* e, const float* pts, const uint32_t* ru
                       (e->nframes > 1 && frame_stride_words == 0)))
             fail(GDF_ERR_CAPACITY, "voxelize_runs: a frame's marks need >= the grid's mark words");
         if (!e->grid_set) fail(GDF_ERR_STATE, "voxelize_runs needs the voxel grid of a frame");
-        if (nsources == 0 || nsources > kMaxParts || !point_base || !run_base)
-            fail(GDF_ERR_ARG, "voxelize_runs: 1..16 sources and their bases");
+        if (nsources == 0 || nsources > kMaxSources || !point_base || !run_base)
+            fail(GDF_ERR_ARG, "voxelize_runs: 1..32 sources and their bases");
         RebaseArgs rb;
         std::memset(&rb, 0, sizeof(rb));
         rb.nsrc = nsources;

@@ -373,11 +373,14 @@ struct SlotX {
     DevBuf tail, tails;       // this rank's halo tails, every rank's (all-gather)
     DevBuf gathered;          // the union of the step's marks: frame f at f * W * S words, rank
                               // j's key range in words [j S, (j + 1) S) (voxelize + all-gather)
-    // partitioned send lists (points, run keys, run starts), split sizes (points then runs per
-    // part), every rank's split sizes
-    DevBuf sp, srk, srs, cnt, cntall;
+    // partitioned send lists (points, run keys, run starts) in buckets b = 2 part + segment
+    // (segment 0: the rank's depth points, 1: its selected rollbuffer points); the split sizes
+    // record [points per bucket (2 W) | runs per bucket (2 W)] (cnt), every rank's (cntall), and
+    // the engine's own one-segment counts [points per part | runs per part] (cnt1)
+    DevBuf sp, srk, srs, cnt, cnt1, cntall;
     DevBuf rp, rrk, rrs;      // received lists
-    uint32_t* host = nullptr;  // pinned copy of cntall (world x 2 world)
+    uint32_t* host = nullptr;  // pinned copy of cntall (world x 4 world)
+    uint32_t order[16] = {};   // the ranks' rollbuffer segments in the selection's order
     hipEvent_t ev = nullptr;
     bool pending = false;
     int average = 1;  // the step's voxel_average
@@ -395,6 +398,7 @@ struct gdf_fused {
     int rank = 0, world = 1;
     std::vector<gdf_stream_camera> cams;
     uint32_t F = 0, Lmax = 0;
+    uint32_t shard_block = 0;  // > 0: the rollbuffer window sharded over the ranks
     SlotX slots[kSlots];
 
     ~gdf_fused() {
@@ -404,7 +408,7 @@ struct gdf_fused {
         }
         for (SlotX& s : slots) {
             for (DevBuf* b : {&s.tail, &s.tails, &s.gathered, &s.sp, &s.srk, &s.srs,
-                              &s.cnt, &s.cntall, &s.rp, &s.rrk, &s.rrs})
+                              &s.cnt, &s.cnt1, &s.cntall, &s.rp, &s.rrk, &s.rrs})
                 b->release();
             if (s.host) hipHostFree(s.host);
             if (s.ev) hipEventDestroy(s.ev);
@@ -472,13 +476,17 @@ void fused_start(gdf_fused* f, const uint16_t* const* depth, uint32_t B, const g
     q.synchronous = 0;
     q.defer_occupancy_grid = 1;
     q.defer_voxelize = 1;
-    if (R != W - 1) q.move_transform_available = 0;  // the rollbuffer: last rank only
+    // the rollbuffer: the last rank's, or every rank's shard of the window
+    const bool sharded = f->shard_block > 0;
+    if (!sharded && R != W - 1) q.move_transform_available = 0;
+    const bool rb = B == 1 && q.move_transform_available;
     // the send lists, written by the compaction itself (gdf_set_emit_partition): sized for the
-    // step's pixels (+ halo) plus, on the rollbuffer rank, every point the window can select
-    uint32_t* cnt = S.cnt.ensure<uint32_t>((size_t)2 * W * 4, st);
-    uint32_t* cntall = S.cntall.ensure<uint32_t>((size_t)2 * W * W * 4, st);
+    // step's pixels (+ halo) plus, on a rollbuffer rank, every point the window can select
+    uint32_t* cnt = S.cnt.ensure<uint32_t>((size_t)4 * W * 4, st);
+    uint32_t* cnt1 = S.cnt1.ensure<uint32_t>((size_t)2 * W * 4, st);
+    uint32_t* cntall = S.cntall.ensure<uint32_t>((size_t)4 * W * W * 4, st);
     size_t want = (size_t)B * c.width * c.height + (halo && R > 0 ? B * (size_t)f->Lmax : 0u);
-    if (R == W - 1 && B == 1 && p->move_transform_available) {  // + the window after the ingest
+    if (rb) {  // + the window after the ingest
         gdf_rollbuffer_state rs{};
         gdfchk(gdf_get_rollbuffer_state(e, &rs));
         uint32_t col = 0;
@@ -491,12 +499,23 @@ void fused_start(gdf_fused* f, const uint16_t* const* depth, uint32_t B, const g
         S.srs.ensure<uint32_t>(cap * 4, st);
         const uint32_t have = (uint32_t)std::min<size_t>({S.sp.cap / 16, S.srk.cap / 4, S.srs.cap / 4});
         gdfchk(gdf_set_emit_partition(e, W, S.sp.as<float>(), S.srk.as<uint32_t>(),
-                                      S.srs.as<uint32_t>(), have, cnt));
+                                      S.srs.as<uint32_t>(), have, rb ? cnt : cnt1));
+        // a rollbuffer frame: buckets [depth | rollbuffer] per part, the record's layout itself
+        if (rb) gdfchk(gdf_set_partition_segments(e, 2));
     };
     arm(std::max<size_t>(want, 1));
     gdfchk(gdf_set_partition_marks(e, 0));
     gdf_frame_result res{};
     gdfchk(gdf_process_frame(e, &q, &res));
+    if (!rb) {  // [points per part | runs per part] -> the record's even (segment 0) buckets
+        hipchk(hipMemsetAsync(cnt, 0, (size_t)4 * W * 4, st), "hipMemsetAsync(record)");
+        hipchk(hipMemcpy2DAsync(cnt, 8, cnt1, 4, 4, (size_t)2 * W, hipMemcpyDeviceToDevice, st),
+               "hipMemcpy2DAsync(record)");
+    }
+    // the ranks' rollbuffer segments in the selection's order (the same on every rank: the
+    // headers are replicated); unsharded, only the last rank's is non-empty
+    for (int k = 0; k < W; ++k) S.order[k] = (uint32_t)k;
+    if (sharded && rb) gdfchk(gdf_get_rollbuffer_shard_order(e, S.order, (uint32_t)W));
     // The compaction sets no marks (gdf_set_partition_marks(e, 0) before the frame): W full
     // bitmasks of B frames (3.4 MB per rank and step at VGA x 8, received W - 1 times) would travel;
     // instead the key-range voxelize of the finish marks every voxel of its range - whole mark
@@ -506,8 +525,8 @@ void fused_start(gdf_fused* f, const uint16_t* const* depth, uint32_t B, const g
     // every rank's split sizes (the partition's, written with the compaction) to pinned memory
     // (no wait here)
     ++x.calls;
-    x.all_gather(cnt, cntall, (size_t)2 * W * 4, kHalo, st);
-    hipchk(hipMemcpyAsync(S.host, cntall, (size_t)2 * W * W * 4, hipMemcpyDeviceToHost, st),
+    x.all_gather(cnt, cntall, (size_t)4 * W * 4, kHalo, st);
+    hipchk(hipMemcpyAsync(S.host, cntall, (size_t)4 * W * W * 4, hipMemcpyDeviceToHost, st),
            "hipMemcpyAsync(counts)");
     hipchk(hipEventRecord(S.ev, st), "hipEventRecord");
     S.average = q.voxel_average ? 1 : 0;
@@ -527,57 +546,83 @@ void fused_finish(gdf_fused* f, int slot, uint32_t* send_counts, uint32_t* recv_
     hipStream_t st = static_cast<hipStream_t>(sv);
     hipchk(hipEventSynchronize(S.ev), "hipEventSynchronize");  // (the later slots keep the GPU busy)
     const int W = f->world, R = f->rank;
-    // rank q's split sizes: host[q * 2W + p] points to part p, host[q * 2W + W + p] runs
-    auto pts_of = [&](int from, int to) -> uint64_t { return S.host[(size_t)from * 2 * W + to]; };
-    auto runs_of = [&](int from, int to) -> uint64_t { return S.host[(size_t)from * 2 * W + W + to]; };
-    uint32_t pbase[17], rbase[17];
-    uint64_t n = 0, nr = 0;
+    // rank q's record: host[q * 4W + 2 p + s] points of bucket (part p, segment s),
+    // host[q * 4W + 2W + 2 p + s] its runs
+    auto pts_of = [&](int from, int to, int sg) -> uint64_t { return S.host[(size_t)from * 4 * W + 2 * to + sg]; };
+    auto runs_of = [&](int from, int to, int sg) -> uint64_t {
+        return S.host[(size_t)from * 4 * W + 2 * W + 2 * to + sg];
+    };
+    // sources in the reference's buffer order: every rank's depth points (rank order = camera
+    // order), then the rollbuffer segments in the selection's order (fusion.cpp:1509-1581)
+    const int NS = 2 * W;
+    int src_rank[32], src_seg[32];
     for (int q = 0; q < W; ++q) {
-        pbase[q] = (uint32_t)n;
-        rbase[q] = (uint32_t)nr;
-        n += pts_of(q, R);
-        nr += runs_of(q, R);
+        src_rank[q] = q;
+        src_seg[q] = 0;
+        src_rank[W + q] = (int)S.order[q];
+        src_seg[W + q] = 1;
+    }
+    uint32_t pbase[33], rbase[33];
+    uint64_t n = 0, nr = 0;
+    uint64_t recv_at[16][2] = {}, rrecv_at[16][2] = {};  // where rank q's segment s lands
+    for (int k = 0; k < NS; ++k) {
+        const int q = src_rank[k], sg = src_seg[k];
+        if (q < 0 || q >= W) fail(GDF_ERR_STATE, "fused finish: bad rollbuffer segment order");
+        pbase[k] = (uint32_t)n;
+        rbase[k] = (uint32_t)nr;
+        recv_at[q][sg] = n;
+        rrecv_at[q][sg] = nr;
+        n += pts_of(q, R, sg);
+        nr += runs_of(q, R, sg);
         if (n >= 0xFFFFFFFFull) fail(GDF_ERR_CAPACITY, "fused finish: 2^32 points received");
     }
-    pbase[W] = (uint32_t)n;
-    rbase[W] = (uint32_t)nr;
+    pbase[NS] = (uint32_t)n;
+    rbase[NS] = (uint32_t)nr;
     float* rp = S.rp.ensure<float>(std::max<uint64_t>(n, 1) * 16, st);
     uint32_t* rrk = S.rrk.ensure<uint32_t>(std::max<uint64_t>(nr, 1) * 4, st);
     uint32_t* rrs = S.rrs.ensure<uint32_t>((nr + 1) * 4, st);
-    size_t soff = 0, sroff = 0;
-    for (int q = 0; q < R; ++q) {
-        soff += pts_of(R, q);
-        sroff += runs_of(R, q);
+    // this rank's send list: bucket-major, bucket (q, s) at the sum of the buckets before it
+    uint64_t send_at[16][2] = {}, rsend_at[16][2] = {};
+    {
+        uint64_t o = 0, ro = 0;
+        for (int q = 0; q < W; ++q)
+            for (int sg = 0; sg < 2; ++sg) {
+                send_at[q][sg] = o;
+                rsend_at[q][sg] = ro;
+                o += pts_of(R, q, sg);
+                ro += runs_of(R, q, sg);
+            }
     }
-    // the rank's own part: a device copy (an RCCL self send / recv is a slower kernel copy)
-    if (const size_t c = pts_of(R, R)) {
-        hipchk(hipMemcpyAsync(rp + 4 * (size_t)pbase[R], S.sp.as<float>() + 4 * soff, 16 * c,
-                              hipMemcpyDeviceToDevice, st), "hipMemcpyAsync(points)");
-        const size_t rc = runs_of(R, R);
-        hipchk(hipMemcpyAsync(rrk + rbase[R], S.srk.as<uint32_t>() + sroff, 4 * rc,
-                              hipMemcpyDeviceToDevice, st), "hipMemcpyAsync(run keys)");
-        hipchk(hipMemcpyAsync(rrs + rbase[R], S.srs.as<uint32_t>() + sroff, 4 * rc,
-                              hipMemcpyDeviceToDevice, st), "hipMemcpyAsync(run starts)");
-    }
+    // the rank's own buckets: device copies (an RCCL self send / recv is a slower kernel copy)
+    for (int sg = 0; sg < 2; ++sg)
+        if (const size_t c = pts_of(R, R, sg)) {
+            const size_t rc = runs_of(R, R, sg);
+            hipchk(hipMemcpyAsync(rp + 4 * recv_at[R][sg], S.sp.as<float>() + 4 * send_at[R][sg], 16 * c,
+                                  hipMemcpyDeviceToDevice, st), "hipMemcpyAsync(points)");
+            hipchk(hipMemcpyAsync(rrk + rrecv_at[R][sg], S.srk.as<uint32_t>() + rsend_at[R][sg], 4 * rc,
+                                  hipMemcpyDeviceToDevice, st), "hipMemcpyAsync(run keys)");
+            hipchk(hipMemcpyAsync(rrs + rrecv_at[R][sg], S.srs.as<uint32_t>() + rsend_at[R][sg], 4 * rc,
+                                  hipMemcpyDeviceToDevice, st), "hipMemcpyAsync(run starts)");
+        }
     if (W > 1) {
         ++x.calls;
         x.group_start(kPoints);
-        soff = sroff = 0;
         for (int q = 0; q < W; ++q) {
-            const size_t sc = pts_of(R, q), sr = runs_of(R, q);
-            const size_t rc = pts_of(q, R), rr = runs_of(q, R);
-            if (q != R && sc) {
-                x.send(S.sp.as<float>() + 4 * soff, 16 * sc, q, kPoints, st);
-                x.send(S.srk.as<uint32_t>() + sroff, 4 * sr, q, kPoints, st);
-                x.send(S.srs.as<uint32_t>() + sroff, 4 * sr, q, kPoints, st);
+            if (q == R) continue;
+            for (int sg = 0; sg < 2; ++sg) {  // (per peer, in the same order on both sides)
+                const size_t sc = pts_of(R, q, sg), sr = runs_of(R, q, sg);
+                if (sc) {
+                    x.send(S.sp.as<float>() + 4 * send_at[q][sg], 16 * sc, q, kPoints, st);
+                    x.send(S.srk.as<uint32_t>() + rsend_at[q][sg], 4 * sr, q, kPoints, st);
+                    x.send(S.srs.as<uint32_t>() + rsend_at[q][sg], 4 * sr, q, kPoints, st);
+                }
+                const size_t rc = pts_of(q, R, sg), rr = runs_of(q, R, sg);
+                if (rc) {
+                    x.recv(rp + 4 * recv_at[q][sg], 16 * rc, q, kPoints, st);
+                    x.recv(rrk + rrecv_at[q][sg], 4 * rr, q, kPoints, st);
+                    x.recv(rrs + rrecv_at[q][sg], 4 * rr, q, kPoints, st);
+                }
             }
-            if (q != R && rc) {
-                x.recv(rp + 4 * (size_t)pbase[q], 16 * rc, q, kPoints, st);
-                x.recv(rrk + rbase[q], 4 * rr, q, kPoints, st);
-                x.recv(rrs + rbase[q], 4 * rr, q, kPoints, st);
-            }
-            soff += sc;
-            sroff += sr;
         }
         x.group_end(kPoints, st);
     }
@@ -591,7 +636,7 @@ void fused_finish(gdf_fused* f, int slot, uint32_t* send_counts, uint32_t* recv_
     const uint64_t stride = Sw * W;
     uint32_t* uni = S.gathered.ensure<uint32_t>(S.nframes * stride * 4, st);
     hipchk(hipMemsetAsync(uni, 0, S.nframes * stride * 4, st), "hipMemsetAsync(marks)");
-    gdfchk(gdf_voxelize_runs_marked(e, rp, rrk, rrs, W, pbase, rbase, S.average, uni, stride));
+    gdfchk(gdf_voxelize_runs_marked(e, rp, rrk, rrs, (uint32_t)NS, pbase, rbase, S.average, uni, stride));
     if (W > 1) {  // (on the points' communicator: the finish's collectives stay in step order,
                   // never behind the next step's start collectives on the halo communicator)
         ++x.calls;
@@ -603,7 +648,7 @@ void fused_finish(gdf_fused* f, int slot, uint32_t* send_counts, uint32_t* recv_
     gdfchk(gdf_voxel_occupancy_grid_batch(e, uni, words, 1, S.nframes, stride, S.nframes * stride,
                                           S.lifetime));
     if (send_counts)
-        for (int q = 0; q < W; ++q) send_counts[q] = (uint32_t)pts_of(R, q);
+        for (int q = 0; q < W; ++q) send_counts[q] = (uint32_t)(pts_of(R, q, 0) + pts_of(R, q, 1));
     if (recv_count) *recv_count = (uint32_t)n;
     S.pending = false;
 }
@@ -626,7 +671,7 @@ gdf_fused* fused_new(gdf_engine* engine, int rank, int world, const gdf_stream_c
         if ((uint64_t)c.width * c.height < f->Lmax)
             fail(GDF_ERR_ARG, "fused multi-GPU frames need cameras taller than F rows");
     for (SlotX& s : f->slots) {
-        hipchk(hipHostMalloc(reinterpret_cast<void**>(&s.host), (size_t)2 * world * world * 4,
+        hipchk(hipHostMalloc(reinterpret_cast<void**>(&s.host), (size_t)4 * world * world * 4,
                              hipHostMallocDefault), "hipHostMalloc");
         hipchk(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming), "hipEventCreate");
     }
@@ -765,6 +810,15 @@ int gdf_fused_info(gdf_fused* f, int* rank, int* world, int* transport_ranks, co
 int gdf_fused_destroy(gdf_fused* f) {
     delete f;
     return GDF_OK;
+}
+
+int gdf_fused_set_rollbuffer_shard(gdf_fused* f, uint32_t block) {
+    if (!f) return GDF_ERR_ARG;
+    return guarded([&] {
+        gdfchk(gdf_set_rollbuffer_shard(f->e, block ? (uint32_t)f->rank : 0u,
+                                        block ? (uint32_t)f->world : 1u, block ? block : 1u));
+        f->shard_block = block;
+    });
 }
 
 int gdf_fused_halo_pixels(gdf_fused* f, uint32_t* pixels) {

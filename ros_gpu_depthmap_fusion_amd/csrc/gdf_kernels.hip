@@ -2328,12 +2328,16 @@ __device__ __forceinline__ bool ps_ok(const float4* pts, float px, float py, flo
     return !(1.0f - c < thr);
 }
 
+// new points [src0, src0 + cnt) of the n uploaded (a sharded engine's own sequences; the
+// filter's neighbours range over all n) into ring slots first, first + 1, ...
 __global__ __launch_bounds__(256) void k_ps_filter_insert(const float4* __restrict__ pts,
                                                           uint32_t n, int do_filter, float thr,
                                                           uint32_t F, float4* __restrict__ ring,
-                                                          uint64_t cap, uint64_t first) {
-    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= n) return;
+                                                          uint64_t cap, uint64_t first,
+                                                          uint32_t src0, uint32_t cnt) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    const uint32_t g = src0 + t;
     const float4 p = pts[g];
     bool valid = true;
     if (do_filter) {
@@ -2352,15 +2356,16 @@ __global__ __launch_bounds__(256) void k_ps_filter_insert(const float4* __restri
             }
         }
     }
-    ring[(first + g) % cap] = make_float4(p.x, p.y, p.z, valid ? 1.0f : 0.0f);
+    ring[(first + t) % cap] = make_float4(p.x, p.y, p.z, valid ? 1.0f : 0.0f);
 }
 
 hipError_t launch_ps_filter_insert(const float4* new_pts, uint32_t n, int do_filter, float thr,
                                    uint32_t F, float4* ring, uint64_t cap, uint64_t first,
-                                   hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_ps_filter_insert, dim3((n + 255) / 256), dim3(256), 0, s, new_pts, n,
-                       do_filter, thr, F, ring, cap, first);
+                                   hipStream_t s, uint32_t src0, uint32_t cnt) {
+    if (cnt == 0xFFFFFFFFu) cnt = n - src0;
+    if (cnt == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_ps_filter_insert, dim3((cnt + 255) / 256), dim3(256), 0, s, new_pts, n,
+                       do_filter, thr, F, ring, cap, first, src0, cnt);
     return hipGetLastError();
 }
 
@@ -4465,41 +4470,44 @@ __global__ __launch_bounds__(256) void k_part_count(const uint32_t* __restrict__
                                                     uint32_t nparts, uint64_t ncells,
                                                     uint32_t ntiles, uint32_t* __restrict__ counts,
                                                     const uint32_t* __restrict__ fstart,
-                                                    uint32_t nframes, uint32_t fshift) {
-    __shared__ uint32_t s_c[2 * kMaxParts];
+                                                    uint32_t nframes, uint32_t fshift,
+                                                    const uint32_t* __restrict__ seg_split) {
+    __shared__ uint32_t s_c[2 * kMaxBuckets];
     __shared__ uint32_t s_fstart[kMaxCams + 1];
     const bool batch = RUNS && fstart != nullptr && nframes > 1;
     if (batch) load_fstart(s_fstart, fstart, nframes);
     const uint32_t n = *count;
+    const uint32_t nseg = seg_split ? 2u : 1u, split = seg_split ? *seg_split : 0xFFFFFFFFu;
+    const uint32_t nb = nparts * nseg;
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {  // block-uniform
-        if (threadIdx.x < 2 * kMaxParts) s_c[threadIdx.x] = 0;
+        if (threadIdx.x < 2 * kMaxBuckets) s_c[threadIdx.x] = 0;
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const uint32_t i = t * kPartTile + q * 256 + threadIdx.x;
             if (i < n) {
                 const uint32_t key = keys[i];
-                const uint32_t part = part_of(key, nparts, ncells);
-                atomicAdd(&s_c[part], 1u);
-                if (RUNS && (i == t * kPartTile ||
+                const uint32_t b = part_of(key, nparts, ncells) * nseg + (i >= split ? 1u : 0u);
+                atomicAdd(&s_c[b], 1u);
+                if (RUNS && (i == t * kPartTile || i == split ||
                              sent_key(keys, i - 1, s_fstart, nframes, fshift, batch) !=
                                  (batch ? key | (frame_of(s_fstart, nframes, i) << fshift) : key)))
-                    atomicAdd(&s_c[kMaxParts + part], 1u);
+                    atomicAdd(&s_c[kMaxBuckets + b], 1u);
             }
         }
         __syncthreads();
-        if (threadIdx.x < nparts) {
+        if (threadIdx.x < nb) {
             counts[threadIdx.x * ntiles + t] = s_c[threadIdx.x];
-            if (RUNS) counts[(nparts + threadIdx.x) * ntiles + t] = s_c[kMaxParts + threadIdx.x];
+            if (RUNS) counts[(nb + threadIdx.x) * ntiles + t] = s_c[kMaxBuckets + threadIdx.x];
         }
         __syncthreads();
     }
 }
 
-// lanes of this wave in the same part as this lane, among the lanes of `m`
+// lanes of this wave in the same bucket as this lane, among the lanes of `m` (buckets < 32)
 __device__ __forceinline__ unsigned long long same_part(unsigned long long m, uint32_t part) {
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
+    for (int b = 0; b < 5; ++b) {
         const bool bit = (part >> b) & 1u;
         const unsigned long long bb = __ballot(bit);
         m &= bit ? bb : ~bb;
@@ -4521,12 +4529,13 @@ __global__ __launch_bounds__(256) void k_part_scatter(const float4* __restrict__
                                                       const uint32_t* __restrict__ fstart,
                                                       uint32_t nframes, uint32_t fshift,
                                                       uint32_t* __restrict__ out_run_keys,
-                                                      uint32_t* __restrict__ out_run_start) {
-    __shared__ uint32_t s_w[4][kMaxParts];  // per-wave running counts (slot-major order)
-    __shared__ uint32_t s_rw[4][kMaxParts];  // (runs)
-    __shared__ uint32_t s_base[kMaxParts];
-    __shared__ uint32_t s_rbase[kMaxParts];
-    __shared__ uint32_t s_pfirst[kMaxParts];  // the part's first send position
+                                                      uint32_t* __restrict__ out_run_start,
+                                                      const uint32_t* __restrict__ seg_split) {
+    __shared__ uint32_t s_w[4][kMaxBuckets];  // per-wave running counts (slot-major order)
+    __shared__ uint32_t s_rw[4][kMaxBuckets];  // (runs)
+    __shared__ uint32_t s_base[kMaxBuckets];
+    __shared__ uint32_t s_rbase[kMaxBuckets];
+    __shared__ uint32_t s_pfirst[kMaxBuckets];  // the bucket's first send position
     __shared__ uint32_t s_fstart[kMaxCams + 1];
     // a batch (fstart): the sent key carries the point's frame above the voxel key, the part
     // comes from the voxel key alone
@@ -4534,25 +4543,27 @@ __global__ __launch_bounds__(256) void k_part_scatter(const float4* __restrict__
     if (batch) load_fstart(s_fstart, fstart, nframes);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t n = *count;
-    const uint32_t mp = nparts * ntiles;  // (RUNS: the run counts' offsets follow the points')
-    if (blockIdx.x == 0 && threadIdx.x < nparts) {
+    const uint32_t nseg = seg_split ? 2u : 1u, split = seg_split ? *seg_split : 0xFFFFFFFFu;
+    const uint32_t nb = nparts * nseg;
+    const uint32_t mp = nb * ntiles;  // (RUNS: the run counts' offsets follow the points')
+    if (blockIdx.x == 0 && threadIdx.x < nb) {
         const uint32_t a = offsets[threadIdx.x * ntiles];
-        const uint32_t b = threadIdx.x + 1 < nparts ? offsets[(threadIdx.x + 1) * ntiles]
-                                                   : (RUNS ? offsets[mp] : *total);
+        const uint32_t b = threadIdx.x + 1 < nb ? offsets[(threadIdx.x + 1) * ntiles]
+                                               : (RUNS ? offsets[mp] : *total);
         part_counts[threadIdx.x] = b - a;
         if (RUNS) {
             const uint32_t ra = offsets[mp + threadIdx.x * ntiles];
-            const uint32_t rb = threadIdx.x + 1 < nparts ? offsets[mp + (threadIdx.x + 1) * ntiles] : *total;
-            part_counts[nparts + threadIdx.x] = rb - ra;
+            const uint32_t rb = threadIdx.x + 1 < nb ? offsets[mp + (threadIdx.x + 1) * ntiles] : *total;
+            part_counts[nb + threadIdx.x] = rb - ra;
         }
     }
     const unsigned long long ltm = lanemask_lt();
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {  // block-uniform
-        if (threadIdx.x < 4 * kMaxParts) {
+        if (threadIdx.x < 4 * kMaxBuckets) {
             (&s_w[0][0])[threadIdx.x] = 0;
             if (RUNS) (&s_rw[0][0])[threadIdx.x] = 0;
         }
-        if (threadIdx.x < nparts) {
+        if (threadIdx.x < nb) {
             s_base[threadIdx.x] = offsets[threadIdx.x * ntiles + t];
             if (RUNS) {
                 s_rbase[threadIdx.x] = offsets[mp + threadIdx.x * ntiles + t] - offsets[mp];
@@ -4570,14 +4581,14 @@ __global__ __launch_bounds__(256) void k_part_scatter(const float4* __restrict__
             const bool ok = i < n;
             key[q] = ok ? keys[i] : 0u;
             if (ok) p[q] = pts[i];
-            part[q] = ok ? part_of(key[q], nparts, ncells) : 0u;
+            part[q] = ok ? part_of(key[q], nparts, ncells) * nseg + (i >= split ? 1u : 0u) : 0u;
             if (batch && ok) key[q] |= frame_of(s_fstart, nframes, i) << fshift;
             const unsigned long long m = same_part(__ballot(ok), part[q]);
             const uint32_t before = (uint32_t)__popcll(m & ltm);
             const uint32_t base = ok ? s_w[w][part[q]] : 0u;
             rank[q] = base + before;
             if (RUNS) {
-                lead[q] = ok && (i == t * kPartTile ||
+                lead[q] = ok && (i == t * kPartTile || i == split ||
                                  sent_key(keys, i - 1, s_fstart, nframes, fshift, batch) != key[q]);
                 const unsigned long long lm = same_part(__ballot(lead[q]), part[q]);
                 const uint32_t rbefore = (uint32_t)__popcll(lm & ltm);
@@ -4596,7 +4607,7 @@ __global__ __launch_bounds__(256) void k_part_scatter(const float4* __restrict__
         }
         __syncthreads();
         // waves before this one in the tile
-        if (threadIdx.x < nparts) {
+        if (threadIdx.x < nb) {
             uint32_t run = 0, rrun = 0;
             for (int ww = 0; ww < 4; ++ww) {
                 const uint32_t c = s_w[ww][threadIdx.x];
@@ -4635,28 +4646,31 @@ hipError_t launch_partition(const float4* pts, const uint32_t* keys, const uint3
                             uint32_t* offsets, uint32_t* total, float4* out_pts,
                             uint32_t* out_keys, uint32_t* part_counts, hipStream_t s,
                             const uint32_t* fstart, uint32_t nframes, uint32_t fshift,
-                            uint32_t* out_run_keys, uint32_t* out_run_start) {
+                            uint32_t* out_run_keys, uint32_t* out_run_start,
+                            const uint32_t* seg_split) {
+    if (nparts == 0 || nparts > kMaxParts) return hipErrorInvalidValue;
     const uint32_t ntiles = std::max<uint32_t>(part_tiles(nmax), 1u);
     const uint32_t blocks = std::min<uint32_t>(ntiles, 2048u);
     const bool runs = out_run_keys != nullptr;
     if (runs)
         hipLaunchKernelGGL(k_part_count<true>, dim3(blocks), dim3(256), 0, s, keys, count, nparts,
-                           ncells, ntiles, counts, fstart, nframes, fshift);
+                           ncells, ntiles, counts, fstart, nframes, fshift, seg_split);
     else
         hipLaunchKernelGGL(k_part_count<false>, dim3(blocks), dim3(256), 0, s, keys, count, nparts,
-                           ncells, ntiles, counts, fstart, nframes, fshift);
+                           ncells, ntiles, counts, fstart, nframes, fshift, seg_split);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    const uint32_t m = (runs ? 2u : 1u) * nparts * ntiles;
+    const uint32_t nb = nparts * (seg_split ? 2u : 1u);
+    const uint32_t m = (runs ? 2u : 1u) * nb * ntiles;
     if ((e = launch_scan(counts, m, offsets, total, nullptr, 1u, s)) != hipSuccess) return e;
     if (runs)
         hipLaunchKernelGGL(k_part_scatter<true>, dim3(blocks), dim3(256), 0, s, pts, keys, count,
                            nparts, ncells, ntiles, offsets, total, out_pts, out_keys, part_counts,
-                           fstart, nframes, fshift, out_run_keys, out_run_start);
+                           fstart, nframes, fshift, out_run_keys, out_run_start, seg_split);
     else
         hipLaunchKernelGGL(k_part_scatter<false>, dim3(blocks), dim3(256), 0, s, pts, keys, count,
                            nparts, ncells, ntiles, offsets, total, out_pts, out_keys, part_counts,
-                           fstart, nframes, fshift, out_run_keys, out_run_start);
+                           fstart, nframes, fshift, out_run_keys, out_run_start, seg_split);
     return hipGetLastError();
 }
 

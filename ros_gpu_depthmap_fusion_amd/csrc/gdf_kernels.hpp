@@ -54,10 +54,11 @@ extern uint32_t g_emit_px2;
 extern uint32_t g_grid_wpt;
 extern uint32_t g_mask_occ8;
 
-// filter_point_sequence + insert into the rollbuffer ring (w = mask)
+// filter_point_sequence + insert into the rollbuffer ring (w = mask): new points
+// [src0, src0 + cnt) (all by default) of the n uploaded, their filter neighbours over all n
 hipError_t launch_ps_filter_insert(const float4* new_pts, uint32_t n, int do_filter, float thr,
                                    uint32_t F, float4* ring, uint64_t cap, uint64_t first,
-                                   hipStream_t s);
+                                   hipStream_t s, uint32_t src0 = 0, uint32_t cnt = 0xFFFFFFFFu);
 // device-resident PointCloud2 records (x, y, z at byte offsets 0/4/8, step % 4 == 0) -> float4 w=1
 hipError_t launch_gather_records(const void* rec, uint32_t n, uint32_t step, float4* out,
                                  hipStream_t s);
@@ -183,6 +184,10 @@ hipError_t launch_transform_points(const float4* in, const uint32_t* mask, float
 // With out_run_keys (runs mode): also the part-major runs of equal sent keys (run keys, run
 // starts relative to the part's first point), part_counts[nparts + p] = runs of part p, counts /
 // offsets twice as long (points' tile counts, then the runs'); out_keys may be null.
+// seg_split (device word, optional): TWO segments, items [0, split) and [split, n) (a frame's depth
+// points, then its rollbuffer points) - buckets b = part * 2 + segment take the place of the parts
+// (bucket-major output, part_counts [2 nparts points | 2 nparts runs], run starts relative to
+// the bucket's first point, a run never crossing the split); workspace sized for 2 nparts.
 uint32_t part_tiles(uint32_t nmax);
 hipError_t launch_partition(const float4* pts, const uint32_t* keys, const uint32_t* count,
                             uint32_t nmax, uint32_t nparts, uint64_t ncells, uint32_t* counts,
@@ -190,7 +195,8 @@ hipError_t launch_partition(const float4* pts, const uint32_t* keys, const uint3
                             uint32_t* out_keys, uint32_t* part_counts, hipStream_t s,
                             const uint32_t* fstart = nullptr, uint32_t nframes = 1,
                             uint32_t fshift = 0, uint32_t* out_run_keys = nullptr,
-                            uint32_t* out_run_start = nullptr);
+                            uint32_t* out_run_start = nullptr,
+                            const uint32_t* seg_split = nullptr);
 
 // gdf_download_frame's prefetch: a single-frame launch chain ends with ONE kernel that writes the
 // frame's downloads - the small counters, the points, voxel coords, voxelized points and the grid
@@ -220,8 +226,8 @@ hipError_t launch_download(const DlArgs& d, hipStream_t s);
 // gdf_voxelize_runs: nsrc received segments, source q's points from point_base[q] and runs from
 // run_base[q] (q <= nsrc: the totals)
 struct RebaseArgs {
-    uint32_t point_base[kMaxParts + 1];
-    uint32_t run_base[kMaxParts + 1];
+    uint32_t point_base[kMaxSources + 1];
+    uint32_t run_base[kMaxSources + 1];
     uint32_t nsrc;
 };
 hipError_t launch_run_rebase(uint32_t* run_start, const RebaseArgs& r, uint32_t* n_points,

@@ -125,6 +125,7 @@ EXPORTED = [
     "gdf_upload_point_sequences", "gdf_filter_new_point_sequences", "gdf_insert_new_point_sequences",
     "gdf_roll_rollbuffer", "gdf_select_timespan", "gdf_prepare_point_and_mask_buffers",
     "gdf_insert_selected_point_sequence", "gdf_transform_point_sequence", "gdf_get_rollbuffer_state",
+    "gdf_set_rollbuffer_shard", "gdf_get_rollbuffer_shard_order",
     "gdf_upload_depthmaps", "gdf_convert_depthmaps", "gdf_filter_flying_pixels", "gdf_crop_points",
     "gdf_apply_point_mask", "gdf_compute_voxel_coords", "gdf_voxelize", "gdf_voxel_occupancy_grid",
     "gdf_get_point_count", "gdf_download_points", "gdf_download_voxel_coords",
@@ -139,13 +140,14 @@ EXPORTED = [
     "gdf_run_depth_stream_alternating",
     "gdf_next_frame_in_batch", "gdf_get_batch_ranges", "gdf_download_batch_occupancy_grid",
     "gdf_mask_dilate", "gdf_transform_points", "gdf_add_halo_depthmap_device",
-    "gdf_partition_points", "gdf_voxelize_points", "gdf_partition_runs", "gdf_voxelize_runs", "gdf_voxelize_runs_marked", "gdf_set_partition_marks", "gdf_set_emit_partition", "gdf_last_sort_items", "gdf_get_stream",
+    "gdf_partition_points", "gdf_voxelize_points", "gdf_partition_runs", "gdf_voxelize_runs", "gdf_voxelize_runs_marked", "gdf_set_partition_marks", "gdf_set_emit_partition", "gdf_set_partition_segments", "gdf_last_sort_items", "gdf_get_stream",
     "gdf_get_graph_stats", "gdf_get_slot", "gdf_select_slot", "gdf_build_info",
     "gdf_download_frame", "gdf_set_slot_streams",
     # include/gdf_fused.h: a rank of the multi-GPU fused cloud in C++ over RCCL
     "gdf_fused_unique_id", "gdf_fused_create", "gdf_fused_destroy", "gdf_fused_halo_pixels",
     "gdf_fused_start", "gdf_fused_finish", "gdf_fused_run", "gdf_fused_local_create",
     "gdf_fused_local_destroy", "gdf_fused_create_local", "gdf_fused_info",
+    "gdf_fused_set_rollbuffer_shard",
     # include/gdf_segment.h: the GPU object-segmentation front end
     "gdf_seg_create", "gdf_seg_destroy", "gdf_seg_set_stream", "gdf_seg_label_layers",
     "gdf_seg_label_engine_grid", "gdf_seg_get_counts", "gdf_seg_download_labels",
@@ -256,10 +258,14 @@ def load_library(path: str = LIB_PATH):
         "gdf_fused_start": (i32, [vp, vp, u32, P(FrameParams), P(i32)]),
         "gdf_fused_finish": (i32, [vp, i32, vp, P(u32)]),
         "gdf_fused_run": (i32, [vp, P(StreamCamera), P(FrameParams), u64, u64, u32, i32]),
+        "gdf_set_rollbuffer_shard": (i32, [vp, u32, u32, u32]),
+        "gdf_get_rollbuffer_shard_order": (i32, [vp, vp, u32]),
+        "gdf_set_partition_segments": (i32, [vp, u32]),
         "gdf_fused_local_create": (i32, [i32, P(vp)]),
         "gdf_fused_local_destroy": (i32, [vp]),
         "gdf_fused_create_local": (i32, [vp, vp, i32, i32, P(StreamCamera), u32, P(vp)]),
         "gdf_fused_info": (i32, [vp, P(i32), P(i32), P(i32), P(C.c_char_p)]),
+        "gdf_fused_set_rollbuffer_shard": (i32, [vp, u32]),
         "gdf_seg_create": (i32, [i32, P(vp)]),
         "gdf_seg_destroy": (i32, [vp]),
         "gdf_seg_set_stream": (i32, [vp, vp]),
@@ -524,6 +530,16 @@ class GPUDepthmapFusion:
 
     def transformPointSequence(self):
         self._check(self._lib.gdf_transform_point_sequence(self._h))
+
+    def set_rollbuffer_shard(self, shard: int, nshards: int, block: int):
+        """gdf_set_rollbuffer_shard: keep the points of sequences (k // block) % nshards == shard."""
+        self._check(self._lib.gdf_set_rollbuffer_shard(self._h, shard, nshards, block))
+
+    def rollbuffer_shard_order(self, nshards: int):
+        """gdf_get_rollbuffer_shard_order: the shards in the selection's order."""
+        out = (C.c_uint32 * nshards)()
+        self._check(self._lib.gdf_get_rollbuffer_shard_order(self._h, out, nshards))
+        return list(out)
 
     def rollbuffer_state(self) -> RollbufferState:
         st = RollbufferState()

@@ -744,6 +744,14 @@ class NativeFusedRank:
         self.has_rollbuffer = rank == self.rollbuffer_rank
         self._pc_move = {}
 
+    def shard_rollbuffer(self, block: int):
+        """gdf_fused_set_rollbuffer_shard: the rollbuffer window spread over the ranks - every
+        rank is given EVERY point sequence and keeps those of blocks (k // block) % world == rank;
+        every rank's steps then carry its share of the selection (before the first sequence)."""
+        self.eng._check(self._lib.gdf_fused_set_rollbuffer_shard(self._h, int(block)))
+        self.has_rollbuffer = block > 0 or self.rank == self.rollbuffer_rank
+        self.shard_block = int(block)
+
     def info(self):
         """(rank, world, the rank count the transport reports, transport name)."""
         import ctypes as C

@@ -34,10 +34,11 @@ def small_params(F=4):
     return p
 
 
-def run_local_world(world, W_, H_, steps, B, params, depth, rb=None, fused_run=False):
+def run_local_world(world, W_, H_, steps, B, params, depth, rb=None, fused_run=False, shard=0):
     """`steps` steps of B frames of `world` cameras through `world` C++ ranks of one local world,
     pipelined `depth` deep.  rb = (LW, LH, first): the last rank ingests fused_ref.schedule's
-    point sequences (one step per frame, B = 1).  Returns (depth frames, per-rank results)."""
+    point sequences (one step per frame, B = 1); shard > 0: EVERY rank ingests them and keeps its
+    blocks of `shard` sequences (the sharded window).  Returns (depth frames, per-rank results)."""
     import fused_ref
     from ros_gpu_depthmap_fusion_amd import build_library, hiprt
     from ros_gpu_depthmap_fusion_amd.gdf import GPUDepthmapFusion
@@ -58,6 +59,9 @@ def run_local_world(world, W_, H_, steps, B, params, depth, rb=None, fused_run=F
     ranks = [NativeFusedRank(engines[r], cams, r, world, params, depth=depth, local=lw)
              for r in range(world)]
     assert all(fr.info() == (r, world, world, "local") for r, fr in enumerate(ranks))
+    if shard:
+        for fr in ranks:
+            fr.shard_rollbuffer(shard)
 
     def body(r):
         fr, eng = ranks[r], engines[r]
@@ -131,7 +135,7 @@ def oracle_frames(cams, depths, params, threads=16, rb=None, nf=None):
                tuple(orc.rollbuffer_state()) if rb is not None else None)
 
 
-def check(tag, world, B, res, oracle_iter, rb=False):
+def check(tag, world, B, res, oracle_iter, rb=False, sharded=False):
     n_checked = 0
     for f, (want, grid, st) in enumerate(oracle_iter):
         got = np.concatenate([res[r][0][f] for r in range(world)])
@@ -140,9 +144,16 @@ def check(tag, world, B, res, oracle_iter, rb=False):
         if f % B == B - 1:  # the grid after the step (the batch's last frame)
             for r in range(world):
                 np.testing.assert_array_equal(res[r][1][f // B], grid, f"{tag} frame {f} rank {r}")
-        if rb:
+        if rb and not sharded:
             assert st[3] > 0, f"{tag} frame {f}: rollbuffer points selected"
             assert res[world - 1][2][f] == st, f"{tag} frame {f} rollbuffer state"
+        elif rb:  # the shards' states: point counts add up, the sequence bookkeeping is the same
+            sts = [res[r][2][f] for r in range(world)]
+            assert st[3] > 0 and sum(1 for x in sts if x[3] > 0) >= 2, f"{tag} frame {f}: shares"
+            assert sum(x[0] for x in sts) == st[0], f"{tag} frame {f}: rollbuffer points"
+            assert sum(x[3] for x in sts) == st[3], f"{tag} frame {f}: selected points"
+            for x in sts:  # num_seqs, selected sequences, earliest / last times
+                assert (x[1],) + tuple(x[4:]) == (st[1],) + tuple(st[4:]), f"{tag} frame {f}"
         n_checked += 1
     return n_checked
 
@@ -199,6 +210,25 @@ def test_local_world_rollbuffer_leg(world):
     rb = (1280, 720, win)
     cams, depths, res = run_local_world(world, 640, 480, 3, 1, p, depth=2, rb=rb)
     assert check(f"rb{world}", world, 1, res, oracle_frames(cams, depths, p, rb=rb), rb=True) == 3
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_local_world_sharded_rollbuffer(world):
+    """The rollbuffer window SHARDED over the ranks (gdf_fused_set_rollbuffer_shard): every rank
+    ingests every 720p point sequence of an 8-sequence window and keeps its blocks of
+    ceil(7 / (world - 1)) sequences; the exchange carries [depth | rollbuffer] buckets, placed as
+    [every rank's depth points, the rollbuffer segments in the selection's order].  VGA cameras at
+    launch defaults, 4 single-frame steps (the window rolls from frame 1, the blocks rotate over
+    the ranks), 2 in flight: every fused cloud and grid equals ONE unsharded oracle engine's, the
+    shards' rollbuffer points add up to its own."""
+    p = ComponentParams()
+    win = 8
+    p.ps_timespan = (win - 0.5) / 30.0
+    rb = (1280, 720, win)
+    block = -(-(win - 1) // (world - 1))
+    cams, depths, res = run_local_world(world, 640, 480, 4, 1, p, depth=2, rb=rb, shard=block)
+    assert check(f"shard{world}", world, 1, res, oracle_frames(cams, depths, p, rb=rb), rb=True,
+                 sharded=True) == 4
 
 
 def test_fused_start_rejects_batched_rollbuffer_frame():
