@@ -667,20 +667,16 @@ __device__ __forceinline__ uint32_t sel_bits(const FrameArgs& a, const SelSeg& g
 }
 
 // Camera descriptors: kernel arguments for up to kArgCams cameras, else the device copy.
-// The kernel-argument table is addressed in the kernarg segment itself, never through `a`: the
-// callers read it with GLOBAL loads (G()), which is valid for the kernarg segment but not for a
-// private copy of the by-value struct - and the compiler may keep one (2.2 KB of scratch per
-// lane: an asm memory clobber in round 4, k_mask_px<4> always).  G() of a scratch address is an
-// address in the private aperture, not a global one: HSA_STATUS_ERROR_MEMORY_APERTURE_VIOLATION
-// (round 4's k_mask_px_o8 fault).  Every caller is a kernel whose only argument is
-// the FrameArgs, at offset 0 of the segment.
+// The callers read the kernel-argument table with GLOBAL loads (G()): valid because the by-value
+// FrameArgs stays in the kernarg segment (a global address).  Were the compiler to keep a private
+// (scratch) copy of it - an asm memory clobber did in round 4, and so did the address of the
+// table escaping into a non-inlined function in the 4-pixel k_mask_px - G() would turn a
+// private-aperture address into a "global" one: HSA_STATUS_ERROR_MEMORY_APERTURE_VIOLATION (round
+// 4's k_mask_px_o8 fault).  tests/test_abi.py checks every kernel's scratch size
+// (no copy).  (Addressing the table through __builtin_amdgcn_kernarg_segment_ptr() instead is
+// immune but cost 15 % of the C2 line: 30+ more SGPRs in every frame kernel, A/B on one box.)
 __device__ __forceinline__ const CamDesc* cam_table(const FrameArgs& a) {
-    if (a.ncams <= kArgCams) {
-        const char* ka = reinterpret_cast<const char*>(
-            (const void*)__builtin_amdgcn_kernarg_segment_ptr());
-        return reinterpret_cast<const CamDesc*>(ka + offsetof(FrameArgs, cams));
-    }
-    return a.cams_dev;
+    return a.ncams <= kArgCams ? a.cams : a.cams_dev;
 }
 
 // block-wide copy of the camera descriptors into LDS
@@ -2195,8 +2191,6 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
                 hipLaunchKernelGGL((k_mask_px<2, 256>), dim3(a.total_segs), dim3(128), lds, s, a);
             else if (km == reinterpret_cast<const void*>(&k_mask_px_o8<2, 256>))
                 hipLaunchKernelGGL((k_mask_px_o8<2, 256>), dim3(a.total_segs), dim3(128), lds, s, a);
-            else if (km == reinterpret_cast<const void*>(&k_mask_px<4, 256>))
-                hipLaunchKernelGGL((k_mask_px<4, 256>), dim3(a.total_segs), dim3(64), lds, s, a);
             else if (km == reinterpret_cast<const void*>(&k_mask_px<2, 640>))
                 hipLaunchKernelGGL((k_mask_px<2, 640>), dim3(a.total_segs), dim3(320), lds, s, a);
             else if (km == reinterpret_cast<const void*>(&k_mask<true, 4>))
@@ -2246,8 +2240,9 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
 // Gpoints/s; VGA single frames, 480 segments = 2400 waves of 320 threads, 8.3 -> 7.6-8.1)
 constexpr uint32_t kPx640MinSegs = 1024;
 
-// k_mask_px (g_mask_px = 2 or 4 pixels per thread) serves 256-pixel segments at F = 4 without
-// rot45 (tuning knob GDF_MASK_PX; 0 or 1: k_mask); k_mask everything else.  Measured on MI355X
+// k_mask_px (2 pixels per thread) serves 256-pixel segments at F = 4 without rot45 (tuning knob
+// GDF_MASK_PX; 0 or 1: k_mask); k_mask everything else.  (The 4-pixel form is gone: slower, and its
+// compiler-made private copy of FrameArgs broke the G() camera-table reads, cam_table above.)  Measured on MI355X
 // (A/B on one box, dense frames, 2 pixels per thread vs k_mask): VGA 8-frame batches
 // 22.1 -> 23.7, 720p 4-frame batches 29.8 -> 32.6, 4K 30.9 -> 32.4 Gpoints/s
 uint32_t g_mask_px2 = 2;
@@ -2255,9 +2250,8 @@ uint32_t g_mask_occ8 = 1;  // k_mask_px<2, 256> at 8 waves per SIMD (GDF_MASK_OC
 const void* mask_kernel(const FrameArgs& a) {
     if (g_mask_px2 >= 2 && a.do_flying && a.F == 4 && !a.rot45 && a.seg_threads == 256 && !a.dbg &&
         a.band_rowb <= 64 * 16)
-        return g_mask_px2 >= 4 ? reinterpret_cast<const void*>(&k_mask_px<4, 256>)
-               : g_mask_occ8   ? reinterpret_cast<const void*>(&k_mask_px_o8<2, 256>)
-                               : reinterpret_cast<const void*>(&k_mask_px<2, 256>);
+        return g_mask_occ8 ? reinterpret_cast<const void*>(&k_mask_px_o8<2, 256>)
+                           : reinterpret_cast<const void*>(&k_mask_px<2, 256>);
     // (half 720p rows: single frames under 1 Mi pixels with enough segments to fill the chip)
     if (g_mask_px2 >= 2 && a.do_flying && a.F == 4 && !a.rot45 && a.seg_threads == 640 && !a.dbg &&
         a.band_rowb <= 2 * 64 * 16 && a.total_segs >= kPx640MinSegs)
@@ -2275,8 +2269,7 @@ bool emit_partition_kernels(const FrameArgs& a) {
     FrameArgs plain = a;
     plain.nparts = 0;
     return (km == reinterpret_cast<const void*>(&k_mask_px<2, 256>) ||
-            km == reinterpret_cast<const void*>(&k_mask_px_o8<2, 256>) ||
-            km == reinterpret_cast<const void*>(&k_mask_px<4, 256>)) &&
+            km == reinterpret_cast<const void*>(&k_mask_px_o8<2, 256>)) &&
            emit_kernel(plain) == reinterpret_cast<const void*>(&k_emit_px2<256>);
 }
 
