@@ -92,6 +92,9 @@ def parse():
                          "this script); local = N ranks of the C++ step in THIS process on one "
                          "GPU (gdf_fused_local: one engine + host thread per rank, device copies "
                          "as the collectives) - exercises the multi-rank step, not a scaling run")
+    ap.add_argument("--rb-shard", action="store_true",
+                    help="with --rb-window (C++ step): the window sharded over the ranks "
+                         "(gdf_fused_set_rollbuffer_shard) instead of held by the last rank")
     ap.add_argument("--rb-window", type=int, default=0,
                     help="N > 1 fused mode: the last rank also runs a rollbuffer of this many "
                          "720p point sequences, one new sequence per step (C5 with its rollbuffer)")
@@ -165,6 +168,15 @@ def roofline_from(ktimes, kt_steps, mb, pmc_key):
         traffic = rec.get("hbm_bytes_per_launch")
         traffic_src = {"kernels": rec.get("kernels"), "dispatches": rec.get("dispatches"),
                        "source": "profiles/pmc_traffic.json[%s]" % pmc_key}
+    # every timed kernel's PMC traffic against its byte model (profiles/pmc_traffic.json, one
+    # batch in flight): > 1 = bytes the model does not count (partial-sector writes, re-reads)
+    pk_traffic = {}
+    allrec = pmc_record(pmc_key)
+    for k in singles:
+        r = allrec.get(k)
+        if r and mb.get(k):
+            pk_traffic[k] = {"model_bytes": round(mb[k]), "pmc_bytes": r.get("hbm_bytes_per_launch"),
+                             "ratio": round(r.get("hbm_bytes_per_launch", 0) / mb[k], 3)}
     valu = None
     sq = os.path.join(ROOT, "profiles", "pmc_sq.json")
     if slot == "mask" and os.path.exists(sq):
@@ -193,6 +205,7 @@ def roofline_from(ktimes, kt_steps, mb, pmc_key):
         "launches_per_step": round(n / kt_steps, 3),
         "bytes_per_launch": round(mb[slot]),
         "per_kernel_us": {k: round(ktimes[k][0] * 1e3 / ktimes[k][1], 3) for k in singles},
+        "per_kernel_traffic": pk_traffic or None,
     }
 
 
@@ -403,10 +416,26 @@ def cpu_baseline(st, params, seconds):
            "kind": "port", "threads": threads, "nproc": os.cpu_count(),
            "affinity_cpus": affinity, "cpu_model": model,
            "runs_Mpoints_s": [round(r, 2) for r in rates],
+           "min": round(min(rates), 3), "max": round(max(rates), 3),
+           "spread": round((max(rates) - min(rates)) / max(statistics.median(rates), 1e-9), 3),
             "sample": f"median of 5 runs x {seconds:.0f} s ({total_frames} frames) of the same "
                       f"{st.W}x{st.H} frames through the C restatement (oracle/gdf_oracle.c, "
                       f"-O3 -ffp-contract=off, OpenMP {threads} threads = the pool's "
                       f"OMP_NUM_THREADS share of this GPU's host)"}
+    # one thread, one run: a per-core figure that does not depend on the host's other tenants
+    # sharing the thread pool's CPUs (the multi-thread median moved 49.5 -> 85 Mpoints/s between
+    # rounds on the same pool)
+    orc.set_threads(1)
+    frame(0)
+    done, t0 = 0, time.perf_counter()
+    while True:
+        frame(done)
+        done += 1
+        t = time.perf_counter() - t0
+        if t >= seconds or done >= 4000:
+            break
+    out["single_thread_Mpoints_s"] = round(done * st.P / t / 1e6, 3)
+    orc.set_threads(threads)
     quota = cgroup_cpu_quota()
     if quota is not None:
         out["cgroup_cpu_quota"] = round(quota, 2)
@@ -588,6 +617,12 @@ def time_multi(args, st, params, dist, world, pmc_key):
             if B != 1:
                 raise SystemExit("--rb-window: frames carrying point sequences run one per step "
                                  "(--batch 1)")
+            if args.rb_shard:
+                if not native:
+                    raise SystemExit("--rb-shard: the C++ step (--fused-impl native, nccl)")
+                # blocks of ceil((window - 1) / (world - 1)) sequences: the window spans at most
+                # `world` blocks, one per rank (include/gdf_fused.h)
+                fr.shard_rollbuffer(max(1, -(-(args.rb_window - 1) // max(world - 1, 1))))
             rb = RollbufferFeed(eng, args.rb_window, params) if fr.has_rollbuffer else None
             params.ps_timespan = (args.rb_window - 0.5) / 30.0
             fr.p = params
@@ -673,10 +708,13 @@ def time_multi(args, st, params, dist, world, pmc_key):
         "roofline": None,
     }
     if rb is not None or (fused and args.rb_window):
-        line["rollbuffer"] = {"window_sequences": args.rb_window, "rank": world - 1,
+        line["rollbuffer"] = {"window_sequences": args.rb_window,
+                              "rank": "all (sharded)" if args.rb_shard else world - 1,
                               "sequence_points": RollbufferFeed.POINTS,
-                              "note": "the last rank holds the rollbuffer (SURVEY 8(e)); "
-                                      "ms_per_step_per_rank shows the imbalance"}
+                              "note": "sharded: every rank holds ~1/N of the window" if args.rb_shard
+                                      else "the last rank holds the rollbuffer (SURVEY 8(e))",
+                              "balance": "gpu_ms_per_step_per_rank: each rank's event-timed GPU "
+                                         "work per step"}
     if not args.no_kernel_timing:
         kt_steps = min(args.steps, 100)
         if depth > 1:
@@ -691,6 +729,13 @@ def time_multi(args, st, params, dist, world, pmc_key):
         eng.set_profiling(False)
         line["roofline"] = roofline_from(kt, kt_steps, model_bytes(st.P, n_avg, g_avg, ncells, fpb),
                                          pmc_key)
+        # each rank's GPU work per step (its event-timed launches): the load (im)balance that the
+        # barrier-to-barrier times above hide
+        g = torch.tensor([sum(ms for ms, _ in kt.values()) / kt_steps], dtype=torch.float64,
+                         device="cuda" if args.dist_backend == "nccl" else "cpu")
+        allg = [torch.zeros_like(g) for _ in range(world)]
+        dist.all_gather(allg, g)
+        line["gpu_ms_per_step_per_rank"] = [round(float(x.item()), 5) for x in allg]
     transport_ranks = dist.get_world_size()
     if fused and native:
         transport_ranks = fr.info()[2]  # (ncclCommCount of the step's points communicator)

@@ -136,6 +136,18 @@ def run_c3(width=1280, height=720, window=256, steps=20, ring=4, profile_steps=5
                          "GBps": round(model[name] / (tot / 1e3 / n) / 1e9, 1)}
     dom = max(per, key=lambda q: per[q]["avg_us"] * per[q]["launches_per_frame"]) if per else None
     achieved = per[dom]["GBps"] if per else 0.0
+    # PMC traffic per launch (profiles/pmc_traffic.json, tools/r5/pmc_secondary.sh) against the model
+    pmc_key = "c3/%dx%d/w%d/%s" % (W, H, window, workload)
+    try:
+        rec = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json"))).get(pmc_key, {})
+    except (OSError, ValueError):
+        rec = {}
+    for name, d in per.items():
+        r = rec.get(name)
+        if r:
+            d["model_bytes"] = round(model[name])
+            d["pmc_bytes"] = r.get("hbm_bytes_per_launch")
+            d["traffic_ratio"] = round(r.get("hbm_bytes_per_launch", 0) / max(model[name], 1), 3)
     # SURVEY §8(d) B_alg for C3: depth 2P + 24N + 9C, plus 24 n_new + 24 n_sel + 32 n_sel
     survey = 2.0 * P + 24.0 * N + 9.0 * ncells + 24.0 * P + 56.0 * S
     return {
@@ -158,6 +170,8 @@ def run_c3(width=1280, height=720, window=256, steps=20, ring=4, profile_steps=5
                    "grid_cells": ncells},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                     "traffic": per.get(dom, {}).get("pmc_bytes"),
+                     "traffic_src": "profiles/pmc_traffic.json[%s]" % pmc_key,
                      "per_kernel": per},
         "setup_s": round(gen_s, 1),
     }

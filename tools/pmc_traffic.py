@@ -30,7 +30,7 @@ SLOT = {"k_mask": "mask", "k_mask_px": "mask", "k_mask_px_o8": "mask", "k_emit":
         "k_group_big": "group_big", "k_group_runs_big": "group_big", "k_scan_counts": "scan",
         "k_scan_reduce": "scan_reduce", "k_grid_u8": "grid", "k_grid_u32": "grid",
         "k_grid_u8_batch": "grid", "k_sel": "sel", "k_sort_hist": "sort_hist",
-        "k_group_count": "group_count"}
+        "k_group_count": "group_count", "k_ps_filter_insert": "ps_insert"}
 
 
 def kname(raw):
