@@ -72,9 +72,17 @@ def main():
     ap.add_argument("write_csv")
     ap.add_argument("--workload", required=True)
     ap.add_argument("--out", default="profiles/pmc_traffic.json")
+    ap.add_argument("--last", type=int, default=0,
+                    help="only the last N steps (from the N-th last compaction dispatch on): runs "
+                         "whose early frames differ, e.g. the C3 window filling up")
     a = ap.parse_args()
     fr, mk = steady(load(a.fetch_csv, "FETCH_SIZE"))
     wr, mk2 = steady(load(a.write_csv, "WRITE_SIZE"))
+    if a.last:
+        def tail(rows, k):
+            idx = [i for i, (_, n, _) in enumerate(rows) if n == k]
+            return rows[idx[-a.last]:] if len(idx) >= a.last else rows
+        fr, wr = tail(fr, mk), tail(wr, mk2)
     fv, wv = per_variant(fr, 2.0), per_variant(wr, 1.0)
     out = {}
     by_slot = collections.defaultdict(list)
@@ -104,7 +112,8 @@ def main():
                         "note": "every dispatch of the steady phase (from the first %s on) per "
                                 "launch of it = per bench step" % mk}
     out["_note"] = ("FETCH_SIZE x2 (gfx950 wide-read rule), WRITE_SIZE as is; uncalibrated for "
-                    "sub-16-B accesses; one batch in flight (--pipeline 1)")
+                    "sub-16-B accesses; one batch in flight (--pipeline 1)" +
+                    ("; the last %d steps" % a.last if a.last else ""))
     try:
         allw = json.load(open(a.out))
     except (OSError, ValueError):
