@@ -331,6 +331,7 @@ struct Slot {
     bool group_marks = false;       // this frame's marks are set by the voxel groups (k_group)
     uint32_t dbg_count = 0;
     DevBuf d_ka, d_kb, d_va, d_vb, d_sstatus, d_sgstatus, d_gstatus, d_ggstatus, d_vox;
+    DevBuf d_seghist, d_segfs, d_segstat, d_seggstat, d_segdone;  // the segmented run sort
     DevBuf d_gcnt, d_goff;          // group starts per tile + their scan (large frames)
     DevBuf d_bigq, d_bigcnt;        // long voxels queued for k_group_big (large frames)
     bool vox_valid = false;
@@ -507,6 +508,9 @@ struct gdf_engine {
     bool use_runs = !getenv("GDF_NO_RUNS");      // voxelize runs of equal keys (depth frames)
     bool force_runs = getenv("GDF_FORCE_RUNS") != nullptr;    // tuning knob: runs at every size
     bool run_hist_in_sort = getenv("GDF_RUN_HIST_SORT") != nullptr;  // tuning knob
+    // the frame's (or batch's) runs sorted per frame by two 11-bit passes (k_seg_sort_pass)
+    // instead of 8/8/9-bit passes over frame | voxel (GDF_NO_SEG_SORT: the latter)
+    bool seg_sort_allowed = !getenv("GDF_NO_SEG_SORT");
     bool run_hist_all = getenv("GDF_RUN_HIST_ALL") != nullptr;  // tuning knob: k_mask counts the
                                                                // run digits at any segment count
     bool xruns = !getenv("GDF_NO_XRUNS");  // voxelize_points sorts the received list's runs
@@ -1253,6 +1257,15 @@ void ensure_misc(gdf_engine* e) {
 
 // Arguments of the fused compaction launch: convert + flying + crop + selected-point transform +
 // ordered compaction (+ voxel keys and occupancy marks when fused_voxel).
+// The segmented run sort serves the engine's own runs (in frame order) of voxel keys <= 22 bits
+// while its tile granules stay within kSegSortTileCap tiles (256 MB; C3's rollbuffer windows of
+// 10^8 points take the 8/8/9-bit passes)
+constexpr uint32_t kSegSortTileCap = 8192;
+bool seg_sort_ok(const gdf_engine* e, uint32_t nmax) {
+    return e->seg_sort_allowed && e->key_bits <= 2 * 11 &&
+           seg_sort_tiles(std::max<uint32_t>(nmax, 1), std::max<uint32_t>(e->nframes, 1)) <= kSegSortTileCap;
+}
+
 FrameArgs frame_args(gdf_engine* e, bool fused_voxel, bool compaction_marks = false) {
     if (!e->prepared) prepare_buffers(e);
     if (!e->depth_uploaded) upload_depthmaps(e);
@@ -1349,7 +1362,7 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel, bool compaction_marks = fa
         // k_sort_hist over the runs (tens of thousands of flushes contend at the atomic units)
         if (a.run_mode)
             a.key_hist = (a.total_segs <= kFusedPrefixSegs || e->run_hist_all) && !e->run_hist_in_sort &&
-                         !a.sel_tiles
+                         !a.sel_tiles && !seg_sort_ok(e, e->sl().n_total)  // (k_seg_hist counts)
                              ? e->sl().d_khist.as<uint32_t>() : nullptr;
     }
     a.out_pts = e->sl().d_pts.as<float4>();
@@ -1571,6 +1584,21 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime,
         v.count = e->sl().d_misc.as<uint32_t>() + (e->sl().runs_sel ? kRunTotal : kRunCount);
         v.run_start = e->sl().d_runstart.as<uint32_t>();
         v.point_count = e->sl().d_misc.as<uint32_t>() + kCount;
+        if (seg_sort_ok(e, nmax)) {  // (the runs come in frame order)
+            Slot& q = e->sl();
+            const uint32_t nf = std::max<uint32_t>(e->nframes, 1);
+            q.d_seghist.ensure_zero((size_t)kMaxCams * 2 * kSegSortDigits * 4, e->s());
+            q.d_segfs.ensure((size_t)(kMaxCams + 1) * 4);
+            q.d_segstat.ensure_zero((size_t)seg_sort_tiles(nmax, nf) * kSegSortDigits * 8, e->s());
+            q.d_seggstat.ensure_zero((size_t)seg_sort_groups(nmax, nf) * kSegSortDigits * 8, e->s());
+            q.d_segdone.ensure_zero(64, e->s());
+            v.seg_sort = 1;
+            v.seg_hist = q.d_seghist.as<uint32_t>();
+            v.seg_fstart = q.d_segfs.as<uint32_t>();
+            v.seg_status = q.d_segstat.as<unsigned long long>();
+            v.seg_gstatus = q.d_seggstat.as<unsigned long long>();
+            v.seg_done = q.d_segdone.as<uint32_t>();
+        }
     }
     v.nmax = nmax;
     v.key_bits = sort_bits(e);

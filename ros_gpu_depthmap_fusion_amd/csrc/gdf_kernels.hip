@@ -3106,6 +3106,224 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
     }
 }
 
+// ---- frame-segmented two-pass radix sort of run keys ---------------------------------------------
+// A frame's runs of equal keys come in frame order (the compaction is frame-major: a batch's frames
+// back to back), and a run's sort key is voxel | frame << fshift - so sorting by the full key is
+// sorting each frame's runs by their voxel key, stably, in place within the frame's segment
+// [fs[f], fs[f + 1]).  The frame bits need no radix pass, and the 22-bit voxel keys of the launch
+// grid take two 11-bit LSD passes (2048 digits) instead of 8 + 8 + 9 bits: tiles never span two
+// frames, each frame's tiles chain their own decoupled look-back (lookback2_chans<8> over the
+// segment's granules), the digit bases come from per-frame histograms (k_seg_hist, which also
+// finds the segments).  The reference's order (radix_sort.h:107-289, a stable LSD sort of the
+// keys) is kept: within a frame the LSD passes are stable, frames stay in order.
+constexpr uint32_t kSegDigitBits = 11, kSegDigits = 1u << kSegDigitBits;
+
+// per (frame, pass) digit counts [nseg][2][2048] (zero on entry; the last pass zeroes them again)
+// and the frames' run starts fstart[0 .. nseg] (a frame without runs starts where the next does)
+__global__ __launch_bounds__(256) void k_seg_hist(const uint32_t* __restrict__ keys,
+                                                  const uint32_t* __restrict__ count, uint32_t nseg,
+                                                  uint32_t fshift, uint32_t* __restrict__ hist,
+                                                  uint32_t* __restrict__ fstart) {
+    const uint32_t n = *count;
+    const uint32_t vmask = nseg > 1 ? (1u << fshift) - 1u : 0xFFFFFFFFu;
+    if (n == 0) {
+        if (blockIdx.x == 0 && threadIdx.x <= nseg) fstart[threadIdx.x] = 0u;
+        return;
+    }
+    const int lane = threadIdx.x & 63;
+    for (uint32_t base = blockIdx.x * 256u; base < n; base += gridDim.x * 256u) {  // block-uniform
+        const uint32_t i = base + threadIdx.x;
+        const bool ok = i < n;
+        const uint32_t k = ok ? keys[i] : 0u;
+        const uint32_t f = ok && nseg > 1 ? min(k >> fshift, nseg - 1u) : 0u;
+        if (ok) {
+            const uint32_t pf = i == 0 ? 0xFFFFFFFFu : (nseg > 1 ? min(keys[i - 1] >> fshift, nseg - 1u) : 0u);
+            if (pf != f)  // frames (pf, f] start here (all frames <= f at i = 0)
+                for (uint32_t g = pf + 1u; g <= f; ++g) fstart[g] = i;
+            if (i == n - 1u)
+                for (uint32_t g = f + 1u; g <= nseg; ++g) fstart[g] = n;
+        }
+        const uint32_t v = k & vmask;
+        // consecutive lanes with the same (frame, digit) count once (a wave's runs often repeat a
+        // voxel's low digit only rarely; the high digit - a row band of the grid - often)
+#pragma unroll
+        for (uint32_t p = 0; p < 2; ++p) {
+            const uint32_t b = ok ? (f * 2u + p) * kSegDigits + ((v >> (kSegDigitBits * p)) & (kSegDigits - 1u))
+                                  : 0xFFFFFFFFu;
+            const uint32_t pb = __shfl_up(b, 1, 64);
+            const bool leader = ok && (lane == 0 || pb != b);
+            const unsigned long long lm = __ballot(leader);
+            const unsigned long long vm = __ballot(ok);
+            if (leader) {
+                const unsigned long long after = lane == 63 ? 0ull : lm & (~0ull << (lane + 1));
+                const uint32_t end = after ? (uint32_t)(__ffsll((long long)after) - 1)
+                                           : (uint32_t)__popcll(vm);
+                atomicAdd(&hist[b], end - (uint32_t)lane);
+            }
+        }
+    }
+}
+
+// One 11-bit pass (pass 0: bits 0..10 of the voxel key, pass 1: bits 11..21) over every frame's
+// segment.  Tile = 256 threads x PT runs of ONE frame; global tile g -> (frame f, tile t of f) from
+// the frames' tile starts; tiles in ticket order (persistent blocks).  Pass 0 also carries the
+// historic-grid update in extra blocks (as k_sort_pass) and zeroes the run-group queue; the
+// last block of pass 1 zeroes the histograms for the next voxelize.
+template <int PT>
+__global__ __launch_bounds__(kSortThreads) void k_seg_sort_pass(
+    const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+    uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, const uint32_t* __restrict__ count,
+    uint32_t* hist, const uint32_t* __restrict__ fstart, uint32_t nseg, uint32_t fshift,
+    uint32_t pass, unsigned long long* status, unsigned long long* gstatus, uint32_t* tile_ctr,
+    uint32_t* epoch_word, uint32_t* err, uint32_t* done_ctr, uint32_t grid_block0, uint4* grid,
+    uint32_t* marks, uint64_t grid_nwords, uint32_t lifetime, GridSeq q, uint32_t nframes,
+    uint64_t mark_words, SnapArgs snap, uint32_t* qreset) {
+    constexpr int kTile = kSortThreads * PT;
+    constexpr int R = kSegDigits / 256;  // digits per thread in the offset phase
+    if (qreset && blockIdx.x == 0 && threadIdx.x == 0) {
+        qreset[0] = 0u;
+        qreset[1] = 0u;
+        qreset[2] = 0u;
+    }
+    if (blockIdx.x >= grid_block0) {  // fused historic-grid update (pass 0 only)
+        const uint32_t f = grid_seq_enter<true>(q);
+        if (nframes > 1)
+            grid_u8_part_frames(grid, marks, grid_nwords, lifetime, blockIdx.x - grid_block0,
+                                gridDim.x - grid_block0, nframes, mark_words, snap);
+        else
+            grid_u8_part(grid, marks, grid_nwords, lifetime, blockIdx.x - grid_block0,
+                         gridDim.x - grid_block0, q);
+        grid_seq_leave<true>(q, f, gridDim.x - grid_block0);
+        return;
+    }
+    __shared__ uint32_t s_fs[kMaxCams + 1], s_ts[kMaxCams + 1], s_gs[kMaxCams + 1];
+    __shared__ uint32_t s_cnt[4][kSegDigits];
+    __shared__ uint32_t s_base[kSegDigits];
+    __shared__ uint32_t s_excl[kSegDigits];
+    __shared__ uint32_t s_wave[4];
+    __shared__ uint32_t s_tile, s_epoch, s_last;
+    if (threadIdx.x == 0) {  // the frames' item, tile and look-back group starts
+        uint32_t t = 0, g = 0;
+        for (uint32_t f = 0; f < nseg; ++f) {
+            const uint32_t a = fstart[f], b = fstart[f + 1];
+            s_fs[f] = a;
+            s_ts[f] = t;
+            s_gs[f] = g;
+            const uint32_t nt = (b - a + kTile - 1) / kTile;
+            t += nt;
+            g += (nt + kSortGroup - 1) / kSortGroup;
+        }
+        s_fs[nseg] = fstart[nseg];
+        s_ts[nseg] = t;
+        s_gs[nseg] = g;
+        s_epoch = read_epoch(epoch_word);
+    }
+    __syncthreads();
+    const uint32_t ntiles = s_ts[nseg];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long ltm = lanemask_lt();
+    const Tickets tk = tickets(ntiles, grid_block0);
+    if (blockIdx.x >= tk.nblk) return;  // (block-uniform: no block past nblk counts itself below)
+    const uint32_t vmask = nseg > 1 ? (1u << fshift) - 1u : 0xFFFFFFFFu;
+    const uint32_t shift = kSegDigitBits * pass;
+    int cur = -1;
+    for (bool first = true;; first = false) {  // persistent: tiles in ticket order
+        if (!first && tk.oneshot) break;
+        if (threadIdx.x == 0) s_tile = next_ticket(tile_ctr, tk, epoch_word, s_epoch);
+        for (uint32_t i = threadIdx.x; i < 4 * kSegDigits; i += kSortThreads) (&s_cnt[0][0])[i] = 0;
+        __syncthreads();
+        const uint32_t tile = s_tile, epoch = s_epoch;
+        if (tile >= ntiles) break;  // block-uniform
+        uint32_t f = 0;
+        while (f + 1 < nseg && s_ts[f + 1] <= tile) ++f;  // (empty frames have no tiles)
+        const uint32_t t = tile - s_ts[f], nt = s_ts[f + 1] - s_ts[f];
+        const uint32_t lo = s_fs[f], hi = s_fs[f + 1];
+        if ((int)f != cur) {  // the frame's digit bases: its run start + the digits before
+            const uint32_t* h = hist + ((size_t)f * 2 + pass) * kSegDigits + R * threadIdx.x;
+            uint32_t v[R], sum = 0;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                v[r] = h[r];
+                sum += v[r];
+            }
+            uint32_t total;
+            uint32_t run = lo + block_exclusive_scan(sum, total, s_wave);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                s_base[R * threadIdx.x + r] = run;
+                run += v[r];
+            }
+            cur = (int)f;
+        }
+        uint32_t key[PT], val[PT], rank[PT];
+        const uint32_t wbase = lo + t * kTile + w * 64 * PT;
+#pragma unroll
+        for (int j = 0; j < PT; ++j) {
+            const uint32_t idx = wbase + j * 64 + lane;
+            const bool ok = idx < hi;
+            key[j] = ok ? kin[idx] : 0xFFFFFFFFu;
+            val[j] = ok ? (vin ? vin[idx] : idx) : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < PT; ++j) {
+            const uint32_t idx = wbase + j * 64 + lane;
+            const bool ok = idx < hi;
+            const uint32_t d = ((key[j] & vmask) >> shift) & (kSegDigits - 1u);
+            unsigned long long m = __ballot(ok);
+            for (uint32_t b = 0; b < kSegDigitBits; ++b) {
+                const bool bit = (d >> b) & 1u;
+                const unsigned long long bb = __ballot(bit);
+                m &= bit ? bb : ~bb;
+            }
+            const uint32_t before = (uint32_t)__popcll(m & ltm);
+            uint32_t base = 0;
+            if (ok) base = s_cnt[w][d];
+            rank[j] = base + before;
+            __builtin_amdgcn_wave_barrier();
+            if (ok && before == 0) s_cnt[w][d] = base + (uint32_t)__popcll(m);
+            __builtin_amdgcn_wave_barrier();
+        }
+        __syncthreads();
+        uint32_t tot[R], ex[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t d = threadIdx.x + 256u * r;
+            tot[r] = 0;
+#pragma unroll
+            for (int ww = 0; ww < 4; ++ww) {
+                const uint32_t c = s_cnt[ww][d];
+                s_cnt[ww][d] = tot[r];
+                tot[r] += c;
+            }
+        }
+        // the frame's own chain: its tiles' granules from the frame's first tile / group on
+        lookback2_chans<R>(status + (size_t)s_ts[f] * kSegDigits, gstatus + (size_t)s_gs[f] * kSegDigits,
+                           t, nt, tot, ex, epoch, err);
+#pragma unroll
+        for (int r = 0; r < R; ++r) s_excl[threadIdx.x + 256u * r] = ex[r];
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < PT; ++j) {
+            const uint32_t idx = wbase + j * 64 + lane;
+            if (idx < hi) {
+                const uint32_t dd = ((key[j] & vmask) >> shift) & (kSegDigits - 1u);
+                const uint32_t pos = s_base[dd] + s_excl[dd] + s_cnt[w][dd] + rank[j];
+                kout[pos] = key[j];
+                vout[pos] = val[j];
+            }
+        }
+        __syncthreads();  // LDS reused by the next tile
+    }
+    if (pass == 1) {  // the last block of the last pass zeroes the histograms (no reader left)
+        if (threadIdx.x == 0) s_last = atomicAdd(done_ctr, 1u) == tk.nblk - 1u ? 1u : 0u;
+        __syncthreads();
+        if (s_last) {
+            for (uint32_t i = threadIdx.x; i < nseg * 2u * kSegDigits; i += kSortThreads) hist[i] = 0u;
+            if (threadIdx.x == 0) atomicExch(done_ctr, 0u);
+        }
+    }
+}
+
 // Voxel groups of the sorted keys and their outputs in ONE kernel (RadixGrouper::makeGroups,
 // inc/radix_grouper.h:35-64, + averageGridCells / occupiedGridCells, inc/voxelize.h:9-71).
 // Tile = 256 sorted keys: group starts (key != previous key), their ids by a block scan plus a
@@ -4193,6 +4411,13 @@ extern "C" int gdf_debug_group_trace_clear() {
 }
 #endif
 
+uint32_t seg_sort_tiles(uint32_t nmax, uint32_t nframes) {
+    return (nmax + kSortThreads * 8 - 1) / (kSortThreads * 8) + std::max<uint32_t>(nframes, 1u);
+}
+uint32_t seg_sort_groups(uint32_t nmax, uint32_t nframes) {
+    return (seg_sort_tiles(nmax, nframes) + kSortGroup - 1) / kSortGroup + std::max<uint32_t>(nframes, 1u);
+}
+
 size_t voxelize_status_words(uint32_t nmax, uint32_t key_bits) {  // (tiles of >= 4 keys per thread)
     return (size_t)((nmax + kSortThreads * 4 - 1) / (kSortThreads * 4) + 1) *
            (radix_wide_last(key_bits) ? 512 : 256);
@@ -4248,7 +4473,7 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
     // persistent blocks (ticket loop): at most kPersistBlocks, fewer when the capacity is small
     const uint32_t sort_tiles = std::min<uint32_t>((a.nmax + tile - 1) / tile, kPersistBlocks);
     hipError_t e;
-    if (!a.hist_ready) {
+    if (!a.hist_ready && !a.seg_sort) {
         unsigned hb = grid_blocks(a.nmax, 256 * 4);
         if (hb > 512) hb = 512;
         hipLaunchKernelGGL(k_sort_hist, dim3(hb), dim3(256), 0, s, a.keys, a.count, npasses, a.hist,
@@ -4260,7 +4485,33 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
     uint32_t* kbuf[2] = {a.keys_a, a.keys_b};
     uint32_t* vbuf[2] = {a.vals_a, a.vals_b};
     const bool runs = a.run_start != nullptr;  // keys are run keys: sort runs, then expand
-    for (uint32_t p = 0; p < npasses; ++p) {
+    if (a.seg_sort) {  // the frames' runs by two 11-bit passes (k_seg_sort_pass), no frame pass
+        HookScope hs(hook, GDF_KERNEL_SORT);
+        const uint32_t nseg = std::max<uint32_t>(a.nframes, 1u);
+        // persistent blocks: at most kPersistBlocks (the granules cover every tile, though)
+        const uint32_t tiles = std::min<uint32_t>(seg_sort_tiles(a.nmax, nseg), kPersistBlocks);
+        const uint32_t hb = std::min<uint32_t>((a.nmax + 255) / 256, 1024u);
+        hipLaunchKernelGGL(k_seg_hist, dim3(std::max<uint32_t>(hb, 1u)), dim3(256), 0, s, a.keys, a.count,
+                           nseg, a.frame_shift, a.seg_hist, a.seg_fstart);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        for (uint32_t p = 0; p < 2; ++p) {
+            const bool g = p == 0 && a.grid8 != nullptr;
+            const uint64_t nwords = g ? (a.ncells + 31) / 32 : 0;
+            const uint32_t gb = g ? fused_grid_blocks(a.ncells) : 0;
+            hipLaunchKernelGGL((k_seg_sort_pass<8>), dim3(tiles + gb), dim3(kSortThreads), 0, s, kin, vin,
+                               kbuf[p], vbuf[p], a.count, a.seg_hist, a.seg_fstart, nseg, a.frame_shift, p,
+                               a.seg_status, a.seg_gstatus,
+                               reinterpret_cast<uint32_t*>(a.ctrs + kCtrSort0 + p),
+                               reinterpret_cast<uint32_t*>(a.ctrs + kCtrEpoch), a.err, a.seg_done, tiles,
+                               reinterpret_cast<uint4*>(a.grid8), a.marks, nwords, a.lifetime, a.gseq,
+                               a.nframes, a.mark_words, a.snap,
+                               p == 0 ? reinterpret_cast<uint32_t*>(a.ctrs + kCtrRunQueue) : nullptr);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            kin = kbuf[p];
+            vin = vbuf[p];
+        }
+    }
+    for (uint32_t p = 0; p < (a.seg_sort ? 0u : npasses); ++p) {
         const uint32_t remaining = a.key_bits > 8 * p ? a.key_bits - 8 * p : 0u;
         // (a 9-bit last digit: radix_wide_last)
         const bool wide = p + 1 == npasses && remaining == 9;
@@ -4285,6 +4536,7 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
         kin = kbuf[p & 1];
         vin = vbuf[p & 1];
     }
+    const uint32_t sorted_passes = a.seg_sort ? 2u : npasses;  // (the free pair: kbuf[passes & 1])
     const uint32_t* gcount = a.count;  // items of the group phase (points, or runs)
     const uint32_t max_tiles = (a.nmax + kGroupThreads - 1) / kGroupThreads;
     const uint32_t group_tiles = std::min<uint32_t>(max_tiles, kPersistBlocks);
@@ -4322,7 +4574,7 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
                            a.average, a.vp, a.group_marks, tile_base, a.bigq, a.bigq_cap, qctr,
                            a.nframes, a.frame_shift, a.frame_vox_start,
                            std::min<uint32_t>(g_run_inblock, g_run_stage >= 2048 ? 2048u : 512u),
-                           kbuf[npasses & 1], vbuf[npasses & 1], g_small_group,  // (free after the sort)
+                           kbuf[sorted_passes & 1], vbuf[sorted_passes & 1], g_small_group,  // (free after the sort)
                            tile_gtot, a.group_mark_stride);
         if (a.average) {
             if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -4332,11 +4584,11 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
             const uint32_t big_blocks = std::min(g_run_big_blocks, rb);
             if (q16)
                 hipLaunchKernelGGL((k_group_runs_big<16>), dim3(big_blocks), dim3(256), 0, s,
-                                   kbuf[npasses & 1], vbuf[npasses & 1], a.pts,
+                                   kbuf[sorted_passes & 1], vbuf[sorted_passes & 1], a.pts,
                                    reinterpret_cast<float*>(a.out), a.bigq, a.bigq_cap, qctr);
             else
                 hipLaunchKernelGGL((k_group_runs_big<8>), dim3(big_blocks), dim3(256), 0, s,
-                                   kbuf[npasses & 1], vbuf[npasses & 1], a.pts,
+                                   kbuf[sorted_passes & 1], vbuf[sorted_passes & 1], a.pts,
                                    reinterpret_cast<float*>(a.out), a.bigq, a.bigq_cap, qctr);
         }
         return hipGetLastError();

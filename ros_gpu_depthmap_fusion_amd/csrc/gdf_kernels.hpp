@@ -152,6 +152,16 @@ struct VoxelizeArgs {
     // the points)
     const uint32_t* run_start;
     const uint32_t* point_count;
+    // frame-segmented two-pass sort of the runs (k_seg_hist + 2 x k_seg_sort_pass: voxel keys of
+    // <= 22 bits, runs in frame order - the engine's own frame or batch): per-frame 11-bit digit
+    // histograms [16][2][2048] (zero on entry and exit), the frames' run starts [17], tile / group
+    // granules (seg_sort_tiles(nmax, nframes) x 2048, epoch-tagged), a self-resetting counter
+    int seg_sort;
+    uint32_t* seg_hist;
+    uint32_t* seg_fstart;
+    unsigned long long* seg_status;
+    unsigned long long* seg_gstatus;
+    uint32_t* seg_done;
     uint64_t ncells;
     uint32_t lifetime;
     uint32_t* err;
@@ -161,6 +171,10 @@ struct VoxelizeArgs {
 };
 hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hook = nullptr);
 size_t voxelize_status_words(uint32_t nmax, uint32_t key_bits);
+// tiles (of 2048 runs) of the segmented sort over nmax items in nframes frames, its group granules
+uint32_t seg_sort_tiles(uint32_t nmax, uint32_t nframes);
+uint32_t seg_sort_groups(uint32_t nmax, uint32_t nframes);
+constexpr uint32_t kSegSortDigits = 2048;
 // capacity (256-key tiles) above which k_group takes its group-id offsets from count + scan
 extern uint32_t g_group_scan_tiles;
 // k_group_runs staging (512 or 2048 points) and in-block group size limit
