@@ -508,9 +508,13 @@ struct gdf_engine {
     bool use_runs = !getenv("GDF_NO_RUNS");      // voxelize runs of equal keys (depth frames)
     bool force_runs = getenv("GDF_FORCE_RUNS") != nullptr;    // tuning knob: runs at every size
     bool run_hist_in_sort = getenv("GDF_RUN_HIST_SORT") != nullptr;  // tuning knob
-    // the frame's (or batch's) runs sorted per frame by two 11-bit passes (k_seg_sort_pass)
-    // instead of 8/8/9-bit passes over frame | voxel (GDF_NO_SEG_SORT: the latter)
-    bool seg_sort_allowed = !getenv("GDF_NO_SEG_SORT");
+    // tuning knob GDF_SEG_SORT: the frame's (or batch's) runs sorted per frame by two 11-bit
+    // passes (k_seg_hist + 2 x k_seg_sort_pass) instead of k_sort_hist + 8/8/9-bit passes over
+    // frame | voxel.  Bit-exact (the GPU suite passes with it), but measured slower on MI355X (A/B
+    // on one box, profiles/r05/segsort/): C2 26.1 vs 28.0 Gpoints/s - the 2048-bin histogram
+    // costs ~2 device atomics per run (8.9 us per VGA batch, 23 us per 4K frame, against 4.8 us
+    // for the 8-bit one) and an 11-bit pass 21 us against 14-17 us, so the sort stays at ~51 us.
+    bool seg_sort_allowed = getenv("GDF_SEG_SORT") != nullptr;
     bool run_hist_all = getenv("GDF_RUN_HIST_ALL") != nullptr;  // tuning knob: k_mask counts the
                                                                // run digits at any segment count
     bool xruns = !getenv("GDF_NO_XRUNS");  // voxelize_points sorts the received list's runs
