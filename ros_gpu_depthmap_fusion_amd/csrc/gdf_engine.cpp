@@ -2004,6 +2004,10 @@ int gdf_create(int device, gdf_engine** out) {
             g_run_q16 = (uint32_t)std::atoi(v);
         if (const char* v = std::getenv("GDF_RUN_BIG_BLOCKS"))  // tuning knob
             g_run_big_blocks = (uint32_t)std::max(1, std::atoi(v));
+        if (const char* v = std::getenv("GDF_SORT_BLOCKS"))  // tuning knob
+            g_sort_blocks = (uint32_t)std::max(1, std::atoi(v));
+        if (const char* v = std::getenv("GDF_GROUP_BLOCKS"))  // tuning knob
+            g_group_blocks = (uint32_t)std::max(1, std::atoi(v));
         if (const char* v = std::getenv("GDF_RUN_INBLOCK"))  // tuning knob
             g_run_inblock = (uint32_t)std::max(0, std::atoi(v));
         if (const char* v = std::getenv("GDF_POINTS_LANE"))  // tuning knob

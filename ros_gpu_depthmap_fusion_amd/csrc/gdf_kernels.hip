@@ -3740,6 +3740,10 @@ uint32_t g_run_inblock = 1024;  // (measured: C2 / 720p x4 / 4K best or within n
 uint32_t g_run_wave = 2;
 
 uint32_t g_run_big_blocks = 1024;  // k_group_runs_big grid (tuning knob GDF_RUN_BIG_BLOCKS)
+// persistent grids of the radix passes and of the group phase, at most (tuning knobs
+// GDF_SORT_BLOCKS / GDF_GROUP_BLOCKS): the launches are sized by the capacity (the item count is
+// on the device), and a run sort's ~10x fewer items leave most blocks with no tile
+uint32_t g_sort_blocks = 2048, g_group_blocks = 2048;
 // chunks of k_group_runs_big (one 4-wave block per queued group): 1 K points (Q = 16) or 512
 // (Q = 8); 0 never 1 K, 1 always, 2 (default) for single frames - 4K depth frames (voxels of
 // ~20 K points) and rollbuffer windows (C3: 4.72 -> 4.49 ms per frame with 1 K chunks) - and 512
@@ -4471,7 +4475,8 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
     const int pt = a.sort_pt == 4 || a.sort_pt == 8 ? a.sort_pt : 16;
     const uint32_t tile = kSortThreads * pt;
     // persistent blocks (ticket loop): at most kPersistBlocks, fewer when the capacity is small
-    const uint32_t sort_tiles = std::min<uint32_t>((a.nmax + tile - 1) / tile, kPersistBlocks);
+    const uint32_t sort_tiles = std::min<uint32_t>((a.nmax + tile - 1) / tile,
+                                                   std::min<uint32_t>(kPersistBlocks, g_sort_blocks));
     hipError_t e;
     if (!a.hist_ready && !a.seg_sort) {
         unsigned hb = grid_blocks(a.nmax, 256 * 4);
@@ -4539,7 +4544,7 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
     const uint32_t sorted_passes = a.seg_sort ? 2u : npasses;  // (the free pair: kbuf[passes & 1])
     const uint32_t* gcount = a.count;  // items of the group phase (points, or runs)
     const uint32_t max_tiles = (a.nmax + kGroupThreads - 1) / kGroupThreads;
-    const uint32_t group_tiles = std::min<uint32_t>(max_tiles, kPersistBlocks);
+    const uint32_t group_tiles = std::min<uint32_t>(max_tiles, std::min<uint32_t>(kPersistBlocks, g_group_blocks));
     HookScope hs(hook, GDF_KERNEL_GROUP);
     const uint32_t* tile_base = nullptr;
     const uint32_t* tile_gtot = nullptr;
