@@ -4475,7 +4475,12 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
     const int pt = a.sort_pt == 4 || a.sort_pt == 8 ? a.sort_pt : 16;
     const uint32_t tile = kSortThreads * pt;
     // persistent blocks (ticket loop): at most kPersistBlocks, fewer when the capacity is small
-    const uint32_t sort_tiles = std::min<uint32_t>((a.nmax + tile - 1) / tile,
+    // a run sort's items are ~10x fewer than the capacity's points: a grid of an eighth (at least
+    // 256 blocks) holds them, and the empty blocks of a full grid only delay the grid-update
+    // blocks behind them (C2 +1 %, profiles/r05/knobs/)
+    const uint32_t cap_tiles = (a.nmax + tile - 1) / tile;
+    const uint32_t run_cap = a.run_start ? std::max<uint32_t>(256u, cap_tiles / 8) : cap_tiles;
+    const uint32_t sort_tiles = std::min<uint32_t>(std::min(cap_tiles, run_cap),
                                                    std::min<uint32_t>(kPersistBlocks, g_sort_blocks));
     hipError_t e;
     if (!a.hist_ready && !a.seg_sort) {
