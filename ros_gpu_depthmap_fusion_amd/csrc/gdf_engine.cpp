@@ -515,6 +515,9 @@ struct gdf_engine {
     // costs ~2 device atomics per run (8.9 us per VGA batch, 23 us per 4K frame, against 4.8 us
     // for the 8-bit one) and an 11-bit pass 21 us against 14-17 us, so the sort stays at ~51 us.
     bool seg_sort_allowed = getenv("GDF_SEG_SORT") != nullptr;
+    // the runs' lengths packed into the sort keys, their first points as the sorted values (the
+    // group phase reads no run_start[index] gathers); GDF_NO_PACK_RUNS: the index form
+    bool pack_runs = !getenv("GDF_NO_PACK_RUNS");
     bool run_hist_all = getenv("GDF_RUN_HIST_ALL") != nullptr;  // tuning knob: k_mask counts the
                                                                // run digits at any segment count
     bool xruns = !getenv("GDF_NO_XRUNS");  // voxelize_points sorts the received list's runs
@@ -643,7 +646,8 @@ struct gdf_engine {
             const uint32_t code = c.h_misc[kErr];
             c.h_misc[kErr] = 0;
             HIPCHK(hipMemsetAsync(c.d_misc.as<uint32_t>() + kErr, 0, 4, s()));
-            fail(GDF_ERR_DEVICE, "device look-back spin limit expired (code " + std::to_string(code) + ")");
+            fail(GDF_ERR_DEVICE, "device error flags (code " + std::to_string(code) +
+                                     ": 1/2/4 look-back / grid spin limit, 8 run-group queue full, 16 run over 64 points)");
         }
     }
     // read the small device counters into pinned memory (after the producing kernels)
@@ -1588,7 +1592,9 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime,
         v.count = e->sl().d_misc.as<uint32_t>() + (e->sl().runs_sel ? kRunTotal : kRunCount);
         v.run_start = e->sl().d_runstart.as<uint32_t>();
         v.point_count = e->sl().d_misc.as<uint32_t>() + kCount;
+        v.pack_runs = e->pack_runs && sort_bits(e) <= 25 ? 1 : 0;
         if (seg_sort_ok(e, nmax)) {  // (the runs come in frame order)
+            v.pack_runs = 0;
             Slot& q = e->sl();
             const uint32_t nf = std::max<uint32_t>(e->nframes, 1);
             q.d_seghist.ensure_zero((size_t)kMaxCams * 2 * kSegSortDigits * 4, e->s());
@@ -2476,7 +2482,7 @@ int gdf_download_frame(gdf_engine* e, uint32_t what, gdf_host_frame* out) {
             const uint32_t* hm = static_cast<const uint32_t*>(M.misc.p);
             if (hm[kErr]) {
                 HIPCHK(hipMemsetAsync(q.d_misc.as<uint32_t>() + kErr, 0, 4, e->s()));
-                fail(GDF_ERR_DEVICE, "device look-back spin limit expired (code " + std::to_string(hm[kErr]) + ")");
+                fail(GDF_ERR_DEVICE, "device error flags (code " + std::to_string(hm[kErr]) + ")");
             }
             std::memcpy(q.h_misc, hm, kMiscWords * 4);
             const uint32_t n = hm[kCount], nv = hm[kVoxCount];

@@ -2895,6 +2895,14 @@ hipError_t launch_scatter(const uint32_t* coords, const uint32_t* count, uint32_
 // them: large frames).  Keys of neighbouring points repeat, so each wave adds run lengths: the
 // first lane of a run of equal digits adds the run (few LDS atomics on hot bins); each thread
 // keeps 4 chunk loads in flight.
+// Packed run keys (VoxelizeArgs::pack_runs): the engine's own runs are at most 64 points long (a
+// run never leaves a 64-lane wave word of the compaction), so the first radix pass stores the
+// run's length - 1 in key bits 26..31 - above every digit the passes extract (sort keys of <= 25
+// bits) - and sorts the run's first point as the value instead of its index: the group phase then
+// reads each sorted run's points range from its own key / value, not by a gather of
+// run_start[index] (8 useful bytes per 64-128-B line: most of k_group_runs' traffic on C3).
+constexpr uint32_t kRunLenShift = 26, kRunKeyMask = (1u << kRunLenShift) - 1u;
+
 // frame of compacted point `idx` in a batch: the number of frame starts (after frame 0) <= idx
 __device__ __forceinline__ uint32_t frame_of(const uint32_t* s_fstart, uint32_t nframes,
                                              uint32_t idx) {
@@ -2997,7 +3005,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
     uint32_t* tile_ctr, uint32_t* epoch_word, uint32_t* err, uint32_t shift, uint32_t dbits,
     uint32_t grid_block0, uint4* grid, uint32_t* marks, uint64_t grid_nwords, uint32_t lifetime,
     GridSeq q, uint32_t nframes, uint32_t fshift, const uint32_t* __restrict__ fstart,
-    uint64_t mark_words, SnapArgs snap, uint32_t* qreset) {
+    uint64_t mark_words, SnapArgs snap, uint32_t* qreset, const uint32_t* __restrict__ pack_rs) {
     constexpr int kTile = kSortThreads * PT;
     // (first pass: the run-group queue counters start from zero for this voxelize's k_group_runs)
     if (qreset && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -3055,6 +3063,12 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
             key[j] = ok ? kin[idx] : 0xFFFFFFFFu;
             val[j] = ok ? (vin ? vin[idx] : idx) : 0u;
             if (add_frame && ok) key[j] |= frame_of(s_fstart, nframes, idx) << fshift;
+            if (pack_rs && ok) {  // (first pass: the run's first point and its length in the key)
+                const uint32_t ps = pack_rs[idx], len = pack_rs[idx + 1] - ps;
+                if (len - 1u > 63u) atomicOr(err, 16u);  // (invariant: runs inside a wave word)
+                val[j] = ps;
+                key[j] |= (min(max(len, 1u), 64u) - 1u) << kRunLenShift;
+            }
         }
 #pragma unroll
         for (int j = 0; j < PT; ++j) {
@@ -3467,7 +3481,7 @@ __global__ __launch_bounds__(256) void k_group_count(const uint32_t* __restrict_
                                                      const uint32_t* __restrict__ count,
                                                      uint32_t* __restrict__ counts,
                                                      uint32_t* gdone, uint32_t* offsets,
-                                                     uint32_t* gtot) {
+                                                     uint32_t* gtot, uint32_t km) {
     __shared__ uint32_t s_w[4];
     __shared__ uint32_t s_last;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -3475,8 +3489,8 @@ __global__ __launch_bounds__(256) void k_group_count(const uint32_t* __restrict_
     const uint32_t ntiles = (n + kGroupThreads - 1) / kGroupThreads;
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {  // block-uniform
         const uint32_t i = t * kGroupThreads + threadIdx.x;
-        const uint32_t key = i < n ? keys[i] : 0u;
-        const uint32_t prev = (i < n && i > 0) ? keys[i - 1] : ~key;
+        const uint32_t key = i < n ? keys[i] & km : 0u;
+        const uint32_t prev = (i < n && i > 0) ? keys[i - 1] & km : ~key;
         const unsigned long long b = __ballot(i < n && (i == 0 || key != prev));
         if (lane == 0) s_w[wid] = (uint32_t)__popcll(b);
         __syncthreads();
@@ -4001,7 +4015,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
     uint32_t* marks, const uint32_t* tile_base, uint4* __restrict__ bigq, uint32_t bigq_cap,
     uint32_t* __restrict__ qctr, uint32_t nframes, uint32_t fshift, uint32_t* __restrict__ fvox,
     uint32_t inblock_max, uint32_t* __restrict__ rps, uint32_t* __restrict__ rlen,
-    uint32_t small_max, const uint32_t* tile_gtot, uint64_t mark_stride) {
+    uint32_t small_max, const uint32_t* tile_gtot, uint64_t mark_stride, uint32_t packed) {
     __shared__ uint32_t s_wave[4];
     __shared__ uint32_t s_tile, s_epoch, s_excl, s_nbig, s_nq, s_qbase, s_wend, s_nx, s_nbase;
     __shared__ uint32_t s_nh, s_hbase;
@@ -4017,6 +4031,9 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
     if (WAVE == 1) wave_soa_init(s_wsoa[wid]);
     if (WAVE == 0) inblock_max = min(inblock_max, small_max);  // longer groups: k_group_runs_big
     const uint32_t n = *count;  // runs
+    // packed run keys: the length bits above the key (kRunLenShift), the first point as the value
+    const uint32_t km = packed ? kRunKeyMask : 0xFFFFFFFFu;
+    auto K = [&](uint32_t j) { return keys[j] & km; };
     const uint32_t ntiles = (n + kGroupThreads - 1) / kGroupThreads;
     const uint32_t kmask = nframes > 1 ? (1u << fshift) - 1u : 0xFFFFFFFFu;
     if (blockIdx.x == 0) {
@@ -4055,14 +4072,14 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
         const uint32_t t0 = tile * kGroupThreads;
         const uint32_t i = t0 + threadIdx.x;
         const uint32_t tend = min(n, t0 + kGroupThreads);
-        const uint32_t key = i < n ? keys[i] : 0u;
-        const uint32_t prev = (i < n && i > 0) ? keys[i - 1] : ~key;
+        const uint32_t key = i < n ? K(i) : 0u;
+        const uint32_t prev = (i < n && i > 0) ? K(i - 1) : ~key;
         const bool start = i < n && (i == 0 || key != prev);
         RunRec rr{0u, 0u};
         if (average && i < n) {  // (and the sorted run records for k_group_runs_big)
             const uint32_t v = rvals[i];
-            rr.ps = run_start[v];
-            rr.len = run_start[v + 1] - rr.ps;
+            rr.ps = packed ? v : run_start[v];
+            rr.len = packed ? (keys[i] >> kRunLenShift) + 1u : run_start[v + 1] - rr.ps;
             rps[i] = rr.ps;
             rlen[i] = rr.len;
         }
@@ -4082,18 +4099,18 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
                 if (tile == ntiles - 1) {
                     *out_count = ex + total;
                     if (fvox)
-                        for (uint32_t f = (keys[n - 1] >> fshift) + 1; f <= nframes; ++f)
+                        for (uint32_t f = (K(n - 1) >> fshift) + 1; f <= nframes; ++f)
                             fvox[f] = ex + total;
                 }
             }
         } else if (wid == 1 && total) {  // end of the tile's last group (as k_group, over runs)
-            const uint32_t lastkey = keys[tend - 1];
+            const uint32_t lastkey = K(tend - 1);
             uint32_t lo = tend, hi = n;
             while (lo < hi) {
                 const uint32_t len = hi - lo;
                 const uint32_t step = len <= 64u || lo == tend ? 1u : (len + 63u) / 64u;
                 const uint32_t j = lo + (uint32_t)lane * step;
-                const unsigned long long ch = __ballot(j < hi && keys[j] > lastkey);
+                const unsigned long long ch = __ballot(j < hi && K(j) > lastkey);
                 if (ch) {
                     const uint32_t f = (uint32_t)(__ffsll((long long)ch) - 1);
                     hi = lo + f * step;
@@ -4111,8 +4128,8 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
                 uint32_t ps = 0, len = 0;
                 if ((uint32_t)lane < nx) {
                     const uint32_t v = rvals[tend + lane];
-                    ps = run_start[v];
-                    len = run_start[v + 1] - ps;
+                    ps = packed ? v : run_start[v];
+                    len = packed ? (keys[tend + lane] >> kRunLenShift) + 1u : run_start[v + 1] - ps;
                 }
                 const uint32_t inc = dpp_sum_scan(len);
                 if ((uint32_t)lane < nx) {
@@ -4219,18 +4236,18 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
                 const uint32_t g = s_excl + threadIdx.x;
                 const uint32_t s = s_start[threadIdx.x], e = s_start[threadIdx.x + 1];
                 if (marks) {  // (mark_stride: a batch's frame f at f * mark_stride words)
-                    const uint32_t k = keys[s] & kmask;
-                    const uint64_t fo = mark_stride && nframes > 1 ? (uint64_t)(keys[s] >> fshift) * mark_stride : 0u;
+                    const uint32_t k = K(s) & kmask;
+                    const uint64_t fo = mark_stride && nframes > 1 ? (uint64_t)(K(s) >> fshift) * mark_stride : 0u;
                     atomicOr(marks + fo + (k >> 5), 1u << (k & 31u));
                 }
                 if (fvox) {
-                    const uint32_t fc = keys[s] >> fshift;
-                    const uint32_t f0 = s == 0 ? 0u : (keys[s - 1] >> fshift) + 1u;
+                    const uint32_t fc = K(s) >> fshift;
+                    const uint32_t f0 = s == 0 ? 0u : (K(s - 1) >> fshift) + 1u;
                     for (uint32_t f = f0; f <= fc; ++f) fvox[f] = g;
                 }
                 if (!average) {
                     float c[4];
-                    group_corner(keys[s] & kmask, vp, c);
+                    group_corner(K(s) & kmask, vp, c);
                     *reinterpret_cast<float4*>(out + 4 * (size_t)g) = make_float4(c[0], c[1], c[2], c[3]);
                 } else if (qlocal != 0xFFFFFFFFu) {  // k_group_runs_big
                     const uint32_t slot = s_qbase + qlocal;
@@ -4275,20 +4292,20 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
                 const uint32_t s = s_start[threadIdx.x], e = s_start[threadIdx.x + 1];
                 float* o = out + 4 * (size_t)g;
                 if (marks) {  // (mark_stride: a batch's frame f at f * mark_stride words)
-                    const uint32_t k = keys[s] & kmask;
-                    const uint64_t fo = mark_stride && nframes > 1 ? (uint64_t)(keys[s] >> fshift) * mark_stride : 0u;
+                    const uint32_t k = K(s) & kmask;
+                    const uint64_t fo = mark_stride && nframes > 1 ? (uint64_t)(K(s) >> fshift) * mark_stride : 0u;
                     atomicOr(marks + fo + (k >> 5), 1u << (k & 31u));
                 }
                 if (fvox) {
-                    const uint32_t fc = keys[s] >> fshift;
-                    const uint32_t f0 = s == 0 ? 0u : (keys[s - 1] >> fshift) + 1u;
+                    const uint32_t fc = K(s) >> fshift;
+                    const uint32_t f0 = s == 0 ? 0u : (K(s - 1) >> fshift) + 1u;
                     for (uint32_t f = f0; f <= fc; ++f) fvox[f] = g;
                 }
                 const uint32_t g0 = s_off[s - t0] - W0;  // staged positions of the group
                 const uint32_t g1 = e <= rend ? s_off[e - t0] - W0 : 0xFFFFFFFFu;
                 if (!average) {
                     float c[4];
-                    group_corner(keys[s] & kmask, vp, c);
+                    group_corner(K(s) & kmask, vp, c);
                     *reinterpret_cast<float4*>(o) = make_float4(c[0], c[1], c[2], c[3]);
                 } else if (qlocal != 0xFFFFFFFFu) {  // past the staged points: k_group_runs_big
                     const uint32_t slot = s_qbase + qlocal;
@@ -4445,7 +4462,8 @@ static void launch_sort_pass(uint32_t tiles, hipStream_t s, const uint32_t* kin,
                        reinterpret_cast<uint4*>(a.grid8), a.marks, nwords, a.lifetime, a.gseq,
                        a.nframes, a.frame_shift, a.frame_pt_start, a.mark_words,
                        a.snap,
-                       p == 0 ? reinterpret_cast<uint32_t*>(a.ctrs + kCtrRunQueue) : nullptr);
+                       p == 0 ? reinterpret_cast<uint32_t*>(a.ctrs + kCtrRunQueue) : nullptr,
+                       p == 0 && a.pack_runs ? a.run_start : nullptr);
 }
 
 // Blocks of k_group_runs_big<8> / <16> the current device holds at once, cached per device (an
@@ -4563,7 +4581,7 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
         const bool gscan = a.group_done && max_tiles <= kMaxGroupScanTiles;
         hipLaunchKernelGGL(k_group_count, dim3(group_tiles), dim3(256), 0, s, kin, gcount,
                            a.group_counts, gscan ? a.group_done : nullptr, a.group_offsets,
-                           a.group_gtot);
+                           a.group_gtot, runs && a.pack_runs && !a.seg_sort ? kRunKeyMask : 0xFFFFFFFFu);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (!gscan && (e = launch_scan(a.group_counts, max_tiles, a.group_offsets, nullptr, gcount,
                                        (uint32_t)kGroupThreads, s)) != hipSuccess)
@@ -4585,7 +4603,7 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
                            a.nframes, a.frame_shift, a.frame_vox_start,
                            std::min<uint32_t>(g_run_inblock, g_run_stage >= 2048 ? 2048u : 512u),
                            kbuf[sorted_passes & 1], vbuf[sorted_passes & 1], g_small_group,  // (free after the sort)
-                           tile_gtot, a.group_mark_stride);
+                           tile_gtot, a.group_mark_stride, a.pack_runs && !a.seg_sort ? 1u : 0u);
         if (a.average) {
             if ((e = hipGetLastError()) != hipSuccess) return e;
             const bool q16 = g_run_q16 == 1 ||

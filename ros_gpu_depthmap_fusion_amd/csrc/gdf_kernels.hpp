@@ -157,6 +157,10 @@ struct VoxelizeArgs {
     // histograms [16][2][2048] (zero on entry and exit), the frames' run starts [17], tile / group
     // granules (seg_sort_tiles(nmax, nframes) x 2048, epoch-tagged), a self-resetting counter
     int seg_sort;
+    // the engine's own runs (<= 64 points each): the first radix pass packs each run's length into
+    // key bits 26..31 and sorts its first point as the value (sort keys of <= 25 bits; not with
+    // seg_sort)
+    int pack_runs;
     uint32_t* seg_hist;
     uint32_t* seg_fstart;
     unsigned long long* seg_status;
