@@ -515,6 +515,17 @@ struct gdf_engine {
     // costs ~2 device atomics per run (8.9 us per VGA batch, 23 us per 4K frame, against 4.8 us
     // for the 8-bit one) and an 11-bit pass 21 us against 14-17 us, so the sort stays at ~51 us.
     bool seg_sort_allowed = getenv("GDF_SEG_SORT") != nullptr;
+    // tuning knob GDF_FRAME_SORT: the runs of each frame of a batch sorted by ONE workgroup in
+    // LDS (k_frame_sort) instead of k_sort_hist + 3 batch-wide look-back passes.  Bit-exact (the
+    // GPU suite passes with it), but measured slower on MI355X (A/B on one box,
+    // profiles/r05/framesort/): C2 26.6 vs 28.2 Gpoints/s - ranking a VGA frame's ~13.4 K runs by
+    // 8-bit digits is VALU-bound on one CU (8.5 us per pass, 45 us per frame against the passes'
+    // ~50 us spread over the chip), and a 1024-thread workgroup at 122 VGPRs dispatches only to an
+    // EMPTY CU.  GDF_FRAME_SORT_CAP=n: frames of more than n runs take the chunked form (tests)
+    bool frame_sort_allowed = getenv("GDF_FRAME_SORT") != nullptr;
+    uint32_t frame_sort_cap = getenv("GDF_FRAME_SORT_CAP")
+                                  ? (uint32_t)strtoul(getenv("GDF_FRAME_SORT_CAP"), nullptr, 10)
+                                  : kFrameSortResident;
     // the runs' lengths packed into the sort keys, their first points as the sorted values (the
     // group phase reads no run_start[index] gathers); GDF_NO_PACK_RUNS: the index form
     bool pack_runs = !getenv("GDF_NO_PACK_RUNS");
@@ -1274,6 +1285,17 @@ bool seg_sort_ok(const gdf_engine* e, uint32_t nmax) {
            seg_sort_tiles(std::max<uint32_t>(nmax, 1), std::max<uint32_t>(e->nframes, 1)) <= kSegSortTileCap;
 }
 
+// The per-frame LDS sort serves the engine's own runs (in frame order, no rollbuffer selection) of
+// voxel keys <= 25 bits (a run item in LDS is the key's digits above 8 bits | a 14-bit index)
+// while a frame holds at most kFrameSortPoints points (VGA: 307 K, ~13 K runs, sorted resident; a
+// 720p / 4K frame's runs take the batch-wide passes, whose many CUs move them faster than the one
+// CU of a frame's chunked form)
+constexpr uint32_t kFrameSortPoints = 1u << 19;
+bool frame_sort_ok(const gdf_engine* e, uint32_t nmax) {
+    return e->frame_sort_allowed && !seg_sort_ok(e, nmax) && e->key_bits <= 25 &&
+           nmax / std::max<uint32_t>(e->nframes, 1) <= kFrameSortPoints;
+}
+
 FrameArgs frame_args(gdf_engine* e, bool fused_voxel, bool compaction_marks = false) {
     if (!e->prepared) prepare_buffers(e);
     if (!e->depth_uploaded) upload_depthmaps(e);
@@ -1370,7 +1392,8 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel, bool compaction_marks = fa
         // k_sort_hist over the runs (tens of thousands of flushes contend at the atomic units)
         if (a.run_mode)
             a.key_hist = (a.total_segs <= kFusedPrefixSegs || e->run_hist_all) && !e->run_hist_in_sort &&
-                         !a.sel_tiles && !seg_sort_ok(e, e->sl().n_total)  // (k_seg_hist counts)
+                         !a.sel_tiles && !seg_sort_ok(e, e->sl().n_total) &&  // (k_seg_hist counts)
+                         !frame_sort_ok(e, e->sl().n_total)  // (k_frame_sort needs no histogram)
                              ? e->sl().d_khist.as<uint32_t>() : nullptr;
     }
     a.out_pts = e->sl().d_pts.as<float4>();
@@ -1608,6 +1631,9 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime,
             v.seg_status = q.d_segstat.as<unsigned long long>();
             v.seg_gstatus = q.d_seggstat.as<unsigned long long>();
             v.seg_done = q.d_segdone.as<uint32_t>();
+        } else if (!e->sl().runs_sel && frame_sort_ok(e, nmax)) {
+            v.frame_sort = 1;
+            v.frame_sort_cap = e->frame_sort_cap;
         }
     }
     v.nmax = nmax;

@@ -3338,6 +3338,355 @@ __global__ __launch_bounds__(kSortThreads) void k_seg_sort_pass(
     }
 }
 
+// ---- per-frame LDS radix sort of a batch's runs ---------------------------------------------------
+// The runs of a batch come in frame order and each frame's runs fit one CU's LDS (a VGA frame has
+// ~14 K runs): ONE workgroup per frame sorts its frame's runs by their voxel key, every LSD pass in
+// LDS, and writes them once - one launch of B workgroups instead of a histogram launch plus three
+// look-back passes over the whole batch (each reading and writing every run), and the other
+// 255 - B CUs stay free for the neighbouring batches' kernels.  The order equals the batch-wide
+// stable sort of voxel | frame << fshift (radix_sort.h:107-289): within a frame the LSD passes
+// are stable, frames keep their order.  In LDS an item is ONE word - the key's remaining digits
+// above its local index (14 bits) - so a pass moves 4 bytes per run; the sorted keys and their
+// values are gathered by that index at the end (staged in LDS).  A frame with more runs than
+// kFsCap (or than the GDF_FRAME_SORT_CAP knob) takes a chunked form of the same passes through
+// the slot's spare key / value buffers (correct, one CU's bandwidth).
+constexpr int kFsThreads = 1024, kFsWaves = kFsThreads / 64, kFsPT = 16, kFsChunkPT = 8;
+// (16 slots: 122 VGPRs; 24 or 32 spill at the 128 of 16 waves per CU)
+constexpr uint32_t kFsIdxBits = 14, kFsCap = (uint32_t)kFsThreads * kFsPT;  // 2^14 items
+static_assert(kFsCap == (1u << kFsIdxBits), "local index field");
+
+struct FsShared {
+    uint32_t buf[kFsCap + 1];     // exchange buffer; at the end the frame's keys / run starts
+    uint32_t cnt[kFsWaves][256];  // per-wave digit counters -> the wave's exclusive prefix
+    uint32_t base[256];           // digit bases (chunked form: the running digit offsets)
+    uint32_t wsum[kFsWaves];
+};
+
+// Rank this wave's items (slot j < S, lane l: item j * 64 + l of the wave) by digit: rk[j] = the
+// number of the wave's earlier items with the same digit, counted on in cntw[digit] (every lane
+// reads its digit's count, the digit group's first lane writes it back advanced; a wave's LDS
+// operations execute in order).  Padding items (past the frame's runs: a suffix of the item
+// order) are ranked like the others; they carry digit 255, so no valid item's position moves.
+// (LDS atomics with return instead: ~1 lane per clock, 4x slower on MI355X.)
+template <int PT, class Dig>
+__device__ __forceinline__ void fs_rank(Dig dig, uint32_t S, uint32_t* cntw, uint32_t (&rk)[PT]) {
+    const unsigned long long ltm = lanemask_lt();
+#pragma unroll
+    for (int j = 0; j < PT; ++j) {
+        if ((uint32_t)j < S) {  // (wave-uniform)
+            const uint32_t d = dig(j);
+            unsigned long long m = ~0ull;
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                const bool bit = (d >> b) & 1u;
+                const unsigned long long bb = __ballot(bit);
+                m &= bit ? bb : ~bb;
+            }
+            const uint32_t before = (uint32_t)__popcll(m & ltm);
+            const uint32_t base = cntw[d];
+            rk[j] = base + before;
+            __builtin_amdgcn_wave_barrier();
+            if (before == 0) cntw[d] = base + (uint32_t)__popcll(m);
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
+// After fs_rank of every wave (and a barrier): cnt[w][d] -> the exclusive prefix of digit d over
+// the waves before w; base[d] = the exclusive prefix of the digit totals (+ base[d] when
+// accumulating: the chunked form's running offsets).  Digit t's total goes to thread t < 256.
+__device__ __forceinline__ uint32_t fs_offsets(FsShared& sh, bool accumulate) {
+    const uint32_t t = threadIdx.x;
+    const int lane = t & 63, wid = t >> 6;
+    uint32_t tot = 0;
+    if (t < 256) {
+#pragma unroll
+        for (int w = 0; w < kFsWaves; ++w) {
+            const uint32_t c = sh.cnt[w][t];
+            sh.cnt[w][t] = tot;
+            tot += c;
+        }
+    }
+    uint32_t x = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (t < 256 && lane == 63) sh.wsum[wid] = x;
+    __syncthreads();
+    if (t < 256) {
+        uint32_t wb = 0;
+        for (int w = 0; w < wid; ++w) wb += sh.wsum[w];
+        const uint32_t ex = wb + x - tot;
+        sh.base[t] = accumulate ? sh.base[t] + ex : ex;
+    }
+    __syncthreads();
+    return tot;
+}
+
+// [s0, s1): the runs of frame f, from the frame bits of the keys (key >> fshift, non-decreasing):
+// 1024 samples locate each bound to one interval, the interval's keys give it
+__device__ __forceinline__ void fs_frame_range(const uint32_t* keys, uint32_t n, uint32_t fshift,
+                                               uint32_t f, uint32_t& s0, uint32_t& s1) {
+    const uint32_t t = threadIdx.x;
+    const uint32_t stride = n ? (n + kFsThreads - 1) / kFsThreads : 1u;
+    const uint64_t i = (uint64_t)t * stride;
+    const uint32_t fr = i < n ? keys[i] >> fshift : 0xFFFFFFFFu;
+    const uint32_t c[2] = {(uint32_t)__syncthreads_count(i < n && fr < f),
+                           (uint32_t)__syncthreads_count(i < n && fr < f + 1u)};
+    uint32_t r[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {  // (block-uniform)
+        r[q] = 0;
+        if (c[q] == 0) continue;
+        const uint32_t start = (c[q] - 1u) * stride + 1u;
+        const uint32_t end = (uint32_t)min((uint64_t)c[q] * stride, (uint64_t)n);
+        uint32_t below = 0;
+        for (uint32_t b = start; b < end; b += kFsThreads) {
+            const uint32_t k = b + t;
+            below += (uint32_t)__syncthreads_count(k < end && (keys[k] >> fshift) < f + (uint32_t)q);
+        }
+        r[q] = start + below;
+    }
+    s0 = r[0];
+    s1 = r[1];
+}
+
+// The resident form of k_frame_sort: the frame's m <= 1024 * S runs as S slots per lane (slot j,
+// lane l of wave w: item w * 64 * S + j * 64 + l), every LSD pass through LDS.  Pass 0 ranks the
+// keys themselves; its exchange stores the packed item (key's voxel bits above 8) << 14 | local
+// index, which the later passes rank.  The padding past m (a suffix of the order) is all ones:
+// digit 255 in every pass.  (The item positions are recomputed from an opaque lane in every
+// phase: kept live across the passes they and their validity masks spill.)
+template <int S>
+__device__ __forceinline__ void fs_resident(FsShared& sh, const uint32_t* __restrict__ keys,
+                                            const uint32_t* __restrict__ run_start,
+                                            uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
+                                            uint32_t s0, uint32_t m, uint32_t npasses, uint32_t vmask,
+                                            uint32_t pack, uint32_t* err) {
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t wbase = __builtin_amdgcn_readfirstlane(w * 64u * (uint32_t)S);
+    uint32_t item[S], rk[S];
+    uint32_t lx = lane;
+    asm volatile("" : "+v"(lx));
+#pragma unroll
+    for (int j = 0; j < S; ++j) item[j] = keys[s0 + min(wbase + (uint32_t)j * 64u + lx, m - 1u)];
+#pragma unroll
+    for (int j = 0; j < S; ++j)
+        if (wbase + (uint32_t)j * 64u + lx >= m) item[j] = 0xFFFFFFFFu;
+    __syncthreads();
+    for (uint32_t p = 0; p < npasses; ++p) {
+        const uint32_t sh_d = p == 0 ? 0u : kFsIdxBits + 8u * (p - 1u);
+        fs_rank<S>([&](int j) { return (item[j] >> sh_d) & 255u; }, S, sh.cnt[w], rk);
+        __syncthreads();
+        (void)fs_offsets(sh, false);
+        lx = lane;
+        asm volatile("" : "+v"(lx));
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+            const uint32_t r = wbase + (uint32_t)j * 64u + lx;
+            const uint32_t d = (item[j] >> sh_d) & 255u;
+            uint32_t word = item[j];
+            if (p == 0) word = r < m ? (((item[j] & vmask) >> 8) << kFsIdxBits) | r : 0xFFFFFFFFu;
+            sh.buf[sh.base[d] + sh.cnt[w][d] + rk[j]] = word;
+        }
+        __syncthreads();
+        lx = lane;
+        asm volatile("" : "+v"(lx));
+#pragma unroll
+        for (int j = 0; j < S; ++j) item[j] = sh.buf[wbase + (uint32_t)j * 64u + lx];
+        for (uint32_t i = t; i < kFsWaves * 256; i += kFsThreads) (&sh.cnt[0][0])[i] = 0u;
+        __syncthreads();
+    }
+    // the values, then the keys of the sorted runs, gathered from LDS by the local index (the
+    // frame's run starts / keys staged by loads all in flight together).  Packed: the run's
+    // first point is the value, its length - 1 goes to key bits 26..31.
+    lx = lane;
+    asm volatile("" : "+v"(lx));
+    if (pack) {
+#pragma unroll
+        for (int j = 0; j < S; ++j) rk[j] = run_start[s0 + min(wbase + (uint32_t)j * 64u + lx, m)];
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+            const uint32_t r = wbase + (uint32_t)j * 64u + lx;
+            if (r <= m) sh.buf[r] = rk[j];
+        }
+        if (t == 0 && m == (uint32_t)kFsThreads * S) sh.buf[m] = run_start[s0 + m];
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+            const uint32_t r = wbase + (uint32_t)j * 64u + lx;
+            if (r < m) {
+                const uint32_t idx = item[j] & (kFsCap - 1u);
+                const uint32_t ps = sh.buf[idx], len = sh.buf[idx + 1] - ps;
+                if (len - 1u > 63u) atomicOr(err, 16u);  // (invariant: runs inside a wave word)
+                vout[s0 + r] = ps;
+                item[j] = idx | ((min(max(len, 1u), 64u) - 1u) << 16);
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < S; ++j) rk[j] = keys[s0 + min(wbase + (uint32_t)j * 64u + lx, m - 1u)];
+#pragma unroll
+    for (int j = 0; j < S; ++j) sh.buf[wbase + (uint32_t)j * 64u + lx] = rk[j];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+        const uint32_t r = wbase + (uint32_t)j * 64u + lx;
+        if (r < m) {
+            const uint32_t idx = item[j] & (kFsCap - 1u);
+            const uint32_t k = sh.buf[idx];
+            if (pack) {
+                kout[s0 + r] = k | (((item[j] >> 16) & 63u) << kRunLenShift);
+            } else {
+                kout[s0 + r] = k;
+                vout[s0 + r] = s0 + idx;
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(kFsThreads) void k_frame_sort(
+    const uint32_t* __restrict__ keys, const uint32_t* __restrict__ count,
+    const uint32_t* __restrict__ run_start, uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
+    uint32_t* __restrict__ ktmp, uint32_t* __restrict__ vtmp, uint32_t nframes, uint32_t fshift,
+    uint32_t vbits, uint32_t pack, uint32_t cap, uint32_t* err, uint32_t* qreset) {
+    __shared__ FsShared sh;
+    if (qreset && blockIdx.x == 0 && threadIdx.x == 0) {  // (the run-group queue of this voxelize)
+        qreset[0] = 0u;
+        qreset[1] = 0u;
+        qreset[2] = 0u;
+    }
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t n = *count;
+    uint32_t s0 = 0, s1 = n;
+    if (nframes > 1) fs_frame_range(keys, n, fshift, blockIdx.x, s0, s1);
+    s0 = __builtin_amdgcn_readfirstlane(s0);  // (block-uniform: scalar slot loops below)
+    s1 = __builtin_amdgcn_readfirstlane(s1);
+    const uint32_t m = s1 - s0;
+    const uint32_t npasses = (max(vbits, 1u) + 7u) / 8u;
+    const uint32_t vmask = vbits >= 32 ? 0xFFFFFFFFu : (1u << vbits) - 1u;
+    for (uint32_t i = t; i < kFsWaves * 256; i += kFsThreads) (&sh.cnt[0][0])[i] = 0u;
+    if (m <= min(cap, kFsCap)) {
+        if (m == 0) return;
+        // ---- resident form: S slots per lane, a multiple of 4 (compile-time: no per-slot guards,
+        // the loads of all slots in flight together) ----
+        switch ((m + 4u * kFsThreads - 1u) / (4u * kFsThreads)) {
+            case 1: fs_resident<4>(sh, keys, run_start, kout, vout, s0, m, npasses, vmask, pack, err); break;
+            case 2: fs_resident<8>(sh, keys, run_start, kout, vout, s0, m, npasses, vmask, pack, err); break;
+            case 3: fs_resident<12>(sh, keys, run_start, kout, vout, s0, m, npasses, vmask, pack, err); break;
+            default: fs_resident<16>(sh, keys, run_start, kout, vout, s0, m, npasses, vmask, pack, err); break;
+        }
+        return;
+    }
+    // ---- chunked form: per pass a digit histogram of the frame, then chunks of S * 1024 items
+    // (S <= kFsChunkPT) ranked as above, scattered to the other buffer pair; only the last chunk
+    // has padding (ranked with the others, a suffix: its counts go to no later chunk) ----
+    const uint32_t S = max(1u, min(cap / (uint32_t)kFsThreads, (uint32_t)kFsChunkPT));
+    const uint32_t chunk = S * kFsThreads;
+    const uint32_t kmask = pack ? kRunKeyMask : 0xFFFFFFFFu;
+    for (uint32_t p = 0; p < npasses; ++p) {
+        const bool to_out = ((npasses - 1u - p) & 1u) == 0u;  // (the last pass lands in kout)
+        uint32_t* kd = to_out ? kout : ktmp;
+        uint32_t* vd = to_out ? vout : vtmp;
+        const uint32_t* ks = p == 0 ? keys : (to_out ? ktmp : kout);
+        const uint32_t* vs = p == 0 ? nullptr : (to_out ? vtmp : vout);
+        const uint32_t shift = 8u * p;
+        __syncthreads();
+#pragma unroll 8
+        for (uint32_t i = t; i < m; i += kFsThreads)  // (the frame's totals as wave 0's counts)
+            atomicAdd(&sh.cnt[0][((ks[s0 + i] & kmask) >> shift) & 255u], 1u);
+        __syncthreads();
+        (void)fs_offsets(sh, false);
+        for (uint32_t i = t; i < kFsWaves * 256; i += kFsThreads) (&sh.cnt[0][0])[i] = 0u;
+        __syncthreads();
+        for (uint32_t c0 = 0; c0 < m; c0 += chunk) {  // (block-uniform)
+            const uint32_t cm = min(chunk, m - c0);
+            const uint32_t wbase = __builtin_amdgcn_readfirstlane(w * 64u * S);
+            const uint32_t nv = cm > wbase ? min(cm - wbase, 64u * S) : 0u;
+            uint32_t kk[kFsChunkPT], vv[kFsChunkPT], rk[kFsChunkPT];
+#pragma unroll
+            for (int j = 0; j < kFsChunkPT; ++j) {
+                const uint32_t r = (uint32_t)j * 64u + lane;
+                const bool ok = (uint32_t)j < S && r < nv;
+                const uint32_t i = s0 + c0 + wbase + r;
+                kk[j] = ok ? ks[i] : 0u;
+                vv[j] = ok ? (vs ? vs[i] : i) : 0u;
+                if (p == 0 && pack && ok) {
+                    const uint32_t ps = run_start[i], len = run_start[i + 1] - ps;
+                    if (len - 1u > 63u) atomicOr(err, 16u);
+                    vv[j] = ps;
+                    kk[j] |= (min(max(len, 1u), 64u) - 1u) << kRunLenShift;
+                }
+            }
+            fs_rank<kFsChunkPT>([&](int j) { return ((kk[j] & kmask) >> shift) & 255u; }, S, sh.cnt[w], rk);
+            __syncthreads();
+            // cnt -> the waves' prefixes; the chunk's items go on top of the running digit offsets
+            uint32_t tot = 0;
+            if (t < 256) {
+#pragma unroll
+                for (int ww = 0; ww < kFsWaves; ++ww) {
+                    const uint32_t c = sh.cnt[ww][t];
+                    sh.cnt[ww][t] = tot;
+                    tot += c;
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < kFsChunkPT; ++j) {
+                const uint32_t r = (uint32_t)j * 64u + lane;
+                if ((uint32_t)j < S && r < nv) {
+                    const uint32_t d = ((kk[j] & kmask) >> shift) & 255u;
+                    const uint32_t pos = s0 + sh.base[d] + sh.cnt[w][d] + rk[j];
+                    kd[pos] = kk[j];
+                    vd[pos] = vv[j];
+                }
+            }
+            __syncthreads();
+            if (t < 256) {
+                sh.base[t] += tot;
+#pragma unroll
+                for (int ww = 0; ww < kFsWaves; ++ww) sh.cnt[ww][t] = 0u;
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// the historic-grid update of a frame-sorted voxelize (the look-back passes carry it in extra
+// blocks; the per-frame sort's workgroups hold a CU's LDS each, so it runs as its own launch).
+// The wait for the previous update (grid_seq_enter's spin) is a one-block launch of its own ahead
+// of it: a k_frame_sort workgroup needs an EMPTY CU (16 waves at 122 VGPRs), and hundreds of
+// spinning grid blocks of later batches on every CU - waiting for an update queued behind that
+// sort on a shared hardware queue - never let one drain (the pipeline of 4 batches hung so).
+__global__ __launch_bounds__(64) void k_grid_wait(GridSeq q) {
+    if (threadIdx.x == 0 && q.ctl) {
+        const uint32_t f = q.fptr ? __hip_atomic_load(q.fptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : q.f;
+        uint32_t spins = 0;
+        while ((int32_t)(__hip_atomic_load(&q.ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - f) < 0) {
+            if (++spins > kSpinLimit) {
+                atomicOr(q.err, 4u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(8);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_grid_fused(uint4* __restrict__ grid, uint32_t* __restrict__ marks,
+                                                     uint64_t nwords, uint32_t lifetime, GridSeq q,
+                                                     uint32_t nframes, uint64_t mark_words, SnapArgs snap) {
+    // (the previous update has completed: k_grid_wait ran before; the grid is read coherently)
+    const uint32_t f = q.ctl ? (q.fptr ? __hip_atomic_load(q.fptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : q.f) : 0u;
+    if (nframes > 1)
+        grid_u8_part_frames(grid, marks, nwords, lifetime, blockIdx.x, gridDim.x, nframes, mark_words, snap);
+    else
+        grid_u8_part(grid, marks, nwords, lifetime, blockIdx.x, gridDim.x, q);
+    grid_seq_leave<true>(q, f, gridDim.x);
+}
+
 // Voxel groups of the sorted keys and their outputs in ONE kernel (RadixGrouper::makeGroups,
 // inc/radix_grouper.h:35-64, + averageGridCells / occupiedGridCells, inc/voxelize.h:9-71).
 // Tile = 256 sorted keys: group starts (key != previous key), their ids by a block scan plus a
@@ -4501,19 +4850,44 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
     const uint32_t sort_tiles = std::min<uint32_t>(std::min(cap_tiles, run_cap),
                                                    std::min<uint32_t>(kPersistBlocks, g_sort_blocks));
     hipError_t e;
-    if (!a.hist_ready && !a.seg_sort) {
+    const uint32_t* kin = a.keys;
+    const uint32_t* vin = nullptr;
+    uint32_t* kbuf[2] = {a.keys_a, a.keys_b};
+    uint32_t* vbuf[2] = {a.vals_a, a.vals_b};
+    const bool runs = a.run_start != nullptr;  // keys are run keys: sort runs, then expand
+    uint32_t sorted_passes = a.seg_sort ? 2u : npasses;  // (the free pair: kbuf[passes & 1])
+    if (a.frame_sort && runs) {  // one workgroup per frame (k_frame_sort), the grid update apart
+        HookScope hs(hook, GDF_KERNEL_SORT);
+        if (a.grid8) {
+            const uint64_t nwords = (a.ncells + 31) / 32;
+            if (a.gseq.ctl) {
+                hipLaunchKernelGGL(k_grid_wait, dim3(1), dim3(64), 0, s, a.gseq);
+                if ((e = hipGetLastError()) != hipSuccess) return e;
+            }
+            hipLaunchKernelGGL(k_grid_fused, dim3(fused_grid_blocks(a.ncells)), dim3(256), 0, s,
+                               reinterpret_cast<uint4*>(a.grid8), a.marks, nwords, a.lifetime, a.gseq,
+                               a.nframes, a.mark_words, a.snap);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
+        const uint32_t nf = std::max<uint32_t>(a.nframes, 1u);
+        const uint32_t vbits = a.nframes > 1 ? a.frame_shift : a.key_bits;
+        hipLaunchKernelGGL(k_frame_sort, dim3(nf), dim3(kFsThreads), 0, s, a.keys, a.count,
+                           a.run_start, kbuf[0], vbuf[0], kbuf[1], vbuf[1], a.nframes, a.frame_shift,
+                           vbits, a.pack_runs ? 1u : 0u, a.frame_sort_cap, a.err,
+                           reinterpret_cast<uint32_t*>(a.ctrs + kCtrRunQueue));
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        kin = kbuf[0];
+        vin = vbuf[0];
+        sorted_passes = 1;
+    }
+    if (!a.hist_ready && !a.seg_sort && !a.frame_sort) {
         unsigned hb = grid_blocks(a.nmax, 256 * 4);
         if (hb > 512) hb = 512;
         hipLaunchKernelGGL(k_sort_hist, dim3(hb), dim3(256), 0, s, a.keys, a.count, npasses, a.hist,
                            a.nframes, a.frame_shift, a.frame_pt_start);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    const uint32_t* kin = a.keys;
-    const uint32_t* vin = nullptr;
-    uint32_t* kbuf[2] = {a.keys_a, a.keys_b};
-    uint32_t* vbuf[2] = {a.vals_a, a.vals_b};
-    const bool runs = a.run_start != nullptr;  // keys are run keys: sort runs, then expand
-    if (a.seg_sort) {  // the frames' runs by two 11-bit passes (k_seg_sort_pass), no frame pass
+    if (a.seg_sort && !a.frame_sort) {  // the frames' runs by two 11-bit passes (k_seg_sort_pass), no frame pass
         HookScope hs(hook, GDF_KERNEL_SORT);
         const uint32_t nseg = std::max<uint32_t>(a.nframes, 1u);
         // persistent blocks: at most kPersistBlocks (the granules cover every tile, though)
@@ -4539,7 +4913,7 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
             vin = vbuf[p];
         }
     }
-    for (uint32_t p = 0; p < (a.seg_sort ? 0u : npasses); ++p) {
+    for (uint32_t p = 0; p < (a.seg_sort || a.frame_sort ? 0u : npasses); ++p) {
         const uint32_t remaining = a.key_bits > 8 * p ? a.key_bits - 8 * p : 0u;
         // (a 9-bit last digit: radix_wide_last)
         const bool wide = p + 1 == npasses && remaining == 9;
@@ -4564,7 +4938,6 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
         kin = kbuf[p & 1];
         vin = vbuf[p & 1];
     }
-    const uint32_t sorted_passes = a.seg_sort ? 2u : npasses;  // (the free pair: kbuf[passes & 1])
     const uint32_t* gcount = a.count;  // items of the group phase (points, or runs)
     const uint32_t max_tiles = (a.nmax + kGroupThreads - 1) / kGroupThreads;
     const uint32_t group_tiles = std::min<uint32_t>(max_tiles, std::min<uint32_t>(kPersistBlocks, g_group_blocks));

@@ -161,6 +161,11 @@ struct VoxelizeArgs {
     // key bits 26..31 and sorts its first point as the value (sort keys of <= 25 bits; not with
     // seg_sort)
     int pack_runs;
+    // per-frame LDS sort of the runs (k_frame_sort: one workgroup per frame, the engine's own runs
+    // in frame order, voxel keys of <= 25 bits); frame_sort_cap: runs of a frame sorted resident in
+    // LDS (above: the chunked form; the knob GDF_FRAME_SORT_CAP lowers it for the tests)
+    int frame_sort;
+    uint32_t frame_sort_cap;
     uint32_t* seg_hist;
     uint32_t* seg_fstart;
     unsigned long long* seg_status;
@@ -179,6 +184,8 @@ size_t voxelize_status_words(uint32_t nmax, uint32_t key_bits);
 uint32_t seg_sort_tiles(uint32_t nmax, uint32_t nframes);
 uint32_t seg_sort_groups(uint32_t nmax, uint32_t nframes);
 constexpr uint32_t kSegSortDigits = 2048;
+// runs per frame the per-frame sort keeps resident in one workgroup's LDS
+constexpr uint32_t kFrameSortResident = 16384;
 // capacity (256-key tiles) above which k_group takes its group-id offsets from count + scan
 extern uint32_t g_group_scan_tiles;
 // k_group_runs staging (512 or 2048 points) and in-block group size limit
