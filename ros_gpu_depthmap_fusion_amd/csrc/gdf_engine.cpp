@@ -523,6 +523,7 @@ struct gdf_engine {
     // ~50 us spread over the chip), and a 1024-thread workgroup at 122 VGPRs dispatches only to an
     // EMPTY CU.  GDF_FRAME_SORT_CAP=n: frames of more than n runs take the chunked form (tests)
     bool frame_sort_allowed = getenv("GDF_FRAME_SORT") != nullptr;
+    bool grid_last = getenv("GDF_GRID_LAST") != nullptr;  // tuning knob (VoxelizeArgs::grid_last)
     uint32_t frame_sort_cap = getenv("GDF_FRAME_SORT_CAP")
                                   ? (uint32_t)strtoul(getenv("GDF_FRAME_SORT_CAP"), nullptr, 10)
                                   : kFrameSortResident;
@@ -1680,6 +1681,7 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime,
         v.marks = marks_ptr(e);
         v.ncells = e->ncells;
         v.lifetime = (uint32_t)fused_grid_lifetime;
+        v.grid_last = e->grid_last ? 1 : 0;
         // the ticket was stored by this frame's k_mask (run_frame: grid_seq = grid_ticket)
         v.gseq = e->grid_seq(0, e->sl().d_misc.as<uint32_t>() + kGridTicket);
         delta_args(e, v.gseq, e->grid_ticket, e->nframes == 1);

@@ -4801,7 +4801,7 @@ static void launch_sort_pass(uint32_t tiles, hipStream_t s, const uint32_t* kin,
                              uint32_t* kout, uint32_t* vout, const VoxelizeArgs& a, uint32_t p,
                              uint32_t dbits) {
     // the first pass also carries the historic-grid update in extra blocks
-    const bool g = p == 0 && a.grid8 != nullptr;
+    const bool g = p == 0 && a.grid8 != nullptr && !a.grid_last;
     const uint64_t nwords = g ? (a.ncells + 31) / 32 : 0;
     const uint32_t gb = g ? fused_grid_blocks(a.ncells) : 0;
     hipLaunchKernelGGL((k_sort_pass<PT, NB>), dim3(tiles + gb), dim3(kSortThreads), 0, s, kin, vin, kout,
@@ -4813,6 +4813,21 @@ static void launch_sort_pass(uint32_t tiles, hipStream_t s, const uint32_t* kin,
                        a.snap,
                        p == 0 ? reinterpret_cast<uint32_t*>(a.ctrs + kCtrRunQueue) : nullptr,
                        p == 0 && a.pack_runs ? a.run_start : nullptr);
+}
+
+// the historic-grid update as launches of its own (a one-block wait for the previous update, then
+// the update's blocks, none of them spinning)
+static hipError_t launch_grid_apart(const VoxelizeArgs& a, hipStream_t s) {
+    const uint64_t nwords = (a.ncells + 31) / 32;
+    if (a.gseq.ctl) {
+        hipLaunchKernelGGL(k_grid_wait, dim3(1), dim3(64), 0, s, a.gseq);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_grid_fused, dim3(fused_grid_blocks(a.ncells)), dim3(256), 0, s,
+                       reinterpret_cast<uint4*>(a.grid8), a.marks, nwords, a.lifetime, a.gseq,
+                       a.nframes, a.mark_words, a.snap);
+    return hipGetLastError();
 }
 
 // Blocks of k_group_runs_big<8> / <16> the current device holds at once, cached per device (an
@@ -4858,17 +4873,7 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
     uint32_t sorted_passes = a.seg_sort ? 2u : npasses;  // (the free pair: kbuf[passes & 1])
     if (a.frame_sort && runs) {  // one workgroup per frame (k_frame_sort), the grid update apart
         HookScope hs(hook, GDF_KERNEL_SORT);
-        if (a.grid8) {
-            const uint64_t nwords = (a.ncells + 31) / 32;
-            if (a.gseq.ctl) {
-                hipLaunchKernelGGL(k_grid_wait, dim3(1), dim3(64), 0, s, a.gseq);
-                if ((e = hipGetLastError()) != hipSuccess) return e;
-            }
-            hipLaunchKernelGGL(k_grid_fused, dim3(fused_grid_blocks(a.ncells)), dim3(256), 0, s,
-                               reinterpret_cast<uint4*>(a.grid8), a.marks, nwords, a.lifetime, a.gseq,
-                               a.nframes, a.mark_words, a.snap);
-            if ((e = hipGetLastError()) != hipSuccess) return e;
-        }
+        if (a.grid8 && !a.grid_last && (e = launch_grid_apart(a, s)) != hipSuccess) return e;
         const uint32_t nf = std::max<uint32_t>(a.nframes, 1u);
         const uint32_t vbits = a.nframes > 1 ? a.frame_shift : a.key_bits;
         hipLaunchKernelGGL(k_frame_sort, dim3(nf), dim3(kFsThreads), 0, s, a.keys, a.count,
@@ -4897,7 +4902,7 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
                            nseg, a.frame_shift, a.seg_hist, a.seg_fstart);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         for (uint32_t p = 0; p < 2; ++p) {
-            const bool g = p == 0 && a.grid8 != nullptr;
+            const bool g = p == 0 && a.grid8 != nullptr && !a.grid_last;
             const uint64_t nwords = g ? (a.ncells + 31) / 32 : 0;
             const uint32_t gb = g ? fused_grid_blocks(a.ncells) : 0;
             hipLaunchKernelGGL((k_seg_sort_pass<8>), dim3(tiles + gb), dim3(kSortThreads), 0, s, kin, vin,
@@ -4992,7 +4997,8 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
                                    kbuf[sorted_passes & 1], vbuf[sorted_passes & 1], a.pts,
                                    reinterpret_cast<float*>(a.out), a.bigq, a.bigq_cap, qctr);
         }
-        return hipGetLastError();
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        return a.grid8 && a.grid_last ? launch_grid_apart(a, s) : hipSuccess;
     }
     hipLaunchKernelGGL(k_group, dim3(group_tiles ? group_tiles : 1), dim3(kGroupThreads), 0, s, kin,
                        vin, gcount, a.pts, reinterpret_cast<float*>(a.out), a.out_count,
@@ -5006,7 +5012,8 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
         hipLaunchKernelGGL(k_group_big, dim3(2048), dim3(256), 0, s, vin, a.pts,
                            reinterpret_cast<float*>(a.out), a.bigq, a.bigcnt, group_tiles, bigcap);
     }
-    return hipGetLastError();
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    return a.grid8 && a.grid_last ? launch_grid_apart(a, s) : hipSuccess;
 }
 
 // ---- orphan shaders of the reference --------------------------------------

@@ -166,6 +166,9 @@ struct VoxelizeArgs {
     // LDS (above: the chunked form; the knob GDF_FRAME_SORT_CAP lowers it for the tests)
     int frame_sort;
     uint32_t frame_sort_cap;
+    // the historic-grid update after the group phase, as launches of its own (k_grid_wait +
+    // k_grid_fused), instead of extra blocks of the first radix pass (knob GDF_GRID_LAST)
+    int grid_last;
     uint32_t* seg_hist;
     uint32_t* seg_fstart;
     unsigned long long* seg_status;
