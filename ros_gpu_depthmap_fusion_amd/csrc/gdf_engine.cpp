@@ -2036,6 +2036,10 @@ int gdf_create(int device, gdf_engine** out) {
             g_mask_px2 = (uint32_t)std::atoi(v);
         if (const char* v = std::getenv("GDF_RUN_Q16"))  // tuning knob
             g_run_q16 = (uint32_t)std::atoi(v);
+        {  // tuning knob (process-wide; every engine creation sets it, default 1)
+            const char* v = std::getenv("GDF_RUN_WAVE_MODE");
+            g_run_wave_mode = v ? (uint32_t)std::atoi(v) : 1u;
+        }
         if (const char* v = std::getenv("GDF_RUN_BIG_BLOCKS"))  // tuning knob
             g_run_big_blocks = (uint32_t)std::max(1, std::atoi(v));
         if (const char* v = std::getenv("GDF_SORT_BLOCKS"))  // tuning knob

@@ -4112,6 +4112,10 @@ uint32_t g_sort_blocks = 2048, g_group_blocks = 2048;
 // ~20 K points) and rollbuffer windows (C3: 4.72 -> 4.49 ms per frame with 1 K chunks) - and 512
 // for multi-frame batches (tuning knob GDF_RUN_Q16)
 uint32_t g_run_q16 = 2;
+// k_group_runs_big sums the groups below the huge region one per wave (wave_stream_sum) when the
+// queue is long (1); tuning knob GDF_RUN_WAVE_MODE=0: every group in block mode, 2: wave mode
+// whatever the queue's length
+uint32_t g_run_wave_mode = 1;
 
 
 // Wave64 inclusive sum scan on DPP (gdf_voxsum.hpp dpp_iscan).
@@ -4206,13 +4210,15 @@ __device__ __forceinline__ void dpp_max_scan_n(int (&v)[N]) {
 // position's point is base[run] + position (s_base: this wave's copy of the batch's bases).
 // Positions past the batch load point 0 (never summed), and no select touches the loaded values:
 // the loads stay in flight until the chunk is stored.
-template <int Q>
+// WAVE: the wave fetches a chunk of its own, Q / 4 rows from batch position c (wave mode of
+// k_group_runs_big; s_mark then holds 64 (Q / 4 + 1) marks of this wave).
+template <int Q, bool WAVE = false>
 __device__ __forceinline__ void fetch_rows4(const RunBatch& bt, uint32_t c, int* s_mark,
                                             const uint32_t* s_base, const float4* __restrict__ pts,
                                             float4 (&p)[Q / 4]) {
     constexpr int RPW = Q / 4;  // rows per wave
-    constexpr uint32_t CH = 64u * Q;
-    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    constexpr uint32_t CH = WAVE ? 64u * RPW : 64u * Q;
+    const uint32_t lane = threadIdx.x & 63, wid = WAVE ? 0u : threadIdx.x >> 6;
     const uint32_t row0 = wid * RPW, pos_w = c + 64u * row0;
 #pragma unroll
     for (int i = 0; i < RPW; ++i) s_mark[64u * (row0 + i) + lane] = -1;
@@ -4339,6 +4345,99 @@ __device__ __forceinline__ float block_stream_sum(const uint32_t* __restrict__ r
         } else {
             break;
         }
+    }
+    return s;
+}
+
+// Wave mode of k_group_runs_big: a queued group streamed by ONE wave, its 4 components side by
+// side (rows4c_chunk: lanes 16 c .. 16 c + 15 sum component c, stretch rows or the chain per
+// component), chunks of 256 points (4 rows) fetched by the wave itself TWO chunks ahead (a
+// chunk's adds take ~1 K cycles, a fetch's memory latency more), the run batches as
+// block_stream_sum's.  A block's 4 waves sum 4 different groups, so a SIMD runs as many chains
+// (the z sums of a window's floor: chain rows) as it holds waves, where the block form ran one per
+// group and its other 3 waves waited at the chunk barriers.  Returns this lane's component sum;
+// npts = the group's points.
+struct WaveCursor {  // the fetch position: batch (records of the next two read ahead), chunk
+    RunBatch b;
+    RunRecs rec1, rec2;
+    uint32_t rb, c;
+    bool live;
+};
+
+__device__ __forceinline__ uint32_t wave_fetch(WaveCursor& f, const uint32_t* __restrict__ rps,
+                                               const uint32_t* __restrict__ rlen, uint32_t re,
+                                               const float4* __restrict__ pts, int* s_mark,
+                                               uint32_t* s_base, float4 (&p)[4]) {
+    constexpr uint32_t CH = 256u, NB = 64u * kRunsPerLane;
+    if (!f.live) return 0u;  // (wave-uniform)
+    fetch_rows4<16, true>(f.b, f.c, s_mark, s_base, pts, p);
+    const uint32_t n = min(CH, f.b.T - f.c);
+    if (f.c + CH < f.b.T) {
+        f.c += CH;
+    } else if (f.rb + NB < re) {
+        f.b = run_batch(f.rec1);
+        f.rec1 = f.rec2;
+        f.rec2 = run_recs(rps, rlen, f.rb + 3u * NB, re);
+        f.rb += NB;
+        f.c = 0;
+        wave_sync();  // (this fetch's base reads are done)
+        put_bases(f.b, s_base);
+        wave_sync();
+    } else {
+        f.live = false;
+    }
+    return n;
+}
+
+__device__ __forceinline__ void wave_store_chunk(float* wsoa, const float4 (&p)[4], uint32_t n) {
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // values past n: -0.0, which leaves any sum as it is
+        const bool in = 64u * i + lane < n;
+        const uint32_t k = i * kRowStride + lane;
+        wsoa[0 * kWaveCompStride + k] = in ? p[i].x : -0.0f;
+        wsoa[1 * kWaveCompStride + k] = in ? p[i].y : -0.0f;
+        wsoa[2 * kWaveCompStride + k] = in ? p[i].z : -0.0f;
+        wsoa[3 * kWaveCompStride + k] = in ? p[i].w : -0.0f;
+    }
+}
+
+__device__ __forceinline__ float wave_stream_sum(const uint32_t* __restrict__ rps,
+                                                 const uint32_t* __restrict__ rlen, uint32_t rs,
+                                                 uint32_t re, const float4* __restrict__ pts,
+                                                 int* s_mark, uint32_t* s_base, float* wsoa,
+                                                 uint32_t& npts) {
+    constexpr uint32_t NB = 64u * kRunsPerLane;
+    WaveCursor f;
+    f.b = run_batch(run_recs(rps, rlen, rs, re));
+    f.rec1 = run_recs(rps, rlen, rs + NB, re);
+    f.rec2 = run_recs(rps, rlen, rs + 2u * NB, re);
+    f.rb = rs;
+    f.c = 0;
+    f.live = true;
+    put_bases(f.b, s_base);
+    wave_sync();
+    float4 p0[4], p1[4];
+    uint32_t n0 = wave_fetch(f, rps, rlen, re, pts, s_mark, s_base, p0);
+    uint32_t n1 = wave_fetch(f, rps, rlen, re, pts, s_mark, s_base, p1);
+    float s = 0.0f;
+    npts = 0;
+    while (n0) {  // wave-uniform: two chunks per iteration, the buffers alternating
+        wave_sync();  // (the previous chunk's rows are read)
+        wave_store_chunk(wsoa, p0, n0);
+        wave_sync();
+        const uint32_t m0 = n0;
+        n0 = wave_fetch(f, rps, rlen, re, pts, s_mark, s_base, p0);
+        s = rows4c_chunk(wsoa, m0, s);
+        npts += m0;
+        if (!n1) break;
+        wave_sync();
+        wave_store_chunk(wsoa, p1, n1);
+        wave_sync();
+        const uint32_t m1 = n1;
+        n1 = wave_fetch(f, rps, rlen, re, pts, s_mark, s_base, p1);
+        s = rows4c_chunk(wsoa, m1, s);
+        npts += m1;
     }
     return s;
 }
@@ -4706,12 +4805,18 @@ __global__ __launch_bounds__(256) void k_group_runs_big(const uint32_t* __restri
                                                        const float4* __restrict__ pts,
                                                        float* __restrict__ out,
                                                        const uint4* __restrict__ bigq,
-                                                       uint32_t bigq_cap, uint32_t* qctr) {
-    __shared__ int s_mark[64 * Q + 64];  // (+ a scratch row: marks of runs outside a wave's rows)
+                                                       uint32_t bigq_cap, uint32_t* qctr,
+                                                       uint32_t wave_mode) {
+    // block mode: s_mark[64 Q + 64], s_soa[4][kRowStride Q]; wave mode: s_mark[4][320] and a
+    // kWaveSoa SoA chunk per wave (the same bytes)
+    constexpr uint32_t kMarkN = 64 * Q + 64 > 4 * 320 ? 64 * Q + 64 : 4 * 320;
+    constexpr uint32_t kSoaN = 4 * kRowStride * Q > 4 * kWaveSoa ? 4 * kRowStride * Q : 4 * kWaveSoa;
+    __shared__ int s_mark[kMarkN];  // (+ a scratch row: marks of runs outside a wave's rows)
     __shared__ uint32_t s_base[4][64 * kRunsPerLane];  // (a copy per wave)
-    __shared__ __attribute__((aligned(16))) float s_soa[4][kRowStride * Q];
+    __shared__ __attribute__((aligned(16))) float s_soa_raw[kSoaN];
+    float (*s_soa)[kRowStride * Q] = reinterpret_cast<float (*)[kRowStride * Q]>(s_soa_raw);
     __shared__ uint32_t s_t;
-    const uint32_t wid = threadIdx.x >> 6;  // (the component)
+    const uint32_t wid = threadIdx.x >> 6;  // (the component, in block mode)
     // logical slot j: the huge region (appended from the top, drawn first), then the others
     const uint32_t na = __hip_atomic_load(qctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t nh = __hip_atomic_load(qctr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -4725,48 +4830,101 @@ __global__ __launch_bounds__(256) void k_group_runs_big(const uint32_t* __restri
         g_gtrace[kTraceSlots - 1][3] = bigq_cap;
     }
 #endif
-    // Block b takes slot b, then draws further slots from the counter.  The grid is sized to the
-    // blocks the chip holds at once (launch_voxelize): a block that is not resident yet must not
-    // hold a slot - with 1024 blocks, the C3 window's 100 K-point groups in slots ~800-1000
-    // started only when the rest of the queue was drained (1.0 ms into a 1.7 ms kernel,
-    // tools/group_trace.py --c3); drawing the first slot from the counter too serialised 10^3
-    // atomics at the start (4K: groups starting up to 13 us late, an empty queue 14 us).  One
-    // slot per draw: queued groups range over 10^3x in length (C3: up to 139 K points), and draws
-    // of 8 consecutive slots measured 1.7 -> 2.8 ms of tail imbalance on the C3 window.
+    // Every resident block / wave takes a first slot, further ones are drawn from the counter.
+    // The grid is sized to the blocks the chip holds at once (launch_voxelize): a block that is
+    // not resident yet must not hold a slot - with 1024 blocks, the C3 window's 100 K-point
+    // groups in slots ~800-1000 started only when the rest of the queue was drained (1.0 ms into
+    // a 1.7 ms kernel, tools/group_trace.py --c3); drawing the first slot from the counter too
+    // serialised 10^3 atomics at the start (4K: groups starting up to 13 us late, an empty queue
+    // 14 us).  One slot per draw: queued groups range over 10^3x in length (C3: up to 139 K
+    // points), and draws of 8 consecutive slots measured 1.7 -> 2.8 ms of tail imbalance on the
+    // C3 window.  The huge region is summed in block mode (wave c: component c, 1 K-point chunks:
+    // the shortest critical path for the longest groups); with wave_mode the other groups are
+    // summed one per wave (wave_stream_sum): blocks past the huge region start in wave mode, a
+    // block mode block switches to it at its first draw past the region (C3 group phase 1.58 ->
+    // 1.33 ms, profiles/r05/wavemode/).
+    // Wave mode only for a long queue (>= 4 normal groups per block: the C3 window's 22 K groups,
+    // not a 4K frame's ~650 - one wave's chain per group lengthens each group's sum, and with
+    // about one group per block that is the launch's critical path: 4K 125 -> 184 us)
+    const uint32_t G = gridDim.x;
+    if (wave_mode == 1 && na < 4u * G) wave_mode = 0;  // (2: always, the tests' knob)
+    const uint32_t nb0 = wave_mode ? min(nh, G) : G;  // blocks starting in block mode
+    const uint32_t start0 = nb0 + (G - nb0) * 4u;     // the first drawn slot
     uint32_t t = blockIdx.x;
-    while (t < nq) {  // block-uniform
+    if (blockIdx.x < nb0) {
+        while (true) {  // block-uniform
+            if (t >= nq) return;
+            if (wave_mode && t >= nh) break;  // (a normal slot: wave mode from here)
+            const uint4 q = bigq[slot_of(t)];
+            uint32_t np = 0;
+#ifdef GDF_TRACE_GROUPS
+            unsigned long long tr[5] = {0, 0, 0, 0, 0};
+            const unsigned long long w0 = wall_clock64(), c0 = clock64();
+            const float sum = block_stream_sum<Q>(rps, rlen, q.y, q.z, pts, s_mark, s_base[wid], s_soa, np, tr);
+            if (threadIdx.x == 128 && t < kTraceSlots) {  // (wave 2: z)
+                unsigned long long* g = g_gtrace[t];
+                g[0] = w0;
+                g[1] = wall_clock64();
+                g[2] = ((unsigned long long)np << 32) | (unsigned)tr[4];
+                g[3] = clock64() - c0;
+                g[4] = tr[0];
+                g[5] = tr[1];
+                g[6] = tr[2];
+                // HW_ID (hwreg 4: wave, simd, pipe, cu, sh, se) and XCC_ID (hwreg 20) bits 0..15
+                const unsigned long long hw = (unsigned)__builtin_amdgcn_s_getreg(4 | (15 << 11)) & 0xFFFFu;
+                const unsigned long long xcc = (unsigned)__builtin_amdgcn_s_getreg(20 | (15 << 11)) & 0xFu;
+                g[7] = tr[3] | (hw << 40) | (xcc << 56);
+            }
+#else
+            const float sum = block_stream_sum<Q>(rps, rlen, q.y, q.z, pts, s_mark, s_base[wid], s_soa, np,
+                                                       nullptr);
+#endif
+            store_comp_mean(out + 4 * (size_t)q.x, wid, sum, np);
+            if (threadIdx.x == 0) s_t = atomicAdd(qctr + 1, 1u);
+            __syncthreads();
+            const uint32_t d = s_t;
+            __syncthreads();  // (also: every wave is done with the block mode's LDS)
+            t = start0 + d;
+        }
+        // wave mode from slot t: wave 0 keeps it, the others draw
+        if (wid != 0) t = 0xFFFFFFFFu;
+    } else {
+        t = nb0 + (blockIdx.x - nb0) * 4u + wid;
+    }
+    // ---- wave mode ----
+    const uint32_t lane = threadIdx.x & 63;
+    int* wmark = s_mark + wid * 320u;
+    float* wsoa = s_soa_raw + wid * kWaveSoa;
+    wave_soa_init(wsoa);
+    while (true) {  // wave-uniform
+        if (t == 0xFFFFFFFFu) {
+            uint32_t d = 0;
+            if (lane == 0) d = atomicAdd(qctr + 1, 1u);
+            t = start0 + (uint32_t)__builtin_amdgcn_readfirstlane((int)d);
+        }
+        if (t >= nq) return;
         const uint4 q = bigq[slot_of(t)];
         uint32_t np = 0;
 #ifdef GDF_TRACE_GROUPS
-        unsigned long long tr[5] = {0, 0, 0, 0, 0};
         const unsigned long long w0 = wall_clock64(), c0 = clock64();
-        const float sum = block_stream_sum<Q>(rps, rlen, q.y, q.z, pts, s_mark, s_base[wid], s_soa, np, tr);
-        if (threadIdx.x == 128 && t < kTraceSlots) {  // (wave 2: z)
+#endif
+        const float sum = wave_stream_sum(rps, rlen, q.y, q.z, pts, wmark, s_base[wid], wsoa, np);
+        const uint32_t c = lane >> 4;
+        if ((lane & 15u) == 0) out[4 * (size_t)q.x + c] = c < 3 ? sum / (float)np : sum;
+#ifdef GDF_TRACE_GROUPS
+        if (lane == 0 && t < kTraceSlots) {
             unsigned long long* g = g_gtrace[t];
             g[0] = w0;
             g[1] = wall_clock64();
-            g[2] = ((unsigned long long)np << 32) | (unsigned)tr[4];
+            g[2] = ((unsigned long long)np << 32) | ((np + 255u) / 256u);
             g[3] = clock64() - c0;
-            g[4] = tr[0];
-            g[5] = tr[1];
-            g[6] = tr[2];
-            // HW_ID (hwreg 4: wave, simd, pipe, cu, sh, se) and XCC_ID (hwreg 20) bits 0..15
+            g[4] = g[5] = g[6] = 0;
             const unsigned long long hw = (unsigned)__builtin_amdgcn_s_getreg(4 | (15 << 11)) & 0xFFFFu;
             const unsigned long long xcc = (unsigned)__builtin_amdgcn_s_getreg(20 | (15 << 11)) & 0xFu;
-            g[7] = tr[3] | (hw << 40) | (xcc << 56);
+            g[7] = (hw << 40) | (xcc << 56);
         }
-#else
-        const float sum = block_stream_sum<Q>(rps, rlen, q.y, q.z, pts, s_mark, s_base[wid], s_soa, np,
-                                                   nullptr);
 #endif
-        store_comp_mean(out + 4 * (size_t)q.x, wid, sum, np);
-        if (nq <= gridDim.x) break;
-        if (threadIdx.x == 0) s_t = atomicAdd(qctr + 1, 1u);
-        __syncthreads();
-        const uint32_t d = s_t;
-        __syncthreads();
-        if (d >= nq - gridDim.x) break;
-        t = gridDim.x + d;
+        t = 0xFFFFFFFFu;
     }
 }
 
@@ -4991,11 +5149,11 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
             if (q16)
                 hipLaunchKernelGGL((k_group_runs_big<16>), dim3(big_blocks), dim3(256), 0, s,
                                    kbuf[sorted_passes & 1], vbuf[sorted_passes & 1], a.pts,
-                                   reinterpret_cast<float*>(a.out), a.bigq, a.bigq_cap, qctr);
+                                   reinterpret_cast<float*>(a.out), a.bigq, a.bigq_cap, qctr, g_run_wave_mode);
             else
                 hipLaunchKernelGGL((k_group_runs_big<8>), dim3(big_blocks), dim3(256), 0, s,
                                    kbuf[sorted_passes & 1], vbuf[sorted_passes & 1], a.pts,
-                                   reinterpret_cast<float*>(a.out), a.bigq, a.bigq_cap, qctr);
+                                   reinterpret_cast<float*>(a.out), a.bigq, a.bigq_cap, qctr, g_run_wave_mode);
         }
         if ((e = hipGetLastError()) != hipSuccess) return e;
         return a.grid8 && a.grid_last ? launch_grid_apart(a, s) : hipSuccess;

@@ -7,6 +7,8 @@
 
 Bar as in test_gpu_parity.py: bit-exact.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -148,12 +150,24 @@ def test_voxel_sums_adversarial_points_mode(Engine, xruns):
         assert ok.all(), (g, len(t), got[out_i], want)
 
 
-def test_voxel_sums_adversarial_run_mode(Engine):
+@pytest.mark.parametrize("wave_mode", [None, "2"])
+def test_voxel_sums_adversarial_run_mode(Engine, wave_mode):
     """The rollbuffer path (run mode: k_sel runs -> run sort -> k_group_runs staged sums and
     k_group_runs_big streams) on point sequences whose voxels hold adversarial values: z on a
     2^-12 grid around 0 (random walks through zero, exact cancellation), subnormal x, ties from
     one-binade-below terms, long runs of one voxel (> 100 K points) - identity move transforms,
-    bit-exact vs the oracle (points, keys, means, grid)."""
+    bit-exact vs the oracle (points, keys, means, grid).  GDF_RUN_WAVE_MODE=2: every queued
+    group below the huge region summed by one wave (wave_stream_sum) however short the queue."""
+    if wave_mode is not None:
+        os.environ["GDF_RUN_WAVE_MODE"] = wave_mode
+    try:
+        _adversarial_run_mode(Engine)
+    finally:
+        os.environ.pop("GDF_RUN_WAVE_MODE", None)
+        Engine().close()  # (the knob is process-wide: an engine created without it resets it)
+
+
+def _adversarial_run_mode(Engine):
     p = ComponentParams()
     p.ps_timespan = 2.5 / 30.0
     p.ps_filter_size = 0  # keep every point (the filter's own parity is tested elsewhere)

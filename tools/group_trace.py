@@ -93,6 +93,9 @@ def main():
         print(f"{slots[i]:5d} {npts[i]:6d} {chunks[i]:5d} {(w0[i] - t0) / 100:8.1f} {(w1[i] - t0) / 100:7.1f} "
               f"{tot[i]:7d} {bar[i]:7d} {sto[i]:7d} {fet[i]:6d} {sm[i]:6d} {tot[i] / max(chunks[i], 1):8.0f} "
               f" {xcc[i]} {(hw[i] >> 8) & 15} {(hw[i] >> 4) & 3}")
+    wave = (bar == 0) & (sto == 0) & (fet == 0)
+    print(f"block-mode groups {int((~wave).sum())} ({int(npts[~wave].sum())} points), wave-mode groups "
+          f"{int(wave.sum())} ({int(npts[wave].sum())} points)")
     cyc = tot.sum()
     print(f"all groups: cycles {cyc}  barrier {bar.sum() / cyc:.2f}  stores {sto.sum() / cyc:.2f}  "
           f"fetch {fet.sum() / cyc:.2f}  sum {sm.sum() / cyc:.2f}  per chunk {cyc / chunks.sum():.0f}")
