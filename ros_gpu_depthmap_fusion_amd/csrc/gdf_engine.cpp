@@ -2039,6 +2039,8 @@ int gdf_create(int device, gdf_engine** out) {
         {  // tuning knob (process-wide; every engine creation sets it, default 1)
             const char* v = std::getenv("GDF_RUN_WAVE_MODE");
             g_run_wave_mode = v ? (uint32_t)std::atoi(v) : 1u;
+            const char* o = std::getenv("GDF_RUN_BIG_OCC4");
+            g_run_big_occ4 = o ? (uint32_t)std::atoi(o) : 0u;
         }
         if (const char* v = std::getenv("GDF_RUN_BIG_BLOCKS"))  // tuning knob
             g_run_big_blocks = (uint32_t)std::max(1, std::atoi(v));

@@ -4116,6 +4116,7 @@ uint32_t g_run_q16 = 2;
 // queue is long (1); tuning knob GDF_RUN_WAVE_MODE=0: every group in block mode, 2: wave mode
 // whatever the queue's length
 uint32_t g_run_wave_mode = 1;
+uint32_t g_run_big_occ4 = 0;  // tuning knob GDF_RUN_BIG_OCC4 (k_group_runs_big at 4 waves per SIMD)
 
 
 // Wave64 inclusive sum scan on DPP (gdf_voxsum.hpp dpp_iscan).
@@ -4799,8 +4800,10 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
 // draws further slots (qctr[1]) while any remain and streams the runs of each (records rps / rlen by sorted run, written by k_group_runs) from global memory
 // (block_stream_sum).  The queue was complete when this launch began; the first sort pass of the
 // next voxelize zeroes the counters.
-template <int Q>
-__global__ __launch_bounds__(256) void k_group_runs_big(const uint32_t* __restrict__ rps,
+// OCC4: compiled for 4 waves per SIMD (128 VGPRs, ~40 of them spilled; tuning knob
+// GDF_RUN_BIG_OCC4), else 3 (167 VGPRs)
+template <int Q, bool OCC4 = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC4 ? 4 : 1, 8))) void k_group_runs_big(const uint32_t* __restrict__ rps,
                                                        const uint32_t* __restrict__ rlen,
                                                        const float4* __restrict__ pts,
                                                        float* __restrict__ out,
@@ -4991,19 +4994,21 @@ static hipError_t launch_grid_apart(const VoxelizeArgs& a, hipStream_t s) {
 // Blocks of k_group_runs_big<8> / <16> the current device holds at once, cached per device (an
 // engine is bound to one device, but a process may drive several; the value is computed once per
 // device and kernel variant, races only recompute the same number)
-static uint32_t resident_big_blocks(bool q16) {
+static uint32_t resident_big_blocks(bool q16, bool occ4) {
     constexpr int kDev = 64;
-    static std::atomic<uint32_t> cache[kDev][2];
+    static std::atomic<uint32_t> cache[kDev][4];
     int dev = 0;
     (void)hipGetDevice(&dev);
-    std::atomic<uint32_t>* slot = dev >= 0 && dev < kDev ? &cache[dev][q16 ? 1 : 0] : nullptr;
+    std::atomic<uint32_t>* slot = dev >= 0 && dev < kDev ? &cache[dev][(q16 ? 1 : 0) + (occ4 ? 2 : 0)] : nullptr;
     uint32_t rb = slot ? slot->load(std::memory_order_relaxed) : 0u;
     if (rb) return rb;
     int per_cu = 0, cus = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, q16 ? reinterpret_cast<const void*>(&k_group_runs_big<16>)
-                     : reinterpret_cast<const void*>(&k_group_runs_big<8>), 256, 0);
+        &per_cu, occ4 ? (q16 ? reinterpret_cast<const void*>(&k_group_runs_big<16, true>)
+                             : reinterpret_cast<const void*>(&k_group_runs_big<8, true>))
+                      : (q16 ? reinterpret_cast<const void*>(&k_group_runs_big<16>)
+                             : reinterpret_cast<const void*>(&k_group_runs_big<8>)), 256, 0);
     // (the API can report one block per CU too many, MI355X_MICROARCH.md)
     rb = per_cu > 1 && cus > 0 ? (uint32_t)((per_cu - 1) * cus) : 256u;
     if (slot) slot->store(rb, std::memory_order_relaxed);
@@ -5144,16 +5149,14 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
             if ((e = hipGetLastError()) != hipSuccess) return e;
             const bool q16 = g_run_q16 == 1 ||
                              (g_run_q16 == 2 && a.nframes <= 1);
-            const uint32_t rb = resident_big_blocks(q16);
+            const bool occ4 = g_run_big_occ4 != 0;
+            const uint32_t rb = resident_big_blocks(q16, occ4);
             const uint32_t big_blocks = std::min(g_run_big_blocks, rb);
-            if (q16)
-                hipLaunchKernelGGL((k_group_runs_big<16>), dim3(big_blocks), dim3(256), 0, s,
-                                   kbuf[sorted_passes & 1], vbuf[sorted_passes & 1], a.pts,
-                                   reinterpret_cast<float*>(a.out), a.bigq, a.bigq_cap, qctr, g_run_wave_mode);
-            else
-                hipLaunchKernelGGL((k_group_runs_big<8>), dim3(big_blocks), dim3(256), 0, s,
-                                   kbuf[sorted_passes & 1], vbuf[sorted_passes & 1], a.pts,
-                                   reinterpret_cast<float*>(a.out), a.bigq, a.bigq_cap, qctr, g_run_wave_mode);
+            auto kb = occ4 ? (q16 ? k_group_runs_big<16, true> : k_group_runs_big<8, true>)
+                           : (q16 ? k_group_runs_big<16, false> : k_group_runs_big<8, false>);
+            hipLaunchKernelGGL(kb, dim3(big_blocks), dim3(256), 0, s, kbuf[sorted_passes & 1],
+                               vbuf[sorted_passes & 1], a.pts, reinterpret_cast<float*>(a.out), a.bigq,
+                               a.bigq_cap, qctr, g_run_wave_mode);
         }
         if ((e = hipGetLastError()) != hipSuccess) return e;
         return a.grid8 && a.grid_last ? launch_grid_apart(a, s) : hipSuccess;

@@ -193,7 +193,7 @@ constexpr uint32_t kFrameSortResident = 16384;
 extern uint32_t g_group_scan_tiles;
 // k_group_runs staging (512 or 2048 points) and in-block group size limit
 extern uint32_t g_run_stage, g_run_inblock, g_run_big_blocks, g_run_q16, g_small_group, g_run_wave, g_points_lane;
-extern uint32_t g_run_wave_mode;
+extern uint32_t g_run_wave_mode, g_run_big_occ4;
 extern uint32_t g_sort_blocks, g_group_blocks;
 size_t voxelize_group_tiles(uint32_t nmax);
 
