@@ -426,7 +426,9 @@ int gdf_set_emit_partition(gdf_engine* engine, uint32_t nparts, float* send_poin
  * selected rollbuffer points] (bucket b = part * 2 + segment, bucket-major send lists, run starts
  * relative to the bucket's first point, part_counts [2 nparts points | 2 nparts runs]): the
  * multi-GPU step places the rollbuffer segments of the ranks behind every rank's depth points
- * (the reference's buffer order, fusion.cpp:1509-1581).  Disarmed (1) with the emit partition. */
+ * (the reference's buffer order, fusion.cpp:1509-1581).  A frame without a selection keeps this
+ * layout with every segment-1 bucket empty (the compaction writes the counts so).  Disarmed (1)
+ * with the emit partition. */
 int gdf_set_partition_segments(gdf_engine* engine, uint32_t nseg);
 /* Whether a deferred frame armed with gdf_set_emit_partition sets its occupancy marks (default 1).
  * 0: a caller that builds the union from gdf_voxelize_runs_marked skips the compaction's marks

@@ -200,6 +200,9 @@ struct FrameArgs {
     uint32_t* part_run_keys;
     uint32_t* part_run_starts;
     uint32_t* part_counts;      // [2 * nparts]: points, then runs per part (device)
+    // 2: the counts in the 2-segment layout [points of (part p, segment s) at 2 p + s | runs at
+    // 2 P + 2 p + s] with segment 1 (a selection's rollbuffer points) empty - a frame without one
+    uint32_t part_nseg;
 };
 static_assert(sizeof(FrameArgs) <= 4096, "kernel arguments are limited to 4 KiB");
 

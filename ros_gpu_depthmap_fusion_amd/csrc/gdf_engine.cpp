@@ -1469,8 +1469,10 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel, bool compaction_marks = fa
     a.frame_shift = e->nframes > 1 ? e->key_bits : 0u;
     a.mark_words = mark_words(e);
     e->sl().sel_frame = a.sel_tiles != 0;  // (the partition pass's [depth | rollbuffer] split)
+    // (2 segments: a frame without a selection has no rollbuffer segment - the counts take the
+    // 2-segment layout, segment 1 empty)
     if (fused_voxel && compaction_marks && e->epart.nparts && e->emit_part && !a.sel_tiles &&
-        e->epart.nseg == 1 && a.total_segs && !e->debug) {
+        a.total_segs && !e->debug) {
         // the compaction writes the key-range partition itself (k_mask_px + k_emit_px2 only;
         // anything else compacts, then partitions: gdf_process_frame)
         FrameArgs t = a;
@@ -1494,6 +1496,7 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel, bool compaction_marks = fa
             t.part_run_keys = e->epart.run_keys;
             t.part_run_starts = e->epart.run_starts;
             t.part_counts = e->epart.counts;
+            t.part_nseg = e->epart.nseg;
             a = t;
         }
     }

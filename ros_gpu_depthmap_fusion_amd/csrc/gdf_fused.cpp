@@ -376,8 +376,7 @@ struct SlotX {
     // partitioned send lists (points, run keys, run starts) in buckets b = 2 part + segment
     // (segment 0: the rank's depth points, 1: its selected rollbuffer points); the split sizes
     // record [points per bucket (2 W) | runs per bucket (2 W)] (cnt), every rank's (cntall), and
-    // the engine's own one-segment counts [points per part | runs per part] (cnt1)
-    DevBuf sp, srk, srs, cnt, cnt1, cntall;
+    DevBuf sp, srk, srs, cnt, cntall;
     DevBuf rp, rrk, rrs;      // received lists
     uint32_t* host = nullptr;  // pinned copy of cntall (world x 4 world)
     uint32_t order[16] = {};   // the ranks' rollbuffer segments in the selection's order
@@ -408,7 +407,7 @@ struct gdf_fused {
         }
         for (SlotX& s : slots) {
             for (DevBuf* b : {&s.tail, &s.tails, &s.gathered, &s.sp, &s.srk, &s.srs,
-                              &s.cnt, &s.cnt1, &s.cntall, &s.rp, &s.rrk, &s.rrs})
+                              &s.cnt, &s.cntall, &s.rp, &s.rrk, &s.rrs})
                 b->release();
             if (s.host) hipHostFree(s.host);
             if (s.ev) hipEventDestroy(s.ev);
@@ -483,7 +482,6 @@ void fused_start(gdf_fused* f, const uint16_t* const* depth, uint32_t B, const g
     // the send lists, written by the compaction itself (gdf_set_emit_partition): sized for the
     // step's pixels (+ halo) plus, on a rollbuffer rank, every point the window can select
     uint32_t* cnt = S.cnt.ensure<uint32_t>((size_t)4 * W * 4, st);
-    uint32_t* cnt1 = S.cnt1.ensure<uint32_t>((size_t)2 * W * 4, st);
     uint32_t* cntall = S.cntall.ensure<uint32_t>((size_t)4 * W * W * 4, st);
     size_t want = (size_t)B * c.width * c.height + (halo && R > 0 ? B * (size_t)f->Lmax : 0u);
     if (rb) {  // + the window after the ingest
@@ -499,19 +497,15 @@ void fused_start(gdf_fused* f, const uint16_t* const* depth, uint32_t B, const g
         S.srs.ensure<uint32_t>(cap * 4, st);
         const uint32_t have = (uint32_t)std::min<size_t>({S.sp.cap / 16, S.srk.cap / 4, S.srs.cap / 4});
         gdfchk(gdf_set_emit_partition(e, W, S.sp.as<float>(), S.srk.as<uint32_t>(),
-                                      S.srs.as<uint32_t>(), have, rb ? cnt : cnt1));
-        // a rollbuffer frame: buckets [depth | rollbuffer] per part, the record's layout itself
-        if (rb) gdfchk(gdf_set_partition_segments(e, 2));
+                                      S.srs.as<uint32_t>(), have, cnt));
+        // buckets [depth | rollbuffer] per part: the record's layout itself (a frame without a
+        // selection: segment 1 empty, written by the compaction)
+        gdfchk(gdf_set_partition_segments(e, 2));
     };
     arm(std::max<size_t>(want, 1));
     gdfchk(gdf_set_partition_marks(e, 0));
     gdf_frame_result res{};
     gdfchk(gdf_process_frame(e, &q, &res));
-    if (!rb) {  // [points per part | runs per part] -> the record's even (segment 0) buckets
-        hipchk(hipMemsetAsync(cnt, 0, (size_t)4 * W * 4, st), "hipMemsetAsync(record)");
-        hipchk(hipMemcpy2DAsync(cnt, 8, cnt1, 4, 4, (size_t)2 * W, hipMemcpyDeviceToDevice, st),
-               "hipMemcpy2DAsync(record)");
-    }
     // the ranks' rollbuffer segments in the selection's order (the same on every rank: the
     // headers are replicated); unsharded, only the last rank's is non-empty
     for (int k = 0; k < W; ++k) S.order[k] = (uint32_t)k;
@@ -635,7 +629,10 @@ void fused_finish(gdf_fused* f, int slot, uint32_t* send_counts, uint32_t* recv_
     const uint64_t Sw = (words + W - 1) / W;  // = part_slice_words(W, ncells), the partition's rule
     const uint64_t stride = Sw * W;
     uint32_t* uni = S.gathered.ensure<uint32_t>(S.nframes * stride * 4, st);
-    hipchk(hipMemsetAsync(uni, 0, S.nframes * stride * 4, st), "hipMemsetAsync(marks)");
+    // (only slice R of each frame: the voxelize marks inside its key range, the all-gather
+    // overwrites the other slices)
+    hipchk(hipMemset2DAsync(uni + (uint64_t)R * Sw, stride * 4, 0, Sw * 4, S.nframes, st),
+           "hipMemset2DAsync(marks)");
     gdfchk(gdf_voxelize_runs_marked(e, rp, rrk, rrs, (uint32_t)NS, pbase, rbase, S.average, uni, stride));
     if (W > 1) {  // (on the points' communicator: the finish's collectives stay in step order,
                   // never behind the next step's start collectives on the halo communicator)

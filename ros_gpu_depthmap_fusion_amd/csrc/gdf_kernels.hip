@@ -1838,7 +1838,12 @@ __device__ __forceinline__ void emit_px2_parts(const FrameArgs& a, uint32_t* s_m
         const uint32_t a0 = G(a.seg_offsets)[(size_t)threadIdx.x * TS];
         const uint32_t a1 = threadIdx.x + 1 < 2u * P ? G(a.seg_offsets)[(size_t)(threadIdx.x + 1) * TS]
                                                      : *G(a.scan_total);
-        G(a.part_counts)[kind * P + p] = a1 - a0;
+        if (a.part_nseg == 2u) {  // (the 2-segment record: this frame has no segment 1)
+            G(a.part_counts)[(kind * P + p) * 2u] = a1 - a0;
+            G(a.part_counts)[(kind * P + p) * 2u + 1u] = 0u;
+        } else {
+            G(a.part_counts)[kind * P + p] = a1 - a0;
+        }
         if (threadIdx.x == 0) *G(a.out_count) = s_tot;
     }
 }
