@@ -112,6 +112,7 @@ struct FrameArgs {
     uint32_t depth_total;       // ΣP of emitting cameras' index space
     uint32_t depth_segs;        // segments over the depth pixels
     uint32_t total_segs;        // segments of the two-pass (depth) compaction: depth_segs
+    uint32_t mask_pairs;        // row pairs of those segments (k_mask_px2r: one workgroup each)
     // flying-pixel filter (sh/filter_flying_pixels.glsl)
     int32_t do_flying;
     uint32_t F;

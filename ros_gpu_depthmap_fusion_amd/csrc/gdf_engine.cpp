@@ -1318,6 +1318,8 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel, bool compaction_marks = fa
     // one item per thread: blocks as wide as the widest segment
     a.seg_threads = e->max_segw ? std::max<uint32_t>(64, e->max_segw) : kSegItems;
     a.total_segs = a.depth_segs;
+    for (const CamDesc& c : e->h_cams)  // (seg_geo_pair's count: rows 2t, 2t + 1 per chunk)
+        if (c.emit) a.mask_pairs += ((c.H + 1u) / 2u) * c.nchunk;
     // k_sel tiles: 4 K points; 16 K for windows over 16 Mi points, whose ~10^4..10^5 tiles would
     // otherwise queue on the one ticket counter (measured on MI355X, C3's 236 M-point window:
     // 57.6 K tiles 2.92 ms, 14.4 K tiles 2.11 ms per frame)
@@ -2033,6 +2035,10 @@ int gdf_create(int device, gdf_engine** out) {
             g_emit_px2 = (uint32_t)std::atoi(v);
         if (const char* v = std::getenv("GDF_MASK_OCC8"))  // tuning knob
             g_mask_occ8 = (uint32_t)std::atoi(v);
+        {  // tuning knob (process-wide, set at every engine creation; default 1)
+            const char* v = std::getenv("GDF_MASK_ROWS");
+            g_mask_rows = v ? (uint32_t)std::atoi(v) : 1u;
+        }
         if (const char* v = std::getenv("GDF_GRID_WPT"))  // tuning knob: 1..8
             g_grid_wpt = (uint32_t)std::min(8, std::max(1, std::atoi(v)));
         if (const char* v = std::getenv("GDF_MASK_PX"))  // tuning knob: pixels per k_mask thread

@@ -412,6 +412,43 @@ __device__ __forceinline__ SegGeo seg_geo(P cams, int ncams, uint32_t s) {
     return g;
 }
 
+// Row pair q of the emitting cameras (k_mask_px ROWS = 2): camera k's pairs are rows (2 t, 2 t + 1)
+// of each column chunk, ((H + 1) / 2) * nchunk of them, cameras in table order.  s0 = the pair's
+// first segment, nrow = 2 unless the camera's last row is alone.
+struct SegGeo2 {
+    SegGeo g;
+    uint32_t s0, nrow, nchunk;
+};
+
+template <class P>
+__device__ __forceinline__ SegGeo2 seg_geo_pair(P cams, int ncams, uint32_t q) {
+    SegGeo2 r;
+    uint32_t p0 = 0, k = 0, pk = 0;
+    for (int c = 0; c < ncams; ++c) {
+        if (!cams[c].emit) continue;
+        const uint32_t np = ((cams[c].H + 1u) / 2u) * cams[c].nchunk;
+        if (q >= p0 && q < p0 + np) {
+            k = (uint32_t)c;
+            pk = p0;
+        }
+        p0 += np;
+    }
+    k = __builtin_amdgcn_readfirstlane(k);
+    pk = __builtin_amdgcn_readfirstlane(pk);
+    const uint32_t nchunk = cams[k].nchunk, segw = cams[k].segw, W = cams[k].W;
+    const uint32_t i = q - pk;
+    const uint32_t t = i / nchunk, j = i - t * nchunk;
+    r.g.k = (int)k;
+    r.g.y = 2u * t;
+    r.g.x0 = j * segw;
+    r.g.len = min(segw, W - r.g.x0);
+    r.g.item0 = (uint32_t)cams[k].off + r.g.y * W + r.g.x0;
+    r.s0 = cams[k].seg0 + r.g.y * nchunk + j;
+    r.nrow = r.g.y + 1u < cams[k].H ? 2u : 1u;
+    r.nchunk = nchunk;
+    return r;
+}
+
 struct Band {
     const uint8_t* b;   // LDS band (bytes)
     const float* xn;    // LDS xn of columns ca..cb-1 (index x - ca)
@@ -1180,30 +1217,40 @@ __device__ __forceinline__ unsigned long long part_lanes(unsigned long long m, b
 // k_mask with PX pixels per thread (x + j * 256 / PX) for 256-pixel segments at F = 4 without
 // rot45: 256 / PX threads per segment, the same band in LDS, the same outputs (validity word
 // w + j * waves from pixel j of wave w; counts, runs, run-key histogram).  No debug stage bits
-// (the engine launches k_mask for those).
-template <int PX, int SEGW>
+// (the engine launches k_mask for those).  ROWS = 2: a block takes the segments of two adjacent
+// rows (same camera and columns: pair t of a camera = rows 2t, 2t + 1) on one band of 2h + 2
+// rows - 5 staged rows per segment instead of 9, and the segment's fixed work (its camera and
+// geometry, the band's loads and barrier) once per two; the waves of row r run as the 1-row
+// kernel's (their band seen from row r: rowoff / yn shifted by r).
+template <int PX, int SEGW, int ROWS = 1>
 __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
-    constexpr int NT = SEGW / PX, NW = NT / 64;          // threads, waves
+    constexpr int NT = SEGW / PX, NW = NT / 64;          // threads, waves (per row)
+    constexpr int NTB = NT * ROWS, NWB = NW * ROWS;      // (per block)
     constexpr int NWORDS = SEGW / 64;                    // validity words of a segment
-    constexpr int QR = (2 * 4 + 1 + NW - 1) / NW;        // band rows per wave (h = 4)
-    constexpr int QX = (SEGW + 2 * 4 + NT - 1) / NT;     // ray factors per thread
+    constexpr int NBR = 2 * 4 + ROWS;                    // band rows (h = 4)
+    constexpr int QR = (NBR + NWB - 1) / NWB;            // band rows per wave
+    constexpr int QX = (SEGW + 2 * 4 + NTB - 1) / NTB;   // ray factors per thread
     constexpr int QC = (((SEGW + 8) * 2 + 15) / 16 + 1 + 63) / 64;  // 16-B chunks per lane and row
     // the segment's camera only (occupancy: 16 descriptors were 3.3 KB of LDS per block; the first
     // rows' general path reads the others from the argument table)
     __shared__ CamDesc s_cams[1];
-    __shared__ float s_yn[2 * kHalo + 1];
-    __shared__ int s_rowoff[2 * kHalo + 1];
-    __shared__ uint32_t s_cnt[NWORDS];
-    __shared__ uint32_t s_rcnt[NWORDS];
-    __shared__ uint32_t s_pc[2][NWORDS][kMaxParts];  // emit partition: points, runs per (word, part)
+    __shared__ float s_yn[2 * kHalo + ROWS];
+    __shared__ int s_rowoff[2 * kHalo + ROWS];
+    __shared__ uint32_t s_cnt[ROWS][NWORDS];
+    __shared__ uint32_t s_rcnt[ROWS][NWORDS];
+    __shared__ uint32_t s_pc[ROWS][2][NWORDS][kMaxParts];  // emit partition: points, runs per (word, part)
     extern __shared__ uint4 s_dyn[];
     // run-key digit histogram: dynamic LDS behind the band, only when the launch counts digits
-    uint32_t* s_hist = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(s_dyn) + a.hist_lds);
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    // (ROWS = 2: one band row more, the launch adds it)
+    uint32_t* s_hist = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(s_dyn) + a.hist_lds +
+                                                   (ROWS - 1) * a.band_rowb);
+    const int lane = threadIdx.x & 63, wall = threadIdx.x >> 6;
+    const int row = ROWS == 1 ? 0 : wall / NW, wid = ROWS == 1 ? wall : wall % NW;
     if (a.nparts)
-        for (uint32_t j = threadIdx.x; j < 2u * NWORDS * kMaxParts; j += NT) (&s_pc[0][0][0])[j] = 0u;
+        for (uint32_t j = threadIdx.x; j < (uint32_t)ROWS * 2u * NWORDS * kMaxParts; j += NTB)
+            (&s_pc[0][0][0][0])[j] = 0u;
     const uint32_t n = gridDim.x, q8 = n / 8, r8 = n % 8, xcd = blockIdx.x % 8;
-    const uint32_t s = xcd * q8 + min(xcd, r8) + blockIdx.x / 8;
+    const uint32_t s_blk = xcd * q8 + min(xcd, r8) + blockIdx.x / 8;  // segment, or row pair
     if (a.grid_seq_out && blockIdx.x == 0 && threadIdx.x == 0) *a.grid_seq_out = a.grid_seq;
     uint32_t bits[PX], rkey[PX];
 #pragma unroll
@@ -1211,12 +1258,21 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
         bits[j] = 0u;
         rkey[j] = 0xFFFFFFFFu;
     }
-    const uint32_t i = threadIdx.x;
+    const uint32_t i = ROWS == 1 ? threadIdx.x : threadIdx.x % NT;  // (thread of the row)
     if (a.run_mode && a.key_hist)
-        for (uint32_t j = threadIdx.x; j < radix_hist_span(a.npasses); j += NT) s_hist[j] = 0;
+        for (uint32_t j = threadIdx.x; j < radix_hist_span(a.npasses); j += NTB) s_hist[j] = 0;
+    uint32_t s = s_blk, nrow = 1;  // this wave's segment; rows of the block
     {
         const gptr<const CamDesc> gcam = G(cam_table(a));
-        const SegGeo sg = seg_geo(gcam, a.ncams, s);
+        SegGeo sg;
+        if constexpr (ROWS == 1) {
+            sg = seg_geo(gcam, a.ncams, s);
+        } else {
+            const SegGeo2 g2 = seg_geo_pair(gcam, a.ncams, s_blk);
+            sg = g2.g;
+            nrow = g2.nrow;
+            s = g2.s0 + (uint32_t)row * g2.nchunk;
+        }
         struct {
             const uint16_t* depth;
             const float *xn, *yn;
@@ -1225,28 +1281,30 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
         const int h = 4;  // (F = 4: the launch checks it)
         const uint32_t ca = sg.x0 >= (uint32_t)h ? sg.x0 - h : 0u;
         const uint32_t cb = min(c.W, sg.x0 + sg.len + h);
-        const uint32_t nrows = 2 * h + 1;
+        const uint32_t nrows = 2 * h + ROWS;
         uint8_t* band = reinterpret_cast<uint8_t*>(s_dyn);
         float* s_xn = reinterpret_cast<float*>(band + (size_t)nrows * a.band_rowb) + kHalo;
         const bool wrap = sg.x0 == 0 && sg.y >= (uint32_t)h && c.W >= (uint32_t)h;
         typedef uint32_t u4v __attribute__((ext_vector_type(4)));
         const uintptr_t dbase = reinterpret_cast<uintptr_t>(c.depth);
         const uint32_t nch = a.band_rowb / 16;  // <= 64 QC (the launch checks it)
-        // rows wid, wid + NW, ...: every load before any store
+        // rows wall, wall + NWB, ...: every load before any store
         u4v v[QR][QC];
         uintptr_t a16[QR], col0[QR];
         uint32_t n16[QR];
         bool rok[QR];
 #pragma unroll
         for (int q = 0; q < QR; ++q) {
-            const uint32_t r = (uint32_t)wid + (uint32_t)NW * q;
+            const uint32_t r = (uint32_t)wall + (uint32_t)NWB * q;
             const int gy = (int)sg.y - h + (int)r;
             rok[q] = r < nrows && gy >= 0 && gy < (int)c.H;
             n16[q] = 0;
             a16[q] = col0[q] = 0;
             if (rok[q]) {
                 col0[q] = dbase + 2 * ((uintptr_t)gy * c.W + ca);
-                const uintptr_t first = col0[q] - (wrap && r == (uint32_t)h ? 2 * (uintptr_t)h : 0);
+                // (a pixel row of a row-start segment: the previous row's end before column 0)
+                const bool pix_row = r >= (uint32_t)h && r < (uint32_t)(h + ROWS);
+                const uintptr_t first = col0[q] - (wrap && pix_row ? 2 * (uintptr_t)h : 0);
                 const uintptr_t last = dbase + 2 * ((uintptr_t)gy * c.W + cb);
                 a16[q] = first & ~(uintptr_t)15;
                 n16[q] = min((uint32_t)((last - a16[q] + 15) / 16), nch);
@@ -1257,24 +1315,25 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
                 }
             }
         }
+        const uint32_t tb = threadIdx.x;  // (thread of the block)
         float xv[QX];
 #pragma unroll
         for (int q = 0; q < QX; ++q)
-            xv[q] = ca + i + (uint32_t)NT * q < cb ? G(c.xn)[ca + i + (uint32_t)NT * q] : 0.0f;
-        if (i < nrows) {
-            const int gyi = (int)sg.y - h + (int)i;
-            s_yn[i] = (gyi >= 0 && gyi < (int)c.H) ? G(c.yn)[gyi] : 0.0f;
+            xv[q] = ca + tb + (uint32_t)NTB * q < cb ? G(c.xn)[ca + tb + (uint32_t)NTB * q] : 0.0f;
+        if (tb < nrows) {
+            const int gyi = (int)sg.y - h + (int)tb;
+            s_yn[tb] = (gyi >= 0 && gyi < (int)c.H) ? G(c.yn)[gyi] : 0.0f;
         }
         float xwv = 0.0f;
-        if (wrap && i < (uint32_t)h) xwv = G(c.xn)[c.W - 1 - i];
+        if (wrap && tb < (uint32_t)h) xwv = G(c.xn)[c.W - 1 - tb];
         {  // camera sg.k's descriptor into LDS
             const uint32_t* src = reinterpret_cast<const uint32_t*>(cam_table(a) + sg.k);
             uint32_t* dst = reinterpret_cast<uint32_t*>(s_cams);
-            for (uint32_t w = threadIdx.x; w < (uint32_t)(sizeof(CamDesc) / 4); w += NT) dst[w] = G(src)[w];
+            for (uint32_t w = threadIdx.x; w < (uint32_t)(sizeof(CamDesc) / 4); w += NTB) dst[w] = G(src)[w];
         }
 #pragma unroll
         for (int q = 0; q < QR; ++q) {
-            const uint32_t r = (uint32_t)wid + (uint32_t)NW * q;
+            const uint32_t r = (uint32_t)wall + (uint32_t)NWB * q;
             if (r < nrows) {
 #pragma unroll
                 for (int cq = 0; cq < QC; ++cq) {
@@ -1288,11 +1347,14 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
         }
 #pragma unroll
         for (int q = 0; q < QX; ++q)
-            if (ca + i + (uint32_t)NT * q < cb) s_xn[i + (uint32_t)NT * q] = xv[q];
-        if (wrap && i < (uint32_t)h) s_xn[-1 - (int)i] = xwv;
+            if (ca + tb + (uint32_t)NTB * q < cb) s_xn[tb + (uint32_t)NTB * q] = xv[q];
+        if (wrap && tb < (uint32_t)h) s_xn[-1 - (int)tb] = xwv;
         __syncthreads();
-        const Band t{band, s_xn, s_rowoff, ca, h};
-        if (64u * (uint32_t)wid < sg.len) {  // wave-uniform
+        // (row r's waves: the band from their own pixel row, h rows above it)
+        const Band t{band, s_xn, s_rowoff + row, ca, h};
+        const float* s_ynr = s_yn + row;
+        sg.y += (uint32_t)row;
+        if ((uint32_t)row < nrow && 64u * (uint32_t)wid < sg.len) {  // wave-uniform
             const uint32_t xw0 = sg.x0 + 64u * wid;
             uint32_t x[PX];
             bool in[PX];
@@ -1302,22 +1364,22 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
                 in[j] = i + (uint32_t)NT * j < sg.len;
             }
             if (PX == 2 && a.mask_packed && sg.y >= 4u && xw0 >= 4u)
-                depth_bits_px2<kInterior>(a, s_cams, 0, t, s_yn, x, sg.y, in, bits);
+                depth_bits_px2<kInterior>(a, s_cams, 0, t, s_ynr, x, sg.y, in, bits);
             else if (PX == 2 && a.mask_packed && wrap)
-                depth_bits_px2<kRowStart>(a, s_cams, 0, t, s_yn, x, sg.y, in, bits);
+                depth_bits_px2<kRowStart>(a, s_cams, 0, t, s_ynr, x, sg.y, in, bits);
             else if (sg.y >= 4u && xw0 >= 4u)
-                depth_bits_px<kInterior, PX>(a, s_cams, 0, t, s_yn, x, sg.y, in, bits);
+                depth_bits_px<kInterior, PX>(a, s_cams, 0, t, s_ynr, x, sg.y, in, bits);
             else if (wrap)
-                depth_bits_px<kRowStart, PX>(a, s_cams, 0, t, s_yn, x, sg.y, in, bits);
+                depth_bits_px<kRowStart, PX>(a, s_cams, 0, t, s_ynr, x, sg.y, in, bits);
             else
 #pragma unroll
                 for (int j = 0; j < PX; ++j)
-                    bits[j] = depth_bits<false, kGeneral, 4>(a, reinterpret_cast<const CamDesc*>(cam_table(a)), sg.k, t, s_yn, x[j], sg.y, in[j]);
+                    bits[j] = depth_bits<false, kGeneral, 4>(a, reinterpret_cast<const CamDesc*>(cam_table(a)), sg.k, t, s_ynr, x[j], sg.y, in[j]);
             if (a.run_mode && PX == 2 && a.mask_packed) {  // both pixels' keys in packed f32
                 const CamDesc& cd = s_cams[0];
                 if ((bits[0] | bits[PX - 1]) & 4u) {
                     const P3x2 p = band_pt2(t, h, (int)x[0], h, (int)x[PX - 1],
-                                            f2(s_yn[h], s_yn[h]), cd.scale);
+                                            f2(s_ynr[h], s_ynr[h]), cd.scale);
                     uint32_t k0, k1;
                     voxel_key2(mrow2(cd.Tw + 0, p.x, p.y, p.z), mrow2(cd.Tw + 4, p.x, p.y, p.z),
                                mrow2(cd.Tw + 8, p.x, p.y, p.z), a.vlo, a.vcs, a.vrcs, a.gmax, a.gs,
@@ -1330,7 +1392,7 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
 #pragma unroll
                 for (int j = 0; j < PX; ++j)
                     if (bits[j] & 4u) {  // the voxel key k_emit will compute (same f32 ops)
-                        const P3 p = band_pt(t, h, x[j], s_yn[h], cd.scale);
+                        const P3 p = band_pt(t, h, x[j], s_ynr[h], cd.scale);
                         const float wx = mrow(cd.Tw + 0, p.x, p.y, p.z, 1.0f);
                         const float wy = mrow(cd.Tw + 4, p.x, p.y, p.z, 1.0f);
                         const float wz = mrow(cd.Tw + 8, p.x, p.y, p.z, 1.0f);
@@ -1340,13 +1402,14 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
             }
         }
     }
+    const bool live_row = (uint32_t)row < nrow;  // (a pair's missing second row: no outputs)
 #pragma unroll
     for (int j = 0; j < PX; ++j) {
         const uint32_t word = (uint32_t)wid + (uint32_t)NW * j;
         const unsigned long long m = __ballot((bits[j] & 4u) != 0u);
-        if (lane == 0) {
+        if (lane == 0 && live_row) {
             G(a.vbits)[(size_t)s * 16 + word] = m;
-            s_cnt[word] = (uint32_t)__popcll(m);
+            s_cnt[row][word] = (uint32_t)__popcll(m);
         }
         if (a.run_mode) {
             const unsigned long long below = m & lanemask_lt();
@@ -1354,9 +1417,9 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
             const uint32_t pkey = __shfl(rkey[j], prev < 0 ? 0 : prev, 64);
             const bool leader = ((bits[j] & 4u) != 0u) && (prev < 0 || pkey != rkey[j]);
             const unsigned long long lm = __ballot(leader);
-            if (lane == 0) {
+            if (lane == 0 && live_row) {
                 G(a.wave_runs)[(size_t)s * 16 + word] = (uint32_t)__popcll(lm);
-                s_rcnt[word] = (uint32_t)__popcll(lm);
+                s_rcnt[row][word] = (uint32_t)__popcll(lm);
             }
             if (leader && a.key_hist)
                 for (uint32_t p = 0; p < a.npasses; ++p)
@@ -1367,37 +1430,50 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
                 const uint32_t part = kept ? emit_part_of(vk, a.nparts, a.part_ncells) : 0u;
                 part_lanes(m, kept, part, [&](uint32_t p, unsigned long long pm) {
                     if (lane == 0) {
-                        s_pc[0][word][p] = (uint32_t)__popcll(pm);
-                        s_pc[1][word][p] = (uint32_t)__popcll(pm & lm);
+                        s_pc[row][0][word][p] = (uint32_t)__popcll(pm);
+                        s_pc[row][1][word][p] = (uint32_t)__popcll(pm & lm);
                     }
                 });
             }
         }
     }
     __syncthreads();
-    if (a.nparts) {  // counts [points of part 0..P-1 | runs of part 0..P-1][segment]
-        if (threadIdx.x < 2u * a.nparts) {
-            const uint32_t kind = threadIdx.x / a.nparts, p = threadIdx.x % a.nparts;
-            uint32_t c = 0;
-            for (int w = 0; w < NWORDS; ++w) c += s_pc[kind][w][p];
-            G(a.seg_counts)[(size_t)threadIdx.x * a.total_segs + s] = c;
-        }
-    } else if (threadIdx.x == 0) {
-        uint32_t tt = 0, r = 0;
-        for (int w = 0; w < NWORDS; ++w) tt += s_cnt[w];
-        publish_count(a.seg_counts + s, tt);
-        if (a.run_mode) {
-            for (int w = 0; w < NWORDS; ++w) r += s_rcnt[w];
-            publish_count(a.seg_counts + a.total_segs + s, r);
+    // (the first wave of each row publishes that row's segment)
+    if (live_row && wid == 0) {
+        if (a.nparts) {  // counts [points of part 0..P-1 | runs of part 0..P-1][segment]
+            if ((uint32_t)lane < 2u * a.nparts) {
+                const uint32_t kind = lane / a.nparts, p = lane % a.nparts;
+                uint32_t c = 0;
+                for (int w = 0; w < NWORDS; ++w) c += s_pc[row][kind][w][p];
+                G(a.seg_counts)[(size_t)lane * a.total_segs + s] = c;
+            }
+        } else if (lane == 0) {
+            uint32_t tt = 0, r = 0;
+            for (int w = 0; w < NWORDS; ++w) tt += s_cnt[row][w];
+            publish_count(a.seg_counts + s, tt);
+            if (a.run_mode) {
+                for (int w = 0; w < NWORDS; ++w) r += s_rcnt[row][w];
+                publish_count(a.seg_counts + a.total_segs + s, r);
+            }
         }
     }
     if (a.run_mode && a.key_hist) {
         const gptr<uint32_t> rep = G(a.key_hist + (blockIdx.x % kHistReps) * 1024u);
-        for (uint32_t j = threadIdx.x; j < radix_hist_span(a.npasses); j += NT)
+        for (uint32_t j = threadIdx.x; j < radix_hist_span(a.npasses); j += NTB)
             if (s_hist[j])
                 __hip_atomic_fetch_add(rep + j, s_hist[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    group_scan_tail(a, s);
+    if constexpr (ROWS == 1) {
+        group_scan_tail(a, s);
+    } else {  // (block-uniform: each row's segment arrives at its scan group)
+        __shared__ uint32_t s_seg[ROWS];
+        if (threadIdx.x % NT == 0) s_seg[row] = s;
+        __syncthreads();
+        // (one call site in a loop: two inlined copies made the compiler keep a private copy of
+        // FrameArgs - 2288 B of scratch, the round-4 aperture fault's precondition)
+#pragma unroll 1
+        for (uint32_t r = 0; r < nrow; ++r) group_scan_tail(a, s_seg[r]);
+    }
 }
 
 template <int PX, int SEGW>
@@ -1408,6 +1484,11 @@ __global__ __launch_bounds__(SEGW / PX) void k_mask_px(FrameArgs a) {
 template <int PX, int SEGW>
 __global__ __launch_bounds__(SEGW / PX) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_mask_px_o8(FrameArgs a) {
     mask_px_body<PX, SEGW>(a);
+}
+// two rows per block (one workgroup per row pair, FrameArgs::mask_pairs of them)
+template <int PX, int SEGW>
+__global__ __launch_bounds__(2 * SEGW / PX) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_mask_px2r_o8(FrameArgs a) {
+    mask_px_body<PX, SEGW, 2>(a);
 }
 
 // Exclusive scan of the segment counts by one workgroup (chunks of 4096 with a running carry);
@@ -2196,6 +2277,9 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
                 hipLaunchKernelGGL((k_mask_px<2, 256>), dim3(a.total_segs), dim3(128), lds, s, a);
             else if (km == reinterpret_cast<const void*>(&k_mask_px_o8<2, 256>))
                 hipLaunchKernelGGL((k_mask_px_o8<2, 256>), dim3(a.total_segs), dim3(128), lds, s, a);
+            else if (km == reinterpret_cast<const void*>(&k_mask_px2r_o8<2, 256>))
+                hipLaunchKernelGGL((k_mask_px2r_o8<2, 256>), dim3(a.mask_pairs), dim3(256),
+                                   lds + a.band_rowb, s, a);
             else if (km == reinterpret_cast<const void*>(&k_mask_px<2, 640>))
                 hipLaunchKernelGGL((k_mask_px<2, 640>), dim3(a.total_segs), dim3(320), lds, s, a);
             else if (km == reinterpret_cast<const void*>(&k_mask<true, 4>))
@@ -2252,11 +2336,15 @@ constexpr uint32_t kPx640MinSegs = 1024;
 // 22.1 -> 23.7, 720p 4-frame batches 29.8 -> 32.6, 4K 30.9 -> 32.4 Gpoints/s
 uint32_t g_mask_px2 = 2;
 uint32_t g_mask_occ8 = 1;  // k_mask_px<2, 256> at 8 waves per SIMD (GDF_MASK_OCC8=0: 7; +2.5 % on C2)
+uint32_t g_mask_rows = 1;  // k_mask_px2r_o8: two rows per block (tuning knob GDF_MASK_ROWS=2)
 const void* mask_kernel(const FrameArgs& a) {
     if (g_mask_px2 >= 2 && a.do_flying && a.F == 4 && !a.rot45 && a.seg_threads == 256 && !a.dbg &&
-        a.band_rowb <= 64 * 16)
+        a.band_rowb <= 64 * 16) {
+        if (g_mask_rows == 2 && g_mask_occ8 && a.mask_pairs)
+            return reinterpret_cast<const void*>(&k_mask_px2r_o8<2, 256>);
         return g_mask_occ8 ? reinterpret_cast<const void*>(&k_mask_px_o8<2, 256>)
                            : reinterpret_cast<const void*>(&k_mask_px<2, 256>);
+    }
     // (half 720p rows: single frames under 1 Mi pixels with enough segments to fill the chip)
     if (g_mask_px2 >= 2 && a.do_flying && a.F == 4 && !a.rot45 && a.seg_threads == 640 && !a.dbg &&
         a.band_rowb <= 2 * 64 * 16 && a.total_segs >= kPx640MinSegs)
@@ -2274,7 +2362,8 @@ bool emit_partition_kernels(const FrameArgs& a) {
     FrameArgs plain = a;
     plain.nparts = 0;
     return (km == reinterpret_cast<const void*>(&k_mask_px<2, 256>) ||
-            km == reinterpret_cast<const void*>(&k_mask_px_o8<2, 256>)) &&
+            km == reinterpret_cast<const void*>(&k_mask_px_o8<2, 256>) ||
+            km == reinterpret_cast<const void*>(&k_mask_px2r_o8<2, 256>)) &&
            emit_kernel(plain) == reinterpret_cast<const void*>(&k_emit_px2<256>);
 }
 

@@ -52,7 +52,7 @@ const void* emit_kernel(const FrameArgs& a);  // the compaction pass-2 kernel la
 bool emit_partition_kernels(const FrameArgs& a);
 extern uint32_t g_emit_px2;
 extern uint32_t g_grid_wpt;
-extern uint32_t g_mask_occ8;
+extern uint32_t g_mask_occ8, g_mask_rows;
 
 // filter_point_sequence + insert into the rollbuffer ring (w = mask): new points
 // [src0, src0 + cnt) (all by default) of the n uploaded, their filter neighbours over all n
