@@ -333,6 +333,7 @@ struct Slot {
     DevBuf d_ka, d_kb, d_va, d_vb, d_sstatus, d_sgstatus, d_gstatus, d_ggstatus, d_vox;
     DevBuf d_seghist, d_segfs, d_segstat, d_seggstat, d_segdone;  // the segmented run sort
     DevBuf d_gcnt, d_goff;          // group starts per tile + their scan (large frames)
+    DevBuf d_gfirst;                // the first group start of each tile (run groups)
     DevBuf d_bigq, d_bigcnt;        // long voxels queued for k_group_big (large frames)
     bool vox_valid = false;
     DevBuf d_markbits;              // this frame's occupancy marks (1 bit per cell; per batch frame)
@@ -1589,6 +1590,7 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime,
     e->sl().d_vox.ensure((size_t)nmax * 16);
     const uint32_t gtiles = (uint32_t)voxelize_group_tiles(nmax);
     e->sl().d_gcnt.ensure((size_t)gtiles * 4);
+    e->sl().d_gfirst.ensure((size_t)gtiles * 4);
     e->sl().d_goff.ensure(seg_offsets_words(gtiles) * 4);
     if (e->group_scan) {  // k_group_count's own group scan (kernels skip it above their bound)
         const size_t ng = ((size_t)gtiles + kScanGroup - 1) / kScanGroup;
@@ -1660,6 +1662,7 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime,
     // keys per thread of a radix tile: small frames want many tiles (latency), big ones few
     // (each tile publishes 256 look-back words: 2 KiB per 1 Ki keys at PT=4)
     v.group_counts = e->sl().d_gcnt.as<uint32_t>();
+    v.group_first = g_group_first ? e->sl().d_gfirst.as<uint32_t>() : nullptr;
     v.group_offsets = e->sl().d_goff.as<uint32_t>();
     v.group_done = e->group_scan ? e->sl().d_ggdone.as<uint32_t>() : nullptr;
     v.group_gtot = e->group_scan ? e->sl().d_ggtot.as<uint32_t>() : nullptr;
@@ -2045,6 +2048,10 @@ int gdf_create(int device, gdf_engine** out) {
             g_mask_px2 = (uint32_t)std::atoi(v);
         if (const char* v = std::getenv("GDF_RUN_Q16"))  // tuning knob
             g_run_q16 = (uint32_t)std::atoi(v);
+        {  // tuning knob GDF_GROUP_FIRST (process-wide, set at every engine creation)
+            const char* v = std::getenv("GDF_GROUP_FIRST");
+            g_group_first = v ? (uint32_t)std::atoi(v) : 0u;
+        }
         {  // tuning knob (process-wide; every engine creation sets it, default 1)
             const char* v = std::getenv("GDF_RUN_WAVE_MODE");
             g_run_wave_mode = v ? (uint32_t)std::atoi(v) : 1u;

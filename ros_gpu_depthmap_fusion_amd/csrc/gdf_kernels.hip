@@ -3924,8 +3924,9 @@ __global__ __launch_bounds__(256) void k_group_count(const uint32_t* __restrict_
                                                      const uint32_t* __restrict__ count,
                                                      uint32_t* __restrict__ counts,
                                                      uint32_t* gdone, uint32_t* offsets,
-                                                     uint32_t* gtot, uint32_t km) {
-    __shared__ uint32_t s_w[4];
+                                                     uint32_t* gtot, uint32_t km,
+                                                     uint32_t* __restrict__ first) {
+    __shared__ uint32_t s_w[4], s_f[4];
     __shared__ uint32_t s_last;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t n = *count;
@@ -3935,9 +3936,13 @@ __global__ __launch_bounds__(256) void k_group_count(const uint32_t* __restrict_
         const uint32_t key = i < n ? keys[i] & km : 0u;
         const uint32_t prev = (i < n && i > 0) ? keys[i - 1] & km : ~key;
         const unsigned long long b = __ballot(i < n && (i == 0 || key != prev));
-        if (lane == 0) s_w[wid] = (uint32_t)__popcll(b);
+        if (lane == 0) {
+            s_w[wid] = (uint32_t)__popcll(b);
+            s_f[wid] = b ? t * kGroupThreads + 64u * wid + (uint32_t)(__ffsll((long long)b) - 1) : 0xFFFFFFFFu;
+        }
         __syncthreads();
         if (threadIdx.x == 0) publish_count(counts + t, s_w[0] + s_w[1] + s_w[2] + s_w[3]);
+        if (first && threadIdx.x == 0) first[t] = min(min(s_f[0], s_f[1]), min(s_f[2], s_f[3]));
         if (gdone) arrive_and_scan(gdone, counts, offsets, gtot, t, ntiles, 1, 0u, &s_last);
         __syncthreads();
     }
@@ -4210,6 +4215,7 @@ uint32_t g_run_q16 = 2;
 // queue is long (1); tuning knob GDF_RUN_WAVE_MODE=0: every group in block mode, 2: wave mode
 // whatever the queue's length
 uint32_t g_run_wave_mode = 1;
+uint32_t g_group_first = 0;  // k_group_runs: the ends of tiles' last groups from k_group_count's first starts
 uint32_t g_run_big_occ4 = 0;  // tuning knob GDF_RUN_BIG_OCC4 (k_group_runs_big at 4 waves per SIMD)
 
 
@@ -4558,7 +4564,8 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
     uint32_t* marks, const uint32_t* tile_base, uint4* __restrict__ bigq, uint32_t bigq_cap,
     uint32_t* __restrict__ qctr, uint32_t nframes, uint32_t fshift, uint32_t* __restrict__ fvox,
     uint32_t inblock_max, uint32_t* __restrict__ rps, uint32_t* __restrict__ rlen,
-    uint32_t small_max, const uint32_t* tile_gtot, uint64_t mark_stride, uint32_t packed) {
+    uint32_t small_max, const uint32_t* tile_gtot, uint64_t mark_stride, uint32_t packed,
+    const uint32_t* __restrict__ tile_first) {
     __shared__ uint32_t s_wave[4];
     __shared__ uint32_t s_tile, s_epoch, s_excl, s_nbig, s_nq, s_qbase, s_wend, s_nx, s_nbase;
     __shared__ uint32_t s_nh, s_hbase;
@@ -4649,6 +4656,23 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
         } else if (wid == 1 && total) {  // end of the tile's last group (as k_group, over runs)
             const uint32_t lastkey = K(tend - 1);
             uint32_t lo = tend, hi = n;
+            if (tile_first) {
+                // the first group start of the next tiles that hold one (k_group_count): 64 tiles
+                // (16 K runs) per probe of a small cached array, not ~4 rounds of 64 scattered key
+                // reads - a window's long groups sent those over the whole run array per tile
+                // (most of this kernel's 1.67 GB per C3 frame)
+                hi = n;
+                for (uint32_t t0x = tile + 1; t0x < ntiles; t0x += 64u) {  // (wave-uniform)
+                    const uint32_t tt = t0x + (uint32_t)lane;
+                    const uint32_t f = tt < ntiles ? tile_first[tt] : 0xFFFFFFFFu;
+                    const unsigned long long has = __ballot(f != 0xFFFFFFFFu);
+                    if (has) {
+                        hi = (uint32_t)__shfl((int)f, __ffsll((long long)has) - 1, 64);
+                        break;
+                    }
+                }
+                lo = hi;  // (done)
+            }
             while (lo < hi) {
                 const uint32_t len = hi - lo;
                 const uint32_t step = len <= 64u || lo == tend ? 1u : (len + 63u) / 64u;
@@ -5206,6 +5230,7 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
     HookScope hs(hook, GDF_KERNEL_GROUP);
     const uint32_t* tile_base = nullptr;
     const uint32_t* tile_gtot = nullptr;
+    const uint32_t* tile_first = nullptr;
     const uint32_t bigcap = (max_tiles + std::max<uint32_t>(group_tiles, 1u) - 1) /
                             std::max<uint32_t>(group_tiles, 1u);  // tiles per block (walk)
     if (a.group_counts && max_tiles > g_group_scan_tiles) {
@@ -5216,13 +5241,15 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
         const bool gscan = a.group_done && max_tiles <= kMaxGroupScanTiles;
         hipLaunchKernelGGL(k_group_count, dim3(group_tiles), dim3(256), 0, s, kin, gcount,
                            a.group_counts, gscan ? a.group_done : nullptr, a.group_offsets,
-                           a.group_gtot, runs && a.pack_runs && !a.seg_sort ? kRunKeyMask : 0xFFFFFFFFu);
+                           a.group_gtot, runs && a.pack_runs && !a.seg_sort ? kRunKeyMask : 0xFFFFFFFFu,
+                           runs ? a.group_first : nullptr);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (!gscan && (e = launch_scan(a.group_counts, max_tiles, a.group_offsets, nullptr, gcount,
                                        (uint32_t)kGroupThreads, s)) != hipSuccess)
             return e;
         tile_base = a.group_offsets;
         tile_gtot = gscan ? a.group_gtot : nullptr;
+        tile_first = runs ? a.group_first : nullptr;
     }
     if (runs) {  // groups of sorted runs; the long ones by k_group_runs_big
         const uint32_t gb = std::max<uint32_t>(group_tiles, 1u);
@@ -5238,7 +5265,7 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
                            a.nframes, a.frame_shift, a.frame_vox_start,
                            std::min<uint32_t>(g_run_inblock, g_run_stage >= 2048 ? 2048u : 512u),
                            kbuf[sorted_passes & 1], vbuf[sorted_passes & 1], g_small_group,  // (free after the sort)
-                           tile_gtot, a.group_mark_stride, a.pack_runs && !a.seg_sort ? 1u : 0u);
+                           tile_gtot, a.group_mark_stride, a.pack_runs && !a.seg_sort ? 1u : 0u, tile_first);
         if (a.average) {
             if ((e = hipGetLastError()) != hipSuccess) return e;
             const bool q16 = g_run_q16 == 1 ||

@@ -129,6 +129,10 @@ struct VoxelizeArgs {
     uint64_t group_mark_stride;     // k_group_runs: frame f's marks at f * stride words (0: one bitmask)
     uint32_t* group_counts;         // [group tiles] group starts per tile (large frames)
     uint32_t* group_offsets;        // [seg_offsets_words(group tiles)] their scan
+    // [group tiles] the first group start of each tile (0xFFFFFFFF: none), written by
+    // k_group_count: k_group_runs finds the end of a tile's last group from these, not from the
+    // run keys past the tile
+    uint32_t* group_first;
     // optional: the scan inside k_group_count (arrive_and_scan, no scan launches) - arrival
     // counters [group tiles / kScanGroup] (self-resetting) and group totals [same]
     uint32_t* group_done;
@@ -193,7 +197,7 @@ constexpr uint32_t kFrameSortResident = 16384;
 extern uint32_t g_group_scan_tiles;
 // k_group_runs staging (512 or 2048 points) and in-block group size limit
 extern uint32_t g_run_stage, g_run_inblock, g_run_big_blocks, g_run_q16, g_small_group, g_run_wave, g_points_lane;
-extern uint32_t g_run_wave_mode, g_run_big_occ4;
+extern uint32_t g_run_wave_mode, g_run_big_occ4, g_group_first;
 extern uint32_t g_sort_blocks, g_group_blocks;
 size_t voxelize_group_tiles(uint32_t nmax);
 
