@@ -12,10 +12,19 @@ def fam(name):
     return n
 
 
-def main(path, frac=0.5):
+def load(path):
+    if path.endswith(".db"):  # rocprofv3's default (rocpd) output: the `kernels` view
+        import sqlite3
+        c = sqlite3.connect(path)
+        return [(int(s), int(e), fam(n), int(gx) // max(int(wx), 1), int(q)) for s, e, n, gx, wx, q in
+                c.execute("select start, end, name, grid_x, workgroup_x, queue_id from kernels")]
     r = [x for x in csv.DictReader(open(path)) if x["Kind"] == "KERNEL_DISPATCH"]
-    ev = [(int(x["Start_Timestamp"]), int(x["End_Timestamp"]), fam(x["Kernel_Name"]),
-           int(x["Grid_Size_X"]) // max(int(x["Workgroup_Size_X"]), 1), int(x["Queue_Id"])) for x in r]
+    return [(int(x["Start_Timestamp"]), int(x["End_Timestamp"]), fam(x["Kernel_Name"]),
+             int(x["Grid_Size_X"]) // max(int(x["Workgroup_Size_X"]), 1), int(x["Queue_Id"])) for x in r]
+
+
+def main(path, frac=0.5):
+    ev = load(path)
     ev.sort()
     t0, t1 = ev[0][0], max(e[1] for e in ev)
     lo = t1 - (t1 - t0) * frac
