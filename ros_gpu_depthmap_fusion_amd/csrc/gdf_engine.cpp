@@ -2030,48 +2030,39 @@ int gdf_create(int device, gdf_engine** out) {
     int rc = guarded(e, [&] {
         create_slot(e->slots[0]);
         if (const char* v = std::getenv("GDF_SORT_PT")) e->sort_pt = std::atoi(v);  // tuning knob
-        if (const char* v = std::getenv("GDF_GROUP_SCAN_TILES"))                   // tuning knob
-            g_group_scan_tiles = (uint32_t)std::max(1, std::atoi(v));
-        if (const char* v = std::getenv("GDF_RUN_STAGE"))  // tuning knob: 512 or 2048
-            g_run_stage = (uint32_t)std::max(1, std::atoi(v));
-        if (const char* v = std::getenv("GDF_EMIT_PX2"))  // tuning knob
-            g_emit_px2 = (uint32_t)std::atoi(v);
-        if (const char* v = std::getenv("GDF_MASK_OCC8"))  // tuning knob
-            g_mask_occ8 = (uint32_t)std::atoi(v);
-        {  // tuning knob (process-wide, set at every engine creation; default 1)
-            const char* v = std::getenv("GDF_MASK_ROWS");
-            g_mask_rows = v ? (uint32_t)std::atoi(v) : 1u;
-        }
-        if (const char* v = std::getenv("GDF_GRID_WPT"))  // tuning knob: 1..8
-            g_grid_wpt = (uint32_t)std::min(8, std::max(1, std::atoi(v)));
-        if (const char* v = std::getenv("GDF_MASK_PX"))  // tuning knob: pixels per k_mask thread
-            g_mask_px2 = (uint32_t)std::atoi(v);
-        if (const char* v = std::getenv("GDF_RUN_Q16"))  // tuning knob
-            g_run_q16 = (uint32_t)std::atoi(v);
-        {  // tuning knob GDF_GROUP_FIRST (process-wide, set at every engine creation)
-            const char* v = std::getenv("GDF_GROUP_FIRST");
-            g_group_first = v ? (uint32_t)std::atoi(v) : 0u;
-        }
-        {  // tuning knob (process-wide; every engine creation sets it, default 1)
-            const char* v = std::getenv("GDF_RUN_WAVE_MODE");
-            g_run_wave_mode = v ? (uint32_t)std::atoi(v) : 1u;
-            const char* o = std::getenv("GDF_RUN_BIG_OCC4");
-            g_run_big_occ4 = o ? (uint32_t)std::atoi(o) : 0u;
-        }
-        if (const char* v = std::getenv("GDF_RUN_BIG_BLOCKS"))  // tuning knob
-            g_run_big_blocks = (uint32_t)std::max(1, std::atoi(v));
-        if (const char* v = std::getenv("GDF_SORT_BLOCKS"))  // tuning knob
-            g_sort_blocks = (uint32_t)std::max(1, std::atoi(v));
-        if (const char* v = std::getenv("GDF_GROUP_BLOCKS"))  // tuning knob
-            g_group_blocks = (uint32_t)std::max(1, std::atoi(v));
-        if (const char* v = std::getenv("GDF_RUN_INBLOCK"))  // tuning knob
-            g_run_inblock = (uint32_t)std::max(0, std::atoi(v));
-        if (const char* v = std::getenv("GDF_POINTS_LANE"))  // tuning knob
-            g_points_lane = (uint32_t)std::atoi(v);
-        if (const char* v = std::getenv("GDF_RUN_WAVE"))  // tuning knob
-            g_run_wave = (uint32_t)std::atoi(v);
-        if (const char* v = std::getenv("GDF_SMALL_GROUP"))  // tuning knob
-            g_small_group = (uint32_t)std::max(0, std::atoi(v));
+        // process-wide tuning knobs: every engine creation sets each one, from its variable or,
+        // when that is absent, from the built-in value (so a knob one engine was created under
+        // never carries over to a later engine created without it)
+        static const struct {
+            uint32_t scan_tiles, run_stage, emit_px2, mask_occ8, mask_rows, grid_wpt, mask_px2,
+                run_q16, group_first, run_wave_mode, run_big_occ4, run_big_blocks, sort_blocks,
+                group_blocks, run_inblock, points_lane, run_wave, small_group;
+        } d = {g_group_scan_tiles, g_run_stage, g_emit_px2, g_mask_occ8, g_mask_rows, g_grid_wpt,
+               g_mask_px2, g_run_q16, g_group_first, g_run_wave_mode, g_run_big_occ4,
+               g_run_big_blocks, g_sort_blocks, g_group_blocks, g_run_inblock, g_points_lane,
+               g_run_wave, g_small_group};
+        auto knob = [](const char* name, uint32_t dflt, int lo = 0, int hi = INT32_MAX) {
+            const char* v = std::getenv(name);
+            return v ? (uint32_t)std::min(hi, std::max(lo, std::atoi(v))) : dflt;
+        };
+        g_group_scan_tiles = knob("GDF_GROUP_SCAN_TILES", d.scan_tiles, 1);
+        g_run_stage = knob("GDF_RUN_STAGE", d.run_stage, 1);  // 512 or 2048
+        g_emit_px2 = knob("GDF_EMIT_PX2", d.emit_px2);
+        g_mask_occ8 = knob("GDF_MASK_OCC8", d.mask_occ8);
+        g_mask_rows = knob("GDF_MASK_ROWS", d.mask_rows);
+        g_grid_wpt = knob("GDF_GRID_WPT", d.grid_wpt, 1, 8);
+        g_mask_px2 = knob("GDF_MASK_PX", d.mask_px2);  // pixels per k_mask thread
+        g_run_q16 = knob("GDF_RUN_Q16", d.run_q16);
+        g_group_first = knob("GDF_GROUP_FIRST", d.group_first);
+        g_run_wave_mode = knob("GDF_RUN_WAVE_MODE", d.run_wave_mode);
+        g_run_big_occ4 = knob("GDF_RUN_BIG_OCC4", d.run_big_occ4);
+        g_run_big_blocks = knob("GDF_RUN_BIG_BLOCKS", d.run_big_blocks, 1);
+        g_sort_blocks = knob("GDF_SORT_BLOCKS", d.sort_blocks, 1);
+        g_group_blocks = knob("GDF_GROUP_BLOCKS", d.group_blocks, 1);
+        g_run_inblock = knob("GDF_RUN_INBLOCK", d.run_inblock);
+        g_points_lane = knob("GDF_POINTS_LANE", d.points_lane);
+        g_run_wave = knob("GDF_RUN_WAVE", d.run_wave);
+        g_small_group = knob("GDF_SMALL_GROUP", d.small_group);
         if (const char* v = std::getenv("GDF_SEG_ITEMS")) {  // tuning knob
             const uint32_t si = (uint32_t)std::atoi(v);
             if (si >= 64 && si <= kSegItems && si % 64 == 0) e->seg_items = si;

@@ -130,7 +130,16 @@ def test_download_frame_grid_mirror_deltas(Engine):
 @pytest.mark.parametrize("knobs", [{}, {"GDF_NO_MASK_PACKED": "1"}, {"GDF_NO_GROUP_SCAN": "1"},
                                    {"GDF_SEG_SORT": "1"}, {"GDF_NO_PACK_RUNS": "1"},
                                    {"GDF_FRAME_SORT": "1"}, {"GDF_GRID_LAST": "1"},
-                                   {"GDF_MASK_ROWS": "2"}, {"GDF_GROUP_FIRST": "1"}])
+                                   {"GDF_MASK_ROWS": "2"}, {"GDF_GROUP_FIRST": "1"},
+                                   # sizes and alternative forms of the sort and group phases
+                                   {"GDF_RUN_HIST_SORT": "1"}, {"GDF_RUN_HIST_ALL": "1"},
+                                   {"GDF_SORT_BLOCKS": "1024"}, {"GDF_GROUP_BLOCKS": "1024"},
+                                   {"GDF_GRID_WPT": "4"}, {"GDF_RUN_STAGE": "512"},
+                                   {"GDF_SMALL_GROUP": "64"}, {"GDF_RUN_WAVE": "1"},
+                                   {"GDF_RUN_WAVE": "0"}, {"GDF_RUN_Q16": "1"},
+                                   {"GDF_RUN_BIG_BLOCKS": "512"},
+                                   # (an engine created after all of them: the built-in values)
+                                   {}])
 def test_batch8_vga_knobs_match_oracle(Engine, knobs):
     """8-frame VGA batches (the C2 bench step) with the round-4 paths on and off: every frame's
     points, keys, voxel means and grid equal the oracle's frame-by-frame results."""
