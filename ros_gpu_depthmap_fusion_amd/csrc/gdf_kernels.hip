@@ -393,14 +393,29 @@ struct SegGeo {
     uint32_t item0;   // first item (global point index)
 };
 
+// The emitting camera whose segments hold segment s (the last one, 0 if none): lane c tests
+// camera c, so every camera's range arrives in ONE load round - a scan over the table issued a
+// dependent scalar-load round per camera (k_mask_px stamps, tools/mask_trace.py: 12.3 K of a
+// block's 36.9 K cycles for 8 cameras).  Wave-uniform result; every lane of the wave active.
+template <class P>
+__device__ __forceinline__ int seg_camera(P cams, int ncams, uint32_t s) {
+    static_assert(kMaxCams <= 64, "one camera per lane");
+    const int lane = threadIdx.x & 63;
+    bool hit = false;
+    if (lane < ncams) {
+        const uint32_t seg0 = cams[lane].seg0;
+        hit = cams[lane].emit && s >= seg0 && s < seg0 + cams[lane].nseg;
+    }
+    const unsigned long long m = __ballot(hit);
+    return m ? 63 - __clzll((long long)m) : 0;
+}
+
 // (P: an LDS copy of the descriptors, or the global / kernel-argument table read with scalar
 // loads - the segment is block-uniform)
 template <class P>
 __device__ __forceinline__ SegGeo seg_geo(P cams, int ncams, uint32_t s) {
     SegGeo g{0, 0, 0, 0, 0};
-    for (int c = 0; c < ncams; ++c)
-        if (cams[c].emit && s >= cams[c].seg0 && s < cams[c].seg0 + cams[c].nseg) g.k = c;
-    g.k = __builtin_amdgcn_readfirstlane(g.k);
+    g.k = seg_camera(cams, ncams, s);
     const uint32_t seg0 = cams[g.k].seg0, nchunk = cams[g.k].nchunk, segw = cams[g.k].segw;
     const uint32_t W = cams[g.k].W;
     const uint32_t i = s - seg0;
@@ -1222,8 +1237,25 @@ __device__ __forceinline__ unsigned long long part_lanes(unsigned long long m, b
 // rows - 5 staged rows per segment instead of 9, and the segment's fixed work (its camera and
 // geometry, the band's loads and barrier) once per two; the waves of row r run as the 1-row
 // kernel's (their band seen from row r: rowoff / yn shifted by r).
+#ifdef GDF_TRACE_GROUPS
+// (diagnostic build, tools/mask_trace.py) per k_mask_px block (ROWS = 1): wall clock at entry and
+// exit, then wave 0's cycles in each phase - segment geometry and camera, band loads landed, LDS
+// stores + barrier, the filter, the ballots + publish barrier, the scan tail - each phase closed by
+// a wait for this wave's outstanding memory operations (which the product kernel does not do)
+constexpr uint32_t kMaskTraceSlots = 1u << 14;
+__device__ unsigned long long g_mtrace[kMaskTraceSlots][8];
+#define GDF_MSTAMP(i)               \
+    __builtin_amdgcn_s_waitcnt(0);  \
+    mt[i] = clock64()
+#endif
+
 template <int PX, int SEGW, int ROWS = 1>
 __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
+#ifdef GDF_TRACE_GROUPS
+    const unsigned long long mw0 = wall_clock64();
+    unsigned long long mt[7] = {};
+    GDF_MSTAMP(0);
+#endif
     constexpr int NT = SEGW / PX, NW = NT / 64;          // threads, waves (per row)
     constexpr int NTB = NT * ROWS, NWB = NW * ROWS;      // (per block)
     constexpr int NWORDS = SEGW / 64;                    // validity words of a segment
@@ -1278,6 +1310,10 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
             const float *xn, *yn;
             uint32_t W, H;
         } c = {gcam[sg.k].depth, gcam[sg.k].xn, gcam[sg.k].yn, gcam[sg.k].W, gcam[sg.k].H};
+#ifdef GDF_TRACE_GROUPS
+        asm volatile("" ::"s"(c.depth), "s"(c.W));  // (the camera's fields before the stamp)
+        GDF_MSTAMP(1);
+#endif
         const int h = 4;  // (F = 4: the launch checks it)
         const uint32_t ca = sg.x0 >= (uint32_t)h ? sg.x0 - h : 0u;
         const uint32_t cb = min(c.W, sg.x0 + sg.len + h);
@@ -1315,6 +1351,9 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
                 }
             }
         }
+#ifdef GDF_TRACE_GROUPS
+        GDF_MSTAMP(2);
+#endif
         const uint32_t tb = threadIdx.x;  // (thread of the block)
         float xv[QX];
 #pragma unroll
@@ -1350,6 +1389,9 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
             if (ca + tb + (uint32_t)NTB * q < cb) s_xn[tb + (uint32_t)NTB * q] = xv[q];
         if (wrap && tb < (uint32_t)h) s_xn[-1 - (int)tb] = xwv;
         __syncthreads();
+#ifdef GDF_TRACE_GROUPS
+        GDF_MSTAMP(3);
+#endif
         // (row r's waves: the band from their own pixel row, h rows above it)
         const Band t{band, s_xn, s_rowoff + row, ca, h};
         const float* s_ynr = s_yn + row;
@@ -1402,6 +1444,9 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
             }
         }
     }
+#ifdef GDF_TRACE_GROUPS
+    GDF_MSTAMP(4);
+#endif
     const bool live_row = (uint32_t)row < nrow;  // (a pair's missing second row: no outputs)
 #pragma unroll
     for (int j = 0; j < PX; ++j) {
@@ -1438,6 +1483,9 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
         }
     }
     __syncthreads();
+#ifdef GDF_TRACE_GROUPS
+    GDF_MSTAMP(5);
+#endif
     // (the first wave of each row publishes that row's segment)
     if (live_row && wid == 0) {
         if (a.nparts) {  // counts [points of part 0..P-1 | runs of part 0..P-1][segment]
@@ -1465,6 +1513,15 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
     }
     if constexpr (ROWS == 1) {
         group_scan_tail(a, s);
+#ifdef GDF_TRACE_GROUPS
+        GDF_MSTAMP(6);
+        if (threadIdx.x == 0 && blockIdx.x < kMaskTraceSlots) {
+            unsigned long long* g = g_mtrace[blockIdx.x];
+            g[0] = mw0;
+            g[1] = wall_clock64();
+            for (int k = 1; k < 7; ++k) g[k + 1] = mt[k] - mt[k - 1];
+        }
+#endif
     } else {  // (block-uniform: each row's segment arrives at its scan group)
         __shared__ uint32_t s_seg[ROWS];
         if (threadIdx.x % NT == 0) s_seg[row] = s;
@@ -1716,9 +1773,7 @@ __global__ __launch_bounds__(1024) void k_emit(FrameArgs a) {
     else if (a.grp_tot) group_partials(a, s, s_red);
     // the segment's geometry and the thread's item source, loaded before the barrier
     const uint32_t i = threadIdx.x;
-    int k = 0;
-    for (int c = 0; c < a.ncams; ++c)
-        if (cams[c].emit && s >= cams[c].seg0 && s < cams[c].seg0 + cams[c].nseg) k = c;
+    int k = seg_camera(cams, a.ncams, s);
     // block-uniform camera: its descriptor (device copy beyond kArgCams cameras) is read with
     // scalar loads, not once per lane
     k = __builtin_amdgcn_readfirstlane(k);
@@ -1836,9 +1891,7 @@ __device__ __forceinline__ void emit_px2_parts(const FrameArgs& a, uint32_t* s_m
     __syncthreads();  // (the zeroed counters and the mark cache before any wave writes them)
     const gptr<const CamDesc> cams = G(cam_table(a));
     const uint32_t i = threadIdx.x;
-    int k = 0;
-    for (int c = 0; c < a.ncams; ++c)
-        if (cams[c].emit && s >= cams[c].seg0 && s < cams[c].seg0 + cams[c].nseg) k = c;
+    int k = seg_camera(cams, a.ncams, s);
     k = __builtin_amdgcn_readfirstlane(k);
     const uint32_t j = s - cams[k].seg0;
     const uint32_t y = j / cams[k].nchunk;
@@ -1945,9 +1998,7 @@ __global__ __launch_bounds__(SEGW / 2) void k_emit_px2(FrameArgs a) {
     if (a.fused_prefix) prefix_partials(a, s, s_red);
     else if (a.grp_tot) group_partials(a, s, s_red);
     const uint32_t i = threadIdx.x;
-    int k = 0;
-    for (int c = 0; c < a.ncams; ++c)
-        if (cams[c].emit && s >= cams[c].seg0 && s < cams[c].seg0 + cams[c].nseg) k = c;
+    int k = seg_camera(cams, a.ncams, s);
     k = __builtin_amdgcn_readfirstlane(k);
     const uint32_t j = s - cams[k].seg0;
     const uint32_t y = j / cams[k].nchunk;
@@ -5057,6 +5108,10 @@ extern "C" int gdf_debug_group_trace(void* dst, size_t bytes) {  // (diagnostic 
 extern "C" int gdf_debug_group_trace_clear() {
     static unsigned long long zero[kTraceSlots][8];
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_gtrace), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
+}
+extern "C" int gdf_debug_mask_trace(void* dst, size_t bytes) {  // (diagnostic build only)
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_mtrace), std::min(bytes, sizeof(g_mtrace)), 0,
+                                    hipMemcpyDeviceToHost);
 }
 #endif
 
