@@ -4266,7 +4266,7 @@ uint32_t g_run_q16 = 2;
 // queue is long (1); tuning knob GDF_RUN_WAVE_MODE=0: every group in block mode, 2: wave mode
 // whatever the queue's length
 uint32_t g_run_wave_mode = 1;
-uint32_t g_group_first = 0;  // k_group_runs: the ends of tiles' last groups from k_group_count's first starts
+uint32_t g_group_first = 1;  // k_group_runs: the ends of tiles' last groups from k_group_count's first starts (GDF_GROUP_FIRST=0: the key search)
 uint32_t g_run_big_occ4 = 0;  // tuning knob GDF_RUN_BIG_OCC4 (k_group_runs_big at 4 waves per SIMD)
 
 

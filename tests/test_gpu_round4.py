@@ -130,7 +130,7 @@ def test_download_frame_grid_mirror_deltas(Engine):
 @pytest.mark.parametrize("knobs", [{}, {"GDF_NO_MASK_PACKED": "1"}, {"GDF_NO_GROUP_SCAN": "1"},
                                    {"GDF_SEG_SORT": "1"}, {"GDF_NO_PACK_RUNS": "1"},
                                    {"GDF_FRAME_SORT": "1"}, {"GDF_GRID_LAST": "1"},
-                                   {"GDF_MASK_ROWS": "2"}, {"GDF_GROUP_FIRST": "1"},
+                                   {"GDF_MASK_ROWS": "2"}, {"GDF_GROUP_FIRST": "0"},
                                    # sizes and alternative forms of the sort and group phases
                                    {"GDF_RUN_HIST_SORT": "1"}, {"GDF_RUN_HIST_ALL": "1"},
                                    {"GDF_SORT_BLOCKS": "1024"}, {"GDF_GROUP_BLOCKS": "1024"},
@@ -174,7 +174,7 @@ def test_batch8_vga_knobs_match_oracle(Engine, knobs):
 @pytest.mark.parametrize("knobs", [{}, {"GDF_NO_GROUP_SCAN": "1"}, {"GDF_SEG_SORT": "1"},
                                    {"GDF_NO_PACK_RUNS": "1"}, {"GDF_GRID_LAST": "1"},
                                    {"GDF_RUN_WAVE_MODE": "2"}, {"GDF_MASK_ROWS": "2"},
-                                   {"GDF_GROUP_FIRST": "1"}])
+                                   {"GDF_GROUP_FIRST": "0"}])
 def test_4k_frame_knobs_match_oracle(Engine, knobs):
     """A dense 4K frame (32 400 compaction segments, runs of equal keys): the group scans on and
     off, every output equal to the oracle's."""
