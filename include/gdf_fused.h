@@ -55,13 +55,38 @@ int gdf_fused_destroy(gdf_fused* rank);
  * streams (matched in issue order like RCCL's; the host only waits for every rank to ISSUE a
  * collective, never for the GPU).  The same gdf_fused_start / finish / run as the RCCL ranks: this
  * is how the multi-rank C++ step runs (and is tested) on a node with fewer GPUs than ranks, where
- * RCCL refuses two ranks on one device.  A rank whose step fails aborts the world: the other
- * ranks' pending and later collectives fail with GDF_ERR_STATE instead of waiting (so does a rank
- * left waiting longer than GDF_LOCAL_TIMEOUT_S seconds, default 300).  Destroy every rank
- * (gdf_fused_destroy) before the world. */
+ * RCCL refuses two ranks on one device.  A rank whose step fails - for any reason, a bad argument
+ * on that rank alone included - aborts the world: the other ranks' pending and later collectives
+ * fail with GDF_ERR_STATE at once instead of waiting (so does a rank left waiting longer than
+ * GDF_LOCAL_TIMEOUT_S seconds, default 300).  Every round's schedule is checked on every rank
+ * before any copy (gdf_fused_local_check_round / _check_arrival below): what RCCL would hang on
+ * or corrupt fails here.  Destroy every rank (gdf_fused_destroy) before the world. */
 typedef struct gdf_fused_local gdf_fused_local;
 int gdf_fused_local_create(int world, gdf_fused_local** out);
 int gdf_fused_local_destroy(gdf_fused_local* world);
+/* Diagnostics of the in-process transport's schedule checks (what a round of it verifies before
+ * any copy; no device work).  gdf_fused_local_check_round: one round, rank q's operations are
+ * ops[sum(nops[0..q)) .. + nops[q]) in its issue order (kind 0 all-gather: src = its send buffer,
+ * dst = its receive buffer of world * bytes; 1 send to `peer` from src; 2 receive from `peer` into
+ * dst), issue[q] = the round's number in rank q's issue order over both communicators.  Fails
+ * (GDF_ERR_STATE, gdf_last_error names it) on a send no receive consumes, a receive without its
+ * send, differing sizes, a bad peer, an all-gather send buffer overlapping its receive buffer
+ * other than at recv + rank * bytes, or issue numbers that differ across the ranks.
+ * gdf_fused_local_check_arrival: rank `rank` arrives in round `round` of communicator `comm`
+ * (0 halo, 1 points) as its collective #issue while waiting[3q .. 3q + 2] = {comm, round, issue}
+ * of the round rank q is blocked in (comm -1: not blocked); fails when another rank waits in a
+ * different round under the same number (the two-communicator deadlock). */
+typedef struct gdf_local_op {
+    int kind;
+    const void* src;
+    void* dst;
+    uint64_t bytes;
+    int peer;
+} gdf_local_op;
+int gdf_fused_local_check_round(int world, const gdf_local_op* ops, const uint32_t* nops,
+                                const uint64_t* issue);
+int gdf_fused_local_check_arrival(int world, int rank, int comm, uint64_t round, uint64_t issue,
+                                  const int64_t* waiting);
 /* Not collective (no rendezvous): creates rank `rank` of the local world on `engine`; cams and
  * flying_filter_size as for gdf_fused_create. */
 int gdf_fused_create_local(gdf_engine* engine, gdf_fused_local* world, int rank, int nranks,

@@ -310,6 +310,39 @@ public:
     void prepareLayersConnections() {}
     void computeLayersConnections() {}
     void downloadLayersConnections() {}
+    // checkAllPointSequenceBuffers (fusion.cpp:859-926; its call sites :856, :975, :1086, :1216 are
+    // commented out): the reference downloads every rollbuffer buffer into function statics for a
+    // debugger.  Here the rollbuffer in the reference's logical B layout (points, mask, sequence
+    // index per point; headers sec / nsec / start / numPoints) lands in the m_check* members.
+    void checkAllPointSequenceBuffers() {
+        syncRollbuffer();
+        const uint32_t R = m_rollBufferNumPoints, S = m_rollBufferNumSeqs;
+        m_checkPoints.resize((size_t)R * 4);
+        m_checkPointsMask.resize(R);
+        m_checkSeqIdcs.resize(R);
+        m_checkSequences.resize((size_t)S * 4);
+        check(gdf_debug_rollbuffer(h_, m_checkPoints.data(), m_checkPointsMask.data(), m_checkSeqIdcs.data(),
+                                   R, m_checkSequences.data(), S));
+    }
+    std::vector<float> m_checkPoints;
+    std::vector<uint32_t> m_checkPointsMask, m_checkSeqIdcs, m_checkSequences;
+
+    // computeLayersConnectionsCPU (fusion.cpp:2153-2197, uncalled in the reference): the same
+    // matrices from the downloaded labels on the host - zero each numLabels[i] x numLabels[i + 1]
+    // matrix, then connection(labelA, labelB) = 1 for every cell (background label 0 included).
+    // Rewrites m_ccLayersConnections' storage with what labelVoxels' device pass already produced.
+    void computeLayersConnectionsCPU() {
+        for (size_t i = 0; i < m_ccLayersConnections.size(); ++i) {
+            Mat_<uint8_t>& mat = m_ccLayersConnections[i];
+            const Mat_<uint16_t>& A = m_ccLabeledLayers[i];
+            const Mat_<uint16_t>& B = m_ccLabeledLayers[i + 1];
+            for (int a = 0; a < (int)m_ccNumLabelsPerLayer[i]; ++a)
+                for (int b = 0; b < (int)m_ccNumLabelsPerLayer[i + 1]; ++b) mat.template at<uint8_t>(a, b) = 0;
+            for (int y = 0; y < A.rows; ++y)
+                for (int x = 0; x < A.cols; ++x)
+                    mat.template at<uint8_t>(A.template at<uint16_t>(y, x), B.template at<uint16_t>(y, x)) = 1;
+        }
+    }
     // mergeLabelsAcrossLayers (:2243-2361): m_ccLabelsMerged / Layer / Local per global label
     void mergeLabelsAcrossLayers() {
         const size_t T = m_ccStatsData.size() / 5;

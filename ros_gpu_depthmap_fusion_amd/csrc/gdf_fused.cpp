@@ -10,6 +10,7 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <condition_variable>
 #include <cstdlib>
@@ -123,7 +124,6 @@ struct Transport {
     virtual void recv(void* buf, size_t bytes, int peer, Comm c, hipStream_t st) = 0;
     virtual void group_end(Comm c, hipStream_t st) = 0;
     virtual void abort() {}
-    uint64_t calls = 0;  // collectives and groups issued (counted by the step)
 };
 
 // RCCL: two communicators of the transport's own, byte-typed transfers.
@@ -164,22 +164,104 @@ struct RcclTransport final : Transport {
 // across the ranks by their k-th call, like RCCL's issue order:
 //   1. each rank records `ready` on its stream (its sends are written) and posts its operations;
 //   2. host barrier: every rank posted round k;
-//   3. each rank copies what it receives, on ITS stream, behind the sender's `ready`;
+//   3. each rank checks the round's schedule (check_round: the same on every rank, so every rank
+//      fails alike), copies what it receives, on ITS stream, behind the sender's `ready`;
 //   4. each rank records `done` (its reads are finished); host barrier;
 //   5. each rank's stream waits for every other rank's `done` before its buffers are reused.
 // The host only waits for the other ranks to ISSUE (not to finish): GPU work stays queued and the
 // steps stay pipelined.  A rank that fails aborts the world, so the others fail instead of waiting.
+//
+// The transport is as strict as RCCL is unforgiving: a schedule RCCL would hang on or corrupt
+// fails here, at once and on every rank -
+//   * a send no peer receives in the same round (RCCL: the sender's kernel never completes), a
+//     receive without its send, sizes that differ, a bad peer;
+//   * an all-gather whose send buffer overlaps its receive buffer anywhere but at recv + rank *
+//     bytes (RCCL's only in-place form), all-gathers of different sizes across the ranks;
+//   * the ranks issuing their collectives over the two communicators in different orders (the
+//     classic two-communicator deadlock: rank 0 blocked in round k of A while rank 1 is blocked in
+//     round m of B) - every rank numbers the rounds it issues over both communicators, a round's
+//     number must be the same on every rank (check_round), and a rank arriving in a round checks
+//     that no other rank waits in a different round under the same number (check_arrival).
+namespace {
+struct LocalOp {
+    int kind;  // 0 all-gather, 1 send, 2 recv
+    const void* src;
+    void* dst;
+    size_t bytes;
+    int peer;
+};
+
+const char* comm_name(int c) { return c == 0 ? "halo" : "points"; }
+
+// The schedule of one round, posts[q] = rank q's operations in its issue order, issue[q] = the
+// round's number in rank q's issue order over both communicators.  Empty: the round is valid.
+std::string check_round(int W, const std::vector<const std::vector<LocalOp>*>& posts,
+                        const std::vector<uint64_t>& issue) {
+    for (int q = 1; q < W; ++q)
+        if (issue[q] != issue[0])
+            return "local transport: cross-communicator issue order differs across ranks (rank 0 "
+                   "issued this round as its collective #" + std::to_string(issue[0]) + ", rank " +
+                   std::to_string(q) + " as #" + std::to_string(issue[q]) + ")";
+    std::vector<std::vector<size_t>> ag(W);  // all-gather sizes per rank, in order
+    for (int q = 0; q < W; ++q)
+        for (const LocalOp& o : *posts[q]) {
+            if (o.kind == 0) {
+                ag[q].push_back(o.bytes);
+                const uintptr_t s = (uintptr_t)o.src, d = (uintptr_t)o.dst;
+                const uintptr_t se = s + o.bytes, de = d + (uintptr_t)W * o.bytes;
+                if (o.bytes && s < de && d < se && s != d + (uintptr_t)q * o.bytes)
+                    return "local transport: rank " + std::to_string(q) + "'s all-gather send "
+                           "buffer overlaps its receive buffer other than at recv + rank * bytes";
+            } else if (o.kind == 1 || o.kind == 2) {
+                if (o.peer < 0 || o.peer >= W || o.peer == q)
+                    return std::string("local transport: bad ") + (o.kind == 1 ? "send" : "receive") +
+                           " peer " + std::to_string(o.peer) + " on rank " + std::to_string(q);
+            } else {
+                return "local transport: unknown operation";
+            }
+        }
+    for (int q = 1; q < W; ++q)
+        if (ag[q] != ag[0]) return "local transport: all-gather sizes differ across ranks";
+    // every send s -> d matched by d's receive from s, n-th with n-th, equal sizes
+    for (int s = 0; s < W; ++s)
+        for (int d = 0; d < W; ++d) {
+            if (s == d) continue;
+            std::vector<size_t> snd, rcv;
+            for (const LocalOp& o : *posts[s])
+                if (o.kind == 1 && o.peer == d) snd.push_back(o.bytes);
+            for (const LocalOp& o : *posts[d])
+                if (o.kind == 2 && o.peer == s) rcv.push_back(o.bytes);
+            const std::string pair = " (rank " + std::to_string(s) + " -> rank " + std::to_string(d) + ")";
+            if (snd.size() > rcv.size()) return "local transport: a send no receive consumes" + pair;
+            if (snd.size() < rcv.size()) return "local transport: a receive without its send" + pair;
+            if (snd != rcv) return "local transport: send / receive sizes differ" + pair;
+        }
+    return std::string();
+}
+
+// Rank R arrives in round k of communicator c as its collective #issue; waiting[q] = {c, k, issue}
+// of the round rank q is blocked in (c = -1: not waiting).  Empty: no crossed order.
+std::string check_arrival(int W, int R, int c, uint64_t k, uint64_t issue,
+                          const std::vector<std::array<int64_t, 3>>& waiting) {
+    for (int q = 0; q < W; ++q) {
+        if (q == R || waiting[q][0] < 0) continue;
+        if ((uint64_t)waiting[q][2] == issue && (waiting[q][0] != c || (uint64_t)waiting[q][1] != k))
+            return "local transport: cross-communicator issue order differs across ranks (rank " +
+                   std::to_string(R) + " issued " + comm_name(c) + " round " + std::to_string(k) +
+                   " as its collective #" + std::to_string(issue) + ", rank " + std::to_string(q) +
+                   " waits in " + comm_name((int)waiting[q][0]) + " round " +
+                   std::to_string(waiting[q][1]) + " under the same number)";
+    }
+    return std::string();
+}
+}  // namespace
+
 struct gdf_fused_local {
-    struct Op {
-        int kind;  // 0 all-gather, 1 send, 2 recv
-        const void* src;
-        void* dst;
-        size_t bytes;
-        int peer;
-    };
+    using Op = LocalOp;
     struct Post {
         std::vector<Op> ops;
         hipEvent_t ready = nullptr, done = nullptr;
+        uint64_t issue = 0;
     };
     struct Round {
         std::vector<Post> posts;
@@ -189,11 +271,19 @@ struct gdf_fused_local {
     std::mutex m;
     std::condition_variable cv;
     std::map<uint64_t, Round> rounds[2];
+    std::vector<std::array<int64_t, 3>> waiting;  // per rank: the round it waits in (check_arrival)
     int refs = 0;  // ranks created on this world and not destroyed
     bool aborted = false;
     std::string abort_reason;
     double timeout_s = 300.0;  // a rank that never arrives (a caller bug) ends the wait
 
+    void abort_locked(const std::string& why) {
+        if (!aborted) {
+            aborted = true;
+            abort_reason = why;
+        }
+        cv.notify_all();
+    }
     template <class Pred>
     void wait(std::unique_lock<std::mutex>& lk, Pred pred, const char* what) {
         const auto until = std::chrono::steady_clock::now() +
@@ -201,9 +291,7 @@ struct gdf_fused_local {
         while (!pred()) {
             if (aborted) fail(GDF_ERR_STATE, std::string("local transport aborted (") + abort_reason + ")");
             if (cv.wait_until(lk, until) == std::cv_status::timeout && !pred()) {
-                aborted = true;
-                abort_reason = std::string("timeout at ") + what;
-                cv.notify_all();
+                abort_locked(std::string("timeout at ") + what);
                 fail(GDF_ERR_STATE, std::string("local transport: a rank did not reach ") + what);
             }
         }
@@ -216,6 +304,7 @@ struct LocalTransport final : Transport {
     gdf_fused_local* w = nullptr;
     int rank = 0;
     uint64_t seq[2] = {0, 0};
+    uint64_t issued = 0;  // rounds issued over both communicators (the issue-order check)
     hipEvent_t ready[2] = {nullptr, nullptr}, done[2] = {nullptr, nullptr};
     bool grouped[2] = {false, false};
     std::vector<gdf_fused_local::Op> ops[2];
@@ -236,11 +325,7 @@ struct LocalTransport final : Transport {
     int ranks() const override { return w->world; }
     void abort() override {
         std::lock_guard<std::mutex> lk(w->m);
-        if (!w->aborted) {
-            w->aborted = true;
-            w->abort_reason = "rank " + std::to_string(rank) + " failed";
-        }
-        w->cv.notify_all();
+        w->abort_locked("rank " + std::to_string(rank) + " failed");
     }
     void all_gather(const void* send, void* recv, size_t bytes, Comm c, hipStream_t st) override {
         ops[c].push_back({0, send, recv, bytes, -1});
@@ -271,20 +356,44 @@ struct LocalTransport final : Transport {
         mine.swap(ops[c]);
         const int W = w->world, R = rank;
         const uint64_t k = seq[c]++;
+        const uint64_t issue = issued++;
         hipchk(hipEventRecord(ready[c], st), "hipEventRecord(ready)");
         gdf_fused_local::Round* rd = nullptr;
         {
             std::unique_lock<std::mutex> lk(w->m);
+            if (w->waiting.size() != (size_t)W) w->waiting.assign(W, {-1, -1, -1});
+            const std::string crossed = check_arrival(W, R, c, k, issue, w->waiting);
+            if (!crossed.empty()) {
+                w->abort_locked(crossed);
+                fail(GDF_ERR_STATE, crossed);
+            }
             rd = &w->rounds[c][k];
             if (rd->posts.empty()) rd->posts.resize(W);
             rd->posts[R].ops = mine;
             rd->posts[R].ready = ready[c];
             rd->posts[R].done = done[c];
+            rd->posts[R].issue = issue;
             ++rd->arrived;
+            w->waiting[R] = {(int64_t)c, (int64_t)k, (int64_t)issue};
             w->cv.notify_all();
             w->wait(lk, [&] { return rd->arrived == W; }, "a collective");
+            w->waiting[R] = {-1, -1, -1};
         }
         // (the posts are written before the barrier and only read after it: no lock needed)
+        {
+            std::vector<const std::vector<LocalOp>*> posts(W);
+            std::vector<uint64_t> issues(W);
+            for (int q = 0; q < W; ++q) {
+                posts[q] = &rd->posts[q].ops;
+                issues[q] = rd->posts[q].issue;
+            }
+            const std::string bad = check_round(W, posts, issues);
+            if (!bad.empty()) {
+                std::lock_guard<std::mutex> lk(w->m);
+                w->abort_locked(bad);
+                fail(GDF_ERR_STATE, bad);
+            }
+        }
         std::vector<char> waited(W, 0);
         auto behind = [&](int q) {
             if (!waited[q]) {
@@ -302,23 +411,16 @@ struct LocalTransport final : Transport {
             if (op.kind == 0) {
                 for (int q = 0; q < W; ++q) {
                     const gdf_fused_local::Op* o = nth(rd->posts[q].ops, 0, -1, ag);
-                    if (!o || o->bytes != op.bytes)
-                        fail(GDF_ERR_STATE, "local transport: all-gather sizes differ across ranks");
                     uint8_t* dst = static_cast<uint8_t*>(op.dst) + (size_t)q * op.bytes;
                     if (q != R) behind(q);
                     copy(dst, o->src, op.bytes);  // (in place: the own slice is already there)
                 }
                 ++ag;
-            } else if (op.kind == 2) {
+            } else if (op.kind == 2) {  // (check_round matched every receive with its send)
                 const int q = op.peer;
-                if (q < 0 || q >= W || q == R) fail(GDF_ERR_STATE, "local transport: bad receive peer");
                 const gdf_fused_local::Op* o = nth(rd->posts[q].ops, 1, R, nrecv[q]++);
-                if (!o) fail(GDF_ERR_STATE, "local transport: a receive without its send");
-                if (o->bytes != op.bytes) fail(GDF_ERR_STATE, "local transport: send / receive sizes differ");
                 behind(q);
                 copy(op.dst, o->src, op.bytes);
-            } else if (op.peer < 0 || op.peer >= W || op.peer == R) {
-                fail(GDF_ERR_STATE, "local transport: bad send peer");
             }
         }
         hipchk(hipEventRecord(done[c], st), "hipEventRecord(done)");
@@ -455,7 +557,6 @@ void fused_start(gdf_fused* f, const uint16_t* const* depth, uint32_t B, const g
         for (uint32_t j = 0; j < B; ++j)
             hipchk(hipMemcpyAsync(tail + j * L2, depth[j] + (npx - f->Lmax), L2,
                                   hipMemcpyDeviceToDevice, st), "hipMemcpyAsync(tail)");
-        ++x.calls;
         x.all_gather(tail, S.tails.as(), B * L2, kHalo, st);
     }
     for (uint32_t j = 0; j < B; ++j) {
@@ -518,7 +619,6 @@ void fused_start(gdf_fused* f, const uint16_t* const* depth, uint32_t B, const g
     S.lifetime = q.occupancy_lifetime;
     // every rank's split sizes (the partition's, written with the compaction) to pinned memory
     // (no wait here)
-    ++x.calls;
     x.all_gather(cnt, cntall, (size_t)4 * W * 4, kHalo, st);
     hipchk(hipMemcpyAsync(S.host, cntall, (size_t)4 * W * W * 4, hipMemcpyDeviceToHost, st),
            "hipMemcpyAsync(counts)");
@@ -599,7 +699,6 @@ void fused_finish(gdf_fused* f, int slot, uint32_t* send_counts, uint32_t* recv_
                                   hipMemcpyDeviceToDevice, st), "hipMemcpyAsync(run starts)");
         }
     if (W > 1) {
-        ++x.calls;
         x.group_start(kPoints);
         for (int q = 0; q < W; ++q) {
             if (q == R) continue;
@@ -636,7 +735,6 @@ void fused_finish(gdf_fused* f, int slot, uint32_t* send_counts, uint32_t* recv_
     gdfchk(gdf_voxelize_runs_marked(e, rp, rrk, rrs, (uint32_t)NS, pbase, rbase, S.average, uni, stride));
     if (W > 1) {  // (on the points' communicator: the finish's collectives stay in step order,
                   // never behind the next step's start collectives on the halo communicator)
-        ++x.calls;
         x.group_start(kPoints);
         for (uint32_t j = 0; j < S.nframes; ++j)
             x.all_gather(uni + j * stride + (uint64_t)R * Sw, uni + j * stride, Sw * 4, kPoints, st);
@@ -686,13 +784,14 @@ bool create_args_ok(gdf_engine* engine, const gdf_stream_camera* cams, gdf_fused
     return true;
 }
 
-// A failed step aborts the in-process world, so the other ranks' threads fail instead of waiting;
-// an argument error raised before the step issued any collective leaves the world usable.
+// ANY failed step aborts the in-process world, so the other ranks' threads fail at once instead of
+// waiting for this rank in a collective it will never issue (an argument error on ONE rank - its
+// peers already wait in the step's first round - is a failure of the world like any other; RCCL
+// ranks cannot be told, and their communicators stay usable only if every rank fails alike).
 template <class F>
 int step_guarded(gdf_fused* f, F&& fn) {
-    const uint64_t before = f->x ? f->x->calls : 0;
     const int rc = guarded(fn);
-    if (rc != GDF_OK && f->x && (rc != GDF_ERR_ARG || f->x->calls != before)) f->x->abort();
+    if (rc != GDF_OK && f->x) f->x->abort();
     return rc;
 }
 
@@ -753,6 +852,40 @@ int gdf_fused_local_create(int world, gdf_fused_local** out) {
         if (const char* v = std::getenv("GDF_LOCAL_TIMEOUT_S")) w->timeout_s = std::atof(v);
         *out = w;
     });
+}
+
+int gdf_fused_local_check_round(int world, const gdf_local_op* ops, const uint32_t* nops,
+                                const uint64_t* issue) {
+    if (world < 1 || world > 16 || !nops || !issue) {
+        gdf::set_last_error("local check: 1 <= world <= 16, nops and issue");
+        return GDF_ERR_ARG;
+    }
+    std::vector<std::vector<LocalOp>> lists(world);
+    std::vector<const std::vector<LocalOp>*> posts(world);
+    size_t at = 0;
+    for (int q = 0; q < world; ++q) {
+        for (uint32_t j = 0; j < nops[q]; ++j, ++at)
+            lists[q].push_back({ops[at].kind, ops[at].src, ops[at].dst, (size_t)ops[at].bytes, ops[at].peer});
+        posts[q] = &lists[q];
+    }
+    const std::string bad = check_round(world, posts, std::vector<uint64_t>(issue, issue + world));
+    if (bad.empty()) return GDF_OK;
+    gdf::set_last_error(bad);
+    return GDF_ERR_STATE;
+}
+
+int gdf_fused_local_check_arrival(int world, int rank, int comm, uint64_t round, uint64_t issue,
+                                  const int64_t* waiting) {
+    if (world < 1 || world > 16 || rank < 0 || rank >= world || comm < 0 || comm > 1 || !waiting) {
+        gdf::set_last_error("local check: 0 <= rank < world <= 16, comm 0 / 1, waiting");
+        return GDF_ERR_ARG;
+    }
+    std::vector<std::array<int64_t, 3>> wt(world);
+    for (int q = 0; q < world; ++q) wt[q] = {waiting[3 * q], waiting[3 * q + 1], waiting[3 * q + 2]};
+    const std::string bad = check_arrival(world, rank, comm, round, issue, wt);
+    if (bad.empty()) return GDF_OK;
+    gdf::set_last_error(bad);
+    return GDF_ERR_STATE;
 }
 
 int gdf_fused_local_destroy(gdf_fused_local* w) {

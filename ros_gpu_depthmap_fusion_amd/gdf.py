@@ -108,6 +108,13 @@ def cc_objects_as_dict(objs) -> dict:
                          else getattr(o, n) for o in objs]) for n in names}
 
 
+class LocalOp(C.Structure):
+    """gdf_local_op (include/gdf_fused.h): one operation of a local-transport round (kind 0
+    all-gather, 1 send, 2 receive)."""
+    _fields_ = [("kind", C.c_int), ("src", C.c_void_p), ("dst", C.c_void_p),
+                ("bytes", C.c_uint64), ("peer", C.c_int)]
+
+
 class GDFError(RuntimeError):
     def __init__(self, status: int, msg: str):
         super().__init__(f"{STATUS_NAMES.get(status, status)}: {msg}")
@@ -147,7 +154,7 @@ EXPORTED = [
     "gdf_fused_unique_id", "gdf_fused_create", "gdf_fused_destroy", "gdf_fused_halo_pixels",
     "gdf_fused_start", "gdf_fused_finish", "gdf_fused_run", "gdf_fused_local_create",
     "gdf_fused_local_destroy", "gdf_fused_create_local", "gdf_fused_info",
-    "gdf_fused_set_rollbuffer_shard",
+    "gdf_fused_set_rollbuffer_shard", "gdf_fused_local_check_round", "gdf_fused_local_check_arrival",
     # include/gdf_segment.h: the GPU object-segmentation front end
     "gdf_seg_create", "gdf_seg_destroy", "gdf_seg_set_stream", "gdf_seg_label_layers",
     "gdf_seg_label_engine_grid", "gdf_seg_get_counts", "gdf_seg_download_labels",
@@ -266,6 +273,8 @@ def load_library(path: str = LIB_PATH):
         "gdf_fused_create_local": (i32, [vp, vp, i32, i32, P(StreamCamera), u32, P(vp)]),
         "gdf_fused_info": (i32, [vp, P(i32), P(i32), P(i32), P(C.c_char_p)]),
         "gdf_fused_set_rollbuffer_shard": (i32, [vp, u32]),
+        "gdf_fused_local_check_round": (i32, [i32, P(LocalOp), P(u32), P(u64)]),
+        "gdf_fused_local_check_arrival": (i32, [i32, i32, i32, u64, u64, P(C.c_int64)]),
         "gdf_seg_create": (i32, [i32, P(vp)]),
         "gdf_seg_destroy": (i32, [vp]),
         "gdf_seg_set_stream": (i32, [vp, vp]),

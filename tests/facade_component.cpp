@@ -177,6 +177,23 @@ int main(int argc, char** argv) {
             glMemoryBarrier(GL_ALL_BARRIER_BITS);
             m_fusion->objectSegmentation();  // component.cpp:313-323
             m_fusion->objectTracking(0.1f);
+            // the two uncalled reference methods: the CPU layer connections equal the device's,
+            // and the rollbuffer check downloads the state the members report
+            const std::vector<uint8_t> dev_conn = m_fusion->m_ccLayersConnectionsData;
+            m_fusion->computeLayersConnectionsCPU();
+            if (m_fusion->m_ccLayersConnectionsData != dev_conn) {
+                std::fprintf(stderr, "frame %d: computeLayersConnectionsCPU differs from the device\n", f);
+                return 3;
+            }
+            m_fusion->checkAllPointSequenceBuffers();
+            uint32_t masked = 0;
+            for (uint32_t m : m_fusion->m_checkPointsMask) masked += m;
+            if (m_fusion->m_checkPoints.size() != 4 * (size_t)m_fusion->m_rollBufferNumPoints ||
+                m_fusion->m_checkSequences.size() != 4 * (size_t)m_fusion->m_rollBufferNumSeqs ||
+                (m_fusion->m_rollBufferNumPoints && !masked)) {
+                std::fprintf(stderr, "frame %d: checkAllPointSequenceBuffers\n", f);
+                return 4;
+            }
         }
         const std::string s = std::to_string(f);
         write_bin(out + "/points" + s + ".bin", reinterpret_cast<const float*>(m_fusion->m_points.data()),

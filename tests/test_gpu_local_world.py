@@ -231,6 +231,65 @@ def test_local_world_sharded_rollbuffer(world):
                  sharded=True) == 4
 
 
+def test_local_world_c5_sharded_full_window():
+    """SURVEY §8(d) C5 as BASELINE states it - 8 cameras x 3840x2160 at launch defaults WITH the
+    rollbuffer - through the product step at world 8: a window of 32 x 720p point sequences (29.5 M
+    points) sharded over the 8 ranks in blocks of ceil(31 / 7) = 5 (up to 2N = 16 sources per
+    voxelize), 3 single-frame steps (the window rolls from frame 1, the blocks rotate), 2 in
+    flight.  The reference's order: depth, then rollbuffer points at offset sum(P)
+    (src/gpu_depthmap_fusion.cpp:1509-1581), one voxelize (:1743-1756) - every fused cloud and
+    every rank's grid equal ONE unsharded oracle engine's, the shards' rollbuffer points add up."""
+    p = ComponentParams()
+    win, world = 32, 8
+    p.ps_timespan = (win - 0.5) / 30.0
+    rb = (1280, 720, win)
+    block = -(-(win - 1) // (world - 1))
+    cams, depths, res = run_local_world(world, 3840, 2160, 3, 1, p, depth=2, rb=rb, shard=block)
+    assert check("C5rb", world, 1, res, oracle_frames(cams, depths, p, rb=rb), rb=True,
+                 sharded=True) == 3
+
+
+def test_one_rank_bad_argument_aborts_the_world_at_once():
+    """One rank of a world-2 step is given a null depth map (GDF_ERR_ARG on that rank alone): its
+    peer, already waiting in the step's first collective, fails with GDF_ERR_STATE at once - not
+    after the transport's 300 s timeout (a failed step aborts the world whatever the error)."""
+    import ctypes as C
+    import time
+    from ros_gpu_depthmap_fusion_amd import build_library, hiprt
+    from ros_gpu_depthmap_fusion_amd.gdf import GPUDepthmapFusion
+    from ros_gpu_depthmap_fusion_amd.multi import LocalFusedWorld, NativeFusedRank
+    build_library()
+    p = small_params(4)
+    cams = [synth.make_camera(k, 160, 120) for k in range(2)]
+    d = [hiprt.DeviceArray.from_numpy(synth.dense_frame(cams[k], k, 0)) for k in range(2)]
+    lw = LocalFusedWorld(2)
+    engines = [GPUDepthmapFusion(0) for _ in range(2)]
+    ranks = [NativeFusedRank(engines[r], cams, r, 2, p, local=lw) for r in range(2)]
+
+    def body(r):
+        fr = ranks[r]
+        arr = (C.c_void_p * 1)(d[r].ptr if r == 0 else None)
+        k = C.c_int()
+        if r == 1:
+            time.sleep(0.5)  # (rank 0 is waiting in the halo all-gather by now)
+        t0 = time.time()
+        rc = fr._lib.gdf_fused_start(fr._h, arr, 1, C.byref(fr.pc), C.byref(k))
+        return rc, fr._lib.gdf_last_error().decode(), time.time() - t0
+
+    try:
+        res = lw.run(body, timeout=120)
+    finally:
+        for e in engines:
+            e.synchronize()
+        for fr in ranks:
+            fr.close()
+        lw.close()
+    (rc0, msg0, t0), (rc1, msg1, _) = res
+    assert rc1 == -1 and "null depth map" in msg1, (rc1, msg1)
+    assert rc0 == -2 and "aborted" in msg0 and "rank 1 failed" in msg0, (rc0, msg0)
+    assert t0 < 30, f"rank 0 waited {t0:.1f} s"
+
+
 def test_fused_start_rejects_batched_rollbuffer_frame():
     """gdf_fused_start with nframes > 1 and a move transform fails with GDF_ERR_ARG (a batch has no
     rollbuffer frame; the window's points must not be dropped silently)."""
