@@ -163,20 +163,21 @@ def roofline_from(ktimes, kt_steps, mb, pmc_key):
     avg_s = max(raw_s - 0.5 * floor_s, 1e-9)
     achieved = mb[slot] / avg_s / 1e9
     traffic, traffic_src = None, None
-    rec = pmc_record(pmc_key).get(slot)
+    allrec = pmc_record(pmc_key)
+    rec = slot_pmc(allrec, slot)
     if rec:
-        traffic = rec.get("hbm_bytes_per_launch")
-        traffic_src = {"kernels": rec.get("kernels"), "dispatches": rec.get("dispatches"),
+        traffic = rec["hbm_bytes_per_launch"]
+        traffic_src = {"kernels": rec["kernels"], "dispatches": rec["dispatches"],
                        "source": "profiles/pmc_traffic.json[%s]" % pmc_key}
-    # every timed kernel's PMC traffic against its byte model (profiles/pmc_traffic.json, one
+    # every timed slot's PMC traffic against its byte model (profiles/pmc_traffic.json, one
     # batch in flight): > 1 = bytes the model does not count (partial-sector writes, re-reads)
     pk_traffic = {}
-    allrec = pmc_record(pmc_key)
     for k in singles:
-        r = allrec.get(k)
+        r = slot_pmc(allrec, k)
         if r and mb.get(k):
-            pk_traffic[k] = {"model_bytes": round(mb[k]), "pmc_bytes": r.get("hbm_bytes_per_launch"),
-                             "ratio": round(r.get("hbm_bytes_per_launch", 0) / mb[k], 3)}
+            pk_traffic[k] = {"model_bytes": round(mb[k]), "pmc_bytes": r["hbm_bytes_per_launch"],
+                             "ratio": round(r["hbm_bytes_per_launch"] / mb[k], 3),
+                             "kernels": r["kernels"]}
     valu = None
     sq = os.path.join(ROOT, "profiles", "pmc_sq.json")
     if slot == "mask" and os.path.exists(sq):
@@ -207,6 +208,27 @@ def roofline_from(ktimes, kt_steps, mb, pmc_key):
         "per_kernel_us": {k: round(ktimes[k][0] * 1e3 / ktimes[k][1], 3) for k in singles},
         "per_kernel_traffic": pk_traffic or None,
     }
+
+
+# the kernels an event-timed slot brackets (the engine's HookScope in gdf_kernels.hip): the group
+# slot is the whole group phase - the tile count, the staged groups and the queued long groups
+SLOT_PMC = {"group": ("group", "group_count", "group_big"), "scan": ("scan", "scan_reduce")}
+
+
+def slot_pmc(allrec, slot):
+    """PMC bytes per launch of a timed SLOT: the bytes of every kernel the slot brackets, per
+    dispatch of its main kernel ({} when none was recorded)."""
+    base = allrec.get(slot)
+    if not base or not base.get("dispatches"):
+        return {}
+    tot, kernels = 0.0, []
+    for k in SLOT_PMC.get(slot, (slot,)):
+        r = allrec.get(k)
+        if r and r.get("dispatches"):
+            tot += r["hbm_bytes_per_launch"] * r["dispatches"]
+            kernels += r.get("kernels") or [k]
+    return {"hbm_bytes_per_launch": round(tot / base["dispatches"]), "kernels": kernels,
+            "dispatches": base["dispatches"]}
 
 
 def pmc_record(pmc_key):

@@ -230,6 +230,13 @@ int gdf_set_rollbuffer_shard(gdf_engine* engine, uint32_t shard, uint32_t nshard
  * selected sequence; shards holding none follow in shard order).  GDF_ERR_STATE when a shard
  * holds two separate pieces of the selection (the window spans more than nshards blocks). */
 int gdf_get_rollbuffer_shard_order(gdf_engine* engine, uint32_t* order, uint32_t nshards);
+/* The pieces of the selected window in the selection's order (after the frame's selection): a
+ * piece is a maximal stretch of selected sequences with points held by one shard; owners[i] = the
+ * shard holding piece i.  *count = the number of pieces (GDF_ERR_CAPACITY when it exceeds
+ * capacity).  A shard's rollbuffer points are its pieces in this order; with a window spanning
+ * more than nshards blocks a shard holds several (the fused step cuts them apart, gdf_fused.h).
+ * Unsharded: one piece, owner 0. */
+int gdf_get_rollbuffer_pieces(gdf_engine* engine, uint32_t* owners, uint32_t capacity, uint32_t* count);
 
 /* ---- depth chain ------------------------------------------------------------------------ */
 int gdf_upload_depthmaps(gdf_engine* engine);                            /* :1583-1593 */
@@ -422,13 +429,15 @@ int gdf_partition_runs(gdf_engine* engine, uint32_t nparts, float* send_points_d
 int gdf_set_emit_partition(gdf_engine* engine, uint32_t nparts, float* send_points_device,
                            uint32_t* send_run_keys_device, uint32_t* send_run_starts_device,
                            uint32_t capacity, uint32_t* part_counts_device);
-/* nseg = 2 for the armed frame: each part is cut into two buckets, [the frame's depth points | its
- * selected rollbuffer points] (bucket b = part * 2 + segment, bucket-major send lists, run starts
- * relative to the bucket's first point, part_counts [2 nparts points | 2 nparts runs]): the
- * multi-GPU step places the rollbuffer segments of the ranks behind every rank's depth points
- * (the reference's buffer order, fusion.cpp:1509-1581).  A frame without a selection keeps this
- * layout with every segment-1 bucket empty (the compaction writes the counts so).  Disarmed (1)
- * with the emit partition. */
+/* nseg (1..4, nparts * nseg <= 32) for the armed frame: each part is cut into nseg buckets,
+ * [the frame's depth points | the pieces of the selection this engine holds, in order] (bucket
+ * b = part * nseg + segment, bucket-major send lists, run starts relative to the bucket's first
+ * point, part_counts [nseg nparts points | nseg nparts runs]; a sharded window's shard holding
+ * more pieces than nseg - 1 fails the frame with GDF_ERR_STATE, on every shard alike): the
+ * multi-GPU step places the ranks' rollbuffer pieces behind every rank's depth points, in the
+ * selection's order (the reference's buffer order, fusion.cpp:1509-1581).  A frame without a
+ * selection keeps this layout with every rollbuffer bucket empty (the compaction writes the counts
+ * so).  Disarmed (1) with the emit partition. */
 int gdf_set_partition_segments(gdf_engine* engine, uint32_t nseg);
 /* Whether a deferred frame armed with gdf_set_emit_partition sets its occupancy marks (default 1).
  * 0: a caller that builds the union from gdf_voxelize_runs_marked skips the compaction's marks

@@ -103,11 +103,14 @@ int gdf_fused_info(gdf_fused* rank, int* rank_out, int* world, int* transport_ra
  * engine, same order) and keeps the points of the sequences k with (k / block) % world == rank
  * (gdf_set_rollbuffer_shard); a rollbuffer step (nframes == 1, move transform) then selects, on
  * every rank, its share of the window, and the exchange carries two buckets per key range - the
- * rank's depth points, its rollbuffer points - which each owner places as [every rank's depth
- * points, the rollbuffer segments in the selection's order] (the reference's buffer, fusion.cpp
- * :1509-1581, restricted to the key range).  The window may span at most `world` blocks (else the
- * step fails: GDF_ERR_STATE); block = ceil((window - 1) / (world - 1)) sequences guarantees it.
- * Call before the first sequence is added. */
+ * rank's depth points, then the pieces of the window it holds (a piece: a stretch of selected
+ * sequences on one rank; gdf_get_rollbuffer_pieces) - which each owner places as [every rank's
+ * depth points, the pieces in the selection's order] (the reference's buffer, fusion.cpp
+ * :1509-1581, restricted to the key range).  A window spanning at most `world` blocks gives one
+ * piece per rank (block = ceil((window - 1) / (world - 1)) sequences guarantees it); a longer one
+ * (a burst of sequences) gives a rank several, up to min(3, 32 / world - 1) - beyond that the step
+ * fails on every rank alike (GDF_ERR_STATE), before any rank's points move.  Call before the
+ * first sequence is added. */
 int gdf_fused_set_rollbuffer_shard(gdf_fused* rank, uint32_t block);
 
 /* Depth values of the halo every rank sends (max over cameras of F * width + F). */

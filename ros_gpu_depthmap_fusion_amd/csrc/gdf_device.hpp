@@ -54,7 +54,8 @@ constexpr int kSumChunk = 128;                               // points per wave 
 constexpr uint32_t kSpinLimit = 1u << 26;                   // bounded look-back spins
 constexpr uint32_t kDilateMaxF = 16;                        // mask_dilate window radius limit
 constexpr uint32_t kMaxParts = 16;                          // ranks of the fused-cloud partition
-constexpr uint32_t kMaxBuckets = 2 * kMaxParts;             // parts x segments [depth | rollbuffer]
+constexpr uint32_t kMaxBuckets = 2 * kMaxParts;             // parts x segments, <= 32 (wave ballots)
+constexpr uint32_t kMaxSegs = 4;                            // segments [depth | <= 3 rollbuffer pieces]
 constexpr uint32_t kMaxSources = 2 * kMaxParts;             // received segments of gdf_voxelize_runs
 
 // Device-wide counters: monotonically increasing tile tickets (the host passes each launch's
@@ -141,6 +142,12 @@ struct FrameArgs {
     uint32_t* sel_ctr;          // tile tickets
     uint32_t* epoch_word;       // look-back epoch (shared with the voxelize launches)
     uint32_t* final_count;      // depth + rollbuffer survivors (out_count then holds the depth part)
+    // the partition's segment cuts (sharded windows: the pieces of the selection this rank holds):
+    // sel_splits[0] = depth survivors, sel_splits[1 + c] = survivors before selected item
+    // sel_cut_at[c] (c < sel_ncuts), the frame's total for the unused cuts (kMaxSegs - 1 words)
+    uint32_t* sel_splits;
+    uint32_t sel_ncuts;
+    uint32_t sel_cut_at[kMaxSegs - 2];
     // voxel keys + occupancy marks (compute_voxel_coords + voxel_grid_occupancy_of_points)
     int32_t do_voxel;
     float vlo[3], vcs[3], gmax[3];
@@ -201,8 +208,9 @@ struct FrameArgs {
     uint32_t* part_run_keys;
     uint32_t* part_run_starts;
     uint32_t* part_counts;      // [2 * nparts]: points, then runs per part (device)
-    // 2: the counts in the 2-segment layout [points of (part p, segment s) at 2 p + s | runs at
-    // 2 P + 2 p + s] with segment 1 (a selection's rollbuffer points) empty - a frame without one
+    // > 1: the counts in the nseg-segment layout [points of (part p, segment s) at nseg p + s |
+    // runs at nseg P + nseg p + s] with segments 1.. (a selection's rollbuffer pieces) empty - a
+    // frame without one
     uint32_t part_nseg;
 };
 static_assert(sizeof(FrameArgs) <= 4096, "kernel arguments are limited to 4 KiB");

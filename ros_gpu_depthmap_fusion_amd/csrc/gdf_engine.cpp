@@ -296,7 +296,9 @@ bool ros_time_minus(uint32_t sec, uint32_t nsec, double seconds, uint32_t* os, u
 enum MiscSlot {
     kCount = 0, kTileCtr = 1, kErr = 2, kVoxCount = 3, kGridTicket = 4, kDepthCount = 5,
     kSelTotal = 6, kPartTotal = 7, kRecvCount = 8, kRunCount = 9, kScanTotal = 10, kRunTotal = 11,
-    kRecvRuns = 12, kDeltaCount = 13, kMiscWords = 16
+    kRecvRuns = 12, kDeltaCount = 13,
+    kSplit0 = 16,  // [kMaxSegs - 1] the partition's segment cuts of a rollbuffer frame (k_sel)
+    kMiscWords = 20
 };
 
 }  // namespace
@@ -493,6 +495,9 @@ struct gdf_engine {
     bool prepared = false, sel_inserted = false;
     DevBuf d_seg_start, d_seg_tf, d_tfw, d_tfc;
     uint32_t nseg = 0;
+    // a sharded window: where the 2nd, 3rd .. piece of the selection this shard holds starts
+    // (selected-item index), the partition cutting its rollbuffer points there
+    std::vector<uint32_t> sel_cuts;
 
     // deferred depth plan
     bool converted = false, flying_set = false, crop_set = false;
@@ -549,7 +554,7 @@ struct gdf_engine {
         uint32_t nparts = 0, cap = 0;
         float* pts = nullptr;
         uint32_t *run_keys = nullptr, *run_starts = nullptr, *counts = nullptr;
-        uint32_t nseg = 1;  // gdf_set_partition_segments: 2 = [depth | rollbuffer] buckets
+        uint32_t nseg = 1;  // gdf_set_partition_segments: [depth | rollbuffer pieces] buckets
     } epart;
     bool emit_part = !getenv("GDF_NO_EMIT_PART");  // (else: compaction, then the partition pass)
     // a frame armed with gdf_set_emit_partition sets its occupancy marks (gdf_set_partition_marks:
@@ -930,6 +935,17 @@ void select_timespan(gdf_engine* e, uint32_t mins, uint32_t minn, uint32_t maxs,
         }
     }
     const int64_t count = last < start ? 0 : 1 + last - start;
+    // a sharded window is the unsharded one spread over the shards only when the selected
+    // sequences are the contiguous run [start, last] (time-ordered headers, as a sensor's are):
+    // an unselected sequence with points inside it would shift each shard's point range differently
+    if (e->nshards > 1)
+        for (int64_t i = start; i <= last && i < (int64_t)e->hdrB.size(); ++i) {
+            const Hdr& q = e->hdrB[i];
+            if (q.num_global && !(compare_time(mins, minn, q.sec, q.nsec) <= 0 &&
+                                  compare_time(q.sec, q.nsec, maxs, maxn) <= 0))
+                fail(GDF_ERR_STATE, "sharded rollbuffer: the selected sequences are not contiguous "
+                                    "(point sequences out of time order)");
+        }
     for (int64_t i = 0; i < start && i < (int64_t)e->hdrB.size(); ++i) pstart += e->hdrB[i].num;
     e->rb.selection_point_start = pstart;
     e->rb.selection_point_count = pcount;
@@ -954,6 +970,34 @@ void insert_selected(gdf_engine* e, const float* Twm, const float* Tcm) {  // fu
     if ((uint64_t)e->depth_total + cnt > e->sl().n_total) fail(GDF_ERR_STATE, "selection exceeds prepared buffers");
     if (cnt && (uint64_t)ps + cnt > e->rb.num_points) fail(GDF_ERR_STATE, "selection exceeds rollbuffer points");
     if (sc && (uint64_t)ss + sc > e->hdrB.size()) fail(GDF_ERR_STATE, "selection exceeds rollbuffer sequences");
+    e->sel_cuts.clear();
+    if (e->nshards > 1 && sc) {
+        // the selection's pieces: maximal stretches of selected sequences (with points) held by one
+        // shard, in order; this shard's rollbuffer points are cut where its 2nd, 3rd .. piece
+        // starts (the exchange places every piece at its place in the unsharded order).  Every
+        // shard sees the same headers, so every shard accepts or rejects the window alike.
+        std::vector<uint32_t> pieces(e->nshards, 0);
+        int64_t cur = -1;
+        uint64_t own = 0;
+        for (uint32_t j = ss; j < ss + sc; ++j) {
+            const Hdr& h = e->hdrB[j];
+            if (!h.num_global) continue;
+            const int64_t k = (int64_t)((h.id / e->shard_block) % e->nshards);
+            if (k != cur) {
+                if (k == (int64_t)e->shard && pieces[k]) e->sel_cuts.push_back((uint32_t)own);
+                ++pieces[k];
+                cur = k;
+            }
+            if (k == (int64_t)e->shard) own += h.num;
+        }
+        const uint32_t most = *std::max_element(pieces.begin(), pieces.end());
+        const uint32_t room = std::min<uint32_t>(kMaxSegs, std::max<uint32_t>(e->epart.nseg, 2u)) - 1u;
+        if (most > room)
+            fail(GDF_ERR_STATE, "sharded rollbuffer: a shard holds " + std::to_string(most) +
+                                " separate pieces of the selected window, the exchange carries " +
+                                std::to_string(room) + " (raise the block size: the window spans " +
+                                "too many blocks)");
+    }
     if (cnt == 0) {  // nothing selected: the frame kernels read no selection table
         e->nseg = 0;
         e->sel_inserted = true;
@@ -1352,6 +1396,11 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel, bool compaction_marks = fa
     a.seg_tf = e->d_seg_tf.as<uint32_t>();
     a.tfw = e->d_tfw.as<float>();
     a.tfc = e->d_tfc.as<float>();
+    if (a.sel_tiles) {  // (the partition's segment cuts: depth | the pieces of the selection)
+        a.sel_splits = e->sl().d_misc.as<uint32_t>() + kSplit0;
+        a.sel_ncuts = (uint32_t)std::min<size_t>(e->sel_cuts.size(), kMaxSegs - 2);
+        for (uint32_t c = 0; c < a.sel_ncuts; ++c) a.sel_cut_at[c] = e->sel_cuts[c];
+    }
     a.do_voxel = fused_voxel ? 1 : 0;
     e->sl().group_marks = fused_voxel && a.sel_tiles && !compaction_marks;
     if (fused_voxel) {
@@ -1955,8 +2004,9 @@ int guarded(gdf_engine* e, F&& f) {
         }                                                                   \
     } while (0)
 
-// nseg = 2: buckets [depth | rollbuffer] per part (the compacted depth points are the first
-// kDepthCount items of a frame with selected rollbuffer points, all of them otherwise)
+// nseg > 1: buckets [depth | rollbuffer pieces] per part (a frame with selected rollbuffer points
+// is cut where k_sel recorded it, kSplit0..: its depth points, then the pieces of the selection
+// this rank holds; any other frame is all depth)
 void partition_runs(gdf_engine* e, uint32_t nparts, float* send_pts, uint32_t* send_run_keys,
                     uint32_t* send_run_starts, uint32_t capacity, uint32_t* part_counts,
                     uint32_t nseg = 1) {
@@ -1964,15 +2014,15 @@ void partition_runs(gdf_engine* e, uint32_t nparts, float* send_pts, uint32_t* s
         Slot& q = e->sl();
         if (!e->grid_set || !q.coords_valid) fail(GDF_ERR_STATE, "partition needs the voxel keys of a frame");
         if (nparts == 0 || nparts > kMaxParts) fail(GDF_ERR_ARG, "partition: 1..16 parts");
-        if (nseg != 1 && nseg != 2) fail(GDF_ERR_ARG, "partition: 1 or 2 segments");
+        if (nseg == 0 || nseg > kMaxSegs || nparts * nseg > kMaxBuckets)
+            fail(GDF_ERR_ARG, "partition: 1..4 segments, parts x segments <= 32");
         if (!send_pts || !send_run_keys || !send_run_starts || !part_counts)
             fail(GDF_ERR_ARG, "partition: null buffer");
         if (capacity < q.n_total) fail(GDF_ERR_CAPACITY, "partition: send buffers smaller than the frame");
         ensure_misc(e);
         const uint32_t nmax = std::max<uint32_t>(q.n_total, 1);
         const uint32_t m = 2 * nparts * nseg * std::max<uint32_t>(part_tiles(nmax), 1u);
-        const uint32_t* split = nseg == 2 ? q.d_misc.as<uint32_t>() + (q.sel_frame ? kDepthCount : kCount)
-                                          : nullptr;
+        const uint32_t* split = q.d_misc.as<uint32_t>() + (q.sel_frame ? kSplit0 : kCount);
         q.d_pcnt.ensure((size_t)m * 4);
         q.d_poff.ensure(seg_offsets_words(m) * 4);
         HIPCHK(launch_partition(q.d_pts.as<float4>(), q.d_coords.as<uint32_t>(),
@@ -1982,7 +2032,7 @@ void partition_runs(gdf_engine* e, uint32_t nparts, float* send_pts, uint32_t* s
                                 reinterpret_cast<float4*>(send_pts), nullptr, part_counts, e->s(),
                                 q.nframes > 1 ? q.d_fstart.as<uint32_t>() : nullptr, q.nframes,
                                 q.nframes > 1 ? e->key_bits : 0u, send_run_keys, send_run_starts,
-                                split));
+                                split, nseg - 1, q.sel_frame ? 1u : 0u));
     }
 }
 
@@ -2375,6 +2425,28 @@ int gdf_get_rollbuffer_shard_order(gdf_engine* e, uint32_t* order, uint32_t nsha
             return fa < fb;
         });
         std::copy(idx.begin(), idx.end(), order);
+    });
+}
+
+int gdf_get_rollbuffer_pieces(gdf_engine* e, uint32_t* owners, uint32_t capacity, uint32_t* count) {
+    ENGINE_OR_FAIL(e);
+    if (!count || (capacity && !owners)) return GDF_ERR_ARG;
+    return guarded(e, [&] {
+        const uint32_t ss = e->rb.selection_sequence_start, sc = e->rb.selection_sequence_count;
+        if (sc && (uint64_t)ss + sc > e->hdrB.size()) fail(GDF_ERR_STATE, "selection exceeds rollbuffer sequences");
+        uint32_t n = 0;
+        int64_t cur = -1;
+        for (uint32_t j = ss; j < ss + sc; ++j) {
+            const Hdr& h = e->hdrB[j];
+            if (!h.num_global) continue;  // (no points on any shard)
+            const int64_t k = (int64_t)((h.id / e->shard_block) % e->nshards);
+            if (k == cur) continue;
+            if (n < capacity) owners[n] = (uint32_t)k;
+            ++n;
+            cur = k;
+        }
+        *count = n;
+        if (n > capacity) fail(GDF_ERR_CAPACITY, "rollbuffer pieces: more pieces than capacity");
     });
 }
 
@@ -2835,7 +2907,7 @@ int gdf_set_emit_partition(gdf_engine* e, uint32_t nparts, float* send_pts, uint
 int gdf_set_partition_segments(gdf_engine* e, uint32_t nseg) {
     ENGINE_OR_FAIL(e);
     return guarded(e, [&] {
-        if (nseg != 1 && nseg != 2) fail(GDF_ERR_ARG, "partition segments: 1 or 2");
+        if (nseg == 0 || nseg > kMaxSegs) fail(GDF_ERR_ARG, "partition segments: 1..4");
         e->epart.nseg = nseg;
     });
 }

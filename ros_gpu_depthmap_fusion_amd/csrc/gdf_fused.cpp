@@ -471,17 +471,23 @@ struct DevBuf {
     }
 };
 
+constexpr uint32_t kSegMax = 4;   // partition segments per key range (gdf_set_partition_segments)
+constexpr uint32_t kSrcMax = 32;  // sources of one voxelize (gdf_voxelize_runs_marked)
+
 struct SlotX {
     DevBuf tail, tails;       // this rank's halo tails, every rank's (all-gather)
     DevBuf gathered;          // the union of the step's marks: frame f at f * W * S words, rank
                               // j's key range in words [j S, (j + 1) S) (voxelize + all-gather)
-    // partitioned send lists (points, run keys, run starts) in buckets b = 2 part + segment
-    // (segment 0: the rank's depth points, 1: its selected rollbuffer points); the split sizes
-    // record [points per bucket (2 W) | runs per bucket (2 W)] (cnt), every rank's (cntall), and
+    // partitioned send lists (points, run keys, run starts) in buckets b = nseg part + segment
+    // (segment 0: the rank's depth points, 1..: the pieces of the selected window it holds, in
+    // order); the split sizes record [points per bucket (nseg W) | runs per bucket (nseg W)]
+    // (cnt), every rank's (cntall), and
     DevBuf sp, srk, srs, cnt, cntall;
     DevBuf rp, rrk, rrs;      // received lists
-    uint32_t* host = nullptr;  // pinned copy of cntall (world x 4 world)
-    uint32_t order[16] = {};   // the ranks' rollbuffer segments in the selection's order
+    uint32_t* host = nullptr;  // pinned copy of cntall (world x 2 nseg world)
+    // the rollbuffer sources in the selection's order: (rank, segment) per piece
+    uint8_t piece_rank[kSrcMax] = {}, piece_seg[kSrcMax] = {};
+    uint32_t npieces = 0;
     hipEvent_t ev = nullptr;
     bool pending = false;
     int average = 1;  // the step's voxel_average
@@ -500,6 +506,9 @@ struct gdf_fused {
     std::vector<gdf_stream_camera> cams;
     uint32_t F = 0, Lmax = 0;
     uint32_t shard_block = 0;  // > 0: the rollbuffer window sharded over the ranks
+    // segments per key range: [depth | up to nseg - 1 pieces of the window per rank] (W nseg <= 32
+    // buckets: 4 up to 8 ranks, 2 at 16)
+    uint32_t nseg = 2;
     SlotX slots[kSlots];
 
     ~gdf_fused() {
@@ -582,8 +591,9 @@ void fused_start(gdf_fused* f, const uint16_t* const* depth, uint32_t B, const g
     const bool rb = B == 1 && q.move_transform_available;
     // the send lists, written by the compaction itself (gdf_set_emit_partition): sized for the
     // step's pixels (+ halo) plus, on a rollbuffer rank, every point the window can select
-    uint32_t* cnt = S.cnt.ensure<uint32_t>((size_t)4 * W * 4, st);
-    uint32_t* cntall = S.cntall.ensure<uint32_t>((size_t)4 * W * W * 4, st);
+    const size_t rec = (size_t)2 * f->nseg * W;  // words of a rank's split-size record
+    uint32_t* cnt = S.cnt.ensure<uint32_t>(rec * 4, st);
+    uint32_t* cntall = S.cntall.ensure<uint32_t>(rec * W * 4, st);
     size_t want = (size_t)B * c.width * c.height + (halo && R > 0 ? B * (size_t)f->Lmax : 0u);
     if (rb) {  // + the window after the ingest
         gdf_rollbuffer_state rs{};
@@ -599,18 +609,37 @@ void fused_start(gdf_fused* f, const uint16_t* const* depth, uint32_t B, const g
         const uint32_t have = (uint32_t)std::min<size_t>({S.sp.cap / 16, S.srk.cap / 4, S.srs.cap / 4});
         gdfchk(gdf_set_emit_partition(e, W, S.sp.as<float>(), S.srk.as<uint32_t>(),
                                       S.srs.as<uint32_t>(), have, cnt));
-        // buckets [depth | rollbuffer] per part: the record's layout itself (a frame without a
-        // selection: segment 1 empty, written by the compaction)
-        gdfchk(gdf_set_partition_segments(e, 2));
+        // buckets [depth | rollbuffer pieces] per part: the record's layout itself (a frame without
+        // a selection: the rollbuffer segments empty, written by the compaction)
+        gdfchk(gdf_set_partition_segments(e, f->nseg));
     };
     arm(std::max<size_t>(want, 1));
     gdfchk(gdf_set_partition_marks(e, 0));
     gdf_frame_result res{};
     gdfchk(gdf_process_frame(e, &q, &res));
-    // the ranks' rollbuffer segments in the selection's order (the same on every rank: the
-    // headers are replicated); unsharded, only the last rank's is non-empty
-    for (int k = 0; k < W; ++k) S.order[k] = (uint32_t)k;
-    if (sharded && rb) gdfchk(gdf_get_rollbuffer_shard_order(e, S.order, (uint32_t)W));
+    // the rollbuffer sources in the selection's order (the same on every rank: the headers are
+    // replicated): sharded, piece i of the window is the next segment of the rank holding it;
+    // unsharded, segment 1 of every rank, only the last rank's non-empty
+    S.npieces = 0;
+    if (sharded && rb) {
+        uint32_t owners[kSrcMax], n = 0, next[16] = {};
+        gdfchk(gdf_get_rollbuffer_pieces(e, owners, kSrcMax, &n));
+        if ((uint64_t)W + n > kSrcMax) fail(GDF_ERR_STATE, "fused start: more window pieces than sources");
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint32_t q = owners[i];
+            if (q >= (uint32_t)W || ++next[q] >= f->nseg)
+                fail(GDF_ERR_STATE, "fused start: a rank holds more window pieces than segments");
+            S.piece_rank[i] = (uint8_t)q;
+            S.piece_seg[i] = (uint8_t)next[q];
+        }
+        S.npieces = n;
+    } else {
+        for (int q = 0; q < W; ++q) {
+            S.piece_rank[q] = (uint8_t)q;
+            S.piece_seg[q] = 1;
+        }
+        S.npieces = (uint32_t)W;
+    }
     // The compaction sets no marks (gdf_set_partition_marks(e, 0) before the frame): W full
     // bitmasks of B frames (3.4 MB per rank and step at VGA x 8, received W - 1 times) would travel;
     // instead the key-range voxelize of the finish marks every voxel of its range - whole mark
@@ -619,8 +648,8 @@ void fused_start(gdf_fused* f, const uint16_t* const* depth, uint32_t B, const g
     S.lifetime = q.occupancy_lifetime;
     // every rank's split sizes (the partition's, written with the compaction) to pinned memory
     // (no wait here)
-    x.all_gather(cnt, cntall, (size_t)4 * W * 4, kHalo, st);
-    hipchk(hipMemcpyAsync(S.host, cntall, (size_t)4 * W * W * 4, hipMemcpyDeviceToHost, st),
+    x.all_gather(cnt, cntall, rec * 4, kHalo, st);
+    hipchk(hipMemcpyAsync(S.host, cntall, rec * W * 4, hipMemcpyDeviceToHost, st),
            "hipMemcpyAsync(counts)");
     hipchk(hipEventRecord(S.ev, st), "hipEventRecord");
     S.average = q.voxel_average ? 1 : 0;
@@ -640,28 +669,33 @@ void fused_finish(gdf_fused* f, int slot, uint32_t* send_counts, uint32_t* recv_
     hipStream_t st = static_cast<hipStream_t>(sv);
     hipchk(hipEventSynchronize(S.ev), "hipEventSynchronize");  // (the later slots keep the GPU busy)
     const int W = f->world, R = f->rank;
-    // rank q's record: host[q * 4W + 2 p + s] points of bucket (part p, segment s),
-    // host[q * 4W + 2W + 2 p + s] its runs
-    auto pts_of = [&](int from, int to, int sg) -> uint64_t { return S.host[(size_t)from * 4 * W + 2 * to + sg]; };
-    auto runs_of = [&](int from, int to, int sg) -> uint64_t {
-        return S.host[(size_t)from * 4 * W + 2 * W + 2 * to + sg];
+    // rank q's record: host[q * rec + nseg p + s] points of bucket (part p, segment s),
+    // host[q * rec + nseg W + nseg p + s] its runs
+    const uint32_t NSg = f->nseg;
+    const size_t rec = (size_t)2 * NSg * W;
+    auto pts_of = [&](int from, int to, uint32_t sg) -> uint64_t { return S.host[(size_t)from * rec + NSg * to + sg]; };
+    auto runs_of = [&](int from, int to, uint32_t sg) -> uint64_t {
+        return S.host[(size_t)from * rec + (size_t)NSg * W + NSg * to + sg];
     };
     // sources in the reference's buffer order: every rank's depth points (rank order = camera
-    // order), then the rollbuffer segments in the selection's order (fusion.cpp:1509-1581)
-    const int NS = 2 * W;
-    int src_rank[32], src_seg[32];
+    // order), then the rollbuffer pieces in the selection's order (fusion.cpp:1509-1581)
+    const int NS = W + (int)S.npieces;
+    if (NS > (int)kSrcMax) fail(GDF_ERR_STATE, "fused finish: too many sources");
+    int src_rank[kSrcMax], src_seg[kSrcMax];
     for (int q = 0; q < W; ++q) {
         src_rank[q] = q;
         src_seg[q] = 0;
-        src_rank[W + q] = (int)S.order[q];
-        src_seg[W + q] = 1;
     }
-    uint32_t pbase[33], rbase[33];
+    for (uint32_t i = 0; i < S.npieces; ++i) {
+        src_rank[W + i] = S.piece_rank[i];
+        src_seg[W + i] = S.piece_seg[i];
+    }
+    uint32_t pbase[kSrcMax + 1], rbase[kSrcMax + 1];
     uint64_t n = 0, nr = 0;
-    uint64_t recv_at[16][2] = {}, rrecv_at[16][2] = {};  // where rank q's segment s lands
+    uint64_t recv_at[16][kSegMax] = {}, rrecv_at[16][kSegMax] = {};  // where rank q's segment s lands
     for (int k = 0; k < NS; ++k) {
         const int q = src_rank[k], sg = src_seg[k];
-        if (q < 0 || q >= W) fail(GDF_ERR_STATE, "fused finish: bad rollbuffer segment order");
+        if (q < 0 || q >= W || sg < 0 || sg >= (int)NSg) fail(GDF_ERR_STATE, "fused finish: bad rollbuffer piece");
         pbase[k] = (uint32_t)n;
         rbase[k] = (uint32_t)nr;
         recv_at[q][sg] = n;
@@ -672,15 +706,23 @@ void fused_finish(gdf_fused* f, int slot, uint32_t* send_counts, uint32_t* recv_
     }
     pbase[NS] = (uint32_t)n;
     rbase[NS] = (uint32_t)nr;
+    // every bucket that carries points is a source (a rank's pieces are exactly its non-empty
+    // rollbuffer segments)
+    for (int q = 0; q < W; ++q)
+        for (uint32_t sg = 1; sg < NSg; ++sg) {
+            bool listed = false;
+            for (int k = W; k < NS; ++k) listed |= src_rank[k] == q && src_seg[k] == (int)sg;
+            if (!listed && pts_of(q, R, sg)) fail(GDF_ERR_STATE, "fused finish: a rollbuffer bucket outside the pieces");
+        }
     float* rp = S.rp.ensure<float>(std::max<uint64_t>(n, 1) * 16, st);
     uint32_t* rrk = S.rrk.ensure<uint32_t>(std::max<uint64_t>(nr, 1) * 4, st);
     uint32_t* rrs = S.rrs.ensure<uint32_t>((nr + 1) * 4, st);
     // this rank's send list: bucket-major, bucket (q, s) at the sum of the buckets before it
-    uint64_t send_at[16][2] = {}, rsend_at[16][2] = {};
+    uint64_t send_at[16][kSegMax] = {}, rsend_at[16][kSegMax] = {};
     {
         uint64_t o = 0, ro = 0;
         for (int q = 0; q < W; ++q)
-            for (int sg = 0; sg < 2; ++sg) {
+            for (uint32_t sg = 0; sg < NSg; ++sg) {
                 send_at[q][sg] = o;
                 rsend_at[q][sg] = ro;
                 o += pts_of(R, q, sg);
@@ -688,7 +730,7 @@ void fused_finish(gdf_fused* f, int slot, uint32_t* send_counts, uint32_t* recv_
             }
     }
     // the rank's own buckets: device copies (an RCCL self send / recv is a slower kernel copy)
-    for (int sg = 0; sg < 2; ++sg)
+    for (uint32_t sg = 0; sg < NSg; ++sg)
         if (const size_t c = pts_of(R, R, sg)) {
             const size_t rc = runs_of(R, R, sg);
             hipchk(hipMemcpyAsync(rp + 4 * recv_at[R][sg], S.sp.as<float>() + 4 * send_at[R][sg], 16 * c,
@@ -702,7 +744,7 @@ void fused_finish(gdf_fused* f, int slot, uint32_t* send_counts, uint32_t* recv_
         x.group_start(kPoints);
         for (int q = 0; q < W; ++q) {
             if (q == R) continue;
-            for (int sg = 0; sg < 2; ++sg) {  // (per peer, in the same order on both sides)
+            for (uint32_t sg = 0; sg < NSg; ++sg) {  // (per peer, in the same order on both sides)
                 const size_t sc = pts_of(R, q, sg), sr = runs_of(R, q, sg);
                 if (sc) {
                     x.send(S.sp.as<float>() + 4 * send_at[q][sg], 16 * sc, q, kPoints, st);
@@ -743,7 +785,11 @@ void fused_finish(gdf_fused* f, int slot, uint32_t* send_counts, uint32_t* recv_
     gdfchk(gdf_voxel_occupancy_grid_batch(e, uni, words, 1, S.nframes, stride, S.nframes * stride,
                                           S.lifetime));
     if (send_counts)
-        for (int q = 0; q < W; ++q) send_counts[q] = (uint32_t)(pts_of(R, q, 0) + pts_of(R, q, 1));
+        for (int q = 0; q < W; ++q) {
+            uint64_t c = 0;
+            for (uint32_t sg = 0; sg < NSg; ++sg) c += pts_of(R, q, sg);
+            send_counts[q] = (uint32_t)c;
+        }
     if (recv_count) *recv_count = (uint32_t)n;
     S.pending = false;
 }
@@ -760,13 +806,14 @@ gdf_fused* fused_new(gdf_engine* engine, int rank, int world, const gdf_stream_c
     f->world = world;
     f->cams.assign(cams, cams + world);
     f->F = flying_filter_size;
+    f->nseg = std::max<uint32_t>(2u, std::min<uint32_t>(kSegMax, 32u / (uint32_t)world));
     for (const gdf_stream_camera& c : f->cams)
         f->Lmax = std::max<uint32_t>(f->Lmax, f->F * c.width + f->F);
     for (const gdf_stream_camera& c : f->cams)
         if ((uint64_t)c.width * c.height < f->Lmax)
             fail(GDF_ERR_ARG, "fused multi-GPU frames need cameras taller than F rows");
     for (SlotX& s : f->slots) {
-        hipchk(hipHostMalloc(reinterpret_cast<void**>(&s.host), (size_t)4 * world * world * 4,
+        hipchk(hipHostMalloc(reinterpret_cast<void**>(&s.host), (size_t)2 * f->nseg * world * world * 4,
                              hipHostMallocDefault), "hipHostMalloc");
         hipchk(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming), "hipEventCreate");
     }

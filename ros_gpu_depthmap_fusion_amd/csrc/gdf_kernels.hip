@@ -1972,9 +1972,10 @@ __device__ __forceinline__ void emit_px2_parts(const FrameArgs& a, uint32_t* s_m
         const uint32_t a0 = G(a.seg_offsets)[(size_t)threadIdx.x * TS];
         const uint32_t a1 = threadIdx.x + 1 < 2u * P ? G(a.seg_offsets)[(size_t)(threadIdx.x + 1) * TS]
                                                      : *G(a.scan_total);
-        if (a.part_nseg == 2u) {  // (the 2-segment record: this frame has no segment 1)
-            G(a.part_counts)[(kind * P + p) * 2u] = a1 - a0;
-            G(a.part_counts)[(kind * P + p) * 2u + 1u] = 0u;
+        if (a.part_nseg > 1u) {  // (the nseg-segment record: this frame has no segment 1..)
+            const uint32_t ns = a.part_nseg;
+            G(a.part_counts)[(kind * P + p) * ns] = a1 - a0;
+            for (uint32_t sg = 1; sg < ns; ++sg) G(a.part_counts)[(kind * P + p) * ns + sg] = 0u;
         } else {
             G(a.part_counts)[kind * P + p] = a1 - a0;
         }
@@ -2270,14 +2271,21 @@ __global__ __launch_bounds__(1024) void k_sel(FrameArgs a) {
             *G(a.run_total) = rtot;
             G(a.run_start)[rtot] = pbase + s_tot[0];
         }
+        if (a.sel_splits)  // (the partition's unused cuts: empty segments at the end)
+            for (uint32_t c = a.sel_ncuts; c < kMaxSegs - 2u; ++c) G(a.sel_splits)[1u + c] = pbase + s_tot[0];
     }
+    if (a.sel_splits && tile == 0u && i == 0) G(a.sel_splits)[0] = d;  // (depth | rollbuffer)
 #pragma unroll
     for (uint32_t j = 0; j < kSelSegs; ++j) {
         const bool valid = (keep >> j) & 1u;
         const unsigned long long m = __ballot(valid);
+        const uint32_t pos = pbase + s_wc[j * nwaves + wid] + (uint32_t)__popcll(m & ltm);
+        // a cut of the selection (sharded window: where the next piece this rank holds starts):
+        // the survivors before that item, kept or not
+        for (uint32_t c = 0; c < a.sel_ncuts; ++c)  // (uniform; sel_ncuts <= kMaxSegs - 2)
+            if (si0 + j * B + i == a.sel_cut_at[c]) G(a.sel_splits)[1u + c] = pos;
         if (!m) continue;  // wave-uniform
         uint32_t key = 0xFFFFFFFFu;
-        const uint32_t pos = pbase + s_wc[j * nwaves + wid] + (uint32_t)__popcll(m & ltm);
         if (valid) {
             const float4 w = world(j);
             gst4(a.out_pts, pos, w);
@@ -5454,6 +5462,28 @@ __device__ __forceinline__ uint32_t sent_key(const uint32_t* __restrict__ keys, 
     return batch ? k | (frame_of(s_fstart, nframes, i) << fshift) : k;
 }
 
+// the segment cuts of a partition (launch_partition's splits): item i lies in segment
+// #{cuts <= i}; a cut starts a run
+struct SegCuts {
+    uint32_t c[kMaxSegs - 1];
+    __device__ SegCuts(const uint32_t* splits, uint32_t nsplit, uint32_t stride) {
+#pragma unroll
+        for (uint32_t k = 0; k < kMaxSegs - 1; ++k) c[k] = k < nsplit ? splits[k * stride] : 0xFFFFFFFFu;
+    }
+    __device__ uint32_t seg(uint32_t i) const {
+        uint32_t s = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kMaxSegs - 1; ++k) s += i >= c[k] ? 1u : 0u;
+        return s;
+    }
+    __device__ bool at(uint32_t i) const {
+        bool b = false;
+#pragma unroll
+        for (uint32_t k = 0; k < kMaxSegs - 1; ++k) b |= i == c[k];
+        return b;
+    }
+};
+
 template <bool RUNS>
 __global__ __launch_bounds__(256) void k_part_count(const uint32_t* __restrict__ keys,
                                                     const uint32_t* __restrict__ count,
@@ -5461,13 +5491,15 @@ __global__ __launch_bounds__(256) void k_part_count(const uint32_t* __restrict__
                                                     uint32_t ntiles, uint32_t* __restrict__ counts,
                                                     const uint32_t* __restrict__ fstart,
                                                     uint32_t nframes, uint32_t fshift,
-                                                    const uint32_t* __restrict__ seg_split) {
+                                                    const uint32_t* __restrict__ splits,
+                                                    uint32_t nsplit, uint32_t stride) {
     __shared__ uint32_t s_c[2 * kMaxBuckets];
     __shared__ uint32_t s_fstart[kMaxCams + 1];
     const bool batch = RUNS && fstart != nullptr && nframes > 1;
     if (batch) load_fstart(s_fstart, fstart, nframes);
     const uint32_t n = *count;
-    const uint32_t nseg = seg_split ? 2u : 1u, split = seg_split ? *seg_split : 0xFFFFFFFFu;
+    const SegCuts cut(splits, nsplit, stride);
+    const uint32_t nseg = nsplit + 1u;
     const uint32_t nb = nparts * nseg;
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {  // block-uniform
         if (threadIdx.x < 2 * kMaxBuckets) s_c[threadIdx.x] = 0;
@@ -5477,9 +5509,9 @@ __global__ __launch_bounds__(256) void k_part_count(const uint32_t* __restrict__
             const uint32_t i = t * kPartTile + q * 256 + threadIdx.x;
             if (i < n) {
                 const uint32_t key = keys[i];
-                const uint32_t b = part_of(key, nparts, ncells) * nseg + (i >= split ? 1u : 0u);
+                const uint32_t b = part_of(key, nparts, ncells) * nseg + cut.seg(i);
                 atomicAdd(&s_c[b], 1u);
-                if (RUNS && (i == t * kPartTile || i == split ||
+                if (RUNS && (i == t * kPartTile || cut.at(i) ||
                              sent_key(keys, i - 1, s_fstart, nframes, fshift, batch) !=
                                  (batch ? key | (frame_of(s_fstart, nframes, i) << fshift) : key)))
                     atomicAdd(&s_c[kMaxBuckets + b], 1u);
@@ -5520,7 +5552,8 @@ __global__ __launch_bounds__(256) void k_part_scatter(const float4* __restrict__
                                                       uint32_t nframes, uint32_t fshift,
                                                       uint32_t* __restrict__ out_run_keys,
                                                       uint32_t* __restrict__ out_run_start,
-                                                      const uint32_t* __restrict__ seg_split) {
+                                                      const uint32_t* __restrict__ splits,
+                                                      uint32_t nsplit, uint32_t stride) {
     __shared__ uint32_t s_w[4][kMaxBuckets];  // per-wave running counts (slot-major order)
     __shared__ uint32_t s_rw[4][kMaxBuckets];  // (runs)
     __shared__ uint32_t s_base[kMaxBuckets];
@@ -5533,7 +5566,8 @@ __global__ __launch_bounds__(256) void k_part_scatter(const float4* __restrict__
     if (batch) load_fstart(s_fstart, fstart, nframes);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t n = *count;
-    const uint32_t nseg = seg_split ? 2u : 1u, split = seg_split ? *seg_split : 0xFFFFFFFFu;
+    const SegCuts cut(splits, nsplit, stride);
+    const uint32_t nseg = nsplit + 1u;
     const uint32_t nb = nparts * nseg;
     const uint32_t mp = nb * ntiles;  // (RUNS: the run counts' offsets follow the points')
     if (blockIdx.x == 0 && threadIdx.x < nb) {
@@ -5571,14 +5605,14 @@ __global__ __launch_bounds__(256) void k_part_scatter(const float4* __restrict__
             const bool ok = i < n;
             key[q] = ok ? keys[i] : 0u;
             if (ok) p[q] = pts[i];
-            part[q] = ok ? part_of(key[q], nparts, ncells) * nseg + (i >= split ? 1u : 0u) : 0u;
+            part[q] = ok ? part_of(key[q], nparts, ncells) * nseg + cut.seg(i) : 0u;
             if (batch && ok) key[q] |= frame_of(s_fstart, nframes, i) << fshift;
             const unsigned long long m = same_part(__ballot(ok), part[q]);
             const uint32_t before = (uint32_t)__popcll(m & ltm);
             const uint32_t base = ok ? s_w[w][part[q]] : 0u;
             rank[q] = base + before;
             if (RUNS) {
-                lead[q] = ok && (i == t * kPartTile || i == split ||
+                lead[q] = ok && (i == t * kPartTile || cut.at(i) ||
                                  sent_key(keys, i - 1, s_fstart, nframes, fshift, batch) != key[q]);
                 const unsigned long long lm = same_part(__ballot(lead[q]), part[q]);
                 const uint32_t rbefore = (uint32_t)__popcll(lm & ltm);
@@ -5637,30 +5671,32 @@ hipError_t launch_partition(const float4* pts, const uint32_t* keys, const uint3
                             uint32_t* out_keys, uint32_t* part_counts, hipStream_t s,
                             const uint32_t* fstart, uint32_t nframes, uint32_t fshift,
                             uint32_t* out_run_keys, uint32_t* out_run_start,
-                            const uint32_t* seg_split) {
+                            const uint32_t* splits, uint32_t nsplit, uint32_t stride) {
     if (nparts == 0 || nparts > kMaxParts) return hipErrorInvalidValue;
+    if (!splits) nsplit = 0;
+    if (nsplit > kMaxSegs - 1 || nparts * (nsplit + 1) > kMaxBuckets) return hipErrorInvalidValue;
     const uint32_t ntiles = std::max<uint32_t>(part_tiles(nmax), 1u);
     const uint32_t blocks = std::min<uint32_t>(ntiles, 2048u);
     const bool runs = out_run_keys != nullptr;
     if (runs)
         hipLaunchKernelGGL(k_part_count<true>, dim3(blocks), dim3(256), 0, s, keys, count, nparts,
-                           ncells, ntiles, counts, fstart, nframes, fshift, seg_split);
+                           ncells, ntiles, counts, fstart, nframes, fshift, splits, nsplit, stride);
     else
         hipLaunchKernelGGL(k_part_count<false>, dim3(blocks), dim3(256), 0, s, keys, count, nparts,
-                           ncells, ntiles, counts, fstart, nframes, fshift, seg_split);
+                           ncells, ntiles, counts, fstart, nframes, fshift, splits, nsplit, stride);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    const uint32_t nb = nparts * (seg_split ? 2u : 1u);
+    const uint32_t nb = nparts * (nsplit + 1u);
     const uint32_t m = (runs ? 2u : 1u) * nb * ntiles;
     if ((e = launch_scan(counts, m, offsets, total, nullptr, 1u, s)) != hipSuccess) return e;
     if (runs)
         hipLaunchKernelGGL(k_part_scatter<true>, dim3(blocks), dim3(256), 0, s, pts, keys, count,
                            nparts, ncells, ntiles, offsets, total, out_pts, out_keys, part_counts,
-                           fstart, nframes, fshift, out_run_keys, out_run_start, seg_split);
+                           fstart, nframes, fshift, out_run_keys, out_run_start, splits, nsplit, stride);
     else
         hipLaunchKernelGGL(k_part_scatter<false>, dim3(blocks), dim3(256), 0, s, pts, keys, count,
                            nparts, ncells, ntiles, offsets, total, out_pts, out_keys, part_counts,
-                           fstart, nframes, fshift, out_run_keys, out_run_start, seg_split);
+                           fstart, nframes, fshift, out_run_keys, out_run_start, splits, nsplit, stride);
     return hipGetLastError();
 }
 

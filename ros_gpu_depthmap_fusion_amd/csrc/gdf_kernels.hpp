@@ -218,10 +218,13 @@ hipError_t launch_transform_points(const float4* in, const uint32_t* mask, float
 // With out_run_keys (runs mode): also the part-major runs of equal sent keys (run keys, run
 // starts relative to the part's first point), part_counts[nparts + p] = runs of part p, counts /
 // offsets twice as long (points' tile counts, then the runs'); out_keys may be null.
-// seg_split (device word, optional): TWO segments, items [0, split) and [split, n) (a frame's depth
-// points, then its rollbuffer points) - buckets b = part * 2 + segment take the place of the parts
-// (bucket-major output, part_counts [2 nparts points | 2 nparts runs], run starts relative to
-// the bucket's first point, a run never crossing the split); workspace sized for 2 nparts.
+// splits (device words, optional): nsplit + 1 <= kMaxSegs SEGMENTS cut at the items splits[0] <=
+// splits[stride] <= ... (stride 0: every cut at the one word splits[0]) - a frame's depth points,
+// then its rollbuffer points in pieces (a sharded window: one piece per stretch of the selection
+// this rank holds) - buckets b = part * nseg + segment take the place of the parts (bucket-major
+// output, part_counts [nseg nparts points | nseg nparts runs], run starts relative to the bucket's
+// first point, a run never crossing a cut); nparts * nseg <= kMaxBuckets, workspace sized for
+// nseg nparts.
 uint32_t part_tiles(uint32_t nmax);
 hipError_t launch_partition(const float4* pts, const uint32_t* keys, const uint32_t* count,
                             uint32_t nmax, uint32_t nparts, uint64_t ncells, uint32_t* counts,
@@ -230,7 +233,8 @@ hipError_t launch_partition(const float4* pts, const uint32_t* keys, const uint3
                             const uint32_t* fstart = nullptr, uint32_t nframes = 1,
                             uint32_t fshift = 0, uint32_t* out_run_keys = nullptr,
                             uint32_t* out_run_start = nullptr,
-                            const uint32_t* seg_split = nullptr);
+                            const uint32_t* splits = nullptr, uint32_t nsplit = 0,
+                            uint32_t split_stride = 0);
 
 // gdf_download_frame's prefetch: a single-frame launch chain ends with ONE kernel that writes the
 // frame's downloads - the small counters, the points, voxel coords, voxelized points and the grid

@@ -132,7 +132,7 @@ EXPORTED = [
     "gdf_upload_point_sequences", "gdf_filter_new_point_sequences", "gdf_insert_new_point_sequences",
     "gdf_roll_rollbuffer", "gdf_select_timespan", "gdf_prepare_point_and_mask_buffers",
     "gdf_insert_selected_point_sequence", "gdf_transform_point_sequence", "gdf_get_rollbuffer_state",
-    "gdf_set_rollbuffer_shard", "gdf_get_rollbuffer_shard_order",
+    "gdf_set_rollbuffer_shard", "gdf_get_rollbuffer_shard_order", "gdf_get_rollbuffer_pieces",
     "gdf_upload_depthmaps", "gdf_convert_depthmaps", "gdf_filter_flying_pixels", "gdf_crop_points",
     "gdf_apply_point_mask", "gdf_compute_voxel_coords", "gdf_voxelize", "gdf_voxel_occupancy_grid",
     "gdf_get_point_count", "gdf_download_points", "gdf_download_voxel_coords",
@@ -267,6 +267,7 @@ def load_library(path: str = LIB_PATH):
         "gdf_fused_run": (i32, [vp, P(StreamCamera), P(FrameParams), u64, u64, u32, i32]),
         "gdf_set_rollbuffer_shard": (i32, [vp, u32, u32, u32]),
         "gdf_get_rollbuffer_shard_order": (i32, [vp, vp, u32]),
+        "gdf_get_rollbuffer_pieces": (i32, [vp, vp, u32, P(u32)]),
         "gdf_set_partition_segments": (i32, [vp, u32]),
         "gdf_fused_local_create": (i32, [i32, P(vp)]),
         "gdf_fused_local_destroy": (i32, [vp]),

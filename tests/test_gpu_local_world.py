@@ -231,6 +231,40 @@ def test_local_world_sharded_rollbuffer(world):
                  sharded=True) == 4
 
 
+@pytest.mark.parametrize("world,block", [(3, 2), (4, 1), (8, 1)])
+def test_local_world_sharded_window_over_the_limit(world, block):
+    """A window spanning MORE than `world` blocks (a burst of sequences against a block size made
+    for a shorter window): a rank holds several separate pieces of the selection (world 3 /
+    block 2: up to 2; world 4 / block 1: 2 each; world 8 / block 1: the 8-sequence window on 8
+    ranks, 1 each, the 9th sequence wrapping onto rank 0 from frame 1).  The partition cuts the
+    rank's rollbuffer points where each piece starts (k_sel records the survivors before the cut)
+    and every owner places the pieces in the selection's order: every fused cloud and grid equal
+    ONE unsharded oracle engine's."""
+    p = ComponentParams()
+    win = 8
+    p.ps_timespan = (win - 0.5) / 30.0
+    rb = (1280, 720, win)
+    cams, depths, res = run_local_world(world, 640, 480, 4, 1, p, depth=2, rb=rb, shard=block)
+    assert check(f"burst{world}", world, 1, res, oracle_frames(cams, depths, p, rb=rb), rb=True,
+                 sharded=True) == 4
+
+
+def test_local_world_sharded_window_too_many_pieces_fails_alike():
+    """World 2, block 1, an 8-sequence window: each rank would hold 4 pieces, more than the 3 the
+    exchange carries - the step fails on EVERY rank with GDF_ERR_STATE at once (the headers are
+    replicated, so the ranks decide alike), naming the pieces; no rank waits for another."""
+    import time
+    from ros_gpu_depthmap_fusion_amd.gdf import GDFError
+    p = ComponentParams()
+    win = 8
+    p.ps_timespan = (win - 0.5) / 30.0
+    t0 = time.time()
+    with pytest.raises(GDFError) as ei:
+        run_local_world(2, 640, 480, 1, 1, p, depth=1, rb=(1280, 720, win), shard=1)
+    assert "separate pieces" in str(ei.value) or "aborted" in str(ei.value), str(ei.value)
+    assert time.time() - t0 < 120
+
+
 def test_local_world_c5_sharded_full_window():
     """SURVEY §8(d) C5 as BASELINE states it - 8 cameras x 3840x2160 at launch defaults WITH the
     rollbuffer - through the product step at world 8: a window of 32 x 720p point sequences (29.5 M
