@@ -221,15 +221,11 @@ int gdf_get_rollbuffer_state(gdf_engine* engine, gdf_rollbuffer_state* out);
  * shards' rollbuffers as a header without points.  So every shard rolls and selects the same
  * sequences by time (rollPointSequenceRollbufferCPU / selectPointSequenceTimespanCPU depend only
  * on the headers, fusion.cpp:1098-1217, 1358-1416) and holds ~1/nshards of the window; the shards'
- * selected points, concatenated in gdf_get_rollbuffer_shard_order, are the unsharded selection
- * (the point filter still sees every new point: its neighbours cross sequences).  The
+ * selected points, placed piece by piece in gdf_get_rollbuffer_pieces' order, are the unsharded
+ * selection (the point filter still sees every new point: its neighbours cross sequences).  The
  * rollbuffer state then counts the shard's own points.  Set before the first sequence is
  * inserted; nshards = 1: off. */
 int gdf_set_rollbuffer_shard(gdf_engine* engine, uint32_t shard, uint32_t nshards, uint32_t block);
-/* The shards in the order their selected points take in the unsharded selection (by their first
- * selected sequence; shards holding none follow in shard order).  GDF_ERR_STATE when a shard
- * holds two separate pieces of the selection (the window spans more than nshards blocks). */
-int gdf_get_rollbuffer_shard_order(gdf_engine* engine, uint32_t* order, uint32_t nshards);
 /* The pieces of the selected window in the selection's order (after the frame's selection): a
  * piece is a maximal stretch of selected sequences with points held by one shard; owners[i] = the
  * shard holding piece i.  *count = the number of pieces (GDF_ERR_CAPACITY when it exceeds
@@ -478,6 +474,12 @@ int gdf_set_profiling(gdf_engine* engine, int enable);
 /* sum of event-measured milliseconds and number of launches per slot since the last reset
  * (synchronises the engine stream) */
 int gdf_get_kernel_times(gdf_engine* engine, double* ms_sum, uint64_t* launches, int slots);
+
+/* The tuning variables (GDF_* launch-shape knobs, none of which changes a result) the engine was
+ * created under, as "NAME=value NAME=value" ("" when none: every built-in default).  Each engine
+ * keeps the snapshot taken at gdf_create - engines created under other environments never retune
+ * it - and gdf_create logs a non-empty one to stderr. */
+int gdf_get_tuning(gdf_engine* engine, char* buf, uint32_t capacity);
 
 /* ---- debug / parity hooks ------------------------------------------------------------------ */
 /* Keep per-point stage masks of the next compaction launch: bit0 = valid after convert

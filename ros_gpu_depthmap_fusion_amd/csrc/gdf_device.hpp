@@ -103,6 +103,32 @@ struct CamDesc {
 };
 static_assert(sizeof(CamDesc) % 16 == 0, "CamDesc must stay 16-byte sized");
 
+// Launch-shape choices of one engine (host-side; the kernels never read it).  None changes a
+// result: each alternative is parity-tested against the oracle (test_gpu_round3/4/5).  An engine
+// takes its snapshot at gdf_create - a GDF_* variable when set, the default otherwise - and its
+// launches read only that snapshot, so engines created under other environments (other threads,
+// the in-process world's ranks) never retune it; gdf_create logs every value that differs from
+// its default.
+struct Tuning {
+    uint32_t mask_px2 = 2;            // GDF_MASK_PX: pixels per k_mask thread (2, or 1: k_mask)
+    uint32_t mask_occ8 = 1;           // GDF_MASK_OCC8: k_mask_px at 8 waves per SIMD
+    uint32_t emit_px2 = 1;            // GDF_EMIT_PX2: two pixels per k_emit thread
+    uint32_t grid_wpt = 2;            // GDF_GRID_WPT: mark words per thread of the grid update (1..8)
+    uint32_t sort_blocks = 2048;      // GDF_SORT_BLOCKS: radix grid cap
+    uint32_t group_blocks = 2048;     // GDF_GROUP_BLOCKS: group-phase grid cap
+    uint32_t group_scan_tiles = 1024; // GDF_GROUP_SCAN_TILES: tiles above which k_group counts + scans
+    uint32_t group_first = 1;         // GDF_GROUP_FIRST: tile ends from k_group_count's first starts
+    uint32_t run_stage = 2048;        // GDF_RUN_STAGE: staged points per k_group_runs tile (512 / 2048)
+    uint32_t run_inblock = 1024;      // GDF_RUN_INBLOCK: in-block group size limit
+    uint32_t run_wave = 2;            // GDF_RUN_WAVE: staged long groups 0 queued, 1 a wave, 2 4 lanes
+    uint32_t small_group = 32;        // GDF_SMALL_GROUP: thread-summed group size
+    uint32_t points_lane = 0;         // GDF_POINTS_LANE: k_group's long staged groups by 4-lane chains
+    uint32_t run_wave_mode = 1;       // GDF_RUN_WAVE_MODE: queued groups 0 block, 1 by queue, 2 wave
+    uint32_t run_big_occ4 = 0;        // GDF_RUN_BIG_OCC4: k_group_runs_big at 4 waves per SIMD
+    uint32_t run_big_blocks = 1024;   // GDF_RUN_BIG_BLOCKS: k_group_runs_big grid cap
+    uint32_t run_q16 = 2;             // GDF_RUN_Q16: chunks of 1 K points 0 never, 1 always, 2 single frames
+};
+
 // Arguments of the compaction launches, passed by value.  Up to kArgCams camera descriptors
 // travel in the kernel arguments (kernel-argument bytes cost launch latency); more cameras are
 // read from a device copy.
@@ -113,7 +139,6 @@ struct FrameArgs {
     uint32_t depth_total;       // ΣP of emitting cameras' index space
     uint32_t depth_segs;        // segments over the depth pixels
     uint32_t total_segs;        // segments of the two-pass (depth) compaction: depth_segs
-    uint32_t mask_pairs;        // row pairs of those segments (k_mask_px2r: one workgroup each)
     // flying-pixel filter (sh/filter_flying_pixels.glsl)
     int32_t do_flying;
     uint32_t F;
@@ -212,6 +237,7 @@ struct FrameArgs {
     // runs at nseg P + nseg p + s] with segments 1.. (a selection's rollbuffer pieces) empty - a
     // frame without one
     uint32_t part_nseg;
+    const Tuning* tune;         // (host) the engine's launch shapes: mask_kernel / emit_kernel
 };
 static_assert(sizeof(FrameArgs) <= 4096, "kernel arguments are limited to 4 KiB");
 

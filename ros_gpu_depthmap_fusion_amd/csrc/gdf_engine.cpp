@@ -304,6 +304,18 @@ enum MiscSlot {
 }  // namespace
 
 
+// every environment variable that selects a launch shape or an alternative form (none changes a
+// result: DESIGN.md §5 "Tuning knobs"); read at gdf_create only
+constexpr const char* kTuningVars[] = {
+    "GDF_MASK_PX", "GDF_MASK_OCC8", "GDF_EMIT_PX2", "GDF_GRID_WPT", "GDF_SORT_BLOCKS",
+    "GDF_GROUP_BLOCKS", "GDF_GROUP_SCAN_TILES", "GDF_GROUP_FIRST", "GDF_RUN_STAGE",
+    "GDF_RUN_INBLOCK", "GDF_RUN_WAVE", "GDF_SMALL_GROUP", "GDF_POINTS_LANE", "GDF_RUN_WAVE_MODE",
+    "GDF_RUN_BIG_OCC4", "GDF_RUN_BIG_BLOCKS", "GDF_RUN_Q16", "GDF_SORT_PT", "GDF_SEG_ITEMS",
+    "GDF_SEL_SHAPE", "GDF_H2D_THREADS", "GDF_NO_GRAPHS", "GDF_NO_RUNS", "GDF_FORCE_RUNS",
+    "GDF_RUN_HIST_SORT", "GDF_RUN_HIST_ALL", "GDF_NO_PACK_RUNS", "GDF_NO_XRUNS",
+    "GDF_NO_GROUP_SCAN", "GDF_NO_MASK_PACKED", "GDF_NO_GRID_DELTA", "GDF_NO_EMIT_PART",
+    "GDF_NO_DL_PREFETCH", "GDF_DL_FORK"};
+
 constexpr int kMaxPipe = 4;
 
 // Everything one frame writes.  Frames rotate over npipe slots (gdf_clear starts a frame), so a
@@ -333,7 +345,6 @@ struct Slot {
     bool group_marks = false;       // this frame's marks are set by the voxel groups (k_group)
     uint32_t dbg_count = 0;
     DevBuf d_ka, d_kb, d_va, d_vb, d_sstatus, d_sgstatus, d_gstatus, d_ggstatus, d_vox;
-    DevBuf d_seghist, d_segfs, d_segstat, d_seggstat, d_segdone;  // the segmented run sort
     DevBuf d_gcnt, d_goff;          // group starts per tile + their scan (large frames)
     DevBuf d_gfirst;                // the first group start of each tile (run groups)
     DevBuf d_bigq, d_bigcnt;        // long voxels queued for k_group_big (large frames)
@@ -506,6 +517,8 @@ struct gdf_engine {
     int rot45 = 0;
     float lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
 
+    Tuning tune;                    // launch shapes, a snapshot at gdf_create
+    std::string tuning_set;         // the GDF_* tuning variables set at creation ("K=V K=V")
     int sort_pt = 0;  // radix keys per thread (4, 8, 16); 0: chosen by frame capacity
     uint32_t sel_segs = kSelSegs, sel_threads = kSelThreads;  // k_sel tile shape
     bool sel_shape_set = false;     // GDF_SEL_SHAPE given (else the shape follows the window)
@@ -514,25 +527,6 @@ struct gdf_engine {
     bool use_runs = !getenv("GDF_NO_RUNS");      // voxelize runs of equal keys (depth frames)
     bool force_runs = getenv("GDF_FORCE_RUNS") != nullptr;    // tuning knob: runs at every size
     bool run_hist_in_sort = getenv("GDF_RUN_HIST_SORT") != nullptr;  // tuning knob
-    // tuning knob GDF_SEG_SORT: the frame's (or batch's) runs sorted per frame by two 11-bit
-    // passes (k_seg_hist + 2 x k_seg_sort_pass) instead of k_sort_hist + 8/8/9-bit passes over
-    // frame | voxel.  Bit-exact (the GPU suite passes with it), but measured slower on MI355X (A/B
-    // on one box, profiles/r05/segsort/): C2 26.1 vs 28.0 Gpoints/s - the 2048-bin histogram
-    // costs ~2 device atomics per run (8.9 us per VGA batch, 23 us per 4K frame, against 4.8 us
-    // for the 8-bit one) and an 11-bit pass 21 us against 14-17 us, so the sort stays at ~51 us.
-    bool seg_sort_allowed = getenv("GDF_SEG_SORT") != nullptr;
-    // tuning knob GDF_FRAME_SORT: the runs of each frame of a batch sorted by ONE workgroup in
-    // LDS (k_frame_sort) instead of k_sort_hist + 3 batch-wide look-back passes.  Bit-exact (the
-    // GPU suite passes with it), but measured slower on MI355X (A/B on one box,
-    // profiles/r05/framesort/): C2 26.6 vs 28.2 Gpoints/s - ranking a VGA frame's ~13.4 K runs by
-    // 8-bit digits is VALU-bound on one CU (8.5 us per pass, 45 us per frame against the passes'
-    // ~50 us spread over the chip), and a 1024-thread workgroup at 122 VGPRs dispatches only to an
-    // EMPTY CU.  GDF_FRAME_SORT_CAP=n: frames of more than n runs take the chunked form (tests)
-    bool frame_sort_allowed = getenv("GDF_FRAME_SORT") != nullptr;
-    bool grid_last = getenv("GDF_GRID_LAST") != nullptr;  // tuning knob (VoxelizeArgs::grid_last)
-    uint32_t frame_sort_cap = getenv("GDF_FRAME_SORT_CAP")
-                                  ? (uint32_t)strtoul(getenv("GDF_FRAME_SORT_CAP"), nullptr, 10)
-                                  : kFrameSortResident;
     // the runs' lengths packed into the sort keys, their first points as the sorted values (the
     // group phase reads no run_start[index] gathers); GDF_NO_PACK_RUNS: the index form
     bool pack_runs = !getenv("GDF_NO_PACK_RUNS");
@@ -1322,32 +1316,13 @@ void ensure_misc(gdf_engine* e) {
 
 // Arguments of the fused compaction launch: convert + flying + crop + selected-point transform +
 // ordered compaction (+ voxel keys and occupancy marks when fused_voxel).
-// The segmented run sort serves the engine's own runs (in frame order) of voxel keys <= 22 bits
-// while its tile granules stay within kSegSortTileCap tiles (256 MB; C3's rollbuffer windows of
-// 10^8 points take the 8/8/9-bit passes)
-constexpr uint32_t kSegSortTileCap = 8192;
-bool seg_sort_ok(const gdf_engine* e, uint32_t nmax) {
-    return e->seg_sort_allowed && e->key_bits <= 2 * 11 &&
-           seg_sort_tiles(std::max<uint32_t>(nmax, 1), std::max<uint32_t>(e->nframes, 1)) <= kSegSortTileCap;
-}
-
-// The per-frame LDS sort serves the engine's own runs (in frame order, no rollbuffer selection) of
-// voxel keys <= 25 bits (a run item in LDS is the key's digits above 8 bits | a 14-bit index)
-// while a frame holds at most kFrameSortPoints points (VGA: 307 K, ~13 K runs, sorted resident; a
-// 720p / 4K frame's runs take the batch-wide passes, whose many CUs move them faster than the one
-// CU of a frame's chunked form)
-constexpr uint32_t kFrameSortPoints = 1u << 19;
-bool frame_sort_ok(const gdf_engine* e, uint32_t nmax) {
-    return e->frame_sort_allowed && !seg_sort_ok(e, nmax) && e->key_bits <= 25 &&
-           nmax / std::max<uint32_t>(e->nframes, 1) <= kFrameSortPoints;
-}
-
 FrameArgs frame_args(gdf_engine* e, bool fused_voxel, bool compaction_marks = false) {
     if (!e->prepared) prepare_buffers(e);
     if (!e->depth_uploaded) upload_depthmaps(e);
     ensure_misc(e);
     FrameArgs a;
     std::memset(&a, 0, sizeof(a));  // padding too: graph keys compare the bytes
+    a.tune = &e->tune;
     a.ncams = (int32_t)e->h_cams.size();
     if (a.ncams <= kArgCams) {
         for (size_t k = 0; k < e->h_cams.size(); ++k) a.cams[k] = e->h_cams[k];
@@ -1363,8 +1338,6 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel, bool compaction_marks = fa
     // one item per thread: blocks as wide as the widest segment
     a.seg_threads = e->max_segw ? std::max<uint32_t>(64, e->max_segw) : kSegItems;
     a.total_segs = a.depth_segs;
-    for (const CamDesc& c : e->h_cams)  // (seg_geo_pair's count: rows 2t, 2t + 1 per chunk)
-        if (c.emit) a.mask_pairs += ((c.H + 1u) / 2u) * c.nchunk;
     // k_sel tiles: 4 K points; 16 K for windows over 16 Mi points, whose ~10^4..10^5 tiles would
     // otherwise queue on the one ticket counter (measured on MI355X, C3's 236 M-point window:
     // 57.6 K tiles 2.92 ms, 14.4 K tiles 2.11 ms per frame)
@@ -1445,8 +1418,7 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel, bool compaction_marks = fa
         // k_sort_hist over the runs (tens of thousands of flushes contend at the atomic units)
         if (a.run_mode)
             a.key_hist = (a.total_segs <= kFusedPrefixSegs || e->run_hist_all) && !e->run_hist_in_sort &&
-                         !a.sel_tiles && !seg_sort_ok(e, e->sl().n_total) &&  // (k_seg_hist counts)
-                         !frame_sort_ok(e, e->sl().n_total)  // (k_frame_sort needs no histogram)
+                         !a.sel_tiles
                              ? e->sl().d_khist.as<uint32_t>() : nullptr;
     }
     a.out_pts = e->sl().d_pts.as<float4>();
@@ -1654,6 +1626,7 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime,
     e->sl().d_bigcnt.ensure(2048 * 4);
     VoxelizeArgs v;
     std::memset(&v, 0, sizeof(v));
+    v.tune = &e->tune;
     v.keys = e->sl().d_coords.as<uint32_t>();
     v.pts = e->sl().d_pts.as<float4>();
     v.count = e->sl().d_misc.as<uint32_t>() + kCount;
@@ -1673,25 +1646,6 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime,
         v.run_start = e->sl().d_runstart.as<uint32_t>();
         v.point_count = e->sl().d_misc.as<uint32_t>() + kCount;
         v.pack_runs = e->pack_runs && sort_bits(e) <= 25 ? 1 : 0;
-        if (seg_sort_ok(e, nmax)) {  // (the runs come in frame order)
-            v.pack_runs = 0;
-            Slot& q = e->sl();
-            const uint32_t nf = std::max<uint32_t>(e->nframes, 1);
-            q.d_seghist.ensure_zero((size_t)kMaxCams * 2 * kSegSortDigits * 4, e->s());
-            q.d_segfs.ensure((size_t)(kMaxCams + 1) * 4);
-            q.d_segstat.ensure_zero((size_t)seg_sort_tiles(nmax, nf) * kSegSortDigits * 8, e->s());
-            q.d_seggstat.ensure_zero((size_t)seg_sort_groups(nmax, nf) * kSegSortDigits * 8, e->s());
-            q.d_segdone.ensure_zero(64, e->s());
-            v.seg_sort = 1;
-            v.seg_hist = q.d_seghist.as<uint32_t>();
-            v.seg_fstart = q.d_segfs.as<uint32_t>();
-            v.seg_status = q.d_segstat.as<unsigned long long>();
-            v.seg_gstatus = q.d_seggstat.as<unsigned long long>();
-            v.seg_done = q.d_segdone.as<uint32_t>();
-        } else if (!e->sl().runs_sel && frame_sort_ok(e, nmax)) {
-            v.frame_sort = 1;
-            v.frame_sort_cap = e->frame_sort_cap;
-        }
     }
     v.nmax = nmax;
     v.key_bits = sort_bits(e);
@@ -1711,7 +1665,7 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime,
     // keys per thread of a radix tile: small frames want many tiles (latency), big ones few
     // (each tile publishes 256 look-back words: 2 KiB per 1 Ki keys at PT=4)
     v.group_counts = e->sl().d_gcnt.as<uint32_t>();
-    v.group_first = g_group_first ? e->sl().d_gfirst.as<uint32_t>() : nullptr;
+    v.group_first = e->tune.group_first ? e->sl().d_gfirst.as<uint32_t>() : nullptr;
     v.group_offsets = e->sl().d_goff.as<uint32_t>();
     v.group_done = e->group_scan ? e->sl().d_ggdone.as<uint32_t>() : nullptr;
     v.group_gtot = e->group_scan ? e->sl().d_ggtot.as<uint32_t>() : nullptr;
@@ -1738,12 +1692,11 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime,
         v.marks = marks_ptr(e);
         v.ncells = e->ncells;
         v.lifetime = (uint32_t)fused_grid_lifetime;
-        v.grid_last = e->grid_last ? 1 : 0;
         // the ticket was stored by this frame's k_mask (run_frame: grid_seq = grid_ticket)
         v.gseq = e->grid_seq(0, e->sl().d_misc.as<uint32_t>() + kGridTicket);
         delta_args(e, v.gseq, e->grid_ticket, e->nframes == 1);
         e->grid_ticket++;
-        if (e->nframes > 1) v.snap = snap_args(e, fused_grid_blocks(e->ncells), e->nframes);
+        if (e->nframes > 1) v.snap = snap_args(e, fused_grid_blocks(e->ncells, e->tune.grid_wpt), e->nframes);
     }
     return v;
 }
@@ -2080,39 +2033,31 @@ int gdf_create(int device, gdf_engine** out) {
     int rc = guarded(e, [&] {
         create_slot(e->slots[0]);
         if (const char* v = std::getenv("GDF_SORT_PT")) e->sort_pt = std::atoi(v);  // tuning knob
-        // process-wide tuning knobs: every engine creation sets each one, from its variable or,
-        // when that is absent, from the built-in value (so a knob one engine was created under
-        // never carries over to a later engine created without it)
-        static const struct {
-            uint32_t scan_tiles, run_stage, emit_px2, mask_occ8, mask_rows, grid_wpt, mask_px2,
-                run_q16, group_first, run_wave_mode, run_big_occ4, run_big_blocks, sort_blocks,
-                group_blocks, run_inblock, points_lane, run_wave, small_group;
-        } d = {g_group_scan_tiles, g_run_stage, g_emit_px2, g_mask_occ8, g_mask_rows, g_grid_wpt,
-               g_mask_px2, g_run_q16, g_group_first, g_run_wave_mode, g_run_big_occ4,
-               g_run_big_blocks, g_sort_blocks, g_group_blocks, g_run_inblock, g_points_lane,
-               g_run_wave, g_small_group};
+        // the engine's launch shapes (Tuning, gdf_device.hpp): a snapshot of the GDF_* variables
+        // at creation, read by this engine's launches only
         auto knob = [](const char* name, uint32_t dflt, int lo = 0, int hi = INT32_MAX) {
             const char* v = std::getenv(name);
             return v ? (uint32_t)std::min(hi, std::max(lo, std::atoi(v))) : dflt;
         };
-        g_group_scan_tiles = knob("GDF_GROUP_SCAN_TILES", d.scan_tiles, 1);
-        g_run_stage = knob("GDF_RUN_STAGE", d.run_stage, 1);  // 512 or 2048
-        g_emit_px2 = knob("GDF_EMIT_PX2", d.emit_px2);
-        g_mask_occ8 = knob("GDF_MASK_OCC8", d.mask_occ8);
-        g_mask_rows = knob("GDF_MASK_ROWS", d.mask_rows);
-        g_grid_wpt = knob("GDF_GRID_WPT", d.grid_wpt, 1, 8);
-        g_mask_px2 = knob("GDF_MASK_PX", d.mask_px2);  // pixels per k_mask thread
-        g_run_q16 = knob("GDF_RUN_Q16", d.run_q16);
-        g_group_first = knob("GDF_GROUP_FIRST", d.group_first);
-        g_run_wave_mode = knob("GDF_RUN_WAVE_MODE", d.run_wave_mode);
-        g_run_big_occ4 = knob("GDF_RUN_BIG_OCC4", d.run_big_occ4);
-        g_run_big_blocks = knob("GDF_RUN_BIG_BLOCKS", d.run_big_blocks, 1);
-        g_sort_blocks = knob("GDF_SORT_BLOCKS", d.sort_blocks, 1);
-        g_group_blocks = knob("GDF_GROUP_BLOCKS", d.group_blocks, 1);
-        g_run_inblock = knob("GDF_RUN_INBLOCK", d.run_inblock);
-        g_points_lane = knob("GDF_POINTS_LANE", d.points_lane);
-        g_run_wave = knob("GDF_RUN_WAVE", d.run_wave);
-        g_small_group = knob("GDF_SMALL_GROUP", d.small_group);
+        const Tuning d;
+        Tuning& t = e->tune;
+        t.group_scan_tiles = knob("GDF_GROUP_SCAN_TILES", d.group_scan_tiles, 1);
+        t.run_stage = knob("GDF_RUN_STAGE", d.run_stage, 1);  // 512 or 2048
+        t.emit_px2 = knob("GDF_EMIT_PX2", d.emit_px2);
+        t.mask_occ8 = knob("GDF_MASK_OCC8", d.mask_occ8);
+        t.grid_wpt = knob("GDF_GRID_WPT", d.grid_wpt, 1, 8);
+        t.mask_px2 = knob("GDF_MASK_PX", d.mask_px2);  // pixels per k_mask thread
+        t.run_q16 = knob("GDF_RUN_Q16", d.run_q16);
+        t.group_first = knob("GDF_GROUP_FIRST", d.group_first);
+        t.run_wave_mode = knob("GDF_RUN_WAVE_MODE", d.run_wave_mode);
+        t.run_big_occ4 = knob("GDF_RUN_BIG_OCC4", d.run_big_occ4);
+        t.run_big_blocks = knob("GDF_RUN_BIG_BLOCKS", d.run_big_blocks, 1);
+        t.sort_blocks = knob("GDF_SORT_BLOCKS", d.sort_blocks, 1);
+        t.group_blocks = knob("GDF_GROUP_BLOCKS", d.group_blocks, 1);
+        t.run_inblock = knob("GDF_RUN_INBLOCK", d.run_inblock);
+        t.points_lane = knob("GDF_POINTS_LANE", d.points_lane);
+        t.run_wave = knob("GDF_RUN_WAVE", d.run_wave);
+        t.small_group = knob("GDF_SMALL_GROUP", d.small_group);
         if (const char* v = std::getenv("GDF_SEG_ITEMS")) {  // tuning knob
             const uint32_t si = (uint32_t)std::atoi(v);
             if (si >= 64 && si <= kSegItems && si % 64 == 0) e->seg_items = si;
@@ -2128,12 +2073,32 @@ int gdf_create(int device, gdf_engine** out) {
         }
         ensure_misc(e);
         HIPCHK(hipStreamSynchronize(e->s()));
+        // every tuning variable this engine was created under (none changes a result; a stray
+        // one must not switch kernels silently): logged once, kept for gdf_get_tuning
+        for (const char* name : kTuningVars)
+            if (const char* v = std::getenv(name)) e->tuning_set += std::string(name) + "=" + v + " ";
+        if (!e->tuning_set.empty()) {
+            e->tuning_set.pop_back();
+            std::fprintf(stderr, "libgdf: engine on device %d created with tuning %s\n", device,
+                         e->tuning_set.c_str());
+        }
     });
     if (rc != GDF_OK) {
         delete e;
         return rc;
     }
     *out = e;
+    return GDF_OK;
+}
+
+int gdf_get_tuning(gdf_engine* e, char* buf, uint32_t capacity) {
+    ENGINE_OR_FAIL(e);
+    if (!buf || capacity == 0) return GDF_ERR_ARG;
+    if (e->tuning_set.size() + 1 > capacity) {
+        g_last_error = "tuning: buffer too small";
+        return GDF_ERR_CAPACITY;
+    }
+    std::memcpy(buf, e->tuning_set.c_str(), e->tuning_set.size() + 1);
     return GDF_OK;
 }
 
@@ -2392,39 +2357,6 @@ int gdf_set_rollbuffer_shard(gdf_engine* e, uint32_t shard, uint32_t nshards, ui
         e->nshards = nshards;
         e->shard_block = block;
         e->seq_counter = 0;
-    });
-}
-
-int gdf_get_rollbuffer_shard_order(gdf_engine* e, uint32_t* order, uint32_t nshards) {
-    ENGINE_OR_FAIL(e);
-    if (!order) return GDF_ERR_ARG;
-    return guarded(e, [&] {
-        if (nshards != e->nshards) fail(GDF_ERR_ARG, "rollbuffer shard order: nshards differs from the engine's");
-        const uint32_t ss = e->rb.selection_sequence_start, sc = e->rb.selection_sequence_count;
-        if (sc && (uint64_t)ss + sc > e->hdrB.size()) fail(GDF_ERR_STATE, "selection exceeds rollbuffer sequences");
-        std::vector<int64_t> first(nshards, -1);
-        std::vector<char> closed(nshards, 0);
-        int64_t cur = -1;
-        for (uint32_t j = ss; j < ss + sc; ++j) {
-            const Hdr& h = e->hdrB[j];
-            if (!h.num_global) continue;  // (no points on any shard)
-            const int64_t k = (int64_t)((h.id / e->shard_block) % e->nshards);
-            if (k == cur) continue;
-            if (cur >= 0) closed[cur] = 1;
-            if (closed[k])
-                fail(GDF_ERR_STATE, "rollbuffer shard order: a shard holds two separate pieces of the "
-                                    "selected window (the window spans more than nshards blocks: "
-                                    "raise the block size)");
-            first[k] = j;
-            cur = k;
-        }
-        std::vector<uint32_t> idx(nshards);
-        for (uint32_t k = 0; k < nshards; ++k) idx[k] = k;
-        std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) {
-            const int64_t fa = first[a] < 0 ? INT64_MAX : first[a], fb = first[b] < 0 ? INT64_MAX : first[b];
-            return fa < fb;
-        });
-        std::copy(idx.begin(), idx.end(), order);
     });
 }
 

@@ -396,10 +396,19 @@ struct SegGeo {
 // The emitting camera whose segments hold segment s (the last one, 0 if none): lane c tests
 // camera c, so every camera's range arrives in ONE load round - a scan over the table issued a
 // dependent scalar-load round per camera (k_mask_px stamps, tools/mask_trace.py: 12.3 K of a
-// block's 36.9 K cycles for 8 cameras).  Wave-uniform result; every lane of the wave active.
+// block's 36.9 K cycles for 8 cameras).  Wave-uniform result.  The ballot needs lanes
+// 0..ncams-1 active: a caller in divergent code (or a block not a multiple of 64 threads) takes
+// the per-camera scan instead (same answer: the last match).
 template <class P>
 __device__ __forceinline__ int seg_camera(P cams, int ncams, uint32_t s) {
     static_assert(kMaxCams <= 64, "one camera per lane");
+    const unsigned long long need = ncams >= 64 ? ~0ull : (1ull << ncams) - 1ull;
+    if ((__builtin_amdgcn_read_exec() & need) != need) {
+        int k = 0;
+        for (int c = 0; c < ncams; ++c)
+            if (cams[c].emit && s >= cams[c].seg0 && s < cams[c].seg0 + cams[c].nseg) k = c;
+        return k;
+    }
     const int lane = threadIdx.x & 63;
     bool hit = false;
     if (lane < ncams) {
@@ -425,43 +434,6 @@ __device__ __forceinline__ SegGeo seg_geo(P cams, int ncams, uint32_t s) {
     g.len = min(segw, W - g.x0);
     g.item0 = (uint32_t)cams[g.k].off + g.y * W + g.x0;
     return g;
-}
-
-// Row pair q of the emitting cameras (k_mask_px ROWS = 2): camera k's pairs are rows (2 t, 2 t + 1)
-// of each column chunk, ((H + 1) / 2) * nchunk of them, cameras in table order.  s0 = the pair's
-// first segment, nrow = 2 unless the camera's last row is alone.
-struct SegGeo2 {
-    SegGeo g;
-    uint32_t s0, nrow, nchunk;
-};
-
-template <class P>
-__device__ __forceinline__ SegGeo2 seg_geo_pair(P cams, int ncams, uint32_t q) {
-    SegGeo2 r;
-    uint32_t p0 = 0, k = 0, pk = 0;
-    for (int c = 0; c < ncams; ++c) {
-        if (!cams[c].emit) continue;
-        const uint32_t np = ((cams[c].H + 1u) / 2u) * cams[c].nchunk;
-        if (q >= p0 && q < p0 + np) {
-            k = (uint32_t)c;
-            pk = p0;
-        }
-        p0 += np;
-    }
-    k = __builtin_amdgcn_readfirstlane(k);
-    pk = __builtin_amdgcn_readfirstlane(pk);
-    const uint32_t nchunk = cams[k].nchunk, segw = cams[k].segw, W = cams[k].W;
-    const uint32_t i = q - pk;
-    const uint32_t t = i / nchunk, j = i - t * nchunk;
-    r.g.k = (int)k;
-    r.g.y = 2u * t;
-    r.g.x0 = j * segw;
-    r.g.len = min(segw, W - r.g.x0);
-    r.g.item0 = (uint32_t)cams[k].off + r.g.y * W + r.g.x0;
-    r.s0 = cams[k].seg0 + r.g.y * nchunk + j;
-    r.nrow = r.g.y + 1u < cams[k].H ? 2u : 1u;
-    r.nchunk = nchunk;
-    return r;
 }
 
 struct Band {
@@ -1232,13 +1204,9 @@ __device__ __forceinline__ unsigned long long part_lanes(unsigned long long m, b
 // k_mask with PX pixels per thread (x + j * 256 / PX) for 256-pixel segments at F = 4 without
 // rot45: 256 / PX threads per segment, the same band in LDS, the same outputs (validity word
 // w + j * waves from pixel j of wave w; counts, runs, run-key histogram).  No debug stage bits
-// (the engine launches k_mask for those).  ROWS = 2: a block takes the segments of two adjacent
-// rows (same camera and columns: pair t of a camera = rows 2t, 2t + 1) on one band of 2h + 2
-// rows - 5 staged rows per segment instead of 9, and the segment's fixed work (its camera and
-// geometry, the band's loads and barrier) once per two; the waves of row r run as the 1-row
-// kernel's (their band seen from row r: rowoff / yn shifted by r).
+// (the engine launches k_mask for those).
 #ifdef GDF_TRACE_GROUPS
-// (diagnostic build, tools/mask_trace.py) per k_mask_px block (ROWS = 1): wall clock at entry and
+// (diagnostic build, tools/mask_trace.py) per k_mask_px block: wall clock at entry and
 // exit, then wave 0's cycles in each phase - segment geometry and camera, band loads landed, LDS
 // stores + barrier, the filter, the ballots + publish barrier, the scan tail - each phase closed by
 // a wait for this wave's outstanding memory operations (which the product kernel does not do)
@@ -1249,40 +1217,35 @@ __device__ unsigned long long g_mtrace[kMaskTraceSlots][8];
     mt[i] = clock64()
 #endif
 
-template <int PX, int SEGW, int ROWS = 1>
+template <int PX, int SEGW>
 __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
 #ifdef GDF_TRACE_GROUPS
     const unsigned long long mw0 = wall_clock64();
     unsigned long long mt[7] = {};
     GDF_MSTAMP(0);
 #endif
-    constexpr int NT = SEGW / PX, NW = NT / 64;          // threads, waves (per row)
-    constexpr int NTB = NT * ROWS, NWB = NW * ROWS;      // (per block)
+    constexpr int NT = SEGW / PX, NW = NT / 64;          // threads, waves
     constexpr int NWORDS = SEGW / 64;                    // validity words of a segment
-    constexpr int NBR = 2 * 4 + ROWS;                    // band rows (h = 4)
-    constexpr int QR = (NBR + NWB - 1) / NWB;            // band rows per wave
-    constexpr int QX = (SEGW + 2 * 4 + NTB - 1) / NTB;   // ray factors per thread
+    constexpr int NBR = 2 * 4 + 1;                       // band rows (h = 4)
+    constexpr int QR = (NBR + NW - 1) / NW;              // band rows per wave
+    constexpr int QX = (SEGW + 2 * 4 + NT - 1) / NT;     // ray factors per thread
     constexpr int QC = (((SEGW + 8) * 2 + 15) / 16 + 1 + 63) / 64;  // 16-B chunks per lane and row
     // the segment's camera only (occupancy: 16 descriptors were 3.3 KB of LDS per block; the first
     // rows' general path reads the others from the argument table)
     __shared__ CamDesc s_cams[1];
-    __shared__ float s_yn[2 * kHalo + ROWS];
-    __shared__ int s_rowoff[2 * kHalo + ROWS];
-    __shared__ uint32_t s_cnt[ROWS][NWORDS];
-    __shared__ uint32_t s_rcnt[ROWS][NWORDS];
-    __shared__ uint32_t s_pc[ROWS][2][NWORDS][kMaxParts];  // emit partition: points, runs per (word, part)
+    __shared__ float s_yn[2 * kHalo + 1];
+    __shared__ int s_rowoff[2 * kHalo + 1];
+    __shared__ uint32_t s_cnt[NWORDS];
+    __shared__ uint32_t s_rcnt[NWORDS];
+    __shared__ uint32_t s_pc[2][NWORDS][kMaxParts];  // emit partition: points, runs per (word, part)
     extern __shared__ uint4 s_dyn[];
     // run-key digit histogram: dynamic LDS behind the band, only when the launch counts digits
-    // (ROWS = 2: one band row more, the launch adds it)
-    uint32_t* s_hist = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(s_dyn) + a.hist_lds +
-                                                   (ROWS - 1) * a.band_rowb);
-    const int lane = threadIdx.x & 63, wall = threadIdx.x >> 6;
-    const int row = ROWS == 1 ? 0 : wall / NW, wid = ROWS == 1 ? wall : wall % NW;
+    uint32_t* s_hist = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(s_dyn) + a.hist_lds);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (a.nparts)
-        for (uint32_t j = threadIdx.x; j < (uint32_t)ROWS * 2u * NWORDS * kMaxParts; j += NTB)
-            (&s_pc[0][0][0][0])[j] = 0u;
+        for (uint32_t j = threadIdx.x; j < 2u * NWORDS * kMaxParts; j += NT) (&s_pc[0][0][0])[j] = 0u;
     const uint32_t n = gridDim.x, q8 = n / 8, r8 = n % 8, xcd = blockIdx.x % 8;
-    const uint32_t s_blk = xcd * q8 + min(xcd, r8) + blockIdx.x / 8;  // segment, or row pair
+    const uint32_t s = xcd * q8 + min(xcd, r8) + blockIdx.x / 8;  // the block's segment
     if (a.grid_seq_out && blockIdx.x == 0 && threadIdx.x == 0) *a.grid_seq_out = a.grid_seq;
     uint32_t bits[PX], rkey[PX];
 #pragma unroll
@@ -1290,21 +1253,12 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
         bits[j] = 0u;
         rkey[j] = 0xFFFFFFFFu;
     }
-    const uint32_t i = ROWS == 1 ? threadIdx.x : threadIdx.x % NT;  // (thread of the row)
+    const uint32_t i = threadIdx.x;
     if (a.run_mode && a.key_hist)
-        for (uint32_t j = threadIdx.x; j < radix_hist_span(a.npasses); j += NTB) s_hist[j] = 0;
-    uint32_t s = s_blk, nrow = 1;  // this wave's segment; rows of the block
+        for (uint32_t j = threadIdx.x; j < radix_hist_span(a.npasses); j += NT) s_hist[j] = 0;
     {
         const gptr<const CamDesc> gcam = G(cam_table(a));
-        SegGeo sg;
-        if constexpr (ROWS == 1) {
-            sg = seg_geo(gcam, a.ncams, s);
-        } else {
-            const SegGeo2 g2 = seg_geo_pair(gcam, a.ncams, s_blk);
-            sg = g2.g;
-            nrow = g2.nrow;
-            s = g2.s0 + (uint32_t)row * g2.nchunk;
-        }
+        SegGeo sg = seg_geo(gcam, a.ncams, s);
         struct {
             const uint16_t* depth;
             const float *xn, *yn;
@@ -1317,29 +1271,29 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
         const int h = 4;  // (F = 4: the launch checks it)
         const uint32_t ca = sg.x0 >= (uint32_t)h ? sg.x0 - h : 0u;
         const uint32_t cb = min(c.W, sg.x0 + sg.len + h);
-        const uint32_t nrows = 2 * h + ROWS;
+        const uint32_t nrows = 2 * h + 1;
         uint8_t* band = reinterpret_cast<uint8_t*>(s_dyn);
         float* s_xn = reinterpret_cast<float*>(band + (size_t)nrows * a.band_rowb) + kHalo;
         const bool wrap = sg.x0 == 0 && sg.y >= (uint32_t)h && c.W >= (uint32_t)h;
         typedef uint32_t u4v __attribute__((ext_vector_type(4)));
         const uintptr_t dbase = reinterpret_cast<uintptr_t>(c.depth);
         const uint32_t nch = a.band_rowb / 16;  // <= 64 QC (the launch checks it)
-        // rows wall, wall + NWB, ...: every load before any store
+        // rows wid, wid + NW, ...: every load before any store
         u4v v[QR][QC];
         uintptr_t a16[QR], col0[QR];
         uint32_t n16[QR];
         bool rok[QR];
 #pragma unroll
         for (int q = 0; q < QR; ++q) {
-            const uint32_t r = (uint32_t)wall + (uint32_t)NWB * q;
+            const uint32_t r = (uint32_t)wid + (uint32_t)NW * q;
             const int gy = (int)sg.y - h + (int)r;
             rok[q] = r < nrows && gy >= 0 && gy < (int)c.H;
             n16[q] = 0;
             a16[q] = col0[q] = 0;
             if (rok[q]) {
                 col0[q] = dbase + 2 * ((uintptr_t)gy * c.W + ca);
-                // (a pixel row of a row-start segment: the previous row's end before column 0)
-                const bool pix_row = r >= (uint32_t)h && r < (uint32_t)(h + ROWS);
+                // (the pixel row of a row-start segment: the previous row's end before column 0)
+                const bool pix_row = r == (uint32_t)h;
                 const uintptr_t first = col0[q] - (wrap && pix_row ? 2 * (uintptr_t)h : 0);
                 const uintptr_t last = dbase + 2 * ((uintptr_t)gy * c.W + cb);
                 a16[q] = first & ~(uintptr_t)15;
@@ -1354,11 +1308,11 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
 #ifdef GDF_TRACE_GROUPS
         GDF_MSTAMP(2);
 #endif
-        const uint32_t tb = threadIdx.x;  // (thread of the block)
+        const uint32_t tb = threadIdx.x;
         float xv[QX];
 #pragma unroll
         for (int q = 0; q < QX; ++q)
-            xv[q] = ca + tb + (uint32_t)NTB * q < cb ? G(c.xn)[ca + tb + (uint32_t)NTB * q] : 0.0f;
+            xv[q] = ca + tb + (uint32_t)NT * q < cb ? G(c.xn)[ca + tb + (uint32_t)NT * q] : 0.0f;
         if (tb < nrows) {
             const int gyi = (int)sg.y - h + (int)tb;
             s_yn[tb] = (gyi >= 0 && gyi < (int)c.H) ? G(c.yn)[gyi] : 0.0f;
@@ -1368,11 +1322,11 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
         {  // camera sg.k's descriptor into LDS
             const uint32_t* src = reinterpret_cast<const uint32_t*>(cam_table(a) + sg.k);
             uint32_t* dst = reinterpret_cast<uint32_t*>(s_cams);
-            for (uint32_t w = threadIdx.x; w < (uint32_t)(sizeof(CamDesc) / 4); w += NTB) dst[w] = G(src)[w];
+            for (uint32_t w = threadIdx.x; w < (uint32_t)(sizeof(CamDesc) / 4); w += NT) dst[w] = G(src)[w];
         }
 #pragma unroll
         for (int q = 0; q < QR; ++q) {
-            const uint32_t r = (uint32_t)wall + (uint32_t)NWB * q;
+            const uint32_t r = (uint32_t)wid + (uint32_t)NW * q;
             if (r < nrows) {
 #pragma unroll
                 for (int cq = 0; cq < QC; ++cq) {
@@ -1386,17 +1340,15 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
         }
 #pragma unroll
         for (int q = 0; q < QX; ++q)
-            if (ca + tb + (uint32_t)NTB * q < cb) s_xn[tb + (uint32_t)NTB * q] = xv[q];
+            if (ca + tb + (uint32_t)NT * q < cb) s_xn[tb + (uint32_t)NT * q] = xv[q];
         if (wrap && tb < (uint32_t)h) s_xn[-1 - (int)tb] = xwv;
         __syncthreads();
 #ifdef GDF_TRACE_GROUPS
         GDF_MSTAMP(3);
 #endif
-        // (row r's waves: the band from their own pixel row, h rows above it)
-        const Band t{band, s_xn, s_rowoff + row, ca, h};
-        const float* s_ynr = s_yn + row;
-        sg.y += (uint32_t)row;
-        if ((uint32_t)row < nrow && 64u * (uint32_t)wid < sg.len) {  // wave-uniform
+        const Band t{band, s_xn, s_rowoff, ca, h};
+        const float* s_ynr = s_yn;
+        if (64u * (uint32_t)wid < sg.len) {  // wave-uniform
             const uint32_t xw0 = sg.x0 + 64u * wid;
             uint32_t x[PX];
             bool in[PX];
@@ -1447,14 +1399,13 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
 #ifdef GDF_TRACE_GROUPS
     GDF_MSTAMP(4);
 #endif
-    const bool live_row = (uint32_t)row < nrow;  // (a pair's missing second row: no outputs)
 #pragma unroll
     for (int j = 0; j < PX; ++j) {
         const uint32_t word = (uint32_t)wid + (uint32_t)NW * j;
         const unsigned long long m = __ballot((bits[j] & 4u) != 0u);
-        if (lane == 0 && live_row) {
+        if (lane == 0) {
             G(a.vbits)[(size_t)s * 16 + word] = m;
-            s_cnt[row][word] = (uint32_t)__popcll(m);
+            s_cnt[word] = (uint32_t)__popcll(m);
         }
         if (a.run_mode) {
             const unsigned long long below = m & lanemask_lt();
@@ -1462,9 +1413,9 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
             const uint32_t pkey = __shfl(rkey[j], prev < 0 ? 0 : prev, 64);
             const bool leader = ((bits[j] & 4u) != 0u) && (prev < 0 || pkey != rkey[j]);
             const unsigned long long lm = __ballot(leader);
-            if (lane == 0 && live_row) {
+            if (lane == 0) {
                 G(a.wave_runs)[(size_t)s * 16 + word] = (uint32_t)__popcll(lm);
-                s_rcnt[row][word] = (uint32_t)__popcll(lm);
+                s_rcnt[word] = (uint32_t)__popcll(lm);
             }
             if (leader && a.key_hist)
                 for (uint32_t p = 0; p < a.npasses; ++p)
@@ -1475,8 +1426,8 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
                 const uint32_t part = kept ? emit_part_of(vk, a.nparts, a.part_ncells) : 0u;
                 part_lanes(m, kept, part, [&](uint32_t p, unsigned long long pm) {
                     if (lane == 0) {
-                        s_pc[row][0][word][p] = (uint32_t)__popcll(pm);
-                        s_pc[row][1][word][p] = (uint32_t)__popcll(pm & lm);
+                        s_pc[0][word][p] = (uint32_t)__popcll(pm);
+                        s_pc[1][word][p] = (uint32_t)__popcll(pm & lm);
                     }
                 });
             }
@@ -1486,51 +1437,41 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
 #ifdef GDF_TRACE_GROUPS
     GDF_MSTAMP(5);
 #endif
-    // (the first wave of each row publishes that row's segment)
-    if (live_row && wid == 0) {
+    // (the first wave publishes the segment)
+    if (wid == 0) {
         if (a.nparts) {  // counts [points of part 0..P-1 | runs of part 0..P-1][segment]
             if ((uint32_t)lane < 2u * a.nparts) {
                 const uint32_t kind = lane / a.nparts, p = lane % a.nparts;
                 uint32_t c = 0;
-                for (int w = 0; w < NWORDS; ++w) c += s_pc[row][kind][w][p];
+                for (int w = 0; w < NWORDS; ++w) c += s_pc[kind][w][p];
                 G(a.seg_counts)[(size_t)lane * a.total_segs + s] = c;
             }
         } else if (lane == 0) {
             uint32_t tt = 0, r = 0;
-            for (int w = 0; w < NWORDS; ++w) tt += s_cnt[row][w];
+            for (int w = 0; w < NWORDS; ++w) tt += s_cnt[w];
             publish_count(a.seg_counts + s, tt);
             if (a.run_mode) {
-                for (int w = 0; w < NWORDS; ++w) r += s_rcnt[row][w];
+                for (int w = 0; w < NWORDS; ++w) r += s_rcnt[w];
                 publish_count(a.seg_counts + a.total_segs + s, r);
             }
         }
     }
     if (a.run_mode && a.key_hist) {
         const gptr<uint32_t> rep = G(a.key_hist + (blockIdx.x % kHistReps) * 1024u);
-        for (uint32_t j = threadIdx.x; j < radix_hist_span(a.npasses); j += NTB)
+        for (uint32_t j = threadIdx.x; j < radix_hist_span(a.npasses); j += NT)
             if (s_hist[j])
                 __hip_atomic_fetch_add(rep + j, s_hist[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if constexpr (ROWS == 1) {
-        group_scan_tail(a, s);
+    group_scan_tail(a, s);
 #ifdef GDF_TRACE_GROUPS
-        GDF_MSTAMP(6);
-        if (threadIdx.x == 0 && blockIdx.x < kMaskTraceSlots) {
-            unsigned long long* g = g_mtrace[blockIdx.x];
-            g[0] = mw0;
-            g[1] = wall_clock64();
-            for (int k = 1; k < 7; ++k) g[k + 1] = mt[k] - mt[k - 1];
-        }
-#endif
-    } else {  // (block-uniform: each row's segment arrives at its scan group)
-        __shared__ uint32_t s_seg[ROWS];
-        if (threadIdx.x % NT == 0) s_seg[row] = s;
-        __syncthreads();
-        // (one call site in a loop: two inlined copies made the compiler keep a private copy of
-        // FrameArgs - 2288 B of scratch, the round-4 aperture fault's precondition)
-#pragma unroll 1
-        for (uint32_t r = 0; r < nrow; ++r) group_scan_tail(a, s_seg[r]);
+    GDF_MSTAMP(6);
+    if (threadIdx.x == 0 && blockIdx.x < kMaskTraceSlots) {
+        unsigned long long* g = g_mtrace[blockIdx.x];
+        g[0] = mw0;
+        g[1] = wall_clock64();
+        for (int k = 1; k < 7; ++k) g[k + 1] = mt[k] - mt[k - 1];
     }
+#endif
 }
 
 template <int PX, int SEGW>
@@ -1541,11 +1482,6 @@ __global__ __launch_bounds__(SEGW / PX) void k_mask_px(FrameArgs a) {
 template <int PX, int SEGW>
 __global__ __launch_bounds__(SEGW / PX) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_mask_px_o8(FrameArgs a) {
     mask_px_body<PX, SEGW>(a);
-}
-// two rows per block (one workgroup per row pair, FrameArgs::mask_pairs of them)
-template <int PX, int SEGW>
-__global__ __launch_bounds__(2 * SEGW / PX) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_mask_px2r_o8(FrameArgs a) {
-    mask_px_body<PX, SEGW, 2>(a);
 }
 
 // Exclusive scan of the segment counts by one workgroup (chunks of 4096 with a running carry);
@@ -2336,9 +2272,6 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
                 hipLaunchKernelGGL((k_mask_px<2, 256>), dim3(a.total_segs), dim3(128), lds, s, a);
             else if (km == reinterpret_cast<const void*>(&k_mask_px_o8<2, 256>))
                 hipLaunchKernelGGL((k_mask_px_o8<2, 256>), dim3(a.total_segs), dim3(128), lds, s, a);
-            else if (km == reinterpret_cast<const void*>(&k_mask_px2r_o8<2, 256>))
-                hipLaunchKernelGGL((k_mask_px2r_o8<2, 256>), dim3(a.mask_pairs), dim3(256),
-                                   lds + a.band_rowb, s, a);
             else if (km == reinterpret_cast<const void*>(&k_mask_px<2, 640>))
                 hipLaunchKernelGGL((k_mask_px<2, 640>), dim3(a.total_segs), dim3(320), lds, s, a);
             else if (km == reinterpret_cast<const void*>(&k_mask<true, 4>))
@@ -2393,43 +2326,35 @@ constexpr uint32_t kPx640MinSegs = 1024;
 // compiler-made private copy of FrameArgs broke the G() camera-table reads, cam_table above.)  Measured on MI355X
 // (A/B on one box, dense frames, 2 pixels per thread vs k_mask): VGA 8-frame batches
 // 22.1 -> 23.7, 720p 4-frame batches 29.8 -> 32.6, 4K 30.9 -> 32.4 Gpoints/s
-uint32_t g_mask_px2 = 2;
-uint32_t g_mask_occ8 = 1;  // k_mask_px<2, 256> at 8 waves per SIMD (GDF_MASK_OCC8=0: 7; +2.5 % on C2)
-uint32_t g_mask_rows = 1;  // k_mask_px2r_o8: two rows per block (tuning knob GDF_MASK_ROWS=2)
 const void* mask_kernel(const FrameArgs& a) {
-    if (g_mask_px2 >= 2 && a.do_flying && a.F == 4 && !a.rot45 && a.seg_threads == 256 && !a.dbg &&
-        a.band_rowb <= 64 * 16) {
-        if (g_mask_rows == 2 && g_mask_occ8 && a.mask_pairs)
-            return reinterpret_cast<const void*>(&k_mask_px2r_o8<2, 256>);
-        return g_mask_occ8 ? reinterpret_cast<const void*>(&k_mask_px_o8<2, 256>)
+    const Tuning& T = *a.tune;
+    if (T.mask_px2 >= 2 && a.do_flying && a.F == 4 && !a.rot45 && a.seg_threads == 256 && !a.dbg &&
+        a.band_rowb <= 64 * 16)
+        return T.mask_occ8 ? reinterpret_cast<const void*>(&k_mask_px_o8<2, 256>)
                            : reinterpret_cast<const void*>(&k_mask_px<2, 256>);
-    }
     // (half 720p rows: single frames under 1 Mi pixels with enough segments to fill the chip)
-    if (g_mask_px2 >= 2 && a.do_flying && a.F == 4 && !a.rot45 && a.seg_threads == 640 && !a.dbg &&
+    if (T.mask_px2 >= 2 && a.do_flying && a.F == 4 && !a.rot45 && a.seg_threads == 640 && !a.dbg &&
         a.band_rowb <= 2 * 64 * 16 && a.total_segs >= kPx640MinSegs)
         return reinterpret_cast<const void*>(&k_mask_px<2, 640>);
     return frame_kernel(0, a.rot45, a.do_flying ? a.F : 0u);
 }
 
 
-// k_emit_px2 (two pixels per thread) for 256-pixel segments unless g_emit_px2 is cleared (tuning
-// knob GDF_EMIT_PX2=0)
-uint32_t g_emit_px2 = 1;
+// k_emit_px2 (two pixels per thread) for 256-pixel segments unless Tuning::emit_px2 is cleared
 // the compaction kernels that write the emit partition (FrameArgs::nparts)
 bool emit_partition_kernels(const FrameArgs& a) {
     const void* km = mask_kernel(a);
     FrameArgs plain = a;
     plain.nparts = 0;
     return (km == reinterpret_cast<const void*>(&k_mask_px<2, 256>) ||
-            km == reinterpret_cast<const void*>(&k_mask_px_o8<2, 256>) ||
-            km == reinterpret_cast<const void*>(&k_mask_px2r_o8<2, 256>)) &&
+            km == reinterpret_cast<const void*>(&k_mask_px_o8<2, 256>)) &&
            emit_kernel(plain) == reinterpret_cast<const void*>(&k_emit_px2<256>);
 }
 
 const void* emit_kernel(const FrameArgs& a) {
     if (a.nparts) return reinterpret_cast<const void*>(&k_emit_px2_parts<256>);
-    if (g_emit_px2 && a.seg_threads == 256) return reinterpret_cast<const void*>(&k_emit_px2<256>);
-    if (g_emit_px2 && a.seg_threads == 640 && a.total_segs >= kPx640MinSegs)
+    if (a.tune->emit_px2 && a.seg_threads == 256) return reinterpret_cast<const void*>(&k_emit_px2<256>);
+    if (a.tune->emit_px2 && a.seg_threads == 640 && a.total_segs >= kPx640MinSegs)
         return reinterpret_cast<const void*>(&k_emit_px2<640>);
     return reinterpret_cast<const void*>(&k_emit);
 }
@@ -2943,8 +2868,7 @@ __global__ __launch_bounds__(256) void k_grid_u8_batch(uint4* __restrict__ grid,
     grid_seq_leave<true>(q, f0, gridDim.x);
 }
 
-uint32_t g_grid_wpt = 2;  // mark words per thread of the grid blocks carried by radix pass 1 (GDF_GRID_WPT)
-uint32_t fused_grid_blocks(uint64_t ncells) { return grid_blocks((ncells + 31) / 32, 256 * g_grid_wpt); }
+uint32_t fused_grid_blocks(uint64_t ncells, uint32_t wpt) { return grid_blocks((ncells + 31) / 32, 256 * wpt); }
 uint32_t batch_grid_blocks(uint64_t ncells) { return grid_blocks((ncells + 31) / 32, 256); }
 
 hipError_t launch_grid_u8_batch(uint8_t* grid, const uint32_t* bits, uint64_t ncells,
@@ -3273,572 +3197,6 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
     }
 }
 
-// ---- frame-segmented two-pass radix sort of run keys ---------------------------------------------
-// A frame's runs of equal keys come in frame order (the compaction is frame-major: a batch's frames
-// back to back), and a run's sort key is voxel | frame << fshift - so sorting by the full key is
-// sorting each frame's runs by their voxel key, stably, in place within the frame's segment
-// [fs[f], fs[f + 1]).  The frame bits need no radix pass, and the 22-bit voxel keys of the launch
-// grid take two 11-bit LSD passes (2048 digits) instead of 8 + 8 + 9 bits: tiles never span two
-// frames, each frame's tiles chain their own decoupled look-back (lookback2_chans<8> over the
-// segment's granules), the digit bases come from per-frame histograms (k_seg_hist, which also
-// finds the segments).  The reference's order (radix_sort.h:107-289, a stable LSD sort of the
-// keys) is kept: within a frame the LSD passes are stable, frames stay in order.
-constexpr uint32_t kSegDigitBits = 11, kSegDigits = 1u << kSegDigitBits;
-
-// per (frame, pass) digit counts [nseg][2][2048] (zero on entry; the last pass zeroes them again)
-// and the frames' run starts fstart[0 .. nseg] (a frame without runs starts where the next does)
-__global__ __launch_bounds__(256) void k_seg_hist(const uint32_t* __restrict__ keys,
-                                                  const uint32_t* __restrict__ count, uint32_t nseg,
-                                                  uint32_t fshift, uint32_t* __restrict__ hist,
-                                                  uint32_t* __restrict__ fstart) {
-    const uint32_t n = *count;
-    const uint32_t vmask = nseg > 1 ? (1u << fshift) - 1u : 0xFFFFFFFFu;
-    if (n == 0) {
-        if (blockIdx.x == 0 && threadIdx.x <= nseg) fstart[threadIdx.x] = 0u;
-        return;
-    }
-    const int lane = threadIdx.x & 63;
-    for (uint32_t base = blockIdx.x * 256u; base < n; base += gridDim.x * 256u) {  // block-uniform
-        const uint32_t i = base + threadIdx.x;
-        const bool ok = i < n;
-        const uint32_t k = ok ? keys[i] : 0u;
-        const uint32_t f = ok && nseg > 1 ? min(k >> fshift, nseg - 1u) : 0u;
-        if (ok) {
-            const uint32_t pf = i == 0 ? 0xFFFFFFFFu : (nseg > 1 ? min(keys[i - 1] >> fshift, nseg - 1u) : 0u);
-            if (pf != f)  // frames (pf, f] start here (all frames <= f at i = 0)
-                for (uint32_t g = pf + 1u; g <= f; ++g) fstart[g] = i;
-            if (i == n - 1u)
-                for (uint32_t g = f + 1u; g <= nseg; ++g) fstart[g] = n;
-        }
-        const uint32_t v = k & vmask;
-        // consecutive lanes with the same (frame, digit) count once (a wave's runs often repeat a
-        // voxel's low digit only rarely; the high digit - a row band of the grid - often)
-#pragma unroll
-        for (uint32_t p = 0; p < 2; ++p) {
-            const uint32_t b = ok ? (f * 2u + p) * kSegDigits + ((v >> (kSegDigitBits * p)) & (kSegDigits - 1u))
-                                  : 0xFFFFFFFFu;
-            const uint32_t pb = __shfl_up(b, 1, 64);
-            const bool leader = ok && (lane == 0 || pb != b);
-            const unsigned long long lm = __ballot(leader);
-            const unsigned long long vm = __ballot(ok);
-            if (leader) {
-                const unsigned long long after = lane == 63 ? 0ull : lm & (~0ull << (lane + 1));
-                const uint32_t end = after ? (uint32_t)(__ffsll((long long)after) - 1)
-                                           : (uint32_t)__popcll(vm);
-                atomicAdd(&hist[b], end - (uint32_t)lane);
-            }
-        }
-    }
-}
-
-// One 11-bit pass (pass 0: bits 0..10 of the voxel key, pass 1: bits 11..21) over every frame's
-// segment.  Tile = 256 threads x PT runs of ONE frame; global tile g -> (frame f, tile t of f) from
-// the frames' tile starts; tiles in ticket order (persistent blocks).  Pass 0 also carries the
-// historic-grid update in extra blocks (as k_sort_pass) and zeroes the run-group queue; the
-// last block of pass 1 zeroes the histograms for the next voxelize.
-template <int PT>
-__global__ __launch_bounds__(kSortThreads) void k_seg_sort_pass(
-    const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
-    uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, const uint32_t* __restrict__ count,
-    uint32_t* hist, const uint32_t* __restrict__ fstart, uint32_t nseg, uint32_t fshift,
-    uint32_t pass, unsigned long long* status, unsigned long long* gstatus, uint32_t* tile_ctr,
-    uint32_t* epoch_word, uint32_t* err, uint32_t* done_ctr, uint32_t grid_block0, uint4* grid,
-    uint32_t* marks, uint64_t grid_nwords, uint32_t lifetime, GridSeq q, uint32_t nframes,
-    uint64_t mark_words, SnapArgs snap, uint32_t* qreset) {
-    constexpr int kTile = kSortThreads * PT;
-    constexpr int R = kSegDigits / 256;  // digits per thread in the offset phase
-    if (qreset && blockIdx.x == 0 && threadIdx.x == 0) {
-        qreset[0] = 0u;
-        qreset[1] = 0u;
-        qreset[2] = 0u;
-    }
-    if (blockIdx.x >= grid_block0) {  // fused historic-grid update (pass 0 only)
-        const uint32_t f = grid_seq_enter<true>(q);
-        if (nframes > 1)
-            grid_u8_part_frames(grid, marks, grid_nwords, lifetime, blockIdx.x - grid_block0,
-                                gridDim.x - grid_block0, nframes, mark_words, snap);
-        else
-            grid_u8_part(grid, marks, grid_nwords, lifetime, blockIdx.x - grid_block0,
-                         gridDim.x - grid_block0, q);
-        grid_seq_leave<true>(q, f, gridDim.x - grid_block0);
-        return;
-    }
-    __shared__ uint32_t s_fs[kMaxCams + 1], s_ts[kMaxCams + 1], s_gs[kMaxCams + 1];
-    __shared__ uint32_t s_cnt[4][kSegDigits];
-    __shared__ uint32_t s_base[kSegDigits];
-    __shared__ uint32_t s_excl[kSegDigits];
-    __shared__ uint32_t s_wave[4];
-    __shared__ uint32_t s_tile, s_epoch, s_last;
-    if (threadIdx.x == 0) {  // the frames' item, tile and look-back group starts
-        uint32_t t = 0, g = 0;
-        for (uint32_t f = 0; f < nseg; ++f) {
-            const uint32_t a = fstart[f], b = fstart[f + 1];
-            s_fs[f] = a;
-            s_ts[f] = t;
-            s_gs[f] = g;
-            const uint32_t nt = (b - a + kTile - 1) / kTile;
-            t += nt;
-            g += (nt + kSortGroup - 1) / kSortGroup;
-        }
-        s_fs[nseg] = fstart[nseg];
-        s_ts[nseg] = t;
-        s_gs[nseg] = g;
-        s_epoch = read_epoch(epoch_word);
-    }
-    __syncthreads();
-    const uint32_t ntiles = s_ts[nseg];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const unsigned long long ltm = lanemask_lt();
-    const Tickets tk = tickets(ntiles, grid_block0);
-    if (blockIdx.x >= tk.nblk) return;  // (block-uniform: no block past nblk counts itself below)
-    const uint32_t vmask = nseg > 1 ? (1u << fshift) - 1u : 0xFFFFFFFFu;
-    const uint32_t shift = kSegDigitBits * pass;
-    int cur = -1;
-    for (bool first = true;; first = false) {  // persistent: tiles in ticket order
-        if (!first && tk.oneshot) break;
-        if (threadIdx.x == 0) s_tile = next_ticket(tile_ctr, tk, epoch_word, s_epoch);
-        for (uint32_t i = threadIdx.x; i < 4 * kSegDigits; i += kSortThreads) (&s_cnt[0][0])[i] = 0;
-        __syncthreads();
-        const uint32_t tile = s_tile, epoch = s_epoch;
-        if (tile >= ntiles) break;  // block-uniform
-        uint32_t f = 0;
-        while (f + 1 < nseg && s_ts[f + 1] <= tile) ++f;  // (empty frames have no tiles)
-        const uint32_t t = tile - s_ts[f], nt = s_ts[f + 1] - s_ts[f];
-        const uint32_t lo = s_fs[f], hi = s_fs[f + 1];
-        if ((int)f != cur) {  // the frame's digit bases: its run start + the digits before
-            const uint32_t* h = hist + ((size_t)f * 2 + pass) * kSegDigits + R * threadIdx.x;
-            uint32_t v[R], sum = 0;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                v[r] = h[r];
-                sum += v[r];
-            }
-            uint32_t total;
-            uint32_t run = lo + block_exclusive_scan(sum, total, s_wave);
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                s_base[R * threadIdx.x + r] = run;
-                run += v[r];
-            }
-            cur = (int)f;
-        }
-        uint32_t key[PT], val[PT], rank[PT];
-        const uint32_t wbase = lo + t * kTile + w * 64 * PT;
-#pragma unroll
-        for (int j = 0; j < PT; ++j) {
-            const uint32_t idx = wbase + j * 64 + lane;
-            const bool ok = idx < hi;
-            key[j] = ok ? kin[idx] : 0xFFFFFFFFu;
-            val[j] = ok ? (vin ? vin[idx] : idx) : 0u;
-        }
-#pragma unroll
-        for (int j = 0; j < PT; ++j) {
-            const uint32_t idx = wbase + j * 64 + lane;
-            const bool ok = idx < hi;
-            const uint32_t d = ((key[j] & vmask) >> shift) & (kSegDigits - 1u);
-            unsigned long long m = __ballot(ok);
-            for (uint32_t b = 0; b < kSegDigitBits; ++b) {
-                const bool bit = (d >> b) & 1u;
-                const unsigned long long bb = __ballot(bit);
-                m &= bit ? bb : ~bb;
-            }
-            const uint32_t before = (uint32_t)__popcll(m & ltm);
-            uint32_t base = 0;
-            if (ok) base = s_cnt[w][d];
-            rank[j] = base + before;
-            __builtin_amdgcn_wave_barrier();
-            if (ok && before == 0) s_cnt[w][d] = base + (uint32_t)__popcll(m);
-            __builtin_amdgcn_wave_barrier();
-        }
-        __syncthreads();
-        uint32_t tot[R], ex[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const uint32_t d = threadIdx.x + 256u * r;
-            tot[r] = 0;
-#pragma unroll
-            for (int ww = 0; ww < 4; ++ww) {
-                const uint32_t c = s_cnt[ww][d];
-                s_cnt[ww][d] = tot[r];
-                tot[r] += c;
-            }
-        }
-        // the frame's own chain: its tiles' granules from the frame's first tile / group on
-        lookback2_chans<R>(status + (size_t)s_ts[f] * kSegDigits, gstatus + (size_t)s_gs[f] * kSegDigits,
-                           t, nt, tot, ex, epoch, err);
-#pragma unroll
-        for (int r = 0; r < R; ++r) s_excl[threadIdx.x + 256u * r] = ex[r];
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < PT; ++j) {
-            const uint32_t idx = wbase + j * 64 + lane;
-            if (idx < hi) {
-                const uint32_t dd = ((key[j] & vmask) >> shift) & (kSegDigits - 1u);
-                const uint32_t pos = s_base[dd] + s_excl[dd] + s_cnt[w][dd] + rank[j];
-                kout[pos] = key[j];
-                vout[pos] = val[j];
-            }
-        }
-        __syncthreads();  // LDS reused by the next tile
-    }
-    if (pass == 1) {  // the last block of the last pass zeroes the histograms (no reader left)
-        if (threadIdx.x == 0) s_last = atomicAdd(done_ctr, 1u) == tk.nblk - 1u ? 1u : 0u;
-        __syncthreads();
-        if (s_last) {
-            for (uint32_t i = threadIdx.x; i < nseg * 2u * kSegDigits; i += kSortThreads) hist[i] = 0u;
-            if (threadIdx.x == 0) atomicExch(done_ctr, 0u);
-        }
-    }
-}
-
-// ---- per-frame LDS radix sort of a batch's runs ---------------------------------------------------
-// The runs of a batch come in frame order and each frame's runs fit one CU's LDS (a VGA frame has
-// ~14 K runs): ONE workgroup per frame sorts its frame's runs by their voxel key, every LSD pass in
-// LDS, and writes them once - one launch of B workgroups instead of a histogram launch plus three
-// look-back passes over the whole batch (each reading and writing every run), and the other
-// 255 - B CUs stay free for the neighbouring batches' kernels.  The order equals the batch-wide
-// stable sort of voxel | frame << fshift (radix_sort.h:107-289): within a frame the LSD passes
-// are stable, frames keep their order.  In LDS an item is ONE word - the key's remaining digits
-// above its local index (14 bits) - so a pass moves 4 bytes per run; the sorted keys and their
-// values are gathered by that index at the end (staged in LDS).  A frame with more runs than
-// kFsCap (or than the GDF_FRAME_SORT_CAP knob) takes a chunked form of the same passes through
-// the slot's spare key / value buffers (correct, one CU's bandwidth).
-constexpr int kFsThreads = 1024, kFsWaves = kFsThreads / 64, kFsPT = 16, kFsChunkPT = 8;
-// (16 slots: 122 VGPRs; 24 or 32 spill at the 128 of 16 waves per CU)
-constexpr uint32_t kFsIdxBits = 14, kFsCap = (uint32_t)kFsThreads * kFsPT;  // 2^14 items
-static_assert(kFsCap == (1u << kFsIdxBits), "local index field");
-
-struct FsShared {
-    uint32_t buf[kFsCap + 1];     // exchange buffer; at the end the frame's keys / run starts
-    uint32_t cnt[kFsWaves][256];  // per-wave digit counters -> the wave's exclusive prefix
-    uint32_t base[256];           // digit bases (chunked form: the running digit offsets)
-    uint32_t wsum[kFsWaves];
-};
-
-// Rank this wave's items (slot j < S, lane l: item j * 64 + l of the wave) by digit: rk[j] = the
-// number of the wave's earlier items with the same digit, counted on in cntw[digit] (every lane
-// reads its digit's count, the digit group's first lane writes it back advanced; a wave's LDS
-// operations execute in order).  Padding items (past the frame's runs: a suffix of the item
-// order) are ranked like the others; they carry digit 255, so no valid item's position moves.
-// (LDS atomics with return instead: ~1 lane per clock, 4x slower on MI355X.)
-template <int PT, class Dig>
-__device__ __forceinline__ void fs_rank(Dig dig, uint32_t S, uint32_t* cntw, uint32_t (&rk)[PT]) {
-    const unsigned long long ltm = lanemask_lt();
-#pragma unroll
-    for (int j = 0; j < PT; ++j) {
-        if ((uint32_t)j < S) {  // (wave-uniform)
-            const uint32_t d = dig(j);
-            unsigned long long m = ~0ull;
-#pragma unroll
-            for (int b = 0; b < 8; ++b) {
-                const bool bit = (d >> b) & 1u;
-                const unsigned long long bb = __ballot(bit);
-                m &= bit ? bb : ~bb;
-            }
-            const uint32_t before = (uint32_t)__popcll(m & ltm);
-            const uint32_t base = cntw[d];
-            rk[j] = base + before;
-            __builtin_amdgcn_wave_barrier();
-            if (before == 0) cntw[d] = base + (uint32_t)__popcll(m);
-            __builtin_amdgcn_wave_barrier();
-        }
-    }
-}
-
-// After fs_rank of every wave (and a barrier): cnt[w][d] -> the exclusive prefix of digit d over
-// the waves before w; base[d] = the exclusive prefix of the digit totals (+ base[d] when
-// accumulating: the chunked form's running offsets).  Digit t's total goes to thread t < 256.
-__device__ __forceinline__ uint32_t fs_offsets(FsShared& sh, bool accumulate) {
-    const uint32_t t = threadIdx.x;
-    const int lane = t & 63, wid = t >> 6;
-    uint32_t tot = 0;
-    if (t < 256) {
-#pragma unroll
-        for (int w = 0; w < kFsWaves; ++w) {
-            const uint32_t c = sh.cnt[w][t];
-            sh.cnt[w][t] = tot;
-            tot += c;
-        }
-    }
-    uint32_t x = tot;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    if (t < 256 && lane == 63) sh.wsum[wid] = x;
-    __syncthreads();
-    if (t < 256) {
-        uint32_t wb = 0;
-        for (int w = 0; w < wid; ++w) wb += sh.wsum[w];
-        const uint32_t ex = wb + x - tot;
-        sh.base[t] = accumulate ? sh.base[t] + ex : ex;
-    }
-    __syncthreads();
-    return tot;
-}
-
-// [s0, s1): the runs of frame f, from the frame bits of the keys (key >> fshift, non-decreasing):
-// 1024 samples locate each bound to one interval, the interval's keys give it
-__device__ __forceinline__ void fs_frame_range(const uint32_t* keys, uint32_t n, uint32_t fshift,
-                                               uint32_t f, uint32_t& s0, uint32_t& s1) {
-    const uint32_t t = threadIdx.x;
-    const uint32_t stride = n ? (n + kFsThreads - 1) / kFsThreads : 1u;
-    const uint64_t i = (uint64_t)t * stride;
-    const uint32_t fr = i < n ? keys[i] >> fshift : 0xFFFFFFFFu;
-    const uint32_t c[2] = {(uint32_t)__syncthreads_count(i < n && fr < f),
-                           (uint32_t)__syncthreads_count(i < n && fr < f + 1u)};
-    uint32_t r[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {  // (block-uniform)
-        r[q] = 0;
-        if (c[q] == 0) continue;
-        const uint32_t start = (c[q] - 1u) * stride + 1u;
-        const uint32_t end = (uint32_t)min((uint64_t)c[q] * stride, (uint64_t)n);
-        uint32_t below = 0;
-        for (uint32_t b = start; b < end; b += kFsThreads) {
-            const uint32_t k = b + t;
-            below += (uint32_t)__syncthreads_count(k < end && (keys[k] >> fshift) < f + (uint32_t)q);
-        }
-        r[q] = start + below;
-    }
-    s0 = r[0];
-    s1 = r[1];
-}
-
-// The resident form of k_frame_sort: the frame's m <= 1024 * S runs as S slots per lane (slot j,
-// lane l of wave w: item w * 64 * S + j * 64 + l), every LSD pass through LDS.  Pass 0 ranks the
-// keys themselves; its exchange stores the packed item (key's voxel bits above 8) << 14 | local
-// index, which the later passes rank.  The padding past m (a suffix of the order) is all ones:
-// digit 255 in every pass.  (The item positions are recomputed from an opaque lane in every
-// phase: kept live across the passes they and their validity masks spill.)
-template <int S>
-__device__ __forceinline__ void fs_resident(FsShared& sh, const uint32_t* __restrict__ keys,
-                                            const uint32_t* __restrict__ run_start,
-                                            uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
-                                            uint32_t s0, uint32_t m, uint32_t npasses, uint32_t vmask,
-                                            uint32_t pack, uint32_t* err) {
-    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const uint32_t wbase = __builtin_amdgcn_readfirstlane(w * 64u * (uint32_t)S);
-    uint32_t item[S], rk[S];
-    uint32_t lx = lane;
-    asm volatile("" : "+v"(lx));
-#pragma unroll
-    for (int j = 0; j < S; ++j) item[j] = keys[s0 + min(wbase + (uint32_t)j * 64u + lx, m - 1u)];
-#pragma unroll
-    for (int j = 0; j < S; ++j)
-        if (wbase + (uint32_t)j * 64u + lx >= m) item[j] = 0xFFFFFFFFu;
-    __syncthreads();
-    for (uint32_t p = 0; p < npasses; ++p) {
-        const uint32_t sh_d = p == 0 ? 0u : kFsIdxBits + 8u * (p - 1u);
-        fs_rank<S>([&](int j) { return (item[j] >> sh_d) & 255u; }, S, sh.cnt[w], rk);
-        __syncthreads();
-        (void)fs_offsets(sh, false);
-        lx = lane;
-        asm volatile("" : "+v"(lx));
-#pragma unroll
-        for (int j = 0; j < S; ++j) {
-            const uint32_t r = wbase + (uint32_t)j * 64u + lx;
-            const uint32_t d = (item[j] >> sh_d) & 255u;
-            uint32_t word = item[j];
-            if (p == 0) word = r < m ? (((item[j] & vmask) >> 8) << kFsIdxBits) | r : 0xFFFFFFFFu;
-            sh.buf[sh.base[d] + sh.cnt[w][d] + rk[j]] = word;
-        }
-        __syncthreads();
-        lx = lane;
-        asm volatile("" : "+v"(lx));
-#pragma unroll
-        for (int j = 0; j < S; ++j) item[j] = sh.buf[wbase + (uint32_t)j * 64u + lx];
-        for (uint32_t i = t; i < kFsWaves * 256; i += kFsThreads) (&sh.cnt[0][0])[i] = 0u;
-        __syncthreads();
-    }
-    // the values, then the keys of the sorted runs, gathered from LDS by the local index (the
-    // frame's run starts / keys staged by loads all in flight together).  Packed: the run's
-    // first point is the value, its length - 1 goes to key bits 26..31.
-    lx = lane;
-    asm volatile("" : "+v"(lx));
-    if (pack) {
-#pragma unroll
-        for (int j = 0; j < S; ++j) rk[j] = run_start[s0 + min(wbase + (uint32_t)j * 64u + lx, m)];
-#pragma unroll
-        for (int j = 0; j < S; ++j) {
-            const uint32_t r = wbase + (uint32_t)j * 64u + lx;
-            if (r <= m) sh.buf[r] = rk[j];
-        }
-        if (t == 0 && m == (uint32_t)kFsThreads * S) sh.buf[m] = run_start[s0 + m];
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < S; ++j) {
-            const uint32_t r = wbase + (uint32_t)j * 64u + lx;
-            if (r < m) {
-                const uint32_t idx = item[j] & (kFsCap - 1u);
-                const uint32_t ps = sh.buf[idx], len = sh.buf[idx + 1] - ps;
-                if (len - 1u > 63u) atomicOr(err, 16u);  // (invariant: runs inside a wave word)
-                vout[s0 + r] = ps;
-                item[j] = idx | ((min(max(len, 1u), 64u) - 1u) << 16);
-            }
-        }
-        __syncthreads();
-    }
-#pragma unroll
-    for (int j = 0; j < S; ++j) rk[j] = keys[s0 + min(wbase + (uint32_t)j * 64u + lx, m - 1u)];
-#pragma unroll
-    for (int j = 0; j < S; ++j) sh.buf[wbase + (uint32_t)j * 64u + lx] = rk[j];
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < S; ++j) {
-        const uint32_t r = wbase + (uint32_t)j * 64u + lx;
-        if (r < m) {
-            const uint32_t idx = item[j] & (kFsCap - 1u);
-            const uint32_t k = sh.buf[idx];
-            if (pack) {
-                kout[s0 + r] = k | (((item[j] >> 16) & 63u) << kRunLenShift);
-            } else {
-                kout[s0 + r] = k;
-                vout[s0 + r] = s0 + idx;
-            }
-        }
-    }
-}
-
-__global__ __launch_bounds__(kFsThreads) void k_frame_sort(
-    const uint32_t* __restrict__ keys, const uint32_t* __restrict__ count,
-    const uint32_t* __restrict__ run_start, uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
-    uint32_t* __restrict__ ktmp, uint32_t* __restrict__ vtmp, uint32_t nframes, uint32_t fshift,
-    uint32_t vbits, uint32_t pack, uint32_t cap, uint32_t* err, uint32_t* qreset) {
-    __shared__ FsShared sh;
-    if (qreset && blockIdx.x == 0 && threadIdx.x == 0) {  // (the run-group queue of this voxelize)
-        qreset[0] = 0u;
-        qreset[1] = 0u;
-        qreset[2] = 0u;
-    }
-    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const uint32_t n = *count;
-    uint32_t s0 = 0, s1 = n;
-    if (nframes > 1) fs_frame_range(keys, n, fshift, blockIdx.x, s0, s1);
-    s0 = __builtin_amdgcn_readfirstlane(s0);  // (block-uniform: scalar slot loops below)
-    s1 = __builtin_amdgcn_readfirstlane(s1);
-    const uint32_t m = s1 - s0;
-    const uint32_t npasses = (max(vbits, 1u) + 7u) / 8u;
-    const uint32_t vmask = vbits >= 32 ? 0xFFFFFFFFu : (1u << vbits) - 1u;
-    for (uint32_t i = t; i < kFsWaves * 256; i += kFsThreads) (&sh.cnt[0][0])[i] = 0u;
-    if (m <= min(cap, kFsCap)) {
-        if (m == 0) return;
-        // ---- resident form: S slots per lane, a multiple of 4 (compile-time: no per-slot guards,
-        // the loads of all slots in flight together) ----
-        switch ((m + 4u * kFsThreads - 1u) / (4u * kFsThreads)) {
-            case 1: fs_resident<4>(sh, keys, run_start, kout, vout, s0, m, npasses, vmask, pack, err); break;
-            case 2: fs_resident<8>(sh, keys, run_start, kout, vout, s0, m, npasses, vmask, pack, err); break;
-            case 3: fs_resident<12>(sh, keys, run_start, kout, vout, s0, m, npasses, vmask, pack, err); break;
-            default: fs_resident<16>(sh, keys, run_start, kout, vout, s0, m, npasses, vmask, pack, err); break;
-        }
-        return;
-    }
-    // ---- chunked form: per pass a digit histogram of the frame, then chunks of S * 1024 items
-    // (S <= kFsChunkPT) ranked as above, scattered to the other buffer pair; only the last chunk
-    // has padding (ranked with the others, a suffix: its counts go to no later chunk) ----
-    const uint32_t S = max(1u, min(cap / (uint32_t)kFsThreads, (uint32_t)kFsChunkPT));
-    const uint32_t chunk = S * kFsThreads;
-    const uint32_t kmask = pack ? kRunKeyMask : 0xFFFFFFFFu;
-    for (uint32_t p = 0; p < npasses; ++p) {
-        const bool to_out = ((npasses - 1u - p) & 1u) == 0u;  // (the last pass lands in kout)
-        uint32_t* kd = to_out ? kout : ktmp;
-        uint32_t* vd = to_out ? vout : vtmp;
-        const uint32_t* ks = p == 0 ? keys : (to_out ? ktmp : kout);
-        const uint32_t* vs = p == 0 ? nullptr : (to_out ? vtmp : vout);
-        const uint32_t shift = 8u * p;
-        __syncthreads();
-#pragma unroll 8
-        for (uint32_t i = t; i < m; i += kFsThreads)  // (the frame's totals as wave 0's counts)
-            atomicAdd(&sh.cnt[0][((ks[s0 + i] & kmask) >> shift) & 255u], 1u);
-        __syncthreads();
-        (void)fs_offsets(sh, false);
-        for (uint32_t i = t; i < kFsWaves * 256; i += kFsThreads) (&sh.cnt[0][0])[i] = 0u;
-        __syncthreads();
-        for (uint32_t c0 = 0; c0 < m; c0 += chunk) {  // (block-uniform)
-            const uint32_t cm = min(chunk, m - c0);
-            const uint32_t wbase = __builtin_amdgcn_readfirstlane(w * 64u * S);
-            const uint32_t nv = cm > wbase ? min(cm - wbase, 64u * S) : 0u;
-            uint32_t kk[kFsChunkPT], vv[kFsChunkPT], rk[kFsChunkPT];
-#pragma unroll
-            for (int j = 0; j < kFsChunkPT; ++j) {
-                const uint32_t r = (uint32_t)j * 64u + lane;
-                const bool ok = (uint32_t)j < S && r < nv;
-                const uint32_t i = s0 + c0 + wbase + r;
-                kk[j] = ok ? ks[i] : 0u;
-                vv[j] = ok ? (vs ? vs[i] : i) : 0u;
-                if (p == 0 && pack && ok) {
-                    const uint32_t ps = run_start[i], len = run_start[i + 1] - ps;
-                    if (len - 1u > 63u) atomicOr(err, 16u);
-                    vv[j] = ps;
-                    kk[j] |= (min(max(len, 1u), 64u) - 1u) << kRunLenShift;
-                }
-            }
-            fs_rank<kFsChunkPT>([&](int j) { return ((kk[j] & kmask) >> shift) & 255u; }, S, sh.cnt[w], rk);
-            __syncthreads();
-            // cnt -> the waves' prefixes; the chunk's items go on top of the running digit offsets
-            uint32_t tot = 0;
-            if (t < 256) {
-#pragma unroll
-                for (int ww = 0; ww < kFsWaves; ++ww) {
-                    const uint32_t c = sh.cnt[ww][t];
-                    sh.cnt[ww][t] = tot;
-                    tot += c;
-                }
-            }
-            __syncthreads();
-#pragma unroll
-            for (int j = 0; j < kFsChunkPT; ++j) {
-                const uint32_t r = (uint32_t)j * 64u + lane;
-                if ((uint32_t)j < S && r < nv) {
-                    const uint32_t d = ((kk[j] & kmask) >> shift) & 255u;
-                    const uint32_t pos = s0 + sh.base[d] + sh.cnt[w][d] + rk[j];
-                    kd[pos] = kk[j];
-                    vd[pos] = vv[j];
-                }
-            }
-            __syncthreads();
-            if (t < 256) {
-                sh.base[t] += tot;
-#pragma unroll
-                for (int ww = 0; ww < kFsWaves; ++ww) sh.cnt[ww][t] = 0u;
-            }
-            __syncthreads();
-        }
-    }
-}
-
-// the historic-grid update of a frame-sorted voxelize (the look-back passes carry it in extra
-// blocks; the per-frame sort's workgroups hold a CU's LDS each, so it runs as its own launch).
-// The wait for the previous update (grid_seq_enter's spin) is a one-block launch of its own ahead
-// of it: a k_frame_sort workgroup needs an EMPTY CU (16 waves at 122 VGPRs), and hundreds of
-// spinning grid blocks of later batches on every CU - waiting for an update queued behind that
-// sort on a shared hardware queue - never let one drain (the pipeline of 4 batches hung so).
-__global__ __launch_bounds__(64) void k_grid_wait(GridSeq q) {
-    if (threadIdx.x == 0 && q.ctl) {
-        const uint32_t f = q.fptr ? __hip_atomic_load(q.fptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : q.f;
-        uint32_t spins = 0;
-        while ((int32_t)(__hip_atomic_load(&q.ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - f) < 0) {
-            if (++spins > kSpinLimit) {
-                atomicOr(q.err, 4u);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(8);
-        }
-    }
-}
-
-__global__ __launch_bounds__(256) void k_grid_fused(uint4* __restrict__ grid, uint32_t* __restrict__ marks,
-                                                     uint64_t nwords, uint32_t lifetime, GridSeq q,
-                                                     uint32_t nframes, uint64_t mark_words, SnapArgs snap) {
-    // (the previous update has completed: k_grid_wait ran before; the grid is read coherently)
-    const uint32_t f = q.ctl ? (q.fptr ? __hip_atomic_load(q.fptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : q.f) : 0u;
-    if (nframes > 1)
-        grid_u8_part_frames(grid, marks, nwords, lifetime, blockIdx.x, gridDim.x, nframes, mark_words, snap);
-    else
-        grid_u8_part(grid, marks, nwords, lifetime, blockIdx.x, gridDim.x, q);
-    grid_seq_leave<true>(q, f, gridDim.x);
-}
 
 // Voxel groups of the sorted keys and their outputs in ONE kernel (RadixGrouper::makeGroups,
 // inc/radix_grouper.h:35-64, + averageGridCells / occupiedGridCells, inc/voxelize.h:9-71).
@@ -3856,15 +3214,12 @@ constexpr uint32_t kPersistBlocks = 2048;  // blocks of a persistent sort / grou
 // above (capacity in 256-key tiles): group-id offsets by count + scan instead of the ticketed
 // look-back in k_group (measured on MI355X: a batch of four VGA frames, ~1.8 K tiles, runs its
 // group phase 1.7x faster through count + scan than through the look-back chain; one VGA frame,
-// 1.2 K tiles of capacity, 4 % faster per frame)
-uint32_t g_group_scan_tiles = 1024;
-// Staged groups of up to g_small_group points are summed by their own thread (thread_group_sum:
-// the four component chains side by side, one group per lane, the groups of a tile in parallel);
-// longer ones by a wave (gdf_voxsum.hpp's stretch sums: a wave per group, serial over a block's
-// groups).  Tuning knob GDF_SMALL_GROUP.
-uint32_t g_small_group = 32;
-uint32_t g_points_lane = 0;  // k_group: staged long groups by 4-lane chains (GDF_POINTS_LANE; measured
-                             // slower on single VGA / 720p frames: 5.7 / 9.9 vs 6.1 / 11.6 Gpoints/s)
+// 1.2 K tiles of capacity, 4 % faster per frame): Tuning::group_scan_tiles.
+// Staged groups of up to Tuning::small_group points are summed by their own thread
+// (thread_group_sum: the four component chains side by side, one group per lane, the groups of a
+// tile in parallel); longer ones by a wave (gdf_voxsum.hpp's stretch sums: a wave per group,
+// serial over a block's groups).  Tuning::points_lane: k_group's staged long groups by 4-lane
+// chains (measured slower on single VGA / 720p frames: 5.7 / 9.9 vs 6.1 / 11.6 Gpoints/s).
 
 // p[0] + ... + p[n-1] per component, in order, by one thread: blocks of 4 points alternate between
 // two register sets, the next block read while the current one is added (LDS latency off the
@@ -4251,31 +3606,20 @@ __global__ __launch_bounds__(256) void k_group_big(const uint32_t* __restrict__ 
 // in the compaction); a voxel group is a maximal sequence of sorted runs with one key and its
 // points are the concatenation of its runs' points - the same stable index order the reference
 // sums in (inc/voxelize.h:29-35), read as contiguous ranges with no per-point (key, index) list.
-// k_group_runs: points of a tile's groups staged in LDS (template: 512 or 2048), and the size up to
-// which a staged group is summed in-block (larger ones are queued); tuning knobs GDF_RUN_STAGE,
-// GDF_RUN_INBLOCK
-uint32_t g_run_stage = 2048;
-uint32_t g_run_inblock = 1024;  // (measured: C2 / 720p x4 / 4K best or within noise of best at 1024)
-// staged groups above g_small_group in k_group_runs (GDF_RUN_WAVE): 0 queued for k_group_runs_big,
-// 1 a wave's stretch sums (wave_group_sum), 2 four lanes' chains (lane_comp_chain, default)
-uint32_t g_run_wave = 2;
-
-uint32_t g_run_big_blocks = 1024;  // k_group_runs_big grid (tuning knob GDF_RUN_BIG_BLOCKS)
-// persistent grids of the radix passes and of the group phase, at most (tuning knobs
-// GDF_SORT_BLOCKS / GDF_GROUP_BLOCKS): the launches are sized by the capacity (the item count is
-// on the device), and a run sort's ~10x fewer items leave most blocks with no tile
-uint32_t g_sort_blocks = 2048, g_group_blocks = 2048;
-// chunks of k_group_runs_big (one 4-wave block per queued group): 1 K points (Q = 16) or 512
-// (Q = 8); 0 never 1 K, 1 always, 2 (default) for single frames - 4K depth frames (voxels of
-// ~20 K points) and rollbuffer windows (C3: 4.72 -> 4.49 ms per frame with 1 K chunks) - and 512
-// for multi-frame batches (tuning knob GDF_RUN_Q16)
-uint32_t g_run_q16 = 2;
-// k_group_runs_big sums the groups below the huge region one per wave (wave_stream_sum) when the
-// queue is long (1); tuning knob GDF_RUN_WAVE_MODE=0: every group in block mode, 2: wave mode
-// whatever the queue's length
-uint32_t g_run_wave_mode = 1;
-uint32_t g_group_first = 1;  // k_group_runs: the ends of tiles' last groups from k_group_count's first starts (GDF_GROUP_FIRST=0: the key search)
-uint32_t g_run_big_occ4 = 0;  // tuning knob GDF_RUN_BIG_OCC4 (k_group_runs_big at 4 waves per SIMD)
+// k_group_runs: points of a tile's groups staged in LDS (Tuning::run_stage: 512 or 2048), and the
+// size up to which a staged group is summed in-block (Tuning::run_inblock; larger ones are queued;
+// measured: C2 / 720p x4 / 4K best or within noise of best at 1024).  Staged groups above
+// small_group (Tuning::run_wave): 0 queued for k_group_runs_big, 1 a wave's stretch sums
+// (wave_group_sum), 2 four lanes' chains (lane_comp_chain, default).
+// Persistent grids of the radix passes and of the group phase, at most (Tuning::sort_blocks /
+// group_blocks): the launches are sized by the capacity (the item count is on the device), and a
+// run sort's ~10x fewer items leave most blocks with no tile.
+// Chunks of k_group_runs_big (one 4-wave block per queued group; grid Tuning::run_big_blocks): 1 K
+// points (Q = 16) or 512 (Q = 8); Tuning::run_q16 0 never 1 K, 1 always, 2 (default) for single
+// frames - 4K depth frames (voxels of ~20 K points) and rollbuffer windows (C3: 4.72 -> 4.49 ms per
+// frame with 1 K chunks) - and 512 for multi-frame batches.  k_group_runs_big sums the groups below
+// the huge region one per wave (wave_stream_sum) when the queue is long (Tuning::run_wave_mode 1;
+// 0: every group in block mode, 2: wave mode whatever the queue's length).
 
 
 // Wave64 inclusive sum scan on DPP (gdf_voxsum.hpp dpp_iscan).
@@ -4609,7 +3953,7 @@ __device__ __forceinline__ float wave_stream_sum(const uint32_t* __restrict__ rp
 // are summed by their thread, longer staged ones by a wave from LDS, and the others (past the
 // staged points, or continuing past the tile) are queued for k_group_runs_big - one append per
 // group, so a block never waits on a long chain.  Marks, frame voxel starts and corners as k_group.
-// WAVE (g_run_wave): staged groups above small_max are 0 queued like the unstaged ones, 1 summed
+// WAVE (Tuning::run_wave): staged groups above small_max are 0 queued like the unstaged ones, 1 summed
 // by a wave from LDS (wave_group_sum: per-wave transpose buffers, 59.4 instead of 37.6 KB of LDS -
 // 2 blocks per CU, not 4), 2 summed by 4 lanes each, one component chain per lane (16 groups per
 // wave, the tile's long groups dealt round-robin over the 4 waves).
@@ -5143,9 +4487,9 @@ static void launch_sort_pass(uint32_t tiles, hipStream_t s, const uint32_t* kin,
                              uint32_t* kout, uint32_t* vout, const VoxelizeArgs& a, uint32_t p,
                              uint32_t dbits) {
     // the first pass also carries the historic-grid update in extra blocks
-    const bool g = p == 0 && a.grid8 != nullptr && !a.grid_last;
+    const bool g = p == 0 && a.grid8 != nullptr;
     const uint64_t nwords = g ? (a.ncells + 31) / 32 : 0;
-    const uint32_t gb = g ? fused_grid_blocks(a.ncells) : 0;
+    const uint32_t gb = g ? fused_grid_blocks(a.ncells, a.tune->grid_wpt) : 0;
     hipLaunchKernelGGL((k_sort_pass<PT, NB>), dim3(tiles + gb), dim3(kSortThreads), 0, s, kin, vin, kout,
                        vout, a.count, a.hist + 256 * p, a.status, a.sgstatus,
                        reinterpret_cast<uint32_t*>(a.ctrs + kCtrSort0 + p),
@@ -5155,21 +4499,6 @@ static void launch_sort_pass(uint32_t tiles, hipStream_t s, const uint32_t* kin,
                        a.snap,
                        p == 0 ? reinterpret_cast<uint32_t*>(a.ctrs + kCtrRunQueue) : nullptr,
                        p == 0 && a.pack_runs ? a.run_start : nullptr);
-}
-
-// the historic-grid update as launches of its own (a one-block wait for the previous update, then
-// the update's blocks, none of them spinning)
-static hipError_t launch_grid_apart(const VoxelizeArgs& a, hipStream_t s) {
-    const uint64_t nwords = (a.ncells + 31) / 32;
-    if (a.gseq.ctl) {
-        hipLaunchKernelGGL(k_grid_wait, dim3(1), dim3(64), 0, s, a.gseq);
-        const hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL(k_grid_fused, dim3(fused_grid_blocks(a.ncells)), dim3(256), 0, s,
-                       reinterpret_cast<uint4*>(a.grid8), a.marks, nwords, a.lifetime, a.gseq,
-                       a.nframes, a.mark_words, a.snap);
-    return hipGetLastError();
 }
 
 // Blocks of k_group_runs_big<8> / <16> the current device holds at once, cached per device (an
@@ -5197,6 +4526,7 @@ static uint32_t resident_big_blocks(bool q16, bool occ4) {
 }
 
 hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hook) {
+    const Tuning& T = *a.tune;
     const uint32_t npasses = radix_passes(a.key_bits);
     const int pt = a.sort_pt == 4 || a.sort_pt == 8 ? a.sort_pt : 16;
     const uint32_t tile = kSortThreads * pt;
@@ -5207,62 +4537,22 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
     const uint32_t cap_tiles = (a.nmax + tile - 1) / tile;
     const uint32_t run_cap = a.run_start ? std::max<uint32_t>(256u, cap_tiles / 8) : cap_tiles;
     const uint32_t sort_tiles = std::min<uint32_t>(std::min(cap_tiles, run_cap),
-                                                   std::min<uint32_t>(kPersistBlocks, g_sort_blocks));
+                                                   std::min<uint32_t>(kPersistBlocks, T.sort_blocks));
     hipError_t e;
     const uint32_t* kin = a.keys;
     const uint32_t* vin = nullptr;
     uint32_t* kbuf[2] = {a.keys_a, a.keys_b};
     uint32_t* vbuf[2] = {a.vals_a, a.vals_b};
     const bool runs = a.run_start != nullptr;  // keys are run keys: sort runs, then expand
-    uint32_t sorted_passes = a.seg_sort ? 2u : npasses;  // (the free pair: kbuf[passes & 1])
-    if (a.frame_sort && runs) {  // one workgroup per frame (k_frame_sort), the grid update apart
-        HookScope hs(hook, GDF_KERNEL_SORT);
-        if (a.grid8 && !a.grid_last && (e = launch_grid_apart(a, s)) != hipSuccess) return e;
-        const uint32_t nf = std::max<uint32_t>(a.nframes, 1u);
-        const uint32_t vbits = a.nframes > 1 ? a.frame_shift : a.key_bits;
-        hipLaunchKernelGGL(k_frame_sort, dim3(nf), dim3(kFsThreads), 0, s, a.keys, a.count,
-                           a.run_start, kbuf[0], vbuf[0], kbuf[1], vbuf[1], a.nframes, a.frame_shift,
-                           vbits, a.pack_runs ? 1u : 0u, a.frame_sort_cap, a.err,
-                           reinterpret_cast<uint32_t*>(a.ctrs + kCtrRunQueue));
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        kin = kbuf[0];
-        vin = vbuf[0];
-        sorted_passes = 1;
-    }
-    if (!a.hist_ready && !a.seg_sort && !a.frame_sort) {
+    const uint32_t sorted_passes = npasses;  // (the free pair: kbuf[passes & 1])
+    if (!a.hist_ready) {
         unsigned hb = grid_blocks(a.nmax, 256 * 4);
         if (hb > 512) hb = 512;
         hipLaunchKernelGGL(k_sort_hist, dim3(hb), dim3(256), 0, s, a.keys, a.count, npasses, a.hist,
                            a.nframes, a.frame_shift, a.frame_pt_start);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    if (a.seg_sort && !a.frame_sort) {  // the frames' runs by two 11-bit passes (k_seg_sort_pass), no frame pass
-        HookScope hs(hook, GDF_KERNEL_SORT);
-        const uint32_t nseg = std::max<uint32_t>(a.nframes, 1u);
-        // persistent blocks: at most kPersistBlocks (the granules cover every tile, though)
-        const uint32_t tiles = std::min<uint32_t>(seg_sort_tiles(a.nmax, nseg), kPersistBlocks);
-        const uint32_t hb = std::min<uint32_t>((a.nmax + 255) / 256, 1024u);
-        hipLaunchKernelGGL(k_seg_hist, dim3(std::max<uint32_t>(hb, 1u)), dim3(256), 0, s, a.keys, a.count,
-                           nseg, a.frame_shift, a.seg_hist, a.seg_fstart);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        for (uint32_t p = 0; p < 2; ++p) {
-            const bool g = p == 0 && a.grid8 != nullptr && !a.grid_last;
-            const uint64_t nwords = g ? (a.ncells + 31) / 32 : 0;
-            const uint32_t gb = g ? fused_grid_blocks(a.ncells) : 0;
-            hipLaunchKernelGGL((k_seg_sort_pass<8>), dim3(tiles + gb), dim3(kSortThreads), 0, s, kin, vin,
-                               kbuf[p], vbuf[p], a.count, a.seg_hist, a.seg_fstart, nseg, a.frame_shift, p,
-                               a.seg_status, a.seg_gstatus,
-                               reinterpret_cast<uint32_t*>(a.ctrs + kCtrSort0 + p),
-                               reinterpret_cast<uint32_t*>(a.ctrs + kCtrEpoch), a.err, a.seg_done, tiles,
-                               reinterpret_cast<uint4*>(a.grid8), a.marks, nwords, a.lifetime, a.gseq,
-                               a.nframes, a.mark_words, a.snap,
-                               p == 0 ? reinterpret_cast<uint32_t*>(a.ctrs + kCtrRunQueue) : nullptr);
-            if ((e = hipGetLastError()) != hipSuccess) return e;
-            kin = kbuf[p];
-            vin = vbuf[p];
-        }
-    }
-    for (uint32_t p = 0; p < (a.seg_sort || a.frame_sort ? 0u : npasses); ++p) {
+    for (uint32_t p = 0; p < npasses; ++p) {
         const uint32_t remaining = a.key_bits > 8 * p ? a.key_bits - 8 * p : 0u;
         // (a 9-bit last digit: radix_wide_last)
         const bool wide = p + 1 == npasses && remaining == 9;
@@ -5289,14 +4579,14 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
     }
     const uint32_t* gcount = a.count;  // items of the group phase (points, or runs)
     const uint32_t max_tiles = (a.nmax + kGroupThreads - 1) / kGroupThreads;
-    const uint32_t group_tiles = std::min<uint32_t>(max_tiles, std::min<uint32_t>(kPersistBlocks, g_group_blocks));
+    const uint32_t group_tiles = std::min<uint32_t>(max_tiles, std::min<uint32_t>(kPersistBlocks, T.group_blocks));
     HookScope hs(hook, GDF_KERNEL_GROUP);
     const uint32_t* tile_base = nullptr;
     const uint32_t* tile_gtot = nullptr;
     const uint32_t* tile_first = nullptr;
     const uint32_t bigcap = (max_tiles + std::max<uint32_t>(group_tiles, 1u) - 1) /
                             std::max<uint32_t>(group_tiles, 1u);  // tiles per block (walk)
-    if (a.group_counts && max_tiles > g_group_scan_tiles) {
+    if (a.group_counts && max_tiles > T.group_scan_tiles) {
         // many tiles: their group-id offsets from a count + scan instead of one ticket each
         // (a single ticket counter serves ~10^2 draws per microsecond)
         // (up to kMaxGroupScanTiles tiles the count kernel scans its groups of kScanGroup tiles
@@ -5304,7 +4594,7 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
         const bool gscan = a.group_done && max_tiles <= kMaxGroupScanTiles;
         hipLaunchKernelGGL(k_group_count, dim3(group_tiles), dim3(256), 0, s, kin, gcount,
                            a.group_counts, gscan ? a.group_done : nullptr, a.group_offsets,
-                           a.group_gtot, runs && a.pack_runs && !a.seg_sort ? kRunKeyMask : 0xFFFFFFFFu,
+                           a.group_gtot, runs && a.pack_runs ? kRunKeyMask : 0xFFFFFFFFu,
                            runs ? a.group_first : nullptr);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (!gscan && (e = launch_scan(a.group_counts, max_tiles, a.group_offsets, nullptr, gcount,
@@ -5317,33 +4607,31 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
     if (runs) {  // groups of sorted runs; the long ones by k_group_runs_big
         const uint32_t gb = std::max<uint32_t>(group_tiles, 1u);
         uint32_t* qctr = reinterpret_cast<uint32_t*>(a.ctrs + kCtrRunQueue);
-        auto kg = g_run_wave == 1 ? (g_run_stage >= 2048 ? k_group_runs<2048, 1> : k_group_runs<512, 1>)
-                : g_run_wave == 2 ? (g_run_stage >= 2048 ? k_group_runs<2048, 2> : k_group_runs<512, 2>)
-                                  : (g_run_stage >= 2048 ? k_group_runs<2048, 0> : k_group_runs<512, 0>);
+        auto kg = T.run_wave == 1 ? (T.run_stage >= 2048 ? k_group_runs<2048, 1> : k_group_runs<512, 1>)
+                : T.run_wave == 2 ? (T.run_stage >= 2048 ? k_group_runs<2048, 2> : k_group_runs<512, 2>)
+                                  : (T.run_stage >= 2048 ? k_group_runs<2048, 0> : k_group_runs<512, 0>);
         hipLaunchKernelGGL(kg, dim3(gb), dim3(kGroupThreads), 0, s, kin, vin, gcount,
                            a.run_start, a.pts, reinterpret_cast<float*>(a.out), a.out_count,
                            a.gstatus, a.ggstatus, reinterpret_cast<uint32_t*>(a.ctrs + kCtrGroup),
                            reinterpret_cast<uint32_t*>(a.ctrs + kCtrEpoch), a.err, a.hist,
                            a.average, a.vp, a.group_marks, tile_base, a.bigq, a.bigq_cap, qctr,
                            a.nframes, a.frame_shift, a.frame_vox_start,
-                           std::min<uint32_t>(g_run_inblock, g_run_stage >= 2048 ? 2048u : 512u),
-                           kbuf[sorted_passes & 1], vbuf[sorted_passes & 1], g_small_group,  // (free after the sort)
-                           tile_gtot, a.group_mark_stride, a.pack_runs && !a.seg_sort ? 1u : 0u, tile_first);
+                           std::min<uint32_t>(T.run_inblock, T.run_stage >= 2048 ? 2048u : 512u),
+                           kbuf[sorted_passes & 1], vbuf[sorted_passes & 1], T.small_group,  // (free after the sort)
+                           tile_gtot, a.group_mark_stride, a.pack_runs ? 1u : 0u, tile_first);
         if (a.average) {
             if ((e = hipGetLastError()) != hipSuccess) return e;
-            const bool q16 = g_run_q16 == 1 ||
-                             (g_run_q16 == 2 && a.nframes <= 1);
-            const bool occ4 = g_run_big_occ4 != 0;
+            const bool q16 = T.run_q16 == 1 || (T.run_q16 == 2 && a.nframes <= 1);
+            const bool occ4 = T.run_big_occ4 != 0;
             const uint32_t rb = resident_big_blocks(q16, occ4);
-            const uint32_t big_blocks = std::min(g_run_big_blocks, rb);
+            const uint32_t big_blocks = std::min(T.run_big_blocks, rb);
             auto kb = occ4 ? (q16 ? k_group_runs_big<16, true> : k_group_runs_big<8, true>)
                            : (q16 ? k_group_runs_big<16, false> : k_group_runs_big<8, false>);
             hipLaunchKernelGGL(kb, dim3(big_blocks), dim3(256), 0, s, kbuf[sorted_passes & 1],
                                vbuf[sorted_passes & 1], a.pts, reinterpret_cast<float*>(a.out), a.bigq,
-                               a.bigq_cap, qctr, g_run_wave_mode);
+                               a.bigq_cap, qctr, T.run_wave_mode);
         }
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        return a.grid8 && a.grid_last ? launch_grid_apart(a, s) : hipSuccess;
+        return hipGetLastError();
     }
     hipLaunchKernelGGL(k_group, dim3(group_tiles ? group_tiles : 1), dim3(kGroupThreads), 0, s, kin,
                        vin, gcount, a.pts, reinterpret_cast<float*>(a.out), a.out_count,
@@ -5351,14 +4639,13 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
                        reinterpret_cast<uint32_t*>(a.ctrs + kCtrEpoch), a.err, a.hist, a.average,
                        a.vp, a.group_marks, tile_base, tile_base ? a.bigq : nullptr,
                        a.bigcnt, bigcap, a.nframes, a.frame_shift, a.frame_vox_start,
-                       g_small_group, g_points_lane, tile_gtot);
+                       T.small_group, T.points_lane, tile_gtot);
     if (tile_base && a.bigq && a.average) {
         if ((e = hipGetLastError()) != hipSuccess) return e;
         hipLaunchKernelGGL(k_group_big, dim3(2048), dim3(256), 0, s, vin, a.pts,
                            reinterpret_cast<float*>(a.out), a.bigq, a.bigcnt, group_tiles, bigcap);
     }
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    return a.grid8 && a.grid_last ? launch_grid_apart(a, s) : hipSuccess;
+    return hipGetLastError();
 }
 
 // ---- orphan shaders of the reference --------------------------------------

@@ -47,12 +47,8 @@ inline size_t seg_offsets_words(uint32_t segs) {
 // `rot45` and flying-pixel rings F (0: no filter) (graph node lookup)
 const void* frame_kernel(int which, int rot45, uint32_t F = 0);
 const void* mask_kernel(const FrameArgs& a);  // the compaction pass-1 kernel launch_frame uses
-extern uint32_t g_mask_px2;
 const void* emit_kernel(const FrameArgs& a);  // the compaction pass-2 kernel launch_frame uses
 bool emit_partition_kernels(const FrameArgs& a);
-extern uint32_t g_emit_px2;
-extern uint32_t g_grid_wpt;
-extern uint32_t g_mask_occ8, g_mask_rows;
 
 // filter_point_sequence + insert into the rollbuffer ring (w = mask): new points
 // [src0, src0 + cnt) (all by default) of the n uploaded, their filter neighbours over all n
@@ -73,8 +69,9 @@ struct SnapArgs {
     uint32_t* cnt;
 };
 void snap_dims(uint64_t ncells, uint32_t nblocks, uint32_t* waves, uint32_t* seg);
-// blocks of the grid update that the first sort pass carries (for the snapshot layout)
-uint32_t fused_grid_blocks(uint64_t ncells);
+// blocks of the grid update that the first sort pass carries (for the snapshot layout), at `wpt`
+// mark words per thread (Tuning::grid_wpt)
+uint32_t fused_grid_blocks(uint64_t ncells, uint32_t wpt);
 // blocks of k_grid_u8_batch
 uint32_t batch_grid_blocks(uint64_t ncells);
 // frame `frame`'s snapshot expanded into a dense u8 grid (out: padded to 32 bytes)
@@ -156,49 +153,19 @@ struct VoxelizeArgs {
     // the points)
     const uint32_t* run_start;
     const uint32_t* point_count;
-    // frame-segmented two-pass sort of the runs (k_seg_hist + 2 x k_seg_sort_pass: voxel keys of
-    // <= 22 bits, runs in frame order - the engine's own frame or batch): per-frame 11-bit digit
-    // histograms [16][2][2048] (zero on entry and exit), the frames' run starts [17], tile / group
-    // granules (seg_sort_tiles(nmax, nframes) x 2048, epoch-tagged), a self-resetting counter
-    int seg_sort;
     // the engine's own runs (<= 64 points each): the first radix pass packs each run's length into
-    // key bits 26..31 and sorts its first point as the value (sort keys of <= 25 bits; not with
-    // seg_sort)
+    // key bits 26..31 and sorts its first point as the value (sort keys of <= 25 bits)
     int pack_runs;
-    // per-frame LDS sort of the runs (k_frame_sort: one workgroup per frame, the engine's own runs
-    // in frame order, voxel keys of <= 25 bits); frame_sort_cap: runs of a frame sorted resident in
-    // LDS (above: the chunked form; the knob GDF_FRAME_SORT_CAP lowers it for the tests)
-    int frame_sort;
-    uint32_t frame_sort_cap;
-    // the historic-grid update after the group phase, as launches of its own (k_grid_wait +
-    // k_grid_fused), instead of extra blocks of the first radix pass (knob GDF_GRID_LAST)
-    int grid_last;
-    uint32_t* seg_hist;
-    uint32_t* seg_fstart;
-    unsigned long long* seg_status;
-    unsigned long long* seg_gstatus;
-    uint32_t* seg_done;
     uint64_t ncells;
     uint32_t lifetime;
     uint32_t* err;
     // outputs
     float4* out;
     uint32_t* out_count;
+    const Tuning* tune;  // the engine's launch shapes (sort / group grids, group-phase forms)
 };
 hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hook = nullptr);
 size_t voxelize_status_words(uint32_t nmax, uint32_t key_bits);
-// tiles (of 2048 runs) of the segmented sort over nmax items in nframes frames, its group granules
-uint32_t seg_sort_tiles(uint32_t nmax, uint32_t nframes);
-uint32_t seg_sort_groups(uint32_t nmax, uint32_t nframes);
-constexpr uint32_t kSegSortDigits = 2048;
-// runs per frame the per-frame sort keeps resident in one workgroup's LDS
-constexpr uint32_t kFrameSortResident = 16384;
-// capacity (256-key tiles) above which k_group takes its group-id offsets from count + scan
-extern uint32_t g_group_scan_tiles;
-// k_group_runs staging (512 or 2048 points) and in-block group size limit
-extern uint32_t g_run_stage, g_run_inblock, g_run_big_blocks, g_run_q16, g_small_group, g_run_wave, g_points_lane;
-extern uint32_t g_run_wave_mode, g_run_big_occ4, g_group_first;
-extern uint32_t g_sort_blocks, g_group_blocks;
 size_t voxelize_group_tiles(uint32_t nmax);
 
 // orphan shaders: mask_dilate (F <= kDilateMaxF) and single-matrix transform_points

@@ -132,7 +132,7 @@ EXPORTED = [
     "gdf_upload_point_sequences", "gdf_filter_new_point_sequences", "gdf_insert_new_point_sequences",
     "gdf_roll_rollbuffer", "gdf_select_timespan", "gdf_prepare_point_and_mask_buffers",
     "gdf_insert_selected_point_sequence", "gdf_transform_point_sequence", "gdf_get_rollbuffer_state",
-    "gdf_set_rollbuffer_shard", "gdf_get_rollbuffer_shard_order", "gdf_get_rollbuffer_pieces",
+    "gdf_set_rollbuffer_shard", "gdf_get_rollbuffer_pieces",
     "gdf_upload_depthmaps", "gdf_convert_depthmaps", "gdf_filter_flying_pixels", "gdf_crop_points",
     "gdf_apply_point_mask", "gdf_compute_voxel_coords", "gdf_voxelize", "gdf_voxel_occupancy_grid",
     "gdf_get_point_count", "gdf_download_points", "gdf_download_voxel_coords",
@@ -148,7 +148,7 @@ EXPORTED = [
     "gdf_next_frame_in_batch", "gdf_get_batch_ranges", "gdf_download_batch_occupancy_grid",
     "gdf_mask_dilate", "gdf_transform_points", "gdf_add_halo_depthmap_device",
     "gdf_partition_points", "gdf_voxelize_points", "gdf_partition_runs", "gdf_voxelize_runs", "gdf_voxelize_runs_marked", "gdf_set_partition_marks", "gdf_set_emit_partition", "gdf_set_partition_segments", "gdf_last_sort_items", "gdf_get_stream",
-    "gdf_get_graph_stats", "gdf_get_slot", "gdf_select_slot", "gdf_build_info",
+    "gdf_get_graph_stats", "gdf_get_slot", "gdf_select_slot", "gdf_build_info", "gdf_get_tuning",
     "gdf_download_frame", "gdf_set_slot_streams",
     # include/gdf_fused.h: a rank of the multi-GPU fused cloud in C++ over RCCL
     "gdf_fused_unique_id", "gdf_fused_create", "gdf_fused_destroy", "gdf_fused_halo_pixels",
@@ -256,6 +256,7 @@ def load_library(path: str = LIB_PATH):
         "gdf_get_slot": (i32, [vp, P(i32)]),
         "gdf_select_slot": (i32, [vp, i32]),
         "gdf_build_info": (C.c_char_p, []),
+        "gdf_get_tuning": (i32, [vp, C.c_char_p, u32]),
         "gdf_download_frame": (i32, [vp, u32, P(HostFrame)]),
         "gdf_set_slot_streams": (i32, [vp, vp, i32]),
         "gdf_fused_unique_id": (i32, [C.c_char_p, vp]),
@@ -266,7 +267,6 @@ def load_library(path: str = LIB_PATH):
         "gdf_fused_finish": (i32, [vp, i32, vp, P(u32)]),
         "gdf_fused_run": (i32, [vp, P(StreamCamera), P(FrameParams), u64, u64, u32, i32]),
         "gdf_set_rollbuffer_shard": (i32, [vp, u32, u32, u32]),
-        "gdf_get_rollbuffer_shard_order": (i32, [vp, vp, u32]),
         "gdf_get_rollbuffer_pieces": (i32, [vp, vp, u32, P(u32)]),
         "gdf_set_partition_segments": (i32, [vp, u32]),
         "gdf_fused_local_create": (i32, [i32, P(vp)]),
@@ -545,11 +545,13 @@ class GPUDepthmapFusion:
         """gdf_set_rollbuffer_shard: keep the points of sequences (k // block) % nshards == shard."""
         self._check(self._lib.gdf_set_rollbuffer_shard(self._h, shard, nshards, block))
 
-    def rollbuffer_shard_order(self, nshards: int):
-        """gdf_get_rollbuffer_shard_order: the shards in the selection's order."""
-        out = (C.c_uint32 * nshards)()
-        self._check(self._lib.gdf_get_rollbuffer_shard_order(self._h, out, nshards))
-        return list(out)
+    def rollbuffer_pieces(self):
+        """gdf_get_rollbuffer_pieces: the shard holding each piece of the selected window, in the
+        selection's order."""
+        out = (C.c_uint32 * 64)()
+        n = C.c_uint32()
+        self._check(self._lib.gdf_get_rollbuffer_pieces(self._h, out, 64, C.byref(n)))
+        return list(out[:n.value])
 
     def rollbuffer_state(self) -> RollbufferState:
         st = RollbufferState()
@@ -890,6 +892,13 @@ class GPUDepthmapFusion:
         c, r = C.c_uint64(0), C.c_uint64(0)
         self._check(self._lib.gdf_get_graph_stats(self._h, C.byref(c), C.byref(r)))
         return c.value, r.value
+
+    def tuning(self) -> str:
+        """gdf_get_tuning: the GDF_* tuning variables this engine was created under ("" = the
+        built-in defaults)."""
+        buf = C.create_string_buffer(4096)
+        self._check(self._lib.gdf_get_tuning(self._h, buf, len(buf)))
+        return buf.value.decode()
 
     def last_sort_items(self):
         """(items, runs): what the last synchronous processFrame's voxelize sorted - runs of

@@ -128,9 +128,7 @@ def test_download_frame_grid_mirror_deltas(Engine):
 
 
 @pytest.mark.parametrize("knobs", [{}, {"GDF_NO_MASK_PACKED": "1"}, {"GDF_NO_GROUP_SCAN": "1"},
-                                   {"GDF_SEG_SORT": "1"}, {"GDF_NO_PACK_RUNS": "1"},
-                                   {"GDF_FRAME_SORT": "1"}, {"GDF_GRID_LAST": "1"},
-                                   {"GDF_MASK_ROWS": "2"}, {"GDF_GROUP_FIRST": "0"},
+                                   {"GDF_NO_PACK_RUNS": "1"}, {"GDF_GROUP_FIRST": "0"},
                                    # sizes and alternative forms of the sort and group phases
                                    {"GDF_RUN_HIST_SORT": "1"}, {"GDF_RUN_HIST_ALL": "1"},
                                    {"GDF_SORT_BLOCKS": "1024"}, {"GDF_GROUP_BLOCKS": "1024"},
@@ -171,10 +169,8 @@ def test_batch8_vga_knobs_match_oracle(Engine, knobs):
                                   orc.downloadVoxelOccupancyGrid()), (knobs, b, j)
 
 
-@pytest.mark.parametrize("knobs", [{}, {"GDF_NO_GROUP_SCAN": "1"}, {"GDF_SEG_SORT": "1"},
-                                   {"GDF_NO_PACK_RUNS": "1"}, {"GDF_GRID_LAST": "1"},
-                                   {"GDF_RUN_WAVE_MODE": "2"}, {"GDF_MASK_ROWS": "2"},
-                                   {"GDF_GROUP_FIRST": "0"}])
+@pytest.mark.parametrize("knobs", [{}, {"GDF_NO_GROUP_SCAN": "1"}, {"GDF_NO_PACK_RUNS": "1"},
+                                   {"GDF_RUN_WAVE_MODE": "2"}, {"GDF_GROUP_FIRST": "0"}])
 def test_4k_frame_knobs_match_oracle(Engine, knobs):
     """A dense 4K frame (32 400 compaction segments, runs of equal keys): the group scans on and
     off, every output equal to the oracle's."""
@@ -277,3 +273,33 @@ def test_partition_runs_voxelize_runs_match_oracle(Engine, nparts, B, emit):
         assert np.array_equal(g.view(np.uint32), want[j].view(np.uint32)), (nparts, B, j)
         assert np.array_equal(union[j, :words], want_marks[j]), (nparts, B, j)
         assert not union[j, words:].any()
+
+
+def test_tuning_is_a_snapshot_per_engine(Engine):
+    """Each engine keeps the tuning taken at its creation (gdf_get_tuning): an engine created
+    under GDF_RUN_STAGE=512 / GDF_RUN_WAVE=1 reports them, one created afterwards without them
+    reports the built-in defaults, and the first one - still running its own shapes after the
+    second was created - stays bit-exact against the oracle on an 8-frame VGA batch."""
+    a = engine_with(Engine, GDF_RUN_STAGE="512", GDF_RUN_WAVE="1")
+    b = engine_with(Engine, GDF_RUN_STAGE=None, GDF_RUN_WAVE=None)
+    assert {"GDF_RUN_STAGE=512", "GDF_RUN_WAVE=1"} <= set(a.tuning().split()), a.tuning()
+    assert all(not t.startswith(("GDF_RUN_STAGE", "GDF_RUN_WAVE=")) for t in b.tuning().split())
+    p = ComponentParams()
+    cam = synth.make_camera(0, 640, 480)
+    frames = [synth.dense_frame(cam, 0, j) for j in range(8)]
+    orc = OracleFusion(threads=16)
+    for gpu in (a, b):
+        gpu.clear()
+        for j, f in enumerate(frames):
+            if j:
+                gpu.nextFrameInBatch()
+            gpu.addDepthmap(*cam_args(cam, f))
+        gpu.processFrame(p)
+    vox_a, vox_b = a.downloadVoxelizedPoints(), b.downloadVoxelizedPoints()
+    assert np.array_equal(vox_a[:, :3].view(np.uint32), vox_b[:, :3].view(np.uint32))
+    _, vs = a.batch_ranges()
+    orc.clear()
+    orc.addDepthmap(*cam_args(cam, frames[7]))
+    orc.processFrame(p)
+    w = orc.downloadVoxelizedPoints()[:, :3]
+    assert np.array_equal(vox_a[vs[7]:vs[8], :3].view(np.uint32), w.view(np.uint32))
