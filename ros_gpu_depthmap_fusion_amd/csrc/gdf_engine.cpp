@@ -314,7 +314,7 @@ constexpr const char* kTuningVars[] = {
     "GDF_SEL_SHAPE", "GDF_H2D_THREADS", "GDF_NO_GRAPHS", "GDF_NO_RUNS", "GDF_FORCE_RUNS",
     "GDF_RUN_HIST_SORT", "GDF_RUN_HIST_ALL", "GDF_NO_PACK_RUNS", "GDF_NO_XRUNS",
     "GDF_NO_GROUP_SCAN", "GDF_NO_MASK_PACKED", "GDF_NO_GRID_DELTA", "GDF_NO_EMIT_PART",
-    "GDF_NO_DL_PREFETCH", "GDF_DL_FORK"};
+    "GDF_NO_DL_PREFETCH", "GDF_DL_FORK", "GDF_GRID_GATE"};
 
 constexpr int kMaxPipe = 4;
 
@@ -574,6 +574,23 @@ struct gdf_engine {
     DevBuf d_snap_dense;  // a batch frame's grid expanded from its sparse snapshot (download)
     DevBuf d_gridctl;               // GridSeq counters [0] updates done, [1] blocks finished
     uint32_t grid_ticket = 0;       // sequence number of the next grid update
+    // The grid updates' order on the device is the ticket (GridSeq: a carrying launch's grid
+    // blocks wait until the updates before theirs are done).  That wait cannot stall: tickets
+    // follow the host's submission order, so the awaited update was submitted earlier - ahead of
+    // the waiter in any hardware queue the two share (in-order dispatch) - and the waiters of at
+    // most 4 slots (<= 4 x ~205 blocks of one wave each) leave the chip's other ~7 K wave slots to
+    // it; kSpinLimit turns a stall into GDF_ERR_DEVICE regardless.
+    // GDF_GRID_GATE=1 orders direct launches by the streams as well: a launch carrying an update
+    // waits for the event recorded after the previous update when that one ran on another stream
+    // (GDF_GRID_GATE=early: recorded right before it - next in its stream, dispatchable), so no
+    // block ever waits for work queued on another stream.  Measured on MI355X (A/B, one box, 2000
+    // steps each, profiles/r06/grid_gate/): C2 30.2 (tickets) vs 28.7 (gate) / 28.9 (early) -
+    // each cross-stream wait costs the batch's chain more than the spin it removes.
+    const char* grid_gate_env = getenv("GDF_GRID_GATE");
+    bool grid_gate = grid_gate_env != nullptr;
+    bool grid_gate_early = grid_gate_env && std::strcmp(grid_gate_env, "early") == 0;
+    hipEvent_t grid_ev = nullptr;       // recorded after the last gated update
+    hipStream_t grid_ev_stream = nullptr;  // ... on this stream (nullptr: none yet)
     uint32_t grid_gen = 0;          // bumped when the grid is (re)allocated: slots re-zero marks
     int grid_mode = 0;  // 0: u8 grid = history (lifetime <= 255); 1: u32 history + u8 output
     bool grid_alloc = false;
@@ -684,6 +701,24 @@ struct gdf_engine {
         q.f = f;
         q.err = sl().d_misc.as<uint32_t>() + kErr;
         return q;
+    }
+    // the stream gate of a grid update launched on st: the event to wait for before it (null:
+    // none - the previous gated update ran on st, or there was none) and the one to record after
+    hipEvent_t grid_gate_wait(hipStream_t st) const {
+        return grid_gate && npipe > 1 && grid_ev_stream && grid_ev_stream != st ? grid_ev : nullptr;
+    }
+    hipEvent_t grid_gate_record(hipStream_t st) {
+        if (!grid_gate || npipe <= 1) return nullptr;
+        if (!grid_ev) HIPCHK(hipEventCreateWithFlags(&grid_ev, hipEventDisableTiming));
+        grid_ev_stream = st;
+        return grid_ev;
+    }
+    // a grid-update launch of its own on st, between the gate's wait and record
+    template <class F>
+    void grid_gated(hipStream_t st, F&& launch) {
+        if (hipEvent_t w = grid_gate_wait(st)) HIPCHK(hipStreamWaitEvent(st, w, 0));
+        launch();
+        if (hipEvent_t r = grid_gate_record(st)) HIPCHK(hipEventRecord(r, st));
     }
 };
 
@@ -1300,8 +1335,10 @@ void widen_if_needed(gdf_engine* e, uint32_t lifetime, hipStream_t st) {
     ensure_misc(e);
     e->d_hist32.ensure((size_t)e->ncells * 4);
     e->d_out8.ensure((size_t)((e->ncells + 31) / 32) * 32);
-    HIPCHK(launch_widen_grid(e->d_grid8.as<uint8_t>(), e->d_hist32.as<uint32_t>(), e->ncells,
-                             e->grid_seq(e->grid_ticket++), st));
+    e->grid_gated(st, [&] {
+        HIPCHK(launch_widen_grid(e->d_grid8.as<uint8_t>(), e->d_hist32.as<uint32_t>(), e->ncells,
+                                 e->grid_seq(e->grid_ticket++), st));
+    });
     e->grid_mode = 1;
 }
 
@@ -1712,9 +1749,19 @@ void voxelize_launched(gdf_engine* e, int fused_grid_lifetime) {
     e->sl().vox_valid = true;
 }
 
+// the stream gate of the grid update a direct voxelize launch carries (its first radix pass)
+VoxelizeArgs gated(gdf_engine* e, VoxelizeArgs v, hipStream_t st) {
+    if (v.grid8) {
+        v.grid_wait = e->grid_gate_wait(st);
+        v.grid_rec = e->grid_gate_record(st);
+        v.grid_rec_early = e->grid_gate_early ? 1 : 0;
+    }
+    return v;
+}
+
 void voxelize(gdf_engine* e, int average, int fused_grid_lifetime = -1) {
     e->sl().pf_valid = false;
-    const VoxelizeArgs v = voxelize_args(e, average, fused_grid_lifetime);
+    const VoxelizeArgs v = gated(e, voxelize_args(e, average, fused_grid_lifetime), e->s());
     e->timed(GDF_KERNEL_VOXELIZE, [&] { HIPCHK(launch_voxelize(v, e->s(), e->hook_ptr())); });
     voxelize_launched(e, fused_grid_lifetime);
 }
@@ -1897,7 +1944,8 @@ void run_fused_frame(gdf_engine* e, int average, uint32_t lifetime) {
         if (e->profiling) e->timed(GDF_KERNEL_EVENT_FLOOR, [] {});
         e->timed(GDF_KERNEL_FRAME, [&] { HIPCHK(launch_frame(a, st, e->hook_ptr())); });
         if (prefetch_fork(e)) prefetch_downloads(e, st, DL_POINTS);
-        e->timed(GDF_KERNEL_VOXELIZE, [&] { HIPCHK(launch_voxelize(v, st, e->hook_ptr())); });
+        const VoxelizeArgs vg = gated(e, v, st);
+        e->timed(GDF_KERNEL_VOXELIZE, [&] { HIPCHK(launch_voxelize(vg, st, e->hook_ptr())); });
     }
     voxelize_launched(e, (int)lifetime);
     prefetch_downloads(e, st, DL_MISC | DL_VOX | DL_DELTA | (prefetch_fork(e) ? 0u : DL_POINTS));
@@ -1916,12 +1964,14 @@ void occupancy_grid(gdf_engine* e, uint32_t lifetime, hipStream_t st) {  // fusi
     GridSeq q = e->grid_seq(e->grid_ticket);
     delta_args(e, q, e->grid_ticket, st == e->s());
     e->grid_ticket++;
-    e->timed_on(GDF_KERNEL_GRID, st, [&] {
-        if (e->grid_mode == 0)
-            HIPCHK(launch_grid_u8(e->d_grid8.as<uint8_t>(), marks_ptr(e), e->ncells, lifetime, q, st));
-        else
-            HIPCHK(launch_grid_u32(e->d_hist32.as<uint32_t>(), marks_ptr(e),
-                                   e->d_out8.as<uint8_t>(), e->ncells, lifetime, q, st));
+    e->grid_gated(st, [&] {
+        e->timed_on(GDF_KERNEL_GRID, st, [&] {
+            if (e->grid_mode == 0)
+                HIPCHK(launch_grid_u8(e->d_grid8.as<uint8_t>(), marks_ptr(e), e->ncells, lifetime, q, st));
+            else
+                HIPCHK(launch_grid_u32(e->d_hist32.as<uint32_t>(), marks_ptr(e),
+                                       e->d_out8.as<uint8_t>(), e->ncells, lifetime, q, st));
+        });
     });
     e->sl().marks_set = false;
     e->invoked_once = true;
@@ -2113,6 +2163,7 @@ int gdf_destroy(gdf_engine* e) {
         (void)hipEventDestroy(p.b);
     }
     for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
+    if (e->grid_ev) (void)hipEventDestroy(e->grid_ev);
     for (Slot& sl : e->slots) {
         sl.graph.reset();
         if (sl.dl_aux) {
@@ -3105,11 +3156,13 @@ int gdf_voxel_occupancy_grid_batch(gdf_engine* e, const uint32_t* bits, uint64_t
             for (uint32_t f0 = 0; f0 < nframes || f0 == 0; f0 += (uint32_t)kMaxCams) {
                 const uint32_t nf = std::min<uint32_t>(nframes - f0, (uint32_t)kMaxCams);
                 const GridSeq q = e->grid_seq(e->grid_ticket++);
-                e->timed_on(GDF_KERNEL_GRID, e->s(), [&] {
-                    HIPCHK(launch_grid_u8_batch(e->d_grid8.as<uint8_t>(),
-                                                bits ? bits + (uint64_t)f0 * frame_stride_words : bits,
-                                                e->ncells, nranks, nf, frame_stride_words,
-                                                rank_stride_words, lifetime, q, sn, e->s()));
+                e->grid_gated(e->s(), [&] {
+                    e->timed_on(GDF_KERNEL_GRID, e->s(), [&] {
+                        HIPCHK(launch_grid_u8_batch(e->d_grid8.as<uint8_t>(),
+                                                    bits ? bits + (uint64_t)f0 * frame_stride_words : bits,
+                                                    e->ncells, nranks, nf, frame_stride_words,
+                                                    rank_stride_words, lifetime, q, sn, e->s()));
+                    });
                 });
                 if (nframes == 0) break;
             }

@@ -4557,6 +4557,9 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
         // (a 9-bit last digit: radix_wide_last)
         const bool wide = p + 1 == npasses && remaining == 9;
         const uint32_t dbits = wide ? 9u : remaining >= 8 ? 8u : (remaining ? remaining : 1u);
+        const bool gate = p == 0 && a.grid8 != nullptr;
+        if (gate && a.grid_wait && (e = hipStreamWaitEvent(s, a.grid_wait, 0)) != hipSuccess) return e;
+        if (gate && a.grid_rec && a.grid_rec_early && (e = hipEventRecord(a.grid_rec, s)) != hipSuccess) return e;
         if (sort_tiles) {
             HookScope hs(hook, GDF_KERNEL_SORT);
             if (wide) {
@@ -4574,6 +4577,7 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
                 launch_sort_pass<16, 256>(sort_tiles, s, kin, vin, kbuf[p & 1], vbuf[p & 1], a, p, dbits);
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
+        if (gate && a.grid_rec && !a.grid_rec_early && (e = hipEventRecord(a.grid_rec, s)) != hipSuccess) return e;
         kin = kbuf[p & 1];
         vin = vbuf[p & 1];
     }

@@ -163,6 +163,12 @@ struct VoxelizeArgs {
     float4* out;
     uint32_t* out_count;
     const Tuning* tune;  // the engine's launch shapes (sort / group grids, group-phase forms)
+    // the stream gate of the grid update carried by the first radix pass (direct launches): wait
+    // for grid_wait before that pass, record grid_rec after it - or, grid_rec_early, right before
+    // it: the next update then waits until this one is next in its stream (dispatchable), not
+    // done (null: none, e.g. graph capture)
+    hipEvent_t grid_wait, grid_rec;
+    int grid_rec_early;
 };
 hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hook = nullptr);
 size_t voxelize_status_words(uint32_t nmax, uint32_t key_bits);
