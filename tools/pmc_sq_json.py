@@ -15,7 +15,8 @@ import json
 SLOT = {"k_mask": ("mask", 64), "k_mask_px<2, 256>": ("mask", 128), "k_mask_px_o8<2, 256>": ("mask", 128), "k_mask_px<4, 256>": ("mask", 256),
         "k_mask_px<2, 640>": ("mask", 128), "k_emit_px2<256>": ("emit", 128), "k_emit": ("emit_1px", 64),
         "k_sort_pass<8, 256>": ("sort", 64), "k_sort_pass<8, 512>": ("sort_wide", 64),
-        "k_group_runs<2048, 2>": ("group", 0)}
+        "k_group_runs<2048, 2>": ("group", 0), "k_sel<16u>": ("sel", 1024), "k_sel<8u>": ("sel", 512),
+        "k_group_runs_big<16, false>": ("group_big", 0)}
 
 
 def main():
@@ -23,6 +24,7 @@ def main():
     ap.add_argument("csv")
     ap.add_argument("--workload", required=True)
     ap.add_argument("--out", default="profiles/pmc_sq.json")
+    ap.add_argument("--source", default=None, help="where the committed CSV lives (recorded)")
     args = ap.parse_args()
     tot = collections.defaultdict(lambda: collections.defaultdict(float))
     disp = collections.defaultdict(set)
@@ -33,7 +35,7 @@ def main():
         disp[k].add(r["Dispatch_Id"])
     out = {}
     for k, c in tot.items():
-        if k not in SLOT or not c.get("SQ_WAVES"):
+        if k not in SLOT or not c.get("SQ_WAVES") or not c.get("SQ_WAVE_CYCLES"):
             continue
         w, wc = c["SQ_WAVES"], c["SQ_WAVE_CYCLES"]
         slot, ppw = SLOT[k]
@@ -51,9 +53,10 @@ def main():
         doc = {}
     doc["_note"] = ("rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES "
                     "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY of `python3 bench.py --steps 10 "
-                    "--warmup 2 --no-secondary --no-cpu-baseline --no-kernel-timing` "
-                    "(tools/pmc_sq_json.py); per-wave ratios (the SQ counters sample a subset of the "
-                    "chip's waves; ratios only)")
+                    "--warmup 2 --no-secondary --no-cpu-baseline --no-kernel-timing --pipeline 1` "
+                    "(C2) / `tools/bench_c3.py --steps 3 --profile-steps 1` (C3), tools/pmc_sq_json.py; "
+                    "per-wave ratios (the SQ counters sample a subset of the chip's waves; ratios only)")
+    out["_source"] = args.source or args.csv
     doc[args.workload] = out
     json.dump(doc, open(args.out, "w"), indent=1)
     print(json.dumps(out, indent=1))
