@@ -452,6 +452,26 @@ int gdf_voxelize_runs_marked(gdf_engine* engine, const float* points_device,
                              const uint32_t* run_keys_device, uint32_t* run_starts_device,
                              uint32_t nsources, const uint32_t* point_base, const uint32_t* run_base,
                              int average_voxels, uint32_t* marks_device, uint64_t frame_stride_words);
+/* The multi-GPU step's receive side (include/gdf_fused.h) with its fixed work folded into the
+ * rebase pass: as gdf_voxelize_runs_marked, where `own` names up to 4 sources that are still in
+ * THIS rank's send lists (its own buckets: read from there - run starts rebased, points and run
+ * keys written into pts / run_keys at their place - instead of device copies first) and mark
+ * words to clear before the voxelize marks its voxels (clear_rows rows of clear_row_words at
+ * clear_stride_words: the key range's slice of each frame). */
+typedef struct gdf_recv_own {
+    uint32_t count;
+    uint32_t source[4];
+    const float* points[4];
+    const uint32_t* run_keys[4];
+    const uint32_t* run_starts[4];
+    uint32_t* clear;
+    uint64_t clear_row_words, clear_stride_words;
+    uint32_t clear_rows;
+} gdf_recv_own;
+int gdf_voxelize_runs_recv(gdf_engine* engine, float* points, uint32_t* run_keys,
+                           uint32_t* run_starts, uint32_t nsources, const uint32_t* point_base,
+                           const uint32_t* run_base, int average, uint32_t* marks,
+                           uint64_t frame_stride_words, const gdf_recv_own* own);
 
 /* ---- live kernel timing (HIP events on the engine stream) ------------------------------------ */
 enum gdf_kernel_slot {

@@ -2916,53 +2916,98 @@ int gdf_voxelize_runs(gdf_engine* e, const float* pts, const uint32_t* run_keys,
                                     average, nullptr, 0);
 }
 
+namespace {
+void voxelize_runs(gdf_engine* e, const float* pts, const uint32_t* run_keys, uint32_t* run_starts,
+                   uint32_t nsources, const uint32_t* point_base, const uint32_t* run_base,
+                   int average, uint32_t* marks, uint64_t frame_stride_words, const gdf_recv_own* own) {
+    if (marks && (frame_stride_words < mark_words(e) || (e->nframes > 1 && frame_stride_words == 0)))
+        fail(GDF_ERR_CAPACITY, "voxelize_runs: a frame's marks need >= the grid's mark words");
+    if (!e->grid_set) fail(GDF_ERR_STATE, "voxelize_runs needs the voxel grid of a frame");
+    if (nsources == 0 || nsources > kMaxSources || !point_base || !run_base)
+        fail(GDF_ERR_ARG, "voxelize_runs: 1..32 sources and their bases");
+    RebaseArgs rb;
+    std::memset(&rb, 0, sizeof(rb));
+    rb.nsrc = nsources;
+    for (uint32_t k = 0; k <= nsources; ++k) {
+        rb.point_base[k] = point_base[k];
+        rb.run_base[k] = run_base[k];
+        if (k && (point_base[k] < point_base[k - 1] || run_base[k] < run_base[k - 1]))
+            fail(GDF_ERR_ARG, "voxelize_runs: bases must not decrease");
+        if (k && (run_base[k] > run_base[k - 1]) != (point_base[k] > point_base[k - 1]))
+            fail(GDF_ERR_ARG, "voxelize_runs: a source has points without runs or runs without points");
+    }
+    const uint32_t n = point_base[nsources], R = run_base[nsources];
+    if (R && (!pts || !run_keys || !run_starts)) fail(GDF_ERR_ARG, "voxelize_runs: null list");
+    if (!run_starts) fail(GDF_ERR_ARG, "voxelize_runs: run_starts needs R + 1 entries");
+    if (own) {
+        if (own->count > kMaxOwnSources) fail(GDF_ERR_ARG, "voxelize_runs: at most 4 own sources");
+        rb.n_own = own->count;
+        for (uint32_t k = 0; k < own->count; ++k) {
+            if (own->source[k] >= nsources) fail(GDF_ERR_ARG, "voxelize_runs: own source out of range");
+            for (uint32_t j = 0; j < k; ++j)
+                if (own->source[j] == own->source[k]) fail(GDF_ERR_ARG, "voxelize_runs: own source twice");
+            const uint32_t q = own->source[k];
+            if (point_base[q + 1] > point_base[q] && (!own->points[k] || !own->run_keys[k] || !own->run_starts[k]))
+                fail(GDF_ERR_ARG, "voxelize_runs: null own list");
+            rb.own_src[k] = q;
+            rb.own_pts[k] = reinterpret_cast<const float4*>(own->points[k]);
+            rb.own_run_keys[k] = own->run_keys[k];
+            rb.own_run_starts[k] = own->run_starts[k];
+        }
+        rb.pts = reinterpret_cast<float4*>(const_cast<float*>(pts));
+        rb.run_keys = const_cast<uint32_t*>(run_keys);
+        if (own->clear && own->clear_rows && own->clear_row_words) {
+            if (own->clear_rows > 1 && own->clear_stride_words < own->clear_row_words)
+                fail(GDF_ERR_ARG, "voxelize_runs: clear rows overlap");
+            rb.zero = own->clear;
+            rb.zero_row_words = own->clear_row_words;
+            rb.zero_stride = own->clear_stride_words;
+            rb.zero_rows = own->clear_rows;
+        }
+    }
+    ensure_misc(e);
+    if (e->sl().khist_pending) {  // the frame's compaction counted ITS keys' digits: not these
+        HIPCHK(hipMemsetAsync(e->sl().d_khist.p, 0, kHistWords * 4, e->s()));
+        e->sl().khist_pending = false;
+    }
+    e->sl().pf_valid = false;
+    uint32_t* misc = e->sl().d_misc.as<uint32_t>();
+    HIPCHK(launch_run_rebase(run_starts, rb, misc + kRecvCount, misc + kRecvRuns, e->s()));
+    VoxSource src;
+    src.pts = reinterpret_cast<const float4*>(pts);
+    src.keys = run_keys;
+    src.n = n;
+    src.run_keys = run_keys;
+    src.run_start = run_starts;
+    VoxelizeArgs v = voxelize_args(e, average, -1, &src);
+    if (marks) {  // every voxel's mark, frame f at f * stride (k_group_runs)
+        v.group_marks = marks;
+        v.group_mark_stride = frame_stride_words;
+    }
+    e->timed(GDF_KERNEL_VOXELIZE, [&] { HIPCHK(launch_voxelize(v, e->s(), e->hook_ptr())); });
+    e->sl().vox_valid = true;
+}
+}  // namespace
+
 int gdf_voxelize_runs_marked(gdf_engine* e, const float* pts, const uint32_t* run_keys,
                              uint32_t* run_starts, uint32_t nsources, const uint32_t* point_base,
                              const uint32_t* run_base, int average, uint32_t* marks,
                              uint64_t frame_stride_words) {
     ENGINE_OR_FAIL(e);
     return guarded(e, [&] {
-        if (marks && (frame_stride_words < mark_words(e) ||
-                      (e->nframes > 1 && frame_stride_words == 0)))
-            fail(GDF_ERR_CAPACITY, "voxelize_runs: a frame's marks need >= the grid's mark words");
-        if (!e->grid_set) fail(GDF_ERR_STATE, "voxelize_runs needs the voxel grid of a frame");
-        if (nsources == 0 || nsources > kMaxSources || !point_base || !run_base)
-            fail(GDF_ERR_ARG, "voxelize_runs: 1..32 sources and their bases");
-        RebaseArgs rb;
-        std::memset(&rb, 0, sizeof(rb));
-        rb.nsrc = nsources;
-        for (uint32_t k = 0; k <= nsources; ++k) {
-            rb.point_base[k] = point_base[k];
-            rb.run_base[k] = run_base[k];
-            if (k && (point_base[k] < point_base[k - 1] || run_base[k] < run_base[k - 1]))
-                fail(GDF_ERR_ARG, "voxelize_runs: bases must not decrease");
-            if (k && (run_base[k] > run_base[k - 1]) != (point_base[k] > point_base[k - 1]))
-                fail(GDF_ERR_ARG, "voxelize_runs: a source has points without runs or runs without points");
-        }
-        const uint32_t n = point_base[nsources], R = run_base[nsources];
-        if (R && (!pts || !run_keys || !run_starts)) fail(GDF_ERR_ARG, "voxelize_runs: null list");
-        if (!run_starts) fail(GDF_ERR_ARG, "voxelize_runs: run_starts needs R + 1 entries");
-        ensure_misc(e);
-        if (e->sl().khist_pending) {  // the frame's compaction counted ITS keys' digits: not these
-            HIPCHK(hipMemsetAsync(e->sl().d_khist.p, 0, kHistWords * 4, e->s()));
-            e->sl().khist_pending = false;
-        }
-        e->sl().pf_valid = false;
-        uint32_t* misc = e->sl().d_misc.as<uint32_t>();
-        HIPCHK(launch_run_rebase(run_starts, rb, misc + kRecvCount, misc + kRecvRuns, e->s()));
-        VoxSource src;
-        src.pts = reinterpret_cast<const float4*>(pts);
-        src.keys = run_keys;
-        src.n = n;
-        src.run_keys = run_keys;
-        src.run_start = run_starts;
-        VoxelizeArgs v = voxelize_args(e, average, -1, &src);
-        if (marks) {  // every voxel's mark, frame f at f * stride (k_group_runs)
-            v.group_marks = marks;
-            v.group_mark_stride = frame_stride_words;
-        }
-        e->timed(GDF_KERNEL_VOXELIZE, [&] { HIPCHK(launch_voxelize(v, e->s(), e->hook_ptr())); });
-        e->sl().vox_valid = true;
+        voxelize_runs(e, pts, run_keys, run_starts, nsources, point_base, run_base, average, marks,
+                      frame_stride_words, nullptr);
+    });
+}
+
+int gdf_voxelize_runs_recv(gdf_engine* e, float* pts, uint32_t* run_keys, uint32_t* run_starts,
+                           uint32_t nsources, const uint32_t* point_base, const uint32_t* run_base,
+                           int average, uint32_t* marks, uint64_t frame_stride_words,
+                           const gdf_recv_own* own) {
+    ENGINE_OR_FAIL(e);
+    return guarded(e, [&] {
+        voxelize_runs(e, pts, run_keys, run_starts, nsources, point_base, run_base, average, marks,
+                      frame_stride_words, own);
     });
 }
 

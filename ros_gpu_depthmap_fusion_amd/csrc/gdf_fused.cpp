@@ -648,8 +648,9 @@ void fused_start(gdf_fused* f, const uint16_t* const* depth, uint32_t B, const g
     S.lifetime = q.occupancy_lifetime;
     // every rank's split sizes (the partition's, written with the compaction) to pinned memory
     // (no wait here)
-    x.all_gather(cnt, cntall, rec * 4, kHalo, st);
-    hipchk(hipMemcpyAsync(S.host, cntall, rec * W * 4, hipMemcpyDeviceToHost, st),
+    // (world 1: the all-gather is the record itself)
+    if (W > 1) x.all_gather(cnt, cntall, rec * 4, kHalo, st);
+    hipchk(hipMemcpyAsync(S.host, W > 1 ? cntall : cnt, rec * W * 4, hipMemcpyDeviceToHost, st),
            "hipMemcpyAsync(counts)");
     hipchk(hipEventRecord(S.ev, st), "hipEventRecord");
     S.average = q.voxel_average ? 1 : 0;
@@ -729,17 +730,20 @@ void fused_finish(gdf_fused* f, int slot, uint32_t* send_counts, uint32_t* recv_
                 ro += runs_of(R, q, sg);
             }
     }
-    // the rank's own buckets: device copies (an RCCL self send / recv is a slower kernel copy)
-    for (uint32_t sg = 0; sg < NSg; ++sg)
-        if (const size_t c = pts_of(R, R, sg)) {
-            const size_t rc = runs_of(R, R, sg);
-            hipchk(hipMemcpyAsync(rp + 4 * recv_at[R][sg], S.sp.as<float>() + 4 * send_at[R][sg], 16 * c,
-                                  hipMemcpyDeviceToDevice, st), "hipMemcpyAsync(points)");
-            hipchk(hipMemcpyAsync(rrk + rrecv_at[R][sg], S.srk.as<uint32_t>() + rsend_at[R][sg], 4 * rc,
-                                  hipMemcpyDeviceToDevice, st), "hipMemcpyAsync(run keys)");
-            hipchk(hipMemcpyAsync(rrs + rrecv_at[R][sg], S.srs.as<uint32_t>() + rsend_at[R][sg], 4 * rc,
-                                  hipMemcpyDeviceToDevice, st), "hipMemcpyAsync(run starts)");
-        }
+    // the rank's own buckets stay in its send lists: the voxelize's rebase pass reads them there
+    // (gdf_voxelize_runs_recv; an RCCL self send / recv would be a kernel copy, a device copy a
+    // launch each)
+    gdf_recv_own own{};
+    for (int k = 0; k < NS; ++k) {
+        if (src_rank[k] != R) continue;
+        const int sg = src_seg[k];
+        if (own.count >= 4) fail(GDF_ERR_STATE, "fused finish: more than 4 own buckets");
+        own.source[own.count] = (uint32_t)k;
+        own.points[own.count] = S.sp.as<float>() + 4 * send_at[R][sg];
+        own.run_keys[own.count] = S.srk.as<uint32_t>() + rsend_at[R][sg];
+        own.run_starts[own.count] = S.srs.as<uint32_t>() + rsend_at[R][sg];
+        ++own.count;
+    }
     if (W > 1) {
         x.group_start(kPoints);
         for (int q = 0; q < W; ++q) {
@@ -770,11 +774,14 @@ void fused_finish(gdf_fused* f, int slot, uint32_t* send_counts, uint32_t* recv_
     const uint64_t Sw = (words + W - 1) / W;  // = part_slice_words(W, ncells), the partition's rule
     const uint64_t stride = Sw * W;
     uint32_t* uni = S.gathered.ensure<uint32_t>(S.nframes * stride * 4, st);
-    // (only slice R of each frame: the voxelize marks inside its key range, the all-gather
-    // overwrites the other slices)
-    hipchk(hipMemset2DAsync(uni + (uint64_t)R * Sw, stride * 4, 0, Sw * 4, S.nframes, st),
-           "hipMemset2DAsync(marks)");
-    gdfchk(gdf_voxelize_runs_marked(e, rp, rrk, rrs, (uint32_t)NS, pbase, rbase, S.average, uni, stride));
+    // (only slice R of each frame is cleared - by the rebase pass: the voxelize marks inside its
+    // key range, the all-gather overwrites the other slices)
+    own.clear = uni + (uint64_t)R * Sw;
+    own.clear_row_words = Sw;
+    own.clear_stride_words = stride;
+    own.clear_rows = S.nframes;
+    gdfchk(gdf_voxelize_runs_recv(e, rp, rrk, rrs, (uint32_t)NS, pbase, rbase, S.average, uni, stride,
+                                  &own));
     if (W > 1) {  // (on the points' communicator: the finish's collectives stay in step order,
                   // never behind the next step's start collectives on the halo communicator)
         x.group_start(kPoints);

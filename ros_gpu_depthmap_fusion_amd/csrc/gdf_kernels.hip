@@ -5019,18 +5019,48 @@ hipError_t launch_download(const DlArgs& d, hipStream_t s) {
 
 // The received run lists of gdf_voxelize_runs: source q's run starts are relative to its point
 // segment - add its point base; close the list (run_start[R] = n) and store the counts the
-// voxelize reads (misc words: points, runs).
+// voxelize reads (misc words: points, runs).  The multi-GPU step's own buckets are read from its
+// send lists here (run starts rebased on the way, points and run keys copied), and the key range's
+// mark words are cleared: one grid-stride pass over [runs | own points | mark words].
 __global__ __launch_bounds__(256) void k_run_rebase(uint32_t* __restrict__ run_start, RebaseArgs r,
                                                     uint32_t* __restrict__ n_points,
                                                     uint32_t* __restrict__ n_runs) {
     const uint32_t R = r.run_base[r.nsrc];
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < R) {
-        uint32_t q = 0;
-        while (q + 1 < r.nsrc && r.run_base[q + 1] <= i) ++q;
-        run_start[i] += r.point_base[q];
+    uint64_t own_pts = 0;
+    for (uint32_t k = 0; k < r.n_own; ++k)
+        own_pts += r.point_base[r.own_src[k] + 1] - r.point_base[r.own_src[k]];
+    const uint64_t e0 = R, e1 = e0 + own_pts, e2 = e1 + r.zero_row_words * r.zero_rows;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < e2; t += stride) {
+        if (t < e0) {
+            const uint32_t i = (uint32_t)t;
+            uint32_t q = 0;
+            while (q + 1 < r.nsrc && r.run_base[q + 1] <= i) ++q;
+            int own = -1;
+            for (uint32_t k = 0; k < r.n_own; ++k)
+                if (r.own_src[k] == q) own = (int)k;
+            if (own < 0) {
+                run_start[i] += r.point_base[q];
+            } else {
+                const uint32_t j = i - r.run_base[q];
+                run_start[i] = r.own_run_starts[own][j] + r.point_base[q];
+                r.run_keys[i] = r.own_run_keys[own][j];
+            }
+        } else if (t < e1) {
+            uint64_t j = t - e0;
+            uint32_t k = 0;
+            for (; k + 1 < r.n_own; ++k) {
+                const uint32_t c = r.point_base[r.own_src[k] + 1] - r.point_base[r.own_src[k]];
+                if (j < c) break;
+                j -= c;
+            }
+            r.pts[r.point_base[r.own_src[k]] + j] = r.own_pts[k][j];
+        } else {
+            const uint64_t w = t - e1, row = w / r.zero_row_words;
+            r.zero[row * r.zero_stride + (w - row * r.zero_row_words)] = 0u;
+        }
     }
-    if (i == 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
         run_start[R] = r.point_base[r.nsrc];
         *n_points = r.point_base[r.nsrc];
         *n_runs = R;
@@ -5039,9 +5069,12 @@ __global__ __launch_bounds__(256) void k_run_rebase(uint32_t* __restrict__ run_s
 
 hipError_t launch_run_rebase(uint32_t* run_start, const RebaseArgs& r, uint32_t* n_points,
                              uint32_t* n_runs, hipStream_t s) {
-    const uint32_t R = r.run_base[r.nsrc];
-    hipLaunchKernelGGL(k_run_rebase, dim3(std::max<uint32_t>((R + 255) / 256, 1u)), dim3(256), 0, s,
-                       run_start, r, n_points, n_runs);
+    uint64_t own_pts = 0;
+    for (uint32_t k = 0; k < r.n_own; ++k)
+        own_pts += r.point_base[r.own_src[k] + 1] - r.point_base[r.own_src[k]];
+    const uint64_t items = (uint64_t)r.run_base[r.nsrc] + own_pts + r.zero_row_words * r.zero_rows;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((items + 255) / 256, 1), 4096);
+    hipLaunchKernelGGL(k_run_rebase, dim3(blocks), dim3(256), 0, s, run_start, r, n_points, n_runs);
     return hipGetLastError();
 }
 

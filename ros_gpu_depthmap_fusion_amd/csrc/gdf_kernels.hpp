@@ -236,10 +236,24 @@ hipError_t launch_download(const DlArgs& d, hipStream_t s);
 
 // gdf_voxelize_runs: nsrc received segments, source q's points from point_base[q] and runs from
 // run_base[q] (q <= nsrc: the totals)
+constexpr uint32_t kMaxOwnSources = 4;  // sources still in the caller's send lists (one rank's buckets)
 struct RebaseArgs {
     uint32_t point_base[kMaxSources + 1];
     uint32_t run_base[kMaxSources + 1];
     uint32_t nsrc;
+    // the multi-GPU step's own buckets, read from its send lists in the same pass (no device
+    // copies first): source own_src[k]'s points, run keys and run starts (relative to the source)
+    uint32_t n_own;
+    uint32_t own_src[kMaxOwnSources];
+    const float4* own_pts[kMaxOwnSources];
+    const uint32_t* own_run_keys[kMaxOwnSources];
+    const uint32_t* own_run_starts[kMaxOwnSources];
+    float4* pts;          // the received list (the own sources' points are written here)
+    uint32_t* run_keys;   // (the own sources' run keys are written here)
+    // mark words cleared in the same pass: zero_rows rows of zero_row_words at zero_stride
+    uint32_t* zero;
+    uint64_t zero_row_words, zero_stride;
+    uint32_t zero_rows;
 };
 hipError_t launch_run_rebase(uint32_t* run_start, const RebaseArgs& r, uint32_t* n_points,
                              uint32_t* n_runs, hipStream_t s);

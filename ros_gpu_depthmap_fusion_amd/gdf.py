@@ -147,7 +147,7 @@ EXPORTED = [
     "gdf_run_depth_stream_alternating",
     "gdf_next_frame_in_batch", "gdf_get_batch_ranges", "gdf_download_batch_occupancy_grid",
     "gdf_mask_dilate", "gdf_transform_points", "gdf_add_halo_depthmap_device",
-    "gdf_partition_points", "gdf_voxelize_points", "gdf_partition_runs", "gdf_voxelize_runs", "gdf_voxelize_runs_marked", "gdf_set_partition_marks", "gdf_set_emit_partition", "gdf_set_partition_segments", "gdf_last_sort_items", "gdf_get_stream",
+    "gdf_partition_points", "gdf_voxelize_points", "gdf_partition_runs", "gdf_voxelize_runs", "gdf_voxelize_runs_marked", "gdf_voxelize_runs_recv", "gdf_set_partition_marks", "gdf_set_emit_partition", "gdf_set_partition_segments", "gdf_last_sort_items", "gdf_get_stream",
     "gdf_get_graph_stats", "gdf_get_slot", "gdf_select_slot", "gdf_build_info", "gdf_get_tuning",
     "gdf_download_frame", "gdf_set_slot_streams",
     # include/gdf_fused.h: a rank of the multi-GPU fused cloud in C++ over RCCL
@@ -246,6 +246,7 @@ def load_library(path: str = LIB_PATH):
         "gdf_set_emit_partition": (i32, [vp, u32, vp, vp, vp, u32, vp]),
         "gdf_voxelize_runs": (i32, [vp, vp, vp, vp, u32, vp, vp, i32]),
         "gdf_voxelize_runs_marked": (i32, [vp, vp, vp, vp, u32, vp, vp, i32, vp, u64]),
+        "gdf_voxelize_runs_recv": (i32, [vp, vp, vp, vp, u32, vp, vp, i32, vp, u64, vp]),
         "gdf_set_partition_marks": (i32, [vp, i32]),
         "gdf_transform_points": (i32, [vp, vp, vp, vp, u32, vp]),
         "gdf_get_batch_ranges": (i32, [vp, vp, vp, u32, P(u32)]),
