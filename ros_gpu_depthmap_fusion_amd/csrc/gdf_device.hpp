@@ -173,6 +173,9 @@ struct FrameArgs {
     uint32_t* sel_splits;
     uint32_t sel_ncuts;
     uint32_t sel_cut_at[kMaxSegs - 2];
+    // run mode: bytes of dynamic LDS where k_sel keeps each item's voxel key from the run
+    // detection for the store pass (0: the store pass recomputes them)
+    uint32_t sel_key_lds;
     // voxel keys + occupancy marks (compute_voxel_coords + voxel_grid_occupancy_of_points)
     int32_t do_voxel;
     float vlo[3], vcs[3], gmax[3];

@@ -314,7 +314,7 @@ constexpr const char* kTuningVars[] = {
     "GDF_SEL_SHAPE", "GDF_H2D_THREADS", "GDF_NO_GRAPHS", "GDF_NO_RUNS", "GDF_FORCE_RUNS",
     "GDF_RUN_HIST_SORT", "GDF_RUN_HIST_ALL", "GDF_NO_PACK_RUNS", "GDF_NO_XRUNS",
     "GDF_NO_GROUP_SCAN", "GDF_NO_MASK_PACKED", "GDF_NO_GRID_DELTA", "GDF_NO_EMIT_PART",
-    "GDF_NO_DL_PREFETCH", "GDF_DL_FORK", "GDF_GRID_GATE"};
+    "GDF_NO_DL_PREFETCH", "GDF_DL_FORK", "GDF_GRID_GATE", "GDF_NO_SEL_KEY_LDS"};
 
 constexpr int kMaxPipe = 4;
 
@@ -535,6 +535,7 @@ struct gdf_engine {
     bool xruns = !getenv("GDF_NO_XRUNS");  // voxelize_points sorts the received list's runs
     bool group_scan = !getenv("GDF_NO_GROUP_SCAN");  // segment offsets without scan launches
     bool mask_packed = !getenv("GDF_NO_MASK_PACKED");  // k_mask_px<2>: packed f32 pixel pairs
+    bool sel_key_lds = !getenv("GDF_NO_SEL_KEY_LDS");  // k_sel: the keys kept in LDS (A/B)
     // host mirror of the u8 grid (gdf_download_frame): after the first grid download, single-frame
     // updates also list the 32-cell groups they changed, and the next download moves only those
     bool grid_delta = false;
@@ -1458,6 +1459,10 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel, bool compaction_marks = fa
                          !a.sel_tiles
                              ? e->sl().d_khist.as<uint32_t>() : nullptr;
     }
+    // k_sel keeps the voxel keys of its run detection in LDS for its store pass (run mode; not for
+    // the debug stage bits' launches).  GDF_NO_SEL_KEY_LDS: the store pass recomputes them.
+    if (a.sel_tiles && a.run_mode && a.do_voxel && e->sel_key_lds && sel_key_lds_allowed(a.sel_tile * 4u))
+        a.sel_key_lds = a.sel_tile * 4u;
     a.out_pts = e->sl().d_pts.as<float4>();
     a.out_coords = e->sl().d_coords.as<uint32_t>();
     // with rollbuffer points the depth compaction counts into kDepthCount and k_sel writes

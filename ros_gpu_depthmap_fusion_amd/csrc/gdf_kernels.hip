@@ -2073,9 +2073,11 @@ __global__ __launch_bounds__(1024) void k_sel(FrameArgs a) {
     static_assert(kSelSegs * 16 <= 256, "k_sel scan covers 256 entries");
     __shared__ uint32_t s_mark[1u << kMarkCacheBits];
     __shared__ uint32_t s_tile, s_epoch, s_tot[2], s_ex[2];
+    extern __shared__ uint32_t s_key[];  // [kSegs * blockDim] with sel_key_lds: item keys
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int nwaves = blockDim.x >> 6;
     const uint32_t B = blockDim.x, i = threadIdx.x;
+    const bool stash = a.sel_key_lds != 0;  // (run mode, keys)
     const Tickets tk = tickets(a.sel_tiles, gridDim.x);  // (one tile per block: oneshot)
     if (i == 0) {
         const uint32_t ep = read_epoch(a.epoch_word);
@@ -2158,6 +2160,7 @@ __global__ __launch_bounds__(1024) void k_sel(FrameArgs a) {
                 const float4 w = world(j);
                 key = voxel_key(w.x, w.y, w.z, a.vlo, a.vcs, a.vrcs, a.gmax, a.gs);
             }
+            if (stash) s_key[j * B + i] = key;  // (read back by the same thread: no barrier)
             const unsigned long long below = m & ltm;
             const int prev = below ? 63 - __clzll((long long)below) : -1;
             const uint32_t pkey = __shfl(key, prev < 0 ? 0 : prev, 64);
@@ -2226,7 +2229,7 @@ __global__ __launch_bounds__(1024) void k_sel(FrameArgs a) {
             const float4 w = world(j);
             gst4(a.out_pts, pos, w);
             if (a.do_voxel) {
-                key = voxel_key(w.x, w.y, w.z, a.vlo, a.vcs, a.vrcs, a.gmax, a.gs);
+                key = stash ? s_key[j * B + i] : voxel_key(w.x, w.y, w.z, a.vlo, a.vcs, a.vrcs, a.gmax, a.gs);
                 G(a.out_coords)[pos] = key;
             }
         }
@@ -2253,6 +2256,21 @@ struct HookScope {  // begin/end of one profiled launch
         if (h) h->end(slot);
     }
 };
+
+// k_sel's key stash (FrameArgs::sel_key_lds) can exceed the default 64 KB of dynamic LDS per
+// workgroup (16 x 1024 items: 64 KB + the static arrays): allowed once per process
+bool sel_key_lds_allowed(uint32_t bytes) {
+    static const bool ok = [] {
+        const int cap = 96 * 1024;
+        return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sel<4>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, cap) == hipSuccess &&
+               hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sel<8>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, cap) == hipSuccess &&
+               hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sel<16>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, cap) == hipSuccess;
+    }();
+    return ok && bytes <= 96u * 1024u;
+}
 
 hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
     hipError_t e;
@@ -2306,12 +2324,13 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s, LaunchHook* hook) {
     if (a.sel_tiles) {  // rollbuffer points: one pass, behind the depth survivors
         HookScope hs(hook, GDF_KERNEL_SEL);
         const uint32_t thr = a.sel_tile / a.sel_segs;
+        const size_t lds = a.sel_key_lds;
         if (a.sel_segs == 4)
-            hipLaunchKernelGGL(k_sel<4>, dim3(a.sel_tiles), dim3(thr), 0, s, a);
+            hipLaunchKernelGGL(k_sel<4>, dim3(a.sel_tiles), dim3(thr), lds, s, a);
         else if (a.sel_segs == 16)
-            hipLaunchKernelGGL(k_sel<16>, dim3(a.sel_tiles), dim3(thr), 0, s, a);
+            hipLaunchKernelGGL(k_sel<16>, dim3(a.sel_tiles), dim3(thr), lds, s, a);
         else
-            hipLaunchKernelGGL(k_sel<8>, dim3(a.sel_tiles), dim3(thr), 0, s, a);
+            hipLaunchKernelGGL(k_sel<8>, dim3(a.sel_tiles), dim3(thr), lds, s, a);
     }
     return hipGetLastError();
 }

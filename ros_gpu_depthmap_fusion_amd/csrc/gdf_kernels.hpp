@@ -46,6 +46,7 @@ inline size_t seg_offsets_words(uint32_t segs) {
 // the compaction kernels (0: k_mask, 1: k_emit, 2/4/5: k_sel<8/4/16>, 3: none) as launched for
 // `rot45` and flying-pixel rings F (0: no filter) (graph node lookup)
 const void* frame_kernel(int which, int rot45, uint32_t F = 0);
+bool sel_key_lds_allowed(uint32_t bytes);  // k_sel's key stash fits (and is enabled) at `bytes`
 const void* mask_kernel(const FrameArgs& a);  // the compaction pass-1 kernel launch_frame uses
 const void* emit_kernel(const FrameArgs& a);  // the compaction pass-2 kernel launch_frame uses
 bool emit_partition_kernels(const FrameArgs& a);
