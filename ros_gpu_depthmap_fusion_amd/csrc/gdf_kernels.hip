@@ -2159,6 +2159,7 @@ __global__ __launch_bounds__(1024) void k_sel(FrameArgs a) {
             if (bits[j] & 4u) {
                 const float4 w = world(j);
                 key = voxel_key(w.x, w.y, w.z, a.vlo, a.vcs, a.vrcs, a.gmax, a.gs);
+                p[j] = w;  // (the store pass writes this world point: the raw one is not read again)
             }
             if (stash) s_key[j * B + i] = key;  // (read back by the same thread: no barrier)
             const unsigned long long below = m & ltm;
@@ -2226,7 +2227,8 @@ __global__ __launch_bounds__(1024) void k_sel(FrameArgs a) {
         if (!m) continue;  // wave-uniform
         uint32_t key = 0xFFFFFFFFu;
         if (valid) {
-            const float4 w = world(j);
+            // (run mode: the world point was computed for the run keys above, 24 VALU per item)
+            const float4 w = a.run_mode ? p[j] : world(j);
             gst4(a.out_pts, pos, w);
             if (a.do_voxel) {
                 key = stash ? s_key[j * B + i] : voxel_key(w.x, w.y, w.z, a.vlo, a.vcs, a.vrcs, a.gmax, a.gs);
