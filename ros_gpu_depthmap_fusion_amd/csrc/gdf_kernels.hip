@@ -2137,12 +2137,23 @@ __global__ __launch_bounds__(1024) void k_sel(FrameArgs a) {
     uint32_t keep = 0;  // bit j: item j of this thread survives the crop
     const unsigned long long ltm = lanemask_lt();
     const gptr<const float> T0 = G(a.tfw + 16 * (size_t)g.tf0);
+    // a tile inside one sequence: its world matrix in registers, read once (through the pointer
+    // the compiler re-read the 64-B matrix for every item - 16 dependent cache round trips per
+    // wave per pass - as it cannot move those loads above the debug-byte stores)
+    float tw[16];  // (block-uniform: scalar registers)
+    if (one_seq) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            tw[q] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, T0[q])));
+    }
     // the world point of selected item j (transform_points_indirect, world matrix)
     auto world = [&](uint32_t j) {
-        const uint32_t si = si0 + j * B + i;
         const float x = p[j].x, y = p[j].y, z = p[j].z;
-        const gptr<const float> Tw =
-            one_seq || si < g.next ? T0 : G(a.tfw + 16 * (size_t)sel_tf(a, si));
+        if (one_seq)  // (block-uniform)
+            return make_float4(mrow(tw + 0, x, y, z, 1.0f), mrow(tw + 4, x, y, z, 1.0f),
+                               mrow(tw + 8, x, y, z, 1.0f), mrow(tw + 12, x, y, z, 1.0f));
+        const uint32_t si = si0 + j * B + i;
+        const gptr<const float> Tw = si < g.next ? T0 : G(a.tfw + 16 * (size_t)sel_tf(a, si));
         return make_float4(mrow(Tw + 0, x, y, z, 1.0f), mrow(Tw + 4, x, y, z, 1.0f),
                            mrow(Tw + 8, x, y, z, 1.0f), mrow(Tw + 12, x, y, z, 1.0f));
     };
