@@ -2065,6 +2065,13 @@ __global__ __launch_bounds__(SEGW / 2) void k_emit_px2_parts(FrameArgs a) {
 // voxel key) and run records straight to their place behind the depth compaction's - one pass
 // over the window, in selection order.  The last tile writes the frame's totals.  Stage bits go
 // to the debug buffer as before.
+#ifdef GDF_TRACE_GROUPS
+// (diagnostic build, tools/sel_trace.py) per k_sel tile: the wall clock (100 MHz) at block entry,
+// ticket, end of the counting pass (every wave past the barrier), end of the look-back, and block
+// end; the hardware id of wave 0
+constexpr uint32_t kSelTraceSlots = 1u << 16;
+__device__ unsigned long long g_strace[kSelTraceSlots][8];
+#endif
 template <uint32_t kSegs>
 __global__ __launch_bounds__(1024) void k_sel(FrameArgs a) {
     constexpr uint32_t kSelSegs = kSegs;
@@ -2079,6 +2086,13 @@ __global__ __launch_bounds__(1024) void k_sel(FrameArgs a) {
     const uint32_t B = blockDim.x, i = threadIdx.x;
     const bool stash = a.sel_key_lds != 0;  // (run mode, keys)
     const Tickets tk = tickets(a.sel_tiles, gridDim.x);  // (one tile per block: oneshot)
+#ifdef GDF_TRACE_GROUPS
+    const unsigned long long sw0 = wall_clock64();
+#endif
+    // the depth compaction's totals (k_emit, earlier on the stream; the rollbuffer points and runs
+    // go behind them): read now, in flight with the ticket, not after the look-back
+    const uint32_t d = __builtin_amdgcn_readfirstlane(*G(a.out_count));
+    const uint32_t rd = __builtin_amdgcn_readfirstlane(a.run_mode ? *G(a.run_count) : 0u);
     if (i == 0) {
         const uint32_t ep = read_epoch(a.epoch_word);
         s_epoch = ep;
@@ -2087,6 +2101,9 @@ __global__ __launch_bounds__(1024) void k_sel(FrameArgs a) {
     __syncthreads();
     const uint32_t tile = s_tile, epoch = s_epoch;
     if (a.grid_seq_out && tile == 0 && i == 0) *a.grid_seq_out = a.grid_seq;  // (as k_mask)
+#ifdef GDF_TRACE_GROUPS
+    const unsigned long long sw1 = wall_clock64();
+#endif
     const uint32_t si0 = tile * kSelSegs * B;
     // the ring loads first (their slots need no search; 32-bit slot arithmetic: ring_cap < 2^32),
     // branch-free (a point past the selection re-reads the tile's first slot and is dropped);
@@ -2183,6 +2200,9 @@ __global__ __launch_bounds__(1024) void k_sel(FrameArgs a) {
         }
     }
     __syncthreads();
+#ifdef GDF_TRACE_GROUPS
+    const unsigned long long sw2 = wall_clock64();
+#endif
     // exclusive scans of the (segment, wave) counts in item order: points by wave 0, runs by
     // wave 1 (<= 256 entries each)
     const uint32_t ne = kSelSegs * (uint32_t)nwaves;
@@ -2212,8 +2232,9 @@ __global__ __launch_bounds__(1024) void k_sel(FrameArgs a) {
         }
     }
     __syncthreads();
-    const uint32_t d = *G(a.out_count);                    // depth survivors (k_emit)
-    const uint32_t rd = a.run_mode ? *G(a.run_count) : 0u;  // depth runs
+#ifdef GDF_TRACE_GROUPS
+    const unsigned long long sw3 = wall_clock64();
+#endif
     const uint32_t pbase = d + s_ex[0], rbase = rd + (a.run_mode ? s_ex[1] : 0u);
     if (tile == a.sel_tiles - 1u && i == 0) {  // the frame's totals
         *G(a.final_count) = pbase + s_tot[0];
@@ -2257,6 +2278,20 @@ __global__ __launch_bounds__(1024) void k_sel(FrameArgs a) {
         }
         if (a.do_voxel && a.marks) mark_and_count(a, a.marks, valid, key, key, nullptr, s_mark);
     }
+#ifdef GDF_TRACE_GROUPS
+    __syncthreads();
+    if (i == 0 && tile < kSelTraceSlots) {
+        unsigned long long* t = g_strace[tile];
+        t[0] = sw0;
+        t[1] = sw1;
+        t[2] = sw2;
+        t[3] = sw3;
+        t[4] = wall_clock64();
+        t[5] = ((unsigned)__builtin_amdgcn_s_getreg(4 | (15 << 11)) & 0xFFFFu) |  // HW_ID
+               (((unsigned long long)__builtin_amdgcn_s_getreg(20 | (15 << 11)) & 0xFu) << 16);  // XCC
+        t[6] = blockIdx.x;
+    }
+#endif
 }
 
 struct HookScope {  // begin/end of one profiled launch
@@ -4492,6 +4527,14 @@ extern "C" int gdf_debug_group_trace(void* dst, size_t bytes) {  // (diagnostic 
 extern "C" int gdf_debug_group_trace_clear() {
     static unsigned long long zero[kTraceSlots][8];
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_gtrace), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
+}
+extern "C" int gdf_debug_sel_trace(void* dst, size_t bytes) {  // (diagnostic build only)
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_strace), std::min(bytes, sizeof(g_strace)), 0,
+                                    hipMemcpyDeviceToHost);
+}
+extern "C" int gdf_debug_sel_trace_clear() {
+    static unsigned long long zero[kSelTraceSlots][8];
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_strace), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
 }
 extern "C" int gdf_debug_mask_trace(void* dst, size_t bytes) {  // (diagnostic build only)
     return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_mtrace), std::min(bytes, sizeof(g_mtrace)), 0,
