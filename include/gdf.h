@@ -277,7 +277,12 @@ int gdf_get_device_results(gdf_engine* engine, const float** points, const uint3
  * frame's stream into engine-owned pinned host mirrors of the addressed slot, with one wait for
  * them all; the pointers stay valid until the slot's next gdf_download_frame (or gdf_destroy):
  * frames processed in between write their prefetched downloads into a second set of mirrors, never
- * into the set last handed out.  `what` is a mask of GDF_DL_*; members not asked for are NULL / 0.  (No single reference
+ * into the set last handed out.  Memory: the mirrors are pinned host memory sized to the largest
+ * frame downloaded - 36 B per point (points 16, coords 4, voxelized 16, the latter per voxel at
+ * most) plus the grid's cells - and a slot holds two sets once frames are downloaded while others
+ * run: ~72 B per point per slot (a rollbuffer window of 10^8 surviving points: ~7 GB per slot);
+ * download only the members needed (`what`) for such windows.
+ * `what` is a mask of GDF_DL_*; members not asked for are NULL / 0.  (No single reference
  * counterpart: it replaces downloadPoints + downloadVoxelCoords + the voxelized download +
  * downloadVoxelOccupancyGrid, fusion.cpp:1712-1718, 1824-1839, 2946-2951.) */
 #define GDF_DL_POINTS 1u
