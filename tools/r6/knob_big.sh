@@ -3,7 +3,7 @@
 # the chain with nothing to do) and the group-phase grid - 2000-step C2 lines, alternating.
 set -o pipefail
 O=gpurun_out/${1:-knobbig}; mkdir -p $O
-V=("GDF_X=0" "GDF_RUN_BIG_BLOCKS=128" "GDF_RUN_BIG_BLOCKS=32" "GDF_GROUP_BLOCKS=512" "GDF_RUN_BIG_BLOCKS=32 GDF_GROUP_BLOCKS=512")
+V=("GDF_X=0" "GDF_GROUP_SCAN_TILES=1000000" "GDF_GROUP_SCAN_TILES=1000000 GDF_GROUP_BLOCKS=512" "GDF_GROUP_SCAN_TILES=1000000 GDF_RUN_BIG_BLOCKS=32")
 for r in 1 2; do
   i=0
   for v in "${V[@]}"; do
