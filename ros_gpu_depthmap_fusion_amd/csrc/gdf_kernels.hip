@@ -3337,6 +3337,42 @@ constexpr uint32_t kRunPasses = 4;   // staging windows per k_group_runs tile (m
 constexpr uint32_t kHugeGroup = 32768;  // queued groups drawn first by k_group_runs_big (points)
 constexpr uint32_t kHugeRuns = 2048;    // ... or runs (a crossing group's point estimate can be low)
 
+// k_group_runs staging: positions [base, base + staged) of a tile's run stream (staged <=
+// kRunStage) into s_pts.  Position q lies in the last run r with s_off[r] <= q (a branch-free
+// search of the nruns <= 320 run offsets) at point s_ps[r] + q - s_off[r].  A thread resolves 4 of
+// its positions, issues their 4 loads together and stores them after: the loop form waited on each
+// load before its LDS store - up to 8 dependent gathers per 2048-position window, the staged-sums
+// phase 82 % of a C2 tile (tools/gruns_trace.py).  (8 loads at once: 108 VGPRs and a spill.)
+template <int kRunStage>
+__device__ __forceinline__ void stage_run_points(float4* s_pts, const float4* __restrict__ pts,
+                                                 const uint32_t* s_ps, const uint32_t* s_off,
+                                                 uint32_t nruns, uint32_t base, uint32_t staged) {
+    constexpr int kPer = kRunStage / kGroupThreads;
+    constexpr int kB = kPer < 4 ? kPer : 4;
+#pragma unroll
+    for (int b0 = 0; b0 < kPer; b0 += kB) {
+        if ((uint32_t)b0 * kGroupThreads >= staged) break;  // (block-uniform)
+        uint32_t src[kB];
+#pragma unroll
+        for (int j = 0; j < kB; ++j) {
+            const uint32_t k = threadIdx.x + (uint32_t)(b0 + j) * kGroupThreads;
+            const uint32_t q = base + k;
+            uint32_t lo = 0;
+#pragma unroll
+            for (uint32_t step = 256; step; step >>= 1)
+                if (lo + step < nruns && s_off[lo + step] <= q) lo += step;
+            src[j] = k < staged ? s_ps[lo] + (q - s_off[lo]) : 0u;  // (past the window: point 0, dropped)
+        }
+        // unconditional loads and stores (a conditional pair became a branch, a load and a wait
+        // each); positions past `staged` hold point 0, never summed (s_pts has kRunStage slots)
+        float4 v[kB];
+#pragma unroll
+        for (int j = 0; j < kB; ++j) v[j] = pts[src[j]];
+#pragma unroll
+        for (int j = 0; j < kB; ++j) s_pts[threadIdx.x + (uint32_t)(b0 + j) * kGroupThreads] = v[j];
+    }
+}
+
 // comp[0] + comp[4] + ... + comp[4 (n - 1)] in order: one component of a staged group by one lane
 // (its 4 lanes hold the group's 4 components); blocks of 8 values alternate between two register
 // sets so the LDS reads of the next block overlap the additions of the current one.
@@ -4024,6 +4060,16 @@ __device__ __forceinline__ float wave_stream_sum(const uint32_t* __restrict__ rp
 // by a wave from LDS (wave_group_sum: per-wave transpose buffers, 59.4 instead of 37.6 KB of LDS -
 // 2 blocks per CU, not 4), 2 summed by 4 lanes each, one component chain per lane (16 groups per
 // wave, the tile's long groups dealt round-robin over the 4 waves).
+#ifdef GDF_TRACE_GROUPS
+// (diagnostic build, tools/gruns_trace.py) per k_group_runs tile: the wall clock (100 MHz) at block
+// entry, tile start, after the run records and block scans, after the tile's offset / last-group
+// end, after the staged sums, at the tile's end; the hardware id of wave 0, the block
+constexpr uint32_t kRunTraceSlots = 1u << 14;
+__device__ unsigned long long g_rtrace[kRunTraceSlots][8];
+#define GDF_RSTAMP(var) const unsigned long long var = wall_clock64()
+#else
+#define GDF_RSTAMP(var)
+#endif
 template <int kRunStage, int WAVE>
 __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
     const uint32_t* __restrict__ keys, const uint32_t* __restrict__ rvals,
@@ -4066,6 +4112,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
     if (!tile_base && blockIdx.x >= tk.nblk) return;
     if (!tile_base && threadIdx.x == 0) s_epoch = read_epoch(epoch_word);
     uint32_t walk = blockIdx.x;
+    GDF_RSTAMP(rw0);
     for (bool first = true;; first = false) {  // persistent
         if (!first && !tile_base && tk.oneshot) return;
         // (group-scanned offsets: the group-local offset + the totals of the groups before)
@@ -4089,6 +4136,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
         __syncthreads();
         const uint32_t tile = s_tile, epoch = s_epoch;
         if (tile >= ntiles) return;  // block-uniform
+        GDF_RSTAMP(rw1);
         const uint32_t t0 = tile * kGroupThreads;
         const uint32_t i = t0 + threadIdx.x;
         const uint32_t tend = min(n, t0 + kGroupThreads);
@@ -4111,6 +4159,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
         s_off[threadIdx.x] = poff;
         if (threadIdx.x == 0) s_off[kGroupThreads] = ptotal;
         __syncthreads();
+        GDF_RSTAMP(rw2);
         if (wid == 0) {
             const uint32_t ex = tile_base ? s_excl
                                           : lookback2_wave(status, gstatus, tile, ntiles, total, epoch, err);
@@ -4183,6 +4232,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
         // of the run offsets), the other groups are queued
         const uint32_t W0 = total ? s_off[s_start[0] - t0] : 0u;
         __syncthreads();  // (the last group's end, s_start[total]; the extra runs)
+        GDF_RSTAMP(rw3);
         const uint32_t rend = tend + s_nx;  // runs with records here
         if constexpr (WAVE == 2) {
             // Windows of kRunStage staged positions, up to kRunPasses per tile: each window starts
@@ -4211,15 +4261,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
                 const uint32_t staged = s_wend;
                 if (threadIdx.x == 0) s_nbase = 0xFFFFFFFFu;  // (read before A by everyone)
                 if (staged == 0) break;  // block-uniform
-                for (uint32_t k = threadIdx.x; k < staged; k += kGroupThreads) {
-                    const uint32_t q = base + k;
-                    uint32_t lo = 0, hi = kGroupThreads + s_nx;  // last run with s_off <= q
-                    while (hi - lo > 1) {
-                        const uint32_t mid = (lo + hi) >> 1;
-                        if (s_off[mid] <= q) lo = mid; else hi = mid;
-                    }
-                    s_pts[k] = pts[s_ps[lo] + (q - s_off[lo])];
-                }
+                stage_run_points<kRunStage>(s_pts, pts, s_ps, s_off, kGroupThreads + s_nx, base, staged);
                 __syncthreads();  // B
                 if (threadIdx.x == 0) s_wend = 0;
                 if (in && ge - gs <= small_max) {
@@ -4248,6 +4290,24 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
                 if (base == 0xFFFFFFFFu) break;  // block-uniform: nothing eligible left
             }
             __syncthreads();
+            GDF_RSTAMP(rw4);
+#ifdef GDF_TRACE_GROUPS
+            auto rtrace = [&]() {
+                if (threadIdx.x == 0 && tile < kRunTraceSlots) {
+                    unsigned long long* g = g_rtrace[tile];
+                    g[0] = rw0;
+                    g[1] = rw1;
+                    g[2] = rw2;
+                    g[3] = rw3;
+                    g[4] = rw4;
+                    g[5] = wall_clock64();
+                    g[6] = ((unsigned)__builtin_amdgcn_s_getreg(4 | (15 << 11)) & 0xFFFFu) |
+                           (((unsigned long long)__builtin_amdgcn_s_getreg(20 | (15 << 11)) & 0xFu) << 16);
+                    g[7] = blockIdx.x;
+                }
+            };
+            if (total == 0) rtrace();
+#endif
             if (total == 0) continue;  // block-uniform
             // queued groups: huge ones (>= kHugeGroup points) into the region at the top of the
             // queue that k_group_runs_big draws first (longest first bounds the tail: the C3
@@ -4296,6 +4356,9 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
                     else atomicOr(err, 8u);
                 }
             }
+#ifdef GDF_TRACE_GROUPS
+            rtrace();
+#endif
         } else {
             bool inblock = false;
             if (threadIdx.x < total && average) {
@@ -4308,15 +4371,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
             }
             __syncthreads();
             const uint32_t staged = s_wend;
-            for (uint32_t k = threadIdx.x; k < staged; k += kGroupThreads) {
-                const uint32_t q = W0 + k;
-                uint32_t lo = 0, hi = kGroupThreads + s_nx;  // last run with s_off <= q
-                while (hi - lo > 1) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (s_off[mid] <= q) lo = mid; else hi = mid;
-                }
-                s_pts[k] = pts[s_ps[lo] + (q - s_off[lo])];
-            }
+            stage_run_points<kRunStage>(s_pts, pts, s_ps, s_off, kGroupThreads + s_nx, W0, staged);
             __syncthreads();
             if (total == 0) continue;  // block-uniform
             uint32_t qlocal = 0xFFFFFFFFu;  // this thread's group in the tile's queue appends
@@ -4535,6 +4590,14 @@ extern "C" int gdf_debug_sel_trace(void* dst, size_t bytes) {  // (diagnostic bu
 extern "C" int gdf_debug_sel_trace_clear() {
     static unsigned long long zero[kSelTraceSlots][8];
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_strace), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
+}
+extern "C" int gdf_debug_runs_trace(void* dst, size_t bytes) {  // (diagnostic build only)
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_rtrace), std::min(bytes, sizeof(g_rtrace)), 0,
+                                    hipMemcpyDeviceToHost);
+}
+extern "C" int gdf_debug_runs_trace_clear() {
+    static unsigned long long zero[kRunTraceSlots][8];
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_rtrace), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
 }
 extern "C" int gdf_debug_mask_trace(void* dst, size_t bytes) {  // (diagnostic build only)
     return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_mtrace), std::min(bytes, sizeof(g_mtrace)), 0,
