@@ -411,9 +411,10 @@ __device__ __forceinline__ int seg_camera(P cams, int ncams, uint32_t s) {
     }
     const int lane = threadIdx.x & 63;
     bool hit = false;
-    if (lane < ncams) {
-        const uint32_t seg0 = cams[lane].seg0;
-        hit = cams[lane].emit && s >= seg0 && s < seg0 + cams[lane].nseg;
+    if (lane < ncams) {  // (the three fields in one load round: no short-circuit between them)
+        const uint32_t seg0 = cams[lane].seg0, nseg = cams[lane].nseg;
+        const bool emit = cams[lane].emit != 0;
+        hit = emit & (s >= seg0) & (s < seg0 + nseg);
     }
     const unsigned long long m = __ballot(hit);
     return m ? 63 - __clzll((long long)m) : 0;
