@@ -785,9 +785,22 @@ __device__ __forceinline__ void group_partials(const FrameArgs& a, uint32_t s, u
     const uint32_t g = s / kScanGroup;
     const uint32_t ng = (a.total_segs + kScanGroup - 1) / kScanGroup;
     uint32_t sum = 0, rsum = 0;
-    for (uint32_t t = threadIdx.x; t < g; t += blockDim.x) {
-        sum += G(a.grp_tot)[t];
-        if (a.run_mode) rsum += G(a.grp_tot)[ng + t];
+    // four strides per round, loaded unconditionally at clamped indices (g >= 1 here): one load
+    // round per 4 block strides, where the loop form waited on each load
+    for (uint32_t t0 = threadIdx.x; t0 < g; t0 += 4u * blockDim.x) {  // (g: block-uniform)
+        uint32_t v[4], w[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t t = min(t0 + (uint32_t)q * blockDim.x, g - 1u);
+            v[q] = G(a.grp_tot)[t];
+            w[q] = a.run_mode ? G(a.grp_tot)[ng + t] : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const bool in = t0 + (uint32_t)q * blockDim.x < g;
+            sum += in ? v[q] : 0u;
+            rsum += in ? w[q] : 0u;
+        }
     }
     for (int o = 32; o > 0; o >>= 1) {
         sum += __shfl_xor(sum, o, 64);
@@ -3451,8 +3464,11 @@ __global__ __launch_bounds__(256) void k_group_count(const uint32_t* __restrict_
     const uint32_t ntiles = (n + kGroupThreads - 1) / kGroupThreads;
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {  // block-uniform
         const uint32_t i = t * kGroupThreads + threadIdx.x;
-        const uint32_t key = i < n ? keys[i] & km : 0u;
-        const uint32_t prev = (i < n && i > 0) ? keys[i - 1] & km : ~key;
+        // (both keys loaded unconditionally at clamped indices: one load round, where the
+        // conditional second load waited for the first)
+        const uint32_t kc = keys[min(i, n - 1u)] & km, kp = keys[i ? min(i - 1u, n - 1u) : 0u] & km;
+        const uint32_t key = i < n ? kc : 0u;
+        const uint32_t prev = (i < n && i > 0) ? kp : ~key;
         const unsigned long long b = __ballot(i < n && (i == 0 || key != prev));
         if (lane == 0) {
             s_w[wid] = (uint32_t)__popcll(b);
@@ -4141,14 +4157,18 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
         const uint32_t t0 = tile * kGroupThreads;
         const uint32_t i = t0 + threadIdx.x;
         const uint32_t tend = min(n, t0 + kGroupThreads);
-        const uint32_t key = i < n ? K(i) : 0u;
-        const uint32_t prev = (i < n && i > 0) ? K(i - 1) : ~key;
+        // (the run's key, its predecessor's and its value loaded unconditionally at clamped
+        // indices: one load round, where the conditional loads waited for each other)
+        const uint32_t ic = min(i, n - 1u);
+        const uint32_t kraw = keys[ic], kp = K(i ? min(i - 1u, n - 1u) : 0u), vraw = rvals[ic];
+        const uint32_t key = i < n ? kraw & km : 0u;
+        const uint32_t prev = (i < n && i > 0) ? kp : ~key;
         const bool start = i < n && (i == 0 || key != prev);
         RunRec rr{0u, 0u};
         if (average && i < n) {  // (and the sorted run records for k_group_runs_big)
-            const uint32_t v = rvals[i];
+            const uint32_t v = vraw;
             rr.ps = packed ? v : run_start[v];
-            rr.len = packed ? (keys[i] >> kRunLenShift) + 1u : run_start[v + 1] - rr.ps;
+            rr.len = packed ? (kraw >> kRunLenShift) + 1u : run_start[v + 1] - rr.ps;
             rps[i] = rr.ps;
             rlen[i] = rr.len;
         }
