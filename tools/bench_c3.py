@@ -142,12 +142,14 @@ def run_c3(width=1280, height=720, window=256, steps=20, ring=4, profile_steps=5
         rec = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json"))).get(pmc_key, {})
     except (OSError, ValueError):
         rec = {}
+    from bench import slot_pmc  # (a timed slot's bytes: every kernel it brackets, bench.SLOT_PMC)
     for name, d in per.items():
-        r = rec.get(name)
+        r = slot_pmc(rec, name)
         if r:
             d["model_bytes"] = round(model[name])
-            d["pmc_bytes"] = r.get("hbm_bytes_per_launch")
-            d["traffic_ratio"] = round(r.get("hbm_bytes_per_launch", 0) / max(model[name], 1), 3)
+            d["pmc_bytes"] = r["hbm_bytes_per_launch"]
+            d["pmc_kernels"] = r["kernels"]
+            d["traffic_ratio"] = round(r["hbm_bytes_per_launch"] / max(model[name], 1), 3)
     # SURVEY §8(d) B_alg for C3: depth 2P + 24N + 9C, plus 24 n_new + 24 n_sel + 32 n_sel
     survey = 2.0 * P + 24.0 * N + 9.0 * ncells + 24.0 * P + 56.0 * S
     return {
