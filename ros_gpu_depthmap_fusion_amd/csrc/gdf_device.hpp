@@ -240,6 +240,9 @@ struct FrameArgs {
     // runs at nseg P + nseg p + s] with segments 1.. (a selection's rollbuffer pieces) empty - a
     // frame without one
     uint32_t part_nseg;
+    // > 0: every camera emits with this many segments, camera k's from segment k * seg_uniform
+    // (a batch of equal frames): a segment's camera is s / seg_uniform, no descriptor load
+    uint32_t seg_uniform;
     const Tuning* tune;         // (host) the engine's launch shapes: mask_kernel / emit_kernel
 };
 static_assert(sizeof(FrameArgs) <= 4096, "kernel arguments are limited to 4 KiB");

@@ -314,7 +314,8 @@ constexpr const char* kTuningVars[] = {
     "GDF_SEL_SHAPE", "GDF_H2D_THREADS", "GDF_NO_GRAPHS", "GDF_NO_RUNS", "GDF_FORCE_RUNS",
     "GDF_RUN_HIST_SORT", "GDF_RUN_HIST_ALL", "GDF_NO_PACK_RUNS", "GDF_NO_XRUNS",
     "GDF_NO_GROUP_SCAN", "GDF_NO_MASK_PACKED", "GDF_NO_GRID_DELTA", "GDF_NO_EMIT_PART",
-    "GDF_NO_DL_PREFETCH", "GDF_DL_FORK", "GDF_GRID_GATE", "GDF_NO_SEL_KEY_LDS"};
+    "GDF_NO_DL_PREFETCH", "GDF_DL_FORK", "GDF_GRID_GATE", "GDF_NO_SEL_KEY_LDS",
+    "GDF_NO_SEG_UNIFORM"};
 
 constexpr int kMaxPipe = 4;
 
@@ -536,6 +537,7 @@ struct gdf_engine {
     bool group_scan = !getenv("GDF_NO_GROUP_SCAN");  // segment offsets without scan launches
     bool mask_packed = !getenv("GDF_NO_MASK_PACKED");  // k_mask_px<2>: packed f32 pixel pairs
     bool sel_key_lds = !getenv("GDF_NO_SEL_KEY_LDS");  // k_sel: the keys kept in LDS (A/B)
+    bool seg_uniform = !getenv("GDF_NO_SEG_UNIFORM");  // equal cameras: segment -> camera by division
     // host mirror of the u8 grid (gdf_download_frame): after the first grid download, single-frame
     // updates also list the 32-cell groups they changed, and the next download moves only those
     bool grid_delta = false;
@@ -1369,6 +1371,14 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel, bool compaction_marks = fa
         HIPCHK(hipMemcpyAsync(e->sl().d_camdesc.p, e->h_cams.data(), e->h_cams.size() * sizeof(CamDesc),
                               hipMemcpyHostToDevice, e->s()));
         a.cams_dev = e->sl().d_camdesc.as<const CamDesc>();
+    }
+    if (e->seg_uniform && !e->h_cams.empty()) {  // (FrameArgs::seg_uniform)
+        uint32_t u = e->h_cams[0].nseg;
+        for (size_t k = 0; k < e->h_cams.size(); ++k) {
+            const CamDesc& d = e->h_cams[k];
+            if (!d.emit || d.nseg != u || d.seg0 != (uint32_t)k * u) u = 0;
+        }
+        a.seg_uniform = u;
     }
     a.depth_total = e->depth_total;
     const uint32_t sel = e->sel_inserted ? e->rb.selection_point_count : 0u;

@@ -399,9 +399,13 @@ struct SegGeo {
 // block's 36.9 K cycles for 8 cameras).  Wave-uniform result.  The ballot needs lanes
 // 0..ncams-1 active: a caller in divergent code (or a block not a multiple of 64 threads) takes
 // the per-camera scan instead (same answer: the last match).
+// uni > 0 (FrameArgs::seg_uniform, equal cameras): the camera by one scalar division - the
+// descriptor fields that follow then come in one scalar-load round instead of after a vector-load
+// round of every camera's range.
 template <class P>
-__device__ __forceinline__ int seg_camera(P cams, int ncams, uint32_t s) {
+__device__ __forceinline__ int seg_camera(P cams, int ncams, uint32_t s, uint32_t uni = 0u) {
     static_assert(kMaxCams <= 64, "one camera per lane");
+    if (uni) return (int)min(s / uni, (uint32_t)ncams - 1u);
     const unsigned long long need = ncams >= 64 ? ~0ull : (1ull << ncams) - 1ull;
     if ((__builtin_amdgcn_read_exec() & need) != need) {
         int k = 0;
@@ -423,9 +427,9 @@ __device__ __forceinline__ int seg_camera(P cams, int ncams, uint32_t s) {
 // (P: an LDS copy of the descriptors, or the global / kernel-argument table read with scalar
 // loads - the segment is block-uniform)
 template <class P>
-__device__ __forceinline__ SegGeo seg_geo(P cams, int ncams, uint32_t s) {
+__device__ __forceinline__ SegGeo seg_geo(P cams, int ncams, uint32_t s, uint32_t uni = 0u) {
     SegGeo g{0, 0, 0, 0, 0};
-    g.k = seg_camera(cams, ncams, s);
+    g.k = __builtin_amdgcn_readfirstlane(seg_camera(cams, ncams, s, uni));  // (scalar field loads)
     const uint32_t seg0 = cams[g.k].seg0, nchunk = cams[g.k].nchunk, segw = cams[g.k].segw;
     const uint32_t W = cams[g.k].W;
     const uint32_t i = s - seg0;
@@ -812,6 +816,50 @@ __device__ __forceinline__ void group_partials(const FrameArgs& a, uint32_t s, u
     }
 }
 
+// group_partials in two halves (k_emit_px2): the first round's loads issued before the segment's
+// own geometry and depth loads, summed after them - one load round for both instead of two
+struct GroupPart {
+    uint32_t v[4], w[4];
+};
+__device__ __forceinline__ GroupPart group_partials_issue(const FrameArgs& a, uint32_t s) {
+    GroupPart p;
+    const uint32_t g = s / kScanGroup;
+    const uint32_t ng = (a.total_segs + kScanGroup - 1) / kScanGroup;
+    const uint32_t last = g ? g - 1u : 0u;  // (clamped: entries past g are loaded, not summed)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t t = min(threadIdx.x + (uint32_t)q * blockDim.x, last);
+        p.v[q] = G(a.grp_tot)[t];
+        p.w[q] = a.run_mode ? G(a.grp_tot)[ng + t] : 0u;
+    }
+    return p;
+}
+__device__ __forceinline__ void group_partials_finish(const FrameArgs& a, uint32_t s,
+                                                      const GroupPart& p, uint32_t* s_red) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t g = s / kScanGroup;
+    const uint32_t ng = (a.total_segs + kScanGroup - 1) / kScanGroup;
+    uint32_t sum = 0, rsum = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const bool in = threadIdx.x + (uint32_t)q * blockDim.x < g;
+        sum += in ? p.v[q] : 0u;
+        rsum += in ? p.w[q] : 0u;
+    }
+    for (uint32_t t = threadIdx.x + 4u * blockDim.x; t < g; t += blockDim.x) {  // (rare: > 4 strides)
+        sum += G(a.grp_tot)[t];
+        if (a.run_mode) rsum += G(a.grp_tot)[ng + t];
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        sum += __shfl_xor(sum, o, 64);
+        rsum += __shfl_xor(rsum, o, 64);
+    }
+    if (lane == 0) {
+        s_red[wid] = sum;
+        s_red[16 + wid] = rsum;
+    }
+}
+
 // Pass 1 of the ordered compaction (apply_point_mask.glsl:42-55 made stable): one block per
 // segment, one item per thread (blockDim = a.seg_threads >= every segment's length).  The ballot
 // of wave w's valid bits is word w of the segment's 16-word bitmask.
@@ -840,7 +888,7 @@ __global__ __launch_bounds__(1024) void k_mask(FrameArgs a) {
         // the block's camera from the descriptor table with scalar loads, so the band loads
         // issue at once; the LDS copy of all descriptors (neighbour lookups) overlaps them
         const gptr<const CamDesc> gcam = G(cam_table(a));
-        const SegGeo sg = seg_geo(gcam, a.ncams, s);
+        const SegGeo sg = seg_geo(gcam, a.ncams, s, a.seg_uniform);
         struct {
             const uint16_t* depth;
             const float *xn, *yn;
@@ -1260,7 +1308,6 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
         for (uint32_t j = threadIdx.x; j < 2u * NWORDS * kMaxParts; j += NT) (&s_pc[0][0][0])[j] = 0u;
     const uint32_t n = gridDim.x, q8 = n / 8, r8 = n % 8, xcd = blockIdx.x % 8;
     const uint32_t s = xcd * q8 + min(xcd, r8) + blockIdx.x / 8;  // the block's segment
-    if (a.grid_seq_out && blockIdx.x == 0 && threadIdx.x == 0) *a.grid_seq_out = a.grid_seq;
     uint32_t bits[PX], rkey[PX];
 #pragma unroll
     for (int j = 0; j < PX; ++j) {
@@ -1272,7 +1319,7 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
         for (uint32_t j = threadIdx.x; j < radix_hist_span(a.npasses); j += NT) s_hist[j] = 0;
     {
         const gptr<const CamDesc> gcam = G(cam_table(a));
-        SegGeo sg = seg_geo(gcam, a.ncams, s);
+        SegGeo sg = seg_geo(gcam, a.ncams, s, a.seg_uniform);
         struct {
             const uint16_t* depth;
             const float *xn, *yn;
@@ -1327,17 +1374,20 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
 #pragma unroll
         for (int q = 0; q < QX; ++q)
             xv[q] = ca + tb + (uint32_t)NT * q < cb ? G(c.xn)[ca + tb + (uint32_t)NT * q] : 0.0f;
-        if (tb < nrows) {
-            const int gyi = (int)sg.y - h + (int)tb;
-            s_yn[tb] = (gyi >= 0 && gyi < (int)c.H) ? G(c.yn)[gyi] : 0.0f;
-        }
-        float xwv = 0.0f;
-        if (wrap && tb < (uint32_t)h) xwv = G(c.xn)[c.W - 1 - tb];
-        {  // camera sg.k's descriptor into LDS
-            const uint32_t* src = reinterpret_cast<const uint32_t*>(cam_table(a) + sg.k);
-            uint32_t* dst = reinterpret_cast<uint32_t*>(s_cams);
-            for (uint32_t w = threadIdx.x; w < (uint32_t)(sizeof(CamDesc) / 4); w += NT) dst[w] = G(src)[w];
-        }
+        // the row factors, the wrap columns' ray factors and the camera descriptor: loaded
+        // unconditionally at clamped indices with the band, stored after (a load in its own
+        // branch waited for every load before it: a second round)
+        const int gyi = (int)sg.y - h + (int)tb;
+        const bool yin = tb < nrows && gyi >= 0 && gyi < (int)c.H;
+        const float ynl = G(c.yn)[min((uint32_t)max(gyi, 0), c.H - 1u)];
+        const float xwl = G(c.xn)[tb < c.W ? c.W - 1u - tb : 0u];
+        static_assert(sizeof(CamDesc) / 4 <= (size_t)NT, "one descriptor word per thread");
+        const uint32_t* csrc = reinterpret_cast<const uint32_t*>(cam_table(a) + sg.k);
+        const uint32_t cdw = G(csrc)[min(threadIdx.x, (uint32_t)(sizeof(CamDesc) / 4) - 1u)];
+        if (tb < nrows) s_yn[tb] = yin ? ynl : 0.0f;
+        const float xwv = wrap && tb < (uint32_t)h ? xwl : 0.0f;
+        if (threadIdx.x < (uint32_t)(sizeof(CamDesc) / 4))  // camera sg.k's descriptor into LDS
+            reinterpret_cast<uint32_t*>(s_cams)[threadIdx.x] = cdw;
 #pragma unroll
         for (int q = 0; q < QR; ++q) {
             const uint32_t r = (uint32_t)wid + (uint32_t)NW * q;
@@ -1476,6 +1526,9 @@ __device__ __forceinline__ void mask_px_body(const FrameArgs& a) {
             if (s_hist[j])
                 __hip_atomic_fetch_add(rep + j, s_hist[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    // (stored after the descriptor reads: a global store before them keeps the compiler from
+    // reading the camera fields with scalar loads)
+    if (a.grid_seq_out && blockIdx.x == 0 && threadIdx.x == 0) *a.grid_seq_out = a.grid_seq;
     group_scan_tail(a, s);
 #ifdef GDF_TRACE_GROUPS
     GDF_MSTAMP(6);
@@ -1723,7 +1776,7 @@ __global__ __launch_bounds__(1024) void k_emit(FrameArgs a) {
     else if (a.grp_tot) group_partials(a, s, s_red);
     // the segment's geometry and the thread's item source, loaded before the barrier
     const uint32_t i = threadIdx.x;
-    int k = seg_camera(cams, a.ncams, s);
+    int k = seg_camera(cams, a.ncams, s, a.seg_uniform);
     // block-uniform camera: its descriptor (device copy beyond kArgCams cameras) is read with
     // scalar loads, not once per lane
     k = __builtin_amdgcn_readfirstlane(k);
@@ -1841,7 +1894,7 @@ __device__ __forceinline__ void emit_px2_parts(const FrameArgs& a, uint32_t* s_m
     __syncthreads();  // (the zeroed counters and the mark cache before any wave writes them)
     const gptr<const CamDesc> cams = G(cam_table(a));
     const uint32_t i = threadIdx.x;
-    int k = seg_camera(cams, a.ncams, s);
+    int k = seg_camera(cams, a.ncams, s, a.seg_uniform);
     k = __builtin_amdgcn_readfirstlane(k);
     const uint32_t j = s - cams[k].seg0;
     const uint32_t y = j / cams[k].nchunk;
@@ -1946,10 +1999,10 @@ __global__ __launch_bounds__(SEGW / 2) void k_emit_px2(FrameArgs a) {
     const bool hist = a.key_hist && !a.run_mode;
     if (hist)
         for (uint32_t i = threadIdx.x; i < radix_hist_span(a.npasses); i += NT) s_hist[i] = 0;
-    if (a.fused_prefix) prefix_partials(a, s, s_red);
-    else if (a.grp_tot) group_partials(a, s, s_red);
+    GroupPart gp{};
+    if (!a.fused_prefix && a.grp_tot) gp = group_partials_issue(a, s);
     const uint32_t i = threadIdx.x;
-    int k = seg_camera(cams, a.ncams, s);
+    int k = seg_camera(cams, a.ncams, s, a.seg_uniform);
     k = __builtin_amdgcn_readfirstlane(k);
     const uint32_t j = s - cams[k].seg0;
     const uint32_t y = j / cams[k].nchunk;
@@ -1958,14 +2011,22 @@ __global__ __launch_bounds__(SEGW / 2) void k_emit_px2(FrameArgs a) {
     uint64_t m[2];
     uint32_t dval[2] = {0u, 0u};
     float xnv[2] = {0.0f, 0.0f};
+    // (both pixels' loads unconditional at clamped columns, selected after: the conditional form
+    // waited for each depth load inside its branch)
+    uint16_t dl[2];
+    float xl[2];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         m[q] = G(a.vbits)[(size_t)s * 16 + wid + NW * q];
-        const uint32_t ii = i + (uint32_t)NT * q;
-        if (ii < len) {
-            dval[q] = G(cams[k].depth)[y * cams[k].W + x0 + ii];
-            xnv[q] = G(cams[k].xn)[x0 + ii];
-        }
+        const uint32_t ic = min(i + (uint32_t)NT * q, len - 1u);
+        dl[q] = G(cams[k].depth)[y * cams[k].W + x0 + ic];
+        xl[q] = G(cams[k].xn)[x0 + ic];
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const bool in = i + (uint32_t)NT * q < len;
+        dval[q] = in ? dl[q] : 0u;
+        xnv[q] = in ? xl[q] : 0.0f;
     }
     const float ynv = G(cams[k].yn)[y];
     // counts (and runs) of the segment's 4 words: the prefix of each of this thread's words
@@ -1984,6 +2045,9 @@ __global__ __launch_bounds__(SEGW / 2) void k_emit_px2(FrameArgs a) {
 #pragma unroll
         for (int w = 0; w < NWORDS; ++w) rc[w] = G(a.wave_runs)[(size_t)s * 16 + w];
     }
+    // (the preceding groups' totals, loaded with the segment's own loads)
+    if (a.fused_prefix) prefix_partials(a, s, s_red);
+    else if (a.grp_tot) group_partials_finish(a, s, gp, s_red);
     __syncthreads();
     uint32_t base = sbase;
     if (a.fused_prefix || a.grp_tot)

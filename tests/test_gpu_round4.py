@@ -136,6 +136,8 @@ def test_download_frame_grid_mirror_deltas(Engine):
                                    {"GDF_SMALL_GROUP": "64"}, {"GDF_RUN_WAVE": "1"},
                                    {"GDF_RUN_WAVE": "0"}, {"GDF_RUN_Q16": "1"},
                                    {"GDF_RUN_BIG_BLOCKS": "512"},
+                                   # the segment's camera by the lane ballot, not by division
+                                   {"GDF_NO_SEG_UNIFORM": "1"},
                                    # (an engine created after all of them: the built-in values)
                                    {}])
 def test_batch8_vga_knobs_match_oracle(Engine, knobs):
