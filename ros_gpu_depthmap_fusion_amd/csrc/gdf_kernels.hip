@@ -775,8 +775,12 @@ __device__ __forceinline__ void group_scan_tail(const FrameArgs& a, uint32_t s) 
 // the sum of the group totals gtot[0 .. idx / kScanGroup) by one wave (every lane gets it)
 __device__ __forceinline__ uint32_t wave_group_prefix(const uint32_t* gtot, uint32_t idx) {
     const uint32_t lane = threadIdx.x & 63;
-    uint32_t sum = 0;
-    for (uint32_t t = lane; t < idx / kScanGroup; t += 64) sum += G(gtot)[t];
+    const uint32_t ng = idx / kScanGroup;
+    // (the first 64 totals unconditionally at a clamped index: a loop's first load waited for
+    // every load issued before it)
+    const uint32_t v0 = G(gtot)[min(lane, ng ? ng - 1u : 0u)];
+    uint32_t sum = lane < ng ? v0 : 0u;
+    for (uint32_t t = lane + 64u; t < ng; t += 64) sum += G(gtot)[t];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
     return sum;
@@ -3185,35 +3189,6 @@ __global__ __launch_bounds__(256) void k_sort_hist(const uint32_t* __restrict__ 
         if (s_h[i]) atomicAdd(&rep[i], s_h[i]);
 }
 
-// Exclusive scan of the 256-entry global digit histogram (4 waves x 64 digits; the sum of the
-// kHistReps replicas), thread d gets the base of digit d.
-__device__ __forceinline__ uint32_t digit_base(const uint32_t* ghist, uint32_t* s_wave) {
-    const uint32_t d = threadIdx.x;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint32_t v = 0;
-#pragma unroll
-    for (int r = 0; r < kHistReps; ++r) v += ghist[r * 1024 + d];
-    uint32_t total;
-    (void)lane;
-    (void)wid;
-    return block_exclusive_scan(v, total, s_wave);
-}
-
-// the same for a 512-digit pass: thread t holds digits 2t and 2t+1
-__device__ __forceinline__ void digit_base512(const uint32_t* ghist, uint32_t* s_wave, uint32_t* s_base) {
-    const uint32_t d = 2u * threadIdx.x;
-    uint32_t v0 = 0, v1 = 0;
-#pragma unroll
-    for (int r = 0; r < kHistReps; ++r) {
-        v0 += ghist[r * 1024 + d];
-        v1 += ghist[r * 1024 + d + 1];
-    }
-    uint32_t total;
-    const uint32_t e = block_exclusive_scan(v0 + v1, total, s_wave);
-    s_base[d] = e;
-    s_base[d + 1] = e + v0;
-}
-
 // Stable scatter of one 8-bit (NB = 256) or 9-bit (NB = 512, the last pass of a 25-bit batch key)
 // digit.  Tile = 256 threads x PT keys: wave w owns keys
 // [w*64*PT, (w+1)*64*PT) of the tile in slot-major order (slot j, lane l -> w*64*PT + j*64 + l),
@@ -3259,15 +3234,35 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(
     const unsigned long long ltm = lanemask_lt();
     const Tickets tk = tickets(ntiles, grid_block0);
     if (blockIdx.x >= tk.nblk) return;
-    if (threadIdx.x == 0) s_epoch = read_epoch(epoch_word);
     // first pass of a batch: the frame index joins the key above its voxel bits
     const bool add_frame = nframes > 1 && vin == nullptr && fstart != nullptr;
-    if (add_frame) load_fstart(s_fstart, fstart, nframes);
+    // the block's prologue reads in one round: the digit counts (the kHistReps replicas of this
+    // thread's digits), the frame starts (unconditionally, at a clamped index), then the epoch,
+    // whose wait covers them (issued one after the other they were three dependent rounds)
+    uint32_t hv0 = 0, hv1 = 0;
+    {
+        const uint32_t d = NB == 256 ? threadIdx.x : 2u * threadIdx.x;
+#pragma unroll
+        for (int r = 0; r < kHistReps; ++r) {
+            hv0 += ghist[r * 1024 + d];
+            if constexpr (NB == 512) hv1 += ghist[r * 1024 + d + 1];
+        }
+    }
+    static_assert(kMaxCams + 1 <= kSortThreads, "one frame start per thread");
+    const uint32_t fsv = (add_frame ? fstart : ghist)[min(threadIdx.x, nframes)];
+    if (threadIdx.x == 0) s_epoch = read_epoch(epoch_word);
+    if (add_frame && threadIdx.x <= nframes) s_fstart[threadIdx.x] = fsv;
     // the digit bases do not depend on the tile
-    if constexpr (NB == 256)
-        s_base[threadIdx.x] = digit_base(ghist, s_wave);
-    else
-        digit_base512(ghist, s_wave, s_base);
+    {
+        uint32_t total;
+        const uint32_t e = block_exclusive_scan(hv0 + hv1, total, s_wave);
+        if constexpr (NB == 256) {
+            s_base[threadIdx.x] = e;
+        } else {
+            s_base[2u * threadIdx.x] = e;
+            s_base[2u * threadIdx.x + 1u] = e + hv0;
+        }
+    }
     for (bool first = true;; first = false) {  // persistent: tiles in ticket order
         if (!first && tk.oneshot) return;
         if (threadIdx.x == 0) s_tile = next_ticket(tile_ctr, tk, epoch_word, s_epoch);
@@ -4196,13 +4191,26 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
     GDF_RSTAMP(rw0);
     for (bool first = true;; first = false) {  // persistent
         if (!first && !tile_base && tk.oneshot) return;
+        // the tile's run records (key, predecessor's key, value), loaded unconditionally at clamped
+        // indices in one round - with tile offsets (tile_base) the tile is the walk index and they
+        // are issued before the barrier, with the offset and group-prefix loads
+        uint32_t kraw = 0, kpraw = 0, vraw = 0;
+        auto load_recs = [&](uint32_t tl) {
+            const uint32_t ii = tl * kGroupThreads + threadIdx.x;
+            const uint32_t ic = min(ii, n - 1u);
+            kraw = keys[ic];
+            kpraw = keys[ii ? min(ii - 1u, n - 1u) : 0u];
+            vraw = rvals[ic];
+        };
+        if (tile_base && walk < ntiles) load_recs(walk);
+        const uint32_t tb0 = tile_base && threadIdx.x == 0 && walk < ntiles ? tile_base[walk] : 0u;
         // (group-scanned offsets: the group-local offset + the totals of the groups before)
         const uint32_t gpre = tile_base && tile_gtot && wid == 0 && walk < ntiles
                                   ? wave_group_prefix(tile_gtot, walk) : 0u;
         if (threadIdx.x == 0) {
             if (tile_base) {
                 s_tile = walk;
-                s_excl = walk < ntiles ? tile_base[walk] + gpre : 0u;
+                s_excl = walk < ntiles ? tb0 + gpre : 0u;
             } else {
                 s_tile = next_ticket(tile_ctr, tk, epoch_word, s_epoch);
             }
@@ -4221,10 +4229,19 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
         const uint32_t t0 = tile * kGroupThreads;
         const uint32_t i = t0 + threadIdx.x;
         const uint32_t tend = min(n, t0 + kGroupThreads);
-        // (the run's key, its predecessor's and its value loaded unconditionally at clamped
-        // indices: one load round, where the conditional loads waited for each other)
-        const uint32_t ic = min(i, n - 1u);
-        const uint32_t kraw = keys[ic], kp = K(i ? min(i - 1u, n - 1u) : 0u), vraw = rvals[ic];
+        if (!tile_base) load_recs(tile);
+        // the reads for the end of the tile's last group (wave 1, below), issued before the scans
+        // by every wave (no branch: a load in one waited for the ones before it): the last key, the
+        // next tiles' first starts
+        const uint32_t lkraw = keys[tend - 1];
+        const uint32_t tt1 = tile + 1u + (uint32_t)lane;
+        const bool has_tf = tile_first != nullptr;
+        const uint32_t pfr = (has_tf ? tile_first : keys)[min(tt1, ntiles - 1u)];
+        const uint32_t pf = (has_tf & (tt1 < ntiles)) ? pfr : 0xFFFFFFFFu;
+        // ... and the records of the (up to kExtraRuns) runs past the tile
+        const uint32_t xi = min(tend + (uint32_t)lane, n - 1u);
+        const uint32_t xvr = rvals[xi], xkr = keys[xi];
+        const uint32_t kp = kpraw & km;
         const uint32_t key = i < n ? kraw & km : 0u;
         const uint32_t prev = (i < n && i > 0) ? kp : ~key;
         const bool start = i < n && (i == 0 || key != prev);
@@ -4258,7 +4275,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
                 }
             }
         } else if (wid == 1 && total) {  // end of the tile's last group (as k_group, over runs)
-            const uint32_t lastkey = K(tend - 1);
+            const uint32_t lastkey = lkraw & km;
             uint32_t lo = tend, hi = n;
             if (tile_first) {
                 // the first group start of the next tiles that hold one (k_group_count): 64 tiles
@@ -4268,7 +4285,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
                 hi = n;
                 for (uint32_t t0x = tile + 1; t0x < ntiles; t0x += 64u) {  // (wave-uniform)
                     const uint32_t tt = t0x + (uint32_t)lane;
-                    const uint32_t f = tt < ntiles ? tile_first[tt] : 0xFFFFFFFFu;
+                    const uint32_t f = t0x == tile + 1u ? pf : tt < ntiles ? tile_first[tt] : 0xFFFFFFFFu;
                     const unsigned long long has = __ballot(f != 0xFFFFFFFFu);
                     if (has) {
                         hi = (uint32_t)__shfl((int)f, __ffsll((long long)has) - 1, 64);
@@ -4297,10 +4314,9 @@ __global__ __launch_bounds__(kGroupThreads) void k_group_runs(
             if (average && hi > tend && hi - tend <= kExtraRuns) {
                 const uint32_t nx = hi - tend;
                 uint32_t ps = 0, len = 0;
-                if ((uint32_t)lane < nx) {
-                    const uint32_t v = rvals[tend + lane];
-                    ps = packed ? v : run_start[v];
-                    len = packed ? (keys[tend + lane] >> kRunLenShift) + 1u : run_start[v + 1] - ps;
+                if ((uint32_t)lane < nx) {  // (lane's record preloaded: xvr, xkr)
+                    ps = packed ? xvr : run_start[xvr];
+                    len = packed ? (xkr >> kRunLenShift) + 1u : run_start[xvr + 1] - ps;
                 }
                 const uint32_t inc = dpp_sum_scan(len);
                 if ((uint32_t)lane < nx) {
