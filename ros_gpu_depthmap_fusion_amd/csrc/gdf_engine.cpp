@@ -318,6 +318,9 @@ constexpr const char* kTuningVars[] = {
     "GDF_NO_SEG_UNIFORM"};
 
 constexpr int kMaxPipe = 4;
+// batches of frames of at most this many depth pixels each run k_group_runs_big on this many blocks
+constexpr uint64_t kSmallFramePixels = 640 * 480;
+constexpr uint32_t kSmallFrameBigBlocks = 32;
 
 // Everything one frame writes.  Frames rotate over npipe slots (gdf_clear starts a frame), so a
 // new frame's compaction runs while the previous frame's sort / grouping still execute.  The
@@ -1698,6 +1701,12 @@ VoxelizeArgs voxelize_args(gdf_engine* e, int average, int fused_grid_lifetime,
         v.run_start = e->sl().d_runstart.as<uint32_t>();
         v.point_count = e->sl().d_misc.as<uint32_t>() + kCount;
         v.pack_runs = e->pack_runs && sort_bits(e) <= 25 ? 1 : 0;
+        // a batch of depth frames of at most VGA size each: a voxel rarely gathers the > 1 K
+        // points of one frame that queue it for k_group_runs_big (profiles/r06/knob_big/: a VGA
+        // batch queues none) - 32 blocks instead of the resident grid (queued groups still run)
+        if (!e->sl().runs_sel && e->nframes > 1 &&
+            e->depth_total <= (uint64_t)e->nframes * kSmallFramePixels)
+            v.big_cap = kSmallFrameBigBlocks;
     }
     v.nmax = nmax;
     v.key_bits = sort_bits(e);

@@ -3150,19 +3150,26 @@ __global__ __launch_bounds__(256) void k_sort_hist(const uint32_t* __restrict__ 
                                                    const uint32_t* __restrict__ fstart) {
     __shared__ uint32_t s_h[4 * 256];
     __shared__ uint32_t s_fstart[kMaxCams + 1];
+    // (the item count and the frame starts read in one round, before the barrier)
+    const uint32_t n = *count;
+    const bool fr = fstart && nframes > 1;
+    const uint32_t fsv = (fr ? fstart : count)[fr ? min(threadIdx.x, nframes) : 0u];
     for (uint32_t i = threadIdx.x; i < 4 * 256; i += 256) s_h[i] = 0;
-    if (fstart) load_fstart(s_fstart, fstart, nframes);
+    if (fr && threadIdx.x <= nframes) s_fstart[threadIdx.x] = fsv;
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const uint32_t n = *count;
     const uint32_t stride = gridDim.x * 256u;
     for (uint32_t base = blockIdx.x * 256u; base < n; base += 4u * stride) {  // block-uniform
         uint32_t k[4];
+        // (the four keys loaded unconditionally at clamped indices first: loaded one by one
+        // between the frame lookups, each waited for the one before)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) k[q] = keys[min(base + q * stride + threadIdx.x, n - 1u)];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const uint32_t i = base + q * stride + threadIdx.x;
-            k[q] = i < n ? keys[i] : 0u;
-            if (nframes > 1 && fstart && i < n) k[q] |= frame_of(s_fstart, nframes, i) << fshift;
+            if (i >= n) k[q] = 0u;
+            else if (fr) k[q] |= frame_of(s_fstart, nframes, i) << fshift;
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -4867,7 +4874,7 @@ hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hoo
             const bool q16 = T.run_q16 == 1 || (T.run_q16 == 2 && a.nframes <= 1);
             const bool occ4 = T.run_big_occ4 != 0;
             const uint32_t rb = resident_big_blocks(q16, occ4);
-            const uint32_t big_blocks = std::min(T.run_big_blocks, rb);
+            const uint32_t big_blocks = std::min(std::min(T.run_big_blocks, rb), a.big_cap ? a.big_cap : rb);
             auto kb = occ4 ? (q16 ? k_group_runs_big<16, true> : k_group_runs_big<8, true>)
                            : (q16 ? k_group_runs_big<16, false> : k_group_runs_big<8, false>);
             hipLaunchKernelGGL(kb, dim3(big_blocks), dim3(256), 0, s, kbuf[sorted_passes & 1],

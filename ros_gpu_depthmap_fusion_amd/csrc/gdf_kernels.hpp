@@ -170,6 +170,9 @@ struct VoxelizeArgs {
     // done (null: none, e.g. graph capture)
     hipEvent_t grid_wait, grid_rec;
     int grid_rec_early;
+    // > 0: k_group_runs_big's grid capped at this many blocks (batches of small frames: their
+    // queue is almost always empty, and the launch of a resident grid is chain time - C2 +1 %)
+    uint32_t big_cap;
 };
 hipError_t launch_voxelize(const VoxelizeArgs& a, hipStream_t s, LaunchHook* hook = nullptr);
 size_t voxelize_status_words(uint32_t nmax, uint32_t key_bits);

@@ -172,7 +172,9 @@ def test_batch8_vga_knobs_match_oracle(Engine, knobs):
 
 
 @pytest.mark.parametrize("knobs", [{}, {"GDF_NO_GROUP_SCAN": "1"}, {"GDF_NO_PACK_RUNS": "1"},
-                                   {"GDF_RUN_WAVE_MODE": "2"}, {"GDF_GROUP_FIRST": "0"}])
+                                   {"GDF_RUN_WAVE_MODE": "2"}, {"GDF_GROUP_FIRST": "0"},
+                                   # ~650 queued long groups on the small-frame batches' grid
+                                   {"GDF_RUN_BIG_BLOCKS": "32"}])
 def test_4k_frame_knobs_match_oracle(Engine, knobs):
     """A dense 4K frame (32 400 compaction segments, runs of equal keys): the group scans on and
     off, every output equal to the oracle's."""
