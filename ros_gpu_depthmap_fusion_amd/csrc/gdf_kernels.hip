@@ -748,11 +748,15 @@ __device__ __forceinline__ void arrive_and_scan(uint32_t* done, const uint32_t* 
     if (!*s_last || threadIdx.x >= 64) return;  // block-uniform, then wave 0
     const uint32_t lane = threadIdx.x;
     const uint32_t ng = (nent + kScanGroup - 1) / kScanGroup;
+    // both series' counts read in one round (at a clamped index), scanned after
+    const uint32_t lc = min(lane, n - 1u);
+    uint32_t vs[2];
+    for (int q = 0; q < 2; ++q)
+        vs[q] = __hip_atomic_load(cnt + (q < nser ? q : 0) * stride + s0 + lc, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
     for (int q = 0; q < nser; ++q) {  // (k_mask: point counts, then run counts)
         const uint32_t base = q * stride;
-        const uint32_t v = lane < n ? __hip_atomic_load(cnt + base + s0 + lane, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT)
-                                    : 0u;
+        const uint32_t v = lane < n ? vs[q] : 0u;
         uint32_t x = v;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
