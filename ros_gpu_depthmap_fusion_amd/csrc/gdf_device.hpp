@@ -153,6 +153,9 @@ struct FrameArgs {
     uint64_t ring_cap;
     uint64_t ring_first;        // physical index of logical point sel_point_start
     uint32_t nseg;
+    // > 0: seg_start[k] = k * sel_uniform - sel_off for k >= 1 (equal sequences): the sequence of
+    // selected point i is (i + sel_off) / sel_uniform, no search
+    uint32_t sel_uniform, sel_off;
     const uint32_t* seg_start;  // relative first point of each covered sequence (ascending)
     const uint32_t* seg_tf;     // transform index of that sequence
     const float* tfw;           // row-major T_world_move·T_move per selected sequence

@@ -509,6 +509,7 @@ struct gdf_engine {
     // selected rollbuffer points
     bool prepared = false, sel_inserted = false;
     DevBuf d_seg_start, d_seg_tf, d_tfw, d_tfc;
+    uint32_t sel_uniform = 0, sel_off = 0;  // (FrameArgs::sel_uniform)
     uint32_t nseg = 0;
     // a sharded window: where the 2nd, 3rd .. piece of the selection this shard holds starts
     // (selected-item index), the partition cutting its rollbuffer points there
@@ -1070,6 +1071,18 @@ void insert_selected(gdf_engine* e, const float* Twm, const float* Tcm) {  // fu
         if (seg_start.empty()) fail(GDF_ERR_STATE, "selected points not covered by sequences");
     }
     e->nseg = (uint32_t)seg_start.size();
+    // equal sequences (FrameArgs::sel_uniform): every start after the first k * S - off
+    e->sel_uniform = e->sel_off = 0;
+    if (e->nseg >= 2) {
+        const uint64_t S = e->nseg >= 3 ? (uint64_t)seg_start[2] - seg_start[1] : seg_start[1];
+        const uint64_t off = S >= seg_start[1] ? S - seg_start[1] : S;
+        bool uni = S > 0 && S >= seg_start[1] && off < S && (uint64_t)cnt + off < (1ull << 32);
+        for (uint32_t k = 1; uni && k < e->nseg; ++k) uni = (uint64_t)seg_start[k] + off == k * S;
+        if (uni) {
+            e->sel_uniform = (uint32_t)S;
+            e->sel_off = (uint32_t)off;
+        }
+    }
     if (e->nseg) {
         e->d_seg_start.ensure(e->nseg * 4);
         e->d_seg_tf.ensure(e->nseg * 4);
@@ -1417,6 +1430,8 @@ FrameArgs frame_args(gdf_engine* e, bool fused_voxel, bool compaction_marks = fa
     a.ring_first = e->ring_cap ? (e->ring_head + e->rb.selection_point_start) % e->ring_cap : 0;
     a.nseg = e->nseg;
     a.seg_start = e->d_seg_start.as<uint32_t>();
+    a.sel_uniform = e->sel_uniform;
+    a.sel_off = e->sel_off;
     a.seg_tf = e->d_seg_tf.as<uint32_t>();
     a.tfw = e->d_tfw.as<float>();
     a.tfc = e->d_tfc.as<float>();

@@ -636,10 +636,14 @@ __device__ __forceinline__ SelSeg sel_seg(const FrameArgs& a, uint32_t si0) {
     // seg_start[0] == 0), one round trip per factor 64 of sequences
     const int lane = threadIdx.x & 63;
     uint32_t lo = 0, hi = a.nseg;
+    if (a.sel_uniform)  // equal sequences (FrameArgs::sel_uniform): no search
+        lo = hi = min((si0 + a.sel_off) / a.sel_uniform, (uint32_t)a.nseg - 1u);
     while (hi - lo > 1) {
         const uint32_t step = (hi - lo + 63u) / 64u;
         const uint32_t j = lo + (uint32_t)lane * step;
-        const unsigned long long le = __ballot(j < hi && G(a.seg_start)[j] <= si0);
+        // (loaded unconditionally at a clamped index: the short-circuit form waited in a branch)
+        const uint32_t sj = G(a.seg_start)[min(j, hi - 1u)];
+        const unsigned long long le = __ballot(j < hi && sj <= si0);
         const uint32_t L = 63u - (uint32_t)__clzll((long long)le);  // bit 0 is always set
         lo = lo + L * step;
         hi = min(hi, lo + step);
@@ -648,8 +652,10 @@ __device__ __forceinline__ SelSeg sel_seg(const FrameArgs& a, uint32_t si0) {
     lo = __builtin_amdgcn_readfirstlane(lo);
     SelSeg g;
     g.si0 = si0;
-    g.tf0 = __builtin_amdgcn_readfirstlane(G(a.seg_tf)[lo]);
-    g.next = __builtin_amdgcn_readfirstlane(lo + 1 < a.nseg ? G(a.seg_start)[lo + 1] : 0xFFFFFFFFu);
+    const uint32_t tf0 = G(a.seg_tf)[lo];
+    const uint32_t nx = G(a.seg_start)[min(lo + 1u, a.nseg - 1u)];  // (one round with tf0)
+    g.tf0 = __builtin_amdgcn_readfirstlane(tf0);
+    g.next = __builtin_amdgcn_readfirstlane(lo + 1 < a.nseg ? nx : 0xFFFFFFFFu);
     g.r0 = (a.ring_first + si0) % a.ring_cap;
     return g;
 }
@@ -2191,9 +2197,10 @@ __global__ __launch_bounds__(1024) void k_sel(FrameArgs a) {
     const unsigned long long sw1 = wall_clock64();
 #endif
     const uint32_t si0 = tile * kSelSegs * B;
-    // the ring loads first (their slots need no search; 32-bit slot arithmetic: ring_cap < 2^32),
+    float tc[12], tw[16];
+    // the ring loads (their slots need no search; 32-bit slot arithmetic: ring_cap < 2^32),
     // branch-free (a point past the selection re-reads the tile's first slot and is dropped);
-    // the sequence search runs while they fly
+    // otherwise the sequence search runs while they fly
     float4 p[kSelSegs];
     {
         const uint32_t cap = (uint32_t)a.ring_cap;
@@ -2215,10 +2222,21 @@ __global__ __launch_bounds__(1024) void k_sel(FrameArgs a) {
         for (uint32_t j = i; j < (1u << kMarkCacheBits); j += B) s_mark[j] = 0xFFFFFFFFu;
     uint32_t bits[kSelSegs];
     if (one_seq) {
+        // both matrices in one load round (the world one's was a second round, after the bits)
         const gptr<const float> Tc = G(a.tfc + 16 * (size_t)g.tf0);
-        float tc[12];
+        const gptr<const float> Tw = G(a.tfw + 16 * (size_t)g.tf0);
+        // (block-uniform: into scalar registers as they arrive, not held in VGPRs beside the points)
+        float tcl[12], twl[16];
 #pragma unroll
-        for (int q = 0; q < 12; ++q) tc[q] = Tc[q];
+        for (int q = 0; q < 12; ++q) tcl[q] = Tc[q];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) twl[q] = Tw[q];
+#pragma unroll
+        for (int q = 0; q < 12; ++q)
+            tc[q] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, tcl[q])));
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            tw[q] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, twl[q])));
 #pragma unroll
         for (uint32_t j = 0; j < kSelSegs; ++j) {
             const float x = p[j].x, y = p[j].y, z = p[j].z;
@@ -2243,12 +2261,7 @@ __global__ __launch_bounds__(1024) void k_sel(FrameArgs a) {
     // a tile inside one sequence: its world matrix in registers, read once (through the pointer
     // the compiler re-read the 64-B matrix for every item - 16 dependent cache round trips per
     // wave per pass - as it cannot move those loads above the debug-byte stores)
-    float tw[16];  // (block-uniform: scalar registers)
-    if (one_seq) {
-#pragma unroll
-        for (int q = 0; q < 16; ++q)
-            tw[q] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, T0[q])));
-    }
+
     // the world point of selected item j (transform_points_indirect, world matrix)
     auto world = [&](uint32_t j) {
         const float x = p[j].x, y = p[j].y, z = p[j].z;
